@@ -1,0 +1,150 @@
+#!/usr/bin/env python3
+"""oracle/gen_golden.py -- TEST INFRASTRUCTURE ONLY; runs in the build container only.
+
+Regenerates every fixture under tests/golden/ and the scene inputs under data/scenes/ by
+running oracle/_ref/refdriver, i.e. the reference's OWN code compiled from /root/reference
+(see oracle/Makefile and oracle/ref_driver.cpp).  Nothing here runs on the GPU box.
+
+    make -C oracle ref && python oracle/gen_golden.py [--skip-head]
+"""
+import argparse
+import gzip
+import hashlib
+import json
+import os
+import struct
+import subprocess
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF = os.path.join(ROOT, "oracle", "_ref", "refdriver")
+GOLD = os.path.join(ROOT, "tests", "golden")
+SCENES = os.path.join(ROOT, "data", "scenes")
+MESHES = "/root/reference/meshes"
+
+# Small full frames (stored whole): (scene, W, H, spp). Ragged tile edges, odd spp, 1x1.
+SMALL_FRAMES = [(s, 128, 96, 4) for s in range(10)] + [
+    (1, 37, 23, 3), (8, 200, 150, 16), (5, 64, 48, 1), (1, 1, 1, 1), (8, 13, 7, 5),
+    (4, 96, 96, 16), (1, 512, 512, 1), (8, 160, 120, 2), (2, 70, 50, 7), (9, 33, 65, 64),
+]
+# Per-sample record crops at 1920x1080x4: (x0, y0) of a 16x16 pixel window
+CROPS = [(952, 532), (640, 720), (1500, 300)]
+
+
+def run(args):
+    out = subprocess.run([REF] + args, check=True, capture_output=True, text=True).stdout
+    line = [l for l in out.splitlines() if l.startswith("RESULT ")][-1]
+    return json.loads(line[len("RESULT "):])
+
+
+def gz(path):
+    """Compress a fixture in place (path -> path.gz) to keep the repo small."""
+    with open(path, "rb") as f:
+        data = f.read()
+    with gzip.GzipFile(path + ".gz", "wb", mtime=0) as f:
+        f.write(data)
+    os.remove(path)
+
+
+def sha(path):
+    with open(path, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--skip-head", action="store_true")
+    a = ap.parse_args()
+    if not os.path.exists(REF):
+        sys.exit("build oracle/_ref/refdriver first: make -C oracle ref")
+    os.makedirs(GOLD, exist_ok=True)
+    os.makedirs(os.path.join(GOLD, "frames"), exist_ok=True)
+    os.makedirs(os.path.join(GOLD, "samples"), exist_ok=True)
+    os.makedirs(SCENES, exist_ok=True)
+
+    run(["dump-scenes", MESHES, SCENES])
+    run(["kat", GOLD])
+    for k in ("ray_tri", "ray_aabb", "genray", "bgra8", "shade", "hammersley"):
+        gz(os.path.join(GOLD, f"kat_{k}.f32"))
+
+    tmp = tempfile.mkdtemp()
+    scenes = {}
+    for sid in range(10):
+        sp = os.path.join(SCENES, f"scene{sid}.rtscene")
+        gp = os.path.join(tmp, "grid.bin")
+        run(["grid", sp, gp])
+        with open(gp, "rb") as f:
+            raw = f.read()
+        dims = struct.unpack_from("<3I", raw, 0)
+        fl = struct.unpack_from("<8I", raw, 12)    # aabb_min, aabb_max, cell_wdh, inv (bits)
+        nc, nr = struct.unpack_from("<2I", raw, 44)
+        csr = raw[52:]
+        assert len(csr) == 4 * (nc + 1 + nr)
+        offs = struct.unpack_from(f"<{nc + 1}I", csr, 0)
+        scenes[str(sid)] = {
+            "rtscene_sha256": sha(sp),
+            "dims": list(dims),
+            "aabb_min_bits": [f"{x:08x}" for x in fl[0:3]],
+            "aabb_max_bits": [f"{x:08x}" for x in fl[3:6]],
+            "cell_wdh_bits": f"{fl[6]:08x}",
+            "inv_cell_wdh_bits": f"{fl[7]:08x}",
+            "num_cells": nc,
+            "num_refs": nr,
+            "max_refs_per_cell": max(offs[i + 1] - offs[i] for i in range(nc)),
+            "empty_cells": sum(1 for i in range(nc) if offs[i + 1] == offs[i]),
+            "csr_sha256": hashlib.sha256(csr).hexdigest(),
+        }
+        print("grid", sid, dims, nr, flush=True)
+
+    frames = {}
+    for sid in range(10):
+        bp, hp = os.path.join(tmp, "f.bgra"), os.path.join(tmp, "f.hits")
+        r = run(["render", os.path.join(SCENES, f"scene{sid}.rtscene"), "1920", "1080", "4",
+                 "--out", bp, "--hits", hp])
+        frames[str(sid)] = {"W": 1920, "H": 1080, "spp": 4, "bgra_sha256": sha(bp),
+                       "hits_sha256": sha(hp), "ref_msamples_per_s_8thr": r["msamples_per_s"]}
+        print("frame", sid, r["msamples_per_s"], flush=True)
+    if not a.skip_head:
+        bp = os.path.join(tmp, "head.bgra")
+        r = run(["render", os.path.join(SCENES, "scene4.rtscene"), "4096", "4096", "16", "--out", bp])
+        frames["head_4096x4096x16"] = {"scene": 4, "W": 4096, "H": 4096, "spp": 16,
+                                       "bgra_sha256": sha(bp),
+                                       "ref_msamples_per_s_8thr": r["msamples_per_s"]}
+        print("head", r["msamples_per_s"], flush=True)
+
+    small = []
+    for (sid, w, h, spp) in SMALL_FRAMES:
+        name = f"scene{sid}_{w}x{h}x{spp}"
+        bp = os.path.join(GOLD, "frames", name + ".bgra")
+        hp = os.path.join(GOLD, "frames", name + ".hits")
+        run(["render", os.path.join(SCENES, f"scene{sid}.rtscene"), str(w), str(h), str(spp),
+             "--out", bp, "--hits", hp])
+        gz(bp)
+        gz(hp)
+        small.append({"scene": sid, "W": w, "H": h, "spp": spp, "name": name})
+
+    crops = []
+    for sid in range(10):
+        for (x0, y0) in CROPS:
+            name = f"scene{sid}_crop{x0}_{y0}"
+            run(["samples", os.path.join(SCENES, f"scene{sid}.rtscene"), "1920", "1080", "4",
+                 str(x0), str(y0), "16", "16", os.path.join(GOLD, "samples", name + ".rec")])
+            gz(os.path.join(GOLD, "samples", name + ".rec"))
+            crops.append({"scene": sid, "W": 1920, "H": 1080, "spp": 4, "x0": x0, "y0": y0,
+                          "w": 16, "h": 16, "name": name})
+
+    meta = {
+        "generator": "oracle/gen_golden.py via oracle/_ref/refdriver (reference sources, g++ "
+                     "-O3 -std=c++11, no -march)",
+        "scenes": scenes, "frames_1080p4": frames, "small_frames": small, "crops": crops,
+        "sample_record": "hit u32, tri u32, t f32, u f32, v f32, r f32, g f32, b f32 "
+                         "(t,u,v = 0 and tri = 0xFFFFFFFF on miss)",
+    }
+    with open(os.path.join(GOLD, "golden.json"), "w") as f:
+        json.dump(meta, f, indent=1, sort_keys=True)
+    print("wrote", os.path.join(GOLD, "golden.json"))
+
+
+if __name__ == "__main__":
+    main()
