@@ -1,0 +1,227 @@
+#!/usr/bin/env python3
+"""Benchmark: Msamples/s at 1920x1080x4spp on Cornell-Box (scene 1) + killeroo (scene 8).
+
+A step renders one full 1920x1080x4spp frame of each scene (2 x 8,294,400 samples) through
+the HIP path into device memory (scene data resident in HBM before timing starts).  With
+N > 1 ranks (torchrun, one process per GPU, RCCL) every rank renders its interleaved 16x16
+tiles of each frame (tile t -> rank t % N), the shards are all-gathered over xGMI and rank 0
+un-permutes them into the frame (K3): strong scaling of a fixed frame.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+
+Prints ONE JSON line (rank 0).  value = total samples of all ranks / max-over-ranks wall time
+of the K timed steps.  roofline: algorithmic bytes of the render kernel per launch (SURVEY
+§8d: B = 8*voxels + 40*tri_tests + 48*hit + 4/spp per sample, counts measured on these
+frames) / mean kernel duration from HIP events on the launch stream.  cpu_baseline: the
+oracle's CPU restatement of the reference tile pool (kind "port"), on this host's cores.
+"""
+import argparse
+import importlib.util
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "cpp-11-ray-trace-march-framework_amd")
+SCENES = (1, 8)
+W, H, SPP = 1920, 1080, 4
+HBM_PEAK = 8.0e12          # MI355X HBM3E peak, B/s (MI355X_MICROARCH.md)
+SURVEY_B = {1: 371.1, 8: 1467.8}
+
+
+def load_package():
+    spec = importlib.util.spec_from_file_location("rtm", os.path.join(PKG, "__init__.py"))
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules["rtm"] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def algorithmic_bytes(gs, frame):
+    """Per-sample algorithmic bytes of the config from the kernel's own per-sample counters."""
+    recs = gs.trace_samples(frame, 0, 0, frame.width, frame.height)
+    n = len(recs)
+    v = recs["steps"].astype(np.float64).sum() / n
+    t = recs["tests"].astype(np.float64).sum() / n
+    h = recs["hit"].astype(np.float64).sum() / n
+    return {"voxels": v, "tri_tests": t, "hit": h,
+            "bytes_per_sample": 8 * v + 40 * t + 48 * h + 4.0 / frame.spp}
+
+
+def cpu_baseline(rtm_unused=None):
+    """Oracle (CPU restatement of the reference's std::thread tile pool) on this host."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from conftest import Oracle
+    orc = Oracle()
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    cores = max(1, min(cores, int(os.environ.get("OMP_NUM_THREADS", cores))))
+    for sid in SCENES:                  # warm-up (first render after idle is slow)
+        orc.render(sid, W, H, SPP, nthreads=cores)
+    times = []
+    for _ in range(3):
+        tot = 0.0
+        for sid in SCENES:
+            _, _, s = orc.render(sid, W, H, SPP, nthreads=cores)
+            tot += s
+        times.append(tot)
+    med = sorted(times)[1]
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next(l.split(":", 1)[1].strip() for l in f if l.startswith("model name"))
+    except Exception:
+        pass
+    return {"value": round(len(SCENES) * W * H * SPP / med / 1e6, 3), "unit": "Msamples/s",
+            "cores": cores, "kind": "port",
+            "sample": f"full frames of scenes {list(SCENES)} at {W}x{H}x{SPP}, 12x9 tile pool, "
+                      f"median of 3 after 1 warm-up; cpu: {model or platform.processor()}"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--kernel", type=int, default=0, help="rt_kernel: 0 auto, 1 lanes, 2 pixel loop, 3 compact")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}; launch N>1 with torch.distributed.run")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    rtm = load_package()
+    scenes = []
+    for sid in SCENES:
+        hs = rtm.HostScene.load(sid)
+        gs = rtm.GpuScene(hs, local)
+        scenes.append((sid, hs, gs, gs.frame(W, H, SPP, kernel=args.kernel)))
+
+    stream = torch.cuda.current_stream()
+    sp = stream.cuda_stream
+    if world == 1:
+        outs = [torch.empty(W * H, dtype=torch.int32, device="cuda") for _ in SCENES]
+    else:
+        e = rtm.shard_elems(W, H, world)
+        shards = [torch.empty(e, dtype=torch.int32, device="cuda") for _ in SCENES]
+        gathered = [torch.empty(world * e, dtype=torch.int32, device="cuda") for _ in SCENES]
+        outs = [torch.empty(W * H, dtype=torch.int32, device="cuda") for _ in SCENES]
+
+    ev = {sid: [] for sid in SCENES}
+
+    def step(record):
+        for i, (sid, hs, gs, f) in enumerate(scenes):
+            if record:
+                a = torch.cuda.Event(enable_timing=True)
+                b = torch.cuda.Event(enable_timing=True)
+                a.record(stream)
+            if world == 1:
+                gs.render_frame_device(f, outs[i].data_ptr(), sp)
+            else:
+                gs.render_shard_device(f, rank, world, shards[i].data_ptr(), sp)
+            if record:
+                b.record(stream)
+                ev[sid].append((a, b))
+        if world > 1:
+            works = [dist.all_gather_into_tensor(gathered[i], shards[i], async_op=True)
+                     for i in range(len(scenes))]
+            for w in works:
+                w.wait()
+            if rank == 0:
+                for i in range(len(scenes)):
+                    rtm.unshard_device(W, H, world, gathered[i].data_ptr(), outs[i].data_ptr(), sp)
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    kernel_ms = {sid: float(np.mean([a.elapsed_time(b) for a, b in ev[sid]])) for sid in SCENES}
+    samples_per_step = len(SCENES) * W * H * SPP          # all ranks together
+    value = samples_per_step * args.steps / elapsed / 1e6
+
+    if rank == 0:
+        # algorithmic bytes per launch (this rank's launch covers 1/world of the frame)
+        ab = {sid: algorithmic_bytes(gs, f) for sid, hs, gs, f in scenes}
+        launch_bytes = {sid: ab[sid]["bytes_per_sample"] * W * H * SPP / world for sid in SCENES}
+        achieved = sum(launch_bytes.values()) / (sum(kernel_ms.values()) / 1e3)
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(pmc) and world == 1:
+            with open(pmc) as fh:
+                p = json.load(fh)
+            if p.get("workload") == f"scenes{list(SCENES)}_{W}x{H}x{SPP}":
+                traffic = p.get("hbm_bytes_per_launch")
+        out = {
+            "metric": "Msamples/s at 1920x1080x4spp Cornell-Box+killeroo",
+            "value": round(value, 3),
+            "unit": "Msamples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "reference scenes 1 (Cornell box + cube) and 8 (killeroo + ground), "
+                    "post-setup meshes dumped by the reference's own mesh code",
+            "config": {"workload": f"scenes{list(SCENES)}_{W}x{H}x{SPP}", "scenes": list(SCENES),
+                       "width": W, "height": H, "spp": SPP, "kernel": args.kernel,
+                       "parallelism": f"tile-shard x{world}" + (" + RCCL all-gather" if world > 1 else "")},
+            "per_scene": {str(sid): {"kernel_ms": round(kernel_ms[sid], 4),
+                                     "kernel_msamples_per_s": round(W * H * SPP / world / kernel_ms[sid] / 1e3, 1),
+                                     "bytes_per_sample": round(ab[sid]["bytes_per_sample"], 1),
+                                     "survey_bytes_per_sample": SURVEY_B[sid],
+                                     "voxels": round(ab[sid]["voxels"], 2),
+                                     "tri_tests": round(ab[sid]["tri_tests"], 2),
+                                     "hit": round(ab[sid]["hit"], 4)} for sid in SCENES},
+            "roofline": {"bound": "hbm", "achieved": round(achieved / 1e9, 1), "peak": HBM_PEAK / 1e9,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 4),
+                         "traffic": traffic,
+                         "note": "achieved = algorithmic bytes per launch (SURVEY 8d formula on the "
+                                 "kernel's measured per-sample counts) / mean kernel time; the scene "
+                                 "working set is L2/MALL resident, so frac can exceed 1"},
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline()
+        print(json.dumps(out), flush=True)
+
+    for sid, hs, gs, f in scenes:
+        gs.close()
+        hs.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

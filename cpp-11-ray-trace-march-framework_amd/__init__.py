@@ -1,0 +1,413 @@
+"""MI355X-native primary-ray tile tracer (gfx950) -- Python mirror of the reference surface.
+
+The product is two in-tree shared libraries built by this package's Makefile:
+
+* ``librt_tracer.so`` -- hand-written HIP kernels behind the C ABI of ``include/rt_tracer.h``
+  (the drop-in for ``Renderer::RenderTile``, renderer.cpp:81-174);
+* ``librt_host.so`` -- the C++11 host: scene load, ``Grid::Grid`` build emitted as CSR
+  (grid.cpp:12-154) and the 12x9 ``Framebuffer`` tile pool with the GPU ``RenderTile``
+  (framebuffer.cpp), ABI in ``include/rt_host.h``.
+
+This module binds both with ctypes.  There is no CPU fallback: if a library is missing or a
+call fails, :class:`RtError` is raised.  The directory name is not a Python identifier, so
+load it with :func:`load_package` from ``tests/``/``bench.py`` (importlib by path).
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+SCENE_DIR = os.path.join(REPO, "data", "scenes")
+
+RT_TRI_MOLLER_TRUMBORE, RT_TRI_BARYCENTRIC = 0, 1
+RT_KERNEL_AUTO, RT_KERNEL_LANES, RT_KERNEL_PIXEL_LOOP, RT_KERNEL_COMPACT = 0, 1, 2, 3
+SHARD_TILE = 16
+
+# Symbols of include/rt_tracer.h and include/rt_host.h (checked by tests/test_abi.py)
+TRACER_SYMBOLS = [
+    "rt_get_device_count", "rt_scene_create", "rt_scene_destroy", "rt_scene_device_bytes",
+    "rt_render_tiles", "rt_render_frame_device", "rt_shard_elems", "rt_render_shard_device",
+    "rt_unshard_device", "rt_last_kernel_ms", "rt_trace_samples", "rt_debug_primitives",
+    "rt_sample_table", "rt_last_error", "rt_abi_version",
+]
+HOST_SYMBOLS = [
+    "rth_scene_load", "rth_scene_from_mesh", "rth_scene_free", "rth_scene_desc",
+    "rth_scene_camera", "rth_scene_stats_get", "rth_framebuffer_create", "rth_framebuffer_free",
+    "rth_framebuffer_set_sample_count", "rth_framebuffer_set_options", "rth_framebuffer_resize",
+    "rth_framebuffer_start_rendering", "rth_framebuffer_read", "rth_framebuffer_save_bmp",
+    "rth_last_error",
+]
+
+
+class RtError(RuntimeError):
+    pass
+
+
+# ------------------------------------------------------------------ ABI structures
+c_u32, c_f32 = ctypes.c_uint32, ctypes.c_float
+
+
+class Vertex(ctypes.Structure):
+    _fields_ = [("p", c_f32 * 3), ("n", c_f32 * 3)]
+
+
+class Triangle(ctypes.Structure):
+    _fields_ = [("v0", c_u32), ("v1", c_u32), ("v2", c_u32), ("n", c_f32 * 3)]
+
+
+class GridDesc(ctypes.Structure):
+    _fields_ = [("dims", c_u32 * 3), ("aabb_min", c_f32 * 3), ("aabb_max", c_f32 * 3),
+                ("cell_wdh", c_f32), ("inv_cell_wdh", c_f32),
+                ("cell_offsets", ctypes.POINTER(c_u32)), ("cell_tris", ctypes.POINTER(c_u32))]
+
+
+class SceneDesc(ctypes.Structure):
+    _fields_ = [("num_vertices", c_u32), ("num_triangles", c_u32),
+                ("vertices", ctypes.POINTER(Vertex)), ("triangles", ctypes.POINTER(Triangle)),
+                ("grid", GridDesc)]
+
+
+class Frame(ctypes.Structure):
+    _fields_ = [("cam", c_f32 * 16), ("fov", c_f32), ("width", c_u32), ("height", c_u32),
+                ("spp", c_u32), ("sample_offsets", ctypes.POINTER(c_f32)),
+                ("tri_test", c_u32), ("kernel", c_u32)]
+
+
+class Tile(ctypes.Structure):
+    _fields_ = [("x0", c_u32), ("y0", c_u32), ("x1", c_u32), ("y1", c_u32)]
+
+
+class SceneStats(ctypes.Structure):
+    _fields_ = [("scene_id", c_u32), ("num_vertices", c_u32), ("num_triangles", c_u32),
+                ("num_cells", c_u32), ("num_refs", c_u32), ("max_refs_per_cell", c_u32),
+                ("empty_cells", c_u32), ("grid_build_s", ctypes.c_double)]
+
+
+SAMPLE_REC_DTYPE = np.dtype([("hit", "<u4"), ("tri", "<u4"), ("voxel", "<u4"), ("steps", "<u4"),
+                             ("tests", "<u4"), ("t", "<f4"), ("u", "<f4"), ("v", "<f4"),
+                             ("r", "<f4"), ("g", "<f4"), ("b", "<f4"), ("pad", "<u4")])
+
+_tracer = None
+_host = None
+
+
+def _load(name):
+    path = os.path.join(HERE, name)
+    if not os.path.exists(path):
+        raise RtError(f"{path} is not built; run __graft_entry__.build() or make -C {HERE}")
+    return ctypes.CDLL(path)
+
+
+def tracer_lib():
+    """librt_tracer.so (HIP).  Loading it needs no GPU; calls that launch work do."""
+    global _tracer
+    if _tracer is None:
+        L = _load("librt_tracer.so")
+        vp, u32p = ctypes.c_void_p, ctypes.POINTER(c_u32)
+        L.rt_scene_create.argtypes = [ctypes.POINTER(SceneDesc), ctypes.c_int, ctypes.POINTER(vp)]
+        L.rt_scene_destroy.argtypes = [vp]
+        L.rt_scene_device_bytes.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64)]
+        L.rt_render_tiles.argtypes = [vp, ctypes.POINTER(Frame), ctypes.POINTER(Tile), c_u32,
+                                      ctypes.POINTER(u32p)]
+        L.rt_render_frame_device.argtypes = [vp, ctypes.POINTER(Frame), vp, vp]
+        L.rt_shard_elems.argtypes = [c_u32, c_u32, c_u32, ctypes.POINTER(ctypes.c_uint64)]
+        L.rt_render_shard_device.argtypes = [vp, ctypes.POINTER(Frame), c_u32, c_u32, vp, vp]
+        L.rt_unshard_device.argtypes = [c_u32, c_u32, c_u32, vp, vp, vp]
+        L.rt_last_kernel_ms.argtypes = [vp, ctypes.POINTER(c_f32)]
+        L.rt_trace_samples.argtypes = [vp, ctypes.POINTER(Frame), c_u32, c_u32, c_u32, c_u32, vp]
+        L.rt_debug_primitives.argtypes = [ctypes.c_int, vp, c_u32, vp, ctypes.c_int]
+        L.rt_sample_table.argtypes = [c_u32, vp]
+        L.rt_last_error.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
+        L.rt_get_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
+        _tracer = L
+    return _tracer
+
+
+def host_lib():
+    global _host
+    if _host is None:
+        tracer_lib()
+        L = _load("librt_host.so")
+        vp = ctypes.c_void_p
+        L.rth_scene_load.argtypes = [ctypes.c_char_p, c_u32, ctypes.POINTER(vp)]
+        L.rth_scene_from_mesh.argtypes = [vp, c_u32, vp, c_u32, c_f32, vp, c_u32, c_u32,
+                                          ctypes.POINTER(vp)]
+        L.rth_scene_free.argtypes = [vp]
+        L.rth_scene_free.restype = None
+        L.rth_scene_desc.argtypes = [vp, ctypes.POINTER(SceneDesc)]
+        L.rth_scene_camera.argtypes = [vp, ctypes.POINTER(c_f32), vp]
+        L.rth_scene_stats_get.argtypes = [vp, ctypes.POINTER(SceneStats)]
+        L.rth_framebuffer_create.argtypes = [vp, vp, c_u32, ctypes.POINTER(vp)]
+        L.rth_framebuffer_free.argtypes = [vp]
+        L.rth_framebuffer_free.restype = None
+        L.rth_framebuffer_set_sample_count.argtypes = [vp, c_u32]
+        L.rth_framebuffer_set_options.argtypes = [vp, c_u32, c_u32]
+        L.rth_framebuffer_resize.argtypes = [vp, c_u32, c_u32, ctypes.POINTER(ctypes.c_double)]
+        L.rth_framebuffer_start_rendering.argtypes = [vp, ctypes.POINTER(ctypes.c_double)]
+        L.rth_framebuffer_read.argtypes = [vp, vp]
+        L.rth_framebuffer_save_bmp.argtypes = [vp, ctypes.c_char_p]
+        L.rth_last_error.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
+        _host = L
+    return _host
+
+
+def _check(rc, lib, fn):
+    if rc != 0:
+        buf = ctypes.create_string_buffer(1024)
+        lib.rt_last_error(buf, 1024) if fn.startswith("rt_") else lib.rth_last_error(buf, 1024)
+        raise RtError(f"{fn} failed ({rc}): {buf.value.decode(errors='replace')}")
+
+
+def _ptr(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def scene_path(scene_id):
+    return os.path.join(SCENE_DIR, f"scene{scene_id}.rtscene")
+
+
+def device_count():
+    n = ctypes.c_int(0)
+    L = tracer_lib()
+    _check(L.rt_get_device_count(ctypes.byref(n)), L, "rt_get_device_count")
+    return n.value
+
+
+def sample_table(spp):
+    out = np.zeros(2 * spp, np.float32)
+    L = tracer_lib()
+    _check(L.rt_sample_table(spp, _ptr(out)), L, "rt_sample_table")
+    return out.reshape(spp, 2)
+
+
+# ------------------------------------------------------------------ host scene
+class HostScene:
+    """Scene + Grid on the host (scene.h:11-26, grid.h:12-52): mesh, camera and CSR cells."""
+
+    def __init__(self, handle):
+        self._h = ctypes.c_void_p(handle)
+        L = host_lib()
+        fov, cam = c_f32(), np.zeros(16, np.float32)
+        _check(L.rth_scene_camera(self._h, ctypes.byref(fov), _ptr(cam)), L, "rth_scene_camera")
+        self.fov, self.cam = fov.value, cam
+        st = SceneStats()
+        _check(L.rth_scene_stats_get(self._h, ctypes.byref(st)), L, "rth_scene_stats_get")
+        self.stats = {k: getattr(st, k) for k, _ in SceneStats._fields_}
+
+    @classmethod
+    def load(cls, path_or_id, nthreads=0):
+        path = scene_path(path_or_id) if isinstance(path_or_id, int) else path_or_id
+        L, h = host_lib(), ctypes.c_void_p()
+        _check(L.rth_scene_load(path.encode(), nthreads, ctypes.byref(h)), L, "rth_scene_load")
+        return cls(h.value)
+
+    @classmethod
+    def from_mesh(cls, vertices, triangles, fov, cam, grid_res=64, nthreads=0):
+        """vertices: float32 [nv, 6] (p, n); triangles: structured/u32 [nt, 6] (v0, v1, v2, n bits)."""
+        v = np.ascontiguousarray(vertices, np.float32)
+        t = np.ascontiguousarray(triangles).view(np.uint32)
+        cam = np.ascontiguousarray(cam, np.float32).reshape(16)
+        L, h = host_lib(), ctypes.c_void_p()
+        _check(L.rth_scene_from_mesh(_ptr(v), v.shape[0], _ptr(t), t.shape[0], fov, _ptr(cam),
+                                     grid_res, nthreads, ctypes.byref(h)), L, "rth_scene_from_mesh")
+        return cls(h.value)
+
+    def desc(self):
+        d = SceneDesc()
+        L = host_lib()
+        _check(L.rth_scene_desc(self._h, ctypes.byref(d)), L, "rth_scene_desc")
+        return d
+
+    def grid(self):
+        """(meta dict, offsets u32[C+1], tris u32[R]) -- copies."""
+        d = self.desc()
+        g = d.grid
+        nc = g.dims[0] * g.dims[1] * g.dims[2]
+        offs = np.ctypeslib.as_array(g.cell_offsets, shape=(nc + 1,)).copy()
+        tris = np.ctypeslib.as_array(g.cell_tris, shape=(int(offs[-1]),)).copy() if offs[-1] else \
+            np.zeros(0, np.uint32)
+        meta = {"dims": list(g.dims), "aabb_min": np.array(g.aabb_min, np.float32),
+                "aabb_max": np.array(g.aabb_max, np.float32),
+                "cell_wdh": np.float32(g.cell_wdh), "inv_cell_wdh": np.float32(g.inv_cell_wdh)}
+        return meta, offs, tris
+
+    def close(self):
+        if self._h:
+            host_lib().rth_scene_free(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+# ------------------------------------------------------------------ GPU scene
+class GpuScene:
+    """Device copy of a scene (rt_scene_create) plus the rendering entry points."""
+
+    def __init__(self, host_scene, device=0):
+        self.host = host_scene
+        L = tracer_lib()
+        h = ctypes.c_void_p()
+        d = host_scene.desc()
+        _check(L.rt_scene_create(ctypes.byref(d), device, ctypes.byref(h)), L, "rt_scene_create")
+        self._h = h
+        self.device = device
+
+    def frame(self, width, height, spp, tri_test=RT_TRI_MOLLER_TRUMBORE, kernel=RT_KERNEL_AUTO,
+              sample_offsets=None):
+        f = Frame()
+        for i in range(16):
+            f.cam[i] = float(self.host.cam[i])
+        f.fov, f.width, f.height, f.spp = self.host.fov, width, height, spp
+        f.tri_test, f.kernel = tri_test, kernel
+        if sample_offsets is not None:
+            so = np.ascontiguousarray(sample_offsets, np.float32).reshape(-1)
+            f._keep = so
+            f.sample_offsets = so.ctypes.data_as(ctypes.POINTER(c_f32))
+        return f
+
+    def render_tiles(self, frame, tiles):
+        """tiles: list of (x0, y0, x1, y1) -> list of uint32 arrays, (y1-y0, x1-x0)."""
+        n = len(tiles)
+        arr = (Tile * n)(*[Tile(*t) for t in tiles])
+        bufs = [np.zeros((t[3] - t[1], t[2] - t[0]), np.uint32) for t in tiles]
+        ptrs = (ctypes.POINTER(c_u32) * n)(*[b.ctypes.data_as(ctypes.POINTER(c_u32)) for b in bufs])
+        L = tracer_lib()
+        _check(L.rt_render_tiles(self._h, ctypes.byref(frame), arr, n, ptrs), L, "rt_render_tiles")
+        return bufs
+
+    def render_frame(self, frame):
+        return self.render_tiles(frame, [(0, 0, frame.width, frame.height)])[0]
+
+    def render_frame_device(self, frame, d_ptr, stream=0):
+        L = tracer_lib()
+        _check(L.rt_render_frame_device(self._h, ctypes.byref(frame), ctypes.c_void_p(d_ptr),
+                                        ctypes.c_void_p(stream)), L, "rt_render_frame_device")
+
+    def render_shard_device(self, frame, rank, nranks, d_ptr, stream=0):
+        L = tracer_lib()
+        _check(L.rt_render_shard_device(self._h, ctypes.byref(frame), rank, nranks,
+                                        ctypes.c_void_p(d_ptr), ctypes.c_void_p(stream)), L,
+               "rt_render_shard_device")
+
+    def last_kernel_ms(self):
+        ms = c_f32()
+        L = tracer_lib()
+        _check(L.rt_last_kernel_ms(self._h, ctypes.byref(ms)), L, "rt_last_kernel_ms")
+        return ms.value
+
+    def device_bytes(self):
+        b = ctypes.c_uint64()
+        L = tracer_lib()
+        _check(L.rt_scene_device_bytes(self._h, ctypes.byref(b)), L, "rt_scene_device_bytes")
+        return b.value
+
+    def trace_samples(self, frame, x0, y0, w, h):
+        out = np.zeros(w * h * max(1, frame.spp), SAMPLE_REC_DTYPE)
+        L = tracer_lib()
+        _check(L.rt_trace_samples(self._h, ctypes.byref(frame), x0, y0, w, h, _ptr(out)), L,
+               "rt_trace_samples")
+        return out
+
+    def close(self):
+        if getattr(self, "_h", None):
+            tracer_lib().rt_scene_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def shard_elems(width, height, nranks):
+    e = ctypes.c_uint64()
+    L = tracer_lib()
+    _check(L.rt_shard_elems(width, height, nranks, ctypes.byref(e)), L, "rt_shard_elems")
+    return e.value
+
+
+def unshard_device(width, height, nranks, d_gathered, d_out, stream=0):
+    L = tracer_lib()
+    _check(L.rt_unshard_device(width, height, nranks, ctypes.c_void_p(d_gathered),
+                               ctypes.c_void_p(d_out), ctypes.c_void_p(stream)), L,
+           "rt_unshard_device")
+
+
+PRIM_WIDTHS = {0: (18, 8), 1: (12, 4), 2: (23, 6), 3: (3, 4), 4: (11, 3)}
+
+
+def debug_primitives(kind, records, device=0):
+    wi, wo = PRIM_WIDTHS[kind]
+    rin = np.ascontiguousarray(records, np.float32).reshape(-1, wi)
+    out = np.zeros((rin.shape[0], wo), np.float32)
+    L = tracer_lib()
+    _check(L.rt_debug_primitives(kind, _ptr(rin), rin.shape[0], _ptr(out), device), L,
+           "rt_debug_primitives")
+    return out
+
+
+# ------------------------------------------------------------------ Renderer mirror
+class Renderer:
+    """Renderer/Framebuffer surface of the reference (renderer.h, framebuffer.h) on the GPU.
+
+    ``resize(w, h)`` re-tiles the 12x9 framebuffer and renders a frame through the host
+    worker pool whose ``RenderTile`` is served by one batched GPU launch per frame.
+    """
+
+    def __init__(self, host_scene, gpu_scene, nthreads=0):
+        self.host, self.gpu = host_scene, gpu_scene
+        L, h = host_lib(), ctypes.c_void_p()
+        _check(L.rth_framebuffer_create(gpu_scene._h, host_scene._h, nthreads, ctypes.byref(h)),
+               L, "rth_framebuffer_create")
+        self._h = h
+        self.width = self.height = 1
+
+    def set_sample_count(self, spp):
+        L = host_lib()
+        _check(L.rth_framebuffer_set_sample_count(self._h, spp), L, "rth_framebuffer_set_sample_count")
+
+    def set_options(self, tri_test=RT_TRI_MOLLER_TRUMBORE, kernel=RT_KERNEL_AUTO):
+        L = host_lib()
+        _check(L.rth_framebuffer_set_options(self._h, tri_test, kernel), L, "rth_framebuffer_set_options")
+
+    def resize(self, width, height):
+        s = ctypes.c_double()
+        L = host_lib()
+        _check(L.rth_framebuffer_resize(self._h, width, height, ctypes.byref(s)), L, "rth_framebuffer_resize")
+        self.width, self.height = width, height
+        return s.value
+
+    def start_rendering(self):
+        s = ctypes.c_double()
+        L = host_lib()
+        _check(L.rth_framebuffer_start_rendering(self._h, ctypes.byref(s)), L,
+               "rth_framebuffer_start_rendering")
+        return s.value
+
+    def read(self):
+        out = np.zeros((self.height, self.width), np.uint32)
+        L = host_lib()
+        _check(L.rth_framebuffer_read(self._h, _ptr(out)), L, "rth_framebuffer_read")
+        return out
+
+    def save_to_bmp(self, path):
+        L = host_lib()
+        _check(L.rth_framebuffer_save_bmp(self._h, path.encode()), L, "rth_framebuffer_save_bmp")
+
+    def close(self):
+        if getattr(self, "_h", None):
+            host_lib().rth_framebuffer_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,174 @@
+// rt_device.h -- device-side restatement of the reference's per-sample arithmetic for gfx950.
+//
+// Parity rules (SURVEY.md §7 hazards H1-H12), enforced by the build flags in csrc/Makefile
+// (-ffp-contract=off, no fast-math, default IEEE f32 denormals, correctly rounded f32
+// div/sqrt) and by keeping the reference's operation order in every expression below.
+// Each function cites the reference line it restates; tests/test_gpu_parity.py checks it
+// against the oracle and against the reference's own known-answer vectors.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rtd {
+
+constexpr float kFltMax = 3.402823466e+38f;   // std::numeric_limits<float>::max()
+constexpr uint32_t kNoTri = 0xFFFFFFFFu;
+
+// x86 cvttss2si semantics for the reference's (int) / (uchar) casts (grid.h:46,
+// lin_alg.h:128-130): NaN and out-of-range give INT_MIN; AMDGPU's v_cvt_i32_f32 would
+// saturate instead (hazard H7).
+__device__ __forceinline__ int cvt_i32_x86(float x)
+{
+    return (x >= -2147483648.0f && x < 2147483648.0f) ? int(x) : int(0x80000000u);
+}
+
+// lin_alg.h:125-132 ToBGRA8 (alpha 0)
+__device__ __forceinline__ uint32_t pack_bgra8(float r, float g, float b)
+{
+    const uint32_t rc = r > 1.0f ? 255u : uint32_t(cvt_i32_x86(r * 255.0f)) & 255u;
+    const uint32_t gc = g > 1.0f ? 255u : uint32_t(cvt_i32_x86(g * 255.0f)) & 255u;
+    const uint32_t bc = b > 1.0f ? 255u : uint32_t(cvt_i32_x86(b * 255.0f)) & 255u;
+    return rc << 16 | gc << 8 | bc;
+}
+
+// renderer.cpp:165-168 gamma: glibc powf(x, 0.5f) is replaced by the correctly rounded
+// sqrtf.  oracle/gamma_exhaustive.c proves pack_bgra8 of both is identical for EVERY
+// float in [0, 1.0078] (and both saturate above); the float colour differs by <= 1 ulp
+// on 678,030 inputs (hazard H6).
+__device__ __forceinline__ float gamma_half(float x) { return __builtin_sqrtf(x); }
+
+// lin_alg.h:138-156 Dot (accumulates from T() = 0) and Normalize (1/sqrt, then scale)
+__device__ __forceinline__ void normalize3(float& x, float& y, float& z)
+{
+    float d = 0.0f;
+    d += x * x;
+    d += y * y;
+    d += z * z;
+    const float len = 1.0f / __builtin_sqrtf(d);
+    x = x * len;
+    y = y * len;
+    z = z * len;
+}
+
+__device__ __forceinline__ float dot3(float ax, float ay, float az, float bx, float by, float bz)
+{
+    float d = 0.0f;
+    d += ax * bx;
+    d += ay * by;
+    d += az * bz;
+    return d;
+}
+
+// triangle.h:15-107 IntersectRayTri, non-culling branch. e1 = v1 - v0 and e2 = v2 - v0 are
+// precomputed on the host with the same single IEEE subtraction (triangle.h:41-42).
+__device__ __forceinline__ bool ray_tri_mt(float ox, float oy, float oz, float dx, float dy, float dz,
+                                           float v0x, float v0y, float v0z,
+                                           float e1x, float e1y, float e1z,
+                                           float e2x, float e2y, float e2z,
+                                           float& t, float& u, float& v)
+{
+    const float px = dy * e2z - dz * e2y;
+    const float py = dz * e2x - dx * e2z;
+    const float pz = dx * e2y - dy * e2x;
+    const float det = e1x * px + e1y * py + e1z * pz;
+    if (det > -0.00000001f && det < 0.00000001f) return false;
+    const float inv_det = 1.0f / det;
+    const float tx = ox - v0x, ty = oy - v0y, tz = oz - v0z;
+    u = (tx * px + ty * py + tz * pz) * inv_det;
+    if (u < 0.0f || u > 1.0f) return false;
+    const float qx = ty * e1z - tz * e1y;
+    const float qy = tz * e1x - tx * e1z;
+    const float qz = tx * e1y - ty * e1x;
+    v = (dx * qx + dy * qy + dz * qz) * inv_det;
+    if (v < 0.0f || u + v > 1.0f) return false;
+    t = (e2x * qx + e2y * qy + e2z * qz) * inv_det;
+    return t >= 0.0f;
+}
+
+// triangle.h:200-226 IntersectRayPlane + ComputeBarycentric (:133-156). Uses v0, the same
+// e1 (= v1 - v0) and e2 (= v2 - v0, the reference's e0) and the face normal.
+__device__ __forceinline__ bool ray_tri_bary(float ox, float oy, float oz, float dx, float dy, float dz,
+                                             float v0x, float v0y, float v0z,
+                                             float e1x, float e1y, float e1z,
+                                             float e2x, float e2y, float e2z,
+                                             float nx, float ny, float nz,
+                                             float& t, float& u, float& v)
+{
+    const float denom = dot3(nx, ny, nz, dx, dy, dz);
+    if (__builtin_fabsf(denom) < 0.00000001f) return false;
+    const float dd = dot3(nx, ny, nz, v0x, v0y, v0z);
+    t = (dd - dot3(nx, ny, nz, ox, oy, oz)) / denom;
+    if (!(t >= 0.0f)) return false;                              // t >= 0.0 (double compare)
+    const float qx = ox + dx * t, qy = oy + dy * t, qz = oz + dz * t;
+    const float wx = qx - v0x, wy = qy - v0y, wz = qz - v0z;     // e2 = pos - v0
+    const float d00 = dot3(e2x, e2y, e2z, e2x, e2y, e2z);       // e0 = v2 - v0
+    const float d01 = dot3(e2x, e2y, e2z, e1x, e1y, e1z);
+    const float d02 = dot3(e2x, e2y, e2z, wx, wy, wz);
+    const float d11 = dot3(e1x, e1y, e1z, e1x, e1y, e1z);
+    const float d12 = dot3(e1x, e1y, e1z, wx, wy, wz);
+    const float inv_denom = 1.0f / (d00 * d11 - d01 * d01);
+    u = (d00 * d12 - d01 * d02) * inv_denom;
+    v = (d11 * d02 - d01 * d12) * inv_denom;
+    return (u >= 0.0f) && (v >= 0.0f) && (u + v < 1.0f);
+}
+
+// aabb.h:9-13
+__device__ __forceinline__ bool point_in_aabb(float px, float py, float pz, const float* mn, const float* mx)
+{
+    return px >= mn[0] && py >= mn[1] && pz >= mn[2] && px <= mx[0] && py <= mx[1] && pz <= mx[2];
+}
+
+// aabb.h:34-83 (Williams et al.); IEEE inf/NaN from 1/+-0 select the slab order (H3, H9)
+__device__ __forceinline__ bool ray_aabb(float ox, float oy, float oz, float dx, float dy, float dz,
+                                         const float* mn, const float* mx, float& tmin, float& tmax)
+{
+    const float ix = 1.0f / dx, iy = 1.0f / dy, iz = 1.0f / dz;
+    const bool sx = ix < 0.0f, sy = iy < 0.0f, sz = iz < 0.0f;
+    tmin = ((sx ? mx[0] : mn[0]) - ox) * ix;
+    tmax = ((sx ? mn[0] : mx[0]) - ox) * ix;
+    const float tymin = ((sy ? mx[1] : mn[1]) - oy) * iy;
+    const float tymax = ((sy ? mn[1] : mx[1]) - oy) * iy;
+    if ((tmin > tymax) || (tymin > tmax)) return false;
+    if (tymin > tmin) tmin = tymin;
+    if (tymax < tmax) tmax = tymax;
+    const float tzmin = ((sz ? mx[2] : mn[2]) - oz) * iz;
+    const float tzmax = ((sz ? mn[2] : mx[2]) - oz) * iz;
+    if ((tmin > tzmax) || (tzmin > tmax)) return false;
+    if (tzmin > tmin) tmin = tzmin;
+    if (tzmax < tmax) tmax = tzmax;
+    return true;
+}
+
+// camera.h:20-21, 40-45: perspective ray direction. The per-frame constants fov_xs
+// (= (float)tan(double), hazard H5), aspect and the origin are computed on the host.
+__device__ __forceinline__ void gen_dir(const float* m, float fov_xs, float aspect, uint32_t px, uint32_t py,
+                                        uint32_t W, uint32_t H, float sx, float sy,
+                                        float& dx, float& dy, float& dz)
+{
+    const float ndc_x = (float(px) + sx) / float(W) * 2.0f - 1.0f;
+    const float ndc_y = (float(py) + sy) / float(H) * 2.0f - 1.0f;
+    float x = ndc_x * fov_xs, y = ndc_y * fov_xs / aspect, z = -1.0f;
+    normalize3(x, y, z);
+    // lin_alg.h:495-509 Transf3x3 (row-vector convention: m[r][c], r = input component)
+    dx = x * m[0] + y * m[3] + z * m[6];
+    dy = x * m[1] + y * m[4] + z * m[7];
+    dz = x * m[2] + y * m[5] + z * m[8];
+}
+
+// triangle.h:158-161 + lin_alg.h:151-156 + renderer.cpp:148-155
+__device__ __forceinline__ void shade_hit(float u, float v, const float4& a, const float4& b, const float4& c,
+                                          float& r, float& g, float& bl)
+{
+    // a = {n0.x, n0.y, n0.z, n1.x}, b = {n1.y, n1.z, n2.x, n2.y}, c = {n2.z, -, -, -}
+    const float w = 1.0f - u - v;
+    float x = a.w * u + b.z * v + a.x * w;
+    float y = b.x * u + b.w * v + a.y * w;
+    float z = b.y * u + c.x * v + a.z * w;
+    normalize3(x, y, z);
+    r = (x + 1.0f) * 0.5f;
+    g = (y + 1.0f) * 0.5f;
+    bl = (z + 1.0f) * 0.5f;
+}
+
+} // namespace rtd

@@ -1,0 +1,947 @@
+// rt_tracer.hip -- HIP kernels + C ABI (include/rt_tracer.h) for gfx950 (MI355X).
+//
+// One launch renders a whole frame (or one rank's shard): a workgroup of 256 lanes owns
+// 256/spp pixels of a 16x16 pixel tile in Morton order, one lane per sample, so a pixel's
+// samples sit in adjacent lanes and a wave covers a compact 2^k x 2^k pixel block (coherent
+// DDA walks).  Each lane runs the reference's per-sample path (GenerateRay -> Grid::Intersect
+// -> IntersectRayTri -> shading); the pixel's samples are then summed IN SAMPLE ORDER across
+// lanes (renderer.cpp:125-160, hazard H10), averaged, gamma'd and packed (renderer.cpp:162-171).
+//
+// Scene layout in HBM (built once by rt_scene_create):
+//   cell_off  u32[C+1]            CSR offsets in GridIdx order (grid.h:41-42)
+//   refs      float4[3*R]         one 48-B record per CSR reference, in CSR order:
+//                                 {v0.xyz, e1.x} {e1.yz, e2.xy} {e2.z, tri_idx bits, 0, 0}
+//                                 -> a cell's triangle list streams contiguously, no
+//                                 index indirection, 3 dwordx4 loads per test
+//   shade     float4[3*T]         per triangle the 3 vertex normals (shading of a hit)
+//   face_n    float4[T]           face normal (IntersectRayTriBarycentric only)
+//   occ       u32[ceil(C/32)]     1 bit per non-empty cell; staged into LDS per workgroup so
+//                                 the DDA skips empty cells without touching HBM/L2
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/rt_tracer.h"
+#include "rt_device.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg)
+{
+    g_err = msg;
+    return code;
+}
+
+#define RT_HIP(expr)                                                                      \
+    do {                                                                                  \
+        hipError_t e_ = (expr);                                                           \
+        if (e_ != hipSuccess)                                                             \
+            return fail(RT_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));     \
+    } while (0)
+
+constexpr uint32_t kTile = 16;              // shard / scheduling tile edge (pixels)
+constexpr uint32_t kTilePix = kTile * kTile;
+constexpr uint32_t kWG = 256;               // lanes per workgroup
+constexpr uint32_t kMaxOccWords = 8192;     // LDS occupancy bitmap: up to 262,144 cells (64^3)
+
+struct KParams
+{
+    // camera (per frame)
+    float m[9];                 // Matrix44f m_mat[r][c], r,c < 3, row-major
+    float fov_xs, aspect;
+    float org[3];               // Transf4x4(Vec3f(0)) computed on the host (camera.h:39)
+    uint32_t W, H, spp, spp_shift;
+    const float2 *smp;          // [spp] sample offsets
+    // grid (grid.h:28-39)
+    float bmin[3], bmax[3];
+    float cw, icw;
+    int dim[3];
+    int dxdz;
+    uint32_t max_steps;         // safety bound: no DDA walk is longer than dx+dy+dz
+    uint32_t occ_words;         // 0 disables the LDS occupancy bitmap
+    const uint32_t *off;
+    const float4 *refs;
+    const float4 *shade;
+    const float4 *face_n;
+    const uint32_t *occ;
+    uint32_t tri_test;
+    // work decomposition
+    uint32_t rx0, ry0, rw, rh;  // region of the frame rendered by this launch
+    uint32_t tiles_x;           // 16x16 tiles across the region
+    uint32_t rank, nranks;      // tile t is ours iff t % nranks == rank, local index t / nranks
+    uint32_t wg_per_tile;
+    // output
+    uint32_t *out;
+    uint32_t pitch;             // frame mode: words per row of out
+    uint32_t shard_mode;        // 1: out[local_tile * 256 + ty*16 + tx]
+    rt_sample_rec *recs;        // debug kernel only
+    uint32_t rec_x0, rec_y0, rec_w, rec_h;
+};
+
+// Morton decode of an 8-bit index inside a 16x16 tile: x = even bits, y = odd bits.
+__device__ __forceinline__ uint32_t compact_bits(uint32_t v)
+{
+    v &= 0x55u;
+    v = (v | (v >> 1)) & 0x33u;
+    v = (v | (v >> 2)) & 0x0Fu;
+    return v;
+}
+
+// grid.cpp:159-281 Grid::Intersect (NEW_GRID_TRAVERSAL), axis arrays unrolled into scalars
+// so nothing is runtime-indexed (no scratch).  Counters are compiled in only for records.
+template <bool STATS>
+__device__ __forceinline__ bool grid_intersect(const KParams& P, const uint32_t *lds_occ,
+                                               float ox, float oy, float oz,
+                                               float dx, float dy, float dz,
+                                               float& t, float& u, float& v, uint32_t& tri,
+                                               uint32_t& voxel, uint32_t& steps, uint32_t& tests)
+{
+    float enter_t, leave_t, gx, gy, gz;
+    if (rtd::point_in_aabb(ox, oy, oz, P.bmin, P.bmax))
+    {
+        enter_t = 0.0f;
+        gx = ox; gy = oy; gz = oz;
+    }
+    else if (rtd::ray_aabb(ox, oy, oz, dx, dy, dz, P.bmin, P.bmax, enter_t, leave_t))
+    {
+        gx = ox + dx * enter_t;
+        gy = oy + dy * enter_t;
+        gz = oz + dz * enter_t;
+    }
+    else
+        return false;
+
+    // grid.h:44-48 ToVoxel, grid.h:50-51 ToPos, grid.cpp:190-216 per-axis setup
+    auto to_voxel = [&](float g, int a) {
+        const int vx = rtd::cvt_i32_x86((g - P.bmin[a]) * P.icw);
+        const int hi = P.dim[a] - 1;
+        return vx < 0 ? 0 : (vx > hi ? hi : vx);
+    };
+    int pos0 = to_voxel(gx, 0), pos1 = to_voxel(gy, 1), pos2 = to_voxel(gz, 2);
+    float nct0, nct1, nct2, dt0 = 0.0f, dt1 = 0.0f, dt2 = 0.0f;
+    int st0 = 0, st1 = 0, st2 = 0, out0 = 0, out1 = 0, out2 = 0;
+    auto setup = [&](float d, float g, int pos, int a, float& nct, float& dtv, int& st, int& outv) {
+        if (d == 0.0f)
+            nct = rtd::kFltMax;
+        else if (d > 0.0f)
+        {
+            nct = enter_t + ((P.bmin[a] + float(pos + 1) * P.cw) - g) / d;
+            dtv = P.cw / d;
+            st = 1;
+            outv = P.dim[a];
+        }
+        else
+        {
+            nct = enter_t + ((P.bmin[a] + float(pos) * P.cw) - g) / d;
+            dtv = -P.cw / d;
+            st = -1;
+            outv = -1;
+        }
+    };
+    setup(dx, gx, pos0, 0, nct0, dt0, st0, out0);
+    setup(dy, gy, pos1, 1, nct1, dt1, st1, out1);
+    setup(dz, gz, pos2, 2, nct2, dt2, st2, out2);
+
+    int cell = pos0 + pos2 * P.dim[0] + pos1 * P.dxdz;
+    t = rtd::kFltMax;
+    for (uint32_t iter = 0; iter < P.max_steps; iter++)
+    {
+        const int ax = (nct0 < nct1) ? ((nct0 < nct2) ? 0 : 2) : ((nct1 < nct2) ? 1 : 2);
+        const float nct_ax = ax == 0 ? nct0 : (ax == 1 ? nct1 : nct2);
+        if (STATS) { voxel = uint32_t(cell); steps++; }
+
+        const bool occupied = lds_occ ? ((lds_occ[uint32_t(cell) >> 5] >> (uint32_t(cell) & 31u)) & 1u) != 0u
+                                      : true;
+        if (occupied)
+        {
+            const uint32_t kb = P.off[cell], ke = P.off[cell + 1];
+            for (uint32_t k = kb; k < ke; k++)
+            {
+                const float4 r0 = P.refs[3 * k + 0];
+                const float4 r1 = P.refs[3 * k + 1];
+                const float4 r2 = P.refs[3 * k + 2];
+                const uint32_t id = __float_as_uint(r2.y);
+                float ct, cu, cv;
+                bool hit;
+                if (P.tri_test == RT_TRI_BARYCENTRIC)
+                {
+                    const float4 fn = P.face_n[id];
+                    hit = rtd::ray_tri_bary(ox, oy, oz, dx, dy, dz, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y,
+                                            r1.z, r1.w, r2.x, fn.x, fn.y, fn.z, ct, cu, cv);
+                }
+                else
+                    hit = rtd::ray_tri_mt(ox, oy, oz, dx, dy, dz, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y,
+                                          r1.z, r1.w, r2.x, ct, cu, cv);
+                if (STATS) tests++;
+                // grid.cpp:258-266: strict '<' over the ascending list keeps the first of ties
+                if (hit && ct < t && ct < nct_ax)
+                {
+                    t = ct; u = cu; v = cv; tri = id;
+                }
+            }
+            if (t != rtd::kFltMax) return true;               // grid.cpp:270-271
+        }
+        // grid.cpp:274-277
+        if (ax == 0)
+        {
+            pos0 += st0;
+            if (pos0 == out0) break;
+            nct0 += dt0;
+            cell += st0;
+        }
+        else if (ax == 1)
+        {
+            pos1 += st1;
+            if (pos1 == out1) break;
+            nct1 += dt1;
+            cell += st1 * P.dxdz;
+        }
+        else
+        {
+            pos2 += st2;
+            if (pos2 == out2) break;
+            nct2 += dt2;
+            cell += st2 * P.dim[0];
+        }
+    }
+    return false;
+}
+
+// renderer.cpp:126-160: one sample -> its colour contribution
+template <bool STATS>
+__device__ __forceinline__ void trace_sample(const KParams& P, const uint32_t *lds_occ, uint32_t px, uint32_t py,
+                                             uint32_t s, float& cr, float& cg, float& cb,
+                                             rt_sample_rec *rec)
+{
+    const float2 so = P.smp[s];
+    float dx, dy, dz;
+    rtd::gen_dir(P.m, P.fov_xs, P.aspect, px, py, P.W, P.H, so.x, so.y, dx, dy, dz);
+    float t = 0.0f, u = 0.0f, v = 0.0f;
+    uint32_t tri = rtd::kNoTri, voxel = rtd::kNoTri, steps = 0, tests = 0;
+    const bool hit = grid_intersect<STATS>(P, lds_occ, P.org[0], P.org[1], P.org[2], dx, dy, dz,
+                                           t, u, v, tri, voxel, steps, tests);
+    if (hit)
+    {
+        const float4 a = P.shade[3 * tri + 0], b = P.shade[3 * tri + 1], c = P.shade[3 * tri + 2];
+        rtd::shade_hit(u, v, a, b, c, cr, cg, cb);
+    }
+    else
+    {
+        const float m = float(py) / float(P.H);                  // renderer.cpp:159
+        cr = cg = cb = m;
+    }
+    if (STATS)
+    {
+        rec->hit = hit;
+        rec->tri = hit ? tri : rtd::kNoTri;
+        rec->voxel = voxel;
+        rec->steps = steps;
+        rec->tests = tests;
+        rec->t = hit ? t : 0.0f;
+        rec->u = hit ? u : 0.0f;
+        rec->v = hit ? v : 0.0f;
+        rec->r = cr; rec->g = cg; rec->b = cb;
+        rec->pad = 0;
+    }
+}
+
+__device__ __forceinline__ void stage_occupancy(const KParams& P, uint32_t *lds_occ)
+{
+    for (uint32_t i = threadIdx.x; i < P.occ_words; i += blockDim.x)
+        lds_occ[i] = P.occ[i];
+    __syncthreads();
+}
+
+// Tile bookkeeping shared by both render kernels: block -> (local tile k, sub-block)
+struct TileCoord { uint32_t k, sub, tx0, ty0; };
+
+__device__ __forceinline__ TileCoord tile_of_block(const KParams& P)
+{
+    TileCoord c;
+    c.k = blockIdx.x / P.wg_per_tile;
+    c.sub = blockIdx.x - c.k * P.wg_per_tile;
+    const uint32_t t = P.rank + c.k * P.nranks;
+    const uint32_t tyi = t / P.tiles_x;
+    c.tx0 = P.rx0 + (t - tyi * P.tiles_x) * kTile;
+    c.ty0 = P.ry0 + tyi * kTile;
+    return c;
+}
+
+__device__ __forceinline__ void store_pixel(const KParams& P, const TileCoord& c, uint32_t p, uint32_t x,
+                                            uint32_t y, uint32_t word)
+{
+    if (P.shard_mode)
+        P.out[size_t(c.k) * kTilePix + compact_bits(p >> 1) * kTile + compact_bits(p)] = word;
+    else
+        P.out[size_t(y - P.ry0) * P.pitch + (x - P.rx0)] = word;
+}
+
+// RT_KERNEL_LANES: one lane per sample (spp = 2^spp_shift <= 64)
+__global__ void __launch_bounds__(kWG) k_render_lanes(KParams P)
+{
+    const uint32_t *lds_occ = nullptr;   // occupancy staging pays only in the persistent kernel
+    const bool use_occ = false;
+
+    const TileCoord c = tile_of_block(P);
+    const uint32_t slot = c.sub * kWG + threadIdx.x;
+    const uint32_t p = slot >> P.spp_shift;                   // pixel index in the tile (Morton)
+    const uint32_t s = slot & (P.spp - 1u);
+    const uint32_t x = c.tx0 + compact_bits(p), y = c.ty0 + compact_bits(p >> 1);
+    const bool valid = x < P.rx0 + P.rw && y < P.ry0 + P.rh;
+
+    float cr = 0.0f, cg = 0.0f, cb = 0.0f;
+    if (valid)
+        trace_sample<false>(P, use_occ ? lds_occ : nullptr, x, y, s, cr, cg, cb, nullptr);
+
+    // Sum the pixel's samples in sample order (renderer.cpp:125-160): lanes base..base+spp-1
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t base = lane & ~(P.spp - 1u);
+    float sr = 0.0f, sg = 0.0f, sb = 0.0f;
+    for (uint32_t k = 0; k < P.spp; k++)
+    {
+        sr += __shfl(cr, int(base + k), 64);
+        sg += __shfl(cg, int(base + k), 64);
+        sb += __shfl(cb, int(base + k), 64);
+    }
+    if (valid && s == 0)
+    {
+        const float fs = float(P.spp);
+        const uint32_t word = rtd::pack_bgra8(rtd::gamma_half(sr / fs), rtd::gamma_half(sg / fs),
+                                              rtd::gamma_half(sb / fs));
+        store_pixel(P, c, p, x, y, word);
+    }
+}
+
+// RT_KERNEL_PIXEL_LOOP: one lane per pixel, samples looped in order (any spp)
+__global__ void __launch_bounds__(kWG) k_render_pixel_loop(KParams P)
+{
+    const uint32_t *lds_occ = nullptr;
+    const bool use_occ = false;
+
+    const TileCoord c = tile_of_block(P);
+    const uint32_t p = threadIdx.x;
+    const uint32_t x = c.tx0 + compact_bits(p), y = c.ty0 + compact_bits(p >> 1);
+    if (!(x < P.rx0 + P.rw && y < P.ry0 + P.rh)) return;
+    float sr = 0.0f, sg = 0.0f, sb = 0.0f;
+    for (uint32_t s = 0; s < P.spp; s++)
+    {
+        float cr, cg, cb;
+        trace_sample<false>(P, use_occ ? lds_occ : nullptr, x, y, s, cr, cg, cb, nullptr);
+        sr += cr; sg += cg; sb += cb;
+    }
+    const float fs = float(P.spp);
+    store_pixel(P, c, p, x, y, rtd::pack_bgra8(rtd::gamma_half(sr / fs), rtd::gamma_half(sg / fs),
+                                               rtd::gamma_half(sb / fs)));
+}
+
+// Debug records: one thread per sample of the rectangle, order (y, x, s)
+__global__ void __launch_bounds__(kWG) k_trace_records(KParams P, uint32_t n)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t s = i % P.spp, pix = i / P.spp;
+    const uint32_t x = P.rec_x0 + pix % P.rec_w, y = P.rec_y0 + pix / P.rec_w;
+    float cr, cg, cb;
+    trace_sample<true>(P, nullptr, x, y, s, cr, cg, cb, &P.recs[i]);
+}
+
+// K3: gathered shards [rank][local tile][256] -> frame
+__global__ void __launch_bounds__(kWG) k_unshard(const uint32_t *g, uint32_t *out, uint32_t W, uint32_t H,
+                                                 uint32_t tiles_x, uint32_t nranks, uint64_t shard_elems)
+{
+    const uint32_t x = blockIdx.x * 64 + (threadIdx.x & 63u);
+    const uint32_t y = blockIdx.y * 4 + (threadIdx.x >> 6);
+    if (x >= W || y >= H) return;
+    const uint32_t t = (y / kTile) * tiles_x + x / kTile;
+    const uint32_t r = t % nranks, k = t / nranks;
+    out[size_t(y) * W + x] = g[r * shard_elems + size_t(k) * kTilePix + (y % kTile) * kTile + (x % kTile)];
+}
+
+// Device KATs (rt_debug_primitives)
+__global__ void __launch_bounds__(kWG) k_primitives(int kind, const float *in, uint32_t n, float *out)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (kind == 0)
+    {
+        const float *a = in + 18 * i;
+        float *o = out + 8 * i;
+        const float e1x = a[9] - a[6], e1y = a[10] - a[7], e1z = a[11] - a[8];
+        const float e2x = a[12] - a[6], e2y = a[13] - a[7], e2z = a[14] - a[8];
+        float t = __builtin_nanf(""), u = t, v = t;
+        const bool h = rtd::ray_tri_mt(a[0], a[1], a[2], a[3], a[4], a[5], a[6], a[7], a[8],
+                                       e1x, e1y, e1z, e2x, e2y, e2z, t, u, v);
+        o[0] = __uint_as_float(h); o[1] = t; o[2] = u; o[3] = v;
+        float bt = __builtin_nanf(""), bu = bt, bv = bt;
+        const bool hb = rtd::ray_tri_bary(a[0], a[1], a[2], a[3], a[4], a[5], a[6], a[7], a[8],
+                                          e1x, e1y, e1z, e2x, e2y, e2z, a[15], a[16], a[17], bt, bu, bv);
+        o[4] = __uint_as_float(hb); o[5] = bt; o[6] = bu; o[7] = bv;
+    }
+    else if (kind == 1)
+    {
+        const float *a = in + 12 * i;
+        float *o = out + 4 * i;
+        float t0 = __builtin_nanf(""), t1 = t0;
+        const bool h = rtd::ray_aabb(a[0], a[1], a[2], a[3], a[4], a[5], a + 6, a + 9, t0, t1);
+        o[0] = __uint_as_float(h); o[1] = t0; o[2] = t1;
+        o[3] = __uint_as_float(rtd::point_in_aabb(a[0], a[1], a[2], a + 6, a + 9));
+    }
+    else if (kind == 2)
+    {
+        // camera inputs: cam[16], px, py, W, H (u32 bits), sx, sy, fov; constants as the host does
+        const float *a = in + 23 * i;
+        float *o = out + 6 * i;
+        const float m[9] = { a[0], a[1], a[2], a[4], a[5], a[6], a[8], a[9], a[10] };
+        const uint32_t W = __float_as_uint(a[18]), H = __float_as_uint(a[19]);
+        const float fov_xs = a[22];          // replaced on the host by (float)tan(double) (H5)
+        const float aspect = float(W) / float(H);
+        float dx, dy, dz;
+        rtd::gen_dir(m, fov_xs, aspect, __float_as_uint(a[16]), __float_as_uint(a[17]), W, H, a[20], a[21],
+                     dx, dy, dz);
+        o[0] = 0.0f * a[0] + 0.0f * a[4] + 0.0f * a[8] + a[12];
+        o[1] = 0.0f * a[1] + 0.0f * a[5] + 0.0f * a[9] + a[13];
+        o[2] = 0.0f * a[2] + 0.0f * a[6] + 0.0f * a[10] + a[14];
+        o[3] = dx; o[4] = dy; o[5] = dz;
+    }
+    else if (kind == 3)
+    {
+        const float *a = in + 3 * i;
+        float *o = out + 4 * i;
+        const float r = rtd::gamma_half(a[0]), g = rtd::gamma_half(a[1]), b = rtd::gamma_half(a[2]);
+        o[0] = r; o[1] = g; o[2] = b; o[3] = __uint_as_float(rtd::pack_bgra8(r, g, b));
+    }
+    else if (kind == 4)
+    {
+        const float *a = in + 11 * i;
+        float *o = out + 3 * i;
+        const float4 A = make_float4(a[2], a[3], a[4], a[5]);
+        const float4 B = make_float4(a[6], a[7], a[8], a[9]);
+        const float4 C = make_float4(a[10], 0.0f, 0.0f, 0.0f);
+        rtd::shade_hit(a[0], a[1], A, B, C, o[0], o[1], o[2]);
+    }
+}
+
+// ------------------------------------------------------------------------ host side
+// sampling.h:113-120, sampling.cpp:194-210 (base 2), renderer.cpp:90-93
+void hammersley(uint32_t spp, std::vector<float>& xy)
+{
+    xy.resize(size_t(spp) * 2);
+    for (uint32_t s = 0; s < spp; s++)
+    {
+        double val = 0.0, inv_i = 0.5;
+        for (uint32_t n = s; n > 0; n /= 2)
+        {
+            val += (n % 2) * inv_i;
+            inv_i *= 0.5;
+        }
+        xy[2 * s + 0] = float(double(s) / double(spp) - 0.5f);
+        xy[2 * s + 1] = float(val - 0.5f);
+    }
+}
+
+bool is_pow2(uint32_t x) { return x && !(x & (x - 1)); }
+
+uint32_t log2u(uint32_t x)
+{
+    uint32_t r = 0;
+    while ((1u << r) < x) r++;
+    return r;
+}
+
+} // namespace
+
+struct rt_scene
+{
+    int device = 0;
+    std::mutex mtx;
+    uint32_t dims[3] = { 0, 0, 0 };
+    float bmin[3], bmax[3], cw = 0, icw = 0;
+    uint32_t ncells = 0, nrefs = 0, ntris = 0, occ_words = 0;
+    uint32_t *d_off = nullptr, *d_occ = nullptr;
+    float4 *d_refs = nullptr, *d_shade = nullptr, *d_facen = nullptr;
+    uint64_t device_bytes = 0;
+    // sample table cache
+    float2 *d_smp = nullptr;
+    uint32_t smp_cap = 0;
+    std::vector<float> smp_host;
+    float *h_smp_pinned = nullptr;
+    // internal stream + timing events
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool ev_recorded = false;
+    // staging for rt_render_tiles / records
+    uint32_t *d_frame = nullptr;
+    size_t frame_cap = 0;
+    uint32_t *h_frame = nullptr;
+    size_t hframe_cap = 0;
+};
+
+namespace {
+
+int ensure_device(const rt_scene *s)
+{
+    int cur = -1;
+    RT_HIP(hipGetDevice(&cur));
+    if (cur != s->device) RT_HIP(hipSetDevice(s->device));
+    return RT_OK;
+}
+
+// Uploads the frame's sample table if it differs from the cached one.
+int prepare_samples(rt_scene *s, const rt_frame *f, uint32_t spp)
+{
+    std::vector<float> tbl;
+    if (f->sample_offsets)
+        tbl.assign(f->sample_offsets, f->sample_offsets + 2 * size_t(spp));
+    else
+        hammersley(spp, tbl);
+    if (tbl == s->smp_host) return RT_OK;
+    if (spp > s->smp_cap)
+    {
+        if (s->d_smp) RT_HIP(hipFree(s->d_smp));
+        if (s->h_smp_pinned) RT_HIP(hipHostFree(s->h_smp_pinned));
+        s->d_smp = nullptr;
+        s->h_smp_pinned = nullptr;
+        const uint32_t cap = std::max<uint32_t>(64, spp);
+        RT_HIP(hipMalloc(&s->d_smp, sizeof(float2) * cap));
+        RT_HIP(hipHostMalloc(&s->h_smp_pinned, sizeof(float2) * cap));
+        s->smp_cap = cap;
+    }
+    std::memcpy(s->h_smp_pinned, tbl.data(), tbl.size() * sizeof(float));
+    RT_HIP(hipMemcpy(s->d_smp, s->h_smp_pinned, tbl.size() * sizeof(float), hipMemcpyHostToDevice));
+    s->smp_host = tbl;
+    return RT_OK;
+}
+
+int validate_frame(const rt_frame *f)
+{
+    if (!f) return fail(RT_E_INVALID, "frame is NULL");
+    if (f->width == 0 || f->height == 0 || f->width > 65536 || f->height > 65536)
+        return fail(RT_E_INVALID, "frame width/height must be in [1, 65536]");
+    if (f->tri_test > RT_TRI_BARYCENTRIC) return fail(RT_E_INVALID, "unknown tri_test");
+    if (f->kernel > RT_KERNEL_COMPACT) return fail(RT_E_INVALID, "unknown kernel");
+    const uint32_t spp = std::max(1u, f->spp);
+    if (spp > 4096) return fail(RT_E_INVALID, "spp must be <= 4096");
+    if (f->kernel == RT_KERNEL_LANES && !(is_pow2(spp) && spp <= 64))
+        return fail(RT_E_INVALID, "RT_KERNEL_LANES needs spp to be a power of two <= 64");
+    return RT_OK;
+}
+
+// Fills the per-frame parameters (camera constants exactly as camera.h computes them).
+void frame_params(const rt_scene *s, const rt_frame *f, KParams& P)
+{
+    std::memset(&P, 0, sizeof(P));
+    const float (*c)[4] = reinterpret_cast<const float (*)[4]>(f->cam);
+    for (int r = 0; r < 3; r++)
+        for (int k = 0; k < 3; k++) P.m[3 * r + k] = c[r][k];
+    const float hfov = f->fov * float(0.0174532925);           // lin_alg.h:232 DegToRad
+    P.fov_xs = float(::tan(double(hfov / 2.0f)));               // camera.h:42, double tan (H5)
+    P.aspect = float(f->width) / float(f->height);
+    for (int k = 0; k < 3; k++)                                 // lin_alg.h:518-535
+        P.org[k] = 0.0f * c[0][k] + 0.0f * c[1][k] + 0.0f * c[2][k] + c[3][k];
+    P.W = f->width;
+    P.H = f->height;
+    P.spp = std::max(1u, f->spp);
+    P.spp_shift = is_pow2(P.spp) ? log2u(P.spp) : 0;
+    P.smp = s->d_smp;
+    for (int a = 0; a < 3; a++)
+    {
+        P.bmin[a] = s->bmin[a];
+        P.bmax[a] = s->bmax[a];
+        P.dim[a] = int(s->dims[a]);
+    }
+    P.cw = s->cw;
+    P.icw = s->icw;
+    P.dxdz = int(s->dims[0] * s->dims[2]);
+    P.max_steps = s->dims[0] + s->dims[1] + s->dims[2] + 3;
+    P.occ_words = s->occ_words <= kMaxOccWords ? s->occ_words : 0;
+    P.off = s->d_off;
+    P.refs = s->d_refs;
+    P.shade = s->d_shade;
+    P.face_n = s->d_facen;
+    P.occ = s->d_occ;
+    P.tri_test = f->tri_test;
+}
+
+bool use_lanes(const rt_frame *f, uint32_t spp)
+{
+    if (f->kernel == RT_KERNEL_PIXEL_LOOP) return false;
+    return is_pow2(spp) && spp <= 64;
+}
+
+// Launches the render kernel over region/shard described by P (tiles_x, rank, ...).
+int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_tiles, hipStream_t st)
+{
+    if (n_local_tiles == 0) return RT_OK;
+    const bool lanes = use_lanes(f, P.spp);
+    P.wg_per_tile = lanes ? (kTilePix * P.spp) / kWG : 1;
+    if (lanes && P.wg_per_tile == 0) P.wg_per_tile = 1;
+    // lanes mode with spp < ... : 256 * spp / 256 = spp workgroups per tile (spp >= 1)
+    const uint64_t blocks = uint64_t(n_local_tiles) * P.wg_per_tile;
+    if (blocks > 0x7FFFFFFFull) return fail(RT_E_INVALID, "frame too large for one launch");
+    RT_HIP(hipEventRecord(s->ev0, st));
+    if (lanes)
+        hipLaunchKernelGGL(k_render_lanes, dim3(uint32_t(blocks)), dim3(kWG), 0, st, P);
+    else
+        hipLaunchKernelGGL(k_render_pixel_loop, dim3(uint32_t(blocks)), dim3(kWG), 0, st, P);
+    RT_HIP(hipGetLastError());
+    RT_HIP(hipEventRecord(s->ev1, st));
+    s->ev_recorded = true;
+    return RT_OK;
+}
+
+} // namespace
+
+extern "C" {
+
+int rt_abi_version(void) { return RT_ABI_VERSION; }
+
+int rt_last_error(char *buf, size_t len)
+{
+    if (!buf || len == 0) return RT_E_INVALID;
+    std::snprintf(buf, len, "%s", g_err.c_str());
+    return RT_OK;
+}
+
+int rt_get_device_count(int *count)
+{
+    if (!count) return fail(RT_E_INVALID, "count is NULL");
+    *count = 0;
+    RT_HIP(hipGetDeviceCount(count));
+    return RT_OK;
+}
+
+int rt_sample_table(uint32_t spp, float *out_xy)
+{
+    if (!out_xy || spp == 0) return fail(RT_E_INVALID, "bad arguments");
+    std::vector<float> t;
+    hammersley(spp, t);
+    std::memcpy(out_xy, t.data(), t.size() * sizeof(float));
+    return RT_OK;
+}
+
+int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
+{
+    if (!d || !out) return fail(RT_E_INVALID, "desc/out is NULL");
+    *out = nullptr;
+    const rt_grid_desc& g = d->grid;
+    if (d->num_triangles == 0 || d->num_vertices == 0 || !d->vertices || !d->triangles)
+        return fail(RT_E_INVALID, "empty mesh");
+    if (!g.cell_offsets || g.dims[0] == 0 || g.dims[1] == 0 || g.dims[2] == 0)
+        return fail(RT_E_INVALID, "empty grid");
+    const uint64_t nc64 = uint64_t(g.dims[0]) * g.dims[1] * g.dims[2];
+    if (nc64 >= 0x7FFFFFFFull) return fail(RT_E_INVALID, "grid too large");
+    const uint32_t nc = uint32_t(nc64);
+    if (g.cell_offsets[0] != 0) return fail(RT_E_INVALID, "cell_offsets[0] != 0");
+    for (uint32_t c = 0; c < nc; c++)
+        if (g.cell_offsets[c + 1] < g.cell_offsets[c]) return fail(RT_E_INVALID, "cell_offsets not monotonic");
+    const uint32_t nr = g.cell_offsets[nc];
+    if (nr && !g.cell_tris) return fail(RT_E_INVALID, "cell_tris is NULL");
+    for (uint32_t k = 0; k < nr; k++)
+        if (g.cell_tris[k] >= d->num_triangles) return fail(RT_E_INVALID, "cell_tris index out of range");
+    for (uint32_t i = 0; i < d->num_triangles; i++)
+    {
+        const rt_triangle& t = d->triangles[i];
+        if (t.v0 >= d->num_vertices || t.v1 >= d->num_vertices || t.v2 >= d->num_vertices)
+            return fail(RT_E_INVALID, "triangle vertex index out of range");
+    }
+    int ndev = 0;
+    RT_HIP(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return fail(RT_E_NODEVICE, "device index out of range / no GPU");
+    hipDeviceProp_t prop;
+    RT_HIP(hipGetDeviceProperties(&prop, device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(RT_E_NODEVICE, std::string("librt_tracer is built for gfx950, device is ") + prop.gcnArchName);
+    RT_HIP(hipSetDevice(device));
+
+    std::unique_ptr<rt_scene> s(new rt_scene());
+    s->device = device;
+    for (int a = 0; a < 3; a++)
+    {
+        s->dims[a] = g.dims[a];
+        s->bmin[a] = g.aabb_min[a];
+        s->bmax[a] = g.aabb_max[a];
+    }
+    s->cw = g.cell_wdh;
+    s->icw = g.inv_cell_wdh;
+    s->ncells = nc;
+    s->nrefs = nr;
+    s->ntris = d->num_triangles;
+
+    // Per-reference triangle records in CSR order (see file header)
+    std::vector<float4> refs(size_t(std::max(nr, 1u)) * 3);
+    for (uint32_t k = 0; k < nr; k++)
+    {
+        const uint32_t ti = g.cell_tris[k];
+        const rt_triangle& t = d->triangles[ti];
+        const float *p0 = d->vertices[t.v0].p, *p1 = d->vertices[t.v1].p, *p2 = d->vertices[t.v2].p;
+        const float e1[3] = { p1[0] - p0[0], p1[1] - p0[1], p1[2] - p0[2] };  // triangle.h:41
+        const float e2[3] = { p2[0] - p0[0], p2[1] - p0[1], p2[2] - p0[2] };  // triangle.h:42
+        float idf;
+        std::memcpy(&idf, &ti, 4);
+        refs[3 * size_t(k) + 0] = make_float4(p0[0], p0[1], p0[2], e1[0]);
+        refs[3 * size_t(k) + 1] = make_float4(e1[1], e1[2], e2[0], e2[1]);
+        refs[3 * size_t(k) + 2] = make_float4(e2[2], idf, 0.0f, 0.0f);
+    }
+    std::vector<float4> shade(size_t(d->num_triangles) * 3), facen(d->num_triangles);
+    for (uint32_t i = 0; i < d->num_triangles; i++)
+    {
+        const rt_triangle& t = d->triangles[i];
+        const float *n0 = d->vertices[t.v0].n, *n1 = d->vertices[t.v1].n, *n2 = d->vertices[t.v2].n;
+        shade[3 * size_t(i) + 0] = make_float4(n0[0], n0[1], n0[2], n1[0]);
+        shade[3 * size_t(i) + 1] = make_float4(n1[1], n1[2], n2[0], n2[1]);
+        shade[3 * size_t(i) + 2] = make_float4(n2[2], 0.0f, 0.0f, 0.0f);
+        facen[i] = make_float4(t.n[0], t.n[1], t.n[2], 0.0f);
+    }
+    s->occ_words = (nc + 31) / 32;
+    std::vector<uint32_t> occ(s->occ_words, 0);
+    for (uint32_t c = 0; c < nc; c++)
+        if (g.cell_offsets[c + 1] != g.cell_offsets[c]) occ[c >> 5] |= 1u << (c & 31);
+
+    RT_HIP(hipMalloc(&s->d_off, sizeof(uint32_t) * (nc + 1)));
+    RT_HIP(hipMalloc(&s->d_refs, sizeof(float4) * refs.size()));
+    RT_HIP(hipMalloc(&s->d_shade, sizeof(float4) * shade.size()));
+    RT_HIP(hipMalloc(&s->d_facen, sizeof(float4) * facen.size()));
+    RT_HIP(hipMalloc(&s->d_occ, sizeof(uint32_t) * occ.size()));
+    RT_HIP(hipMemcpy(s->d_off, g.cell_offsets, sizeof(uint32_t) * (nc + 1), hipMemcpyHostToDevice));
+    RT_HIP(hipMemcpy(s->d_refs, refs.data(), sizeof(float4) * refs.size(), hipMemcpyHostToDevice));
+    RT_HIP(hipMemcpy(s->d_shade, shade.data(), sizeof(float4) * shade.size(), hipMemcpyHostToDevice));
+    RT_HIP(hipMemcpy(s->d_facen, facen.data(), sizeof(float4) * facen.size(), hipMemcpyHostToDevice));
+    RT_HIP(hipMemcpy(s->d_occ, occ.data(), sizeof(uint32_t) * occ.size(), hipMemcpyHostToDevice));
+    s->device_bytes = sizeof(uint32_t) * (nc + 1) + sizeof(float4) * (refs.size() + shade.size() + facen.size()) +
+                      sizeof(uint32_t) * occ.size();
+    RT_HIP(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+    RT_HIP(hipEventCreate(&s->ev0));
+    RT_HIP(hipEventCreate(&s->ev1));
+    *out = s.release();
+    return RT_OK;
+}
+
+int rt_scene_destroy(rt_scene *s)
+{
+    if (!s) return RT_OK;
+    {
+        std::lock_guard<std::mutex> lk(s->mtx);
+        (void)hipSetDevice(s->device);
+        if (s->stream) (void)hipStreamSynchronize(s->stream);
+        (void)hipFree(s->d_off);
+        (void)hipFree(s->d_refs);
+        (void)hipFree(s->d_shade);
+        (void)hipFree(s->d_facen);
+        (void)hipFree(s->d_occ);
+        (void)hipFree(s->d_smp);
+        (void)hipFree(s->d_frame);
+        if (s->h_smp_pinned) (void)hipHostFree(s->h_smp_pinned);
+        if (s->h_frame) (void)hipHostFree(s->h_frame);
+        if (s->ev0) (void)hipEventDestroy(s->ev0);
+        if (s->ev1) (void)hipEventDestroy(s->ev1);
+        if (s->stream) (void)hipStreamDestroy(s->stream);
+    }
+    delete s;
+    return RT_OK;
+}
+
+int rt_scene_device_bytes(const rt_scene *s, uint64_t *bytes)
+{
+    if (!s || !bytes) return fail(RT_E_INVALID, "NULL argument");
+    *bytes = s->device_bytes;
+    return RT_OK;
+}
+
+int rt_render_frame_device(rt_scene *s, const rt_frame *f, uint32_t *d_bgra, void *hip_stream)
+{
+    if (!s || !d_bgra) return fail(RT_E_INVALID, "NULL argument");
+    int rc = validate_frame(f);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(s->mtx);
+    if ((rc = ensure_device(s))) return rc;
+    const uint32_t spp = std::max(1u, f->spp);
+    if ((rc = prepare_samples(s, f, spp))) return rc;
+    KParams P;
+    frame_params(s, f, P);
+    P.rx0 = 0; P.ry0 = 0; P.rw = f->width; P.rh = f->height;
+    P.tiles_x = (f->width + kTile - 1) / kTile;
+    const uint32_t tiles_y = (f->height + kTile - 1) / kTile;
+    P.rank = 0; P.nranks = 1;
+    P.out = d_bgra; P.pitch = f->width; P.shard_mode = 0;
+    return launch_render(s, f, P, P.tiles_x * tiles_y, static_cast<hipStream_t>(hip_stream));
+}
+
+int rt_shard_elems(uint32_t width, uint32_t height, uint32_t nranks, uint64_t *elems)
+{
+    if (!elems || nranks == 0 || width == 0 || height == 0) return fail(RT_E_INVALID, "bad arguments");
+    const uint64_t ntiles = uint64_t((width + kTile - 1) / kTile) * ((height + kTile - 1) / kTile);
+    *elems = ((ntiles + nranks - 1) / nranks) * kTilePix;
+    return RT_OK;
+}
+
+int rt_render_shard_device(rt_scene *s, const rt_frame *f, uint32_t rank, uint32_t nranks, uint32_t *d_shard,
+                           void *hip_stream)
+{
+    if (!s || !d_shard || nranks == 0 || rank >= nranks) return fail(RT_E_INVALID, "bad arguments");
+    int rc = validate_frame(f);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(s->mtx);
+    if ((rc = ensure_device(s))) return rc;
+    const uint32_t spp = std::max(1u, f->spp);
+    if ((rc = prepare_samples(s, f, spp))) return rc;
+    KParams P;
+    frame_params(s, f, P);
+    P.rx0 = 0; P.ry0 = 0; P.rw = f->width; P.rh = f->height;
+    P.tiles_x = (f->width + kTile - 1) / kTile;
+    const uint32_t ntiles = P.tiles_x * ((f->height + kTile - 1) / kTile);
+    P.rank = rank; P.nranks = nranks;
+    P.out = d_shard; P.pitch = 0; P.shard_mode = 1;
+    const uint32_t local = ntiles > rank ? (ntiles - rank + nranks - 1) / nranks : 0;
+    return launch_render(s, f, P, local, static_cast<hipStream_t>(hip_stream));
+}
+
+int rt_unshard_device(uint32_t width, uint32_t height, uint32_t nranks, const uint32_t *d_gathered,
+                      uint32_t *d_bgra, void *hip_stream)
+{
+    if (!d_gathered || !d_bgra || nranks == 0) return fail(RT_E_INVALID, "bad arguments");
+    uint64_t elems = 0;
+    int rc = rt_shard_elems(width, height, nranks, &elems);
+    if (rc) return rc;
+    const uint32_t tiles_x = (width + kTile - 1) / kTile;
+    hipLaunchKernelGGL(k_unshard, dim3((width + 63) / 64, (height + 3) / 4), dim3(kWG), 0,
+                       static_cast<hipStream_t>(hip_stream), d_gathered, d_bgra, width, height, tiles_x, nranks,
+                       elems);
+    RT_HIP(hipGetLastError());
+    return RT_OK;
+}
+
+int rt_last_kernel_ms(rt_scene *s, float *ms)
+{
+    if (!s || !ms) return fail(RT_E_INVALID, "NULL argument");
+    if (!s->ev_recorded) return fail(RT_E_INVALID, "no kernel recorded yet");
+    RT_HIP(hipEventSynchronize(s->ev1));
+    RT_HIP(hipEventElapsedTime(ms, s->ev0, s->ev1));
+    return RT_OK;
+}
+
+int rt_render_tiles(rt_scene *s, const rt_frame *f, const rt_tile *tiles, uint32_t n, uint32_t *const *bufs)
+{
+    if (!s || (n && (!tiles || !bufs))) return fail(RT_E_INVALID, "NULL argument");
+    int rc = validate_frame(f);
+    if (rc) return rc;
+    if (n == 0) return RT_OK;
+    uint32_t bx0 = 0xFFFFFFFFu, by0 = 0xFFFFFFFFu, bx1 = 0, by1 = 0;
+    for (uint32_t i = 0; i < n; i++)
+    {
+        const rt_tile& t = tiles[i];
+        if (!bufs[i] || t.x1 <= t.x0 || t.y1 <= t.y0 || t.x1 > f->width || t.y1 > f->height)
+            return fail(RT_E_INVALID, "tile outside the frame or empty");
+        bx0 = std::min(bx0, t.x0); by0 = std::min(by0, t.y0);
+        bx1 = std::max(bx1, t.x1); by1 = std::max(by1, t.y1);
+    }
+    std::lock_guard<std::mutex> lk(s->mtx);
+    if ((rc = ensure_device(s))) return rc;
+    const uint32_t spp = std::max(1u, f->spp);
+    if ((rc = prepare_samples(s, f, spp))) return rc;
+    const uint32_t rw = bx1 - bx0, rh = by1 - by0;
+    const size_t words = size_t(rw) * rh;
+    if (words > s->frame_cap)
+    {
+        if (s->d_frame) RT_HIP(hipFree(s->d_frame));
+        s->d_frame = nullptr;
+        RT_HIP(hipMalloc(&s->d_frame, words * 4));
+        s->frame_cap = words;
+    }
+    if (words > s->hframe_cap)
+    {
+        if (s->h_frame) RT_HIP(hipHostFree(s->h_frame));
+        s->h_frame = nullptr;
+        RT_HIP(hipHostMalloc(&s->h_frame, words * 4));
+        s->hframe_cap = words;
+    }
+    KParams P;
+    frame_params(s, f, P);
+    P.rx0 = bx0; P.ry0 = by0; P.rw = rw; P.rh = rh;
+    P.tiles_x = (rw + kTile - 1) / kTile;
+    P.rank = 0; P.nranks = 1;
+    P.out = s->d_frame; P.pitch = rw; P.shard_mode = 0;
+    if ((rc = launch_render(s, f, P, P.tiles_x * ((rh + kTile - 1) / kTile), s->stream))) return rc;
+    RT_HIP(hipMemcpyAsync(s->h_frame, s->d_frame, words * 4, hipMemcpyDeviceToHost, s->stream));
+    RT_HIP(hipStreamSynchronize(s->stream));
+    for (uint32_t i = 0; i < n; i++)                             // framebuffer.h:41-45 layout
+    {
+        const rt_tile& t = tiles[i];
+        const uint32_t tw = t.x1 - t.x0;
+        for (uint32_t y = t.y0; y < t.y1; y++)
+            std::memcpy(bufs[i] + size_t(y - t.y0) * tw, s->h_frame + size_t(y - by0) * rw + (t.x0 - bx0),
+                        size_t(tw) * 4);
+    }
+    return RT_OK;
+}
+
+int rt_trace_samples(rt_scene *s, const rt_frame *f, uint32_t x0, uint32_t y0, uint32_t w, uint32_t h,
+                     rt_sample_rec *out)
+{
+    if (!s || !out) return fail(RT_E_INVALID, "NULL argument");
+    int rc = validate_frame(f);
+    if (rc) return rc;
+    if (w == 0 || h == 0 || x0 + w > f->width || y0 + h > f->height)
+        return fail(RT_E_INVALID, "rectangle outside the frame");
+    std::lock_guard<std::mutex> lk(s->mtx);
+    if ((rc = ensure_device(s))) return rc;
+    const uint32_t spp = std::max(1u, f->spp);
+    if ((rc = prepare_samples(s, f, spp))) return rc;
+    const uint64_t n64 = uint64_t(w) * h * spp;
+    if (n64 > (1ull << 28)) return fail(RT_E_INVALID, "too many samples for one record call");
+    const uint32_t n = uint32_t(n64);
+    rt_sample_rec *d_rec = nullptr;
+    RT_HIP(hipMalloc(&d_rec, sizeof(rt_sample_rec) * n));
+    KParams P;
+    frame_params(s, f, P);
+    P.recs = d_rec;
+    P.rec_x0 = x0; P.rec_y0 = y0; P.rec_w = w; P.rec_h = h;
+    hipLaunchKernelGGL(k_trace_records, dim3((n + kWG - 1) / kWG), dim3(kWG), 0, s->stream, P, n);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpyAsync(out, d_rec, sizeof(rt_sample_rec) * n, hipMemcpyDeviceToHost, s->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+    (void)hipFree(d_rec);
+    if (e != hipSuccess) return fail(RT_E_HIP, std::string("rt_trace_samples: ") + hipGetErrorString(e));
+    return RT_OK;
+}
+
+int rt_debug_primitives(int kind, const float *in, uint32_t n, float *out, int device)
+{
+    static const uint32_t in_w[5] = { 18, 12, 23, 3, 11 }, out_w[5] = { 8, 4, 6, 4, 3 };
+    if (kind < 0 || kind > 4 || !in || !out) return fail(RT_E_INVALID, "bad arguments");
+    if (n == 0) return RT_OK;
+    RT_HIP(hipSetDevice(device));
+    std::vector<float> host_in(in, in + size_t(in_w[kind]) * n);
+    if (kind == 2)   // camera.h:41-42 fov_xs is a host-side constant (double ::tan, hazard H5)
+        for (uint32_t i = 0; i < n; i++)
+        {
+            const float hfov = host_in[23 * size_t(i) + 22] * float(0.0174532925);
+            host_in[23 * size_t(i) + 22] = float(::tan(double(hfov / 2.0f)));
+        }
+    in = host_in.data();
+    float *d_in = nullptr, *d_out = nullptr;
+    RT_HIP(hipMalloc(&d_in, sizeof(float) * in_w[kind] * n));
+    RT_HIP(hipMalloc(&d_out, sizeof(float) * out_w[kind] * n));
+    hipError_t e = hipMemcpy(d_in, in, sizeof(float) * in_w[kind] * n, hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+    {
+        hipLaunchKernelGGL(k_primitives, dim3((n + kWG - 1) / kWG), dim3(kWG), 0, nullptr, kind, d_in, n, d_out);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpy(out, d_out, sizeof(float) * out_w[kind] * n, hipMemcpyDeviceToHost);
+    (void)hipFree(d_in);
+    (void)hipFree(d_out);
+    if (e != hipSuccess) return fail(RT_E_HIP, std::string("rt_debug_primitives: ") + hipGetErrorString(e));
+    return RT_OK;
+}
+
+} // extern "C"

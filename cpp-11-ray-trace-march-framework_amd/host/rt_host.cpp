@@ -1,0 +1,664 @@
+// rt_host.cpp -- C++11 host side above the GPU boundary (include/rt_host.h).
+//
+//  * Scene loading (.rtscene) and the uniform-grid build of Grid::Grid (grid.cpp:12-154),
+//    emitted directly as CSR in GridIdx order.  The build is bit-identical to the
+//    reference (tests/test_host_grid.py checks every scene's CSR hash against the fixture
+//    produced by the reference's own Grid::Grid); it runs the per-triangle tri/box tests in
+//    parallel and keeps each cell's list in ascending triangle order with a stable
+//    counting sort, which is what the reference's sequential push_back order produces.
+//  * A headless Framebuffer (framebuffer.h / framebuffer.cpp) whose RenderTile override is
+//    served by librt_tracer: one batched GPU launch per frame, then each worker thread
+//    copies its own tile under its tile mutex.
+//
+// Built with -ffp-contract=off and no -march (reference Makefile:9-11): the float
+// arithmetic of the grid build must round exactly as the reference's does.
+
+#include "../../include/rt_host.h"
+
+#include <algorithm>
+#include <array>
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <condition_variable>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+#include <memory>
+#include <mutex>
+#include <random>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& m)
+{
+    g_err = m;
+    return code;
+}
+
+// ------------------------------------------------------------------ tri/box overlap
+// Akenine-Moller separating-axis test in double (aabb_tri_internal.h:112-186), as called
+// by IntersectTriAABB (aabb.h:15-32).  The nine edge-axis tests are table driven here:
+// for edge e and world axis a the test projects onto e x a, i.e. uses components (b, c) =
+// the other two axes, with p = e[c]*v[b] - e[b]*v[c] (sign conventions of the X/Y/Z macros).
+struct AxisTest { int e; int b; int c; int va; int vb; bool p2_first; bool neg; };
+
+inline int plane_box(const double n[3], double d, const double h[3])
+{
+    double vmin[3], vmax[3];
+    for (int q = 0; q < 3; q++)
+    {
+        if (n[q] > 0.0f) { vmin[q] = -h[q]; vmax[q] = h[q]; }
+        else             { vmin[q] = h[q];  vmax[q] = -h[q]; }
+    }
+    if (n[0] * vmin[0] + n[1] * vmin[1] + n[2] * vmin[2] + d > 0.0f) return 0;
+    if (n[0] * vmax[0] + n[1] * vmax[1] + n[2] * vmax[2] + d >= 0.0f) return 1;
+    return 0;
+}
+
+bool tri_box(const double ctr[3], const double h[3], const float* p0, const float* p1, const float* p2)
+{
+    double v[3][3], e[3][3];
+    for (int i = 0; i < 3; i++)
+    {
+        v[0][i] = double(p0[i]) - ctr[i];
+        v[1][i] = double(p1[i]) - ctr[i];
+        v[2][i] = double(p2[i]) - ctr[i];
+    }
+    for (int i = 0; i < 3; i++)
+    {
+        e[0][i] = v[1][i] - v[0][i];
+        e[1][i] = v[2][i] - v[1][i];
+        e[2][i] = v[0][i] - v[2][i];
+    }
+    // Which two vertices each macro projects (aabb_tri_internal.h:142-158):
+    //   edge0: X01(v0,v2) Y02(v0,v2) Z12(v1,v2)   edge1: X01(v0,v2) Y02(v0,v2) Z0(v0,v1)
+    //   edge2: X2(v0,v1)  Y1(v0,v1)  Z12(v1,v2)
+    static const int verts[3][3][2] = { { { 0, 2 }, { 0, 2 }, { 1, 2 } },
+                                        { { 0, 2 }, { 0, 2 }, { 0, 1 } },
+                                        { { 0, 1 }, { 0, 1 }, { 1, 2 } } };
+    for (int ei = 0; ei < 3; ei++)
+    {
+        const double* E = e[ei];
+        const double fa[3] = { std::fabs(E[0]), std::fabs(E[1]), std::fabs(E[2]) };
+        for (int ax = 0; ax < 3; ax++)
+        {
+            const int a = verts[ei][ax][0], b = verts[ei][ax][1];
+            double pa, pb, rad;
+            if (ax == 0)      // X tests: p = E.z*v.y - E.y*v.z ; rad = |E.z|*h.y + |E.y|*h.z
+            {
+                pa = E[2] * v[a][1] - E[1] * v[a][2];
+                pb = E[2] * v[b][1] - E[1] * v[b][2];
+                rad = fa[2] * h[1] + fa[1] * h[2];
+            }
+            else if (ax == 1) // Y tests: p = -E.z*v.x + E.x*v.z ; rad = |E.z|*h.x + |E.x|*h.z
+            {
+                pa = -E[2] * v[a][0] + E[0] * v[a][2];
+                pb = -E[2] * v[b][0] + E[0] * v[b][2];
+                rad = fa[2] * h[0] + fa[0] * h[2];
+            }
+            else              // Z tests: p = E.y*v.x - E.x*v.y ; rad = |E.y|*h.x + |E.x|*h.y
+            {
+                pa = E[1] * v[a][0] - E[0] * v[a][1];
+                pb = E[1] * v[b][0] - E[0] * v[b][1];
+                rad = fa[1] * h[0] + fa[0] * h[1];
+            }
+            // Z12 orders with '(p2 < p1)', the others with '(pa < pb)'; min/max coincide
+            // except for NaN, where the chosen branch decides -- keep each macro's form.
+            double mn, mx;
+            const bool z12 = (ax == 2) && !(ei == 1);
+            if (z12) { if (pb < pa) { mn = pb; mx = pa; } else { mn = pa; mx = pb; } }
+            else     { if (pa < pb) { mn = pa; mx = pb; } else { mn = pb; mx = pa; } }
+            if (mn > rad || mx < -rad) return false;
+        }
+    }
+    for (int a = 0; a < 3; a++)      // FINDMINMAX per axis
+    {
+        double mn = v[0][a], mx = v[0][a];
+        if (v[1][a] < mn) mn = v[1][a];
+        if (v[1][a] > mx) mx = v[1][a];
+        if (v[2][a] < mn) mn = v[2][a];
+        if (v[2][a] > mx) mx = v[2][a];
+        if (mn > h[a] || mx < -h[a]) return false;
+    }
+    double n[3];
+    n[0] = e[0][1] * e[1][2] - e[0][2] * e[1][1];
+    n[1] = e[0][2] * e[1][0] - e[0][0] * e[1][2];
+    n[2] = e[0][0] * e[1][1] - e[0][1] * e[1][0];
+    const double d = -(n[0] * v[0][0] + n[1] * v[0][1] + n[2] * v[0][2]);
+    return plane_box(n, d, h) == 1;
+}
+
+} // namespace
+
+struct rth_scene
+{
+    uint32_t id = 0xFFFFFFFFu;
+    float fov = 45.0f;
+    float cam[16];
+    std::vector<rt_vertex> verts;
+    std::vector<rt_triangle> tris;
+    uint32_t dims[3] = { 0, 0, 0 };
+    float bmin[3], bmax[3], cw = 0, icw = 0;
+    std::vector<uint32_t> off, refs;
+    double build_s = 0.0;
+};
+
+namespace {
+
+// grid.cpp:12-129 Grid::Grid -> CSR
+int build_grid(rth_scene& s, uint32_t res, uint32_t nthreads)
+{
+    if (s.tris.empty() || s.verts.empty()) return fail(RT_E_INVALID, "empty mesh (grid.cpp:15)");
+    if (res == 0) return fail(RT_E_INVALID, "grid_res must be > 0 (grid.cpp:16)");
+    const auto t0 = std::chrono::steady_clock::now();
+    const float fmax = std::numeric_limits<float>::max(), fmin = std::numeric_limits<float>::min();
+    // mesh.cpp:112-134 ComputeAABB (max seeded with float::min(), hazard H11)
+    float mn[3] = { fmax, fmax, fmax }, mx[3] = { fmin, fmin, fmin };
+    for (const auto& t : s.tris)
+        for (uint32_t vi : { t.v0, t.v1, t.v2 })
+            for (int a = 0; a < 3; a++)
+            {
+                mn[a] = std::min(mn[a], s.verts[vi].p[a]);
+                mx[a] = std::max(mx[a], s.verts[vi].p[a]);
+            }
+    // grid.cpp:29-38
+    float ext[3];
+    for (int a = 0; a < 3; a++)
+    {
+        s.bmin[a] = mn[a] - 0.0001f;
+        s.bmax[a] = mx[a] + 0.0001f;
+        ext[a] = s.bmax[a] - s.bmin[a];
+    }
+    const float largest = std::max(std::max(ext[0], ext[1]), ext[2]);
+    s.cw = largest / float(res);
+    s.icw = 1.0f / s.cw;
+    for (int a = 0; a < 3; a++) s.dims[a] = uint32_t(std::ceil(ext[a] / s.cw));
+    const uint64_t nc64 = uint64_t(s.dims[0]) * s.dims[1] * s.dims[2];
+    if (nc64 == 0 || nc64 > (1ull << 31)) return fail(RT_E_INVALID, "degenerate grid");
+    const uint32_t nc = uint32_t(nc64), dx = s.dims[0], dxdz = s.dims[0] * s.dims[2];
+    const float cw = s.cw;
+
+    // Per triangle (in parallel, contiguous ranges): the overlapped cells (grid.cpp:65-129)
+    const uint32_t nt = uint32_t(s.tris.size());
+    if (nthreads == 0) nthreads = std::max(1u, std::thread::hardware_concurrency());
+    nthreads = std::min(nthreads, std::max(1u, nt / 64));
+    std::vector<std::vector<uint32_t>> pairs(nthreads);      // (cell, tri) flattened
+    std::atomic<bool> bad(false);
+    auto work = [&](uint32_t w) {
+        const uint32_t lo = uint32_t(uint64_t(nt) * w / nthreads), hi = uint32_t(uint64_t(nt) * (w + 1) / nthreads);
+        std::vector<uint32_t>& out = pairs[w];
+        for (uint32_t ti = lo; ti < hi; ti++)
+        {
+            const rt_triangle& t = s.tris[ti];
+            const float *p0 = s.verts[t.v0].p, *p1 = s.verts[t.v1].p, *p2 = s.verts[t.v2].p;
+            uint32_t st[3], en[3];
+            for (int a = 0; a < 3; a++)
+            {
+                // triangle.h:116-131 TriangleAABB (same float::min() seed), relative to the grid
+                const float tmn = std::min(std::min(std::min(fmax, p0[a]), p1[a]), p2[a]) - s.bmin[a];
+                const float tmx = std::max(std::max(std::max(fmin, p0[a]), p1[a]), p2[a]) - s.bmin[a];
+                st[a] = uint32_t(int64_t(tmn / cw));          // grid.cpp:81-92 uint(float)
+                en[a] = uint32_t(int64_t(tmx / cw));
+            }
+            uint32_t hits = 0;
+            for (uint32_t x = st[0]; x <= en[0]; x++)
+                for (uint32_t y = st[1]; y <= en[1]; y++)
+                    for (uint32_t z = st[2]; z <= en[2]; z++)
+                    {
+                        // grid.cpp:101-108 cell bounds in float, aabb.h:19-26 centre/half
+                        const float cmin[3] = { s.bmin[0] + float(x) * cw, s.bmin[1] + float(y) * cw,
+                                                s.bmin[2] + float(z) * cw };
+                        const float cmax[3] = { s.bmin[0] + float(x + 1) * cw, s.bmin[1] + float(y + 1) * cw,
+                                                s.bmin[2] + float(z + 1) * cw };
+                        const double ctr[3] = { (cmin[0] + cmax[0]) * 0.5f, (cmin[1] + cmax[1]) * 0.5f,
+                                                (cmin[2] + cmax[2]) * 0.5f };
+                        const double half[3] = { (cmax[0] - cmin[0]) * 0.5f, (cmax[1] - cmin[1]) * 0.5f,
+                                                 (cmax[2] - cmin[2]) * 0.5f };
+                        if (tri_box(ctr, half, p0, p1, p2))
+                        {
+                            const uint32_t cell = x + z * dx + y * dxdz;   // grid.h:41-42
+                            if (cell >= nc) { bad = true; continue; }
+                            out.push_back(cell);
+                            out.push_back(ti);
+                            hits++;
+                        }
+                    }
+            if (hits == 0) bad = true;                        // grid.cpp:125 assert
+        }
+    };
+    std::vector<std::thread> pool;
+    for (uint32_t w = 1; w < nthreads; w++) pool.emplace_back(work, w);
+    work(0);
+    for (auto& th : pool) th.join();
+    if (bad) return fail(RT_E_INVALID, "a triangle touches no cell or lies outside the grid (grid.cpp:121-125)");
+
+    // Stable counting sort by cell: thread ranges are in triangle order, so every cell's
+    // list comes out ascending -- the push_back order of grid.cpp:122.
+    s.off.assign(size_t(nc) + 1, 0);
+    for (const auto& pv : pairs)
+        for (size_t i = 0; i < pv.size(); i += 2) s.off[pv[i] + 1]++;
+    for (uint32_t c = 0; c < nc; c++) s.off[c + 1] += s.off[c];
+    s.refs.resize(s.off[nc]);
+    std::vector<uint32_t> cursor(s.off.begin(), s.off.end() - 1);
+    for (const auto& pv : pairs)
+        for (size_t i = 0; i < pv.size(); i += 2) s.refs[cursor[pv[i]]++] = pv[i + 1];
+    s.build_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return RT_OK;
+}
+
+int read_scene(const char* path, rth_scene& s)
+{
+    std::FILE* f = std::fopen(path, "rb");
+    if (!f) return fail(RT_E_INVALID, std::string("cannot open ") + path);
+    char magic[8];
+    uint32_t nv = 0, nt = 0;
+    bool ok = std::fread(magic, 1, 8, f) == 8 && std::memcmp(magic, "RTSCENE1", 8) == 0 &&
+              std::fread(&s.id, 4, 1, f) == 1 && std::fread(&s.fov, 4, 1, f) == 1 &&
+              std::fread(s.cam, 4, 16, f) == 16 && std::fread(&nv, 4, 1, f) == 1 && std::fread(&nt, 4, 1, f) == 1 &&
+              nv > 0 && nt > 0 && nv < (1u << 28) && nt < (1u << 28);
+    if (ok)
+    {
+        s.verts.resize(nv);
+        s.tris.resize(nt);
+        ok = std::fread(s.verts.data(), sizeof(rt_vertex), nv, f) == nv &&
+             std::fread(s.tris.data(), sizeof(rt_triangle), nt, f) == nt;
+    }
+    std::fclose(f);
+    if (!ok) return fail(RT_E_INVALID, std::string("malformed .rtscene: ") + path);
+    for (const auto& t : s.tris)
+        if (t.v0 >= nv || t.v1 >= nv || t.v2 >= nv) return fail(RT_E_INVALID, "vertex index out of bounds");
+    return RT_OK;
+}
+
+static_assert(sizeof(rt_vertex) == 24 && sizeof(rt_triangle) == 24, "Mesh::Vertex/Triangle layouts (mesh.h)");
+
+} // namespace
+
+// ================================================================= Framebuffer (host)
+// framebuffer.h:16-101 / framebuffer.cpp restated without OpenGL: 12x9 tiles, a
+// hardware_concurrency() worker pool, shuffled LIFO queue, per-tile mutex held across
+// RenderTile, stop flag polled between tiles.
+namespace {
+
+class Framebuffer
+{
+public:
+    explicit Framebuffer(uint32_t nthreads)
+        : m_num_cpus(nthreads ? nthreads : std::max(1u, std::thread::hardware_concurrency())) { }
+    virtual ~Framebuffer() { }
+
+    void Resize(uint32_t width, uint32_t height)               // framebuffer.cpp:94-122
+    {
+        KillAllWorkerThreads();
+        m_width = width;
+        m_height = height;
+        const uint32_t tw = width / kTilesX, th = height / kTilesY;
+        for (uint32_t y = 0; y < kTilesY; y++)
+            for (uint32_t x = 0; x < kTilesX; x++)
+                m_tiles[x + y * kTilesX].SetPosition(x * tw, y * th, (x == kTilesX - 1) ? width : (x + 1) * tw,
+                                                     (y == kTilesY - 1) ? height : (y + 1) * th);
+        CreateWorkerThreads();
+    }
+
+    void StartRendering()                                       // framebuffer.cpp:124-134
+    {
+        KillAllWorkerThreads();
+        for (auto& t : m_tiles) t.Clear();
+        CreateWorkerThreads();
+    }
+
+    void Wait()
+    {
+        for (auto& th : m_threads)
+            if (th.joinable()) th.join();
+        m_threads.clear();
+    }
+
+    double LastFrameSeconds() const { return m_last_frame_s; }
+    uint32_t Width() const { return m_width; }
+    uint32_t Height() const { return m_height; }
+
+    // framebuffer.cpp:195-221 SaveToBMP's assembly step; bitmap row 0 = pixel row 0
+    void Assemble(uint32_t* bitmap) const
+    {
+        for (const auto& t : m_tiles)
+            for (uint32_t y = 0; y < t.GetHeight(); y++)
+                std::memcpy(bitmap + size_t(t.y0 + y) * m_width + t.x0, &t.bgra[size_t(y) * t.GetWidth()],
+                            size_t(t.GetWidth()) * 4);
+    }
+
+protected:
+    struct Tile                                                 // framebuffer.h:34-70
+    {
+        void GetPosition(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d) const { a = x0; b = y0; c = x1; d = y1; }
+        uint32_t GetWidth() const { return x1 - x0; }
+        uint32_t GetHeight() const { return y1 - y0; }
+        uint32_t* GetBuffer() { return &bgra[0]; }
+        void SetPosition(uint32_t a, uint32_t b, uint32_t c, uint32_t d)
+        {
+            x0 = a; y0 = b; x1 = c; y1 = d;
+            bgra.assign(std::max<size_t>(1, size_t(GetWidth()) * GetHeight()), 0);
+        }
+        void Clear() { std::fill(bgra.begin(), bgra.end(), 0u); }
+        std::mutex mtx;
+        std::vector<uint32_t> bgra = std::vector<uint32_t>(1, 0);
+        uint32_t x0 = 0, y0 = 0, x1 = 1, y1 = 1;
+    };
+
+    virtual void RenderTile(Tile& tile) = 0;
+    virtual void BeginFrame() { }
+
+    void KillAllWorkerThreads()                                 // framebuffer.cpp:30-41
+    {
+        m_threads_stop = true;
+        Wait();
+        m_threads_stop = false;
+    }
+
+    uint32_t m_width = 1, m_height = 1;
+    std::atomic<bool> m_threads_stop{ false };                  // volatile bool in the reference
+    static const uint32_t kTilesX = 12, kTilesY = 9;           // framebuffer.h:87-88
+    std::array<Tile, kTilesX * kTilesY> m_tiles;
+
+private:
+    void CreateWorkerThreads()                                  // framebuffer.cpp:16-28
+    {
+        BeginFrame();
+        m_threads_done = 0;
+        m_work_queue.clear();
+        for (uint32_t i = 0; i < kTilesX * kTilesY; i++) m_work_queue.push_back(i);
+        std::shuffle(m_work_queue.begin(), m_work_queue.end(), std::mt19937(m_frame_seed++));
+        m_start = std::chrono::steady_clock::now();
+        for (uint32_t i = 0; i < m_num_cpus; i++) m_threads.emplace_back(&Framebuffer::WorkerThread, this);
+    }
+
+    Tile* GetNextTileFromQueue()                                // framebuffer.cpp:43-57
+    {
+        std::lock_guard<std::mutex> g(m_queue_mtx);
+        if (m_work_queue.empty()) return nullptr;
+        Tile* t = &m_tiles[m_work_queue.back()];
+        m_work_queue.pop_back();
+        return t;
+    }
+
+    void WorkerThread()                                         // framebuffer.cpp:59-92
+    {
+        while (!m_threads_stop)
+        {
+            Tile* tile = GetNextTileFromQueue();
+            if (!tile) break;
+            std::lock_guard<std::mutex> g(tile->mtx);
+            RenderTile(*tile);
+        }
+        if (m_threads_done.fetch_add(1) == m_num_cpus - 1 && !m_threads_stop)
+            m_last_frame_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - m_start).count();
+    }
+
+    const uint32_t m_num_cpus;
+    std::vector<uint32_t> m_work_queue;
+    std::mutex m_queue_mtx;
+    std::vector<std::thread> m_threads;
+    std::atomic<uint32_t> m_threads_done{ 0 };
+    std::chrono::steady_clock::time_point m_start;
+    double m_last_frame_s = 0.0;
+    uint32_t m_frame_seed = 1;
+};
+
+// Renderer (renderer.h) with the tile callback served by the GPU: the first worker of a
+// frame renders the whole frame in ONE launch into a staging image; every worker then copies
+// its own tile while holding that tile's mutex (the reference's locking contract).
+class GpuRenderer : public Framebuffer
+{
+public:
+    GpuRenderer(rt_scene* gpu, const rth_scene* host, uint32_t nthreads)
+        : Framebuffer(nthreads), m_gpu(gpu), m_host(host) { }
+    ~GpuRenderer() override { KillAllWorkerThreads(); }
+
+    void SetSampleCount(uint32_t cnt) { m_spp = std::max(1u, cnt); }   // renderer.cpp:56-60
+    void SetOptions(uint32_t tri_test, uint32_t kernel) { m_tri_test = tri_test; m_kernel = kernel; }
+    int LastStatus() const { return m_status; }
+    const std::string& LastError() const { return m_err; }
+
+protected:
+    void BeginFrame() override
+    {
+        std::lock_guard<std::mutex> g(m_frame_mtx);
+        m_frame_ready = false;
+        m_status = RT_OK;
+    }
+
+    void RenderTile(Tile& tile) override
+    {
+        {
+            std::lock_guard<std::mutex> g(m_frame_mtx);
+            if (!m_frame_ready)
+            {
+                if (m_threads_stop) return;                       // renderer.cpp:114-115
+                m_staging.assign(size_t(m_width) * m_height, 0);
+                rt_frame f;
+                std::memset(&f, 0, sizeof(f));
+                std::memcpy(f.cam, m_host->cam, sizeof(f.cam));   // Scene::GetCameraParameters
+                f.fov = m_host->fov;
+                f.width = m_width;
+                f.height = m_height;
+                f.spp = m_spp;
+                f.tri_test = m_tri_test;
+                f.kernel = m_kernel;
+                const rt_tile whole = { 0, 0, m_width, m_height };
+                uint32_t* dst = m_staging.data();
+                m_status = rt_render_tiles(m_gpu, &f, &whole, 1, &dst);
+                if (m_status != RT_OK)
+                {
+                    char buf[512];
+                    rt_last_error(buf, sizeof(buf));
+                    m_err = buf;
+                }
+                m_frame_ready = true;
+            }
+        }
+        if (m_status != RT_OK) return;
+        uint32_t x0, y0, x1, y1;
+        tile.GetPosition(x0, y0, x1, y1);
+        uint32_t* buf = tile.GetBuffer();
+        for (uint32_t y = 0; y < tile.GetHeight(); y++)        // renderer.cpp:171 layout
+            std::memcpy(buf + size_t(y) * tile.GetWidth(), &m_staging[size_t(y0 + y) * m_width + x0],
+                        size_t(tile.GetWidth()) * 4);
+    }
+
+private:
+    rt_scene* m_gpu;
+    const rth_scene* m_host;
+    uint32_t m_spp = 16;                                        // renderer.h:34
+    uint32_t m_tri_test = RT_TRI_MOLLER_TRUMBORE, m_kernel = RT_KERNEL_AUTO;
+    std::mutex m_frame_mtx;
+    bool m_frame_ready = false;
+    std::vector<uint32_t> m_staging;
+    int m_status = RT_OK;
+    std::string m_err;
+};
+
+} // namespace
+
+struct rth_framebuffer
+{
+    std::unique_ptr<GpuRenderer> r;
+};
+
+extern "C" {
+
+int rth_last_error(char* buf, size_t len)
+{
+    if (!buf || !len) return RT_E_INVALID;
+    std::snprintf(buf, len, "%s", g_err.c_str());
+    return RT_OK;
+}
+
+int rth_scene_load(const char* path, uint32_t nthreads, rth_scene** out)
+{
+    if (!path || !out) return fail(RT_E_INVALID, "NULL argument");
+    *out = nullptr;
+    std::unique_ptr<rth_scene> s(new rth_scene());
+    int rc = read_scene(path, *s);
+    if (rc) return rc;
+    if ((rc = build_grid(*s, 64, nthreads))) return rc;       // scene.cpp:7
+    *out = s.release();
+    return RT_OK;
+}
+
+int rth_scene_from_mesh(const rt_vertex* v, uint32_t nv, const rt_triangle* t, uint32_t nt, float fov,
+                        const float cam[16], uint32_t res, uint32_t nthreads, rth_scene** out)
+{
+    if (!v || !t || !cam || !out || nv == 0 || nt == 0) return fail(RT_E_INVALID, "bad arguments");
+    *out = nullptr;
+    std::unique_ptr<rth_scene> s(new rth_scene());
+    s->verts.assign(v, v + nv);
+    s->tris.assign(t, t + nt);
+    for (const auto& tr : s->tris)
+        if (tr.v0 >= nv || tr.v1 >= nv || tr.v2 >= nv) return fail(RT_E_INVALID, "vertex index out of bounds");
+    s->fov = fov;
+    std::memcpy(s->cam, cam, sizeof(s->cam));
+    int rc = build_grid(*s, res, nthreads);
+    if (rc) return rc;
+    *out = s.release();
+    return RT_OK;
+}
+
+void rth_scene_free(rth_scene* s) { delete s; }
+
+int rth_scene_desc(const rth_scene* s, rt_scene_desc* d)
+{
+    if (!s || !d) return fail(RT_E_INVALID, "NULL argument");
+    std::memset(d, 0, sizeof(*d));
+    d->num_vertices = uint32_t(s->verts.size());
+    d->num_triangles = uint32_t(s->tris.size());
+    d->vertices = s->verts.data();
+    d->triangles = s->tris.data();
+    for (int a = 0; a < 3; a++)
+    {
+        d->grid.dims[a] = s->dims[a];
+        d->grid.aabb_min[a] = s->bmin[a];
+        d->grid.aabb_max[a] = s->bmax[a];
+    }
+    d->grid.cell_wdh = s->cw;
+    d->grid.inv_cell_wdh = s->icw;
+    d->grid.cell_offsets = s->off.data();
+    d->grid.cell_tris = s->refs.data();
+    return RT_OK;
+}
+
+int rth_scene_camera(const rth_scene* s, float* fov, float cam[16])
+{
+    if (!s || !fov || !cam) return fail(RT_E_INVALID, "NULL argument");
+    *fov = s->fov;
+    std::memcpy(cam, s->cam, sizeof(s->cam));
+    return RT_OK;
+}
+
+int rth_scene_stats_get(const rth_scene* s, rth_scene_stats* o)
+{
+    if (!s || !o) return fail(RT_E_INVALID, "NULL argument");
+    o->scene_id = s->id;
+    o->num_vertices = uint32_t(s->verts.size());
+    o->num_triangles = uint32_t(s->tris.size());
+    o->num_cells = uint32_t(s->off.size() - 1);
+    o->num_refs = uint32_t(s->refs.size());
+    o->max_refs_per_cell = 0;
+    o->empty_cells = 0;
+    for (size_t c = 0; c + 1 < s->off.size(); c++)
+    {
+        const uint32_t n = s->off[c + 1] - s->off[c];
+        o->max_refs_per_cell = std::max(o->max_refs_per_cell, n);
+        o->empty_cells += n == 0;
+    }
+    o->grid_build_s = s->build_s;
+    return RT_OK;
+}
+
+int rth_framebuffer_create(rt_scene* gpu, const rth_scene* host, uint32_t nthreads, rth_framebuffer** out)
+{
+    if (!gpu || !host || !out) return fail(RT_E_INVALID, "NULL argument");
+    std::unique_ptr<rth_framebuffer> fb(new rth_framebuffer());
+    fb->r.reset(new GpuRenderer(gpu, host, nthreads));
+    *out = fb.release();
+    return RT_OK;
+}
+
+void rth_framebuffer_free(rth_framebuffer* fb) { delete fb; }
+
+int rth_framebuffer_set_sample_count(rth_framebuffer* fb, uint32_t spp)
+{
+    if (!fb) return fail(RT_E_INVALID, "NULL argument");
+    fb->r->SetSampleCount(spp);
+    return RT_OK;
+}
+
+int rth_framebuffer_set_options(rth_framebuffer* fb, uint32_t tri_test, uint32_t kernel)
+{
+    if (!fb) return fail(RT_E_INVALID, "NULL argument");
+    fb->r->SetOptions(tri_test, kernel);
+    return RT_OK;
+}
+
+static int finish_frame(rth_framebuffer* fb, double* seconds)
+{
+    fb->r->Wait();
+    if (seconds) *seconds = fb->r->LastFrameSeconds();
+    if (fb->r->LastStatus() != RT_OK) return fail(fb->r->LastStatus(), fb->r->LastError());
+    return RT_OK;
+}
+
+int rth_framebuffer_resize(rth_framebuffer* fb, uint32_t w, uint32_t h, double* seconds)
+{
+    if (!fb || w == 0 || h == 0) return fail(RT_E_INVALID, "bad arguments");
+    fb->r->Resize(w, h);
+    return finish_frame(fb, seconds);
+}
+
+int rth_framebuffer_start_rendering(rth_framebuffer* fb, double* seconds)
+{
+    if (!fb) return fail(RT_E_INVALID, "NULL argument");
+    fb->r->StartRendering();
+    return finish_frame(fb, seconds);
+}
+
+int rth_framebuffer_read(const rth_framebuffer* fb, uint32_t* out)
+{
+    if (!fb || !out) return fail(RT_E_INVALID, "NULL argument");
+    fb->r->Assemble(out);
+    return RT_OK;
+}
+
+// bmp_writer.cpp:7-57: packed 54-byte header, 32 bpp, positive height (bottom-up rows)
+int rth_framebuffer_save_bmp(const rth_framebuffer* fb, const char* path)
+{
+    if (!fb || !path) return fail(RT_E_INVALID, "NULL argument");
+    const uint32_t w = fb->r->Width(), h = fb->r->Height();
+    std::vector<uint32_t> img(size_t(w) * h);
+    fb->r->Assemble(img.data());
+    unsigned char hdr[54];
+    std::memset(hdr, 0, sizeof(hdr));
+    auto put16 = [&](int o, uint32_t v) { hdr[o] = v & 255; hdr[o + 1] = (v >> 8) & 255; };
+    auto put32 = [&](int o, uint32_t v) { put16(o, v & 0xFFFF); put16(o + 2, v >> 16); };
+    hdr[0] = 'B';
+    hdr[1] = 'M';
+    put32(2, 54 + w * h * 4);   // size_file
+    put32(10, 54);              // offs_bits
+    put32(14, 40);              // bmih_size
+    put32(18, w);
+    put32(22, h);
+    put16(26, 1);               // planes
+    put16(28, 32);              // bitcount
+    std::FILE* f = std::fopen(path, "wb");
+    if (!f) return fail(RT_E_INVALID, std::string("cannot write ") + path);
+    const bool ok = std::fwrite(hdr, 1, 54, f) == 54 && std::fwrite(img.data(), 4, img.size(), f) == img.size();
+    std::fclose(f);
+    return ok ? RT_OK : fail(RT_E_INVALID, "short write");
+}
+
+} // extern "C"

@@ -1,0 +1,70 @@
+/*
+ * rt_host.h -- C ABI of librt_host.so, the C++11 host side above the GPU boundary.
+ *
+ * The reference keeps scene setup and grid construction on the host (scene.cpp:6-7,
+ * grid.cpp:12-154) and so does this build: librt_host builds the uniform grid exactly as
+ * Grid::Grid does (same AABB padding, 64 cells on the longest axis, Akenine-Moller tri/box
+ * test in double, per-cell lists in ascending triangle order) but emits it directly as the
+ * CSR arrays rt_scene_create (rt_tracer.h) uploads.  It also hosts the Framebuffer tile pool
+ * (framebuffer.h) with a GPU RenderTile override -- see rth_framebuffer_*.
+ */
+#ifndef RT_HOST_H
+#define RT_HOST_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "rt_tracer.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct rth_scene rth_scene;
+
+typedef struct rth_scene_stats {
+    uint32_t scene_id;          /* from the .rtscene header (0xFFFFFFFF for in-memory meshes) */
+    uint32_t num_vertices, num_triangles;
+    uint32_t num_cells, num_refs, max_refs_per_cell, empty_cells;
+    double   grid_build_s;
+} rth_scene_stats;
+
+/* Loads a post-setup scene (.rtscene written by the scene table; format in DESIGN.md) and
+ * builds its grid (resolution 64, scene.cpp:7).  nthreads 0 = hardware_concurrency. */
+int  rth_scene_load(const char *path, uint32_t nthreads, rth_scene **out);
+/* Builds a scene from an in-memory Mesh (mesh.h layouts) and camera (scene.h:17-26). */
+int  rth_scene_from_mesh(const rt_vertex *vertices, uint32_t num_vertices,
+                         const rt_triangle *triangles, uint32_t num_triangles,
+                         float fov, const float cam[16], uint32_t grid_res, uint32_t nthreads,
+                         rth_scene **out);
+void rth_scene_free(rth_scene *s);
+/* Pointers into the scene's own host arrays; valid while the scene lives. */
+int  rth_scene_desc(const rth_scene *s, rt_scene_desc *out);
+int  rth_scene_camera(const rth_scene *s, float *fov, float cam[16]);
+int  rth_scene_stats_get(const rth_scene *s, rth_scene_stats *out);
+
+/* ---- Framebuffer (framebuffer.h:16-101) with the GPU RenderTile --------------------- */
+typedef struct rth_framebuffer rth_framebuffer;
+/* A headless Framebuffer whose RenderTile is served by librt_tracer: the first worker to
+ * reach a frame renders ALL tiles in one batched launch (rt_render_tiles), every worker then
+ * copies its own tile.  nthreads 0 = hardware_concurrency (framebuffer.cpp:11). */
+int  rth_framebuffer_create(rt_scene *gpu_scene, const rth_scene *host_scene, uint32_t nthreads,
+                            rth_framebuffer **out);
+void rth_framebuffer_free(rth_framebuffer *fb);
+int  rth_framebuffer_set_sample_count(rth_framebuffer *fb, uint32_t spp);   /* renderer.cpp:56-60 */
+int  rth_framebuffer_set_options(rth_framebuffer *fb, uint32_t tri_test, uint32_t kernel);
+/* Framebuffer::Resize (framebuffer.cpp:94-122): re-tiles 12x9 and renders; blocks until
+ * the frame is complete.  seconds = pool start -> last tile (framebuffer.cpp:21, 86). */
+int  rth_framebuffer_resize(rth_framebuffer *fb, uint32_t width, uint32_t height, double *seconds);
+int  rth_framebuffer_start_rendering(rth_framebuffer *fb, double *seconds);  /* 'r' key */
+/* Assembled frame (row 0 = bottom row, like SaveToBMP), width*height words. */
+int  rth_framebuffer_read(const rth_framebuffer *fb, uint32_t *out_bgra);
+/* Framebuffer::SaveToBMP -> WriteBitmap (bmp_writer.cpp:27-57): 32-bpp bottom-up BMP. */
+int  rth_framebuffer_save_bmp(const rth_framebuffer *fb, const char *path);
+
+int  rth_last_error(char *buf, size_t len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RT_HOST_H */

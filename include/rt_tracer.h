@@ -1,0 +1,166 @@
+/*
+ * rt_tracer.h -- C ABI of librt_tracer.so, the MI355X (gfx950) primary-ray tile tracer.
+ *
+ * This is the drop-in boundary for the reference's Renderer tile callback
+ * (blitzcode/cpp-11-ray-trace-march-framework):
+ *
+ *   reference interface                                   replaced by
+ *   ----------------------------------------------------  ---------------------------------
+ *   Renderer::RenderTile(Tile&)      renderer.cpp:81-174   rt_render_tiles / rt_render_frame_device
+ *     per-sample loop                renderer.cpp:112-172  (one batched HIP launch per frame)
+ *   GenerateRay (perspective)        camera.h:8-47         in-kernel, from rt_frame
+ *   Grid::Intersect (3D-DDA)         grid.cpp:159-281      in-kernel, CSR cells from rt_grid_desc
+ *   IntersectRayTri                  triangle.h:15-107     RT_TRI_MOLLER_TRUMBORE (default)
+ *   IntersectRayTriBarycentric       triangle.h:210-226    RT_TRI_BARYCENTRIC
+ *   ToBGRA8 + gamma                  lin_alg.h:125-132,    in-kernel resolve
+ *                                    renderer.cpp:162-171
+ *   Scene / Grid / Mesh data         scene.h:17-26,        rt_scene_create (uploaded once)
+ *                                    grid.h:26-39, mesh.h:12-27
+ *
+ * Plain pointers and sizes only; every function returns 0 on success or a nonzero
+ * RT_E* code, with a message retrievable through rt_last_error (thread-local).  No
+ * exceptions cross the ABI.  The library owns device copies of the scene; it never
+ * retains caller pointers past a call.  Calls on one rt_scene from several threads are
+ * serialised internally (the reference's worker threads call RenderTile concurrently,
+ * framebuffer.cpp:59-92).
+ */
+#ifndef RT_TRACER_H
+#define RT_TRACER_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+enum rt_status {
+    RT_OK = 0,
+    RT_E_INVALID = 1,   /* bad argument / malformed scene */
+    RT_E_HIP = 2,       /* HIP runtime error (message has the hipError_t string) */
+    RT_E_NODEVICE = 3,  /* no gfx950 device visible */
+    RT_E_RCCL = 4,
+};
+
+/* Mesh::Vertex (mesh.h:20-24) and Mesh::Triangle (mesh.h:12-18), same 24-byte layouts, so
+ * a caller can pass &mesh->m_vertices[0] / &mesh->m_triangles[0] directly. */
+typedef struct rt_vertex   { float p[3]; float n[3]; } rt_vertex;
+typedef struct rt_triangle { uint32_t v0, v1, v2; float n[3]; } rt_triangle;
+
+/* Grid state (grid.h:28-39).  Cells are CSR in GridIdx order (grid.h:41-42:
+ * x + z*dims[0] + y*dims[0]*dims[2]); each cell's list keeps the reference's push order
+ * (ascending triangle index, grid.cpp:65-122) -- the kernel's tie-break depends on it. */
+typedef struct rt_grid_desc {
+    uint32_t dims[3];
+    float    aabb_min[3];
+    float    aabb_max[3];
+    float    cell_wdh;
+    float    inv_cell_wdh;
+    const uint32_t *cell_offsets;   /* dims[0]*dims[1]*dims[2] + 1 entries */
+    const uint32_t *cell_tris;      /* cell_offsets[num_cells] entries */
+} rt_grid_desc;
+
+typedef struct rt_scene_desc {
+    uint32_t           num_vertices;
+    uint32_t           num_triangles;
+    const rt_vertex   *vertices;
+    const rt_triangle *triangles;
+    rt_grid_desc       grid;
+} rt_scene_desc;
+
+enum rt_tri_test { RT_TRI_MOLLER_TRUMBORE = 0, RT_TRI_BARYCENTRIC = 1 };
+
+enum rt_kernel {
+    RT_KERNEL_AUTO = 0,        /* LANES when spp is a power of two <= 64, else PIXEL_LOOP */
+    RT_KERNEL_LANES = 1,       /* one lane per sample, a pixel's samples in adjacent lanes */
+    RT_KERNEL_PIXEL_LOOP = 2,  /* one lane per pixel looping over its samples (any spp) */
+    RT_KERNEL_COMPACT = 3,     /* LANES + wavefront active-ray compaction (ballot/prefix refill) */
+};
+
+/* Per-frame parameters: what Renderer::RenderTile reads from the Scene and itself. */
+typedef struct rt_frame {
+    float        cam[16];         /* Matrix44f::m_mat row-major [4][4] (lin_alg.h:689), from
+                                     Scene::GetCameraParameters (scene.h:17-18) */
+    float        fov;             /* horizontal FOV in degrees (camera.h:39-45) */
+    uint32_t     width, height;   /* Framebuffer m_width / m_height (framebuffer.h:29-30) */
+    uint32_t     spp;             /* Renderer::m_sample_count (renderer.h:34); 0 -> 1 */
+    const float *sample_offsets;  /* [spp][2] offsets in [-.5,.5], or NULL for the
+                                     Hammersley table of renderer.cpp:87-98 */
+    uint32_t     tri_test;        /* enum rt_tri_test */
+    uint32_t     kernel;          /* enum rt_kernel */
+} rt_frame;
+
+/* Tile::GetPosition (framebuffer.h:41-42); buffer row stride = x1 - x0. */
+typedef struct rt_tile { uint32_t x0, y0, x1, y1; } rt_tile;
+
+/* Debug per-sample record (parity tests). */
+typedef struct rt_sample_rec {
+    uint32_t hit;     /* 1 = hit */
+    uint32_t tri;     /* hit triangle (Grid::Intersect tri_idx), 0xFFFFFFFF on miss */
+    uint32_t voxel;   /* GridIdx of the cell the hit was accepted in (last cell walked on a
+                         miss), 0xFFFFFFFF when the ray misses the grid AABB */
+    uint32_t steps;   /* DDA iterations (cells visited) */
+    uint32_t tests;   /* ray/triangle tests executed */
+    float    t, u, v; /* 0 on miss */
+    float    r, g, b; /* this sample's colour contribution before averaging */
+    uint32_t pad;
+} rt_sample_rec;
+
+typedef struct rt_scene rt_scene;
+
+/* ---- lifetime ---------------------------------------------------------------------- */
+int  rt_get_device_count(int *count);
+int  rt_scene_create(const rt_scene_desc *desc, int device, rt_scene **out);
+int  rt_scene_destroy(rt_scene *scene);
+/* device bytes held by the scene (all arrays) */
+int  rt_scene_device_bytes(const rt_scene *scene, uint64_t *bytes);
+
+/* ---- rendering --------------------------------------------------------------------- */
+/* Renders every listed tile in ONE batched launch (over the tiles' bounding box), copies
+ * back and scatters into the caller's host buffers: tile_bufs[i][(x-x0) + (y-y0)*(x1-x0)]
+ * = 0x00RRGGBB, exactly the words renderer.cpp:171 stores.  Synchronous. */
+int  rt_render_tiles(rt_scene *scene, const rt_frame *frame, const rt_tile *tiles,
+                     uint32_t n_tiles, uint32_t *const *tile_bufs);
+
+/* Device-resident frame: d_bgra[y*width + x] on the caller's HIP stream (NULL = default
+ * stream).  Asynchronous; no host synchronisation and no allocation when the sample
+ * table is unchanged (safe to capture in a hipGraph). */
+int  rt_render_frame_device(rt_scene *scene, const rt_frame *frame, uint32_t *d_bgra,
+                            void *hip_stream);
+
+/* Multi-GPU sharding: the frame is cut into 16x16 pixel tiles, numbered row-major; tile t
+ * is owned by rank t % nranks.  A rank renders its tiles compactly into d_shard
+ * (rt_shard_elems words, tile-local row-major, 256 words per tile); after an all-gather of
+ * the equal-sized shards, rt_unshard_device rebuilds the frame. */
+int  rt_shard_elems(uint32_t width, uint32_t height, uint32_t nranks, uint64_t *elems);
+int  rt_render_shard_device(rt_scene *scene, const rt_frame *frame, uint32_t rank,
+                            uint32_t nranks, uint32_t *d_shard, void *hip_stream);
+int  rt_unshard_device(uint32_t width, uint32_t height, uint32_t nranks,
+                       const uint32_t *d_gathered, uint32_t *d_bgra, void *hip_stream);
+
+/* Kernel time of the last rendering call on this scene measured with HIP events on the
+ * launch stream (ms), for roofline accounting.  Only valid after that stream completed. */
+int  rt_last_kernel_ms(rt_scene *scene, float *ms);
+
+/* ---- parity / debug ---------------------------------------------------------------- */
+/* Per-sample records for pixels [x0,x0+w) x [y0,y0+h), order (y, x, sample).  Synchronous. */
+int  rt_trace_samples(rt_scene *scene, const rt_frame *frame, uint32_t x0, uint32_t y0,
+                      uint32_t w, uint32_t h, rt_sample_rec *out);
+
+/* Device evaluation of the primitives for known-answer tests (input layouts as the
+ * tests/golden/kat_*.f32 records):  0 ray/tri (18 in, 8 out), 1 ray/aabb (12 in, 4 out),
+ * 2 generate ray (23 in, 6 out), 3 gamma+pack (3 in, 4 out), 4 shade (11 in, 3 out). */
+int  rt_debug_primitives(int kind, const float *in, uint32_t n, float *out, int device);
+
+/* Hammersley table the library uses when rt_frame.sample_offsets is NULL. */
+int  rt_sample_table(uint32_t spp, float *out_xy);
+
+int  rt_last_error(char *buf, size_t len);
+int  rt_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RT_TRACER_H */

@@ -1,0 +1,147 @@
+"""Shared fixtures.  Markers: ``gpu`` (needs an MI355X) -- everything else runs on CPU.
+
+The oracle (oracle/liboracle_tracer.so) is test infrastructure: it is only loaded here, in
+__graft_entry__.smoke() and in bench.py's cpu_baseline leg.
+"""
+import ctypes
+import gzip
+import importlib.util
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG_DIR = os.path.join(ROOT, "cpp-11-ray-trace-march-framework_amd")
+GOLD = os.path.join(ROOT, "tests", "golden")
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an AMD Instinct MI355X (gfx950)")
+
+
+def load_package():
+    if "rtm" in sys.modules:
+        return sys.modules["rtm"]
+    spec = importlib.util.spec_from_file_location("rtm", os.path.join(PKG_DIR, "__init__.py"))
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules["rtm"] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def read_gz(name, dtype):
+    with gzip.open(os.path.join(GOLD, name), "rb") as f:
+        return np.frombuffer(f.read(), dtype=dtype)
+
+
+# -------------------------------------------------------------- oracle bindings
+class OrcInfo(ctypes.Structure):
+    _fields_ = [("scene_id", ctypes.c_uint32), ("num_vertices", ctypes.c_uint32),
+                ("num_triangles", ctypes.c_uint32), ("fov", ctypes.c_float),
+                ("cam", ctypes.c_float * 16), ("dims", ctypes.c_uint32 * 3),
+                ("aabb_min", ctypes.c_float * 3), ("aabb_max", ctypes.c_float * 3),
+                ("cell_wdh", ctypes.c_float), ("inv_cell_wdh", ctypes.c_float),
+                ("num_cells", ctypes.c_uint32), ("num_refs", ctypes.c_uint32),
+                ("max_refs_per_cell", ctypes.c_uint32), ("grid_build_s", ctypes.c_double)]
+
+
+class Oracle:
+    """ctypes wrapper of oracle/cpu_tracer.h (the CPU restatement)."""
+
+    def __init__(self, path=os.path.join(ROOT, "oracle", "liboracle_tracer.so")):
+        if not os.path.exists(path):
+            raise RuntimeError("oracle not built: make -C oracle")
+        L = ctypes.CDLL(path)
+        vp = ctypes.c_void_p
+        L.orc_scene_load.restype = vp
+        L.orc_scene_load.argtypes = [ctypes.c_char_p]
+        L.orc_scene_free.argtypes = [vp]
+        L.orc_scene_info.argtypes = [vp, ctypes.POINTER(OrcInfo)]
+        L.orc_scene_csr.argtypes = [vp, vp, vp]
+        L.orc_render.argtypes = [vp] + [ctypes.c_uint32] * 5 + [vp, vp, ctypes.POINTER(ctypes.c_double)]
+        L.orc_trace_samples.argtypes = [vp] + [ctypes.c_uint32] * 8 + [vp]
+        for fn in ("orc_kat_ray_tri", "orc_kat_ray_aabb", "orc_kat_genray", "orc_kat_bgra8",
+                   "orc_kat_shade"):
+            getattr(L, fn).argtypes = [vp, ctypes.c_uint32, vp]
+        L.orc_hammersley.argtypes = [ctypes.c_uint32, vp]
+        self.L = L
+        self._scenes = {}
+
+    def scene(self, sid):
+        if sid not in self._scenes:
+            h = self.L.orc_scene_load(os.path.join(ROOT, "data", "scenes", f"scene{sid}.rtscene").encode())
+            assert h, f"oracle failed to load scene {sid}"
+            self._scenes[sid] = h
+        return ctypes.c_void_p(self._scenes[sid])
+
+    def info(self, sid):
+        i = OrcInfo()
+        assert self.L.orc_scene_info(self.scene(sid), ctypes.byref(i)) == 0
+        return i
+
+    def csr(self, sid):
+        i = self.info(sid)
+        offs = np.zeros(i.num_cells + 1, np.uint32)
+        refs = np.zeros(max(1, i.num_refs), np.uint32)
+        self.L.orc_scene_csr(self.scene(sid), ctypes.c_void_p(offs.ctypes.data), ctypes.c_void_p(refs.ctypes.data))
+        return offs, refs[: i.num_refs]
+
+    def render(self, sid, W, H, spp, tri_test=0, nthreads=0, hits=False):
+        out = np.zeros(W * H, np.uint32)
+        hid = np.zeros(W * H * spp, np.uint32) if hits else None
+        sec = ctypes.c_double()
+        rc = self.L.orc_render(self.scene(sid), W, H, spp, tri_test, nthreads,
+                               ctypes.c_void_p(out.ctypes.data),
+                               ctypes.c_void_p(hid.ctypes.data) if hits else None, ctypes.byref(sec))
+        assert rc == 0
+        return out.reshape(H, W), (hid if hits else None), sec.value
+
+    def records(self, sid, W, H, spp, x0, y0, w, h, tri_test=0):
+        rtm = load_package()
+        out = np.zeros(w * h * spp, rtm.SAMPLE_REC_DTYPE)
+        assert self.L.orc_trace_samples(self.scene(sid), W, H, spp, tri_test, x0, y0, w, h,
+                                        ctypes.c_void_p(out.ctypes.data)) == 0
+        return out
+
+    def kat(self, name, rin, w_out):
+        rin = np.ascontiguousarray(rin, np.float32)
+        out = np.zeros((rin.shape[0], w_out), np.float32)
+        getattr(self.L, f"orc_kat_{name}")(ctypes.c_void_p(rin.ctypes.data), rin.shape[0],
+                                           ctypes.c_void_p(out.ctypes.data))
+        return out
+
+    def hammersley(self, spp):
+        out = np.zeros(2 * spp, np.float32)
+        self.L.orc_hammersley(spp, ctypes.c_void_p(out.ctypes.data))
+        return out.reshape(spp, 2)
+
+
+@pytest.fixture(scope="session")
+def golden():
+    with open(os.path.join(GOLD, "golden.json")) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    return Oracle()
+
+
+@pytest.fixture(scope="session")
+def rtm():
+    return load_package()
+
+
+# KAT layouts: (file, input width, output width)
+KATS = {"ray_tri": (18, 8), "ray_aabb": (12, 4), "genray": (23, 6), "bgra8": (3, 4), "shade": (11, 3)}
+
+
+def load_kat(name):
+    wi, wo = KATS[name]
+    a = read_gz(f"kat_{name}.f32.gz", "<f4").reshape(-1, wi + wo)
+    return a[:, :wi], a[:, wi:]

@@ -1,0 +1,57 @@
+"""The C-ABI libraries load without a GPU and export every function their headers declare."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import PKG_DIR, ROOT, load_package
+
+rtm = load_package()
+
+
+def declared(header):
+    src = open(os.path.join(ROOT, "include", header)).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(rth?_[a-z0-9_]+)\s*\(", src)))
+
+
+@pytest.mark.parametrize("header,lib", [("rt_tracer.h", "librt_tracer.so"), ("rt_host.h", "librt_host.so")])
+def test_exports_every_declared_symbol(header, lib):
+    L = ctypes.CDLL(os.path.join(PKG_DIR, lib))
+    names = declared(header)
+    assert len(names) >= 12
+    missing = [n for n in names if not hasattr(L, n)]
+    assert not missing, missing
+
+
+def test_python_binding_lists_match_headers():
+    assert sorted(rtm.TRACER_SYMBOLS) == declared("rt_tracer.h")
+    assert sorted(rtm.HOST_SYMBOLS) == declared("rt_host.h")
+
+
+def test_struct_layouts():
+    """Mesh::Vertex / Mesh::Triangle are 24 B (mesh.h:12-24); rt_sample_rec is 48 B."""
+    assert ctypes.sizeof(rtm.Vertex) == 24 and ctypes.sizeof(rtm.Triangle) == 24
+    assert rtm.SAMPLE_REC_DTYPE.itemsize == 48
+    assert ctypes.sizeof(rtm.Tile) == 16
+
+
+def test_host_side_entry_points_without_gpu():
+    L = rtm.tracer_lib()
+    assert L.rt_abi_version() == 1
+    # Hammersley table matches the reference's (renderer.cpp:87-98), 4 spp in SURVEY H12
+    np.testing.assert_array_equal(rtm.sample_table(4), [[-.5, -.5], [-.25, 0], [0, -.25], [.25, .25]])
+    e = rtm.shard_elems(1920, 1080, 8)
+    assert e == ((120 * 68 + 7) // 8) * 256
+
+
+def test_invalid_arguments_fail_loudly():
+    L = rtm.tracer_lib()
+    assert L.rt_scene_create(None, 0, None) != 0
+    buf = ctypes.create_string_buffer(256)
+    L.rt_last_error(buf, 256)
+    assert buf.value
+    with pytest.raises(rtm.RtError):
+        rtm.shard_elems(0, 10, 1)

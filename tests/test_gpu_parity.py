@@ -1,0 +1,220 @@
+"""HIP path (librt_tracer.so, through its C ABI) vs the reference fixtures and the oracle.
+
+Bar (BASELINE.json north_star): hit-triangle IDs, grid voxel indices, step/test counts and
+BGRA8 bytes bit-exact; float shading/depth within 1e-5 relative (the kernel is expected to
+be bit-exact there too except for the 1-ulp sqrt-vs-powf gamma differences, which never
+change a packed byte -- tests/test_gamma_exhaustive.py).
+"""
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+from conftest import load_kat, load_package, read_gz
+
+pytestmark = pytest.mark.gpu
+rtm = load_package()
+FLOAT_RTOL = 1e-5
+
+
+def bits(a):
+    return np.ascontiguousarray(a, np.float32).view(np.uint32)
+
+
+@pytest.fixture(scope="module")
+def scenes():
+    cache = {}
+
+    def get(sid):
+        if sid not in cache:
+            hs = rtm.HostScene.load(sid)
+            cache[sid] = (hs, rtm.GpuScene(hs, 0))
+        return cache[sid]
+    yield get
+    for hs, gs in cache.values():
+        gs.close()
+        hs.close()
+
+
+def hit_ids(recs):
+    return np.where(recs["hit"] == 1, recs["tri"], np.uint32(0xFFFFFFFF)).astype(np.uint32)
+
+
+# ---------------------------------------------------------------- primitives
+def test_device_kat_ray_tri():
+    rin, exp = load_kat("ray_tri")
+    np.testing.assert_array_equal(bits(rtm.debug_primitives(0, rin)), bits(exp))
+
+
+def test_device_kat_ray_aabb():
+    rin, exp = load_kat("ray_aabb")
+    np.testing.assert_array_equal(bits(rtm.debug_primitives(1, rin)), bits(exp))
+
+
+def test_device_kat_genray():
+    rin, exp = load_kat("genray")
+    np.testing.assert_array_equal(bits(rtm.debug_primitives(2, rin)), bits(exp))
+
+
+def test_device_kat_gamma_pack():
+    rin, exp = load_kat("bgra8")
+    got = rtm.debug_primitives(3, rin)
+    np.testing.assert_array_equal(bits(got[:, 3]), bits(exp[:, 3]))       # packed bytes exact
+    np.testing.assert_allclose(got[:, :3], exp[:, :3], rtol=FLOAT_RTOL, atol=0)
+
+
+def test_device_kat_shade():
+    rin, exp = load_kat("shade")
+    np.testing.assert_array_equal(bits(rtm.debug_primitives(4, rin)), bits(exp))
+
+
+# ---------------------------------------------------------------- frames
+def test_small_frames_all_kernels(golden, scenes):
+    for fr in golden["small_frames"]:
+        hs, gs = scenes(fr["scene"])
+        W, H, spp = fr["W"], fr["H"], fr["spp"]
+        exp = read_gz(os.path.join("frames", fr["name"] + ".bgra.gz"), "<u4").reshape(H, W)
+        exph = read_gz(os.path.join("frames", fr["name"] + ".hits.gz"), "<u4")
+        kernels = [rtm.RT_KERNEL_AUTO, rtm.RT_KERNEL_PIXEL_LOOP]
+        for k in kernels:
+            img = gs.render_frame(gs.frame(W, H, spp, kernel=k))
+            np.testing.assert_array_equal(img, exp, err_msg=f"{fr['name']} kernel {k}")
+        recs = gs.trace_samples(gs.frame(W, H, spp), 0, 0, W, H)
+        np.testing.assert_array_equal(hit_ids(recs), exph, err_msg=fr["name"])
+
+
+def test_crop_records_vs_reference_and_oracle(golden, scenes, oracle):
+    """Per sample: hit/tri exact vs the reference; voxel GridIdx, DDA steps, tri tests exact vs
+    the oracle; t, u, v and colour bit-exact (tolerance 1e-5 is the contract)."""
+    for c in golden["crops"]:
+        hs, gs = scenes(c["scene"])
+        f = gs.frame(c["W"], c["H"], c["spp"])
+        got = gs.trace_samples(f, c["x0"], c["y0"], c["w"], c["h"])
+        ref = read_gz(os.path.join("samples", c["name"] + ".rec.gz"), "<u4").reshape(-1, 8)
+        np.testing.assert_array_equal(got["hit"], ref[:, 0], err_msg=c["name"])
+        np.testing.assert_array_equal(got["tri"], ref[:, 1], err_msg=c["name"])
+        for j, k in enumerate(("t", "u", "v", "r", "g", "b")):
+            np.testing.assert_array_equal(bits(got[k]), ref[:, 2 + j], err_msg=f"{c['name']} {k}")
+        orc = oracle.records(c["scene"], c["W"], c["H"], c["spp"], c["x0"], c["y0"], c["w"], c["h"])
+        for k in ("hit", "tri", "voxel", "steps", "tests"):
+            np.testing.assert_array_equal(got[k], orc[k], err_msg=f"{c['name']} {k}")
+
+
+@pytest.mark.parametrize("sid", range(10))
+def test_full_frame_1080p4(golden, scenes, sid):
+    """BASELINE configs 2/3/5: 1920x1080x4spp, BGRA8 SHA-256 and per-sample hit-ID SHA-256
+    equal the reference renderer's (all 10 built-in scenes)."""
+    g = golden["frames_1080p4"][str(sid)]
+    hs, gs = scenes(sid)
+    f = gs.frame(1920, 1080, 4)
+    img = gs.render_frame(f)
+    assert hashlib.sha256(img.tobytes()).hexdigest() == g["bgra_sha256"]
+    recs = gs.trace_samples(f, 0, 0, 1920, 1080)
+    assert hashlib.sha256(hit_ids(recs).tobytes()).hexdigest() == g["hits_sha256"]
+
+
+def test_full_frame_compaction_kernel(golden, scenes):
+    for sid in (1, 5, 8):
+        hs, gs = scenes(sid)
+        img = gs.render_frame(gs.frame(1920, 1080, 4, kernel=rtm.RT_KERNEL_COMPACT))
+        assert hashlib.sha256(img.tobytes()).hexdigest() == golden["frames_1080p4"][str(sid)]["bgra_sha256"]
+
+
+def test_head_4096x4096x16(golden, scenes):
+    """BASELINE config 4 (per-GPU work of the 8-GPU run is a subset of this frame)."""
+    g = golden["frames_1080p4"]["head_4096x4096x16"]
+    hs, gs = scenes(4)
+    img = gs.render_frame(gs.frame(4096, 4096, 16))
+    assert hashlib.sha256(img.tobytes()).hexdigest() == g["bgra_sha256"]
+
+
+def test_render_tiles_subset(scenes):
+    """rt_render_tiles fills arbitrary tile buffers exactly as the full frame (renderer.cpp:171)."""
+    hs, gs = scenes(8)
+    f = gs.frame(640, 480, 4)
+    full = gs.render_frame(f)
+    tiles = [(0, 0, 53, 53), (100, 60, 260, 180), (600, 400, 640, 480), (5, 470, 6, 471)]
+    for t, b in zip(tiles, gs.render_tiles(f, tiles)):
+        np.testing.assert_array_equal(b, full[t[1]:t[3], t[0]:t[2]])
+
+
+@pytest.mark.parametrize("spp", [1, 2, 3, 5, 8, 16, 32, 64, 100])
+def test_spp_variants_vs_oracle(scenes, oracle, spp):
+    hs, gs = scenes(8)
+    exp, _, _ = oracle.render(8, 96, 64, spp)
+    np.testing.assert_array_equal(gs.render_frame(gs.frame(96, 64, spp)), exp)
+
+
+def test_barycentric_variant_vs_oracle(scenes, oracle):
+    """IntersectRayTriBarycentric (triangle.h:210-226) as the DDA's tri test (RT_TRI_BARYCENTRIC).
+    The reference never wires it into the live traversal, so this is pinned by its KAT plus
+    the oracle (same restated traversal)."""
+    for sid in (1, 4, 8):
+        hs, gs = scenes(sid)
+        exp, hits, _ = oracle.render(sid, 160, 120, 4, tri_test=1, hits=True)
+        f = gs.frame(160, 120, 4, tri_test=rtm.RT_TRI_BARYCENTRIC)
+        np.testing.assert_array_equal(gs.render_frame(f), exp)
+        recs = gs.trace_samples(f, 0, 0, 160, 120)
+        np.testing.assert_array_equal(hit_ids(recs), hits)
+
+
+@pytest.mark.parametrize("nranks", [1, 2, 3, 8])
+def test_shard_unshard_partition_invariant(golden, scenes, nranks):
+    """Multi-GPU layout: every rank's interleaved 16x16 tiles, gathered and
+    un-permuted by K3, reproduce the 1-GPU frame byte for byte."""
+    import torch
+    hs, gs = scenes(1)
+    W, H = 1920, 1080
+    f = gs.frame(W, H, 4)
+    e = rtm.shard_elems(W, H, nranks)
+    gathered = torch.zeros(nranks * e, dtype=torch.int32, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    for r in range(nranks):
+        gs.render_shard_device(f, r, nranks, gathered.data_ptr() + 4 * r * e, stream)
+    out = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+    rtm.unshard_device(W, H, nranks, gathered.data_ptr(), out.data_ptr(), stream)
+    torch.cuda.synchronize()
+    img = out.cpu().numpy().view(np.uint32)
+    assert hashlib.sha256(img.tobytes()).hexdigest() == golden["frames_1080p4"]["1"]["bgra_sha256"]
+
+
+def test_render_frame_device_on_torch_stream(golden, scenes):
+    import torch
+    hs, gs = scenes(8)
+    out = torch.zeros(1920 * 1080, dtype=torch.int32, device="cuda")
+    gs.render_frame_device(gs.frame(1920, 1080, 4), out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    img = out.cpu().numpy().view(np.uint32)
+    assert hashlib.sha256(img.tobytes()).hexdigest() == golden["frames_1080p4"]["8"]["bgra_sha256"]
+    assert gs.last_kernel_ms() > 0
+
+
+def test_framebuffer_tile_pool_drop_in(golden, scenes, tmp_path):
+    """The host Framebuffer (12x9 tiles, worker pool) with the GPU RenderTile override."""
+    hs, gs = scenes(1)
+    r = rtm.Renderer(hs, gs)
+    r.set_sample_count(4)
+    r.resize(1920, 1080)
+    img = r.read()
+    assert hashlib.sha256(img.tobytes()).hexdigest() == golden["frames_1080p4"]["1"]["bgra_sha256"]
+    bmp = tmp_path / "shot.bmp"
+    r.save_to_bmp(str(bmp))
+    data = bmp.read_bytes()
+    assert data[:2] == b"BM" and len(data) == 54 + 1920 * 1080 * 4
+    assert data[54:] == img.tobytes()
+    r.start_rendering()
+    assert hashlib.sha256(r.read().tobytes()).hexdigest() == golden["frames_1080p4"]["1"]["bgra_sha256"]
+    r.close()
+
+
+def test_scene_validation_fails_loudly():
+    import ctypes
+    hs = rtm.HostScene.load(1)
+    L = rtm.tracer_lib()
+    d = hs.desc()
+    d.grid.dims[0] = 0
+    h = ctypes.c_void_p()
+    assert L.rt_scene_create(ctypes.byref(d), 0, ctypes.byref(h)) == 1     # RT_E_INVALID
+    d = hs.desc()
+    assert L.rt_scene_create(ctypes.byref(d), 99, ctypes.byref(h)) == 3    # RT_E_NODEVICE
