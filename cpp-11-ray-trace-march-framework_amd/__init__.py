@@ -8,7 +8,10 @@ The product is two in-tree shared libraries built by this package's Makefile:
   (grid.cpp:12-154) and the 12x9 ``Framebuffer`` tile pool with the GPU ``RenderTile``
   (framebuffer.cpp), ABI in ``include/rt_host.h``.
 
-This module binds both with ctypes.  There is no CPU fallback: if a library is missing or a
+This module binds both with ctypes.  In a process that also uses PyTorch, import torch
+BEFORE calling any function here: torch's wheel ships its own HIP runtime with the soname
+``librt_tracer.so`` links to, so loading torch first makes both share one runtime (device
+pointers and streams then interoperate).  There is no CPU fallback: if a library is missing or a
 call fails, :class:`RtError` is raised.  The directory name is not a Python identifier, so
 load it with :func:`load_package` from ``tests/``/``bench.py`` (importlib by path).
 """
