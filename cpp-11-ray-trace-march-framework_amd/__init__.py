@@ -25,7 +25,8 @@ REPO = os.path.dirname(HERE)
 SCENE_DIR = os.path.join(REPO, "data", "scenes")
 
 RT_TRI_MOLLER_TRUMBORE, RT_TRI_BARYCENTRIC = 0, 1
-RT_KERNEL_AUTO, RT_KERNEL_LANES, RT_KERNEL_PIXEL_LOOP, RT_KERNEL_COMPACT = 0, 1, 2, 3
+RT_KERNEL_AUTO, RT_KERNEL_LANES, RT_KERNEL_PIXEL_LOOP, RT_KERNEL_COMPACT, RT_KERNEL_PERSISTENT = 0, 1, 2, 3, 4
+RT_KERNEL_FLAG_PREFETCH = 0x100
 SHARD_TILE = 16
 
 # Symbols of include/rt_tracer.h and include/rt_host.h (checked by tests/test_abi.py)
@@ -414,3 +415,51 @@ class Renderer:
             self.close()
         except Exception:
             pass
+
+
+# ------------------------------------------------------------------ multi-GPU helpers
+def shard_tile_ids(width, height, rank, nranks):
+    """Tile indices (16x16 tiles, row-major) owned by `rank`: t % nranks == rank."""
+    tiles_x = (width + SHARD_TILE - 1) // SHARD_TILE
+    tiles_y = (height + SHARD_TILE - 1) // SHARD_TILE
+    return list(range(rank, tiles_x * tiles_y, nranks))
+
+
+def shard_from_frame(frame, rank, nranks):
+    """Host mirror of the kernel's shard layout: the rank's tiles, 256 words each, tile-local
+    row-major, zero padding outside the frame, padded to shard_elems(...)."""
+    H, W = frame.shape
+    tiles_x = (W + SHARD_TILE - 1) // SHARD_TILE
+    elems = (((W + 15) // 16) * ((H + 15) // 16) + nranks - 1) // nranks * 256
+    out = np.zeros(elems, np.uint32)
+    for k, t in enumerate(shard_tile_ids(W, H, rank, nranks)):
+        ty, tx = divmod(t, tiles_x)
+        blk = np.zeros((SHARD_TILE, SHARD_TILE), np.uint32)
+        src = frame[ty * 16:(ty + 1) * 16, tx * 16:(tx + 1) * 16]
+        blk[:src.shape[0], :src.shape[1]] = src
+        out[k * 256:(k + 1) * 256] = blk.reshape(-1)
+    return out
+
+
+def frame_from_shards(gathered, width, height, nranks):
+    """Host mirror of k_unshard (K3): gathered = concatenation of every rank's shard."""
+    elems = gathered.size // nranks
+    tiles_x = (width + SHARD_TILE - 1) // SHARD_TILE
+    y, x = np.mgrid[0:height, 0:width]
+    t = (y // 16) * tiles_x + x // 16
+    r, k = t % nranks, t // nranks
+    return gathered[r * elems + k * 256 + (y % 16) * 16 + (x % 16)].astype(np.uint32)
+
+
+def all_gather_shards(shard, world, group=None):
+    """All-gather equal-sized shards (RCCL over xGMI on GPUs, gloo on CPU tensors)."""
+    import torch
+    import torch.distributed as dist
+    out = torch.empty(world * shard.numel(), dtype=shard.dtype, device=shard.device)
+    if dist.get_backend(group) == "gloo":
+        parts = list(out.chunk(world))
+        dist.all_gather(parts, shard, group=group)
+        out = torch.cat(parts)
+    else:
+        dist.all_gather_into_tensor(out, shard, group=group)
+    return out

@@ -99,7 +99,7 @@ __device__ __forceinline__ uint32_t compact_bits(uint32_t v)
 
 // grid.cpp:159-281 Grid::Intersect (NEW_GRID_TRAVERSAL), axis arrays unrolled into scalars
 // so nothing is runtime-indexed (no scratch).  Counters are compiled in only for records.
-template <bool STATS>
+template <bool STATS, int TRI, bool PIPE>
 __device__ __forceinline__ bool grid_intersect(const KParams& P, const uint32_t *lds_occ,
                                                float ox, float oy, float oz,
                                                float dx, float dy, float dz,
@@ -121,36 +121,38 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, const uint32_t 
     else
         return false;
 
-    // grid.h:44-48 ToVoxel, grid.h:50-51 ToPos, grid.cpp:190-216 per-axis setup
+    // grid.h:44-48 ToVoxel, grid.h:50-51 ToPos, grid.cpp:190-216 per-axis setup.  Instead of
+    // pos/step/out per axis the walk keeps the cells left before 'pos == out' (rem) and the
+    // signed GridIdx stride of a step (cs): grid.cpp:274-277 exits after the same steps.
     auto to_voxel = [&](float g, int a) {
         const int vx = rtd::cvt_i32_x86((g - P.bmin[a]) * P.icw);
         const int hi = P.dim[a] - 1;
         return vx < 0 ? 0 : (vx > hi ? hi : vx);
     };
-    int pos0 = to_voxel(gx, 0), pos1 = to_voxel(gy, 1), pos2 = to_voxel(gz, 2);
+    const int pos0 = to_voxel(gx, 0), pos1 = to_voxel(gy, 1), pos2 = to_voxel(gz, 2);
     float nct0, nct1, nct2, dt0 = 0.0f, dt1 = 0.0f, dt2 = 0.0f;
-    int st0 = 0, st1 = 0, st2 = 0, out0 = 0, out1 = 0, out2 = 0;
-    auto setup = [&](float d, float g, int pos, int a, float& nct, float& dtv, int& st, int& outv) {
+    int rem0 = 0, rem1 = 0, rem2 = 0, cs0 = 0, cs1 = 0, cs2 = 0;
+    auto setup = [&](float d, float g, int pos, int a, int stride, float& nct, float& dtv, int& rem, int& cs) {
         if (d == 0.0f)
             nct = rtd::kFltMax;
         else if (d > 0.0f)
         {
             nct = enter_t + ((P.bmin[a] + float(pos + 1) * P.cw) - g) / d;
             dtv = P.cw / d;
-            st = 1;
-            outv = P.dim[a];
+            rem = P.dim[a] - 1 - pos;           // steps until pos + 1 == dim
+            cs = stride;
         }
         else
         {
             nct = enter_t + ((P.bmin[a] + float(pos) * P.cw) - g) / d;
             dtv = -P.cw / d;
-            st = -1;
-            outv = -1;
+            rem = pos;                          // steps until pos - 1 == -1
+            cs = -stride;
         }
     };
-    setup(dx, gx, pos0, 0, nct0, dt0, st0, out0);
-    setup(dy, gy, pos1, 1, nct1, dt1, st1, out1);
-    setup(dz, gz, pos2, 2, nct2, dt2, st2, out2);
+    setup(dx, gx, pos0, 0, 1, nct0, dt0, rem0, cs0);
+    setup(dy, gy, pos1, 1, P.dxdz, nct1, dt1, rem1, cs1);
+    setup(dz, gz, pos2, 2, P.dim[0], nct2, dt2, rem2, cs2);
 
     int cell = pos0 + pos2 * P.dim[0] + pos1 * P.dxdz;
     t = rtd::kFltMax;
@@ -165,15 +167,38 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, const uint32_t 
         if (occupied)
         {
             const uint32_t kb = P.off[cell], ke = P.off[cell + 1];
+            // Optionally software-pipelined over the cell's contiguous 48-B records (the loads
+            // of record k+1 in flight while record k is tested; costs registers/occupancy).
+            float4 n0, n1, n2;
+            if (PIPE && kb < ke)
+            {
+                n0 = P.refs[3 * kb + 0];
+                n1 = P.refs[3 * kb + 1];
+                n2 = P.refs[3 * kb + 2];
+            }
             for (uint32_t k = kb; k < ke; k++)
             {
-                const float4 r0 = P.refs[3 * k + 0];
-                const float4 r1 = P.refs[3 * k + 1];
-                const float4 r2 = P.refs[3 * k + 2];
+                float4 r0, r1, r2;
+                if (PIPE)
+                {
+                    r0 = n0; r1 = n1; r2 = n2;
+                    if (k + 1 < ke)
+                    {
+                        n0 = P.refs[3 * (k + 1) + 0];
+                        n1 = P.refs[3 * (k + 1) + 1];
+                        n2 = P.refs[3 * (k + 1) + 2];
+                    }
+                }
+                else
+                {
+                    r0 = P.refs[3 * k + 0];
+                    r1 = P.refs[3 * k + 1];
+                    r2 = P.refs[3 * k + 2];
+                }
                 const uint32_t id = __float_as_uint(r2.y);
                 float ct, cu, cv;
                 bool hit;
-                if (P.tri_test == RT_TRI_BARYCENTRIC)
+                if (TRI == RT_TRI_BARYCENTRIC)
                 {
                     const float4 fn = P.face_n[id];
                     hit = rtd::ray_tri_bary(ox, oy, oz, dx, dy, dz, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y,
@@ -194,31 +219,28 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, const uint32_t 
         // grid.cpp:274-277
         if (ax == 0)
         {
-            pos0 += st0;
-            if (pos0 == out0) break;
+            if (rem0-- == 0) break;
             nct0 += dt0;
-            cell += st0;
+            cell += cs0;
         }
         else if (ax == 1)
         {
-            pos1 += st1;
-            if (pos1 == out1) break;
+            if (rem1-- == 0) break;
             nct1 += dt1;
-            cell += st1 * P.dxdz;
+            cell += cs1;
         }
         else
         {
-            pos2 += st2;
-            if (pos2 == out2) break;
+            if (rem2-- == 0) break;
             nct2 += dt2;
-            cell += st2 * P.dim[0];
+            cell += cs2;
         }
     }
     return false;
 }
 
 // renderer.cpp:126-160: one sample -> its colour contribution
-template <bool STATS>
+template <bool STATS, int TRI, bool PIPE>
 __device__ __forceinline__ void trace_sample(const KParams& P, const uint32_t *lds_occ, uint32_t px, uint32_t py,
                                              uint32_t s, float& cr, float& cg, float& cb,
                                              rt_sample_rec *rec)
@@ -228,7 +250,7 @@ __device__ __forceinline__ void trace_sample(const KParams& P, const uint32_t *l
     rtd::gen_dir(P.m, P.fov_xs, P.aspect, px, py, P.W, P.H, so.x, so.y, dx, dy, dz);
     float t = 0.0f, u = 0.0f, v = 0.0f;
     uint32_t tri = rtd::kNoTri, voxel = rtd::kNoTri, steps = 0, tests = 0;
-    const bool hit = grid_intersect<STATS>(P, lds_occ, P.org[0], P.org[1], P.org[2], dx, dy, dz,
+    const bool hit = grid_intersect<STATS, TRI, PIPE>(P, lds_occ, P.org[0], P.org[1], P.org[2], dx, dy, dz,
                                            t, u, v, tri, voxel, steps, tests);
     if (hit)
     {
@@ -255,13 +277,6 @@ __device__ __forceinline__ void trace_sample(const KParams& P, const uint32_t *l
     }
 }
 
-__device__ __forceinline__ void stage_occupancy(const KParams& P, uint32_t *lds_occ)
-{
-    for (uint32_t i = threadIdx.x; i < P.occ_words; i += blockDim.x)
-        lds_occ[i] = P.occ[i];
-    __syncthreads();
-}
-
 // Tile bookkeeping shared by both render kernels: block -> (local tile k, sub-block)
 struct TileCoord { uint32_t k, sub, tx0, ty0; };
 
@@ -286,25 +301,44 @@ __device__ __forceinline__ void store_pixel(const KParams& P, const TileCoord& c
         P.out[size_t(y - P.ry0) * P.pitch + (x - P.rx0)] = word;
 }
 
-// RT_KERNEL_LANES: one lane per sample (spp = 2^spp_shift <= 64)
-__global__ void __launch_bounds__(kWG) k_render_lanes(KParams P)
+// One wave-sized work item = 64 consecutive sample slots of a 16x16 tile in Morton order
+// (a 2^k x 2^k pixel block x spp samples).  Traces the lane's sample, sums the pixel's
+// samples across its adjacent lanes in sample order (renderer.cpp:125-160, hazard H10) and
+// stores the packed pixel (renderer.cpp:162-171).
+struct ItemCoord { TileCoord c; uint32_t p, s, x, y; bool valid; };
+
+// Pixel/sample of this lane in work item `item` (wave-uniform).  Called before AND after the
+// traversal so none of it is live (in VGPRs) across the DDA walk.
+__device__ __forceinline__ ItemCoord item_coord(const KParams& P, uint32_t item, uint32_t lane)
 {
-    const uint32_t *lds_occ = nullptr;   // occupancy staging pays only in the persistent kernel
-    const bool use_occ = false;
+    ItemCoord ic;
+    const uint32_t items_per_tile = P.wg_per_tile * (kWG / 64u);
+    ic.c.k = item / items_per_tile;
+    const uint32_t slot = (item - ic.c.k * items_per_tile) * 64u + lane;
+    const uint32_t t = P.rank + ic.c.k * P.nranks;
+    const uint32_t tyi = t / P.tiles_x;
+    ic.c.tx0 = P.rx0 + (t - tyi * P.tiles_x) * kTile;
+    ic.c.ty0 = P.ry0 + tyi * kTile;
+    ic.p = slot >> P.spp_shift;                               // pixel index in the tile (Morton)
+    ic.s = slot & (P.spp - 1u);
+    ic.x = ic.c.tx0 + compact_bits(ic.p);
+    ic.y = ic.c.ty0 + compact_bits(ic.p >> 1);
+    ic.valid = ic.x < P.rx0 + P.rw && ic.y < P.ry0 + P.rh;
+    return ic;
+}
 
-    const TileCoord c = tile_of_block(P);
-    const uint32_t slot = c.sub * kWG + threadIdx.x;
-    const uint32_t p = slot >> P.spp_shift;                   // pixel index in the tile (Morton)
-    const uint32_t s = slot & (P.spp - 1u);
-    const uint32_t x = c.tx0 + compact_bits(p), y = c.ty0 + compact_bits(p >> 1);
-    const bool valid = x < P.rx0 + P.rw && y < P.ry0 + P.rh;
-
-    float cr = 0.0f, cg = 0.0f, cb = 0.0f;
-    if (valid)
-        trace_sample<false>(P, use_occ ? lds_occ : nullptr, x, y, s, cr, cg, cb, nullptr);
-
-    // Sum the pixel's samples in sample order (renderer.cpp:125-160): lanes base..base+spp-1
+template <int TRI, bool PIPE>
+__device__ __forceinline__ void process_item(const KParams& P, const uint32_t *lds_occ, uint32_t item)
+{
+    item = __builtin_amdgcn_readfirstlane(item);
     const uint32_t lane = threadIdx.x & 63u;
+    float cr = 0.0f, cg = 0.0f, cb = 0.0f;
+    {
+        const ItemCoord ic = item_coord(P, item, lane);
+        if (ic.valid)
+            trace_sample<false, TRI, PIPE>(P, lds_occ, ic.x, ic.y, ic.s, cr, cg, cb, nullptr);
+    }
+    const ItemCoord ic = item_coord(P, item, lane);
     const uint32_t base = lane & ~(P.spp - 1u);
     float sr = 0.0f, sg = 0.0f, sb = 0.0f;
     for (uint32_t k = 0; k < P.spp; k++)
@@ -313,16 +347,45 @@ __global__ void __launch_bounds__(kWG) k_render_lanes(KParams P)
         sg += __shfl(cg, int(base + k), 64);
         sb += __shfl(cb, int(base + k), 64);
     }
-    if (valid && s == 0)
+    if (ic.valid && ic.s == 0)
     {
         const float fs = float(P.spp);
         const uint32_t word = rtd::pack_bgra8(rtd::gamma_half(sr / fs), rtd::gamma_half(sg / fs),
                                               rtd::gamma_half(sb / fs));
-        store_pixel(P, c, p, x, y, word);
+        store_pixel(P, ic.c, ic.p, ic.x, ic.y, word);
     }
 }
 
+// RT_KERNEL_LANES: one lane per sample (spp = 2^spp_shift <= 64), one work item per wave,
+// no LDS.  Kept as the A/B baseline of the persistent kernel.
+template <int TRI, bool PIPE>
+__global__ void __launch_bounds__(kWG) k_render_lanes(KParams P)
+{
+    process_item<TRI, PIPE>(P, nullptr, blockIdx.x * (kWG / 64u) + (threadIdx.x >> 6));
+}
+
+// RT_KERNEL_PERSISTENT (spp a power of two <= 64): persistent 512-lane workgroups, 4 per CU.  The
+// 1-bit-per-cell occupancy bitmap (<= 32 KiB for a 64^3 grid) is staged into LDS once per
+// workgroup, so walking an empty cell costs one ds_read instead of a dependent L2 round trip
+// for its CSR offsets.  Waves take work items round-robin (item = wave, wave + nwaves, ...):
+// neighbouring items cost alike, so the static interleave balances without atomics.
+constexpr uint32_t kPersistWG = 512;    // 8 waves; 4 workgroups (128 KiB of bitmaps) per CU
+
+template <int TRI, bool PIPE>
+__global__ void __launch_bounds__(kPersistWG, 8) k_render_persistent(KParams P, uint32_t n_items)
+{
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds_occ[];
+    for (uint32_t i = threadIdx.x; i < P.occ_words; i += blockDim.x)
+        lds_occ[i] = P.occ[i];
+    __syncthreads();
+    const uint32_t waves_per_wg = blockDim.x >> 6;
+    const uint32_t nwaves = gridDim.x * waves_per_wg;
+    for (uint32_t item = blockIdx.x * waves_per_wg + (threadIdx.x >> 6); item < n_items; item += nwaves)
+        process_item<TRI, PIPE>(P, lds_occ, item);
+}
+
 // RT_KERNEL_PIXEL_LOOP: one lane per pixel, samples looped in order (any spp)
+template <int TRI>
 __global__ void __launch_bounds__(kWG) k_render_pixel_loop(KParams P)
 {
     const uint32_t *lds_occ = nullptr;
@@ -336,7 +399,7 @@ __global__ void __launch_bounds__(kWG) k_render_pixel_loop(KParams P)
     for (uint32_t s = 0; s < P.spp; s++)
     {
         float cr, cg, cb;
-        trace_sample<false>(P, use_occ ? lds_occ : nullptr, x, y, s, cr, cg, cb, nullptr);
+        trace_sample<false, TRI, false>(P, use_occ ? lds_occ : nullptr, x, y, s, cr, cg, cb, nullptr);
         sr += cr; sg += cg; sb += cb;
     }
     const float fs = float(P.spp);
@@ -352,7 +415,10 @@ __global__ void __launch_bounds__(kWG) k_trace_records(KParams P, uint32_t n)
     const uint32_t s = i % P.spp, pix = i / P.spp;
     const uint32_t x = P.rec_x0 + pix % P.rec_w, y = P.rec_y0 + pix / P.rec_w;
     float cr, cg, cb;
-    trace_sample<true>(P, nullptr, x, y, s, cr, cg, cb, &P.recs[i]);
+    if (P.tri_test == RT_TRI_BARYCENTRIC)
+        trace_sample<true, RT_TRI_BARYCENTRIC, false>(P, nullptr, x, y, s, cr, cg, cb, &P.recs[i]);
+    else
+        trace_sample<true, RT_TRI_MOLLER_TRUMBORE, false>(P, nullptr, x, y, s, cr, cg, cb, &P.recs[i]);
 }
 
 // K3: gathered shards [rank][local tile][256] -> frame
@@ -470,6 +536,7 @@ struct rt_scene
     uint32_t *d_off = nullptr, *d_occ = nullptr;
     float4 *d_refs = nullptr, *d_shade = nullptr, *d_facen = nullptr;
     uint64_t device_bytes = 0;
+    uint32_t persist_wgs = 1024;    // persistent grid: 4 x 512-lane workgroups per CU
     // sample table cache
     float2 *d_smp = nullptr;
     uint32_t smp_cap = 0;
@@ -528,10 +595,12 @@ int validate_frame(const rt_frame *f)
     if (f->width == 0 || f->height == 0 || f->width > 65536 || f->height > 65536)
         return fail(RT_E_INVALID, "frame width/height must be in [1, 65536]");
     if (f->tri_test > RT_TRI_BARYCENTRIC) return fail(RT_E_INVALID, "unknown tri_test");
-    if (f->kernel > RT_KERNEL_COMPACT) return fail(RT_E_INVALID, "unknown kernel");
+    if ((f->kernel & 0xFFu) > RT_KERNEL_PERSISTENT || (f->kernel & ~(0xFFu | RT_KERNEL_FLAG_PREFETCH)))
+        return fail(RT_E_INVALID, "unknown kernel");
     const uint32_t spp = std::max(1u, f->spp);
     if (spp > 4096) return fail(RT_E_INVALID, "spp must be <= 4096");
-    if (f->kernel == RT_KERNEL_LANES && !(is_pow2(spp) && spp <= 64))
+    if (((f->kernel & 0xFFu) == RT_KERNEL_LANES || (f->kernel & 0xFFu) == RT_KERNEL_PERSISTENT) &&
+        !(is_pow2(spp) && spp <= 64))
         return fail(RT_E_INVALID, "RT_KERNEL_LANES needs spp to be a power of two <= 64");
     return RT_OK;
 }
@@ -574,7 +643,7 @@ void frame_params(const rt_scene *s, const rt_frame *f, KParams& P)
 
 bool use_lanes(const rt_frame *f, uint32_t spp)
 {
-    if (f->kernel == RT_KERNEL_PIXEL_LOOP) return false;
+    if ((f->kernel & 0xFFu) == RT_KERNEL_PIXEL_LOOP) return false;
     return is_pow2(spp) && spp <= 64;
 }
 
@@ -584,15 +653,39 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
     if (n_local_tiles == 0) return RT_OK;
     const bool lanes = use_lanes(f, P.spp);
     P.wg_per_tile = lanes ? (kTilePix * P.spp) / kWG : 1;
-    if (lanes && P.wg_per_tile == 0) P.wg_per_tile = 1;
-    // lanes mode with spp < ... : 256 * spp / 256 = spp workgroups per tile (spp >= 1)
+    if (P.wg_per_tile == 0) P.wg_per_tile = 1;
     const uint64_t blocks = uint64_t(n_local_tiles) * P.wg_per_tile;
-    if (blocks > 0x7FFFFFFFull) return fail(RT_E_INVALID, "frame too large for one launch");
+    if (blocks > 0x3FFFFFFFull) return fail(RT_E_INVALID, "frame too large for one launch");
     RT_HIP(hipEventRecord(s->ev0, st));
-    if (lanes)
-        hipLaunchKernelGGL(k_render_lanes, dim3(uint32_t(blocks)), dim3(kWG), 0, st, P);
+    const uint32_t kind = f->kernel & 0xFFu;
+    const bool pipe = (f->kernel & RT_KERNEL_FLAG_PREFETCH) != 0;
+    const bool bary = P.tri_test == RT_TRI_BARYCENTRIC;
+    if (lanes && kind == RT_KERNEL_PERSISTENT && P.occ_words)
+    {
+        const uint32_t n_items = uint32_t(blocks * (kWG / 64u));
+        const uint32_t per_wg = kPersistWG / 64u;
+        const uint32_t grid = std::max(1u, std::min(s->persist_wgs, (n_items + per_wg - 1) / per_wg));
+        const size_t lds = P.occ_words * 4u;
+        if (bary)
+            hipLaunchKernelGGL((k_render_persistent<RT_TRI_BARYCENTRIC, false>), dim3(grid), dim3(kPersistWG), lds, st, P, n_items);
+        else if (pipe)
+            hipLaunchKernelGGL((k_render_persistent<RT_TRI_MOLLER_TRUMBORE, true>), dim3(grid), dim3(kPersistWG), lds, st, P, n_items);
+        else
+            hipLaunchKernelGGL((k_render_persistent<RT_TRI_MOLLER_TRUMBORE, false>), dim3(grid), dim3(kPersistWG), lds, st, P, n_items);
+    }
+    else if (lanes)
+    {
+        if (bary)
+            hipLaunchKernelGGL((k_render_lanes<RT_TRI_BARYCENTRIC, false>), dim3(uint32_t(blocks)), dim3(kWG), 0, st, P);
+        else if (pipe)
+            hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, true>), dim3(uint32_t(blocks)), dim3(kWG), 0, st, P);
+        else
+            hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, false>), dim3(uint32_t(blocks)), dim3(kWG), 0, st, P);
+    }
+    else if (bary)
+        hipLaunchKernelGGL((k_render_pixel_loop<RT_TRI_BARYCENTRIC>), dim3(uint32_t(blocks)), dim3(kWG), 0, st, P);
     else
-        hipLaunchKernelGGL(k_render_pixel_loop, dim3(uint32_t(blocks)), dim3(kWG), 0, st, P);
+        hipLaunchKernelGGL((k_render_pixel_loop<RT_TRI_MOLLER_TRUMBORE>), dim3(uint32_t(blocks)), dim3(kWG), 0, st, P);
     RT_HIP(hipGetLastError());
     RT_HIP(hipEventRecord(s->ev1, st));
     s->ev_recorded = true;
@@ -665,6 +758,7 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
 
     std::unique_ptr<rt_scene> s(new rt_scene());
     s->device = device;
+    s->persist_wgs = 4u * uint32_t(std::max(1, prop.multiProcessorCount));
     for (int a = 0; a < 3; a++)
     {
         s->dims[a] = g.dims[a];

@@ -73,10 +73,12 @@ typedef struct rt_scene_desc {
 enum rt_tri_test { RT_TRI_MOLLER_TRUMBORE = 0, RT_TRI_BARYCENTRIC = 1 };
 
 enum rt_kernel {
-    RT_KERNEL_AUTO = 0,        /* LANES when spp is a power of two <= 64, else PIXEL_LOOP */
+    RT_KERNEL_AUTO = 0,        /* the fastest measured variant for the frame's spp */
     RT_KERNEL_LANES = 1,       /* one lane per sample, a pixel's samples in adjacent lanes */
     RT_KERNEL_PIXEL_LOOP = 2,  /* one lane per pixel looping over its samples (any spp) */
     RT_KERNEL_COMPACT = 3,     /* LANES + wavefront active-ray compaction (ballot/prefix refill) */
+    RT_KERNEL_PERSISTENT = 4,  /* LANES in persistent workgroups with the LDS cell-occupancy bitmap */
+    RT_KERNEL_FLAG_PREFETCH = 0x100,  /* OR-able: software-pipelined triangle record loads */
 };
 
 /* Per-frame parameters: what Renderer::RenderTile reads from the Scene and itself. */
