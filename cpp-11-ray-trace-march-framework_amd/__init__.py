@@ -344,7 +344,7 @@ def unshard_device(width, height, nranks, d_gathered, d_out, stream=0):
            "rt_unshard_device")
 
 
-PRIM_WIDTHS = {0: (18, 8), 1: (12, 4), 2: (23, 6), 3: (3, 4), 4: (11, 3)}
+PRIM_WIDTHS = {0: (18, 8), 1: (12, 4), 2: (23, 6), 3: (3, 4), 4: (11, 3), 5: (18, 8)}
 
 
 def debug_primitives(kind, records, device=0):

@@ -86,6 +86,35 @@ __device__ __forceinline__ bool ray_tri_mt(float ox, float oy, float oz, float d
     return t >= 0.0f;
 }
 
+// Branch-free form of ray_tri_mt for the traversal loop: every quantity is computed with the
+// same operations in the same order, and the early-outs of triangle.h:77-101 become one
+// predicate.  For an accepted hit t, u, v are bit-identical to ray_tri_mt's; rejected
+// lanes merely carry garbage the caller ignores.  No divergent branches -> no exec-mask
+// bookkeeping per test (SQ counters: SALU ~ VALU in the branchy loop).
+__device__ __forceinline__ bool ray_tri_mt_pred(float ox, float oy, float oz, float dx, float dy, float dz,
+                                                float v0x, float v0y, float v0z,
+                                                float e1x, float e1y, float e1z,
+                                                float e2x, float e2y, float e2z,
+                                                float& t, float& u, float& v)
+{
+    const float px = dy * e2z - dz * e2y;
+    const float py = dz * e2x - dx * e2z;
+    const float pz = dx * e2y - dy * e2x;
+    const float det = e1x * px + e1y * py + e1z * pz;
+    const float inv_det = 1.0f / det;
+    const float tx = ox - v0x, ty = oy - v0y, tz = oz - v0z;
+    u = (tx * px + ty * py + tz * pz) * inv_det;
+    const float qx = ty * e1z - tz * e1y;
+    const float qy = tz * e1x - tx * e1z;
+    const float qz = tx * e1y - ty * e1x;
+    v = (dx * qx + dy * qy + dz * qz) * inv_det;
+    t = (e2x * qx + e2y * qy + e2z * qz) * inv_det;
+    const bool det_ok = !(det > -0.00000001f && det < 0.00000001f);
+    const bool u_ok = !(u < 0.0f || u > 1.0f);
+    const bool v_ok = !(v < 0.0f || u + v > 1.0f);
+    return det_ok & u_ok & v_ok & (t >= 0.0f);
+}
+
 // triangle.h:200-226 IntersectRayPlane + ComputeBarycentric (:133-156). Uses v0, the same
 // e1 (= v1 - v0) and e2 (= v2 - v0, the reference's e0) and the face normal.
 __device__ __forceinline__ bool ray_tri_bary(float ox, float oy, float oz, float dx, float dy, float dz,
@@ -111,6 +140,31 @@ __device__ __forceinline__ bool ray_tri_bary(float ox, float oy, float oz, float
     u = (d00 * d12 - d01 * d02) * inv_denom;
     v = (d11 * d02 - d01 * d12) * inv_denom;
     return (u >= 0.0f) && (v >= 0.0f) && (u + v < 1.0f);
+}
+
+// Branch-free form of ray_tri_bary (same operations; accepted results bit-identical).
+__device__ __forceinline__ bool ray_tri_bary_pred(float ox, float oy, float oz, float dx, float dy, float dz,
+                                                  float v0x, float v0y, float v0z,
+                                                  float e1x, float e1y, float e1z,
+                                                  float e2x, float e2y, float e2z,
+                                                  float nx, float ny, float nz,
+                                                  float& t, float& u, float& v)
+{
+    const float denom = dot3(nx, ny, nz, dx, dy, dz);
+    const float dd = dot3(nx, ny, nz, v0x, v0y, v0z);
+    t = (dd - dot3(nx, ny, nz, ox, oy, oz)) / denom;
+    const float qx = ox + dx * t, qy = oy + dy * t, qz = oz + dz * t;
+    const float wx = qx - v0x, wy = qy - v0y, wz = qz - v0z;
+    const float d00 = dot3(e2x, e2y, e2z, e2x, e2y, e2z);
+    const float d01 = dot3(e2x, e2y, e2z, e1x, e1y, e1z);
+    const float d02 = dot3(e2x, e2y, e2z, wx, wy, wz);
+    const float d11 = dot3(e1x, e1y, e1z, e1x, e1y, e1z);
+    const float d12 = dot3(e1x, e1y, e1z, wx, wy, wz);
+    const float inv_denom = 1.0f / (d00 * d11 - d01 * d01);
+    u = (d00 * d12 - d01 * d02) * inv_denom;
+    v = (d11 * d02 - d01 * d12) * inv_denom;
+    const bool plane_ok = !(__builtin_fabsf(denom) < 0.00000001f) & (t >= 0.0f);
+    return plane_ok & (u >= 0.0f) & (v >= 0.0f) & (u + v < 1.0f);
 }
 
 // aabb.h:9-13

@@ -201,40 +201,31 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, const uint32_t 
                 if (TRI == RT_TRI_BARYCENTRIC)
                 {
                     const float4 fn = P.face_n[id];
-                    hit = rtd::ray_tri_bary(ox, oy, oz, dx, dy, dz, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y,
-                                            r1.z, r1.w, r2.x, fn.x, fn.y, fn.z, ct, cu, cv);
+                    hit = rtd::ray_tri_bary_pred(ox, oy, oz, dx, dy, dz, r0.x, r0.y, r0.z, r0.w, r1.x,
+                                                 r1.y, r1.z, r1.w, r2.x, fn.x, fn.y, fn.z, ct, cu, cv);
                 }
                 else
-                    hit = rtd::ray_tri_mt(ox, oy, oz, dx, dy, dz, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y,
-                                          r1.z, r1.w, r2.x, ct, cu, cv);
+                    hit = rtd::ray_tri_mt_pred(ox, oy, oz, dx, dy, dz, r0.x, r0.y, r0.z, r0.w, r1.x,
+                                               r1.y, r1.z, r1.w, r2.x, ct, cu, cv);
                 if (STATS) tests++;
                 // grid.cpp:258-266: strict '<' over the ascending list keeps the first of ties
-                if (hit && ct < t && ct < nct_ax)
-                {
-                    t = ct; u = cu; v = cv; tri = id;
-                }
+                const bool take = hit & (ct < t) & (ct < nct_ax);
+                t = take ? ct : t;
+                u = take ? cu : u;
+                v = take ? cv : v;
+                tri = take ? id : tri;
             }
             if (t != rtd::kFltMax) return true;               // grid.cpp:270-271
         }
-        // grid.cpp:274-277
-        if (ax == 0)
-        {
-            if (rem0-- == 0) break;
-            nct0 += dt0;
-            cell += cs0;
-        }
-        else if (ax == 1)
-        {
-            if (rem1-- == 0) break;
-            nct1 += dt1;
-            cell += cs1;
-        }
-        else
-        {
-            if (rem2-- == 0) break;
-            nct2 += dt2;
-            cell += cs2;
-        }
+        // grid.cpp:274-277 as selects (exact: untouched axes keep their values)
+        const bool a0 = ax == 0, a1 = ax == 1, a2 = ax == 2;
+        const int rem = a0 ? rem0 : (a1 ? rem1 : rem2);
+        if (rem == 0) break;
+        rem0 -= int(a0); rem1 -= int(a1); rem2 -= int(a2);
+        nct0 = a0 ? nct0 + dt0 : nct0;
+        nct1 = a1 ? nct1 + dt1 : nct1;
+        nct2 = a2 ? nct2 + dt2 : nct2;
+        cell += a0 ? cs0 : (a1 ? cs1 : cs2);
     }
     return false;
 }
@@ -451,6 +442,20 @@ __global__ void __launch_bounds__(kWG) k_primitives(int kind, const float *in, u
         float bt = __builtin_nanf(""), bu = bt, bv = bt;
         const bool hb = rtd::ray_tri_bary(a[0], a[1], a[2], a[3], a[4], a[5], a[6], a[7], a[8],
                                           e1x, e1y, e1z, e2x, e2y, e2z, a[15], a[16], a[17], bt, bu, bv);
+        o[4] = __uint_as_float(hb); o[5] = bt; o[6] = bu; o[7] = bv;
+    }
+    else if (kind == 5)   // branch-free traversal variants: hit flag + t,u,v (hits only)
+    {
+        const float *a = in + 18 * i;
+        float *o = out + 8 * i;
+        const float e1x = a[9] - a[6], e1y = a[10] - a[7], e1z = a[11] - a[8];
+        const float e2x = a[12] - a[6], e2y = a[13] - a[7], e2z = a[14] - a[8];
+        float t, u, v, bt, bu, bv;
+        const bool h = rtd::ray_tri_mt_pred(a[0], a[1], a[2], a[3], a[4], a[5], a[6], a[7], a[8],
+                                            e1x, e1y, e1z, e2x, e2y, e2z, t, u, v);
+        const bool hb = rtd::ray_tri_bary_pred(a[0], a[1], a[2], a[3], a[4], a[5], a[6], a[7], a[8],
+                                               e1x, e1y, e1z, e2x, e2y, e2z, a[15], a[16], a[17], bt, bu, bv);
+        o[0] = __uint_as_float(h); o[1] = t; o[2] = u; o[3] = v;
         o[4] = __uint_as_float(hb); o[5] = bt; o[6] = bu; o[7] = bv;
     }
     else if (kind == 1)
@@ -1010,8 +1015,8 @@ int rt_trace_samples(rt_scene *s, const rt_frame *f, uint32_t x0, uint32_t y0, u
 
 int rt_debug_primitives(int kind, const float *in, uint32_t n, float *out, int device)
 {
-    static const uint32_t in_w[5] = { 18, 12, 23, 3, 11 }, out_w[5] = { 8, 4, 6, 4, 3 };
-    if (kind < 0 || kind > 4 || !in || !out) return fail(RT_E_INVALID, "bad arguments");
+    static const uint32_t in_w[6] = { 18, 12, 23, 3, 11, 18 }, out_w[6] = { 8, 4, 6, 4, 3, 8 };
+    if (kind < 0 || kind > 5 || !in || !out) return fail(RT_E_INVALID, "bad arguments");
     if (n == 0) return RT_OK;
     RT_HIP(hipSetDevice(device));
     std::vector<float> host_in(in, in + size_t(in_w[kind]) * n);

@@ -153,7 +153,8 @@ int  rt_trace_samples(rt_scene *scene, const rt_frame *frame, uint32_t x0, uint3
 
 /* Device evaluation of the primitives for known-answer tests (input layouts as the
  * tests/golden/kat_*.f32 records):  0 ray/tri (18 in, 8 out), 1 ray/aabb (12 in, 4 out),
- * 2 generate ray (23 in, 6 out), 3 gamma+pack (3 in, 4 out), 4 shade (11 in, 3 out). */
+ * 2 generate ray (23 in, 6 out), 3 gamma+pack (3 in, 4 out), 4 shade (11 in, 3 out),
+ * 5 the branch-free ray/tri forms the traversal uses (18 in, 8 out; t,u,v valid on hits). */
 int  rt_debug_primitives(int kind, const float *in, uint32_t n, float *out, int device);
 
 /* Hammersley table the library uses when rt_frame.sample_offsets is NULL. */

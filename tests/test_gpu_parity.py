@@ -47,6 +47,16 @@ def test_device_kat_ray_tri():
     np.testing.assert_array_equal(bits(rtm.debug_primitives(0, rin)), bits(exp))
 
 
+def test_device_kat_branch_free_ray_tri():
+    """The predicated tests used inside the DDA loop: same hit flags, bit-identical t,u,v on hits."""
+    rin, exp = load_kat("ray_tri")
+    got = rtm.debug_primitives(5, rin)
+    for h, cols in ((0, [1, 2, 3]), (4, [5, 6, 7])):
+        np.testing.assert_array_equal(bits(got[:, h]), bits(exp[:, h]))
+        m = bits(exp[:, h]) == 1
+        np.testing.assert_array_equal(bits(got[m][:, cols]), bits(exp[m][:, cols]))
+
+
 def test_device_kat_ray_aabb():
     rin, exp = load_kat("ray_aabb")
     np.testing.assert_array_equal(bits(rtm.debug_primitives(1, rin)), bits(exp))
