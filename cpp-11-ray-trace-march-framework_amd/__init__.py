@@ -27,6 +27,8 @@ SCENE_DIR = os.path.join(REPO, "data", "scenes")
 RT_TRI_MOLLER_TRUMBORE, RT_TRI_BARYCENTRIC = 0, 1
 RT_KERNEL_AUTO, RT_KERNEL_LANES, RT_KERNEL_PIXEL_LOOP, RT_KERNEL_COMPACT, RT_KERNEL_PERSISTENT = 0, 1, 2, 3, 4
 RT_KERNEL_FLAG_PREFETCH = 0x100
+RT_KERNEL_FLAG_WAVE_GATE = 0x200
+RT_KERNEL_FLAG_LOOKAHEAD = 0x400
 SHARD_TILE = 16
 
 # Symbols of include/rt_tracer.h and include/rt_host.h (checked by tests/test_abi.py)

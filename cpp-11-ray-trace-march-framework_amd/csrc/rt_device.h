@@ -115,6 +115,32 @@ __device__ __forceinline__ bool ray_tri_mt_pred(float ox, float oy, float oz, fl
     return det_ok & u_ok & v_ok & (t >= 0.0f);
 }
 
+// ray_tri_mt_pred with a wave-uniform early out: when no active lane passes the det and u
+// checks (triangle.h:77-87) the q/v/t half is skipped for the whole wave.  A scalar branch
+// (s_cbranch on a ballot), not a divergent one; results identical to ray_tri_mt_pred.
+__device__ __forceinline__ bool ray_tri_mt_gated(float ox, float oy, float oz, float dx, float dy, float dz,
+                                                 float v0x, float v0y, float v0z,
+                                                 float e1x, float e1y, float e1z,
+                                                 float e2x, float e2y, float e2z,
+                                                 float& t, float& u, float& v)
+{
+    const float px = dy * e2z - dz * e2y;
+    const float py = dz * e2x - dx * e2z;
+    const float pz = dx * e2y - dy * e2x;
+    const float det = e1x * px + e1y * py + e1z * pz;
+    const float inv_det = 1.0f / det;
+    const float tx = ox - v0x, ty = oy - v0y, tz = oz - v0z;
+    u = (tx * px + ty * py + tz * pz) * inv_det;
+    const bool ok1 = !(det > -0.00000001f && det < 0.00000001f) & !(u < 0.0f || u > 1.0f);
+    if (!__any(ok1)) return false;
+    const float qx = ty * e1z - tz * e1y;
+    const float qy = tz * e1x - tx * e1z;
+    const float qz = tx * e1y - ty * e1x;
+    v = (dx * qx + dy * qy + dz * qz) * inv_det;
+    t = (e2x * qx + e2y * qy + e2z * qz) * inv_det;
+    return ok1 & !(v < 0.0f || u + v > 1.0f) & (t >= 0.0f);
+}
+
 // triangle.h:200-226 IntersectRayPlane + ComputeBarycentric (:133-156). Uses v0, the same
 // e1 (= v1 - v0) and e2 (= v2 - v0, the reference's e0) and the face normal.
 __device__ __forceinline__ bool ray_tri_bary(float ox, float oy, float oz, float dx, float dy, float dz,

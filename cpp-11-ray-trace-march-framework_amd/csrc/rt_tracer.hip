@@ -53,6 +53,9 @@ constexpr uint32_t kTile = 16;              // shard / scheduling tile edge (pix
 constexpr uint32_t kTilePix = kTile * kTile;
 constexpr uint32_t kWG = 256;               // lanes per workgroup
 constexpr uint32_t kMaxOccWords = 8192;     // LDS occupancy bitmap: up to 262,144 cells (64^3)
+constexpr int kVarPrefetch = 1;             // RT_KERNEL_FLAG_PREFETCH
+constexpr int kVarWaveGate = 2;             // RT_KERNEL_FLAG_WAVE_GATE
+constexpr int kVarLookahead = 4;            // RT_KERNEL_FLAG_LOOKAHEAD
 
 struct KParams
 {
@@ -97,9 +100,93 @@ __device__ __forceinline__ uint32_t compact_bits(uint32_t v)
     return v;
 }
 
+// Tests a cell's list [kb, ke) in order (grid.cpp:243-267); true when it produced a hit.
+// t starts at FLT_MAX for every cell the walk reaches (a hit returns, grid.cpp:270-271).
+template <bool STATS, int TRI, int VAR>
+__device__ __forceinline__ bool test_cell(const KParams& P, float ox, float oy, float oz, float dx, float dy,
+                                          float dz, uint32_t kb, uint32_t ke, float nct_ax, float& t,
+                                          float& u, float& v, uint32_t& tri, uint32_t& tests)
+{
+        float4 n0, n1, n2;
+    if ((VAR & kVarPrefetch) && kb < ke)
+    {
+        const float4 *rp = P.refs + size_t(kb) * 3;
+        n0 = rp[0];
+        n1 = rp[1];
+        n2 = rp[2];
+    }
+    for (uint32_t k = kb; k < ke; k++)
+    {
+        float4 r0, r1, r2;
+        if (VAR & kVarPrefetch)
+        {
+            r0 = n0; r1 = n1; r2 = n2;
+            if (k + 1 < ke)
+            {
+                const float4 *rp = P.refs + size_t(k + 1) * 3;
+                n0 = rp[0];
+                n1 = rp[1];
+                n2 = rp[2];
+            }
+        }
+        else
+        {
+            const float4 *rp = P.refs + size_t(k) * 3;   // one address, immediate offsets
+            r0 = rp[0];
+            r1 = rp[1];
+            r2 = rp[2];
+        }
+        const uint32_t id = __float_as_uint(r2.y);
+        float ct, cu, cv;
+        bool hit;
+        if (TRI == RT_TRI_BARYCENTRIC)
+        {
+            const float4 fn = P.face_n[id];
+            hit = rtd::ray_tri_bary_pred(ox, oy, oz, dx, dy, dz, r0.x, r0.y, r0.z, r0.w, r1.x,
+                                         r1.y, r1.z, r1.w, r2.x, fn.x, fn.y, fn.z, ct, cu, cv);
+        }
+        else if (VAR & kVarWaveGate)
+            hit = rtd::ray_tri_mt_gated(ox, oy, oz, dx, dy, dz, r0.x, r0.y, r0.z, r0.w, r1.x,
+                                        r1.y, r1.z, r1.w, r2.x, ct, cu, cv);
+        else
+            hit = rtd::ray_tri_mt_pred(ox, oy, oz, dx, dy, dz, r0.x, r0.y, r0.z, r0.w, r1.x,
+                                       r1.y, r1.z, r1.w, r2.x, ct, cu, cv);
+        if (STATS) tests++;
+        // grid.cpp:258-266: strict '<' over the ascending list keeps the first of ties
+        const bool take = hit & (ct < t) & (ct < nct_ax);
+        t = take ? ct : t;
+        u = take ? cu : u;
+        v = take ? cv : v;
+        tri = take ? id : tri;
+    }
+    return t != rtd::kFltMax;                             // grid.cpp:270-271
+}
+
+// One DDA advance over plain local variables (grid.cpp:236-239 + 274-277) written as
+// selects, exact because untouched axes keep their values.  A macro, not a member function or
+// a capturing lambda: selecting between struct fields through `this`/references becomes a
+// pointer select, which defeats SROA and put the walk state in LDS/scratch (measured).
+// Sets NCT_AX to the step axis' crossing t and MORE to false when the ray leaves the grid.
+#define RT_DDA_ADVANCE(NCT_AX, MORE)                                                           \
+    do {                                                                                       \
+        const int ax_ = (nct0 < nct1) ? ((nct0 < nct2) ? 0 : 2) : ((nct1 < nct2) ? 1 : 2);    \
+        const bool a0_ = ax_ == 0, a1_ = ax_ == 1, a2_ = ax_ == 2;                             \
+        NCT_AX = a0_ ? nct0 : (a1_ ? nct1 : nct2);                                             \
+        const int rem_ = a0_ ? rem0 : (a1_ ? rem1 : rem2);                                     \
+        MORE = rem_ != 0;                                                                      \
+        if (MORE)                                                                              \
+        {                                                                                      \
+            rem0 -= int(a0_); rem1 -= int(a1_); rem2 -= int(a2_);                              \
+            nct0 = a0_ ? nct0 + dt0 : nct0;                                                    \
+            nct1 = a1_ ? nct1 + dt1 : nct1;                                                    \
+            nct2 = a2_ ? nct2 + dt2 : nct2;                                                    \
+            cell += a0_ ? cs0 : (a1_ ? cs1 : cs2);                                             \
+        }                                                                                      \
+    } while (0)
+
 // grid.cpp:159-281 Grid::Intersect (NEW_GRID_TRAVERSAL), axis arrays unrolled into scalars
 // so nothing is runtime-indexed (no scratch).  Counters are compiled in only for records.
-template <bool STATS, int TRI, bool PIPE>
+template <bool STATS, int TRI, int VAR>
 __device__ __forceinline__ bool grid_intersect(const KParams& P, const uint32_t *lds_occ,
                                                float ox, float oy, float oz,
                                                float dx, float dy, float dz,
@@ -153,85 +240,60 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, const uint32_t 
     setup(dx, gx, pos0, 0, 1, nct0, dt0, rem0, cs0);
     setup(dy, gy, pos1, 1, P.dxdz, nct1, dt1, rem1, cs1);
     setup(dz, gz, pos2, 2, P.dim[0], nct2, dt2, rem2, cs2);
-
     int cell = pos0 + pos2 * P.dim[0] + pos1 * P.dxdz;
     t = rtd::kFltMax;
+
+    if (VAR & kVarLookahead)
+    {
+        // Pipelined walk: the CSR offsets of the NEXT cell are loaded while the current cell
+        // is processed.  The current cell's step-axis crossing (nct_ax) is captured before the
+        // advance mutates the state, exactly as grid.cpp:236-260 uses it.
+        uint32_t kb = P.off[cell], ke = P.off[cell + 1];
+        for (uint32_t iter = 0; iter < P.max_steps; iter++)
+        {
+            if (STATS) { voxel = uint32_t(cell); steps++; }
+            float nct_cur;
+            bool more;
+            RT_DDA_ADVANCE(nct_cur, more);
+            uint32_t nkb = 0, nke = 0;
+            if (more)
+            {
+                nkb = P.off[cell];
+                nke = P.off[cell + 1];
+            }
+            if (kb < ke && test_cell<STATS, TRI, VAR>(P, ox, oy, oz, dx, dy, dz, kb, ke, nct_cur, t, u, v, tri, tests))
+                return true;
+            if (!more) break;
+            kb = nkb;
+            ke = nke;
+        }
+        return false;
+    }
+
     for (uint32_t iter = 0; iter < P.max_steps; iter++)
     {
-        const int ax = (nct0 < nct1) ? ((nct0 < nct2) ? 0 : 2) : ((nct1 < nct2) ? 1 : 2);
-        const float nct_ax = ax == 0 ? nct0 : (ax == 1 ? nct1 : nct2);
         if (STATS) { voxel = uint32_t(cell); steps++; }
-
-        const bool occupied = lds_occ ? ((lds_occ[uint32_t(cell) >> 5] >> (uint32_t(cell) & 31u)) & 1u) != 0u
-                                      : true;
+        const uint32_t ucell = uint32_t(cell);
+        const bool occupied = lds_occ ? ((lds_occ[ucell >> 5] >> (ucell & 31u)) & 1u) != 0u : true;
+        // Issue the CSR offset loads first; the step's ALU work below overlaps their latency.
+        uint32_t kb = 0, ke = 0;
         if (occupied)
         {
-            const uint32_t kb = P.off[cell], ke = P.off[cell + 1];
-            // Optionally software-pipelined over the cell's contiguous 48-B records (the loads
-            // of record k+1 in flight while record k is tested; costs registers/occupancy).
-            float4 n0, n1, n2;
-            if (PIPE && kb < ke)
-            {
-                n0 = P.refs[3 * kb + 0];
-                n1 = P.refs[3 * kb + 1];
-                n2 = P.refs[3 * kb + 2];
-            }
-            for (uint32_t k = kb; k < ke; k++)
-            {
-                float4 r0, r1, r2;
-                if (PIPE)
-                {
-                    r0 = n0; r1 = n1; r2 = n2;
-                    if (k + 1 < ke)
-                    {
-                        n0 = P.refs[3 * (k + 1) + 0];
-                        n1 = P.refs[3 * (k + 1) + 1];
-                        n2 = P.refs[3 * (k + 1) + 2];
-                    }
-                }
-                else
-                {
-                    r0 = P.refs[3 * k + 0];
-                    r1 = P.refs[3 * k + 1];
-                    r2 = P.refs[3 * k + 2];
-                }
-                const uint32_t id = __float_as_uint(r2.y);
-                float ct, cu, cv;
-                bool hit;
-                if (TRI == RT_TRI_BARYCENTRIC)
-                {
-                    const float4 fn = P.face_n[id];
-                    hit = rtd::ray_tri_bary_pred(ox, oy, oz, dx, dy, dz, r0.x, r0.y, r0.z, r0.w, r1.x,
-                                                 r1.y, r1.z, r1.w, r2.x, fn.x, fn.y, fn.z, ct, cu, cv);
-                }
-                else
-                    hit = rtd::ray_tri_mt_pred(ox, oy, oz, dx, dy, dz, r0.x, r0.y, r0.z, r0.w, r1.x,
-                                               r1.y, r1.z, r1.w, r2.x, ct, cu, cv);
-                if (STATS) tests++;
-                // grid.cpp:258-266: strict '<' over the ascending list keeps the first of ties
-                const bool take = hit & (ct < t) & (ct < nct_ax);
-                t = take ? ct : t;
-                u = take ? cu : u;
-                v = take ? cv : v;
-                tri = take ? id : tri;
-            }
-            if (t != rtd::kFltMax) return true;               // grid.cpp:270-271
+            kb = P.off[ucell];
+            ke = P.off[ucell + 1];
         }
-        // grid.cpp:274-277 as selects (exact: untouched axes keep their values)
-        const bool a0 = ax == 0, a1 = ax == 1, a2 = ax == 2;
-        const int rem = a0 ? rem0 : (a1 ? rem1 : rem2);
-        if (rem == 0) break;
-        rem0 -= int(a0); rem1 -= int(a1); rem2 -= int(a2);
-        nct0 = a0 ? nct0 + dt0 : nct0;
-        nct1 = a1 ? nct1 + dt1 : nct1;
-        nct2 = a2 ? nct2 + dt2 : nct2;
-        cell += a0 ? cs0 : (a1 ? cs1 : cs2);
+        float nct_ax;
+        bool more;
+        RT_DDA_ADVANCE(nct_ax, more);
+        if (kb < ke && test_cell<STATS, TRI, VAR>(P, ox, oy, oz, dx, dy, dz, kb, ke, nct_ax, t, u, v, tri, tests))
+            return true;
+        if (!more) break;
     }
     return false;
 }
 
 // renderer.cpp:126-160: one sample -> its colour contribution
-template <bool STATS, int TRI, bool PIPE>
+template <bool STATS, int TRI, int VAR>
 __device__ __forceinline__ void trace_sample(const KParams& P, const uint32_t *lds_occ, uint32_t px, uint32_t py,
                                              uint32_t s, float& cr, float& cg, float& cb,
                                              rt_sample_rec *rec)
@@ -241,7 +303,7 @@ __device__ __forceinline__ void trace_sample(const KParams& P, const uint32_t *l
     rtd::gen_dir(P.m, P.fov_xs, P.aspect, px, py, P.W, P.H, so.x, so.y, dx, dy, dz);
     float t = 0.0f, u = 0.0f, v = 0.0f;
     uint32_t tri = rtd::kNoTri, voxel = rtd::kNoTri, steps = 0, tests = 0;
-    const bool hit = grid_intersect<STATS, TRI, PIPE>(P, lds_occ, P.org[0], P.org[1], P.org[2], dx, dy, dz,
+    const bool hit = grid_intersect<STATS, TRI, VAR>(P, lds_occ, P.org[0], P.org[1], P.org[2], dx, dy, dz,
                                            t, u, v, tri, voxel, steps, tests);
     if (hit)
     {
@@ -318,7 +380,7 @@ __device__ __forceinline__ ItemCoord item_coord(const KParams& P, uint32_t item,
     return ic;
 }
 
-template <int TRI, bool PIPE>
+template <int TRI, int VAR>
 __device__ __forceinline__ void process_item(const KParams& P, const uint32_t *lds_occ, uint32_t item)
 {
     item = __builtin_amdgcn_readfirstlane(item);
@@ -327,7 +389,7 @@ __device__ __forceinline__ void process_item(const KParams& P, const uint32_t *l
     {
         const ItemCoord ic = item_coord(P, item, lane);
         if (ic.valid)
-            trace_sample<false, TRI, PIPE>(P, lds_occ, ic.x, ic.y, ic.s, cr, cg, cb, nullptr);
+            trace_sample<false, TRI, VAR>(P, lds_occ, ic.x, ic.y, ic.s, cr, cg, cb, nullptr);
     }
     const ItemCoord ic = item_coord(P, item, lane);
     const uint32_t base = lane & ~(P.spp - 1u);
@@ -349,10 +411,10 @@ __device__ __forceinline__ void process_item(const KParams& P, const uint32_t *l
 
 // RT_KERNEL_LANES: one lane per sample (spp = 2^spp_shift <= 64), one work item per wave,
 // no LDS.  Kept as the A/B baseline of the persistent kernel.
-template <int TRI, bool PIPE>
+template <int TRI, int VAR>
 __global__ void __launch_bounds__(kWG) k_render_lanes(KParams P)
 {
-    process_item<TRI, PIPE>(P, nullptr, blockIdx.x * (kWG / 64u) + (threadIdx.x >> 6));
+    process_item<TRI, VAR>(P, nullptr, blockIdx.x * (kWG / 64u) + (threadIdx.x >> 6));
 }
 
 // RT_KERNEL_PERSISTENT (spp a power of two <= 64): persistent 512-lane workgroups, 4 per CU.  The
@@ -362,7 +424,7 @@ __global__ void __launch_bounds__(kWG) k_render_lanes(KParams P)
 // neighbouring items cost alike, so the static interleave balances without atomics.
 constexpr uint32_t kPersistWG = 512;    // 8 waves; 4 workgroups (128 KiB of bitmaps) per CU
 
-template <int TRI, bool PIPE>
+template <int TRI, int VAR>
 __global__ void __launch_bounds__(kPersistWG, 8) k_render_persistent(KParams P, uint32_t n_items)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_occ[];
@@ -372,7 +434,7 @@ __global__ void __launch_bounds__(kPersistWG, 8) k_render_persistent(KParams P, 
     const uint32_t waves_per_wg = blockDim.x >> 6;
     const uint32_t nwaves = gridDim.x * waves_per_wg;
     for (uint32_t item = blockIdx.x * waves_per_wg + (threadIdx.x >> 6); item < n_items; item += nwaves)
-        process_item<TRI, PIPE>(P, lds_occ, item);
+        process_item<TRI, VAR>(P, lds_occ, item);
 }
 
 // RT_KERNEL_PIXEL_LOOP: one lane per pixel, samples looped in order (any spp)
@@ -390,7 +452,7 @@ __global__ void __launch_bounds__(kWG) k_render_pixel_loop(KParams P)
     for (uint32_t s = 0; s < P.spp; s++)
     {
         float cr, cg, cb;
-        trace_sample<false, TRI, false>(P, use_occ ? lds_occ : nullptr, x, y, s, cr, cg, cb, nullptr);
+        trace_sample<false, TRI, 0>(P, use_occ ? lds_occ : nullptr, x, y, s, cr, cg, cb, nullptr);
         sr += cr; sg += cg; sb += cb;
     }
     const float fs = float(P.spp);
@@ -407,9 +469,9 @@ __global__ void __launch_bounds__(kWG) k_trace_records(KParams P, uint32_t n)
     const uint32_t x = P.rec_x0 + pix % P.rec_w, y = P.rec_y0 + pix / P.rec_w;
     float cr, cg, cb;
     if (P.tri_test == RT_TRI_BARYCENTRIC)
-        trace_sample<true, RT_TRI_BARYCENTRIC, false>(P, nullptr, x, y, s, cr, cg, cb, &P.recs[i]);
+        trace_sample<true, RT_TRI_BARYCENTRIC, 0>(P, nullptr, x, y, s, cr, cg, cb, &P.recs[i]);
     else
-        trace_sample<true, RT_TRI_MOLLER_TRUMBORE, false>(P, nullptr, x, y, s, cr, cg, cb, &P.recs[i]);
+        trace_sample<true, RT_TRI_MOLLER_TRUMBORE, 0>(P, nullptr, x, y, s, cr, cg, cb, &P.recs[i]);
 }
 
 // K3: gathered shards [rank][local tile][256] -> frame
@@ -600,7 +662,8 @@ int validate_frame(const rt_frame *f)
     if (f->width == 0 || f->height == 0 || f->width > 65536 || f->height > 65536)
         return fail(RT_E_INVALID, "frame width/height must be in [1, 65536]");
     if (f->tri_test > RT_TRI_BARYCENTRIC) return fail(RT_E_INVALID, "unknown tri_test");
-    if ((f->kernel & 0xFFu) > RT_KERNEL_PERSISTENT || (f->kernel & ~(0xFFu | RT_KERNEL_FLAG_PREFETCH)))
+    if ((f->kernel & 0xFFu) > RT_KERNEL_PERSISTENT ||
+        (f->kernel & ~(0xFFu | RT_KERNEL_FLAG_PREFETCH | RT_KERNEL_FLAG_WAVE_GATE | RT_KERNEL_FLAG_LOOKAHEAD)))
         return fail(RT_E_INVALID, "unknown kernel");
     const uint32_t spp = std::max(1u, f->spp);
     if (spp > 4096) return fail(RT_E_INVALID, "spp must be <= 4096");
@@ -663,34 +726,43 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
     if (blocks > 0x3FFFFFFFull) return fail(RT_E_INVALID, "frame too large for one launch");
     RT_HIP(hipEventRecord(s->ev0, st));
     const uint32_t kind = f->kernel & 0xFFu;
-    const bool pipe = (f->kernel & RT_KERNEL_FLAG_PREFETCH) != 0;
+    // RT_KERNEL_AUTO = lanes + wave gate: fastest arm of tools/ab_kernels.py on MI355X
+    // (scenes 1/4/5/8, 1080p x 4spp).
+    const uint32_t fk = kind == RT_KERNEL_AUTO ? (RT_KERNEL_LANES | RT_KERNEL_FLAG_WAVE_GATE) : f->kernel;
+    const int var = ((fk & RT_KERNEL_FLAG_PREFETCH) ? kVarPrefetch : 0) |
+                    ((fk & RT_KERNEL_FLAG_WAVE_GATE) ? kVarWaveGate : 0) |
+                    ((fk & RT_KERNEL_FLAG_LOOKAHEAD) ? kVarLookahead : 0);
     const bool bary = P.tri_test == RT_TRI_BARYCENTRIC;
+    const dim3 wg(kWG);
     if (lanes && kind == RT_KERNEL_PERSISTENT && P.occ_words)
     {
         const uint32_t n_items = uint32_t(blocks * (kWG / 64u));
         const uint32_t per_wg = kPersistWG / 64u;
-        const uint32_t grid = std::max(1u, std::min(s->persist_wgs, (n_items + per_wg - 1) / per_wg));
+        const dim3 grid(std::max(1u, std::min(s->persist_wgs, (n_items + per_wg - 1) / per_wg)));
+        const dim3 pwg(kPersistWG);
         const size_t lds = P.occ_words * 4u;
-        if (bary)
-            hipLaunchKernelGGL((k_render_persistent<RT_TRI_BARYCENTRIC, false>), dim3(grid), dim3(kPersistWG), lds, st, P, n_items);
-        else if (pipe)
-            hipLaunchKernelGGL((k_render_persistent<RT_TRI_MOLLER_TRUMBORE, true>), dim3(grid), dim3(kPersistWG), lds, st, P, n_items);
-        else
-            hipLaunchKernelGGL((k_render_persistent<RT_TRI_MOLLER_TRUMBORE, false>), dim3(grid), dim3(kPersistWG), lds, st, P, n_items);
+        if (bary)           hipLaunchKernelGGL((k_render_persistent<RT_TRI_BARYCENTRIC, 0>), grid, pwg, lds, st, P, n_items);
+        else if (var == 1)  hipLaunchKernelGGL((k_render_persistent<RT_TRI_MOLLER_TRUMBORE, 1>), grid, pwg, lds, st, P, n_items);
+        else if (var == 2)  hipLaunchKernelGGL((k_render_persistent<RT_TRI_MOLLER_TRUMBORE, 2>), grid, pwg, lds, st, P, n_items);
+        else if (var == 3)  hipLaunchKernelGGL((k_render_persistent<RT_TRI_MOLLER_TRUMBORE, 3>), grid, pwg, lds, st, P, n_items);
+        else                hipLaunchKernelGGL((k_render_persistent<RT_TRI_MOLLER_TRUMBORE, 0>), grid, pwg, lds, st, P, n_items);
     }
     else if (lanes)
     {
-        if (bary)
-            hipLaunchKernelGGL((k_render_lanes<RT_TRI_BARYCENTRIC, false>), dim3(uint32_t(blocks)), dim3(kWG), 0, st, P);
-        else if (pipe)
-            hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, true>), dim3(uint32_t(blocks)), dim3(kWG), 0, st, P);
-        else
-            hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, false>), dim3(uint32_t(blocks)), dim3(kWG), 0, st, P);
+        const dim3 grid{uint32_t(blocks)};
+        if (bary)           hipLaunchKernelGGL((k_render_lanes<RT_TRI_BARYCENTRIC, 0>), grid, wg, 0, st, P);
+        else if (var == 1)  hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 1>), grid, wg, 0, st, P);
+        else if (var == 2)  hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 2>), grid, wg, 0, st, P);
+        else if (var == 3)  hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 3>), grid, wg, 0, st, P);
+        else if (var == 4)  hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 4>), grid, wg, 0, st, P);
+        else if (var == 6)  hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 6>), grid, wg, 0, st, P);
+        else if (var == 7)  hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 7>), grid, wg, 0, st, P);
+        else                hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 0>), grid, wg, 0, st, P);
     }
     else if (bary)
-        hipLaunchKernelGGL((k_render_pixel_loop<RT_TRI_BARYCENTRIC>), dim3(uint32_t(blocks)), dim3(kWG), 0, st, P);
+        hipLaunchKernelGGL((k_render_pixel_loop<RT_TRI_BARYCENTRIC>), dim3(uint32_t(blocks)), wg, 0, st, P);
     else
-        hipLaunchKernelGGL((k_render_pixel_loop<RT_TRI_MOLLER_TRUMBORE>), dim3(uint32_t(blocks)), dim3(kWG), 0, st, P);
+        hipLaunchKernelGGL((k_render_pixel_loop<RT_TRI_MOLLER_TRUMBORE>), dim3(uint32_t(blocks)), wg, 0, st, P);
     RT_HIP(hipGetLastError());
     RT_HIP(hipEventRecord(s->ev1, st));
     s->ev_recorded = true;

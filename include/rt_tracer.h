@@ -79,6 +79,8 @@ enum rt_kernel {
     RT_KERNEL_COMPACT = 3,     /* LANES + wavefront active-ray compaction (ballot/prefix refill) */
     RT_KERNEL_PERSISTENT = 4,  /* LANES in persistent workgroups with the LDS cell-occupancy bitmap */
     RT_KERNEL_FLAG_PREFETCH = 0x100,  /* OR-able: software-pipelined triangle record loads */
+    RT_KERNEL_FLAG_WAVE_GATE = 0x200, /* OR-able: skip a test's second half when no lane needs it */
+    RT_KERNEL_FLAG_LOOKAHEAD = 0x400, /* OR-able: load the next cell's CSR offsets one step ahead */
 };
 
 /* Per-frame parameters: what Renderer::RenderTile reads from the Scene and itself. */
