@@ -56,6 +56,8 @@ constexpr uint32_t kMaxOccWords = 8192;     // LDS occupancy bitmap: up to 262,1
 constexpr int kVarPrefetch = 1;             // RT_KERNEL_FLAG_PREFETCH
 constexpr int kVarWaveGate = 2;             // RT_KERNEL_FLAG_WAVE_GATE
 constexpr int kVarLookahead = 4;            // RT_KERNEL_FLAG_LOOKAHEAD
+constexpr int kVarDistSkip = 8;             // RT_KERNEL_FLAG_DIST_SKIP
+constexpr int kVarNestedStep = 16;          // RT_KERNEL_FLAG_NESTED_STEP (A/B arm)
 
 struct KParams
 {
@@ -64,6 +66,7 @@ struct KParams
     float fov_xs, aspect;
     float org[3];               // Transf4x4(Vec3f(0)) computed on the host (camera.h:39)
     uint32_t W, H, spp, spp_shift;
+    float inv_spp;              // 2^-spp_shift when spp is a power of two (x/spp == x*inv_spp), else 0
     const float2 *smp;          // [spp] sample offsets
     // grid (grid.h:28-39)
     float bmin[3], bmax[3];
@@ -73,6 +76,7 @@ struct KParams
     uint32_t max_steps;         // safety bound: no DDA walk is longer than dx+dy+dz
     uint32_t occ_words;         // 0 disables the LDS occupancy bitmap
     const uint32_t *off;
+    const uint32_t *cellw;      // packed cell ranges (start << 11 | count) or null
     const float4 *refs;
     const float4 *shade;
     const float4 *face_n;
@@ -98,6 +102,24 @@ __device__ __forceinline__ uint32_t compact_bits(uint32_t v)
     v = (v | (v >> 1)) & 0x33u;
     v = (v | (v >> 2)) & 0x0Fu;
     return v;
+}
+
+// CSR range of a cell: one u32 load of the packed (start << 11 | count) word when the scene
+// fits the packing (every scene of the reference does), else the two CSR offsets.
+__device__ __forceinline__ void cell_range(const KParams& P, uint32_t cell, uint32_t& kb, uint32_t& ke)
+{
+    if (P.cellw)
+    {
+        const uint32_t w = P.cellw[cell];
+        const uint32_t cnt = w & 2047u;
+        kb = cnt ? (w >> 11) : 0u;
+        ke = kb + cnt;
+    }
+    else
+    {
+        kb = P.off[cell];
+        ke = P.off[cell + 1];
+    }
 }
 
 // Tests a cell's list [kb, ke) in order (grid.cpp:243-267); true when it produced a hit.
@@ -167,7 +189,7 @@ __device__ __forceinline__ bool test_cell(const KParams& P, float ox, float oy, 
 // a capturing lambda: selecting between struct fields through `this`/references becomes a
 // pointer select, which defeats SROA and put the walk state in LDS/scratch (measured).
 // Sets NCT_AX to the step axis' crossing t and MORE to false when the ray leaves the grid.
-#define RT_DDA_ADVANCE(NCT_AX, MORE)                                                           \
+#define RT_DDA_ADVANCE_NESTED(NCT_AX, MORE)                                                           \
     do {                                                                                       \
         const int ax_ = (nct0 < nct1) ? ((nct0 < nct2) ? 0 : 2) : ((nct1 < nct2) ? 1 : 2);    \
         const bool a0_ = ax_ == 0, a1_ = ax_ == 1, a2_ = ax_ == 2;                             \
@@ -182,6 +204,27 @@ __device__ __forceinline__ bool test_cell(const KParams& P, float ox, float oy, 
             nct2 = a2_ ? nct2 + dt2 : nct2;                                                    \
             cell += a0_ ? cs0 : (a1_ ? cs1 : cs2);                                             \
         }                                                                                      \
+    } while (0)
+
+// Step axis of grid.cpp:236-239 restated: with m = min(nct), the nested strict '<' chain picks
+// the HIGHEST axis index among those equal to m (all 7 tie patterns checked), so
+// a2 = nct2 == m, a1 = !a2 && nct1 == m, else a0.  nct is never NaN (finite setup, FLT_MAX for
+// zero components).  The state updates run unconditionally -- when MORE is false the caller
+// breaks and the state is dead -- so the step has no divergent branch.
+#define RT_DDA_ADVANCE(NCT_AX, MORE)                                                           \
+    do {                                                                                       \
+        const float m_ = __builtin_fminf(__builtin_fminf(nct0, nct1), nct2);                   \
+        const bool a2_ = nct2 == m_;                                                           \
+        const bool a1_ = !a2_ && nct1 == m_;                                                   \
+        const bool a0_ = !a2_ && !a1_;                                                         \
+        NCT_AX = m_;                                                                           \
+        MORE = (a2_ ? rem2 : (a1_ ? rem1 : rem0)) != 0;                                        \
+        const float n_ = (a2_ ? nct2 : (a1_ ? nct1 : nct0)) + (a2_ ? dt2 : (a1_ ? dt1 : dt0));   \
+        nct0 = a0_ ? n_ : nct0;                                                                \
+        nct1 = a1_ ? n_ : nct1;                                                                \
+        nct2 = a2_ ? n_ : nct2;                                                                \
+        rem0 -= int(a0_); rem1 -= int(a1_); rem2 -= int(a2_);                                  \
+        cell += a2_ ? cs2 : (a1_ ? cs1 : cs0);                                                 \
     } while (0)
 
 // grid.cpp:159-281 Grid::Intersect (NEW_GRID_TRAVERSAL), axis arrays unrolled into scalars
@@ -248,7 +291,8 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, const uint32_t 
         // Pipelined walk: the CSR offsets of the NEXT cell are loaded while the current cell
         // is processed.  The current cell's step-axis crossing (nct_ax) is captured before the
         // advance mutates the state, exactly as grid.cpp:236-260 uses it.
-        uint32_t kb = P.off[cell], ke = P.off[cell + 1];
+        uint32_t kb, ke;
+        cell_range(P, uint32_t(cell), kb, ke);
         for (uint32_t iter = 0; iter < P.max_steps; iter++)
         {
             if (STATS) { voxel = uint32_t(cell); steps++; }
@@ -256,16 +300,41 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, const uint32_t 
             bool more;
             RT_DDA_ADVANCE(nct_cur, more);
             uint32_t nkb = 0, nke = 0;
-            if (more)
-            {
-                nkb = P.off[cell];
-                nke = P.off[cell + 1];
-            }
+            if (more) cell_range(P, uint32_t(cell), nkb, nke);
             if (kb < ke && test_cell<STATS, TRI, VAR>(P, ox, oy, oz, dx, dy, dz, kb, ke, nct_cur, t, u, v, tri, tests))
                 return true;
             if (!more) break;
             kb = nkb;
             ke = nke;
+        }
+        return false;
+    }
+
+    if (P.cellw && !lds_occ && (VAR & kVarDistSkip))
+    {
+        // Distance skipping: after an empty cell at L-inf distance d from geometry the next
+        // d-1 cells of the walk are provably empty, so they take the DDA step only.
+        int skip = 0;
+        for (uint32_t iter = 0; iter < P.max_steps; iter++)
+        {
+            if (STATS) { voxel = uint32_t(cell); steps++; }
+            uint32_t kb = 0, ke = 0;
+            if (skip == 0)
+            {
+                const uint32_t w = P.cellw[uint32_t(cell)];
+                const uint32_t cnt = w & 2047u;
+                kb = w >> 11;
+                ke = kb + cnt;
+                skip = cnt ? 0 : int(kb) - 1;
+            }
+            else
+                skip--;
+            float nct_ax;
+            bool more;
+            RT_DDA_ADVANCE(nct_ax, more);
+            if (kb < ke && test_cell<STATS, TRI, VAR>(P, ox, oy, oz, dx, dy, dz, kb, ke, nct_ax, t, u, v, tri, tests))
+                return true;
+            if (!more) break;
         }
         return false;
     }
@@ -277,14 +346,13 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, const uint32_t 
         const bool occupied = lds_occ ? ((lds_occ[ucell >> 5] >> (ucell & 31u)) & 1u) != 0u : true;
         // Issue the CSR offset loads first; the step's ALU work below overlaps their latency.
         uint32_t kb = 0, ke = 0;
-        if (occupied)
-        {
-            kb = P.off[ucell];
-            ke = P.off[ucell + 1];
-        }
+        if (occupied) cell_range(P, ucell, kb, ke);
         float nct_ax;
         bool more;
-        RT_DDA_ADVANCE(nct_ax, more);
+        if (VAR & kVarNestedStep)
+            RT_DDA_ADVANCE_NESTED(nct_ax, more);
+        else
+            RT_DDA_ADVANCE(nct_ax, more);
         if (kb < ke && test_cell<STATS, TRI, VAR>(P, ox, oy, oz, dx, dy, dz, kb, ke, nct_ax, t, u, v, tri, tests))
             return true;
         if (!more) break;
@@ -358,6 +426,12 @@ __device__ __forceinline__ void store_pixel(const KParams& P, const TileCoord& c
 // (a 2^k x 2^k pixel block x spp samples).  Traces the lane's sample, sums the pixel's
 // samples across its adjacent lanes in sample order (renderer.cpp:125-160, hazard H10) and
 // stores the packed pixel (renderer.cpp:162-171).
+// renderer.cpp:162 col / float(spp); exact as a multiply when spp is a power of two
+__device__ __forceinline__ float average(const KParams& P, float sum)
+{
+    return P.inv_spp != 0.0f ? sum * P.inv_spp : sum / float(P.spp);
+}
+
 struct ItemCoord { TileCoord c; uint32_t p, s, x, y; bool valid; };
 
 // Pixel/sample of this lane in work item `item` (wave-uniform).  Called before AND after the
@@ -402,9 +476,8 @@ __device__ __forceinline__ void process_item(const KParams& P, const uint32_t *l
     }
     if (ic.valid && ic.s == 0)
     {
-        const float fs = float(P.spp);
-        const uint32_t word = rtd::pack_bgra8(rtd::gamma_half(sr / fs), rtd::gamma_half(sg / fs),
-                                              rtd::gamma_half(sb / fs));
+        const uint32_t word = rtd::pack_bgra8(rtd::gamma_half(average(P, sr)), rtd::gamma_half(average(P, sg)),
+                                              rtd::gamma_half(average(P, sb)));
         store_pixel(P, ic.c, ic.p, ic.x, ic.y, word);
     }
 }
@@ -455,9 +528,8 @@ __global__ void __launch_bounds__(kWG) k_render_pixel_loop(KParams P)
         trace_sample<false, TRI, 0>(P, use_occ ? lds_occ : nullptr, x, y, s, cr, cg, cb, nullptr);
         sr += cr; sg += cg; sb += cb;
     }
-    const float fs = float(P.spp);
-    store_pixel(P, c, p, x, y, rtd::pack_bgra8(rtd::gamma_half(sr / fs), rtd::gamma_half(sg / fs),
-                                               rtd::gamma_half(sb / fs)));
+    store_pixel(P, c, p, x, y, rtd::pack_bgra8(rtd::gamma_half(average(P, sr)), rtd::gamma_half(average(P, sg)),
+                                               rtd::gamma_half(average(P, sb))));
 }
 
 // Debug records: one thread per sample of the rectangle, order (y, x, s)
@@ -468,10 +540,13 @@ __global__ void __launch_bounds__(kWG) k_trace_records(KParams P, uint32_t n)
     const uint32_t s = i % P.spp, pix = i / P.spp;
     const uint32_t x = P.rec_x0 + pix % P.rec_w, y = P.rec_y0 + pix / P.rec_w;
     float cr, cg, cb;
+    // Records walk the production traversal (wave gate + distance skipping) so the per-sample
+    // parity tests (hit, tri, voxel, steps, tests) cover exactly the code the frames use.
     if (P.tri_test == RT_TRI_BARYCENTRIC)
-        trace_sample<true, RT_TRI_BARYCENTRIC, 0>(P, nullptr, x, y, s, cr, cg, cb, &P.recs[i]);
+        trace_sample<true, RT_TRI_BARYCENTRIC, kVarDistSkip>(P, nullptr, x, y, s, cr, cg, cb, &P.recs[i]);
     else
-        trace_sample<true, RT_TRI_MOLLER_TRUMBORE, 0>(P, nullptr, x, y, s, cr, cg, cb, &P.recs[i]);
+        trace_sample<true, RT_TRI_MOLLER_TRUMBORE, kVarWaveGate | kVarDistSkip>(P, nullptr, x, y, s, cr, cg, cb,
+                                                                              &P.recs[i]);
 }
 
 // K3: gathered shards [rank][local tile][256] -> frame
@@ -600,7 +675,7 @@ struct rt_scene
     uint32_t dims[3] = { 0, 0, 0 };
     float bmin[3], bmax[3], cw = 0, icw = 0;
     uint32_t ncells = 0, nrefs = 0, ntris = 0, occ_words = 0;
-    uint32_t *d_off = nullptr, *d_occ = nullptr;
+    uint32_t *d_off = nullptr, *d_occ = nullptr, *d_cellw = nullptr;
     float4 *d_refs = nullptr, *d_shade = nullptr, *d_facen = nullptr;
     uint64_t device_bytes = 0;
     uint32_t persist_wgs = 1024;    // persistent grid: 4 x 512-lane workgroups per CU
@@ -663,7 +738,8 @@ int validate_frame(const rt_frame *f)
         return fail(RT_E_INVALID, "frame width/height must be in [1, 65536]");
     if (f->tri_test > RT_TRI_BARYCENTRIC) return fail(RT_E_INVALID, "unknown tri_test");
     if ((f->kernel & 0xFFu) > RT_KERNEL_PERSISTENT ||
-        (f->kernel & ~(0xFFu | RT_KERNEL_FLAG_PREFETCH | RT_KERNEL_FLAG_WAVE_GATE | RT_KERNEL_FLAG_LOOKAHEAD)))
+        (f->kernel & ~(0xFFu | RT_KERNEL_FLAG_PREFETCH | RT_KERNEL_FLAG_WAVE_GATE | RT_KERNEL_FLAG_LOOKAHEAD |
+                       RT_KERNEL_FLAG_CSR_OFFSETS | RT_KERNEL_FLAG_DIST_SKIP | RT_KERNEL_FLAG_NESTED_STEP)))
         return fail(RT_E_INVALID, "unknown kernel");
     const uint32_t spp = std::max(1u, f->spp);
     if (spp > 4096) return fail(RT_E_INVALID, "spp must be <= 4096");
@@ -689,6 +765,7 @@ void frame_params(const rt_scene *s, const rt_frame *f, KParams& P)
     P.H = f->height;
     P.spp = std::max(1u, f->spp);
     P.spp_shift = is_pow2(P.spp) ? log2u(P.spp) : 0;
+    P.inv_spp = is_pow2(P.spp) ? 1.0f / float(P.spp) : 0.0f;
     P.smp = s->d_smp;
     for (int a = 0; a < 3; a++)
     {
@@ -702,6 +779,7 @@ void frame_params(const rt_scene *s, const rt_frame *f, KParams& P)
     P.max_steps = s->dims[0] + s->dims[1] + s->dims[2] + 3;
     P.occ_words = s->occ_words <= kMaxOccWords ? s->occ_words : 0;
     P.off = s->d_off;
+    P.cellw = (f->kernel & RT_KERNEL_FLAG_CSR_OFFSETS) ? nullptr : s->d_cellw;
     P.refs = s->d_refs;
     P.shade = s->d_shade;
     P.face_n = s->d_facen;
@@ -726,12 +804,16 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
     if (blocks > 0x3FFFFFFFull) return fail(RT_E_INVALID, "frame too large for one launch");
     RT_HIP(hipEventRecord(s->ev0, st));
     const uint32_t kind = f->kernel & 0xFFu;
-    // RT_KERNEL_AUTO = lanes + wave gate: fastest arm of tools/ab_kernels.py on MI355X
-    // (scenes 1/4/5/8, 1080p x 4spp).
-    const uint32_t fk = kind == RT_KERNEL_AUTO ? (RT_KERNEL_LANES | RT_KERNEL_FLAG_WAVE_GATE) : f->kernel;
+    // RT_KERNEL_AUTO = lanes + wave gate + distance skip: fastest arm of tools/ab_kernels.py on
+    // MI355X (scenes 1/4/5/8, 1080p x 4spp).
+    const uint32_t fk = kind == RT_KERNEL_AUTO
+                            ? (f->kernel | RT_KERNEL_LANES | RT_KERNEL_FLAG_WAVE_GATE | RT_KERNEL_FLAG_DIST_SKIP)
+                            : f->kernel;
     const int var = ((fk & RT_KERNEL_FLAG_PREFETCH) ? kVarPrefetch : 0) |
                     ((fk & RT_KERNEL_FLAG_WAVE_GATE) ? kVarWaveGate : 0) |
-                    ((fk & RT_KERNEL_FLAG_LOOKAHEAD) ? kVarLookahead : 0);
+                    ((fk & RT_KERNEL_FLAG_LOOKAHEAD) ? kVarLookahead : 0) |
+                    ((fk & RT_KERNEL_FLAG_DIST_SKIP) ? kVarDistSkip : 0) |
+                    ((fk & RT_KERNEL_FLAG_NESTED_STEP) ? kVarNestedStep : 0);
     const bool bary = P.tri_test == RT_TRI_BARYCENTRIC;
     const dim3 wg(kWG);
     if (lanes && kind == RT_KERNEL_PERSISTENT && P.occ_words)
@@ -757,6 +839,9 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
         else if (var == 4)  hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 4>), grid, wg, 0, st, P);
         else if (var == 6)  hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 6>), grid, wg, 0, st, P);
         else if (var == 7)  hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 7>), grid, wg, 0, st, P);
+        else if (var == 8)  hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 8>), grid, wg, 0, st, P);
+        else if (var == 10) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 10>), grid, wg, 0, st, P);
+        else if (var == 18) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 18>), grid, wg, 0, st, P);
         else                hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 0>), grid, wg, 0, st, P);
     }
     else if (bary)
@@ -873,6 +958,47 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
         shade[3 * size_t(i) + 2] = make_float4(n2[2], 0.0f, 0.0f, 0.0f);
         facen[i] = make_float4(t.n[0], t.n[1], t.n[2], 0.0f);
     }
+    // Packed cell ranges: start < 2^21 and count < 2^11 for every cell -> one load per DDA step
+    std::vector<uint32_t> cellw;
+    bool packable = nr < (1u << 21);
+    for (uint32_t c = 0; c < nc && packable; c++) packable = g.cell_offsets[c + 1] - g.cell_offsets[c] < 2048u;
+    if (packable)
+    {
+        // Empty cells carry their Chebyshev (L-inf) distance to the nearest non-empty cell in
+        // the start field: a DDA step moves to a face neighbour, so the next dist-1 cells of
+        // any walk leaving this cell are empty and need no lookup.  BFS over 26-neighbours
+        // from all non-empty cells gives exactly the L-inf distance.
+        const uint32_t dxs = g.dims[0], dys = g.dims[1], dzs = g.dims[2];
+        std::vector<uint32_t> dist(nc, 0xFFFFFFFFu), frontier, next;
+        for (uint32_t c = 0; c < nc; c++)
+            if (g.cell_offsets[c + 1] != g.cell_offsets[c]) { dist[c] = 0; frontier.push_back(c); }
+        for (uint32_t d = 1; !frontier.empty(); d++)
+        {
+            next.clear();
+            for (uint32_t c : frontier)
+            {
+                const uint32_t x = c % dxs, z = (c / dxs) % dzs, y = c / (dxs * dzs);   // grid.h:41-42
+                for (int oy = -1; oy <= 1; oy++)
+                    for (int oz = -1; oz <= 1; oz++)
+                        for (int ox = -1; ox <= 1; ox++)
+                        {
+                            const int nx = int(x) + ox, ny = int(y) + oy, nz = int(z) + oz;
+                            if (nx < 0 || ny < 0 || nz < 0 || nx >= int(dxs) || ny >= int(dys) || nz >= int(dzs))
+                                continue;
+                            const uint32_t n = uint32_t(nx) + uint32_t(nz) * dxs + uint32_t(ny) * dxs * dzs;
+                            if (dist[n] == 0xFFFFFFFFu) { dist[n] = d; next.push_back(n); }
+                        }
+            }
+            frontier.swap(next);
+        }
+        cellw.resize(nc);
+        for (uint32_t c = 0; c < nc; c++)
+        {
+            const uint32_t cnt = g.cell_offsets[c + 1] - g.cell_offsets[c];
+            cellw[c] = cnt ? ((g.cell_offsets[c] << 11) | cnt)
+                           : (std::min<uint32_t>(dist[c] == 0xFFFFFFFFu ? 0x1FFFFFu : dist[c], 0x1FFFFFu) << 11);
+        }
+    }
     s->occ_words = (nc + 31) / 32;
     std::vector<uint32_t> occ(s->occ_words, 0);
     for (uint32_t c = 0; c < nc; c++)
@@ -888,8 +1014,13 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
     RT_HIP(hipMemcpy(s->d_shade, shade.data(), sizeof(float4) * shade.size(), hipMemcpyHostToDevice));
     RT_HIP(hipMemcpy(s->d_facen, facen.data(), sizeof(float4) * facen.size(), hipMemcpyHostToDevice));
     RT_HIP(hipMemcpy(s->d_occ, occ.data(), sizeof(uint32_t) * occ.size(), hipMemcpyHostToDevice));
+    if (packable)
+    {
+        RT_HIP(hipMalloc(&s->d_cellw, sizeof(uint32_t) * nc));
+        RT_HIP(hipMemcpy(s->d_cellw, cellw.data(), sizeof(uint32_t) * nc, hipMemcpyHostToDevice));
+    }
     s->device_bytes = sizeof(uint32_t) * (nc + 1) + sizeof(float4) * (refs.size() + shade.size() + facen.size()) +
-                      sizeof(uint32_t) * occ.size();
+                      sizeof(uint32_t) * (occ.size() + cellw.size());
     RT_HIP(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
     RT_HIP(hipEventCreate(&s->ev0));
     RT_HIP(hipEventCreate(&s->ev1));
@@ -909,6 +1040,7 @@ int rt_scene_destroy(rt_scene *s)
         (void)hipFree(s->d_shade);
         (void)hipFree(s->d_facen);
         (void)hipFree(s->d_occ);
+        (void)hipFree(s->d_cellw);
         (void)hipFree(s->d_smp);
         (void)hipFree(s->d_frame);
         if (s->h_smp_pinned) (void)hipHostFree(s->h_smp_pinned);

@@ -1,0 +1,52 @@
+"""Build-level guards for the HIP kernels (CPU-only; needs hipcc, which this image has).
+
+* Hazard H1/H2: the device IR must contain no FMA contraction (llvm.fmuladd,
+  `contract`) and no fast-math flags (afn/arcp/nnan/ninf/nsz/reassoc) -- the bit-exact
+  parity of every float on the path depends on it.
+* The traversal kernels must not spill or put walk state in LDS/scratch (a pointer-select
+  over struct fields once did exactly that and cost 14%).
+"""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+from conftest import PKG_DIR
+
+SRC = os.path.join(PKG_DIR, "csrc", "rt_tracer.hip")
+HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize",
+         "--cuda-device-only"]
+pytestmark = pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+
+
+def test_device_ir_has_no_contraction_or_fast_math(tmp_path):
+    ll = tmp_path / "rt.ll"
+    subprocess.run([HIPCC] + FLAGS + ["-emit-llvm", "-S", "-o", str(ll), SRC], check=True,
+                   capture_output=True)
+    ir = ll.read_text()
+    assert "fmuladd" not in ir
+    assert not re.search(r"\bllvm\.fma\.f32\b", ir)
+    for flag in (" contract ", " afn ", " arcp ", " nnan ", " ninf ", " nsz ", " reassoc ", " fast "):
+        assert flag not in ir, flag
+    assert "denormal-fp-math-f32" not in ir or '"denormal-fp-math-f32"="ieee' in ir
+
+
+def test_render_kernels_do_not_spill(tmp_path):
+    out = subprocess.run([HIPCC] + FLAGS + ["-c", "-o", str(tmp_path / "rt.o"), SRC,
+                          "-Rpass-analysis=kernel-resource-usage"], check=True, capture_output=True,
+                         text=True).stderr
+    names = re.findall(r"Function Name: (\S+)", out)
+    scratch = [int(x) for x in re.findall(r"ScratchSize \[bytes/lane\]: (\d+)", out)]
+    vgprs = [int(x) for x in re.findall(r"VGPRs: (\d+)", out)]
+    assert len(names) == len(scratch) == len(vgprs)
+    table = dict(zip(names, zip(scratch, vgprs)))
+    lanes = {n: v for n, v in table.items() if "k_render_lanes" in n}
+    assert lanes, table
+    for n, (sc, vg) in lanes.items():
+        assert sc == 0, f"{n} spills {sc} B/lane"
+    # the default kernel (lanes + wave gate, Moller-Trumbore) keeps 8 waves/SIMD
+    default = [v for n, v in lanes.items() if "ILi0ELi2E" in n]
+    assert default and default[0][1] <= 64, default
