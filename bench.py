@@ -84,12 +84,93 @@ def cpu_baseline(rtm_unused=None):
                       f"median of 3 after 1 warm-up; cpu: {model or platform.processor()}"}
 
 
+class GpuWorkload:
+    """The bench workload on this rank's GPU: one frame of every scene per step."""
+
+    def __init__(self, rtm, torch, world, rank, local, kernel):
+        self.rtm, self.torch, self.world, self.rank = rtm, torch, world, rank
+        self.scenes = []
+        for sid in SCENES:
+            hs = rtm.HostScene.load(sid)
+            gs = rtm.GpuScene(hs, local)
+            self.scenes.append((sid, hs, gs, gs.frame(W, H, SPP, kernel=kernel)))
+        self.stream = torch.cuda.current_stream()
+        n = W * H if world == 1 else rtm.shard_elems(W, H, world)
+        self.bufs = [torch.empty(n, dtype=torch.int32, device="cuda") for _ in SCENES]
+        self.frames = [torch.empty(W * H, dtype=torch.int32, device="cuda") for _ in SCENES]
+        self.events = {sid: [] for sid in SCENES}
+
+    def render(self, i, record):
+        sid, hs, gs, f = self.scenes[i]
+        if record:
+            a = self.torch.cuda.Event(enable_timing=True)
+            b = self.torch.cuda.Event(enable_timing=True)
+            a.record(self.stream)
+        if self.world == 1:
+            gs.render_frame_device(f, self.bufs[i].data_ptr(), self.stream.cuda_stream)
+        else:
+            gs.render_shard_device(f, self.rank, self.world, self.bufs[i].data_ptr(), self.stream.cuda_stream)
+        if record:
+            b.record(self.stream)
+            self.events[sid].append((a, b))
+
+    def unshard(self, i, gathered):
+        self.rtm.unshard_device(W, H, self.world, gathered.data_ptr(), self.frames[i].data_ptr(),
+                                self.stream.cuda_stream)
+
+    def sync(self):
+        self.torch.cuda.synchronize()
+
+    def kernel_ms(self):
+        return {sid: float(np.mean([a.elapsed_time(b) for a, b in ev])) for sid, ev in self.events.items()}
+
+    def close(self):
+        for sid, hs, gs, f in self.scenes:
+            gs.close()
+            hs.close()
+
+
+def run_steps(work, world, rank, steps, warmup, dist=None):
+    """W untimed warm-up steps, then K timed steps between barrier+sync on both sides; returns
+    the max-over-ranks wall time.  A step renders every scene (this rank's tiles when N > 1),
+    all-gathers the shards (RCCL over xGMI) and rank 0 un-permutes them into the frames."""
+    def step(record):
+        for i in range(len(SCENES)):
+            work.render(i, record)
+        if world > 1:
+            gathered = [work.rtm.all_gather_shards(work.bufs[i], world) for i in range(len(SCENES))]
+            if rank == 0:
+                for i in range(len(SCENES)):
+                    work.unshard(i, gathered[i])
+
+    for _ in range(warmup):
+        step(False)
+    work.sync()
+    if world > 1:
+        dist.barrier()
+    work.sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step(True)
+    work.sync()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        import torch
+        dev = work.bufs[0].device
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--kernel", type=int, default=0, help="rt_kernel: 0 auto, 1 lanes, 2 pixel loop, 3 compact")
+    ap.add_argument("--kernel", type=int, default=0, help="rt_kernel value (0 = AUTO; see include/rt_tracer.h)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -106,71 +187,15 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     rtm = load_package()
-    scenes = []
-    for sid in SCENES:
-        hs = rtm.HostScene.load(sid)
-        gs = rtm.GpuScene(hs, local)
-        scenes.append((sid, hs, gs, gs.frame(W, H, SPP, kernel=args.kernel)))
-
-    stream = torch.cuda.current_stream()
-    sp = stream.cuda_stream
-    if world == 1:
-        outs = [torch.empty(W * H, dtype=torch.int32, device="cuda") for _ in SCENES]
-    else:
-        e = rtm.shard_elems(W, H, world)
-        shards = [torch.empty(e, dtype=torch.int32, device="cuda") for _ in SCENES]
-        gathered = [torch.empty(world * e, dtype=torch.int32, device="cuda") for _ in SCENES]
-        outs = [torch.empty(W * H, dtype=torch.int32, device="cuda") for _ in SCENES]
-
-    ev = {sid: [] for sid in SCENES}
-
-    def step(record):
-        for i, (sid, hs, gs, f) in enumerate(scenes):
-            if record:
-                a = torch.cuda.Event(enable_timing=True)
-                b = torch.cuda.Event(enable_timing=True)
-                a.record(stream)
-            if world == 1:
-                gs.render_frame_device(f, outs[i].data_ptr(), sp)
-            else:
-                gs.render_shard_device(f, rank, world, shards[i].data_ptr(), sp)
-            if record:
-                b.record(stream)
-                ev[sid].append((a, b))
-        if world > 1:
-            works = [dist.all_gather_into_tensor(gathered[i], shards[i], async_op=True)
-                     for i in range(len(scenes))]
-            for w in works:
-                w.wait()
-            if rank == 0:
-                for i in range(len(scenes)):
-                    rtm.unshard_device(W, H, world, gathered[i].data_ptr(), outs[i].data_ptr(), sp)
-
-    for _ in range(args.warmup):
-        step(False)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(True)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
-    kernel_ms = {sid: float(np.mean([a.elapsed_time(b) for a, b in ev[sid]])) for sid in SCENES}
+    work = GpuWorkload(rtm, torch, world, rank, local, args.kernel)
+    elapsed = run_steps(work, world, rank, args.steps, args.warmup, dist if world > 1 else None)
+    kernel_ms = work.kernel_ms()
     samples_per_step = len(SCENES) * W * H * SPP          # all ranks together
     value = samples_per_step * args.steps / elapsed / 1e6
 
     if rank == 0:
         # algorithmic bytes per launch (this rank's launch covers 1/world of the frame)
-        ab = {sid: algorithmic_bytes(gs, f) for sid, hs, gs, f in scenes}
+        ab = {sid: algorithmic_bytes(gs, f) for sid, hs, gs, f in work.scenes}
         launch_bytes = {sid: ab[sid]["bytes_per_sample"] * W * H * SPP / world for sid in SCENES}
         achieved = sum(launch_bytes.values()) / (sum(kernel_ms.values()) / 1e3)
         traffic = None
@@ -216,9 +241,7 @@ def main():
             out["cpu_baseline"] = cpu_baseline()
         print(json.dumps(out), flush=True)
 
-    for sid, hs, gs, f in scenes:
-        gs.close()
-        hs.close()
+    work.close()
     if world > 1:
         dist.destroy_process_group()
 

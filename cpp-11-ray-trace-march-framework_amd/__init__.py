@@ -32,6 +32,7 @@ RT_KERNEL_FLAG_LOOKAHEAD = 0x400
 RT_KERNEL_FLAG_CSR_OFFSETS = 0x800
 RT_KERNEL_FLAG_DIST_SKIP = 0x1000
 RT_KERNEL_FLAG_NESTED_STEP = 0x2000
+RT_KERNEL_FLAG_PRE_GATE = 0x4000
 SHARD_TILE = 16
 
 # Symbols of include/rt_tracer.h and include/rt_host.h (checked by tests/test_abi.py)
@@ -349,7 +350,7 @@ def unshard_device(width, height, nranks, d_gathered, d_out, stream=0):
            "rt_unshard_device")
 
 
-PRIM_WIDTHS = {0: (18, 8), 1: (12, 4), 2: (23, 6), 3: (3, 4), 4: (11, 3), 5: (18, 8)}
+PRIM_WIDTHS = {0: (18, 8), 1: (12, 4), 2: (23, 6), 3: (3, 4), 4: (11, 3), 5: (18, 8), 6: (18, 8)}
 
 
 def debug_primitives(kind, records, device=0):

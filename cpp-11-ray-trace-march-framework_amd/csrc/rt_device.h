@@ -141,6 +141,44 @@ __device__ __forceinline__ bool ray_tri_mt_gated(float ox, float oy, float oz, f
     return ok1 & !(v < 0.0f || u + v > 1.0f) & (t >= 0.0f);
 }
 
+// ray_tri_mt_gated preceded by a division-free wave-uniform pre-gate.  With q = udot/det the
+// reference's u = RN(udot * RN(1/det)); a lane is PROVABLY rejected by triangle.h:77-87 when
+//   det fails the epsilon test, or
+//   sign(udot) != sign(det), |udot| >= 2^-100 and |det| <= 2^40: u is a nonzero negative
+//     (|u| >= 2^-100 * 2^-40 * (1 - 2^-24) >> 2^-149, so it cannot round to -0), or
+//   same signs and |udot| > RN(|det| * 1.000001f): q > 1.00000094, u >= q (1 - 2^-24)^2 > 1 + 2^-23.
+// If no active lane survives, the whole test (incl. the correctly rounded division) is skipped;
+// otherwise the lanes run ray_tri_mt_gated unchanged, so results are bit-identical.
+__device__ __forceinline__ bool ray_tri_mt_pregated(float ox, float oy, float oz, float dx, float dy, float dz,
+                                                    float v0x, float v0y, float v0z,
+                                                    float e1x, float e1y, float e1z,
+                                                    float e2x, float e2y, float e2z,
+                                                    float& t, float& u, float& v)
+{
+    const float px = dy * e2z - dz * e2y;
+    const float py = dz * e2x - dx * e2z;
+    const float pz = dx * e2y - dy * e2x;
+    const float det = e1x * px + e1y * py + e1z * pz;
+    const float tx = ox - v0x, ty = oy - v0y, tz = oz - v0z;
+    const float udot = tx * px + ty * py + tz * pz;
+    const bool det_ok = !(det > -0.00000001f && det < 0.00000001f);
+    const float ad = __builtin_fabsf(det), au = __builtin_fabsf(udot);
+    const bool opposite = (udot < 0.0f) != (det < 0.0f);
+    const bool surely_neg = opposite & (au >= 7.888609052210118e-31f) & (ad <= 1.099511627776e12f);
+    const bool surely_big = !opposite & (au > ad * 1.000001f);
+    if (!__any(det_ok & !surely_neg & !surely_big)) return false;
+    const float inv_det = 1.0f / det;
+    u = udot * inv_det;
+    const bool ok1 = det_ok & !(u < 0.0f || u > 1.0f);
+    if (!__any(ok1)) return false;
+    const float qx = ty * e1z - tz * e1y;
+    const float qy = tz * e1x - tx * e1z;
+    const float qz = tx * e1y - ty * e1x;
+    v = (dx * qx + dy * qy + dz * qz) * inv_det;
+    t = (e2x * qx + e2y * qy + e2z * qz) * inv_det;
+    return ok1 & !(v < 0.0f || u + v > 1.0f) & (t >= 0.0f);
+}
+
 // triangle.h:200-226 IntersectRayPlane + ComputeBarycentric (:133-156). Uses v0, the same
 // e1 (= v1 - v0) and e2 (= v2 - v0, the reference's e0) and the face normal.
 __device__ __forceinline__ bool ray_tri_bary(float ox, float oy, float oz, float dx, float dy, float dz,

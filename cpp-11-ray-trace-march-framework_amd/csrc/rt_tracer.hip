@@ -58,6 +58,7 @@ constexpr int kVarWaveGate = 2;             // RT_KERNEL_FLAG_WAVE_GATE
 constexpr int kVarLookahead = 4;            // RT_KERNEL_FLAG_LOOKAHEAD
 constexpr int kVarDistSkip = 8;             // RT_KERNEL_FLAG_DIST_SKIP
 constexpr int kVarNestedStep = 16;          // RT_KERNEL_FLAG_NESTED_STEP (A/B arm)
+constexpr int kVarPreGate = 32;             // RT_KERNEL_FLAG_PRE_GATE
 
 struct KParams
 {
@@ -581,6 +582,20 @@ __global__ void __launch_bounds__(kWG) k_primitives(int kind, const float *in, u
                                           e1x, e1y, e1z, e2x, e2y, e2z, a[15], a[16], a[17], bt, bu, bv);
         o[4] = __uint_as_float(hb); o[5] = bt; o[6] = bu; o[7] = bv;
     }
+    else if (kind == 6)   // pre-gated + gated variants (wave-uniform exits): hit flag + t,u,v on hits
+    {
+        const float *a = in + 18 * i;
+        float *o = out + 8 * i;
+        const float e1x = a[9] - a[6], e1y = a[10] - a[7], e1z = a[11] - a[8];
+        const float e2x = a[12] - a[6], e2y = a[13] - a[7], e2z = a[14] - a[8];
+        float t = 0, u = 0, v = 0, gt = 0, gu = 0, gv = 0;
+        const bool h = rtd::ray_tri_mt_pregated(a[0], a[1], a[2], a[3], a[4], a[5], a[6], a[7], a[8],
+                                                e1x, e1y, e1z, e2x, e2y, e2z, t, u, v);
+        const bool hg = rtd::ray_tri_mt_gated(a[0], a[1], a[2], a[3], a[4], a[5], a[6], a[7], a[8],
+                                              e1x, e1y, e1z, e2x, e2y, e2z, gt, gu, gv);
+        o[0] = __uint_as_float(h); o[1] = t; o[2] = u; o[3] = v;
+        o[4] = __uint_as_float(hg); o[5] = gt; o[6] = gu; o[7] = gv;
+    }
     else if (kind == 5)   // branch-free traversal variants: hit flag + t,u,v (hits only)
     {
         const float *a = in + 18 * i;
@@ -739,7 +754,8 @@ int validate_frame(const rt_frame *f)
     if (f->tri_test > RT_TRI_BARYCENTRIC) return fail(RT_E_INVALID, "unknown tri_test");
     if ((f->kernel & 0xFFu) > RT_KERNEL_PERSISTENT ||
         (f->kernel & ~(0xFFu | RT_KERNEL_FLAG_PREFETCH | RT_KERNEL_FLAG_WAVE_GATE | RT_KERNEL_FLAG_LOOKAHEAD |
-                       RT_KERNEL_FLAG_CSR_OFFSETS | RT_KERNEL_FLAG_DIST_SKIP | RT_KERNEL_FLAG_NESTED_STEP)))
+                       RT_KERNEL_FLAG_CSR_OFFSETS | RT_KERNEL_FLAG_DIST_SKIP | RT_KERNEL_FLAG_NESTED_STEP |
+                       RT_KERNEL_FLAG_PRE_GATE)))
         return fail(RT_E_INVALID, "unknown kernel");
     const uint32_t spp = std::max(1u, f->spp);
     if (spp > 4096) return fail(RT_E_INVALID, "spp must be <= 4096");
@@ -813,7 +829,8 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
                     ((fk & RT_KERNEL_FLAG_WAVE_GATE) ? kVarWaveGate : 0) |
                     ((fk & RT_KERNEL_FLAG_LOOKAHEAD) ? kVarLookahead : 0) |
                     ((fk & RT_KERNEL_FLAG_DIST_SKIP) ? kVarDistSkip : 0) |
-                    ((fk & RT_KERNEL_FLAG_NESTED_STEP) ? kVarNestedStep : 0);
+                    ((fk & RT_KERNEL_FLAG_NESTED_STEP) ? kVarNestedStep : 0) |
+                    ((fk & RT_KERNEL_FLAG_PRE_GATE) ? kVarPreGate : 0);
     const bool bary = P.tri_test == RT_TRI_BARYCENTRIC;
     const dim3 wg(kWG);
     if (lanes && kind == RT_KERNEL_PERSISTENT && P.occ_words)
@@ -842,6 +859,8 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
         else if (var == 8)  hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 8>), grid, wg, 0, st, P);
         else if (var == 10) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 10>), grid, wg, 0, st, P);
         else if (var == 18) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 18>), grid, wg, 0, st, P);
+        else if (var == 40) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 40>), grid, wg, 0, st, P);
+        else if (var == 42) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 42>), grid, wg, 0, st, P);
         else                hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 0>), grid, wg, 0, st, P);
     }
     else if (bary)
@@ -1219,8 +1238,8 @@ int rt_trace_samples(rt_scene *s, const rt_frame *f, uint32_t x0, uint32_t y0, u
 
 int rt_debug_primitives(int kind, const float *in, uint32_t n, float *out, int device)
 {
-    static const uint32_t in_w[6] = { 18, 12, 23, 3, 11, 18 }, out_w[6] = { 8, 4, 6, 4, 3, 8 };
-    if (kind < 0 || kind > 5 || !in || !out) return fail(RT_E_INVALID, "bad arguments");
+    static const uint32_t in_w[7] = { 18, 12, 23, 3, 11, 18, 18 }, out_w[7] = { 8, 4, 6, 4, 3, 8, 8 };
+    if (kind < 0 || kind > 6 || !in || !out) return fail(RT_E_INVALID, "bad arguments");
     if (n == 0) return RT_OK;
     RT_HIP(hipSetDevice(device));
     std::vector<float> host_in(in, in + size_t(in_w[kind]) * n);

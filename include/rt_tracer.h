@@ -87,6 +87,8 @@ enum rt_kernel {
                                            proves empty (needs the packed words) */
     RT_KERNEL_FLAG_NESTED_STEP = 0x2000, /* OR-able: the step axis via grid.cpp's nested compares
                                             (A/B arm of the min3 form) */
+    RT_KERNEL_FLAG_PRE_GATE = 0x4000,   /* OR-able: division-free wave-uniform pre-reject before
+                                            the ray/triangle test's 1/det */
 };
 
 /* Per-frame parameters: what Renderer::RenderTile reads from the Scene and itself. */
@@ -162,7 +164,8 @@ int  rt_trace_samples(rt_scene *scene, const rt_frame *frame, uint32_t x0, uint3
 /* Device evaluation of the primitives for known-answer tests (input layouts as the
  * tests/golden/kat_*.f32 records):  0 ray/tri (18 in, 8 out), 1 ray/aabb (12 in, 4 out),
  * 2 generate ray (23 in, 6 out), 3 gamma+pack (3 in, 4 out), 4 shade (11 in, 3 out),
- * 5 the branch-free ray/tri forms the traversal uses (18 in, 8 out; t,u,v valid on hits). */
+ * 5 the branch-free ray/tri forms the traversal uses (18 in, 8 out; t,u,v valid on hits),
+ * 6 the wave-gated forms: pre-gated MT, gated MT (18 in, 8 out; t,u,v valid on hits). */
 int  rt_debug_primitives(int kind, const float *in, uint32_t n, float *out, int device);
 
 /* Hammersley table the library uses when rt_frame.sample_offsets is NULL. */

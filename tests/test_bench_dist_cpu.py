@@ -1,0 +1,74 @@
+"""bench.py's multi-rank step (render shard -> all-gather -> rank-0 un-permute -> timing with
+barrier + max over ranks) driven under gloo on CPU, world_size 2.  The GPU render is replaced
+by the oracle rendering this rank's tiles; everything else is bench.run_steps itself."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import Oracle, load_package
+
+W, H, SPP = 64, 48, 4
+
+
+class CpuWorkload:
+    def __init__(self, rtm, world, rank, scenes):
+        self.rtm, self.world, self.rank = rtm, world, rank
+        orc = Oracle()
+        self.full = [orc.render(sid, W, H, SPP, nthreads=1)[0] for sid in scenes]
+        n = rtm.shard_elems(W, H, world)
+        self.bufs = [torch.zeros(n, dtype=torch.int32) for _ in scenes]
+        self.frames = [None for _ in scenes]
+        self.renders = 0
+
+    def render(self, i, record):
+        shard = self.rtm.shard_from_frame(self.full[i], self.rank, self.world)
+        self.bufs[i].copy_(torch.from_numpy(shard.view(np.int32)))
+        self.renders += 1
+
+    def unshard(self, i, gathered):
+        self.frames[i] = self.rtm.frame_from_shards(gathered.numpy().view(np.uint32), W, H, self.world)
+
+    def sync(self):
+        pass
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import bench
+        bench.W, bench.H, bench.SPP = W, H, SPP
+        rtm = load_package()
+        work = CpuWorkload(rtm, world, rank, bench.SCENES)
+        elapsed = bench.run_steps(work, world, rank, steps=3, warmup=1, dist=dist)
+        if rank == 0:
+            same = all(np.array_equal(work.frames[i], work.full[i]) for i in range(len(bench.SCENES)))
+            q.put(("ok", same, elapsed, work.renders))
+        dist.barrier()
+    except Exception as e:  # pragma: no cover
+        q.put(("err", repr(e), 0, 0))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_run_steps_two_ranks_gloo():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    status, same, elapsed, renders = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+    assert status == "ok", same
+    assert same
+    assert elapsed > 0
+    assert renders == (3 + 1) * 2        # (steps + warmup) x scenes

@@ -57,6 +57,17 @@ def test_device_kat_branch_free_ray_tri():
         np.testing.assert_array_equal(bits(got[m][:, cols]), bits(exp[m][:, cols]))
 
 
+def test_device_kat_wave_gated_ray_tri():
+    """Pre-gated and gated Moller-Trumbore (wave-uniform exits): hit flags equal the reference's,
+    t,u,v bit-identical on hits -- evaluated 64 records per wave, so the exits really fire."""
+    rin, exp = load_kat("ray_tri")
+    got = rtm.debug_primitives(6, rin)
+    m = bits(exp[:, 0]) == 1
+    for h in (0, 4):
+        np.testing.assert_array_equal(bits(got[:, h]), bits(exp[:, 0]))
+        np.testing.assert_array_equal(bits(got[m][:, h + 1:h + 4]), bits(exp[m][:, 1:4]))
+
+
 def test_device_kat_ray_aabb():
     rin, exp = load_kat("ray_aabb")
     np.testing.assert_array_equal(bits(rtm.debug_primitives(1, rin)), bits(exp))
