@@ -40,7 +40,8 @@ TRACER_SYMBOLS = [
     "rt_get_device_count", "rt_scene_create", "rt_scene_destroy", "rt_scene_device_bytes",
     "rt_render_tiles", "rt_render_frame_device", "rt_shard_elems", "rt_render_shard_device",
     "rt_unshard_device", "rt_last_kernel_ms", "rt_trace_samples", "rt_debug_primitives",
-    "rt_sample_table", "rt_last_error", "rt_abi_version",
+    "rt_sample_table", "rt_last_error", "rt_abi_version", "rt_grid_build", "rt_grid_free",
+    "rt_scene_create_from_mesh",
 ]
 HOST_SYMBOLS = [
     "rth_scene_load", "rth_scene_from_mesh", "rth_scene_free", "rth_scene_desc",
@@ -131,6 +132,10 @@ def tracer_lib():
         L.rt_sample_table.argtypes = [c_u32, vp]
         L.rt_last_error.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
         L.rt_get_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
+        L.rt_grid_build.argtypes = [vp, c_u32, vp, c_u32, c_u32, ctypes.c_int, ctypes.POINTER(GridDesc),
+                                    ctypes.POINTER(c_f32)]
+        L.rt_grid_free.argtypes = [ctypes.POINTER(GridDesc)]
+        L.rt_scene_create_from_mesh.argtypes = [vp, c_u32, vp, c_u32, c_u32, ctypes.c_int, ctypes.POINTER(vp)]
         _tracer = L
     return _tracer
 
@@ -243,6 +248,13 @@ class HostScene:
                 "cell_wdh": np.float32(g.cell_wdh), "inv_cell_wdh": np.float32(g.inv_cell_wdh)}
         return meta, offs, tris
 
+    def mesh(self):
+        """(vertices float32 [nv, 6], triangles uint32 [nt, 6]) -- copies of Mesh (mesh.h:12-27)."""
+        d = self.desc()
+        v = np.ctypeslib.as_array(ctypes.cast(d.vertices, ctypes.POINTER(c_f32)), shape=(d.num_vertices, 6))
+        t = np.ctypeslib.as_array(ctypes.cast(d.triangles, ctypes.POINTER(c_u32)), shape=(d.num_triangles, 6))
+        return v.copy(), t.copy()
+
     def close(self):
         if self._h:
             host_lib().rth_scene_free(self._h)
@@ -256,15 +268,43 @@ class HostScene:
 
 
 # ------------------------------------------------------------------ GPU scene
-class GpuScene:
-    """Device copy of a scene (rt_scene_create) plus the rendering entry points."""
+def gpu_grid_build(vertices, triangles, grid_res=64, device=0):
+    """Grid::Grid on the GPU (rt_grid_build) -> (meta, offsets u32[C+1], tris u32[R], device_ms)."""
+    v = np.ascontiguousarray(vertices, np.float32)
+    t = np.ascontiguousarray(triangles).view(np.uint32)
+    L, g, ms = tracer_lib(), GridDesc(), c_f32()
+    _check(L.rt_grid_build(_ptr(v), v.shape[0], _ptr(t), t.shape[0], grid_res, device, ctypes.byref(g),
+                           ctypes.byref(ms)), L, "rt_grid_build")
+    try:
+        nc = g.dims[0] * g.dims[1] * g.dims[2]
+        offs = np.ctypeslib.as_array(g.cell_offsets, shape=(nc + 1,)).copy()
+        tris = np.ctypeslib.as_array(g.cell_tris, shape=(int(offs[-1]),)).copy() if offs[-1] else \
+            np.zeros(0, np.uint32)
+        meta = {"dims": list(g.dims), "aabb_min": np.array(g.aabb_min, np.float32),
+                "aabb_max": np.array(g.aabb_max, np.float32),
+                "cell_wdh": np.float32(g.cell_wdh), "inv_cell_wdh": np.float32(g.inv_cell_wdh)}
+    finally:
+        L.rt_grid_free(ctypes.byref(g))
+    return meta, offs, tris, ms.value
 
-    def __init__(self, host_scene, device=0):
+
+class GpuScene:
+    """Device copy of a scene (rt_scene_create) plus the rendering entry points.
+
+    gpu_grid=True rebuilds the grid from the host scene's mesh on the GPU
+    (rt_scene_create_from_mesh) instead of uploading the host-built CSR."""
+
+    def __init__(self, host_scene, device=0, gpu_grid=False, grid_res=64):
         self.host = host_scene
         L = tracer_lib()
         h = ctypes.c_void_p()
-        d = host_scene.desc()
-        _check(L.rt_scene_create(ctypes.byref(d), device, ctypes.byref(h)), L, "rt_scene_create")
+        if gpu_grid:
+            v, t = host_scene.mesh()
+            _check(L.rt_scene_create_from_mesh(_ptr(v), v.shape[0], _ptr(t), t.shape[0], grid_res, device,
+                                               ctypes.byref(h)), L, "rt_scene_create_from_mesh")
+        else:
+            d = host_scene.desc()
+            _check(L.rt_scene_create(ctypes.byref(d), device, ctypes.byref(h)), L, "rt_scene_create")
         self._h = h
         self.device = device
 

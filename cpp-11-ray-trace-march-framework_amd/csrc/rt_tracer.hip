@@ -31,6 +31,7 @@
 
 #include "../../include/rt_tracer.h"
 #include "rt_device.h"
+#include "rt_internal.h"
 
 namespace {
 
@@ -875,6 +876,22 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
 
 } // namespace
 
+int rt_internal_fail(int code, const std::string& msg) { return fail(code, msg); }
+
+int rt_internal_use_device(int device, int *num_cus)
+{
+    int ndev = 0;
+    RT_HIP(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return fail(RT_E_NODEVICE, "device index out of range / no GPU");
+    hipDeviceProp_t prop;
+    RT_HIP(hipGetDeviceProperties(&prop, device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(RT_E_NODEVICE, std::string("librt_tracer is built for gfx950, device is ") + prop.gcnArchName);
+    RT_HIP(hipSetDevice(device));
+    if (num_cus) *num_cus = prop.multiProcessorCount;
+    return RT_OK;
+}
+
 extern "C" {
 
 int rt_abi_version(void) { return RT_ABI_VERSION; }
@@ -928,18 +945,12 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
         if (t.v0 >= d->num_vertices || t.v1 >= d->num_vertices || t.v2 >= d->num_vertices)
             return fail(RT_E_INVALID, "triangle vertex index out of range");
     }
-    int ndev = 0;
-    RT_HIP(hipGetDeviceCount(&ndev));
-    if (device < 0 || device >= ndev) return fail(RT_E_NODEVICE, "device index out of range / no GPU");
-    hipDeviceProp_t prop;
-    RT_HIP(hipGetDeviceProperties(&prop, device));
-    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
-        return fail(RT_E_NODEVICE, std::string("librt_tracer is built for gfx950, device is ") + prop.gcnArchName);
-    RT_HIP(hipSetDevice(device));
+    int ncus = 0;
+    if (int rc = rt_internal_use_device(device, &ncus)) return rc;
 
     std::unique_ptr<rt_scene> s(new rt_scene());
     s->device = device;
-    s->persist_wgs = 4u * uint32_t(std::max(1, prop.multiProcessorCount));
+    s->persist_wgs = 4u * uint32_t(std::max(1, ncus));
     for (int a = 0; a < 3; a++)
     {
         s->dims[a] = g.dims[a];

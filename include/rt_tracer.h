@@ -129,6 +129,21 @@ int  rt_scene_destroy(rt_scene *scene);
 /* device bytes held by the scene (all arrays) */
 int  rt_scene_device_bytes(const rt_scene *scene, uint64_t *bytes);
 
+/* ---- grid build on the GPU (Grid::Grid, grid.cpp:12-154; grid.h:15) ----------------------
+ * Voxelizes the mesh into the reference's uniform grid on `device`: the same AABB, cell size
+ * and dims (grid.cpp:18-41), the same exact double tri/box test per candidate cell
+ * (aabb.h:15-32), every cell's list in ascending triangle order (grid.cpp:119-122).  `out`
+ * receives host arrays (cell_offsets, cell_tris) owned by the caller until rt_grid_free.
+ * device_ms (optional): device time of the build kernels (HIP events). */
+int  rt_grid_build(const rt_vertex *vertices, uint32_t num_vertices, const rt_triangle *triangles,
+                   uint32_t num_triangles, uint32_t grid_res, int device, rt_grid_desc *out,
+                   float *device_ms);
+int  rt_grid_free(rt_grid_desc *grid);
+/* Scene::Scene's mesh + Grid(mesh, grid_res) in one call: rt_grid_build + rt_scene_create. */
+int  rt_scene_create_from_mesh(const rt_vertex *vertices, uint32_t num_vertices,
+                               const rt_triangle *triangles, uint32_t num_triangles,
+                               uint32_t grid_res, int device, rt_scene **out);
+
 /* ---- rendering --------------------------------------------------------------------- */
 /* Renders every listed tile in ONE batched launch (over the tiles' bounding box), copies
  * back and scatters into the caller's host buffers: tile_bufs[i][(x-x0) + (y-y0)*(x1-x0)]
