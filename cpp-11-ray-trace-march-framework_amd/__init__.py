@@ -33,6 +33,9 @@ RT_KERNEL_FLAG_CSR_OFFSETS = 0x800
 RT_KERNEL_FLAG_DIST_SKIP = 0x1000
 RT_KERNEL_FLAG_NESTED_STEP = 0x2000
 RT_KERNEL_FLAG_PRE_GATE = 0x4000
+RT_ISECT_GRID = 0
+RT_ISECT_BRUTE_FORCE = 1
+RT_ISECT_RAY_MARCH = 2
 SHARD_TILE = 16
 
 # Symbols of include/rt_tracer.h and include/rt_host.h (checked by tests/test_abi.py)
@@ -46,7 +49,8 @@ TRACER_SYMBOLS = [
 HOST_SYMBOLS = [
     "rth_scene_load", "rth_scene_from_mesh", "rth_scene_free", "rth_scene_desc",
     "rth_scene_camera", "rth_scene_stats_get", "rth_framebuffer_create", "rth_framebuffer_free",
-    "rth_framebuffer_set_sample_count", "rth_framebuffer_set_options", "rth_framebuffer_resize",
+    "rth_framebuffer_set_sample_count", "rth_framebuffer_set_options", "rth_framebuffer_set_intersector",
+    "rth_framebuffer_resize",
     "rth_framebuffer_start_rendering", "rth_framebuffer_read", "rth_framebuffer_save_bmp",
     "rth_last_error",
 ]
@@ -83,7 +87,7 @@ class SceneDesc(ctypes.Structure):
 class Frame(ctypes.Structure):
     _fields_ = [("cam", c_f32 * 16), ("fov", c_f32), ("width", c_u32), ("height", c_u32),
                 ("spp", c_u32), ("sample_offsets", ctypes.POINTER(c_f32)),
-                ("tri_test", c_u32), ("kernel", c_u32)]
+                ("tri_test", c_u32), ("kernel", c_u32), ("intersector", c_u32)]
 
 
 class Tile(ctypes.Structure):
@@ -159,6 +163,7 @@ def host_lib():
         L.rth_framebuffer_free.restype = None
         L.rth_framebuffer_set_sample_count.argtypes = [vp, c_u32]
         L.rth_framebuffer_set_options.argtypes = [vp, c_u32, c_u32]
+        L.rth_framebuffer_set_intersector.argtypes = [vp, c_u32]
         L.rth_framebuffer_resize.argtypes = [vp, c_u32, c_u32, ctypes.POINTER(ctypes.c_double)]
         L.rth_framebuffer_start_rendering.argtypes = [vp, ctypes.POINTER(ctypes.c_double)]
         L.rth_framebuffer_read.argtypes = [vp, vp]
@@ -309,12 +314,12 @@ class GpuScene:
         self.device = device
 
     def frame(self, width, height, spp, tri_test=RT_TRI_MOLLER_TRUMBORE, kernel=RT_KERNEL_AUTO,
-              sample_offsets=None):
+              sample_offsets=None, intersector=RT_ISECT_GRID):
         f = Frame()
         for i in range(16):
             f.cam[i] = float(self.host.cam[i])
         f.fov, f.width, f.height, f.spp = self.host.fov, width, height, spp
-        f.tri_test, f.kernel = tri_test, kernel
+        f.tri_test, f.kernel, f.intersector = tri_test, kernel, intersector
         if sample_offsets is not None:
             so = np.ascontiguousarray(sample_offsets, np.float32).reshape(-1)
             f._keep = so
@@ -390,7 +395,7 @@ def unshard_device(width, height, nranks, d_gathered, d_out, stream=0):
            "rt_unshard_device")
 
 
-PRIM_WIDTHS = {0: (18, 8), 1: (12, 4), 2: (23, 6), 3: (3, 4), 4: (11, 3), 5: (18, 8), 6: (18, 8)}
+PRIM_WIDTHS = {0: (18, 8), 1: (12, 4), 2: (23, 6), 3: (3, 4), 4: (11, 3), 5: (18, 8), 6: (18, 8), 7: (12, 1)}
 
 
 def debug_primitives(kind, records, device=0):
@@ -426,6 +431,10 @@ class Renderer:
     def set_options(self, tri_test=RT_TRI_MOLLER_TRUMBORE, kernel=RT_KERNEL_AUTO):
         L = host_lib()
         _check(L.rth_framebuffer_set_options(self._h, tri_test, kernel), L, "rth_framebuffer_set_options")
+
+    def set_intersector(self, intersector=RT_ISECT_GRID):
+        L = host_lib()
+        _check(L.rth_framebuffer_set_intersector(self._h, intersector), L, "rth_framebuffer_set_intersector")
 
     def resize(self, width, height):
         s = ctypes.c_double()

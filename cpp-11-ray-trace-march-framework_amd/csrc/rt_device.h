@@ -231,6 +231,57 @@ __device__ __forceinline__ bool ray_tri_bary_pred(float ox, float oy, float oz, 
     return plane_ok & (u >= 0.0f) & (v >= 0.0f) & (u + v < 1.0f);
 }
 
+// triangle.h:163-172 LineSegMinDistSq(a, b, p); ab = b - a and len_sq = Dot(ab, ab) come
+// precomputed (same single IEEE operations), Clamp is lin_alg.h:205-212 (NaN passes through).
+__device__ __forceinline__ float seg_dist_sq(float ax, float ay, float az, float abx, float aby, float abz,
+                                             float len_sq, float px, float py, float pz)
+{
+    float t = dot3(px - ax, py - ay, pz - az, abx, aby, abz) / len_sq;
+    t = t < 0.0f ? 0.0f : (t > 1.0f ? 1.0f : t);
+    const float qx = ax + t * abx, qy = ay + t * aby, qz = az + t * abz;
+    const float dx = px - qx, dy = py - qy, dz = pz - qz;
+    return dot3(dx, dy, dz, dx, dy, dz);
+}
+
+// Per-triangle record of the distance kernels (6 float4, built by rt_scene_create):
+//   {v0.xyz, v1.x} {v1.yz, v2.xy} {v2.z, e0.xyz} {e1.xyz, e12.x} {e12.yz, dot00, dot01}
+//   {dot11, inv_denom, len12, 0}
+// with e0 = v2 - v0, e1 = v1 - v0, e12 = v2 - v1 and the position-independent terms of
+// ComputeBarycentric (triangle.h:140-150): dot00 = Dot(e0,e0), dot01 = Dot(e0,e1),
+// dot11 = Dot(e1,e1), inv_denom = 1 / (dot00*dot11 - dot01*dot01); len12 = Dot(e12,e12).
+// LineSegMinDistSq(v0,v1) / (v0,v2) reuse e1 / e0 and dot11 / dot00: the same operations.
+//
+// triangle.h:174-198 DistancePointTri(pos, v0, v1, v2)
+__device__ __forceinline__ float dist_point_tri(float px, float py, float pz, const float4& r0, const float4& r1,
+                                                const float4& r2, const float4& r3, const float4& r4,
+                                                const float4& r5)
+{
+    const float v0x = r0.x, v0y = r0.y, v0z = r0.z, v1x = r0.w, v1y = r1.x, v1z = r1.y;
+    const float v2x = r1.z, v2y = r1.w, v2z = r2.x;
+    // ComputeBarycentric (triangle.h:133-156) with e2 = pos - v0
+    const float wx = px - v0x, wy = py - v0y, wz = pz - v0z;
+    const float dot02 = dot3(r2.y, r2.z, r2.w, wx, wy, wz);
+    const float dot12 = dot3(r3.x, r3.y, r3.z, wx, wy, wz);
+    const float dot00 = r4.z, dot01 = r4.w, dot11 = r5.x, inv_denom = r5.y;
+    const float u = (dot00 * dot12 - dot01 * dot02) * inv_denom;
+    const float v = (dot11 * dot02 - dot01 * dot12) * inv_denom;
+    if ((u >= 0.0f) && (v >= 0.0f) && (u + v < 1.0f))
+    {
+        // BarycentricInterpolate (triangle.h:158-161): v1*u + v2*v + v0*(1 - u - v)
+        const float w = 1.0f - u - v;
+        const float qx = v1x * u + v2x * v + v0x * w;
+        const float qy = v1y * u + v2y * v + v0y * w;
+        const float qz = v1z * u + v2z * v + v0z * w;
+        const float dx = px - qx, dy = py - qy, dz = pz - qz;
+        return __builtin_sqrtf(dot3(dx, dy, dz, dx, dy, dz));   // Distance, lin_alg.h:149-150
+    }
+    const float l01 = seg_dist_sq(v0x, v0y, v0z, r3.x, r3.y, r3.z, dot11, px, py, pz);
+    const float l02 = seg_dist_sq(v0x, v0y, v0z, r2.y, r2.z, r2.w, dot00, px, py, pz);
+    const float l12 = seg_dist_sq(v1x, v1y, v1z, r3.w, r4.x, r4.y, r5.z, px, py, pz);
+    const float inner = (l12 < l02) ? l12 : l02;                // std::min(l02, l12)
+    return __builtin_sqrtf((inner < l01) ? inner : l01);         // std::min(l01, inner)
+}
+
 // aabb.h:9-13
 __device__ __forceinline__ bool point_in_aabb(float px, float py, float pz, const float* mn, const float* mx)
 {

@@ -60,6 +60,9 @@ constexpr int kVarLookahead = 4;            // RT_KERNEL_FLAG_LOOKAHEAD
 constexpr int kVarDistSkip = 8;             // RT_KERNEL_FLAG_DIST_SKIP
 constexpr int kVarNestedStep = 16;          // RT_KERNEL_FLAG_NESTED_STEP (A/B arm)
 constexpr int kVarPreGate = 32;             // RT_KERNEL_FLAG_PRE_GATE
+constexpr int kVarBrute = 64;               // RT_ISECT_BRUTE_FORCE (renderer.cpp:157-197)
+constexpr int kVarMarch = 128;              // RT_ISECT_RAY_MARCH (renderer.cpp:24-41, 138-155)
+constexpr uint32_t kMarchSteps = 128;       // renderer.cpp:26
 
 struct KParams
 {
@@ -83,7 +86,11 @@ struct KParams
     const float4 *shade;
     const float4 *face_n;
     const uint32_t *occ;
+    const float4 *tri_mt;       // per triangle {v0, e1, e2} in triangle order (brute force)
+    const float4 *tri_dist;     // per triangle distance record (rtd::dist_point_tri)
+    uint32_t ntris;
     uint32_t tri_test;
+    uint32_t isect;             // enum rt_intersector
     // work decomposition
     uint32_t rx0, ry0, rw, rh;  // region of the frame rendered by this launch
     uint32_t tiles_x;           // 16x16 tiles across the region
@@ -362,6 +369,62 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, const uint32_t 
     return false;
 }
 
+// Renderer::IntersectBruteForce (renderer.cpp:157-197): every triangle in index order, the
+// closest accepted hit wins, ties keep the lower index (strict '<', :187).  All lanes of a wave
+// walk the same triangle sequence, so the records arrive through wave-uniform (scalar) loads
+// and the wave-gated test skips a triangle's second half when no lane can still hit it.
+template <bool STATS>
+__device__ __forceinline__ bool brute_intersect(const KParams& P, float ox, float oy, float oz, float dx, float dy,
+                                                float dz, float& t, float& u, float& v, uint32_t& tri,
+                                                uint32_t& tests)
+{
+    t = rtd::kFltMax;
+    for (uint32_t i = 0; i < P.ntris; i++)
+    {
+        const float4 a = P.tri_mt[3 * i + 0], b = P.tri_mt[3 * i + 1], c = P.tri_mt[3 * i + 2];
+        float ct = 0.0f, cu = 0.0f, cv = 0.0f;
+        const bool h = rtd::ray_tri_mt_gated(ox, oy, oz, dx, dy, dz, a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x,
+                                             ct, cu, cv);
+        if (h && ct < t)
+        {
+            t = ct;
+            u = cu;
+            v = cv;
+            tri = i;
+        }
+    }
+    if (STATS) tests = P.ntris;
+    return t != rtd::kFltMax;
+}
+
+// Renderer::RayMarch (renderer.cpp:24-41) over Renderer::DistanceBruteForce (:138-155):
+// sphere tracing from the camera, at most 128 steps, hit when a step's distance < 0.001.
+template <bool STATS>
+__device__ __forceinline__ bool ray_march(const KParams& P, float ox, float oy, float oz, float dx, float dy,
+                                          float dz, float& t, uint32_t& steps, uint32_t& tests)
+{
+    t = 0.0f;
+    for (uint32_t s = 0; s < kMarchSteps; s++)
+    {
+        const float px = ox + t * dx, py = oy + t * dy, pz = oz + t * dz;
+        float dist = rtd::kFltMax;
+        for (uint32_t i = 0; i < P.ntris; i++)
+        {
+            const float4 *r = P.tri_dist + 6 * size_t(i);
+            const float d = rtd::dist_point_tri(px, py, pz, r[0], r[1], r[2], r[3], r[4], r[5]);
+            dist = (d < dist) ? d : dist;                            // std::min(dist, d)
+        }
+        t += dist;
+        if (STATS)
+        {
+            steps = s + 1;
+            tests += P.ntris;
+        }
+        if (dist < 0.001f) return true;
+    }
+    return false;
+}
+
 // renderer.cpp:126-160: one sample -> its colour contribution
 template <bool STATS, int TRI, int VAR>
 __device__ __forceinline__ void trace_sample(const KParams& P, const uint32_t *lds_occ, uint32_t px, uint32_t py,
@@ -373,9 +436,22 @@ __device__ __forceinline__ void trace_sample(const KParams& P, const uint32_t *l
     rtd::gen_dir(P.m, P.fov_xs, P.aspect, px, py, P.W, P.H, so.x, so.y, dx, dy, dz);
     float t = 0.0f, u = 0.0f, v = 0.0f;
     uint32_t tri = rtd::kNoTri, voxel = rtd::kNoTri, steps = 0, tests = 0;
-    const bool hit = grid_intersect<STATS, TRI, VAR>(P, lds_occ, P.org[0], P.org[1], P.org[2], dx, dy, dz,
-                                           t, u, v, tri, voxel, steps, tests);
-    if (hit)
+    bool hit;
+    if constexpr ((VAR & kVarMarch) != 0)
+        hit = ray_march<STATS>(P, P.org[0], P.org[1], P.org[2], dx, dy, dz, t, steps, tests);
+    else if constexpr ((VAR & kVarBrute) != 0)
+        hit = brute_intersect<STATS>(P, P.org[0], P.org[1], P.org[2], dx, dy, dz, t, u, v, tri, tests);
+    else
+        hit = grid_intersect<STATS, TRI, VAR>(P, lds_occ, P.org[0], P.org[1], P.org[2], dx, dy, dz, t, u, v, tri,
+                                              voxel, steps, tests);
+    if constexpr ((VAR & kVarMarch) != 0)
+    {
+        // The reference's RayMarch leaves u, v, tri_idx unset (renderer.cpp:103), so the
+        // march is shaded by depth: the reference's own alternative at renderer.cpp:118.
+        if (hit) cr = cg = cb = t / 3.0f;
+        else cr = cg = cb = float(py) / float(P.H);
+    }
+    else if (hit)
     {
         const float4 a = P.shade[3 * tri + 0], b = P.shade[3 * tri + 1], c = P.shade[3 * tri + 2];
         rtd::shade_hit(u, v, a, b, c, cr, cg, cb);
@@ -513,7 +589,7 @@ __global__ void __launch_bounds__(kPersistWG, 8) k_render_persistent(KParams P, 
 }
 
 // RT_KERNEL_PIXEL_LOOP: one lane per pixel, samples looped in order (any spp)
-template <int TRI>
+template <int TRI, int VAR>
 __global__ void __launch_bounds__(kWG) k_render_pixel_loop(KParams P)
 {
     const uint32_t *lds_occ = nullptr;
@@ -527,7 +603,7 @@ __global__ void __launch_bounds__(kWG) k_render_pixel_loop(KParams P)
     for (uint32_t s = 0; s < P.spp; s++)
     {
         float cr, cg, cb;
-        trace_sample<false, TRI, 0>(P, use_occ ? lds_occ : nullptr, x, y, s, cr, cg, cb, nullptr);
+        trace_sample<false, TRI, VAR>(P, use_occ ? lds_occ : nullptr, x, y, s, cr, cg, cb, nullptr);
         sr += cr; sg += cg; sb += cb;
     }
     store_pixel(P, c, p, x, y, rtd::pack_bgra8(rtd::gamma_half(average(P, sr)), rtd::gamma_half(average(P, sg)),
@@ -544,7 +620,11 @@ __global__ void __launch_bounds__(kWG) k_trace_records(KParams P, uint32_t n)
     float cr, cg, cb;
     // Records walk the production traversal (wave gate + distance skipping) so the per-sample
     // parity tests (hit, tri, voxel, steps, tests) cover exactly the code the frames use.
-    if (P.tri_test == RT_TRI_BARYCENTRIC)
+    if (P.isect == RT_ISECT_RAY_MARCH)
+        trace_sample<true, RT_TRI_MOLLER_TRUMBORE, kVarMarch>(P, nullptr, x, y, s, cr, cg, cb, &P.recs[i]);
+    else if (P.isect == RT_ISECT_BRUTE_FORCE)
+        trace_sample<true, RT_TRI_MOLLER_TRUMBORE, kVarBrute>(P, nullptr, x, y, s, cr, cg, cb, &P.recs[i]);
+    else if (P.tri_test == RT_TRI_BARYCENTRIC)
         trace_sample<true, RT_TRI_BARYCENTRIC, kVarDistSkip>(P, nullptr, x, y, s, cr, cg, cb, &P.recs[i]);
     else
         trace_sample<true, RT_TRI_MOLLER_TRUMBORE, kVarWaveGate | kVarDistSkip>(P, nullptr, x, y, s, cr, cg, cb,
@@ -610,6 +690,11 @@ __global__ void __launch_bounds__(kWG) k_primitives(int kind, const float *in, u
                                                e1x, e1y, e1z, e2x, e2y, e2z, a[15], a[16], a[17], bt, bu, bv);
         o[0] = __uint_as_float(h); o[1] = t; o[2] = u; o[3] = v;
         o[4] = __uint_as_float(hb); o[5] = bt; o[6] = bu; o[7] = bv;
+    }
+    else if (kind == 7)   // DistancePointTri over the scene's distance record
+    {
+        const float4 *a = reinterpret_cast<const float4 *>(in + 28 * size_t(i));
+        out[i] = rtd::dist_point_tri(a[0].x, a[0].y, a[0].z, a[1], a[2], a[3], a[4], a[5], a[6]);
     }
     else if (kind == 1)
     {
@@ -682,6 +767,33 @@ uint32_t log2u(uint32_t x)
     return r;
 }
 
+// Dot (lin_alg.h:138-144), accumulating from T() = 0
+float dot_ref(const float *a, const float *b)
+{
+    float r = 0.0f;
+    r += a[0] * b[0];
+    r += a[1] * b[1];
+    r += a[2] * b[2];
+    return r;
+}
+
+// Distance record of one triangle (layout: rtd::dist_point_tri); the position-independent
+// terms of ComputeBarycentric / LineSegMinDistSq (triangle.h:140-150, 166-167)
+void dist_record(const float *p0, const float *p1, const float *p2, float4 *r)
+{
+    const float e0[3] = { p2[0] - p0[0], p2[1] - p0[1], p2[2] - p0[2] };
+    const float e1[3] = { p1[0] - p0[0], p1[1] - p0[1], p1[2] - p0[2] };
+    const float e12[3] = { p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2] };
+    const float d00 = dot_ref(e0, e0), d01 = dot_ref(e0, e1), d11 = dot_ref(e1, e1);
+    const float inv_denom = 1 / (d00 * d11 - d01 * d01);
+    r[0] = make_float4(p0[0], p0[1], p0[2], p1[0]);
+    r[1] = make_float4(p1[1], p1[2], p2[0], p2[1]);
+    r[2] = make_float4(p2[2], e0[0], e0[1], e0[2]);
+    r[3] = make_float4(e1[0], e1[1], e1[2], e12[0]);
+    r[4] = make_float4(e12[1], e12[2], d00, d01);
+    r[5] = make_float4(d11, inv_denom, dot_ref(e12, e12), 0.0f);
+}
+
 } // namespace
 
 struct rt_scene
@@ -693,6 +805,7 @@ struct rt_scene
     uint32_t ncells = 0, nrefs = 0, ntris = 0, occ_words = 0;
     uint32_t *d_off = nullptr, *d_occ = nullptr, *d_cellw = nullptr;
     float4 *d_refs = nullptr, *d_shade = nullptr, *d_facen = nullptr;
+    float4 *d_trimt = nullptr, *d_tridist = nullptr;
     uint64_t device_bytes = 0;
     uint32_t persist_wgs = 1024;    // persistent grid: 4 x 512-lane workgroups per CU
     // sample table cache
@@ -753,6 +866,9 @@ int validate_frame(const rt_frame *f)
     if (f->width == 0 || f->height == 0 || f->width > 65536 || f->height > 65536)
         return fail(RT_E_INVALID, "frame width/height must be in [1, 65536]");
     if (f->tri_test > RT_TRI_BARYCENTRIC) return fail(RT_E_INVALID, "unknown tri_test");
+    if (f->intersector > RT_ISECT_RAY_MARCH) return fail(RT_E_INVALID, "unknown intersector");
+    if (f->intersector == RT_ISECT_BRUTE_FORCE && f->tri_test != RT_TRI_MOLLER_TRUMBORE)
+        return fail(RT_E_INVALID, "IntersectBruteForce uses IntersectRayTri only (renderer.cpp:176)");
     if ((f->kernel & 0xFFu) > RT_KERNEL_PERSISTENT ||
         (f->kernel & ~(0xFFu | RT_KERNEL_FLAG_PREFETCH | RT_KERNEL_FLAG_WAVE_GATE | RT_KERNEL_FLAG_LOOKAHEAD |
                        RT_KERNEL_FLAG_CSR_OFFSETS | RT_KERNEL_FLAG_DIST_SKIP | RT_KERNEL_FLAG_NESTED_STEP |
@@ -801,7 +917,11 @@ void frame_params(const rt_scene *s, const rt_frame *f, KParams& P)
     P.shade = s->d_shade;
     P.face_n = s->d_facen;
     P.occ = s->d_occ;
+    P.tri_mt = s->d_trimt;
+    P.tri_dist = s->d_tridist;
+    P.ntris = s->ntris;
     P.tri_test = f->tri_test;
+    P.isect = f->intersector;
 }
 
 bool use_lanes(const rt_frame *f, uint32_t spp)
@@ -834,7 +954,7 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
                     ((fk & RT_KERNEL_FLAG_PRE_GATE) ? kVarPreGate : 0);
     const bool bary = P.tri_test == RT_TRI_BARYCENTRIC;
     const dim3 wg(kWG);
-    if (lanes && kind == RT_KERNEL_PERSISTENT && P.occ_words)
+    if (lanes && kind == RT_KERNEL_PERSISTENT && P.occ_words && P.isect == RT_ISECT_GRID)
     {
         const uint32_t n_items = uint32_t(blocks * (kWG / 64u));
         const uint32_t per_wg = kPersistWG / 64u;
@@ -846,6 +966,14 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
         else if (var == 2)  hipLaunchKernelGGL((k_render_persistent<RT_TRI_MOLLER_TRUMBORE, 2>), grid, pwg, lds, st, P, n_items);
         else if (var == 3)  hipLaunchKernelGGL((k_render_persistent<RT_TRI_MOLLER_TRUMBORE, 3>), grid, pwg, lds, st, P, n_items);
         else                hipLaunchKernelGGL((k_render_persistent<RT_TRI_MOLLER_TRUMBORE, 0>), grid, pwg, lds, st, P, n_items);
+    }
+    else if (lanes && P.isect != RT_ISECT_GRID)
+    {
+        const dim3 grid{uint32_t(blocks)};
+        if (P.isect == RT_ISECT_RAY_MARCH)
+            hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, kVarMarch>), grid, wg, 0, st, P);
+        else
+            hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, kVarBrute>), grid, wg, 0, st, P);
     }
     else if (lanes)
     {
@@ -864,10 +992,14 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
         else if (var == 42) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 42>), grid, wg, 0, st, P);
         else                hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 0>), grid, wg, 0, st, P);
     }
+    else if (P.isect == RT_ISECT_RAY_MARCH)
+        hipLaunchKernelGGL((k_render_pixel_loop<RT_TRI_MOLLER_TRUMBORE, kVarMarch>), dim3(uint32_t(blocks)), wg, 0, st, P);
+    else if (P.isect == RT_ISECT_BRUTE_FORCE)
+        hipLaunchKernelGGL((k_render_pixel_loop<RT_TRI_MOLLER_TRUMBORE, kVarBrute>), dim3(uint32_t(blocks)), wg, 0, st, P);
     else if (bary)
-        hipLaunchKernelGGL((k_render_pixel_loop<RT_TRI_BARYCENTRIC>), dim3(uint32_t(blocks)), wg, 0, st, P);
+        hipLaunchKernelGGL((k_render_pixel_loop<RT_TRI_BARYCENTRIC, 0>), dim3(uint32_t(blocks)), wg, 0, st, P);
     else
-        hipLaunchKernelGGL((k_render_pixel_loop<RT_TRI_MOLLER_TRUMBORE>), dim3(uint32_t(blocks)), wg, 0, st, P);
+        hipLaunchKernelGGL((k_render_pixel_loop<RT_TRI_MOLLER_TRUMBORE, 0>), dim3(uint32_t(blocks)), wg, 0, st, P);
     RT_HIP(hipGetLastError());
     RT_HIP(hipEventRecord(s->ev1, st));
     s->ev_recorded = true;
@@ -979,9 +1111,20 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
         refs[3 * size_t(k) + 2] = make_float4(e2[2], idf, 0.0f, 0.0f);
     }
     std::vector<float4> shade(size_t(d->num_triangles) * 3), facen(d->num_triangles);
+    std::vector<float4> trimt(size_t(d->num_triangles) * 3), tridist(size_t(d->num_triangles) * 6);
     for (uint32_t i = 0; i < d->num_triangles; i++)
     {
         const rt_triangle& t = d->triangles[i];
+        const float *p0 = d->vertices[t.v0].p, *p1 = d->vertices[t.v1].p, *p2 = d->vertices[t.v2].p;
+        {
+            // brute force: {v0, e1 = v1 - v0, e2 = v2 - v0} (triangle.h:41-42) in triangle order
+            const float e1[3] = { p1[0] - p0[0], p1[1] - p0[1], p1[2] - p0[2] };
+            const float e2[3] = { p2[0] - p0[0], p2[1] - p0[1], p2[2] - p0[2] };
+            trimt[3 * size_t(i) + 0] = make_float4(p0[0], p0[1], p0[2], e1[0]);
+            trimt[3 * size_t(i) + 1] = make_float4(e1[1], e1[2], e2[0], e2[1]);
+            trimt[3 * size_t(i) + 2] = make_float4(e2[2], 0.0f, 0.0f, 0.0f);
+            dist_record(p0, p1, p2, &tridist[6 * size_t(i)]);
+        }
         const float *n0 = d->vertices[t.v0].n, *n1 = d->vertices[t.v1].n, *n2 = d->vertices[t.v2].n;
         shade[3 * size_t(i) + 0] = make_float4(n0[0], n0[1], n0[2], n1[0]);
         shade[3 * size_t(i) + 1] = make_float4(n1[1], n1[2], n2[0], n2[1]);
@@ -1044,12 +1187,17 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
     RT_HIP(hipMemcpy(s->d_shade, shade.data(), sizeof(float4) * shade.size(), hipMemcpyHostToDevice));
     RT_HIP(hipMemcpy(s->d_facen, facen.data(), sizeof(float4) * facen.size(), hipMemcpyHostToDevice));
     RT_HIP(hipMemcpy(s->d_occ, occ.data(), sizeof(uint32_t) * occ.size(), hipMemcpyHostToDevice));
+    RT_HIP(hipMalloc(&s->d_trimt, sizeof(float4) * trimt.size()));
+    RT_HIP(hipMalloc(&s->d_tridist, sizeof(float4) * tridist.size()));
+    RT_HIP(hipMemcpy(s->d_trimt, trimt.data(), sizeof(float4) * trimt.size(), hipMemcpyHostToDevice));
+    RT_HIP(hipMemcpy(s->d_tridist, tridist.data(), sizeof(float4) * tridist.size(), hipMemcpyHostToDevice));
     if (packable)
     {
         RT_HIP(hipMalloc(&s->d_cellw, sizeof(uint32_t) * nc));
         RT_HIP(hipMemcpy(s->d_cellw, cellw.data(), sizeof(uint32_t) * nc, hipMemcpyHostToDevice));
     }
-    s->device_bytes = sizeof(uint32_t) * (nc + 1) + sizeof(float4) * (refs.size() + shade.size() + facen.size()) +
+    s->device_bytes = sizeof(uint32_t) * (nc + 1) +
+                      sizeof(float4) * (refs.size() + shade.size() + facen.size() + trimt.size() + tridist.size()) +
                       sizeof(uint32_t) * (occ.size() + cellw.size());
     RT_HIP(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
     RT_HIP(hipEventCreate(&s->ev0));
@@ -1071,6 +1219,8 @@ int rt_scene_destroy(rt_scene *s)
         (void)hipFree(s->d_facen);
         (void)hipFree(s->d_occ);
         (void)hipFree(s->d_cellw);
+        (void)hipFree(s->d_trimt);
+        (void)hipFree(s->d_tridist);
         (void)hipFree(s->d_smp);
         (void)hipFree(s->d_frame);
         if (s->h_smp_pinned) (void)hipHostFree(s->h_smp_pinned);
@@ -1249,11 +1399,25 @@ int rt_trace_samples(rt_scene *s, const rt_frame *f, uint32_t x0, uint32_t y0, u
 
 int rt_debug_primitives(int kind, const float *in, uint32_t n, float *out, int device)
 {
-    static const uint32_t in_w[7] = { 18, 12, 23, 3, 11, 18, 18 }, out_w[7] = { 8, 4, 6, 4, 3, 8, 8 };
-    if (kind < 0 || kind > 6 || !in || !out) return fail(RT_E_INVALID, "bad arguments");
+    // kind 7 (DistancePointTri) reaches the device as pos + pad + the 24-float scene record
+    static const uint32_t in_w[8] = { 18, 12, 23, 3, 11, 18, 18, 28 }, out_w[8] = { 8, 4, 6, 4, 3, 8, 8, 1 };
+    if (kind < 0 || kind > 7 || !in || !out) return fail(RT_E_INVALID, "bad arguments");
     if (n == 0) return RT_OK;
     RT_HIP(hipSetDevice(device));
-    std::vector<float> host_in(in, in + size_t(in_w[kind]) * n);
+    std::vector<float> host_in;
+    if (kind == 7)
+    {
+        host_in.resize(size_t(28) * n);
+        for (uint32_t i = 0; i < n; i++)
+        {
+            const float *a = in + 12 * size_t(i);
+            float *o = &host_in[28 * size_t(i)];
+            o[0] = a[0]; o[1] = a[1]; o[2] = a[2]; o[3] = 0.0f;
+            dist_record(a + 3, a + 6, a + 9, reinterpret_cast<float4 *>(o + 4));
+        }
+    }
+    else
+        host_in.assign(in, in + size_t(in_w[kind]) * n);
     if (kind == 2)   // camera.h:41-42 fov_xs is a host-side constant (double ::tan, hazard H5)
         for (uint32_t i = 0; i < n; i++)
         {

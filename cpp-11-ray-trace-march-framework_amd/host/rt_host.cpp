@@ -422,6 +422,7 @@ public:
 
     void SetSampleCount(uint32_t cnt) { m_spp = std::max(1u, cnt); }   // renderer.cpp:56-60
     void SetOptions(uint32_t tri_test, uint32_t kernel) { m_tri_test = tri_test; m_kernel = kernel; }
+    void SetIntersector(uint32_t isect) { m_isect = isect; }             // renderer.cpp:103-105
     int LastStatus() const { return m_status; }
     const std::string& LastError() const { return m_err; }
 
@@ -450,6 +451,7 @@ protected:
                 f.spp = m_spp;
                 f.tri_test = m_tri_test;
                 f.kernel = m_kernel;
+                f.intersector = m_isect;
                 const rt_tile whole = { 0, 0, m_width, m_height };
                 uint32_t* dst = m_staging.data();
                 m_status = rt_render_tiles(m_gpu, &f, &whole, 1, &dst);
@@ -475,7 +477,7 @@ private:
     rt_scene* m_gpu;
     const rth_scene* m_host;
     uint32_t m_spp = 16;                                        // renderer.h:34
-    uint32_t m_tri_test = RT_TRI_MOLLER_TRUMBORE, m_kernel = RT_KERNEL_AUTO;
+    uint32_t m_tri_test = RT_TRI_MOLLER_TRUMBORE, m_kernel = RT_KERNEL_AUTO, m_isect = RT_ISECT_GRID;
     std::mutex m_frame_mtx;
     bool m_frame_ready = false;
     std::vector<uint32_t> m_staging;
@@ -602,6 +604,14 @@ int rth_framebuffer_set_options(rth_framebuffer* fb, uint32_t tri_test, uint32_t
 {
     if (!fb) return fail(RT_E_INVALID, "NULL argument");
     fb->r->SetOptions(tri_test, kernel);
+    return RT_OK;
+}
+
+int rth_framebuffer_set_intersector(rth_framebuffer* fb, uint32_t intersector)
+{
+    if (!fb) return fail(RT_E_INVALID, "NULL argument");
+    if (intersector > RT_ISECT_RAY_MARCH) return fail(RT_E_INVALID, "unknown intersector");
+    fb->r->SetIntersector(intersector);
     return RT_OK;
 }
 

@@ -53,6 +53,8 @@ int  rth_framebuffer_create(rt_scene *gpu_scene, const rth_scene *host_scene, ui
 void rth_framebuffer_free(rth_framebuffer *fb);
 int  rth_framebuffer_set_sample_count(rth_framebuffer *fb, uint32_t spp);   /* renderer.cpp:56-60 */
 int  rth_framebuffer_set_options(rth_framebuffer *fb, uint32_t tri_test, uint32_t kernel);
+/* Which of Renderer::RenderTile's intersectors runs (renderer.cpp:103-105; enum rt_intersector). */
+int  rth_framebuffer_set_intersector(rth_framebuffer *fb, uint32_t intersector);
 /* Framebuffer::Resize (framebuffer.cpp:94-122): re-tiles 12x9 and renders; blocks until
  * the frame is complete.  seconds = pool start -> last tile (framebuffer.cpp:21, 86). */
 int  rth_framebuffer_resize(rth_framebuffer *fb, uint32_t width, uint32_t height, double *seconds);

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 1
+#define RT_ABI_VERSION 2
 
 enum rt_status {
     RT_OK = 0,
@@ -72,6 +72,15 @@ typedef struct rt_scene_desc {
 
 enum rt_tri_test { RT_TRI_MOLLER_TRUMBORE = 0, RT_TRI_BARYCENTRIC = 1 };
 
+/* The per-sample intersector of Renderer::RenderTile (renderer.cpp:103-105). */
+enum rt_intersector {
+    RT_ISECT_GRID = 0,         /* Grid::Intersect 3D-DDA (grid.cpp:159-281), the default */
+    RT_ISECT_BRUTE_FORCE = 1,  /* Renderer::IntersectBruteForce (renderer.cpp:157-197); MT only */
+    RT_ISECT_RAY_MARCH = 2,    /* Renderer::RayMarch over DistanceBruteForce (renderer.cpp:24-41,
+                                  138-155).  Shaded by depth, t/3 (renderer.cpp:118): the live
+                                  reference line would read the unset tri_idx/u/v */
+};
+
 enum rt_kernel {
     RT_KERNEL_AUTO = 0,        /* the fastest measured variant for the frame's spp */
     RT_KERNEL_LANES = 1,       /* one lane per sample, a pixel's samples in adjacent lanes */
@@ -102,6 +111,7 @@ typedef struct rt_frame {
                                      Hammersley table of renderer.cpp:87-98 */
     uint32_t     tri_test;        /* enum rt_tri_test */
     uint32_t     kernel;          /* enum rt_kernel */
+    uint32_t     intersector;     /* enum rt_intersector (ABI version 2) */
 } rt_frame;
 
 /* Tile::GetPosition (framebuffer.h:41-42); buffer row stride = x1 - x0. */
@@ -112,9 +122,10 @@ typedef struct rt_sample_rec {
     uint32_t hit;     /* 1 = hit */
     uint32_t tri;     /* hit triangle (Grid::Intersect tri_idx), 0xFFFFFFFF on miss */
     uint32_t voxel;   /* GridIdx of the cell the hit was accepted in (last cell walked on a
-                         miss), 0xFFFFFFFF when the ray misses the grid AABB */
-    uint32_t steps;   /* DDA iterations (cells visited) */
-    uint32_t tests;   /* ray/triangle tests executed */
+                         miss), 0xFFFFFFFF when the ray misses the grid AABB and for the
+                         brute-force and ray-march intersectors */
+    uint32_t steps;   /* DDA iterations (cells visited); ray march: march steps */
+    uint32_t tests;   /* ray/triangle tests executed; ray march: point/triangle distances */
     float    t, u, v; /* 0 on miss */
     float    r, g, b; /* this sample's colour contribution before averaging */
     uint32_t pad;
@@ -180,7 +191,9 @@ int  rt_trace_samples(rt_scene *scene, const rt_frame *frame, uint32_t x0, uint3
  * tests/golden/kat_*.f32 records):  0 ray/tri (18 in, 8 out), 1 ray/aabb (12 in, 4 out),
  * 2 generate ray (23 in, 6 out), 3 gamma+pack (3 in, 4 out), 4 shade (11 in, 3 out),
  * 5 the branch-free ray/tri forms the traversal uses (18 in, 8 out; t,u,v valid on hits),
- * 6 the wave-gated forms: pre-gated MT, gated MT (18 in, 8 out; t,u,v valid on hits). */
+ * 6 the wave-gated forms: pre-gated MT, gated MT (18 in, 8 out; t,u,v valid on hits),
+ * 7 DistancePointTri through the ray-march kernel's per-triangle record (12 in: pos, v0, v1,
+ * v2; 1 out). */
 int  rt_debug_primitives(int kind, const float *in, uint32_t n, float *out, int device);
 
 /* Hammersley table the library uses when rt_frame.sample_offsets is NULL. */

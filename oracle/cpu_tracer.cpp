@@ -427,17 +427,106 @@ bool Intersect(const Scene& s, const V3& o, const V3& d, int tri_test, float& t,
     return false;
 }
 
-// renderer.cpp:126-160: one sample
-inline V3 TraceSample(const Scene& s, const float* smp, uint32_t px, uint32_t py, uint32_t W, uint32_t H,
-                      uint32_t si, int tri_test, orc_rec *rec)
+// renderer.cpp:157-197 Renderer::IntersectBruteForce: all triangles in index order, closest
+// accepted IntersectRayTri hit, strict '<' keeps the lower index on ties
+bool IntersectBruteForce(const Scene& s, const V3& o, const V3& d, float& t, float& u, float& v,
+                         uint32_t& tri_idx, uint32_t& tests)
 {
+    t = std::numeric_limits<float>::max();
+    for (uint32_t i=0; i<uint32_t(s.tris.size()); i++)
+    {
+        const Triangle& tr = s.tris[i];
+        float ct, cu, cv;
+        const bool hit = RayTri(o, d, s.verts[tr.v0].p, s.verts[tr.v1].p, s.verts[tr.v2].p, ct, cu, cv);
+        if (hit && ct < t)
+        {
+            t = ct; u = cu; v = cv; tri_idx = i;
+        }
+    }
+    tests = uint32_t(s.tris.size());
+    return t != std::numeric_limits<float>::max();
+}
+
+// triangle.h:163-172 LineSegMinDistSq; Clamp = lin_alg.h:205-212
+inline float LineSegMinDistSq(const V3& a, const V3& b, const V3& p)
+{
+    const V3 ab = sub(b, a);
+    const float len_sq = dot0(ab, ab);
+    float t = dot0(sub(p, a), ab) / len_sq;
+    if (t < 0.0f) t = 0.0f;
+    else if (t > 1.0f) t = 1.0f;
+    const V3 proj = mk(a.x + t * ab.x, a.y + t * ab.y, a.z + t * ab.z);
+    return dot0(sub(p, proj), sub(p, proj));
+}
+
+// triangle.h:174-198 DistancePointTri with ComputeBarycentric (:133-156) and
+// BarycentricInterpolate (:158-161); std::min(a, b) = (b < a) ? b : a
+inline float DistancePointTri(const V3& pos, const V3& v0, const V3& v1, const V3& v2)
+{
+    const V3 e0 = sub(v2, v0), e1 = sub(v1, v0), e2 = sub(pos, v0);
+    const float dot00 = dot0(e0, e0), dot01 = dot0(e0, e1), dot02 = dot0(e0, e2);
+    const float dot11 = dot0(e1, e1), dot12 = dot0(e1, e2);
+    const float inv_denom = 1 / (dot00 * dot11 - dot01 * dot01);
+    const float u = (dot00 * dot12 - dot01 * dot02) * inv_denom;
+    const float v = (dot11 * dot02 - dot01 * dot12) * inv_denom;
+    if ((u >= 0) && (v >= 0) && (u + v < 1))
+    {
+        const float w = 1 - u - v;
+        const V3 q = mk(v1.x * u + v2.x * v + v0.x * w, v1.y * u + v2.y * v + v0.y * w,
+                        v1.z * u + v2.z * v + v0.z * w);
+        return std::sqrt(dot0(sub(pos, q), sub(pos, q)));
+    }
+    const float a = LineSegMinDistSq(v0, v1, pos), b = LineSegMinDistSq(v0, v2, pos),
+                c = LineSegMinDistSq(v1, v2, pos);
+    const float bc = (c < b) ? c : b;
+    return std::sqrt((bc < a) ? bc : a);
+}
+
+// renderer.cpp:24-41 Renderer::RayMarch over DistanceBruteForce (:138-155)
+bool RayMarch(const Scene& s, const V3& o, const V3& d, float& t, uint32_t& steps, uint32_t& tests)
+{
+    const uint32_t max_steps = 128;
+    const float min_dist = 0.001f;
+    t = 0.0f;
+    steps = tests = 0;
+    for (uint32_t i=0; i<max_steps; i++)
+    {
+        const V3 pos = mk(o.x + t * d.x, o.y + t * d.y, o.z + t * d.z);
+        float dist = std::numeric_limits<float>::max();
+        for (const auto& tr : s.tris)
+        {
+            const float di = DistancePointTri(pos, s.verts[tr.v0].p, s.verts[tr.v1].p, s.verts[tr.v2].p);
+            dist = (di < dist) ? di : dist;
+        }
+        t += dist;
+        steps = i + 1;
+        tests += uint32_t(s.tris.size());
+        if (dist < min_dist) return true;
+    }
+    return false;
+}
+
+// renderer.cpp:126-160: one sample.  mode = tri_test | intersector << 8 (rt_intersector)
+inline V3 TraceSample(const Scene& s, const float* smp, uint32_t px, uint32_t py, uint32_t W, uint32_t H,
+                      uint32_t si, int mode, orc_rec *rec)
+{
+    const int tri_test = mode & 0xFF, isect = mode >> 8;
     V3 o, d;
     GenRay(s.cam, px, py, W, H, smp[2 * si], smp[2 * si + 1], s.fov, o, d);
     float t = 0, u = 0, v = 0;
-    uint32_t tri = 0xFFFFFFFFu, voxel, steps, tests;
-    const bool hit = Intersect(s, o, d, tri_test, t, u, v, tri, voxel, steps, tests);
+    uint32_t tri = 0xFFFFFFFFu, voxel = 0xFFFFFFFFu, steps = 0, tests = 0;
+    bool hit;
+    if (isect == 2) hit = RayMarch(s, o, d, t, steps, tests);
+    else if (isect == 1) hit = IntersectBruteForce(s, o, d, t, u, v, tri, tests);
+    else hit = Intersect(s, o, d, tri_test, t, u, v, tri, voxel, steps, tests);
     V3 c;
-    if (hit)
+    if (hit && isect == 2)
+    {
+        c = mk(t / 3, t / 3, t / 3);                               // renderer.cpp:118 (depth)
+        u = v = 0.0f;
+        tri = 0xFFFFFFFFu;
+    }
+    else if (hit)
     {
         const Triangle& tr = s.tris[tri];
         c = ShadeHit(u, v, s.verts[tr.v0].n, s.verts[tr.v1].n, s.verts[tr.v2].n);
@@ -672,6 +761,16 @@ void orc_kat_ray_tri(const float *in, uint32_t n, float *out)
         const bool h2 = RayTriBary(o, d, a, b, c, nn, bt, bu, bv);
         out[0] = bitsf(h1); out[1] = t; out[2] = u; out[3] = v;
         out[4] = bitsf(h2); out[5] = bt; out[6] = bu; out[7] = bv;
+    }
+}
+
+void orc_kat_dist(const float *in, uint32_t n, float *out)
+{
+    for (uint32_t i=0; i<n; i++)
+    {
+        const float *a = in + 12 * size_t(i);
+        out[i] = DistancePointTri(mk(a[0], a[1], a[2]), mk(a[3], a[4], a[5]), mk(a[6], a[7], a[8]),
+                                  mk(a[9], a[10], a[11]));
     }
 }
 

@@ -51,7 +51,9 @@ int        orc_scene_csr(const orc_scene *s, uint32_t *offsets, uint32_t *refs);
 /* mesh arrays as in the file: vertices [nv][6] f32, triangles [nt][6] (3 u32 + 3 f32) */
 int        orc_scene_mesh(const orc_scene *s, float *vertices, uint32_t *triangles);
 
-/* tri_test: 0 = IntersectRayTri (Moller-Trumbore, default), 1 = IntersectRayTriBarycentric */
+/* tri_test: 0 = IntersectRayTri (Moller-Trumbore, default), 1 = IntersectRayTriBarycentric,
+ * OR'ed with (intersector << 8): 0 = Grid::Intersect, 1 = Renderer::IntersectBruteForce
+ * (renderer.cpp:157-197), 2 = Renderer::RayMarch (renderer.cpp:24-41, shaded by depth t/3). */
 /* Full frame through the restated 12x9 std::thread tile pool; out_bgra W*H row-major.
  * hit_ids (optional, W*H*spp): tri index per sample or 0xFFFFFFFF.  seconds = pool span. */
 int orc_render(const orc_scene *s, uint32_t W, uint32_t H, uint32_t spp, uint32_t tri_test,
@@ -67,6 +69,7 @@ void orc_kat_ray_aabb(const float *in12, uint32_t n, float *out4);
 void orc_kat_genray(const float *in23, uint32_t n, float *out6);
 void orc_kat_bgra8(const float *in3, uint32_t n, float *out4);
 void orc_kat_shade(const float *in11, uint32_t n, float *out3);
+void orc_kat_dist(const float *in12, uint32_t n, float *out1);   /* triangle.h:174-198 */
 
 #ifdef __cplusplus
 }

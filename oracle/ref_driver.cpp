@@ -15,6 +15,8 @@
 //   * the scene table of Application::InitializeScene        (application.cpp:304-517)
 //   * the per-pixel/per-sample loop body of Renderer::RenderTile (renderer.cpp:81-174)
 //   * the 12x9 std::thread tile pool of Framebuffer           (framebuffer.cpp:10-130)
+//   * the loops of Renderer::IntersectBruteForce / DistanceBruteForce / RayMarch
+//     (renderer.cpp:24-41, 138-197) around the reference's IntersectRayTri / DistancePointTri
 // The restated glue only sequences calls into the reference's functions above.
 //
 // Subcommands (all output little-endian binary files or one "RESULT {json}" line):
@@ -22,7 +24,11 @@
 //   grid   <scene.rtscene> <out.bin>         grid meta + CSR export of Grid::Grid's cells
 //   render <scene.rtscene> W H spp [--threads N] [--reps R] [--out f] [--hits f]
 //   samples <scene.rtscene> W H spp x0 y0 w h <out.bin>    per-sample records
+//   alt-samples <scene.rtscene> W H spp x0 y0 w h brute|march <out.bin>
+//                                            records of Renderer::IntersectBruteForce / RayMarch
+//   render ... [--isect grid|brute|march]   the frame with another intersector (renderer.cpp:103-105)
 //   kat <outdir>                             primitive known-answer vectors
+//   kat-dist <out.f32>                       DistancePointTri known answers
 
 #include <memory>
 #include <vector>
@@ -309,7 +315,52 @@ struct Frame
     Matrix44f cam;
     float fov;
     uint width, height, spp;
+    int isect = 0;                  // 0 Grid::Intersect, 1 IntersectBruteForce, 2 RayMarch
 };
+
+// renderer.cpp:157-197 (loop glue; IntersectRayTri is the reference's, triangle.h:15-107)
+bool IntersectBruteForceRef(const Mesh *mesh, Vec3f origin, Vec3f dir, float& t, float& u, float& v,
+                            uint32& tri_idx)
+{
+    t = std::numeric_limits<float>::max();
+    const uint32 n = uint32(mesh->m_triangles.size());
+    for (uint32 i=0; i<n; i++)
+    {
+        const Mesh::Triangle& tri = mesh->m_triangles[i];
+        float ct, cu, cv;
+        const bool hit = IntersectRayTri(origin, dir, mesh->m_vertices[tri.v0].p, mesh->m_vertices[tri.v1].p,
+                                         mesh->m_vertices[tri.v2].p, ct, cu, cv);
+        if (hit && ct < t) { t = ct; u = cu; v = cv; tri_idx = i; }
+    }
+    return t != std::numeric_limits<float>::max();
+}
+
+// renderer.cpp:138-155 (loop glue; DistancePointTri is the reference's, triangle.h:174-198)
+float DistanceBruteForceRef(const Mesh *mesh, Vec3f pos)
+{
+    float dist = std::numeric_limits<float>::max();
+    for (const auto& tri : mesh->m_triangles)
+        dist = std::min(dist, DistancePointTri(pos, mesh->m_vertices[tri.v0].p, mesh->m_vertices[tri.v1].p,
+                                               mesh->m_vertices[tri.v2].p));
+    return dist;
+}
+
+// renderer.cpp:24-41; steps_out counts the march steps taken (instrumentation only)
+bool RayMarchRef(const Mesh *mesh, Vec3f origin, Vec3f dir, float& t, uint& steps_out)
+{
+    const uint max_steps = 128;
+    const float min_dist = 0.001f;
+    t = 0.0f;
+    for (uint steps=0; steps<max_steps; steps++)
+    {
+        const Vec3f pos = origin + t * dir;
+        const float dist = DistanceBruteForceRef(mesh, pos);
+        t += dist;
+        steps_out = steps + 1;
+        if (dist < min_dist) return true;
+    }
+    return false;
+}
 
 std::vector<Vec2f> SampleTable(uint spp)
 {
@@ -343,8 +394,17 @@ void RenderTileRef(const Frame& fr, uint x0, uint y0, uint x1, uint y1, uint32 *
                 GenerateRay(fr.cam, pixel, fr.width, fr.height, smp_loc[smp], false, fr.fov, origin, dir);
                 float t, u, v;
                 uint32 tri_idx;
-                bool hit = fr.grid->Intersect(origin, dir, t, u, v, tri_idx);
-                if (hit)
+                uint steps = 0;
+                bool hit;
+                if (fr.isect == 2) hit = RayMarchRef(fr.mesh, origin, dir, t, steps);
+                else if (fr.isect == 1) hit = IntersectBruteForceRef(fr.mesh, origin, dir, t, u, v, tri_idx);
+                else hit = fr.grid->Intersect(origin, dir, t, u, v, tri_idx);
+                if (hit && fr.isect == 2)
+                {
+                    col += Vec3f(t / 3);                              // renderer.cpp:118
+                    tri_idx = 0xFFFFFFFFu;
+                }
+                else if (hit)
                 {
                     const Mesh::Triangle& tri = fr.mesh->m_triangles[tri_idx];
                     const Vec3f n = Normalize(BarycentricInterpolate(
@@ -454,6 +514,45 @@ float RandF(std::mt19937& g, float lo, float hi)
 Vec3f RandV(std::mt19937& g, float lo, float hi)
 {
     return Vec3f(RandF(g, lo, hi), RandF(g, lo, hi), RandF(g, lo, hi));
+}
+
+// DistancePointTri (triangle.h:174-198) known answers: in pos, v0, v1, v2 (12 f32), out dist
+int CmdKatDist(const char *path)
+{
+    std::mt19937 g(20261016u);
+    std::vector<float> rec;
+    const int N = 6000;
+    for (int i=0; i<N; i++)
+    {
+        Vec3f v0 = RandV(g, -1, 1), v1 = RandV(g, -1, 1), v2 = RandV(g, -1, 1), pos = RandV(g, -2, 2);
+        const int kind = i % 8;
+        if (kind == 1)          // on the plane, inside or just outside (barycentric edge cases)
+        {
+            const float a = RandF(g, -0.1f, 1.1f), b = RandF(g, -0.1f, 1.1f);
+            pos = v0 + (v1 - v0) * a + (v2 - v0) * b;
+        }
+        else if (kind == 2)     // at a vertex or an edge midpoint
+            pos = (i & 8) ? v2 : (v1 + v2) * 0.5f;
+        else if (kind == 3)     // repeated vertex (zero area -> inf/NaN barycentrics)
+            v2 = v0;
+        else if (kind == 4)     // collinear
+            v2 = v0 + (v1 - v0) * RandF(g, -1.0f, 2.0f);
+        else if (kind == 5)     // all three vertices equal (zero-length edges -> 0/0 clamps)
+            v1 = v2 = v0;
+        else if (kind == 6)     // tiny triangle far away
+        {
+            v1 = v0 + RandV(g, -1e-4f, 1e-4f);
+            v2 = v0 + RandV(g, -1e-4f, 1e-4f);
+            pos = pos * 50.0f;
+        }
+        const float d = DistancePointTri(pos, v0, v1, v2);
+        const Vec3f in[4] = { pos, v0, v1, v2 };
+        for (const auto& x : in) { rec.push_back(x.x); rec.push_back(x.y); rec.push_back(x.z); }
+        rec.push_back(d);
+    }
+    if (!WriteFile(path, &rec[0], rec.size() * 4)) return 1;
+    std::printf("RESULT {\"kat_dist\": %d}\n", N);
+    return 0;
 }
 
 int CmdKat(const char *outdir)
@@ -669,8 +768,11 @@ int main(int argc, char **argv)
 
     if (cmd == "kat" && argc == 3)
         return CmdKat(argv[2]);
+    if (cmd == "kat-dist" && argc == 3)
+        return CmdKatDist(argv[2]);
 
-    if ((cmd == "grid" && argc == 4) || (cmd == "render" && argc >= 6) || (cmd == "samples" && argc == 11))
+    if ((cmd == "grid" && argc == 4) || (cmd == "render" && argc >= 6) || (cmd == "samples" && argc == 11) ||
+        (cmd == "alt-samples" && argc == 12))
     {
         SceneFile sf;
         if (!ReadScene(argv[2], sf)) { std::fprintf(stderr, "bad scene file\n"); return 1; }
@@ -738,6 +840,60 @@ int main(int argc, char **argv)
             return 0;
         }
 
+        if (cmd == "alt-samples")
+        {
+            // u32 hit, tri, steps | f32 t, u, v, r, g, b   (t, u, v = 0 and tri = ~0 on a miss)
+            struct AltRec { uint32 hit, tri, steps; float t, u, v, r, g, b; };
+            const uint x0 = std::atoi(argv[6]), y0 = std::atoi(argv[7]);
+            const uint w = std::atoi(argv[8]), h = std::atoi(argv[9]);
+            const std::string mode = argv[10];
+            if (mode != "brute" && mode != "march") return Usage();
+            const std::vector<Vec2f> smp_loc = SampleTable(fr.spp);
+            std::vector<AltRec> recs;
+            for (uint y=y0; y<y0 + h; y++)
+                for (uint x=x0; x<x0 + w; x++)
+                    for (uint s=0; s<fr.spp; s++)
+                    {
+                        Vec3f origin, dir;
+                        GenerateRay(fr.cam, Vec2ui(x, y), fr.width, fr.height, smp_loc[s], false, fr.fov, origin, dir);
+                        AltRec r;
+                        float t = 0, u = 0, v = 0;
+                        uint32 tri = 0xFFFFFFFFu;
+                        uint steps = 0;
+                        Vec3f c;
+                        bool hit;
+                        if (mode == "march")
+                        {
+                            hit = RayMarchRef(mesh_ptr, origin, dir, t, steps);
+                            if (hit) c = Vec3f(t / 3);
+                        }
+                        else
+                        {
+                            hit = IntersectBruteForceRef(mesh_ptr, origin, dir, t, u, v, tri);
+                            if (hit)
+                            {
+                                const Mesh::Triangle& tr = mesh_ptr->m_triangles[tri];
+                                const Vec3f n = Normalize(BarycentricInterpolate(u, v,
+                                    mesh_ptr->m_vertices[tr.v0].n, mesh_ptr->m_vertices[tr.v1].n,
+                                    mesh_ptr->m_vertices[tr.v2].n));
+                                c = Vec3f((n + 1.0f) * 0.5f);
+                            }
+                        }
+                        if (!hit)
+                        {
+                            c = Vec3f(float(y) / float(fr.height));
+                            t = u = v = 0.0f;
+                            tri = 0xFFFFFFFFu;
+                        }
+                        r.hit = hit; r.tri = tri; r.steps = steps; r.t = t; r.u = u; r.v = v;
+                        r.r = c.x; r.g = c.y; r.b = c.z;
+                        recs.push_back(r);
+                    }
+            if (!WriteFile(argv[11], &recs[0], recs.size() * sizeof(AltRec))) return 1;
+            std::printf("RESULT {\"samples\": %zu}\n", recs.size());
+            return 0;
+        }
+
         // render
         uint nthreads = std::max(1u, std::thread::hardware_concurrency());   // framebuffer.cpp:11
         uint reps = 1;
@@ -749,6 +905,11 @@ int main(int argc, char **argv)
             else if (a == "--reps" && i + 1 < argc) reps = std::atoi(argv[++i]);
             else if (a == "--out" && i + 1 < argc) out = argv[++i];
             else if (a == "--hits" && i + 1 < argc) hits = argv[++i];
+            else if (a == "--isect" && i + 1 < argc)
+            {
+                const std::string m = argv[++i];
+                fr.isect = m == "brute" ? 1 : (m == "march" ? 2 : 0);
+            }
         }
         TilePool pool;
         pool.Resize(fr.width, fr.height);

@@ -76,7 +76,7 @@ class Oracle:
         L.orc_render.argtypes = [vp] + [ctypes.c_uint32] * 5 + [vp, vp, ctypes.POINTER(ctypes.c_double)]
         L.orc_trace_samples.argtypes = [vp] + [ctypes.c_uint32] * 8 + [vp]
         for fn in ("orc_kat_ray_tri", "orc_kat_ray_aabb", "orc_kat_genray", "orc_kat_bgra8",
-                   "orc_kat_shade"):
+                   "orc_kat_shade", "orc_kat_dist"):
             getattr(L, fn).argtypes = [vp, ctypes.c_uint32, vp]
         L.orc_hammersley.argtypes = [ctypes.c_uint32, vp]
         self.L = L
@@ -138,6 +138,27 @@ def golden():
 
 
 @pytest.fixture(scope="session")
+def golden_alt():
+    with open(os.path.join(GOLD, "alt.json")) as f:
+        return json.load(f)
+
+
+# records of oracle/_ref/refdriver alt-samples (tests/golden/alt/*.rec.gz)
+ALT_REC_DTYPE = np.dtype([("hit", "<u4"), ("tri", "<u4"), ("steps", "<u4"), ("t", "<f4"), ("u", "<f4"),
+                          ("v", "<f4"), ("r", "<f4"), ("g", "<f4"), ("b", "<f4")])
+ISECT = {"brute": 1, "march": 2}
+
+
+def nan_equal_bits(a, b):
+    """Bitwise equality where NaN == NaN regardless of payload/sign: x86 produces the negative
+    default NaN (0xFFC00000), gfx950 the positive canonical one (0x7FC00000)."""
+    a = np.ascontiguousarray(a, np.float32)
+    b = np.ascontiguousarray(b, np.float32)
+    both_nan = np.isnan(a) & np.isnan(b)
+    return bool(np.all(both_nan | (a.view(np.uint32) == b.view(np.uint32))))
+
+
+@pytest.fixture(scope="session")
 def oracle():
     return Oracle()
 
@@ -148,7 +169,8 @@ def rtm():
 
 
 # KAT layouts: (file, input width, output width)
-KATS = {"ray_tri": (18, 8), "ray_aabb": (12, 4), "genray": (23, 6), "bgra8": (3, 4), "shade": (11, 3)}
+KATS = {"ray_tri": (18, 8), "ray_aabb": (12, 4), "genray": (23, 6), "bgra8": (3, 4), "shade": (11, 3),
+        "dist": (12, 1)}
 
 
 def load_kat(name):

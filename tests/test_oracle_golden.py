@@ -108,3 +108,12 @@ def test_full_frame_1080p4(oracle, golden, sid):
     img, hits, _ = oracle.render(sid, 1920, 1080, 4, hits=True)
     assert hashlib.sha256(img.tobytes()).hexdigest() == g["bgra_sha256"]
     assert hashlib.sha256(hits.tobytes()).hexdigest() == g["hits_sha256"]
+
+
+def test_kat_dist(oracle):
+    """DistancePointTri (triangle.h:174-198): inside/outside the prism, on vertices and edges,
+    zero-area, collinear and all-equal vertices (inf/NaN barycentrics and 0/0 clamps)."""
+    rin, exp = load_kat("dist")
+    got = oracle.kat("dist", rin, 1)
+    np.testing.assert_array_equal(bits(got), bits(exp))      # same x86 NaNs on both sides
+    assert np.isnan(exp).sum() > 100
