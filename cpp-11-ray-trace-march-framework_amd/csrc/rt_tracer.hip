@@ -62,7 +62,9 @@ constexpr int kVarNestedStep = 16;          // RT_KERNEL_FLAG_NESTED_STEP (A/B a
 constexpr int kVarPreGate = 32;             // RT_KERNEL_FLAG_PRE_GATE
 constexpr int kVarBrute = 64;               // RT_ISECT_BRUTE_FORCE (renderer.cpp:157-197)
 constexpr int kVarMarch = 128;              // RT_ISECT_RAY_MARCH (renderer.cpp:24-41, 138-155)
+constexpr int kVarExhaustive = 256;         // RT_KERNEL_FLAG_EXHAUSTIVE: march without block culling
 constexpr uint32_t kMarchSteps = 128;       // renderer.cpp:26
+constexpr uint32_t kDistBlock = 32;         // triangles per culling block of the distance kernels
 
 struct KParams
 {
@@ -87,7 +89,11 @@ struct KParams
     const float4 *face_n;
     const uint32_t *occ;
     const float4 *tri_mt;       // per triangle {v0, e1, e2} in triangle order (brute force)
-    const float4 *tri_dist;     // per triangle distance record (rtd::dist_point_tri)
+    const float4 *tri_dist;     // per triangle distance record (rtd::dist_point_tri), Morton order
+    const float4 *dist_blk;     // per kDistBlock records: {aabb min, -}{aabb max, -}
+    uint32_t ndist_blk;
+    float scene_scale;          // max |vertex coordinate| (error bound of the block cull)
+    float smin[3], smax[3];     // vertex AABB (exact float min / max)
     uint32_t ntris;
     uint32_t tri_test;
     uint32_t isect;             // enum rt_intersector
@@ -399,27 +405,110 @@ __device__ __forceinline__ bool brute_intersect(const KParams& P, float ox, floa
 
 // Renderer::RayMarch (renderer.cpp:24-41) over Renderer::DistanceBruteForce (:138-155):
 // sphere tracing from the camera, at most 128 steps, hit when a step's distance < 0.001.
-template <bool STATS>
+//
+// DistanceBruteForce is a minimum, and the minimum of a set does not depend on the order it
+// is taken in ((d < dist) ? d : dist never selects a NaN, ties have equal values), so any
+// triangle whose computed distance is provably above the minimum can be skipped, and any member
+// may seed it, without changing a bit.  The records are Morton-sorted into blocks of kDistBlock
+// triangles with an exact float AABB.  Error model: every computed DistancePointTri is the
+// distance to a point of the triangle (the inside branch's convex combination or a clamped
+// segment point) up to ~10 ulp of (|p| + |v|); float box distances are off by a few ulp of the
+// same scale.  margin = 1e-5 * (|p|_inf + scene_scale) (>= 166 ulp) therefore gives
+//   lb(block) - margin <= every computed distance of the block's triangles.
+// Per step and lane: the minimum is seeded with the computed distance to the lane's previous
+// nearest triangle, blocks are swept outward from that triangle's block (lane 0's), and a block
+// is skipped when lb - margin > running minimum for every active lane (wave-uniform branch).
+//
+// Miss early-out: once p is outside the vertex AABB with box distance Db, receding from it at a
+// rate r = dir . (p - clamp(p)) / Db >= 2e-5, and Db > 1.00001 * (margin + 0.001), every later
+// point p' = p + s * dir has Db' >= Db + r s and margin' <= margin + 1e-5 s (|dir| <= 1), so
+// every later computed distance exceeds 0.001: the reference marches to its 128-step limit
+// without a hit (renderer.cpp:30-40).  The march stops there and reports exactly that.
+__device__ __forceinline__ void march_eval_block(const KParams& P, uint32_t b, float px, float py, float pz,
+                                                 float& dist, uint32_t& best_k)
+{
+    const uint32_t k0 = b * kDistBlock, k1 = min(k0 + kDistBlock, P.ntris);
+    for (uint32_t k = k0; k < k1; k++)
+    {
+        const float4 *r = P.tri_dist + 6 * size_t(k);
+        const float d = rtd::dist_point_tri(px, py, pz, r[0], r[1], r[2], r[3], r[4], r[5]);
+        if (d < dist)
+        {
+            dist = d;
+            best_k = k;
+        }
+    }
+}
+
+// true when block b can still lower some active lane's minimum
+__device__ __forceinline__ bool march_block_needed(const KParams& P, uint32_t b, float px, float py, float pz,
+                                                   float margin, float dist)
+{
+    const float4 mn = P.dist_blk[2 * b], mx = P.dist_blk[2 * b + 1];
+    const float ex = fmaxf(fmaxf(mn.x - px, px - mx.x), 0.0f);
+    const float ey = fmaxf(fmaxf(mn.y - py, py - mx.y), 0.0f);
+    const float ez = fmaxf(fmaxf(mn.z - pz, pz - mx.z), 0.0f);
+    const float lb = __builtin_sqrtf(ex * ex + ey * ey + ez * ez) - margin;
+    return __any(!(lb > dist));
+}
+
+template <bool STATS, bool EXHAUSTIVE>
 __device__ __forceinline__ bool ray_march(const KParams& P, float ox, float oy, float oz, float dx, float dy,
                                           float dz, float& t, uint32_t& steps, uint32_t& tests)
 {
     t = 0.0f;
+    uint32_t best_k = 0;                 // sorted index of the previous step's nearest triangle
     for (uint32_t s = 0; s < kMarchSteps; s++)
     {
         const float px = ox + t * dx, py = oy + t * dy, pz = oz + t * dz;
         float dist = rtd::kFltMax;
-        for (uint32_t i = 0; i < P.ntris; i++)
+        if (EXHAUSTIVE)
         {
-            const float4 *r = P.tri_dist + 6 * size_t(i);
-            const float d = rtd::dist_point_tri(px, py, pz, r[0], r[1], r[2], r[3], r[4], r[5]);
-            dist = (d < dist) ? d : dist;                            // std::min(dist, d)
+            for (uint32_t i = 0; i < P.ntris; i++)
+            {
+                const float4 *r = P.tri_dist + 6 * size_t(i);
+                const float d = rtd::dist_point_tri(px, py, pz, r[0], r[1], r[2], r[3], r[4], r[5]);
+                dist = (d < dist) ? d : dist;                        // std::min(dist, d)
+            }
+            if (STATS) tests += P.ntris;
+        }
+        else
+        {
+            const float margin = 1e-5f * (fmaxf(fmaxf(fabsf(px), fabsf(py)), fabsf(pz)) + P.scene_scale);
+            {
+                const float wx = px - fminf(fmaxf(px, P.smin[0]), P.smax[0]);
+                const float wy = py - fminf(fmaxf(py, P.smin[1]), P.smax[1]);
+                const float wz = pz - fminf(fmaxf(pz, P.smin[2]), P.smax[2]);
+                const float db = __builtin_sqrtf(wx * wx + wy * wy + wz * wz);
+                const float rate = dx * wx + dy * wy + dz * wz;
+                if (db > 1.00001f * (margin + 0.001f) && rate >= 2e-5f * db)
+                {
+                    if (STATS) steps = kMarchSteps;
+                    return false;
+                }
+            }
+            {
+                const float4 *r = P.tri_dist + 6 * size_t(best_k);
+                dist = rtd::dist_point_tri(px, py, pz, r[0], r[1], r[2], r[3], r[4], r[5]);
+            }
+            uint32_t evals = 1;
+            const uint32_t start = __builtin_amdgcn_readfirstlane(best_k / kDistBlock);
+            for (uint32_t b = start; b < P.ndist_blk; b++)
+            {
+                if (!march_block_needed(P, b, px, py, pz, margin, dist)) continue;
+                march_eval_block(P, b, px, py, pz, dist, best_k);
+                evals += min(b * kDistBlock + kDistBlock, P.ntris) - b * kDistBlock;
+            }
+            for (uint32_t b = start; b-- > 0;)
+            {
+                if (!march_block_needed(P, b, px, py, pz, margin, dist)) continue;
+                march_eval_block(P, b, px, py, pz, dist, best_k);
+                evals += min(b * kDistBlock + kDistBlock, P.ntris) - b * kDistBlock;
+            }
+            if (STATS) tests += evals;
         }
         t += dist;
-        if (STATS)
-        {
-            steps = s + 1;
-            tests += P.ntris;
-        }
+        if (STATS) steps = s + 1;
         if (dist < 0.001f) return true;
     }
     return false;
@@ -438,7 +527,8 @@ __device__ __forceinline__ void trace_sample(const KParams& P, const uint32_t *l
     uint32_t tri = rtd::kNoTri, voxel = rtd::kNoTri, steps = 0, tests = 0;
     bool hit;
     if constexpr ((VAR & kVarMarch) != 0)
-        hit = ray_march<STATS>(P, P.org[0], P.org[1], P.org[2], dx, dy, dz, t, steps, tests);
+        hit = ray_march<STATS, (VAR & kVarExhaustive) != 0>(P, P.org[0], P.org[1], P.org[2], dx, dy, dz, t, steps,
+                                                             tests);
     else if constexpr ((VAR & kVarBrute) != 0)
         hit = brute_intersect<STATS>(P, P.org[0], P.org[1], P.org[2], dx, dy, dz, t, u, v, tri, tests);
     else
@@ -622,6 +712,9 @@ __global__ void __launch_bounds__(kWG) k_trace_records(KParams P, uint32_t n)
     // parity tests (hit, tri, voxel, steps, tests) cover exactly the code the frames use.
     if (P.isect == RT_ISECT_RAY_MARCH)
         trace_sample<true, RT_TRI_MOLLER_TRUMBORE, kVarMarch>(P, nullptr, x, y, s, cr, cg, cb, &P.recs[i]);
+    else if (P.isect == RT_ISECT_RAY_MARCH + 0x100)   // exhaustive arm (RT_KERNEL_FLAG_EXHAUSTIVE)
+        trace_sample<true, RT_TRI_MOLLER_TRUMBORE, kVarMarch | kVarExhaustive>(P, nullptr, x, y, s, cr, cg, cb,
+                                                                              &P.recs[i]);
     else if (P.isect == RT_ISECT_BRUTE_FORCE)
         trace_sample<true, RT_TRI_MOLLER_TRUMBORE, kVarBrute>(P, nullptr, x, y, s, cr, cg, cb, &P.recs[i]);
     else if (P.tri_test == RT_TRI_BARYCENTRIC)
@@ -805,7 +898,10 @@ struct rt_scene
     uint32_t ncells = 0, nrefs = 0, ntris = 0, occ_words = 0;
     uint32_t *d_off = nullptr, *d_occ = nullptr, *d_cellw = nullptr;
     float4 *d_refs = nullptr, *d_shade = nullptr, *d_facen = nullptr;
-    float4 *d_trimt = nullptr, *d_tridist = nullptr;
+    float4 *d_trimt = nullptr, *d_tridist = nullptr, *d_distblk = nullptr;
+    uint32_t ndist_blk = 0;
+    float scene_scale = 0.0f;
+    float vmin[3] = { 0, 0, 0 }, vmax[3] = { 0, 0, 0 };
     uint64_t device_bytes = 0;
     uint32_t persist_wgs = 1024;    // persistent grid: 4 x 512-lane workgroups per CU
     // sample table cache
@@ -872,7 +968,7 @@ int validate_frame(const rt_frame *f)
     if ((f->kernel & 0xFFu) > RT_KERNEL_PERSISTENT ||
         (f->kernel & ~(0xFFu | RT_KERNEL_FLAG_PREFETCH | RT_KERNEL_FLAG_WAVE_GATE | RT_KERNEL_FLAG_LOOKAHEAD |
                        RT_KERNEL_FLAG_CSR_OFFSETS | RT_KERNEL_FLAG_DIST_SKIP | RT_KERNEL_FLAG_NESTED_STEP |
-                       RT_KERNEL_FLAG_PRE_GATE)))
+                       RT_KERNEL_FLAG_PRE_GATE | RT_KERNEL_FLAG_EXHAUSTIVE)))
         return fail(RT_E_INVALID, "unknown kernel");
     const uint32_t spp = std::max(1u, f->spp);
     if (spp > 4096) return fail(RT_E_INVALID, "spp must be <= 4096");
@@ -919,6 +1015,14 @@ void frame_params(const rt_scene *s, const rt_frame *f, KParams& P)
     P.occ = s->d_occ;
     P.tri_mt = s->d_trimt;
     P.tri_dist = s->d_tridist;
+    P.dist_blk = s->d_distblk;
+    P.ndist_blk = s->ndist_blk;
+    P.scene_scale = s->scene_scale;
+    for (int a = 0; a < 3; a++)
+    {
+        P.smin[a] = s->vmin[a];
+        P.smax[a] = s->vmax[a];
+    }
     P.ntris = s->ntris;
     P.tri_test = f->tri_test;
     P.isect = f->intersector;
@@ -970,7 +1074,9 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
     else if (lanes && P.isect != RT_ISECT_GRID)
     {
         const dim3 grid{uint32_t(blocks)};
-        if (P.isect == RT_ISECT_RAY_MARCH)
+        if (P.isect == RT_ISECT_RAY_MARCH && (f->kernel & RT_KERNEL_FLAG_EXHAUSTIVE))
+            hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, kVarMarch | kVarExhaustive>), grid, wg, 0, st, P);
+        else if (P.isect == RT_ISECT_RAY_MARCH)
             hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, kVarMarch>), grid, wg, 0, st, P);
         else
             hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, kVarBrute>), grid, wg, 0, st, P);
@@ -992,6 +1098,9 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
         else if (var == 42) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 42>), grid, wg, 0, st, P);
         else                hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 0>), grid, wg, 0, st, P);
     }
+    else if (P.isect == RT_ISECT_RAY_MARCH && (f->kernel & RT_KERNEL_FLAG_EXHAUSTIVE))
+        hipLaunchKernelGGL((k_render_pixel_loop<RT_TRI_MOLLER_TRUMBORE, kVarMarch | kVarExhaustive>),
+                           dim3(uint32_t(blocks)), wg, 0, st, P);
     else if (P.isect == RT_ISECT_RAY_MARCH)
         hipLaunchKernelGGL((k_render_pixel_loop<RT_TRI_MOLLER_TRUMBORE, kVarMarch>), dim3(uint32_t(blocks)), wg, 0, st, P);
     else if (P.isect == RT_ISECT_BRUTE_FORCE)
@@ -1123,7 +1232,6 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
             trimt[3 * size_t(i) + 0] = make_float4(p0[0], p0[1], p0[2], e1[0]);
             trimt[3 * size_t(i) + 1] = make_float4(e1[1], e1[2], e2[0], e2[1]);
             trimt[3 * size_t(i) + 2] = make_float4(e2[2], 0.0f, 0.0f, 0.0f);
-            dist_record(p0, p1, p2, &tridist[6 * size_t(i)]);
         }
         const float *n0 = d->vertices[t.v0].n, *n1 = d->vertices[t.v1].n, *n2 = d->vertices[t.v2].n;
         shade[3 * size_t(i) + 0] = make_float4(n0[0], n0[1], n0[2], n1[0]);
@@ -1187,6 +1295,67 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
     RT_HIP(hipMemcpy(s->d_shade, shade.data(), sizeof(float4) * shade.size(), hipMemcpyHostToDevice));
     RT_HIP(hipMemcpy(s->d_facen, facen.data(), sizeof(float4) * facen.size(), hipMemcpyHostToDevice));
     RT_HIP(hipMemcpy(s->d_occ, occ.data(), sizeof(uint32_t) * occ.size(), hipMemcpyHostToDevice));
+    // Distance records in Morton order of the triangle centroids, blocks of kDistBlock with their
+    // exact float AABB (the ray march's block cull, see ray_march)
+    std::vector<float4> distblk;
+    {
+        const uint32_t nt = d->num_triangles;
+        float mn[3] = { rtd::kFltMax, rtd::kFltMax, rtd::kFltMax }, mx[3] = { -rtd::kFltMax, -rtd::kFltMax, -rtd::kFltMax };
+        float scale = 0.0f;
+        for (uint32_t i = 0; i < d->num_vertices; i++)
+            for (int a = 0; a < 3; a++)
+            {
+                mn[a] = std::min(mn[a], d->vertices[i].p[a]);
+                mx[a] = std::max(mx[a], d->vertices[i].p[a]);
+                scale = std::max(scale, std::fabs(d->vertices[i].p[a]));
+            }
+        std::vector<std::pair<uint64_t, uint32_t>> order(nt);
+        for (uint32_t i = 0; i < nt; i++)
+        {
+            const rt_triangle& t = d->triangles[i];
+            uint64_t code = 0;
+            uint32_t q[3];
+            for (int a = 0; a < 3; a++)
+            {
+                const double c = (double(d->vertices[t.v0].p[a]) + d->vertices[t.v1].p[a] + d->vertices[t.v2].p[a]) / 3.0;
+                const double ext = double(mx[a]) - double(mn[a]);
+                const double f = ext > 0.0 ? (c - mn[a]) / ext : 0.0;
+                q[a] = uint32_t(std::min(1023.0, std::max(0.0, f * 1024.0)));
+            }
+            for (int bit = 9; bit >= 0; bit--)
+                for (int a = 0; a < 3; a++) code = (code << 1) | ((q[a] >> bit) & 1u);
+            order[i] = { code, i };
+        }
+        std::sort(order.begin(), order.end());
+        s->ndist_blk = (nt + kDistBlock - 1) / kDistBlock;
+        distblk.resize(size_t(s->ndist_blk) * 2);
+        for (uint32_t b = 0; b < s->ndist_blk; b++)
+        {
+            float bmn[3] = { rtd::kFltMax, rtd::kFltMax, rtd::kFltMax }, bmx[3] = { -rtd::kFltMax, -rtd::kFltMax, -rtd::kFltMax };
+            for (uint32_t k = b * kDistBlock; k < std::min(nt, (b + 1) * kDistBlock); k++)
+            {
+                const rt_triangle& t = d->triangles[order[k].second];
+                const float *p[3] = { d->vertices[t.v0].p, d->vertices[t.v1].p, d->vertices[t.v2].p };
+                dist_record(p[0], p[1], p[2], &tridist[6 * size_t(k)]);
+                for (int v = 0; v < 3; v++)
+                    for (int a = 0; a < 3; a++)
+                    {
+                        bmn[a] = std::min(bmn[a], p[v][a]);
+                        bmx[a] = std::max(bmx[a], p[v][a]);
+                    }
+            }
+            distblk[2 * b] = make_float4(bmn[0], bmn[1], bmn[2], 0.0f);
+            distblk[2 * b + 1] = make_float4(bmx[0], bmx[1], bmx[2], 0.0f);
+        }
+        s->scene_scale = scale;
+        for (int a = 0; a < 3; a++)
+        {
+            s->vmin[a] = mn[a];
+            s->vmax[a] = mx[a];
+        }
+    }
+    RT_HIP(hipMalloc(&s->d_distblk, sizeof(float4) * std::max<size_t>(1, distblk.size())));
+    RT_HIP(hipMemcpy(s->d_distblk, distblk.data(), sizeof(float4) * distblk.size(), hipMemcpyHostToDevice));
     RT_HIP(hipMalloc(&s->d_trimt, sizeof(float4) * trimt.size()));
     RT_HIP(hipMalloc(&s->d_tridist, sizeof(float4) * tridist.size()));
     RT_HIP(hipMemcpy(s->d_trimt, trimt.data(), sizeof(float4) * trimt.size(), hipMemcpyHostToDevice));
@@ -1197,7 +1366,8 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
         RT_HIP(hipMemcpy(s->d_cellw, cellw.data(), sizeof(uint32_t) * nc, hipMemcpyHostToDevice));
     }
     s->device_bytes = sizeof(uint32_t) * (nc + 1) +
-                      sizeof(float4) * (refs.size() + shade.size() + facen.size() + trimt.size() + tridist.size()) +
+                      sizeof(float4) * (refs.size() + shade.size() + facen.size() + trimt.size() + tridist.size() +
+                                        distblk.size()) +
                       sizeof(uint32_t) * (occ.size() + cellw.size());
     RT_HIP(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
     RT_HIP(hipEventCreate(&s->ev0));
@@ -1221,6 +1391,7 @@ int rt_scene_destroy(rt_scene *s)
         (void)hipFree(s->d_cellw);
         (void)hipFree(s->d_trimt);
         (void)hipFree(s->d_tridist);
+        (void)hipFree(s->d_distblk);
         (void)hipFree(s->d_smp);
         (void)hipFree(s->d_frame);
         if (s->h_smp_pinned) (void)hipHostFree(s->h_smp_pinned);
@@ -1388,6 +1559,7 @@ int rt_trace_samples(rt_scene *s, const rt_frame *f, uint32_t x0, uint32_t y0, u
     frame_params(s, f, P);
     P.recs = d_rec;
     P.rec_x0 = x0; P.rec_y0 = y0; P.rec_w = w; P.rec_h = h;
+    if (P.isect == RT_ISECT_RAY_MARCH && (f->kernel & RT_KERNEL_FLAG_EXHAUSTIVE)) P.isect += 0x100;
     hipLaunchKernelGGL(k_trace_records, dim3((n + kWG - 1) / kWG), dim3(kWG), 0, s->stream, P, n);
     hipError_t e = hipGetLastError();
     if (e == hipSuccess) e = hipMemcpyAsync(out, d_rec, sizeof(rt_sample_rec) * n, hipMemcpyDeviceToHost, s->stream);

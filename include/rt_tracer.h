@@ -98,6 +98,8 @@ enum rt_kernel {
                                             (A/B arm of the min3 form) */
     RT_KERNEL_FLAG_PRE_GATE = 0x4000,   /* OR-able: division-free wave-uniform pre-reject before
                                             the ray/triangle test's 1/det */
+    RT_KERNEL_FLAG_EXHAUSTIVE = 0x8000, /* OR-able, ray march: evaluate every triangle per step
+                                           (no block culling; A/B arm, identical results) */
 };
 
 /* Per-frame parameters: what Renderer::RenderTile reads from the Scene and itself. */

@@ -125,3 +125,36 @@ def test_alt_validation_fails_loudly(scenes):
         gs.render_frame(gs.frame(8, 8, 1, intersector=rtm.RT_ISECT_BRUTE_FORCE, tri_test=rtm.RT_TRI_BARYCENTRIC))
     with pytest.raises(rtm.RtError, match="intersector"):
         gs.render_frame(gs.frame(8, 8, 1, intersector=7))
+
+
+@pytest.mark.parametrize("sid", [0, 4, 8])
+def test_march_block_cull_is_exact(scenes, sid):
+    """The block-culled march (default) and the exhaustive arm: identical frames and records
+    (hit, t, march steps); the cull only skips triangles that cannot lower the minimum."""
+    hs, gs = scenes(sid)
+    for W, H, spp, x0, y0, w, h in ((64, 36, 1, 0, 0, 64, 36), (1920, 1080, 4, 900, 480, 32, 16)):
+        a = gs.frame(W, H, spp, intersector=rtm.RT_ISECT_RAY_MARCH)
+        b = gs.frame(W, H, spp, intersector=rtm.RT_ISECT_RAY_MARCH, kernel=rtm.RT_KERNEL_FLAG_EXHAUSTIVE)
+        if W < 100:
+            np.testing.assert_array_equal(gs.render_frame(a), gs.render_frame(b))
+        ra, rb = gs.trace_samples(a, x0, y0, w, h), gs.trace_samples(b, x0, y0, w, h)
+        np.testing.assert_array_equal(ra["hit"], rb["hit"])
+        np.testing.assert_array_equal(ra["steps"], rb["steps"])
+        np.testing.assert_array_equal(bits(ra["t"]), bits(rb["t"]))
+        assert ra["tests"].sum() <= rb["tests"].sum()
+
+
+def test_march_cull_exact_all_scenes(scenes):
+    """Culled march (block cull + seeded minimum + receding-miss early-out) == exhaustive march
+    (every DistancePointTri of every step, as DistanceBruteForce does) on every scene: frames
+    and per-sample hit / t / step counts (a miss that stopped early reports the 128 steps the
+    reference takes)."""
+    for sid in range(10):
+        hs, gs = scenes(sid)
+        a = gs.frame(160, 90, 1, intersector=rtm.RT_ISECT_RAY_MARCH)
+        b = gs.frame(160, 90, 1, intersector=rtm.RT_ISECT_RAY_MARCH, kernel=rtm.RT_KERNEL_FLAG_EXHAUSTIVE)
+        np.testing.assert_array_equal(gs.render_frame(a), gs.render_frame(b), err_msg=f"scene {sid}")
+        ra, rb = gs.trace_samples(a, 0, 0, 160, 90), gs.trace_samples(b, 0, 0, 160, 90)
+        np.testing.assert_array_equal(ra["hit"], rb["hit"], err_msg=f"scene {sid}")
+        np.testing.assert_array_equal(ra["steps"], rb["steps"], err_msg=f"scene {sid}")
+        np.testing.assert_array_equal(bits(ra["t"]), bits(rb["t"]), err_msg=f"scene {sid}")

@@ -5,6 +5,8 @@ reference loops on a bounded sample.
 
     python tools/alt_bench.py [--reps 5] [--out profiles/r01_alt_bench.json]
 
+The march also runs its exhaustive arm (RT_KERNEL_FLAG_EXHAUSTIVE, no block cull; same
+results): units then count every DistancePointTri the reference evaluates.
 Per config: GPU kernel ms (HIP events on the launch stream, median of reps after a warm-up),
 Msamples/s, work units/s (ray/triangle tests, or point/triangle distances for the march) from
 the kernel's own per-sample counters, and the oracle's Msamples/s on `cpu_rows` rows of the same
@@ -48,10 +50,13 @@ def main():
     cores = max(1, min(cores, int(os.environ.get("OMP_NUM_THREADS", cores))))
     rows = []
     stream = torch.cuda.current_stream()
-    for mode, sid, W, H, spp, cpu_rows in CONFIGS:
+    arms = [(m, s, W, H, spp, cr, 0) for (m, s, W, H, spp, cr) in CONFIGS]
+    arms += [(m, s, W, H, spp, cr, rtm.RT_KERNEL_FLAG_EXHAUSTIVE) for (m, s, W, H, spp, cr) in CONFIGS
+             if m == "march"]
+    for mode, sid, W, H, spp, cpu_rows, kflags in arms:
         hs = rtm.HostScene.load(sid)
         gs = rtm.GpuScene(hs, 0)
-        f = gs.frame(W, H, spp, intersector=isect[mode])
+        f = gs.frame(W, H, spp, intersector=isect[mode], kernel=kflags)
         buf = torch.empty(W * H, dtype=torch.int32, device="cuda")
         gs.render_frame_device(f, buf.data_ptr(), stream.cuda_stream)   # warm-up
         torch.cuda.synchronize()
@@ -69,14 +74,19 @@ def main():
         y0 = (H - band) // 2
         recs = gs.trace_samples(f, 0, y0, W, band)
         units_per_sample = float(recs["tests"].astype(np.float64).mean())
+        nt = int(hs.stats["num_triangles"])
+        # the reference's work: ntris tests per sample, ntris distances per march step
+        ref_units = float(nt if mode == "brute" else recs["steps"].astype(np.float64).mean() * nt)
         samples = W * H * spp
-        row = {"mode": mode, "scene": sid, "W": W, "H": H, "spp": spp, "triangles": int(hs.stats["num_triangles"]),
+        row = {"mode": mode + ("-exhaustive" if kflags else ""), "scene": sid, "W": W, "H": H, "spp": spp, "triangles": int(hs.stats["num_triangles"]),
                "kernel_ms": round(kms, 3), "msamples_per_s": round(samples / kms / 1e3, 2),
                "units_per_sample_midband": round(units_per_sample, 1),
                "gunits_per_s": round(samples * units_per_sample / kms / 1e6, 1),
+               "ref_units_per_sample_midband": round(ref_units, 1),
+               "ref_gunits_per_s": round(samples * ref_units / kms / 1e6, 1),
                "tflops_algorithmic": round(samples * units_per_sample * FLOP[mode] / kms / 1e9, 2)}
         row["fp32_peak_frac"] = round(row["tflops_algorithmic"] / FP32_PEAK_TFLOPS, 3)
-        if oracle is not None:
+        if oracle is not None and not kflags:
             # bounded CPU sample: `cpu_rows` full rows through the oracle's per-sample loop
             t0 = time.perf_counter()
             oracle.records(sid, W, H, spp, 0, H // 2, W, cpu_rows, tri_test=isect[mode] << 8)
