@@ -141,6 +141,30 @@ __device__ __forceinline__ bool ray_tri_mt_gated(float ox, float oy, float oz, f
     return ok1 & !(v < 0.0f || u + v > 1.0f) & (t >= 0.0f);
 }
 
+// ray_tri_mt_gated for rays that share one origin (every primary ray of a frame starts at the
+// camera, camera.h:39): tvec = o - v0 and qvec = tvec x e1 (triangle.h:71, 87) do not depend
+// on the direction, so they come precomputed per frame (k_origin_pre, same operations).  Only
+// the direction-dependent operations remain; results identical to ray_tri_mt_gated.
+__device__ __forceinline__ bool ray_tri_mt_gated_pre(float dx, float dy, float dz,
+                                                     float e1x, float e1y, float e1z,
+                                                     float e2x, float e2y, float e2z,
+                                                     float tx, float ty, float tz,
+                                                     float qx, float qy, float qz,
+                                                     float& t, float& u, float& v)
+{
+    const float px = dy * e2z - dz * e2y;
+    const float py = dz * e2x - dx * e2z;
+    const float pz = dx * e2y - dy * e2x;
+    const float det = e1x * px + e1y * py + e1z * pz;
+    const float inv_det = 1.0f / det;
+    u = (tx * px + ty * py + tz * pz) * inv_det;
+    const bool ok1 = !(det > -0.00000001f && det < 0.00000001f) & !(u < 0.0f || u > 1.0f);
+    if (!__any(ok1)) return false;
+    v = (dx * qx + dy * qy + dz * qz) * inv_det;
+    t = (e2x * qx + e2y * qy + e2z * qz) * inv_det;
+    return ok1 & !(v < 0.0f || u + v > 1.0f) & (t >= 0.0f);
+}
+
 // ray_tri_mt_gated preceded by a division-free wave-uniform pre-gate.  With q = udot/det the
 // reference's u = RN(udot * RN(1/det)); a lane is PROVABLY rejected by triangle.h:77-87 when
 //   det fails the epsilon test, or

@@ -63,6 +63,7 @@ constexpr int kVarPreGate = 32;             // RT_KERNEL_FLAG_PRE_GATE
 constexpr int kVarBrute = 64;               // RT_ISECT_BRUTE_FORCE (renderer.cpp:157-197)
 constexpr int kVarMarch = 128;              // RT_ISECT_RAY_MARCH (renderer.cpp:24-41, 138-155)
 constexpr int kVarExhaustive = 256;         // RT_KERNEL_FLAG_EXHAUSTIVE: march without block culling
+constexpr int kVarOriginPre = 512;          // RT_KERNEL_FLAG_ORIGIN_PRE: per-frame o - v0, (o - v0) x e1
 constexpr uint32_t kMarchSteps = 128;       // renderer.cpp:26
 constexpr uint32_t kDistBlock = 32;         // triangles per culling block of the distance kernels
 
@@ -85,6 +86,7 @@ struct KParams
     const uint32_t *off;
     const uint32_t *cellw;      // packed cell ranges (start << 11 | count) or null
     const float4 *refs;
+    const float4 *frefs;        // per frame (kVarOriginPre): {e1, e2.x}{e2.yz, tvec.xy}{tvec.z, qvec}
     const float4 *shade;
     const float4 *face_n;
     const uint32_t *occ;
@@ -168,15 +170,23 @@ __device__ __forceinline__ bool test_cell(const KParams& P, float ox, float oy, 
         }
         else
         {
-            const float4 *rp = P.refs + size_t(k) * 3;   // one address, immediate offsets
+            const float4 *rp = ((VAR & kVarOriginPre) && TRI == RT_TRI_MOLLER_TRUMBORE ? P.frefs : P.refs) +
+                               size_t(k) * 3;              // one address, immediate offsets
             r0 = rp[0];
             r1 = rp[1];
             r2 = rp[2];
         }
-        const uint32_t id = __float_as_uint(r2.y);
         float ct, cu, cv;
         bool hit;
-        if (TRI == RT_TRI_BARYCENTRIC)
+        uint32_t id = __float_as_uint(r2.y);
+        if ((VAR & kVarOriginPre) && TRI == RT_TRI_MOLLER_TRUMBORE)
+        {
+            // r0..r2 = the frame record; the triangle id is resolved from refs after the walk
+            id = k;
+            hit = rtd::ray_tri_mt_gated_pre(dx, dy, dz, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x,
+                                            r2.y, r2.z, r2.w, ct, cu, cv);
+        }
+        else if (TRI == RT_TRI_BARYCENTRIC)
         {
             const float4 fn = P.face_n[id];
             hit = rtd::ray_tri_bary_pred(ox, oy, oz, dx, dy, dz, r0.x, r0.y, r0.z, r0.w, r1.x,
@@ -532,8 +542,12 @@ __device__ __forceinline__ void trace_sample(const KParams& P, const uint32_t *l
     else if constexpr ((VAR & kVarBrute) != 0)
         hit = brute_intersect<STATS>(P, P.org[0], P.org[1], P.org[2], dx, dy, dz, t, u, v, tri, tests);
     else
+    {
         hit = grid_intersect<STATS, TRI, VAR>(P, lds_occ, P.org[0], P.org[1], P.org[2], dx, dy, dz, t, u, v, tri,
                                               voxel, steps, tests);
+        if ((VAR & kVarOriginPre) && TRI == RT_TRI_MOLLER_TRUMBORE && hit)
+            tri = __float_as_uint(P.refs[3 * size_t(tri) + 2].y);     // CSR reference -> triangle id
+    }
     if constexpr ((VAR & kVarMarch) != 0)
     {
         // The reference's RayMarch leaves u, v, tri_idx unset (renderer.cpp:103), so the
@@ -736,6 +750,24 @@ __global__ void __launch_bounds__(kWG) k_unshard(const uint32_t *g, uint32_t *ou
     out[size_t(y) * W + x] = g[r * shard_elems + size_t(k) * kTilePix + (y % kTile) * kTile + (x % kTile)];
 }
 
+// Per-frame records of the origin-shared Moller-Trumbore terms (kVarOriginPre): for CSR
+// reference k, tvec = o - v0 and qvec = tvec x e1 exactly as triangle.h:71, 87 compute them.
+__global__ void __launch_bounds__(kWG) k_origin_pre(const float4 *refs, float4 *frefs, uint32_t n, float ox,
+                                                    float oy, float oz)
+{
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const float4 r0 = refs[3 * size_t(k)], r1 = refs[3 * size_t(k) + 1], r2 = refs[3 * size_t(k) + 2];
+    const float e1x = r0.w, e1y = r1.x, e1z = r1.y;
+    const float tx = ox - r0.x, ty = oy - r0.y, tz = oz - r0.z;
+    const float qx = ty * e1z - tz * e1y;
+    const float qy = tz * e1x - tx * e1z;
+    const float qz = tx * e1y - ty * e1x;
+    frefs[3 * size_t(k) + 0] = make_float4(e1x, e1y, e1z, r1.z);
+    frefs[3 * size_t(k) + 1] = make_float4(r1.w, r2.x, tx, ty);
+    frefs[3 * size_t(k) + 2] = make_float4(tz, qx, qy, qz);
+}
+
 // Device KATs (rt_debug_primitives)
 __global__ void __launch_bounds__(kWG) k_primitives(int kind, const float *in, uint32_t n, float *out)
 {
@@ -897,7 +929,7 @@ struct rt_scene
     float bmin[3], bmax[3], cw = 0, icw = 0;
     uint32_t ncells = 0, nrefs = 0, ntris = 0, occ_words = 0;
     uint32_t *d_off = nullptr, *d_occ = nullptr, *d_cellw = nullptr;
-    float4 *d_refs = nullptr, *d_shade = nullptr, *d_facen = nullptr;
+    float4 *d_refs = nullptr, *d_shade = nullptr, *d_facen = nullptr, *d_frefs = nullptr;
     float4 *d_trimt = nullptr, *d_tridist = nullptr, *d_distblk = nullptr;
     uint32_t ndist_blk = 0;
     float scene_scale = 0.0f;
@@ -913,6 +945,7 @@ struct rt_scene
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool ev_recorded = false;
+    hipStream_t last_stream = nullptr;  // stream of the last launch (cross-stream ordering)
     // staging for rt_render_tiles / records
     uint32_t *d_frame = nullptr;
     size_t frame_cap = 0;
@@ -968,7 +1001,7 @@ int validate_frame(const rt_frame *f)
     if ((f->kernel & 0xFFu) > RT_KERNEL_PERSISTENT ||
         (f->kernel & ~(0xFFu | RT_KERNEL_FLAG_PREFETCH | RT_KERNEL_FLAG_WAVE_GATE | RT_KERNEL_FLAG_LOOKAHEAD |
                        RT_KERNEL_FLAG_CSR_OFFSETS | RT_KERNEL_FLAG_DIST_SKIP | RT_KERNEL_FLAG_NESTED_STEP |
-                       RT_KERNEL_FLAG_PRE_GATE | RT_KERNEL_FLAG_EXHAUSTIVE)))
+                       RT_KERNEL_FLAG_PRE_GATE | RT_KERNEL_FLAG_EXHAUSTIVE | RT_KERNEL_FLAG_ORIGIN_PRE)))
         return fail(RT_E_INVALID, "unknown kernel");
     const uint32_t spp = std::max(1u, f->spp);
     if (spp > 4096) return fail(RT_E_INVALID, "spp must be <= 4096");
@@ -1010,6 +1043,7 @@ void frame_params(const rt_scene *s, const rt_frame *f, KParams& P)
     P.off = s->d_off;
     P.cellw = (f->kernel & RT_KERNEL_FLAG_CSR_OFFSETS) ? nullptr : s->d_cellw;
     P.refs = s->d_refs;
+    P.frefs = s->d_frefs;
     P.shade = s->d_shade;
     P.face_n = s->d_facen;
     P.occ = s->d_occ;
@@ -1043,19 +1077,29 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
     if (P.wg_per_tile == 0) P.wg_per_tile = 1;
     const uint64_t blocks = uint64_t(n_local_tiles) * P.wg_per_tile;
     if (blocks > 0x3FFFFFFFull) return fail(RT_E_INVALID, "frame too large for one launch");
+    // The per-frame records (frefs) are scene state: a launch on another stream than the last
+    // one waits for it, so frames of one scene never overlap on the device.
+    if (s->ev_recorded && st != s->last_stream) RT_HIP(hipStreamWaitEvent(st, s->ev1, 0));
+    s->last_stream = st;
     RT_HIP(hipEventRecord(s->ev0, st));
     const uint32_t kind = f->kernel & 0xFFu;
-    // RT_KERNEL_AUTO = lanes + wave gate + distance skip: fastest arm of tools/ab_kernels.py on
-    // MI355X (scenes 1/4/5/8, 1080p x 4spp).
+    // RT_KERNEL_AUTO = lanes + wave gate + distance skip + per-frame origin terms: fastest arm of
+    // tools/ab_kernels.py on MI355X (scenes 1/4/5/8, 1080p x 4spp).
     const uint32_t fk = kind == RT_KERNEL_AUTO
-                            ? (f->kernel | RT_KERNEL_LANES | RT_KERNEL_FLAG_WAVE_GATE | RT_KERNEL_FLAG_DIST_SKIP)
+                            ? (f->kernel | RT_KERNEL_LANES | RT_KERNEL_FLAG_WAVE_GATE | RT_KERNEL_FLAG_DIST_SKIP |
+                               RT_KERNEL_FLAG_ORIGIN_PRE)
                             : f->kernel;
+    if ((fk & RT_KERNEL_FLAG_ORIGIN_PRE) && lanes && P.isect == RT_ISECT_GRID &&
+        P.tri_test == RT_TRI_MOLLER_TRUMBORE && s->nrefs)
+        hipLaunchKernelGGL(k_origin_pre, dim3((s->nrefs + kWG - 1) / kWG), dim3(kWG), 0, st, s->d_refs, s->d_frefs,
+                           s->nrefs, P.org[0], P.org[1], P.org[2]);
     const int var = ((fk & RT_KERNEL_FLAG_PREFETCH) ? kVarPrefetch : 0) |
                     ((fk & RT_KERNEL_FLAG_WAVE_GATE) ? kVarWaveGate : 0) |
                     ((fk & RT_KERNEL_FLAG_LOOKAHEAD) ? kVarLookahead : 0) |
                     ((fk & RT_KERNEL_FLAG_DIST_SKIP) ? kVarDistSkip : 0) |
                     ((fk & RT_KERNEL_FLAG_NESTED_STEP) ? kVarNestedStep : 0) |
-                    ((fk & RT_KERNEL_FLAG_PRE_GATE) ? kVarPreGate : 0);
+                    ((fk & RT_KERNEL_FLAG_PRE_GATE) ? kVarPreGate : 0) |
+                    ((fk & RT_KERNEL_FLAG_ORIGIN_PRE) ? kVarOriginPre : 0);
     const bool bary = P.tri_test == RT_TRI_BARYCENTRIC;
     const dim3 wg(kWG);
     if (lanes && kind == RT_KERNEL_PERSISTENT && P.occ_words && P.isect == RT_ISECT_GRID)
@@ -1096,6 +1140,7 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
         else if (var == 18) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 18>), grid, wg, 0, st, P);
         else if (var == 40) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 40>), grid, wg, 0, st, P);
         else if (var == 42) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 42>), grid, wg, 0, st, P);
+        else if (var == 522) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 522>), grid, wg, 0, st, P);
         else                hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 0>), grid, wg, 0, st, P);
     }
     else if (P.isect == RT_ISECT_RAY_MARCH && (f->kernel & RT_KERNEL_FLAG_EXHAUSTIVE))
@@ -1287,6 +1332,7 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
 
     RT_HIP(hipMalloc(&s->d_off, sizeof(uint32_t) * (nc + 1)));
     RT_HIP(hipMalloc(&s->d_refs, sizeof(float4) * refs.size()));
+    RT_HIP(hipMalloc(&s->d_frefs, sizeof(float4) * refs.size()));
     RT_HIP(hipMalloc(&s->d_shade, sizeof(float4) * shade.size()));
     RT_HIP(hipMalloc(&s->d_facen, sizeof(float4) * facen.size()));
     RT_HIP(hipMalloc(&s->d_occ, sizeof(uint32_t) * occ.size()));
@@ -1366,7 +1412,7 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
         RT_HIP(hipMemcpy(s->d_cellw, cellw.data(), sizeof(uint32_t) * nc, hipMemcpyHostToDevice));
     }
     s->device_bytes = sizeof(uint32_t) * (nc + 1) +
-                      sizeof(float4) * (refs.size() + shade.size() + facen.size() + trimt.size() + tridist.size() +
+                      sizeof(float4) * (2 * refs.size() + shade.size() + facen.size() + trimt.size() + tridist.size() +
                                         distblk.size()) +
                       sizeof(uint32_t) * (occ.size() + cellw.size());
     RT_HIP(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
@@ -1385,6 +1431,7 @@ int rt_scene_destroy(rt_scene *s)
         if (s->stream) (void)hipStreamSynchronize(s->stream);
         (void)hipFree(s->d_off);
         (void)hipFree(s->d_refs);
+        (void)hipFree(s->d_frefs);
         (void)hipFree(s->d_shade);
         (void)hipFree(s->d_facen);
         (void)hipFree(s->d_occ);

@@ -100,6 +100,9 @@ enum rt_kernel {
                                             the ray/triangle test's 1/det */
     RT_KERNEL_FLAG_EXHAUSTIVE = 0x8000, /* OR-able, ray march: evaluate every triangle per step
                                            (no block culling; A/B arm, identical results) */
+    RT_KERNEL_FLAG_ORIGIN_PRE = 0x10000, /* OR-able (grid, Moller-Trumbore, with WAVE_GATE +
+                                            DIST_SKIP): per-frame precompute of the origin-only
+                                            terms o - v0, (o - v0) x e1 of every reference */
 };
 
 /* Per-frame parameters: what Renderer::RenderTile reads from the Scene and itself. */

@@ -16,19 +16,23 @@ import pytest
 from conftest import PKG_DIR
 
 SRC = os.path.join(PKG_DIR, "csrc", "rt_tracer.hip")
+GRID_SRC = os.path.join(PKG_DIR, "csrc", "rt_grid_build.hip")
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize",
          "--cuda-device-only"]
 pytestmark = pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
 
 
-def test_device_ir_has_no_contraction_or_fast_math(tmp_path):
+@pytest.mark.parametrize("src", [SRC, GRID_SRC], ids=["tracer", "grid_build"])
+def test_device_ir_has_no_contraction_or_fast_math(tmp_path, src):
+    """Covers the fp64 tri/box SAT of the grid build too (aabb_tri_internal.h is exact only
+    without contraction)."""
     ll = tmp_path / "rt.ll"
-    subprocess.run([HIPCC] + FLAGS + ["-emit-llvm", "-S", "-o", str(ll), SRC], check=True,
+    subprocess.run([HIPCC] + FLAGS + ["-emit-llvm", "-S", "-o", str(ll), src], check=True,
                    capture_output=True)
     ir = ll.read_text()
     assert "fmuladd" not in ir
-    assert not re.search(r"\bllvm\.fma\.f32\b", ir)
+    assert not re.search(r"\bllvm\.fma\.f(32|64)\b", ir)
     for flag in (" contract ", " afn ", " arcp ", " nnan ", " ninf ", " nsz ", " reassoc ", " fast "):
         assert flag not in ir, flag
     assert "denormal-fp-math-f32" not in ir or '"denormal-fp-math-f32"="ieee' in ir
@@ -47,6 +51,8 @@ def test_render_kernels_do_not_spill(tmp_path):
     assert lanes, table
     for n, (sc, vg) in lanes.items():
         assert sc == 0, f"{n} spills {sc} B/lane"
-    # the default kernel (lanes + wave gate, Moller-Trumbore) keeps 8 waves/SIMD
-    default = [v for n, v in lanes.items() if "ILi0ELi2E" in n]
-    assert default and default[0][1] <= 64, default
+    # the AUTO kernel (lanes + wave gate + distance skip + origin terms, Moller-Trumbore) and
+    # its no-precompute arm keep 8 waves/SIMD
+    for key in ("ILi0ELi522E", "ILi0ELi10E"):
+        arm = [v for n, v in lanes.items() if key in n]
+        assert arm and arm[0][1] <= 64, (key, arm)
