@@ -35,6 +35,7 @@ RT_KERNEL_FLAG_NESTED_STEP = 0x2000
 RT_KERNEL_FLAG_PRE_GATE = 0x4000
 RT_KERNEL_FLAG_EXHAUSTIVE = 0x8000
 RT_KERNEL_FLAG_ORIGIN_PRE = 0x10000
+RT_KERNEL_COMPACT_REFILL_SHIFT = 24      # RT_KERNEL_COMPACT: idle lanes before a refill (1..64)
 RT_ISECT_GRID = 0
 RT_ISECT_BRUTE_FORCE = 1
 RT_ISECT_RAY_MARCH = 2

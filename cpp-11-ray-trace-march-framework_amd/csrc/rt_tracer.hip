@@ -252,14 +252,13 @@ __device__ __forceinline__ bool test_cell(const KParams& P, float ox, float oy, 
         cell += a2_ ? cs2 : (a1_ ? cs1 : cs0);                                                 \
     } while (0)
 
-// grid.cpp:159-281 Grid::Intersect (NEW_GRID_TRAVERSAL), axis arrays unrolled into scalars
-// so nothing is runtime-indexed (no scratch).  Counters are compiled in only for records.
-template <bool STATS, int TRI, int VAR>
-__device__ __forceinline__ bool grid_intersect(const KParams& P, const uint32_t *lds_occ,
-                                               float ox, float oy, float oz,
-                                               float dx, float dy, float dz,
-                                               float& t, float& u, float& v, uint32_t& tri,
-                                               uint32_t& voxel, uint32_t& steps, uint32_t& tests)
+// Grid entry + per-axis DDA setup of Grid::Intersect (aabb.h:9-83, grid.h:44-51,
+// grid.cpp:167-216), axis arrays unrolled into scalars.  Instead of pos/step/out per axis the
+// walk keeps the cells left before 'pos == out' (rem) and the signed GridIdx stride of a step
+// (cs): grid.cpp:274-277 exits after the same steps.  False when the ray misses the grid.
+__device__ __forceinline__ bool dda_setup(const KParams& P, float ox, float oy, float oz, float dx, float dy, float dz,
+                                          float& nct0, float& nct1, float& nct2, float& dt0, float& dt1, float& dt2,
+                                          int& rem0, int& rem1, int& rem2, int& cs0, int& cs1, int& cs2, int& cell)
 {
     float enter_t, leave_t, gx, gy, gz;
     if (rtd::point_in_aabb(ox, oy, oz, P.bmin, P.bmax))
@@ -276,17 +275,15 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, const uint32_t 
     else
         return false;
 
-    // grid.h:44-48 ToVoxel, grid.h:50-51 ToPos, grid.cpp:190-216 per-axis setup.  Instead of
-    // pos/step/out per axis the walk keeps the cells left before 'pos == out' (rem) and the
-    // signed GridIdx stride of a step (cs): grid.cpp:274-277 exits after the same steps.
+    // grid.h:44-48 ToVoxel, grid.h:50-51 ToPos, grid.cpp:190-216 per-axis setup
     auto to_voxel = [&](float g, int a) {
         const int vx = rtd::cvt_i32_x86((g - P.bmin[a]) * P.icw);
         const int hi = P.dim[a] - 1;
         return vx < 0 ? 0 : (vx > hi ? hi : vx);
     };
     const int pos0 = to_voxel(gx, 0), pos1 = to_voxel(gy, 1), pos2 = to_voxel(gz, 2);
-    float nct0, nct1, nct2, dt0 = 0.0f, dt1 = 0.0f, dt2 = 0.0f;
-    int rem0 = 0, rem1 = 0, rem2 = 0, cs0 = 0, cs1 = 0, cs2 = 0;
+    dt0 = dt1 = dt2 = 0.0f;
+    rem0 = rem1 = rem2 = cs0 = cs1 = cs2 = 0;
     auto setup = [&](float d, float g, int pos, int a, int stride, float& nct, float& dtv, int& rem, int& cs) {
         if (d == 0.0f)
             nct = rtd::kFltMax;
@@ -308,7 +305,24 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, const uint32_t 
     setup(dx, gx, pos0, 0, 1, nct0, dt0, rem0, cs0);
     setup(dy, gy, pos1, 1, P.dxdz, nct1, dt1, rem1, cs1);
     setup(dz, gz, pos2, 2, P.dim[0], nct2, dt2, rem2, cs2);
-    int cell = pos0 + pos2 * P.dim[0] + pos1 * P.dxdz;
+    cell = pos0 + pos2 * P.dim[0] + pos1 * P.dxdz;
+    return true;
+}
+
+// grid.cpp:159-281 Grid::Intersect (NEW_GRID_TRAVERSAL), axis arrays unrolled into scalars
+// so nothing is runtime-indexed (no scratch).  Counters are compiled in only for records.
+template <bool STATS, int TRI, int VAR>
+__device__ __forceinline__ bool grid_intersect(const KParams& P, const uint32_t *lds_occ,
+                                               float ox, float oy, float oz,
+                                               float dx, float dy, float dz,
+                                               float& t, float& u, float& v, uint32_t& tri,
+                                               uint32_t& voxel, uint32_t& steps, uint32_t& tests)
+{
+    float nct0, nct1, nct2, dt0, dt1, dt2;
+    int rem0, rem1, rem2, cs0, cs1, cs2, cell;
+    if (!dda_setup(P, ox, oy, oz, dx, dy, dz, nct0, nct1, nct2, dt0, dt1, dt2, rem0, rem1, rem2, cs0, cs1, cs2,
+                   cell))
+        return false;
     t = rtd::kFltMax;
 
     if (VAR & kVarLookahead)
@@ -692,6 +706,231 @@ __global__ void __launch_bounds__(kPersistWG, 8) k_render_persistent(KParams P, 
         process_item<TRI, VAR>(P, lds_occ, item);
 }
 
+// RT_KERNEL_COMPACT (grid intersector, spp a power of two <= 64): wavefront active-ray
+// compaction.  In the LANES kernel a wave lives until its slowest ray ends, so lanes whose ray
+// already hit (or left the grid) idle through the rest of the walk (~23 % of lane-cycles on
+// the bench frames).  Here persistent waves keep 64 rays in flight: each iteration walks the
+// active lanes cell by cell until `refill` of them have finished, stores the finished samples'
+// colours in LDS, and hands the idle lanes fresh samples from the wave's work items with a
+// ballot + prefix count (mbcnt) -- the lanes of one refill take consecutive samples, so new
+// rays stay spatially coherent.  Items (64 sample slots, as in LANES) are dealt to the waves
+// round-robin; a wave holds up to kCompactSlots items whose per-sample colours wait in LDS until
+// all 64 are stored, then the pixel sums run over LDS in sample order from 0.0f (hazard H10),
+// bit-identical to the shuffle sums of process_item.
+constexpr uint32_t kCompactSlots = 4;            // work items in flight per wave
+constexpr uint32_t kCompactRefill = 48;          // default: refill when this many lanes idle
+
+struct CompactLds
+{
+    float col[kWG / 64u][kCompactSlots][3][64];  // per-sample colours until the item resolves
+    uint32_t left[kWG / 64u][kCompactSlots];     // samples of the slot's item not yet stored
+    uint32_t item[kWG / 64u][kCompactSlots];     // work item held by the slot
+};
+
+// Orders this wave's LDS writes before its later LDS reads of other lanes' data (a wave
+// executes its LDS operations in order; this keeps the compiler from reordering them).
+__device__ __forceinline__ void wave_lds_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+template <int TRI, int VAR>
+__global__ void __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(8, 8)))
+k_render_compact(KParams P, uint32_t n_items, uint32_t refill)
+{
+    __shared__ CompactLds L;
+    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const float ox = P.org[0], oy = P.org[1], oz = P.org[2];
+    if (lane < kCompactSlots) L.left[wv][lane] = 0u;
+    // wave-uniform bookkeeping
+    uint32_t busy = 0u;                          // slots holding an item
+    uint32_t feed_slot = 0u, feed_next = 64u;    // next sample slot to hand out (64: none)
+    bool drained = false;                        // the global item counter ran out
+    // Items are dealt statically, wave w taking w, w + nwaves, ...: neighbouring items cost
+    // alike, so the interleave balances, and a global atomic counter measured 2-4x slower
+    // (one device-scope atomic per item serialises at the memory side).
+    const uint32_t nwaves = gridDim.x * (kWG / 64u);
+    uint32_t next_item = blockIdx.x * (kWG / 64u) + wv;
+    const uint32_t walk_min = 64u - refill;
+    // lane state: 0 idle, 1 walking, 2 finished (colour not yet stored)
+    uint32_t state = 0u, tag = 0u, iter = 0u;
+    float dx = 0.0f, dy = 0.0f, dz = 0.0f, t = 0.0f, u = 0.0f, v = 0.0f;
+    uint32_t tri = 0u;
+    bool hit = false;
+    float nct0 = 0.0f, nct1 = 0.0f, nct2 = 0.0f, dt0 = 0.0f, dt1 = 0.0f, dt2 = 0.0f;
+    int rem0 = 0, rem1 = 0, rem2 = 0, cs0 = 0, cs1 = 0, cs2 = 0, cell = 0, skip = 0;
+    for (;;)
+    {
+        // (1) store the colours of finished samples (renderer.cpp:147-159)
+        if (state == 2u)
+        {
+            const uint32_t slot = tag >> 6, j = tag & 63u;
+            const ItemCoord ic = item_coord(P, L.item[wv][slot], j);
+            float cr = 0.0f, cg = 0.0f, cb = 0.0f;
+            if (ic.valid)
+            {
+                if (hit)
+                {
+                    if ((VAR & kVarOriginPre) && TRI == RT_TRI_MOLLER_TRUMBORE)
+                        tri = __float_as_uint(P.refs[3 * size_t(tri) + 2].y);   // CSR ref -> triangle id
+                    const float4 a = P.shade[3 * tri + 0], b = P.shade[3 * tri + 1], c = P.shade[3 * tri + 2];
+                    rtd::shade_hit(u, v, a, b, c, cr, cg, cb);
+                }
+                else
+                    cr = cg = cb = float(ic.y) / float(P.H);                    // renderer.cpp:159
+            }
+            L.col[wv][slot][0][j] = cr;
+            L.col[wv][slot][1][j] = cg;
+            L.col[wv][slot][2][j] = cb;
+            __hip_atomic_fetch_sub(&L.left[wv][slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            state = 0u;
+        }
+        wave_lds_sync();
+        // (2) resolve items whose 64 samples are all stored (renderer.cpp:162-171)
+        uint64_t ready = __ballot(lane < kCompactSlots && ((busy >> lane) & 1u) &&
+                                  __hip_atomic_load(&L.left[wv][lane < kCompactSlots ? lane : 0u], __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_WORKGROUP) == 0u);
+        while (ready)
+        {
+            const uint32_t r = uint32_t(__builtin_ctzll(ready));
+            ready &= ready - 1u;
+            busy &= ~(1u << r);
+            const uint32_t item = __builtin_amdgcn_readfirstlane(L.item[wv][r]);
+            const ItemCoord ic = item_coord(P, item, lane);
+            const uint32_t base = lane & ~(P.spp - 1u);
+            float sr = 0.0f, sg = 0.0f, sb = 0.0f;
+            for (uint32_t k = 0; k < P.spp; k++)
+            {
+                sr += L.col[wv][r][0][base + k];
+                sg += L.col[wv][r][1][base + k];
+                sb += L.col[wv][r][2][base + k];
+            }
+            if (ic.valid && ic.s == 0)
+            {
+                const uint32_t word = rtd::pack_bgra8(rtd::gamma_half(average(P, sr)),
+                                                      rtd::gamma_half(average(P, sg)),
+                                                      rtd::gamma_half(average(P, sb)));
+                store_pixel(P, ic.c, ic.p, ic.x, ic.y, word);
+            }
+        }
+        // (3) refill: idle lanes take the next sample slots in lane order (ballot + mbcnt)
+        const uint64_t idle = __ballot(state == 0u);
+        const uint32_t n_idle = uint32_t(__popcll(idle));
+        if (!drained && n_idle >= refill)
+        {
+            const uint32_t rank = uint32_t(__builtin_amdgcn_mbcnt_hi(uint32_t(idle >> 32),
+                                                                     __builtin_amdgcn_mbcnt_lo(uint32_t(idle), 0u)));
+            const uint32_t avail = 64u - feed_next;
+            uint32_t new_slot = kCompactSlots;
+            if (n_idle > avail && busy != (1u << kCompactSlots) - 1u)
+            {
+                const uint32_t item = next_item;
+                next_item += nwaves;
+                if (item >= n_items)
+                    drained = true;
+                else
+                {
+                    new_slot = uint32_t(__builtin_ctz(~busy));
+                    busy |= 1u << new_slot;
+                    if (lane == 0u)
+                    {
+                        L.item[wv][new_slot] = item;
+                        L.left[wv][new_slot] = 64u;
+                    }
+                }
+            }
+            wave_lds_sync();
+            if (state == 0u)
+            {
+                bool take = false;
+                uint32_t slot = 0u, j = 0u;
+                if (rank < avail)
+                {
+                    take = true;
+                    slot = feed_slot;
+                    j = feed_next + rank;
+                }
+                else if (new_slot < kCompactSlots)
+                {
+                    take = true;
+                    slot = new_slot;
+                    j = rank - avail;
+                }
+                if (take)
+                {
+                    tag = (slot << 6) | j;
+                    state = 2u;
+                    hit = false;
+                    const ItemCoord ic = item_coord(P, L.item[wv][slot], j);
+                    if (ic.valid)
+                    {
+                        const float2 so = P.smp[ic.s];
+                        rtd::gen_dir(P.m, P.fov_xs, P.aspect, ic.x, ic.y, P.W, P.H, so.x, so.y, dx, dy, dz);
+                        if (dda_setup(P, ox, oy, oz, dx, dy, dz, nct0, nct1, nct2, dt0, dt1, dt2, rem0, rem1, rem2,
+                                      cs0, cs1, cs2, cell))
+                        {
+                            state = 1u;
+                            t = rtd::kFltMax;
+                            iter = 0u;
+                            skip = 0;
+                        }
+                    }
+                }
+            }
+            if (new_slot < kCompactSlots)
+            {
+                feed_slot = new_slot;
+                feed_next = n_idle - avail;
+            }
+            else
+                feed_next += avail < n_idle ? avail : n_idle;
+        }
+        // Nothing in flight: after a refill attempt this means the counter is drained and every
+        // held item has been resolved (an item is resolved in the iteration its last sample is
+        // stored), so the wave is done.
+        if (__ballot(state != 0u) == 0u) break;
+        // (4) walk the active lanes until `refill` of them have finished (all, once drained)
+        const uint32_t wmin = drained ? 0u : walk_min;
+        do
+        {
+            if (state == 1u)
+            {
+                iter++;
+                uint32_t kb = 0u, ke = 0u;
+                if ((VAR & kVarDistSkip) && P.cellw)
+                {
+                    if (skip == 0)
+                    {
+                        const uint32_t cw = P.cellw[uint32_t(cell)];
+                        const uint32_t cnt = cw & 2047u;
+                        kb = cw >> 11;
+                        ke = kb + cnt;
+                        skip = cnt ? 0 : int(kb) - 1;
+                    }
+                    else
+                        skip--;
+                }
+                else
+                    cell_range(P, uint32_t(cell), kb, ke);
+                float nct_ax;
+                bool more;
+                RT_DDA_ADVANCE(nct_ax, more);
+                uint32_t tests = 0u;
+                if (kb < ke &&
+                    test_cell<false, TRI, VAR>(P, ox, oy, oz, dx, dy, dz, kb, ke, nct_ax, t, u, v, tri, tests))
+                {
+                    state = 2u;
+                    hit = true;
+                }
+                else if (!more || iter >= P.max_steps)
+                    state = 2u;
+            }
+        } while (uint32_t(__popcll(__ballot(state == 1u))) > wmin);
+    }
+}
+
 // RT_KERNEL_PIXEL_LOOP: one lane per pixel, samples looped in order (any spp)
 template <int TRI, int VAR>
 __global__ void __launch_bounds__(kWG) k_render_pixel_loop(KParams P)
@@ -936,6 +1175,7 @@ struct rt_scene
     float vmin[3] = { 0, 0, 0 }, vmax[3] = { 0, 0, 0 };
     uint64_t device_bytes = 0;
     uint32_t persist_wgs = 1024;    // persistent grid: 4 x 512-lane workgroups per CU
+    uint32_t compact_wgs = 2048;    // RT_KERNEL_COMPACT grid: 8 x 256-lane workgroups per CU
     // sample table cache
     float2 *d_smp = nullptr;
     uint32_t smp_cap = 0;
@@ -1001,11 +1241,15 @@ int validate_frame(const rt_frame *f)
     if ((f->kernel & 0xFFu) > RT_KERNEL_PERSISTENT ||
         (f->kernel & ~(0xFFu | RT_KERNEL_FLAG_PREFETCH | RT_KERNEL_FLAG_WAVE_GATE | RT_KERNEL_FLAG_LOOKAHEAD |
                        RT_KERNEL_FLAG_CSR_OFFSETS | RT_KERNEL_FLAG_DIST_SKIP | RT_KERNEL_FLAG_NESTED_STEP |
-                       RT_KERNEL_FLAG_PRE_GATE | RT_KERNEL_FLAG_EXHAUSTIVE | RT_KERNEL_FLAG_ORIGIN_PRE)))
+                       RT_KERNEL_FLAG_PRE_GATE | RT_KERNEL_FLAG_EXHAUSTIVE | RT_KERNEL_FLAG_ORIGIN_PRE |
+                       RT_KERNEL_COMPACT_REFILL_MASK)))
         return fail(RT_E_INVALID, "unknown kernel");
     const uint32_t spp = std::max(1u, f->spp);
     if (spp > 4096) return fail(RT_E_INVALID, "spp must be <= 4096");
-    if (((f->kernel & 0xFFu) == RT_KERNEL_LANES || (f->kernel & 0xFFu) == RT_KERNEL_PERSISTENT) &&
+    if (((f->kernel & RT_KERNEL_COMPACT_REFILL_MASK) >> RT_KERNEL_COMPACT_REFILL_SHIFT) > 64u)
+        return fail(RT_E_INVALID, "compaction refill threshold must be <= 64 lanes");
+    if (((f->kernel & 0xFFu) == RT_KERNEL_LANES || (f->kernel & 0xFFu) == RT_KERNEL_PERSISTENT ||
+         (f->kernel & 0xFFu) == RT_KERNEL_COMPACT) &&
         !(is_pow2(spp) && spp <= 64))
         return fail(RT_E_INVALID, "RT_KERNEL_LANES needs spp to be a power of two <= 64");
     return RT_OK;
@@ -1085,7 +1329,8 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
     const uint32_t kind = f->kernel & 0xFFu;
     // RT_KERNEL_AUTO = lanes + wave gate + distance skip + per-frame origin terms: fastest arm of
     // tools/ab_kernels.py on MI355X (scenes 1/4/5/8, 1080p x 4spp).
-    const uint32_t fk = kind == RT_KERNEL_AUTO
+    // RT_KERNEL_COMPACT runs the same per-ray code as AUTO (its A/B baseline).
+    const uint32_t fk = (kind == RT_KERNEL_AUTO || kind == RT_KERNEL_COMPACT)
                             ? (f->kernel | RT_KERNEL_LANES | RT_KERNEL_FLAG_WAVE_GATE | RT_KERNEL_FLAG_DIST_SKIP |
                                RT_KERNEL_FLAG_ORIGIN_PRE)
                             : f->kernel;
@@ -1102,7 +1347,20 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
                     ((fk & RT_KERNEL_FLAG_ORIGIN_PRE) ? kVarOriginPre : 0);
     const bool bary = P.tri_test == RT_TRI_BARYCENTRIC;
     const dim3 wg(kWG);
-    if (lanes && kind == RT_KERNEL_PERSISTENT && P.occ_words && P.isect == RT_ISECT_GRID)
+    if (lanes && kind == RT_KERNEL_COMPACT && P.isect == RT_ISECT_GRID)
+    {
+        const uint32_t n_items = uint32_t(blocks * (kWG / 64u));
+        uint32_t refill = (f->kernel & RT_KERNEL_COMPACT_REFILL_MASK) >> RT_KERNEL_COMPACT_REFILL_SHIFT;
+        if (refill == 0u) refill = kCompactRefill;
+        const dim3 grid(std::max(1u, std::min(s->compact_wgs, (n_items + 3u) / 4u)));
+        if (bary)
+            hipLaunchKernelGGL((k_render_compact<RT_TRI_BARYCENTRIC, kVarDistSkip>), grid, wg, 0, st, P, n_items,
+                               refill);
+        else
+            hipLaunchKernelGGL((k_render_compact<RT_TRI_MOLLER_TRUMBORE, kVarWaveGate | kVarDistSkip | kVarOriginPre>),
+                               grid, wg, 0, st, P, n_items, refill);
+    }
+    else if (lanes && kind == RT_KERNEL_PERSISTENT && P.occ_words && P.isect == RT_ISECT_GRID)
     {
         const uint32_t n_items = uint32_t(blocks * (kWG / 64u));
         const uint32_t per_wg = kPersistWG / 64u;
@@ -1237,6 +1495,7 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
     std::unique_ptr<rt_scene> s(new rt_scene());
     s->device = device;
     s->persist_wgs = 4u * uint32_t(std::max(1, ncus));
+    s->compact_wgs = 8u * uint32_t(std::max(1, ncus));
     for (int a = 0; a < 3; a++)
     {
         s->dims[a] = g.dims[a];

@@ -85,7 +85,9 @@ enum rt_kernel {
     RT_KERNEL_AUTO = 0,        /* the fastest measured variant for the frame's spp */
     RT_KERNEL_LANES = 1,       /* one lane per sample, a pixel's samples in adjacent lanes */
     RT_KERNEL_PIXEL_LOOP = 2,  /* one lane per pixel looping over its samples (any spp) */
-    RT_KERNEL_COMPACT = 3,     /* LANES + wavefront active-ray compaction (ballot/prefix refill) */
+    RT_KERNEL_COMPACT = 3,     /* AUTO's per-ray code in persistent waves with wavefront active-ray
+                                  compaction: finished lanes are refilled with new samples by
+                                  ballot + prefix count (grid intersector; else = LANES) */
     RT_KERNEL_PERSISTENT = 4,  /* LANES in persistent workgroups with the LDS cell-occupancy bitmap */
     RT_KERNEL_FLAG_PREFETCH = 0x100,  /* OR-able: software-pipelined triangle record loads */
     RT_KERNEL_FLAG_WAVE_GATE = 0x200, /* OR-able: skip a test's second half when no lane needs it */
@@ -103,6 +105,9 @@ enum rt_kernel {
     RT_KERNEL_FLAG_ORIGIN_PRE = 0x10000, /* OR-able (grid, Moller-Trumbore, with WAVE_GATE +
                                             DIST_SKIP): per-frame precompute of the origin-only
                                             terms o - v0, (o - v0) x e1 of every reference */
+    RT_KERNEL_COMPACT_REFILL_SHIFT = 24,  /* RT_KERNEL_COMPACT: bits 24-30 = lanes that must be
+                                             idle before a wave refills (1..64; 0 = default 48) */
+    RT_KERNEL_COMPACT_REFILL_MASK = 0x7F000000,
 };
 
 /* Per-frame parameters: what Renderer::RenderTile reads from the Scene and itself. */

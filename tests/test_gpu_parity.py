@@ -135,11 +135,29 @@ def test_full_frame_1080p4(golden, scenes, sid):
     assert hashlib.sha256(hit_ids(recs).tobytes()).hexdigest() == g["hits_sha256"]
 
 
-def test_full_frame_compaction_kernel(golden, scenes):
-    for sid in (1, 5, 8):
-        hs, gs = scenes(sid)
-        img = gs.render_frame(gs.frame(1920, 1080, 4, kernel=rtm.RT_KERNEL_COMPACT))
-        assert hashlib.sha256(img.tobytes()).hexdigest() == golden["frames_1080p4"][str(sid)]["bgra_sha256"]
+@pytest.mark.parametrize("sid", range(10))
+def test_full_frame_compaction_kernel(golden, scenes, sid):
+    """RT_KERNEL_COMPACT (wavefront active-ray compaction) at refill thresholds 1 (refill as soon
+    as one lane is idle), the default, 40 and 64 (never refill a partly busy wave): BGRA8 equal to
+    the reference frame on all 10 scenes at 1080p x 4spp."""
+    hs, gs = scenes(sid)
+    want = golden["frames_1080p4"][str(sid)]["bgra_sha256"]
+    for refill in (0, 1, 40, 64):
+        k = rtm.RT_KERNEL_COMPACT | (refill << rtm.RT_KERNEL_COMPACT_REFILL_SHIFT)
+        img = gs.render_frame(gs.frame(1920, 1080, 4, kernel=k))
+        assert hashlib.sha256(img.tobytes()).hexdigest() == want, (sid, refill)
+
+
+@pytest.mark.parametrize("spp", [1, 2, 8, 64])
+def test_compaction_ragged_vs_oracle(scenes, oracle, spp):
+    """Ragged frames (partial 16x16 tiles -> invalid sample slots inside work items), every
+    power-of-two spp the kernel takes, both triangle tests."""
+    hs, gs = scenes(8)
+    exp, _, _ = oracle.render(8, 97, 61, spp)
+    np.testing.assert_array_equal(gs.render_frame(gs.frame(97, 61, spp, kernel=rtm.RT_KERNEL_COMPACT)), exp)
+    exp, _, _ = oracle.render(8, 97, 61, spp, tri_test=1)
+    f = gs.frame(97, 61, spp, kernel=rtm.RT_KERNEL_COMPACT, tri_test=rtm.RT_TRI_BARYCENTRIC)
+    np.testing.assert_array_equal(gs.render_frame(f), exp)
 
 
 def test_head_4096x4096x16(golden, scenes):
@@ -180,14 +198,14 @@ def test_barycentric_variant_vs_oracle(scenes, oracle):
         np.testing.assert_array_equal(hit_ids(recs), hits)
 
 
-@pytest.mark.parametrize("nranks", [1, 2, 3, 8])
-def test_shard_unshard_partition_invariant(golden, scenes, nranks):
+@pytest.mark.parametrize("nranks,kernel", [(1, 0), (2, 0), (3, 0), (8, 0), (3, 3), (8, 3)])
+def test_shard_unshard_partition_invariant(golden, scenes, nranks, kernel):
     """Multi-GPU layout: every rank's interleaved 16x16 tiles, gathered and
-    un-permuted by K3, reproduce the 1-GPU frame byte for byte."""
+    un-permuted by K3, reproduce the 1-GPU frame byte for byte (AUTO and COMPACT kernels)."""
     import torch
     hs, gs = scenes(1)
     W, H = 1920, 1080
-    f = gs.frame(W, H, 4)
+    f = gs.frame(W, H, 4, kernel=kernel)
     e = rtm.shard_elems(W, H, nranks)
     gathered = torch.zeros(nranks * e, dtype=torch.int32, device="cuda")
     stream = torch.cuda.current_stream().cuda_stream
