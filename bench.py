@@ -7,7 +7,11 @@ N > 1 ranks (torchrun, one process per GPU, RCCL) every rank renders its interle
 tiles of each frame (tile t -> rank t % N), the shards are all-gathered over xGMI and rank 0
 un-permutes them into the frame (K3): strong scaling of a fixed frame.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload bench|head4096|batch10]
+
+--workload (default "bench" = the BASELINE metric above) also runs BASELINE's other GPU
+configs: "head4096" = config 4 (head.dat, 4096x4096x16spp, the 8-GPU tile-shard case) and
+"batch10" = config 5 (all 10 built-in scenes at 1920x1080x4spp, one frame each per step).
 
 Prints ONE JSON line (rank 0).  value = total samples of all ranks / max-over-ranks wall time
 of the K timed steps.  roofline: algorithmic bytes of the render kernel per launch (SURVEY
@@ -29,8 +33,23 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(ROOT, "cpp-11-ray-trace-march-framework_amd")
 SCENES = (1, 8)
 W, H, SPP = 1920, 1080, 4
+# workload -> (scenes, W, H, spp, frame the per-sample counts are measured on, CPU-baseline frame)
+WORKLOADS = {
+    "bench": ((1, 8), 1920, 1080, 4, (1920, 1080, 4), (1920, 1080, 4)),
+    "head4096": ((4,), 4096, 4096, 16, (1024, 1024, 16), (1024, 1024, 16)),
+    "batch10": (tuple(range(10)), 1920, 1080, 4, (1920, 1080, 4), (960, 540, 4)),
+}
 HBM_PEAK = 8.0e12          # MI355X HBM3E peak, B/s (MI355X_MICROARCH.md)
-SURVEY_B = {1: 371.1, 8: 1467.8}
+SURVEY_B = {0: 390.2, 1: 371.1, 2: 796.1, 3: 573.7, 4: 487.8, 5: 1755.6, 6: 544.1, 7: 1220.7, 8: 1467.8,
+            9: 873.4}                        # SURVEY.md §8d (scene 4 at 4096^2 x 16)
+METRIC = {"bench": "Msamples/s at 1920x1080x4spp Cornell-Box+killeroo",
+          "head4096": "Msamples/s at 4096x4096x16spp head.dat (BASELINE config 4)",
+          "batch10": "Msamples/s at 1920x1080x4spp, all 10 built-in scenes (BASELINE config 5)"}
+SCENE_NAMES = {0: "torusknot/column/teapot", 1: "Cornell box + cube", 2: "room/table/chair/tv",
+               3: "table/chair", 4: "head", 5: "room + cat", 6: "water surface + torus knot",
+               7: "griebel + teapot", 8: "killeroo + ground", 9: "dwarf/hand/blob"}
+COUNT_FRAME = (1920, 1080, 4)               # frame the per-sample counts are measured on
+CPU_FRAME = (1920, 1080, 4)                 # frame of the CPU baseline sample
 
 
 def load_package():
@@ -42,12 +61,19 @@ def load_package():
 
 
 def algorithmic_bytes(gs, frame):
-    """Per-sample algorithmic bytes of the config from the kernel's own per-sample counters."""
-    recs = gs.trace_samples(frame, 0, 0, frame.width, frame.height)
-    n = len(recs)
-    v = recs["steps"].astype(np.float64).sum() / n
-    t = recs["tests"].astype(np.float64).sum() / n
-    h = recs["hit"].astype(np.float64).sum() / n
+    """Per-sample algorithmic bytes of the config from the kernel's own per-sample counters,
+    measured on COUNT_FRAME (the full frame, except head4096: 1024^2 x 16, as SURVEY §8d)."""
+    cw, ch, cs = COUNT_FRAME
+    f = gs.frame(cw, ch, cs)
+    v = t = h = 0.0
+    n = 0
+    for y0 in range(0, ch, 256):                       # row bands: bounded record buffers
+        recs = gs.trace_samples(f, 0, y0, cw, min(256, ch - y0))
+        n += len(recs)
+        v += recs["steps"].astype(np.float64).sum()
+        t += recs["tests"].astype(np.float64).sum()
+        h += recs["hit"].astype(np.float64).sum()
+    v, t, h = v / n, t / n, h / n
     return {"voxels": v, "tri_tests": t, "hit": h,
             "bytes_per_sample": 8 * v + 40 * t + 48 * h + 4.0 / frame.spp}
 
@@ -62,13 +88,14 @@ def cpu_baseline(rtm_unused=None):
     except AttributeError:
         cores = os.cpu_count() or 1
     cores = max(1, min(cores, int(os.environ.get("OMP_NUM_THREADS", cores))))
+    cw, ch, cs = CPU_FRAME
     for sid in SCENES:                  # warm-up (first render after idle is slow)
-        orc.render(sid, W, H, SPP, nthreads=cores)
+        orc.render(sid, cw, ch, cs, nthreads=cores)
     times = []
     for _ in range(3):
         tot = 0.0
         for sid in SCENES:
-            _, _, s = orc.render(sid, W, H, SPP, nthreads=cores)
+            _, _, s = orc.render(sid, cw, ch, cs, nthreads=cores)
             tot += s
         times.append(tot)
     med = sorted(times)[1]
@@ -78,9 +105,9 @@ def cpu_baseline(rtm_unused=None):
             model = next(l.split(":", 1)[1].strip() for l in f if l.startswith("model name"))
     except Exception:
         pass
-    return {"value": round(len(SCENES) * W * H * SPP / med / 1e6, 3), "unit": "Msamples/s",
+    return {"value": round(len(SCENES) * cw * ch * cs / med / 1e6, 3), "unit": "Msamples/s",
             "cores": cores, "kind": "port",
-            "sample": f"full frames of scenes {list(SCENES)} at {W}x{H}x{SPP}, 12x9 tile pool, "
+            "sample": f"full frames of scenes {list(SCENES)} at {cw}x{ch}x{cs}, 12x9 tile pool, "
                       f"median of 3 after 1 warm-up; cpu: {model or platform.processor()}"}
 
 
@@ -132,16 +159,25 @@ class GpuWorkload:
 
 def run_steps(work, world, rank, steps, warmup, dist=None):
     """W untimed warm-up steps, then K timed steps between barrier+sync on both sides; returns
-    the max-over-ranks wall time.  A step renders every scene (this rank's tiles when N > 1),
-    all-gathers the shards (RCCL over xGMI) and rank 0 un-permutes them into the frames."""
+    the max-over-ranks wall time.  A step renders every scene (this rank's tiles when N > 1);
+    each scene's shards are all-gathered (RCCL over xGMI) as soon as that scene is rendered, so
+    the gather of scene 1 overlaps the render of scene 8, and rank 0 un-permutes the frames."""
+    gathered = []
+    if world > 1:
+        import torch
+        gathered = [torch.empty(world * b.numel(), dtype=b.dtype, device=b.device) for b in work.bufs]
+
     def step(record):
+        pending = []
         for i in range(len(SCENES)):
             work.render(i, record)
-        if world > 1:
-            gathered = [work.rtm.all_gather_shards(work.bufs[i], world) for i in range(len(SCENES))]
+            if world > 1:
+                pending.append(work.rtm.all_gather_shards(work.bufs[i], world, out=gathered[i], async_op=True))
+        for i, (g, h) in enumerate(pending):
+            if h is not None:
+                h.wait()
             if rank == 0:
-                for i in range(len(SCENES)):
-                    work.unshard(i, gathered[i])
+                work.unshard(i, g)
 
     for _ in range(warmup):
         step(False)
@@ -172,7 +208,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--kernel", type=int, default=0, help="rt_kernel value (0 = AUTO; see include/rt_tracer.h)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="bench")
     args = ap.parse_args()
+    global SCENES, W, H, SPP, COUNT_FRAME, CPU_FRAME
+    SCENES, W, H, SPP, COUNT_FRAME, CPU_FRAME = WORKLOADS[args.workload]
 
     import torch
     import torch.distributed as dist
@@ -206,7 +245,7 @@ def main():
             if p.get("workload") == f"scenes{list(SCENES)}_{W}x{H}x{SPP}":
                 traffic = p.get("hbm_bytes_per_launch")
         out = {
-            "metric": "Msamples/s at 1920x1080x4spp Cornell-Box+killeroo",
+            "metric": METRIC[args.workload],
             "value": round(value, 3),
             "unit": "Msamples/s",
             "n_gpus": world,
@@ -217,7 +256,7 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "reference scenes 1 (Cornell box + cube) and 8 (killeroo + ground), "
+            "data": f"reference scenes {list(SCENES)} ({', '.join(SCENE_NAMES[x] for x in SCENES)}), "
                     "post-setup meshes dumped by the reference's own mesh code",
             "config": {"workload": f"scenes{list(SCENES)}_{W}x{H}x{SPP}", "scenes": list(SCENES),
                        "width": W, "height": H, "spp": SPP, "kernel": args.kernel,

@@ -509,15 +509,19 @@ def frame_from_shards(gathered, width, height, nranks):
     return gathered[r * elems + k * 256 + (y % 16) * 16 + (x % 16)].astype(np.uint32)
 
 
-def all_gather_shards(shard, world, group=None):
-    """All-gather equal-sized shards (RCCL over xGMI on GPUs, gloo on CPU tensors)."""
+def all_gather_shards(shard, world, group=None, out=None, async_op=False):
+    """All-gather equal-sized shards (RCCL over xGMI on GPUs, gloo on CPU tensors) into `out`
+    ([rank][shard] layout, allocated when None).  async_op=True returns (out, work): the RCCL
+    transfer runs on its own stream after the work already queued on the current stream, and
+    work.wait() orders the current stream after it (gloo completes before returning: work None)."""
     import torch
     import torch.distributed as dist
-    out = torch.empty(world * shard.numel(), dtype=shard.dtype, device=shard.device)
+    if out is None:
+        out = torch.empty(world * shard.numel(), dtype=shard.dtype, device=shard.device)
+    work = None
     if dist.get_backend(group) == "gloo":
         parts = list(out.chunk(world))
         dist.all_gather(parts, shard, group=group)
-        out = torch.cat(parts)
     else:
-        dist.all_gather_into_tensor(out, shard, group=group)
-    return out
+        work = dist.all_gather_into_tensor(out, shard, group=group, async_op=async_op)
+    return (out, work) if async_op else out
