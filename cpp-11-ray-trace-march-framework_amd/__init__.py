@@ -35,6 +35,9 @@ RT_KERNEL_FLAG_NESTED_STEP = 0x2000
 RT_KERNEL_FLAG_PRE_GATE = 0x4000
 RT_KERNEL_FLAG_EXHAUSTIVE = 0x8000
 RT_KERNEL_FLAG_ORIGIN_PRE = 0x10000
+RT_KERNEL_FLAG_SELECT_STEP = 0x20000
+RT_KERNEL_FLAG_FAST_RCP = 0x40000
+RT_KERNEL_FLAG_PACKED_REM = 0x80000
 RT_KERNEL_COMPACT_REFILL_SHIFT = 24      # RT_KERNEL_COMPACT: idle lanes before a refill (1..64)
 RT_ISECT_GRID = 0
 RT_ISECT_BRUTE_FORCE = 1
@@ -46,6 +49,7 @@ TRACER_SYMBOLS = [
     "rt_get_device_count", "rt_scene_create", "rt_scene_destroy", "rt_scene_device_bytes",
     "rt_render_tiles", "rt_render_frame_device", "rt_shard_elems", "rt_render_shard_device",
     "rt_unshard_device", "rt_last_kernel_ms", "rt_trace_samples", "rt_debug_primitives",
+    "rt_debug_rcp_check",
     "rt_sample_table", "rt_last_error", "rt_abi_version", "rt_grid_build", "rt_grid_free",
     "rt_scene_create_from_mesh",
 ]
@@ -136,6 +140,7 @@ def tracer_lib():
         L.rt_last_kernel_ms.argtypes = [vp, ctypes.POINTER(c_f32)]
         L.rt_trace_samples.argtypes = [vp, ctypes.POINTER(Frame), c_u32, c_u32, c_u32, c_u32, vp]
         L.rt_debug_primitives.argtypes = [ctypes.c_int, vp, c_u32, vp, ctypes.c_int]
+        L.rt_debug_rcp_check.argtypes = [vp, ctypes.c_int]
         L.rt_sample_table.argtypes = [c_u32, vp]
         L.rt_last_error.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
         L.rt_get_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
@@ -399,6 +404,14 @@ def unshard_device(width, height, nranks, d_gathered, d_out, stream=0):
 
 
 PRIM_WIDTHS = {0: (18, 8), 1: (12, 4), 2: (23, 6), 3: (3, 4), 4: (11, 3), 5: (18, 8), 6: (18, 8), 7: (12, 1)}
+
+
+def debug_rcp_check(device=0):
+    """Mismatch counts per biased exponent of the kernels' reciprocal vs 1.0f / x (all floats)."""
+    bad = np.zeros(256, np.uint64)
+    L = tracer_lib()
+    _check(L.rt_debug_rcp_check(_ptr(bad), device), L, "rt_debug_rcp_check")
+    return bad
 
 
 def debug_primitives(kind, records, device=0):

@@ -60,6 +60,22 @@ __device__ __forceinline__ float dot3(float ax, float ay, float az, float bx, fl
     return d;
 }
 
+// 1.0f / x without the v_div_scale / v_div_fmas / v_div_fixup wrapper of the correctly rounded
+// division (12 VALU -> 3): the v_rcp_f32 estimate refined by one FMA Newton step.  The
+// result equals the correctly rounded 1.0f / x for EVERY float x with 2^-126 <= |x| < 2^126,
+// checked exhaustively on gfx950 (rt_debug_rcp_check, tests/test_gpu_parity.py); callers use
+// it only inside that range.  The two FMAs are explicit, not contraction (hazard H1 concerns
+// a * b + c in the reference's expressions, which stay separately rounded).
+constexpr float kRcpLo = 1e-8f;              // below it triangle.h:77 rejects det anyway
+constexpr float kRcpHi = 8.5070591730234616e+37f;   // 2^126 (exclusive): exponents 253/254 and
+                                                    // subnormal x mismatch (measured)
+__device__ __forceinline__ float rcp_nr(float x)
+{
+    const float r = __builtin_amdgcn_rcpf(x);
+    const float e = __builtin_fmaf(-x, r, 1.0f);
+    return __builtin_fmaf(e, r, r);
+}
+
 // triangle.h:15-107 IntersectRayTri, non-culling branch. e1 = v1 - v0 and e2 = v2 - v0 are
 // precomputed on the host with the same single IEEE subtraction (triangle.h:41-42).
 __device__ __forceinline__ bool ray_tri_mt(float ox, float oy, float oz, float dx, float dy, float dz,
@@ -145,6 +161,10 @@ __device__ __forceinline__ bool ray_tri_mt_gated(float ox, float oy, float oz, f
 // camera, camera.h:39): tvec = o - v0 and qvec = tvec x e1 (triangle.h:71, 87) do not depend
 // on the direction, so they come precomputed per frame (k_origin_pre, same operations).  Only
 // the direction-dependent operations remain; results identical to ray_tri_mt_gated.
+// FAST_RCP: inv_det by rcp_nr, exact wherever the result is used: |det| < 1e-8 is rejected
+// below, and the launch selects FAST_RCP only for scenes whose |e1|_1 |e2|_1 bounds |det| far
+// below 2^126 (rt_scene::rcp_safe).
+template <bool FAST_RCP>
 __device__ __forceinline__ bool ray_tri_mt_gated_pre(float dx, float dy, float dz,
                                                      float e1x, float e1y, float e1z,
                                                      float e2x, float e2y, float e2z,
@@ -156,7 +176,11 @@ __device__ __forceinline__ bool ray_tri_mt_gated_pre(float dx, float dy, float d
     const float py = dz * e2x - dx * e2z;
     const float pz = dx * e2y - dy * e2x;
     const float det = e1x * px + e1y * py + e1z * pz;
-    const float inv_det = 1.0f / det;
+    float inv_det;
+    if (FAST_RCP)
+        inv_det = rcp_nr(det);
+    else
+        inv_det = 1.0f / det;
     u = (tx * px + ty * py + tz * pz) * inv_det;
     const bool ok1 = !(det > -0.00000001f && det < 0.00000001f) & !(u < 0.0f || u > 1.0f);
     if (!__any(ok1)) return false;

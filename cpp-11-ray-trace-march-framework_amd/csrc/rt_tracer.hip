@@ -64,6 +64,9 @@ constexpr int kVarBrute = 64;               // RT_ISECT_BRUTE_FORCE (renderer.cp
 constexpr int kVarMarch = 128;              // RT_ISECT_RAY_MARCH (renderer.cpp:24-41, 138-155)
 constexpr int kVarExhaustive = 256;         // RT_KERNEL_FLAG_EXHAUSTIVE: march without block culling
 constexpr int kVarOriginPre = 512;          // RT_KERNEL_FLAG_ORIGIN_PRE: per-frame o - v0, (o - v0) x e1
+constexpr int kVarSelStep = 1024;           // RT_KERNEL_FLAG_SELECT_STEP: select-form DDA step + bound (A/B)
+constexpr int kVarFastRcp = 2048;           // RT_KERNEL_FLAG_FAST_RCP: Newton-refined exact 1/det
+constexpr int kVarPackedRem = 4096;         // RT_KERNEL_FLAG_PACKED_REM: one packed remaining-cells word
 constexpr uint32_t kMarchSteps = 128;       // renderer.cpp:26
 constexpr uint32_t kDistBlock = 32;         // triangles per culling block of the distance kernels
 
@@ -183,7 +186,7 @@ __device__ __forceinline__ bool test_cell(const KParams& P, float ox, float oy, 
         {
             // r0..r2 = the frame record; the triangle id is resolved from refs after the walk
             id = k;
-            hit = rtd::ray_tri_mt_gated_pre(dx, dy, dz, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x,
+            hit = rtd::ray_tri_mt_gated_pre<(VAR & kVarFastRcp) != 0>(dx, dy, dz, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x,
                                             r2.y, r2.z, r2.w, ct, cu, cv);
         }
         else if (TRI == RT_TRI_BARYCENTRIC)
@@ -249,6 +252,46 @@ __device__ __forceinline__ bool test_cell(const KParams& P, float ox, float oy, 
         nct1 = a1_ ? n_ : nct1;                                                                \
         nct2 = a2_ ? n_ : nct2;                                                                \
         rem0 -= int(a0_); rem1 -= int(a1_); rem2 -= int(a2_);                                  \
+        cell += a2_ ? cs2 : (a1_ ? cs1 : cs0);                                                 \
+    } while (0)
+
+// RT_DDA_ADVANCE with each crossing time advanced by an add of the selected step:
+// nct_a + (a ? dt_a : 0.0f).  Bit-identical: the step axis gets the same single IEEE add, and
+// x + 0.0f == x for every value nct takes (finite or +inf, never -0 or NaN: every setup term is
+// >= 0, see dda_setup).  Two VALU fewer per step than the select-then-write-back form.
+#define RT_DDA_ADVANCE_ADD(NCT_AX, MORE)                                                       \
+    do {                                                                                       \
+        const float m_ = __builtin_fminf(__builtin_fminf(nct0, nct1), nct2);                   \
+        const bool a2_ = nct2 == m_;                                                           \
+        const bool a1_ = !a2_ && nct1 == m_;                                                   \
+        const bool a0_ = !a2_ && !a1_;                                                         \
+        NCT_AX = m_;                                                                           \
+        MORE = (a2_ ? rem2 : (a1_ ? rem1 : rem0)) != 0;                                        \
+        nct0 += a0_ ? dt0 : 0.0f;                                                              \
+        nct1 += a1_ ? dt1 : 0.0f;                                                              \
+        nct2 += a2_ ? dt2 : 0.0f;                                                              \
+        rem0 -= int(a0_); rem1 -= int(a1_); rem2 -= int(a2_);                                  \
+        cell += a2_ ? cs2 : (a1_ ? cs1 : cs0);                                                 \
+    } while (0)
+
+// RT_DDA_ADVANCE_ADD with the three remaining-cell counts packed into one word: rem0 in bits
+// 0-9, rem1 in 11-20, rem2 in 22-30, guard bits 10, 21, 31 (needs dims <= 512; rt_scene::
+// pack_ok).  The step subtracts the axis unit unconditionally; a count that was 0 borrows into
+// its guard bit, so MORE = no guard bit set == (rem of the step axis != 0) -- the walk exits
+// exactly where RT_DDA_ADVANCE's does (the borrowed state is dead after the exit).
+constexpr int kRemGuards = int((1u << 10) | (1u << 21) | (1u << 31));
+#define RT_DDA_ADVANCE_PACKED(NCT_AX, MORE)                                                    \
+    do {                                                                                       \
+        const float m_ = __builtin_fminf(__builtin_fminf(nct0, nct1), nct2);                   \
+        const bool a2_ = nct2 == m_;                                                           \
+        const bool a1_ = !a2_ && nct1 == m_;                                                   \
+        const bool a0_ = !a2_ && !a1_;                                                         \
+        NCT_AX = m_;                                                                           \
+        remp -= a2_ ? (1 << 22) : (a1_ ? (1 << 11) : 1);                                       \
+        MORE = (remp & kRemGuards) == 0;                                                       \
+        nct0 += a0_ ? dt0 : 0.0f;                                                              \
+        nct1 += a1_ ? dt1 : 0.0f;                                                              \
+        nct2 += a2_ ? dt2 : 0.0f;                                                              \
         cell += a2_ ? cs2 : (a1_ ? cs1 : cs0);                                                 \
     } while (0)
 
@@ -353,9 +396,14 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, const uint32_t 
     {
         // Distance skipping: after an empty cell at L-inf distance d from geometry the next
         // d-1 cells of the walk are provably empty, so they take the DDA step only.
+        // Termination: every iteration that does not exit decrements a positive rem (the step
+        // axis' count; MORE is false when it is 0), so a walk ends within rem0+rem1+rem2+1
+        // iterations whatever nct holds -- the P.max_steps bound is kept only in the A/B arm.
         int skip = 0;
-        for (uint32_t iter = 0; iter < P.max_steps; iter++)
+        int remp = rem0 | (rem1 << 11) | (rem2 << 22);      // kVarPackedRem only
+        for (uint32_t iter = 0;; iter++)
         {
+            if ((VAR & kVarSelStep) && iter >= P.max_steps) break;
             if (STATS) { voxel = uint32_t(cell); steps++; }
             uint32_t kb = 0, ke = 0;
             if (skip == 0)
@@ -370,7 +418,12 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, const uint32_t 
                 skip--;
             float nct_ax;
             bool more;
-            RT_DDA_ADVANCE(nct_ax, more);
+            if (VAR & kVarSelStep)
+                RT_DDA_ADVANCE(nct_ax, more);
+            else if (VAR & kVarPackedRem)
+                RT_DDA_ADVANCE_PACKED(nct_ax, more);
+            else
+                RT_DDA_ADVANCE_ADD(nct_ax, more);
             if (kb < ke && test_cell<STATS, TRI, VAR>(P, ox, oy, oz, dx, dy, dz, kb, ke, nct_ax, t, u, v, tri, tests))
                 return true;
             if (!more) break;
@@ -755,7 +808,7 @@ k_render_compact(KParams P, uint32_t n_items, uint32_t refill)
     uint32_t next_item = blockIdx.x * (kWG / 64u) + wv;
     const uint32_t walk_min = 64u - refill;
     // lane state: 0 idle, 1 walking, 2 finished (colour not yet stored)
-    uint32_t state = 0u, tag = 0u, iter = 0u;
+    uint32_t state = 0u, tag = 0u;
     float dx = 0.0f, dy = 0.0f, dz = 0.0f, t = 0.0f, u = 0.0f, v = 0.0f;
     uint32_t tri = 0u;
     bool hit = false;
@@ -873,7 +926,6 @@ k_render_compact(KParams P, uint32_t n_items, uint32_t refill)
                         {
                             state = 1u;
                             t = rtd::kFltMax;
-                            iter = 0u;
                             skip = 0;
                         }
                     }
@@ -897,7 +949,6 @@ k_render_compact(KParams P, uint32_t n_items, uint32_t refill)
         {
             if (state == 1u)
             {
-                iter++;
                 uint32_t kb = 0u, ke = 0u;
                 if ((VAR & kVarDistSkip) && P.cellw)
                 {
@@ -916,7 +967,7 @@ k_render_compact(KParams P, uint32_t n_items, uint32_t refill)
                     cell_range(P, uint32_t(cell), kb, ke);
                 float nct_ax;
                 bool more;
-                RT_DDA_ADVANCE(nct_ax, more);
+                RT_DDA_ADVANCE_ADD(nct_ax, more);
                 uint32_t tests = 0u;
                 if (kb < ke &&
                     test_cell<false, TRI, VAR>(P, ox, oy, oz, dx, dy, dz, kb, ke, nct_ax, t, u, v, tri, tests))
@@ -924,7 +975,7 @@ k_render_compact(KParams P, uint32_t n_items, uint32_t refill)
                     state = 2u;
                     hit = true;
                 }
-                else if (!more || iter >= P.max_steps)
+                else if (!more)                   // terminates: see grid_intersect
                     state = 2u;
             }
         } while (uint32_t(__popcll(__ballot(state == 1u))) > wmin);
@@ -1008,6 +1059,21 @@ __global__ void __launch_bounds__(kWG) k_origin_pre(const float4 *refs, float4 *
 }
 
 // Device KATs (rt_debug_primitives)
+// Exhaustive check of rtd::rcp_nr against the correctly rounded 1.0f / x over every finite
+// nonzero float: mismatches counted per biased exponent (bad[256]).
+__global__ void __launch_bounds__(kWG) k_rcp_check(unsigned long long *bad)
+{
+    const uint64_t n = 1ull << 32;
+    for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x)
+    {
+        const uint32_t b = uint32_t(i);
+        const uint32_t ex = (b >> 23) & 255u;
+        if (ex == 255u || (b & 0x7FFFFFFFu) == 0u) continue;
+        const float x = __uint_as_float(b);
+        if (__float_as_uint(rtd::rcp_nr(x)) != __float_as_uint(1.0f / x)) atomicAdd(&bad[ex], 1ull);
+    }
+}
+
 __global__ void __launch_bounds__(kWG) k_primitives(int kind, const float *in, uint32_t n, float *out)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1176,6 +1242,8 @@ struct rt_scene
     uint64_t device_bytes = 0;
     uint32_t persist_wgs = 1024;    // persistent grid: 4 x 512-lane workgroups per CU
     uint32_t compact_wgs = 2048;    // RT_KERNEL_COMPACT grid: 8 x 256-lane workgroups per CU
+    bool rcp_safe = false;          // every |det| of the ray/tri test is far below 2^126 (FAST_RCP)
+    bool pack_ok = false;           // dims <= 512: the remaining-cell counts pack into one word
     // sample table cache
     float2 *d_smp = nullptr;
     uint32_t smp_cap = 0;
@@ -1242,6 +1310,7 @@ int validate_frame(const rt_frame *f)
         (f->kernel & ~(0xFFu | RT_KERNEL_FLAG_PREFETCH | RT_KERNEL_FLAG_WAVE_GATE | RT_KERNEL_FLAG_LOOKAHEAD |
                        RT_KERNEL_FLAG_CSR_OFFSETS | RT_KERNEL_FLAG_DIST_SKIP | RT_KERNEL_FLAG_NESTED_STEP |
                        RT_KERNEL_FLAG_PRE_GATE | RT_KERNEL_FLAG_EXHAUSTIVE | RT_KERNEL_FLAG_ORIGIN_PRE |
+                       RT_KERNEL_FLAG_SELECT_STEP | RT_KERNEL_FLAG_FAST_RCP | RT_KERNEL_FLAG_PACKED_REM |
                        RT_KERNEL_COMPACT_REFILL_MASK)))
         return fail(RT_E_INVALID, "unknown kernel");
     const uint32_t spp = std::max(1u, f->spp);
@@ -1327,12 +1396,13 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
     s->last_stream = st;
     RT_HIP(hipEventRecord(s->ev0, st));
     const uint32_t kind = f->kernel & 0xFFu;
-    // RT_KERNEL_AUTO = lanes + wave gate + distance skip + per-frame origin terms: fastest arm of
-    // tools/ab_kernels.py on MI355X (scenes 1/4/5/8, 1080p x 4spp).
+    // RT_KERNEL_AUTO = lanes + wave gate + distance skip + per-frame origin terms + Newton
+    // reciprocal + packed remaining-cell counts (the last two where the scene allows them):
+    // fastest arm of tools/ab_kernels.py on MI355X (scenes 1/4/5/8, 1080p x 4spp).
     // RT_KERNEL_COMPACT runs the same per-ray code as AUTO (its A/B baseline).
     const uint32_t fk = (kind == RT_KERNEL_AUTO || kind == RT_KERNEL_COMPACT)
                             ? (f->kernel | RT_KERNEL_LANES | RT_KERNEL_FLAG_WAVE_GATE | RT_KERNEL_FLAG_DIST_SKIP |
-                               RT_KERNEL_FLAG_ORIGIN_PRE)
+                               RT_KERNEL_FLAG_ORIGIN_PRE | RT_KERNEL_FLAG_FAST_RCP | RT_KERNEL_FLAG_PACKED_REM)
                             : f->kernel;
     if ((fk & RT_KERNEL_FLAG_ORIGIN_PRE) && lanes && P.isect == RT_ISECT_GRID &&
         P.tri_test == RT_TRI_MOLLER_TRUMBORE && s->nrefs)
@@ -1344,7 +1414,10 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
                     ((fk & RT_KERNEL_FLAG_DIST_SKIP) ? kVarDistSkip : 0) |
                     ((fk & RT_KERNEL_FLAG_NESTED_STEP) ? kVarNestedStep : 0) |
                     ((fk & RT_KERNEL_FLAG_PRE_GATE) ? kVarPreGate : 0) |
-                    ((fk & RT_KERNEL_FLAG_ORIGIN_PRE) ? kVarOriginPre : 0);
+                    ((fk & RT_KERNEL_FLAG_ORIGIN_PRE) ? kVarOriginPre : 0) |
+                    ((fk & RT_KERNEL_FLAG_SELECT_STEP) ? kVarSelStep : 0) |
+                    ((fk & RT_KERNEL_FLAG_FAST_RCP) && s->rcp_safe ? kVarFastRcp : 0) |
+                    ((fk & RT_KERNEL_FLAG_PACKED_REM) && s->pack_ok ? kVarPackedRem : 0);
     const bool bary = P.tri_test == RT_TRI_BARYCENTRIC;
     const dim3 wg(kWG);
     if (lanes && kind == RT_KERNEL_COMPACT && P.isect == RT_ISECT_GRID)
@@ -1399,6 +1472,10 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
         else if (var == 40) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 40>), grid, wg, 0, st, P);
         else if (var == 42) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 42>), grid, wg, 0, st, P);
         else if (var == 522) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 522>), grid, wg, 0, st, P);
+        else if (var == 1546) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 1546>), grid, wg, 0, st, P);
+        else if (var == 2570) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 2570>), grid, wg, 0, st, P);
+        else if (var == 4618) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 4618>), grid, wg, 0, st, P);
+        else if (var == 6666) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 6666>), grid, wg, 0, st, P);
         else                hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 0>), grid, wg, 0, st, P);
     }
     else if (P.isect == RT_ISECT_RAY_MARCH && (f->kernel & RT_KERNEL_FLAG_EXHAUSTIVE))
@@ -1510,6 +1587,7 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
 
     // Per-reference triangle records in CSR order (see file header)
     std::vector<float4> refs(size_t(std::max(nr, 1u)) * 3);
+    double det_bound = 0.0;
     for (uint32_t k = 0; k < nr; k++)
     {
         const uint32_t ti = g.cell_tris[k];
@@ -1522,7 +1600,13 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
         refs[3 * size_t(k) + 0] = make_float4(p0[0], p0[1], p0[2], e1[0]);
         refs[3 * size_t(k) + 1] = make_float4(e1[1], e1[2], e2[0], e2[1]);
         refs[3 * size_t(k) + 2] = make_float4(e2[2], idf, 0.0f, 0.0f);
+        // |det| = |e1 . (d x e2)| <= |e1|_1 |e2|_1 for |d| ~ 1 (FAST_RCP range, rcp_nr)
+        const double b = (std::fabs(double(e1[0])) + std::fabs(double(e1[1])) + std::fabs(double(e1[2]))) *
+                         (std::fabs(double(e2[0])) + std::fabs(double(e2[1])) + std::fabs(double(e2[2])));
+        det_bound = (b > det_bound || b != b) ? b : det_bound;
     }
+    s->rcp_safe = det_bound == det_bound && det_bound < 0x1p120;
+    s->pack_ok = g.dims[0] <= 512 && g.dims[1] <= 512 && g.dims[2] <= 512;
     std::vector<float4> shade(size_t(d->num_triangles) * 3), facen(d->num_triangles);
     std::vector<float4> trimt(size_t(d->num_triangles) * 3), tridist(size_t(d->num_triangles) * 6);
     for (uint32_t i = 0; i < d->num_triangles; i++)
@@ -1872,6 +1956,24 @@ int rt_trace_samples(rt_scene *s, const rt_frame *f, uint32_t x0, uint32_t y0, u
     if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
     (void)hipFree(d_rec);
     if (e != hipSuccess) return fail(RT_E_HIP, std::string("rt_trace_samples: ") + hipGetErrorString(e));
+    return RT_OK;
+}
+
+int rt_debug_rcp_check(uint64_t *bad_by_exponent, int device)
+{
+    if (!bad_by_exponent) return fail(RT_E_INVALID, "NULL argument");
+    RT_HIP(hipSetDevice(device));
+    unsigned long long *d_bad = nullptr;
+    RT_HIP(hipMalloc(&d_bad, 256 * sizeof(unsigned long long)));
+    hipError_t e = hipMemset(d_bad, 0, 256 * sizeof(unsigned long long));
+    if (e == hipSuccess)
+    {
+        hipLaunchKernelGGL(k_rcp_check, dim3(8192), dim3(kWG), 0, nullptr, d_bad);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpy(bad_by_exponent, d_bad, 256 * sizeof(uint64_t), hipMemcpyDeviceToHost);
+    (void)hipFree(d_bad);
+    if (e != hipSuccess) return fail(RT_E_HIP, std::string("rt_debug_rcp_check: ") + hipGetErrorString(e));
     return RT_OK;
 }
 

@@ -105,6 +105,14 @@ enum rt_kernel {
     RT_KERNEL_FLAG_ORIGIN_PRE = 0x10000, /* OR-able (grid, Moller-Trumbore, with WAVE_GATE +
                                             DIST_SKIP): per-frame precompute of the origin-only
                                             terms o - v0, (o - v0) x e1 of every reference */
+    RT_KERNEL_FLAG_SELECT_STEP = 0x20000, /* OR-able (A/B arm): the DDA step's crossing times
+                                             updated by select + write-back, walk bounded by
+                                             dims sum (the pre-add-step form) */
+    RT_KERNEL_FLAG_FAST_RCP = 0x40000,    /* OR-able (with ORIGIN_PRE): 1/det of the ray/triangle
+                                             test by a Newton-refined v_rcp_f32, exhaustively
+                                             checked equal to 1.0f / det where it is used */
+    RT_KERNEL_FLAG_PACKED_REM = 0x80000,  /* OR-able (with DIST_SKIP): the DDA's three remaining-
+                                             cell counts in one guarded word (dims <= 512) */
     RT_KERNEL_COMPACT_REFILL_SHIFT = 24,  /* RT_KERNEL_COMPACT: bits 24-30 = lanes that must be
                                              idle before a wave refills (1..64; 0 = default 48) */
     RT_KERNEL_COMPACT_REFILL_MASK = 0x7F000000,
@@ -205,6 +213,10 @@ int  rt_trace_samples(rt_scene *scene, const rt_frame *frame, uint32_t x0, uint3
  * 7 DistancePointTri through the ray-march kernel's per-triangle record (12 in: pos, v0, v1,
  * v2; 1 out). */
 int  rt_debug_primitives(int kind, const float *in, uint32_t n, float *out, int device);
+/* Exhaustive check of the kernels' Newton-refined reciprocal (rt_device.h rcp_nr) against the
+   correctly rounded 1.0f / x for all 2^32 - 2^24 finite nonzero floats; bad_by_exponent[256]
+   receives the mismatch count per biased exponent. */
+int  rt_debug_rcp_check(uint64_t *bad_by_exponent, int device);
 
 /* Hammersley table the library uses when rt_frame.sample_offsets is NULL. */
 int  rt_sample_table(uint32_t spp, float *out_xy);

@@ -32,7 +32,13 @@ def test_device_ir_has_no_contraction_or_fast_math(tmp_path, src):
                    capture_output=True)
     ir = ll.read_text()
     assert "fmuladd" not in ir
-    assert not re.search(r"\bllvm\.fma\.f(32|64)\b", ir)
+    # explicit FMAs are allowed only in rtd::rcp_nr (the Newton step of the exhaustively
+    # checked reciprocal); any other llvm.fma would be a contraction in disguise
+    assert not re.search(r"\bllvm\.fma\.f64\b", ir)
+    for f in (SRC, GRID_SRC, os.path.join(PKG_DIR, "csrc", "rt_device.h")):
+        lines = [l for l in open(f) if re.search(r"\bfmaf?\b|__builtin_fma", l)]
+        assert all("__builtin_fmaf(" in l for l in lines), lines
+        assert len(lines) == (2 if f.endswith("rt_device.h") else 0), (f, lines)
     for flag in (" contract ", " afn ", " arcp ", " nnan ", " ninf ", " nsz ", " reassoc ", " fast "):
         assert flag not in ir, flag
     assert "denormal-fp-math-f32" not in ir or '"denormal-fp-math-f32"="ieee' in ir
@@ -51,8 +57,9 @@ def test_render_kernels_do_not_spill(tmp_path):
     assert lanes, table
     for n, (sc, vg) in lanes.items():
         assert sc == 0, f"{n} spills {sc} B/lane"
-    # the AUTO kernel (lanes + wave gate + distance skip + origin terms, Moller-Trumbore) and
-    # its no-precompute arm keep 8 waves/SIMD
-    for key in ("ILi0ELi522E", "ILi0ELi10E"):
+    # the AUTO kernel (lanes + wave gate + distance skip + origin terms + Newton reciprocal +
+    # packed counts, Moller-Trumbore), its plain-division arm and its no-precompute arm keep
+    # 8 waves/SIMD
+    for key in ("ILi0ELi6666E", "ILi0ELi522E", "ILi0ELi10E"):
         arm = [v for n, v in lanes.items() if key in n]
         assert arm and arm[0][1] <= 64, (key, arm)

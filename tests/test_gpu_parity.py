@@ -160,6 +160,28 @@ def test_compaction_ragged_vs_oracle(scenes, oracle, spp):
     np.testing.assert_array_equal(gs.render_frame(f), exp)
 
 
+def test_newton_reciprocal_exhaustive():
+    """rtd::rcp_nr (the kernels' 1/det) equals the correctly rounded 1.0f / x for every normal
+    float with |x| < 2^126 -- all 2^32 inputs checked on the device.  The kernels use it only
+    for |det| in [1e-8, 2^120] (RT_KERNEL_FLAG_FAST_RCP, rt_scene::rcp_safe)."""
+    bad = rtm.debug_rcp_check(0)
+    assert int(bad[1:253].sum()) == 0, {e: int(c) for e, c in enumerate(bad) if c}
+
+
+def test_auto_equals_plain_arms(golden, scenes):
+    """AUTO (Newton reciprocal + packed counts) and the plain-division / unpacked arm render the
+    same bytes as the reference on the two bench scenes and the densest one."""
+    base = (rtm.RT_KERNEL_LANES | rtm.RT_KERNEL_FLAG_WAVE_GATE | rtm.RT_KERNEL_FLAG_DIST_SKIP |
+            rtm.RT_KERNEL_FLAG_ORIGIN_PRE)
+    for sid in (1, 5, 8):
+        hs, gs = scenes(sid)
+        want = golden["frames_1080p4"][str(sid)]["bgra_sha256"]
+        for k in (base, base | rtm.RT_KERNEL_FLAG_FAST_RCP, base | rtm.RT_KERNEL_FLAG_PACKED_REM,
+                  base | rtm.RT_KERNEL_FLAG_SELECT_STEP):
+            img = gs.render_frame(gs.frame(1920, 1080, 4, kernel=k))
+            assert hashlib.sha256(img.tobytes()).hexdigest() == want, (sid, hex(k))
+
+
 def test_head_4096x4096x16(golden, scenes):
     """BASELINE config 4 (per-GPU work of the 8-GPU run is a subset of this frame)."""
     g = golden["frames_1080p4"]["head_4096x4096x16"]
