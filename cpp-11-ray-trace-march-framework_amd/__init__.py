@@ -23,6 +23,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 SCENE_DIR = os.path.join(REPO, "data", "scenes")
+MESH_DATA_DIR = os.path.join(REPO, "data", "meshes")     # cornell_box_quads.txt (scene table)
 
 RT_TRI_MOLLER_TRUMBORE, RT_TRI_BARYCENTRIC = 0, 1
 RT_KERNEL_AUTO, RT_KERNEL_LANES, RT_KERNEL_PIXEL_LOOP, RT_KERNEL_COMPACT, RT_KERNEL_PERSISTENT = 0, 1, 2, 3, 4
@@ -59,7 +60,9 @@ HOST_SYMBOLS = [
     "rth_framebuffer_set_sample_count", "rth_framebuffer_set_options", "rth_framebuffer_set_intersector",
     "rth_framebuffer_resize",
     "rth_framebuffer_start_rendering", "rth_framebuffer_read", "rth_framebuffer_save_bmp",
-    "rth_last_error",
+    "rth_last_error", "rth_scene_set_id", "rth_scene_save", "rth_mesh_read", "rth_mesh_normalize_dimensions",
+    "rth_mesh_transform", "rth_mesh_add_quad", "rth_mesh_add_mesh", "rth_mesh_data", "rth_mesh_free",
+    "rth_look_at", "rth_scene_table",
 ]
 
 
@@ -177,6 +180,19 @@ def host_lib():
         L.rth_framebuffer_read.argtypes = [vp, vp]
         L.rth_framebuffer_save_bmp.argtypes = [vp, ctypes.c_char_p]
         L.rth_last_error.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
+        L.rth_scene_set_id.argtypes = [vp, c_u32]
+        L.rth_scene_save.argtypes = [vp, ctypes.c_char_p]
+        L.rth_mesh_read.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(vp)]
+        L.rth_mesh_normalize_dimensions.argtypes = [vp]
+        L.rth_mesh_transform.argtypes = [vp, vp]
+        L.rth_mesh_add_quad.argtypes = [vp, vp]
+        L.rth_mesh_add_mesh.argtypes = [vp, vp]
+        L.rth_mesh_data.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(c_u32), ctypes.POINTER(vp),
+                                    ctypes.POINTER(c_u32)]
+        L.rth_mesh_free.argtypes = [vp]
+        L.rth_mesh_free.restype = None
+        L.rth_look_at.argtypes = [vp, vp, vp]
+        L.rth_scene_table.argtypes = [c_u32, ctypes.c_char_p, ctypes.c_char_p, c_u32, ctypes.POINTER(vp)]
         _host = L
     return _host
 
@@ -210,6 +226,72 @@ def sample_table(spp):
     return out.reshape(spp, 2)
 
 
+# ------------------------------------------------------------------ mesh ingestion
+class Mesh:
+    """Mesh (mesh.h:10-38) on the host: Read / NormalizeDimensions / Transform / AddQuad /
+    AddMesh restated in C++ (host/rt_scene_table.cpp)."""
+
+    def __init__(self, handle):
+        self._h = ctypes.c_void_p(handle)
+
+    @classmethod
+    def read(cls, path, flip_winding=False):
+        L, h = host_lib(), ctypes.c_void_p()
+        _check(L.rth_mesh_read(str(path).encode(), int(flip_winding), ctypes.byref(h)), L, "rth_mesh_read")
+        return cls(h.value)
+
+    def normalize_dimensions(self):
+        L = host_lib()
+        _check(L.rth_mesh_normalize_dimensions(self._h), L, "rth_mesh_normalize_dimensions")
+
+    def transform(self, mat):
+        m = np.ascontiguousarray(mat, np.float32).reshape(16)
+        L = host_lib()
+        _check(L.rth_mesh_transform(self._h, _ptr(m)), L, "rth_mesh_transform")
+
+    def add_quad(self, quad):
+        q = np.ascontiguousarray(quad, np.float32).reshape(12)
+        L = host_lib()
+        _check(L.rth_mesh_add_quad(self._h, _ptr(q)), L, "rth_mesh_add_quad")
+
+    def add_mesh(self, other):
+        L = host_lib()
+        _check(L.rth_mesh_add_mesh(self._h, other._h), L, "rth_mesh_add_mesh")
+
+    def arrays(self):
+        """(vertices float32 [nv, 6], triangles uint32 [nt, 6]) -- copies."""
+        L = host_lib()
+        vp_, tp_, nv, nt = ctypes.c_void_p(), ctypes.c_void_p(), c_u32(), c_u32()
+        _check(L.rth_mesh_data(self._h, ctypes.byref(vp_), ctypes.byref(nv), ctypes.byref(tp_), ctypes.byref(nt)),
+               L, "rth_mesh_data")
+        v = np.ctypeslib.as_array(ctypes.cast(vp_, ctypes.POINTER(c_f32)), shape=(nv.value, 6)).copy() \
+            if nv.value else np.zeros((0, 6), np.float32)
+        t = np.ctypeslib.as_array(ctypes.cast(tp_, ctypes.POINTER(c_u32)), shape=(nt.value, 6)).copy() \
+            if nt.value else np.zeros((0, 6), np.uint32)
+        return v, t
+
+    def close(self):
+        if self._h:
+            host_lib().rth_mesh_free(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def look_at(eye, at):
+    """Matrix44f::BuildLookAtMatrix (lin_alg.h:431-467) -> float32[16] (m_mat row-major)."""
+    e = np.ascontiguousarray(eye, np.float32)
+    a = np.ascontiguousarray(at, np.float32)
+    cam = np.zeros(16, np.float32)
+    L = host_lib()
+    _check(L.rth_look_at(_ptr(e), _ptr(a), _ptr(cam)), L, "rth_look_at")
+    return cam
+
+
 # ------------------------------------------------------------------ host scene
 class HostScene:
     """Scene + Grid on the host (scene.h:11-26, grid.h:12-52): mesh, camera and CSR cells."""
@@ -241,6 +323,20 @@ class HostScene:
         _check(L.rth_scene_from_mesh(_ptr(v), v.shape[0], _ptr(t), t.shape[0], fov, _ptr(cam),
                                      grid_res, nthreads, ctypes.byref(h)), L, "rth_scene_from_mesh")
         return cls(h.value)
+
+    @classmethod
+    def from_table(cls, scene_id, mesh_dir, nthreads=0):
+        """Application::InitializeScene(scene_id) from the reference's .dat meshes in mesh_dir
+        (application.cpp:304-517), restated in C++ (host/rt_scene_table.cpp)."""
+        L, h = host_lib(), ctypes.c_void_p()
+        _check(L.rth_scene_table(scene_id, mesh_dir.encode(), MESH_DATA_DIR.encode(), nthreads, ctypes.byref(h)),
+               L, "rth_scene_table")
+        return cls(h.value)
+
+    def save(self, path):
+        """Writes the .rtscene cache (mesh + camera) that load() reads back."""
+        L = host_lib()
+        _check(L.rth_scene_save(self._h, path.encode()), L, "rth_scene_save")
 
     def desc(self):
         d = SceneDesc()

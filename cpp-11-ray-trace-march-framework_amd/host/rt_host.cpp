@@ -280,6 +280,8 @@ static_assert(sizeof(rt_vertex) == 24 && sizeof(rt_triangle) == 24, "Mesh::Verte
 
 } // namespace
 
+int rth_internal_fail(int code, const std::string& m) { return fail(code, m); }
+
 // ================================================================= Framebuffer (host)
 // framebuffer.h:16-101 / framebuffer.cpp restated without OpenGL: 12x9 tiles, a
 // hardware_concurrency() worker pool, shuffled LIFO queue, per-tile mutex held across
@@ -532,6 +534,29 @@ int rth_scene_from_mesh(const rt_vertex* v, uint32_t nv, const rt_triangle* t, u
 }
 
 void rth_scene_free(rth_scene* s) { delete s; }
+
+int rth_scene_set_id(rth_scene* s, uint32_t id)
+{
+    if (!s) return fail(RT_E_INVALID, "NULL scene");
+    s->id = id;
+    return RT_OK;
+}
+
+// The .rtscene cache: what rth_scene_load reads back, bit for bit.
+int rth_scene_save(const rth_scene* s, const char* path)
+{
+    if (!s || !path) return fail(RT_E_INVALID, "NULL argument");
+    std::FILE* f = std::fopen(path, "wb");
+    if (!f) return fail(RT_E_INVALID, std::string("cannot create ") + path);
+    const uint32_t nv = uint32_t(s->verts.size()), nt = uint32_t(s->tris.size());
+    bool ok = std::fwrite("RTSCENE1", 1, 8, f) == 8 && std::fwrite(&s->id, 4, 1, f) == 1 &&
+              std::fwrite(&s->fov, 4, 1, f) == 1 && std::fwrite(s->cam, 4, 16, f) == 16 &&
+              std::fwrite(&nv, 4, 1, f) == 1 && std::fwrite(&nt, 4, 1, f) == 1 &&
+              std::fwrite(s->verts.data(), sizeof(rt_vertex), nv, f) == nv &&
+              std::fwrite(s->tris.data(), sizeof(rt_triangle), nt, f) == nt;
+    ok = (std::fclose(f) == 0) && ok;
+    return ok ? RT_OK : fail(RT_E_INVALID, std::string("write failed: ") + path);
+}
 
 int rth_scene_desc(const rth_scene* s, rt_scene_desc* d)
 {

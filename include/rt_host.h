@@ -38,6 +38,32 @@ int  rth_scene_from_mesh(const rt_vertex *vertices, uint32_t num_vertices,
                          float fov, const float cam[16], uint32_t grid_res, uint32_t nthreads,
                          rth_scene **out);
 void rth_scene_free(rth_scene *s);
+int  rth_scene_set_id(rth_scene *s, uint32_t scene_id);
+/* Writes the scene (mesh + camera) as .rtscene -- the binary scene cache rth_scene_load reads. */
+int  rth_scene_save(const rth_scene *s, const char *path);
+
+/* ---- Mesh ingestion and the built-in scene table --------------- */
+typedef struct rth_mesh rth_mesh;
+/* Mesh::Read (mesh.cpp:138-391): ASCII .dat, indexed or flat, "x y z [n [uv|rgb]]" vertices;
+ * flip_winding swaps v0/v1 of every triangle.  Face normals = TriangleNormal; position-only
+ * meshes copy them to the vertices. */
+int  rth_mesh_read(const char *path, int flip_winding, rth_mesh **out);
+int  rth_mesh_normalize_dimensions(rth_mesh *m);                  /* mesh.cpp:121-136 */
+/* Mesh::Transform (mesh.cpp:96-119); mat = Matrix44f::m_mat row-major (translation in row 3) */
+int  rth_mesh_transform(rth_mesh *m, const float mat[16]);
+int  rth_mesh_add_quad(rth_mesh *m, const float quad[12]);          /* mesh.cpp:27-53 */
+int  rth_mesh_add_mesh(rth_mesh *m, const rth_mesh *other);         /* mesh.cpp:55-70 */
+/* Pointers into the mesh's own arrays (mesh.h layouts); valid while the mesh lives. */
+int  rth_mesh_data(const rth_mesh *m, const rt_vertex **vertices, uint32_t *num_vertices,
+                   const rt_triangle **triangles, uint32_t *num_triangles);
+void rth_mesh_free(rth_mesh *m);
+/* Matrix44f::BuildLookAtMatrix(eye, at, up = +Y) (lin_alg.h:431-467) -> cam[16] */
+int  rth_look_at(const float eye[3], const float at[3], float cam[16]);
+/* Application::InitializeScene (application.cpp:304-517): builds built-in scene 0..9 from the
+ * reference's .dat meshes in mesh_dir (data_dir holds cornell_box_quads.txt, the Cornell box
+ * geometry table) and its grid (resolution 64).  Bit-identical to the reference's own setup. */
+int  rth_scene_table(uint32_t scene_id, const char *mesh_dir, const char *data_dir, uint32_t nthreads,
+                     rth_scene **out);
 /* Pointers into the scene's own host arrays; valid while the scene lives. */
 int  rth_scene_desc(const rth_scene *s, rt_scene_desc *out);
 int  rth_scene_camera(const rth_scene *s, float *fov, float cam[16]);

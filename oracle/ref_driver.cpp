@@ -48,6 +48,7 @@
 #include "types.h"
 #include "lin_alg.h"
 #include "mesh.h"
+#include "cornell_box.h"
 #include "grid.h"
 #include "sampling.h"
 #include "camera.h"
@@ -763,6 +764,39 @@ int main(int argc, char **argv)
             if (!WriteScene(path.c_str(), id, fov, cam, mesh)) return 1;
         }
         std::printf("RESULT {\"dump\": \"ok\"}\n");
+        return 0;
+    }
+
+    if (cmd == "mesh-read" && argc == 5)
+    {
+        // Mesh::Read(path, flip) [+ NormalizeDimensions when argv[3] has bit 1] -> raw dump:
+        // u32 ok | u32 nv | u32 nt | nv x Vertex | nt x Triangle (mesh.h layouts)
+        const int mode = std::atoi(argv[3]);
+        Mesh m;
+        uint32 ok = m.Read(argv[2], (mode & 1) != 0) ? 1u : 0u;
+        if (ok && (mode & 2)) m.NormalizeDimensions();
+        const uint32 nv = uint32(m.m_vertices.size()), nt = uint32(m.m_triangles.size());
+        std::FILE *f = std::fopen(argv[4], "wb");
+        if (!f) return 1;
+        std::fwrite(&ok, 4, 1, f);
+        std::fwrite(&nv, 4, 1, f);
+        std::fwrite(&nt, 4, 1, f);
+        if (nv) std::fwrite(&m.m_vertices[0], sizeof(Mesh::Vertex), nv, f);
+        if (nt) std::fwrite(&m.m_triangles[0], sizeof(Mesh::Triangle), nt, f);
+        std::fclose(f);
+        return 0;
+    }
+
+    if (cmd == "cornell-quads" && argc == 3)
+    {
+        // the reference's Cornell box geometry table (cornell_box.cpp), one vertex per line
+        // with 9 significant digits (round-trips every float): data for the host scene table
+        std::FILE *f = std::fopen(argv[2], "w");
+        if (!f) return 1;
+        std::fprintf(f, "%u\n", g_cornell_num_quads);
+        for (uint i = 0; i < g_cornell_num_quads * 4; i++)
+            std::fprintf(f, "%.9g %.9g %.9g\n", g_cornell_quads[i][0], g_cornell_quads[i][1], g_cornell_quads[i][2]);
+        std::fclose(f);
         return 0;
     }
 
