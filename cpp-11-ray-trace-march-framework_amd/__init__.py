@@ -39,6 +39,7 @@ RT_KERNEL_FLAG_ORIGIN_PRE = 0x10000
 RT_KERNEL_FLAG_SELECT_STEP = 0x20000
 RT_KERNEL_FLAG_FAST_RCP = 0x40000
 RT_KERNEL_FLAG_PACKED_REM = 0x80000
+RT_KERNEL_FLAG_XCD_BANDS = 0x100000
 RT_KERNEL_COMPACT_REFILL_SHIFT = 24      # RT_KERNEL_COMPACT: idle lanes before a refill (1..64)
 RT_ISECT_GRID = 0
 RT_ISECT_BRUTE_FORCE = 1

@@ -67,6 +67,7 @@ constexpr int kVarOriginPre = 512;          // RT_KERNEL_FLAG_ORIGIN_PRE: per-fr
 constexpr int kVarSelStep = 1024;           // RT_KERNEL_FLAG_SELECT_STEP: select-form DDA step + bound (A/B)
 constexpr int kVarFastRcp = 2048;           // RT_KERNEL_FLAG_FAST_RCP: Newton-refined exact 1/det
 constexpr int kVarPackedRem = 4096;         // RT_KERNEL_FLAG_PACKED_REM: one packed remaining-cells word
+constexpr int kVarXcdBands = 8192;          // RT_KERNEL_FLAG_XCD_BANDS: XCD-aware block -> tile order
 constexpr uint32_t kMarchSteps = 128;       // renderer.cpp:26
 constexpr uint32_t kDistBlock = 32;         // triangles per culling block of the distance kernels
 
@@ -107,6 +108,7 @@ struct KParams
     uint32_t tiles_x;           // 16x16 tiles across the region
     uint32_t rank, nranks;      // tile t is ours iff t % nranks == rank, local index t / nranks
     uint32_t wg_per_tile;
+    uint32_t xcd_chunk;         // kVarXcdBands: consecutive blocks per XCD turn (0 = one band each)
     // output
     uint32_t *out;
     uint32_t pitch;             // frame mode: words per row of out
@@ -731,12 +733,36 @@ __device__ __forceinline__ void process_item(const KParams& P, const uint32_t *l
     }
 }
 
+// XCD-aware block order (kVarXcdBands).  The dispatcher deals workgroups round-robin to the 8
+// XCDs (block b runs on XCD b % 8), so consecutive blocks -- the 4 workgroups of one tile and
+// the tiles of one row -- land on 8 different L2s, and every XCD's L2 caches the whole visible
+// scene.  Remapped, XCD x takes turns of `chunk` consecutive blocks (one tile row): rows x,
+// x + 8, x + 16, ... -- compact rows for its L2, and the frame's cost still spread over all
+// XCDs.  chunk 0: one contiguous band per XCD (measured: load imbalance, up to 58 % slower).
+// A bijection on [0, nblocks) for any grid size (the tail past whole 8-turn rounds keeps its
+// order); on a device with another XCD count only the locality changes.
+constexpr uint32_t kXcds = 8;
+__device__ __forceinline__ uint32_t xcd_band_block(uint32_t b, uint32_t nb, uint32_t chunk)
+{
+    if (chunk == 0u)
+    {
+        const uint32_t q = nb / kXcds, r = nb % kXcds;
+        const uint32_t x = b % kXcds, i = b / kXcds;
+        return x < r ? x * (q + 1u) + i : r * (q + 1u) + (x - r) * q + i;
+    }
+    const uint32_t full = nb / (kXcds * chunk) * (kXcds * chunk);
+    if (b >= full) return b;
+    const uint32_t x = b % kXcds, i = b / kXcds;
+    return ((i / chunk) * kXcds + x) * chunk + i % chunk;
+}
+
 // RT_KERNEL_LANES: one lane per sample (spp = 2^spp_shift <= 64), one work item per wave,
-// no LDS.  Kept as the A/B baseline of the persistent kernel.
+// no LDS (the AUTO kernel).
 template <int TRI, int VAR>
 __global__ void __launch_bounds__(kWG) k_render_lanes(KParams P)
 {
-    process_item<TRI, VAR>(P, nullptr, blockIdx.x * (kWG / 64u) + (threadIdx.x >> 6));
+    const uint32_t b = (VAR & kVarXcdBands) ? xcd_band_block(blockIdx.x, gridDim.x, P.xcd_chunk) : blockIdx.x;
+    process_item<TRI, VAR>(P, nullptr, b * (kWG / 64u) + (threadIdx.x >> 6));
 }
 
 // RT_KERNEL_PERSISTENT (spp a power of two <= 64): persistent 512-lane workgroups, 4 per CU.  The
@@ -1311,6 +1337,7 @@ int validate_frame(const rt_frame *f)
                        RT_KERNEL_FLAG_CSR_OFFSETS | RT_KERNEL_FLAG_DIST_SKIP | RT_KERNEL_FLAG_NESTED_STEP |
                        RT_KERNEL_FLAG_PRE_GATE | RT_KERNEL_FLAG_EXHAUSTIVE | RT_KERNEL_FLAG_ORIGIN_PRE |
                        RT_KERNEL_FLAG_SELECT_STEP | RT_KERNEL_FLAG_FAST_RCP | RT_KERNEL_FLAG_PACKED_REM |
+                       RT_KERNEL_FLAG_XCD_BANDS |
                        RT_KERNEL_COMPACT_REFILL_MASK)))
         return fail(RT_E_INVALID, "unknown kernel");
     const uint32_t spp = std::max(1u, f->spp);
@@ -1396,13 +1423,19 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
     s->last_stream = st;
     RT_HIP(hipEventRecord(s->ev0, st));
     const uint32_t kind = f->kernel & 0xFFu;
+    // kVarXcdBands turn size: one row of this launch's tiles (ceil(tiles_x / nranks) local tiles
+    // span a full frame row in shard mode).  Measured best of 1/4 .. 4 rows and 1..16 tiles:
+    // whole rows interleave over the XCDs, so each L2 sees compact rows AND the frame's cost
+    // spreads evenly (half rows put every left half on the even XCDs).
+    P.xcd_chunk = ((P.tiles_x + P.nranks - 1u) / P.nranks) * P.wg_per_tile;
     // RT_KERNEL_AUTO = lanes + wave gate + distance skip + per-frame origin terms + Newton
-    // reciprocal + packed remaining-cell counts (the last two where the scene allows them):
-    // fastest arm of tools/ab_kernels.py on MI355X (scenes 1/4/5/8, 1080p x 4spp).
-    // RT_KERNEL_COMPACT runs the same per-ray code as AUTO (its A/B baseline).
+    // reciprocal + packed remaining-cell counts (the last two where the scene allows them) +
+    // XCD row interleave: fastest arm of tools/ab_kernels.py on MI355X (scenes 1/2/4/5/7/8,
+    // 1080p x 4spp).  RT_KERNEL_COMPACT runs the same per-ray code as AUTO.
     const uint32_t fk = (kind == RT_KERNEL_AUTO || kind == RT_KERNEL_COMPACT)
                             ? (f->kernel | RT_KERNEL_LANES | RT_KERNEL_FLAG_WAVE_GATE | RT_KERNEL_FLAG_DIST_SKIP |
-                               RT_KERNEL_FLAG_ORIGIN_PRE | RT_KERNEL_FLAG_FAST_RCP | RT_KERNEL_FLAG_PACKED_REM)
+                               RT_KERNEL_FLAG_ORIGIN_PRE | RT_KERNEL_FLAG_FAST_RCP | RT_KERNEL_FLAG_PACKED_REM |
+                               RT_KERNEL_FLAG_XCD_BANDS)
                             : f->kernel;
     if ((fk & RT_KERNEL_FLAG_ORIGIN_PRE) && lanes && P.isect == RT_ISECT_GRID &&
         P.tri_test == RT_TRI_MOLLER_TRUMBORE && s->nrefs)
@@ -1417,7 +1450,8 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
                     ((fk & RT_KERNEL_FLAG_ORIGIN_PRE) ? kVarOriginPre : 0) |
                     ((fk & RT_KERNEL_FLAG_SELECT_STEP) ? kVarSelStep : 0) |
                     ((fk & RT_KERNEL_FLAG_FAST_RCP) && s->rcp_safe ? kVarFastRcp : 0) |
-                    ((fk & RT_KERNEL_FLAG_PACKED_REM) && s->pack_ok ? kVarPackedRem : 0);
+                    ((fk & RT_KERNEL_FLAG_PACKED_REM) && s->pack_ok ? kVarPackedRem : 0) |
+                    ((fk & RT_KERNEL_FLAG_XCD_BANDS) ? kVarXcdBands : 0);
     const bool bary = P.tri_test == RT_TRI_BARYCENTRIC;
     const dim3 wg(kWG);
     if (lanes && kind == RT_KERNEL_COMPACT && P.isect == RT_ISECT_GRID)
@@ -1476,6 +1510,11 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
         else if (var == 2570) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 2570>), grid, wg, 0, st, P);
         else if (var == 4618) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 4618>), grid, wg, 0, st, P);
         else if (var == 6666) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 6666>), grid, wg, 0, st, P);
+        else if (var == 14858) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 14858>), grid, wg, 0, st, P);
+        // AUTO on scenes outside the FAST_RCP / PACKED_REM ranges
+        else if (var == 8714) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 8714>), grid, wg, 0, st, P);
+        else if (var == 10762) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 10762>), grid, wg, 0, st, P);
+        else if (var == 12810) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 12810>), grid, wg, 0, st, P);
         else                hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 0>), grid, wg, 0, st, P);
     }
     else if (P.isect == RT_ISECT_RAY_MARCH && (f->kernel & RT_KERNEL_FLAG_EXHAUSTIVE))

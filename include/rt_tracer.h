@@ -113,6 +113,8 @@ enum rt_kernel {
                                              checked equal to 1.0f / det where it is used */
     RT_KERNEL_FLAG_PACKED_REM = 0x80000,  /* OR-able (with DIST_SKIP): the DDA's three remaining-
                                              cell counts in one guarded word (dims <= 512) */
+    RT_KERNEL_FLAG_XCD_BANDS = 0x100000,  /* OR-able: XCD-aware block order, each of the 8 XCDs
+                                             renders one contiguous band of tiles (L2 locality) */
     RT_KERNEL_COMPACT_REFILL_SHIFT = 24,  /* RT_KERNEL_COMPACT: bits 24-30 = lanes that must be
                                              idle before a wave refills (1..64; 0 = default 48) */
     RT_KERNEL_COMPACT_REFILL_MASK = 0x7F000000,

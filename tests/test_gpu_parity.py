@@ -169,15 +169,16 @@ def test_newton_reciprocal_exhaustive():
 
 
 def test_auto_equals_plain_arms(golden, scenes):
-    """AUTO (Newton reciprocal + packed counts) and the plain-division / unpacked arm render the
-    same bytes as the reference on the two bench scenes and the densest one."""
+    """AUTO (Newton reciprocal + packed counts + XCD row interleave) and the plain-division /
+    unpacked / dispatch-order arms render the same bytes as the reference on the two bench
+    scenes and the densest one."""
     base = (rtm.RT_KERNEL_LANES | rtm.RT_KERNEL_FLAG_WAVE_GATE | rtm.RT_KERNEL_FLAG_DIST_SKIP |
             rtm.RT_KERNEL_FLAG_ORIGIN_PRE)
     for sid in (1, 5, 8):
         hs, gs = scenes(sid)
         want = golden["frames_1080p4"][str(sid)]["bgra_sha256"]
         for k in (base, base | rtm.RT_KERNEL_FLAG_FAST_RCP, base | rtm.RT_KERNEL_FLAG_PACKED_REM,
-                  base | rtm.RT_KERNEL_FLAG_SELECT_STEP):
+                  base | rtm.RT_KERNEL_FLAG_SELECT_STEP, base | rtm.RT_KERNEL_FLAG_XCD_BANDS):
             img = gs.render_frame(gs.frame(1920, 1080, 4, kernel=k))
             assert hashlib.sha256(img.tobytes()).hexdigest() == want, (sid, hex(k))
 
