@@ -27,6 +27,7 @@ MESH_DATA_DIR = os.path.join(REPO, "data", "meshes")     # cornell_box_quads.txt
 
 RT_TRI_MOLLER_TRUMBORE, RT_TRI_BARYCENTRIC = 0, 1
 RT_KERNEL_AUTO, RT_KERNEL_LANES, RT_KERNEL_PIXEL_LOOP, RT_KERNEL_COMPACT, RT_KERNEL_PERSISTENT = 0, 1, 2, 3, 4
+RT_KERNEL_WIDE = 5
 RT_KERNEL_FLAG_PREFETCH = 0x100
 RT_KERNEL_FLAG_WAVE_GATE = 0x200
 RT_KERNEL_FLAG_LOOKAHEAD = 0x400
@@ -40,6 +41,10 @@ RT_KERNEL_FLAG_SELECT_STEP = 0x20000
 RT_KERNEL_FLAG_FAST_RCP = 0x40000
 RT_KERNEL_FLAG_PACKED_REM = 0x80000
 RT_KERNEL_FLAG_XCD_BANDS = 0x100000
+RT_KERNEL_FLAG_UNROLL_PAIRS = 0x200000
+RT_KERNEL_FLAG_WAVE_CLOCK = 0x400000
+RT_KERNEL_FLAG_UNIFORM_CELLS = 0x800000
+RT_KERNEL_FLAG_BAIL_WIDE = 0x80000000
 RT_KERNEL_COMPACT_REFILL_SHIFT = 24      # RT_KERNEL_COMPACT: idle lanes before a refill (1..64)
 RT_ISECT_GRID = 0
 RT_ISECT_BRUTE_FORCE = 1
@@ -51,7 +56,7 @@ TRACER_SYMBOLS = [
     "rt_get_device_count", "rt_scene_create", "rt_scene_destroy", "rt_scene_device_bytes",
     "rt_render_tiles", "rt_render_frame_device", "rt_shard_elems", "rt_render_shard_device",
     "rt_unshard_device", "rt_last_kernel_ms", "rt_trace_samples", "rt_debug_primitives",
-    "rt_debug_rcp_check",
+    "rt_debug_rcp_check", "rt_debug_wave_clocks",
     "rt_sample_table", "rt_last_error", "rt_abi_version", "rt_grid_build", "rt_grid_free",
     "rt_scene_create_from_mesh",
 ]
@@ -145,6 +150,7 @@ def tracer_lib():
         L.rt_trace_samples.argtypes = [vp, ctypes.POINTER(Frame), c_u32, c_u32, c_u32, c_u32, vp]
         L.rt_debug_primitives.argtypes = [ctypes.c_int, vp, c_u32, vp, ctypes.c_int]
         L.rt_debug_rcp_check.argtypes = [vp, ctypes.c_int]
+        L.rt_debug_wave_clocks.argtypes = [vp, vp, c_u32, ctypes.POINTER(c_u32)]
         L.rt_sample_table.argtypes = [c_u32, vp]
         L.rt_last_error.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
         L.rt_get_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
@@ -454,6 +460,15 @@ class GpuScene:
         _check(L.rt_render_shard_device(self._h, ctypes.byref(frame), rank, nranks,
                                         ctypes.c_void_p(d_ptr), ctypes.c_void_p(stream)), L,
                "rt_render_shard_device")
+
+    def wave_clocks(self):
+        """{start, end} s_memtime per work item of the last RT_KERNEL_FLAG_WAVE_CLOCK launch."""
+        L = tracer_lib()
+        n = c_u32()
+        _check(L.rt_debug_wave_clocks(self._h, None, 0, ctypes.byref(n)), L, "rt_debug_wave_clocks")
+        out = np.zeros((n.value, 2), np.uint64)
+        _check(L.rt_debug_wave_clocks(self._h, _ptr(out), n.value, ctypes.byref(n)), L, "rt_debug_wave_clocks")
+        return out
 
     def last_kernel_ms(self):
         ms = c_f32()

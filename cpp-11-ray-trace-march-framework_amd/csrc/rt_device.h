@@ -189,6 +189,31 @@ __device__ __forceinline__ bool ray_tri_mt_gated_pre(float dx, float dy, float d
     return ok1 & !(v < 0.0f || u + v > 1.0f) & (t >= 0.0f);
 }
 
+// ray_tri_mt_gated_pre split at its gate, for a caller that interleaves two independent tests
+// (instruction-level parallelism in latency-bound waves).  Same operations, same results.
+template <bool FAST_RCP>
+__device__ __forceinline__ bool mt_pre_first(float dx, float dy, float dz, float e1x, float e1y, float e1z,
+                                             float e2x, float e2y, float e2z, float tx, float ty, float tz,
+                                             float& inv_det, float& u)
+{
+    const float px = dy * e2z - dz * e2y;
+    const float py = dz * e2x - dx * e2z;
+    const float pz = dx * e2y - dy * e2x;
+    const float det = e1x * px + e1y * py + e1z * pz;
+    inv_det = FAST_RCP ? rcp_nr(det) : 1.0f / det;
+    u = (tx * px + ty * py + tz * pz) * inv_det;
+    return !(det > -0.00000001f && det < 0.00000001f) & !(u < 0.0f || u > 1.0f);
+}
+
+__device__ __forceinline__ bool mt_pre_second(float dx, float dy, float dz, float e2x, float e2y, float e2z,
+                                              float qx, float qy, float qz, float inv_det, float u, float& v,
+                                              float& t)
+{
+    v = (dx * qx + dy * qy + dz * qz) * inv_det;
+    t = (e2x * qx + e2y * qy + e2z * qz) * inv_det;
+    return !(v < 0.0f || u + v > 1.0f) & (t >= 0.0f);
+}
+
 // ray_tri_mt_gated preceded by a division-free wave-uniform pre-gate.  With q = udot/det the
 // reference's u = RN(udot * RN(1/det)); a lane is PROVABLY rejected by triangle.h:77-87 when
 //   det fails the epsilon test, or

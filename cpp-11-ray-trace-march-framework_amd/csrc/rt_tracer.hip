@@ -68,6 +68,10 @@ constexpr int kVarSelStep = 1024;           // RT_KERNEL_FLAG_SELECT_STEP: selec
 constexpr int kVarFastRcp = 2048;           // RT_KERNEL_FLAG_FAST_RCP: Newton-refined exact 1/det
 constexpr int kVarPackedRem = 4096;         // RT_KERNEL_FLAG_PACKED_REM: one packed remaining-cells word
 constexpr int kVarXcdBands = 8192;          // RT_KERNEL_FLAG_XCD_BANDS: XCD-aware block -> tile order
+constexpr int kVarUnroll = 16384;           // RT_KERNEL_FLAG_UNROLL_PAIRS: uniform lists tested two records at a time
+constexpr int kVarWaveClock = 32768;        // RT_KERNEL_FLAG_WAVE_CLOCK: per-item s_memtime (debug)
+constexpr int kVarUniform = 65536;          // RT_KERNEL_FLAG_UNIFORM_CELLS: scalar loop for wave-uniform lists
+constexpr int kVarBail = 131072;            // RT_KERNEL_FLAG_BAIL_WIDE phase 1: test budget + pixel queue
 constexpr uint32_t kMarchSteps = 128;       // renderer.cpp:26
 constexpr uint32_t kDistBlock = 32;         // triangles per culling block of the distance kernels
 
@@ -109,6 +113,11 @@ struct KParams
     uint32_t rank, nranks;      // tile t is ours iff t % nranks == rank, local index t / nranks
     uint32_t wg_per_tile;
     uint32_t xcd_chunk;         // kVarXcdBands: consecutive blocks per XCD turn (0 = one band each)
+    uint64_t *wave_clk;         // kVarWaveClock: {start, end} s_memtime per work item
+    const uint32_t *tile_order; // tile order (position -> local tile) or null = natural order
+    uint32_t bail_tests;        // BAIL_WIDE phase 1: test budget per sample
+    uint32_t *bail_count;       // BAIL_WIDE: queued pixels
+    uint32_t *bail_queue;       // BAIL_WIDE: (local tile << 8 | Morton pixel) per queued pixel
     // output
     uint32_t *out;
     uint32_t pitch;             // frame mode: words per row of out
@@ -151,6 +160,98 @@ __device__ __forceinline__ bool test_cell(const KParams& P, float ox, float oy, 
                                           float dz, uint32_t kb, uint32_t ke, float nct_ax, float& t,
                                           float& u, float& v, uint32_t& tri, uint32_t& tests)
 {
+    if constexpr ((VAR & kVarUniform) != 0 && (VAR & kVarOriginPre) != 0 && TRI == RT_TRI_MOLLER_TRUMBORE)
+    {
+        // Wave-uniform list: every lane testing this step sits in the same cell (the common case
+        // in dense geometry: a wave is a 4x4-pixel x 4-sample block).  The loop runs on scalar
+        // registers and the records arrive through the scalar cache (s_load_dwordx4), off the
+        // vector-memory path; results are the same ray/record pairs in the same order.
+        const uint32_t kb0 = __builtin_amdgcn_readfirstlane(kb), ke0 = __builtin_amdgcn_readfirstlane(ke);
+        if (__all((kb == kb0) & (ke == ke0)))
+        {
+            // constant address space: uniform loads of memory no store of this kernel touches
+            // (frefs are written by k_origin_pre, an earlier launch) select s_load
+            typedef float vf4 __attribute__((ext_vector_type(4)));
+            typedef const __attribute__((address_space(4))) vf4 cvf4;
+            cvf4 *crefs = (cvf4 *)P.frefs;
+            // software pipeline: record k + 1 is in flight while record k is tested (scalar
+            // loads may return out of order, so the wait for record k sits at its copy, before
+            // the next load is issued)
+            vf4 n0 = crefs[size_t(kb0) * 3], n1 = crefs[size_t(kb0) * 3 + 1], n2 = crefs[size_t(kb0) * 3 + 2];
+            uint32_t k = kb0;
+            if constexpr ((VAR & kVarUnroll) != 0)
+            {
+                // two records per iteration: both first halves (det, 1/det, u) are independent
+                // dependency chains the scheduler interleaves; acceptance stays in list order
+                constexpr bool F = (VAR & kVarFastRcp) != 0;
+                vf4 m0 = n0, m1 = n1, m2 = n2;
+                if (k + 1u < ke0)
+                {
+                    m0 = crefs[size_t(k + 1u) * 3];
+                    m1 = crefs[size_t(k + 1u) * 3 + 1];
+                    m2 = crefs[size_t(k + 1u) * 3 + 2];
+                }
+                for (; k + 1u < ke0; k += 2u)
+                {
+                    const vf4 a0 = n0, a1 = n1, a2 = n2, b0 = m0, b1 = m1, b2 = m2;
+                    if (k + 2u < ke0)
+                    {
+                        n0 = crefs[size_t(k + 2u) * 3];
+                        n1 = crefs[size_t(k + 2u) * 3 + 1];
+                        n2 = crefs[size_t(k + 2u) * 3 + 2];
+                    }
+                    if (k + 3u < ke0)
+                    {
+                        m0 = crefs[size_t(k + 3u) * 3];
+                        m1 = crefs[size_t(k + 3u) * 3 + 1];
+                        m2 = crefs[size_t(k + 3u) * 3 + 2];
+                    }
+                    float ia, ua, ib, ub, va = 0.0f, ta = 0.0f, vb = 0.0f, tb = 0.0f;
+                    const bool oka = rtd::mt_pre_first<F>(dx, dy, dz, a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z,
+                                                          a1.w, a2.x, ia, ua);
+                    const bool okb = rtd::mt_pre_first<F>(dx, dy, dz, b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z,
+                                                          b1.w, b2.x, ib, ub);
+                    bool ha = false, hb = false;
+                    if (__any(oka))
+                        ha = oka & rtd::mt_pre_second(dx, dy, dz, a0.w, a1.x, a1.y, a2.y, a2.z, a2.w, ia, ua, va, ta);
+                    if (__any(okb))
+                        hb = okb & rtd::mt_pre_second(dx, dy, dz, b0.w, b1.x, b1.y, b2.y, b2.z, b2.w, ib, ub, vb, tb);
+                    if (STATS) tests += 2u;
+                    const bool takea = ha & (ta < t) & (ta < nct_ax);
+                    t = takea ? ta : t;
+                    u = takea ? ua : u;
+                    v = takea ? va : v;
+                    tri = takea ? k : tri;
+                    const bool takeb = hb & (tb < t) & (tb < nct_ax);
+                    t = takeb ? tb : t;
+                    u = takeb ? ub : u;
+                    v = takeb ? vb : v;
+                    tri = takeb ? k + 1u : tri;
+                }
+            }
+            for (; k < ke0; k++)
+            {
+                const vf4 r0 = n0, r1 = n1, r2 = n2;
+                if (k + 1u < ke0)
+                {
+                    cvf4 *np = crefs + size_t(k + 1u) * 3;
+                    n0 = np[0];
+                    n1 = np[1];
+                    n2 = np[2];
+                }
+                float ct, cu, cv;
+                const bool hit = rtd::ray_tri_mt_gated_pre<(VAR & kVarFastRcp) != 0>(
+                    dx, dy, dz, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w, ct, cu, cv);
+                if (STATS) tests++;
+                const bool take = hit & (ct < t) & (ct < nct_ax);
+                t = take ? ct : t;
+                u = take ? cu : u;
+                v = take ? cv : v;
+                tri = take ? k : tri;
+            }
+            return t != rtd::kFltMax;
+        }
+    }
         float4 n0, n1, n2;
     if ((VAR & kVarPrefetch) && kb < ke)
     {
@@ -361,7 +462,8 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, const uint32_t 
                                                float ox, float oy, float oz,
                                                float dx, float dy, float dz,
                                                float& t, float& u, float& v, uint32_t& tri,
-                                               uint32_t& voxel, uint32_t& steps, uint32_t& tests)
+                                               uint32_t& voxel, uint32_t& steps, uint32_t& tests,
+                                               bool *bailed = nullptr)
 {
     float nct0, nct1, nct2, dt0, dt1, dt2;
     int rem0, rem1, rem2, cs0, cs1, cs2, cell;
@@ -403,6 +505,7 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, const uint32_t 
         // iterations whatever nct holds -- the P.max_steps bound is kept only in the A/B arm.
         int skip = 0;
         int remp = rem0 | (rem1 << 11) | (rem2 << 22);      // kVarPackedRem only
+        int budget = int(P.bail_tests);                      // kVarBail only
         for (uint32_t iter = 0;; iter++)
         {
             if ((VAR & kVarSelStep) && iter >= P.max_steps) break;
@@ -426,6 +529,20 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, const uint32_t 
                 RT_DDA_ADVANCE_PACKED(nct_ax, more);
             else
                 RT_DDA_ADVANCE_ADD(nct_ax, more);
+            if constexpr ((VAR & kVarBail) != 0)
+            {
+                // two-phase arm: a sample whose walk would pass bail_tests tests stops here and
+                // is re-traced by the wide phase (k_render_bailed); nothing of it is stored
+                if (kb < ke)
+                {
+                    budget -= int(ke - kb);
+                    if (budget < 0)
+                    {
+                        *bailed = true;
+                        return false;
+                    }
+                }
+            }
             if (kb < ke && test_cell<STATS, TRI, VAR>(P, ox, oy, oz, dx, dy, dz, kb, ke, nct_ax, t, u, v, tri, tests))
                 return true;
             if (!more) break;
@@ -597,7 +714,7 @@ __device__ __forceinline__ bool ray_march(const KParams& P, float ox, float oy, 
 template <bool STATS, int TRI, int VAR>
 __device__ __forceinline__ void trace_sample(const KParams& P, const uint32_t *lds_occ, uint32_t px, uint32_t py,
                                              uint32_t s, float& cr, float& cg, float& cb,
-                                             rt_sample_rec *rec)
+                                             rt_sample_rec *rec, bool *bailed = nullptr)
 {
     const float2 so = P.smp[s];
     float dx, dy, dz;
@@ -613,7 +730,7 @@ __device__ __forceinline__ void trace_sample(const KParams& P, const uint32_t *l
     else
     {
         hit = grid_intersect<STATS, TRI, VAR>(P, lds_occ, P.org[0], P.org[1], P.org[2], dx, dy, dz, t, u, v, tri,
-                                              voxel, steps, tests);
+                                              voxel, steps, tests, bailed);
         if ((VAR & kVarOriginPre) && TRI == RT_TRI_MOLLER_TRUMBORE && hit)
             tri = __float_as_uint(P.refs[3 * size_t(tri) + 2].y);     // CSR reference -> triangle id
     }
@@ -687,12 +804,11 @@ struct ItemCoord { TileCoord c; uint32_t p, s, x, y; bool valid; };
 
 // Pixel/sample of this lane in work item `item` (wave-uniform).  Called before AND after the
 // traversal so none of it is live (in VGPRs) across the DDA walk.
-__device__ __forceinline__ ItemCoord item_coord(const KParams& P, uint32_t item, uint32_t lane)
+// Sample slot `slot` (pixel-major, Morton pixel order) of local tile k.
+__device__ __forceinline__ ItemCoord tile_slot_coord(const KParams& P, uint32_t k, uint32_t slot)
 {
     ItemCoord ic;
-    const uint32_t items_per_tile = P.wg_per_tile * (kWG / 64u);
-    ic.c.k = item / items_per_tile;
-    const uint32_t slot = (item - ic.c.k * items_per_tile) * 64u + lane;
+    ic.c.k = k;
     const uint32_t t = P.rank + ic.c.k * P.nranks;
     const uint32_t tyi = t / P.tiles_x;
     ic.c.tx0 = P.rx0 + (t - tyi * P.tiles_x) * kTile;
@@ -705,25 +821,56 @@ __device__ __forceinline__ ItemCoord item_coord(const KParams& P, uint32_t item,
     return ic;
 }
 
+__device__ __forceinline__ ItemCoord item_coord(const KParams& P, uint32_t item, uint32_t lane)
+{
+    const uint32_t items_per_tile = P.wg_per_tile * (kWG / 64u);
+    const uint32_t kseq = item / items_per_tile;              // position in the launch's tile order
+    const uint32_t slot = (item - kseq * items_per_tile) * 64u + lane;
+    return tile_slot_coord(P, P.tile_order ? P.tile_order[kseq] : kseq, slot);   // local tile k
+}
+
 template <int TRI, int VAR>
 __device__ __forceinline__ void process_item(const KParams& P, const uint32_t *lds_occ, uint32_t item)
 {
     item = __builtin_amdgcn_readfirstlane(item);
     const uint32_t lane = threadIdx.x & 63u;
     float cr = 0.0f, cg = 0.0f, cb = 0.0f;
+    bool bailed = false;
     {
         const ItemCoord ic = item_coord(P, item, lane);
         if (ic.valid)
-            trace_sample<false, TRI, VAR>(P, lds_occ, ic.x, ic.y, ic.s, cr, cg, cb, nullptr);
+            trace_sample<false, TRI, VAR>(P, lds_occ, ic.x, ic.y, ic.s, cr, cg, cb, nullptr, &bailed);
     }
     const ItemCoord ic = item_coord(P, item, lane);
     const uint32_t base = lane & ~(P.spp - 1u);
     float sr = 0.0f, sg = 0.0f, sb = 0.0f;
+    bool pixel_bailed = false;
     for (uint32_t k = 0; k < P.spp; k++)
     {
         sr += __shfl(cr, int(base + k), 64);
         sg += __shfl(cg, int(base + k), 64);
         sb += __shfl(cb, int(base + k), 64);
+        if (VAR & kVarBail) pixel_bailed |= __shfl(int(bailed), int(base + k), 64) != 0;
+    }
+    if constexpr ((VAR & kVarBail) != 0)
+    {
+        // a pixel with a bailed sample goes to the wide phase whole (its samples are summed
+        // there, in order); one atomic per wave reserves the queue slots
+        const bool enq = pixel_bailed && ic.valid && ic.s == 0;
+        const uint64_t m = __ballot(enq);
+        if (m)
+        {
+            uint32_t base_q = 0u;
+            if (lane == uint32_t(__builtin_ctzll(m))) base_q = atomicAdd(P.bail_count, uint32_t(__popcll(m)));
+            base_q = __shfl(base_q, int(__builtin_ctzll(m)), 64);
+            if (enq)
+            {
+                const uint32_t r = uint32_t(__builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32),
+                                                                      __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u)));
+                P.bail_queue[base_q + r] = (ic.c.k << 8) | ic.p;
+            }
+        }
+        if (pixel_bailed) return;
     }
     if (ic.valid && ic.s == 0)
     {
@@ -742,6 +889,11 @@ __device__ __forceinline__ void process_item(const KParams& P, const uint32_t *l
 // A bijection on [0, nblocks) for any grid size (the tail past whole 8-turn rounds keeps its
 // order); on a device with another XCD count only the locality changes.
 constexpr uint32_t kXcds = 8;
+constexpr uint32_t kWideG = 4;              // RT_KERNEL_WIDE: lanes per sample
+constexpr uint32_t kBailTests = 256;        // BAIL_WIDE: default phase-1 test budget per sample
+constexpr uint32_t kBailAutoRanks = 8;      // AUTO: two-phase arm from this many shard ranks ...
+constexpr uint32_t kBailAutoRefs = 128;     // ... on scenes with a cell this dense
+constexpr uint32_t kBailAutoTests = 128;    // ... with this budget (best of 128 / 256 / 512 at 8 ranks)
 __device__ __forceinline__ uint32_t xcd_band_block(uint32_t b, uint32_t nb, uint32_t chunk)
 {
     if (chunk == 0u)
@@ -762,7 +914,217 @@ template <int TRI, int VAR>
 __global__ void __launch_bounds__(kWG) k_render_lanes(KParams P)
 {
     const uint32_t b = (VAR & kVarXcdBands) ? xcd_band_block(blockIdx.x, gridDim.x, P.xcd_chunk) : blockIdx.x;
-    process_item<TRI, VAR>(P, nullptr, b * (kWG / 64u) + (threadIdx.x >> 6));
+    const uint32_t item = b * (kWG / 64u) + (threadIdx.x >> 6);
+    if (VAR & kVarWaveClock)
+    {
+        // debug arm (RT_KERNEL_FLAG_WAVE_CLOCK): s_memtime at the item's start and end
+        const uint64_t t0 = __builtin_amdgcn_s_memtime();
+        process_item<TRI, VAR>(P, nullptr, item);
+        const uint64_t t1 = __builtin_amdgcn_s_memtime();
+        if ((threadIdx.x & 63u) == 0u)
+        {
+            P.wave_clk[2 * size_t(item)] = t0;
+            P.wave_clk[2 * size_t(item) + 1] = t1;
+        }
+    }
+    else
+        process_item<TRI, VAR>(P, nullptr, item);
+}
+
+// RT_KERNEL_WIDE (AUTO's record layout, spp a power of two <= 64 / G): G lanes per sample.
+// The heaviest waves of a frame (killeroo's body, scene 5's cat) run ~1000 triangle tests per
+// lane in a serial chain -- ~1M cycles per wave, the launch's critical path once a rank renders
+// 1/8 of the frame.  Here the G lanes of a group walk the same ray (identical state, so
+// identical control flow) and split each cell's list: sublane j tests references kb + j,
+// kb + j + G, ... with strict '<' in ascending order, and a butterfly over the group takes the
+// lexicographic minimum of (t, k) -- the first minimum in list order, exactly what
+// grid.cpp:258-266 keeps.  The chain per lane shrinks by G; the DDA walk is repeated G times.
+// One sample of the wide mode, traced by the G lanes of a group (sub = this lane's index in it):
+// the same walk in every lane of the group, each cell's list split over the group.  Returns the
+// sample's colour in every lane of the group.
+template <int VAR, int G>
+__device__ __forceinline__ void wide_trace(const KParams& P, uint32_t k, uint32_t slot, uint32_t sub, float& cr,
+                                           float& cg, float& cb)
+{
+    static_assert((VAR & kVarOriginPre) && (VAR & kVarDistSkip) && (VAR & kVarPackedRem), "AUTO layout");
+    const float ox = P.org[0], oy = P.org[1], oz = P.org[2];
+    cr = cg = cb = 0.0f;
+    {
+        const ItemCoord ic = tile_slot_coord(P, k, slot);
+        if (ic.valid)
+        {
+            const float2 so = P.smp[ic.s];
+            float dx, dy, dz;
+            rtd::gen_dir(P.m, P.fov_xs, P.aspect, ic.x, ic.y, P.W, P.H, so.x, so.y, dx, dy, dz);
+            float nct0, nct1, nct2, dt0, dt1, dt2;
+            int rem0, rem1, rem2, cs0, cs1, cs2, cell;
+            bool hit = false;
+            float t = rtd::kFltMax, u = 0.0f, v = 0.0f;
+            uint32_t tri = 0u;
+            if (dda_setup(P, ox, oy, oz, dx, dy, dz, nct0, nct1, nct2, dt0, dt1, dt2, rem0, rem1, rem2, cs0, cs1,
+                          cs2, cell))
+            {
+                int skip = 0;
+                int remp = rem0 | (rem1 << 11) | (rem2 << 22);
+                for (;;)
+                {
+                    uint32_t kb = 0u, ke = 0u;
+                    if (skip == 0)
+                    {
+                        const uint32_t w = P.cellw[uint32_t(cell)];
+                        const uint32_t cnt = w & 2047u;
+                        kb = w >> 11;
+                        ke = kb + cnt;
+                        skip = cnt ? 0 : int(kb) - 1;
+                    }
+                    else
+                        skip--;
+                    float nct_ax;
+                    bool more;
+                    RT_DDA_ADVANCE_PACKED(nct_ax, more);
+                    if (kb < ke)
+                    {
+                        float bt = rtd::kFltMax, bu = 0.0f, bv = 0.0f;
+                        uint32_t bk = 0xFFFFFFFFu;
+                        for (uint32_t k = kb + sub; k < ke; k += uint32_t(G))
+                        {
+                            const float4 *rp = P.frefs + size_t(k) * 3;
+                            const float4 r0 = rp[0], r1 = rp[1], r2 = rp[2];
+                            float ct, cu, cv;
+                            const bool h = rtd::ray_tri_mt_gated_pre<(VAR & kVarFastRcp) != 0>(
+                                dx, dy, dz, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w,
+                                ct, cu, cv);
+                            const bool take = h & (ct < bt) & (ct < nct_ax);
+                            bt = take ? ct : bt;
+                            bu = take ? cu : bu;
+                            bv = take ? cv : bv;
+                            bk = take ? k : bk;
+                        }
+                        for (int m = 1; m < G; m <<= 1)
+                        {
+                            const float ot = __shfl_xor(bt, m, 64), ou = __shfl_xor(bu, m, 64),
+                                        ov = __shfl_xor(bv, m, 64);
+                            const uint32_t ok = uint32_t(__shfl_xor(int(bk), m, 64));
+                            const bool better = (ot < bt) | ((ot == bt) & (ok < bk));
+                            bt = better ? ot : bt;
+                            bu = better ? ou : bu;
+                            bv = better ? ov : bv;
+                            bk = better ? ok : bk;
+                        }
+                        if (bt != rtd::kFltMax)
+                        {
+                            t = bt;
+                            u = bu;
+                            v = bv;
+                            tri = bk;
+                            hit = true;
+                            break;
+                        }
+                    }
+                    if (!more) break;
+                }
+            }
+            if (hit)
+            {
+                tri = __float_as_uint(P.refs[3 * size_t(tri) + 2].y);     // CSR reference -> triangle id
+                const float4 a = P.shade[3 * tri + 0], bb = P.shade[3 * tri + 1], c = P.shade[3 * tri + 2];
+                rtd::shade_hit(u, v, a, bb, c, cr, cg, cb);
+            }
+            else
+                cr = cg = cb = float(ic.y) / float(P.H);                   // renderer.cpp:159
+            (void)t;
+        }
+    }
+}
+
+// One wave of the wide mode: the 64 / G consecutive sample slots slot0 .. of local tile k.
+template <int VAR, int G>
+__device__ __forceinline__ void wide_samples(const KParams& P, uint32_t k, uint32_t slot0)
+{
+    const uint32_t lane = threadIdx.x & 63u, sub = lane & uint32_t(G - 1), grp = lane / uint32_t(G);
+    const uint32_t slot = slot0 + grp;
+    float cr, cg, cb;
+    wide_trace<VAR, G>(P, k, slot, sub, cr, cg, cb);
+    // the pixel's samples are the groups grp0 .. grp0 + spp - 1 of this wave: sum in sample order
+    const ItemCoord ic = tile_slot_coord(P, k, slot);
+    const uint32_t grp0 = grp & ~(P.spp - 1u);
+    float sr = 0.0f, sg = 0.0f, sb = 0.0f;
+    for (uint32_t j = 0; j < P.spp; j++)
+    {
+        const int src = int((grp0 + j) * uint32_t(G));
+        sr += __shfl(cr, src, 64);
+        sg += __shfl(cg, src, 64);
+        sb += __shfl(cb, src, 64);
+    }
+    if (ic.valid && ic.s == 0 && sub == 0)
+    {
+        const uint32_t word = rtd::pack_bgra8(rtd::gamma_half(average(P, sr)), rtd::gamma_half(average(P, sg)),
+                                              rtd::gamma_half(average(P, sb)));
+        store_pixel(P, ic.c, ic.p, ic.x, ic.y, word);
+    }
+}
+
+// RT_KERNEL_WIDE: every tile in wide mode (the A/B arm of the hybrid below)
+template <int VAR, int G>
+__global__ void __launch_bounds__(kWG) k_render_wide(KParams P)
+{
+    const uint32_t b = (VAR & kVarXcdBands) ? xcd_band_block(blockIdx.x, gridDim.x, P.xcd_chunk) : blockIdx.x;
+    const uint32_t witem = __builtin_amdgcn_readfirstlane(b * (kWG / 64u) + (threadIdx.x >> 6));
+    const uint32_t per_tile = kTilePix * P.spp;                       // sample slots per tile
+    const uint32_t g = witem * (64u / uint32_t(G));                   // first slot, launch order
+    const uint32_t kseq = g / per_tile;
+    wide_samples<VAR, G>(P, P.tile_order ? P.tile_order[kseq] : kseq, g - kseq * per_tile);
+}
+
+// RT_KERNEL_FLAG_BAIL_WIDE, phase 1: the AUTO kernel with the test budget, held to 8 waves/SIMD
+template <int VAR>
+__global__ void __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(8, 8))) k_render_bail1(KParams P)
+{
+    const uint32_t b = (VAR & kVarXcdBands) ? xcd_band_block(blockIdx.x, gridDim.x, P.xcd_chunk) : blockIdx.x;
+    process_item<RT_TRI_MOLLER_TRUMBORE, VAR>(P, nullptr, b * (kWG / 64u) + (threadIdx.x >> 6));
+}
+
+// RT_KERNEL_FLAG_BAIL_WIDE, phase 2 (AUTO, spp <= 16).  Phase 1 is the AUTO kernel with a test
+// budget: a sample whose walk would pass bail_tests triangle tests stops, and its pixel goes to
+// bail_queue instead of the frame.  Those are the samples that made the frame's critical path
+// (~1000 serial tests per lane in the densest tiles).  This kernel re-traces the queued pixels
+// from the start in the wide mode: kWideG lanes per sample split every cell's list, so each
+// lane's chain is a quarter long, and the pixel's samples are summed in order as in phase 1.
+// Persistent waves take queue entries round-robin; every pixel is stored by exactly one phase.
+template <int VAR>
+__global__ void __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(8, 8))) k_render_bailed(KParams P)
+{
+    const uint32_t n = *P.bail_count;                                // phase 1 finished on this stream
+    const uint32_t lpp = P.spp * kWideG;                             // lanes per pixel (<= 64)
+    const uint32_t per_wave = 64u / lpp;
+    const uint32_t lane = threadIdx.x & 63u, g = lane / lpp, r = lane - g * lpp;
+    const uint32_t smp = r / kWideG, sub = r - smp * kWideG;
+    const uint32_t nwaves = gridDim.x * (kWG / 64u);
+    for (uint32_t e0 = (blockIdx.x * (kWG / 64u) + (threadIdx.x >> 6)) * per_wave; e0 < n; e0 += nwaves * per_wave)
+    {
+        const uint32_t e = e0 + g;
+        const bool live = e < n;
+        const uint32_t q = live ? P.bail_queue[e] : 0u;
+        const uint32_t k = q >> 8, p = q & 255u;
+        float cr = 0.0f, cg = 0.0f, cb = 0.0f;
+        if (live) wide_trace<VAR, kWideG>(P, k, p * P.spp + smp, sub, cr, cg, cb);
+        float sr = 0.0f, sg = 0.0f, sb = 0.0f;
+        for (uint32_t j = 0; j < P.spp; j++)
+        {
+            const int src = int(g * lpp + j * kWideG);
+            sr += __shfl(cr, src, 64);
+            sg += __shfl(cg, src, 64);
+            sb += __shfl(cb, src, 64);
+        }
+        if (live && r == 0u)
+        {
+            const ItemCoord ic = tile_slot_coord(P, k, p * P.spp);
+            const uint32_t word = rtd::pack_bgra8(rtd::gamma_half(average(P, sr)),
+                                                  rtd::gamma_half(average(P, sg)),
+                                                  rtd::gamma_half(average(P, sb)));
+            store_pixel(P, ic.c, ic.p, ic.x, ic.y, word);
+        }
+    }
 }
 
 // RT_KERNEL_PERSISTENT (spp a power of two <= 64): persistent 512-lane workgroups, 4 per CU.  The
@@ -1258,7 +1620,7 @@ struct rt_scene
     std::mutex mtx;
     uint32_t dims[3] = { 0, 0, 0 };
     float bmin[3], bmax[3], cw = 0, icw = 0;
-    uint32_t ncells = 0, nrefs = 0, ntris = 0, occ_words = 0;
+    uint32_t ncells = 0, nrefs = 0, ntris = 0, occ_words = 0, max_cell_refs = 0;
     uint32_t *d_off = nullptr, *d_occ = nullptr, *d_cellw = nullptr;
     float4 *d_refs = nullptr, *d_shade = nullptr, *d_facen = nullptr, *d_frefs = nullptr;
     float4 *d_trimt = nullptr, *d_tridist = nullptr, *d_distblk = nullptr;
@@ -1270,6 +1632,12 @@ struct rt_scene
     uint32_t compact_wgs = 2048;    // RT_KERNEL_COMPACT grid: 8 x 256-lane workgroups per CU
     bool rcp_safe = false;          // every |det| of the ray/tri test is far below 2^126 (FAST_RCP)
     bool pack_ok = false;           // dims <= 512: the remaining-cell counts pack into one word
+    uint32_t *d_bail = nullptr;     // RT_KERNEL_FLAG_BAIL_WIDE: queued-pixel count + queue
+    size_t bail_cap = 0;
+    uint32_t bail_wgs = 1024;       // phase-2 persistent grid: 4 workgroups per CU
+    uint64_t *d_clk = nullptr;      // RT_KERNEL_FLAG_WAVE_CLOCK records of the last such launch
+    size_t clk_cap = 0;
+    uint32_t clk_items = 0;
     // sample table cache
     float2 *d_smp = nullptr;
     uint32_t smp_cap = 0;
@@ -1332,12 +1700,13 @@ int validate_frame(const rt_frame *f)
     if (f->intersector > RT_ISECT_RAY_MARCH) return fail(RT_E_INVALID, "unknown intersector");
     if (f->intersector == RT_ISECT_BRUTE_FORCE && f->tri_test != RT_TRI_MOLLER_TRUMBORE)
         return fail(RT_E_INVALID, "IntersectBruteForce uses IntersectRayTri only (renderer.cpp:176)");
-    if ((f->kernel & 0xFFu) > RT_KERNEL_PERSISTENT ||
+    if ((f->kernel & 0xFFu) > RT_KERNEL_WIDE ||
         (f->kernel & ~(0xFFu | RT_KERNEL_FLAG_PREFETCH | RT_KERNEL_FLAG_WAVE_GATE | RT_KERNEL_FLAG_LOOKAHEAD |
                        RT_KERNEL_FLAG_CSR_OFFSETS | RT_KERNEL_FLAG_DIST_SKIP | RT_KERNEL_FLAG_NESTED_STEP |
                        RT_KERNEL_FLAG_PRE_GATE | RT_KERNEL_FLAG_EXHAUSTIVE | RT_KERNEL_FLAG_ORIGIN_PRE |
                        RT_KERNEL_FLAG_SELECT_STEP | RT_KERNEL_FLAG_FAST_RCP | RT_KERNEL_FLAG_PACKED_REM |
-                       RT_KERNEL_FLAG_XCD_BANDS |
+                       RT_KERNEL_FLAG_XCD_BANDS | RT_KERNEL_FLAG_UNROLL_PAIRS | RT_KERNEL_FLAG_WAVE_CLOCK |
+                       RT_KERNEL_FLAG_UNIFORM_CELLS | RT_KERNEL_FLAG_BAIL_WIDE |
                        RT_KERNEL_COMPACT_REFILL_MASK)))
         return fail(RT_E_INVALID, "unknown kernel");
     const uint32_t spp = std::max(1u, f->spp);
@@ -1400,6 +1769,12 @@ void frame_params(const rt_scene *s, const rt_frame *f, KParams& P)
     P.ntris = s->ntris;
     P.tri_test = f->tri_test;
     P.isect = f->intersector;
+    P.tile_order = nullptr;
+    P.bail_tests = 0;
+    P.bail_count = nullptr;
+    P.bail_queue = nullptr;
+    P.wave_clk = nullptr;
+    P.xcd_chunk = 0;
 }
 
 bool use_lanes(const rt_frame *f, uint32_t spp)
@@ -1432,10 +1807,10 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
     // reciprocal + packed remaining-cell counts (the last two where the scene allows them) +
     // XCD row interleave: fastest arm of tools/ab_kernels.py on MI355X (scenes 1/2/4/5/7/8,
     // 1080p x 4spp).  RT_KERNEL_COMPACT runs the same per-ray code as AUTO.
-    const uint32_t fk = (kind == RT_KERNEL_AUTO || kind == RT_KERNEL_COMPACT)
+    const uint32_t fk = (kind == RT_KERNEL_AUTO || kind == RT_KERNEL_COMPACT || kind == RT_KERNEL_WIDE)
                             ? (f->kernel | RT_KERNEL_LANES | RT_KERNEL_FLAG_WAVE_GATE | RT_KERNEL_FLAG_DIST_SKIP |
                                RT_KERNEL_FLAG_ORIGIN_PRE | RT_KERNEL_FLAG_FAST_RCP | RT_KERNEL_FLAG_PACKED_REM |
-                               RT_KERNEL_FLAG_XCD_BANDS)
+                               RT_KERNEL_FLAG_XCD_BANDS | RT_KERNEL_FLAG_UNIFORM_CELLS)
                             : f->kernel;
     if ((fk & RT_KERNEL_FLAG_ORIGIN_PRE) && lanes && P.isect == RT_ISECT_GRID &&
         P.tri_test == RT_TRI_MOLLER_TRUMBORE && s->nrefs)
@@ -1451,10 +1826,62 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
                     ((fk & RT_KERNEL_FLAG_SELECT_STEP) ? kVarSelStep : 0) |
                     ((fk & RT_KERNEL_FLAG_FAST_RCP) && s->rcp_safe ? kVarFastRcp : 0) |
                     ((fk & RT_KERNEL_FLAG_PACKED_REM) && s->pack_ok ? kVarPackedRem : 0) |
-                    ((fk & RT_KERNEL_FLAG_XCD_BANDS) ? kVarXcdBands : 0);
+                    ((fk & RT_KERNEL_FLAG_XCD_BANDS) ? kVarXcdBands : 0) |
+                    ((fk & RT_KERNEL_FLAG_UNROLL_PAIRS) ? kVarUnroll : 0) |
+                    ((fk & RT_KERNEL_FLAG_WAVE_CLOCK) ? kVarWaveClock : 0) |
+                    ((fk & RT_KERNEL_FLAG_UNIFORM_CELLS) ? kVarUniform : 0);
+    if (var & kVarWaveClock)
+    {
+        const size_t need = size_t(blocks) * (kWG / 64u) * 2u;
+        if (need > s->clk_cap)
+        {
+            if (s->d_clk) RT_HIP(hipFree(s->d_clk));
+            s->d_clk = nullptr;
+            RT_HIP(hipMalloc(&s->d_clk, need * sizeof(uint64_t)));
+            s->clk_cap = need;
+        }
+        s->clk_items = uint32_t(need / 2u);
+        P.wave_clk = s->d_clk;
+    }
     const bool bary = P.tri_test == RT_TRI_BARYCENTRIC;
     const dim3 wg(kWG);
-    if (lanes && kind == RT_KERNEL_COMPACT && P.isect == RT_ISECT_GRID)
+    // AUTO takes the two-phase arm for a shard of >= 8 ranks of a scene with dense cells: there a
+    // rank's launch is bound by its few ~1000-test waves, which the wide phase shortens 4x
+    // (measured, tools/shard_scaling.py: killeroo rank of 8 0.46 -> 0.31 ms, scene 5 0.68 -> 0.38,
+    // head 0.29 -> 0.20); on a whole frame, or a scene without dense cells, the phase-1 budget
+    // check costs more than it saves (Cornell +40 %, killeroo 1 GPU +45 %).
+    const bool bail_auto = kind == RT_KERNEL_AUTO && P.nranks >= kBailAutoRanks && s->max_cell_refs >= kBailAutoRefs;
+    if (((f->kernel & RT_KERNEL_FLAG_BAIL_WIDE) || bail_auto) && lanes &&
+        (kind == RT_KERNEL_AUTO || kind == RT_KERNEL_LANES) && P.isect == RT_ISECT_GRID && !bary &&
+        (var == 14858 || var == 80394) && P.spp * kWideG <= 64u)
+    {
+        const size_t need = size_t(n_local_tiles) * kTilePix + 1u;   // count + one entry per pixel
+        if (need > s->bail_cap)
+        {
+            // grows once per larger frame; the steady state allocates nothing
+            if (s->d_bail) RT_HIP(hipFree(s->d_bail));
+            s->d_bail = nullptr;
+            RT_HIP(hipMalloc(&s->d_bail, sizeof(uint32_t) * need));
+            s->bail_cap = need;
+        }
+        const uint32_t tb = (f->kernel & RT_KERNEL_COMPACT_REFILL_MASK) >> RT_KERNEL_COMPACT_REFILL_SHIFT;
+        P.bail_tests = tb ? 16u * tb : (bail_auto && !(f->kernel & RT_KERNEL_FLAG_BAIL_WIDE) ? kBailAutoTests : kBailTests);
+        P.bail_count = s->d_bail;
+        P.bail_queue = s->d_bail + 1;
+        RT_HIP(hipMemsetAsync(s->d_bail, 0, sizeof(uint32_t), st));
+        if (var == 80394)
+            hipLaunchKernelGGL((k_render_bail1<80394 | kVarBail>), dim3(uint32_t(blocks)), wg, 0, st, P);
+        else
+            hipLaunchKernelGGL((k_render_bail1<14858 | kVarBail>), dim3(uint32_t(blocks)), wg, 0, st, P);
+        hipLaunchKernelGGL((k_render_bailed<14858>), dim3(s->bail_wgs), wg, 0, st, P);
+    }
+    else if (lanes && kind == RT_KERNEL_WIDE && P.isect == RT_ISECT_GRID && !bary && (var == 14858 || var == 80394) &&
+        P.spp * kWideG <= 64u)
+    {
+        P.xcd_chunk *= kWideG;
+        hipLaunchKernelGGL((k_render_wide<14858, kWideG>), dim3(uint32_t(blocks) * kWideG), wg, 0, st, P);
+    }
+    else if (lanes && kind == RT_KERNEL_COMPACT && P.isect == RT_ISECT_GRID)
     {
         const uint32_t n_items = uint32_t(blocks * (kWG / 64u));
         uint32_t refill = (f->kernel & RT_KERNEL_COMPACT_REFILL_MASK) >> RT_KERNEL_COMPACT_REFILL_SHIFT;
@@ -1511,10 +1938,17 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
         else if (var == 4618) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 4618>), grid, wg, 0, st, P);
         else if (var == 6666) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 6666>), grid, wg, 0, st, P);
         else if (var == 14858) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 14858>), grid, wg, 0, st, P);
+        else if (var == 96778) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 96778>), grid, wg, 0, st, P);
+        else if (var == 47626) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 47626>), grid, wg, 0, st, P);
+        else if (var == 80394) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 80394>), grid, wg, 0, st, P);
+        else if (var == 113162) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 113162>), grid, wg, 0, st, P);
         // AUTO on scenes outside the FAST_RCP / PACKED_REM ranges
         else if (var == 8714) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 8714>), grid, wg, 0, st, P);
         else if (var == 10762) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 10762>), grid, wg, 0, st, P);
         else if (var == 12810) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 12810>), grid, wg, 0, st, P);
+        else if (var == 74250) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 74250>), grid, wg, 0, st, P);
+        else if (var == 76298) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 76298>), grid, wg, 0, st, P);
+        else if (var == 78346) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 78346>), grid, wg, 0, st, P);
         else                hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 0>), grid, wg, 0, st, P);
     }
     else if (P.isect == RT_ISECT_RAY_MARCH && (f->kernel & RT_KERNEL_FLAG_EXHAUSTIVE))
@@ -1612,6 +2046,7 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
     s->device = device;
     s->persist_wgs = 4u * uint32_t(std::max(1, ncus));
     s->compact_wgs = 8u * uint32_t(std::max(1, ncus));
+    s->bail_wgs = 4u * uint32_t(std::max(1, ncus));
     for (int a = 0; a < 3; a++)
     {
         s->dims[a] = g.dims[a];
@@ -1710,7 +2145,10 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
     s->occ_words = (nc + 31) / 32;
     std::vector<uint32_t> occ(s->occ_words, 0);
     for (uint32_t c = 0; c < nc; c++)
+    {
         if (g.cell_offsets[c + 1] != g.cell_offsets[c]) occ[c >> 5] |= 1u << (c & 31);
+        s->max_cell_refs = std::max(s->max_cell_refs, g.cell_offsets[c + 1] - g.cell_offsets[c]);
+    }
 
     RT_HIP(hipMalloc(&s->d_off, sizeof(uint32_t) * (nc + 1)));
     RT_HIP(hipMalloc(&s->d_refs, sizeof(float4) * refs.size()));
@@ -1821,6 +2259,8 @@ int rt_scene_destroy(rt_scene *s)
         (void)hipFree(s->d_trimt);
         (void)hipFree(s->d_tridist);
         (void)hipFree(s->d_distblk);
+        (void)hipFree(s->d_clk);
+        (void)hipFree(s->d_bail);
         (void)hipFree(s->d_smp);
         (void)hipFree(s->d_frame);
         if (s->h_smp_pinned) (void)hipHostFree(s->h_smp_pinned);
@@ -1995,6 +2435,19 @@ int rt_trace_samples(rt_scene *s, const rt_frame *f, uint32_t x0, uint32_t y0, u
     if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
     (void)hipFree(d_rec);
     if (e != hipSuccess) return fail(RT_E_HIP, std::string("rt_trace_samples: ") + hipGetErrorString(e));
+    return RT_OK;
+}
+
+int rt_debug_wave_clocks(rt_scene *s, uint64_t *out, uint32_t max_items, uint32_t *n_items)
+{
+    if (!s || !n_items) return fail(RT_E_INVALID, "NULL argument");
+    std::lock_guard<std::mutex> lk(s->mtx);
+    int rc;
+    if ((rc = ensure_device(s))) return rc;
+    *n_items = s->clk_items;
+    if (!out || !s->d_clk) return RT_OK;
+    RT_HIP(hipDeviceSynchronize());
+    RT_HIP(hipMemcpy(out, s->d_clk, sizeof(uint64_t) * 2 * std::min(max_items, s->clk_items), hipMemcpyDeviceToHost));
     return RT_OK;
 }
 

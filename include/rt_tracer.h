@@ -89,6 +89,8 @@ enum rt_kernel {
                                   compaction: finished lanes are refilled with new samples by
                                   ballot + prefix count (grid intersector; else = LANES) */
     RT_KERNEL_PERSISTENT = 4,  /* LANES in persistent workgroups with the LDS cell-occupancy bitmap */
+    RT_KERNEL_WIDE = 5,        /* AUTO's per-ray code with 4 lanes per sample splitting every cell's
+                                  triangle list (spp <= 16; else = AUTO) */
     RT_KERNEL_FLAG_PREFETCH = 0x100,  /* OR-able: software-pipelined triangle record loads */
     RT_KERNEL_FLAG_WAVE_GATE = 0x200, /* OR-able: skip a test's second half when no lane needs it */
     RT_KERNEL_FLAG_LOOKAHEAD = 0x400, /* OR-able: load the next cell's CSR offsets one step ahead */
@@ -115,10 +117,22 @@ enum rt_kernel {
                                              cell counts in one guarded word (dims <= 512) */
     RT_KERNEL_FLAG_XCD_BANDS = 0x100000,  /* OR-able: XCD-aware block order, each of the 8 XCDs
                                              renders one contiguous band of tiles (L2 locality) */
+    RT_KERNEL_FLAG_UNROLL_PAIRS = 0x200000, /* OR-able (with UNIFORM_CELLS): the scalar loop tests
+                                               two records per iteration, interleaved */
+    RT_KERNEL_FLAG_WAVE_CLOCK = 0x400000, /* OR-able, debug: record s_memtime {start, end} of
+                                             every 64-sample work item (rt_debug_wave_clocks) */
+    RT_KERNEL_FLAG_UNIFORM_CELLS = 0x800000, /* OR-able (AUTO's record layout): a cell list shared
+                                                by every testing lane of the wave runs as a scalar
+                                                loop over scalar-cache record loads */
     RT_KERNEL_COMPACT_REFILL_SHIFT = 24,  /* RT_KERNEL_COMPACT: bits 24-30 = lanes that must be
                                              idle before a wave refills (1..64; 0 = default 48) */
     RT_KERNEL_COMPACT_REFILL_MASK = 0x7F000000,
 };
+/* OR-able (AUTO/LANES, grid, Moller-Trumbore, spp <= 16): two-phase frame.  Samples whose walk
+   would pass a triangle-test budget (bits 24-30 x 16, 0 = 256) stop; their pixels are re-traced
+   by a second kernel with 4 lanes per sample splitting each cell's list.  Bit 31 (not an enum
+   constant: it does not fit a C int). */
+#define RT_KERNEL_FLAG_BAIL_WIDE 0x80000000u
 
 /* Per-frame parameters: what Renderer::RenderTile reads from the Scene and itself. */
 typedef struct rt_frame {
@@ -219,6 +233,9 @@ int  rt_debug_primitives(int kind, const float *in, uint32_t n, float *out, int 
    correctly rounded 1.0f / x for all 2^32 - 2^24 finite nonzero floats; bad_by_exponent[256]
    receives the mismatch count per biased exponent. */
 int  rt_debug_rcp_check(uint64_t *bad_by_exponent, int device);
+/* {start, end} shader-clock pairs of the last RT_KERNEL_FLAG_WAVE_CLOCK launch on this scene,
+   one per 64-sample work item in launch item order; *n_items = how many the launch wrote. */
+int  rt_debug_wave_clocks(rt_scene *s, uint64_t *out, uint32_t max_items, uint32_t *n_items);
 
 /* Hammersley table the library uses when rt_frame.sample_offsets is NULL. */
 int  rt_sample_table(uint32_t spp, float *out_xy);

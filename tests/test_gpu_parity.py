@@ -169,18 +169,66 @@ def test_newton_reciprocal_exhaustive():
 
 
 def test_auto_equals_plain_arms(golden, scenes):
-    """AUTO (Newton reciprocal + packed counts + XCD row interleave) and the plain-division /
-    unpacked / dispatch-order arms render the same bytes as the reference on the two bench
-    scenes and the densest one."""
+    """AUTO (Newton reciprocal + packed counts + XCD row interleave + uniform-cell scalar loop)
+    and the plain-division / unpacked / dispatch-order / unrolled arms, the wide kernel (4 lanes
+    per sample) and the two-phase arm (budgets 256 and 64: many pixels re-traced) render the
+    same bytes as the reference on the two bench scenes and the densest one."""
     base = (rtm.RT_KERNEL_LANES | rtm.RT_KERNEL_FLAG_WAVE_GATE | rtm.RT_KERNEL_FLAG_DIST_SKIP |
             rtm.RT_KERNEL_FLAG_ORIGIN_PRE)
     for sid in (1, 5, 8):
         hs, gs = scenes(sid)
         want = golden["frames_1080p4"][str(sid)]["bgra_sha256"]
+        full = (base | rtm.RT_KERNEL_FLAG_FAST_RCP | rtm.RT_KERNEL_FLAG_PACKED_REM | rtm.RT_KERNEL_FLAG_XCD_BANDS)
         for k in (base, base | rtm.RT_KERNEL_FLAG_FAST_RCP, base | rtm.RT_KERNEL_FLAG_PACKED_REM,
-                  base | rtm.RT_KERNEL_FLAG_SELECT_STEP, base | rtm.RT_KERNEL_FLAG_XCD_BANDS):
+                  base | rtm.RT_KERNEL_FLAG_SELECT_STEP, base | rtm.RT_KERNEL_FLAG_XCD_BANDS,
+                  full | rtm.RT_KERNEL_FLAG_UNIFORM_CELLS,
+                  full | rtm.RT_KERNEL_FLAG_UNIFORM_CELLS | rtm.RT_KERNEL_FLAG_UNROLL_PAIRS,
+                  rtm.RT_KERNEL_WIDE, rtm.RT_KERNEL_FLAG_BAIL_WIDE, rtm.RT_KERNEL_FLAG_BAIL_WIDE | (4 << 24)):
             img = gs.render_frame(gs.frame(1920, 1080, 4, kernel=k))
             assert hashlib.sha256(img.tobytes()).hexdigest() == want, (sid, hex(k))
+
+
+@pytest.mark.parametrize("spp", [1, 2, 4, 16, 32])
+def test_wide_and_two_phase_vs_oracle(scenes, oracle, spp):
+    """Wide kernel and two-phase arm on ragged frames at every spp they take (32 falls back to
+    AUTO), budget 16 tests so most pixels go through the wide phase."""
+    hs, gs = scenes(5)
+    exp, _, _ = oracle.render(5, 97, 61, spp)
+    for k in (rtm.RT_KERNEL_WIDE, rtm.RT_KERNEL_FLAG_BAIL_WIDE | (1 << 24)):
+        np.testing.assert_array_equal(gs.render_frame(gs.frame(97, 61, spp, kernel=k)), exp, err_msg=hex(k))
+
+
+@pytest.mark.parametrize("sid,nranks", [(8, 8), (5, 8), (8, 3), (4, 16)])
+def test_shard_partition_dense_scenes(golden, scenes, sid, nranks):
+    """Shards of >= 8 ranks of a dense scene take AUTO's two-phase arm; every partition
+    reassembles into the reference frame."""
+    import torch
+    hs, gs = scenes(sid)
+    W, H = 1920, 1080
+    f = gs.frame(W, H, 4)
+    e = rtm.shard_elems(W, H, nranks)
+    gathered = torch.zeros(nranks * e, dtype=torch.int32, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    for r in range(nranks):
+        gs.render_shard_device(f, r, nranks, gathered.data_ptr() + 4 * r * e, stream)
+    out = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+    rtm.unshard_device(W, H, nranks, gathered.data_ptr(), out.data_ptr(), stream)
+    torch.cuda.synchronize()
+    img = out.cpu().numpy().view(np.uint32)
+    assert hashlib.sha256(img.tobytes()).hexdigest() == golden["frames_1080p4"][str(sid)]["bgra_sha256"]
+
+
+def test_wave_clock_debug_arm(scenes):
+    """RT_KERNEL_FLAG_WAVE_CLOCK records {start, end} per work item and leaves the frame alone."""
+    hs, gs = scenes(1)
+    f0 = gs.frame(160, 120, 4)
+    f1 = gs.frame(160, 120, 4, kernel=(rtm.RT_KERNEL_LANES | rtm.RT_KERNEL_FLAG_WAVE_GATE | rtm.RT_KERNEL_FLAG_DIST_SKIP |
+                                         rtm.RT_KERNEL_FLAG_ORIGIN_PRE | rtm.RT_KERNEL_FLAG_FAST_RCP |
+                                         rtm.RT_KERNEL_FLAG_PACKED_REM | rtm.RT_KERNEL_FLAG_XCD_BANDS |
+                                         rtm.RT_KERNEL_FLAG_WAVE_CLOCK))
+    np.testing.assert_array_equal(gs.render_frame(f1), gs.render_frame(f0))
+    clk = gs.wave_clocks()
+    assert clk.shape == (10 * 8 * 16, 2) and (clk[:, 1] >= clk[:, 0]).all() and clk[:, 0].any()
 
 
 def test_head_4096x4096x16(golden, scenes):
