@@ -82,7 +82,9 @@ enum rt_intersector {
 };
 
 enum rt_kernel {
-    RT_KERNEL_AUTO = 0,        /* the fastest measured variant for the frame's spp */
+    RT_KERNEL_AUTO = 0,        /* the fastest measured variant for the frame's spp (LANES + WAVE_GATE
+                                  + DIST_SKIP + ORIGIN_PRE + FAST_RCP + PACKED_REM + XCD_BANDS +
+                                  UNIFORM_CELLS; BAIL_WIDE for >= 8-rank shards of dense scenes) */
     RT_KERNEL_LANES = 1,       /* one lane per sample, a pixel's samples in adjacent lanes */
     RT_KERNEL_PIXEL_LOOP = 2,  /* one lane per pixel looping over its samples (any spp) */
     RT_KERNEL_COMPACT = 3,     /* AUTO's per-ray code in persistent waves with wavefront active-ray
@@ -115,8 +117,8 @@ enum rt_kernel {
                                              checked equal to 1.0f / det where it is used */
     RT_KERNEL_FLAG_PACKED_REM = 0x80000,  /* OR-able (with DIST_SKIP): the DDA's three remaining-
                                              cell counts in one guarded word (dims <= 512) */
-    RT_KERNEL_FLAG_XCD_BANDS = 0x100000,  /* OR-able: XCD-aware block order, each of the 8 XCDs
-                                             renders one contiguous band of tiles (L2 locality) */
+    RT_KERNEL_FLAG_XCD_BANDS = 0x100000,  /* OR-able: XCD-aware block order, the 8 XCDs take
+                                             whole tile rows in turn (L2 locality) */
     RT_KERNEL_FLAG_UNROLL_PAIRS = 0x200000, /* OR-able (with UNIFORM_CELLS): the scalar loop tests
                                                two records per iteration, interleaved */
     RT_KERNEL_FLAG_WAVE_CLOCK = 0x400000, /* OR-able, debug: record s_memtime {start, end} of
