@@ -30,7 +30,7 @@ RT_KERNEL_AUTO, RT_KERNEL_LANES, RT_KERNEL_PIXEL_LOOP, RT_KERNEL_COMPACT, RT_KER
 RT_KERNEL_WIDE = 5
 RT_KERNEL_FLAG_PREFETCH = 0x100
 RT_KERNEL_FLAG_WAVE_GATE = 0x200
-RT_KERNEL_FLAG_LOOKAHEAD = 0x400
+RT_KERNEL_FLAG_SKIP_RUN = 0x400
 RT_KERNEL_FLAG_CSR_OFFSETS = 0x800
 RT_KERNEL_FLAG_DIST_SKIP = 0x1000
 RT_KERNEL_FLAG_NESTED_STEP = 0x2000

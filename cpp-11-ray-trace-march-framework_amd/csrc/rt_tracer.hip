@@ -56,7 +56,7 @@ constexpr uint32_t kWG = 256;               // lanes per workgroup
 constexpr uint32_t kMaxOccWords = 8192;     // LDS occupancy bitmap: up to 262,144 cells (64^3)
 constexpr int kVarPrefetch = 1;             // RT_KERNEL_FLAG_PREFETCH
 constexpr int kVarWaveGate = 2;             // RT_KERNEL_FLAG_WAVE_GATE
-constexpr int kVarLookahead = 4;            // RT_KERNEL_FLAG_LOOKAHEAD
+constexpr int kVarSkipRun = 4;             // RT_KERNEL_FLAG_SKIP_RUN: provably empty runs in a tight loop
 constexpr int kVarDistSkip = 8;             // RT_KERNEL_FLAG_DIST_SKIP
 constexpr int kVarNestedStep = 16;          // RT_KERNEL_FLAG_NESTED_STEP (A/B arm)
 constexpr int kVarPreGate = 32;             // RT_KERNEL_FLAG_PRE_GATE
@@ -472,30 +472,6 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, const uint32_t 
         return false;
     t = rtd::kFltMax;
 
-    if (VAR & kVarLookahead)
-    {
-        // Pipelined walk: the CSR offsets of the NEXT cell are loaded while the current cell
-        // is processed.  The current cell's step-axis crossing (nct_ax) is captured before the
-        // advance mutates the state, exactly as grid.cpp:236-260 uses it.
-        uint32_t kb, ke;
-        cell_range(P, uint32_t(cell), kb, ke);
-        for (uint32_t iter = 0; iter < P.max_steps; iter++)
-        {
-            if (STATS) { voxel = uint32_t(cell); steps++; }
-            float nct_cur;
-            bool more;
-            RT_DDA_ADVANCE(nct_cur, more);
-            uint32_t nkb = 0, nke = 0;
-            if (more) cell_range(P, uint32_t(cell), nkb, nke);
-            if (kb < ke && test_cell<STATS, TRI, VAR>(P, ox, oy, oz, dx, dy, dz, kb, ke, nct_cur, t, u, v, tri, tests))
-                return true;
-            if (!more) break;
-            kb = nkb;
-            ke = nke;
-        }
-        return false;
-    }
-
     if (P.cellw && !lds_occ && (VAR & kVarDistSkip))
     {
         // Distance skipping: after an empty cell at L-inf distance d from geometry the next
@@ -529,6 +505,36 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, const uint32_t 
                 RT_DDA_ADVANCE_PACKED(nct_ax, more);
             else
                 RT_DDA_ADVANCE_ADD(nct_ax, more);
+            if constexpr ((VAR & kVarSkipRun) != 0 && (VAR & kVarPackedRem) != 0 && !STATS)
+            {
+                // The next `skip` cells are provably empty (L-inf distance field): take their
+                // steps in a tight loop with no cell index or test work -- the same advances as
+                // the one-step-per-iteration form -- and move `cell` once by the steps each axis
+                // took (the drop of its remaining count).  An exit inside the run leaves the
+                // walk, where cell is dead.
+                if (kb >= ke && skip > 0 && more)
+                {
+                    const int r0 = remp;
+                    int n = skip;
+                    do
+                    {
+                        const float m_ = __builtin_fminf(__builtin_fminf(nct0, nct1), nct2);
+                        const bool a2_ = nct2 == m_;
+                        const bool a1_ = !a2_ && nct1 == m_;
+                        const bool a0_ = !a2_ && !a1_;
+                        remp -= a2_ ? (1 << 22) : (a1_ ? (1 << 11) : 1);
+                        more = (remp & kRemGuards) == 0;
+                        nct0 += a0_ ? dt0 : 0.0f;
+                        nct1 += a1_ ? dt1 : 0.0f;
+                        nct2 += a2_ ? dt2 : 0.0f;
+                    } while (--n > 0 && more);
+                    if (!more) break;
+                    cell += ((r0 & 1023) - (remp & 1023)) * cs0 + (((r0 >> 11) & 1023) - ((remp >> 11) & 1023)) * cs1 +
+                            (((r0 >> 22) & 511) - ((remp >> 22) & 511)) * cs2;
+                    skip = 0;
+                    continue;
+                }
+            }
             if constexpr ((VAR & kVarBail) != 0)
             {
                 // two-phase arm: a sample whose walk would pass bail_tests tests stops here and
@@ -1701,7 +1707,7 @@ int validate_frame(const rt_frame *f)
     if (f->intersector == RT_ISECT_BRUTE_FORCE && f->tri_test != RT_TRI_MOLLER_TRUMBORE)
         return fail(RT_E_INVALID, "IntersectBruteForce uses IntersectRayTri only (renderer.cpp:176)");
     if ((f->kernel & 0xFFu) > RT_KERNEL_WIDE ||
-        (f->kernel & ~(0xFFu | RT_KERNEL_FLAG_PREFETCH | RT_KERNEL_FLAG_WAVE_GATE | RT_KERNEL_FLAG_LOOKAHEAD |
+        (f->kernel & ~(0xFFu | RT_KERNEL_FLAG_PREFETCH | RT_KERNEL_FLAG_WAVE_GATE | RT_KERNEL_FLAG_SKIP_RUN |
                        RT_KERNEL_FLAG_CSR_OFFSETS | RT_KERNEL_FLAG_DIST_SKIP | RT_KERNEL_FLAG_NESTED_STEP |
                        RT_KERNEL_FLAG_PRE_GATE | RT_KERNEL_FLAG_EXHAUSTIVE | RT_KERNEL_FLAG_ORIGIN_PRE |
                        RT_KERNEL_FLAG_SELECT_STEP | RT_KERNEL_FLAG_FAST_RCP | RT_KERNEL_FLAG_PACKED_REM |
@@ -1818,7 +1824,7 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
                            s->nrefs, P.org[0], P.org[1], P.org[2]);
     const int var = ((fk & RT_KERNEL_FLAG_PREFETCH) ? kVarPrefetch : 0) |
                     ((fk & RT_KERNEL_FLAG_WAVE_GATE) ? kVarWaveGate : 0) |
-                    ((fk & RT_KERNEL_FLAG_LOOKAHEAD) ? kVarLookahead : 0) |
+                    ((fk & RT_KERNEL_FLAG_SKIP_RUN) ? kVarSkipRun : 0) |
                     ((fk & RT_KERNEL_FLAG_DIST_SKIP) ? kVarDistSkip : 0) |
                     ((fk & RT_KERNEL_FLAG_NESTED_STEP) ? kVarNestedStep : 0) |
                     ((fk & RT_KERNEL_FLAG_PRE_GATE) ? kVarPreGate : 0) |
@@ -1949,6 +1955,7 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
         else if (var == 74250) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 74250>), grid, wg, 0, st, P);
         else if (var == 76298) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 76298>), grid, wg, 0, st, P);
         else if (var == 78346) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 78346>), grid, wg, 0, st, P);
+        else if (var == 80398) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 80398>), grid, wg, 0, st, P);
         else                hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 0>), grid, wg, 0, st, P);
     }
     else if (P.isect == RT_ISECT_RAY_MARCH && (f->kernel & RT_KERNEL_FLAG_EXHAUSTIVE))

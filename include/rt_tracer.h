@@ -95,7 +95,8 @@ enum rt_kernel {
                                   triangle list (spp <= 16; else = AUTO) */
     RT_KERNEL_FLAG_PREFETCH = 0x100,  /* OR-able: software-pipelined triangle record loads */
     RT_KERNEL_FLAG_WAVE_GATE = 0x200, /* OR-able: skip a test's second half when no lane needs it */
-    RT_KERNEL_FLAG_LOOKAHEAD = 0x400, /* OR-able: load the next cell's CSR offsets one step ahead */
+    RT_KERNEL_FLAG_SKIP_RUN = 0x400,  /* OR-able (with DIST_SKIP + PACKED_REM): a run of cells the
+                                         distance field proves empty is stepped in a tight loop */
     RT_KERNEL_FLAG_CSR_OFFSETS = 0x800, /* OR-able: read the two CSR offsets per cell instead of
                                            the packed (start << 11 | count) word */
     RT_KERNEL_FLAG_DIST_SKIP = 0x1000,  /* OR-able: skip lookups of cells an L-inf distance field
