@@ -40,6 +40,7 @@ WORKLOADS = {
     "batch10": (tuple(range(10)), 1920, 1080, 4, (1920, 1080, 4), (960, 540, 4)),
 }
 HBM_PEAK = 8.0e12          # MI355X HBM3E peak, B/s (MI355X_MICROARCH.md)
+VALU_PEAK = 256 * 4 * 0.5 * 2.4e9   # wave64 VALU issue: 2 clk per instruction per SIMD
 SURVEY_B = {0: 390.2, 1: 371.1, 2: 796.1, 3: 573.7, 4: 487.8, 5: 1755.6, 6: 544.1, 7: 1220.7, 8: 1467.8,
             9: 873.4}                        # SURVEY.md §8d (scene 4 at 4096^2 x 16)
 METRIC = {"bench": "Msamples/s at 1920x1080x4spp Cornell-Box+killeroo",
@@ -244,6 +245,19 @@ def main():
                 p = json.load(fh)
             if p.get("workload") == f"scenes{list(SCENES)}_{W}x{H}x{SPP}":
                 traffic = p.get("hbm_bytes_per_launch")
+        # VALU-issue companion roofline: SQ_INSTS_VALU per launch from the committed PMC pass
+        # (profiles/r01e_counters.json, same scenes, kernel 0, one GPU) over the live kernel time;
+        # peak = 256 CU x 4 SIMD x 1/2 wave64 VALU instruction per clock x 2.4 GHz
+        valu = None
+        cnt = os.path.join(ROOT, "profiles", "r01e_counters.json")
+        if os.path.exists(cnt) and world == 1 and args.kernel == 0 and args.workload == "bench":
+            with open(cnt) as fh:
+                c = json.load(fh)["scenes"]
+            insts = sum(c[str(sid)]["SQ_INSTS_VALU"] for sid in SCENES)
+            rate = insts / (sum(kernel_ms.values()) / 1e3)
+            valu = {"achieved": round(rate / 1e9, 1), "peak": VALU_PEAK / 1e9,
+                    "unit": "Gwave-inst/s", "frac": round(rate / VALU_PEAK, 4),
+                    "insts_per_launch": {str(sid): c[str(sid)]["SQ_INSTS_VALU"] for sid in SCENES}}
         out = {
             "metric": METRIC[args.workload],
             "value": round(value, 3),
@@ -273,7 +287,8 @@ def main():
                          "traffic": traffic,
                          "note": "achieved = algorithmic bytes per launch (SURVEY 8d formula on the "
                                  "kernel's measured per-sample counts) / mean kernel time; the scene "
-                                 "working set is L2/MALL resident, so frac can exceed 1"},
+                                 "working set is L2/MALL resident, so frac can exceed 1",
+                         "valu_issue": valu},
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu_baseline:
