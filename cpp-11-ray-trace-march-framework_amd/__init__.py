@@ -28,6 +28,9 @@ MESH_DATA_DIR = os.path.join(REPO, "data", "meshes")     # cornell_box_quads.txt
 RT_TRI_MOLLER_TRUMBORE, RT_TRI_BARYCENTRIC = 0, 1
 RT_KERNEL_AUTO, RT_KERNEL_LANES, RT_KERNEL_PIXEL_LOOP, RT_KERNEL_COMPACT, RT_KERNEL_PERSISTENT = 0, 1, 2, 3, 4
 RT_KERNEL_WIDE = 5
+RT_KERNEL_KIND_MASK = 0x3F
+RT_KERNEL_FLAG_WIDE16 = 0x40
+RT_KERNEL_FLAG_LDS_CELLS = 0x80
 RT_KERNEL_FLAG_PREFETCH = 0x100
 RT_KERNEL_FLAG_WAVE_GATE = 0x200
 RT_KERNEL_FLAG_SKIP_RUN = 0x400
@@ -462,11 +465,12 @@ class GpuScene:
                "rt_render_shard_device")
 
     def wave_clocks(self):
-        """{start, end} s_memtime per work item of the last RT_KERNEL_FLAG_WAVE_CLOCK launch."""
+        """Per work item of the last RT_KERNEL_FLAG_WAVE_CLOCK launch: {start, end} s_memtime,
+        records tested in wave-uniform loops, per-lane list-loop iterations."""
         L = tracer_lib()
         n = c_u32()
         _check(L.rt_debug_wave_clocks(self._h, None, 0, ctypes.byref(n)), L, "rt_debug_wave_clocks")
-        out = np.zeros((n.value, 2), np.uint64)
+        out = np.zeros((n.value, 4), np.uint64)
         _check(L.rt_debug_wave_clocks(self._h, _ptr(out), n.value, ctypes.byref(n)), L, "rt_debug_wave_clocks")
         return out
 

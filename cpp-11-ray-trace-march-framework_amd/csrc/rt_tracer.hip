@@ -53,6 +53,8 @@ int fail(int code, const std::string& msg)
 constexpr uint32_t kTile = 16;              // shard / scheduling tile edge (pixels)
 constexpr uint32_t kTilePix = kTile * kTile;
 constexpr uint32_t kWG = 256;               // lanes per workgroup
+constexpr uint32_t kLdsStage = 64;          // kVarLdsCells: records per LDS chunk (3 KiB per wave)
+constexpr uint32_t kLdsMinRefs = 16;        // kVarLdsCells: shortest list staged through LDS
 constexpr uint32_t kMaxOccWords = 8192;     // LDS occupancy bitmap: up to 262,144 cells (64^3)
 constexpr int kVarPrefetch = 1;             // RT_KERNEL_FLAG_PREFETCH
 constexpr int kVarWaveGate = 2;             // RT_KERNEL_FLAG_WAVE_GATE
@@ -72,6 +74,7 @@ constexpr int kVarUnroll = 16384;           // RT_KERNEL_FLAG_UNROLL_PAIRS: unif
 constexpr int kVarWaveClock = 32768;        // RT_KERNEL_FLAG_WAVE_CLOCK: per-item s_memtime (debug)
 constexpr int kVarUniform = 65536;          // RT_KERNEL_FLAG_UNIFORM_CELLS: scalar loop for wave-uniform lists
 constexpr int kVarBail = 131072;            // RT_KERNEL_FLAG_BAIL_WIDE phase 1: test budget + pixel queue
+constexpr int kVarLdsCells = 262144;        // RT_KERNEL_FLAG_LDS_CELLS: long uniform lists staged through LDS
 constexpr uint32_t kMarchSteps = 128;       // renderer.cpp:26
 constexpr uint32_t kDistBlock = 32;         // triangles per culling block of the distance kernels
 
@@ -113,7 +116,7 @@ struct KParams
     uint32_t rank, nranks;      // tile t is ours iff t % nranks == rank, local index t / nranks
     uint32_t wg_per_tile;
     uint32_t xcd_chunk;         // kVarXcdBands: consecutive blocks per XCD turn (0 = one band each)
-    uint64_t *wave_clk;         // kVarWaveClock: {start, end} s_memtime per work item
+    uint64_t *wave_clk;         // kVarWaveClock: {start, end, uniform tests, lane-loop iterations} per item
     const uint32_t *tile_order; // tile order (position -> local tile) or null = natural order
     uint32_t bail_tests;        // BAIL_WIDE phase 1: test budget per sample
     uint32_t *bail_count;       // BAIL_WIDE: queued pixels
@@ -133,6 +136,28 @@ __device__ __forceinline__ uint32_t compact_bits(uint32_t v)
     v = (v | (v >> 1)) & 0x33u;
     v = (v | (v >> 2)) & 0x0Fu;
     return v;
+}
+
+// Orders this wave's LDS writes before its later LDS reads of other lanes' data (a wave
+// executes its LDS operations in order; this keeps the compiler from reordering them).
+__device__ __forceinline__ void wave_lds_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// kVarWaveClock debug counters of this wave: [0] records tested in wave-uniform loops,
+// [1] iterations of the per-lane list loop
+__device__ __forceinline__ uint32_t *wave_counters()
+{
+    __shared__ uint32_t c[(kWG / 64u) * 2u];
+    return c + (threadIdx.x >> 6) * 2u;
+}
+
+__device__ __forceinline__ bool first_active_lane()
+{
+    return (threadIdx.x & 63u) == uint32_t(__ffsll((long long)__ballot(1)) - 1);
 }
 
 // CSR range of a cell: one u32 load of the packed (start << 11 | count) word when the scene
@@ -169,11 +194,86 @@ __device__ __forceinline__ bool test_cell(const KParams& P, float ox, float oy, 
         const uint32_t kb0 = __builtin_amdgcn_readfirstlane(kb), ke0 = __builtin_amdgcn_readfirstlane(ke);
         if (__all((kb == kb0) & (ke == ke0)))
         {
+            if constexpr ((VAR & kVarWaveClock) != 0)
+                if (first_active_lane()) wave_counters()[0] += ke0 - kb0;
             // constant address space: uniform loads of memory no store of this kernel touches
             // (frefs are written by k_origin_pre, an earlier launch) select s_load
             typedef float vf4 __attribute__((ext_vector_type(4)));
             typedef const __attribute__((address_space(4))) vf4 cvf4;
             cvf4 *crefs = (cvf4 *)P.frefs;
+            if constexpr ((VAR & kVarLdsCells) != 0)
+            {
+                // A long list (the dense cells behind the latency tail) is staged
+                // through LDS kLdsStage records at a time: the active lanes copy a chunk with all
+                // its loads in flight at once, then every lane reads each record at one uniform
+                // LDS address.  One memory round trip per chunk instead of one exposed scalar-load
+                // latency per record; same records, same order.
+                if (ke0 - kb0 >= kLdsMinRefs)
+                {
+                    __shared__ float4 s_cells[(kWG / 64u) * kLdsStage * 3u];
+                    float4 *st = s_cells + (threadIdx.x >> 6) * (kLdsStage * 3u);
+                    const uint64_t act = __ballot(1);
+                    const uint32_t rank = __builtin_amdgcn_mbcnt_hi(uint32_t(act >> 32),
+                                                                    __builtin_amdgcn_mbcnt_lo(uint32_t(act), 0u));
+                    const uint32_t nact = uint32_t(__popcll(act));
+                    for (uint32_t base = kb0; base < ke0; base += kLdsStage)
+                    {
+                        const uint32_t n3 = 3u * min(kLdsStage, ke0 - base);
+                        const float4 *src = P.frefs + size_t(base) * 3u;
+                        if (act == ~0ull)
+                        {
+                            // full wave: LDS-DMA, no VGPR staging (writes base + lane x 16 B; lanes
+                            // past the chunk re-read its last record into unused slots)
+                            const uint32_t lane = threadIdx.x & 63u;
+                            for (uint32_t j = 0; 64u * j < n3; j++)
+                                __builtin_amdgcn_global_load_lds(
+                                    (__attribute__((address_space(1))) void *)(src + min(lane + 64u * j, n3 - 1u)),
+                                    (__attribute__((address_space(3))) void *)(st + 64u * j), 16, 0, 0);
+                        }
+                        else
+                            for (uint32_t q = rank; q < n3; q += nact)
+                                st[q] = src[q];
+                        wave_lds_sync();
+                        float4 n0 = st[0], n1 = st[1], n2 = st[2];   // kVarUnroll: one record ahead
+                        for (uint32_t i = 0; 3u * i < n3; i++)
+                        {
+                            // the whole record in one LDS round trip (the empty asm keeps the reads
+                            // of its second half from being sunk into the gate)
+                            float4 r0, r1, r2;
+                            if constexpr ((VAR & kVarUnroll) != 0)
+                            {
+                                r0 = n0; r1 = n1; r2 = n2;
+                                const uint32_t j = 3u * i + 3u < n3 ? 3u * i + 3u : 3u * i;
+                                n0 = st[j];
+                                n1 = st[j + 1u];
+                                n2 = st[j + 2u];
+                                asm volatile("" ::"v"(n0.x), "v"(n0.y), "v"(n0.z), "v"(n0.w), "v"(n1.x), "v"(n1.y),
+                                             "v"(n1.z), "v"(n1.w), "v"(n2.x), "v"(n2.y), "v"(n2.z), "v"(n2.w));
+                            }
+                            else
+                            {
+                                r0 = st[3u * i];
+                                r1 = st[3u * i + 1u];
+                                r2 = st[3u * i + 2u];
+                                asm volatile("" ::"v"(r0.x), "v"(r0.y), "v"(r0.z), "v"(r0.w), "v"(r1.x), "v"(r1.y),
+                                             "v"(r1.z), "v"(r1.w), "v"(r2.x), "v"(r2.y), "v"(r2.z), "v"(r2.w));
+                            }
+                            float ct, cu, cv;
+                            const bool hit = rtd::ray_tri_mt_gated_pre<(VAR & kVarFastRcp) != 0>(
+                                dx, dy, dz, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w,
+                                ct, cu, cv);
+                            if (STATS) tests++;
+                            const bool take = hit & (ct < t) & (ct < nct_ax);
+                            t = take ? ct : t;
+                            u = take ? cu : u;
+                            v = take ? cv : v;
+                            tri = take ? base + i : tri;
+                        }
+                        wave_lds_sync();                  // reads of this chunk before the next copy
+                    }
+                    return t != rtd::kFltMax;
+                }
+            }
             // software pipeline: record k + 1 is in flight while record k is tested (scalar
             // loads may return out of order, so the wait for record k sits at its copy, before
             // the next load is issued)
@@ -252,23 +352,27 @@ __device__ __forceinline__ bool test_cell(const KParams& P, float ox, float oy, 
             return t != rtd::kFltMax;
         }
     }
-        float4 n0, n1, n2;
+    // the per-frame records (ORIGIN_PRE) or the scene's reference records
+    const float4 *recs = ((VAR & kVarOriginPre) && TRI == RT_TRI_MOLLER_TRUMBORE) ? P.frefs : P.refs;
+    float4 n0, n1, n2;
     if ((VAR & kVarPrefetch) && kb < ke)
     {
-        const float4 *rp = P.refs + size_t(kb) * 3;
+        const float4 *rp = recs + size_t(kb) * 3;
         n0 = rp[0];
         n1 = rp[1];
         n2 = rp[2];
     }
     for (uint32_t k = kb; k < ke; k++)
     {
+        if constexpr ((VAR & kVarWaveClock) != 0)
+            if (first_active_lane()) wave_counters()[1] += 1u;
         float4 r0, r1, r2;
         if (VAR & kVarPrefetch)
         {
             r0 = n0; r1 = n1; r2 = n2;
             if (k + 1 < ke)
             {
-                const float4 *rp = P.refs + size_t(k + 1) * 3;
+                const float4 *rp = recs + size_t(k + 1) * 3;
                 n0 = rp[0];
                 n1 = rp[1];
                 n2 = rp[2];
@@ -276,8 +380,7 @@ __device__ __forceinline__ bool test_cell(const KParams& P, float ox, float oy, 
         }
         else
         {
-            const float4 *rp = ((VAR & kVarOriginPre) && TRI == RT_TRI_MOLLER_TRUMBORE ? P.frefs : P.refs) +
-                               size_t(k) * 3;              // one address, immediate offsets
+            const float4 *rp = recs + size_t(k) * 3;     // one address, immediate offsets
             r0 = rp[0];
             r1 = rp[1];
             r2 = rp[2];
@@ -538,16 +641,19 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, const uint32_t 
             if constexpr ((VAR & kVarBail) != 0)
             {
                 // two-phase arm: a sample whose walk would pass bail_tests tests stops here and
-                // is re-traced by the wide phase (k_render_bailed); nothing of it is stored
-                if (kb < ke)
+                // is re-traced by the wide phase (k_render_bailed); nothing of it is stored.
+                // Branch-free count (ke - kb is 0 for skipped and empty cells); the stop shares
+                // the walk's exit, so the loop keeps two exits, not three.
+                budget -= int(ke - kb);
+                if (kb < ke && budget >= 0 &&
+                    test_cell<STATS, TRI, VAR>(P, ox, oy, oz, dx, dy, dz, kb, ke, nct_ax, t, u, v, tri, tests))
+                    return true;
+                if (!more || budget < 0)
                 {
-                    budget -= int(ke - kb);
-                    if (budget < 0)
-                    {
-                        *bailed = true;
-                        return false;
-                    }
+                    *bailed = budget < 0;
+                    break;
                 }
+                continue;
             }
             if (kb < ke && test_cell<STATS, TRI, VAR>(P, ox, oy, oz, dx, dy, dz, kb, ke, nct_ax, t, u, v, tri, tests))
                 return true;
@@ -897,9 +1003,10 @@ __device__ __forceinline__ void process_item(const KParams& P, const uint32_t *l
 constexpr uint32_t kXcds = 8;
 constexpr uint32_t kWideG = 4;              // RT_KERNEL_WIDE: lanes per sample
 constexpr uint32_t kBailTests = 256;        // BAIL_WIDE: default phase-1 test budget per sample
-constexpr uint32_t kBailAutoRanks = 8;      // AUTO: two-phase arm from this many shard ranks ...
-constexpr uint32_t kBailAutoRefs = 128;     // ... on scenes with a cell this dense
-constexpr uint32_t kBailAutoTests = 128;    // ... with this budget (best of 128 / 256 / 512 at 8 ranks)
+constexpr uint32_t kBailAutoRanks = 2;      // AUTO: two-phase arm from this many shard ranks ...
+constexpr uint32_t kBailAutoRefs = 128;     // ... on scenes with a cell this dense: budget 256 and
+constexpr uint32_t kBailAutoWideRanks = 4;  // 4 lanes per sample, from 4 ranks budget 128 and 16
+constexpr uint32_t kBailAutoTests = 128;    // lanes (tools/shard_scaling.py)
 __device__ __forceinline__ uint32_t xcd_band_block(uint32_t b, uint32_t nb, uint32_t chunk)
 {
     if (chunk == 0u)
@@ -923,14 +1030,27 @@ __global__ void __launch_bounds__(kWG) k_render_lanes(KParams P)
     const uint32_t item = b * (kWG / 64u) + (threadIdx.x >> 6);
     if (VAR & kVarWaveClock)
     {
-        // debug arm (RT_KERNEL_FLAG_WAVE_CLOCK): s_memtime at the item's start and end
+        // debug arm (RT_KERNEL_FLAG_WAVE_CLOCK): s_memtime at the item's start and end, and how
+        // many records the item tested in wave-uniform loops vs lane-loop iterations
+        if ((threadIdx.x & 63u) == 0u)
+        {
+            wave_counters()[0] = 0u;
+            wave_counters()[1] = 0u;
+        }
+        wave_lds_sync();
         const uint64_t t0 = __builtin_amdgcn_s_memtime();
         process_item<TRI, VAR>(P, nullptr, item);
         const uint64_t t1 = __builtin_amdgcn_s_memtime();
         if ((threadIdx.x & 63u) == 0u)
         {
-            P.wave_clk[2 * size_t(item)] = t0;
-            P.wave_clk[2 * size_t(item) + 1] = t1;
+            P.wave_clk[4 * size_t(item)] = t0;
+            P.wave_clk[4 * size_t(item) + 1] = t1;
+        }
+        wave_lds_sync();
+        if ((threadIdx.x & 63u) == 0u)
+        {
+            P.wave_clk[4 * size_t(item) + 2] = wave_counters()[0];
+            P.wave_clk[4 * size_t(item) + 3] = wave_counters()[1];
         }
     }
     else
@@ -1097,14 +1217,14 @@ __global__ void __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(8, 8))
 // from the start in the wide mode: kWideG lanes per sample split every cell's list, so each
 // lane's chain is a quarter long, and the pixel's samples are summed in order as in phase 1.
 // Persistent waves take queue entries round-robin; every pixel is stored by exactly one phase.
-template <int VAR>
+template <int VAR, int G>
 __global__ void __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(8, 8))) k_render_bailed(KParams P)
 {
     const uint32_t n = *P.bail_count;                                // phase 1 finished on this stream
-    const uint32_t lpp = P.spp * kWideG;                             // lanes per pixel (<= 64)
+    const uint32_t lpp = P.spp * uint32_t(G);                        // lanes per pixel (<= 64)
     const uint32_t per_wave = 64u / lpp;
     const uint32_t lane = threadIdx.x & 63u, g = lane / lpp, r = lane - g * lpp;
-    const uint32_t smp = r / kWideG, sub = r - smp * kWideG;
+    const uint32_t smp = r / uint32_t(G), sub = r - smp * uint32_t(G);
     const uint32_t nwaves = gridDim.x * (kWG / 64u);
     for (uint32_t e0 = (blockIdx.x * (kWG / 64u) + (threadIdx.x >> 6)) * per_wave; e0 < n; e0 += nwaves * per_wave)
     {
@@ -1113,11 +1233,11 @@ __global__ void __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(8, 8))
         const uint32_t q = live ? P.bail_queue[e] : 0u;
         const uint32_t k = q >> 8, p = q & 255u;
         float cr = 0.0f, cg = 0.0f, cb = 0.0f;
-        if (live) wide_trace<VAR, kWideG>(P, k, p * P.spp + smp, sub, cr, cg, cb);
+        if (live) wide_trace<VAR, G>(P, k, p * P.spp + smp, sub, cr, cg, cb);
         float sr = 0.0f, sg = 0.0f, sb = 0.0f;
         for (uint32_t j = 0; j < P.spp; j++)
         {
-            const int src = int(g * lpp + j * kWideG);
+            const int src = int(g * lpp + j * uint32_t(G));
             sr += __shfl(cr, src, 64);
             sg += __shfl(cg, src, 64);
             sb += __shfl(cb, src, 64);
@@ -1173,15 +1293,6 @@ struct CompactLds
     uint32_t left[kWG / 64u][kCompactSlots];     // samples of the slot's item not yet stored
     uint32_t item[kWG / 64u][kCompactSlots];     // work item held by the slot
 };
-
-// Orders this wave's LDS writes before its later LDS reads of other lanes' data (a wave
-// executes its LDS operations in order; this keeps the compiler from reordering them).
-__device__ __forceinline__ void wave_lds_sync()
-{
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
 
 template <int TRI, int VAR>
 __global__ void __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(8, 8)))
@@ -1706,8 +1817,8 @@ int validate_frame(const rt_frame *f)
     if (f->intersector > RT_ISECT_RAY_MARCH) return fail(RT_E_INVALID, "unknown intersector");
     if (f->intersector == RT_ISECT_BRUTE_FORCE && f->tri_test != RT_TRI_MOLLER_TRUMBORE)
         return fail(RT_E_INVALID, "IntersectBruteForce uses IntersectRayTri only (renderer.cpp:176)");
-    if ((f->kernel & 0xFFu) > RT_KERNEL_WIDE ||
-        (f->kernel & ~(0xFFu | RT_KERNEL_FLAG_PREFETCH | RT_KERNEL_FLAG_WAVE_GATE | RT_KERNEL_FLAG_SKIP_RUN |
+    if ((f->kernel & RT_KERNEL_KIND_MASK) > RT_KERNEL_WIDE ||
+        (f->kernel & ~(RT_KERNEL_KIND_MASK | RT_KERNEL_FLAG_LDS_CELLS | RT_KERNEL_FLAG_WIDE16 | RT_KERNEL_FLAG_PREFETCH | RT_KERNEL_FLAG_WAVE_GATE | RT_KERNEL_FLAG_SKIP_RUN |
                        RT_KERNEL_FLAG_CSR_OFFSETS | RT_KERNEL_FLAG_DIST_SKIP | RT_KERNEL_FLAG_NESTED_STEP |
                        RT_KERNEL_FLAG_PRE_GATE | RT_KERNEL_FLAG_EXHAUSTIVE | RT_KERNEL_FLAG_ORIGIN_PRE |
                        RT_KERNEL_FLAG_SELECT_STEP | RT_KERNEL_FLAG_FAST_RCP | RT_KERNEL_FLAG_PACKED_REM |
@@ -1719,8 +1830,8 @@ int validate_frame(const rt_frame *f)
     if (spp > 4096) return fail(RT_E_INVALID, "spp must be <= 4096");
     if (((f->kernel & RT_KERNEL_COMPACT_REFILL_MASK) >> RT_KERNEL_COMPACT_REFILL_SHIFT) > 64u)
         return fail(RT_E_INVALID, "compaction refill threshold must be <= 64 lanes");
-    if (((f->kernel & 0xFFu) == RT_KERNEL_LANES || (f->kernel & 0xFFu) == RT_KERNEL_PERSISTENT ||
-         (f->kernel & 0xFFu) == RT_KERNEL_COMPACT) &&
+    if (((f->kernel & RT_KERNEL_KIND_MASK) == RT_KERNEL_LANES || (f->kernel & RT_KERNEL_KIND_MASK) == RT_KERNEL_PERSISTENT ||
+         (f->kernel & RT_KERNEL_KIND_MASK) == RT_KERNEL_COMPACT) &&
         !(is_pow2(spp) && spp <= 64))
         return fail(RT_E_INVALID, "RT_KERNEL_LANES needs spp to be a power of two <= 64");
     return RT_OK;
@@ -1785,7 +1896,7 @@ void frame_params(const rt_scene *s, const rt_frame *f, KParams& P)
 
 bool use_lanes(const rt_frame *f, uint32_t spp)
 {
-    if ((f->kernel & 0xFFu) == RT_KERNEL_PIXEL_LOOP) return false;
+    if ((f->kernel & RT_KERNEL_KIND_MASK) == RT_KERNEL_PIXEL_LOOP) return false;
     return is_pow2(spp) && spp <= 64;
 }
 
@@ -1803,7 +1914,7 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
     if (s->ev_recorded && st != s->last_stream) RT_HIP(hipStreamWaitEvent(st, s->ev1, 0));
     s->last_stream = st;
     RT_HIP(hipEventRecord(s->ev0, st));
-    const uint32_t kind = f->kernel & 0xFFu;
+    const uint32_t kind = f->kernel & RT_KERNEL_KIND_MASK;
     // kVarXcdBands turn size: one row of this launch's tiles (ceil(tiles_x / nranks) local tiles
     // span a full frame row in shard mode).  Measured best of 1/4 .. 4 rows and 1..16 tiles:
     // whole rows interleave over the XCDs, so each L2 sees compact rows AND the frame's cost
@@ -1835,10 +1946,11 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
                     ((fk & RT_KERNEL_FLAG_XCD_BANDS) ? kVarXcdBands : 0) |
                     ((fk & RT_KERNEL_FLAG_UNROLL_PAIRS) ? kVarUnroll : 0) |
                     ((fk & RT_KERNEL_FLAG_WAVE_CLOCK) ? kVarWaveClock : 0) |
-                    ((fk & RT_KERNEL_FLAG_UNIFORM_CELLS) ? kVarUniform : 0);
+                    ((fk & RT_KERNEL_FLAG_UNIFORM_CELLS) ? kVarUniform : 0) |
+                    ((fk & RT_KERNEL_FLAG_LDS_CELLS) ? kVarLdsCells : 0);
     if (var & kVarWaveClock)
     {
-        const size_t need = size_t(blocks) * (kWG / 64u) * 2u;
+        const size_t need = size_t(blocks) * (kWG / 64u) * 4u;
         if (need > s->clk_cap)
         {
             if (s->d_clk) RT_HIP(hipFree(s->d_clk));
@@ -1846,17 +1958,21 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
             RT_HIP(hipMalloc(&s->d_clk, need * sizeof(uint64_t)));
             s->clk_cap = need;
         }
-        s->clk_items = uint32_t(need / 2u);
+        s->clk_items = uint32_t(need / 4u);
         P.wave_clk = s->d_clk;
     }
     const bool bary = P.tri_test == RT_TRI_BARYCENTRIC;
     const dim3 wg(kWG);
-    // AUTO takes the two-phase arm for a shard of >= 8 ranks of a scene with dense cells: there a
-    // rank's launch is bound by its few ~1000-test waves, which the wide phase shortens 4x
-    // (measured, tools/shard_scaling.py: killeroo rank of 8 0.46 -> 0.31 ms, scene 5 0.68 -> 0.38,
-    // head 0.29 -> 0.20); on a whole frame, or a scene without dense cells, the phase-1 budget
-    // check costs more than it saves (Cornell +40 %, killeroo 1 GPU +45 %).
+    // RT_KERNEL_FLAG_WIDE16: 16 lanes per sample in the wide kernel / wide phase (spp <= 4)
     const bool bail_auto = kind == RT_KERNEL_AUTO && P.nranks >= kBailAutoRanks && s->max_cell_refs >= kBailAutoRefs;
+    const bool wide_auto = bail_auto && P.nranks >= kBailAutoWideRanks && !(f->kernel & RT_KERNEL_FLAG_BAIL_WIDE);
+    const bool g16 = ((f->kernel & RT_KERNEL_FLAG_WIDE16) || wide_auto) && P.spp * 16u <= 64u;
+    // AUTO takes the two-phase arm for a shard of >= 2 ranks of a scene with dense cells: there a
+    // rank's launch is bound by its few ~1000-test waves, which the wide phase splits 4 or 16
+    // ways (measured, tools/shard_scaling.py, killeroo rank of 2 / 4 / 8: 0.60 / 0.50 / 0.46 ms
+    // -> 0.55 (budget 256, 4 lanes) / 0.41 / 0.26 (budget 128, 16 lanes); scene 5 rank of 8
+    // 0.69 -> 0.29).  On a whole frame, or a scene without dense cells, phase 1's budget count
+    // (+6-10 %) and the re-trace cost more than they save.
     if (((f->kernel & RT_KERNEL_FLAG_BAIL_WIDE) || bail_auto) && lanes &&
         (kind == RT_KERNEL_AUTO || kind == RT_KERNEL_LANES) && P.isect == RT_ISECT_GRID && !bary &&
         (var == 14858 || var == 80394) && P.spp * kWideG <= 64u)
@@ -1871,7 +1987,7 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
             s->bail_cap = need;
         }
         const uint32_t tb = (f->kernel & RT_KERNEL_COMPACT_REFILL_MASK) >> RT_KERNEL_COMPACT_REFILL_SHIFT;
-        P.bail_tests = tb ? 16u * tb : (bail_auto && !(f->kernel & RT_KERNEL_FLAG_BAIL_WIDE) ? kBailAutoTests : kBailTests);
+        P.bail_tests = tb ? 16u * tb : (wide_auto ? kBailAutoTests : kBailTests);
         P.bail_count = s->d_bail;
         P.bail_queue = s->d_bail + 1;
         RT_HIP(hipMemsetAsync(s->d_bail, 0, sizeof(uint32_t), st));
@@ -1879,13 +1995,24 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
             hipLaunchKernelGGL((k_render_bail1<80394 | kVarBail>), dim3(uint32_t(blocks)), wg, 0, st, P);
         else
             hipLaunchKernelGGL((k_render_bail1<14858 | kVarBail>), dim3(uint32_t(blocks)), wg, 0, st, P);
-        hipLaunchKernelGGL((k_render_bailed<14858>), dim3(s->bail_wgs), wg, 0, st, P);
+        if (g16)
+            hipLaunchKernelGGL((k_render_bailed<14858, 16>), dim3(s->bail_wgs), wg, 0, st, P);
+        else
+            hipLaunchKernelGGL((k_render_bailed<14858, kWideG>), dim3(s->bail_wgs), wg, 0, st, P);
     }
     else if (lanes && kind == RT_KERNEL_WIDE && P.isect == RT_ISECT_GRID && !bary && (var == 14858 || var == 80394) &&
         P.spp * kWideG <= 64u)
     {
-        P.xcd_chunk *= kWideG;
-        hipLaunchKernelGGL((k_render_wide<14858, kWideG>), dim3(uint32_t(blocks) * kWideG), wg, 0, st, P);
+        if (g16)
+        {
+            P.xcd_chunk *= 16u;
+            hipLaunchKernelGGL((k_render_wide<14858, 16>), dim3(uint32_t(blocks) * 16u), wg, 0, st, P);
+        }
+        else
+        {
+            P.xcd_chunk *= kWideG;
+            hipLaunchKernelGGL((k_render_wide<14858, kWideG>), dim3(uint32_t(blocks) * kWideG), wg, 0, st, P);
+        }
     }
     else if (lanes && kind == RT_KERNEL_COMPACT && P.isect == RT_ISECT_GRID)
     {
@@ -1956,6 +2083,24 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
         else if (var == 76298) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 76298>), grid, wg, 0, st, P);
         else if (var == 78346) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 78346>), grid, wg, 0, st, P);
         else if (var == 80398) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 80398>), grid, wg, 0, st, P);
+        else if (var == (96778 | kVarWaveClock))
+            hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 96778 | kVarWaveClock>), grid, wg, 0, st, P);
+        else if (var == (80394 | kVarPrefetch))
+            hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 80394 | kVarPrefetch>), grid, wg, 0, st, P);
+        else if (var == (80394 | kVarPrefetch | kVarWaveClock))
+            hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 80394 | kVarPrefetch | kVarWaveClock>), grid, wg, 0,
+                               st, P);
+        else if (var == (80394 | kVarLdsCells))
+            hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 80394 | kVarLdsCells>), grid, wg, 0, st, P);
+        else if (var == (80394 | kVarLdsCells | kVarUnroll))
+            hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 80394 | kVarLdsCells | kVarUnroll>), grid, wg, 0,
+                               st, P);
+        else if (var == (80394 | kVarLdsCells | kVarUnroll | kVarWaveClock))
+            hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 80394 | kVarLdsCells | kVarUnroll | kVarWaveClock>),
+                               grid, wg, 0, st, P);
+        else if (var == (80394 | kVarLdsCells | kVarWaveClock))
+            hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 80394 | kVarLdsCells | kVarWaveClock>), grid, wg, 0,
+                               st, P);
         else                hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 0>), grid, wg, 0, st, P);
     }
     else if (P.isect == RT_ISECT_RAY_MARCH && (f->kernel & RT_KERNEL_FLAG_EXHAUSTIVE))
@@ -2454,7 +2599,7 @@ int rt_debug_wave_clocks(rt_scene *s, uint64_t *out, uint32_t max_items, uint32_
     *n_items = s->clk_items;
     if (!out || !s->d_clk) return RT_OK;
     RT_HIP(hipDeviceSynchronize());
-    RT_HIP(hipMemcpy(out, s->d_clk, sizeof(uint64_t) * 2 * std::min(max_items, s->clk_items), hipMemcpyDeviceToHost));
+    RT_HIP(hipMemcpy(out, s->d_clk, sizeof(uint64_t) * 4 * std::min(max_items, s->clk_items), hipMemcpyDeviceToHost));
     return RT_OK;
 }
 

@@ -84,7 +84,8 @@ enum rt_intersector {
 enum rt_kernel {
     RT_KERNEL_AUTO = 0,        /* the fastest measured variant for the frame's spp (LANES + WAVE_GATE
                                   + DIST_SKIP + ORIGIN_PRE + FAST_RCP + PACKED_REM + XCD_BANDS +
-                                  UNIFORM_CELLS; BAIL_WIDE for >= 8-rank shards of dense scenes) */
+                                  UNIFORM_CELLS; BAIL_WIDE for >= 2-rank shards of dense scenes, with
+                                  WIDE16 and budget 128 from 4 ranks) */
     RT_KERNEL_LANES = 1,       /* one lane per sample, a pixel's samples in adjacent lanes */
     RT_KERNEL_PIXEL_LOOP = 2,  /* one lane per pixel looping over its samples (any spp) */
     RT_KERNEL_COMPACT = 3,     /* AUTO's per-ray code in persistent waves with wavefront active-ray
@@ -93,6 +94,11 @@ enum rt_kernel {
     RT_KERNEL_PERSISTENT = 4,  /* LANES in persistent workgroups with the LDS cell-occupancy bitmap */
     RT_KERNEL_WIDE = 5,        /* AUTO's per-ray code with 4 lanes per sample splitting every cell's
                                   triangle list (spp <= 16; else = AUTO) */
+    RT_KERNEL_KIND_MASK = 0x3F,       /* the kernel kind above; the bits above it are flags */
+    RT_KERNEL_FLAG_WIDE16 = 0x40,     /* OR-able (WIDE kernel, BAIL_WIDE phase 2; spp <= 4): 16 lanes
+                                         per sample instead of 4 */
+    RT_KERNEL_FLAG_LDS_CELLS = 0x80,  /* OR-able (with UNIFORM_CELLS): a wave-uniform list of >= 16
+                                         references is staged through LDS 64 records at a time */
     RT_KERNEL_FLAG_PREFETCH = 0x100,  /* OR-able: software-pipelined triangle record loads */
     RT_KERNEL_FLAG_WAVE_GATE = 0x200, /* OR-able: skip a test's second half when no lane needs it */
     RT_KERNEL_FLAG_SKIP_RUN = 0x400,  /* OR-able (with DIST_SKIP + PACKED_REM): a run of cells the
@@ -236,8 +242,10 @@ int  rt_debug_primitives(int kind, const float *in, uint32_t n, float *out, int 
    correctly rounded 1.0f / x for all 2^32 - 2^24 finite nonzero floats; bad_by_exponent[256]
    receives the mismatch count per biased exponent. */
 int  rt_debug_rcp_check(uint64_t *bad_by_exponent, int device);
-/* {start, end} shader-clock pairs of the last RT_KERNEL_FLAG_WAVE_CLOCK launch on this scene,
-   one per 64-sample work item in launch item order; *n_items = how many the launch wrote. */
+/* Per 64-sample work item of the last RT_KERNEL_FLAG_WAVE_CLOCK launch on this scene, in launch
+   item order, four words: {start, end} shader clock, records tested in wave-uniform list loops,
+   iterations of the per-lane list loop.  out holds 4 x max_items words; *n_items = how many
+   items the launch wrote. */
 int  rt_debug_wave_clocks(rt_scene *s, uint64_t *out, uint32_t max_items, uint32_t *n_items);
 
 /* Hammersley table the library uses when rt_frame.sample_offsets is NULL. */

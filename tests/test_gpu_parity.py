@@ -183,7 +183,12 @@ def test_auto_equals_plain_arms(golden, scenes):
                   base | rtm.RT_KERNEL_FLAG_SELECT_STEP, base | rtm.RT_KERNEL_FLAG_XCD_BANDS,
                   full | rtm.RT_KERNEL_FLAG_UNIFORM_CELLS,
                   full | rtm.RT_KERNEL_FLAG_UNIFORM_CELLS | rtm.RT_KERNEL_FLAG_UNROLL_PAIRS,
-                  rtm.RT_KERNEL_WIDE, rtm.RT_KERNEL_FLAG_BAIL_WIDE, rtm.RT_KERNEL_FLAG_BAIL_WIDE | (4 << 24)):
+                  full | rtm.RT_KERNEL_FLAG_UNIFORM_CELLS | rtm.RT_KERNEL_FLAG_LDS_CELLS,
+                  full | rtm.RT_KERNEL_FLAG_UNIFORM_CELLS | rtm.RT_KERNEL_FLAG_LDS_CELLS | rtm.RT_KERNEL_FLAG_UNROLL_PAIRS,
+                  full | rtm.RT_KERNEL_FLAG_UNIFORM_CELLS | rtm.RT_KERNEL_FLAG_PREFETCH,
+                  rtm.RT_KERNEL_WIDE, rtm.RT_KERNEL_FLAG_BAIL_WIDE, rtm.RT_KERNEL_FLAG_BAIL_WIDE | (4 << 24),
+                  rtm.RT_KERNEL_WIDE | rtm.RT_KERNEL_FLAG_WIDE16,
+                  rtm.RT_KERNEL_FLAG_BAIL_WIDE | rtm.RT_KERNEL_FLAG_WIDE16 | (4 << 24)):
             img = gs.render_frame(gs.frame(1920, 1080, 4, kernel=k))
             assert hashlib.sha256(img.tobytes()).hexdigest() == want, (sid, hex(k))
 
@@ -194,14 +199,31 @@ def test_wide_and_two_phase_vs_oracle(scenes, oracle, spp):
     AUTO), budget 16 tests so most pixels go through the wide phase."""
     hs, gs = scenes(5)
     exp, _, _ = oracle.render(5, 97, 61, spp)
-    for k in (rtm.RT_KERNEL_WIDE, rtm.RT_KERNEL_FLAG_BAIL_WIDE | (1 << 24)):
+    for k in (rtm.RT_KERNEL_WIDE, rtm.RT_KERNEL_FLAG_BAIL_WIDE | (1 << 24),
+              rtm.RT_KERNEL_WIDE | rtm.RT_KERNEL_FLAG_WIDE16,
+              rtm.RT_KERNEL_FLAG_BAIL_WIDE | rtm.RT_KERNEL_FLAG_WIDE16 | (1 << 24)):
         np.testing.assert_array_equal(gs.render_frame(gs.frame(97, 61, spp, kernel=k)), exp, err_msg=hex(k))
 
 
-@pytest.mark.parametrize("sid,nranks", [(8, 8), (5, 8), (8, 3), (4, 16)])
+@pytest.mark.parametrize("sid,spp", [(5, 1), (5, 4), (5, 64), (8, 2), (8, 16), (4, 4)])
+def test_lds_cells_vs_oracle(scenes, oracle, sid, spp):
+    """LDS-staged uniform lists on ragged frames: partial waves (pixels off the frame, lanes
+    already done) take the register copy, full waves the LDS-DMA copy; frames equal the
+    reference's."""
+    hs, gs = scenes(sid)
+    exp, _, _ = oracle.render(sid, 97, 61, spp)
+    k = rtm.RT_KERNEL_LANES | (rtm.RT_KERNEL_FLAG_WAVE_GATE | rtm.RT_KERNEL_FLAG_DIST_SKIP |
+                                rtm.RT_KERNEL_FLAG_ORIGIN_PRE | rtm.RT_KERNEL_FLAG_FAST_RCP |
+                                rtm.RT_KERNEL_FLAG_PACKED_REM | rtm.RT_KERNEL_FLAG_XCD_BANDS |
+                                rtm.RT_KERNEL_FLAG_UNIFORM_CELLS | rtm.RT_KERNEL_FLAG_LDS_CELLS)
+    np.testing.assert_array_equal(gs.render_frame(gs.frame(97, 61, spp, kernel=k)), exp)
+
+
+@pytest.mark.parametrize("sid,nranks", [(8, 8), (5, 8), (8, 3), (4, 16), (8, 2), (5, 4)])
 def test_shard_partition_dense_scenes(golden, scenes, sid, nranks):
-    """Shards of >= 8 ranks of a dense scene take AUTO's two-phase arm; every partition
-    reassembles into the reference frame."""
+    """Shards of >= 2 ranks of a dense scene take AUTO's two-phase arm (budget 256 with 4 lanes
+    per sample below 4 ranks, budget 128 with 16 lanes from 4); every partition reassembles
+    into the reference frame."""
     import torch
     hs, gs = scenes(sid)
     W, H = 1920, 1080
@@ -228,7 +250,8 @@ def test_wave_clock_debug_arm(scenes):
                                          rtm.RT_KERNEL_FLAG_WAVE_CLOCK))
     np.testing.assert_array_equal(gs.render_frame(f1), gs.render_frame(f0))
     clk = gs.wave_clocks()
-    assert clk.shape == (10 * 8 * 16, 2) and (clk[:, 1] >= clk[:, 0]).all() and clk[:, 0].any()
+    assert clk.shape == (10 * 8 * 16, 4) and (clk[:, 1] >= clk[:, 0]).all() and clk[:, 0].any()
+    assert clk[:, 2].any() or clk[:, 3].any()
 
 
 def test_head_4096x4096x16(golden, scenes):
