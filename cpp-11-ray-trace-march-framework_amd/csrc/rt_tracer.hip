@@ -55,6 +55,7 @@ constexpr uint32_t kTilePix = kTile * kTile;
 constexpr uint32_t kWG = 256;               // lanes per workgroup
 constexpr uint32_t kLdsStage = 64;          // kVarLdsCells: records per LDS chunk (3 KiB per wave)
 constexpr uint32_t kLdsMinRefs = 16;        // kVarLdsCells: shortest list staged through LDS
+constexpr uint32_t kAltMinRefs = 8;         // kVarAltLoads: shortest list run on alternating sets
 constexpr uint32_t kMaxOccWords = 8192;     // LDS occupancy bitmap: up to 262,144 cells (64^3)
 constexpr int kVarPrefetch = 1;             // RT_KERNEL_FLAG_PREFETCH
 constexpr int kVarWaveGate = 2;             // RT_KERNEL_FLAG_WAVE_GATE
@@ -75,6 +76,7 @@ constexpr int kVarWaveClock = 32768;        // RT_KERNEL_FLAG_WAVE_CLOCK: per-it
 constexpr int kVarUniform = 65536;          // RT_KERNEL_FLAG_UNIFORM_CELLS: scalar loop for wave-uniform lists
 constexpr int kVarBail = 131072;            // RT_KERNEL_FLAG_BAIL_WIDE phase 1: test budget + pixel queue
 constexpr int kVarLdsCells = 262144;        // RT_KERNEL_FLAG_LDS_CELLS: long uniform lists staged through LDS
+constexpr int kVarAltLoads = 524288;        // RT_KERNEL_FLAG_ALT_LOADS: uniform loop on two record sets in turn
 constexpr uint32_t kMarchSteps = 128;       // renderer.cpp:26
 constexpr uint32_t kDistBlock = 32;         // triangles per culling block of the distance kernels
 
@@ -328,6 +330,48 @@ __device__ __forceinline__ bool test_cell(const KParams& P, float ox, float oy, 
                     v = takeb ? vb : v;
                     tri = takeb ? k + 1u : tri;
                 }
+            }
+            if ((VAR & kVarAltLoads) != 0 && ke0 - kb0 >= kAltMinRefs)
+            {
+                // Two record register sets used in turn, so nothing is copied between records.
+                // Scalar loads complete out of order and a wait covers every load in flight, so
+                // each set's wait is forced (empty asm) before the other set's loads are issued:
+                // record k + 1 still loads while record k is tested.
+                auto test_rec = [&](const vf4& r0, const vf4& r1, const vf4& r2, uint32_t kk) {
+                    float ct, cu, cv;
+                    const bool hit = rtd::ray_tri_mt_gated_pre<(VAR & kVarFastRcp) != 0>(
+                        dx, dy, dz, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w, ct, cu,
+                        cv);
+                    if (STATS) tests++;
+                    const bool take = hit & (ct < t) & (ct < nct_ax);
+                    t = take ? ct : t;
+                    u = take ? cu : u;
+                    v = take ? cv : v;
+                    tri = take ? kk : tri;
+                };
+                vf4 b0, b1, b2;
+                for (;;)
+                {
+                    asm volatile("" ::"s"(n0), "s"(n1), "s"(n2));
+                    if (k + 1u < ke0)
+                    {
+                        b0 = crefs[size_t(k + 1u) * 3];
+                        b1 = crefs[size_t(k + 1u) * 3 + 1];
+                        b2 = crefs[size_t(k + 1u) * 3 + 2];
+                    }
+                    test_rec(n0, n1, n2, k);
+                    if (++k >= ke0) break;
+                    asm volatile("" ::"s"(b0), "s"(b1), "s"(b2));
+                    if (k + 1u < ke0)
+                    {
+                        n0 = crefs[size_t(k + 1u) * 3];
+                        n1 = crefs[size_t(k + 1u) * 3 + 1];
+                        n2 = crefs[size_t(k + 1u) * 3 + 2];
+                    }
+                    test_rec(b0, b1, b2, k);
+                    if (++k >= ke0) break;
+                }
+                return t != rtd::kFltMax;
             }
             for (; k < ke0; k++)
             {
@@ -1818,7 +1862,8 @@ int validate_frame(const rt_frame *f)
     if (f->intersector == RT_ISECT_BRUTE_FORCE && f->tri_test != RT_TRI_MOLLER_TRUMBORE)
         return fail(RT_E_INVALID, "IntersectBruteForce uses IntersectRayTri only (renderer.cpp:176)");
     if ((f->kernel & RT_KERNEL_KIND_MASK) > RT_KERNEL_WIDE ||
-        (f->kernel & ~(RT_KERNEL_KIND_MASK | RT_KERNEL_FLAG_LDS_CELLS | RT_KERNEL_FLAG_WIDE16 | RT_KERNEL_FLAG_PREFETCH | RT_KERNEL_FLAG_WAVE_GATE | RT_KERNEL_FLAG_SKIP_RUN |
+        (f->kernel & ~(RT_KERNEL_KIND_MASK | RT_KERNEL_FLAG_LDS_CELLS | RT_KERNEL_FLAG_WIDE16 |
+                       RT_KERNEL_FLAG_ALT_LOADS | RT_KERNEL_FLAG_PREFETCH | RT_KERNEL_FLAG_WAVE_GATE | RT_KERNEL_FLAG_SKIP_RUN |
                        RT_KERNEL_FLAG_CSR_OFFSETS | RT_KERNEL_FLAG_DIST_SKIP | RT_KERNEL_FLAG_NESTED_STEP |
                        RT_KERNEL_FLAG_PRE_GATE | RT_KERNEL_FLAG_EXHAUSTIVE | RT_KERNEL_FLAG_ORIGIN_PRE |
                        RT_KERNEL_FLAG_SELECT_STEP | RT_KERNEL_FLAG_FAST_RCP | RT_KERNEL_FLAG_PACKED_REM |
@@ -1947,7 +1992,8 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
                     ((fk & RT_KERNEL_FLAG_UNROLL_PAIRS) ? kVarUnroll : 0) |
                     ((fk & RT_KERNEL_FLAG_WAVE_CLOCK) ? kVarWaveClock : 0) |
                     ((fk & RT_KERNEL_FLAG_UNIFORM_CELLS) ? kVarUniform : 0) |
-                    ((fk & RT_KERNEL_FLAG_LDS_CELLS) ? kVarLdsCells : 0);
+                    ((fk & RT_KERNEL_FLAG_LDS_CELLS) ? kVarLdsCells : 0) |
+                    ((fk & RT_KERNEL_FLAG_ALT_LOADS) ? kVarAltLoads : 0);
     if (var & kVarWaveClock)
     {
         const size_t need = size_t(blocks) * (kWG / 64u) * 4u;
@@ -2089,6 +2135,11 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
             hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 80394 | kVarPrefetch>), grid, wg, 0, st, P);
         else if (var == (80394 | kVarPrefetch | kVarWaveClock))
             hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 80394 | kVarPrefetch | kVarWaveClock>), grid, wg, 0,
+                               st, P);
+        else if (var == (80394 | kVarAltLoads))
+            hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 80394 | kVarAltLoads>), grid, wg, 0, st, P);
+        else if (var == (80394 | kVarAltLoads | kVarWaveClock))
+            hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 80394 | kVarAltLoads | kVarWaveClock>), grid, wg, 0,
                                st, P);
         else if (var == (80394 | kVarLdsCells))
             hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 80394 | kVarLdsCells>), grid, wg, 0, st, P);
