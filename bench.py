@@ -158,6 +158,21 @@ class GpuWorkload:
             hs.close()
 
 
+def check_frames(work, world):
+    """Rank 0: every frame assembled from the ranks' shards (N > 1) or rendered whole (N = 1)
+    equals a one-launch render of the full frame, byte for byte.  Raises on a mismatch."""
+    torch = work.torch
+    ref = torch.empty(W * H, dtype=torch.int32, device="cuda")
+    for i, (sid, hs, gs, f) in enumerate(work.scenes):
+        f1 = gs.frame(W, H, SPP)
+        gs.render_frame_device(f1, ref.data_ptr(), work.stream.cuda_stream)
+        got = work.frames[i] if world > 1 else work.bufs[i]
+        work.sync()
+        if not torch.equal(ref, got):
+            raise SystemExit(f"scene {sid}: frame assembled from {world} ranks differs from the one-GPU render")
+    return f"{len(work.scenes)} frames equal to the one-GPU render"
+
+
 def run_steps(work, world, rank, steps, warmup, dist=None):
     """W untimed warm-up steps, then K timed steps between barrier+sync on both sides; returns
     the max-over-ranks wall time.  A step renders every scene (this rank's tiles when N > 1);
@@ -210,6 +225,12 @@ def main():
     ap.add_argument("--kernel", type=int, default=0, help="rt_kernel value (0 = AUTO; see include/rt_tracer.h)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="bench")
+    ap.add_argument("--check", action="store_true",
+                    help="after timing, rank 0 compares every assembled frame with a one-GPU render")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="rehearsal only: 'gloo' runs the N>1 path without RCCL")
+    ap.add_argument("--one-device", action="store_true",
+                    help="rehearsal only: every rank on GPU 0 (N>1 path on a one-GPU box)")
     args = ap.parse_args()
     global SCENES, W, H, SPP, COUNT_FRAME, CPU_FRAME
     SCENES, W, H, SPP, COUNT_FRAME, CPU_FRAME = WORKLOADS[args.workload]
@@ -222,9 +243,14 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}; launch N>1 with torch.distributed.run")
+    if args.one_device:
+        local = 0
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.dist_backend)
 
     rtm = load_package()
     work = GpuWorkload(rtm, torch, world, rank, local, args.kernel)
@@ -291,6 +317,10 @@ def main():
                          "valu_issue": valu},
             "cpu_baseline": None,
         }
+        if args.check:
+            out["check"] = check_frames(work, world)
+        if args.one_device or args.dist_backend != "nccl":
+            out["config"]["rehearsal"] = f"{args.dist_backend}, one device" if args.one_device else args.dist_backend
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline()
         print(json.dumps(out), flush=True)

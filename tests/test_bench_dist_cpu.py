@@ -72,3 +72,28 @@ def test_bench_run_steps_two_ranks_gloo():
     assert same
     assert elapsed > 0
     assert renders == (3 + 1) * 2        # (steps + warmup) x scenes
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(240)
+def test_bench_two_ranks_one_gpu_rehearsal():
+    """The whole N > 1 bench path on the GPU -- AUTO's shard kernels (two-phase arm on
+    killeroo), the all-gather, the K3 un-permute and the max-over-ranks timing -- as two
+    processes on one device under gloo (RCCL needs one GPU per rank).  Rank 0's --check
+    compares both assembled 1080p frames with a one-GPU render, byte for byte."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(root, "bench.py"),
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--check", "--dist-backend", "gloo",
+           "--one-device"]
+    r = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=220)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = next(l for l in r.stdout.splitlines() if l.startswith("{"))
+    out = json.loads(line)
+    assert out["n_gpus"] == 2 and out["check"] == "2 frames equal to the one-GPU render"
