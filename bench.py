@@ -272,10 +272,10 @@ def main():
             if p.get("workload") == f"scenes{list(SCENES)}_{W}x{H}x{SPP}":
                 traffic = p.get("hbm_bytes_per_launch")
         # VALU-issue companion roofline: SQ_INSTS_VALU per launch from the committed PMC pass
-        # (profiles/r01e_counters.json, same scenes, kernel 0, one GPU) over the live kernel time;
+        # (profiles/auto_counters.json: the current AUTO kernel, same scenes, one GPU) over the live kernel time;
         # peak = 256 CU x 4 SIMD x 1/2 wave64 VALU instruction per clock x 2.4 GHz
         valu = None
-        cnt = os.path.join(ROOT, "profiles", "r01e_counters.json")
+        cnt = os.path.join(ROOT, "profiles", "auto_counters.json")
         if os.path.exists(cnt) and world == 1 and args.kernel == 0 and args.workload == "bench":
             with open(cnt) as fh:
                 c = json.load(fh)["scenes"]

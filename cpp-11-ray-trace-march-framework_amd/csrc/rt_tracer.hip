@@ -59,7 +59,7 @@ constexpr uint32_t kAltMinRefs = 8;         // kVarAltLoads: shortest list run o
 constexpr uint32_t kMaxOccWords = 8192;     // LDS occupancy bitmap: up to 262,144 cells (64^3)
 constexpr int kVarPrefetch = 1;             // RT_KERNEL_FLAG_PREFETCH
 constexpr int kVarWaveGate = 2;             // RT_KERNEL_FLAG_WAVE_GATE
-constexpr int kVarSkipRun = 4;             // RT_KERNEL_FLAG_SKIP_RUN: provably empty runs in a tight loop
+constexpr int kVarSkipRun = 4;             // RT_KERNEL_FLAG_SKIP_RUN: wave-uniform empty runs in a tight loop
 constexpr int kVarDistSkip = 8;             // RT_KERNEL_FLAG_DIST_SKIP
 constexpr int kVarNestedStep = 16;          // RT_KERNEL_FLAG_NESTED_STEP (A/B arm)
 constexpr int kVarPreGate = 32;             // RT_KERNEL_FLAG_PRE_GATE
@@ -652,36 +652,6 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, const uint32_t 
                 RT_DDA_ADVANCE_PACKED(nct_ax, more);
             else
                 RT_DDA_ADVANCE_ADD(nct_ax, more);
-            if constexpr ((VAR & kVarSkipRun) != 0 && (VAR & kVarPackedRem) != 0 && !STATS)
-            {
-                // The next `skip` cells are provably empty (L-inf distance field): take their
-                // steps in a tight loop with no cell index or test work -- the same advances as
-                // the one-step-per-iteration form -- and move `cell` once by the steps each axis
-                // took (the drop of its remaining count).  An exit inside the run leaves the
-                // walk, where cell is dead.
-                if (kb >= ke && skip > 0 && more)
-                {
-                    const int r0 = remp;
-                    int n = skip;
-                    do
-                    {
-                        const float m_ = __builtin_fminf(__builtin_fminf(nct0, nct1), nct2);
-                        const bool a2_ = nct2 == m_;
-                        const bool a1_ = !a2_ && nct1 == m_;
-                        const bool a0_ = !a2_ && !a1_;
-                        remp -= a2_ ? (1 << 22) : (a1_ ? (1 << 11) : 1);
-                        more = (remp & kRemGuards) == 0;
-                        nct0 += a0_ ? dt0 : 0.0f;
-                        nct1 += a1_ ? dt1 : 0.0f;
-                        nct2 += a2_ ? dt2 : 0.0f;
-                    } while (--n > 0 && more);
-                    if (!more) break;
-                    cell += ((r0 & 1023) - (remp & 1023)) * cs0 + (((r0 >> 11) & 1023) - ((remp >> 11) & 1023)) * cs1 +
-                            (((r0 >> 22) & 511) - ((remp >> 22) & 511)) * cs2;
-                    skip = 0;
-                    continue;
-                }
-            }
             if constexpr ((VAR & kVarBail) != 0)
             {
                 // two-phase arm: a sample whose walk would pass bail_tests tests stops here and
@@ -702,6 +672,34 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, const uint32_t 
             if (kb < ke && test_cell<STATS, TRI, VAR>(P, ox, oy, oz, dx, dy, dz, kb, ke, nct_ax, t, u, v, tri, tests))
                 return true;
             if (!more) break;
+            if constexpr ((VAR & kVarSkipRun) != 0 && (VAR & kVarPackedRem) != 0 && (VAR & kVarSelStep) == 0 &&
+                          !STATS)
+            {
+                // Wave-uniform empty run: while every active lane is inside a run of cells the
+                // distance field proves empty, the wave takes bare DDA steps -- the same advances
+                // and the same exits as one iteration per cell, with no cell word or test work.
+                // Uniform, so no lane waits on another's run; the run ends when the first lane's
+                // does.
+                if (__all(skip > 0))
+                {
+                    bool more;
+                    do
+                    {
+                        skip--;
+                        const float m_ = __builtin_fminf(__builtin_fminf(nct0, nct1), nct2);
+                        const bool a2_ = nct2 == m_;
+                        const bool a1_ = !a2_ && nct1 == m_;
+                        const bool a0_ = !a2_ && !a1_;
+                        remp -= a2_ ? (1 << 22) : (a1_ ? (1 << 11) : 1);
+                        more = (remp & kRemGuards) == 0;
+                        nct0 += a0_ ? dt0 : 0.0f;
+                        nct1 += a1_ ? dt1 : 0.0f;
+                        nct2 += a2_ ? dt2 : 0.0f;
+                        cell += a2_ ? cs2 : (a1_ ? cs1 : cs0);
+                    } while (__all((skip > 0) & more));
+                    if (!more) break;
+                }
+            }
         }
         return false;
     }
@@ -1972,13 +1970,13 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
     const uint32_t fk = (kind == RT_KERNEL_AUTO || kind == RT_KERNEL_COMPACT || kind == RT_KERNEL_WIDE)
                             ? (f->kernel | RT_KERNEL_LANES | RT_KERNEL_FLAG_WAVE_GATE | RT_KERNEL_FLAG_DIST_SKIP |
                                RT_KERNEL_FLAG_ORIGIN_PRE | RT_KERNEL_FLAG_FAST_RCP | RT_KERNEL_FLAG_PACKED_REM |
-                               RT_KERNEL_FLAG_XCD_BANDS | RT_KERNEL_FLAG_UNIFORM_CELLS)
+                               RT_KERNEL_FLAG_XCD_BANDS | RT_KERNEL_FLAG_UNIFORM_CELLS | RT_KERNEL_FLAG_SKIP_RUN)
                             : f->kernel;
     if ((fk & RT_KERNEL_FLAG_ORIGIN_PRE) && lanes && P.isect == RT_ISECT_GRID &&
         P.tri_test == RT_TRI_MOLLER_TRUMBORE && s->nrefs)
         hipLaunchKernelGGL(k_origin_pre, dim3((s->nrefs + kWG - 1) / kWG), dim3(kWG), 0, st, s->d_refs, s->d_frefs,
                            s->nrefs, P.org[0], P.org[1], P.org[2]);
-    const int var = ((fk & RT_KERNEL_FLAG_PREFETCH) ? kVarPrefetch : 0) |
+    int var = ((fk & RT_KERNEL_FLAG_PREFETCH) ? kVarPrefetch : 0) |
                     ((fk & RT_KERNEL_FLAG_WAVE_GATE) ? kVarWaveGate : 0) |
                     ((fk & RT_KERNEL_FLAG_SKIP_RUN) ? kVarSkipRun : 0) |
                     ((fk & RT_KERNEL_FLAG_DIST_SKIP) ? kVarDistSkip : 0) |
@@ -1994,6 +1992,11 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
                     ((fk & RT_KERNEL_FLAG_UNIFORM_CELLS) ? kVarUniform : 0) |
                     ((fk & RT_KERNEL_FLAG_LDS_CELLS) ? kVarLdsCells : 0) |
                     ((fk & RT_KERNEL_FLAG_ALT_LOADS) ? kVarAltLoads : 0);
+    // the wave-uniform empty run needs the packed counts (scenes with a grid dimension > 512
+    // walk without it)
+    if (!(var & kVarPackedRem)) var &= ~kVarSkipRun;
+    // the two-phase and wide arms run AUTO's per-ray code; the empty run is not part of them
+    const int wvar = var & ~kVarSkipRun;
     if (var & kVarWaveClock)
     {
         const size_t need = size_t(blocks) * (kWG / 64u) * 4u;
@@ -2021,7 +2024,7 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
     // (+6-10 %) and the re-trace cost more than they save.
     if (((f->kernel & RT_KERNEL_FLAG_BAIL_WIDE) || bail_auto) && lanes &&
         (kind == RT_KERNEL_AUTO || kind == RT_KERNEL_LANES) && P.isect == RT_ISECT_GRID && !bary &&
-        (var == 14858 || var == 80394) && P.spp * kWideG <= 64u)
+        (wvar == 14858 || wvar == 80394) && P.spp * kWideG <= 64u)
     {
         const size_t need = size_t(n_local_tiles) * kTilePix + 1u;   // count + one entry per pixel
         if (need > s->bail_cap)
@@ -2037,7 +2040,7 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
         P.bail_count = s->d_bail;
         P.bail_queue = s->d_bail + 1;
         RT_HIP(hipMemsetAsync(s->d_bail, 0, sizeof(uint32_t), st));
-        if (var == 80394)
+        if (wvar == 80394)
             hipLaunchKernelGGL((k_render_bail1<80394 | kVarBail>), dim3(uint32_t(blocks)), wg, 0, st, P);
         else
             hipLaunchKernelGGL((k_render_bail1<14858 | kVarBail>), dim3(uint32_t(blocks)), wg, 0, st, P);
@@ -2046,7 +2049,7 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
         else
             hipLaunchKernelGGL((k_render_bailed<14858, kWideG>), dim3(s->bail_wgs), wg, 0, st, P);
     }
-    else if (lanes && kind == RT_KERNEL_WIDE && P.isect == RT_ISECT_GRID && !bary && (var == 14858 || var == 80394) &&
+    else if (lanes && kind == RT_KERNEL_WIDE && P.isect == RT_ISECT_GRID && !bary && (wvar == 14858 || wvar == 80394) &&
         P.spp * kWideG <= 64u)
     {
         if (g16)
@@ -2120,6 +2123,9 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
         else if (var == 96778) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 96778>), grid, wg, 0, st, P);
         else if (var == 47626) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 47626>), grid, wg, 0, st, P);
         else if (var == 80394) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 80394>), grid, wg, 0, st, P);
+        else if (var == 78350) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 78350>), grid, wg, 0, st, P);
+        else if (var == (80398 | kVarWaveClock))
+            hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 80398 | kVarWaveClock>), grid, wg, 0, st, P);
         else if (var == 113162) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 113162>), grid, wg, 0, st, P);
         // AUTO on scenes outside the FAST_RCP / PACKED_REM ranges
         else if (var == 8714) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 8714>), grid, wg, 0, st, P);

@@ -84,7 +84,7 @@ enum rt_intersector {
 enum rt_kernel {
     RT_KERNEL_AUTO = 0,        /* the fastest measured variant for the frame's spp (LANES + WAVE_GATE
                                   + DIST_SKIP + ORIGIN_PRE + FAST_RCP + PACKED_REM + XCD_BANDS +
-                                  UNIFORM_CELLS; BAIL_WIDE for >= 2-rank shards of dense scenes, with
+                                  UNIFORM_CELLS + SKIP_RUN; BAIL_WIDE for >= 2-rank shards of dense scenes, with
                                   WIDE16 and budget 128 from 4 ranks) */
     RT_KERNEL_LANES = 1,       /* one lane per sample, a pixel's samples in adjacent lanes */
     RT_KERNEL_PIXEL_LOOP = 2,  /* one lane per pixel looping over its samples (any spp) */
@@ -103,8 +103,9 @@ enum rt_kernel {
                                          references is staged through LDS 64 records at a time */
     RT_KERNEL_FLAG_PREFETCH = 0x100,  /* OR-able: software-pipelined triangle record loads */
     RT_KERNEL_FLAG_WAVE_GATE = 0x200, /* OR-able: skip a test's second half when no lane needs it */
-    RT_KERNEL_FLAG_SKIP_RUN = 0x400,  /* OR-able (with DIST_SKIP + PACKED_REM): a run of cells the
-                                         distance field proves empty is stepped in a tight loop */
+    RT_KERNEL_FLAG_SKIP_RUN = 0x400,  /* OR-able (with DIST_SKIP + PACKED_REM; in AUTO): while every
+                                         active lane is in a run of cells the distance field proves
+                                         empty, the wave takes bare DDA steps in a tight loop */
     RT_KERNEL_FLAG_CSR_OFFSETS = 0x800, /* OR-able: read the two CSR offsets per cell instead of
                                            the packed (start << 11 | count) word */
     RT_KERNEL_FLAG_DIST_SKIP = 0x1000,  /* OR-able: skip lookups of cells an L-inf distance field

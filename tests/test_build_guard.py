@@ -58,8 +58,7 @@ def test_render_kernels_do_not_spill(tmp_path):
     for n, (sc, vg) in lanes.items():
         assert sc == 0, f"{n} spills {sc} B/lane"
     # the AUTO kernel (lanes + wave gate + distance skip + origin terms + Newton reciprocal +
-    # packed counts, Moller-Trumbore), its plain-division arm and its no-precompute arm keep
-    # 8 waves/SIMD
-    for key in ("ILi0ELi14858E", "ILi0ELi6666E", "ILi0ELi522E", "ILi0ELi10E"):
+    # packed counts + uniform cells + empty runs, Moller-Trumbore) and its arms keep 8 waves/SIMD
+    for key in ("ILi0ELi80398E", "ILi0ELi80394E", "ILi0ELi14858E", "ILi0ELi6666E", "ILi0ELi522E", "ILi0ELi10E"):
         arm = [v for n, v in lanes.items() if key in n]
         assert arm and arm[0][1] <= 64, (key, arm)
