@@ -77,6 +77,7 @@ constexpr int kVarUniform = 65536;          // RT_KERNEL_FLAG_UNIFORM_CELLS: sca
 constexpr int kVarBail = 131072;            // RT_KERNEL_FLAG_BAIL_WIDE phase 1: test budget + pixel queue
 constexpr int kVarLdsCells = 262144;        // RT_KERNEL_FLAG_LDS_CELLS: long uniform lists staged through LDS
 constexpr int kVarAltLoads = 524288;        // RT_KERNEL_FLAG_ALT_LOADS: uniform loop on two record sets in turn
+constexpr int kVarCenterOut = 1048576;      // RT_KERNEL_FLAG_CENTER_OUT: XCD row turns from the middle row out
 constexpr uint32_t kMarchSteps = 128;       // renderer.cpp:26
 constexpr uint32_t kDistBlock = 32;         // triangles per culling block of the distance kernels
 
@@ -1049,6 +1050,16 @@ constexpr uint32_t kBailAutoRanks = 2;      // AUTO: two-phase arm from this man
 constexpr uint32_t kBailAutoRefs = 128;     // ... on scenes with a cell this dense: budget 256 and
 constexpr uint32_t kBailAutoWideRanks = 4;  // 4 lanes per sample, from 4 ranks budget 128 and 16
 constexpr uint32_t kBailAutoTests = 128;    // lanes (tools/shard_scaling.py)
+// Center-out row order (kVarCenterOut): dispatch turn j takes row m, m - 1, m + 1, m - 2, ...
+// (m = R / 2), a bijection on [0, R).  A camera frames its subject, so the dense rows -- whose
+// waves are the launch's longest -- start first instead of mid-launch.
+__device__ __forceinline__ uint32_t center_out_row(uint32_t j, uint32_t R)
+{
+    const uint32_t m = R / 2u;
+    return (j & 1u) ? m - (j + 1u) / 2u : m + j / 2u;
+}
+
+template <bool CENTER = false>
 __device__ __forceinline__ uint32_t xcd_band_block(uint32_t b, uint32_t nb, uint32_t chunk)
 {
     if (chunk == 0u)
@@ -1060,7 +1071,8 @@ __device__ __forceinline__ uint32_t xcd_band_block(uint32_t b, uint32_t nb, uint
     const uint32_t full = nb / (kXcds * chunk) * (kXcds * chunk);
     if (b >= full) return b;
     const uint32_t x = b % kXcds, i = b / kXcds;
-    return ((i / chunk) * kXcds + x) * chunk + i % chunk;
+    const uint32_t row = (i / chunk) * kXcds + x;
+    return (CENTER ? center_out_row(row, full / chunk) : row) * chunk + i % chunk;
 }
 
 // RT_KERNEL_LANES: one lane per sample (spp = 2^spp_shift <= 64), one work item per wave,
@@ -1068,7 +1080,9 @@ __device__ __forceinline__ uint32_t xcd_band_block(uint32_t b, uint32_t nb, uint
 template <int TRI, int VAR>
 __global__ void __launch_bounds__(kWG) k_render_lanes(KParams P)
 {
-    const uint32_t b = (VAR & kVarXcdBands) ? xcd_band_block(blockIdx.x, gridDim.x, P.xcd_chunk) : blockIdx.x;
+    const uint32_t b = (VAR & kVarXcdBands)
+                           ? xcd_band_block<(VAR & kVarCenterOut) != 0>(blockIdx.x, gridDim.x, P.xcd_chunk)
+                           : blockIdx.x;
     const uint32_t item = b * (kWG / 64u) + (threadIdx.x >> 6);
     if (VAR & kVarWaveClock)
     {
@@ -1861,7 +1875,7 @@ int validate_frame(const rt_frame *f)
         return fail(RT_E_INVALID, "IntersectBruteForce uses IntersectRayTri only (renderer.cpp:176)");
     if ((f->kernel & RT_KERNEL_KIND_MASK) > RT_KERNEL_WIDE ||
         (f->kernel & ~(RT_KERNEL_KIND_MASK | RT_KERNEL_FLAG_LDS_CELLS | RT_KERNEL_FLAG_WIDE16 |
-                       RT_KERNEL_FLAG_ALT_LOADS | RT_KERNEL_FLAG_PREFETCH | RT_KERNEL_FLAG_WAVE_GATE | RT_KERNEL_FLAG_SKIP_RUN |
+                       RT_KERNEL_FLAG_ALT_LOADS | RT_KERNEL_FLAG_CENTER_OUT | RT_KERNEL_FLAG_PREFETCH | RT_KERNEL_FLAG_WAVE_GATE | RT_KERNEL_FLAG_SKIP_RUN |
                        RT_KERNEL_FLAG_CSR_OFFSETS | RT_KERNEL_FLAG_DIST_SKIP | RT_KERNEL_FLAG_NESTED_STEP |
                        RT_KERNEL_FLAG_PRE_GATE | RT_KERNEL_FLAG_EXHAUSTIVE | RT_KERNEL_FLAG_ORIGIN_PRE |
                        RT_KERNEL_FLAG_SELECT_STEP | RT_KERNEL_FLAG_FAST_RCP | RT_KERNEL_FLAG_PACKED_REM |
@@ -1991,7 +2005,8 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
                     ((fk & RT_KERNEL_FLAG_WAVE_CLOCK) ? kVarWaveClock : 0) |
                     ((fk & RT_KERNEL_FLAG_UNIFORM_CELLS) ? kVarUniform : 0) |
                     ((fk & RT_KERNEL_FLAG_LDS_CELLS) ? kVarLdsCells : 0) |
-                    ((fk & RT_KERNEL_FLAG_ALT_LOADS) ? kVarAltLoads : 0);
+                    ((fk & RT_KERNEL_FLAG_ALT_LOADS) ? kVarAltLoads : 0) |
+                    ((fk & RT_KERNEL_FLAG_CENTER_OUT) ? kVarCenterOut : 0);
     // the wave-uniform empty run needs the packed counts (scenes with a grid dimension > 512
     // walk without it)
     if (!(var & kVarPackedRem)) var &= ~kVarSkipRun;
@@ -2124,6 +2139,11 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
         else if (var == 47626) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 47626>), grid, wg, 0, st, P);
         else if (var == 80394) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 80394>), grid, wg, 0, st, P);
         else if (var == 78350) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 78350>), grid, wg, 0, st, P);
+        else if (var == (80398 | kVarCenterOut))
+            hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 80398 | kVarCenterOut>), grid, wg, 0, st, P);
+        else if (var == (80398 | kVarCenterOut | kVarWaveClock))
+            hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 80398 | kVarCenterOut | kVarWaveClock>), grid, wg,
+                               0, st, P);
         else if (var == (80398 | kVarWaveClock))
             hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 80398 | kVarWaveClock>), grid, wg, 0, st, P);
         else if (var == 113162) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 113162>), grid, wg, 0, st, P);
