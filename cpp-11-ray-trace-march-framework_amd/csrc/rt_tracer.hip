@@ -1168,10 +1168,26 @@ __device__ __forceinline__ void wide_trace(const KParams& P, uint32_t k, uint32_
                     {
                         float bt = rtd::kFltMax, bu = 0.0f, bv = 0.0f;
                         uint32_t bk = 0xFFFFFFFFu;
+                        // record k + G loads while record k is tested: the wide phase runs few,
+                        // latency-bound waves, so the extra registers cost no throughput
+                        float4 n0, n1, n2;
+                        if (kb + sub < ke)
+                        {
+                            const float4 *rp = P.frefs + size_t(kb + sub) * 3;
+                            n0 = rp[0];
+                            n1 = rp[1];
+                            n2 = rp[2];
+                        }
                         for (uint32_t k = kb + sub; k < ke; k += uint32_t(G))
                         {
-                            const float4 *rp = P.frefs + size_t(k) * 3;
-                            const float4 r0 = rp[0], r1 = rp[1], r2 = rp[2];
+                            const float4 r0 = n0, r1 = n1, r2 = n2;
+                            if (k + uint32_t(G) < ke)
+                            {
+                                const float4 *rp = P.frefs + size_t(k + uint32_t(G)) * 3;
+                                n0 = rp[0];
+                                n1 = rp[1];
+                                n2 = rp[2];
+                            }
                             float ct, cu, cv;
                             const bool h = rtd::ray_tri_mt_gated_pre<(VAR & kVarFastRcp) != 0>(
                                 dx, dy, dz, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w,
@@ -1274,7 +1290,7 @@ __global__ void __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(8, 8))
 // lane's chain is a quarter long, and the pixel's samples are summed in order as in phase 1.
 // Persistent waves take queue entries round-robin; every pixel is stored by exactly one phase.
 template <int VAR, int G>
-__global__ void __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(8, 8))) k_render_bailed(KParams P)
+__global__ void __launch_bounds__(kWG) k_render_bailed(KParams P)
 {
     const uint32_t n = *P.bail_count;                                // phase 1 finished on this stream
     const uint32_t lpp = P.spp * uint32_t(G);                        // lanes per pixel (<= 64)
