@@ -668,11 +668,13 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, const uint32_t 
                     *bailed = budget < 0;
                     break;
                 }
-                continue;
             }
-            if (kb < ke && test_cell<STATS, TRI, VAR>(P, ox, oy, oz, dx, dy, dz, kb, ke, nct_ax, t, u, v, tri, tests))
-                return true;
-            if (!more) break;
+            else
+            {
+                if (kb < ke && test_cell<STATS, TRI, VAR>(P, ox, oy, oz, dx, dy, dz, kb, ke, nct_ax, t, u, v, tri, tests))
+                    return true;
+                if (!more) break;
+            }
             if constexpr ((VAR & kVarSkipRun) != 0 && (VAR & kVarPackedRem) != 0 && (VAR & kVarSelStep) == 0 &&
                           !STATS)
             {
@@ -1276,7 +1278,7 @@ __global__ void __launch_bounds__(kWG) k_render_wide(KParams P)
 
 // RT_KERNEL_FLAG_BAIL_WIDE, phase 1: the AUTO kernel with the test budget, held to 8 waves/SIMD
 template <int VAR>
-__global__ void __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(8, 8))) k_render_bail1(KParams P)
+__global__ void __launch_bounds__(kWG) k_render_bail1(KParams P)
 {
     const uint32_t b = (VAR & kVarXcdBands) ? xcd_band_block(blockIdx.x, gridDim.x, P.xcd_chunk) : blockIdx.x;
     process_item<RT_TRI_MOLLER_TRUMBORE, VAR>(P, nullptr, b * (kWG / 64u) + (threadIdx.x >> 6));
@@ -2026,7 +2028,7 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
     // the wave-uniform empty run needs the packed counts (scenes with a grid dimension > 512
     // walk without it)
     if (!(var & kVarPackedRem)) var &= ~kVarSkipRun;
-    // the two-phase and wide arms run AUTO's per-ray code; the empty run is not part of them
+    // the wide arms run AUTO's per-ray code without the empty run (phase 1 keeps it)
     const int wvar = var & ~kVarSkipRun;
     if (var & kVarWaveClock)
     {
@@ -2071,7 +2073,9 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
         P.bail_count = s->d_bail;
         P.bail_queue = s->d_bail + 1;
         RT_HIP(hipMemsetAsync(s->d_bail, 0, sizeof(uint32_t), st));
-        if (wvar == 80394)
+        if (var == 80398)
+            hipLaunchKernelGGL((k_render_bail1<80398 | kVarBail>), dim3(uint32_t(blocks)), wg, 0, st, P);
+        else if (wvar == 80394)
             hipLaunchKernelGGL((k_render_bail1<80394 | kVarBail>), dim3(uint32_t(blocks)), wg, 0, st, P);
         else
             hipLaunchKernelGGL((k_render_bail1<14858 | kVarBail>), dim3(uint32_t(blocks)), wg, 0, st, P);
