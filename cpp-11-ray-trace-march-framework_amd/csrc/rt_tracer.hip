@@ -1049,9 +1049,12 @@ constexpr uint32_t kXcds = 8;
 constexpr uint32_t kWideG = 4;              // RT_KERNEL_WIDE: lanes per sample
 constexpr uint32_t kBailTests = 256;        // BAIL_WIDE: default phase-1 test budget per sample
 constexpr uint32_t kBailAutoRanks = 2;      // AUTO: two-phase arm from this many shard ranks ...
-constexpr uint32_t kBailAutoRefs = 128;     // ... on scenes with a cell this dense: budget 256 and
-constexpr uint32_t kBailAutoWideRanks = 4;  // 4 lanes per sample, from 4 ranks budget 128 and 16
-constexpr uint32_t kBailAutoTests = 128;    // lanes (tools/shard_scaling.py)
+constexpr uint32_t kBailAutoRefs = 128;     // ... on scenes with a cell this dense, 16 lanes per
+// sample, and a budget that shrinks as the shard does (tools/shard_scaling.py)
+__host__ __device__ constexpr uint32_t bail_auto_tests(uint32_t nranks)
+{
+    return nranks >= 8u ? 128u : (nranks >= 4u ? 192u : 384u);
+}
 // Center-out row order (kVarCenterOut): dispatch turn j takes row m, m - 1, m + 1, m - 2, ...
 // (m = R / 2), a bijection on [0, R).  A camera frames its subject, so the dense rows -- whose
 // waves are the launch's longest -- start first instead of mid-launch.
@@ -2047,14 +2050,14 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
     const dim3 wg(kWG);
     // RT_KERNEL_FLAG_WIDE16: 16 lanes per sample in the wide kernel / wide phase (spp <= 4)
     const bool bail_auto = kind == RT_KERNEL_AUTO && P.nranks >= kBailAutoRanks && s->max_cell_refs >= kBailAutoRefs;
-    const bool wide_auto = bail_auto && P.nranks >= kBailAutoWideRanks && !(f->kernel & RT_KERNEL_FLAG_BAIL_WIDE);
+    const bool wide_auto = bail_auto && !(f->kernel & RT_KERNEL_FLAG_BAIL_WIDE);
     const bool g16 = ((f->kernel & RT_KERNEL_FLAG_WIDE16) || wide_auto) && P.spp * 16u <= 64u;
     // AUTO takes the two-phase arm for a shard of >= 2 ranks of a scene with dense cells: there a
-    // rank's launch is bound by its few ~1000-test waves, which the wide phase splits 4 or 16
-    // ways (measured, tools/shard_scaling.py, killeroo rank of 2 / 4 / 8: 0.60 / 0.50 / 0.46 ms
-    // -> 0.55 (budget 256, 4 lanes) / 0.41 / 0.26 (budget 128, 16 lanes); scene 5 rank of 8
-    // 0.69 -> 0.29).  On a whole frame, or a scene without dense cells, phase 1's budget count
-    // (+6-10 %) and the re-trace cost more than they save.
+    // rank's launch is bound by its few ~1000-test waves, which the wide phase splits 16 ways
+    // (measured, tools/shard_scaling.py, killeroo rank of 2 / 4 / 8: 0.60 / 0.50 / 0.46 ms with
+    // the plain kernel -> 0.48 / 0.35 / 0.25 with budgets 384 / 192 / 128).  On a whole frame,
+    // or a scene without dense cells, phase 1's budget count and the re-trace cost more than
+    // they save.
     if (((f->kernel & RT_KERNEL_FLAG_BAIL_WIDE) || bail_auto) && lanes &&
         (kind == RT_KERNEL_AUTO || kind == RT_KERNEL_LANES) && P.isect == RT_ISECT_GRID && !bary &&
         (wvar == 14858 || wvar == 80394) && P.spp * kWideG <= 64u)
@@ -2069,7 +2072,7 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
             s->bail_cap = need;
         }
         const uint32_t tb = (f->kernel & RT_KERNEL_COMPACT_REFILL_MASK) >> RT_KERNEL_COMPACT_REFILL_SHIFT;
-        P.bail_tests = tb ? 16u * tb : (wide_auto ? kBailAutoTests : kBailTests);
+        P.bail_tests = tb ? 16u * tb : (wide_auto ? bail_auto_tests(P.nranks) : kBailTests);
         P.bail_count = s->d_bail;
         P.bail_queue = s->d_bail + 1;
         RT_HIP(hipMemsetAsync(s->d_bail, 0, sizeof(uint32_t), st));

@@ -84,8 +84,8 @@ enum rt_intersector {
 enum rt_kernel {
     RT_KERNEL_AUTO = 0,        /* the fastest measured variant for the frame's spp (LANES + WAVE_GATE
                                   + DIST_SKIP + ORIGIN_PRE + FAST_RCP + PACKED_REM + XCD_BANDS +
-                                  UNIFORM_CELLS + SKIP_RUN; BAIL_WIDE for >= 2-rank shards of dense scenes, with
-                                  WIDE16 and budget 128 from 4 ranks) */
+                                  UNIFORM_CELLS + SKIP_RUN; for >= 2-rank shards of dense scenes BAIL_WIDE
+                                  with WIDE16, budget 384 / 192 / 128 from 2 / 4 / 8 ranks) */
     RT_KERNEL_LANES = 1,       /* one lane per sample, a pixel's samples in adjacent lanes */
     RT_KERNEL_PIXEL_LOOP = 2,  /* one lane per pixel looping over its samples (any spp) */
     RT_KERNEL_COMPACT = 3,     /* AUTO's per-ray code in persistent waves with wavefront active-ray

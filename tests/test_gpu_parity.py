@@ -224,9 +224,9 @@ def test_lds_cells_vs_oracle(scenes, oracle, sid, spp):
 
 @pytest.mark.parametrize("sid,nranks", [(8, 8), (5, 8), (8, 3), (4, 16), (8, 2), (5, 4)])
 def test_shard_partition_dense_scenes(golden, scenes, sid, nranks):
-    """Shards of >= 2 ranks of a dense scene take AUTO's two-phase arm (budget 256 with 4 lanes
-    per sample below 4 ranks, budget 128 with 16 lanes from 4); every partition reassembles
-    into the reference frame."""
+    """Shards of >= 2 ranks of a dense scene take AUTO's two-phase arm (16 lanes per sample,
+    budget 384 / 192 / 128 from 2 / 4 / 8 ranks); every partition reassembles into the
+    reference frame."""
     import torch
     hs, gs = scenes(sid)
     W, H = 1920, 1080
