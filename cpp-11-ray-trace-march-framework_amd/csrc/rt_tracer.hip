@@ -124,6 +124,8 @@ struct KParams
     uint32_t bail_tests;        // BAIL_WIDE phase 1: test budget per sample
     uint32_t *bail_count;       // BAIL_WIDE: queued pixels
     uint32_t *bail_queue;       // BAIL_WIDE: (local tile << 8 | Morton pixel) per queued pixel
+    float4 *bail_state;         // BAIL_WIDE: per sample slot of a queued pixel, 2 x float4: the walk
+                                // state where phase 1 stopped, or (kb > ke) its finished colour
     // output
     uint32_t *out;
     uint32_t pitch;             // frame mode: words per row of out
@@ -611,7 +613,7 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, const uint32_t 
                                                float dx, float dy, float dz,
                                                float& t, float& u, float& v, uint32_t& tri,
                                                uint32_t& voxel, uint32_t& steps, uint32_t& tests,
-                                               bool *bailed = nullptr)
+                                               bool *bailed = nullptr, uint32_t bail_idx = 0u)
 {
     float nct0, nct1, nct2, dt0, dt1, dt2;
     int rem0, rem1, rem2, cs0, cs1, cs2, cell;
@@ -666,6 +668,15 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, const uint32_t 
                 if (!more || budget < 0)
                 {
                     *bailed = budget < 0;
+                    if (budget < 0)
+                    {
+                        // where the walk stopped: the untested cell [kb, ke) with its exit time
+                        // and the state after its step -- phase 2 resumes exactly here
+                        P.bail_state[2 * size_t(bail_idx)] = make_float4(nct0, nct1, nct2, nct_ax);
+                        P.bail_state[2 * size_t(bail_idx) + 1] =
+                            make_float4(__int_as_float(remp), __int_as_float(cell), __uint_as_float(kb),
+                                        __uint_as_float(ke));
+                    }
                     break;
                 }
             }
@@ -871,7 +882,7 @@ __device__ __forceinline__ bool ray_march(const KParams& P, float ox, float oy, 
 template <bool STATS, int TRI, int VAR>
 __device__ __forceinline__ void trace_sample(const KParams& P, const uint32_t *lds_occ, uint32_t px, uint32_t py,
                                              uint32_t s, float& cr, float& cg, float& cb,
-                                             rt_sample_rec *rec, bool *bailed = nullptr)
+                                             rt_sample_rec *rec, bool *bailed = nullptr, uint32_t bail_idx = 0u)
 {
     const float2 so = P.smp[s];
     float dx, dy, dz;
@@ -887,7 +898,7 @@ __device__ __forceinline__ void trace_sample(const KParams& P, const uint32_t *l
     else
     {
         hit = grid_intersect<STATS, TRI, VAR>(P, lds_occ, P.org[0], P.org[1], P.org[2], dx, dy, dz, t, u, v, tri,
-                                              voxel, steps, tests, bailed);
+                                              voxel, steps, tests, bailed, bail_idx);
         if ((VAR & kVarOriginPre) && TRI == RT_TRI_MOLLER_TRUMBORE && hit)
             tri = __float_as_uint(P.refs[3 * size_t(tri) + 2].y);     // CSR reference -> triangle id
     }
@@ -996,7 +1007,8 @@ __device__ __forceinline__ void process_item(const KParams& P, const uint32_t *l
     {
         const ItemCoord ic = item_coord(P, item, lane);
         if (ic.valid)
-            trace_sample<false, TRI, VAR>(P, lds_occ, ic.x, ic.y, ic.s, cr, cg, cb, nullptr, &bailed);
+            trace_sample<false, TRI, VAR>(P, lds_occ, ic.x, ic.y, ic.s, cr, cg, cb, nullptr, &bailed,
+                                          item * 64u + lane);
     }
     const ItemCoord ic = item_coord(P, item, lane);
     const uint32_t base = lane & ~(P.spp - 1u);
@@ -1027,7 +1039,17 @@ __device__ __forceinline__ void process_item(const KParams& P, const uint32_t *l
                 P.bail_queue[base_q + r] = (ic.c.k << 8) | ic.p;
             }
         }
-        if (pixel_bailed) return;
+        if (pixel_bailed)
+        {
+            // the pixel's finished samples hand their colour to phase 2 (kb = 1 > ke = 0)
+            if (ic.valid && !bailed)
+            {
+                const size_t i = 2 * (size_t(item) * 64u + lane);
+                P.bail_state[i] = make_float4(cr, cg, cb, 0.0f);
+                P.bail_state[i + 1] = make_float4(0.0f, 0.0f, __uint_as_float(1u), __uint_as_float(0u));
+            }
+            return;
+        }
     }
     if (ic.valid && ic.s == 0)
     {
@@ -1129,7 +1151,7 @@ __global__ void __launch_bounds__(kWG) k_render_lanes(KParams P)
 // One sample of the wide mode, traced by the G lanes of a group (sub = this lane's index in it):
 // the same walk in every lane of the group, each cell's list split over the group.  Returns the
 // sample's colour in every lane of the group.
-template <int VAR, int G>
+template <int VAR, int G, bool RESUME = false>
 __device__ __forceinline__ void wide_trace(const KParams& P, uint32_t k, uint32_t slot, uint32_t sub, float& cr,
                                            float& cg, float& cb)
 {
@@ -1138,6 +1160,21 @@ __device__ __forceinline__ void wide_trace(const KParams& P, uint32_t k, uint32_
     cr = cg = cb = 0.0f;
     {
         const ItemCoord ic = tile_slot_coord(P, k, slot);
+        float4 st0, st1;
+        if (RESUME && ic.valid)
+        {
+            // phase 2: the sample's state from phase 1 (slot index = item * 64 + lane there)
+            const size_t i = 2 * (size_t(k) * kTilePix * P.spp + slot);
+            st0 = P.bail_state[i];
+            st1 = P.bail_state[i + 1];
+            if (__float_as_uint(st1.z) > __float_as_uint(st1.w))
+            {
+                cr = st0.x;                       // finished in phase 1
+                cg = st0.y;
+                cb = st0.z;
+                return;
+            }
+        }
         if (ic.valid)
         {
             const float2 so = P.smp[ic.s];
@@ -1153,22 +1190,44 @@ __device__ __forceinline__ void wide_trace(const KParams& P, uint32_t k, uint32_
             {
                 int skip = 0;
                 int remp = rem0 | (rem1 << 11) | (rem2 << 22);
+                bool pending = false;
+                if (RESUME)
+                {
+                    nct0 = st0.x;
+                    nct1 = st0.y;
+                    nct2 = st0.z;
+                    remp = __float_as_int(st1.x);
+                    cell = __float_as_int(st1.y);
+                    pending = true;
+                }
                 for (;;)
                 {
                     uint32_t kb = 0u, ke = 0u;
-                    if (skip == 0)
-                    {
-                        const uint32_t w = P.cellw[uint32_t(cell)];
-                        const uint32_t cnt = w & 2047u;
-                        kb = w >> 11;
-                        ke = kb + cnt;
-                        skip = cnt ? 0 : int(kb) - 1;
-                    }
-                    else
-                        skip--;
                     float nct_ax;
                     bool more;
-                    RT_DDA_ADVANCE_PACKED(nct_ax, more);
+                    if (RESUME && pending)
+                    {
+                        // the cell phase 1 stopped before testing, then the walk from its step on
+                        kb = __float_as_uint(st1.z);
+                        ke = __float_as_uint(st1.w);
+                        nct_ax = st0.w;
+                        more = (remp & kRemGuards) == 0;
+                        pending = false;
+                    }
+                    else
+                    {
+                        if (skip == 0)
+                        {
+                            const uint32_t w = P.cellw[uint32_t(cell)];
+                            const uint32_t cnt = w & 2047u;
+                            kb = w >> 11;
+                            ke = kb + cnt;
+                            skip = cnt ? 0 : int(kb) - 1;
+                        }
+                        else
+                            skip--;
+                        RT_DDA_ADVANCE_PACKED(nct_ax, more);
+                    }
                     if (kb < ke)
                     {
                         float bt = rtd::kFltMax, bu = 0.0f, bv = 0.0f;
@@ -1310,7 +1369,7 @@ __global__ void __launch_bounds__(kWG) k_render_bailed(KParams P)
         const uint32_t q = live ? P.bail_queue[e] : 0u;
         const uint32_t k = q >> 8, p = q & 255u;
         float cr = 0.0f, cg = 0.0f, cb = 0.0f;
-        if (live) wide_trace<VAR, G>(P, k, p * P.spp + smp, sub, cr, cg, cb);
+        if (live) wide_trace<VAR, G, true>(P, k, p * P.spp + smp, sub, cr, cg, cb);
         float sr = 0.0f, sg = 0.0f, sb = 0.0f;
         for (uint32_t j = 0; j < P.spp; j++)
         {
@@ -1828,6 +1887,8 @@ struct rt_scene
     bool pack_ok = false;           // dims <= 512: the remaining-cell counts pack into one word
     uint32_t *d_bail = nullptr;     // RT_KERNEL_FLAG_BAIL_WIDE: queued-pixel count + queue
     size_t bail_cap = 0;
+    float4 *d_bail_state = nullptr; // RT_KERNEL_FLAG_BAIL_WIDE: phase 1 -> phase 2 per-sample state
+    size_t bail_state_cap = 0;
     uint32_t bail_wgs = 1024;       // phase-2 persistent grid: 4 workgroups per CU
     uint64_t *d_clk = nullptr;      // RT_KERNEL_FLAG_WAVE_CLOCK records of the last such launch
     size_t clk_cap = 0;
@@ -1968,6 +2029,7 @@ void frame_params(const rt_scene *s, const rt_frame *f, KParams& P)
     P.bail_tests = 0;
     P.bail_count = nullptr;
     P.bail_queue = nullptr;
+    P.bail_state = nullptr;
     P.wave_clk = nullptr;
     P.xcd_chunk = 0;
 }
@@ -2073,6 +2135,15 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
         }
         const uint32_t tb = (f->kernel & RT_KERNEL_COMPACT_REFILL_MASK) >> RT_KERNEL_COMPACT_REFILL_SHIFT;
         P.bail_tests = tb ? 16u * tb : (wide_auto ? bail_auto_tests(P.nranks) : kBailTests);
+        const size_t nstate = size_t(n_local_tiles) * kTilePix * P.spp * 2u;   // 2 float4 per sample slot
+        if (nstate > s->bail_state_cap)
+        {
+            if (s->d_bail_state) RT_HIP(hipFree(s->d_bail_state));
+            s->d_bail_state = nullptr;
+            RT_HIP(hipMalloc(&s->d_bail_state, sizeof(float4) * nstate));
+            s->bail_state_cap = nstate;
+        }
+        P.bail_state = s->d_bail_state;
         P.bail_count = s->d_bail;
         P.bail_queue = s->d_bail + 1;
         RT_HIP(hipMemsetAsync(s->d_bail, 0, sizeof(uint32_t), st));
@@ -2513,6 +2584,7 @@ int rt_scene_destroy(rt_scene *s)
         (void)hipFree(s->d_distblk);
         (void)hipFree(s->d_clk);
         (void)hipFree(s->d_bail);
+        (void)hipFree(s->d_bail_state);
         (void)hipFree(s->d_smp);
         (void)hipFree(s->d_frame);
         if (s->h_smp_pinned) (void)hipHostFree(s->h_smp_pinned);
