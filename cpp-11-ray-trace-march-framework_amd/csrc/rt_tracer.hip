@@ -1075,7 +1075,7 @@ constexpr uint32_t kBailAutoRefs = 128;     // ... on scenes with a cell this de
 // sample, and a budget that shrinks as the shard does (tools/shard_scaling.py)
 __host__ __device__ constexpr uint32_t bail_auto_tests(uint32_t nranks)
 {
-    return nranks >= 8u ? 128u : (nranks >= 4u ? 192u : 384u);
+    return nranks >= 16u ? 64u : (nranks >= 8u ? 128u : (nranks >= 4u ? 192u : 384u));
 }
 // Center-out row order (kVarCenterOut): dispatch turn j takes row m, m - 1, m + 1, m - 2, ...
 // (m = R / 2), a bijection on [0, R).  A camera frames its subject, so the dense rows -- whose
