@@ -1967,7 +1967,8 @@ int validate_frame(const rt_frame *f)
         return fail(RT_E_INVALID, "unknown kernel");
     const uint32_t spp = std::max(1u, f->spp);
     if (spp > 4096) return fail(RT_E_INVALID, "spp must be <= 4096");
-    if (((f->kernel & RT_KERNEL_COMPACT_REFILL_MASK) >> RT_KERNEL_COMPACT_REFILL_SHIFT) > 64u)
+    if ((f->kernel & RT_KERNEL_KIND_MASK) == RT_KERNEL_COMPACT &&
+        ((f->kernel & RT_KERNEL_COMPACT_REFILL_MASK) >> RT_KERNEL_COMPACT_REFILL_SHIFT) > 64u)
         return fail(RT_E_INVALID, "compaction refill threshold must be <= 64 lanes");
     if (((f->kernel & RT_KERNEL_KIND_MASK) == RT_KERNEL_LANES || (f->kernel & RT_KERNEL_KIND_MASK) == RT_KERNEL_PERSISTENT ||
          (f->kernel & RT_KERNEL_KIND_MASK) == RT_KERNEL_COMPACT) &&
