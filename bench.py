@@ -176,19 +176,36 @@ def check_frames(work, world):
 def run_steps(work, world, rank, steps, warmup, dist=None):
     """W untimed warm-up steps, then K timed steps between barrier+sync on both sides; returns
     the max-over-ranks wall time.  A step renders every scene (this rank's tiles when N > 1);
-    each scene's shards are all-gathered (RCCL over xGMI) as soon as that scene is rendered, so
-    the gather of scene 1 overlaps the render of scene 8, and rank 0 un-permutes the frames."""
+    each scene's shards are gathered to rank 0 (one RCCL gather: every peer sends its slice on
+    its own xGMI link) as soon as that scene is rendered, so the gather of scene 1 overlaps the
+    render of scene 8, and rank 0 un-permutes the frames."""
     gathered = []
     if world > 1:
         import torch
-        gathered = [torch.empty(world * b.numel(), dtype=b.dtype, device=b.device) for b in work.bufs]
+        gathered = [torch.empty(world * b.numel(), dtype=b.dtype, device=b.device) if rank == 0 else None
+                    for b in work.bufs]
+
+    rooted = [True]    # one RCCL gather to rank 0; the all-gather if this torch build lacks it
+
+    def collect(i):
+        if rooted[0]:
+            try:
+                return work.rtm.gather_shards(work.bufs[i], world, dst=0, out=gathered[i], async_op=True)
+            except (RuntimeError, NotImplementedError) as e:    # raised on every rank alike
+                print(f"bench: rooted gather unavailable ({e}); using the all-gather", file=sys.stderr)
+                rooted[0] = False
+        if gathered[i] is None:
+            import torch
+            gathered[i] = torch.empty(world * work.bufs[i].numel(), dtype=work.bufs[i].dtype,
+                                      device=work.bufs[i].device)
+        return work.rtm.all_gather_shards(work.bufs[i], world, out=gathered[i], async_op=True)
 
     def step(record):
         pending = []
         for i in range(len(SCENES)):
             work.render(i, record)
             if world > 1:
-                pending.append(work.rtm.all_gather_shards(work.bufs[i], world, out=gathered[i], async_op=True))
+                pending.append(collect(i))
         for i, (g, h) in enumerate(pending):
             if h is not None:
                 h.wait()
@@ -300,7 +317,7 @@ def main():
                     "post-setup meshes dumped by the reference's own mesh code",
             "config": {"workload": f"scenes{list(SCENES)}_{W}x{H}x{SPP}", "scenes": list(SCENES),
                        "width": W, "height": H, "spp": SPP, "kernel": args.kernel,
-                       "parallelism": f"tile-shard x{world}" + (" + RCCL all-gather" if world > 1 else "")},
+                       "parallelism": f"tile-shard x{world}" + (" + RCCL gather to rank 0" if world > 1 else "")},
             "per_scene": {str(sid): {"kernel_ms": round(kernel_ms[sid], 4),
                                      "kernel_msamples_per_s": round(W * H * SPP / world / kernel_ms[sid] / 1e3, 1),
                                      "bytes_per_sample": round(ab[sid]["bytes_per_sample"], 1),

@@ -640,6 +640,30 @@ def frame_from_shards(gathered, width, height, nranks):
     return gathered[r * elems + k * 256 + (y % 16) * 16 + (x % 16)].astype(np.uint32)
 
 
+def gather_shards(shard, world, dst=0, group=None, out=None, async_op=False):
+    """Gather equal-sized shards to rank `dst` only ([rank][shard] layout in `out` there; other
+    ranks return out=None): on GPUs one RCCL gather, i.e. grouped ncclSend / ncclRecv, so every
+    peer sends its slice on its own xGMI link to the root instead of an
+    all-gather that moves N x the frame through every link.  gloo on CPU tensors uses its
+    gather.  For gloo on GPU tensors (the one-GPU rehearsal of bench.py) the all-gather path
+    is used.  async_op=True returns (out, work) as all_gather_shards does."""
+    import torch
+    import torch.distributed as dist
+    rank = dist.get_rank(group)
+    if dist.get_backend(group) == "gloo" and shard.is_cuda:
+        res = all_gather_shards(shard, world, group=group, out=out, async_op=async_op)
+        if rank != dst:
+            return (None, res[1]) if async_op else None
+        return res
+    if rank == dst and out is None:
+        out = torch.empty(world * shard.numel(), dtype=shard.dtype, device=shard.device)
+    parts = list(out.chunk(world)) if rank == dst else None
+    work = dist.gather(shard, gather_list=parts, dst=dst, group=group, async_op=async_op)
+    if rank != dst:
+        out = None
+    return (out, work) if async_op else out
+
+
 def all_gather_shards(shard, world, group=None, out=None, async_op=False):
     """All-gather equal-sized shards (RCCL over xGMI on GPUs, gloo on CPU tensors) into `out`
     ([rank][shard] layout, allocated when None).  async_op=True returns (out, work): the RCCL

@@ -1,5 +1,6 @@
 """Multi-rank sharding on CPU (gloo, world_size 2 and 3): every rank renders only the 16x16
-tiles it owns (t % N == rank), shards are all-gathered, rank 0 un-permutes, and the frame is
+tiles it owns (t % N == rank), shards are all-gathered and gathered to rank 0, rank 0
+un-permutes, and the frame is
 byte-identical to the single-process frame (partition invariance).
 The per-tile pixels come from the oracle here; on GPUs the same layout is produced by
 rt_render_shard_device and undone by rt_unshard_device (tests/test_gpu_parity.py)."""
@@ -31,9 +32,14 @@ def _worker(rank, world, port, q):
         full, _, _ = Oracle().render(SCENE, W, H, SPP, nthreads=2)
         shard = torch.from_numpy(rtm.shard_from_frame(full, rank, world).view(np.int32))
         gathered = rtm.all_gather_shards(shard, world)
+        rooted = rtm.gather_shards(shard, world, dst=0)
         if rank == 0:
             img = rtm.frame_from_shards(gathered.numpy().view(np.uint32), W, H, world)
-            q.put(("ok", bool(np.array_equal(img, full)), len(rtm.shard_tile_ids(W, H, 0, world))))
+            img2 = rtm.frame_from_shards(rooted.numpy().view(np.uint32), W, H, world)
+            q.put(("ok", bool(np.array_equal(img, full) and np.array_equal(img2, full)),
+                   len(rtm.shard_tile_ids(W, H, 0, world))))
+        else:
+            assert rooted is None
         dist.barrier()
     except Exception as e:  # pragma: no cover - reported to the parent
         q.put(("err", repr(e), 0))
