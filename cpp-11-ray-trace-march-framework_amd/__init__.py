@@ -28,7 +28,8 @@ MESH_DATA_DIR = os.path.join(REPO, "data", "meshes")     # cornell_box_quads.txt
 RT_TRI_MOLLER_TRUMBORE, RT_TRI_BARYCENTRIC = 0, 1
 RT_KERNEL_AUTO, RT_KERNEL_LANES, RT_KERNEL_PIXEL_LOOP, RT_KERNEL_COMPACT, RT_KERNEL_PERSISTENT = 0, 1, 2, 3, 4
 RT_KERNEL_WIDE = 5
-RT_KERNEL_KIND_MASK = 0x0F
+RT_KERNEL_KIND_MASK = 0x07
+RT_KERNEL_FLAG_EARLY_LOAD = 0x08
 RT_KERNEL_FLAG_CENTER_OUT = 0x10
 RT_KERNEL_FLAG_ALT_LOADS = 0x20
 RT_KERNEL_FLAG_WIDE16 = 0x40

@@ -78,6 +78,7 @@ constexpr int kVarBail = 131072;            // RT_KERNEL_FLAG_BAIL_WIDE phase 1:
 constexpr int kVarLdsCells = 262144;        // RT_KERNEL_FLAG_LDS_CELLS: long uniform lists staged through LDS
 constexpr int kVarAltLoads = 524288;        // RT_KERNEL_FLAG_ALT_LOADS: uniform loop on two record sets in turn
 constexpr int kVarCenterOut = 1048576;      // RT_KERNEL_FLAG_CENTER_OUT: XCD row turns from the middle row out
+constexpr int kVarEarlyLoad = 2097152;      // RT_KERNEL_FLAG_EARLY_LOAD: cell word issued before the step
 constexpr uint32_t kMarchSteps = 128;       // renderer.cpp:26
 constexpr uint32_t kDistBlock = 32;         // triangles per culling block of the distance kernels
 
@@ -637,24 +638,42 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, const uint32_t 
             if ((VAR & kVarSelStep) && iter >= P.max_steps) break;
             if (STATS) { voxel = uint32_t(cell); steps++; }
             uint32_t kb = 0, ke = 0;
-            if (skip == 0)
-            {
-                const uint32_t w = P.cellw[uint32_t(cell)];
-                const uint32_t cnt = w & 2047u;
-                kb = w >> 11;
-                ke = kb + cnt;
-                skip = cnt ? 0 : int(kb) - 1;
-            }
-            else
-                skip--;
             float nct_ax;
             bool more;
-            if (VAR & kVarSelStep)
-                RT_DDA_ADVANCE(nct_ax, more);
-            else if (VAR & kVarPackedRem)
+            if constexpr ((VAR & kVarEarlyLoad) != 0 && (VAR & kVarPackedRem) != 0 && (VAR & kVarSelStep) == 0)
+            {
+                // The cell word is loaded for every cell (also inside a proven-empty run, where
+                // it goes unused) and issued before the step, so the step's VALU work runs while
+                // the load is in flight instead of after its wait.
+                const uint32_t w = P.cellw[uint32_t(cell)];
                 RT_DDA_ADVANCE_PACKED(nct_ax, more);
+                // branch-free decode: the word is used on every path, so the load is not sunk
+                // back into a skip == 0 branch behind the step
+                const bool fresh = skip == 0;
+                const uint32_t cnt = fresh ? (w & 2047u) : 0u;
+                kb = fresh ? (w >> 11) : 0u;
+                ke = kb + cnt;
+                skip = fresh ? (cnt ? 0 : int(kb) - 1) : skip - 1;
+            }
             else
-                RT_DDA_ADVANCE_ADD(nct_ax, more);
+            {
+                if (skip == 0)
+                {
+                    const uint32_t w = P.cellw[uint32_t(cell)];
+                    const uint32_t cnt = w & 2047u;
+                    kb = w >> 11;
+                    ke = kb + cnt;
+                    skip = cnt ? 0 : int(kb) - 1;
+                }
+                else
+                    skip--;
+                if (VAR & kVarSelStep)
+                    RT_DDA_ADVANCE(nct_ax, more);
+                else if (VAR & kVarPackedRem)
+                    RT_DDA_ADVANCE_PACKED(nct_ax, more);
+                else
+                    RT_DDA_ADVANCE_ADD(nct_ax, more);
+            }
             if constexpr ((VAR & kVarBail) != 0)
             {
                 // two-phase arm: a sample whose walk would pass bail_tests tests stops here and
@@ -1957,7 +1976,7 @@ int validate_frame(const rt_frame *f)
         return fail(RT_E_INVALID, "IntersectBruteForce uses IntersectRayTri only (renderer.cpp:176)");
     if ((f->kernel & RT_KERNEL_KIND_MASK) > RT_KERNEL_WIDE ||
         (f->kernel & ~(RT_KERNEL_KIND_MASK | RT_KERNEL_FLAG_LDS_CELLS | RT_KERNEL_FLAG_WIDE16 |
-                       RT_KERNEL_FLAG_ALT_LOADS | RT_KERNEL_FLAG_CENTER_OUT | RT_KERNEL_FLAG_PREFETCH | RT_KERNEL_FLAG_WAVE_GATE | RT_KERNEL_FLAG_SKIP_RUN |
+                       RT_KERNEL_FLAG_ALT_LOADS | RT_KERNEL_FLAG_CENTER_OUT | RT_KERNEL_FLAG_EARLY_LOAD | RT_KERNEL_FLAG_PREFETCH | RT_KERNEL_FLAG_WAVE_GATE | RT_KERNEL_FLAG_SKIP_RUN |
                        RT_KERNEL_FLAG_CSR_OFFSETS | RT_KERNEL_FLAG_DIST_SKIP | RT_KERNEL_FLAG_NESTED_STEP |
                        RT_KERNEL_FLAG_PRE_GATE | RT_KERNEL_FLAG_EXHAUSTIVE | RT_KERNEL_FLAG_ORIGIN_PRE |
                        RT_KERNEL_FLAG_SELECT_STEP | RT_KERNEL_FLAG_FAST_RCP | RT_KERNEL_FLAG_PACKED_REM |
@@ -2090,7 +2109,8 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
                     ((fk & RT_KERNEL_FLAG_UNIFORM_CELLS) ? kVarUniform : 0) |
                     ((fk & RT_KERNEL_FLAG_LDS_CELLS) ? kVarLdsCells : 0) |
                     ((fk & RT_KERNEL_FLAG_ALT_LOADS) ? kVarAltLoads : 0) |
-                    ((fk & RT_KERNEL_FLAG_CENTER_OUT) ? kVarCenterOut : 0);
+                    ((fk & RT_KERNEL_FLAG_CENTER_OUT) ? kVarCenterOut : 0) |
+                    ((fk & RT_KERNEL_FLAG_EARLY_LOAD) ? kVarEarlyLoad : 0);
     // the wave-uniform empty run needs the packed counts (scenes with a grid dimension > 512
     // walk without it)
     if (!(var & kVarPackedRem)) var &= ~kVarSkipRun;
@@ -2234,6 +2254,8 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
         else if (var == 47626) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 47626>), grid, wg, 0, st, P);
         else if (var == 80394) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 80394>), grid, wg, 0, st, P);
         else if (var == 78350) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 78350>), grid, wg, 0, st, P);
+        else if (var == (80398 | kVarEarlyLoad))
+            hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 80398 | kVarEarlyLoad>), grid, wg, 0, st, P);
         else if (var == (80398 | kVarCenterOut))
             hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 80398 | kVarCenterOut>), grid, wg, 0, st, P);
         else if (var == (80398 | kVarCenterOut | kVarWaveClock))

@@ -94,7 +94,9 @@ enum rt_kernel {
     RT_KERNEL_PERSISTENT = 4,  /* LANES in persistent workgroups with the LDS cell-occupancy bitmap */
     RT_KERNEL_WIDE = 5,        /* AUTO's per-ray code with 4 lanes per sample splitting every cell's
                                   triangle list (spp <= 16; else = AUTO) */
-    RT_KERNEL_KIND_MASK = 0x0F,       /* the kernel kind above; the bits above it are flags */
+    RT_KERNEL_KIND_MASK = 0x07,       /* the kernel kind above; the bits above it are flags */
+    RT_KERNEL_FLAG_EARLY_LOAD = 0x08, /* OR-able (with PACKED_REM): every cell's word is loaded,
+                                         issued before the DDA step */
     RT_KERNEL_FLAG_CENTER_OUT = 0x10, /* OR-able (with XCD_BANDS): the XCDs' row turns start at the
                                          frame's middle row and move outward */
     RT_KERNEL_FLAG_ALT_LOADS = 0x20,  /* OR-able (with UNIFORM_CELLS): the scalar loop alternates

@@ -185,6 +185,7 @@ def test_auto_equals_plain_arms(golden, scenes):
                   full | rtm.RT_KERNEL_FLAG_UNIFORM_CELLS | rtm.RT_KERNEL_FLAG_UNROLL_PAIRS,
                   full | rtm.RT_KERNEL_FLAG_UNIFORM_CELLS | rtm.RT_KERNEL_FLAG_ALT_LOADS,
                   full | rtm.RT_KERNEL_FLAG_UNIFORM_CELLS | rtm.RT_KERNEL_FLAG_SKIP_RUN,
+                  full | rtm.RT_KERNEL_FLAG_UNIFORM_CELLS | rtm.RT_KERNEL_FLAG_SKIP_RUN | rtm.RT_KERNEL_FLAG_EARLY_LOAD,
                   full | rtm.RT_KERNEL_FLAG_UNIFORM_CELLS | rtm.RT_KERNEL_FLAG_SKIP_RUN | rtm.RT_KERNEL_FLAG_CENTER_OUT,
                   full | rtm.RT_KERNEL_FLAG_UNIFORM_CELLS | rtm.RT_KERNEL_FLAG_LDS_CELLS,
                   full | rtm.RT_KERNEL_FLAG_UNIFORM_CELLS | rtm.RT_KERNEL_FLAG_LDS_CELLS | rtm.RT_KERNEL_FLAG_UNROLL_PAIRS,
