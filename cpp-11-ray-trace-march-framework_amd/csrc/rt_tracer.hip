@@ -614,7 +614,7 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, const uint32_t 
                                                float dx, float dy, float dz,
                                                float& t, float& u, float& v, uint32_t& tri,
                                                uint32_t& voxel, uint32_t& steps, uint32_t& tests,
-                                               bool *bailed = nullptr, uint32_t bail_idx = 0u)
+                                               bool *bailed = nullptr, uint32_t bail_idx = 0u)   // work item
 {
     float nct0, nct1, nct2, dt0, dt1, dt2;
     int rem0, rem1, rem2, cs0, cs1, cs2, cell;
@@ -691,8 +691,9 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, const uint32_t 
                     {
                         // where the walk stopped: the untested cell [kb, ke) with its exit time
                         // and the state after its step -- phase 2 resumes exactly here
-                        P.bail_state[2 * size_t(bail_idx)] = make_float4(nct0, nct1, nct2, nct_ax);
-                        P.bail_state[2 * size_t(bail_idx) + 1] =
+                        const size_t bi = 2 * ((size_t(bail_idx) << 6) | (threadIdx.x & 63u));
+                        P.bail_state[bi] = make_float4(nct0, nct1, nct2, nct_ax);
+                        P.bail_state[bi + 1] =
                             make_float4(__int_as_float(remp), __int_as_float(cell), __uint_as_float(kb),
                                         __uint_as_float(ke));
                     }
@@ -1026,8 +1027,7 @@ __device__ __forceinline__ void process_item(const KParams& P, const uint32_t *l
     {
         const ItemCoord ic = item_coord(P, item, lane);
         if (ic.valid)
-            trace_sample<false, TRI, VAR>(P, lds_occ, ic.x, ic.y, ic.s, cr, cg, cb, nullptr, &bailed,
-                                          item * 64u + lane);
+            trace_sample<false, TRI, VAR>(P, lds_occ, ic.x, ic.y, ic.s, cr, cg, cb, nullptr, &bailed, item);
     }
     const ItemCoord ic = item_coord(P, item, lane);
     const uint32_t base = lane & ~(P.spp - 1u);
