@@ -55,3 +55,24 @@ def test_invalid_arguments_fail_loudly():
     assert buf.value
     with pytest.raises(rtm.RtError):
         rtm.shard_elems(0, 10, 1)
+
+
+def test_python_constants_match_header_enums():
+    """Every RT_* enum constant / #define in rt_tracer.h has the same value in the Python
+    mirror (the kernel flags are shared bit positions: a drifted one selects another arm)."""
+    src = open(os.path.join(ROOT, "include", "rt_tracer.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    vals = {}
+    for name, val in re.findall(r"\b(RT_[A-Z0-9_]+)\s*=\s*(0x[0-9A-Fa-f]+|\d+)u?\b", src):
+        vals[name] = int(val, 0)
+    for name, val in re.findall(r"#define\s+(RT_[A-Z0-9_]+)\s+(0x[0-9A-Fa-f]+|\d+)u?\b", src):
+        vals[name] = int(val, 0)
+    assert len(vals) > 30
+    mirrored = {n: v for n, v in vals.items() if hasattr(rtm, n)}
+    assert len(mirrored) >= 25, sorted(set(vals) - set(mirrored))
+    for n, v in mirrored.items():
+        assert getattr(rtm, n) == v, (n, getattr(rtm, n), v)
+    flags = [v for n, v in vals.items() if n.startswith("RT_KERNEL_FLAG_")]
+    assert len(flags) == len(set(flags)), "two kernel flags share a bit"
+    assert all(f & vals["RT_KERNEL_KIND_MASK"] == 0 for f in flags)
+    assert vals["RT_KERNEL_WIDE"] <= vals["RT_KERNEL_KIND_MASK"]
