@@ -131,6 +131,10 @@ _host = None
 
 
 def _load(name):
+    # RT_TRACER_LIB names another build of librt_tracer.so in the package directory (A/B of
+    # two builds in one process, tools/ab_libs.py); read when the library is first loaded
+    if name == "librt_tracer.so" and os.environ.get("RT_TRACER_LIB"):
+        name = os.path.basename(os.environ["RT_TRACER_LIB"])
     path = os.path.join(HERE, name)
     if not os.path.exists(path):
         raise RtError(f"{path} is not built; run __graft_entry__.build() or make -C {HERE}")

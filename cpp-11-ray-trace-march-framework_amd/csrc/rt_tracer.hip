@@ -387,15 +387,23 @@ __device__ __forceinline__ bool test_cell(const KParams& P, float ox, float oy, 
                     n1 = np[1];
                     n2 = np[2];
                 }
-                float ct, cu, cv;
-                const bool hit = rtd::ray_tri_mt_gated_pre<(VAR & kVarFastRcp) != 0>(
-                    dx, dy, dz, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w, ct, cu, cv);
                 if (STATS) tests++;
-                const bool take = hit & (ct < t) & (ct < nct_ax);
-                t = take ? ct : t;
-                u = take ? cu : u;
-                v = take ? cv : v;
-                tri = take ? k : tri;
+                // the gate skips the record's second half AND the acceptance for the whole wave
+                // when no lane passes det and u (the common case in a dense cell)
+                float inv, cu;
+                const bool ok1 = rtd::mt_pre_first<(VAR & kVarFastRcp) != 0>(
+                    dx, dy, dz, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x, inv, cu);
+                if (__any(ok1))
+                {
+                    float cv, ct;
+                    const bool hit =
+                        ok1 & rtd::mt_pre_second(dx, dy, dz, r0.w, r1.x, r1.y, r2.y, r2.z, r2.w, inv, cu, cv, ct);
+                    const bool take = hit & (ct < t) & (ct < nct_ax);
+                    t = take ? ct : t;
+                    u = take ? cu : u;
+                    v = take ? cv : v;
+                    tri = take ? k : tri;
+                }
             }
             return t != rtd::kFltMax;
         }
@@ -433,17 +441,30 @@ __device__ __forceinline__ bool test_cell(const KParams& P, float ox, float oy, 
             r1 = rp[1];
             r2 = rp[2];
         }
+        if constexpr ((VAR & kVarOriginPre) != 0 && TRI == RT_TRI_MOLLER_TRUMBORE)
+        {
+            // r0..r2 = the frame record; the triangle id is resolved from refs after the walk.
+            // The gate skips the second half and the acceptance when no lane passes det and u.
+            if (STATS) tests++;
+            float inv, pu;
+            const bool ok1 = rtd::mt_pre_first<(VAR & kVarFastRcp) != 0>(
+                dx, dy, dz, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x, inv, pu);
+            if (__any(ok1))
+            {
+                float pv, pt;
+                const bool h = ok1 & rtd::mt_pre_second(dx, dy, dz, r0.w, r1.x, r1.y, r2.y, r2.z, r2.w, inv, pu, pv, pt);
+                const bool take = h & (pt < t) & (pt < nct_ax);   // grid.cpp:258-266
+                t = take ? pt : t;
+                u = take ? pu : u;
+                v = take ? pv : v;
+                tri = take ? k : tri;
+            }
+            continue;
+        }
         float ct, cu, cv;
         bool hit;
         uint32_t id = __float_as_uint(r2.y);
-        if ((VAR & kVarOriginPre) && TRI == RT_TRI_MOLLER_TRUMBORE)
-        {
-            // r0..r2 = the frame record; the triangle id is resolved from refs after the walk
-            id = k;
-            hit = rtd::ray_tri_mt_gated_pre<(VAR & kVarFastRcp) != 0>(dx, dy, dz, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x,
-                                            r2.y, r2.z, r2.w, ct, cu, cv);
-        }
-        else if (TRI == RT_TRI_BARYCENTRIC)
+        if (TRI == RT_TRI_BARYCENTRIC)
         {
             const float4 fn = P.face_n[id];
             hit = rtd::ray_tri_bary_pred(ox, oy, oz, dx, dy, dz, r0.x, r0.y, r0.z, r0.w, r1.x,
@@ -1271,15 +1292,20 @@ __device__ __forceinline__ void wide_trace(const KParams& P, uint32_t k, uint32_
                                 n1 = rp[1];
                                 n2 = rp[2];
                             }
-                            float ct, cu, cv;
-                            const bool h = rtd::ray_tri_mt_gated_pre<(VAR & kVarFastRcp) != 0>(
-                                dx, dy, dz, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w,
-                                ct, cu, cv);
-                            const bool take = h & (ct < bt) & (ct < nct_ax);
-                            bt = take ? ct : bt;
-                            bu = take ? cu : bu;
-                            bv = take ? cv : bv;
-                            bk = take ? k : bk;
+                            float inv, cu;
+                            const bool ok1 = rtd::mt_pre_first<(VAR & kVarFastRcp) != 0>(
+                                dx, dy, dz, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x, inv, cu);
+                            if (__any(ok1))
+                            {
+                                float cv, ct;
+                                const bool h = ok1 & rtd::mt_pre_second(dx, dy, dz, r0.w, r1.x, r1.y, r2.y, r2.z,
+                                                                        r2.w, inv, cu, cv, ct);
+                                const bool take = h & (ct < bt) & (ct < nct_ax);
+                                bt = take ? ct : bt;
+                                bu = take ? cu : bu;
+                                bv = take ? cv : bv;
+                                bk = take ? k : bk;
+                            }
                         }
                         for (int m = 1; m < G; m <<= 1)
                         {
