@@ -23,6 +23,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -1117,6 +1118,17 @@ __host__ __device__ constexpr uint32_t bail_auto_tests(uint32_t nranks)
 {
     return nranks >= 16u ? 64u : (nranks >= 8u ? 128u : (nranks >= 4u ? 192u : 384u));
 }
+constexpr uint32_t kRowTuneFrames = 4;      // AUTO row-order tuning: frames timed (two per order)
+constexpr float kRowTuneMargin = 0.97f;     // centre-out kept only when >= 3 % faster
+// RT_ROW_TUNE=0 pins AUTO to the plain row order (A/B runs, tools/ab_libs.py)
+static bool row_tune_enabled()
+{
+    static const bool on = [] {
+        const char *e = std::getenv("RT_ROW_TUNE");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
 // Center-out row order (kVarCenterOut): dispatch turn j takes row m, m - 1, m + 1, m - 2, ...
 // (m = R / 2), a bijection on [0, R).  A camera frames its subject, so the dense rows -- whose
 // waves are the launch's longest -- start first instead of mid-launch.
@@ -1948,6 +1960,13 @@ struct rt_scene
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool ev_recorded = false;
     hipStream_t last_stream = nullptr;  // stream of the last launch (cross-stream ordering)
+    // AUTO's row order at one rank, chosen per scene and launch shape from its own first frames
+    // (calls 0..3 alternate plain / centre-out; both orders give identical pixels)
+    uint64_t row_key = 0;        // (blocks, spp) the choice was made for
+    uint32_t row_calls = 0;      // tuning frames launched for row_key
+    int row_pending = -1;        // order of the frame ev0/ev1 bracket, not yet read
+    int row_choice = -1;         // 0 plain, 1 centre-out, -1 still tuning
+    float row_best[2] = {0.f, 0.f};
     // staging for rt_render_tiles / records
     uint32_t *d_frame = nullptr;
     size_t frame_cap = 0;
@@ -2099,6 +2118,18 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
     // one waits for it, so frames of one scene never overlap on the device.
     if (s->ev_recorded && st != s->last_stream) RT_HIP(hipStreamWaitEvent(st, s->ev1, 0));
     s->last_stream = st;
+    if (s->row_pending >= 0)
+    {
+        // a tuning frame's time (host waits only during the first few frames of a launch shape)
+        float ms = 0.f;
+        RT_HIP(hipEventSynchronize(s->ev1));
+        RT_HIP(hipEventElapsedTime(&ms, s->ev0, s->ev1));
+        float &best = s->row_best[s->row_pending];
+        if (best == 0.f || ms < best) best = ms;
+        s->row_pending = -1;
+        if (s->row_calls >= kRowTuneFrames)
+            s->row_choice = s->row_best[1] < kRowTuneMargin * s->row_best[0] ? 1 : 0;
+    }
     RT_HIP(hipEventRecord(s->ev0, st));
     const uint32_t kind = f->kernel & RT_KERNEL_KIND_MASK;
     // kVarXcdBands turn size: one row of this launch's tiles (ceil(tiles_x / nranks) local tiles
@@ -2140,6 +2171,30 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
     // the wave-uniform empty run needs the packed counts (scenes with a grid dimension > 512
     // walk without it)
     if (!(var & kVarPackedRem)) var &= ~kVarSkipRun;
+    // AUTO at one rank: centre-out row turns cut killeroo's tail ~6 % but cost Cornell +6 % and
+    // scene 5 +76 %, so each scene times both orders on its first frames of a
+    // launch shape and keeps the faster.  Results are bit-identical either way.
+    if (kind == RT_KERNEL_AUTO && P.nranks == 1u && var == 80398 && !(f->kernel & RT_KERNEL_FLAG_BAIL_WIDE) &&
+        row_tune_enabled())
+    {
+        const uint64_t key = (uint64_t(blocks) << 8) | P.spp;
+        if (key != s->row_key)
+        {
+            s->row_key = key;
+            s->row_calls = 0;
+            s->row_choice = -1;
+            s->row_pending = -1;
+            s->row_best[0] = s->row_best[1] = 0.f;
+        }
+        int order = s->row_choice;
+        if (order < 0)
+        {
+            order = int(s->row_calls & 1u);
+            s->row_pending = order;
+            ++s->row_calls;
+        }
+        if (order == 1) var |= kVarCenterOut;
+    }
     // the wide arms run AUTO's per-ray code without the empty run (phase 1 keeps it)
     const int wvar = var & ~kVarSkipRun;
     if (var & kVarWaveClock)

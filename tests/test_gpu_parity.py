@@ -197,6 +197,19 @@ def test_auto_equals_plain_arms(golden, scenes):
             assert hashlib.sha256(img.tobytes()).hexdigest() == want, (sid, hex(k))
 
 
+def test_auto_row_order_tuning_frames(golden, scenes):
+    """AUTO at one rank times plain and centre-out row order on a launch shape's first four
+    frames (alternating), then keeps the faster: every frame of that sequence, and the ones
+    after the choice, are the reference's bytes."""
+    for sid in (1, 8):
+        hs, gs = scenes(sid)
+        want = golden["frames_1080p4"][str(sid)]["bgra_sha256"]
+        fr = gs.frame(1920, 1080, 4, kernel=rtm.RT_KERNEL_AUTO)
+        for i in range(7):
+            img = gs.render_frame(fr)
+            assert hashlib.sha256(img.tobytes()).hexdigest() == want, (sid, i)
+
+
 @pytest.mark.parametrize("spp", [1, 2, 4, 16, 32])
 def test_wide_and_two_phase_vs_oracle(scenes, oracle, spp):
     """Wide kernel and two-phase arm on ragged frames at every spp they take (32 falls back to
