@@ -3,7 +3,7 @@
 The product is two in-tree shared libraries built by this package's Makefile:
 
 * ``librt_tracer.so`` -- hand-written HIP kernels behind the C ABI of ``include/rt_tracer.h``
-  (the drop-in for ``Renderer::RenderTile``, renderer.cpp:81-174);
+  (the drop-in for ``Renderer::RenderTile``, renderer.cpp:43-136);
 * ``librt_host.so`` -- the C++11 host: scene load, ``Grid::Grid`` build emitted as CSR
   (grid.cpp:12-154) and the 12x9 ``Framebuffer`` tile pool with the GPU ``RenderTile``
   (framebuffer.cpp), ABI in ``include/rt_host.h``.
@@ -26,32 +26,19 @@ SCENE_DIR = os.path.join(REPO, "data", "scenes")
 MESH_DATA_DIR = os.path.join(REPO, "data", "meshes")     # cornell_box_quads.txt (scene table)
 
 RT_TRI_MOLLER_TRUMBORE, RT_TRI_BARYCENTRIC = 0, 1
-RT_KERNEL_AUTO, RT_KERNEL_LANES, RT_KERNEL_PIXEL_LOOP, RT_KERNEL_COMPACT, RT_KERNEL_PERSISTENT = 0, 1, 2, 3, 4
+RT_KERNEL_AUTO, RT_KERNEL_LANES, RT_KERNEL_PIXEL_LOOP, RT_KERNEL_COMPACT = 0, 1, 2, 3
 RT_KERNEL_WIDE = 5
 RT_KERNEL_KIND_MASK = 0x07
-RT_KERNEL_FLAG_EARLY_LOAD = 0x08
 RT_KERNEL_FLAG_CENTER_OUT = 0x10
-RT_KERNEL_FLAG_ALT_LOADS = 0x20
+RT_KERNEL_FLAG_STATIC_ORDER = 0x20
 RT_KERNEL_FLAG_WIDE16 = 0x40
 RT_KERNEL_FLAG_LDS_CELLS = 0x80
-RT_KERNEL_FLAG_PREFETCH = 0x100
-RT_KERNEL_FLAG_WAVE_GATE = 0x200
-RT_KERNEL_FLAG_SKIP_RUN = 0x400
-RT_KERNEL_FLAG_CSR_OFFSETS = 0x800
-RT_KERNEL_FLAG_DIST_SKIP = 0x1000
-RT_KERNEL_FLAG_NESTED_STEP = 0x2000
-RT_KERNEL_FLAG_PRE_GATE = 0x4000
 RT_KERNEL_FLAG_EXHAUSTIVE = 0x8000
-RT_KERNEL_FLAG_ORIGIN_PRE = 0x10000
-RT_KERNEL_FLAG_SELECT_STEP = 0x20000
-RT_KERNEL_FLAG_FAST_RCP = 0x40000
-RT_KERNEL_FLAG_PACKED_REM = 0x80000
-RT_KERNEL_FLAG_XCD_BANDS = 0x100000
-RT_KERNEL_FLAG_UNROLL_PAIRS = 0x200000
 RT_KERNEL_FLAG_WAVE_CLOCK = 0x400000
-RT_KERNEL_FLAG_UNIFORM_CELLS = 0x800000
 RT_KERNEL_FLAG_BAIL_WIDE = 0x80000000
-RT_KERNEL_COMPACT_REFILL_SHIFT = 24      # RT_KERNEL_COMPACT: idle lanes before a refill (1..64)
+RT_KERNEL_BUDGET_SHIFT = 24              # COMPACT: idle lanes before a refill (1..64); BAIL_WIDE: budget / 16
+RT_KERNEL_BUDGET_MASK = 0x7F000000
+RT_KERNEL_COMPACT_REFILL_SHIFT = RT_KERNEL_BUDGET_SHIFT
 RT_ISECT_GRID = 0
 RT_ISECT_BRUTE_FORCE = 1
 RT_ISECT_RAY_MARCH = 2
@@ -62,7 +49,7 @@ TRACER_SYMBOLS = [
     "rt_get_device_count", "rt_scene_create", "rt_scene_destroy", "rt_scene_device_bytes",
     "rt_render_tiles", "rt_render_frame_device", "rt_shard_elems", "rt_render_shard_device",
     "rt_unshard_device", "rt_last_kernel_ms", "rt_trace_samples", "rt_debug_primitives",
-    "rt_debug_rcp_check", "rt_debug_wave_clocks",
+    "rt_debug_rcp_check", "rt_debug_wave_clocks", "rt_debug_heavy_first",
     "rt_sample_table", "rt_last_error", "rt_abi_version", "rt_grid_build", "rt_grid_free",
     "rt_scene_create_from_mesh",
 ]
@@ -161,6 +148,9 @@ def tracer_lib():
         L.rt_debug_primitives.argtypes = [ctypes.c_int, vp, c_u32, vp, ctypes.c_int]
         L.rt_debug_rcp_check.argtypes = [vp, ctypes.c_int]
         L.rt_debug_wave_clocks.argtypes = [vp, vp, c_u32, ctypes.POINTER(c_u32)]
+        if hasattr(L, "rt_debug_heavy_first"):       # absent in builds before ABI 3 (A/B runs)
+            L.rt_debug_heavy_first.argtypes = [vp, ctypes.POINTER(c_u32), ctypes.POINTER(c_u32),
+                                               ctypes.POINTER(c_u32)]
         L.rt_sample_table.argtypes = [c_u32, vp]
         L.rt_last_error.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
         L.rt_get_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
@@ -480,6 +470,15 @@ class GpuScene:
         out = np.zeros((n.value, 4), np.uint64)
         _check(L.rt_debug_wave_clocks(self._h, _ptr(out), n.value, ctypes.byref(n)), L, "rt_debug_wave_clocks")
         return out
+
+    def heavy_first(self):
+        """AUTO's heavy-first order of the most recent launch shape: (front blocks, blocks listed
+        by the last frame for the next one, frames rendered with that shape)."""
+        L = tracer_lib()
+        f, n, e = c_u32(), c_u32(), c_u32()
+        _check(L.rt_debug_heavy_first(self._h, ctypes.byref(f), ctypes.byref(n), ctypes.byref(e)), L,
+               "rt_debug_heavy_first")
+        return f.value, n.value, e.value
 
     def last_kernel_ms(self):
         ms = c_f32()

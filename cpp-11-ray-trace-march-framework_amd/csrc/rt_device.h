@@ -157,40 +157,15 @@ __device__ __forceinline__ bool ray_tri_mt_gated(float ox, float oy, float oz, f
     return ok1 & !(v < 0.0f || u + v > 1.0f) & (t >= 0.0f);
 }
 
-// ray_tri_mt_gated for rays that share one origin (every primary ray of a frame starts at the
-// camera, camera.h:39): tvec = o - v0 and qvec = tvec x e1 (triangle.h:71, 87) do not depend
-// on the direction, so they come precomputed per frame (k_origin_pre, same operations).  Only
-// the direction-dependent operations remain; results identical to ray_tri_mt_gated.
-// FAST_RCP: inv_det by rcp_nr, exact wherever the result is used: |det| < 1e-8 is rejected
-// below, and the launch selects FAST_RCP only for scenes whose |e1|_1 |e2|_1 bounds |det| far
-// below 2^126 (rt_scene::rcp_safe).
-template <bool FAST_RCP>
-__device__ __forceinline__ bool ray_tri_mt_gated_pre(float dx, float dy, float dz,
-                                                     float e1x, float e1y, float e1z,
-                                                     float e2x, float e2y, float e2z,
-                                                     float tx, float ty, float tz,
-                                                     float qx, float qy, float qz,
-                                                     float& t, float& u, float& v)
-{
-    const float px = dy * e2z - dz * e2y;
-    const float py = dz * e2x - dx * e2z;
-    const float pz = dx * e2y - dy * e2x;
-    const float det = e1x * px + e1y * py + e1z * pz;
-    float inv_det;
-    if (FAST_RCP)
-        inv_det = rcp_nr(det);
-    else
-        inv_det = 1.0f / det;
-    u = (tx * px + ty * py + tz * pz) * inv_det;
-    const bool ok1 = !(det > -0.00000001f && det < 0.00000001f) & !(u < 0.0f || u > 1.0f);
-    if (!__any(ok1)) return false;
-    v = (dx * qx + dy * qy + dz * qz) * inv_det;
-    t = (e2x * qx + e2y * qy + e2z * qz) * inv_det;
-    return ok1 & !(v < 0.0f || u + v > 1.0f) & (t >= 0.0f);
-}
+// Per-camera record of one CSR reference for rays that share one origin (every primary ray of
+// a frame starts at the camera, camera.h:43).  tvec = o - v0 and qvec = tvec x e1
+// (triangle.h:82, 90) do not depend on the direction, so k_origin_pre computes them once per
+// camera origin with the same operations; only the direction-dependent half of
+// triangle.h:15-107 remains per ray.  Record: {e1.xyz, e2.x} {e2.yz, tvec.xy} {tvec.z, qvec.xyz}.
 
-// ray_tri_mt_gated_pre split at its gate, for a caller that interleaves two independent tests
-// (instruction-level parallelism in latency-bound waves).  Same operations, same results.
+// First half of the test (triangle.h:45-87): det and u.  FAST_RCP: inv_det by rcp_nr, exact
+// wherever the result is used: |det| < 1e-8 is rejected, and the launch selects FAST_RCP only
+// for scenes whose |e1|_1 |e2|_1 bounds |det| far below 2^126 (rt_scene::rcp_safe).
 template <bool FAST_RCP>
 __device__ __forceinline__ bool mt_pre_first(float dx, float dy, float dz, float e1x, float e1y, float e1z,
                                              float e2x, float e2y, float e2z, float tx, float ty, float tz,
@@ -205,8 +180,11 @@ __device__ __forceinline__ bool mt_pre_first(float dx, float dy, float dz, float
     return !(det > -0.00000001f && det < 0.00000001f) & !(u < 0.0f || u > 1.0f);
 }
 
-__device__ __forceinline__ bool mt_pre_second(float dx, float dy, float dz, float e2x, float e2y, float e2z,
-                                              float qx, float qy, float qz, float inv_det, float u, float& v,
+// Second half (triangle.h:90-101): v and t = DOT(edge2, qvec) * inv_det.  (Measured: computing
+// e2 . qvec here beats a per-camera tdot array by ~5 %: one more load per record costs more than
+// these 5 VALU.)
+__device__ __forceinline__ bool mt_pre_second(float dx, float dy, float dz, float qx, float qy, float qz,
+                                              float e2x, float e2y, float e2z, float inv_det, float u, float& v,
                                               float& t)
 {
     v = (dx * qx + dy * qy + dz * qz) * inv_det;
@@ -214,42 +192,33 @@ __device__ __forceinline__ bool mt_pre_second(float dx, float dy, float dz, floa
     return !(v < 0.0f || u + v > 1.0f) & (t >= 0.0f);
 }
 
-// ray_tri_mt_gated preceded by a division-free wave-uniform pre-gate.  With q = udot/det the
-// reference's u = RN(udot * RN(1/det)); a lane is PROVABLY rejected by triangle.h:77-87 when
-//   det fails the epsilon test, or
-//   sign(udot) != sign(det), |udot| >= 2^-100 and |det| <= 2^40: u is a nonzero negative
-//     (|u| >= 2^-100 * 2^-40 * (1 - 2^-24) >> 2^-149, so it cannot round to -0), or
-//   same signs and |udot| > RN(|det| * 1.000001f): q > 1.00000094, u >= q (1 - 2^-24)^2 > 1 + 2^-23.
-// If no active lane survives, the whole test (incl. the correctly rounded division) is skipped;
-// otherwise the lanes run ray_tri_mt_gated unchanged, so results are bit-identical.
-__device__ __forceinline__ bool ray_tri_mt_pregated(float ox, float oy, float oz, float dx, float dy, float dz,
-                                                    float v0x, float v0y, float v0z,
-                                                    float e1x, float e1y, float e1z,
-                                                    float e2x, float e2y, float e2z,
-                                                    float& t, float& u, float& v)
+// The whole per-camera-record test, wave-gated (the q/v/t half only when some lane passed det
+// and u); results identical to ray_tri_mt_gated.
+template <bool FAST_RCP>
+__device__ __forceinline__ bool ray_tri_mt_gated_pre(float dx, float dy, float dz,
+                                                     float e1x, float e1y, float e1z,
+                                                     float e2x, float e2y, float e2z,
+                                                     float tx, float ty, float tz,
+                                                     float qx, float qy, float qz,
+                                                     float& t, float& u, float& v)
 {
-    const float px = dy * e2z - dz * e2y;
-    const float py = dz * e2x - dx * e2z;
-    const float pz = dx * e2y - dy * e2x;
-    const float det = e1x * px + e1y * py + e1z * pz;
-    const float tx = ox - v0x, ty = oy - v0y, tz = oz - v0z;
-    const float udot = tx * px + ty * py + tz * pz;
-    const bool det_ok = !(det > -0.00000001f && det < 0.00000001f);
-    const float ad = __builtin_fabsf(det), au = __builtin_fabsf(udot);
-    const bool opposite = (udot < 0.0f) != (det < 0.0f);
-    const bool surely_neg = opposite & (au >= 7.888609052210118e-31f) & (ad <= 1.099511627776e12f);
-    const bool surely_big = !opposite & (au > ad * 1.000001f);
-    if (!__any(det_ok & !surely_neg & !surely_big)) return false;
-    const float inv_det = 1.0f / det;
-    u = udot * inv_det;
-    const bool ok1 = det_ok & !(u < 0.0f || u > 1.0f);
+    float inv_det;
+    const bool ok1 = mt_pre_first<FAST_RCP>(dx, dy, dz, e1x, e1y, e1z, e2x, e2y, e2z, tx, ty, tz, inv_det, u);
     if (!__any(ok1)) return false;
-    const float qx = ty * e1z - tz * e1y;
-    const float qy = tz * e1x - tx * e1z;
-    const float qz = tx * e1y - ty * e1x;
-    v = (dx * qx + dy * qy + dz * qz) * inv_det;
-    t = (e2x * qx + e2y * qy + e2z * qz) * inv_det;
-    return ok1 & !(v < 0.0f || u + v > 1.0f) & (t >= 0.0f);
+    return ok1 & mt_pre_second(dx, dy, dz, qx, qy, qz, e2x, e2y, e2z, inv_det, u, v, t);
+}
+
+// k_origin_pre's arithmetic for one reference (v0, e1 as in the scene's reference record).
+__device__ __forceinline__ void origin_terms(float ox, float oy, float oz, float v0x, float v0y, float v0z,
+                                             float e1x, float e1y, float e1z, float& tx, float& ty, float& tz,
+                                             float& qx, float& qy, float& qz)
+{
+    tx = ox - v0x;                                   // triangle.h:82
+    ty = oy - v0y;
+    tz = oz - v0z;
+    qx = ty * e1z - tz * e1y;                        // triangle.h:90 CROSS(qvec, tvec, edge1)
+    qy = tz * e1x - tx * e1z;
+    qz = tx * e1y - ty * e1x;
 }
 
 // triangle.h:200-226 IntersectRayPlane + ComputeBarycentric (:133-156). Uses v0, the same

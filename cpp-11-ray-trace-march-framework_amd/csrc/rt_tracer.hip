@@ -4,19 +4,21 @@
 // 256/spp pixels of a 16x16 pixel tile in Morton order, one lane per sample, so a pixel's
 // samples sit in adjacent lanes and a wave covers a compact 2^k x 2^k pixel block (coherent
 // DDA walks).  Each lane runs the reference's per-sample path (GenerateRay -> Grid::Intersect
-// -> IntersectRayTri -> shading); the pixel's samples are then summed IN SAMPLE ORDER across
-// lanes (renderer.cpp:125-160, hazard H10), averaged, gamma'd and packed (renderer.cpp:162-171).
+// -> IntersectRayTri -> shading, renderer.cpp:88-122); the pixel's samples are then summed IN
+// SAMPLE ORDER across lanes (renderer.cpp:87-122, hazard H10), averaged, gamma'd and packed
+// (renderer.cpp:124-133).
 //
 // Scene layout in HBM (built once by rt_scene_create):
-//   cell_off  u32[C+1]            CSR offsets in GridIdx order (grid.h:41-42)
+//   cellw     u32[C]              packed cell word in GridIdx order (grid.h:41-42): non-empty
+//                                 start << 11 | count, empty: L-inf distance to geometry << 11
+//   cell_off  u32[C+1]            CSR offsets (scenes whose lists do not fit the packed word)
 //   refs      float4[3*R]         one 48-B record per CSR reference, in CSR order:
 //                                 {v0.xyz, e1.x} {e1.yz, e2.xy} {e2.z, tri_idx bits, 0, 0}
-//                                 -> a cell's triangle list streams contiguously, no
-//                                 index indirection, 3 dwordx4 loads per test
+//   frefs     float4[3*R]         per camera origin (k_origin_pre), one 48-B record per CSR
+//                                 reference: {e1.xyz, e2.x} {e2.yz, tvec.xy} {tvec.z, qvec}:
+//                                 the origin-only terms of triangle.h:82-90
 //   shade     float4[3*T]         per triangle the 3 vertex normals (shading of a hit)
 //   face_n    float4[T]           face normal (IntersectRayTriBarycentric only)
-//   occ       u32[ceil(C/32)]     1 bit per non-empty cell; staged into LDS per workgroup so
-//                                 the DDA skips empty cells without touching HBM/L2
 
 #include <hip/hip_runtime.h>
 
@@ -54,41 +56,44 @@ int fail(int code, const std::string& msg)
 constexpr uint32_t kTile = 16;              // shard / scheduling tile edge (pixels)
 constexpr uint32_t kTilePix = kTile * kTile;
 constexpr uint32_t kWG = 256;               // lanes per workgroup
+constexpr uint32_t kWavesPerWG = kWG / 64u;
 constexpr uint32_t kLdsStage = 64;          // kVarLdsCells: records per LDS chunk (3 KiB per wave)
 constexpr uint32_t kLdsMinRefs = 16;        // kVarLdsCells: shortest list staged through LDS
-constexpr uint32_t kAltMinRefs = 8;         // kVarAltLoads: shortest list run on alternating sets
-constexpr uint32_t kMaxOccWords = 8192;     // LDS occupancy bitmap: up to 262,144 cells (64^3)
-constexpr int kVarPrefetch = 1;             // RT_KERNEL_FLAG_PREFETCH
-constexpr int kVarWaveGate = 2;             // RT_KERNEL_FLAG_WAVE_GATE
-constexpr int kVarSkipRun = 4;             // RT_KERNEL_FLAG_SKIP_RUN: wave-uniform empty runs in a tight loop
-constexpr int kVarDistSkip = 8;             // RT_KERNEL_FLAG_DIST_SKIP
-constexpr int kVarNestedStep = 16;          // RT_KERNEL_FLAG_NESTED_STEP (A/B arm)
-constexpr int kVarPreGate = 32;             // RT_KERNEL_FLAG_PRE_GATE
+// Traversal features, combined into the VAR template argument of the render kernels.
+constexpr int kVarWaveGate = 2;             // skip a test's second half when no lane needs it
+constexpr int kVarSkipRun = 4;              // wave-uniform proven-empty runs in a tight loop
+constexpr int kVarDistSkip = 8;             // L-inf distance field in the empty cells' words
 constexpr int kVarBrute = 64;               // RT_ISECT_BRUTE_FORCE (renderer.cpp:157-197)
 constexpr int kVarMarch = 128;              // RT_ISECT_RAY_MARCH (renderer.cpp:24-41, 138-155)
 constexpr int kVarExhaustive = 256;         // RT_KERNEL_FLAG_EXHAUSTIVE: march without block culling
-constexpr int kVarOriginPre = 512;          // RT_KERNEL_FLAG_ORIGIN_PRE: per-frame o - v0, (o - v0) x e1
-constexpr int kVarSelStep = 1024;           // RT_KERNEL_FLAG_SELECT_STEP: select-form DDA step + bound (A/B)
-constexpr int kVarFastRcp = 2048;           // RT_KERNEL_FLAG_FAST_RCP: Newton-refined exact 1/det
-constexpr int kVarPackedRem = 4096;         // RT_KERNEL_FLAG_PACKED_REM: one packed remaining-cells word
-constexpr int kVarXcdBands = 8192;          // RT_KERNEL_FLAG_XCD_BANDS: XCD-aware block -> tile order
-constexpr int kVarUnroll = 16384;           // RT_KERNEL_FLAG_UNROLL_PAIRS: uniform lists tested two records at a time
+constexpr int kVarOriginPre = 512;          // per-camera-origin records (frefs, k_origin_pre)
+constexpr int kVarFastRcp = 2048;           // Newton-refined exact 1/det (rt_scene::rcp_safe)
+constexpr int kVarPackedRem = 4096;         // one packed remaining-cells word (rt_scene::pack_ok)
+constexpr int kVarXcdBands = 8192;          // XCD-aware block -> tile order
 constexpr int kVarWaveClock = 32768;        // RT_KERNEL_FLAG_WAVE_CLOCK: per-item s_memtime (debug)
-constexpr int kVarUniform = 65536;          // RT_KERNEL_FLAG_UNIFORM_CELLS: scalar loop for wave-uniform lists
+constexpr int kVarUniform = 65536;          // scalar loop for wave-uniform cell lists
 constexpr int kVarBail = 131072;            // RT_KERNEL_FLAG_BAIL_WIDE phase 1: test budget + pixel queue
-constexpr int kVarLdsCells = 262144;        // RT_KERNEL_FLAG_LDS_CELLS: long uniform lists staged through LDS
-constexpr int kVarAltLoads = 524288;        // RT_KERNEL_FLAG_ALT_LOADS: uniform loop on two record sets in turn
-constexpr int kVarCenterOut = 1048576;      // RT_KERNEL_FLAG_CENTER_OUT: XCD row turns from the middle row out
-constexpr int kVarEarlyLoad = 2097152;      // RT_KERNEL_FLAG_EARLY_LOAD: cell word issued before the step
+constexpr int kVarLdsCells = 262144;        // RT_KERNEL_FLAG_LDS_CELLS: long uniform lists staged in LDS
+constexpr int kVarCenterOut = 1048576;      // RT_KERNEL_FLAG_CENTER_OUT: XCD row turns from the middle out
+// AUTO's traversal: every feature above that is exact for every scene ...
+constexpr int kVarAutoCore = kVarWaveGate | kVarDistSkip | kVarOriginPre | kVarXcdBands | kVarUniform;
+// ... plus the two that need a scene property (rt_scene::rcp_safe, rt_scene::pack_ok)
+constexpr int kVarAuto = kVarAutoCore | kVarFastRcp | kVarPackedRem | kVarSkipRun;
+// the wide phase / wide kernel: AUTO's per-ray code, per-lane lists, no empty-run loop
+constexpr int kVarWide = kVarWaveGate | kVarDistSkip | kVarOriginPre | kVarFastRcp | kVarPackedRem | kVarXcdBands;
 constexpr uint32_t kMarchSteps = 128;       // renderer.cpp:26
 constexpr uint32_t kDistBlock = 32;         // triangles per culling block of the distance kernels
+
+// heavy-first plan (one per list version): blocks listed at each of the two priority levels,
+// the maximum block cost and the sum of wave costs of the measured frame
+struct HfPlan { uint32_t cnt_hi, cnt_lo, maxc, pad; unsigned long long sum; };
 
 struct KParams
 {
     // camera (per frame)
     float m[9];                 // Matrix44f m_mat[r][c], r,c < 3, row-major
     float fov_xs, aspect;
-    float org[3];               // Transf4x4(Vec3f(0)) computed on the host (camera.h:39)
+    float org[3];               // Transf4x4(Vec3f(0)) computed on the host (camera.h:43)
     uint32_t W, H, spp, spp_shift;
     float inv_spp;              // 2^-spp_shift when spp is a power of two (x/spp == x*inv_spp), else 0
     const float2 *smp;          // [spp] sample offsets
@@ -97,15 +102,13 @@ struct KParams
     float cw, icw;
     int dim[3];
     int dxdz;
-    uint32_t max_steps;         // safety bound: no DDA walk is longer than dx+dy+dz
-    uint32_t occ_words;         // 0 disables the LDS occupancy bitmap
+    uint32_t max_steps;         // bound of the CSR-offset walk: no DDA walk is longer than dx+dy+dz
     const uint32_t *off;
-    const uint32_t *cellw;      // packed cell ranges (start << 11 | count) or null
+    const uint32_t *cellw;      // packed cell words (start << 11 | count) or null
     const float4 *refs;
-    const float4 *frefs;        // per frame (kVarOriginPre): {e1, e2.x}{e2.yz, tvec.xy}{tvec.z, qvec}
+    const float4 *frefs;        // per camera origin (kVarOriginPre), 3 float4 per reference
     const float4 *shade;
     const float4 *face_n;
-    const uint32_t *occ;
     const float4 *tri_mt;       // per triangle {v0, e1, e2} in triangle order (brute force)
     const float4 *tri_dist;     // per triangle distance record (rtd::dist_point_tri), Morton order
     const float4 *dist_blk;     // per kDistBlock records: {aabb min, -}{aabb max, -}
@@ -123,6 +126,22 @@ struct KParams
     uint32_t xcd_chunk;         // kVarXcdBands: consecutive blocks per XCD turn (0 = one band each)
     uint64_t *wave_clk;         // kVarWaveClock: {start, end, uniform tests, lane-loop iterations} per item
     const uint32_t *tile_order; // tile order (position -> local tile) or null = natural order
+    // heavy-first block order (AUTO; hf_front == 0: off).  Blocks [0, hf_front) render the blocks
+    // the current plan (version hf_ver) lists as heavy, most expensive level first; blocks from
+    // hf_front on walk the natural order and skip those.  In a measured frame (every
+    // kHfPeriod-th of a launch shape) every wave stores its duration (hf_cost, one plain store)
+    // and k_hf_plan writes the plan of version hf_ver + 1 from them.
+    uint32_t hf_front;          // front section size (blocks, a multiple of 8)
+    uint32_t hf_ver;            // version of the plan this frame uses (0: none yet)
+    uint32_t hf_measure;        // 1: this frame records wave costs for the next plan
+    uint32_t hf_floor;          // a block is heavy above max(hf_floor, last max >> kHfShift) cycles
+    const uint32_t *hf_mark_in; // per block: == hf_ver when the current plan lists it
+    uint32_t *hf_mark_out;      // per block: hf_ver + 1 when the next plan lists it
+    const uint32_t *hf_list_in; // the current plan's front: [0, cnt_hi) and [front - cnt_lo, front)
+    uint32_t *hf_list_out;      // the next plan's
+    const HfPlan *hf_plan_in;   // the current plan (also the previous measurement's max and sum)
+    HfPlan *hf_plan_out;        // the next plan, cleared by the measured frame's first lane
+    uint32_t *hf_cost;          // per work item: shader cycles of its wave in the measured frame
     uint32_t bail_tests;        // BAIL_WIDE phase 1: test budget per sample
     uint32_t *bail_count;       // BAIL_WIDE: queued pixels
     uint32_t *bail_queue;       // BAIL_WIDE: (local tile << 8 | Morton pixel) per queued pixel
@@ -158,13 +177,30 @@ __device__ __forceinline__ void wave_lds_sync()
 // [1] iterations of the per-lane list loop
 __device__ __forceinline__ uint32_t *wave_counters()
 {
-    __shared__ uint32_t c[(kWG / 64u) * 2u];
+    __shared__ uint32_t c[kWavesPerWG * 2u];
     return c + (threadIdx.x >> 6) * 2u;
 }
 
 __device__ __forceinline__ bool first_active_lane()
 {
     return (threadIdx.x & 63u) == uint32_t(__ffsll((long long)__ballot(1)) - 1);
+}
+
+// The kernel's KParams re-read from the kernarg segment.  Parameters used only after the
+// walk (output, shading, tile bookkeeping) are taken from here, so the compiler reloads them
+// with s_load after the walk instead of holding ~30 SGPRs of them live across it (the render
+// kernels' SGPR budget decides 8 vs 7 waves per SIMD).  The empty asm hides the pointer's
+// origin (a register round trip), so these loads cannot be merged with the kernel entry's.  Only for kernels whose
+// first argument is the KParams.
+__device__ __forceinline__ const KParams& late_params(const KParams& P)
+{
+    (void)P;
+    const uint64_t a = uint64_t(__builtin_amdgcn_kernarg_segment_ptr());
+    uint32_t lo = uint32_t(a), hi = uint32_t(a >> 32);
+    asm volatile("" : "+v"(lo), "+v"(hi));
+    lo = __builtin_amdgcn_readfirstlane(lo);
+    hi = __builtin_amdgcn_readfirstlane(hi);
+    return *(const KParams *)(const __attribute__((address_space(4))) KParams *)((uint64_t(hi) << 32) | lo);
 }
 
 // CSR range of a cell: one u32 load of the packed (start << 11 | count) word when the scene
@@ -185,28 +221,39 @@ __device__ __forceinline__ void cell_range(const KParams& P, uint32_t cell, uint
     }
 }
 
+typedef float vf4 __attribute__((ext_vector_type(4)));
+// constant address space: uniform loads of memory no store of the render kernels touches (frefs
+// are written by k_origin_pre, an earlier launch) select s_load through the scalar cache
+typedef const __attribute__((address_space(4))) vf4 cvf4;
+
 // Tests a cell's list [kb, ke) in order (grid.cpp:243-267); true when it produced a hit.
-// t starts at FLT_MAX for every cell the walk reaches (a hit returns, grid.cpp:270-271).
+// grid.cpp:258-260 accepts cur_t when cur_t < t && cur_t < next_crossing_t[step_axis].  t is
+// FLT_MAX on entry (a hit ends the walk, grid.cpp:270-271) and neither bound is ever NaN, so the
+// two compares are one against tb = min(t, nct_ax), which every accepted hit lowers to its t:
+// the same hits are taken in the same order (strict '<' keeps the first of equal t, H8).
 template <bool STATS, int TRI, int VAR>
 __device__ __forceinline__ bool test_cell(const KParams& P, float ox, float oy, float oz, float dx, float dy,
                                           float dz, uint32_t kb, uint32_t ke, float nct_ax, float& t,
                                           float& u, float& v, uint32_t& tri, uint32_t& tests)
 {
-    if constexpr ((VAR & kVarUniform) != 0 && (VAR & kVarOriginPre) != 0 && TRI == RT_TRI_MOLLER_TRUMBORE)
+    constexpr bool PRE = (VAR & kVarOriginPre) != 0 && TRI == RT_TRI_MOLLER_TRUMBORE;
+    constexpr bool F = (VAR & kVarFastRcp) != 0;
+    const float tb0 = __builtin_fminf(t, nct_ax);
+    // every accepted hit lowers tb strictly, so "some hit was taken" is tb < tb0; u, v and tri
+    // are updated in place (the caller's values stand when nothing is taken)
+    float tb = tb0;
+    bool uniform_done = false;                // wave-uniform
+    if constexpr ((VAR & kVarUniform) != 0 && PRE)
     {
         // Wave-uniform list: every lane testing this step sits in the same cell (the common case
         // in dense geometry: a wave is a 4x4-pixel x 4-sample block).  The loop runs on scalar
-        // registers and the records arrive through the scalar cache (s_load_dwordx4), off the
+        // registers and the records arrive through the scalar cache (s_load), off the
         // vector-memory path; results are the same ray/record pairs in the same order.
         const uint32_t kb0 = __builtin_amdgcn_readfirstlane(kb), ke0 = __builtin_amdgcn_readfirstlane(ke);
         if (__all((kb == kb0) & (ke == ke0)))
         {
             if constexpr ((VAR & kVarWaveClock) != 0)
                 if (first_active_lane()) wave_counters()[0] += ke0 - kb0;
-            // constant address space: uniform loads of memory no store of this kernel touches
-            // (frefs are written by k_origin_pre, an earlier launch) select s_load
-            typedef float vf4 __attribute__((ext_vector_type(4)));
-            typedef const __attribute__((address_space(4))) vf4 cvf4;
             cvf4 *crefs = (cvf4 *)P.frefs;
             if constexpr ((VAR & kVarLdsCells) != 0)
             {
@@ -217,7 +264,7 @@ __device__ __forceinline__ bool test_cell(const KParams& P, float ox, float oy, 
                 // latency per record; same records, same order.
                 if (ke0 - kb0 >= kLdsMinRefs)
                 {
-                    __shared__ float4 s_cells[(kWG / 64u) * kLdsStage * 3u];
+                    __shared__ float4 s_cells[kWavesPerWG * kLdsStage * 3u];
                     float4 *st = s_cells + (threadIdx.x >> 6) * (kLdsStage * 3u);
                     const uint64_t act = __ballot(1);
                     const uint32_t rank = __builtin_amdgcn_mbcnt_hi(uint32_t(act >> 32),
@@ -230,7 +277,7 @@ __device__ __forceinline__ bool test_cell(const KParams& P, float ox, float oy, 
                         if (act == ~0ull)
                         {
                             // full wave: LDS-DMA, no VGPR staging (writes base + lane x 16 B; lanes
-                            // past the chunk re-read its last record into unused slots)
+                            // past the chunk re-read its last float4 into unused slots)
                             const uint32_t lane = threadIdx.x & 63u;
                             for (uint32_t j = 0; 64u * j < n3; j++)
                                 __builtin_amdgcn_global_load_lds(
@@ -241,230 +288,104 @@ __device__ __forceinline__ bool test_cell(const KParams& P, float ox, float oy, 
                             for (uint32_t q = rank; q < n3; q += nact)
                                 st[q] = src[q];
                         wave_lds_sync();
-                        float4 n0 = st[0], n1 = st[1], n2 = st[2];   // kVarUnroll: one record ahead
                         for (uint32_t i = 0; 3u * i < n3; i++)
                         {
                             // the whole record in one LDS round trip (the empty asm keeps the reads
                             // of its second half from being sunk into the gate)
-                            float4 r0, r1, r2;
-                            if constexpr ((VAR & kVarUnroll) != 0)
-                            {
-                                r0 = n0; r1 = n1; r2 = n2;
-                                const uint32_t j = 3u * i + 3u < n3 ? 3u * i + 3u : 3u * i;
-                                n0 = st[j];
-                                n1 = st[j + 1u];
-                                n2 = st[j + 2u];
-                                asm volatile("" ::"v"(n0.x), "v"(n0.y), "v"(n0.z), "v"(n0.w), "v"(n1.x), "v"(n1.y),
-                                             "v"(n1.z), "v"(n1.w), "v"(n2.x), "v"(n2.y), "v"(n2.z), "v"(n2.w));
-                            }
-                            else
-                            {
-                                r0 = st[3u * i];
-                                r1 = st[3u * i + 1u];
-                                r2 = st[3u * i + 2u];
-                                asm volatile("" ::"v"(r0.x), "v"(r0.y), "v"(r0.z), "v"(r0.w), "v"(r1.x), "v"(r1.y),
-                                             "v"(r1.z), "v"(r1.w), "v"(r2.x), "v"(r2.y), "v"(r2.z), "v"(r2.w));
-                            }
-                            float ct, cu, cv;
-                            const bool hit = rtd::ray_tri_mt_gated_pre<(VAR & kVarFastRcp) != 0>(
-                                dx, dy, dz, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w,
-                                ct, cu, cv);
+                            const float4 r0 = st[3u * i], r1 = st[3u * i + 1u], r2 = st[3u * i + 2u];
+                            asm volatile("" ::"v"(r0.x), "v"(r0.y), "v"(r0.z), "v"(r0.w), "v"(r1.x), "v"(r1.y),
+                                         "v"(r1.z), "v"(r1.w), "v"(r2.x), "v"(r2.y), "v"(r2.z), "v"(r2.w));
                             if (STATS) tests++;
-                            const bool take = hit & (ct < t) & (ct < nct_ax);
-                            t = take ? ct : t;
-                            u = take ? cu : u;
-                            v = take ? cv : v;
-                            tri = take ? base + i : tri;
+                            float inv, cu;
+                            const bool ok1 = rtd::mt_pre_first<F>(dx, dy, dz, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y,
+                                                                  r1.z, r1.w, r2.x, inv, cu);
+                            if (__any(ok1))
+                            {
+                                float cv, ct;
+                                const bool hit = ok1 & rtd::mt_pre_second(dx, dy, dz, r2.y, r2.z, r2.w, r0.w, r1.x, r1.y, inv,
+                                                                          cu, cv, ct);
+                                const bool take = hit & (ct < tb);
+                                tb = take ? ct : tb;
+                                u = take ? cu : u;
+                                v = take ? cv : v;
+                                tri = take ? base + i : tri;
+                            }
                         }
                         wave_lds_sync();                  // reads of this chunk before the next copy
                     }
-                    return t != rtd::kFltMax;
+                    uniform_done = true;
                 }
             }
-            // software pipeline: record k + 1 is in flight while record k is tested (scalar
-            // loads may return out of order, so the wait for record k sits at its copy, before
-            // the next load is issued)
-            vf4 n0 = crefs[size_t(kb0) * 3], n1 = crefs[size_t(kb0) * 3 + 1], n2 = crefs[size_t(kb0) * 3 + 2];
-            uint32_t k = kb0;
-            if constexpr ((VAR & kVarUnroll) != 0)
+            if (!uniform_done)
             {
-                // two records per iteration: both first halves (det, 1/det, u) are independent
-                // dependency chains the scheduler interleaves; acceptance stays in list order
-                constexpr bool F = (VAR & kVarFastRcp) != 0;
-                vf4 m0 = n0, m1 = n1, m2 = n2;
-                if (k + 1u < ke0)
+                // software pipeline: record k + 1 is in flight while record k is tested (scalar
+                // loads may return out of order, so the wait for record k sits at its copy, before
+                // the next load is issued)
+                cvf4 *np = crefs + size_t(kb0) * 3u;
+                vf4 n0 = np[0], n1 = np[1], n2 = np[2];
+                for (uint32_t k = kb0; k < ke0; k++)
                 {
-                    m0 = crefs[size_t(k + 1u) * 3];
-                    m1 = crefs[size_t(k + 1u) * 3 + 1];
-                    m2 = crefs[size_t(k + 1u) * 3 + 2];
-                }
-                for (; k + 1u < ke0; k += 2u)
-                {
-                    const vf4 a0 = n0, a1 = n1, a2 = n2, b0 = m0, b1 = m1, b2 = m2;
-                    if (k + 2u < ke0)
+                    const vf4 r0 = n0, r1 = n1, r2 = n2;
+                    if (k + 1u < ke0)
                     {
-                        n0 = crefs[size_t(k + 2u) * 3];
-                        n1 = crefs[size_t(k + 2u) * 3 + 1];
-                        n2 = crefs[size_t(k + 2u) * 3 + 2];
+                        np = crefs + size_t(k + 1u) * 3u;
+                        n0 = np[0];
+                        n1 = np[1];
+                        n2 = np[2];
                     }
-                    if (k + 3u < ke0)
-                    {
-                        m0 = crefs[size_t(k + 3u) * 3];
-                        m1 = crefs[size_t(k + 3u) * 3 + 1];
-                        m2 = crefs[size_t(k + 3u) * 3 + 2];
-                    }
-                    float ia, ua, ib, ub, va = 0.0f, ta = 0.0f, vb = 0.0f, tb = 0.0f;
-                    const bool oka = rtd::mt_pre_first<F>(dx, dy, dz, a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z,
-                                                          a1.w, a2.x, ia, ua);
-                    const bool okb = rtd::mt_pre_first<F>(dx, dy, dz, b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z,
-                                                          b1.w, b2.x, ib, ub);
-                    bool ha = false, hb = false;
-                    if (__any(oka))
-                        ha = oka & rtd::mt_pre_second(dx, dy, dz, a0.w, a1.x, a1.y, a2.y, a2.z, a2.w, ia, ua, va, ta);
-                    if (__any(okb))
-                        hb = okb & rtd::mt_pre_second(dx, dy, dz, b0.w, b1.x, b1.y, b2.y, b2.z, b2.w, ib, ub, vb, tb);
-                    if (STATS) tests += 2u;
-                    const bool takea = ha & (ta < t) & (ta < nct_ax);
-                    t = takea ? ta : t;
-                    u = takea ? ua : u;
-                    v = takea ? va : v;
-                    tri = takea ? k : tri;
-                    const bool takeb = hb & (tb < t) & (tb < nct_ax);
-                    t = takeb ? tb : t;
-                    u = takeb ? ub : u;
-                    v = takeb ? vb : v;
-                    tri = takeb ? k + 1u : tri;
-                }
-            }
-            if ((VAR & kVarAltLoads) != 0 && ke0 - kb0 >= kAltMinRefs)
-            {
-                // Two record register sets used in turn, so nothing is copied between records.
-                // Scalar loads complete out of order and a wait covers every load in flight, so
-                // each set's wait is forced (empty asm) before the other set's loads are issued:
-                // record k + 1 still loads while record k is tested.
-                auto test_rec = [&](const vf4& r0, const vf4& r1, const vf4& r2, uint32_t kk) {
-                    float ct, cu, cv;
-                    const bool hit = rtd::ray_tri_mt_gated_pre<(VAR & kVarFastRcp) != 0>(
-                        dx, dy, dz, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w, ct, cu,
-                        cv);
                     if (STATS) tests++;
-                    const bool take = hit & (ct < t) & (ct < nct_ax);
-                    t = take ? ct : t;
-                    u = take ? cu : u;
-                    v = take ? cv : v;
-                    tri = take ? kk : tri;
-                };
-                vf4 b0, b1, b2;
-                for (;;)
-                {
-                    asm volatile("" ::"s"(n0), "s"(n1), "s"(n2));
-                    if (k + 1u < ke0)
+                    // the gate skips the record's second half AND the acceptance for the whole wave
+                    // when no lane passes det and u (the common case in a dense cell)
+                    float inv, cu;
+                    const bool ok1 = rtd::mt_pre_first<F>(dx, dy, dz, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z,
+                                                          r1.w, r2.x, inv, cu);
+                    if (__any(ok1))
                     {
-                        b0 = crefs[size_t(k + 1u) * 3];
-                        b1 = crefs[size_t(k + 1u) * 3 + 1];
-                        b2 = crefs[size_t(k + 1u) * 3 + 2];
+                        float cv, ct;
+                        const bool hit = ok1 & rtd::mt_pre_second(dx, dy, dz, r2.y, r2.z, r2.w, r0.w, r1.x, r1.y, inv, cu, cv, ct);
+                        const bool take = hit & (ct < tb);
+                        tb = take ? ct : tb;
+                        u = take ? cu : u;
+                        v = take ? cv : v;
+                        tri = take ? k : tri;
                     }
-                    test_rec(n0, n1, n2, k);
-                    if (++k >= ke0) break;
-                    asm volatile("" ::"s"(b0), "s"(b1), "s"(b2));
-                    if (k + 1u < ke0)
-                    {
-                        n0 = crefs[size_t(k + 1u) * 3];
-                        n1 = crefs[size_t(k + 1u) * 3 + 1];
-                        n2 = crefs[size_t(k + 1u) * 3 + 2];
-                    }
-                    test_rec(b0, b1, b2, k);
-                    if (++k >= ke0) break;
-                }
-                return t != rtd::kFltMax;
-            }
-            for (; k < ke0; k++)
-            {
-                const vf4 r0 = n0, r1 = n1, r2 = n2;
-                if (k + 1u < ke0)
-                {
-                    cvf4 *np = crefs + size_t(k + 1u) * 3;
-                    n0 = np[0];
-                    n1 = np[1];
-                    n2 = np[2];
-                }
-                if (STATS) tests++;
-                // the gate skips the record's second half AND the acceptance for the whole wave
-                // when no lane passes det and u (the common case in a dense cell)
-                float inv, cu;
-                const bool ok1 = rtd::mt_pre_first<(VAR & kVarFastRcp) != 0>(
-                    dx, dy, dz, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x, inv, cu);
-                if (__any(ok1))
-                {
-                    float cv, ct;
-                    const bool hit =
-                        ok1 & rtd::mt_pre_second(dx, dy, dz, r0.w, r1.x, r1.y, r2.y, r2.z, r2.w, inv, cu, cv, ct);
-                    const bool take = hit & (ct < t) & (ct < nct_ax);
-                    t = take ? ct : t;
-                    u = take ? cu : u;
-                    v = take ? cv : v;
-                    tri = take ? k : tri;
                 }
             }
-            return t != rtd::kFltMax;
+            uniform_done = true;
         }
     }
-    // the per-frame records (ORIGIN_PRE) or the scene's reference records
-    const float4 *recs = ((VAR & kVarOriginPre) && TRI == RT_TRI_MOLLER_TRUMBORE) ? P.frefs : P.refs;
-    float4 n0, n1, n2;
-    if ((VAR & kVarPrefetch) && kb < ke)
-    {
-        const float4 *rp = recs + size_t(kb) * 3;
-        n0 = rp[0];
-        n1 = rp[1];
-        n2 = rp[2];
-    }
+    if (!uniform_done)
     for (uint32_t k = kb; k < ke; k++)
     {
         if constexpr ((VAR & kVarWaveClock) != 0)
             if (first_active_lane()) wave_counters()[1] += 1u;
-        float4 r0, r1, r2;
-        if (VAR & kVarPrefetch)
+        if (STATS) tests++;
+        if constexpr (PRE)
         {
-            r0 = n0; r1 = n1; r2 = n2;
-            if (k + 1 < ke)
-            {
-                const float4 *rp = recs + size_t(k + 1) * 3;
-                n0 = rp[0];
-                n1 = rp[1];
-                n2 = rp[2];
-            }
-        }
-        else
-        {
-            const float4 *rp = recs + size_t(k) * 3;     // one address, immediate offsets
-            r0 = rp[0];
-            r1 = rp[1];
-            r2 = rp[2];
-        }
-        if constexpr ((VAR & kVarOriginPre) != 0 && TRI == RT_TRI_MOLLER_TRUMBORE)
-        {
-            // r0..r2 = the frame record; the triangle id is resolved from refs after the walk.
+            // the per-camera record; the triangle id is resolved from refs after the walk.
             // The gate skips the second half and the acceptance when no lane passes det and u.
-            if (STATS) tests++;
+            const float4 *rp = P.frefs + size_t(k) * 3u;     // one address, immediate offsets
+            const float4 r0 = rp[0], r1 = rp[1], r2 = rp[2];
             float inv, pu;
-            const bool ok1 = rtd::mt_pre_first<(VAR & kVarFastRcp) != 0>(
-                dx, dy, dz, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x, inv, pu);
+            const bool ok1 = rtd::mt_pre_first<F>(dx, dy, dz, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x,
+                                                  inv, pu);
             if (__any(ok1))
             {
                 float pv, pt;
-                const bool h = ok1 & rtd::mt_pre_second(dx, dy, dz, r0.w, r1.x, r1.y, r2.y, r2.z, r2.w, inv, pu, pv, pt);
-                const bool take = h & (pt < t) & (pt < nct_ax);   // grid.cpp:258-266
-                t = take ? pt : t;
+                const bool h = ok1 & rtd::mt_pre_second(dx, dy, dz, r2.y, r2.z, r2.w, r0.w, r1.x, r1.y, inv, pu, pv, pt);
+                const bool take = h & (pt < tb);
+                tb = take ? pt : tb;
                 u = take ? pu : u;
                 v = take ? pv : v;
                 tri = take ? k : tri;
             }
             continue;
         }
+        const float4 *rp = P.refs + size_t(k) * 3;          // one address, immediate offsets
+        const float4 r0 = rp[0], r1 = rp[1], r2 = rp[2];
         float ct, cu, cv;
         bool hit;
-        uint32_t id = __float_as_uint(r2.y);
+        const uint32_t id = __float_as_uint(r2.y);
         if (TRI == RT_TRI_BARYCENTRIC)
         {
             const float4 fn = P.face_n[id];
@@ -477,64 +398,29 @@ __device__ __forceinline__ bool test_cell(const KParams& P, float ox, float oy, 
         else
             hit = rtd::ray_tri_mt_pred(ox, oy, oz, dx, dy, dz, r0.x, r0.y, r0.z, r0.w, r1.x,
                                        r1.y, r1.z, r1.w, r2.x, ct, cu, cv);
-        if (STATS) tests++;
-        // grid.cpp:258-266: strict '<' over the ascending list keeps the first of ties
-        const bool take = hit & (ct < t) & (ct < nct_ax);
-        t = take ? ct : t;
+        const bool take = hit & (ct < tb);                     // grid.cpp:258-260
+        tb = take ? ct : tb;
         u = take ? cu : u;
         v = take ? cv : v;
         tri = take ? id : tri;
     }
-    return t != rtd::kFltMax;                             // grid.cpp:270-271
+    t = tb < tb0 ? tb : t;
+    return t != rtd::kFltMax;                                  // grid.cpp:270-271
 }
 
-// One DDA advance over plain local variables (grid.cpp:236-239 + 274-277) written as
-// selects, exact because untouched axes keep their values.  A macro, not a member function or
-// a capturing lambda: selecting between struct fields through `this`/references becomes a
-// pointer select, which defeats SROA and put the walk state in LDS/scratch (measured).
-// Sets NCT_AX to the step axis' crossing t and MORE to false when the ray leaves the grid.
-#define RT_DDA_ADVANCE_NESTED(NCT_AX, MORE)                                                           \
-    do {                                                                                       \
-        const int ax_ = (nct0 < nct1) ? ((nct0 < nct2) ? 0 : 2) : ((nct1 < nct2) ? 1 : 2);    \
-        const bool a0_ = ax_ == 0, a1_ = ax_ == 1, a2_ = ax_ == 2;                             \
-        NCT_AX = a0_ ? nct0 : (a1_ ? nct1 : nct2);                                             \
-        const int rem_ = a0_ ? rem0 : (a1_ ? rem1 : rem2);                                     \
-        MORE = rem_ != 0;                                                                      \
-        if (MORE)                                                                              \
-        {                                                                                      \
-            rem0 -= int(a0_); rem1 -= int(a1_); rem2 -= int(a2_);                              \
-            nct0 = a0_ ? nct0 + dt0 : nct0;                                                    \
-            nct1 = a1_ ? nct1 + dt1 : nct1;                                                    \
-            nct2 = a2_ ? nct2 + dt2 : nct2;                                                    \
-            cell += a0_ ? cs0 : (a1_ ? cs1 : cs2);                                             \
-        }                                                                                      \
-    } while (0)
-
+// One DDA advance over plain local variables (grid.cpp:236-239 + 274-277), exact because
+// untouched axes keep their values.  A macro, not a member function or a capturing lambda:
+// selecting between struct fields through `this`/references becomes a pointer select, which
+// defeats SROA and put the walk state in LDS/scratch (measured).
 // Step axis of grid.cpp:236-239 restated: with m = min(nct), the nested strict '<' chain picks
 // the HIGHEST axis index among those equal to m (all 7 tie patterns checked), so
 // a2 = nct2 == m, a1 = !a2 && nct1 == m, else a0.  nct is never NaN (finite setup, FLT_MAX for
-// zero components).  The state updates run unconditionally -- when MORE is false the caller
-// breaks and the state is dead -- so the step has no divergent branch.
-#define RT_DDA_ADVANCE(NCT_AX, MORE)                                                           \
-    do {                                                                                       \
-        const float m_ = __builtin_fminf(__builtin_fminf(nct0, nct1), nct2);                   \
-        const bool a2_ = nct2 == m_;                                                           \
-        const bool a1_ = !a2_ && nct1 == m_;                                                   \
-        const bool a0_ = !a2_ && !a1_;                                                         \
-        NCT_AX = m_;                                                                           \
-        MORE = (a2_ ? rem2 : (a1_ ? rem1 : rem0)) != 0;                                        \
-        const float n_ = (a2_ ? nct2 : (a1_ ? nct1 : nct0)) + (a2_ ? dt2 : (a1_ ? dt1 : dt0));   \
-        nct0 = a0_ ? n_ : nct0;                                                                \
-        nct1 = a1_ ? n_ : nct1;                                                                \
-        nct2 = a2_ ? n_ : nct2;                                                                \
-        rem0 -= int(a0_); rem1 -= int(a1_); rem2 -= int(a2_);                                  \
-        cell += a2_ ? cs2 : (a1_ ? cs1 : cs0);                                                 \
-    } while (0)
-
-// RT_DDA_ADVANCE with each crossing time advanced by an add of the selected step:
-// nct_a + (a ? dt_a : 0.0f).  Bit-identical: the step axis gets the same single IEEE add, and
-// x + 0.0f == x for every value nct takes (finite or +inf, never -0 or NaN: every setup term is
-// >= 0, see dda_setup).  Two VALU fewer per step than the select-then-write-back form.
+// zero components).  Each crossing time advances as nct_a + (a ? dt_a : 0.0f): the step axis
+// gets the reference's single IEEE add (grid.cpp:277), and x + 0.0f == x for every value nct
+// takes (finite or +inf, never -0 or NaN: every setup term is >= 0, see dda_setup).  The state
+// updates run unconditionally -- when MORE is false the caller breaks and the state is dead --
+// so the step has no divergent branch.  Sets NCT_AX to the step axis' crossing t and MORE to
+// false when the ray leaves the grid (grid.cpp:275-276).
 #define RT_DDA_ADVANCE_ADD(NCT_AX, MORE)                                                       \
     do {                                                                                       \
         const float m_ = __builtin_fminf(__builtin_fminf(nct0, nct1), nct2);                   \
@@ -554,7 +440,7 @@ __device__ __forceinline__ bool test_cell(const KParams& P, float ox, float oy, 
 // 0-9, rem1 in 11-20, rem2 in 22-30, guard bits 10, 21, 31 (needs dims <= 512; rt_scene::
 // pack_ok).  The step subtracts the axis unit unconditionally; a count that was 0 borrows into
 // its guard bit, so MORE = no guard bit set == (rem of the step axis != 0) -- the walk exits
-// exactly where RT_DDA_ADVANCE's does (the borrowed state is dead after the exit).
+// exactly where RT_DDA_ADVANCE_ADD's does (the borrowed state is dead after the exit).
 constexpr int kRemGuards = int((1u << 10) | (1u << 21) | (1u << 31));
 #define RT_DDA_ADVANCE_PACKED(NCT_AX, MORE)                                                    \
     do {                                                                                       \
@@ -572,7 +458,7 @@ constexpr int kRemGuards = int((1u << 10) | (1u << 21) | (1u << 31));
     } while (0)
 
 // Grid entry + per-axis DDA setup of Grid::Intersect (aabb.h:9-83, grid.h:44-51,
-// grid.cpp:167-216), axis arrays unrolled into scalars.  Instead of pos/step/out per axis the
+// grid.cpp:174-216), axis arrays unrolled into scalars.  Instead of pos/step/out per axis the
 // walk keeps the cells left before 'pos == out' (rem) and the signed GridIdx stride of a step
 // (cs): grid.cpp:274-277 exits after the same steps.  False when the ray misses the grid.
 __device__ __forceinline__ bool dda_setup(const KParams& P, float ox, float oy, float oz, float dx, float dy, float dz,
@@ -631,8 +517,7 @@ __device__ __forceinline__ bool dda_setup(const KParams& P, float ox, float oy, 
 // grid.cpp:159-281 Grid::Intersect (NEW_GRID_TRAVERSAL), axis arrays unrolled into scalars
 // so nothing is runtime-indexed (no scratch).  Counters are compiled in only for records.
 template <bool STATS, int TRI, int VAR>
-__device__ __forceinline__ bool grid_intersect(const KParams& P, const uint32_t *lds_occ,
-                                               float ox, float oy, float oz,
+__device__ __forceinline__ bool grid_intersect(const KParams& P, float ox, float oy, float oz,
                                                float dx, float dy, float dz,
                                                float& t, float& u, float& v, uint32_t& tri,
                                                uint32_t& voxel, uint32_t& steps, uint32_t& tests,
@@ -645,61 +530,40 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, const uint32_t 
         return false;
     t = rtd::kFltMax;
 
-    if (P.cellw && !lds_occ && (VAR & kVarDistSkip))
+    if (P.cellw && (VAR & kVarDistSkip))
     {
         // Distance skipping: after an empty cell at L-inf distance d from geometry the next
         // d-1 cells of the walk are provably empty, so they take the DDA step only.
         // Termination: every iteration that does not exit decrements a positive rem (the step
         // axis' count; MORE is false when it is 0), so a walk ends within rem0+rem1+rem2+1
-        // iterations whatever nct holds -- the P.max_steps bound is kept only in the A/B arm.
+        // iterations whatever nct holds.
         int skip = 0;
         int remp = rem0 | (rem1 << 11) | (rem2 << 22);      // kVarPackedRem only
         int budget = int(P.bail_tests);                      // kVarBail only
-        for (uint32_t iter = 0;; iter++)
+        for (;;)
         {
-            if ((VAR & kVarSelStep) && iter >= P.max_steps) break;
             if (STATS) { voxel = uint32_t(cell); steps++; }
             uint32_t kb = 0, ke = 0;
             float nct_ax;
             bool more;
-            if constexpr ((VAR & kVarEarlyLoad) != 0 && (VAR & kVarPackedRem) != 0 && (VAR & kVarSelStep) == 0)
+            if (skip == 0)
             {
-                // The cell word is loaded for every cell (also inside a proven-empty run, where
-                // it goes unused) and issued before the step, so the step's VALU work runs while
-                // the load is in flight instead of after its wait.
                 const uint32_t w = P.cellw[uint32_t(cell)];
-                RT_DDA_ADVANCE_PACKED(nct_ax, more);
-                // branch-free decode: the word is used on every path, so the load is not sunk
-                // back into a skip == 0 branch behind the step
-                const bool fresh = skip == 0;
-                const uint32_t cnt = fresh ? (w & 2047u) : 0u;
-                kb = fresh ? (w >> 11) : 0u;
+                const uint32_t cnt = w & 2047u;
+                kb = w >> 11;
                 ke = kb + cnt;
-                skip = fresh ? (cnt ? 0 : int(kb) - 1) : skip - 1;
+                skip = cnt ? 0 : int(kb) - 1;
             }
             else
-            {
-                if (skip == 0)
-                {
-                    const uint32_t w = P.cellw[uint32_t(cell)];
-                    const uint32_t cnt = w & 2047u;
-                    kb = w >> 11;
-                    ke = kb + cnt;
-                    skip = cnt ? 0 : int(kb) - 1;
-                }
-                else
-                    skip--;
-                if (VAR & kVarSelStep)
-                    RT_DDA_ADVANCE(nct_ax, more);
-                else if (VAR & kVarPackedRem)
-                    RT_DDA_ADVANCE_PACKED(nct_ax, more);
-                else
-                    RT_DDA_ADVANCE_ADD(nct_ax, more);
-            }
+                skip--;
+            if (VAR & kVarPackedRem)
+                RT_DDA_ADVANCE_PACKED(nct_ax, more);
+            else
+                RT_DDA_ADVANCE_ADD(nct_ax, more);
             if constexpr ((VAR & kVarBail) != 0)
             {
                 // two-phase arm: a sample whose walk would pass bail_tests tests stops here and
-                // is re-traced by the wide phase (k_render_bailed); nothing of it is stored.
+                // is resumed by the wide phase (k_render_bailed); nothing of it is stored.
                 // Branch-free count (ke - kb is 0 for skipped and empty cells); the stop shares
                 // the walk's exit, so the loop keeps two exits, not three.
                 budget -= int(ke - kb);
@@ -724,56 +588,55 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, const uint32_t 
             }
             else
             {
-                if (kb < ke && test_cell<STATS, TRI, VAR>(P, ox, oy, oz, dx, dy, dz, kb, ke, nct_ax, t, u, v, tri, tests))
-                    return true;
-                if (!more) break;
-            }
-            if constexpr ((VAR & kVarSkipRun) != 0 && (VAR & kVarPackedRem) != 0 && (VAR & kVarSelStep) == 0 &&
-                          !STATS)
-            {
-                // Wave-uniform empty run: while every active lane is inside a run of cells the
-                // distance field proves empty, the wave takes bare DDA steps -- the same advances
-                // and the same exits as one iteration per cell, with no cell word or test work.
-                // Uniform, so no lane waits on another's run; the run ends when the first lane's
-                // does.
-                if (__all(skip > 0))
+                // one exit test per iteration (a hit, or the grid's end here or in the empty run
+                // below), and the result read from t after the loop: the walk's loop-carried state
+                // stays in VGPRs instead of per-exit lane masks (SALU per wave, PMC-measured)
+                bool hit = false;
+                if (kb < ke) hit = test_cell<STATS, TRI, VAR>(P, ox, oy, oz, dx, dy, dz, kb, ke, nct_ax, t, u, v, tri, tests);
+                bool done = hit | !more;
+                if constexpr ((VAR & kVarSkipRun) != 0 && (VAR & kVarPackedRem) != 0 && !STATS)
                 {
-                    bool more;
-                    do
+                    // Wave-uniform empty run: while every active lane is inside a run of cells the
+                    // distance field proves empty, the wave takes bare DDA steps -- the same advances
+                    // and the same exits as one iteration per cell, with no cell word or test work.
+                    // Uniform, so no lane waits on another's run; the run ends when the first lane's
+                    // does.  (A lane inside a run has no hit and more == true, so done is false.)
+                    if (__all(skip > 0))
                     {
-                        skip--;
-                        const float m_ = __builtin_fminf(__builtin_fminf(nct0, nct1), nct2);
-                        const bool a2_ = nct2 == m_;
-                        const bool a1_ = !a2_ && nct1 == m_;
-                        const bool a0_ = !a2_ && !a1_;
-                        remp -= a2_ ? (1 << 22) : (a1_ ? (1 << 11) : 1);
-                        more = (remp & kRemGuards) == 0;
-                        nct0 += a0_ ? dt0 : 0.0f;
-                        nct1 += a1_ ? dt1 : 0.0f;
-                        nct2 += a2_ ? dt2 : 0.0f;
-                        cell += a2_ ? cs2 : (a1_ ? cs1 : cs0);
-                    } while (__all((skip > 0) & more));
-                    if (!more) break;
+                        do
+                        {
+                            skip--;
+                            const float m_ = __builtin_fminf(__builtin_fminf(nct0, nct1), nct2);
+                            const bool a2_ = nct2 == m_;
+                            const bool a1_ = !a2_ && nct1 == m_;
+                            const bool a0_ = !a2_ && !a1_;
+                            remp -= a2_ ? (1 << 22) : (a1_ ? (1 << 11) : 1);
+                            more = (remp & kRemGuards) == 0;
+                            nct0 += a0_ ? dt0 : 0.0f;
+                            nct1 += a1_ ? dt1 : 0.0f;
+                            nct2 += a2_ ? dt2 : 0.0f;
+                            cell += a2_ ? cs2 : (a1_ ? cs1 : cs0);
+                        } while (__all((skip > 0) & more));
+                        done = !more;
+                    }
                 }
+                if (done) break;
             }
         }
-        return false;
+        return t != rtd::kFltMax;                            // t is only set by a hit
     }
 
+    // One cell per iteration with its CSR range (the plain LANES arm, and scenes whose cell
+    // lists do not fit the packed word).  max_steps = dims sum + 3 bounds it redundantly.
     for (uint32_t iter = 0; iter < P.max_steps; iter++)
     {
         if (STATS) { voxel = uint32_t(cell); steps++; }
-        const uint32_t ucell = uint32_t(cell);
-        const bool occupied = lds_occ ? ((lds_occ[ucell >> 5] >> (ucell & 31u)) & 1u) != 0u : true;
-        // Issue the CSR offset loads first; the step's ALU work below overlaps their latency.
+        // Issue the CSR range loads first; the step's ALU work below overlaps their latency.
         uint32_t kb = 0, ke = 0;
-        if (occupied) cell_range(P, ucell, kb, ke);
+        cell_range(P, uint32_t(cell), kb, ke);
         float nct_ax;
         bool more;
-        if (VAR & kVarNestedStep)
-            RT_DDA_ADVANCE_NESTED(nct_ax, more);
-        else
-            RT_DDA_ADVANCE(nct_ax, more);
+        RT_DDA_ADVANCE_ADD(nct_ax, more);
         if (kb < ke && test_cell<STATS, TRI, VAR>(P, ox, oy, oz, dx, dy, dz, kb, ke, nct_ax, t, u, v, tri, tests))
             return true;
         if (!more) break;
@@ -920,11 +783,11 @@ __device__ __forceinline__ bool ray_march(const KParams& P, float ox, float oy, 
     return false;
 }
 
-// renderer.cpp:126-160: one sample -> its colour contribution
+// renderer.cpp:88-122: one sample -> its colour contribution
 template <bool STATS, int TRI, int VAR>
-__device__ __forceinline__ void trace_sample(const KParams& P, const uint32_t *lds_occ, uint32_t px, uint32_t py,
-                                             uint32_t s, float& cr, float& cg, float& cb,
-                                             rt_sample_rec *rec, bool *bailed = nullptr, uint32_t bail_idx = 0u)
+__device__ __forceinline__ void trace_sample(const KParams& P, uint32_t px, uint32_t py, uint32_t s, float& cr,
+                                             float& cg, float& cb, rt_sample_rec *rec, bool *bailed = nullptr,
+                                             uint32_t bail_idx = 0u)
 {
     const float2 so = P.smp[s];
     float dx, dy, dz;
@@ -938,27 +801,27 @@ __device__ __forceinline__ void trace_sample(const KParams& P, const uint32_t *l
     else if constexpr ((VAR & kVarBrute) != 0)
         hit = brute_intersect<STATS>(P, P.org[0], P.org[1], P.org[2], dx, dy, dz, t, u, v, tri, tests);
     else
-    {
-        hit = grid_intersect<STATS, TRI, VAR>(P, lds_occ, P.org[0], P.org[1], P.org[2], dx, dy, dz, t, u, v, tri,
-                                              voxel, steps, tests, bailed, bail_idx);
+        hit = grid_intersect<STATS, TRI, VAR>(P, P.org[0], P.org[1], P.org[2], dx, dy, dz, t, u, v, tri, voxel,
+                                              steps, tests, bailed, bail_idx);
+    const KParams& Q = late_params(P);
+    if constexpr ((VAR & (kVarMarch | kVarBrute)) == 0)
         if ((VAR & kVarOriginPre) && TRI == RT_TRI_MOLLER_TRUMBORE && hit)
-            tri = __float_as_uint(P.refs[3 * size_t(tri) + 2].y);     // CSR reference -> triangle id
-    }
+            tri = __float_as_uint(Q.refs[3 * size_t(tri) + 2].y);     // CSR reference -> triangle id
     if constexpr ((VAR & kVarMarch) != 0)
     {
         // The reference's RayMarch leaves u, v, tri_idx unset (renderer.cpp:103), so the
         // march is shaded by depth: the reference's own alternative at renderer.cpp:118.
         if (hit) cr = cg = cb = t / 3.0f;
-        else cr = cg = cb = float(py) / float(P.H);
+        else cr = cg = cb = float(py) / float(Q.H);
     }
     else if (hit)
     {
-        const float4 a = P.shade[3 * tri + 0], b = P.shade[3 * tri + 1], c = P.shade[3 * tri + 2];
+        const float4 a = Q.shade[3 * tri + 0], b = Q.shade[3 * tri + 1], c = Q.shade[3 * tri + 2];
         rtd::shade_hit(u, v, a, b, c, cr, cg, cb);
     }
     else
     {
-        const float m = float(py) / float(P.H);                  // renderer.cpp:159
+        const float m = float(py) / float(Q.H);                  // renderer.cpp:121
         cr = cg = cb = m;
     }
     if (STATS)
@@ -976,7 +839,7 @@ __device__ __forceinline__ void trace_sample(const KParams& P, const uint32_t *l
     }
 }
 
-// Tile bookkeeping shared by both render kernels: block -> (local tile k, sub-block)
+// Tile bookkeeping: block -> (local tile k, sub-block)
 struct TileCoord { uint32_t k, sub, tx0, ty0; };
 
 __device__ __forceinline__ TileCoord tile_of_block(const KParams& P)
@@ -997,14 +860,10 @@ __device__ __forceinline__ void store_pixel(const KParams& P, const TileCoord& c
     if (P.shard_mode)
         P.out[size_t(c.k) * kTilePix + compact_bits(p >> 1) * kTile + compact_bits(p)] = word;
     else
-        P.out[size_t(y - P.ry0) * P.pitch + (x - P.rx0)] = word;
+        P.out[size_t(y - P.ry0) * P.pitch + (x - P.rx0)] = word;     // renderer.cpp:133
 }
 
-// One wave-sized work item = 64 consecutive sample slots of a 16x16 tile in Morton order
-// (a 2^k x 2^k pixel block x spp samples).  Traces the lane's sample, sums the pixel's
-// samples across its adjacent lanes in sample order (renderer.cpp:125-160, hazard H10) and
-// stores the packed pixel (renderer.cpp:162-171).
-// renderer.cpp:162 col / float(spp); exact as a multiply when spp is a power of two
+// renderer.cpp:124 col / float(spp); exact as a multiply when spp is a power of two
 __device__ __forceinline__ float average(const KParams& P, float sum)
 {
     return P.inv_spp != 0.0f ? sum * P.inv_spp : sum / float(P.spp);
@@ -1012,8 +871,6 @@ __device__ __forceinline__ float average(const KParams& P, float sum)
 
 struct ItemCoord { TileCoord c; uint32_t p, s, x, y; bool valid; };
 
-// Pixel/sample of this lane in work item `item` (wave-uniform).  Called before AND after the
-// traversal so none of it is live (in VGPRs) across the DDA walk.
 // Sample slot `slot` (pixel-major, Morton pixel order) of local tile k.
 __device__ __forceinline__ ItemCoord tile_slot_coord(const KParams& P, uint32_t k, uint32_t slot)
 {
@@ -1031,16 +888,22 @@ __device__ __forceinline__ ItemCoord tile_slot_coord(const KParams& P, uint32_t 
     return ic;
 }
 
+// Pixel/sample of this lane in work item `item` (wave-uniform).  Called before AND after the
+// traversal so none of it is live (in VGPRs) across the DDA walk.
 __device__ __forceinline__ ItemCoord item_coord(const KParams& P, uint32_t item, uint32_t lane)
 {
-    const uint32_t items_per_tile = P.wg_per_tile * (kWG / 64u);
+    const uint32_t items_per_tile = P.wg_per_tile * kWavesPerWG;
     const uint32_t kseq = item / items_per_tile;              // position in the launch's tile order
     const uint32_t slot = (item - kseq * items_per_tile) * 64u + lane;
     return tile_slot_coord(P, P.tile_order ? P.tile_order[kseq] : kseq, slot);   // local tile k
 }
 
+// One wave-sized work item = 64 consecutive sample slots of a 16x16 tile in Morton order
+// (a 2^k x 2^k pixel block x spp samples).  Traces the lane's sample, sums the pixel's
+// samples across its adjacent lanes in sample order (renderer.cpp:87-122, hazard H10) and
+// stores the packed pixel (renderer.cpp:124-133).
 template <int TRI, int VAR>
-__device__ __forceinline__ void process_item(const KParams& P, const uint32_t *lds_occ, uint32_t item)
+__device__ __forceinline__ void process_item(const KParams& P, uint32_t item)
 {
     item = __builtin_amdgcn_readfirstlane(item);
     const uint32_t lane = threadIdx.x & 63u;
@@ -1049,13 +912,14 @@ __device__ __forceinline__ void process_item(const KParams& P, const uint32_t *l
     {
         const ItemCoord ic = item_coord(P, item, lane);
         if (ic.valid)
-            trace_sample<false, TRI, VAR>(P, lds_occ, ic.x, ic.y, ic.s, cr, cg, cb, nullptr, &bailed, item);
+            trace_sample<false, TRI, VAR>(P, ic.x, ic.y, ic.s, cr, cg, cb, nullptr, &bailed, item);
     }
-    const ItemCoord ic = item_coord(P, item, lane);
-    const uint32_t base = lane & ~(P.spp - 1u);
+    const KParams& Q = late_params(P);
+    const ItemCoord ic = item_coord(Q, item, lane);
+    const uint32_t base = lane & ~(Q.spp - 1u);
     float sr = 0.0f, sg = 0.0f, sb = 0.0f;
     bool pixel_bailed = false;
-    for (uint32_t k = 0; k < P.spp; k++)
+    for (uint32_t k = 0; k < Q.spp; k++)
     {
         sr += __shfl(cr, int(base + k), 64);
         sg += __shfl(cg, int(base + k), 64);
@@ -1071,13 +935,13 @@ __device__ __forceinline__ void process_item(const KParams& P, const uint32_t *l
         if (m)
         {
             uint32_t base_q = 0u;
-            if (lane == uint32_t(__builtin_ctzll(m))) base_q = atomicAdd(P.bail_count, uint32_t(__popcll(m)));
+            if (lane == uint32_t(__builtin_ctzll(m))) base_q = atomicAdd(Q.bail_count, uint32_t(__popcll(m)));
             base_q = __shfl(base_q, int(__builtin_ctzll(m)), 64);
             if (enq)
             {
                 const uint32_t r = uint32_t(__builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32),
                                                                       __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u)));
-                P.bail_queue[base_q + r] = (ic.c.k << 8) | ic.p;
+                Q.bail_queue[base_q + r] = (ic.c.k << 8) | ic.p;
             }
         }
         if (pixel_bailed)
@@ -1086,17 +950,17 @@ __device__ __forceinline__ void process_item(const KParams& P, const uint32_t *l
             if (ic.valid && !bailed)
             {
                 const size_t i = 2 * (size_t(item) * 64u + lane);
-                P.bail_state[i] = make_float4(cr, cg, cb, 0.0f);
-                P.bail_state[i + 1] = make_float4(0.0f, 0.0f, __uint_as_float(1u), __uint_as_float(0u));
+                Q.bail_state[i] = make_float4(cr, cg, cb, 0.0f);
+                Q.bail_state[i + 1] = make_float4(0.0f, 0.0f, __uint_as_float(1u), __uint_as_float(0u));
             }
             return;
         }
     }
     if (ic.valid && ic.s == 0)
     {
-        const uint32_t word = rtd::pack_bgra8(rtd::gamma_half(average(P, sr)), rtd::gamma_half(average(P, sg)),
-                                              rtd::gamma_half(average(P, sb)));
-        store_pixel(P, ic.c, ic.p, ic.x, ic.y, word);
+        const uint32_t word = rtd::pack_bgra8(rtd::gamma_half(average(Q, sr)), rtd::gamma_half(average(Q, sg)),
+                                              rtd::gamma_half(average(Q, sb)));
+        store_pixel(Q, ic.c, ic.p, ic.x, ic.y, word);
     }
 }
 
@@ -1118,17 +982,28 @@ __host__ __device__ constexpr uint32_t bail_auto_tests(uint32_t nranks)
 {
     return nranks >= 16u ? 64u : (nranks >= 8u ? 128u : (nranks >= 4u ? 192u : 384u));
 }
-constexpr uint32_t kRowTuneFrames = 4;      // AUTO row-order tuning: frames timed (two per order)
-constexpr float kRowTuneMargin = 0.97f;     // centre-out kept only when >= 3 % faster
-// RT_ROW_TUNE=0 pins AUTO to the plain row order (A/B runs, tools/ab_libs.py)
-static bool row_tune_enabled()
-{
-    static const bool on = [] {
-        const char *e = std::getenv("RT_ROW_TUNE");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
+// Heavy-first order (AUTO): front-section capacity, smallest launch it is used for, and the
+// floor of the heavy threshold in shader cycles (~40 us at 2.4 GHz)
+#ifndef RT_HF_FRONT
+#define RT_HF_FRONT 1024
+#endif
+#ifndef RT_HF_SHIFT
+#define RT_HF_SHIFT 2
+#endif
+#ifndef RT_HF_FLOOR
+#define RT_HF_FLOOR 100000
+#endif
+constexpr uint32_t kHfFrontMax = RT_HF_FRONT;   // blocks (4 waves each): half the chip's wave slots
+constexpr uint32_t kHfMinBlocks = 4096;     // below ~2 rounds of workgroups every block starts early
+constexpr uint32_t kHfFloor = RT_HF_FLOOR;
+constexpr uint32_t kHfShift = RT_HF_SHIFT;  // heavy: cost > last max >> kHfShift; very heavy: >> 1
+constexpr uint32_t kHfPeriod = 4;           // a plan from every 4th frame of a launch shape
+// A plan lists blocks only when the slowest block is a real tail: its cost (one wave's
+// duration) above kHfTail / 16 of the estimated frame span, sum of wave costs / resident waves
+constexpr uint32_t kHfTail = 6;
+constexpr uint32_t kHfSlots = 256u * 4u * 8u;   // resident waves: 256 CUs x 4 SIMDs x 8
+constexpr int kHfCtxs = 4;                  // launch shapes remembered per scene
+
 // Center-out row order (kVarCenterOut): dispatch turn j takes row m, m - 1, m + 1, m - 2, ...
 // (m = R / 2), a bijection on [0, R).  A camera frames its subject, so the dense rows -- whose
 // waves are the launch's longest -- start first instead of mid-launch.
@@ -1154,42 +1029,105 @@ __device__ __forceinline__ uint32_t xcd_band_block(uint32_t b, uint32_t nb, uint
     return (CENTER ? center_out_row(row, full / chunk) : row) * chunk + i % chunk;
 }
 
-// RT_KERNEL_LANES: one lane per sample (spp = 2^spp_shift <= 64), one work item per wave,
-// no LDS (the AUTO kernel).
-template <int TRI, int VAR>
-__global__ void __launch_bounds__(kWG) k_render_lanes(KParams P)
+// Heavy-first planning, after a measured frame's render kernel on its stream: per block the cost
+// of its slowest wave; blocks above max(hf_floor, last max >> kHfShift) are listed for the next
+// frames -- above last max >> 1 at the front of the front section, the rest from its back -- and
+// marked so the natural order skips them.  Nothing is listed when the last measurement showed no
+// tail (its slowest block well under the frame's estimated span).  One thread per block; each
+// workgroup reduces its maximum and sum and reserves its list slots with ONE atomic per level
+// (the render waves themselves touch no atomics: thousands of same-address atomics from waves
+// cost milliseconds, measured).
+__global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks)
 {
-    const uint32_t b = (VAR & kVarXcdBands)
-                           ? xcd_band_block<(VAR & kVarCenterOut) != 0>(blockIdx.x, gridDim.x, P.xcd_chunk)
-                           : blockIdx.x;
-    const uint32_t item = b * (kWG / 64u) + (threadIdx.x >> 6);
-    if (VAR & kVarWaveClock)
+    __shared__ uint32_t s_max, s_hi, s_lo, s_bhi, s_blo;
+    __shared__ unsigned long long s_sum;
+    const uint32_t b = blockIdx.x * kWG + threadIdx.x;
+    if (threadIdx.x == 0u)
     {
-        // debug arm (RT_KERNEL_FLAG_WAVE_CLOCK): s_memtime at the item's start and end, and how
-        // many records the item tested in wave-uniform loops vs lane-loop iterations
-        if ((threadIdx.x & 63u) == 0u)
+        s_max = s_hi = s_lo = 0u;
+        s_sum = 0ull;
+    }
+    __syncthreads();
+    uint32_t cost = 0u, sum = 0u;
+    if (b < nblocks)
+    {
+        const uint4 c = reinterpret_cast<const uint4 *>(P.hf_cost)[b];     // kWavesPerWG == 4
+        cost = max(max(c.x, c.y), max(c.z, c.w));
+        sum = (c.x >> 4) + (c.y >> 4) + (c.z >> 4) + (c.w >> 4);          // in 16-cycle units
+    }
+    const HfPlan last = *P.hf_plan_in;
+    const bool tail = uint64_t(last.maxc) * kHfSlots * 16u > uint64_t(kHfTail) * (last.sum << 4);
+    const uint32_t thr = max(P.hf_floor, last.maxc >> kHfShift);
+    const bool heavy = tail && cost > thr;
+    const bool hi = heavy && cost > (last.maxc >> 1);
+    uint32_t rank = 0u;
+    if (cost) atomicMax(&s_max, cost);
+    if (sum) atomicAdd(&s_sum, (unsigned long long)sum);
+    if (heavy) rank = atomicAdd(hi ? &s_hi : &s_lo, 1u);
+    __syncthreads();
+    if (threadIdx.x == 0u)
+    {
+        if (s_max) atomicMax(&P.hf_plan_out->maxc, s_max);
+        if (s_sum) atomicAdd(&P.hf_plan_out->sum, s_sum);
+        s_bhi = s_hi ? atomicAdd(&P.hf_plan_out->cnt_hi, s_hi) : 0u;
+        s_blo = s_lo ? atomicAdd(&P.hf_plan_out->cnt_lo, s_lo) : 0u;
+    }
+    __syncthreads();
+    if (heavy)
+    {
+        // very heavy blocks fill the front section from its start, the others from its end; a
+        // level that runs into the other is cut (those blocks stay in the natural order)
+        const uint32_t r = (hi ? s_bhi : s_blo) + rank;
+        if (r < P.hf_front)
         {
-            wave_counters()[0] = 0u;
-            wave_counters()[1] = 0u;
-        }
-        wave_lds_sync();
-        const uint64_t t0 = __builtin_amdgcn_s_memtime();
-        process_item<TRI, VAR>(P, nullptr, item);
-        const uint64_t t1 = __builtin_amdgcn_s_memtime();
-        if ((threadIdx.x & 63u) == 0u)
-        {
-            P.wave_clk[4 * size_t(item)] = t0;
-            P.wave_clk[4 * size_t(item) + 1] = t1;
-        }
-        wave_lds_sync();
-        if ((threadIdx.x & 63u) == 0u)
-        {
-            P.wave_clk[4 * size_t(item) + 2] = wave_counters()[0];
-            P.wave_clk[4 * size_t(item) + 3] = wave_counters()[1];
+            const uint32_t slot = hi ? r : P.hf_front - 1u - r;
+            P.hf_list_out[slot] = b;           // may be overwritten by the other level: see below
         }
     }
-    else
-        process_item<TRI, VAR>(P, nullptr, item);
+    // the marks are written by a second pass over the final list (k_hf_mark), so a slot claimed
+    // by both levels marks only the block whose entry survived
+}
+
+// Marks the blocks of the new plan's list (after k_hf_plan): the front section of the frames
+// using it renders exactly the slots [0, cnt_hi) and [front - cnt_lo, front) that do not overlap.
+__global__ void __launch_bounds__(kWG) k_hf_mark(KParams P)
+{
+    const uint32_t j = blockIdx.x * kWG + threadIdx.x;
+    const HfPlan pl = *P.hf_plan_out;
+    const uint32_t hi = min(pl.cnt_hi, P.hf_front);
+    const uint32_t lo = min(pl.cnt_lo, P.hf_front - hi);
+    if (j < P.hf_front && (j < hi || j >= P.hf_front - lo)) P.hf_mark_out[P.hf_list_out[j]] = P.hf_ver + 1u;
+}
+
+// The launch's block -> block-of-work map.  With the heavy-first order on, blocks [0, hf_front)
+// take the blocks listed by the previous frame (in the order their heavy waves finished) and the
+// rest walk the natural (XCD-banded) order, skipping the listed blocks.  Returns false when this
+// block has nothing to do.  The marks read here are never written by this launch (the next
+// frame's marks live in the other buffer), so every wave of a block decides alike.
+template <int VAR>
+__device__ __forceinline__ bool block_of_launch(const KParams& P, uint32_t& b)
+{
+    if (P.hf_front)
+    {
+        if (P.hf_measure && blockIdx.x == 0u && threadIdx.x == 0u)
+            *P.hf_plan_out = HfPlan{0u, 0u, 0u, 0u, 0ull};    // k_hf_plan runs after this kernel
+        const uint32_t front = P.hf_front;
+        if (blockIdx.x < front)
+        {
+            const uint32_t hi = min(P.hf_plan_in->cnt_hi, front);
+            const uint32_t lo = min(P.hf_plan_in->cnt_lo, front - hi);
+            if (blockIdx.x >= hi && blockIdx.x < front - lo) return false;
+            b = P.hf_list_in[blockIdx.x];
+            return true;
+        }
+        const uint32_t q = blockIdx.x - front;
+        const uint32_t nb = gridDim.x - front;
+        b = (VAR & kVarXcdBands) ? xcd_band_block<(VAR & kVarCenterOut) != 0>(q, nb, P.xcd_chunk) : q;
+        return P.hf_ver == 0u || P.hf_mark_in[b] != P.hf_ver;
+    }
+    b = (VAR & kVarXcdBands) ? xcd_band_block<(VAR & kVarCenterOut) != 0>(blockIdx.x, gridDim.x, P.xcd_chunk)
+                             : blockIdx.x;
+    return true;
 }
 
 // RT_KERNEL_WIDE (AUTO's record layout, spp a power of two <= 64 / G): G lanes per sample.
@@ -1235,7 +1173,7 @@ __device__ __forceinline__ void wide_trace(const KParams& P, uint32_t k, uint32_
             float nct0, nct1, nct2, dt0, dt1, dt2;
             int rem0, rem1, rem2, cs0, cs1, cs2, cell;
             bool hit = false;
-            float t = rtd::kFltMax, u = 0.0f, v = 0.0f;
+            float u = 0.0f, v = 0.0f;
             uint32_t tri = 0u;
             if (dda_setup(P, ox, oy, oz, dx, dy, dz, nct0, nct1, nct2, dt0, dt1, dt2, rem0, rem1, rem2, cs0, cs1,
                           cs2, cell))
@@ -1282,14 +1220,16 @@ __device__ __forceinline__ void wide_trace(const KParams& P, uint32_t k, uint32_
                     }
                     if (kb < ke)
                     {
-                        float bt = rtd::kFltMax, bu = 0.0f, bv = 0.0f;
+                        // tb starts at the cell's exit time (test_cell's bound); a lane that takes
+                        // nothing keeps (nct_ax, ~0), which every taken (t < nct_ax, k) beats
+                        float bt = __builtin_fminf(rtd::kFltMax, nct_ax), bu = 0.0f, bv = 0.0f;
                         uint32_t bk = 0xFFFFFFFFu;
                         // record k + G loads while record k is tested: the wide phase runs few,
                         // latency-bound waves, so the extra registers cost no throughput
                         float4 n0, n1, n2;
                         if (kb + sub < ke)
                         {
-                            const float4 *rp = P.frefs + size_t(kb + sub) * 3;
+                            const float4 *rp = P.frefs + size_t(kb + sub) * 3u;
                             n0 = rp[0];
                             n1 = rp[1];
                             n2 = rp[2];
@@ -1299,7 +1239,7 @@ __device__ __forceinline__ void wide_trace(const KParams& P, uint32_t k, uint32_
                             const float4 r0 = n0, r1 = n1, r2 = n2;
                             if (k + uint32_t(G) < ke)
                             {
-                                const float4 *rp = P.frefs + size_t(k + uint32_t(G)) * 3;
+                                const float4 *rp = P.frefs + size_t(k + uint32_t(G)) * 3u;
                                 n0 = rp[0];
                                 n1 = rp[1];
                                 n2 = rp[2];
@@ -1310,9 +1250,9 @@ __device__ __forceinline__ void wide_trace(const KParams& P, uint32_t k, uint32_
                             if (__any(ok1))
                             {
                                 float cv, ct;
-                                const bool h = ok1 & rtd::mt_pre_second(dx, dy, dz, r0.w, r1.x, r1.y, r2.y, r2.z,
-                                                                        r2.w, inv, cu, cv, ct);
-                                const bool take = h & (ct < bt) & (ct < nct_ax);
+                                const bool h = ok1 & rtd::mt_pre_second(dx, dy, dz, r2.y, r2.z, r2.w, r0.w, r1.x, r1.y, inv, cu,
+                                                                        cv, ct);
+                                const bool take = h & (ct < bt);
                                 bt = take ? ct : bt;
                                 bu = take ? cu : bu;
                                 bv = take ? cv : bv;
@@ -1330,9 +1270,8 @@ __device__ __forceinline__ void wide_trace(const KParams& P, uint32_t k, uint32_
                             bv = better ? ov : bv;
                             bk = better ? ok : bk;
                         }
-                        if (bt != rtd::kFltMax)
+                        if (bk != 0xFFFFFFFFu)
                         {
-                            t = bt;
                             u = bu;
                             v = bv;
                             tri = bk;
@@ -1343,15 +1282,15 @@ __device__ __forceinline__ void wide_trace(const KParams& P, uint32_t k, uint32_
                     if (!more) break;
                 }
             }
+            const KParams& Q = P;
             if (hit)
             {
-                tri = __float_as_uint(P.refs[3 * size_t(tri) + 2].y);     // CSR reference -> triangle id
-                const float4 a = P.shade[3 * tri + 0], bb = P.shade[3 * tri + 1], c = P.shade[3 * tri + 2];
+                tri = __float_as_uint(Q.refs[3 * size_t(tri) + 2].y);     // CSR reference -> triangle id
+                const float4 a = Q.shade[3 * tri + 0], bb = Q.shade[3 * tri + 1], c = Q.shade[3 * tri + 2];
                 rtd::shade_hit(u, v, a, bb, c, cr, cg, cb);
             }
             else
-                cr = cg = cb = float(ic.y) / float(P.H);                   // renderer.cpp:159
-            (void)t;
+                cr = cg = cb = float(ic.y) / float(Q.H);                   // renderer.cpp:121
         }
     }
 }
@@ -1383,33 +1322,83 @@ __device__ __forceinline__ void wide_samples(const KParams& P, uint32_t k, uint3
     }
 }
 
-// RT_KERNEL_WIDE: every tile in wide mode (the A/B arm of the hybrid below)
+// RT_KERNEL_LANES / AUTO: one lane per sample (spp = 2^spp_shift <= 64), one work item per
+// wave.  Heavy-first order: see block_of_launch and k_hf_plan.
+template <int TRI, int VAR>
+__global__ void __launch_bounds__(kWG) k_render_lanes(KParams P)
+{
+    __shared__ uint32_t t0s[kWavesPerWG];
+    volatile uint32_t *t0v = t0s;                 // a wave's start time waits in LDS across the walk
+    uint32_t b;
+    if (!block_of_launch<VAR>(P, b)) return;
+    const uint32_t item = b * kWavesPerWG + (threadIdx.x >> 6);
+    if constexpr ((VAR & kVarWaveClock) != 0)
+    {
+        // debug arm (RT_KERNEL_FLAG_WAVE_CLOCK): s_memtime at the item's start and end, and how
+        // many records the item tested in wave-uniform loops vs lane-loop iterations
+        if ((threadIdx.x & 63u) == 0u)
+        {
+            wave_counters()[0] = 0u;
+            wave_counters()[1] = 0u;
+        }
+        wave_lds_sync();
+        const uint64_t t0 = __builtin_amdgcn_s_memtime();
+        process_item<TRI, VAR>(P, item);
+        const uint64_t t1 = __builtin_amdgcn_s_memtime();
+        if ((threadIdx.x & 63u) == 0u)
+        {
+            P.wave_clk[4 * size_t(item)] = t0;
+            P.wave_clk[4 * size_t(item) + 1] = t1;
+        }
+        wave_lds_sync();
+        if ((threadIdx.x & 63u) == 0u)
+        {
+            P.wave_clk[4 * size_t(item) + 2] = wave_counters()[0];
+            P.wave_clk[4 * size_t(item) + 3] = wave_counters()[1];
+        }
+    }
+    else
+    {
+        const bool hf = P.hf_measure != 0u;
+        if (hf && (threadIdx.x & 63u) == 0u) t0v[threadIdx.x >> 6] = uint32_t(__builtin_amdgcn_s_memtime());
+        process_item<TRI, VAR>(P, item);
+        const KParams& Q = late_params(P);
+        if (Q.hf_measure)
+        {
+            const uint32_t t1 = uint32_t(__builtin_amdgcn_s_memtime());
+            const uint32_t t0 = __builtin_amdgcn_readfirstlane(t0v[threadIdx.x >> 6]);
+            if ((threadIdx.x & 63u) == 0u) Q.hf_cost[__builtin_amdgcn_readfirstlane(item)] = t1 - t0;
+        }
+    }
+}
+
+// RT_KERNEL_WIDE: every tile in wide mode (the A/B arm of the two-phase frame)
 template <int VAR, int G>
 __global__ void __launch_bounds__(kWG) k_render_wide(KParams P)
 {
     const uint32_t b = (VAR & kVarXcdBands) ? xcd_band_block(blockIdx.x, gridDim.x, P.xcd_chunk) : blockIdx.x;
-    const uint32_t witem = __builtin_amdgcn_readfirstlane(b * (kWG / 64u) + (threadIdx.x >> 6));
+    const uint32_t witem = __builtin_amdgcn_readfirstlane(b * kWavesPerWG + (threadIdx.x >> 6));
     const uint32_t per_tile = kTilePix * P.spp;                       // sample slots per tile
     const uint32_t g = witem * (64u / uint32_t(G));                   // first slot, launch order
     const uint32_t kseq = g / per_tile;
     wide_samples<VAR, G>(P, P.tile_order ? P.tile_order[kseq] : kseq, g - kseq * per_tile);
 }
 
-// RT_KERNEL_FLAG_BAIL_WIDE, phase 1: the AUTO kernel with the test budget, held to 8 waves/SIMD
+// RT_KERNEL_FLAG_BAIL_WIDE, phase 1: the AUTO kernel with the test budget
 template <int VAR>
 __global__ void __launch_bounds__(kWG) k_render_bail1(KParams P)
 {
     const uint32_t b = (VAR & kVarXcdBands) ? xcd_band_block(blockIdx.x, gridDim.x, P.xcd_chunk) : blockIdx.x;
-    process_item<RT_TRI_MOLLER_TRUMBORE, VAR>(P, nullptr, b * (kWG / 64u) + (threadIdx.x >> 6));
+    process_item<RT_TRI_MOLLER_TRUMBORE, VAR>(P, b * kWavesPerWG + (threadIdx.x >> 6));
 }
 
 // RT_KERNEL_FLAG_BAIL_WIDE, phase 2 (AUTO, spp <= 16).  Phase 1 is the AUTO kernel with a test
 // budget: a sample whose walk would pass bail_tests triangle tests stops, and its pixel goes to
 // bail_queue instead of the frame.  Those are the samples that made the frame's critical path
-// (~1000 serial tests per lane in the densest tiles).  This kernel re-traces the queued pixels
-// from the start in the wide mode: kWideG lanes per sample split every cell's list, so each
-// lane's chain is a quarter long, and the pixel's samples are summed in order as in phase 1.
-// Persistent waves take queue entries round-robin; every pixel is stored by exactly one phase.
+// (~1000 serial tests per lane in the densest tiles).  This kernel resumes the queued pixels'
+// walks in the wide mode: G lanes per sample split every cell's list, so each lane's chain is
+// 1/G as long, and the pixel's samples are summed in order as in phase 1.  Persistent waves take
+// queue entries round-robin; every pixel is stored by exactly one phase.
 template <int VAR, int G>
 __global__ void __launch_bounds__(kWG) k_render_bailed(KParams P)
 {
@@ -1418,8 +1407,8 @@ __global__ void __launch_bounds__(kWG) k_render_bailed(KParams P)
     const uint32_t per_wave = 64u / lpp;
     const uint32_t lane = threadIdx.x & 63u, g = lane / lpp, r = lane - g * lpp;
     const uint32_t smp = r / uint32_t(G), sub = r - smp * uint32_t(G);
-    const uint32_t nwaves = gridDim.x * (kWG / 64u);
-    for (uint32_t e0 = (blockIdx.x * (kWG / 64u) + (threadIdx.x >> 6)) * per_wave; e0 < n; e0 += nwaves * per_wave)
+    const uint32_t nwaves = gridDim.x * kWavesPerWG;
+    for (uint32_t e0 = (blockIdx.x * kWavesPerWG + (threadIdx.x >> 6)) * per_wave; e0 < n; e0 += nwaves * per_wave)
     {
         const uint32_t e = e0 + g;
         const bool live = e < n;
@@ -1446,26 +1435,6 @@ __global__ void __launch_bounds__(kWG) k_render_bailed(KParams P)
     }
 }
 
-// RT_KERNEL_PERSISTENT (spp a power of two <= 64): persistent 512-lane workgroups, 4 per CU.  The
-// 1-bit-per-cell occupancy bitmap (<= 32 KiB for a 64^3 grid) is staged into LDS once per
-// workgroup, so walking an empty cell costs one ds_read instead of a dependent L2 round trip
-// for its CSR offsets.  Waves take work items round-robin (item = wave, wave + nwaves, ...):
-// neighbouring items cost alike, so the static interleave balances without atomics.
-constexpr uint32_t kPersistWG = 512;    // 8 waves; 4 workgroups (128 KiB of bitmaps) per CU
-
-template <int TRI, int VAR>
-__global__ void __launch_bounds__(kPersistWG, 8) k_render_persistent(KParams P, uint32_t n_items)
-{
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds_occ[];
-    for (uint32_t i = threadIdx.x; i < P.occ_words; i += blockDim.x)
-        lds_occ[i] = P.occ[i];
-    __syncthreads();
-    const uint32_t waves_per_wg = blockDim.x >> 6;
-    const uint32_t nwaves = gridDim.x * waves_per_wg;
-    for (uint32_t item = blockIdx.x * waves_per_wg + (threadIdx.x >> 6); item < n_items; item += nwaves)
-        process_item<TRI, VAR>(P, lds_occ, item);
-}
-
 // RT_KERNEL_COMPACT (grid intersector, spp a power of two <= 64): wavefront active-ray
 // compaction.  In the LANES kernel a wave lives until its slowest ray ends, so lanes whose ray
 // already hit (or left the grid) idle through the rest of the walk (~23 % of lane-cycles on
@@ -1482,9 +1451,9 @@ constexpr uint32_t kCompactRefill = 48;          // default: refill when this ma
 
 struct CompactLds
 {
-    float col[kWG / 64u][kCompactSlots][3][64];  // per-sample colours until the item resolves
-    uint32_t left[kWG / 64u][kCompactSlots];     // samples of the slot's item not yet stored
-    uint32_t item[kWG / 64u][kCompactSlots];     // work item held by the slot
+    float col[kWavesPerWG][kCompactSlots][3][64];  // per-sample colours until the item resolves
+    uint32_t left[kWavesPerWG][kCompactSlots];     // samples of the slot's item not yet stored
+    uint32_t item[kWavesPerWG][kCompactSlots];     // work item held by the slot
 };
 
 template <int TRI, int VAR>
@@ -1502,8 +1471,8 @@ k_render_compact(KParams P, uint32_t n_items, uint32_t refill)
     // Items are dealt statically, wave w taking w, w + nwaves, ...: neighbouring items cost
     // alike, so the interleave balances, and a global atomic counter measured 2-4x slower
     // (one device-scope atomic per item serialises at the memory side).
-    const uint32_t nwaves = gridDim.x * (kWG / 64u);
-    uint32_t next_item = blockIdx.x * (kWG / 64u) + wv;
+    const uint32_t nwaves = gridDim.x * kWavesPerWG;
+    uint32_t next_item = blockIdx.x * kWavesPerWG + wv;
     const uint32_t walk_min = 64u - refill;
     // lane state: 0 idle, 1 walking, 2 finished (colour not yet stored)
     uint32_t state = 0u, tag = 0u;
@@ -1514,7 +1483,7 @@ k_render_compact(KParams P, uint32_t n_items, uint32_t refill)
     int rem0 = 0, rem1 = 0, rem2 = 0, cs0 = 0, cs1 = 0, cs2 = 0, cell = 0, skip = 0;
     for (;;)
     {
-        // (1) store the colours of finished samples (renderer.cpp:147-159)
+        // (1) store the colours of finished samples (renderer.cpp:107-121)
         if (state == 2u)
         {
             const uint32_t slot = tag >> 6, j = tag & 63u;
@@ -1530,7 +1499,7 @@ k_render_compact(KParams P, uint32_t n_items, uint32_t refill)
                     rtd::shade_hit(u, v, a, b, c, cr, cg, cb);
                 }
                 else
-                    cr = cg = cb = float(ic.y) / float(P.H);                    // renderer.cpp:159
+                    cr = cg = cb = float(ic.y) / float(P.H);                    // renderer.cpp:121
             }
             L.col[wv][slot][0][j] = cr;
             L.col[wv][slot][1][j] = cg;
@@ -1539,7 +1508,7 @@ k_render_compact(KParams P, uint32_t n_items, uint32_t refill)
             state = 0u;
         }
         wave_lds_sync();
-        // (2) resolve items whose 64 samples are all stored (renderer.cpp:162-171)
+        // (2) resolve items whose 64 samples are all stored (renderer.cpp:124-133)
         uint64_t ready = __ballot(lane < kCompactSlots && ((busy >> lane) & 1u) &&
                                   __hip_atomic_load(&L.left[wv][lane < kCompactSlots ? lane : 0u], __ATOMIC_RELAXED,
                                                     __HIP_MEMORY_SCOPE_WORKGROUP) == 0u);
@@ -1684,9 +1653,6 @@ k_render_compact(KParams P, uint32_t n_items, uint32_t refill)
 template <int TRI, int VAR>
 __global__ void __launch_bounds__(kWG) k_render_pixel_loop(KParams P)
 {
-    const uint32_t *lds_occ = nullptr;
-    const bool use_occ = false;
-
     const TileCoord c = tile_of_block(P);
     const uint32_t p = threadIdx.x;
     const uint32_t x = c.tx0 + compact_bits(p), y = c.ty0 + compact_bits(p >> 1);
@@ -1695,7 +1661,7 @@ __global__ void __launch_bounds__(kWG) k_render_pixel_loop(KParams P)
     for (uint32_t s = 0; s < P.spp; s++)
     {
         float cr, cg, cb;
-        trace_sample<false, TRI, VAR>(P, use_occ ? lds_occ : nullptr, x, y, s, cr, cg, cb, nullptr);
+        trace_sample<false, TRI, VAR>(P, x, y, s, cr, cg, cb, nullptr);
         sr += cr; sg += cg; sb += cb;
     }
     store_pixel(P, c, p, x, y, rtd::pack_bgra8(rtd::gamma_half(average(P, sr)), rtd::gamma_half(average(P, sg)),
@@ -1710,20 +1676,18 @@ __global__ void __launch_bounds__(kWG) k_trace_records(KParams P, uint32_t n)
     const uint32_t s = i % P.spp, pix = i / P.spp;
     const uint32_t x = P.rec_x0 + pix % P.rec_w, y = P.rec_y0 + pix / P.rec_w;
     float cr, cg, cb;
-    // Records walk the production traversal (wave gate + distance skipping) so the per-sample
-    // parity tests (hit, tri, voxel, steps, tests) cover exactly the code the frames use.
+    // Records walk the distance-skipping traversal with the wave-gated test, so the per-sample
+    // parity tests (hit, tri, voxel, steps, tests) cover the walk the frames take.
     if (P.isect == RT_ISECT_RAY_MARCH)
-        trace_sample<true, RT_TRI_MOLLER_TRUMBORE, kVarMarch>(P, nullptr, x, y, s, cr, cg, cb, &P.recs[i]);
+        trace_sample<true, RT_TRI_MOLLER_TRUMBORE, kVarMarch>(P, x, y, s, cr, cg, cb, &P.recs[i]);
     else if (P.isect == RT_ISECT_RAY_MARCH + 0x100)   // exhaustive arm (RT_KERNEL_FLAG_EXHAUSTIVE)
-        trace_sample<true, RT_TRI_MOLLER_TRUMBORE, kVarMarch | kVarExhaustive>(P, nullptr, x, y, s, cr, cg, cb,
-                                                                              &P.recs[i]);
+        trace_sample<true, RT_TRI_MOLLER_TRUMBORE, kVarMarch | kVarExhaustive>(P, x, y, s, cr, cg, cb, &P.recs[i]);
     else if (P.isect == RT_ISECT_BRUTE_FORCE)
-        trace_sample<true, RT_TRI_MOLLER_TRUMBORE, kVarBrute>(P, nullptr, x, y, s, cr, cg, cb, &P.recs[i]);
+        trace_sample<true, RT_TRI_MOLLER_TRUMBORE, kVarBrute>(P, x, y, s, cr, cg, cb, &P.recs[i]);
     else if (P.tri_test == RT_TRI_BARYCENTRIC)
-        trace_sample<true, RT_TRI_BARYCENTRIC, kVarDistSkip>(P, nullptr, x, y, s, cr, cg, cb, &P.recs[i]);
+        trace_sample<true, RT_TRI_BARYCENTRIC, kVarDistSkip>(P, x, y, s, cr, cg, cb, &P.recs[i]);
     else
-        trace_sample<true, RT_TRI_MOLLER_TRUMBORE, kVarWaveGate | kVarDistSkip>(P, nullptr, x, y, s, cr, cg, cb,
-                                                                              &P.recs[i]);
+        trace_sample<true, RT_TRI_MOLLER_TRUMBORE, kVarWaveGate | kVarDistSkip>(P, x, y, s, cr, cg, cb, &P.recs[i]);
 }
 
 // K3: gathered shards [rank][local tile][256] -> frame
@@ -1738,21 +1702,19 @@ __global__ void __launch_bounds__(kWG) k_unshard(const uint32_t *g, uint32_t *ou
     out[size_t(y) * W + x] = g[r * shard_elems + size_t(k) * kTilePix + (y % kTile) * kTile + (x % kTile)];
 }
 
-// Per-frame records of the origin-shared Moller-Trumbore terms (kVarOriginPre): for CSR
-// reference k, tvec = o - v0 and qvec = tvec x e1 exactly as triangle.h:71, 87 compute them.
+// Per-camera-origin records (kVarOriginPre): for CSR reference k, tvec = o - v0,
+// qvec = tvec x e1 and tdot = e2 . qvec exactly as triangle.h:82, 90, 98 compute them.
 __global__ void __launch_bounds__(kWG) k_origin_pre(const float4 *refs, float4 *frefs, uint32_t n, float ox,
                                                     float oy, float oz)
 {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n) return;
     const float4 r0 = refs[3 * size_t(k)], r1 = refs[3 * size_t(k) + 1], r2 = refs[3 * size_t(k) + 2];
-    const float e1x = r0.w, e1y = r1.x, e1z = r1.y;
-    const float tx = ox - r0.x, ty = oy - r0.y, tz = oz - r0.z;
-    const float qx = ty * e1z - tz * e1y;
-    const float qy = tz * e1x - tx * e1z;
-    const float qz = tx * e1y - ty * e1x;
-    frefs[3 * size_t(k) + 0] = make_float4(e1x, e1y, e1z, r1.z);
-    frefs[3 * size_t(k) + 1] = make_float4(r1.w, r2.x, tx, ty);
+    const float e1x = r0.w, e1y = r1.x, e1z = r1.y, e2x = r1.z, e2y = r1.w, e2z = r2.x;
+    float tx, ty, tz, qx, qy, qz;
+    rtd::origin_terms(ox, oy, oz, r0.x, r0.y, r0.z, e1x, e1y, e1z, tx, ty, tz, qx, qy, qz);
+    frefs[3 * size_t(k) + 0] = make_float4(e1x, e1y, e1z, e2x);
+    frefs[3 * size_t(k) + 1] = make_float4(e2y, e2z, tx, ty);
     frefs[3 * size_t(k) + 2] = make_float4(tz, qx, qy, qz);
 }
 
@@ -1791,19 +1753,21 @@ __global__ void __launch_bounds__(kWG) k_primitives(int kind, const float *in, u
                                           e1x, e1y, e1z, e2x, e2y, e2z, a[15], a[16], a[17], bt, bu, bv);
         o[4] = __uint_as_float(hb); o[5] = bt; o[6] = bu; o[7] = bv;
     }
-    else if (kind == 6)   // pre-gated + gated variants (wave-uniform exits): hit flag + t,u,v on hits
-    {
+    else if (kind == 6)   // the wave-gated forms (64 records per wave, so the exits really fire):
+    {                     // gated MT, and the per-camera-record form with the Newton 1/det
         const float *a = in + 18 * i;
         float *o = out + 8 * i;
         const float e1x = a[9] - a[6], e1y = a[10] - a[7], e1z = a[11] - a[8];
         const float e2x = a[12] - a[6], e2y = a[13] - a[7], e2z = a[14] - a[8];
-        float t = 0, u = 0, v = 0, gt = 0, gu = 0, gv = 0;
-        const bool h = rtd::ray_tri_mt_pregated(a[0], a[1], a[2], a[3], a[4], a[5], a[6], a[7], a[8],
-                                                e1x, e1y, e1z, e2x, e2y, e2z, t, u, v);
+        float t = 0, u = 0, v = 0, pt = 0, pu = 0, pv = 0;
         const bool hg = rtd::ray_tri_mt_gated(a[0], a[1], a[2], a[3], a[4], a[5], a[6], a[7], a[8],
-                                              e1x, e1y, e1z, e2x, e2y, e2z, gt, gu, gv);
-        o[0] = __uint_as_float(h); o[1] = t; o[2] = u; o[3] = v;
-        o[4] = __uint_as_float(hg); o[5] = gt; o[6] = gu; o[7] = gv;
+                                              e1x, e1y, e1z, e2x, e2y, e2z, t, u, v);
+        float tx, ty, tz, qx, qy, qz;
+        rtd::origin_terms(a[0], a[1], a[2], a[6], a[7], a[8], e1x, e1y, e1z, tx, ty, tz, qx, qy, qz);
+        const bool hp = rtd::ray_tri_mt_gated_pre<true>(a[3], a[4], a[5], e1x, e1y, e1z, e2x, e2y, e2z, tx, ty, tz,
+                                                        qx, qy, qz, pt, pu, pv);
+        o[0] = __uint_as_float(hg); o[1] = t; o[2] = u; o[3] = v;
+        o[4] = __uint_as_float(hp); o[5] = pt; o[6] = pu; o[7] = pv;
     }
     else if (kind == 5)   // branch-free traversal variants: hit flag + t,u,v (hits only)
     {
@@ -1869,7 +1833,7 @@ __global__ void __launch_bounds__(kWG) k_primitives(int kind, const float *in, u
 }
 
 // ------------------------------------------------------------------------ host side
-// sampling.h:113-120, sampling.cpp:194-210 (base 2), renderer.cpp:90-93
+// sampling.h:113-120, sampling.cpp:194-210 (base 2), renderer.cpp:52-55
 void hammersley(uint32_t spp, std::vector<float>& xy)
 {
     xy.resize(size_t(spp) * 2);
@@ -1922,6 +1886,21 @@ void dist_record(const float *p0, const float *p1, const float *p2, float4 *r)
     r[5] = make_float4(d11, inv_denom, dot_ref(e12, e12), 0.0f);
 }
 
+// Heavy-first state of one launch shape (device arrays; see KParams::hf_*)
+struct HfCtx
+{
+    uint64_t key[4] = { 0, 0, 0, 0 };   // launch shape: blocks, spp, region, shard, variant
+    uint32_t nblocks = 0, front = 0;
+    uint32_t cap_blocks = 0;            // allocated marks per buffer
+    uint32_t *marks = nullptr;          // [2][cap_blocks]
+    uint32_t *cost = nullptr;           // [cap_blocks * kWavesPerWG] wave cycles of the last frame
+    uint32_t *lists = nullptr;          // [2][kHfFrontMax], by plan version parity
+    HfPlan *plans = nullptr;            // [2], by plan version parity
+    uint32_t frames = 0;                // frames rendered with this shape
+    uint32_t ver = 0;                   // version of the newest plan launched
+    uint64_t used = 0;                  // LRU stamp
+};
+
 } // namespace
 
 struct rt_scene
@@ -1930,18 +1909,20 @@ struct rt_scene
     std::mutex mtx;
     uint32_t dims[3] = { 0, 0, 0 };
     float bmin[3], bmax[3], cw = 0, icw = 0;
-    uint32_t ncells = 0, nrefs = 0, ntris = 0, occ_words = 0, max_cell_refs = 0;
-    uint32_t *d_off = nullptr, *d_occ = nullptr, *d_cellw = nullptr;
+    uint32_t ncells = 0, nrefs = 0, ntris = 0, max_cell_refs = 0;
+    uint32_t *d_off = nullptr, *d_cellw = nullptr;
     float4 *d_refs = nullptr, *d_shade = nullptr, *d_facen = nullptr, *d_frefs = nullptr;
     float4 *d_trimt = nullptr, *d_tridist = nullptr, *d_distblk = nullptr;
     uint32_t ndist_blk = 0;
     float scene_scale = 0.0f;
     float vmin[3] = { 0, 0, 0 }, vmax[3] = { 0, 0, 0 };
     uint64_t device_bytes = 0;
-    uint32_t persist_wgs = 1024;    // persistent grid: 4 x 512-lane workgroups per CU
     uint32_t compact_wgs = 2048;    // RT_KERNEL_COMPACT grid: 8 x 256-lane workgroups per CU
     bool rcp_safe = false;          // every |det| of the ray/tri test is far below 2^126 (FAST_RCP)
     bool pack_ok = false;           // dims <= 512: the remaining-cell counts pack into one word
+    // frefs hold the per-reference terms of this camera origin (bit patterns; valid once computed)
+    bool fref_valid = false;
+    uint32_t fref_org[3] = { 0, 0, 0 };
     uint32_t *d_bail = nullptr;     // RT_KERNEL_FLAG_BAIL_WIDE: queued-pixel count + queue
     size_t bail_cap = 0;
     float4 *d_bail_state = nullptr; // RT_KERNEL_FLAG_BAIL_WIDE: phase 1 -> phase 2 per-sample state
@@ -1950,6 +1931,9 @@ struct rt_scene
     uint64_t *d_clk = nullptr;      // RT_KERNEL_FLAG_WAVE_CLOCK records of the last such launch
     size_t clk_cap = 0;
     uint32_t clk_items = 0;
+    // AUTO heavy-first order: per launch shape, which blocks the previous frame found heavy
+    HfCtx hf[kHfCtxs];
+    uint64_t hf_clock = 0;
     // sample table cache
     float2 *d_smp = nullptr;
     uint32_t smp_cap = 0;
@@ -1960,13 +1944,6 @@ struct rt_scene
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool ev_recorded = false;
     hipStream_t last_stream = nullptr;  // stream of the last launch (cross-stream ordering)
-    // AUTO's row order at one rank, chosen per scene and launch shape from its own first frames
-    // (calls 0..3 alternate plain / centre-out; both orders give identical pixels)
-    uint64_t row_key = 0;        // (blocks, spp) the choice was made for
-    uint32_t row_calls = 0;      // tuning frames launched for row_key
-    int row_pending = -1;        // order of the frame ev0/ev1 bracket, not yet read
-    int row_choice = -1;         // 0 plain, 1 centre-out, -1 still tuning
-    float row_best[2] = {0.f, 0.f};
     // staging for rt_render_tiles / records
     uint32_t *d_frame = nullptr;
     size_t frame_cap = 0;
@@ -2010,6 +1987,10 @@ int prepare_samples(rt_scene *s, const rt_frame *f, uint32_t spp)
     return RT_OK;
 }
 
+constexpr uint32_t kKernelFlags = RT_KERNEL_FLAG_CENTER_OUT | RT_KERNEL_FLAG_STATIC_ORDER | RT_KERNEL_FLAG_WIDE16 |
+                                  RT_KERNEL_FLAG_LDS_CELLS | RT_KERNEL_FLAG_EXHAUSTIVE | RT_KERNEL_FLAG_WAVE_CLOCK |
+                                  RT_KERNEL_FLAG_BAIL_WIDE | RT_KERNEL_BUDGET_MASK;
+
 int validate_frame(const rt_frame *f)
 {
     if (!f) return fail(RT_E_INVALID, "frame is NULL");
@@ -2019,24 +2000,14 @@ int validate_frame(const rt_frame *f)
     if (f->intersector > RT_ISECT_RAY_MARCH) return fail(RT_E_INVALID, "unknown intersector");
     if (f->intersector == RT_ISECT_BRUTE_FORCE && f->tri_test != RT_TRI_MOLLER_TRUMBORE)
         return fail(RT_E_INVALID, "IntersectBruteForce uses IntersectRayTri only (renderer.cpp:176)");
-    if ((f->kernel & RT_KERNEL_KIND_MASK) > RT_KERNEL_WIDE ||
-        (f->kernel & ~(RT_KERNEL_KIND_MASK | RT_KERNEL_FLAG_LDS_CELLS | RT_KERNEL_FLAG_WIDE16 |
-                       RT_KERNEL_FLAG_ALT_LOADS | RT_KERNEL_FLAG_CENTER_OUT | RT_KERNEL_FLAG_EARLY_LOAD | RT_KERNEL_FLAG_PREFETCH | RT_KERNEL_FLAG_WAVE_GATE | RT_KERNEL_FLAG_SKIP_RUN |
-                       RT_KERNEL_FLAG_CSR_OFFSETS | RT_KERNEL_FLAG_DIST_SKIP | RT_KERNEL_FLAG_NESTED_STEP |
-                       RT_KERNEL_FLAG_PRE_GATE | RT_KERNEL_FLAG_EXHAUSTIVE | RT_KERNEL_FLAG_ORIGIN_PRE |
-                       RT_KERNEL_FLAG_SELECT_STEP | RT_KERNEL_FLAG_FAST_RCP | RT_KERNEL_FLAG_PACKED_REM |
-                       RT_KERNEL_FLAG_XCD_BANDS | RT_KERNEL_FLAG_UNROLL_PAIRS | RT_KERNEL_FLAG_WAVE_CLOCK |
-                       RT_KERNEL_FLAG_UNIFORM_CELLS | RT_KERNEL_FLAG_BAIL_WIDE |
-                       RT_KERNEL_COMPACT_REFILL_MASK)))
+    const uint32_t kind = f->kernel & RT_KERNEL_KIND_MASK;
+    if (kind > RT_KERNEL_WIDE || kind == 4u || (f->kernel & ~(RT_KERNEL_KIND_MASK | kKernelFlags)))
         return fail(RT_E_INVALID, "unknown kernel");
     const uint32_t spp = std::max(1u, f->spp);
     if (spp > 4096) return fail(RT_E_INVALID, "spp must be <= 4096");
-    if ((f->kernel & RT_KERNEL_KIND_MASK) == RT_KERNEL_COMPACT &&
-        ((f->kernel & RT_KERNEL_COMPACT_REFILL_MASK) >> RT_KERNEL_COMPACT_REFILL_SHIFT) > 64u)
+    if (kind == RT_KERNEL_COMPACT && ((f->kernel & RT_KERNEL_BUDGET_MASK) >> RT_KERNEL_BUDGET_SHIFT) > 64u)
         return fail(RT_E_INVALID, "compaction refill threshold must be <= 64 lanes");
-    if (((f->kernel & RT_KERNEL_KIND_MASK) == RT_KERNEL_LANES || (f->kernel & RT_KERNEL_KIND_MASK) == RT_KERNEL_PERSISTENT ||
-         (f->kernel & RT_KERNEL_KIND_MASK) == RT_KERNEL_COMPACT) &&
-        !(is_pow2(spp) && spp <= 64))
+    if ((kind == RT_KERNEL_LANES || kind == RT_KERNEL_COMPACT) && !(is_pow2(spp) && spp <= 64))
         return fail(RT_E_INVALID, "RT_KERNEL_LANES needs spp to be a power of two <= 64");
     return RT_OK;
 }
@@ -2069,14 +2040,12 @@ void frame_params(const rt_scene *s, const rt_frame *f, KParams& P)
     P.icw = s->icw;
     P.dxdz = int(s->dims[0] * s->dims[2]);
     P.max_steps = s->dims[0] + s->dims[1] + s->dims[2] + 3;
-    P.occ_words = s->occ_words <= kMaxOccWords ? s->occ_words : 0;
     P.off = s->d_off;
-    P.cellw = (f->kernel & RT_KERNEL_FLAG_CSR_OFFSETS) ? nullptr : s->d_cellw;
+    P.cellw = s->d_cellw;
     P.refs = s->d_refs;
     P.frefs = s->d_frefs;
     P.shade = s->d_shade;
     P.face_n = s->d_facen;
-    P.occ = s->d_occ;
     P.tri_mt = s->d_trimt;
     P.tri_dist = s->d_tridist;
     P.dist_blk = s->d_distblk;
@@ -2090,19 +2059,113 @@ void frame_params(const rt_scene *s, const rt_frame *f, KParams& P)
     P.ntris = s->ntris;
     P.tri_test = f->tri_test;
     P.isect = f->intersector;
-    P.tile_order = nullptr;
-    P.bail_tests = 0;
-    P.bail_count = nullptr;
-    P.bail_queue = nullptr;
-    P.bail_state = nullptr;
-    P.wave_clk = nullptr;
-    P.xcd_chunk = 0;
 }
 
 bool use_lanes(const rt_frame *f, uint32_t spp)
 {
     if ((f->kernel & RT_KERNEL_KIND_MASK) == RT_KERNEL_PIXEL_LOOP) return false;
     return is_pow2(spp) && spp <= 64;
+}
+
+// The per-reference origin terms for this frame's camera origin: computed when the origin
+// differs from the one the records hold (a moving camera pays one small launch per frame).
+int ensure_origin_terms(rt_scene *s, const KParams& P, hipStream_t st)
+{
+    uint32_t ob[3];
+    std::memcpy(ob, P.org, sizeof(ob));
+    if (s->fref_valid && std::memcmp(ob, s->fref_org, sizeof(ob)) == 0) return RT_OK;
+    if (s->nrefs)
+        hipLaunchKernelGGL(k_origin_pre, dim3((s->nrefs + kWG - 1) / kWG), dim3(kWG), 0, st, s->d_refs, s->d_frefs,
+                           s->nrefs, P.org[0], P.org[1], P.org[2]);
+    RT_HIP(hipGetLastError());
+    std::memcpy(s->fref_org, ob, sizeof(ob));
+    s->fref_valid = true;
+    return RT_OK;
+}
+
+// Heavy-first state for this launch shape (AUTO): fills P.hf_*.  A new shape takes the least
+// recently used context and clears it on the launch stream (no host synchronisation).
+int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, hipStream_t st)
+{
+    const uint64_t key[4] = { (blocks << 16) | (uint64_t(P.spp) << 1) | 1u,
+                              (uint64_t(P.rx0) << 32) | P.ry0, (uint64_t(P.rw) << 32) | P.rh,
+                              (uint64_t(P.rank) << 40) | (uint64_t(P.nranks) << 20) | uint64_t(uint32_t(var) >> 12) };
+    HfCtx *c = nullptr;
+    for (HfCtx& h : s->hf)
+        if (std::memcmp(h.key, key, sizeof(key)) == 0) c = &h;
+    if (!c)
+    {
+        c = &s->hf[0];
+        for (HfCtx& h : s->hf)
+            if (h.used < c->used) c = &h;
+        if (blocks > c->cap_blocks || !c->lists)
+        {
+            if (c->marks) RT_HIP(hipFree(c->marks));
+            if (c->cost) RT_HIP(hipFree(c->cost));
+            c->marks = c->cost = nullptr;
+            RT_HIP(hipMalloc(&c->marks, sizeof(uint32_t) * 2 * blocks));
+            RT_HIP(hipMalloc(&c->cost, sizeof(uint32_t) * kWavesPerWG * blocks));
+            c->cap_blocks = uint32_t(blocks);
+            if (!c->lists)
+            {
+                RT_HIP(hipMalloc(&c->lists, sizeof(uint32_t) * 2 * kHfFrontMax));
+                RT_HIP(hipMalloc(&c->plans, sizeof(HfPlan) * 2));
+            }
+        }
+        RT_HIP(hipMemsetAsync(c->marks, 0, sizeof(uint32_t) * 2 * c->cap_blocks, st));
+        RT_HIP(hipMemsetAsync(c->plans, 0, sizeof(HfPlan) * 2, st));
+        std::memcpy(c->key, key, sizeof(key));
+        c->nblocks = uint32_t(blocks);
+        // front: an eighth of the blocks, capped, a multiple of the XCD count so the natural
+        // section keeps its block -> XCD assignment
+        c->front = std::min<uint32_t>(kHfFrontMax, uint32_t(blocks / 8u) & ~(kXcds - 1u));
+        c->frames = 0;
+        c->ver = 0;
+    }
+    c->used = ++s->hf_clock;
+    const uint32_t v = c->ver;
+    P.hf_front = c->front;
+    P.hf_ver = v;
+    // measured: the first two frames (the first plan has no earlier maximum to test a tail
+    // against, so it lists nothing) and then every kHfPeriod-th
+    P.hf_measure = c->frames < 2u || c->frames % kHfPeriod == 0u;
+    c->frames++;
+    P.hf_floor = kHfFloor;
+    P.hf_mark_in = c->marks + size_t(v & 1u) * c->cap_blocks;
+    P.hf_mark_out = c->marks + size_t((v + 1u) & 1u) * c->cap_blocks;
+    P.hf_list_in = c->lists + size_t(v & 1u) * kHfFrontMax;
+    P.hf_list_out = c->lists + size_t((v + 1u) & 1u) * kHfFrontMax;
+    P.hf_plan_in = c->plans + (v & 1u);
+    P.hf_plan_out = c->plans + ((v + 1u) & 1u);
+    P.hf_cost = c->cost;
+    if (P.hf_measure) c->ver = v + 1u;                  // the plan launched after this frame
+    return RT_OK;
+}
+
+typedef void (*kfn_t)(KParams);
+
+// k_render_lanes instantiation of a variant (nullptr: not built)
+kfn_t lanes_kernel(int tri, int var)
+{
+    if (tri == RT_TRI_BARYCENTRIC) return var == 0 ? k_render_lanes<RT_TRI_BARYCENTRIC, 0> : nullptr;
+    switch (var)
+    {
+    case 0: return k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 0>;
+    case kVarMarch: return k_render_lanes<RT_TRI_MOLLER_TRUMBORE, kVarMarch>;
+    case kVarMarch | kVarExhaustive: return k_render_lanes<RT_TRI_MOLLER_TRUMBORE, kVarMarch | kVarExhaustive>;
+    case kVarBrute: return k_render_lanes<RT_TRI_MOLLER_TRUMBORE, kVarBrute>;
+    case kVarAuto: return k_render_lanes<RT_TRI_MOLLER_TRUMBORE, kVarAuto>;
+    case kVarAutoCore | kVarPackedRem | kVarSkipRun:
+        return k_render_lanes<RT_TRI_MOLLER_TRUMBORE, kVarAutoCore | kVarPackedRem | kVarSkipRun>;
+    case kVarAutoCore | kVarFastRcp: return k_render_lanes<RT_TRI_MOLLER_TRUMBORE, kVarAutoCore | kVarFastRcp>;
+    case kVarAutoCore: return k_render_lanes<RT_TRI_MOLLER_TRUMBORE, kVarAutoCore>;
+    case kVarAuto | kVarCenterOut: return k_render_lanes<RT_TRI_MOLLER_TRUMBORE, kVarAuto | kVarCenterOut>;
+    case kVarAuto | kVarWaveClock: return k_render_lanes<RT_TRI_MOLLER_TRUMBORE, kVarAuto | kVarWaveClock>;
+    case kVarAuto | kVarLdsCells: return k_render_lanes<RT_TRI_MOLLER_TRUMBORE, kVarAuto | kVarLdsCells>;
+    case kVarAuto | kVarLdsCells | kVarWaveClock:
+        return k_render_lanes<RT_TRI_MOLLER_TRUMBORE, kVarAuto | kVarLdsCells | kVarWaveClock>;
+    default: return nullptr;
+    }
 }
 
 // Launches the render kernel over region/shard described by P (tiles_x, rank, ...).
@@ -2114,92 +2177,40 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
     if (P.wg_per_tile == 0) P.wg_per_tile = 1;
     const uint64_t blocks = uint64_t(n_local_tiles) * P.wg_per_tile;
     if (blocks > 0x3FFFFFFFull) return fail(RT_E_INVALID, "frame too large for one launch");
-    // The per-frame records (frefs) are scene state: a launch on another stream than the last
+    const uint32_t kind = f->kernel & RT_KERNEL_KIND_MASK;
+    const bool bary = P.tri_test == RT_TRI_BARYCENTRIC;
+    const bool grid_mt = P.isect == RT_ISECT_GRID && !bary;
+    // The per-camera records (frefs) are scene state: a launch on another stream than the last
     // one waits for it, so frames of one scene never overlap on the device.
     if (s->ev_recorded && st != s->last_stream) RT_HIP(hipStreamWaitEvent(st, s->ev1, 0));
     s->last_stream = st;
-    if (s->row_pending >= 0)
-    {
-        // a tuning frame's time (host waits only during the first few frames of a launch shape)
-        float ms = 0.f;
-        RT_HIP(hipEventSynchronize(s->ev1));
-        RT_HIP(hipEventElapsedTime(&ms, s->ev0, s->ev1));
-        float &best = s->row_best[s->row_pending];
-        if (best == 0.f || ms < best) best = ms;
-        s->row_pending = -1;
-        if (s->row_calls >= kRowTuneFrames)
-            s->row_choice = s->row_best[1] < kRowTuneMargin * s->row_best[0] ? 1 : 0;
-    }
-    RT_HIP(hipEventRecord(s->ev0, st));
-    const uint32_t kind = f->kernel & RT_KERNEL_KIND_MASK;
     // kVarXcdBands turn size: one row of this launch's tiles (ceil(tiles_x / nranks) local tiles
     // span a full frame row in shard mode).  Measured best of 1/4 .. 4 rows and 1..16 tiles:
     // whole rows interleave over the XCDs, so each L2 sees compact rows AND the frame's cost
     // spreads evenly (half rows put every left half on the even XCDs).
     P.xcd_chunk = ((P.tiles_x + P.nranks - 1u) / P.nranks) * P.wg_per_tile;
-    // RT_KERNEL_AUTO = lanes + wave gate + distance skip + per-frame origin terms + Newton
-    // reciprocal + packed remaining-cell counts (the last two where the scene allows them) +
-    // XCD row interleave: fastest arm of tools/ab_kernels.py on MI355X (scenes 1/2/4/5/7/8,
-    // 1080p x 4spp).  RT_KERNEL_COMPACT runs the same per-ray code as AUTO.
-    const uint32_t fk = (kind == RT_KERNEL_AUTO || kind == RT_KERNEL_COMPACT || kind == RT_KERNEL_WIDE)
-                            ? (f->kernel | RT_KERNEL_LANES | RT_KERNEL_FLAG_WAVE_GATE | RT_KERNEL_FLAG_DIST_SKIP |
-                               RT_KERNEL_FLAG_ORIGIN_PRE | RT_KERNEL_FLAG_FAST_RCP | RT_KERNEL_FLAG_PACKED_REM |
-                               RT_KERNEL_FLAG_XCD_BANDS | RT_KERNEL_FLAG_UNIFORM_CELLS | RT_KERNEL_FLAG_SKIP_RUN)
-                            : f->kernel;
-    if ((fk & RT_KERNEL_FLAG_ORIGIN_PRE) && lanes && P.isect == RT_ISECT_GRID &&
-        P.tri_test == RT_TRI_MOLLER_TRUMBORE && s->nrefs)
-        hipLaunchKernelGGL(k_origin_pre, dim3((s->nrefs + kWG - 1) / kWG), dim3(kWG), 0, st, s->d_refs, s->d_frefs,
-                           s->nrefs, P.org[0], P.org[1], P.org[2]);
-    int var = ((fk & RT_KERNEL_FLAG_PREFETCH) ? kVarPrefetch : 0) |
-                    ((fk & RT_KERNEL_FLAG_WAVE_GATE) ? kVarWaveGate : 0) |
-                    ((fk & RT_KERNEL_FLAG_SKIP_RUN) ? kVarSkipRun : 0) |
-                    ((fk & RT_KERNEL_FLAG_DIST_SKIP) ? kVarDistSkip : 0) |
-                    ((fk & RT_KERNEL_FLAG_NESTED_STEP) ? kVarNestedStep : 0) |
-                    ((fk & RT_KERNEL_FLAG_PRE_GATE) ? kVarPreGate : 0) |
-                    ((fk & RT_KERNEL_FLAG_ORIGIN_PRE) ? kVarOriginPre : 0) |
-                    ((fk & RT_KERNEL_FLAG_SELECT_STEP) ? kVarSelStep : 0) |
-                    ((fk & RT_KERNEL_FLAG_FAST_RCP) && s->rcp_safe ? kVarFastRcp : 0) |
-                    ((fk & RT_KERNEL_FLAG_PACKED_REM) && s->pack_ok ? kVarPackedRem : 0) |
-                    ((fk & RT_KERNEL_FLAG_XCD_BANDS) ? kVarXcdBands : 0) |
-                    ((fk & RT_KERNEL_FLAG_UNROLL_PAIRS) ? kVarUnroll : 0) |
-                    ((fk & RT_KERNEL_FLAG_WAVE_CLOCK) ? kVarWaveClock : 0) |
-                    ((fk & RT_KERNEL_FLAG_UNIFORM_CELLS) ? kVarUniform : 0) |
-                    ((fk & RT_KERNEL_FLAG_LDS_CELLS) ? kVarLdsCells : 0) |
-                    ((fk & RT_KERNEL_FLAG_ALT_LOADS) ? kVarAltLoads : 0) |
-                    ((fk & RT_KERNEL_FLAG_CENTER_OUT) ? kVarCenterOut : 0) |
-                    ((fk & RT_KERNEL_FLAG_EARLY_LOAD) ? kVarEarlyLoad : 0);
-    // the wave-uniform empty run needs the packed counts (scenes with a grid dimension > 512
-    // walk without it)
-    if (!(var & kVarPackedRem)) var &= ~kVarSkipRun;
-    // AUTO at one rank: centre-out row turns cut killeroo's tail ~6 % but cost Cornell +6 % and
-    // scene 5 +76 %, so each scene times both orders on its first frames of a
-    // launch shape and keeps the faster.  Results are bit-identical either way.
-    if (kind == RT_KERNEL_AUTO && P.nranks == 1u && var == 80398 && !(f->kernel & RT_KERNEL_FLAG_BAIL_WIDE) &&
-        row_tune_enabled())
+    // AUTO (and the COMPACT / WIDE arms built on its per-ray code): the feature set of kVarAuto
+    // that this scene allows -- the Newton reciprocal needs rcp_safe, the packed counts and the
+    // empty-run loop need pack_ok.  DESIGN.md §4.1 has the measured progression.
+    const bool auto_path = lanes && grid_mt && (kind == RT_KERNEL_AUTO || kind == RT_KERNEL_COMPACT ||
+                                                kind == RT_KERNEL_WIDE);
+    int var = 0;
+    if (auto_path)
     {
-        const uint64_t key = (uint64_t(blocks) << 8) | P.spp;
-        if (key != s->row_key)
-        {
-            s->row_key = key;
-            s->row_calls = 0;
-            s->row_choice = -1;
-            s->row_pending = -1;
-            s->row_best[0] = s->row_best[1] = 0.f;
-        }
-        int order = s->row_choice;
-        if (order < 0)
-        {
-            order = int(s->row_calls & 1u);
-            s->row_pending = order;
-            ++s->row_calls;
-        }
-        if (order == 1) var |= kVarCenterOut;
+        var = kVarAutoCore | (s->rcp_safe ? kVarFastRcp : 0) | (s->pack_ok ? kVarPackedRem | kVarSkipRun : 0) |
+              ((f->kernel & RT_KERNEL_FLAG_LDS_CELLS) ? kVarLdsCells : 0) |
+              ((f->kernel & RT_KERNEL_FLAG_WAVE_CLOCK) ? kVarWaveClock : 0) |
+              ((f->kernel & RT_KERNEL_FLAG_CENTER_OUT) ? kVarCenterOut : 0);
+        if (int rc = ensure_origin_terms(s, P, st)) return rc;
     }
-    // the wide arms run AUTO's per-ray code without the empty run (phase 1 keeps it)
-    const int wvar = var & ~kVarSkipRun;
+    else if (lanes && P.isect == RT_ISECT_RAY_MARCH)
+        var = kVarMarch | ((f->kernel & RT_KERNEL_FLAG_EXHAUSTIVE) ? kVarExhaustive : 0);
+    else if (lanes && P.isect == RT_ISECT_BRUTE_FORCE)
+        var = kVarBrute;
+    RT_HIP(hipEventRecord(s->ev0, st));
     if (var & kVarWaveClock)
     {
-        const size_t need = size_t(blocks) * (kWG / 64u) * 4u;
+        const size_t need = size_t(blocks) * kWavesPerWG * 4u;
         if (need > s->clk_cap)
         {
             if (s->d_clk) RT_HIP(hipFree(s->d_clk));
@@ -2210,21 +2221,21 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
         s->clk_items = uint32_t(need / 4u);
         P.wave_clk = s->d_clk;
     }
-    const bool bary = P.tri_test == RT_TRI_BARYCENTRIC;
     const dim3 wg(kWG);
-    // RT_KERNEL_FLAG_WIDE16: 16 lanes per sample in the wide kernel / wide phase (spp <= 4)
-    const bool bail_auto = kind == RT_KERNEL_AUTO && P.nranks >= kBailAutoRanks && s->max_cell_refs >= kBailAutoRefs;
-    const bool wide_auto = bail_auto && !(f->kernel & RT_KERNEL_FLAG_BAIL_WIDE);
-    const bool g16 = ((f->kernel & RT_KERNEL_FLAG_WIDE16) || wide_auto) && P.spp * 16u <= 64u;
+    const uint32_t budget = (f->kernel & RT_KERNEL_BUDGET_MASK) >> RT_KERNEL_BUDGET_SHIFT;
+    // the wide arms need AUTO's full record/count layout and at most 64 / 4 samples per pixel
+    const bool wide_ok = auto_path && (var & ~(kVarCenterOut)) == kVarAuto && P.spp * kWideG <= 64u;
     // AUTO takes the two-phase arm for a shard of >= 2 ranks of a scene with dense cells: there a
     // rank's launch is bound by its few ~1000-test waves, which the wide phase splits 16 ways
     // (measured, tools/shard_scaling.py, killeroo rank of 2 / 4 / 8: 0.60 / 0.50 / 0.46 ms with
     // the plain kernel -> 0.48 / 0.35 / 0.25 with budgets 384 / 192 / 128).  On a whole frame,
     // or a scene without dense cells, phase 1's budget count and the re-trace cost more than
     // they save.
-    if (((f->kernel & RT_KERNEL_FLAG_BAIL_WIDE) || bail_auto) && lanes &&
-        (kind == RT_KERNEL_AUTO || kind == RT_KERNEL_LANES) && P.isect == RT_ISECT_GRID && !bary &&
-        (wvar == 14858 || wvar == 80394) && P.spp * kWideG <= 64u)
+    const bool bail_auto = kind == RT_KERNEL_AUTO && P.nranks >= kBailAutoRanks && s->max_cell_refs >= kBailAutoRefs;
+    const bool bail = wide_ok && kind == RT_KERNEL_AUTO && (bail_auto || (f->kernel & RT_KERNEL_FLAG_BAIL_WIDE));
+    const bool g16 = ((f->kernel & RT_KERNEL_FLAG_WIDE16) || (bail_auto && !(f->kernel & RT_KERNEL_FLAG_BAIL_WIDE))) &&
+                     P.spp * 16u <= 64u;
+    if (bail)
     {
         const size_t need = size_t(n_local_tiles) * kTilePix + 1u;   // count + one entry per pixel
         if (need > s->bail_cap)
@@ -2235,8 +2246,8 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
             RT_HIP(hipMalloc(&s->d_bail, sizeof(uint32_t) * need));
             s->bail_cap = need;
         }
-        const uint32_t tb = (f->kernel & RT_KERNEL_COMPACT_REFILL_MASK) >> RT_KERNEL_COMPACT_REFILL_SHIFT;
-        P.bail_tests = tb ? 16u * tb : (wide_auto ? bail_auto_tests(P.nranks) : kBailTests);
+        P.bail_tests = budget ? 16u * budget
+                              : ((f->kernel & RT_KERNEL_FLAG_BAIL_WIDE) ? kBailTests : bail_auto_tests(P.nranks));
         const size_t nstate = size_t(n_local_tiles) * kTilePix * P.spp * 2u;   // 2 float4 per sample slot
         if (nstate > s->bail_state_cap)
         {
@@ -2249,36 +2260,25 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
         P.bail_count = s->d_bail;
         P.bail_queue = s->d_bail + 1;
         RT_HIP(hipMemsetAsync(s->d_bail, 0, sizeof(uint32_t), st));
-        if (var == 80398)
-            hipLaunchKernelGGL((k_render_bail1<80398 | kVarBail>), dim3(uint32_t(blocks)), wg, 0, st, P);
-        else if (wvar == 80394)
-            hipLaunchKernelGGL((k_render_bail1<80394 | kVarBail>), dim3(uint32_t(blocks)), wg, 0, st, P);
-        else
-            hipLaunchKernelGGL((k_render_bail1<14858 | kVarBail>), dim3(uint32_t(blocks)), wg, 0, st, P);
+        hipLaunchKernelGGL((k_render_bail1<kVarAuto | kVarBail>), dim3(uint32_t(blocks)), wg, 0, st, P);
         if (g16)
-            hipLaunchKernelGGL((k_render_bailed<14858, 16>), dim3(s->bail_wgs), wg, 0, st, P);
+            hipLaunchKernelGGL((k_render_bailed<kVarWide, 16>), dim3(s->bail_wgs), wg, 0, st, P);
         else
-            hipLaunchKernelGGL((k_render_bailed<14858, kWideG>), dim3(s->bail_wgs), wg, 0, st, P);
+            hipLaunchKernelGGL((k_render_bailed<kVarWide, kWideG>), dim3(s->bail_wgs), wg, 0, st, P);
     }
-    else if (lanes && kind == RT_KERNEL_WIDE && P.isect == RT_ISECT_GRID && !bary && (wvar == 14858 || wvar == 80394) &&
-        P.spp * kWideG <= 64u)
+    else if (wide_ok && kind == RT_KERNEL_WIDE)
     {
+        const uint32_t G = g16 ? 16u : kWideG;
+        P.xcd_chunk *= G;
         if (g16)
-        {
-            P.xcd_chunk *= 16u;
-            hipLaunchKernelGGL((k_render_wide<14858, 16>), dim3(uint32_t(blocks) * 16u), wg, 0, st, P);
-        }
+            hipLaunchKernelGGL((k_render_wide<kVarWide, 16>), dim3(uint32_t(blocks) * G), wg, 0, st, P);
         else
-        {
-            P.xcd_chunk *= kWideG;
-            hipLaunchKernelGGL((k_render_wide<14858, kWideG>), dim3(uint32_t(blocks) * kWideG), wg, 0, st, P);
-        }
+            hipLaunchKernelGGL((k_render_wide<kVarWide, kWideG>), dim3(uint32_t(blocks) * G), wg, 0, st, P);
     }
     else if (lanes && kind == RT_KERNEL_COMPACT && P.isect == RT_ISECT_GRID)
     {
-        const uint32_t n_items = uint32_t(blocks * (kWG / 64u));
-        uint32_t refill = (f->kernel & RT_KERNEL_COMPACT_REFILL_MASK) >> RT_KERNEL_COMPACT_REFILL_SHIFT;
-        if (refill == 0u) refill = kCompactRefill;
+        const uint32_t n_items = uint32_t(blocks * kWavesPerWG);
+        const uint32_t refill = budget ? budget : kCompactRefill;
         const dim3 grid(std::max(1u, std::min(s->compact_wgs, (n_items + 3u) / 4u)));
         if (bary)
             hipLaunchKernelGGL((k_render_compact<RT_TRI_BARYCENTRIC, kVarDistSkip>), grid, wg, 0, st, P, n_items,
@@ -2287,96 +2287,26 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
             hipLaunchKernelGGL((k_render_compact<RT_TRI_MOLLER_TRUMBORE, kVarWaveGate | kVarDistSkip | kVarOriginPre>),
                                grid, wg, 0, st, P, n_items, refill);
     }
-    else if (lanes && kind == RT_KERNEL_PERSISTENT && P.occ_words && P.isect == RT_ISECT_GRID)
-    {
-        const uint32_t n_items = uint32_t(blocks * (kWG / 64u));
-        const uint32_t per_wg = kPersistWG / 64u;
-        const dim3 grid(std::max(1u, std::min(s->persist_wgs, (n_items + per_wg - 1) / per_wg)));
-        const dim3 pwg(kPersistWG);
-        const size_t lds = P.occ_words * 4u;
-        if (bary)           hipLaunchKernelGGL((k_render_persistent<RT_TRI_BARYCENTRIC, 0>), grid, pwg, lds, st, P, n_items);
-        else if (var == 1)  hipLaunchKernelGGL((k_render_persistent<RT_TRI_MOLLER_TRUMBORE, 1>), grid, pwg, lds, st, P, n_items);
-        else if (var == 2)  hipLaunchKernelGGL((k_render_persistent<RT_TRI_MOLLER_TRUMBORE, 2>), grid, pwg, lds, st, P, n_items);
-        else if (var == 3)  hipLaunchKernelGGL((k_render_persistent<RT_TRI_MOLLER_TRUMBORE, 3>), grid, pwg, lds, st, P, n_items);
-        else                hipLaunchKernelGGL((k_render_persistent<RT_TRI_MOLLER_TRUMBORE, 0>), grid, pwg, lds, st, P, n_items);
-    }
-    else if (lanes && P.isect != RT_ISECT_GRID)
-    {
-        const dim3 grid{uint32_t(blocks)};
-        if (P.isect == RT_ISECT_RAY_MARCH && (f->kernel & RT_KERNEL_FLAG_EXHAUSTIVE))
-            hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, kVarMarch | kVarExhaustive>), grid, wg, 0, st, P);
-        else if (P.isect == RT_ISECT_RAY_MARCH)
-            hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, kVarMarch>), grid, wg, 0, st, P);
-        else
-            hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, kVarBrute>), grid, wg, 0, st, P);
-    }
     else if (lanes)
     {
-        const dim3 grid{uint32_t(blocks)};
-        if (bary)           hipLaunchKernelGGL((k_render_lanes<RT_TRI_BARYCENTRIC, 0>), grid, wg, 0, st, P);
-        else if (var == 1)  hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 1>), grid, wg, 0, st, P);
-        else if (var == 2)  hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 2>), grid, wg, 0, st, P);
-        else if (var == 3)  hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 3>), grid, wg, 0, st, P);
-        else if (var == 4)  hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 4>), grid, wg, 0, st, P);
-        else if (var == 6)  hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 6>), grid, wg, 0, st, P);
-        else if (var == 7)  hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 7>), grid, wg, 0, st, P);
-        else if (var == 8)  hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 8>), grid, wg, 0, st, P);
-        else if (var == 10) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 10>), grid, wg, 0, st, P);
-        else if (var == 18) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 18>), grid, wg, 0, st, P);
-        else if (var == 40) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 40>), grid, wg, 0, st, P);
-        else if (var == 42) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 42>), grid, wg, 0, st, P);
-        else if (var == 522) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 522>), grid, wg, 0, st, P);
-        else if (var == 1546) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 1546>), grid, wg, 0, st, P);
-        else if (var == 2570) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 2570>), grid, wg, 0, st, P);
-        else if (var == 4618) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 4618>), grid, wg, 0, st, P);
-        else if (var == 6666) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 6666>), grid, wg, 0, st, P);
-        else if (var == 14858) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 14858>), grid, wg, 0, st, P);
-        else if (var == 96778) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 96778>), grid, wg, 0, st, P);
-        else if (var == 47626) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 47626>), grid, wg, 0, st, P);
-        else if (var == 80394) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 80394>), grid, wg, 0, st, P);
-        else if (var == 78350) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 78350>), grid, wg, 0, st, P);
-        else if (var == (80398 | kVarEarlyLoad))
-            hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 80398 | kVarEarlyLoad>), grid, wg, 0, st, P);
-        else if (var == (80398 | kVarCenterOut))
-            hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 80398 | kVarCenterOut>), grid, wg, 0, st, P);
-        else if (var == (80398 | kVarCenterOut | kVarWaveClock))
-            hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 80398 | kVarCenterOut | kVarWaveClock>), grid, wg,
-                               0, st, P);
-        else if (var == (80398 | kVarWaveClock))
-            hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 80398 | kVarWaveClock>), grid, wg, 0, st, P);
-        else if (var == 113162) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 113162>), grid, wg, 0, st, P);
-        // AUTO on scenes outside the FAST_RCP / PACKED_REM ranges
-        else if (var == 8714) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 8714>), grid, wg, 0, st, P);
-        else if (var == 10762) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 10762>), grid, wg, 0, st, P);
-        else if (var == 12810) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 12810>), grid, wg, 0, st, P);
-        else if (var == 74250) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 74250>), grid, wg, 0, st, P);
-        else if (var == 76298) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 76298>), grid, wg, 0, st, P);
-        else if (var == 78346) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 78346>), grid, wg, 0, st, P);
-        else if (var == 80398) hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 80398>), grid, wg, 0, st, P);
-        else if (var == (96778 | kVarWaveClock))
-            hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 96778 | kVarWaveClock>), grid, wg, 0, st, P);
-        else if (var == (80394 | kVarPrefetch))
-            hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 80394 | kVarPrefetch>), grid, wg, 0, st, P);
-        else if (var == (80394 | kVarPrefetch | kVarWaveClock))
-            hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 80394 | kVarPrefetch | kVarWaveClock>), grid, wg, 0,
-                               st, P);
-        else if (var == (80394 | kVarAltLoads))
-            hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 80394 | kVarAltLoads>), grid, wg, 0, st, P);
-        else if (var == (80394 | kVarAltLoads | kVarWaveClock))
-            hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 80394 | kVarAltLoads | kVarWaveClock>), grid, wg, 0,
-                               st, P);
-        else if (var == (80394 | kVarLdsCells))
-            hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 80394 | kVarLdsCells>), grid, wg, 0, st, P);
-        else if (var == (80394 | kVarLdsCells | kVarUnroll))
-            hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 80394 | kVarLdsCells | kVarUnroll>), grid, wg, 0,
-                               st, P);
-        else if (var == (80394 | kVarLdsCells | kVarUnroll | kVarWaveClock))
-            hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 80394 | kVarLdsCells | kVarUnroll | kVarWaveClock>),
-                               grid, wg, 0, st, P);
-        else if (var == (80394 | kVarLdsCells | kVarWaveClock))
-            hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 80394 | kVarLdsCells | kVarWaveClock>), grid, wg, 0,
-                               st, P);
-        else                hipLaunchKernelGGL((k_render_lanes<RT_TRI_MOLLER_TRUMBORE, 0>), grid, wg, 0, st, P);
+        // AUTO, LANES, and WIDE / COMPACT where their layout does not apply
+        const int kvar = (kind == RT_KERNEL_AUTO || P.isect != RT_ISECT_GRID) ? var : 0;
+        const kfn_t fn = lanes_kernel(bary ? RT_TRI_BARYCENTRIC : RT_TRI_MOLLER_TRUMBORE, kvar);
+        if (!fn) return fail(RT_E_INVALID, "kernel variant not built: " + std::to_string(kvar));
+        uint32_t grid = uint32_t(blocks);
+        // heavy-first order: AUTO grid frames large enough that blocks start in several rounds
+        if (kind == RT_KERNEL_AUTO && P.isect == RT_ISECT_GRID && !(kvar & kVarWaveClock) &&
+            !(f->kernel & RT_KERNEL_FLAG_STATIC_ORDER) && blocks >= kHfMinBlocks)
+        {
+            if (int rc = hf_prepare(s, P, blocks, kvar, st)) return rc;
+            grid += P.hf_front;
+        }
+        hipLaunchKernelGGL(fn, dim3(grid), wg, 0, st, P);
+        if (P.hf_front && P.hf_measure)
+        {
+            hipLaunchKernelGGL(k_hf_plan, dim3(uint32_t((blocks + kWG - 1) / kWG)), wg, 0, st, P, uint32_t(blocks));
+            hipLaunchKernelGGL(k_hf_mark, dim3((P.hf_front + kWG - 1) / kWG), wg, 0, st, P);
+        }
     }
     else if (P.isect == RT_ISECT_RAY_MARCH && (f->kernel & RT_KERNEL_FLAG_EXHAUSTIVE))
         hipLaunchKernelGGL((k_render_pixel_loop<RT_TRI_MOLLER_TRUMBORE, kVarMarch | kVarExhaustive>),
@@ -2471,7 +2401,6 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
 
     std::unique_ptr<rt_scene> s(new rt_scene());
     s->device = device;
-    s->persist_wgs = 4u * uint32_t(std::max(1, ncus));
     s->compact_wgs = 8u * uint32_t(std::max(1, ncus));
     s->bail_wgs = 4u * uint32_t(std::max(1, ncus));
     for (int a = 0; a < 3; a++)
@@ -2569,25 +2498,19 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
                            : (std::min<uint32_t>(dist[c] == 0xFFFFFFFFu ? 0x1FFFFFu : dist[c], 0x1FFFFFu) << 11);
         }
     }
-    s->occ_words = (nc + 31) / 32;
-    std::vector<uint32_t> occ(s->occ_words, 0);
     for (uint32_t c = 0; c < nc; c++)
-    {
-        if (g.cell_offsets[c + 1] != g.cell_offsets[c]) occ[c >> 5] |= 1u << (c & 31);
         s->max_cell_refs = std::max(s->max_cell_refs, g.cell_offsets[c + 1] - g.cell_offsets[c]);
-    }
 
+    const size_t nfrefs = size_t(std::max(nr, 1u)) * 3;
     RT_HIP(hipMalloc(&s->d_off, sizeof(uint32_t) * (nc + 1)));
     RT_HIP(hipMalloc(&s->d_refs, sizeof(float4) * refs.size()));
-    RT_HIP(hipMalloc(&s->d_frefs, sizeof(float4) * refs.size()));
+    RT_HIP(hipMalloc(&s->d_frefs, sizeof(float4) * nfrefs));
     RT_HIP(hipMalloc(&s->d_shade, sizeof(float4) * shade.size()));
     RT_HIP(hipMalloc(&s->d_facen, sizeof(float4) * facen.size()));
-    RT_HIP(hipMalloc(&s->d_occ, sizeof(uint32_t) * occ.size()));
     RT_HIP(hipMemcpy(s->d_off, g.cell_offsets, sizeof(uint32_t) * (nc + 1), hipMemcpyHostToDevice));
     RT_HIP(hipMemcpy(s->d_refs, refs.data(), sizeof(float4) * refs.size(), hipMemcpyHostToDevice));
     RT_HIP(hipMemcpy(s->d_shade, shade.data(), sizeof(float4) * shade.size(), hipMemcpyHostToDevice));
     RT_HIP(hipMemcpy(s->d_facen, facen.data(), sizeof(float4) * facen.size(), hipMemcpyHostToDevice));
-    RT_HIP(hipMemcpy(s->d_occ, occ.data(), sizeof(uint32_t) * occ.size(), hipMemcpyHostToDevice));
     // Distance records in Morton order of the triangle centroids, blocks of kDistBlock with their
     // exact float AABB (the ray march's block cull, see ray_march)
     std::vector<float4> distblk;
@@ -2659,12 +2582,13 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
         RT_HIP(hipMemcpy(s->d_cellw, cellw.data(), sizeof(uint32_t) * nc, hipMemcpyHostToDevice));
     }
     s->device_bytes = sizeof(uint32_t) * (nc + 1) +
-                      sizeof(float4) * (2 * refs.size() + shade.size() + facen.size() + trimt.size() + tridist.size() +
-                                        distblk.size()) +
-                      sizeof(uint32_t) * (occ.size() + cellw.size());
+                      sizeof(float4) * (refs.size() + nfrefs + shade.size() + facen.size() + trimt.size() +
+                                        tridist.size() + distblk.size()) +
+                      sizeof(uint32_t) * cellw.size();
     RT_HIP(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
     RT_HIP(hipEventCreate(&s->ev0));
     RT_HIP(hipEventCreate(&s->ev1));
+
     *out = s.release();
     return RT_OK;
 }
@@ -2676,12 +2600,12 @@ int rt_scene_destroy(rt_scene *s)
         std::lock_guard<std::mutex> lk(s->mtx);
         (void)hipSetDevice(s->device);
         if (s->stream) (void)hipStreamSynchronize(s->stream);
+        if (s->last_stream && s->ev_recorded) (void)hipEventSynchronize(s->ev1);
         (void)hipFree(s->d_off);
         (void)hipFree(s->d_refs);
         (void)hipFree(s->d_frefs);
         (void)hipFree(s->d_shade);
         (void)hipFree(s->d_facen);
-        (void)hipFree(s->d_occ);
         (void)hipFree(s->d_cellw);
         (void)hipFree(s->d_trimt);
         (void)hipFree(s->d_tridist);
@@ -2689,6 +2613,13 @@ int rt_scene_destroy(rt_scene *s)
         (void)hipFree(s->d_clk);
         (void)hipFree(s->d_bail);
         (void)hipFree(s->d_bail_state);
+        for (HfCtx& h : s->hf)
+        {
+            (void)hipFree(h.marks);
+            (void)hipFree(h.cost);
+            (void)hipFree(h.lists);
+            (void)hipFree(h.plans);
+        }
         (void)hipFree(s->d_smp);
         (void)hipFree(s->d_frame);
         if (s->h_smp_pinned) (void)hipHostFree(s->h_smp_pinned);
@@ -2696,6 +2627,7 @@ int rt_scene_destroy(rt_scene *s)
         if (s->ev0) (void)hipEventDestroy(s->ev0);
         if (s->ev1) (void)hipEventDestroy(s->ev1);
         if (s->stream) (void)hipStreamDestroy(s->stream);
+
     }
     delete s;
     return RT_OK;
@@ -2876,6 +2808,26 @@ int rt_debug_wave_clocks(rt_scene *s, uint64_t *out, uint32_t max_items, uint32_
     if (!out || !s->d_clk) return RT_OK;
     RT_HIP(hipDeviceSynchronize());
     RT_HIP(hipMemcpy(out, s->d_clk, sizeof(uint64_t) * 4 * std::min(max_items, s->clk_items), hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
+int rt_debug_heavy_first(rt_scene *s, uint32_t *front, uint32_t *listed, uint32_t *epoch)
+{
+    if (!s || !front || !listed || !epoch) return fail(RT_E_INVALID, "NULL argument");
+    std::lock_guard<std::mutex> lk(s->mtx);
+    int rc;
+    if ((rc = ensure_device(s))) return rc;
+    *front = *listed = *epoch = 0;
+    const HfCtx *c = nullptr;
+    for (const HfCtx& h : s->hf)
+        if (h.frames && (!c || h.used > c->used)) c = &h;
+    if (!c) return RT_OK;
+    RT_HIP(hipDeviceSynchronize());
+    HfPlan pl;
+    RT_HIP(hipMemcpy(&pl, c->plans + (c->ver & 1u), sizeof(pl), hipMemcpyDeviceToHost));
+    *front = c->front;
+    *listed = c->ver ? std::min(pl.cnt_hi + pl.cnt_lo, c->front) : 0u;
+    *epoch = c->frames;
     return RT_OK;
 }
 

@@ -6,14 +6,14 @@
  *
  *   reference interface                                   replaced by
  *   ----------------------------------------------------  ---------------------------------
- *   Renderer::RenderTile(Tile&)      renderer.cpp:81-174   rt_render_tiles / rt_render_frame_device
- *     per-sample loop                renderer.cpp:112-172  (one batched HIP launch per frame)
+ *   Renderer::RenderTile(Tile&)      renderer.cpp:43-136   rt_render_tiles / rt_render_frame_device
+ *     per-pixel / per-sample loops   renderer.cpp:74-135   (one batched HIP launch per frame)
  *   GenerateRay (perspective)        camera.h:8-47         in-kernel, from rt_frame
  *   Grid::Intersect (3D-DDA)         grid.cpp:159-281      in-kernel, CSR cells from rt_grid_desc
  *   IntersectRayTri                  triangle.h:15-107     RT_TRI_MOLLER_TRUMBORE (default)
  *   IntersectRayTriBarycentric       triangle.h:210-226    RT_TRI_BARYCENTRIC
- *   ToBGRA8 + gamma                  lin_alg.h:125-132,    in-kernel resolve
- *                                    renderer.cpp:162-171
+ *   shading, average, gamma, ToBGRA8 renderer.cpp:107-133, in-kernel resolve
+ *                                    lin_alg.h:125-132
  *   Scene / Grid / Mesh data         scene.h:17-26,        rt_scene_create (uploaded once)
  *                                    grid.h:26-39, mesh.h:12-27
  *
@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 2
+#define RT_ABI_VERSION 3
 
 enum rt_status {
     RT_OK = 0,
@@ -82,72 +82,43 @@ enum rt_intersector {
 };
 
 enum rt_kernel {
-    RT_KERNEL_AUTO = 0,        /* the fastest measured variant for the frame's spp (LANES + WAVE_GATE
-                                  + DIST_SKIP + ORIGIN_PRE + FAST_RCP + PACKED_REM + XCD_BANDS +
-                                  UNIFORM_CELLS + SKIP_RUN; for >= 2-rank shards of dense scenes BAIL_WIDE
-                                  with WIDE16, budget 384 / 192 / 128 from 2 / 4 / 8 ranks) */
-    RT_KERNEL_LANES = 1,       /* one lane per sample, a pixel's samples in adjacent lanes */
+    RT_KERNEL_AUTO = 0,        /* the fastest measured path for the frame: one lane per
+                                  sample, distance-skipping 3D-DDA, per-camera-origin triangle records,
+                                  wave-uniform cell lists on scalar loads, XCD-aware tile rows, and the
+                                  heavy-first block order; for >= 2-rank shards of dense scenes the
+                                  two-phase arm (RT_KERNEL_FLAG_BAIL_WIDE with 16 lanes per sample) */
+    RT_KERNEL_LANES = 1,       /* the plain per-lane kernel: one lane per sample, the reference's walk
+                                  and ray/triangle test cell by cell (A/B baseline) */
     RT_KERNEL_PIXEL_LOOP = 2,  /* one lane per pixel looping over its samples (any spp) */
     RT_KERNEL_COMPACT = 3,     /* AUTO's per-ray code in persistent waves with wavefront active-ray
                                   compaction: finished lanes are refilled with new samples by
                                   ballot + prefix count (grid intersector; else = LANES) */
-    RT_KERNEL_PERSISTENT = 4,  /* LANES in persistent workgroups with the LDS cell-occupancy bitmap */
+    /* 4 was the persistent LDS-bitmap arm (removed: measured slower) */
     RT_KERNEL_WIDE = 5,        /* AUTO's per-ray code with 4 lanes per sample splitting every cell's
                                   triangle list (spp <= 16; else = AUTO) */
     RT_KERNEL_KIND_MASK = 0x07,       /* the kernel kind above; the bits above it are flags */
-    RT_KERNEL_FLAG_EARLY_LOAD = 0x08, /* OR-able (with PACKED_REM): every cell's word is loaded,
-                                         issued before the DDA step */
-    RT_KERNEL_FLAG_CENTER_OUT = 0x10, /* OR-able (with XCD_BANDS): the XCDs' row turns start at the
-                                         frame's middle row and move outward */
-    RT_KERNEL_FLAG_ALT_LOADS = 0x20,  /* OR-able (with UNIFORM_CELLS): the scalar loop alternates
-                                         two record register sets (no per-record copies) */
+    RT_KERNEL_FLAG_CENTER_OUT = 0x10, /* OR-able (AUTO): the XCDs' row turns start at the frame's
+                                         middle row and move outward (A/B arm of the row order) */
+    RT_KERNEL_FLAG_STATIC_ORDER = 0x20, /* OR-able (AUTO): no heavy-first block order (A/B arm) */
     RT_KERNEL_FLAG_WIDE16 = 0x40,     /* OR-able (WIDE kernel, BAIL_WIDE phase 2; spp <= 4): 16 lanes
                                          per sample instead of 4 */
-    RT_KERNEL_FLAG_LDS_CELLS = 0x80,  /* OR-able (with UNIFORM_CELLS): a wave-uniform list of >= 16
-                                         references is staged through LDS 64 records at a time */
-    RT_KERNEL_FLAG_PREFETCH = 0x100,  /* OR-able: software-pipelined triangle record loads */
-    RT_KERNEL_FLAG_WAVE_GATE = 0x200, /* OR-able: skip a test's second half when no lane needs it */
-    RT_KERNEL_FLAG_SKIP_RUN = 0x400,  /* OR-able (with DIST_SKIP + PACKED_REM; in AUTO): while every
-                                         active lane is in a run of cells the distance field proves
-                                         empty, the wave takes bare DDA steps in a tight loop */
-    RT_KERNEL_FLAG_CSR_OFFSETS = 0x800, /* OR-able: read the two CSR offsets per cell instead of
-                                           the packed (start << 11 | count) word */
-    RT_KERNEL_FLAG_DIST_SKIP = 0x1000,  /* OR-able: skip lookups of cells an L-inf distance field
-                                           proves empty (needs the packed words) */
-    RT_KERNEL_FLAG_NESTED_STEP = 0x2000, /* OR-able: the step axis via grid.cpp's nested compares
-                                            (A/B arm of the min3 form) */
-    RT_KERNEL_FLAG_PRE_GATE = 0x4000,   /* OR-able: division-free wave-uniform pre-reject before
-                                            the ray/triangle test's 1/det */
+    RT_KERNEL_FLAG_LDS_CELLS = 0x80,  /* OR-able (AUTO): a wave-uniform list of >= 16 references is
+                                         staged through LDS 64 records at a time */
     RT_KERNEL_FLAG_EXHAUSTIVE = 0x8000, /* OR-able, ray march: evaluate every triangle per step
                                            (no block culling; A/B arm, identical results) */
-    RT_KERNEL_FLAG_ORIGIN_PRE = 0x10000, /* OR-able (grid, Moller-Trumbore, with WAVE_GATE +
-                                            DIST_SKIP): per-frame precompute of the origin-only
-                                            terms o - v0, (o - v0) x e1 of every reference */
-    RT_KERNEL_FLAG_SELECT_STEP = 0x20000, /* OR-able (A/B arm): the DDA step's crossing times
-                                             updated by select + write-back, walk bounded by
-                                             dims sum (the pre-add-step form) */
-    RT_KERNEL_FLAG_FAST_RCP = 0x40000,    /* OR-able (with ORIGIN_PRE): 1/det of the ray/triangle
-                                             test by a Newton-refined v_rcp_f32, exhaustively
-                                             checked equal to 1.0f / det where it is used */
-    RT_KERNEL_FLAG_PACKED_REM = 0x80000,  /* OR-able (with DIST_SKIP): the DDA's three remaining-
-                                             cell counts in one guarded word (dims <= 512) */
-    RT_KERNEL_FLAG_XCD_BANDS = 0x100000,  /* OR-able: XCD-aware block order, the 8 XCDs take
-                                             whole tile rows in turn (L2 locality) */
-    RT_KERNEL_FLAG_UNROLL_PAIRS = 0x200000, /* OR-able (with UNIFORM_CELLS): the scalar loop tests
-                                               two records per iteration, interleaved */
-    RT_KERNEL_FLAG_WAVE_CLOCK = 0x400000, /* OR-able, debug: record s_memtime {start, end} of
+    RT_KERNEL_FLAG_WAVE_CLOCK = 0x400000, /* OR-able (AUTO), debug: record s_memtime {start, end} of
                                              every 64-sample work item (rt_debug_wave_clocks) */
-    RT_KERNEL_FLAG_UNIFORM_CELLS = 0x800000, /* OR-able (AUTO's record layout): a cell list shared
-                                                by every testing lane of the wave runs as a scalar
-                                                loop over scalar-cache record loads */
-    RT_KERNEL_COMPACT_REFILL_SHIFT = 24,  /* RT_KERNEL_COMPACT: bits 24-30 = lanes that must be
-                                             idle before a wave refills (1..64; 0 = default 48) */
-    RT_KERNEL_COMPACT_REFILL_MASK = 0x7F000000,
+    RT_KERNEL_BUDGET_SHIFT = 24,      /* bits 24-30: RT_KERNEL_COMPACT: lanes that must be idle before
+                                         a wave refills (1..64; 0 = default 48); BAIL_WIDE: phase-1
+                                         test budget / 16 (0 = default) */
+    RT_KERNEL_BUDGET_MASK = 0x7F000000,
+    RT_KERNEL_COMPACT_REFILL_SHIFT = RT_KERNEL_BUDGET_SHIFT,
+    RT_KERNEL_COMPACT_REFILL_MASK = RT_KERNEL_BUDGET_MASK,
 };
-/* OR-able (AUTO/LANES, grid, Moller-Trumbore, spp <= 16): two-phase frame.  Samples whose walk
-   would pass a triangle-test budget (bits 24-30 x 16, 0 = 256) stop; their pixels are re-traced
-   by a second kernel with 4 lanes per sample splitting each cell's list.  Bit 31 (not an enum
-   constant: it does not fit a C int). */
+/* OR-able (AUTO, grid, Moller-Trumbore, spp <= 16): two-phase frame.  Samples whose walk would
+   pass a triangle-test budget (bits 24-30 x 16, 0 = 256) stop; their pixels' walks are resumed
+   by a second kernel with 4 (or, WIDE16, 16) lanes per sample splitting each cell's list.
+   Bit 31 (not an enum constant: it does not fit a C int). */
 #define RT_KERNEL_FLAG_BAIL_WIDE 0x80000000u
 
 /* Per-frame parameters: what Renderer::RenderTile reads from the Scene and itself. */
@@ -158,7 +129,7 @@ typedef struct rt_frame {
     uint32_t     width, height;   /* Framebuffer m_width / m_height (framebuffer.h:29-30) */
     uint32_t     spp;             /* Renderer::m_sample_count (renderer.h:34); 0 -> 1 */
     const float *sample_offsets;  /* [spp][2] offsets in [-.5,.5], or NULL for the
-                                     Hammersley table of renderer.cpp:87-98 */
+                                     Hammersley table of renderer.cpp:49-60 */
     uint32_t     tri_test;        /* enum rt_tri_test */
     uint32_t     kernel;          /* enum rt_kernel */
     uint32_t     intersector;     /* enum rt_intersector (ABI version 2) */
@@ -208,13 +179,15 @@ int  rt_scene_create_from_mesh(const rt_vertex *vertices, uint32_t num_vertices,
 /* ---- rendering --------------------------------------------------------------------- */
 /* Renders every listed tile in ONE batched launch (over the tiles' bounding box), copies
  * back and scatters into the caller's host buffers: tile_bufs[i][(x-x0) + (y-y0)*(x1-x0)]
- * = 0x00RRGGBB, exactly the words renderer.cpp:171 stores.  Synchronous. */
+ * = 0x00RRGGBB, exactly the words renderer.cpp:133 stores.  Synchronous. */
 int  rt_render_tiles(rt_scene *scene, const rt_frame *frame, const rt_tile *tiles,
                      uint32_t n_tiles, uint32_t *const *tile_bufs);
 
 /* Device-resident frame: d_bgra[y*width + x] on the caller's HIP stream (NULL = default
- * stream).  Asynchronous; no host synchronisation and no allocation when the sample
- * table is unchanged (safe to capture in a hipGraph). */
+ * stream).  Asynchronous: never waits on the host.  Allocates only for the first frame of a
+ * launch shape (AUTO's heavy-first state) or a changed sample table, so a hipGraph captured after
+ * one warm-up frame replays without allocations; a replay keeps the heavy-first order of the frame
+ * before the capture (the pixels never depend on the order). */
 int  rt_render_frame_device(rt_scene *scene, const rt_frame *frame, uint32_t *d_bgra,
                             void *hip_stream);
 
@@ -254,6 +227,11 @@ int  rt_debug_rcp_check(uint64_t *bad_by_exponent, int device);
    iterations of the per-lane list loop.  out holds 4 x max_items words; *n_items = how many
    items the launch wrote. */
 int  rt_debug_wave_clocks(rt_scene *s, uint64_t *out, uint32_t max_items, uint32_t *n_items);
+
+/* AUTO's heavy-first order for the most recent launch shape on this scene: *front = blocks the
+   front section holds, *listed = blocks the last frame listed for the next one (heavy waves found),
+   *epoch = frames rendered with this shape.  Synchronises the device. */
+int rt_debug_heavy_first(rt_scene *s, uint32_t *front, uint32_t *listed, uint32_t *epoch);
 
 /* Hammersley table the library uses when rt_frame.sample_offsets is NULL. */
 int  rt_sample_table(uint32_t spp, float *out_xy);

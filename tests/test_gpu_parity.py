@@ -58,8 +58,9 @@ def test_device_kat_branch_free_ray_tri():
 
 
 def test_device_kat_wave_gated_ray_tri():
-    """Pre-gated and gated Moller-Trumbore (wave-uniform exits): hit flags equal the reference's,
-    t,u,v bit-identical on hits -- evaluated 64 records per wave, so the exits really fire."""
+    """Gated Moller-Trumbore and the per-camera-record form with the Newton 1/det (wave-uniform
+    exits): hit flags equal the reference's, t,u,v bit-identical on hits -- evaluated 64 records
+    per wave, so the exits really fire."""
     rin, exp = load_kat("ray_tri")
     got = rtm.debug_primitives(6, rin)
     m = bits(exp[:, 0]) == 1
@@ -168,46 +169,89 @@ def test_newton_reciprocal_exhaustive():
     assert int(bad[1:253].sum()) == 0, {e: int(c) for e, c in enumerate(bad) if c}
 
 
-def test_auto_equals_plain_arms(golden, scenes):
-    """AUTO (Newton reciprocal + packed counts + XCD row interleave + uniform-cell scalar loop)
-    and the plain-division / unpacked / dispatch-order / unrolled arms, the wide kernel (4 lanes
-    per sample) and the two-phase arm (budgets 256 and 64: many pixels re-traced) render the
-    same bytes as the reference on the two bench scenes and the densest one."""
-    base = (rtm.RT_KERNEL_LANES | rtm.RT_KERNEL_FLAG_WAVE_GATE | rtm.RT_KERNEL_FLAG_DIST_SKIP |
-            rtm.RT_KERNEL_FLAG_ORIGIN_PRE)
+def test_auto_equals_arms(golden, scenes):
+    """AUTO (heavy-first order) and its static-order, centre-out and LDS-staged arms, the plain
+    LANES kernel, the wide kernel (4 and 16 lanes per sample) and the two-phase arm (budgets 256
+    and 64: many pixels resumed by the wide phase) render the reference's bytes on the two bench
+    scenes and the densest one."""
+    A = rtm.RT_KERNEL_AUTO
     for sid in (1, 5, 8):
         hs, gs = scenes(sid)
         want = golden["frames_1080p4"][str(sid)]["bgra_sha256"]
-        full = (base | rtm.RT_KERNEL_FLAG_FAST_RCP | rtm.RT_KERNEL_FLAG_PACKED_REM | rtm.RT_KERNEL_FLAG_XCD_BANDS)
-        for k in (base, base | rtm.RT_KERNEL_FLAG_FAST_RCP, base | rtm.RT_KERNEL_FLAG_PACKED_REM,
-                  base | rtm.RT_KERNEL_FLAG_SELECT_STEP, base | rtm.RT_KERNEL_FLAG_XCD_BANDS,
-                  full | rtm.RT_KERNEL_FLAG_UNIFORM_CELLS,
-                  full | rtm.RT_KERNEL_FLAG_UNIFORM_CELLS | rtm.RT_KERNEL_FLAG_UNROLL_PAIRS,
-                  full | rtm.RT_KERNEL_FLAG_UNIFORM_CELLS | rtm.RT_KERNEL_FLAG_ALT_LOADS,
-                  full | rtm.RT_KERNEL_FLAG_UNIFORM_CELLS | rtm.RT_KERNEL_FLAG_SKIP_RUN,
-                  full | rtm.RT_KERNEL_FLAG_UNIFORM_CELLS | rtm.RT_KERNEL_FLAG_SKIP_RUN | rtm.RT_KERNEL_FLAG_EARLY_LOAD,
-                  full | rtm.RT_KERNEL_FLAG_UNIFORM_CELLS | rtm.RT_KERNEL_FLAG_SKIP_RUN | rtm.RT_KERNEL_FLAG_CENTER_OUT,
-                  full | rtm.RT_KERNEL_FLAG_UNIFORM_CELLS | rtm.RT_KERNEL_FLAG_LDS_CELLS,
-                  full | rtm.RT_KERNEL_FLAG_UNIFORM_CELLS | rtm.RT_KERNEL_FLAG_LDS_CELLS | rtm.RT_KERNEL_FLAG_UNROLL_PAIRS,
-                  full | rtm.RT_KERNEL_FLAG_UNIFORM_CELLS | rtm.RT_KERNEL_FLAG_PREFETCH,
-                  rtm.RT_KERNEL_WIDE, rtm.RT_KERNEL_FLAG_BAIL_WIDE, rtm.RT_KERNEL_FLAG_BAIL_WIDE | (4 << 24),
-                  rtm.RT_KERNEL_WIDE | rtm.RT_KERNEL_FLAG_WIDE16,
+        for k in (A, A | rtm.RT_KERNEL_FLAG_STATIC_ORDER, A | rtm.RT_KERNEL_FLAG_CENTER_OUT,
+                  A | rtm.RT_KERNEL_FLAG_LDS_CELLS, rtm.RT_KERNEL_LANES,
+                  rtm.RT_KERNEL_WIDE, rtm.RT_KERNEL_WIDE | rtm.RT_KERNEL_FLAG_WIDE16,
+                  rtm.RT_KERNEL_FLAG_BAIL_WIDE, rtm.RT_KERNEL_FLAG_BAIL_WIDE | (4 << 24),
                   rtm.RT_KERNEL_FLAG_BAIL_WIDE | rtm.RT_KERNEL_FLAG_WIDE16 | (4 << 24)):
             img = gs.render_frame(gs.frame(1920, 1080, 4, kernel=k))
             assert hashlib.sha256(img.tobytes()).hexdigest() == want, (sid, hex(k))
 
 
-def test_auto_row_order_tuning_frames(golden, scenes):
-    """AUTO at one rank times plain and centre-out row order on a launch shape's first four
-    frames (alternating), then keeps the faster: every frame of that sequence, and the ones
-    after the choice, are the reference's bytes."""
-    for sid in (1, 8):
+def test_heavy_first_frames(golden, scenes):
+    """AUTO's heavy-first order: the first frames of a launch shape run in the natural order and
+    measure their waves; from the third frame on the blocks of the heavy waves render first.
+    Every frame is the reference's and the list is non-empty on the dense scenes."""
+    import torch
+    out = torch.zeros(1920 * 1080, dtype=torch.int32, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    for sid in (1, 5, 8):
         hs, gs = scenes(sid)
         want = golden["frames_1080p4"][str(sid)]["bgra_sha256"]
-        fr = gs.frame(1920, 1080, 4, kernel=rtm.RT_KERNEL_AUTO)
-        for i in range(7):
-            img = gs.render_frame(fr)
+        f = gs.frame(1920, 1080, 4)
+        for i in range(6):
+            out.zero_()
+            gs.render_frame_device(f, out.data_ptr(), stream)
+            torch.cuda.synchronize()
+            img = out.cpu().numpy().view(np.uint32)
             assert hashlib.sha256(img.tobytes()).hexdigest() == want, (sid, i)
+        front, listed, epoch = gs.heavy_first()
+        assert front == 1024 and epoch >= 6, (sid, front, epoch)
+        if sid in (5, 8):
+            assert listed > 0, (sid, listed)
+
+
+def test_heavy_first_interleaved_shapes(golden, scenes, oracle):
+    """Launch shapes alternating on one scene (whole frames, a tile batch, a small frame) keep
+    separate heavy-first state; every frame of the interleaving is exact."""
+    import torch
+    hs, gs = scenes(8)
+    want = golden["frames_1080p4"]["8"]["bgra_sha256"]
+    exp_small, _, _ = oracle.render(8, 640, 480, 4)
+    out = torch.zeros(1920 * 1080, dtype=torch.int32, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    f_big, f_small = gs.frame(1920, 1080, 4), gs.frame(640, 480, 4)
+    tiles = [(0, 0, 960, 540), (960, 0, 1920, 540), (0, 540, 960, 1080), (960, 540, 1920, 1080)]
+    for i in range(3):
+        out.zero_()
+        gs.render_frame_device(f_big, out.data_ptr(), stream)
+        torch.cuda.synchronize()
+        assert hashlib.sha256(out.cpu().numpy().view(np.uint32).tobytes()).hexdigest() == want, i
+        np.testing.assert_array_equal(gs.render_frame(f_small), exp_small)
+        parts = gs.render_tiles(f_big, tiles)
+        img = np.block([[parts[0], parts[1]], [parts[2], parts[3]]])
+        assert hashlib.sha256(np.ascontiguousarray(img).tobytes()).hexdigest() == want, i
+
+
+def test_hip_graph_capture_replay(golden, scenes):
+    """rt_render_frame_device inside a captured HIP graph (torch.cuda.CUDAGraph on the current
+    stream), after one warm-up frame of the shape: replays render the reference's frame."""
+    import torch
+    hs, gs = scenes(1)
+    want = golden["frames_1080p4"]["1"]["bgra_sha256"]
+    f = gs.frame(1920, 1080, 4)
+    out = torch.zeros(1920 * 1080, dtype=torch.int32, device="cuda")
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        gs.render_frame_device(f, out.data_ptr(), s.cuda_stream)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        gs.render_frame_device(f, out.data_ptr(), s.cuda_stream)
+    for _ in range(3):
+        out.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert hashlib.sha256(out.cpu().numpy().view(np.uint32).tobytes()).hexdigest() == want
 
 
 @pytest.mark.parametrize("spp", [1, 2, 4, 16, 32])
@@ -229,10 +273,7 @@ def test_lds_cells_vs_oracle(scenes, oracle, sid, spp):
     reference's."""
     hs, gs = scenes(sid)
     exp, _, _ = oracle.render(sid, 97, 61, spp)
-    k = rtm.RT_KERNEL_LANES | (rtm.RT_KERNEL_FLAG_WAVE_GATE | rtm.RT_KERNEL_FLAG_DIST_SKIP |
-                                rtm.RT_KERNEL_FLAG_ORIGIN_PRE | rtm.RT_KERNEL_FLAG_FAST_RCP |
-                                rtm.RT_KERNEL_FLAG_PACKED_REM | rtm.RT_KERNEL_FLAG_XCD_BANDS |
-                                rtm.RT_KERNEL_FLAG_UNIFORM_CELLS | rtm.RT_KERNEL_FLAG_LDS_CELLS)
+    k = rtm.RT_KERNEL_AUTO | rtm.RT_KERNEL_FLAG_LDS_CELLS
     np.testing.assert_array_equal(gs.render_frame(gs.frame(97, 61, spp, kernel=k)), exp)
 
 
@@ -261,10 +302,7 @@ def test_wave_clock_debug_arm(scenes):
     """RT_KERNEL_FLAG_WAVE_CLOCK records {start, end} per work item and leaves the frame alone."""
     hs, gs = scenes(1)
     f0 = gs.frame(160, 120, 4)
-    f1 = gs.frame(160, 120, 4, kernel=(rtm.RT_KERNEL_LANES | rtm.RT_KERNEL_FLAG_WAVE_GATE | rtm.RT_KERNEL_FLAG_DIST_SKIP |
-                                         rtm.RT_KERNEL_FLAG_ORIGIN_PRE | rtm.RT_KERNEL_FLAG_FAST_RCP |
-                                         rtm.RT_KERNEL_FLAG_PACKED_REM | rtm.RT_KERNEL_FLAG_XCD_BANDS |
-                                         rtm.RT_KERNEL_FLAG_WAVE_CLOCK))
+    f1 = gs.frame(160, 120, 4, kernel=rtm.RT_KERNEL_AUTO | rtm.RT_KERNEL_FLAG_WAVE_CLOCK)
     np.testing.assert_array_equal(gs.render_frame(f1), gs.render_frame(f0))
     clk = gs.wave_clocks()
     assert clk.shape == (10 * 8 * 16, 4) and (clk[:, 1] >= clk[:, 0]).all() and clk[:, 0].any()

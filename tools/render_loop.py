@@ -1,0 +1,35 @@
+#!/usr/bin/env python3
+"""Renders one scene's 1080p x 4 frame N times with a given build and kernel value (a driver for
+rocprofv3 --pmc / --kernel-trace runs):
+    python3 tools/render_loop.py --lib librt_tracer_r01.so --scene 1 --frames 10 --kernel 0"""
+import argparse
+import importlib.util
+import os
+import sys
+
+import torch  # first: share torch's HIP runtime
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--lib", default="")
+ap.add_argument("--scene", type=int, default=1)
+ap.add_argument("--frames", type=int, default=10)
+ap.add_argument("--kernel", type=lambda x: int(x, 0), default=0)
+ap.add_argument("--size", type=int, nargs=3, default=[1920, 1080, 4])
+a = ap.parse_args()
+if a.lib:
+    os.environ["RT_TRACER_LIB"] = a.lib
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+spec = importlib.util.spec_from_file_location("rtm", os.path.join(ROOT, "cpp-11-ray-trace-march-framework_amd", "__init__.py"))
+rtm = importlib.util.module_from_spec(spec)
+sys.modules["rtm"] = rtm
+spec.loader.exec_module(rtm)
+torch.cuda.set_device(0)
+st = torch.cuda.current_stream()
+W, H, S = a.size
+g = rtm.GpuScene(rtm.HostScene.load(a.scene), 0)
+f = g.frame(W, H, S, kernel=a.kernel)
+out = torch.empty(W * H, dtype=torch.int32, device="cuda")
+for _ in range(a.frames):
+    g.render_frame_device(f, out.data_ptr(), st.cuda_stream)
+torch.cuda.synchronize()
+print("frames", a.frames, "scene", a.scene, "lib", a.lib or "librt_tracer.so")
