@@ -16,8 +16,11 @@ configs: "head4096" = config 4 (head.dat, 4096x4096x16spp, the 8-GPU tile-shard 
 Prints ONE JSON line (rank 0).  value = total samples of all ranks / max-over-ranks wall time
 of the K timed steps.  roofline: algorithmic bytes of the render kernel per launch (SURVEY
 §8d: B = 8*voxels + 40*tri_tests + 48*hit + 4/spp per sample, counts measured on these
-frames) / mean kernel duration from HIP events on the launch stream.  cpu_baseline: the
-oracle's CPU restatement of the reference tile pool (kind "port"), on this host's cores.
+frames) / mean render-kernel duration (HIP events the library records on the launch stream
+around each render kernel, rt_kernel_times) is kept as the secondary
+algorithmic_frac; the graded bound is VALU issue (valu_roofline).  end_to_end: the host
+Framebuffer drop-in path, frame to tile buffers incl. PCIe.  cpu_baseline: the oracle's CPU
+restatement (kind "port") of the reference's per-sample loop and 12x9 tile pool, on this host.
 """
 import argparse
 import importlib.util
@@ -79,27 +82,113 @@ def algorithmic_bytes(gs, frame):
             "bytes_per_sample": 8 * v + 40 * t + 48 * h + 4.0 / frame.spp}
 
 
+def host_cores():
+    """CPU threads this process may use: the affinity set, capped by OMP_NUM_THREADS (16 on the
+    GPU box, whose nproc shows the whole machine)."""
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    return max(1, min(cores, int(os.environ.get("OMP_NUM_THREADS", cores))))
+
+
+def end_to_end(rtm, work, reps=7):
+    """The drop-in path the reference calls (framebuffer.cpp:59-92, renderer.cpp:133): the host
+    Framebuffer's 12x9 tile workers with the GPU RenderTile -- one launch, copy-back in tile-row
+    bands into page-locked memory, each worker copying its tile out -- timed per frame from
+    rth_framebuffer_start_rendering's call to its return (pool start -> last tile in its host
+    buffer), median of `reps` after one warm-up.  Also the frame alone into host memory
+    (rt_render_frame_host + wait = kernel + PCIe D2H)."""
+    nthreads = host_cores()
+    per = {}
+    for sid, hs, gs, f in work.scenes:
+        r = rtm.Renderer(hs, gs, nthreads)
+        r.set_sample_count(SPP)
+        r.resize(W, H)
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            r.start_rendering()
+            ts.append(time.perf_counter() - t0)
+        r.close()
+        pf = rtm.PinnedFrame(W, H)
+        hf = []
+        try:
+            for i in range(reps + 1):
+                t0 = time.perf_counter()
+                gs.render_frame_host(f, pf)
+                gs.wait_rows(H)
+                if i:
+                    hf.append(time.perf_counter() - t0)
+        finally:
+            pf.close()
+        per[str(sid)] = {"framebuffer_ms": round(1e3 * sorted(ts)[len(ts) // 2], 4),
+                         "frame_to_host_ms": round(1e3 * sorted(hf)[len(hf) // 2], 4)}
+    tot = sum(p["framebuffer_ms"] for p in per.values())
+    return {"value": round(len(work.scenes) * W * H * SPP / (tot / 1e3) / 1e6, 3), "unit": "Msamples/s",
+            "ms_per_step": round(tot, 4), "threads": nthreads, "per_scene": per,
+            "note": "host-buffer delivery incl. PCIe; value is never the bench value"}
+
+
+def valu_roofline(rtm, kernel_ms, args, world, algorithmic):
+    """The bound that binds: VALU issue.  SQ_INSTS_VALU per launch comes from
+    profiles/counters.json (tools/collect_counters.py, rocprofv3 --pmc on this workload), used
+    only when its source_hash equals the hash of the kernel sources being timed; achieved =
+    instructions per launch / the live mean kernel time (HIP events).  peak = 256 CU x 4 SIMD x
+    1/2 wave64 VALU instruction per clock x 2.4 GHz.  traffic = PMC HBM bytes per launch from the
+    same file.  The SURVEY 8d algorithmic-bytes rate stays as a labelled secondary
+    (algorithmic_frac): the scene is L2/MALL resident, so it can exceed 1."""
+    roof = {"bound": "valu", "achieved": None, "peak": round(VALU_PEAK / 1e9, 1), "unit": "Gwave-inst/s",
+            "frac": None, "traffic": None,
+            "algorithmic_frac": round(algorithmic / HBM_PEAK, 4),
+            "algorithmic": {"achieved": round(algorithmic / 1e9, 1), "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                            "note": "SURVEY 8d bytes per launch / mean kernel time; L2-served"}}
+    path = os.path.join(ROOT, "profiles", "counters.json")
+    want = f"scenes{list(SCENES)}_{W}x{H}x{SPP}"
+    if world != 1 or args.kernel != 0:
+        roof["counters"] = "not collected for this launch shape"
+        return roof
+    if not os.path.exists(path):
+        roof["counters"] = "profiles/counters.json missing"
+        return roof
+    with open(path) as fh:
+        c = json.load(fh)
+    src = rtm.kernel_source_hash()
+    if c.get("source_hash") != src:
+        roof["counters"] = f"refused: counters are for sources {c.get('source_hash')}, timed build is {src}"
+        return roof
+    if c.get("workload") != want:
+        roof["counters"] = f"refused: counters are for {c.get('workload')}, not {want}"
+        return roof
+    sc = c["scenes"]
+    insts = sum(sc[str(sid)]["SQ_INSTS_VALU"] for sid in SCENES)
+    rate = insts / (sum(kernel_ms.values()) / 1e3)
+    roof.update({"achieved": round(rate / 1e9, 1), "frac": round(rate / VALU_PEAK, 4),
+                 "traffic": round(sum(sc[str(sid)]["hbm_bytes"] for sid in SCENES) / len(SCENES)),
+                 "traffic_unit": "HBM bytes per launch (mean over scenes)",
+                 "per_scene_valu_frac": {str(sid): round(sc[str(sid)]["SQ_INSTS_VALU"] / (kernel_ms[sid] / 1e3)
+                                                         / VALU_PEAK, 4) for sid in SCENES},
+                 "counters": f"profiles/counters.json, source hash {src}"})
+    return roof
+
+
 def cpu_baseline(rtm_unused=None):
     """Oracle (CPU restatement of the reference's std::thread tile pool) on this host."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from conftest import Oracle
     orc = Oracle()
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count() or 1
-    cores = max(1, min(cores, int(os.environ.get("OMP_NUM_THREADS", cores))))
+    cores = host_cores()
     cw, ch, cs = CPU_FRAME
     for sid in SCENES:                  # warm-up (first render after idle is slow)
         orc.render(sid, cw, ch, cs, nthreads=cores)
     times = []
-    for _ in range(3):
+    for _ in range(5):
         tot = 0.0
         for sid in SCENES:
             _, _, s = orc.render(sid, cw, ch, cs, nthreads=cores)
             tot += s
         times.append(tot)
-    med = sorted(times)[1]
+    med = sorted(times)[2]
     model = ""
     try:
         with open("/proc/cpuinfo") as f:
@@ -109,7 +198,7 @@ def cpu_baseline(rtm_unused=None):
     return {"value": round(len(SCENES) * cw * ch * cs / med / 1e6, 3), "unit": "Msamples/s",
             "cores": cores, "kind": "port",
             "sample": f"full frames of scenes {list(SCENES)} at {cw}x{ch}x{cs}, 12x9 tile pool, "
-                      f"median of 3 after 1 warm-up; cpu: {model or platform.processor()}"}
+                      f"median of 5 after 1 warm-up; cpu: {model or platform.processor()}"}
 
 
 class GpuWorkload:
@@ -126,21 +215,16 @@ class GpuWorkload:
         n = W * H if world == 1 else rtm.shard_elems(W, H, world)
         self.bufs = [torch.empty(n, dtype=torch.int32, device="cuda") for _ in SCENES]
         self.frames = [torch.empty(W * H, dtype=torch.int32, device="cuda") for _ in SCENES]
-        self.events = {sid: [] for sid in SCENES}
-
-    def render(self, i, record):
+    def render(self, i):
         sid, hs, gs, f = self.scenes[i]
-        if record:
-            a = self.torch.cuda.Event(enable_timing=True)
-            b = self.torch.cuda.Event(enable_timing=True)
-            a.record(self.stream)
         if self.world == 1:
             gs.render_frame_device(f, self.bufs[i].data_ptr(), self.stream.cuda_stream)
         else:
             gs.render_shard_device(f, self.rank, self.world, self.bufs[i].data_ptr(), self.stream.cuda_stream)
-        if record:
-            b.record(self.stream)
-            self.events[sid].append((a, b))
+
+    def reset_times(self):
+        for sid, hs, gs, f in self.scenes:
+            gs.kernel_times()
 
     def unshard(self, i, gathered):
         self.rtm.unshard_device(W, H, self.world, gathered.data_ptr(), self.frames[i].data_ptr(),
@@ -149,8 +233,16 @@ class GpuWorkload:
     def sync(self):
         self.torch.cuda.synchronize()
 
-    def kernel_ms(self):
-        return {sid: float(np.mean([a.elapsed_time(b) for a, b in ev])) for sid, ev in self.events.items()}
+    def kernel_ms(self, steps):
+        """Mean render-kernel ms per scene over the timed steps: HIP events the library records
+        on the launch stream immediately around each render kernel (rt_kernel_times)."""
+        out = {}
+        for sid, hs, gs, f in self.scenes:
+            t = gs.kernel_times()
+            if len(t) != min(steps, 64):
+                raise SystemExit(f"scene {sid}: {len(t)} kernel times for {steps} timed steps")
+            out[sid] = float(np.mean(t))
+        return out
 
     def close(self):
         for sid, hs, gs, f in self.scenes:
@@ -200,10 +292,10 @@ def run_steps(work, world, rank, steps, warmup, dist=None):
                                       device=work.bufs[i].device)
         return work.rtm.all_gather_shards(work.bufs[i], world, out=gathered[i], async_op=True)
 
-    def step(record):
+    def step():
         pending = []
         for i in range(len(SCENES)):
-            work.render(i, record)
+            work.render(i)
             if world > 1:
                 pending.append(collect(i))
         for i, (g, h) in enumerate(pending):
@@ -213,14 +305,15 @@ def run_steps(work, world, rank, steps, warmup, dist=None):
                 work.unshard(i, g)
 
     for _ in range(warmup):
-        step(False)
+        step()
     work.sync()
+    work.reset_times()
     if world > 1:
         dist.barrier()
     work.sync()
     t0 = time.perf_counter()
     for _ in range(steps):
-        step(True)
+        step()
     work.sync()
     if world > 1:
         dist.barrier()
@@ -241,6 +334,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--kernel", type=int, default=0, help="rt_kernel value (0 = AUTO; see include/rt_tracer.h)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-end-to-end", action="store_true")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="bench")
     ap.add_argument("--check", action="store_true",
                     help="after timing, rank 0 compares every assembled frame with a one-GPU render")
@@ -272,7 +366,7 @@ def main():
     rtm = load_package()
     work = GpuWorkload(rtm, torch, world, rank, local, args.kernel)
     elapsed = run_steps(work, world, rank, args.steps, args.warmup, dist if world > 1 else None)
-    kernel_ms = work.kernel_ms()
+    kernel_ms = work.kernel_ms(args.steps)
     samples_per_step = len(SCENES) * W * H * SPP          # all ranks together
     value = samples_per_step * args.steps / elapsed / 1e6
 
@@ -281,26 +375,7 @@ def main():
         ab = {sid: algorithmic_bytes(gs, f) for sid, hs, gs, f in work.scenes}
         launch_bytes = {sid: ab[sid]["bytes_per_sample"] * W * H * SPP / world for sid in SCENES}
         achieved = sum(launch_bytes.values()) / (sum(kernel_ms.values()) / 1e3)
-        traffic = None
-        pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc) and world == 1:
-            with open(pmc) as fh:
-                p = json.load(fh)
-            if p.get("workload") == f"scenes{list(SCENES)}_{W}x{H}x{SPP}":
-                traffic = p.get("hbm_bytes_per_launch")
-        # VALU-issue companion roofline: SQ_INSTS_VALU per launch from the committed PMC pass
-        # (profiles/auto_counters.json: the current AUTO kernel, same scenes, one GPU) over the live kernel time;
-        # peak = 256 CU x 4 SIMD x 1/2 wave64 VALU instruction per clock x 2.4 GHz
-        valu = None
-        cnt = os.path.join(ROOT, "profiles", "auto_counters.json")
-        if os.path.exists(cnt) and world == 1 and args.kernel == 0 and args.workload == "bench":
-            with open(cnt) as fh:
-                c = json.load(fh)["scenes"]
-            insts = sum(c[str(sid)]["SQ_INSTS_VALU"] for sid in SCENES)
-            rate = insts / (sum(kernel_ms.values()) / 1e3)
-            valu = {"achieved": round(rate / 1e9, 1), "peak": VALU_PEAK / 1e9,
-                    "unit": "Gwave-inst/s", "frac": round(rate / VALU_PEAK, 4),
-                    "insts_per_launch": {str(sid): c[str(sid)]["SQ_INSTS_VALU"] for sid in SCENES}}
+        roof = valu_roofline(rtm, kernel_ms, args, world, achieved)
         out = {
             "metric": METRIC[args.workload],
             "value": round(value, 3),
@@ -325,19 +400,15 @@ def main():
                                      "voxels": round(ab[sid]["voxels"], 2),
                                      "tri_tests": round(ab[sid]["tri_tests"], 2),
                                      "hit": round(ab[sid]["hit"], 4)} for sid in SCENES},
-            "roofline": {"bound": "hbm", "achieved": round(achieved / 1e9, 1), "peak": HBM_PEAK / 1e9,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 4),
-                         "traffic": traffic,
-                         "note": "achieved = algorithmic bytes per launch (SURVEY 8d formula on the "
-                                 "kernel's measured per-sample counts) / mean kernel time; the scene "
-                                 "working set is L2/MALL resident, so frac can exceed 1",
-                         "valu_issue": valu},
+            "roofline": roof,
             "cpu_baseline": None,
         }
         if args.check:
             out["check"] = check_frames(work, world)
         if args.one_device or args.dist_backend != "nccl":
             out["config"]["rehearsal"] = f"{args.dist_backend}, one device" if args.one_device else args.dist_backend
+        if world == 1 and args.workload == "bench" and not args.no_end_to_end:
+            out["end_to_end"] = end_to_end(rtm, work)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline()
         print(json.dumps(out), flush=True)

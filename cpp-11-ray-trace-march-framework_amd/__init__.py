@@ -21,6 +21,19 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+# Everything librt_tracer.so is compiled from: PMC counter files are valid only for this hash
+KERNEL_SOURCES = ("csrc/rt_tracer.hip", "csrc/rt_grid_build.hip", "csrc/rt_device.h",
+                  "csrc/rt_internal.h", "csrc/Makefile", "../include/rt_tracer.h")
+
+
+def kernel_source_hash():
+    """SHA-256 (first 16 hex digits) over the kernel sources, in KERNEL_SOURCES order."""
+    import hashlib
+    h = hashlib.sha256()
+    for rel in KERNEL_SOURCES:
+        with open(os.path.normpath(os.path.join(HERE, rel)), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
 REPO = os.path.dirname(HERE)
 SCENE_DIR = os.path.join(REPO, "data", "scenes")
 MESH_DATA_DIR = os.path.join(REPO, "data", "meshes")     # cornell_box_quads.txt (scene table)
@@ -51,7 +64,8 @@ TRACER_SYMBOLS = [
     "rt_unshard_device", "rt_last_kernel_ms", "rt_trace_samples", "rt_debug_primitives",
     "rt_debug_rcp_check", "rt_debug_wave_clocks", "rt_debug_heavy_first",
     "rt_sample_table", "rt_last_error", "rt_abi_version", "rt_grid_build", "rt_grid_free",
-    "rt_scene_create_from_mesh",
+    "rt_scene_create_from_mesh", "rt_kernel_times", "rt_render_frame_host", "rt_frame_host_wait", "rt_host_alloc",
+    "rt_host_free",
 ]
 HOST_SYMBOLS = [
     "rth_scene_load", "rth_scene_from_mesh", "rth_scene_free", "rth_scene_desc",
@@ -122,7 +136,8 @@ def _load(name):
     # two builds in one process, tools/ab_libs.py); read when the library is first loaded
     if name == "librt_tracer.so" and os.environ.get("RT_TRACER_LIB"):
         name = os.path.basename(os.environ["RT_TRACER_LIB"])
-    path = os.path.join(HERE, name)
+    # RT_LIB_DIR: load both libraries from another build directory (tools/e2e_ab.py)
+    path = os.path.join(os.environ.get("RT_LIB_DIR", HERE), name)
     if not os.path.exists(path):
         raise RtError(f"{path} is not built; run __graft_entry__.build() or make -C {HERE}")
     return ctypes.CDLL(path)
@@ -140,6 +155,12 @@ def tracer_lib():
         L.rt_render_tiles.argtypes = [vp, ctypes.POINTER(Frame), ctypes.POINTER(Tile), c_u32,
                                       ctypes.POINTER(u32p)]
         L.rt_render_frame_device.argtypes = [vp, ctypes.POINTER(Frame), vp, vp]
+        if hasattr(L, "rt_render_frame_host"):       # ABI 4
+            L.rt_kernel_times.argtypes = [vp, vp, c_u32, ctypes.POINTER(c_u32)]
+            L.rt_render_frame_host.argtypes = [vp, ctypes.POINTER(Frame), vp, u32p, c_u32]
+            L.rt_frame_host_wait.argtypes = [vp, c_u32]
+            L.rt_host_alloc.argtypes = [ctypes.c_size_t, ctypes.POINTER(vp)]
+            L.rt_host_free.argtypes = [vp]
         L.rt_shard_elems.argtypes = [c_u32, c_u32, c_u32, ctypes.POINTER(ctypes.c_uint64)]
         L.rt_render_shard_device.argtypes = [vp, ctypes.POINTER(Frame), c_u32, c_u32, vp, vp]
         L.rt_unshard_device.argtypes = [c_u32, c_u32, c_u32, vp, vp, vp]
@@ -404,6 +425,24 @@ def gpu_grid_build(vertices, triangles, grid_res=64, device=0):
     return meta, offs, tris, ms.value
 
 
+class PinnedFrame:
+    """Page-locked host frame (rt_host_alloc) viewed as a (height, width) uint32 array."""
+
+    def __init__(self, width, height):
+        L = tracer_lib()
+        p = ctypes.c_void_p()
+        _check(L.rt_host_alloc(width * height * 4, ctypes.byref(p)), L, "rt_host_alloc")
+        self.ptr = p.value
+        buf = (ctypes.c_uint32 * (width * height)).from_address(self.ptr)
+        self.array = np.ctypeslib.as_array(buf).reshape(height, width)
+
+    def close(self):
+        if self.ptr:
+            self.array = None
+            tracer_lib().rt_host_free(ctypes.c_void_p(self.ptr))
+            self.ptr = None
+
+
 class GpuScene:
     """Device copy of a scene (rt_scene_create) plus the rendering entry points.
 
@@ -449,6 +488,27 @@ class GpuScene:
 
     def render_frame(self, frame):
         return self.render_tiles(frame, [(0, 0, frame.width, frame.height)])[0]
+
+    def render_frame_host(self, frame, host_frame, band_y1=()):
+        """Asynchronous whole frame into a PinnedFrame, D2H in row bands ending at band_y1;
+        follow with wait_rows()."""
+        L = tracer_lib()
+        n = len(band_y1)
+        arr = (c_u32 * max(1, n))(*band_y1)
+        _check(L.rt_render_frame_host(self._h, ctypes.byref(frame), ctypes.c_void_p(host_frame.ptr),
+                                      arr, n), L, "rt_render_frame_host")
+
+    def kernel_times(self):
+        """Render-kernel ms of the launches since the previous call (at most the last 64)."""
+        L = tracer_lib()
+        out = np.zeros(64, np.float32)
+        n = c_u32()
+        _check(L.rt_kernel_times(self._h, _ptr(out), 64, ctypes.byref(n)), L, "rt_kernel_times")
+        return out[:n.value].copy()
+
+    def wait_rows(self, y1):
+        L = tracer_lib()
+        _check(L.rt_frame_host_wait(self._h, y1), L, "rt_frame_host_wait")
 
     def render_frame_device(self, frame, d_ptr, stream=0):
         L = tracer_lib()

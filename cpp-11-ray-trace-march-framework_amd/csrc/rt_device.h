@@ -32,7 +32,7 @@ __device__ __forceinline__ uint32_t pack_bgra8(float r, float g, float b)
     return rc << 16 | gc << 8 | bc;
 }
 
-// renderer.cpp:165-168 gamma: glibc powf(x, 0.5f) is replaced by the correctly rounded
+// renderer.cpp:125-131 gamma: glibc powf(x, 0.5f) is replaced by the correctly rounded
 // sqrtf.  oracle/gamma_exhaustive.c proves pack_bgra8 of both is identical for EVERY
 // float in [0, 1.0078] (and both saturate above); the float colour differs by <= 1 ulp
 // on 678,030 inputs (hazard H6).
@@ -367,7 +367,7 @@ __device__ __forceinline__ void gen_dir(const float* m, float fov_xs, float aspe
     dz = x * m[2] + y * m[5] + z * m[8];
 }
 
-// triangle.h:158-161 + lin_alg.h:151-156 + renderer.cpp:148-155
+// triangle.h:158-161 + lin_alg.h:151-156 + renderer.cpp:110-117
 __device__ __forceinline__ void shade_hit(float u, float v, const float4& a, const float4& b, const float4& c,
                                           float& r, float& g, float& bl)
 {

@@ -1903,6 +1903,10 @@ struct HfCtx
 
 } // namespace
 
+constexpr uint32_t kTimeRing = 64;  // rt_kernel_times: launches kept
+constexpr uint32_t kMaxBands = 64;   // rt_render_frame_host: row bands per frame
+constexpr uint32_t kTileBands = 8;   // rt_render_tiles: D2H bands overlapped with the scatter
+
 struct rt_scene
 {
     int device = 0;
@@ -1943,12 +1947,22 @@ struct rt_scene
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool ev_recorded = false;
+    // render-kernel-only timing: event pair around the render kernel(s) of each launch (not the
+    // heavy-first planning kernels), a ring of the last kTimeRing launches (rt_kernel_times)
+    hipEvent_t kt0[kTimeRing] = {}, kt1[kTimeRing] = {};
+    uint32_t kt_next = 0, kt_count = 0;
     hipStream_t last_stream = nullptr;  // stream of the last launch (cross-stream ordering)
     // staging for rt_render_tiles / records
     uint32_t *d_frame = nullptr;
     size_t frame_cap = 0;
     uint32_t *h_frame = nullptr;
     size_t hframe_cap = 0;
+    // D2H row bands: rt_render_frame_host's (band_ev/band_y1, read by rt_frame_host_wait) and
+    // rt_render_tiles' own (tile_ev), each event recorded after its band's copy
+    hipEvent_t band_ev[kMaxBands] = {};
+    uint32_t band_y1[kMaxBands] = {};
+    uint32_t nbands = 0;
+    hipEvent_t tile_ev[kTileBands] = {};
 };
 
 namespace {
@@ -2208,6 +2222,23 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
     else if (lanes && P.isect == RT_ISECT_BRUTE_FORCE)
         var = kVarBrute;
     RT_HIP(hipEventRecord(s->ev0, st));
+    // kernel-time events only outside stream capture (a captured record has no time to read)
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    RT_HIP(hipStreamIsCapturing(st, &cap));
+    const bool timed = cap == hipStreamCaptureStatusNone;
+    const uint32_t kslot = s->kt_next;
+    hipEvent_t kt0 = nullptr, kt1 = nullptr;        // null stand for "not timed"
+    if (timed && !s->kt0[kslot])
+    {
+        RT_HIP(hipEventCreate(&s->kt0[kslot]));
+        RT_HIP(hipEventCreate(&s->kt1[kslot]));
+    }
+    if (timed)
+    {
+        kt0 = s->kt0[kslot];
+        kt1 = s->kt1[kslot];
+    }
+    auto mark = [&](hipEvent_t e) { return e ? hipEventRecord(e, st) : hipSuccess; };
     if (var & kVarWaveClock)
     {
         const size_t need = size_t(blocks) * kWavesPerWG * 4u;
@@ -2260,32 +2291,38 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
         P.bail_count = s->d_bail;
         P.bail_queue = s->d_bail + 1;
         RT_HIP(hipMemsetAsync(s->d_bail, 0, sizeof(uint32_t), st));
+        RT_HIP(mark(kt0));
         hipLaunchKernelGGL((k_render_bail1<kVarAuto | kVarBail>), dim3(uint32_t(blocks)), wg, 0, st, P);
         if (g16)
             hipLaunchKernelGGL((k_render_bailed<kVarWide, 16>), dim3(s->bail_wgs), wg, 0, st, P);
         else
             hipLaunchKernelGGL((k_render_bailed<kVarWide, kWideG>), dim3(s->bail_wgs), wg, 0, st, P);
+        RT_HIP(mark(kt1));
     }
     else if (wide_ok && kind == RT_KERNEL_WIDE)
     {
         const uint32_t G = g16 ? 16u : kWideG;
         P.xcd_chunk *= G;
+        RT_HIP(mark(kt0));
         if (g16)
             hipLaunchKernelGGL((k_render_wide<kVarWide, 16>), dim3(uint32_t(blocks) * G), wg, 0, st, P);
         else
             hipLaunchKernelGGL((k_render_wide<kVarWide, kWideG>), dim3(uint32_t(blocks) * G), wg, 0, st, P);
+        RT_HIP(mark(kt1));
     }
     else if (lanes && kind == RT_KERNEL_COMPACT && P.isect == RT_ISECT_GRID)
     {
         const uint32_t n_items = uint32_t(blocks * kWavesPerWG);
         const uint32_t refill = budget ? budget : kCompactRefill;
         const dim3 grid(std::max(1u, std::min(s->compact_wgs, (n_items + 3u) / 4u)));
+        RT_HIP(mark(kt0));
         if (bary)
             hipLaunchKernelGGL((k_render_compact<RT_TRI_BARYCENTRIC, kVarDistSkip>), grid, wg, 0, st, P, n_items,
                                refill);
         else
             hipLaunchKernelGGL((k_render_compact<RT_TRI_MOLLER_TRUMBORE, kVarWaveGate | kVarDistSkip | kVarOriginPre>),
                                grid, wg, 0, st, P, n_items, refill);
+        RT_HIP(mark(kt1));
     }
     else if (lanes)
     {
@@ -2301,30 +2338,64 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
             if (int rc = hf_prepare(s, P, blocks, kvar, st)) return rc;
             grid += P.hf_front;
         }
+        RT_HIP(mark(kt0));
         hipLaunchKernelGGL(fn, dim3(grid), wg, 0, st, P);
+        RT_HIP(mark(kt1));
         if (P.hf_front && P.hf_measure)
         {
             hipLaunchKernelGGL(k_hf_plan, dim3(uint32_t((blocks + kWG - 1) / kWG)), wg, 0, st, P, uint32_t(blocks));
             hipLaunchKernelGGL(k_hf_mark, dim3((P.hf_front + kWG - 1) / kWG), wg, 0, st, P);
         }
     }
-    else if (P.isect == RT_ISECT_RAY_MARCH && (f->kernel & RT_KERNEL_FLAG_EXHAUSTIVE))
-        hipLaunchKernelGGL((k_render_pixel_loop<RT_TRI_MOLLER_TRUMBORE, kVarMarch | kVarExhaustive>),
-                           dim3(uint32_t(blocks)), wg, 0, st, P);
-    else if (P.isect == RT_ISECT_RAY_MARCH)
-        hipLaunchKernelGGL((k_render_pixel_loop<RT_TRI_MOLLER_TRUMBORE, kVarMarch>), dim3(uint32_t(blocks)), wg, 0, st, P);
-    else if (P.isect == RT_ISECT_BRUTE_FORCE)
-        hipLaunchKernelGGL((k_render_pixel_loop<RT_TRI_MOLLER_TRUMBORE, kVarBrute>), dim3(uint32_t(blocks)), wg, 0, st, P);
-    else if (bary)
-        hipLaunchKernelGGL((k_render_pixel_loop<RT_TRI_BARYCENTRIC, 0>), dim3(uint32_t(blocks)), wg, 0, st, P);
     else
-        hipLaunchKernelGGL((k_render_pixel_loop<RT_TRI_MOLLER_TRUMBORE, 0>), dim3(uint32_t(blocks)), wg, 0, st, P);
+    {
+        RT_HIP(mark(kt0));
+        if (P.isect == RT_ISECT_RAY_MARCH && (f->kernel & RT_KERNEL_FLAG_EXHAUSTIVE))
+            hipLaunchKernelGGL((k_render_pixel_loop<RT_TRI_MOLLER_TRUMBORE, kVarMarch | kVarExhaustive>),
+                               dim3(uint32_t(blocks)), wg, 0, st, P);
+        else if (P.isect == RT_ISECT_RAY_MARCH)
+            hipLaunchKernelGGL((k_render_pixel_loop<RT_TRI_MOLLER_TRUMBORE, kVarMarch>), dim3(uint32_t(blocks)), wg, 0, st, P);
+        else if (P.isect == RT_ISECT_BRUTE_FORCE)
+            hipLaunchKernelGGL((k_render_pixel_loop<RT_TRI_MOLLER_TRUMBORE, kVarBrute>), dim3(uint32_t(blocks)), wg, 0, st, P);
+        else if (bary)
+            hipLaunchKernelGGL((k_render_pixel_loop<RT_TRI_BARYCENTRIC, 0>), dim3(uint32_t(blocks)), wg, 0, st, P);
+        else
+            hipLaunchKernelGGL((k_render_pixel_loop<RT_TRI_MOLLER_TRUMBORE, 0>), dim3(uint32_t(blocks)), wg, 0, st, P);
+        RT_HIP(mark(kt1));
+    }
     RT_HIP(hipGetLastError());
     RT_HIP(hipEventRecord(s->ev1, st));
     s->ev_recorded = true;
+    if (timed)
+    {
+        s->kt_next = (kslot + 1u) % kTimeRing;
+        s->kt_count = std::min(s->kt_count + 1u, kTimeRing);
+    }
     return RT_OK;
 }
 
+} // namespace
+
+namespace {
+// Device staging frame (and, for rt_render_tiles, the scene's pinned host frame) of >= words.
+int ensure_frame(rt_scene *s, size_t words, bool host)
+{
+    if (words > s->frame_cap)
+    {
+        if (s->d_frame) RT_HIP(hipFree(s->d_frame));
+        s->d_frame = nullptr;
+        RT_HIP(hipMalloc(&s->d_frame, words * 4));
+        s->frame_cap = words;
+    }
+    if (host && words > s->hframe_cap)
+    {
+        if (s->h_frame) RT_HIP(hipHostFree(s->h_frame));
+        s->h_frame = nullptr;
+        RT_HIP(hipHostMalloc(&s->h_frame, words * 4));
+        s->hframe_cap = words;
+    }
+    return RT_OK;
+}
 } // namespace
 
 int rt_internal_fail(int code, const std::string& msg) { return fail(code, msg); }
@@ -2626,6 +2697,10 @@ int rt_scene_destroy(rt_scene *s)
         if (s->h_frame) (void)hipHostFree(s->h_frame);
         if (s->ev0) (void)hipEventDestroy(s->ev0);
         if (s->ev1) (void)hipEventDestroy(s->ev1);
+        for (hipEvent_t e : s->band_ev) if (e) (void)hipEventDestroy(e);
+        for (hipEvent_t e : s->kt0) if (e) (void)hipEventDestroy(e);
+        for (hipEvent_t e : s->kt1) if (e) (void)hipEventDestroy(e);
+        for (hipEvent_t e : s->tile_ev) if (e) (void)hipEventDestroy(e);
         if (s->stream) (void)hipStreamDestroy(s->stream);
 
     }
@@ -2712,6 +2787,22 @@ int rt_last_kernel_ms(rt_scene *s, float *ms)
     return RT_OK;
 }
 
+int rt_kernel_times(rt_scene *s, float *ms, uint32_t max_n, uint32_t *n)
+{
+    if (!s || !n || (max_n && !ms)) return fail(RT_E_INVALID, "NULL argument");
+    std::lock_guard<std::mutex> lk(s->mtx);
+    const uint32_t cnt = std::min(max_n, s->kt_count);
+    for (uint32_t i = 0; i < cnt; i++)
+    {
+        const uint32_t slot = (s->kt_next + kTimeRing - cnt + i) % kTimeRing;
+        RT_HIP(hipEventSynchronize(s->kt1[slot]));
+        RT_HIP(hipEventElapsedTime(&ms[i], s->kt0[slot], s->kt1[slot]));
+    }
+    *n = cnt;
+    s->kt_count = 0;
+    return RT_OK;
+}
+
 int rt_render_tiles(rt_scene *s, const rt_frame *f, const rt_tile *tiles, uint32_t n, uint32_t *const *bufs)
 {
     if (!s || (n && (!tiles || !bufs))) return fail(RT_E_INVALID, "NULL argument");
@@ -2733,20 +2824,7 @@ int rt_render_tiles(rt_scene *s, const rt_frame *f, const rt_tile *tiles, uint32
     if ((rc = prepare_samples(s, f, spp))) return rc;
     const uint32_t rw = bx1 - bx0, rh = by1 - by0;
     const size_t words = size_t(rw) * rh;
-    if (words > s->frame_cap)
-    {
-        if (s->d_frame) RT_HIP(hipFree(s->d_frame));
-        s->d_frame = nullptr;
-        RT_HIP(hipMalloc(&s->d_frame, words * 4));
-        s->frame_cap = words;
-    }
-    if (words > s->hframe_cap)
-    {
-        if (s->h_frame) RT_HIP(hipHostFree(s->h_frame));
-        s->h_frame = nullptr;
-        RT_HIP(hipHostMalloc(&s->h_frame, words * 4));
-        s->hframe_cap = words;
-    }
+    if ((rc = ensure_frame(s, words, true))) return rc;
     KParams P;
     frame_params(s, f, P);
     P.rx0 = bx0; P.ry0 = by0; P.rw = rw; P.rh = rh;
@@ -2754,16 +2832,100 @@ int rt_render_tiles(rt_scene *s, const rt_frame *f, const rt_tile *tiles, uint32
     P.rank = 0; P.nranks = 1;
     P.out = s->d_frame; P.pitch = rw; P.shard_mode = 0;
     if ((rc = launch_render(s, f, P, P.tiles_x * ((rh + kTile - 1) / kTile), s->stream))) return rc;
-    RT_HIP(hipMemcpyAsync(s->h_frame, s->d_frame, words * 4, hipMemcpyDeviceToHost, s->stream));
-    RT_HIP(hipStreamSynchronize(s->stream));
-    for (uint32_t i = 0; i < n; i++)                             // framebuffer.h:41-45 layout
+    // D2H in row bands; band k's rows are scattered into the tiles while band k+1 is in flight
+    const uint32_t nb = std::min(kTileBands, rh), bh = (rh + nb - 1) / nb;
+    for (uint32_t b = 0; b < nb; b++)
     {
-        const rt_tile& t = tiles[i];
-        const uint32_t tw = t.x1 - t.x0;
-        for (uint32_t y = t.y0; y < t.y1; y++)
-            std::memcpy(bufs[i] + size_t(y - t.y0) * tw, s->h_frame + size_t(y - by0) * rw + (t.x0 - bx0),
-                        size_t(tw) * 4);
+        const uint32_t ya = b * bh, yb = std::min(rh, ya + bh);
+        if (ya >= yb) break;
+        if (!s->tile_ev[b]) RT_HIP(hipEventCreateWithFlags(&s->tile_ev[b], hipEventDisableTiming));
+        RT_HIP(hipMemcpyAsync(s->h_frame + size_t(ya) * rw, s->d_frame + size_t(ya) * rw,
+                              size_t(yb - ya) * rw * 4, hipMemcpyDeviceToHost, s->stream));
+        RT_HIP(hipEventRecord(s->tile_ev[b], s->stream));
     }
+    for (uint32_t b = 0; b < nb; b++)
+    {
+        const uint32_t ya = by0 + b * bh, yb = std::min(by1, ya + bh);
+        if (ya >= yb) break;
+        RT_HIP(hipEventSynchronize(s->tile_ev[b]));
+        for (uint32_t i = 0; i < n; i++)                         // framebuffer.h:41-45 layout
+        {
+            const rt_tile& t = tiles[i];
+            const uint32_t tw = t.x1 - t.x0;
+            for (uint32_t y = std::max(t.y0, ya); y < std::min(t.y1, yb); y++)
+                std::memcpy(bufs[i] + size_t(y - t.y0) * tw, s->h_frame + size_t(y - by0) * rw + (t.x0 - bx0),
+                            size_t(tw) * 4);
+        }
+    }
+    return RT_OK;
+}
+
+int rt_host_alloc(size_t bytes, void **out)
+{
+    if (!out || bytes == 0) return fail(RT_E_INVALID, "bad arguments");
+    *out = nullptr;
+    RT_HIP(hipHostMalloc(out, bytes));
+    return RT_OK;
+}
+
+int rt_host_free(void *p)
+{
+    if (p) RT_HIP(hipHostFree(p));
+    return RT_OK;
+}
+
+int rt_render_frame_host(rt_scene *s, const rt_frame *f, uint32_t *h_bgra, const uint32_t *band_y1,
+                         uint32_t nbands)
+{
+    if (!s || !h_bgra || (nbands && !band_y1)) return fail(RT_E_INVALID, "NULL argument");
+    int rc = validate_frame(f);
+    if (rc) return rc;
+    if (nbands > kMaxBands) return fail(RT_E_INVALID, "more than 64 row bands");
+    for (uint32_t b = 0; b < nbands; b++)
+        if (band_y1[b] == 0 || band_y1[b] > f->height || (b && band_y1[b] <= band_y1[b - 1]) ||
+            (b + 1 == nbands && band_y1[b] != f->height))
+            return fail(RT_E_INVALID, "band ends must increase strictly and end at the frame height");
+    std::lock_guard<std::mutex> lk(s->mtx);
+    if ((rc = ensure_device(s))) return rc;
+    const uint32_t spp = std::max(1u, f->spp);
+    if ((rc = prepare_samples(s, f, spp))) return rc;
+    const uint32_t W = f->width, H = f->height;
+    if ((rc = ensure_frame(s, size_t(W) * H, false))) return rc;
+    KParams P;
+    frame_params(s, f, P);
+    P.rx0 = 0; P.ry0 = 0; P.rw = W; P.rh = H;
+    P.tiles_x = (W + kTile - 1) / kTile;
+    P.rank = 0; P.nranks = 1;
+    P.out = s->d_frame; P.pitch = W; P.shard_mode = 0;
+    s->nbands = 0;
+    if ((rc = launch_render(s, f, P, P.tiles_x * ((H + kTile - 1) / kTile), s->stream))) return rc;
+    const uint32_t nb = nbands ? nbands : 1;
+    for (uint32_t b = 0, ya = 0; b < nb; b++)
+    {
+        const uint32_t yb = nbands ? band_y1[b] : H;
+        if (!s->band_ev[b]) RT_HIP(hipEventCreateWithFlags(&s->band_ev[b], hipEventDisableTiming));
+        RT_HIP(hipMemcpyAsync(h_bgra + size_t(ya) * W, s->d_frame + size_t(ya) * W, size_t(yb - ya) * W * 4,
+                              hipMemcpyDeviceToHost, s->stream));
+        RT_HIP(hipEventRecord(s->band_ev[b], s->stream));
+        s->band_y1[b] = yb;
+        ya = yb;
+    }
+    s->nbands = nb;
+    return RT_OK;
+}
+
+int rt_frame_host_wait(rt_scene *s, uint32_t y1)
+{
+    if (!s) return fail(RT_E_INVALID, "NULL argument");
+    hipEvent_t ev = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(s->mtx);
+        if (s->nbands == 0) return fail(RT_E_INVALID, "no rt_render_frame_host in flight");
+        uint32_t b = 0;
+        while (b + 1 < s->nbands && s->band_y1[b] < y1) b++;
+        ev = s->band_ev[b];
+    }
+    RT_HIP(hipEventSynchronize(ev));     // events are only re-recorded by a later frame
     return RT_OK;
 }
 

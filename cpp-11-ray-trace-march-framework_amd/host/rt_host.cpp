@@ -412,21 +412,35 @@ private:
     uint32_t m_frame_seed = 1;
 };
 
-// Renderer (renderer.h) with the tile callback served by the GPU: the first worker of a
-// frame renders the whole frame in ONE launch into a staging image; every worker then copies
-// its own tile while holding that tile's mutex (the reference's locking contract).
+// Renderer (renderer.h) with the tile callback served by the GPU: the first worker of a frame
+// issues the whole frame as ONE launch whose copy-back lands, tile row by tile row, in this
+// renderer's page-locked frame (rt_render_frame_host); every worker then waits only for its own
+// tile row and copies its tile straight out of that frame while holding the tile's mutex (the
+// reference's locking contract, framebuffer.cpp:71-74).  One DMA pass and one tile copy per pixel.
 class GpuRenderer : public Framebuffer
 {
 public:
     GpuRenderer(rt_scene* gpu, const rth_scene* host, uint32_t nthreads)
         : Framebuffer(nthreads), m_gpu(gpu), m_host(host) { }
-    ~GpuRenderer() override { KillAllWorkerThreads(); }
+    ~GpuRenderer() override
+    {
+        KillAllWorkerThreads();
+        DrainFrame();
+        if (m_frame) rt_host_free(m_frame);
+    }
 
-    void SetSampleCount(uint32_t cnt) { m_spp = std::max(1u, cnt); }   // renderer.cpp:56-60
+    void SetSampleCount(uint32_t cnt) { m_spp = std::max(1u, cnt); }   // renderer.cpp:18-22
     void SetOptions(uint32_t tri_test, uint32_t kernel) { m_tri_test = tri_test; m_kernel = kernel; }
     void SetIntersector(uint32_t isect) { m_isect = isect; }             // renderer.cpp:103-105
     int LastStatus() const { return m_status; }
     const std::string& LastError() const { return m_err; }
+
+    // The last frame, whole, when every tile of it was delivered (else nullptr): what
+    // SaveToBMP's assembly (framebuffer.cpp:197-216) would rebuild from the tiles.
+    const uint32_t* CompleteFrame() const
+    {
+        return (m_status == RT_OK && m_issued && m_tiles_done.load() == kTilesX * kTilesY) ? m_frame : nullptr;
+    }
 
 protected:
     void BeginFrame() override
@@ -434,6 +448,7 @@ protected:
         std::lock_guard<std::mutex> g(m_frame_mtx);
         m_frame_ready = false;
         m_status = RT_OK;
+        m_tiles_done = 0;
     }
 
     void RenderTile(Tile& tile) override
@@ -442,47 +457,96 @@ protected:
             std::lock_guard<std::mutex> g(m_frame_mtx);
             if (!m_frame_ready)
             {
-                if (m_threads_stop) return;                       // renderer.cpp:114-115
-                m_staging.assign(size_t(m_width) * m_height, 0);
-                rt_frame f;
-                std::memset(&f, 0, sizeof(f));
-                std::memcpy(f.cam, m_host->cam, sizeof(f.cam));   // Scene::GetCameraParameters
-                f.fov = m_host->fov;
-                f.width = m_width;
-                f.height = m_height;
-                f.spp = m_spp;
-                f.tri_test = m_tri_test;
-                f.kernel = m_kernel;
-                f.intersector = m_isect;
-                const rt_tile whole = { 0, 0, m_width, m_height };
-                uint32_t* dst = m_staging.data();
-                m_status = rt_render_tiles(m_gpu, &f, &whole, 1, &dst);
-                if (m_status != RT_OK)
-                {
-                    char buf[512];
-                    rt_last_error(buf, sizeof(buf));
-                    m_err = buf;
-                }
+                if (m_threads_stop) return;                       // renderer.cpp:76-77
                 m_frame_ready = true;
+                IssueFrame();
             }
+            if (m_status != RT_OK) return;
         }
-        if (m_status != RT_OK) return;
         uint32_t x0, y0, x1, y1;
         tile.GetPosition(x0, y0, x1, y1);
+        const int rc = rt_frame_host_wait(m_gpu, y1);
+        if (rc != RT_OK)
+        {
+            std::lock_guard<std::mutex> g(m_frame_mtx);
+            SetError(rc);
+            return;
+        }
         uint32_t* buf = tile.GetBuffer();
-        for (uint32_t y = 0; y < tile.GetHeight(); y++)        // renderer.cpp:171 layout
-            std::memcpy(buf + size_t(y) * tile.GetWidth(), &m_staging[size_t(y0 + y) * m_width + x0],
+        for (uint32_t y = 0; y < tile.GetHeight(); y++)        // renderer.cpp:133 layout
+            std::memcpy(buf + size_t(y) * tile.GetWidth(), m_frame + size_t(y0 + y) * m_width + x0,
                         size_t(tile.GetWidth()) * 4);
+        m_tiles_done.fetch_add(1);
     }
 
 private:
+    void SetError(int rc)
+    {
+        m_status = rc;
+        char msg[512];
+        rt_last_error(msg, sizeof(msg));
+        m_err = msg;
+    }
+
+    // A frame's copy-back may still be landing in m_frame (workers stopped early): wait it out
+    // before the frame memory is reused or freed.
+    void DrainFrame()
+    {
+        if (m_issued && m_issued_h) (void)rt_frame_host_wait(m_gpu, m_issued_h);
+        m_issued = false;
+    }
+
+    void IssueFrame()                                           // under m_frame_mtx
+    {
+        const size_t words = size_t(m_width) * m_height;
+        if (words > m_frame_cap)
+        {
+            DrainFrame();
+            if (m_frame) rt_host_free(m_frame);
+            m_frame = nullptr;
+            m_frame_cap = 0;
+            void* p = nullptr;
+            const int rc = rt_host_alloc(words * 4, &p);
+            if (rc != RT_OK) { SetError(rc); return; }
+            m_frame = static_cast<uint32_t*>(p);
+            m_frame_cap = words;
+        }
+        rt_frame f;
+        std::memset(&f, 0, sizeof(f));
+        std::memcpy(f.cam, m_host->cam, sizeof(f.cam));         // Scene::GetCameraParameters
+        f.fov = m_host->fov;
+        f.width = m_width;
+        f.height = m_height;
+        f.spp = m_spp;
+        f.tri_test = m_tri_test;
+        f.kernel = m_kernel;
+        f.intersector = m_isect;
+        // one copy-back band per tile row (framebuffer.cpp:106-117: rows of height/9, the last
+        // row absorbs the remainder)
+        uint32_t ends[kTilesY];
+        uint32_t nb = 0;
+        for (uint32_t j = 0; j < kTilesY; j++)
+        {
+            const uint32_t e = (j == kTilesY - 1) ? m_height : (j + 1) * (m_height / kTilesY);
+            if (e > (nb ? ends[nb - 1] : 0u)) ends[nb++] = e;
+        }
+        const int rc = rt_render_frame_host(m_gpu, &f, m_frame, ends, nb);
+        if (rc != RT_OK) { SetError(rc); return; }
+        m_issued = true;
+        m_issued_h = m_height;
+    }
+
     rt_scene* m_gpu;
     const rth_scene* m_host;
     uint32_t m_spp = 16;                                        // renderer.h:34
     uint32_t m_tri_test = RT_TRI_MOLLER_TRUMBORE, m_kernel = RT_KERNEL_AUTO, m_isect = RT_ISECT_GRID;
     std::mutex m_frame_mtx;
     bool m_frame_ready = false;
-    std::vector<uint32_t> m_staging;
+    uint32_t* m_frame = nullptr;                                // page-locked, m_width x m_height
+    size_t m_frame_cap = 0;
+    bool m_issued = false;
+    uint32_t m_issued_h = 0;
+    std::atomic<uint32_t> m_tiles_done{ 0 };
     int m_status = RT_OK;
     std::string m_err;
 };
@@ -665,7 +729,10 @@ int rth_framebuffer_start_rendering(rth_framebuffer* fb, double* seconds)
 int rth_framebuffer_read(const rth_framebuffer* fb, uint32_t* out)
 {
     if (!fb || !out) return fail(RT_E_INVALID, "NULL argument");
-    fb->r->Assemble(out);
+    if (const uint32_t* whole = fb->r->CompleteFrame())
+        std::memcpy(out, whole, size_t(fb->r->Width()) * fb->r->Height() * 4);
+    else
+        fb->r->Assemble(out);
     return RT_OK;
 }
 
@@ -674,8 +741,16 @@ int rth_framebuffer_save_bmp(const rth_framebuffer* fb, const char* path)
 {
     if (!fb || !path) return fail(RT_E_INVALID, "NULL argument");
     const uint32_t w = fb->r->Width(), h = fb->r->Height();
-    std::vector<uint32_t> img(size_t(w) * h);
-    fb->r->Assemble(img.data());
+    // a complete frame is written straight from the page-locked frame; otherwise the tiles are
+    // assembled as SaveToBMP does (tiles never rendered stay as they are)
+    std::vector<uint32_t> img;
+    const uint32_t* src = fb->r->CompleteFrame();
+    if (!src)
+    {
+        img.resize(size_t(w) * h);
+        fb->r->Assemble(img.data());
+        src = img.data();
+    }
     unsigned char hdr[54];
     std::memset(hdr, 0, sizeof(hdr));
     auto put16 = [&](int o, uint32_t v) { hdr[o] = v & 255; hdr[o + 1] = (v >> 8) & 255; };
@@ -691,7 +766,8 @@ int rth_framebuffer_save_bmp(const rth_framebuffer* fb, const char* path)
     put16(28, 32);              // bitcount
     std::FILE* f = std::fopen(path, "wb");
     if (!f) return fail(RT_E_INVALID, std::string("cannot write ") + path);
-    const bool ok = std::fwrite(hdr, 1, 54, f) == 54 && std::fwrite(img.data(), 4, img.size(), f) == img.size();
+    const size_t n = size_t(w) * h;
+    const bool ok = std::fwrite(hdr, 1, 54, f) == 54 && std::fwrite(src, 4, n, f) == n;
     std::fclose(f);
     return ok ? RT_OK : fail(RT_E_INVALID, "short write");
 }

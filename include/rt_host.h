@@ -77,7 +77,7 @@ typedef struct rth_framebuffer rth_framebuffer;
 int  rth_framebuffer_create(rt_scene *gpu_scene, const rth_scene *host_scene, uint32_t nthreads,
                             rth_framebuffer **out);
 void rth_framebuffer_free(rth_framebuffer *fb);
-int  rth_framebuffer_set_sample_count(rth_framebuffer *fb, uint32_t spp);   /* renderer.cpp:56-60 */
+int  rth_framebuffer_set_sample_count(rth_framebuffer *fb, uint32_t spp);   /* renderer.cpp:18-22 */
 int  rth_framebuffer_set_options(rth_framebuffer *fb, uint32_t tri_test, uint32_t kernel);
 /* Which of Renderer::RenderTile's intersectors runs (renderer.cpp:103-105; enum rt_intersector). */
 int  rth_framebuffer_set_intersector(rth_framebuffer *fb, uint32_t intersector);

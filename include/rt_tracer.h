@@ -6,7 +6,9 @@
  *
  *   reference interface                                   replaced by
  *   ----------------------------------------------------  ---------------------------------
- *   Renderer::RenderTile(Tile&)      renderer.cpp:43-136   rt_render_tiles / rt_render_frame_device
+ *   Renderer::RenderTile(Tile&)      renderer.cpp:43-136   rt_render_frame_host + rt_frame_host_wait
+ *                                                          (the Framebuffer's tiles, framebuffer.cpp:
+ *                                                          59-92), rt_render_tiles, rt_render_frame_device
  *     per-pixel / per-sample loops   renderer.cpp:74-135   (one batched HIP launch per frame)
  *   GenerateRay (perspective)        camera.h:8-47         in-kernel, from rt_frame
  *   Grid::Intersect (3D-DDA)         grid.cpp:159-281      in-kernel, CSR cells from rt_grid_desc
@@ -34,7 +36,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 3
+#define RT_ABI_VERSION 4
 
 enum rt_status {
     RT_OK = 0,
@@ -179,9 +181,24 @@ int  rt_scene_create_from_mesh(const rt_vertex *vertices, uint32_t num_vertices,
 /* ---- rendering --------------------------------------------------------------------- */
 /* Renders every listed tile in ONE batched launch (over the tiles' bounding box), copies
  * back and scatters into the caller's host buffers: tile_bufs[i][(x-x0) + (y-y0)*(x1-x0)]
- * = 0x00RRGGBB, exactly the words renderer.cpp:133 stores.  Synchronous. */
+ * = 0x00RRGGBB, exactly the words renderer.cpp:133 stores.  The copy-back runs in 8 row bands,
+ * each band scattered while the next is in flight.  Synchronous. */
 int  rt_render_tiles(rt_scene *scene, const rt_frame *frame, const rt_tile *tiles,
                      uint32_t n_tiles, uint32_t *const *tile_bufs);
+
+/* Whole frame to host memory, asynchronously: one launch, then the D2H copy in row bands
+ * [0, band_y1[0]), [band_y1[0], band_y1[1]), ... (strictly increasing, last = height; nbands <= 64,
+ * 0 = one band).  h_bgra[y*width + x] = 0x00RRGGBB; page-locked memory from rt_host_alloc makes
+ * the copy a DMA.  rt_frame_host_wait(scene, y1) blocks until rows [0, y1) have landed, so the
+ * reference's tile workers (framebuffer.cpp:59-92) each copy their tile out of h_bgra as soon as
+ * its tile row is there -- the drop-in for RenderTile's per-tile buffer writes, renderer.cpp:133.
+ * Call the wait (for y1 = height at least once) before reusing h_bgra or the scene. */
+int  rt_render_frame_host(rt_scene *scene, const rt_frame *frame, uint32_t *h_bgra,
+                          const uint32_t *band_y1, uint32_t nbands);
+int  rt_frame_host_wait(rt_scene *scene, uint32_t y1);
+/* Page-locked host memory (hipHostMalloc) for rt_render_frame_host. */
+int  rt_host_alloc(size_t bytes, void **out);
+int  rt_host_free(void *p);
 
 /* Device-resident frame: d_bgra[y*width + x] on the caller's HIP stream (NULL = default
  * stream).  Asynchronous: never waits on the host.  Allocates only for the first frame of a
@@ -204,6 +221,10 @@ int  rt_unshard_device(uint32_t width, uint32_t height, uint32_t nranks,
 /* Kernel time of the last rendering call on this scene measured with HIP events on the
  * launch stream (ms), for roofline accounting.  Only valid after that stream completed. */
 int  rt_last_kernel_ms(rt_scene *scene, float *ms);
+/* Render-kernel durations (ms, HIP events recorded on the launch stream immediately around the
+ * render kernel(s) of each launch -- not the heavy-first planning kernels), for the launches since
+ * the previous call, oldest first, at most max_n and at most the last 64.  Waits for them. */
+int  rt_kernel_times(rt_scene *scene, float *ms, uint32_t max_n, uint32_t *n);
 
 /* ---- parity / debug ---------------------------------------------------------------- */
 /* Per-sample records for pixels [x0,x0+w) x [y0,y0+h), order (y, x, sample).  Synchronous. */

@@ -322,7 +322,7 @@ inline void GenRay(const float m[4][4], uint32_t px, uint32_t py, uint32_t W, ui
            p.x * m[0][2] + p.y * m[1][2] + p.z * m[2][2]);
 }
 
-// triangle.h:158-161 BarycentricInterpolate + Normalize + renderer.cpp:155 (n+1)*0.5
+// triangle.h:158-161 BarycentricInterpolate + Normalize + renderer.cpp:117 (n+1)*0.5
 inline V3 ShadeHit(float u, float v, const V3& n0, const V3& n1, const V3& n2)
 {
     const float w = 1.0f - u - v;
@@ -342,7 +342,7 @@ inline uint32_t Pack(float r, float g, float b)
     return rc << 16 | gc << 8 | bc;
 }
 
-// sampling.h:113-120 + sampling.cpp:194-210 (base 2) + renderer.cpp:90-93
+// sampling.h:113-120 + sampling.cpp:194-210 (base 2) + renderer.cpp:52-55
 std::vector<float> Hammersley(uint32_t spp)
 {
     std::vector<float> xy(size_t(spp) * 2);
@@ -361,19 +361,28 @@ std::vector<float> Hammersley(uint32_t spp)
 }
 
 // -------------------------------------------------------------- grid traversal
-// grid.cpp:159-281 Grid::Intersect (NEW_GRID_TRAVERSAL), instrumented with counters
-bool Intersect(const Scene& s, const V3& o, const V3& d, int tri_test, float& t, float& u, float& v,
-               uint32_t& tri_idx, uint32_t& voxel, uint32_t& steps, uint32_t& tests)
+// grid.cpp:159-281 Grid::Intersect (NEW_GRID_TRAVERSAL), instrumented with counters.  Like the
+// reference (origin/dir by value, grid.cpp:160-161) the walk runs on locals: results and counters
+// are stored once at the end, so no store inside the loop can alias the ray or the scene arrays.
+template <int TRI_TEST>
+bool IntersectT(const Scene& s, const V3 o, const V3 d, float& t_out, float& u_out, float& v_out,
+                uint32_t& tri_out, uint32_t& voxel_out, uint32_t& steps_out, uint32_t& tests_out)
 {
-    steps = tests = 0;
-    voxel = 0xFFFFFFFFu;
+    uint32_t steps = 0, tests = 0, voxel = 0xFFFFFFFFu;
     float enter_t, leave_t;
     V3 g;
+    bool found = false;
+    float t = std::numeric_limits<float>::max(), u = 0.0f, v = 0.0f;
+    uint32_t tri_idx = tri_out;
     if (PointAABB(o, s.aabb_min, s.aabb_max)) { enter_t = 0.0f; g = o; }
     else if (RayAABB(o, d, s.aabb_min, s.aabb_max, enter_t, leave_t))
         g = mk(o.x + d.x * enter_t, o.y + d.y * enter_t, o.z + d.z * enter_t);
     else
+    {
+        steps_out = tests_out = 0;
+        voxel_out = voxel;
         return false;
+    }
 
     float nct[3], dt[3] = { 0, 0, 0 };
     int step[3] = { 0, 0, 0 }, out[3] = { 0, 0, 0 }, pos[3];
@@ -398,33 +407,46 @@ bool Intersect(const Scene& s, const V3& o, const V3& d, int tri_test, float& t,
             out[a] = -1;
         }
     }
-    t = std::numeric_limits<float>::max();
+    const uint32_t *off = s.off.data(), *refs = s.refs.data();
+    const Triangle *tris = s.tris.data();
+    const Vertex *verts = s.verts.data();
     while (true)
     {
         const int ax = (nct[0] < nct[1]) ? ((nct[0] < nct[2]) ? 0 : 2) : ((nct[1] < nct[2]) ? 1 : 2);
         const uint32_t cell = s.GridIdx(pos[0], pos[1], pos[2]);
         voxel = cell;
         steps++;
-        for (uint32_t k=s.off[cell]; k<s.off[cell + 1]; k++)
+        const uint32_t k1 = off[cell + 1];
+        for (uint32_t k=off[cell]; k<k1; k++)
         {
-            const uint32_t ci = s.refs[k];
-            const Triangle& tr = s.tris[ci];
+            const uint32_t ci = refs[k];
+            const Triangle& tr = tris[ci];
             float ct, cu, cv;
             tests++;
-            const bool hit = tri_test == 1
-                ? RayTriBary(o, d, s.verts[tr.v0].p, s.verts[tr.v1].p, s.verts[tr.v2].p, tr.n, ct, cu, cv)
-                : RayTri(o, d, s.verts[tr.v0].p, s.verts[tr.v1].p, s.verts[tr.v2].p, ct, cu, cv);
+            const bool hit = TRI_TEST == 1
+                ? RayTriBary(o, d, verts[tr.v0].p, verts[tr.v1].p, verts[tr.v2].p, tr.n, ct, cu, cv)
+                : RayTri(o, d, verts[tr.v0].p, verts[tr.v1].p, verts[tr.v2].p, ct, cu, cv);
             if (hit && ct < t && ct < nct[ax])
             {
                 t = ct; u = cu; v = cv; tri_idx = ci;
             }
         }
-        if (t != std::numeric_limits<float>::max()) return true;
+        if (t != std::numeric_limits<float>::max()) { found = true; break; }
         pos[ax] += step[ax];
         if (pos[ax] == out[ax]) break;
         nct[ax] += dt[ax];
     }
-    return false;
+    t_out = t;
+    if (found) { u_out = u; v_out = v; tri_out = tri_idx; }
+    voxel_out = voxel; steps_out = steps; tests_out = tests;
+    return found;
+}
+
+inline bool Intersect(const Scene& s, const V3& o, const V3& d, int tri_test, float& t, float& u, float& v,
+                      uint32_t& tri_idx, uint32_t& voxel, uint32_t& steps, uint32_t& tests)
+{
+    return tri_test == 1 ? IntersectT<1>(s, o, d, t, u, v, tri_idx, voxel, steps, tests)
+                         : IntersectT<0>(s, o, d, t, u, v, tri_idx, voxel, steps, tests);
 }
 
 // renderer.cpp:157-197 Renderer::IntersectBruteForce: all triangles in index order, closest
@@ -506,7 +528,7 @@ bool RayMarch(const Scene& s, const V3& o, const V3& d, float& t, uint32_t& step
     return false;
 }
 
-// renderer.cpp:126-160: one sample.  mode = tri_test | intersector << 8 (rt_intersector)
+// renderer.cpp:90-121: one sample.  mode = tri_test | intersector << 8 (rt_intersector)
 inline V3 TraceSample(const Scene& s, const float* smp, uint32_t px, uint32_t py, uint32_t W, uint32_t H,
                       uint32_t si, int mode, orc_rec *rec)
 {
@@ -546,7 +568,7 @@ inline V3 TraceSample(const Scene& s, const float* smp, uint32_t px, uint32_t py
     return c;
 }
 
-// renderer.cpp:81-174 Renderer::RenderTile
+// renderer.cpp:43-136 Renderer::RenderTile
 void RenderTile(const Scene& s, uint32_t W, uint32_t H, uint32_t spp, int tri_test,
                 uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1, uint32_t *buf, uint32_t *hit_ids)
 {
@@ -683,7 +705,7 @@ int orc_render(const orc_scene *h, uint32_t W, uint32_t H, uint32_t spp, uint32_
                uint32_t nthreads, uint32_t *out, uint32_t *hit_ids, double *seconds)
 {
     if (!h || !out || W == 0 || H == 0) return 1;
-    spp = std::max(1u, spp);                                     // renderer.cpp:59
+    spp = std::max(1u, spp);                                     // renderer.cpp:21
     if (nthreads == 0) nthreads = std::max(1u, std::thread::hardware_concurrency());
     // framebuffer.cpp:94-122: 12 x 9 tiles, edge tiles absorb the remainder
     const uint32_t TX = 12, TY = 9, tw = W / TX, th = H / TY;

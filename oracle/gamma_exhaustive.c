@@ -1,6 +1,6 @@
 /* oracle/gamma_exhaustive.c -- TEST INFRASTRUCTURE ONLY (tests/test_gamma_exhaustive.py).
  *
- * Proves hazard H6 away: the reference gammas with glibc powf(x, 0.5f) (renderer.cpp:165-168)
+ * Proves hazard H6 away: the reference gammas with glibc powf(x, 0.5f) (renderer.cpp:125-131)
  * and packs with ToBGRA8 (lin_alg.h:125-132); the HIP kernel uses the correctly rounded
  * sqrtf.  For EVERY float x in [0, 0x3F810000] (= [0, 1.0078]; averaged colours lie in
  * [0, 1 + 2 ulp]) this counts inputs where the float results differ and where the packed

@@ -17,8 +17,11 @@ import subprocess
 import sys
 import tempfile
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REF = os.path.join(ROOT, "oracle", "_ref", "refdriver")
+REF_INSTR = os.path.join(ROOT, "oracle", "_ref", "refdriver_instr")   # grid.cpp + ref_instr.h
 GOLD = os.path.join(ROOT, "tests", "golden")
 SCENES = os.path.join(ROOT, "data", "scenes")
 MESHES = "/root/reference/meshes"
@@ -32,8 +35,8 @@ SMALL_FRAMES = [(s, 128, 96, 4) for s in range(10)] + [
 CROPS = [(952, 532), (640, 720), (1500, 300)]
 
 
-def run(args):
-    out = subprocess.run([REF] + args, check=True, capture_output=True, text=True).stdout
+def run(args, exe=REF):
+    out = subprocess.run([exe] + args, check=True, capture_output=True, text=True).stdout
     line = [l for l in out.splitlines() if l.startswith("RESULT ")][-1]
     return json.loads(line[len("RESULT "):])
 
@@ -52,10 +55,74 @@ def sha(path):
         return hashlib.sha256(f.read()).hexdigest()
 
 
+SAMPLE_RECORD = ("hit u32, tri u32, t f32, u f32, v f32, r f32, g f32, b f32, voxel u32, steps u32, "
+                 "tests u32 (t,u,v = 0 and tri = 0xFFFFFFFF on miss; voxel = last GridIdx the "
+                 "reference's walk evaluated, 0xFFFFFFFF if none; steps = its DDA iterations; "
+                 "tests = its IntersectRayTri calls)")
+
+
+def bmp_golden(tmp):
+    """Framebuffer::SaveToBMP -> WriteBitmap (framebuffer.cpp:195-221, bmp_writer.cpp:27-57) of
+    scene 1 at 1920x1080x4: the reference's own writer, linked into refdriver.  The 8.3 MB file
+    is pinned by its SHA-256 and its 54-byte header (kept verbatim)."""
+    bp = os.path.join(tmp, "scene1.bmp")
+    run(["render", os.path.join(SCENES, "scene1.rtscene"), "1920", "1080", "4", "--bmp", bp])
+    with open(bp, "rb") as f:
+        raw = f.read()
+    assert len(raw) == 54 + 1920 * 1080 * 4
+    return {"scene": 1, "W": 1920, "H": 1080, "spp": 4, "bytes": len(raw),
+            "sha256": hashlib.sha256(raw).hexdigest(), "header_hex": raw[:54].hex()}
+
+
+def crop_records(tmp):
+    """16x16 crops at 1920x1080x4, one 11-word record per sample.  Columns 0-7 come from the
+    plain refdriver; voxel/steps/tests from refdriver_instr, whose own columns 0-7 must equal
+    the plain build's bit for bit (the instrumentation only counts)."""
+    crops = []
+    for sid in range(10):
+        for (x0, y0) in CROPS:
+            name = f"scene{sid}_crop{x0}_{y0}"
+            args = ["samples", os.path.join(SCENES, f"scene{sid}.rtscene"), "1920", "1080", "4",
+                    str(x0), str(y0), "16", "16"]
+            pp, ip = os.path.join(tmp, "plain.rec"), os.path.join(tmp, "instr.rec")
+            run(args + [pp])
+            run(args + [ip], exe=REF_INSTR)
+            with open(pp, "rb") as f:
+                plain = np.frombuffer(f.read(), "<u4").reshape(-1, 8)
+            with open(ip, "rb") as f:
+                inst = np.frombuffer(f.read(), "<u4").reshape(-1, 11)
+            assert np.array_equal(plain, inst[:, :8]), name
+            hit = inst[:, 0] == 1
+            assert (inst[hit, 8] != 0xFFFFFFFF).all() and (inst[hit, 9] >= 1).all(), name
+            out = os.path.join(GOLD, "samples", name + ".rec")
+            with open(out, "wb") as f:
+                f.write(inst.tobytes())
+            gz(out)
+            crops.append({"scene": sid, "W": 1920, "H": 1080, "spp": 4, "x0": x0, "y0": y0,
+                          "w": 16, "h": 16, "name": name})
+    return crops
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-head", action="store_true")
+    ap.add_argument("--only", choices=["crops", "bmp"],
+                    help="regenerate one section and merge it into the existing golden.json")
     a = ap.parse_args()
+    if a.only:
+        path = os.path.join(GOLD, "golden.json")
+        with open(path) as f:
+            meta = json.load(f)
+        tmp = tempfile.mkdtemp()
+        if a.only == "crops":
+            meta["crops"] = crop_records(tmp)
+        else:
+            meta["bmp"] = bmp_golden(tmp)
+        meta["sample_record"] = SAMPLE_RECORD
+        with open(path, "w") as f:
+            json.dump(meta, f, indent=1, sort_keys=True)
+        print("updated", a.only, "in", path)
+        return
     if not os.path.exists(REF):
         sys.exit("build oracle/_ref/refdriver first: make -C oracle ref")
     os.makedirs(GOLD, exist_ok=True)
@@ -124,22 +191,12 @@ def main():
         gz(hp)
         small.append({"scene": sid, "W": w, "H": h, "spp": spp, "name": name})
 
-    crops = []
-    for sid in range(10):
-        for (x0, y0) in CROPS:
-            name = f"scene{sid}_crop{x0}_{y0}"
-            run(["samples", os.path.join(SCENES, f"scene{sid}.rtscene"), "1920", "1080", "4",
-                 str(x0), str(y0), "16", "16", os.path.join(GOLD, "samples", name + ".rec")])
-            gz(os.path.join(GOLD, "samples", name + ".rec"))
-            crops.append({"scene": sid, "W": 1920, "H": 1080, "spp": 4, "x0": x0, "y0": y0,
-                          "w": 16, "h": 16, "name": name})
-
+    crops = crop_records(tmp)
     meta = {
         "generator": "oracle/gen_golden.py via oracle/_ref/refdriver (reference sources, g++ "
                      "-O3 -std=c++11, no -march)",
         "scenes": scenes, "frames_1080p4": frames, "small_frames": small, "crops": crops,
-        "sample_record": "hit u32, tri u32, t f32, u f32, v f32, r f32, g f32, b f32 "
-                         "(t,u,v = 0 and tri = 0xFFFFFFFF on miss)",
+        "sample_record": SAMPLE_RECORD, "bmp": bmp_golden(tmp),
     }
     with open(os.path.join(GOLD, "golden.json"), "w") as f:
         json.dump(meta, f, indent=1, sort_keys=True)

@@ -13,7 +13,7 @@
 // What is restated here (because renderer.cpp / framebuffer.cpp / application.cpp
 // include <OpenGL/gl.h> or GLUT, which this image lacks -- unbuildable):
 //   * the scene table of Application::InitializeScene        (application.cpp:304-517)
-//   * the per-pixel/per-sample loop body of Renderer::RenderTile (renderer.cpp:81-174)
+//   * the per-pixel/per-sample loop body of Renderer::RenderTile (renderer.cpp:43-136)
 //   * the 12x9 std::thread tile pool of Framebuffer           (framebuffer.cpp:10-130)
 //   * the loops of Renderer::IntersectBruteForce / DistanceBruteForce / RayMarch
 //     (renderer.cpp:24-41, 138-197) around the reference's IntersectRayTri / DistancePointTri
@@ -22,8 +22,10 @@
 // Subcommands (all output little-endian binary files or one "RESULT {json}" line):
 //   dump-scenes <meshdir> <outdir>           post-setup meshes + cameras -> <outdir>/scene<i>.rtscene
 //   grid   <scene.rtscene> <out.bin>         grid meta + CSR export of Grid::Grid's cells
-//   render <scene.rtscene> W H spp [--threads N] [--reps R] [--out f] [--hits f]
-//   samples <scene.rtscene> W H spp x0 y0 w h <out.bin>    per-sample records
+//   render <scene.rtscene> W H spp [--threads N] [--reps R] [--out f] [--hits f] [--bmp f]
+//                                            --bmp: the reference's WriteBitmap of the gathered frame
+//   samples <scene.rtscene> W H spp x0 y0 w h <out.bin>    per-sample records; refdriver_instr
+//                                            (grid.cpp + ref_instr.h) appends voxel, steps, tests
 //   alt-samples <scene.rtscene> W H spp x0 y0 w h brute|march <out.bin>
 //                                            records of Renderer::IntersectBruteForce / RayMarch
 //   render ... [--isect grid|brute|march]   the frame with another intersector (renderer.cpp:103-105)
@@ -55,6 +57,13 @@
 #include "triangle.h"
 #include "aabb.h"
 #include "timer.h"
+#include "bmp_writer.h"
+
+#ifdef RT_REF_INSTR
+#define RT_REF_INSTR_NO_HOOKS
+#include "ref_instr.h"
+thread_local RtRefWalk g_rt_ref_walk;   // written by the instrumented grid.cpp (ref_instr.h)
+#endif
 
 namespace {
 
@@ -308,7 +317,7 @@ struct GridExport : public Grid
     }
 };
 
-// ----------------------------------------- per-sample loop (renderer.cpp:81-174, glue only)
+// ----------------------------------------- per-sample loop (renderer.cpp:74-135, glue only)
 struct Frame
 {
     const Grid *grid;
@@ -365,7 +374,7 @@ bool RayMarchRef(const Mesh *mesh, Vec3f origin, Vec3f dir, float& t, uint& step
 
 std::vector<Vec2f> SampleTable(uint spp)
 {
-    // renderer.cpp:87-98
+    // renderer.cpp:49-60
     std::vector<Vec2f> smp_loc(spp);
     for (uint smp=0; smp<spp; smp++)
     {
@@ -375,7 +384,15 @@ std::vector<Vec2f> SampleTable(uint spp)
     return smp_loc;
 }
 
-struct SampleRec { uint32 hit, tri; float t, u, v, r, g, b; };
+// u32 hit, tri | f32 t, u, v, r, g, b [| u32 voxel, steps, tests in the instrumented build]
+struct SampleRec
+{
+    uint32 hit, tri;
+    float t, u, v, r, g, b;
+#ifdef RT_REF_INSTR
+    uint32 voxel, steps, tests;
+#endif
+};
 
 // One tile, exactly the reference's arithmetic order; optionally records per-sample hits.
 void RenderTileRef(const Frame& fr, uint x0, uint y0, uint x1, uint y1, uint32 *buf,
@@ -481,7 +498,7 @@ struct TilePool
         return TimerGetTick() - t0;
     }
 
-    void Gather(std::vector<uint32>& img) const
+    void Gather(std::vector<uint32>& img) const                 // framebuffer.cpp:197-216
     {
         img.assign(size_t(width) * height, 0);
         for (const auto& t : tiles)
@@ -705,7 +722,7 @@ int CmdKat(const char *outdir)
         WriteFile((dir + "/kat_bgra8.f32").c_str(), &rec[0], rec.size() * 4);
     }
 
-    // ---- Hammersley sample tables (renderer.cpp:87-98) for spp 1..64 and 128, 256
+    // ---- Hammersley sample tables (renderer.cpp:49-60) for spp 1..64 and 128, 256
     {
         std::vector<float> rec;
         std::vector<uint> spps;
@@ -849,6 +866,9 @@ int main(int argc, char **argv)
                         SampleRec r;
                         float t = 0, u = 0, v = 0;
                         uint32 tri = 0xFFFFFFFFu;
+#ifdef RT_REF_INSTR
+                        g_rt_ref_walk = RtRefWalk{0xFFFFFFFFu, 0u, 0u};
+#endif
                         const bool hit = grid.Intersect(origin, dir, t, u, v, tri);
                         Vec3f c;
                         if (hit)
@@ -867,6 +887,10 @@ int main(int argc, char **argv)
                         }
                         r.hit = hit; r.tri = tri; r.t = t; r.u = u; r.v = v;
                         r.r = c.x; r.g = c.y; r.b = c.z;
+#ifdef RT_REF_INSTR
+                        r.voxel = g_rt_ref_walk.cell; r.steps = g_rt_ref_walk.steps;
+                        r.tests = g_rt_ref_walk.tests;
+#endif
                         recs.push_back(r);
                     }
             if (!WriteFile(argv[10], &recs[0], recs.size() * sizeof(SampleRec))) return 1;
@@ -931,7 +955,7 @@ int main(int argc, char **argv)
         // render
         uint nthreads = std::max(1u, std::thread::hardware_concurrency());   // framebuffer.cpp:11
         uint reps = 1;
-        const char *out = nullptr, *hits = nullptr;
+        const char *out = nullptr, *hits = nullptr, *bmp = nullptr;
         for (int i=6; i<argc; i++)
         {
             const std::string a = argv[i];
@@ -939,6 +963,7 @@ int main(int argc, char **argv)
             else if (a == "--reps" && i + 1 < argc) reps = std::atoi(argv[++i]);
             else if (a == "--out" && i + 1 < argc) out = argv[++i];
             else if (a == "--hits" && i + 1 < argc) hits = argv[++i];
+            else if (a == "--bmp" && i + 1 < argc) bmp = argv[++i];
             else if (a == "--isect" && i + 1 < argc)
             {
                 const std::string m = argv[++i];
@@ -959,6 +984,7 @@ int main(int argc, char **argv)
         pool.Gather(img);
         if (out && !WriteFile(out, &img[0], img.size() * 4)) return 1;
         if (hits && !WriteFile(hits, &hit_ids[0], hit_ids.size() * 4)) return 1;
+        if (bmp) WriteBitmap(bmp, fr.width, fr.height, &img[0]);   // bmp_writer.cpp:27-57 (SaveToBMP's call)
         std::printf("RESULT {\"threads\": %u, \"reps\": %u, \"median_s\": %.6f, \"first_s\": %.6f, "
                     "\"samples\": %llu, \"msamples_per_s\": %.3f, \"grid_build_s\": %.6f}\n",
                     nthreads, reps, med, times[0],

@@ -25,7 +25,7 @@ class CpuWorkload:
         self.frames = [None for _ in scenes]
         self.renders = 0
 
-    def render(self, i, record):
+    def render(self, i):
         shard = self.rtm.shard_from_frame(self.full[i], self.rank, self.world)
         self.bufs[i].copy_(torch.from_numpy(shard.view(np.int32)))
         self.renders += 1
@@ -34,6 +34,9 @@ class CpuWorkload:
         self.frames[i] = self.rtm.frame_from_shards(gathered.numpy().view(np.uint32), W, H, self.world)
 
     def sync(self):
+        pass
+
+    def reset_times(self):
         pass
 
 

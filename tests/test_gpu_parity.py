@@ -107,15 +107,16 @@ def test_small_frames_all_kernels(golden, scenes):
 
 
 def test_crop_records_vs_reference_and_oracle(golden, scenes, oracle):
-    """Per sample: hit/tri exact vs the reference; voxel GridIdx, DDA steps, tri tests exact vs
-    the oracle; t, u, v and colour bit-exact (tolerance 1e-5 is the contract)."""
+    """Per sample, exact vs the reference's own walk (instrumented refdriver fixtures): hit, tri,
+    voxel GridIdx of the accepted cell (last cell on a miss), DDA steps and triangle tests; t, u,
+    v and colour bit-exact (tolerance 1e-5 is the contract).  Then the same vs the oracle."""
     for c in golden["crops"]:
         hs, gs = scenes(c["scene"])
         f = gs.frame(c["W"], c["H"], c["spp"])
         got = gs.trace_samples(f, c["x0"], c["y0"], c["w"], c["h"])
-        ref = read_gz(os.path.join("samples", c["name"] + ".rec.gz"), "<u4").reshape(-1, 8)
-        np.testing.assert_array_equal(got["hit"], ref[:, 0], err_msg=c["name"])
-        np.testing.assert_array_equal(got["tri"], ref[:, 1], err_msg=c["name"])
+        ref = read_gz(os.path.join("samples", c["name"] + ".rec.gz"), "<u4").reshape(-1, 11)
+        for j, k in ((0, "hit"), (1, "tri"), (8, "voxel"), (9, "steps"), (10, "tests")):
+            np.testing.assert_array_equal(got[k], ref[:, j], err_msg=f"{c['name']} {k}")
         for j, k in enumerate(("t", "u", "v", "r", "g", "b")):
             np.testing.assert_array_equal(bits(got[k]), ref[:, 2 + j], err_msg=f"{c['name']} {k}")
         orc = oracle.records(c["scene"], c["W"], c["H"], c["spp"], c["x0"], c["y0"], c["w"], c["h"])
@@ -318,7 +319,7 @@ def test_head_4096x4096x16(golden, scenes):
 
 
 def test_render_tiles_subset(scenes):
-    """rt_render_tiles fills arbitrary tile buffers exactly as the full frame (renderer.cpp:171)."""
+    """rt_render_tiles fills arbitrary tile buffers exactly as the full frame (renderer.cpp:133)."""
     hs, gs = scenes(8)
     f = gs.frame(640, 480, 4)
     full = gs.render_frame(f)
@@ -378,6 +379,19 @@ def test_render_frame_device_on_torch_stream(golden, scenes):
     assert gs.last_kernel_ms() > 0
 
 
+def test_kernel_times_ring(scenes):
+    """rt_kernel_times: one positive render-kernel time per launch since the previous call."""
+    import torch
+    hs, gs = scenes(1)
+    out = torch.zeros(1920 * 1080, dtype=torch.int32, device="cuda")
+    gs.kernel_times()
+    for _ in range(3):
+        gs.render_frame_device(gs.frame(1920, 1080, 4), out.data_ptr(), 0)
+    t = gs.kernel_times()
+    assert len(t) == 3 and (t > 0.01).all() and (t < 50).all()
+    assert len(gs.kernel_times()) == 0
+
+
 def test_framebuffer_tile_pool_drop_in(golden, scenes, tmp_path):
     """The host Framebuffer (12x9 tiles, worker pool) with the GPU RenderTile override."""
     hs, gs = scenes(1)
@@ -389,11 +403,55 @@ def test_framebuffer_tile_pool_drop_in(golden, scenes, tmp_path):
     bmp = tmp_path / "shot.bmp"
     r.save_to_bmp(str(bmp))
     data = bmp.read_bytes()
-    assert data[:2] == b"BM" and len(data) == 54 + 1920 * 1080 * 4
+    gb = golden["bmp"]
+    assert gb["scene"] == 1 and (gb["W"], gb["H"], gb["spp"]) == (1920, 1080, 4)
+    # byte for byte the reference's SaveToBMP -> WriteBitmap file, 54-byte header included
+    assert data[:54].hex() == gb["header_hex"]
+    assert len(data) == gb["bytes"] and hashlib.sha256(data).hexdigest() == gb["sha256"]
     assert data[54:] == img.tobytes()
     r.start_rendering()
     assert hashlib.sha256(r.read().tobytes()).hexdigest() == golden["frames_1080p4"]["1"]["bgra_sha256"]
     r.close()
+
+
+def test_framebuffer_ragged_frames(golden, scenes):
+    """The tile pool on frames whose 12x9 tiles are ragged or empty (copy-back bands per tile
+    row collapse when height < 9) equals the reference's small-frame fixtures."""
+    hs, gs = scenes(1)
+    r = rtm.Renderer(hs, gs)
+    for fr in golden["small_frames"]:
+        if fr["scene"] != 1:
+            continue
+        W, H, spp = fr["W"], fr["H"], fr["spp"]
+        exp = read_gz(os.path.join("frames", fr["name"] + ".bgra.gz"), "<u4").reshape(H, W)
+        r.set_sample_count(spp)
+        r.resize(W, H)
+        np.testing.assert_array_equal(r.read(), exp, err_msg=fr["name"])
+    r.close()
+
+
+def test_render_frame_host_bands(golden, scenes):
+    """rt_render_frame_host: banded copy-back into page-locked memory; rows [0, y1) are final
+    once rt_frame_host_wait(y1) returns; the whole frame equals the reference's."""
+    hs, gs = scenes(8)
+    pf = rtm.PinnedFrame(1920, 1080)
+    try:
+        ends = [120 * (j + 1) for j in range(8)] + [1080]
+        for rep in range(2):
+            pf.array[:] = 0xDEADBEEF
+            gs.render_frame_host(gs.frame(1920, 1080, 4), pf, ends)
+            gs.wait_rows(120)
+            head = pf.array[:120].copy()
+            gs.wait_rows(1080)
+            np.testing.assert_array_equal(head, pf.array[:120])
+            assert hashlib.sha256(pf.array.tobytes()).hexdigest() == golden["frames_1080p4"]["8"]["bgra_sha256"]
+        with pytest.raises(rtm.RtError):
+            gs.render_frame_host(gs.frame(1920, 1080, 4), pf, [500, 400, 1080])
+        gs.render_frame_host(gs.frame(1920, 1080, 4), pf)                    # one band
+        gs.wait_rows(1080)
+        assert hashlib.sha256(pf.array.tobytes()).hexdigest() == golden["frames_1080p4"]["8"]["bgra_sha256"]
+    finally:
+        pf.close()
 
 
 def test_scene_validation_fails_loudly():

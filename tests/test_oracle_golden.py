@@ -58,19 +58,19 @@ def test_kat_genray(oracle):
 
 
 def test_kat_gamma_pack(oracle):
-    """std::pow(x, 0.5f) gamma + ToBGRA8 (renderer.cpp:163-171, lin_alg.h:125-132)."""
+    """std::pow(x, 0.5f) gamma + ToBGRA8 (renderer.cpp:124-133, lin_alg.h:125-132)."""
     rin, exp = load_kat("bgra8")
     np.testing.assert_array_equal(bits(oracle.kat("bgra8", rin, 4)), bits(exp))
 
 
 def test_kat_shade(oracle):
-    """BarycentricInterpolate + Normalize + (n+1)*0.5 (triangle.h:158-161, renderer.cpp:147-155)."""
+    """BarycentricInterpolate + Normalize + (n+1)*0.5 (triangle.h:158-161, renderer.cpp:110-117)."""
     rin, exp = load_kat("shade")
     np.testing.assert_array_equal(bits(oracle.kat("shade", rin, 3)), bits(exp))
 
 
 def test_hammersley_tables(oracle):
-    """HammersleySequence<ScrambleNone> - 0.5f for spp 1..64, 128, 256 (renderer.cpp:87-98)."""
+    """HammersleySequence<ScrambleNone> - 0.5f for spp 1..64, 128, 256 (renderer.cpp:49-60)."""
     exp = read_gz("kat_hammersley.f32.gz", "<f4")
     spps = list(range(1, 65)) + [128, 256]
     got = np.concatenate([oracle.hammersley(s).reshape(-1) for s in spps])
@@ -91,13 +91,22 @@ def test_small_frames(oracle, golden):
 
 
 def test_sample_records(oracle, golden):
-    """Per-sample hit, tri, t, u, v and colour on 16x16 crops of every scene at 1080p x 4spp."""
+    """Per-sample hit, tri, t, u, v, colour AND the walk itself -- the GridIdx of the accepted
+    (or last) cell, the DDA iteration count and the IntersectRayTri count -- on 16x16 crops of
+    every scene at 1080p x 4spp.  The walk columns come from the reference's own Grid::Intersect
+    compiled with oracle/ref_instr.h's counting hooks (grid.h:41-42 GridIdx, triangle.h:15)."""
     for c in golden["crops"]:
-        exp = read_gz(os.path.join("samples", c["name"] + ".rec.gz"), "<u4").reshape(-1, 8)
+        exp = read_gz(os.path.join("samples", c["name"] + ".rec.gz"), "<u4").reshape(-1, 11)
         got = oracle.records(c["scene"], c["W"], c["H"], c["spp"], c["x0"], c["y0"], c["w"], c["h"])
         g = np.stack([got["hit"], got["tri"], bits(got["t"]), bits(got["u"]), bits(got["v"]),
-                      bits(got["r"]), bits(got["g"]), bits(got["b"])], axis=1)
+                      bits(got["r"]), bits(got["g"]), bits(got["b"]), got["voxel"], got["steps"],
+                      got["tests"]], axis=1)
         np.testing.assert_array_equal(g, exp, err_msg=c["name"])
+    walked = np.concatenate([read_gz(os.path.join("samples", c["name"] + ".rec.gz"), "<u4")
+                             .reshape(-1, 11) for c in golden["crops"]])
+    # the crops exercise long walks, many tests and rays that miss the grid entirely
+    assert walked[:, 9].max() > 20 and walked[:, 10].max() > 100
+    assert (walked[:, 8] == 0xFFFFFFFF).any() and (walked[:, 0] == 0).any()
 
 
 @pytest.mark.parametrize("sid", SCENES)

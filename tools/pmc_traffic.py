@@ -4,7 +4,7 @@ rocprofv3 passes of tools/gpu_profile.sh (MI355X_MICROARCH.md §HBM): FETCH_SIZE
 are KiB per dispatch; on gfx950 FETCH_SIZE reads 1/2 of the bytes of a wide streaming read, so
 the corrected read bytes are 2 x FETCH_SIZE (upper bound for this kernel's narrower gathers).
 
-    python3 tools/pmc_traffic.py gpurun_out/prof_r01d profiles/pmc_traffic.json
+    python3 tools/pmc_traffic.py gpurun_out/prof_r01d profiles/r01h_pmc_traffic.json
 """
 import csv
 import json
