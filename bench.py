@@ -23,6 +23,7 @@ Framebuffer drop-in path, frame to tile buffers incl. PCIe.  cpu_baseline: the o
 restatement (kind "port") of the reference's per-sample loop and 12x9 tile pool, on this host.
 """
 import argparse
+import contextlib
 import importlib.util
 import json
 import os
@@ -206,23 +207,54 @@ class GpuWorkload:
 
     def __init__(self, rtm, torch, world, rank, local, kernel):
         self.rtm, self.torch, self.world, self.rank = rtm, torch, world, rank
+        self.graphs = None              # per-scene hipGraphs of the render launch (--graph)
+        self.gevents = {}
         self.scenes = []
         for sid in SCENES:
             hs = rtm.HostScene.load(sid)
             gs = rtm.GpuScene(hs, local)
             self.scenes.append((sid, hs, gs, gs.frame(W, H, SPP, kernel=kernel)))
-        self.stream = torch.cuda.current_stream()
+        self.stream = torch.cuda.Stream()       # every launch, capture and collective of a step
         n = W * H if world == 1 else rtm.shard_elems(W, H, world)
         self.bufs = [torch.empty(n, dtype=torch.int32, device="cuda") for _ in SCENES]
         self.frames = [torch.empty(W * H, dtype=torch.int32, device="cuda") for _ in SCENES]
+    def stream_ctx(self):
+        return self.torch.cuda.stream(self.stream)
+
     def render(self, i):
+        if self.graphs is not None:
+            sid = self.scenes[i][0]
+            a = self.torch.cuda.Event(enable_timing=True)
+            b = self.torch.cuda.Event(enable_timing=True)
+            a.record(self.stream)
+            self.graphs[i].replay()
+            b.record(self.stream)
+            self.gevents.setdefault(sid, []).append((a, b))
+            return
+        self._launch(i)
+
+    def _launch(self, i):
         sid, hs, gs, f = self.scenes[i]
         if self.world == 1:
             gs.render_frame_device(f, self.bufs[i].data_ptr(), self.stream.cuda_stream)
         else:
             gs.render_shard_device(f, self.rank, self.world, self.bufs[i].data_ptr(), self.stream.cuda_stream)
 
+    def capture(self):
+        """One hipGraph per scene holding that scene's render launch (after the warm-up, so the
+        heavy-first order is the one the warm-up frames planned; replays keep it)."""
+        self.sync()
+        graphs = []
+        for i in range(len(self.scenes)):
+            g = self.torch.cuda.CUDAGraph()
+            with self.torch.cuda.graph(g, stream=self.stream):
+                self._launch(i)
+            graphs.append(g)
+        self.sync()
+        self.graphs = graphs
+
     def reset_times(self):
+        self.gevents = {}
         for sid, hs, gs, f in self.scenes:
             gs.kernel_times()
 
@@ -237,6 +269,9 @@ class GpuWorkload:
         """Mean render-kernel ms per scene over the timed steps: HIP events the library records
         on the launch stream immediately around each render kernel (rt_kernel_times)."""
         out = {}
+        if self.graphs is not None:
+            # HIP events on the launch stream around each replay of the scene's one-kernel graph
+            return {sid: float(np.mean([a.elapsed_time(b) for a, b in ev])) for sid, ev in self.gevents.items()}
         for sid, hs, gs, f in self.scenes:
             t = gs.kernel_times()
             if len(t) != min(steps, 64):
@@ -265,7 +300,7 @@ def check_frames(work, world):
     return f"{len(work.scenes)} frames equal to the one-GPU render"
 
 
-def run_steps(work, world, rank, steps, warmup, dist=None):
+def run_steps(work, world, rank, steps, warmup, dist=None, graph=False):
     """W untimed warm-up steps, then K timed steps between barrier+sync on both sides; returns
     the max-over-ranks wall time.  A step renders every scene (this rank's tiles when N > 1);
     each scene's shards are gathered to rank 0 (one RCCL gather: every peer sends its slice on
@@ -304,16 +339,21 @@ def run_steps(work, world, rank, steps, warmup, dist=None):
             if rank == 0:
                 work.unshard(i, g)
 
-    for _ in range(warmup):
-        step()
+    ctx = work.stream_ctx() if hasattr(work, "stream_ctx") else contextlib.nullcontext()
+    with ctx:
+        for _ in range(warmup):
+            step()
+        if graph:
+            work.capture()
     work.sync()
     work.reset_times()
     if world > 1:
         dist.barrier()
     work.sync()
     t0 = time.perf_counter()
-    for _ in range(steps):
-        step()
+    with ctx:
+        for _ in range(steps):
+            step()
     work.sync()
     if world > 1:
         dist.barrier()
@@ -335,6 +375,8 @@ def main():
     ap.add_argument("--kernel", type=int, default=0, help="rt_kernel value (0 = AUTO; see include/rt_tracer.h)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-end-to-end", action="store_true")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay each scene's render launch from a hipGraph captured after the warm-up")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="bench")
     ap.add_argument("--check", action="store_true",
                     help="after timing, rank 0 compares every assembled frame with a one-GPU render")
@@ -365,7 +407,8 @@ def main():
 
     rtm = load_package()
     work = GpuWorkload(rtm, torch, world, rank, local, args.kernel)
-    elapsed = run_steps(work, world, rank, args.steps, args.warmup, dist if world > 1 else None)
+    elapsed = run_steps(work, world, rank, args.steps, args.warmup, dist if world > 1 else None,
+                        graph=args.graph)
     kernel_ms = work.kernel_ms(args.steps)
     samples_per_step = len(SCENES) * W * H * SPP          # all ranks together
     value = samples_per_step * args.steps / elapsed / 1e6
@@ -392,7 +435,8 @@ def main():
                     "post-setup meshes dumped by the reference's own mesh code",
             "config": {"workload": f"scenes{list(SCENES)}_{W}x{H}x{SPP}", "scenes": list(SCENES),
                        "width": W, "height": H, "spp": SPP, "kernel": args.kernel,
-                       "parallelism": f"tile-shard x{world}" + (" + RCCL gather to rank 0" if world > 1 else "")},
+                       "parallelism": f"tile-shard x{world}" + (" + RCCL gather to rank 0" if world > 1 else ""),
+                       "launch": "hipGraph per scene" if args.graph else "direct"},
             "per_scene": {str(sid): {"kernel_ms": round(kernel_ms[sid], 4),
                                      "kernel_msamples_per_s": round(W * H * SPP / world / kernel_ms[sid] / 1e3, 1),
                                      "bytes_per_sample": round(ab[sid]["bytes_per_sample"], 1),

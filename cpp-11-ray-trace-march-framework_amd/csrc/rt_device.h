@@ -163,62 +163,78 @@ __device__ __forceinline__ bool ray_tri_mt_gated(float ox, float oy, float oz, f
 // camera origin with the same operations; only the direction-dependent half of
 // triangle.h:15-107 remains per ray.  Record: {e1.xyz, e2.x} {e2.yz, tvec.xy} {tvec.z, qvec.xyz}.
 
-// First half of the test (triangle.h:45-87): det and u.  FAST_RCP: inv_det by rcp_nr, exact
-// wherever the result is used: |det| < 1e-8 is rejected, and the launch selects FAST_RCP only
-// for scenes whose |e1|_1 |e2|_1 bounds |det| far below 2^126 (rt_scene::rcp_safe).
+// ---- the per-camera record test (AUTO's hot loop) ---------------------------------------
+// With one camera origin per frame, tvec = origin - v0 (triangle.h:82), qvec = tvec x edge1
+// (:90) and DOT(edge2, qvec) (:98) are per-reference constants: k_origin_pre computes them once
+// per camera with the reference's exact operations (make_frec) into a 64-byte record laid out
+// for packed f32 math: every pair below is one 64-bit register operand of a v_pk_mul_f32 /
+// v_pk_add_f32, which perform two IEEE single-precision operations -- the same roundings as two
+// v_mul_f32 / v_add_f32 -- so the reference's bits are kept while the instruction count drops.
+//
+//   r0 = (e1x, tx, e1y, ty)   r1 = (e1z, tz, e2y, e2z)   r2 = (e2x, e2y, qx, qy)   r3 = (qz, tq, 0, 0)
+//
+// The ray enters as two VGPR pairs a = (dx, dy) and c = (dy, dz).
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+struct FRec { float4 r0, r1, r2, r3; };
+
+// k_origin_pre's arithmetic for one reference (v0, e1, e2 as in the scene's reference record).
+__device__ __forceinline__ FRec make_frec(float ox, float oy, float oz, float v0x, float v0y, float v0z,
+                                          float e1x, float e1y, float e1z, float e2x, float e2y, float e2z)
+{
+    const float tx = ox - v0x, ty = oy - v0y, tz = oz - v0z;   // triangle.h:82 SUB(tvec, origin, vert0)
+    const float qx = ty * e1z - tz * e1y;                      // triangle.h:90 CROSS(qvec, tvec, edge1)
+    const float qy = tz * e1x - tx * e1z;
+    const float qz = tx * e1y - ty * e1x;
+    const float tq = e2x * qx + e2y * qy + e2z * qz;           // triangle.h:98 DOT(edge2, qvec)
+    FRec f;
+    f.r0 = make_float4(e1x, tx, e1y, ty);
+    f.r1 = make_float4(e1z, tz, e2y, e2z);
+    f.r2 = make_float4(e2x, e2y, qx, qy);
+    f.r3 = make_float4(qz, tq, 0.0f, 0.0f);
+    return f;
+}
+
+// First half (triangle.h:45-87): pvec = dir x edge2, det = edge1 . pvec, u = tvec . pvec * inv_det.
+// Products and sums in the reference's order, two lanes of each pair at a time:
+//   (pz, px) = (dx*e2y, dy*e2z) - (dy*e2x, dz*e2y),   py = dz*e2x - dx*e2z
+//   (det, u') = ((e1x, tx)*px + (e1y, ty)*py) + (e1z, tz)*pz
+// FAST_RCP: inv_det by rcp_nr, exact wherever the result is used: |det| < 1e-8 is rejected, and
+// the launch selects FAST_RCP only for scenes whose |e1|_1 |e2|_1 bounds |det| far below 2^126.
 template <bool FAST_RCP>
-__device__ __forceinline__ bool mt_pre_first(float dx, float dy, float dz, float e1x, float e1y, float e1z,
-                                             float e2x, float e2y, float e2z, float tx, float ty, float tz,
+__device__ __forceinline__ bool mt_rec_first(f2v a, f2v c, f2v e1t_x, f2v e1t_y, f2v e1t_z, f2v e2yz, f2v e2xy,
                                              float& inv_det, float& u)
 {
-    const float px = dy * e2z - dz * e2y;
-    const float py = dz * e2x - dx * e2z;
-    const float pz = dx * e2y - dy * e2x;
-    const float det = e1x * px + e1y * py + e1z * pz;
+    const f2v zx = a * e2yz - c * e2xy;                        // (pz, px)
+    const float py = c.y * e2xy.x - a.x * e2yz.y;
+    const f2v m = (e1t_x * zx.y + e1t_y * py) + e1t_z * zx.x;  // (det, DOT(tvec, pvec))
+    const float det = m.x;
     inv_det = FAST_RCP ? rcp_nr(det) : 1.0f / det;
-    u = (tx * px + ty * py + tz * pz) * inv_det;
+    u = m.y * inv_det;
     return !(det > -0.00000001f && det < 0.00000001f) & !(u < 0.0f || u > 1.0f);
 }
 
-// Second half (triangle.h:90-101): v and t = DOT(edge2, qvec) * inv_det.  (Measured: computing
-// e2 . qvec here beats a per-camera tdot array by ~5 %: one more load per record costs more than
-// these 5 VALU.)
-__device__ __forceinline__ bool mt_pre_second(float dx, float dy, float dz, float qx, float qy, float qz,
-                                              float e2x, float e2y, float e2z, float inv_det, float u, float& v,
-                                              float& t)
+// Second half (triangle.h:90-101): v = DOT(dir, qvec) * inv_det, t = DOT(edge2, qvec) * inv_det
+// with the record's constant DOT(edge2, qvec).
+__device__ __forceinline__ bool mt_rec_second(f2v a, f2v c, f2v qxy, float qz, float tq, float inv_det, float u,
+                                              float& v, float& t)
 {
-    v = (dx * qx + dy * qy + dz * qz) * inv_det;
-    t = (e2x * qx + e2y * qy + e2z * qz) * inv_det;
+    const f2v dq = a * qxy;
+    v = ((dq.x + dq.y) + c.y * qz) * inv_det;
+    t = tq * inv_det;
     return !(v < 0.0f || u + v > 1.0f) & (t >= 0.0f);
 }
 
-// The whole per-camera-record test, wave-gated (the q/v/t half only when some lane passed det
-// and u); results identical to ray_tri_mt_gated.
+// The whole record test, wave-gated (the v/t half only when some lane passed det and u);
+// results identical to ray_tri_mt_gated on the hits.
 template <bool FAST_RCP>
-__device__ __forceinline__ bool ray_tri_mt_gated_pre(float dx, float dy, float dz,
-                                                     float e1x, float e1y, float e1z,
-                                                     float e2x, float e2y, float e2z,
-                                                     float tx, float ty, float tz,
-                                                     float qx, float qy, float qz,
-                                                     float& t, float& u, float& v)
+__device__ __forceinline__ bool ray_tri_frec_gated(f2v a, f2v c, const FRec& r, float& t, float& u, float& v)
 {
     float inv_det;
-    const bool ok1 = mt_pre_first<FAST_RCP>(dx, dy, dz, e1x, e1y, e1z, e2x, e2y, e2z, tx, ty, tz, inv_det, u);
+    const bool ok1 = mt_rec_first<FAST_RCP>(a, c, f2v{r.r0.x, r.r0.y}, f2v{r.r0.z, r.r0.w}, f2v{r.r1.x, r.r1.y},
+                                            f2v{r.r1.z, r.r1.w}, f2v{r.r2.x, r.r2.y}, inv_det, u);
     if (!__any(ok1)) return false;
-    return ok1 & mt_pre_second(dx, dy, dz, qx, qy, qz, e2x, e2y, e2z, inv_det, u, v, t);
-}
-
-// k_origin_pre's arithmetic for one reference (v0, e1 as in the scene's reference record).
-__device__ __forceinline__ void origin_terms(float ox, float oy, float oz, float v0x, float v0y, float v0z,
-                                             float e1x, float e1y, float e1z, float& tx, float& ty, float& tz,
-                                             float& qx, float& qy, float& qz)
-{
-    tx = ox - v0x;                                   // triangle.h:82
-    ty = oy - v0y;
-    tz = oz - v0z;
-    qx = ty * e1z - tz * e1y;                        // triangle.h:90 CROSS(qvec, tvec, edge1)
-    qy = tz * e1x - tx * e1z;
-    qz = tx * e1y - ty * e1x;
+    return ok1 & mt_rec_second(a, c, f2v{r.r2.z, r.r2.w}, r.r3.x, r.r3.y, inv_det, u, v, t);
 }
 
 // triangle.h:200-226 IntersectRayPlane + ComputeBarycentric (:133-156). Uses v0, the same

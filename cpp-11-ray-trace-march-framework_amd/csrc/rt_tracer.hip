@@ -57,7 +57,7 @@ constexpr uint32_t kTile = 16;              // shard / scheduling tile edge (pix
 constexpr uint32_t kTilePix = kTile * kTile;
 constexpr uint32_t kWG = 256;               // lanes per workgroup
 constexpr uint32_t kWavesPerWG = kWG / 64u;
-constexpr uint32_t kLdsStage = 64;          // kVarLdsCells: records per LDS chunk (3 KiB per wave)
+constexpr uint32_t kLdsStage = 64;          // kVarLdsCells: records per LDS chunk (4 KiB per wave)
 constexpr uint32_t kLdsMinRefs = 16;        // kVarLdsCells: shortest list staged through LDS
 // Traversal features, combined into the VAR template argument of the render kernels.
 constexpr int kVarWaveGate = 2;             // skip a test's second half when no lane needs it
@@ -238,6 +238,7 @@ __device__ __forceinline__ bool test_cell(const KParams& P, float ox, float oy, 
 {
     constexpr bool PRE = (VAR & kVarOriginPre) != 0 && TRI == RT_TRI_MOLLER_TRUMBORE;
     constexpr bool F = (VAR & kVarFastRcp) != 0;
+    const rtd::f2v ra = {dx, dy}, rc = {dy, dz};   // the ray as the record test's register pairs
     const float tb0 = __builtin_fminf(t, nct_ax);
     // every accepted hit lowers tb strictly, so "some hit was taken" is tb < tb0; u, v and tri
     // are updated in place (the caller's values stand when nothing is taken)
@@ -264,16 +265,16 @@ __device__ __forceinline__ bool test_cell(const KParams& P, float ox, float oy, 
                 // latency per record; same records, same order.
                 if (ke0 - kb0 >= kLdsMinRefs)
                 {
-                    __shared__ float4 s_cells[kWavesPerWG * kLdsStage * 3u];
-                    float4 *st = s_cells + (threadIdx.x >> 6) * (kLdsStage * 3u);
+                    __shared__ float4 s_cells[kWavesPerWG * kLdsStage * 4u];
+                    float4 *st = s_cells + (threadIdx.x >> 6) * (kLdsStage * 4u);
                     const uint64_t act = __ballot(1);
                     const uint32_t rank = __builtin_amdgcn_mbcnt_hi(uint32_t(act >> 32),
                                                                     __builtin_amdgcn_mbcnt_lo(uint32_t(act), 0u));
                     const uint32_t nact = uint32_t(__popcll(act));
                     for (uint32_t base = kb0; base < ke0; base += kLdsStage)
                     {
-                        const uint32_t n3 = 3u * min(kLdsStage, ke0 - base);
-                        const float4 *src = P.frefs + size_t(base) * 3u;
+                        const uint32_t n3 = 4u * min(kLdsStage, ke0 - base);
+                        const float4 *src = P.frefs + size_t(base) * 4u;
                         if (act == ~0ull)
                         {
                             // full wave: LDS-DMA, no VGPR staging (writes base + lane x 16 B; lanes
@@ -288,21 +289,24 @@ __device__ __forceinline__ bool test_cell(const KParams& P, float ox, float oy, 
                             for (uint32_t q = rank; q < n3; q += nact)
                                 st[q] = src[q];
                         wave_lds_sync();
-                        for (uint32_t i = 0; 3u * i < n3; i++)
+                        for (uint32_t i = 0; 4u * i < n3; i++)
                         {
                             // the whole record in one LDS round trip (the empty asm keeps the reads
                             // of its second half from being sunk into the gate)
-                            const float4 r0 = st[3u * i], r1 = st[3u * i + 1u], r2 = st[3u * i + 2u];
+                            const float4 r0 = st[4u * i], r1 = st[4u * i + 1u], r2 = st[4u * i + 2u],
+                                         r3 = st[4u * i + 3u];
                             asm volatile("" ::"v"(r0.x), "v"(r0.y), "v"(r0.z), "v"(r0.w), "v"(r1.x), "v"(r1.y),
-                                         "v"(r1.z), "v"(r1.w), "v"(r2.x), "v"(r2.y), "v"(r2.z), "v"(r2.w));
+                                         "v"(r1.z), "v"(r1.w), "v"(r2.x), "v"(r2.y), "v"(r2.z), "v"(r2.w),
+                                         "v"(r3.x), "v"(r3.y));
                             if (STATS) tests++;
                             float inv, cu;
-                            const bool ok1 = rtd::mt_pre_first<F>(dx, dy, dz, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y,
-                                                                  r1.z, r1.w, r2.x, inv, cu);
+                            const bool ok1 = rtd::mt_rec_first<F>(ra, rc, rtd::f2v{r0.x, r0.y}, rtd::f2v{r0.z, r0.w},
+                                                                  rtd::f2v{r1.x, r1.y}, rtd::f2v{r1.z, r1.w},
+                                                                  rtd::f2v{r2.x, r2.y}, inv, cu);
                             if (__any(ok1))
                             {
                                 float cv, ct;
-                                const bool hit = ok1 & rtd::mt_pre_second(dx, dy, dz, r2.y, r2.z, r2.w, r0.w, r1.x, r1.y, inv,
+                                const bool hit = ok1 & rtd::mt_rec_second(ra, rc, rtd::f2v{r2.z, r2.w}, r3.x, r3.y, inv,
                                                                           cu, cv, ct);
                                 const bool take = hit & (ct < tb);
                                 tb = take ? ct : tb;
@@ -318,69 +322,99 @@ __device__ __forceinline__ bool test_cell(const KParams& P, float ox, float oy, 
             }
             if (!uniform_done)
             {
-                // software pipeline: record k + 1 is in flight while record k is tested (scalar
-                // loads may return out of order, so the wait for record k sits at its copy, before
-                // the next load is issued)
-                cvf4 *np = crefs + size_t(kb0) * 3u;
-                vf4 n0 = np[0], n1 = np[1], n2 = np[2];
-                for (uint32_t k = kb0; k < ke0; k++)
-                {
-                    const vf4 r0 = n0, r1 = n1, r2 = n2;
-                    if (k + 1u < ke0)
-                    {
-                        np = crefs + size_t(k + 1u) * 3u;
-                        n0 = np[0];
-                        n1 = np[1];
-                        n2 = np[2];
-                    }
+                // software pipeline over two register sets in turn: record k + 1 is in flight
+                // while record k is tested, with no per-record register copies (scalar loads may
+                // return out of order, so each set is waited for where it is first read)
+                auto test_rec = [&](const vf4 r0, const vf4 r1, const vf4 r2, const vf4 r3, uint32_t k) {
                     if (STATS) tests++;
-                    // the gate skips the record's second half AND the acceptance for the whole wave
-                    // when no lane passes det and u (the common case in a dense cell)
+                    // the gate skips the record's second half AND the acceptance for the whole
+                    // wave when no lane passes det and u (the common case in a dense cell)
                     float inv, cu;
-                    const bool ok1 = rtd::mt_pre_first<F>(dx, dy, dz, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z,
-                                                          r1.w, r2.x, inv, cu);
+                    const bool ok1 = rtd::mt_rec_first<F>(ra, rc, rtd::f2v{r0.x, r0.y}, rtd::f2v{r0.z, r0.w},
+                                                          rtd::f2v{r1.x, r1.y}, rtd::f2v{r1.z, r1.w},
+                                                          rtd::f2v{r2.x, r2.y}, inv, cu);
                     if (__any(ok1))
                     {
                         float cv, ct;
-                        const bool hit = ok1 & rtd::mt_pre_second(dx, dy, dz, r2.y, r2.z, r2.w, r0.w, r1.x, r1.y, inv, cu, cv, ct);
+                        const bool hit = ok1 & rtd::mt_rec_second(ra, rc, rtd::f2v{r2.z, r2.w}, r3.x, r3.y, inv, cu,
+                                                                  cv, ct);
                         const bool take = hit & (ct < tb);
                         tb = take ? ct : tb;
                         u = take ? cu : u;
                         v = take ? cv : v;
                         tri = take ? k : tri;
                     }
+                };
+                cvf4 *np = crefs + size_t(kb0) * 4u;
+                vf4 a0 = np[0], a1 = np[1], a2 = np[2], a3 = np[3];
+                for (uint32_t k = kb0;; k += 2u)
+                {
+                    vf4 b0, b1, b2, b3;
+                    const bool more1 = k + 1u < ke0;
+                    if (more1)
+                    {
+                        np = crefs + size_t(k + 1u) * 4u;
+                        b0 = np[0];
+                        b1 = np[1];
+                        b2 = np[2];
+                        b3 = np[3];
+                    }
+                    test_rec(a0, a1, a2, a3, k);
+                    if (!more1) break;
+                    const bool more2 = k + 2u < ke0;
+                    if (more2)
+                    {
+                        np = crefs + size_t(k + 2u) * 4u;
+                        a0 = np[0];
+                        a1 = np[1];
+                        a2 = np[2];
+                        a3 = np[3];
+                    }
+                    test_rec(b0, b1, b2, b3, k + 1u);
+                    if (!more2) break;
                 }
             }
             uniform_done = true;
         }
     }
-    if (!uniform_done)
+    if constexpr (PRE)
+    {
+        if (!uniform_done)
+        {
+            // Per-lane lists: the first-half terms (r0..r2) per iteration, the second-half terms
+            // (r3) only when the gate passes.  Measured against a one-ahead prefetch in VGPRs
+            // (+12, 6 waves/SIMD) and by LDS-DMA into a per-wave slot (global_load_lds_dwordx4;
+            // no VGPRs, but four DMA issues per record): both slower on the frame and no shorter
+            // on the lone heavy waves (profiles/r02e_ab_lane_prefetch.json).
+            for (uint32_t k = kb; k < ke; k++)
+            {
+                if constexpr ((VAR & kVarWaveClock) != 0)
+                    if (first_active_lane()) wave_counters()[1] += 1u;
+                if (STATS) tests++;
+                const float4 *rp = P.frefs + size_t(k) * 4u;     // one address, immediate offsets
+                const float4 r0 = rp[0], r1 = rp[1], r2 = rp[2];
+                float inv, pu;
+                const bool ok1 = rtd::mt_rec_first<F>(ra, rc, rtd::f2v{r0.x, r0.y}, rtd::f2v{r0.z, r0.w},
+                                                      rtd::f2v{r1.x, r1.y}, rtd::f2v{r1.z, r1.w},
+                                                      rtd::f2v{r2.x, r2.y}, inv, pu);
+                if (__any(ok1))
+                {
+                    const float2 r3 = *reinterpret_cast<const float2 *>(rp + 3);
+                    float pv, pt;
+                    const bool h = ok1 & rtd::mt_rec_second(ra, rc, rtd::f2v{r2.z, r2.w}, r3.x, r3.y, inv, pu, pv, pt);
+                    const bool take = h & (pt < tb);
+                    tb = take ? pt : tb;
+                    u = take ? pu : u;
+                    v = take ? pv : v;
+                    tri = take ? k : tri;
+                }
+            }
+        }
+    }
+    else
     for (uint32_t k = kb; k < ke; k++)
     {
-        if constexpr ((VAR & kVarWaveClock) != 0)
-            if (first_active_lane()) wave_counters()[1] += 1u;
         if (STATS) tests++;
-        if constexpr (PRE)
-        {
-            // the per-camera record; the triangle id is resolved from refs after the walk.
-            // The gate skips the second half and the acceptance when no lane passes det and u.
-            const float4 *rp = P.frefs + size_t(k) * 3u;     // one address, immediate offsets
-            const float4 r0 = rp[0], r1 = rp[1], r2 = rp[2];
-            float inv, pu;
-            const bool ok1 = rtd::mt_pre_first<F>(dx, dy, dz, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x,
-                                                  inv, pu);
-            if (__any(ok1))
-            {
-                float pv, pt;
-                const bool h = ok1 & rtd::mt_pre_second(dx, dy, dz, r2.y, r2.z, r2.w, r0.w, r1.x, r1.y, inv, pu, pv, pt);
-                const bool take = h & (pt < tb);
-                tb = take ? pt : tb;
-                u = take ? pu : u;
-                v = take ? pv : v;
-                tri = take ? k : tri;
-            }
-            continue;
-        }
         const float4 *rp = P.refs + size_t(k) * 3;          // one address, immediate offsets
         const float4 r0 = rp[0], r1 = rp[1], r2 = rp[2];
         float ct, cu, cv;
@@ -1226,31 +1260,35 @@ __device__ __forceinline__ void wide_trace(const KParams& P, uint32_t k, uint32_
                         uint32_t bk = 0xFFFFFFFFu;
                         // record k + G loads while record k is tested: the wide phase runs few,
                         // latency-bound waves, so the extra registers cost no throughput
-                        float4 n0, n1, n2;
+                        float4 n0, n1, n2, n3;
                         if (kb + sub < ke)
                         {
-                            const float4 *rp = P.frefs + size_t(kb + sub) * 3u;
+                            const float4 *rp = P.frefs + size_t(kb + sub) * 4u;
                             n0 = rp[0];
                             n1 = rp[1];
                             n2 = rp[2];
+                            n3 = rp[3];
                         }
+                        const rtd::f2v ra = {dx, dy}, rc = {dy, dz};
                         for (uint32_t k = kb + sub; k < ke; k += uint32_t(G))
                         {
-                            const float4 r0 = n0, r1 = n1, r2 = n2;
+                            const float4 r0 = n0, r1 = n1, r2 = n2, r3 = n3;
                             if (k + uint32_t(G) < ke)
                             {
-                                const float4 *rp = P.frefs + size_t(k + uint32_t(G)) * 3u;
+                                const float4 *rp = P.frefs + size_t(k + uint32_t(G)) * 4u;
                                 n0 = rp[0];
                                 n1 = rp[1];
                                 n2 = rp[2];
+                                n3 = rp[3];
                             }
                             float inv, cu;
-                            const bool ok1 = rtd::mt_pre_first<(VAR & kVarFastRcp) != 0>(
-                                dx, dy, dz, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x, inv, cu);
+                            const bool ok1 = rtd::mt_rec_first<(VAR & kVarFastRcp) != 0>(
+                                ra, rc, rtd::f2v{r0.x, r0.y}, rtd::f2v{r0.z, r0.w}, rtd::f2v{r1.x, r1.y},
+                                rtd::f2v{r1.z, r1.w}, rtd::f2v{r2.x, r2.y}, inv, cu);
                             if (__any(ok1))
                             {
                                 float cv, ct;
-                                const bool h = ok1 & rtd::mt_pre_second(dx, dy, dz, r2.y, r2.z, r2.w, r0.w, r1.x, r1.y, inv, cu,
+                                const bool h = ok1 & rtd::mt_rec_second(ra, rc, rtd::f2v{r2.z, r2.w}, r3.x, r3.y, inv, cu,
                                                                         cv, ct);
                                 const bool take = h & (ct < bt);
                                 bt = take ? ct : bt;
@@ -1703,19 +1741,19 @@ __global__ void __launch_bounds__(kWG) k_unshard(const uint32_t *g, uint32_t *ou
 }
 
 // Per-camera-origin records (kVarOriginPre): for CSR reference k, tvec = o - v0,
-// qvec = tvec x e1 and tdot = e2 . qvec exactly as triangle.h:82, 90, 98 compute them.
+// qvec = tvec x e1 and DOT(e2, qvec) exactly as triangle.h:82, 90, 98 compute them, in the
+// packed-pair layout of rtd::make_frec (64 B per reference).
 __global__ void __launch_bounds__(kWG) k_origin_pre(const float4 *refs, float4 *frefs, uint32_t n, float ox,
                                                     float oy, float oz)
 {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n) return;
     const float4 r0 = refs[3 * size_t(k)], r1 = refs[3 * size_t(k) + 1], r2 = refs[3 * size_t(k) + 2];
-    const float e1x = r0.w, e1y = r1.x, e1z = r1.y, e2x = r1.z, e2y = r1.w, e2z = r2.x;
-    float tx, ty, tz, qx, qy, qz;
-    rtd::origin_terms(ox, oy, oz, r0.x, r0.y, r0.z, e1x, e1y, e1z, tx, ty, tz, qx, qy, qz);
-    frefs[3 * size_t(k) + 0] = make_float4(e1x, e1y, e1z, e2x);
-    frefs[3 * size_t(k) + 1] = make_float4(e2y, e2z, tx, ty);
-    frefs[3 * size_t(k) + 2] = make_float4(tz, qx, qy, qz);
+    const rtd::FRec f = rtd::make_frec(ox, oy, oz, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x);
+    frefs[4 * size_t(k) + 0] = f.r0;
+    frefs[4 * size_t(k) + 1] = f.r1;
+    frefs[4 * size_t(k) + 2] = f.r2;
+    frefs[4 * size_t(k) + 3] = f.r3;
 }
 
 // Device KATs (rt_debug_primitives)
@@ -1762,10 +1800,8 @@ __global__ void __launch_bounds__(kWG) k_primitives(int kind, const float *in, u
         float t = 0, u = 0, v = 0, pt = 0, pu = 0, pv = 0;
         const bool hg = rtd::ray_tri_mt_gated(a[0], a[1], a[2], a[3], a[4], a[5], a[6], a[7], a[8],
                                               e1x, e1y, e1z, e2x, e2y, e2z, t, u, v);
-        float tx, ty, tz, qx, qy, qz;
-        rtd::origin_terms(a[0], a[1], a[2], a[6], a[7], a[8], e1x, e1y, e1z, tx, ty, tz, qx, qy, qz);
-        const bool hp = rtd::ray_tri_mt_gated_pre<true>(a[3], a[4], a[5], e1x, e1y, e1z, e2x, e2y, e2z, tx, ty, tz,
-                                                        qx, qy, qz, pt, pu, pv);
+        const rtd::FRec fr = rtd::make_frec(a[0], a[1], a[2], a[6], a[7], a[8], e1x, e1y, e1z, e2x, e2y, e2z);
+        const bool hp = rtd::ray_tri_frec_gated<true>(rtd::f2v{a[3], a[4]}, rtd::f2v{a[4], a[5]}, fr, pt, pu, pv);
         o[0] = __uint_as_float(hg); o[1] = t; o[2] = u; o[3] = v;
         o[4] = __uint_as_float(hp); o[5] = pt; o[6] = pu; o[7] = pv;
     }
@@ -2572,7 +2608,7 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
     for (uint32_t c = 0; c < nc; c++)
         s->max_cell_refs = std::max(s->max_cell_refs, g.cell_offsets[c + 1] - g.cell_offsets[c]);
 
-    const size_t nfrefs = size_t(std::max(nr, 1u)) * 3;
+    const size_t nfrefs = size_t(std::max(nr, 1u)) * 4;
     RT_HIP(hipMalloc(&s->d_off, sizeof(uint32_t) * (nc + 1)));
     RT_HIP(hipMalloc(&s->d_refs, sizeof(float4) * refs.size()));
     RT_HIP(hipMalloc(&s->d_frefs, sizeof(float4) * nfrefs));
@@ -2792,14 +2828,21 @@ int rt_kernel_times(rt_scene *s, float *ms, uint32_t max_n, uint32_t *n)
     if (!s || !n || (max_n && !ms)) return fail(RT_E_INVALID, "NULL argument");
     std::lock_guard<std::mutex> lk(s->mtx);
     const uint32_t cnt = std::min(max_n, s->kt_count);
+    const uint32_t next = s->kt_next;
+    s->kt_count = 0;                      // consumed whatever happens below
+    uint32_t got = 0;
     for (uint32_t i = 0; i < cnt; i++)
     {
-        const uint32_t slot = (s->kt_next + kTimeRing - cnt + i) % kTimeRing;
-        RT_HIP(hipEventSynchronize(s->kt1[slot]));
-        RT_HIP(hipEventElapsedTime(&ms[i], s->kt0[slot], s->kt1[slot]));
+        // a pair that cannot be read (a launch that failed between its two records) is skipped
+        const uint32_t slot = (next + kTimeRing - cnt + i) % kTimeRing;
+        float v = 0.0f;
+        if (hipEventSynchronize(s->kt1[slot]) == hipSuccess &&
+            hipEventElapsedTime(&v, s->kt0[slot], s->kt1[slot]) == hipSuccess && v >= 0.0f)
+            ms[got++] = v;
+        else
+            (void)hipGetLastError();
     }
-    *n = cnt;
-    s->kt_count = 0;
+    *n = got;
     return RT_OK;
 }
 

@@ -285,7 +285,11 @@ int rth_internal_fail(int code, const std::string& m) { return fail(code, m); }
 // ================================================================= Framebuffer (host)
 // framebuffer.h:16-101 / framebuffer.cpp restated without OpenGL: 12x9 tiles, a
 // hardware_concurrency() worker pool, shuffled LIFO queue, per-tile mutex held across
-// RenderTile, stop flag polled between tiles.
+// RenderTile, stop flag polled between tiles.  Two changes that nothing outside can observe:
+// the workers are created once and parked between frames (the reference spawns and joins a
+// std::thread per worker per frame, framebuffer.cpp:16-41), and StartRendering's tile clear
+// (framebuffer.cpp:127-131) is deferred: a tile RenderTile overwrites whole is never cleared,
+// and the tiles a stopped frame left unrendered are cleared when the frame is finished.
 namespace {
 
 class Framebuffer
@@ -293,7 +297,7 @@ class Framebuffer
 public:
     explicit Framebuffer(uint32_t nthreads)
         : m_num_cpus(nthreads ? nthreads : std::max(1u, std::thread::hardware_concurrency())) { }
-    virtual ~Framebuffer() { }
+    virtual ~Framebuffer() { Shutdown(); }
 
     void Resize(uint32_t width, uint32_t height)               // framebuffer.cpp:94-122
     {
@@ -311,15 +315,22 @@ public:
     void StartRendering()                                       // framebuffer.cpp:124-134
     {
         KillAllWorkerThreads();
-        for (auto& t : m_tiles) t.Clear();
+        for (auto& t : m_tiles) t.clear_pending = true;         // Tile::Clear, deferred
         CreateWorkerThreads();
     }
 
+    // Blocks until every worker has finished the current frame (the reference's join).
     void Wait()
     {
-        for (auto& th : m_threads)
-            if (th.joinable()) th.join();
-        m_threads.clear();
+        std::unique_lock<std::mutex> lk(m_pool_mtx);
+        m_pool_cv.wait(lk, [&] { return m_threads_done == m_running; });
+        lk.unlock();
+        for (auto& t : m_tiles)                                 // tiles the frame did not reach
+            if (t.clear_pending)
+            {
+                t.Clear();
+                t.clear_pending = false;
+            }
     }
 
     double LastFrameSeconds() const { return m_last_frame_s; }
@@ -346,14 +357,18 @@ protected:
         {
             x0 = a; y0 = b; x1 = c; y1 = d;
             bgra.assign(std::max<size_t>(1, size_t(GetWidth()) * GetHeight()), 0);
+            clear_pending = false;
         }
         void Clear() { std::fill(bgra.begin(), bgra.end(), 0u); }
         std::mutex mtx;
         std::vector<uint32_t> bgra = std::vector<uint32_t>(1, 0);
         uint32_t x0 = 0, y0 = 0, x1 = 1, y1 = 1;
+        bool clear_pending = false;                             // StartRendering's clear, deferred
     };
 
-    virtual void RenderTile(Tile& tile) = 0;
+    // true = the whole tile buffer was written (renderer.cpp:74-135 writes every pixel), false =
+    // it returned early (stop flag, renderer.cpp:76-77) and the tile keeps its cleared state.
+    virtual bool RenderTile(Tile& tile) = 0;
     virtual void BeginFrame() { }
 
     void KillAllWorkerThreads()                                 // framebuffer.cpp:30-41
@@ -361,6 +376,21 @@ protected:
         m_threads_stop = true;
         Wait();
         m_threads_stop = false;
+    }
+
+    // Stops and joins the parked workers (derived destructors call it first: the workers call
+    // the derived RenderTile).
+    void Shutdown()
+    {
+        KillAllWorkerThreads();
+        {
+            std::lock_guard<std::mutex> lk(m_pool_mtx);
+            m_shutdown = true;
+        }
+        m_pool_cv.notify_all();
+        for (auto& th : m_threads)
+            if (th.joinable()) th.join();
+        m_threads.clear();
     }
 
     uint32_t m_width = 1, m_height = 1;
@@ -372,12 +402,19 @@ private:
     void CreateWorkerThreads()                                  // framebuffer.cpp:16-28
     {
         BeginFrame();
-        m_threads_done = 0;
         m_work_queue.clear();
         for (uint32_t i = 0; i < kTilesX * kTilesY; i++) m_work_queue.push_back(i);
         std::shuffle(m_work_queue.begin(), m_work_queue.end(), std::mt19937(m_frame_seed++));
-        m_start = std::chrono::steady_clock::now();
-        for (uint32_t i = 0; i < m_num_cpus; i++) m_threads.emplace_back(&Framebuffer::WorkerThread, this);
+        while (m_threads.size() < m_num_cpus)
+            m_threads.emplace_back(&Framebuffer::PoolThread, this, uint32_t(m_threads.size()));
+        {
+            std::lock_guard<std::mutex> lk(m_pool_mtx);
+            m_threads_done = 0;
+            m_running = m_num_cpus;
+            m_start = std::chrono::steady_clock::now();
+            m_generation++;
+        }
+        m_pool_cv.notify_all();
     }
 
     Tile* GetNextTileFromQueue()                                // framebuffer.cpp:43-57
@@ -389,6 +426,21 @@ private:
         return t;
     }
 
+    void PoolThread(uint32_t)
+    {
+        uint64_t seen = 0;
+        for (;;)
+        {
+            {
+                std::unique_lock<std::mutex> lk(m_pool_mtx);
+                m_pool_cv.wait(lk, [&] { return m_shutdown || m_generation != seen; });
+                if (m_shutdown) return;
+                seen = m_generation;
+            }
+            WorkerThread();
+        }
+    }
+
     void WorkerThread()                                         // framebuffer.cpp:59-92
     {
         while (!m_threads_stop)
@@ -396,17 +448,26 @@ private:
             Tile* tile = GetNextTileFromQueue();
             if (!tile) break;
             std::lock_guard<std::mutex> g(tile->mtx);
-            RenderTile(*tile);
+            if (RenderTile(*tile)) tile->clear_pending = false;
         }
-        if (m_threads_done.fetch_add(1) == m_num_cpus - 1 && !m_threads_stop)
-            m_last_frame_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - m_start).count();
+        std::lock_guard<std::mutex> lk(m_pool_mtx);
+        if (++m_threads_done == m_running)
+        {
+            if (!m_threads_stop)
+                m_last_frame_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - m_start).count();
+            m_pool_cv.notify_all();
+        }
     }
 
     const uint32_t m_num_cpus;
     std::vector<uint32_t> m_work_queue;
     std::mutex m_queue_mtx;
     std::vector<std::thread> m_threads;
-    std::atomic<uint32_t> m_threads_done{ 0 };
+    std::mutex m_pool_mtx;                                      // generation / done counters
+    std::condition_variable m_pool_cv;
+    uint64_t m_generation = 0;
+    uint32_t m_threads_done = 0, m_running = 0;
+    bool m_shutdown = false;
     std::chrono::steady_clock::time_point m_start;
     double m_last_frame_s = 0.0;
     uint32_t m_frame_seed = 1;
@@ -424,7 +485,7 @@ public:
         : Framebuffer(nthreads), m_gpu(gpu), m_host(host) { }
     ~GpuRenderer() override
     {
-        KillAllWorkerThreads();
+        Shutdown();
         DrainFrame();
         if (m_frame) rt_host_free(m_frame);
     }
@@ -451,17 +512,17 @@ protected:
         m_tiles_done = 0;
     }
 
-    void RenderTile(Tile& tile) override
+    bool RenderTile(Tile& tile) override
     {
         {
             std::lock_guard<std::mutex> g(m_frame_mtx);
             if (!m_frame_ready)
             {
-                if (m_threads_stop) return;                       // renderer.cpp:76-77
+                if (m_threads_stop) return false;                 // renderer.cpp:76-77
                 m_frame_ready = true;
                 IssueFrame();
             }
-            if (m_status != RT_OK) return;
+            if (m_status != RT_OK) return false;
         }
         uint32_t x0, y0, x1, y1;
         tile.GetPosition(x0, y0, x1, y1);
@@ -470,13 +531,14 @@ protected:
         {
             std::lock_guard<std::mutex> g(m_frame_mtx);
             SetError(rc);
-            return;
+            return false;
         }
         uint32_t* buf = tile.GetBuffer();
         for (uint32_t y = 0; y < tile.GetHeight(); y++)        // renderer.cpp:133 layout
             std::memcpy(buf + size_t(y) * tile.GetWidth(), m_frame + size_t(y0 + y) * m_width + x0,
                         size_t(tile.GetWidth()) * 4);
         m_tiles_done.fetch_add(1);
+        return true;
     }
 
 private:

@@ -20,7 +20,7 @@ spec.loader.exec_module(rtm)
 torch.cuda.set_device(0)
 st = torch.cuda.current_stream()
 W, H, SPP, N = 1920, 1080, 4, 1024
-KER = int(sys.argv[1]) if len(sys.argv) > 1 else 10293761
+KER = int(sys.argv[1], 0) if len(sys.argv) > 1 else 0
 CLK = 0x400000
 
 
@@ -82,4 +82,6 @@ for sid in (8, 5):
                 "alone_cycles_per_test_worst": round(alone[worst][0] / max(alone[worst][1], 1), 1),
                 "full_cycles_per_test_worst": round(full[worst] / max(alone[worst][1], 1), 1)}
     print(sid, json.dumps(res[sid]), flush=True)
-json.dump(res, open(os.path.join(ROOT, "gpurun_out", f"tail_probe_{KER}.json"), "w"), indent=1)
+lib = os.path.splitext(os.path.basename(os.environ.get("RT_TRACER_LIB", "librt_tracer.so")))[0]
+res["lib"] = lib
+json.dump(res, open(os.path.join(ROOT, "gpurun_out", f"tail_probe_{lib}_{KER}.json"), "w"), indent=1)
