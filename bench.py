@@ -40,7 +40,7 @@ W, H, SPP = 1920, 1080, 4
 # workload -> (scenes, W, H, spp, frame the per-sample counts are measured on, CPU-baseline frame)
 WORKLOADS = {
     "bench": ((1, 8), 1920, 1080, 4, (1920, 1080, 4), (1920, 1080, 4)),
-    "head4096": ((4,), 4096, 4096, 16, (1024, 1024, 16), (1024, 1024, 16)),
+    "head4096": ((4,), 4096, 4096, 16, (1024, 1024, 16), (4096, 4096, 16)),
     "batch10": (tuple(range(10)), 1920, 1080, 4, (1920, 1080, 4), (960, 540, 4)),
 }
 HBM_PEAK = 8.0e12          # MI355X HBM3E peak, B/s (MI355X_MICROARCH.md)
@@ -133,7 +133,7 @@ def end_to_end(rtm, work, reps=7):
 
 def valu_roofline(rtm, kernel_ms, args, world, algorithmic):
     """The bound that binds: VALU issue.  SQ_INSTS_VALU per launch comes from
-    profiles/counters.json (tools/collect_counters.py, rocprofv3 --pmc on this workload), used
+    profiles/counters_<workload>.json (tools/collect_counters.py, rocprofv3 --pmc on this workload), used
     only when its source_hash equals the hash of the kernel sources being timed; achieved =
     instructions per launch / the live mean kernel time (HIP events).  peak = 256 CU x 4 SIMD x
     1/2 wave64 VALU instruction per clock x 2.4 GHz.  traffic = PMC HBM bytes per launch from the
@@ -144,13 +144,13 @@ def valu_roofline(rtm, kernel_ms, args, world, algorithmic):
             "algorithmic_frac": round(algorithmic / HBM_PEAK, 4),
             "algorithmic": {"achieved": round(algorithmic / 1e9, 1), "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                             "note": "SURVEY 8d bytes per launch / mean kernel time; L2-served"}}
-    path = os.path.join(ROOT, "profiles", "counters.json")
+    path = os.path.join(ROOT, "profiles", f"counters_{args.workload}.json")
     want = f"scenes{list(SCENES)}_{W}x{H}x{SPP}"
     if world != 1 or args.kernel != 0:
         roof["counters"] = "not collected for this launch shape"
         return roof
     if not os.path.exists(path):
-        roof["counters"] = "profiles/counters.json missing"
+        roof["counters"] = f"{os.path.relpath(path, ROOT)} missing"
         return roof
     with open(path) as fh:
         c = json.load(fh)
@@ -169,7 +169,7 @@ def valu_roofline(rtm, kernel_ms, args, world, algorithmic):
                  "traffic_unit": "HBM bytes per launch (mean over scenes)",
                  "per_scene_valu_frac": {str(sid): round(sc[str(sid)]["SQ_INSTS_VALU"] / (kernel_ms[sid] / 1e3)
                                                          / VALU_PEAK, 4) for sid in SCENES},
-                 "counters": f"profiles/counters.json, source hash {src}"})
+                 "counters": f"{os.path.relpath(path, ROOT)}, source hash {src}"})
     return roof
 
 
@@ -182,14 +182,17 @@ def cpu_baseline(rtm_unused=None):
     cw, ch, cs = CPU_FRAME
     for sid in SCENES:                  # warm-up (first render after idle is slow)
         orc.render(sid, cw, ch, cs, nthreads=cores)
+    # median of 5; a step of > 100 M samples (head at 4096^2 x 16: ~5 s per frame on
+    # 16 cores) takes the median of 3 to stay within the bounded sample
+    reps = 5 if len(SCENES) * cw * ch * cs <= 100_000_000 else 3
     times = []
-    for _ in range(5):
+    for _ in range(reps):
         tot = 0.0
         for sid in SCENES:
             _, _, s = orc.render(sid, cw, ch, cs, nthreads=cores)
             tot += s
         times.append(tot)
-    med = sorted(times)[2]
+    med = sorted(times)[reps // 2]
     model = ""
     try:
         with open("/proc/cpuinfo") as f:
@@ -199,7 +202,7 @@ def cpu_baseline(rtm_unused=None):
     return {"value": round(len(SCENES) * cw * ch * cs / med / 1e6, 3), "unit": "Msamples/s",
             "cores": cores, "kind": "port",
             "sample": f"full frames of scenes {list(SCENES)} at {cw}x{ch}x{cs}, 12x9 tile pool, "
-                      f"median of 5 after 1 warm-up; cpu: {model or platform.processor()}"}
+                      f"median of {reps} after 1 warm-up; cpu: {model or platform.processor()}"}
 
 
 class GpuWorkload:

@@ -1028,7 +1028,10 @@ __host__ __device__ constexpr uint32_t bail_auto_tests(uint32_t nranks)
 #define RT_HF_FLOOR 100000
 #endif
 constexpr uint32_t kHfFrontMax = RT_HF_FRONT;   // blocks (4 waves each): half the chip's wave slots
-constexpr uint32_t kHfMinBlocks = 4096;     // below ~2 rounds of workgroups every block starts early
+#ifndef RT_HF_MIN_BLOCKS
+#define RT_HF_MIN_BLOCKS 4096
+#endif
+constexpr uint32_t kHfMinBlocks = RT_HF_MIN_BLOCKS;   // below ~2 rounds of workgroups every block starts early
 constexpr uint32_t kHfFloor = RT_HF_FLOOR;
 constexpr uint32_t kHfShift = RT_HF_SHIFT;  // heavy: cost > last max >> kHfShift; very heavy: >> 1
 constexpr uint32_t kHfPeriod = 4;           // a plan from every 4th frame of a launch shape
@@ -2038,7 +2041,8 @@ int prepare_samples(rt_scene *s, const rt_frame *f, uint32_t spp)
 }
 
 constexpr uint32_t kKernelFlags = RT_KERNEL_FLAG_CENTER_OUT | RT_KERNEL_FLAG_STATIC_ORDER | RT_KERNEL_FLAG_WIDE16 |
-                                  RT_KERNEL_FLAG_LDS_CELLS | RT_KERNEL_FLAG_EXHAUSTIVE | RT_KERNEL_FLAG_WAVE_CLOCK |
+                                  RT_KERNEL_FLAG_LDS_CELLS | RT_KERNEL_FLAG_ONE_PHASE | RT_KERNEL_FLAG_EXHAUSTIVE |
+                                  RT_KERNEL_FLAG_WAVE_CLOCK |
                                   RT_KERNEL_FLAG_BAIL_WIDE | RT_KERNEL_BUDGET_MASK;
 
 int validate_frame(const rt_frame *f)
@@ -2298,7 +2302,8 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
     // the plain kernel -> 0.48 / 0.35 / 0.25 with budgets 384 / 192 / 128).  On a whole frame,
     // or a scene without dense cells, phase 1's budget count and the re-trace cost more than
     // they save.
-    const bool bail_auto = kind == RT_KERNEL_AUTO && P.nranks >= kBailAutoRanks && s->max_cell_refs >= kBailAutoRefs;
+    const bool bail_auto = kind == RT_KERNEL_AUTO && P.nranks >= kBailAutoRanks && s->max_cell_refs >= kBailAutoRefs &&
+                           !(f->kernel & RT_KERNEL_FLAG_ONE_PHASE);
     const bool bail = wide_ok && kind == RT_KERNEL_AUTO && (bail_auto || (f->kernel & RT_KERNEL_FLAG_BAIL_WIDE));
     const bool g16 = ((f->kernel & RT_KERNEL_FLAG_WIDE16) || (bail_auto && !(f->kernel & RT_KERNEL_FLAG_BAIL_WIDE))) &&
                      P.spp * 16u <= 64u;

@@ -106,6 +106,8 @@ enum rt_kernel {
                                          per sample instead of 4 */
     RT_KERNEL_FLAG_LDS_CELLS = 0x80,  /* OR-able (AUTO): a wave-uniform list of >= 16 references is
                                          staged through LDS 64 records at a time */
+    RT_KERNEL_FLAG_ONE_PHASE = 0x100, /* OR-able (AUTO): never the two-phase arm, also for shards of
+                                         dense scenes (A/B arm of the rank-count policy) */
     RT_KERNEL_FLAG_EXHAUSTIVE = 0x8000, /* OR-able, ray march: evaluate every triangle per step
                                            (no block culling; A/B arm, identical results) */
     RT_KERNEL_FLAG_WAVE_CLOCK = 0x400000, /* OR-able (AUTO), debug: record s_memtime {start, end} of

@@ -6,7 +6,7 @@ pass under its own time limit), driving tools/render_loop.py (one scene's 1080p 
 N times).  Per scene it keeps the median over the k_render_* dispatches after the first two
 (warm-up / heavy-first bootstrap) and writes
 
-    profiles/counters.json = {"source_hash": rtm.kernel_source_hash(), "workload": ...,
+    profiles/counters_<workload>.json = {"source_hash": rtm.kernel_source_hash(), "workload": ...,
                               "scenes": {"1": {"SQ_INSTS_VALU": ..., "FETCH_SIZE_KiB": ...,
                                                "WRITE_SIZE_KiB": ..., "hbm_bytes": ...}, ...}}
 
@@ -14,7 +14,7 @@ bench.py uses it only when source_hash equals the hash of the sources it runs.
 HBM bytes follow MI355X_MICROARCH.md (HBM / rocprofv3): FETCH_SIZE and WRITE_SIZE are KiB per
 dispatch; gfx950's FETCH_SIZE reports half of a wide streaming read, so reads count 2 x.
 
-    python3 tools/collect_counters.py [--scenes 1 8] [--frames 12] [--out profiles/counters.json]
+    python3 tools/collect_counters.py [--workload bench|head4096|batch10] [--frames 12]
 """
 import argparse
 import csv
@@ -26,6 +26,8 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+WORKLOADS = {"bench": ([1, 8], [1920, 1080, 4]), "head4096": ([4], [4096, 4096, 16]),
+             "batch10": (list(range(10)), [1920, 1080, 4])}      # = bench.py WORKLOADS
 SETS = {
     "sq": "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_WAVES SQ_WAVE_CYCLES "
           "SQ_BUSY_CYCLES SQ_WAIT_INST_ANY",
@@ -60,12 +62,14 @@ def medians(path):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--scenes", type=int, nargs="+", default=[1, 8])
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="bench")
     ap.add_argument("--frames", type=int, default=12)
-    ap.add_argument("--size", type=int, nargs=3, default=[1920, 1080, 4])
-    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "counters.json"))
+    ap.add_argument("--out", default=None, help="default profiles/counters_<workload>.json")
     ap.add_argument("--work", default=os.path.join(ROOT, "gpurun_out", "counters"))
     a = ap.parse_args()
+    a.scenes, a.size = WORKLOADS[a.workload]
+    if a.out is None:
+        a.out = os.path.join(ROOT, "profiles", f"counters_{a.workload}.json")
     a.out, a.work = os.path.abspath(a.out), os.path.abspath(a.work)     # the passes run in /tmp
     rtm = load_rtm()
     os.makedirs(a.work, exist_ok=True)
@@ -75,7 +79,7 @@ def main():
     for sid in a.scenes:
         c = {}
         for tag, counters in SETS.items():
-            d = os.path.join(a.work, f"s{sid}_{tag}")
+            d = os.path.join(a.work, f"{a.workload}_s{sid}_{tag}")
             cmd = ["timeout", "-k", "10", "120", "rocprofv3", "--pmc"] + counters.split() + [
                 "--output-format", "csv", "-d", d, "-o", "run", "--",
                 "python3", os.path.join(ROOT, "tools", "render_loop.py"), "--scene", str(sid),
@@ -96,6 +100,7 @@ def main():
         c["lane_util"] = round(c["SQ_THREAD_CYCLES_VALU"] / max(1.0, c["SQ_ACTIVE_INST_VALU"]), 2)
         res[str(sid)] = c
     out = {"source_hash": rtm.kernel_source_hash(), "workload": f"scenes{a.scenes}_{W}x{H}x{S}",
+           "workload_name": a.workload,
            "kernel": "AUTO (rt_kernel 0)", "frames_per_scene": a.frames,
            "statistic": "median over k_render_* dispatches after the first two",
            "hbm_note": "hbm_bytes = (2 x FETCH_SIZE + WRITE_SIZE) KiB x 1024 (gfx950 FETCH_SIZE "

@@ -1,6 +1,6 @@
 #!/bin/bash
 # One GPU-box session: the GPU tests, an optional in-process A/B of this build against another,
-# PMC counters of this build (profiles/counters.json, keyed by the kernel-source hash), the bench
+# PMC counters of this build (profiles/counters_bench.json, keyed by the kernel-source hash), the bench
 # line, and the rocprofv3 kernel-trace stats of the same bench command.  Stops at the first step
 # that faults, aborts or times out.
 #   gpurun -- bash tools/gpu_session.sh <tag> [lib_b]
@@ -33,11 +33,11 @@ if [ -n "${E2E_AB:-}" ]; then
     ok $rc || exit $rc
 fi
 if [ "${COUNTERS:-1}" = 1 ]; then
-    timeout -k 10 900 python3 -u tools/collect_counters.py --out gpurun_out/${TAG}_counters.json \
+    timeout -k 10 900 python3 -u tools/collect_counters.py --workload bench --out gpurun_out/${TAG}_counters.json \
         --work gpurun_out/${TAG}_pmc > gpurun_out/${TAG}_counters.log 2>&1
     rc=$?; echo "counters rc=$rc"; tail -2 gpurun_out/${TAG}_counters.log
     [ $rc -eq 0 ] || exit $rc
-    cp gpurun_out/${TAG}_counters.json profiles/counters.json
+    cp gpurun_out/${TAG}_counters.json profiles/counters_bench.json
 fi
 timeout -k 10 300 python -u bench.py ${BENCH_ARGS:-} > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err
 rc=$?; echo "bench rc=$rc"; cat gpurun_out/${TAG}_bench.json

@@ -1,6 +1,12 @@
 #!/usr/bin/env python3
-"""Per-scene render time of one rank's shard at N = 1..8 (emulated on one GPU: rank r of N),
-to expose the latency floor of strong scaling (the slowest wave's dependent-load chain)."""
+"""Per-rank shard cost at N = 1, 2, 4, 8 emulated on one GPU (rank r of N, every rank), for
+the bench pair (Cornell + killeroo) and the dense scenes: what one step costs the slowest rank
+before the gather.  Per (scene, kernel, N, rank): median of HIP-event times around
+render_shard_device (all kernels of the launch) over 8 reps after 3 warm-ups (heavy-first
+planning frames included).  pair_max_ms[k][N] = max over ranks of (Cornell + killeroo).
+
+    python3 tools/shard_scaling.py [kernel ...]      (default: 0 = AUTO, 0x100 = AUTO one-phase)
+"""
 import importlib.util
 import json
 import os
@@ -16,24 +22,33 @@ spec.loader.exec_module(rtm)
 torch.cuda.set_device(0)
 st = torch.cuda.current_stream()
 W, H, SPP = 1920, 1080, 4
-kernels = [int(k) for k in sys.argv[1:]] or [0]
-res = {}
-for sid in (1, 8, 4, 5):
+kernels = [int(k, 0) for k in sys.argv[1:]] or [0, 0x100]
+NS = (1, 2, 4, 8)
+res = {"per_rank": {}, "pair_max_ms": {}, "scene_max_ms": {}}
+for sid in (1, 8, 5):
     g = rtm.GpuScene(rtm.HostScene.load(sid), 0)
     for k in kernels:
         f = g.frame(W, H, SPP, kernel=k)
-        for n in (1, 2, 4, 8, 16, 32):
+        for n in NS:
             buf = torch.empty(rtm.shard_elems(W, H, n), dtype=torch.int32, device="cuda")
-            ranks = [0] if n == 1 else [0, n // 2, n - 1]
-            for r in ranks:
+            for r in range(n):
                 ts = []
-                for rep in range(8):
+                for rep in range(11):
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     e0.record(st)
                     g.render_shard_device(f, r, n, buf.data_ptr(), st.cuda_stream)
                     e1.record(st)
                     torch.cuda.synchronize()
-                    if rep >= 2:
+                    if rep >= 3:
                         ts.append(e0.elapsed_time(e1))
-                res[f"s{sid}_k{k}_n{n}_r{r}"] = round(sorted(ts)[len(ts) // 2], 4)
-print(json.dumps(res))
+                res["per_rank"][f"s{sid}_k{k:#x}_n{n}_r{r}"] = round(sorted(ts)[len(ts) // 2], 4)
+            res["scene_max_ms"][f"s{sid}_k{k:#x}_n{n}"] = max(res["per_rank"][f"s{sid}_k{k:#x}_n{n}_r{r}"] for r in range(n))
+        print(sid, k, {n: res["scene_max_ms"][f"s{sid}_k{k:#x}_n{n}"] for n in NS}, flush=True)
+    g.close()
+for k in kernels:
+    res["pair_max_ms"][f"{k:#x}"] = {n: round(max(res["per_rank"][f"s1_k{k:#x}_n{n}_r{r}"] + res["per_rank"][f"s8_k{k:#x}_n{n}_r{r}"]
+                                                 for r in range(n)), 4) for n in NS}
+print(json.dumps(res["pair_max_ms"]))
+os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+lib = os.path.splitext(os.path.basename(os.environ.get("RT_TRACER_LIB", "librt_tracer.so")))[0]
+json.dump(res, open(os.path.join(ROOT, "gpurun_out", f"shard_scaling_{lib}.json"), "w"), indent=1)
