@@ -1009,12 +1009,15 @@ __device__ __forceinline__ void process_item(const KParams& P, uint32_t item)
 constexpr uint32_t kXcds = 8;
 constexpr uint32_t kWideG = 4;              // RT_KERNEL_WIDE: lanes per sample
 constexpr uint32_t kBailTests = 256;        // BAIL_WIDE: default phase-1 test budget per sample
-constexpr uint32_t kBailAutoRanks = 2;      // AUTO: two-phase arm from this many shard ranks ...
+constexpr uint32_t kBailAutoRanks = 4;      // AUTO: two-phase arm from this many shard ranks ...
 constexpr uint32_t kBailAutoRefs = 128;     // ... on scenes with a cell this dense, 16 lanes per
 // sample, and a budget that shrinks as the shard does (tools/shard_scaling.py)
 __host__ __device__ constexpr uint32_t bail_auto_tests(uint32_t nranks)
 {
-    return nranks >= 16u ? 64u : (nranks >= 8u ? 128u : (nranks >= 4u ? 192u : 384u));
+    // re-tuned in round 2 (phase 1 got cheaper with the packed record test): killeroo rank of 8
+    // 0.26 / 0.25 / 0.27 ms at 128 / 192 / 256, rank of 4 flat over 192..384
+    // (profiles/r02h_shard_budgets.json); below 4 ranks one phase with heavy-first order wins
+    return nranks >= 16u ? 128u : 192u;
 }
 // Heavy-first order (AUTO): front-section capacity, smallest launch it is used for, and the
 // floor of the heavy threshold in shader cycles (~40 us at 2.4 GHz)

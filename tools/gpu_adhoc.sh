@@ -2,7 +2,5 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"; mkdir -p gpurun_out; export TMPDIR=/tmp
 T=${1:-adhoc}
-timeout -k 10 200 python3 -u tools/stream_overlap.py > gpurun_out/${T}_streams.json 2> gpurun_out/${T}_streams.err
-rc=$?; cat gpurun_out/${T}_streams.json; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 200 python -u bench.py --no-cpu-baseline --no-end-to-end > gpurun_out/${T}_bench_w5.json 2>&1 && timeout -k 10 200 python -u bench.py --no-cpu-baseline --no-end-to-end --warmup 100 --steps 200 > gpurun_out/${T}_bench_w100.json 2>&1
-rc=$?; cut -c1-330 gpurun_out/${T}_bench_w5.json gpurun_out/${T}_bench_w100.json; exit $rc
+timeout -k 10 600 python3 -u tools/shard_scaling.py 0x8C000040 0x90000040 0x98000040 0x90000000 > gpurun_out/${T}_shard_budgets.log 2>&1
+rc=$?; tail -n1 gpurun_out/${T}_shard_budgets.log; exit $rc
