@@ -45,7 +45,9 @@ def load_rtm():
     return m
 
 
-def medians(path):
+def medians(path, nscenes):
+    """Per scene (dispatch order: frames of scene 0, then scene 1, ...) and counter: the median
+    over that scene's k_render_* dispatches after its first two."""
     per = {}
     for r in csv.DictReader(open(path)):
         if "k_render" not in r["Kernel_Name"]:
@@ -53,10 +55,13 @@ def medians(path):
         d = per.setdefault(r["Counter_Name"], {})
         k = int(r["Dispatch_Id"])
         d[k] = d.get(k, 0.0) + float(r["Counter_Value"])
-    out = {}
+    out = [dict() for _ in range(nscenes)]
     for name, disp in per.items():
-        v = sorted([disp[k] for k in sorted(disp)][2:] or list(disp.values()))
-        out[name] = v[len(v) // 2]
+        vals = [disp[k] for k in sorted(disp)]
+        n = len(vals) // nscenes
+        for i in range(nscenes):
+            v = sorted(vals[i * n:(i + 1) * n][2:] or vals[i * n:(i + 1) * n])
+            out[i][name] = v[len(v) // 2]
     return out
 
 
@@ -75,34 +80,34 @@ def main():
     os.makedirs(a.work, exist_ok=True)
     env = dict(os.environ, TMPDIR="/tmp")
     W, H, S = a.size
-    res = {}
+    res = {str(sid): {} for sid in a.scenes}
+    for tag, counters in SETS.items():
+        d = os.path.join(a.work, f"{a.workload}_{tag}")
+        cmd = ["timeout", "-k", "10", "300", "rocprofv3", "--pmc"] + counters.split() + [
+            "--output-format", "csv", "-d", d, "-o", "run", "--",
+            "python3", os.path.join(ROOT, "tools", "render_loop.py"), "--scenes", *map(str, a.scenes),
+            "--frames", str(a.frames), "--size", str(W), str(H), str(S)]
+        with open(d + ".log", "w") as log:
+            rc = subprocess.run(cmd, cwd="/tmp", env=env, stdout=log, stderr=subprocess.STDOUT).returncode
+        print(f"{a.workload} {tag} rc={rc}", flush=True)
+        if rc != 0:
+            sys.exit(rc)
+        f = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+        if not f:
+            sys.exit(f"no counter csv under {d}")
+        for sid, m in zip(a.scenes, medians(f[0], len(a.scenes))):
+            res[str(sid)].update(m)
     for sid in a.scenes:
-        c = {}
-        for tag, counters in SETS.items():
-            d = os.path.join(a.work, f"{a.workload}_s{sid}_{tag}")
-            cmd = ["timeout", "-k", "10", "120", "rocprofv3", "--pmc"] + counters.split() + [
-                "--output-format", "csv", "-d", d, "-o", "run", "--",
-                "python3", os.path.join(ROOT, "tools", "render_loop.py"), "--scene", str(sid),
-                "--frames", str(a.frames), "--size", str(W), str(H), str(S)]
-            with open(d + ".log", "w") as log:
-                rc = subprocess.run(cmd, cwd="/tmp", env=env, stdout=log, stderr=subprocess.STDOUT).returncode
-            print(f"scene {sid} {tag} rc={rc}", flush=True)
-            if rc != 0:
-                sys.exit(rc)
-            f = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
-            if not f:
-                sys.exit(f"no counter csv under {d}")
-            c.update(medians(f[0]))
+        c = res[str(sid)]
         c["FETCH_SIZE_KiB"] = c.pop("FETCH_SIZE", None)
         c["WRITE_SIZE_KiB"] = c.pop("WRITE_SIZE", None)
         c["hbm_bytes"] = round((2 * c["FETCH_SIZE_KiB"] + c["WRITE_SIZE_KiB"]) * 1024)
         c["valu_per_wave"] = round(c["SQ_INSTS_VALU"] / c["SQ_WAVES"], 1)
         c["lane_util"] = round(c["SQ_THREAD_CYCLES_VALU"] / max(1.0, c["SQ_ACTIVE_INST_VALU"]), 2)
-        res[str(sid)] = c
     out = {"source_hash": rtm.kernel_source_hash(), "workload": f"scenes{a.scenes}_{W}x{H}x{S}",
            "workload_name": a.workload,
            "kernel": "AUTO (rt_kernel 0)", "frames_per_scene": a.frames,
-           "statistic": "median over k_render_* dispatches after the first two",
+           "statistic": "per scene, median over its k_render_* dispatches after its first two",
            "hbm_note": "hbm_bytes = (2 x FETCH_SIZE + WRITE_SIZE) KiB x 1024 (gfx950 FETCH_SIZE "
                        "counts half of a wide read; MI355X_MICROARCH.md)",
            "scenes": res}

@@ -12,6 +12,7 @@ import torch  # first: share torch's HIP runtime
 ap = argparse.ArgumentParser()
 ap.add_argument("--lib", default="")
 ap.add_argument("--scene", type=int, default=1)
+ap.add_argument("--scenes", type=int, nargs="+", default=None, help="several scenes, --frames each, in order")
 ap.add_argument("--frames", type=int, default=10)
 ap.add_argument("--kernel", type=lambda x: int(x, 0), default=0)
 ap.add_argument("--size", type=int, nargs=3, default=[1920, 1080, 4])
@@ -26,10 +27,12 @@ spec.loader.exec_module(rtm)
 torch.cuda.set_device(0)
 st = torch.cuda.current_stream()
 W, H, S = a.size
-g = rtm.GpuScene(rtm.HostScene.load(a.scene), 0)
-f = g.frame(W, H, S, kernel=a.kernel)
 out = torch.empty(W * H, dtype=torch.int32, device="cuda")
-for _ in range(a.frames):
-    g.render_frame_device(f, out.data_ptr(), st.cuda_stream)
-torch.cuda.synchronize()
-print("frames", a.frames, "scene", a.scene, "lib", a.lib or "librt_tracer.so")
+for sid in (a.scenes or [a.scene]):
+    g = rtm.GpuScene(rtm.HostScene.load(sid), 0)
+    f = g.frame(W, H, S, kernel=a.kernel)
+    for _ in range(a.frames):
+        g.render_frame_device(f, out.data_ptr(), st.cuda_stream)
+    torch.cuda.synchronize()
+    g.close()
+print("frames", a.frames, "scenes", a.scenes or [a.scene], "lib", a.lib or "librt_tracer.so")
