@@ -47,7 +47,6 @@ RT_KERNEL_FLAG_STATIC_ORDER = 0x20
 RT_KERNEL_FLAG_WIDE16 = 0x40
 RT_KERNEL_FLAG_LDS_CELLS = 0x80
 RT_KERNEL_FLAG_ONE_PHASE = 0x100
-RT_KERNEL_FLAG_NO_CULL = 0x200
 RT_KERNEL_FLAG_EXHAUSTIVE = 0x8000
 RT_KERNEL_FLAG_WAVE_CLOCK = 0x400000
 RT_KERNEL_FLAG_BAIL_WIDE = 0x80000000

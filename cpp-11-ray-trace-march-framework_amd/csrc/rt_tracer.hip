@@ -58,9 +58,7 @@ constexpr uint32_t kTilePix = kTile * kTile;
 constexpr uint32_t kWG = 256;               // lanes per workgroup
 constexpr uint32_t kWavesPerWG = kWG / 64u;
 constexpr uint32_t kLdsStage = 64;          // kVarLdsCells: records per LDS chunk (4 KiB per wave)
-constexpr uint32_t kLdsMinRefs = 16;
-// A wave's pixel box (x0 | x1 << 16, y0 | y1 << 16) that overlaps every record box: no cull
-constexpr uint32_t kWaveBoxAll = 0xFFFF0000u;        // kVarLdsCells: shortest list staged through LDS
+constexpr uint32_t kLdsMinRefs = 16;        // kVarLdsCells: shortest list staged through LDS
 // Traversal features, combined into the VAR template argument of the render kernels.
 constexpr int kVarWaveGate = 2;             // skip a test's second half when no lane needs it
 constexpr int kVarSkipRun = 4;              // wave-uniform proven-empty runs in a tight loop
@@ -120,7 +118,6 @@ struct KParams
     uint32_t ntris;
     uint32_t tri_test;
     uint32_t isect;             // enum rt_intersector
-    uint32_t cull;              // 1: skip records whose screen box misses the wave's pixels (§4.7)
     // work decomposition
     uint32_t rx0, ry0, rw, rh;  // region of the frame rendered by this launch
     uint32_t tiles_x;           // 16x16 tiles across the region
@@ -229,15 +226,6 @@ typedef float vf4 __attribute__((ext_vector_type(4)));
 // are written by k_origin_pre, an earlier launch) select s_load through the scalar cache
 typedef const __attribute__((address_space(4))) vf4 cvf4;
 
-// Record screen box (r3.zw: x0 | x1 << 16, y0 | y1 << 16, k_origin_pre) against the wave's
-// pixel box: false = no sample of the wave can have the record accepted (§4.7), so the
-// reference's IntersectRayTri rejects it for every lane and the record is skipped.
-__device__ __forceinline__ bool box_overlap(uint32_t bx, uint32_t by, uint32_t wbx, uint32_t wby)
-{
-    return ((bx & 0xFFFFu) <= (wbx >> 16)) & ((wbx & 0xFFFFu) <= (bx >> 16)) &
-           ((by & 0xFFFFu) <= (wby >> 16)) & ((wby & 0xFFFFu) <= (by >> 16));
-}
-
 // Tests a cell's list [kb, ke) in order (grid.cpp:243-267); true when it produced a hit.
 // grid.cpp:258-260 accepts cur_t when cur_t < t && cur_t < next_crossing_t[step_axis].  t is
 // FLT_MAX on entry (a hit ends the walk, grid.cpp:270-271) and neither bound is ever NaN, so the
@@ -246,8 +234,7 @@ __device__ __forceinline__ bool box_overlap(uint32_t bx, uint32_t by, uint32_t w
 template <bool STATS, int TRI, int VAR>
 __device__ __forceinline__ bool test_cell(const KParams& P, float ox, float oy, float oz, float dx, float dy,
                                           float dz, uint32_t kb, uint32_t ke, float nct_ax, float& t,
-                                          float& u, float& v, uint32_t& tri, uint32_t& tests, uint32_t wbx,
-                                          uint32_t wby)
+                                          float& u, float& v, uint32_t& tri, uint32_t& tests)
 {
     constexpr bool PRE = (VAR & kVarOriginPre) != 0 && TRI == RT_TRI_MOLLER_TRUMBORE;
     constexpr bool F = (VAR & kVarFastRcp) != 0;
@@ -312,9 +299,6 @@ __device__ __forceinline__ bool test_cell(const KParams& P, float ox, float oy, 
                                          "v"(r1.z), "v"(r1.w), "v"(r2.x), "v"(r2.y), "v"(r2.z), "v"(r2.w),
                                          "v"(r3.x), "v"(r3.y));
                             if (STATS) tests++;
-                            if (!box_overlap(__float_as_uint(st[4u * i + 3u].z), __float_as_uint(st[4u * i + 3u].w),
-                                             wbx, wby))
-                                continue;
                             float inv, cu;
                             const bool ok1 = rtd::mt_rec_first<F>(ra, rc, rtd::f2v{r0.x, r0.y}, rtd::f2v{r0.z, r0.w},
                                                                   rtd::f2v{r1.x, r1.y}, rtd::f2v{r1.z, r1.w},
@@ -341,14 +325,8 @@ __device__ __forceinline__ bool test_cell(const KParams& P, float ox, float oy, 
                 // software pipeline over two register sets in turn: record k + 1 is in flight
                 // while record k is tested, with no per-record register copies (scalar loads may
                 // return out of order, so each set is waited for where it is first read)
-#ifndef RT_CULL_MIN
-#define RT_CULL_MIN 0
-#endif
-                // the box check pays off on long lists only (wave-uniform)
-                const bool cull_list = ke0 - kb0 >= RT_CULL_MIN;
                 auto test_rec = [&](const vf4 r0, const vf4 r1, const vf4 r2, const vf4 r3, uint32_t k) {
                     if (STATS) tests++;
-                    if (cull_list && !box_overlap(__float_as_uint(r3.z), __float_as_uint(r3.w), wbx, wby)) return;
                     // the gate skips the record's second half AND the acceptance for the whole
                     // wave when no lane passes det and u (the common case in a dense cell)
                     float inv, cu;
@@ -372,10 +350,6 @@ __device__ __forceinline__ bool test_cell(const KParams& P, float ox, float oy, 
                 for (uint32_t k = kb0;; k += 2u)
                 {
                     vf4 b0, b1, b2, b3;
-                    // record k has arrived before record k + 1 is requested: scalar loads return
-                    // out of order, so a wait for k issued after k + 1's load would also wait
-                    // for k + 1 (s_waitcnt lgkmcnt(0))
-                    asm volatile("" ::"s"(a3.w) : "memory");
                     const bool more1 = k + 1u < ke0;
                     if (more1)
                     {
@@ -387,7 +361,6 @@ __device__ __forceinline__ bool test_cell(const KParams& P, float ox, float oy, 
                     }
                     test_rec(a0, a1, a2, a3, k);
                     if (!more1) break;
-                    asm volatile("" ::"s"(b3.w) : "memory");
                     const bool more2 = k + 2u < ke0;
                     if (more2)
                     {
@@ -408,9 +381,8 @@ __device__ __forceinline__ bool test_cell(const KParams& P, float ox, float oy, 
     {
         if (!uniform_done)
         {
-            // Per-lane lists: the first-half terms (r0..r2) and the screen box per iteration (a
-            // record no lane's wave box reaches is skipped), the second-half terms (r3.xy) only
-            // when the gate passes.  Measured against a one-ahead prefetch in VGPRs
+            // Per-lane lists: the first-half terms (r0..r2) per iteration, the second-half terms
+            // (r3) only when the gate passes.  Measured against a one-ahead prefetch in VGPRs
             // (+12, 6 waves/SIMD) and by LDS-DMA into a per-wave slot (global_load_lds_dwordx4;
             // no VGPRs, but four DMA issues per record): both slower on the frame and no shorter
             // on the lone heavy waves (profiles/r02e_ab_lane_prefetch.json).
@@ -420,10 +392,7 @@ __device__ __forceinline__ bool test_cell(const KParams& P, float ox, float oy, 
                     if (first_active_lane()) wave_counters()[1] += 1u;
                 if (STATS) tests++;
                 const float4 *rp = P.frefs + size_t(k) * 4u;     // one address, immediate offsets
-                // the box first: vector loads return in order, so its check waits for it alone
-                const float2 rb = *reinterpret_cast<const float2 *>(reinterpret_cast<const float *>(rp + 3) + 2);
                 const float4 r0 = rp[0], r1 = rp[1], r2 = rp[2];
-                if (!__any(box_overlap(__float_as_uint(rb.x), __float_as_uint(rb.y), wbx, wby))) continue;
                 float inv, pu;
                 const bool ok1 = rtd::mt_rec_first<F>(ra, rc, rtd::f2v{r0.x, r0.y}, rtd::f2v{r0.z, r0.w},
                                                       rtd::f2v{r1.x, r1.y}, rtd::f2v{r1.z, r1.w},
@@ -586,8 +555,7 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, float ox, float
                                                float dx, float dy, float dz,
                                                float& t, float& u, float& v, uint32_t& tri,
                                                uint32_t& voxel, uint32_t& steps, uint32_t& tests,
-                                               bool *bailed = nullptr, uint32_t bail_idx = 0u,   // work item
-                                               uint32_t wbx = kWaveBoxAll, uint32_t wby = kWaveBoxAll)
+                                               bool *bailed = nullptr, uint32_t bail_idx = 0u)   // work item
 {
     float nct0, nct1, nct2, dt0, dt1, dt2;
     int rem0, rem1, rem2, cs0, cs1, cs2, cell;
@@ -634,7 +602,7 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, float ox, float
                 // the walk's exit, so the loop keeps two exits, not three.
                 budget -= int(ke - kb);
                 if (kb < ke && budget >= 0 &&
-                    test_cell<STATS, TRI, VAR>(P, ox, oy, oz, dx, dy, dz, kb, ke, nct_ax, t, u, v, tri, tests, wbx, wby))
+                    test_cell<STATS, TRI, VAR>(P, ox, oy, oz, dx, dy, dz, kb, ke, nct_ax, t, u, v, tri, tests))
                     return true;
                 if (!more || budget < 0)
                 {
@@ -658,7 +626,7 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, float ox, float
                 // below), and the result read from t after the loop: the walk's loop-carried state
                 // stays in VGPRs instead of per-exit lane masks (SALU per wave, PMC-measured)
                 bool hit = false;
-                if (kb < ke) hit = test_cell<STATS, TRI, VAR>(P, ox, oy, oz, dx, dy, dz, kb, ke, nct_ax, t, u, v, tri, tests, wbx, wby);
+                if (kb < ke) hit = test_cell<STATS, TRI, VAR>(P, ox, oy, oz, dx, dy, dz, kb, ke, nct_ax, t, u, v, tri, tests);
                 bool done = hit | !more;
                 if constexpr ((VAR & kVarSkipRun) != 0 && (VAR & kVarPackedRem) != 0 && !STATS)
                 {
@@ -703,7 +671,7 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, float ox, float
         float nct_ax;
         bool more;
         RT_DDA_ADVANCE_ADD(nct_ax, more);
-        if (kb < ke && test_cell<STATS, TRI, VAR>(P, ox, oy, oz, dx, dy, dz, kb, ke, nct_ax, t, u, v, tri, tests, wbx, wby))
+        if (kb < ke && test_cell<STATS, TRI, VAR>(P, ox, oy, oz, dx, dy, dz, kb, ke, nct_ax, t, u, v, tri, tests))
             return true;
         if (!more) break;
     }
@@ -853,8 +821,7 @@ __device__ __forceinline__ bool ray_march(const KParams& P, float ox, float oy, 
 template <bool STATS, int TRI, int VAR>
 __device__ __forceinline__ void trace_sample(const KParams& P, uint32_t px, uint32_t py, uint32_t s, float& cr,
                                              float& cg, float& cb, rt_sample_rec *rec, bool *bailed = nullptr,
-                                             uint32_t bail_idx = 0u, uint32_t wbx = kWaveBoxAll,
-                                             uint32_t wby = kWaveBoxAll)
+                                             uint32_t bail_idx = 0u)
 {
     const float2 so = P.smp[s];
     float dx, dy, dz;
@@ -869,7 +836,7 @@ __device__ __forceinline__ void trace_sample(const KParams& P, uint32_t px, uint
         hit = brute_intersect<STATS>(P, P.org[0], P.org[1], P.org[2], dx, dy, dz, t, u, v, tri, tests);
     else
         hit = grid_intersect<STATS, TRI, VAR>(P, P.org[0], P.org[1], P.org[2], dx, dy, dz, t, u, v, tri, voxel,
-                                              steps, tests, bailed, bail_idx, wbx, wby);
+                                              steps, tests, bailed, bail_idx);
     const KParams& Q = late_params(P);
     if constexpr ((VAR & (kVarMarch | kVarBrute)) == 0)
         if ((VAR & kVarOriginPre) && TRI == RT_TRI_MOLLER_TRUMBORE && hit)
@@ -977,17 +944,9 @@ __device__ __forceinline__ void process_item(const KParams& P, uint32_t item)
     float cr = 0.0f, cg = 0.0f, cb = 0.0f;
     bool bailed = false;
     {
-        // the wave's pixels: an aligned Morton block, from its first and last slot (uniform)
-        uint32_t wbx = kWaveBoxAll, wby = kWaveBoxAll;
-        if ((VAR & kVarOriginPre) && P.cull)
-        {
-            const ItemCoord c0 = item_coord(P, item, 0u), c1 = item_coord(P, item, 63u);
-            wbx = c0.x | (c1.x << 16);
-            wby = c0.y | (c1.y << 16);
-        }
         const ItemCoord ic = item_coord(P, item, lane);
         if (ic.valid)
-            trace_sample<false, TRI, VAR>(P, ic.x, ic.y, ic.s, cr, cg, cb, nullptr, &bailed, item, wbx, wby);
+            trace_sample<false, TRI, VAR>(P, ic.x, ic.y, ic.s, cr, cg, cb, nullptr, &bailed, item);
     }
     const KParams& Q = late_params(P);
     const ItemCoord ic = item_coord(Q, item, lane);
@@ -1721,9 +1680,8 @@ k_render_compact(KParams P, uint32_t n_items, uint32_t refill)
                 bool more;
                 RT_DDA_ADVANCE_ADD(nct_ax, more);
                 uint32_t tests = 0u;
-                const uint32_t wbx = kWaveBoxAll, wby = kWaveBoxAll;   // lanes of several items: no cull
                 if (kb < ke &&
-                    test_cell<false, TRI, VAR>(P, ox, oy, oz, dx, dy, dz, kb, ke, nct_ax, t, u, v, tri, tests, wbx, wby))
+                    test_cell<false, TRI, VAR>(P, ox, oy, oz, dx, dy, dz, kb, ke, nct_ax, t, u, v, tri, tests))
                 {
                     state = 2u;
                     hit = true;
@@ -1788,170 +1746,16 @@ __global__ void __launch_bounds__(kWG) k_unshard(const uint32_t *g, uint32_t *ou
     out[size_t(y) * W + x] = g[r * shard_elems + size_t(k) * kTilePix + (y % kTile) * kTile + (x % kTile)];
 }
 
-// ---- record screen boxes (the proof is DESIGN.md §4.7) --------------------------------------
-// The camera of the frame as the records see it: rows of its 3x3 (gen_dir), the NDC scales
-// fx = fov_xs, fy = fov_xs / aspect, the frame size and the range of the sample offsets.
-struct CullCam
-{
-    float m[9];
-    float fx, fy;
-    uint32_t W, H;
-    float sx_lo, sx_hi, sy_lo, sy_hi;
-    uint32_t on;                // 0: every box is the whole range (no culling possible)
-};
-
-// Keeps the part of the convex polygon (px, py)[n] where a*X + b*Y + c >= 0 (double).
-__device__ void clip_half_plane(double *px, double *py, int& n, double a, double b, double c)
-{
-    double qx[16], qy[16];
-    int m = 0;
-    for (int i = 0; i < n && m < 15; i++)
-    {
-        const int j = (i + 1 == n) ? 0 : i + 1;
-        const double vi = a * px[i] + b * py[i] + c, vj = a * px[j] + b * py[j] + c;
-        if (vi >= 0.0) { qx[m] = px[i]; qy[m] = py[i]; m++; }
-        if ((vi >= 0.0) != (vj >= 0.0))
-        {
-            const double t = vi / (vi - vj);
-            qx[m] = px[i] + t * (px[j] - px[i]);
-            qy[m] = py[i] + t * (py[j] - py[i]);
-            m++;
-        }
-    }
-    for (int i = 0; i < m; i++) { px[i] = qx[i]; py[i] = qy[i]; }
-    n = m;
-}
-
-// Bounding box (continuous pixel coordinates X = px + sx) of the screen rectangle clipped by
-// the half-planes sgn[i] * (q . c'_i) >= -thr[i], q = (fx (2X/W - 1), fy (2Y/H - 1), -1).
-__device__ void region_box(const CullCam& C, const double (*cp)[3], const double *sgn, const double *thr, int nh,
-                           double& x0, double& x1, double& y0, double& y1)
-{
-    double px[16] = { -1.0, double(C.W) + 1.0, double(C.W) + 1.0, -1.0 };
-    double py[16] = { -1.0, -1.0, double(C.H) + 1.0, double(C.H) + 1.0 };
-    int n = 4;
-    for (int i = 0; i < nh && n > 0; i++)
-    {
-        const double a = sgn[i] * 2.0 * double(C.fx) * cp[i][0] / double(C.W);
-        const double b = sgn[i] * 2.0 * double(C.fy) * cp[i][1] / double(C.H);
-        const double c = sgn[i] * (-double(C.fx) * cp[i][0] - double(C.fy) * cp[i][1] - cp[i][2]) + thr[i];
-        clip_half_plane(px, py, n, a, b, c);
-    }
-    for (int i = 0; i < n; i++)
-    {
-        x0 = fmin(x0, px[i]); x1 = fmax(x1, px[i]);
-        y0 = fmin(y0, py[i]); y1 = fmax(y1, py[i]);
-    }
-}
-
-// Pixels of the frame some sample of which the reference's IntersectRayTri (triangle.h:15-107,
-// non-culling branch, f32) might accept for the record (tvec, e1, e2, qvec as stored), packed
-// x0 | x1 << 16 and y0 | y1 << 16; an empty box is x0 > x1.  Every other pixel's samples are
-// provably rejected (u < 0, v < 0 or u + v > 1 with the reference's roundings; §4.7).
-__device__ void record_screen_box(const CullCam& C, const float T[3], const float E1[3], const float E2[3],
-                                  const float Q[3], uint32_t& bx, uint32_t& by)
-{
-    bx = by = 0xFFFF0000u;                                      // [0, 65535]: never culled
-    if (!C.on) return;
-    const double u = 5.9604644775390625e-08;                    // 2^-24
-    double t[3], e1[3], e2[3], q[3];
-    for (int i = 0; i < 3; i++) { t[i] = T[i]; e1[i] = E1[i]; e2[i] = E2[i]; q[i] = Q[i]; }
-    // exact-real edge normals of the f32 inputs (products of floats are exact in double)
-    auto cross = [](const double *a, const double *b, double *o) {
-        o[0] = a[1] * b[2] - a[2] * b[1];
-        o[1] = a[2] * b[0] - a[0] * b[2];
-        o[2] = a[0] * b[1] - a[1] * b[0];
-    };
-    double cu[3], cd[3], cw[3];
-    cross(e2, t, cu);                                           // U = T.(D x E2) = D.(E2 x T)
-    cross(e2, e1, cd);                                          // Det = E1.(D x E2) = D.(E2 x E1)
-    for (int i = 0; i < 3; i++) cw[i] = cd[i] - cu[i] - q[i];   // W = Det - U - V, V = D.Q
-    // |D_i| <= Dmax: column norms of the camera rows (|normalize(q)| = 1)
-    double dmax = 0.0;
-    for (int i = 0; i < 3; i++)
-        dmax = fmax(dmax, sqrt(double(C.m[i]) * C.m[i] + double(C.m[3 + i]) * C.m[3 + i] +
-                               double(C.m[6 + i]) * C.m[6 + i]));
-    dmax *= 1.0 + 1e-5;
-    const double s0 = fabs(e2[1]) + fabs(e2[2]), s1 = fabs(e2[0]) + fabs(e2[2]), s2 = fabs(e2[0]) + fabs(e2[1]);
-    auto l1 = [](const double *a) { return fabs(a[0]) + fabs(a[1]) + fabs(a[2]); };
-    // rounding of the reference's f32 evaluation against the exact values at its own f32 ray
-    const double eu = 6.0 * u * dmax * (fabs(t[0]) * s0 + fabs(t[1]) * s1 + fabs(t[2]) * s2);
-    const double ed = 6.0 * u * dmax * (fabs(e1[0]) * s0 + fabs(e1[1]) * s1 + fabs(e1[2]) * s2);
-    const double ev = 4.0 * u * dmax * l1(q);
-    const double tiny = 7.2e-43 * (1.0 + dmax * l1(cd));        // 2^-140: no underflow to -0
-    // the f32 ray against the exact ray of its pixel coordinates (GenerateRay's roundings)
-    const double dd = (48.0 + 8.0 * fmax(double(C.fx), double(C.fy))) * u * dmax;
-    const double du = dd * l1(cu), dv = dd * l1(q), ddet = dd * l1(cd), dw = dd * l1(cw);
-    const double EU = eu + du + tiny, EV = ev + dv + tiny, ED = ed + ddet;
-    const double EW = eu + ev + 1.0001 * ed + 4.0 * u * dmax * l1(cd) + dw + tiny;
-    // |q| over the (extended) screen
-    const double nx = 1.0 + 3.0 / double(C.W), ny = 1.0 + 3.0 / double(C.H);
-    const double qmax = sqrt(double(C.fx) * C.fx * nx * nx + double(C.fy) * C.fy * ny * ny + 1.0) * (1.0 + 1e-6);
-    const double K = 4.0;                                       // safety factor on every margin
-    // edge normals in camera coordinates: c'_j = row_j . C
-    double cp[4][3];
-    const double *cs[4] = { cd, cu, q, cw };
-    for (int e = 0; e < 4; e++)
-        for (int j = 0; j < 3; j++)
-            cp[e][j] = double(C.m[3 * j]) * cs[e][0] + double(C.m[3 * j + 1]) * cs[e][1] + double(C.m[3 * j + 2]) * cs[e][2];
-    double x0 = 1e300, x1 = -1e300, y0 = 1e300, y1 = -1e300;
-    {   // det' > 0 side: not provably rejected => U, V, W >= -margins
-        const double sg[4] = { 1.0, 1.0, 1.0, 1.0 };
-        const double th[4] = { K * ddet * qmax, K * EU * qmax, K * EV * qmax, K * EW * qmax };
-        region_box(C, cp, sg, th, 4, x0, x1, y0, y1);
-    }
-    {   // det' < 0 side
-        const double sg[4] = { -1.0, -1.0, -1.0, -1.0 };
-        const double th[4] = { K * ddet * qmax, K * EU * qmax, K * EV * qmax, K * EW * qmax };
-        region_box(C, cp, sg, th, 4, x0, x1, y0, y1);
-    }
-    // |Det| <= Ed band: rejected by |det'| < 1e-8 when 2 Ed is below it, else only where
-    // |u'| > 1 or |v'| > 1 is provable
-    if (K * 2.0 * ed >= 1e-8)
-    {
-        const double cb[6][3] = { { cp[0][0], cp[0][1], cp[0][2] }, { cp[0][0], cp[0][1], cp[0][2] },
-                                  { cp[1][0], cp[1][1], cp[1][2] }, { cp[1][0], cp[1][1], cp[1][2] },
-                                  { cp[2][0], cp[2][1], cp[2][2] }, { cp[2][0], cp[2][1], cp[2][2] } };
-        const double sg[6] = { 1.0, -1.0, 1.0, -1.0, 1.0, -1.0 };
-        const double bd = K * (ed + ddet) * qmax, bu = K * (eu + 2.0001 * ed + du + tiny) * qmax,
-                     bv = K * (ev + 2.0001 * ed + dv + tiny) * qmax;
-        const double th[6] = { bd, bd, bu, bu, bv, bv };
-        region_box(C, cb, sg, th, 6, x0, x1, y0, y1);
-    }
-    if (!(x0 <= x1) || !(y0 <= y1))
-    {
-        bx = by = 1u;                                           // empty: [1, 0]
-        return;
-    }
-    // pixel px has samples X in [px + sx_lo, px + sx_hi]; one pixel of slack on each side
-    const double lx = floor(x0 - double(C.sx_hi)) - 1.0, hx = ceil(x1 - double(C.sx_lo)) + 1.0;
-    const double ly = floor(y0 - double(C.sy_hi)) - 1.0, hy = ceil(y1 - double(C.sy_lo)) + 1.0;
-    auto clamp16 = [](double v) { return uint32_t(fmin(fmax(v, 0.0), 65535.0)); };
-    if (hx < 0.0 || hy < 0.0 || lx > 65535.0 || ly > 65535.0)
-    {
-        bx = by = 1u;
-        return;
-    }
-    bx = clamp16(lx) | (clamp16(hx) << 16);
-    by = clamp16(ly) | (clamp16(hy) << 16);
-}
-
 // Per-camera-origin records (kVarOriginPre): for CSR reference k, tvec = o - v0,
 // qvec = tvec x e1 and DOT(e2, qvec) exactly as triangle.h:82, 90, 98 compute them, in the
-// packed-pair layout of rtd::make_frec (64 B per reference), plus the record's screen box.
+// packed-pair layout of rtd::make_frec (64 B per reference).
 __global__ void __launch_bounds__(kWG) k_origin_pre(const float4 *refs, float4 *frefs, uint32_t n, float ox,
-                                                    float oy, float oz, CullCam cam)
+                                                    float oy, float oz)
 {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n) return;
     const float4 r0 = refs[3 * size_t(k)], r1 = refs[3 * size_t(k) + 1], r2 = refs[3 * size_t(k) + 2];
-    rtd::FRec f = rtd::make_frec(ox, oy, oz, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x);
-    const float T[3] = { f.r0.y, f.r0.w, f.r1.y }, E1[3] = { r0.w, r1.x, r1.y }, E2[3] = { r1.z, r1.w, r2.x };
-    const float Q[3] = { f.r2.z, f.r2.w, f.r3.x };
-    uint32_t bx, by;
-    record_screen_box(cam, T, E1, E2, Q, bx, by);
-    f.r3.z = __uint_as_float(bx);
-    f.r3.w = __uint_as_float(by);
+    const rtd::FRec f = rtd::make_frec(ox, oy, oz, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x);
     frefs[4 * size_t(k) + 0] = f.r0;
     frefs[4 * size_t(k) + 1] = f.r1;
     frefs[4 * size_t(k) + 2] = f.r2;
@@ -2164,7 +1968,7 @@ struct rt_scene
     bool pack_ok = false;           // dims <= 512: the remaining-cell counts pack into one word
     // frefs hold the per-reference terms of this camera origin (bit patterns; valid once computed)
     bool fref_valid = false;
-    uint32_t fref_key[20] = {};     // origin, camera rows, fx, fy, W, H, sample-offset range (bits)
+    uint32_t fref_org[3] = { 0, 0, 0 };
     uint32_t *d_bail = nullptr;     // RT_KERNEL_FLAG_BAIL_WIDE: queued-pixel count + queue
     size_t bail_cap = 0;
     float4 *d_bail_state = nullptr; // RT_KERNEL_FLAG_BAIL_WIDE: phase 1 -> phase 2 per-sample state
@@ -2240,8 +2044,7 @@ int prepare_samples(rt_scene *s, const rt_frame *f, uint32_t spp)
 }
 
 constexpr uint32_t kKernelFlags = RT_KERNEL_FLAG_CENTER_OUT | RT_KERNEL_FLAG_STATIC_ORDER | RT_KERNEL_FLAG_WIDE16 |
-                                  RT_KERNEL_FLAG_LDS_CELLS | RT_KERNEL_FLAG_ONE_PHASE | RT_KERNEL_FLAG_NO_CULL |
-                                  RT_KERNEL_FLAG_EXHAUSTIVE |
+                                  RT_KERNEL_FLAG_LDS_CELLS | RT_KERNEL_FLAG_ONE_PHASE | RT_KERNEL_FLAG_EXHAUSTIVE |
                                   RT_KERNEL_FLAG_WAVE_CLOCK |
                                   RT_KERNEL_FLAG_BAIL_WIDE | RT_KERNEL_BUDGET_MASK;
 
@@ -2313,7 +2116,6 @@ void frame_params(const rt_scene *s, const rt_frame *f, KParams& P)
     P.ntris = s->ntris;
     P.tri_test = f->tri_test;
     P.isect = f->intersector;
-    P.cull = (f->kernel & RT_KERNEL_FLAG_NO_CULL) ? 0u : 1u;
 }
 
 bool use_lanes(const rt_frame *f, uint32_t spp)
@@ -2326,41 +2128,14 @@ bool use_lanes(const rt_frame *f, uint32_t spp)
 // differs from the one the records hold (a moving camera pays one small launch per frame).
 int ensure_origin_terms(rt_scene *s, const KParams& P, hipStream_t st)
 {
-    CullCam cam;
-    std::memcpy(cam.m, P.m, sizeof(cam.m));
-    cam.fx = P.fov_xs;
-    cam.fy = P.fov_xs / P.aspect;
-    cam.W = P.W;
-    cam.H = P.H;
-    cam.sx_lo = cam.sy_lo = 1e30f;
-    cam.sx_hi = cam.sy_hi = -1e30f;
-    for (size_t i = 0; i + 1 < s->smp_host.size(); i += 2)
-    {
-        cam.sx_lo = std::min(cam.sx_lo, s->smp_host[i]);
-        cam.sx_hi = std::max(cam.sx_hi, s->smp_host[i]);
-        cam.sy_lo = std::min(cam.sy_lo, s->smp_host[i + 1]);
-        cam.sy_hi = std::max(cam.sy_hi, s->smp_host[i + 1]);
-    }
-    // 16-bit pixel boxes; finite sample offsets
-    cam.on = P.W <= 65535u && P.H <= 65535u && std::isfinite(cam.sx_lo) && std::isfinite(cam.sx_hi) &&
-             std::isfinite(cam.sy_lo) && std::isfinite(cam.sy_hi) && cam.sx_lo <= cam.sx_hi;
-    uint32_t key[20];
-    std::memcpy(key, P.org, 12);
-    std::memcpy(key + 3, cam.m, 36);
-    std::memcpy(key + 12, &cam.fx, 4);
-    std::memcpy(key + 13, &cam.fy, 4);
-    key[14] = cam.W;
-    key[15] = cam.H;
-    std::memcpy(key + 16, &cam.sx_lo, 4);
-    std::memcpy(key + 17, &cam.sx_hi, 4);
-    std::memcpy(key + 18, &cam.sy_lo, 4);
-    std::memcpy(key + 19, &cam.sy_hi, 4);
-    if (s->fref_valid && std::memcmp(key, s->fref_key, sizeof(key)) == 0) return RT_OK;
+    uint32_t ob[3];
+    std::memcpy(ob, P.org, sizeof(ob));
+    if (s->fref_valid && std::memcmp(ob, s->fref_org, sizeof(ob)) == 0) return RT_OK;
     if (s->nrefs)
         hipLaunchKernelGGL(k_origin_pre, dim3((s->nrefs + kWG - 1) / kWG), dim3(kWG), 0, st, s->d_refs, s->d_frefs,
-                           s->nrefs, P.org[0], P.org[1], P.org[2], cam);
+                           s->nrefs, P.org[0], P.org[1], P.org[2]);
     RT_HIP(hipGetLastError());
-    std::memcpy(s->fref_key, key, sizeof(key));
+    std::memcpy(s->fref_org, ob, sizeof(ob));
     s->fref_valid = true;
     return RT_OK;
 }

@@ -108,8 +108,6 @@ enum rt_kernel {
                                          staged through LDS 64 records at a time */
     RT_KERNEL_FLAG_ONE_PHASE = 0x100, /* OR-able (AUTO): never the two-phase arm, also for shards of
                                          dense scenes (A/B arm of the rank-count policy) */
-    RT_KERNEL_FLAG_NO_CULL = 0x200,   /* OR-able (AUTO): test every reference of every walked cell
-                                         (no screen-box skip of provably rejected references; A/B) */
     RT_KERNEL_FLAG_EXHAUSTIVE = 0x8000, /* OR-able, ray march: evaluate every triangle per step
                                            (no block culling; A/B arm, identical results) */
     RT_KERNEL_FLAG_WAVE_CLOCK = 0x400000, /* OR-able (AUTO), debug: record s_memtime {start, end} of

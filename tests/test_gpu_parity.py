@@ -379,54 +379,6 @@ def test_render_frame_device_on_torch_stream(golden, scenes):
     assert gs.last_kernel_ms() > 0
 
 
-@pytest.mark.parametrize("sid", [8, 1, 5, 2])
-def test_record_cull_random_cameras(scenes, sid):
-    """The screen-box skip of provably rejected references changes no byte:
-    AUTO vs AUTO | RT_KERNEL_FLAG_NO_CULL on random cameras -- inside the grid, grazing close
-    to the geometry, far away, scaled (non-orthonormal) camera matrices, narrow and wide fov,
-    ragged frame sizes, spp 1/4/16 and custom sample offsets reaching the pixel edges."""
-    import torch
-    hs, gs = scenes(sid)
-    d = hs.desc()
-    lo = np.array(list(d.grid.aabb_min), np.float64)
-    hi = np.array(list(d.grid.aabb_max), np.float64)
-    ctr, ext = (lo + hi) / 2, (hi - lo)
-    rng = np.random.default_rng(1234 + sid)
-    checked = 0
-    for case in range(14):
-        kind = case % 4
-        if kind == 0:      # inside the grid
-            eye = lo + rng.uniform(0.05, 0.95, 3) * ext
-        elif kind == 1:    # close to the surface region, looking across it
-            eye = ctr + rng.uniform(-0.7, 0.7, 3) * ext
-        elif kind == 2:    # far
-            eye = ctr + rng.normal(size=3) * 4.0 * np.linalg.norm(ext)
-        else:              # along an axis (axis-aligned rays, zero direction components)
-            eye = ctr.copy()
-            eye[case % 3] += 1.5 * ext[case % 3]
-        at = ctr + rng.uniform(-0.3, 0.3, 3) * ext
-        cam = rtm.look_at(eye.astype(np.float32), at.astype(np.float32))
-        if case % 5 == 4:
-            cam[:12] = (cam[:12] * np.float32(rng.uniform(0.6, 1.6))).astype(np.float32)
-        W, H = [(160, 120), (97, 61), (256, 64), (33, 200)][case % 4]
-        spp = [1, 4, 16][case % 3]
-        offs = None
-        if case % 7 == 3:
-            offs = rng.uniform(-0.5, 0.5, (spp, 2)).astype(np.float32)
-            offs[0] = (-0.5, -0.5)
-        f0 = gs.frame(W, H, spp, sample_offsets=offs)
-        f1 = gs.frame(W, H, spp, sample_offsets=offs, kernel=rtm.RT_KERNEL_FLAG_NO_CULL)
-        for f in (f0, f1):
-            for i in range(16):
-                f.cam[i] = float(cam[i])
-            f.fov = float(rng.uniform(10.0, 120.0)) if f is f0 else f0.fov
-        a = gs.render_frame(f0)
-        b = gs.render_frame(f1)
-        np.testing.assert_array_equal(a, b, err_msg=f"scene {sid} case {case}")
-        checked += int((a != a[0, 0]).any())
-    assert checked >= 4          # most cameras see geometry
-
-
 def test_kernel_times_ring(scenes):
     """rt_kernel_times: one positive render-kernel time per launch since the previous call."""
     import torch

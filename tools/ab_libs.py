@@ -60,19 +60,18 @@ def main():
     st = torch.cuda.current_stream()
     W, H, S = a.size
     out = torch.empty(W * H, dtype=torch.int32, device="cuda")
+    # one scene object per arm: arms never share per-scene state (heavy-first plans, records)
     scenes = {}
     for name, lib, k in arms:
         m = mods[lib]
         for sid in a.scenes:
-            key = (lib, sid)
-            if key not in scenes:
-                scenes[key] = m.GpuScene(m.HostScene.load(sid), 0)
+            scenes[(name, sid)] = m.GpuScene(m.HostScene.load(sid), 0)
     times = {(n, sid): [] for n, _, _ in arms for sid in a.scenes}
     dig = {}
     for r in range(a.rounds + 1):
         for name, lib, k in arms:
             for sid in a.scenes:
-                gs = scenes[(lib, sid)]
+                gs = scenes[(name, sid)]
                 f = gs.frame(W, H, S, kernel=k)
                 evs = []
                 for _ in range(a.reps):
