@@ -47,6 +47,7 @@ RT_KERNEL_FLAG_STATIC_ORDER = 0x20
 RT_KERNEL_FLAG_WIDE16 = 0x40
 RT_KERNEL_FLAG_LDS_CELLS = 0x80
 RT_KERNEL_FLAG_ONE_PHASE = 0x100
+RT_KERNEL_FLAG_WIDE_HEAVY = 0x200
 RT_KERNEL_FLAG_EXHAUSTIVE = 0x8000
 RT_KERNEL_FLAG_WAVE_CLOCK = 0x400000
 RT_KERNEL_FLAG_BAIL_WIDE = 0x80000000
@@ -63,7 +64,7 @@ TRACER_SYMBOLS = [
     "rt_get_device_count", "rt_scene_create", "rt_scene_destroy", "rt_scene_device_bytes",
     "rt_render_tiles", "rt_render_frame_device", "rt_shard_elems", "rt_render_shard_device",
     "rt_unshard_device", "rt_last_kernel_ms", "rt_trace_samples", "rt_debug_primitives",
-    "rt_debug_rcp_check", "rt_debug_wave_clocks", "rt_debug_heavy_first",
+    "rt_debug_rcp_check", "rt_debug_wave_clocks", "rt_debug_heavy_first", "rt_debug_wide_items",
     "rt_sample_table", "rt_last_error", "rt_abi_version", "rt_grid_build", "rt_grid_free",
     "rt_scene_create_from_mesh", "rt_kernel_times", "rt_render_frame_host", "rt_frame_host_wait", "rt_host_alloc",
     "rt_host_free",
@@ -173,6 +174,8 @@ def tracer_lib():
         if hasattr(L, "rt_debug_heavy_first"):       # absent in builds before ABI 3 (A/B runs)
             L.rt_debug_heavy_first.argtypes = [vp, ctypes.POINTER(c_u32), ctypes.POINTER(c_u32),
                                                ctypes.POINTER(c_u32)]
+        if hasattr(L, "rt_debug_wide_items"):
+            L.rt_debug_wide_items.argtypes = [vp, ctypes.POINTER(c_u32)]
         L.rt_sample_table.argtypes = [c_u32, vp]
         L.rt_last_error.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
         L.rt_get_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
@@ -540,6 +543,13 @@ class GpuScene:
         _check(L.rt_debug_heavy_first(self._h, ctypes.byref(f), ctypes.byref(n), ctypes.byref(e)), L,
                "rt_debug_heavy_first")
         return f.value, n.value, e.value
+
+    def wide_items(self):
+        """RT_KERNEL_FLAG_WIDE_HEAVY: work items the newest plan lists for the wide section."""
+        L = tracer_lib()
+        n = c_u32()
+        _check(L.rt_debug_wide_items(self._h, ctypes.byref(n)), L, "rt_debug_wide_items")
+        return n.value
 
     def last_kernel_ms(self):
         ms = c_f32()

@@ -74,6 +74,7 @@ constexpr int kVarWaveClock = 32768;        // RT_KERNEL_FLAG_WAVE_CLOCK: per-it
 constexpr int kVarUniform = 65536;          // scalar loop for wave-uniform cell lists
 constexpr int kVarBail = 131072;            // RT_KERNEL_FLAG_BAIL_WIDE phase 1: test budget + pixel queue
 constexpr int kVarLdsCells = 262144;        // RT_KERNEL_FLAG_LDS_CELLS: long uniform lists staged in LDS
+constexpr int kVarWideHeavy = 524288;       // RT_KERNEL_FLAG_WIDE_HEAVY: heavy items traced wide at the start
 constexpr int kVarCenterOut = 1048576;      // RT_KERNEL_FLAG_CENTER_OUT: XCD row turns from the middle out
 // AUTO's traversal: every feature above that is exact for every scene ...
 constexpr int kVarAutoCore = kVarWaveGate | kVarDistSkip | kVarOriginPre | kVarXcdBands | kVarUniform;
@@ -85,8 +86,9 @@ constexpr uint32_t kMarchSteps = 128;       // renderer.cpp:26
 constexpr uint32_t kDistBlock = 32;         // triangles per culling block of the distance kernels
 
 // heavy-first plan (one per list version): blocks listed at each of the two priority levels,
-// the maximum block cost and the sum of wave costs of the measured frame
-struct HfPlan { uint32_t cnt_hi, cnt_lo, maxc, pad; unsigned long long sum; };
+// the maximum block cost, the work items listed for the wide section (kVarWideHeavy) and the
+// sum of wave costs of the measured frame
+struct HfPlan { uint32_t cnt_hi, cnt_lo, maxc, cnt_w; unsigned long long sum; };
 
 struct KParams
 {
@@ -142,6 +144,21 @@ struct KParams
     const HfPlan *hf_plan_in;   // the current plan (also the previous measurement's max and sum)
     HfPlan *hf_plan_out;        // the next plan, cleared by the measured frame's first lane
     uint32_t *hf_cost;          // per work item: shader cycles of its wave in the measured frame
+                                // (a wide item: the sum over its waves)
+    // wide section (kVarWideHeavy; wh_on == 0: off).  k_render_wh's wh_wgs workgroups trace the
+    // work items the current plan lists as heavy (wh_list_in, plan->cnt_w of them), G lanes per
+    // sample, and the lane waves skip items whose wh_mark_in == hf_ver; with wh_wgs == 0 (no
+    // list seen yet, or a refresh frame) the lane waves render every item.  k_hf_plan lists an
+    // item when its lane-mode cost passes max(wh_floor, wh_alpha16 / 16 x the estimated frame
+    // span), and keeps the current plan's items (their cost words still hold the lane-mode cost
+    // of the last frame that measured them) except in a refresh frame.
+    uint32_t wh_on, wh_wgs, wh_refresh;
+    uint32_t wh_floor, wh_alpha16;
+    const uint32_t *wh_mark_in;
+    uint32_t *wh_mark_out;
+    const uint32_t *wh_list_in;
+    uint32_t *wh_list_out;
+    uint32_t *wh_host_cnt;      // host-mapped: the newest plan's cnt_w (sizes the next launches)
     uint32_t bail_tests;        // BAIL_WIDE phase 1: test budget per sample
     uint32_t *bail_count;       // BAIL_WIDE: queued pixels
     uint32_t *bail_queue;       // BAIL_WIDE: (local tile << 8 | Morton pixel) per queued pixel
@@ -1031,6 +1048,10 @@ __host__ __device__ constexpr uint32_t bail_auto_tests(uint32_t nranks)
 #define RT_HF_FLOOR 100000
 #endif
 constexpr uint32_t kHfFrontMax = RT_HF_FRONT;   // blocks (4 waves each): half the chip's wave slots
+constexpr uint32_t kWhMax = 4096;
+#ifndef RT_WH_PF
+#define RT_WH_PF false                      // kVarWideHeavy: one-ahead record prefetch in the wide waves
+#endif           // kVarWideHeavy: work items the wide section can list
 #ifndef RT_HF_MIN_BLOCKS
 #define RT_HF_MIN_BLOCKS 4096
 #endif
@@ -1079,31 +1100,50 @@ __device__ __forceinline__ uint32_t xcd_band_block(uint32_t b, uint32_t nb, uint
 // cost milliseconds, measured).
 __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks)
 {
-    __shared__ uint32_t s_max, s_hi, s_lo, s_bhi, s_blo;
+    __shared__ uint32_t s_max, s_hi, s_lo, s_w, s_bhi, s_blo, s_bw;
     __shared__ unsigned long long s_sum;
     const uint32_t b = blockIdx.x * kWG + threadIdx.x;
     if (threadIdx.x == 0u)
     {
-        s_max = s_hi = s_lo = 0u;
+        s_max = s_hi = s_lo = s_w = 0u;
         s_sum = 0ull;
     }
     __syncthreads();
-    uint32_t cost = 0u, sum = 0u;
+    const HfPlan last = *P.hf_plan_in;
+    uint32_t cost = 0u, sum = 0u, wmask = 0u;
+    uint4 c = make_uint4(0u, 0u, 0u, 0u);
     if (b < nblocks)
     {
-        const uint4 c = reinterpret_cast<const uint4 *>(P.hf_cost)[b];     // kWavesPerWG == 4
-        cost = max(max(c.x, c.y), max(c.z, c.w));
+        c = reinterpret_cast<const uint4 *>(P.hf_cost)[b];                // kWavesPerWG == 4
         sum = (c.x >> 4) + (c.y >> 4) + (c.z >> 4) + (c.w >> 4);          // in 16-cycle units
+        if (P.wh_on && last.sum)
+        {
+            // wide section: items above a fraction of the frame span estimated from the last
+            // measurement (sum of wave costs over the resident waves)
+            const uint64_t span = (last.sum << 4) / kHfSlots;
+            const uint32_t thr = max(P.wh_floor, uint32_t(min<uint64_t>(span * P.wh_alpha16 / 16u, 0xFFFFFFFFull)));
+            wmask = uint32_t(c.x > thr) | (uint32_t(c.y > thr) << 1) | (uint32_t(c.z > thr) << 2) |
+                    (uint32_t(c.w > thr) << 3);
+        }
+        if (P.wh_on && !P.wh_refresh && P.hf_ver)
+        {
+            const uint4 m = reinterpret_cast<const uint4 *>(P.wh_mark_in)[b];
+            wmask |= uint32_t(m.x == P.hf_ver) | (uint32_t(m.y == P.hf_ver) << 1) | (uint32_t(m.z == P.hf_ver) << 2) |
+                     (uint32_t(m.w == P.hf_ver) << 3);
+        }
+        // the heavy-first order ranks a block by its slowest wave left in the lane section
+        cost = max(max((wmask & 1u) ? 0u : c.x, (wmask & 2u) ? 0u : c.y),
+                   max((wmask & 4u) ? 0u : c.z, (wmask & 8u) ? 0u : c.w));
     }
-    const HfPlan last = *P.hf_plan_in;
     const bool tail = uint64_t(last.maxc) * kHfSlots * 16u > uint64_t(kHfTail) * (last.sum << 4);
     const uint32_t thr = max(P.hf_floor, last.maxc >> kHfShift);
-    const bool heavy = tail && cost > thr;
+    const bool heavy = P.hf_front && tail && cost > thr;
     const bool hi = heavy && cost > (last.maxc >> 1);
-    uint32_t rank = 0u;
+    uint32_t rank = 0u, wrank = 0u;
     if (cost) atomicMax(&s_max, cost);
     if (sum) atomicAdd(&s_sum, (unsigned long long)sum);
     if (heavy) rank = atomicAdd(hi ? &s_hi : &s_lo, 1u);
+    if (wmask) wrank = atomicAdd(&s_w, uint32_t(__popc(wmask)));
     __syncthreads();
     if (threadIdx.x == 0u)
     {
@@ -1111,6 +1151,7 @@ __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks)
         if (s_sum) atomicAdd(&P.hf_plan_out->sum, s_sum);
         s_bhi = s_hi ? atomicAdd(&P.hf_plan_out->cnt_hi, s_hi) : 0u;
         s_blo = s_lo ? atomicAdd(&P.hf_plan_out->cnt_lo, s_lo) : 0u;
+        s_bw = s_w ? atomicAdd(&P.hf_plan_out->cnt_w, s_w) : 0u;
     }
     __syncthreads();
     if (heavy)
@@ -1124,12 +1165,26 @@ __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks)
             P.hf_list_out[slot] = b;           // may be overwritten by the other level: see below
         }
     }
-    // the marks are written by a second pass over the final list (k_hf_mark), so a slot claimed
-    // by both levels marks only the block whose entry survived
+    // wide items: listed and marked for the next plan's frames (beyond kWhMax they stay in the
+    // lane section)
+    for (uint32_t j = 0; j < kWavesPerWG; j++)
+        if (wmask & (1u << j))
+        {
+            const uint32_t r = s_bw + wrank++;
+            if (r < kWhMax)
+            {
+                const uint32_t item = b * kWavesPerWG + j;
+                P.wh_list_out[r] = item;
+                P.wh_mark_out[item] = P.hf_ver + 1u;
+            }
+        }
+    // the block marks are written by a second pass over the final list (k_hf_mark), so a slot
+    // claimed by both levels marks only the block whose entry survived
 }
 
 // Marks the blocks of the new plan's list (after k_hf_plan): the front section of the frames
 // using it renders exactly the slots [0, cnt_hi) and [front - cnt_lo, front) that do not overlap.
+// Also hands the wide section's item count to the host (it sizes the section of later launches).
 __global__ void __launch_bounds__(kWG) k_hf_mark(KParams P)
 {
     const uint32_t j = blockIdx.x * kWG + threadIdx.x;
@@ -1137,6 +1192,7 @@ __global__ void __launch_bounds__(kWG) k_hf_mark(KParams P)
     const uint32_t hi = min(pl.cnt_hi, P.hf_front);
     const uint32_t lo = min(pl.cnt_lo, P.hf_front - hi);
     if (j < P.hf_front && (j < hi || j >= P.hf_front - lo)) P.hf_mark_out[P.hf_list_out[j]] = P.hf_ver + 1u;
+    if (j == 0u && P.wh_host_cnt) *(volatile uint32_t *)P.wh_host_cnt = min(pl.cnt_w, kWhMax);
 }
 
 // The launch's block -> block-of-work map.  With the heavy-first order on, blocks [0, hf_front)
@@ -1147,26 +1203,28 @@ __global__ void __launch_bounds__(kWG) k_hf_mark(KParams P)
 template <int VAR>
 __device__ __forceinline__ bool block_of_launch(const KParams& P, uint32_t& b)
 {
+    const uint32_t bid = blockIdx.x, nblk = gridDim.x;
+    if ((VAR & kVarWideHeavy) && P.hf_measure && bid == 0u && threadIdx.x == 0u)
+        *P.hf_plan_out = HfPlan{0u, 0u, 0u, 0u, 0ull};        // k_hf_plan runs after this kernel
     if (P.hf_front)
     {
-        if (P.hf_measure && blockIdx.x == 0u && threadIdx.x == 0u)
+        if (P.hf_measure && bid == 0u && threadIdx.x == 0u)
             *P.hf_plan_out = HfPlan{0u, 0u, 0u, 0u, 0ull};    // k_hf_plan runs after this kernel
         const uint32_t front = P.hf_front;
-        if (blockIdx.x < front)
+        if (bid < front)
         {
             const uint32_t hi = min(P.hf_plan_in->cnt_hi, front);
             const uint32_t lo = min(P.hf_plan_in->cnt_lo, front - hi);
-            if (blockIdx.x >= hi && blockIdx.x < front - lo) return false;
-            b = P.hf_list_in[blockIdx.x];
+            if (bid >= hi && bid < front - lo) return false;
+            b = P.hf_list_in[bid];
             return true;
         }
-        const uint32_t q = blockIdx.x - front;
-        const uint32_t nb = gridDim.x - front;
+        const uint32_t q = bid - front;
+        const uint32_t nb = nblk - front;
         b = (VAR & kVarXcdBands) ? xcd_band_block<(VAR & kVarCenterOut) != 0>(q, nb, P.xcd_chunk) : q;
         return P.hf_ver == 0u || P.hf_mark_in[b] != P.hf_ver;
     }
-    b = (VAR & kVarXcdBands) ? xcd_band_block<(VAR & kVarCenterOut) != 0>(blockIdx.x, gridDim.x, P.xcd_chunk)
-                             : blockIdx.x;
+    b = (VAR & kVarXcdBands) ? xcd_band_block<(VAR & kVarCenterOut) != 0>(bid, nblk, P.xcd_chunk) : bid;
     return true;
 }
 
@@ -1181,7 +1239,7 @@ __device__ __forceinline__ bool block_of_launch(const KParams& P, uint32_t& b)
 // One sample of the wide mode, traced by the G lanes of a group (sub = this lane's index in it):
 // the same walk in every lane of the group, each cell's list split over the group.  Returns the
 // sample's colour in every lane of the group.
-template <int VAR, int G, bool RESUME = false>
+template <int VAR, int G, bool RESUME = false, bool PF = true>
 __device__ __forceinline__ void wide_trace(const KParams& P, uint32_t k, uint32_t slot, uint32_t sub, float& cr,
                                            float& cg, float& cb)
 {
@@ -1267,7 +1325,7 @@ __device__ __forceinline__ void wide_trace(const KParams& P, uint32_t k, uint32_
                         // record k + G loads while record k is tested: the wide phase runs few,
                         // latency-bound waves, so the extra registers cost no throughput
                         float4 n0, n1, n2, n3;
-                        if (kb + sub < ke)
+                        if (PF && kb + sub < ke)
                         {
                             const float4 *rp = P.frefs + size_t(kb + sub) * 4u;
                             n0 = rp[0];
@@ -1278,8 +1336,16 @@ __device__ __forceinline__ void wide_trace(const KParams& P, uint32_t k, uint32_
                         const rtd::f2v ra = {dx, dy}, rc = {dy, dz};
                         for (uint32_t k = kb + sub; k < ke; k += uint32_t(G))
                         {
-                            const float4 r0 = n0, r1 = n1, r2 = n2, r3 = n3;
-                            if (k + uint32_t(G) < ke)
+                            float4 r0 = n0, r1 = n1, r2 = n2, r3 = n3;
+                            if (!PF)
+                            {
+                                const float4 *rp = P.frefs + size_t(k) * 4u;
+                                r0 = rp[0];
+                                r1 = rp[1];
+                                r2 = rp[2];
+                                r3 = rp[3];
+                            }
+                            else if (k + uint32_t(G) < ke)
                             {
                                 const float4 *rp = P.frefs + size_t(k + uint32_t(G)) * 4u;
                                 n0 = rp[0];
@@ -1340,13 +1406,13 @@ __device__ __forceinline__ void wide_trace(const KParams& P, uint32_t k, uint32_
 }
 
 // One wave of the wide mode: the 64 / G consecutive sample slots slot0 .. of local tile k.
-template <int VAR, int G>
+template <int VAR, int G, bool PF = true>
 __device__ __forceinline__ void wide_samples(const KParams& P, uint32_t k, uint32_t slot0)
 {
     const uint32_t lane = threadIdx.x & 63u, sub = lane & uint32_t(G - 1), grp = lane / uint32_t(G);
     const uint32_t slot = slot0 + grp;
     float cr, cg, cb;
-    wide_trace<VAR, G>(P, k, slot, sub, cr, cg, cb);
+    wide_trace<VAR, G, false, PF>(P, k, slot, sub, cr, cg, cb);
     // the pixel's samples are the groups grp0 .. grp0 + spp - 1 of this wave: sum in sample order
     const ItemCoord ic = tile_slot_coord(P, k, slot);
     const uint32_t grp0 = grp & ~(P.spp - 1u);
@@ -1366,8 +1432,32 @@ __device__ __forceinline__ void wide_samples(const KParams& P, uint32_t k, uint3
     }
 }
 
+// kVarWideHeavy: the launch's wide section.  Its waves take the current plan's heavy work items
+// in list order, G waves per item (each 64 / G of the item's sample slots, G lanes per sample):
+// persistent over the list, so a section smaller than the list (the host sizes it from an older
+// plan's count) still renders every listed item.  They record no cost: an item's cost word keeps
+// its lane-mode measurement until a refresh frame renders it one lane per sample again.
+template <int G>
+__device__ __forceinline__ void wide_section(const KParams& P)
+{
+    const uint32_t n = P.hf_ver ? min(P.hf_plan_in->cnt_w, kWhMax) : 0u;
+    const uint32_t w = blockIdx.x * kWavesPerWG + (threadIdx.x >> 6), nw = P.wh_wgs * kWavesPerWG;
+    const uint32_t ipt = P.wg_per_tile * kWavesPerWG;              // items per tile
+    for (uint32_t e = w; e < n * uint32_t(G); e += nw)
+    {
+        const uint32_t item = __builtin_amdgcn_readfirstlane(P.wh_list_in[e / uint32_t(G)]);
+        const uint32_t part = e % uint32_t(G);
+        const uint32_t kseq = item / ipt;
+        const uint32_t slot0 = (item - kseq * ipt) * 64u + part * (64u / uint32_t(G));
+        // the parameters re-read per item (late_params): hoisted out of the loop they held ~30
+        // more SGPRs across it and spilled
+        const KParams& Q = late_params(P);
+        wide_samples<kVarWide, G, RT_WH_PF>(Q, Q.tile_order ? Q.tile_order[kseq] : kseq, slot0);
+    }
+}
+
 // RT_KERNEL_LANES / AUTO: one lane per sample (spp = 2^spp_shift <= 64), one work item per
-// wave.  Heavy-first order: see block_of_launch and k_hf_plan.
+// wave.  Heavy-first order: see block_of_launch and k_hf_plan; wide section: wide_section.
 template <int TRI, int VAR>
 __global__ void __launch_bounds__(kWG) k_render_lanes(KParams P)
 {
@@ -1376,6 +1466,8 @@ __global__ void __launch_bounds__(kWG) k_render_lanes(KParams P)
     uint32_t b;
     if (!block_of_launch<VAR>(P, b)) return;
     const uint32_t item = b * kWavesPerWG + (threadIdx.x >> 6);
+    if constexpr ((VAR & kVarWideHeavy) != 0)
+        if (P.wh_wgs && P.hf_ver && P.wh_mark_in[item] == P.hf_ver) return;   // traced by the wide section
     if constexpr ((VAR & kVarWaveClock) != 0)
     {
         // debug arm (RT_KERNEL_FLAG_WAVE_CLOCK): s_memtime at the item's start and end, and how
@@ -1414,6 +1506,13 @@ __global__ void __launch_bounds__(kWG) k_render_lanes(KParams P)
             if ((threadIdx.x & 63u) == 0u) Q.hf_cost[__builtin_amdgcn_readfirstlane(item)] = t1 - t0;
         }
     }
+}
+
+// kVarWideHeavy: the wide section, launched on the scene's side stream beside the lane kernel
+// (its own register allocation: folded into the lane kernel it cost 106 SGPRs and spills)
+__global__ void __launch_bounds__(kWG) k_render_wh(KParams P)
+{
+    wide_section<16>(P);
 }
 
 // RT_KERNEL_WIDE: every tile in wide mode (the A/B arm of the two-phase frame)
@@ -1938,6 +2037,9 @@ struct HfCtx
     uint32_t *cost = nullptr;           // [cap_blocks * kWavesPerWG] wave cycles of the last frame
     uint32_t *lists = nullptr;          // [2][kHfFrontMax], by plan version parity
     HfPlan *plans = nullptr;            // [2], by plan version parity
+    uint32_t *wh_marks = nullptr;       // [2][cap_blocks * kWavesPerWG] wide items, by version parity
+    uint32_t *wh_lists = nullptr;       // [2][kWhMax]
+    uint32_t *wh_cnt = nullptr;         // host-mapped: the newest plan's wide item count
     uint32_t frames = 0;                // frames rendered with this shape
     uint32_t ver = 0;                   // version of the newest plan launched
     uint64_t used = 0;                  // LRU stamp
@@ -1994,6 +2096,9 @@ struct rt_scene
     hipEvent_t kt0[kTimeRing] = {}, kt1[kTimeRing] = {};
     uint32_t kt_next = 0, kt_count = 0;
     hipStream_t last_stream = nullptr;  // stream of the last launch (cross-stream ordering)
+    // RT_KERNEL_FLAG_WIDE_HEAVY: side stream of the wide section, fork / join events
+    hipStream_t side = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     // staging for rt_render_tiles / records
     uint32_t *d_frame = nullptr;
     size_t frame_cap = 0;
@@ -2044,6 +2149,7 @@ int prepare_samples(rt_scene *s, const rt_frame *f, uint32_t spp)
 }
 
 constexpr uint32_t kKernelFlags = RT_KERNEL_FLAG_CENTER_OUT | RT_KERNEL_FLAG_STATIC_ORDER | RT_KERNEL_FLAG_WIDE16 |
+                                  RT_KERNEL_FLAG_WIDE_HEAVY |
                                   RT_KERNEL_FLAG_LDS_CELLS | RT_KERNEL_FLAG_ONE_PHASE | RT_KERNEL_FLAG_EXHAUSTIVE |
                                   RT_KERNEL_FLAG_WAVE_CLOCK |
                                   RT_KERNEL_FLAG_BAIL_WIDE | RT_KERNEL_BUDGET_MASK;
@@ -2140,9 +2246,20 @@ int ensure_origin_terms(rt_scene *s, const KParams& P, hipStream_t st)
     return RT_OK;
 }
 
+// kVarWideHeavy thresholds: an item goes wide above max(floor, alpha16 / 16 x estimated span)
+// shader cycles; RT_WH_FLOOR / RT_WH_ALPHA16 override them (A/B sweeps)
+constexpr uint32_t kWhFloor = 200000;
+constexpr uint32_t kWhRefresh = 64;         // frames between refresh frames (a multiple of kHfPeriod)
+constexpr uint32_t kWhAlpha16 = 32;
+uint32_t wh_tunable(const char *name, uint32_t dflt)
+{
+    const char *e = std::getenv(name);
+    return e && *e ? uint32_t(std::strtoul(e, nullptr, 0)) : dflt;
+}
+
 // Heavy-first state for this launch shape (AUTO): fills P.hf_*.  A new shape takes the least
 // recently used context and clears it on the launch stream (no host synchronisation).
-int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, hipStream_t st)
+int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hipStream_t st)
 {
     const uint64_t key[4] = { (blocks << 16) | (uint64_t(P.spp) << 1) | 1u,
                               (uint64_t(P.rx0) << 32) | P.ry0, (uint64_t(P.rw) << 32) | P.rh,
@@ -2159,23 +2276,29 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, hipStream_t st
         {
             if (c->marks) RT_HIP(hipFree(c->marks));
             if (c->cost) RT_HIP(hipFree(c->cost));
-            c->marks = c->cost = nullptr;
+            if (c->wh_marks) RT_HIP(hipFree(c->wh_marks));
+            c->marks = c->cost = c->wh_marks = nullptr;
             RT_HIP(hipMalloc(&c->marks, sizeof(uint32_t) * 2 * blocks));
             RT_HIP(hipMalloc(&c->cost, sizeof(uint32_t) * kWavesPerWG * blocks));
+            RT_HIP(hipMalloc(&c->wh_marks, sizeof(uint32_t) * 2 * kWavesPerWG * blocks));
             c->cap_blocks = uint32_t(blocks);
             if (!c->lists)
             {
                 RT_HIP(hipMalloc(&c->lists, sizeof(uint32_t) * 2 * kHfFrontMax));
                 RT_HIP(hipMalloc(&c->plans, sizeof(HfPlan) * 2));
+                RT_HIP(hipMalloc(&c->wh_lists, sizeof(uint32_t) * 2 * kWhMax));
+                RT_HIP(hipHostMalloc(&c->wh_cnt, sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent));
             }
         }
         RT_HIP(hipMemsetAsync(c->marks, 0, sizeof(uint32_t) * 2 * c->cap_blocks, st));
+        RT_HIP(hipMemsetAsync(c->wh_marks, 0, sizeof(uint32_t) * 2 * kWavesPerWG * c->cap_blocks, st));
         RT_HIP(hipMemsetAsync(c->plans, 0, sizeof(HfPlan) * 2, st));
+        *(volatile uint32_t *)c->wh_cnt = 0u;
         std::memcpy(c->key, key, sizeof(key));
         c->nblocks = uint32_t(blocks);
         // front: an eighth of the blocks, capped, a multiple of the XCD count so the natural
         // section keeps its block -> XCD assignment
-        c->front = std::min<uint32_t>(kHfFrontMax, uint32_t(blocks / 8u) & ~(kXcds - 1u));
+        c->front = front ? std::min<uint32_t>(kHfFrontMax, uint32_t(blocks / 8u) & ~(kXcds - 1u)) : 0u;
         c->frames = 0;
         c->ver = 0;
     }
@@ -2195,6 +2318,28 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, hipStream_t st
     P.hf_plan_in = c->plans + (v & 1u);
     P.hf_plan_out = c->plans + ((v + 1u) & 1u);
     P.hf_cost = c->cost;
+    if (var & kVarWideHeavy)
+    {
+        // the section holds G waves per listed item of the newest plan the host has seen (a
+        // plan or two old: the count is read without waiting); at least one workgroup, since
+        // the device-side list may already be longer (the section is persistent over it)
+        // refresh: every kWhRefresh-th frame renders every item one lane per sample, so the
+        // next plan re-ranks all items on lane-mode costs (the wide set is otherwise sticky)
+        const uint32_t G = 16u;
+        const uint32_t cnt = *(volatile uint32_t *)c->wh_cnt;
+        P.wh_on = 1u;
+        P.wh_refresh = (c->frames - 1u) % kWhRefresh == 0u;       // frames counts this one
+        P.wh_wgs = P.wh_refresh ? 0u : (cnt * G + kWavesPerWG - 1u) / kWavesPerWG;
+        P.wh_floor = wh_tunable("RT_WH_FLOOR", kWhFloor);
+        P.wh_alpha16 = wh_tunable("RT_WH_ALPHA16", kWhAlpha16);
+        P.wh_mark_in = c->wh_marks + size_t(v & 1u) * kWavesPerWG * c->cap_blocks;
+        P.wh_mark_out = c->wh_marks + size_t((v + 1u) & 1u) * kWavesPerWG * c->cap_blocks;
+        P.wh_list_in = c->wh_lists + size_t(v & 1u) * kWhMax;
+        P.wh_list_out = c->wh_lists + size_t((v + 1u) & 1u) * kWhMax;
+        void *dev = nullptr;
+        RT_HIP(hipHostGetDevicePointer(&dev, c->wh_cnt, 0));
+        P.wh_host_cnt = static_cast<uint32_t *>(dev);
+    }
     if (P.hf_measure) c->ver = v + 1u;                  // the plan launched after this frame
     return RT_OK;
 }
@@ -2217,6 +2362,7 @@ kfn_t lanes_kernel(int tri, int var)
     case kVarAutoCore | kVarFastRcp: return k_render_lanes<RT_TRI_MOLLER_TRUMBORE, kVarAutoCore | kVarFastRcp>;
     case kVarAutoCore: return k_render_lanes<RT_TRI_MOLLER_TRUMBORE, kVarAutoCore>;
     case kVarAuto | kVarCenterOut: return k_render_lanes<RT_TRI_MOLLER_TRUMBORE, kVarAuto | kVarCenterOut>;
+    case kVarAuto | kVarWideHeavy: return k_render_lanes<RT_TRI_MOLLER_TRUMBORE, kVarAuto | kVarWideHeavy>;
     case kVarAuto | kVarWaveClock: return k_render_lanes<RT_TRI_MOLLER_TRUMBORE, kVarAuto | kVarWaveClock>;
     case kVarAuto | kVarLdsCells: return k_render_lanes<RT_TRI_MOLLER_TRUMBORE, kVarAuto | kVarLdsCells>;
     case kVarAuto | kVarLdsCells | kVarWaveClock:
@@ -2305,8 +2451,11 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
     // the plain kernel -> 0.48 / 0.35 / 0.25 with budgets 384 / 192 / 128).  On a whole frame,
     // or a scene without dense cells, phase 1's budget count and the re-trace cost more than
     // they save.
+    // the wide section (kVarWideHeavy) needs the wide code's layout and spp <= 16
+    const bool wide_heavy = wide_ok && kind == RT_KERNEL_AUTO && (f->kernel & RT_KERNEL_FLAG_WIDE_HEAVY) && P.spp <= 4u &&
+                            !(f->kernel & RT_KERNEL_FLAG_BAIL_WIDE);
     const bool bail_auto = kind == RT_KERNEL_AUTO && P.nranks >= kBailAutoRanks && s->max_cell_refs >= kBailAutoRefs &&
-                           !(f->kernel & RT_KERNEL_FLAG_ONE_PHASE);
+                           !(f->kernel & RT_KERNEL_FLAG_ONE_PHASE) && !wide_heavy;
     const bool bail = wide_ok && kind == RT_KERNEL_AUTO && (bail_auto || (f->kernel & RT_KERNEL_FLAG_BAIL_WIDE));
     const bool g16 = ((f->kernel & RT_KERNEL_FLAG_WIDE16) || (bail_auto && !(f->kernel & RT_KERNEL_FLAG_BAIL_WIDE))) &&
                      P.spp * 16u <= 64u;
@@ -2371,24 +2520,47 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
     else if (lanes)
     {
         // AUTO, LANES, and WIDE / COMPACT where their layout does not apply
-        const int kvar = (kind == RT_KERNEL_AUTO || P.isect != RT_ISECT_GRID) ? var : 0;
+        const int kvar = ((kind == RT_KERNEL_AUTO || P.isect != RT_ISECT_GRID) ? var : 0) |
+                         (wide_heavy ? kVarWideHeavy : 0);
         const kfn_t fn = lanes_kernel(bary ? RT_TRI_BARYCENTRIC : RT_TRI_MOLLER_TRUMBORE, kvar);
         if (!fn) return fail(RT_E_INVALID, "kernel variant not built: " + std::to_string(kvar));
         uint32_t grid = uint32_t(blocks);
         // heavy-first order: AUTO grid frames large enough that blocks start in several rounds
-        if (kind == RT_KERNEL_AUTO && P.isect == RT_ISECT_GRID && !(kvar & kVarWaveClock) &&
-            !(f->kernel & RT_KERNEL_FLAG_STATIC_ORDER) && blocks >= kHfMinBlocks)
+        const bool front = kind == RT_KERNEL_AUTO && P.isect == RT_ISECT_GRID && !(kvar & kVarWaveClock) &&
+                           !(f->kernel & RT_KERNEL_FLAG_STATIC_ORDER) &&
+                           (blocks >= kHfMinBlocks || (wide_heavy && blocks >= 64u && wh_tunable("RT_WH_FRONT", 0u)));
+        if (front || wide_heavy)
         {
-            if (int rc = hf_prepare(s, P, blocks, kvar, st)) return rc;
+            if (int rc = hf_prepare(s, P, blocks, kvar, front, st)) return rc;
             grid += P.hf_front;
         }
         RT_HIP(mark(kt0));
+        if (P.wh_wgs)
+        {
+            // the wide section runs on the side stream beside the lane kernel (fork / join by
+            // events, so the pair also captures into a hipGraph); submitted first so its waves
+            // -- the frame's longest -- start first
+            if (!s->side)
+            {
+                RT_HIP(hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking));
+                RT_HIP(hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming));
+                RT_HIP(hipEventCreateWithFlags(&s->ev_join, hipEventDisableTiming));
+            }
+            RT_HIP(hipEventRecord(s->ev_fork, st));
+            RT_HIP(hipStreamWaitEvent(s->side, s->ev_fork, 0));
+            hipLaunchKernelGGL(k_render_wh, dim3(P.wh_wgs), wg, 0, s->side, P);
+        }
         hipLaunchKernelGGL(fn, dim3(grid), wg, 0, st, P);
+        if (P.wh_wgs)
+        {
+            RT_HIP(hipEventRecord(s->ev_join, s->side));
+            RT_HIP(hipStreamWaitEvent(st, s->ev_join, 0));
+        }
         RT_HIP(mark(kt1));
-        if (P.hf_front && P.hf_measure)
+        if ((P.hf_front || P.wh_on) && P.hf_measure)
         {
             hipLaunchKernelGGL(k_hf_plan, dim3(uint32_t((blocks + kWG - 1) / kWG)), wg, 0, st, P, uint32_t(blocks));
-            hipLaunchKernelGGL(k_hf_mark, dim3((P.hf_front + kWG - 1) / kWG), wg, 0, st, P);
+            hipLaunchKernelGGL(k_hf_mark, dim3(std::max(1u, (P.hf_front + kWG - 1) / kWG)), wg, 0, st, P);
         }
     }
     else
@@ -2734,7 +2906,13 @@ int rt_scene_destroy(rt_scene *s)
             (void)hipFree(h.cost);
             (void)hipFree(h.lists);
             (void)hipFree(h.plans);
+            (void)hipFree(h.wh_marks);
+            (void)hipFree(h.wh_lists);
+            if (h.wh_cnt) (void)hipHostFree(h.wh_cnt);
         }
+        if (s->side) (void)hipStreamDestroy(s->side);
+        if (s->ev_fork) (void)hipEventDestroy(s->ev_fork);
+        if (s->ev_join) (void)hipEventDestroy(s->ev_join);
         (void)hipFree(s->d_smp);
         (void)hipFree(s->d_frame);
         if (s->h_smp_pinned) (void)hipHostFree(s->h_smp_pinned);
@@ -3041,6 +3219,18 @@ int rt_debug_heavy_first(rt_scene *s, uint32_t *front, uint32_t *listed, uint32_
     *front = c->front;
     *listed = c->ver ? std::min(pl.cnt_hi + pl.cnt_lo, c->front) : 0u;
     *epoch = c->frames;
+    return RT_OK;
+}
+
+int rt_debug_wide_items(rt_scene *s, uint32_t *count)
+{
+    if (!s || !count) return fail(RT_E_INVALID, "NULL argument");
+    std::lock_guard<std::mutex> lk(s->mtx);
+    const HfCtx *c = nullptr;
+    for (const HfCtx& h : s->hf)
+        if (h.wh_cnt && (!c || h.used > c->used)) c = &h;
+    if (c) RT_HIP(hipDeviceSynchronize());
+    *count = c ? *(volatile uint32_t *)c->wh_cnt : 0u;
     return RT_OK;
 }
 

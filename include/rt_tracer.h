@@ -108,6 +108,10 @@ enum rt_kernel {
                                          staged through LDS 64 records at a time */
     RT_KERNEL_FLAG_ONE_PHASE = 0x100, /* OR-able (AUTO): never the two-phase arm, also for shards of
                                          dense scenes (A/B arm of the rank-count policy) */
+    RT_KERNEL_FLAG_WIDE_HEAVY = 0x200, /* OR-able (AUTO, spp <= 4): work items that earlier frames of
+                                          the same launch shape measured as heavy are traced wide (16
+                                          lanes per sample) by a kernel on the scene's side stream,
+                                          beside the one-lane-per-sample kernel (fork / join) */
     RT_KERNEL_FLAG_EXHAUSTIVE = 0x8000, /* OR-able, ray march: evaluate every triangle per step
                                            (no block culling; A/B arm, identical results) */
     RT_KERNEL_FLAG_WAVE_CLOCK = 0x400000, /* OR-able (AUTO), debug: record s_memtime {start, end} of
@@ -255,6 +259,9 @@ int  rt_debug_wave_clocks(rt_scene *s, uint64_t *out, uint32_t max_items, uint32
    front section holds, *listed = blocks the last frame listed for the next one (heavy waves found),
    *epoch = frames rendered with this shape.  Synchronises the device. */
 int rt_debug_heavy_first(rt_scene *s, uint32_t *front, uint32_t *listed, uint32_t *epoch);
+/* RT_KERNEL_FLAG_WIDE_HEAVY: work items the newest plan of the most recent wide-section launch
+   shape lists for the wide section.  Synchronises the device. */
+int rt_debug_wide_items(rt_scene *s, uint32_t *count);
 
 /* Hammersley table the library uses when rt_frame.sample_offsets is NULL. */
 int  rt_sample_table(uint32_t spp, float *out_xy);

@@ -299,6 +299,91 @@ def test_shard_partition_dense_scenes(golden, scenes, sid, nranks):
     assert hashlib.sha256(img.tobytes()).hexdigest() == golden["frames_1080p4"][str(sid)]["bgra_sha256"]
 
 
+@pytest.mark.parametrize("sid,nranks", [(8, 8), (5, 4), (8, 2)])
+def test_wide_heavy_shard_frames(golden, scenes, sid, nranks):
+    """RT_KERNEL_FLAG_WIDE_HEAVY over consecutive frames of every rank: frames 0-1 render one
+    lane per sample and measure, later frames trace the listed heavy items on the side stream
+    (16 lanes per sample); every frame's shard equals the one-lane-per-sample shard, and the
+    partition reassembles into the reference frame."""
+    import torch
+    hs, gs = scenes(sid)
+    W, H = 1920, 1080
+    f = gs.frame(W, H, 4, kernel=rtm.RT_KERNEL_AUTO | rtm.RT_KERNEL_FLAG_WIDE_HEAVY)
+    f_ref = gs.frame(W, H, 4, kernel=rtm.RT_KERNEL_AUTO | rtm.RT_KERNEL_FLAG_ONE_PHASE)
+    e = rtm.shard_elems(W, H, nranks)
+    gathered = torch.zeros(nranks * e, dtype=torch.int32, device="cuda")
+    ref = torch.zeros(e, dtype=torch.int32, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    listed = 0
+    for r in range(nranks):
+        gs.render_shard_device(f_ref, r, nranks, ref.data_ptr(), stream)
+        part = gathered[r * e:(r + 1) * e]
+        for i in range(6):
+            part.zero_()
+            gs.render_shard_device(f, r, nranks, part.data_ptr(), stream)
+            torch.cuda.synchronize()
+            assert torch.equal(part, ref), (sid, nranks, r, i)
+        listed = max(listed, gs.wide_items())
+    assert listed > 0, (sid, nranks)
+    out = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+    rtm.unshard_device(W, H, nranks, gathered.data_ptr(), out.data_ptr(), stream)
+    torch.cuda.synchronize()
+    img = out.cpu().numpy().view(np.uint32)
+    assert hashlib.sha256(img.tobytes()).hexdigest() == golden["frames_1080p4"][str(sid)]["bgra_sha256"]
+
+
+@pytest.mark.parametrize("spp", [1, 2, 4])
+def test_wide_heavy_ragged_vs_oracle(scenes, oracle, spp, monkeypatch):
+    """The wide section on ragged frames (partial tiles, spp 1/2/4) with the floor lowered so
+    that most items go wide, over 70 frames: the sticky list, the refresh frame (frame 64 renders
+    every item one lane per sample) and the re-listing after it all render the reference's
+    bytes."""
+    monkeypatch.setenv("RT_WH_FLOOR", "2000")
+    monkeypatch.setenv("RT_WH_ALPHA16", "1")
+    hs, gs = scenes(8)
+    exp, _, _ = oracle.render(8, 97, 61, spp)
+    f = gs.frame(97, 61, spp, kernel=rtm.RT_KERNEL_AUTO | rtm.RT_KERNEL_FLAG_WIDE_HEAVY)
+    listed = 0
+    for i in range(70):
+        np.testing.assert_array_equal(gs.render_frame(f), exp, err_msg=str(i))
+        if i in (3, 40, 69):
+            listed = max(listed, gs.wide_items())
+    assert listed > 0
+
+
+def test_wide_heavy_graph_replay(golden, scenes):
+    """The wide section's fork / join onto the side stream inside a captured HIP graph (after
+    warm-up frames that listed heavy items): replays render the reference's frame."""
+    import torch
+    hs, gs = scenes(8)
+    want = golden["frames_1080p4"]["8"]["bgra_sha256"]
+    W, H, N = 1920, 1080, 4
+    f = gs.frame(W, H, 4, kernel=rtm.RT_KERNEL_AUTO | rtm.RT_KERNEL_FLAG_WIDE_HEAVY)
+    e = rtm.shard_elems(W, H, N)
+    gathered = torch.zeros(N * e, dtype=torch.int32, device="cuda")
+    out = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+    s = torch.cuda.Stream()
+    graphs = []
+    for r in range(N):
+        part = gathered[r * e:(r + 1) * e]
+        with torch.cuda.stream(s):
+            for _ in range(4):
+                gs.render_shard_device(f, r, N, part.data_ptr(), s.cuda_stream)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            gs.render_shard_device(f, r, N, part.data_ptr(), s.cuda_stream)
+        graphs.append(g)
+    assert gs.wide_items() > 0
+    for _ in range(2):
+        gathered.zero_()
+        for g in graphs:
+            g.replay()
+        rtm.unshard_device(W, H, N, gathered.data_ptr(), out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        assert hashlib.sha256(out.cpu().numpy().view(np.uint32).tobytes()).hexdigest() == want
+
+
 def test_wave_clock_debug_arm(scenes):
     """RT_KERNEL_FLAG_WAVE_CLOCK records {start, end} per work item and leaves the frame alone."""
     hs, gs = scenes(1)
