@@ -2248,9 +2248,13 @@ int ensure_origin_terms(rt_scene *s, const KParams& P, hipStream_t st)
 
 // kVarWideHeavy thresholds: an item goes wide above max(floor, alpha16 / 16 x estimated span)
 // shader cycles; RT_WH_FLOOR / RT_WH_ALPHA16 override them (A/B sweeps)
-constexpr uint32_t kWhFloor = 200000;
-constexpr uint32_t kWhRefresh = 64;         // frames between refresh frames (a multiple of kHfPeriod)
-constexpr uint32_t kWhAlpha16 = 32;
+// (tools/wh_probe.py sweeps, profiles/r02m_wide_heavy_sweep.json: the floor keeps Cornell's
+// items in the lanes -- at 60000 cycles its rank of 8 lists ~900 items and doubles -- and the
+// span factor is 1x below 8 ranks, 2x from 8)
+constexpr uint32_t kWhFloor = 100000;
+constexpr uint32_t kWhRefresh = 128;        // frames between refresh frames (a multiple of kHfPeriod)
+constexpr uint32_t kWhAlpha16 = 16;
+constexpr uint32_t kWhAlpha16Wide = 32;
 uint32_t wh_tunable(const char *name, uint32_t dflt)
 {
     const char *e = std::getenv(name);
@@ -2331,7 +2335,7 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
         P.wh_refresh = (c->frames - 1u) % kWhRefresh == 0u;       // frames counts this one
         P.wh_wgs = P.wh_refresh ? 0u : (cnt * G + kWavesPerWG - 1u) / kWavesPerWG;
         P.wh_floor = wh_tunable("RT_WH_FLOOR", kWhFloor);
-        P.wh_alpha16 = wh_tunable("RT_WH_ALPHA16", kWhAlpha16);
+        P.wh_alpha16 = wh_tunable("RT_WH_ALPHA16", P.nranks >= 8u ? kWhAlpha16Wide : kWhAlpha16);
         P.wh_mark_in = c->wh_marks + size_t(v & 1u) * kWavesPerWG * c->cap_blocks;
         P.wh_mark_out = c->wh_marks + size_t((v + 1u) & 1u) * kWavesPerWG * c->cap_blocks;
         P.wh_list_in = c->wh_lists + size_t(v & 1u) * kWhMax;
@@ -2451,9 +2455,15 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
     // the plain kernel -> 0.48 / 0.35 / 0.25 with budgets 384 / 192 / 128).  On a whole frame,
     // or a scene without dense cells, phase 1's budget count and the re-trace cost more than
     // they save.
-    // the wide section (kVarWideHeavy) needs the wide code's layout and spp <= 16
-    const bool wide_heavy = wide_ok && kind == RT_KERNEL_AUTO && (f->kernel & RT_KERNEL_FLAG_WIDE_HEAVY) && P.spp <= 4u &&
-                            !(f->kernel & RT_KERNEL_FLAG_BAIL_WIDE);
+    // AUTO takes the wide section (kVarWideHeavy: the wide code's layout, spp <= 4) for a shard of
+    // >= 2 ranks of a scene with dense cells: there a rank's launch is bound by its few ~1000-test
+    // waves, which the section splits 16 ways beside the lane kernel (measured, tools/wh_probe.py,
+    // killeroo rank of 2 / 4 / 8: 0.36 / 0.33 / 0.25 ms with the lane kernel alone -> 0.35 / 0.20
+    // / 0.15).  On a whole frame the lanes are busy with other items anyway and
+    // the section's repeated walks cost more than they save (+1-3 %).
+    const bool wide_heavy = wide_ok && kind == RT_KERNEL_AUTO && P.spp <= 4u && !(f->kernel & RT_KERNEL_FLAG_BAIL_WIDE) &&
+                            ((f->kernel & RT_KERNEL_FLAG_WIDE_HEAVY) ||
+                             (P.nranks >= 2u && s->max_cell_refs >= kBailAutoRefs && !(f->kernel & RT_KERNEL_FLAG_ONE_PHASE)));
     const bool bail_auto = kind == RT_KERNEL_AUTO && P.nranks >= kBailAutoRanks && s->max_cell_refs >= kBailAutoRefs &&
                            !(f->kernel & RT_KERNEL_FLAG_ONE_PHASE) && !wide_heavy;
     const bool bail = wide_ok && kind == RT_KERNEL_AUTO && (bail_auto || (f->kernel & RT_KERNEL_FLAG_BAIL_WIDE));
@@ -2528,7 +2538,7 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
         // heavy-first order: AUTO grid frames large enough that blocks start in several rounds
         const bool front = kind == RT_KERNEL_AUTO && P.isect == RT_ISECT_GRID && !(kvar & kVarWaveClock) &&
                            !(f->kernel & RT_KERNEL_FLAG_STATIC_ORDER) &&
-                           (blocks >= kHfMinBlocks || (wide_heavy && blocks >= 64u && wh_tunable("RT_WH_FRONT", 0u)));
+                           (blocks >= kHfMinBlocks || (wide_heavy && blocks >= 64u && wh_tunable("RT_WH_FRONT", 1u)));
         if (front || wide_heavy)
         {
             if (int rc = hf_prepare(s, P, blocks, kvar, front, st)) return rc;

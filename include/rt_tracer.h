@@ -87,8 +87,9 @@ enum rt_kernel {
     RT_KERNEL_AUTO = 0,        /* the fastest measured path for the frame: one lane per
                                   sample, distance-skipping 3D-DDA, per-camera-origin triangle records,
                                   wave-uniform cell lists on scalar loads, XCD-aware tile rows, and the
-                                  heavy-first block order; for >= 2-rank shards of dense scenes the
-                                  two-phase arm (RT_KERNEL_FLAG_BAIL_WIDE with 16 lanes per sample) */
+                                  heavy-first block order; for >= 2-rank shards of dense scenes at
+                                  spp <= 4 the wide section (RT_KERNEL_FLAG_WIDE_HEAVY), at spp 8-16
+                                  from 4 ranks the two-phase arm (RT_KERNEL_FLAG_BAIL_WIDE) */
     RT_KERNEL_LANES = 1,       /* the plain per-lane kernel: one lane per sample, the reference's walk
                                   and ray/triangle test cell by cell (A/B baseline) */
     RT_KERNEL_PIXEL_LOOP = 2,  /* one lane per pixel looping over its samples (any spp) */
@@ -108,7 +109,8 @@ enum rt_kernel {
                                          staged through LDS 64 records at a time */
     RT_KERNEL_FLAG_ONE_PHASE = 0x100, /* OR-able (AUTO): never the two-phase arm, also for shards of
                                          dense scenes (A/B arm of the rank-count policy) */
-    RT_KERNEL_FLAG_WIDE_HEAVY = 0x200, /* OR-able (AUTO, spp <= 4): work items that earlier frames of
+    RT_KERNEL_FLAG_WIDE_HEAVY = 0x200, /* OR-able (AUTO, spp <= 4; AUTO's own choice for >= 2-rank
+                                          shards of dense scenes): work items that earlier frames of
                                           the same launch shape measured as heavy are traced wide (16
                                           lanes per sample) by a kernel on the scene's side stream,
                                           beside the one-lane-per-sample kernel (fork / join) */

@@ -280,8 +280,9 @@ def test_lds_cells_vs_oracle(scenes, oracle, sid, spp):
 
 @pytest.mark.parametrize("sid,nranks", [(8, 8), (5, 8), (8, 3), (4, 16), (8, 2), (5, 4)])
 def test_shard_partition_dense_scenes(golden, scenes, sid, nranks):
-    """Shards of >= 2 ranks of a dense scene take AUTO's two-phase arm (16 lanes per sample,
-    budget 384 / 192 / 128 from 2 / 4 / 8 ranks); every partition reassembles into the
+    """Shards of >= 2 ranks of a dense scene take AUTO's wide section (RT_KERNEL_FLAG_WIDE_HEAVY:
+    the first frame of a shape renders one lane per sample, later ones trace the heavy items 16
+    lanes per sample); three frames per rank, and every partition reassembles into the
     reference frame."""
     import torch
     hs, gs = scenes(sid)
@@ -291,7 +292,8 @@ def test_shard_partition_dense_scenes(golden, scenes, sid, nranks):
     gathered = torch.zeros(nranks * e, dtype=torch.int32, device="cuda")
     stream = torch.cuda.current_stream().cuda_stream
     for r in range(nranks):
-        gs.render_shard_device(f, r, nranks, gathered.data_ptr() + 4 * r * e, stream)
+        for _ in range(3):
+            gs.render_shard_device(f, r, nranks, gathered.data_ptr() + 4 * r * e, stream)
     out = torch.zeros(W * H, dtype=torch.int32, device="cuda")
     rtm.unshard_device(W, H, nranks, gathered.data_ptr(), out.data_ptr(), stream)
     torch.cuda.synchronize()
@@ -299,16 +301,17 @@ def test_shard_partition_dense_scenes(golden, scenes, sid, nranks):
     assert hashlib.sha256(img.tobytes()).hexdigest() == golden["frames_1080p4"][str(sid)]["bgra_sha256"]
 
 
-@pytest.mark.parametrize("sid,nranks", [(8, 8), (5, 4), (8, 2)])
-def test_wide_heavy_shard_frames(golden, scenes, sid, nranks):
+@pytest.mark.parametrize("sid,nranks,kernel", [(8, 8, 0), (5, 4, 0), (8, 2, 0x200), (5, 1, 0x200)])
+def test_wide_heavy_shard_frames(golden, scenes, sid, nranks, kernel):
     """RT_KERNEL_FLAG_WIDE_HEAVY over consecutive frames of every rank: frames 0-1 render one
     lane per sample and measure, later frames trace the listed heavy items on the side stream
     (16 lanes per sample); every frame's shard equals the one-lane-per-sample shard, and the
-    partition reassembles into the reference frame."""
+    partition reassembles into the reference frame.  kernel 0: AUTO's own policy (>= 2 ranks of
+    a dense scene), 0x200: the flag forced (also on a whole frame)."""
     import torch
     hs, gs = scenes(sid)
     W, H = 1920, 1080
-    f = gs.frame(W, H, 4, kernel=rtm.RT_KERNEL_AUTO | rtm.RT_KERNEL_FLAG_WIDE_HEAVY)
+    f = gs.frame(W, H, 4, kernel=kernel)
     f_ref = gs.frame(W, H, 4, kernel=rtm.RT_KERNEL_AUTO | rtm.RT_KERNEL_FLAG_ONE_PHASE)
     e = rtm.shard_elems(W, H, nranks)
     gathered = torch.zeros(nranks * e, dtype=torch.int32, device="cuda")
@@ -445,7 +448,8 @@ def test_shard_unshard_partition_invariant(golden, scenes, nranks, kernel):
     gathered = torch.zeros(nranks * e, dtype=torch.int32, device="cuda")
     stream = torch.cuda.current_stream().cuda_stream
     for r in range(nranks):
-        gs.render_shard_device(f, r, nranks, gathered.data_ptr() + 4 * r * e, stream)
+        for _ in range(3):
+            gs.render_shard_device(f, r, nranks, gathered.data_ptr() + 4 * r * e, stream)
     out = torch.zeros(W * H, dtype=torch.int32, device="cuda")
     rtm.unshard_device(W, H, nranks, gathered.data_ptr(), out.data_ptr(), stream)
     torch.cuda.synchronize()
