@@ -88,7 +88,7 @@ constexpr uint32_t kDistBlock = 32;         // triangles per culling block of th
 // heavy-first plan (one per list version): blocks listed at each of the two priority levels,
 // the maximum block cost, the work items listed for the wide section (kVarWideHeavy) and the
 // sum of wave costs of the measured frame
-struct HfPlan { uint32_t cnt_hi, cnt_lo, maxc, cnt_w; unsigned long long sum; };
+struct HfPlan { uint32_t cnt_hi, cnt_lo, maxc, cnt_w; unsigned long long sum; uint32_t cnt_w4, pad; };
 
 struct KParams
 {
@@ -154,11 +154,13 @@ struct KParams
     // of the last frame that measured them) except in a refresh frame.
     uint32_t wh_on, wh_wgs, wh_refresh;
     uint32_t wh_floor, wh_alpha16;
+    uint32_t wh_alpha16_4;      // items between max(floor, wh_alpha16_4 / 16 x span) and the 16-lane
+                                // threshold go wide 4 lanes per sample (second list, wh_list + kWhMax)
     const uint32_t *wh_mark_in;
     uint32_t *wh_mark_out;
     const uint32_t *wh_list_in;
     uint32_t *wh_list_out;
-    uint32_t *wh_host_cnt;      // host-mapped: the newest plan's cnt_w (sizes the next launches)
+    uint32_t *wh_host_cnt;      // host-mapped: the newest plan's {cnt_w, cnt_w4} (sizes the next launches)
     uint32_t bail_tests;        // BAIL_WIDE phase 1: test budget per sample
     uint32_t *bail_count;       // BAIL_WIDE: queued pixels
     uint32_t *bail_queue;       // BAIL_WIDE: (local tile << 8 | Morton pixel) per queued pixel
@@ -1100,17 +1102,17 @@ __device__ __forceinline__ uint32_t xcd_band_block(uint32_t b, uint32_t nb, uint
 // cost milliseconds, measured).
 __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks)
 {
-    __shared__ uint32_t s_max, s_hi, s_lo, s_w, s_bhi, s_blo, s_bw;
+    __shared__ uint32_t s_max, s_hi, s_lo, s_w, s_w4, s_bhi, s_blo, s_bw, s_bw4;
     __shared__ unsigned long long s_sum;
     const uint32_t b = blockIdx.x * kWG + threadIdx.x;
     if (threadIdx.x == 0u)
     {
-        s_max = s_hi = s_lo = s_w = 0u;
+        s_max = s_hi = s_lo = s_w = s_w4 = 0u;
         s_sum = 0ull;
     }
     __syncthreads();
     const HfPlan last = *P.hf_plan_in;
-    uint32_t cost = 0u, sum = 0u, wmask = 0u;
+    uint32_t cost = 0u, sum = 0u, wmask = 0u, w4mask = 0u;     // w4mask: the 4-lane tier
     uint4 c = make_uint4(0u, 0u, 0u, 0u);
     if (b < nblocks)
     {
@@ -1122,28 +1124,40 @@ __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks)
             // measurement (sum of wave costs over the resident waves)
             const uint64_t span = (last.sum << 4) / kHfSlots;
             const uint32_t thr = max(P.wh_floor, uint32_t(min<uint64_t>(span * P.wh_alpha16 / 16u, 0xFFFFFFFFull)));
+            const uint32_t thr4 = max(P.wh_floor, uint32_t(min<uint64_t>(span * P.wh_alpha16_4 / 16u, 0xFFFFFFFFull)));
             wmask = uint32_t(c.x > thr) | (uint32_t(c.y > thr) << 1) | (uint32_t(c.z > thr) << 2) |
                     (uint32_t(c.w > thr) << 3);
+            if (thr4 < thr)
+                w4mask = (uint32_t(c.x > thr4) | (uint32_t(c.y > thr4) << 1) | (uint32_t(c.z > thr4) << 2) |
+                          (uint32_t(c.w > thr4) << 3)) & ~wmask;
         }
         if (P.wh_on && !P.wh_refresh && P.hf_ver)
         {
+            // sticky: the current plan's items keep their tier (mark = version << 1 | 4-lane tier)
             const uint4 m = reinterpret_cast<const uint4 *>(P.wh_mark_in)[b];
-            wmask |= uint32_t(m.x == P.hf_ver) | (uint32_t(m.y == P.hf_ver) << 1) | (uint32_t(m.z == P.hf_ver) << 2) |
-                     (uint32_t(m.w == P.hf_ver) << 3);
+            const uint32_t mv[4] = { m.x, m.y, m.z, m.w };
+            for (uint32_t j = 0; j < kWavesPerWG; j++)
+                if ((mv[j] >> 1) == P.hf_ver && !((wmask | w4mask) & (1u << j)))
+                {
+                    if (mv[j] & 1u) w4mask |= 1u << j;
+                    else wmask |= 1u << j;
+                }
         }
+        const uint32_t any = wmask | w4mask;
         // the heavy-first order ranks a block by its slowest wave left in the lane section
-        cost = max(max((wmask & 1u) ? 0u : c.x, (wmask & 2u) ? 0u : c.y),
-                   max((wmask & 4u) ? 0u : c.z, (wmask & 8u) ? 0u : c.w));
+        cost = max(max((any & 1u) ? 0u : c.x, (any & 2u) ? 0u : c.y),
+                   max((any & 4u) ? 0u : c.z, (any & 8u) ? 0u : c.w));
     }
     const bool tail = uint64_t(last.maxc) * kHfSlots * 16u > uint64_t(kHfTail) * (last.sum << 4);
     const uint32_t thr = max(P.hf_floor, last.maxc >> kHfShift);
     const bool heavy = P.hf_front && tail && cost > thr;
     const bool hi = heavy && cost > (last.maxc >> 1);
-    uint32_t rank = 0u, wrank = 0u;
+    uint32_t rank = 0u, wrank = 0u, w4rank = 0u;
     if (cost) atomicMax(&s_max, cost);
     if (sum) atomicAdd(&s_sum, (unsigned long long)sum);
     if (heavy) rank = atomicAdd(hi ? &s_hi : &s_lo, 1u);
     if (wmask) wrank = atomicAdd(&s_w, uint32_t(__popc(wmask)));
+    if (w4mask) w4rank = atomicAdd(&s_w4, uint32_t(__popc(w4mask)));
     __syncthreads();
     if (threadIdx.x == 0u)
     {
@@ -1152,6 +1166,7 @@ __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks)
         s_bhi = s_hi ? atomicAdd(&P.hf_plan_out->cnt_hi, s_hi) : 0u;
         s_blo = s_lo ? atomicAdd(&P.hf_plan_out->cnt_lo, s_lo) : 0u;
         s_bw = s_w ? atomicAdd(&P.hf_plan_out->cnt_w, s_w) : 0u;
+        s_bw4 = s_w4 ? atomicAdd(&P.hf_plan_out->cnt_w4, s_w4) : 0u;
     }
     __syncthreads();
     if (heavy)
@@ -1168,16 +1183,27 @@ __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks)
     // wide items: listed and marked for the next plan's frames (beyond kWhMax they stay in the
     // lane section)
     for (uint32_t j = 0; j < kWavesPerWG; j++)
+    {
+        const uint32_t item = b * kWavesPerWG + j;
         if (wmask & (1u << j))
         {
             const uint32_t r = s_bw + wrank++;
             if (r < kWhMax)
             {
-                const uint32_t item = b * kWavesPerWG + j;
                 P.wh_list_out[r] = item;
-                P.wh_mark_out[item] = P.hf_ver + 1u;
+                P.wh_mark_out[item] = (P.hf_ver + 1u) << 1;
             }
         }
+        else if (w4mask & (1u << j))
+        {
+            const uint32_t r = s_bw4 + w4rank++;
+            if (r < kWhMax)
+            {
+                P.wh_list_out[kWhMax + r] = item;
+                P.wh_mark_out[item] = ((P.hf_ver + 1u) << 1) | 1u;
+            }
+        }
+    }
     // the block marks are written by a second pass over the final list (k_hf_mark), so a slot
     // claimed by both levels marks only the block whose entry survived
 }
@@ -1192,7 +1218,12 @@ __global__ void __launch_bounds__(kWG) k_hf_mark(KParams P)
     const uint32_t hi = min(pl.cnt_hi, P.hf_front);
     const uint32_t lo = min(pl.cnt_lo, P.hf_front - hi);
     if (j < P.hf_front && (j < hi || j >= P.hf_front - lo)) P.hf_mark_out[P.hf_list_out[j]] = P.hf_ver + 1u;
-    if (j == 0u && P.wh_host_cnt) *(volatile uint32_t *)P.wh_host_cnt = min(pl.cnt_w, kWhMax);
+    if (j == 0u && P.wh_host_cnt)
+    {
+        volatile uint32_t *h = P.wh_host_cnt;
+        h[0] = min(pl.cnt_w, kWhMax);
+        h[1] = min(pl.cnt_w4, kWhMax);
+    }
 }
 
 // The launch's block -> block-of-work map.  With the heavy-first order on, blocks [0, hf_front)
@@ -1205,11 +1236,11 @@ __device__ __forceinline__ bool block_of_launch(const KParams& P, uint32_t& b)
 {
     const uint32_t bid = blockIdx.x, nblk = gridDim.x;
     if ((VAR & kVarWideHeavy) && P.hf_measure && bid == 0u && threadIdx.x == 0u)
-        *P.hf_plan_out = HfPlan{0u, 0u, 0u, 0u, 0ull};        // k_hf_plan runs after this kernel
+        *P.hf_plan_out = HfPlan{};                            // k_hf_plan runs after this kernel
     if (P.hf_front)
     {
         if (P.hf_measure && bid == 0u && threadIdx.x == 0u)
-            *P.hf_plan_out = HfPlan{0u, 0u, 0u, 0u, 0ull};    // k_hf_plan runs after this kernel
+            *P.hf_plan_out = HfPlan{};                        // k_hf_plan runs after this kernel
         const uint32_t front = P.hf_front;
         if (bid < front)
         {
@@ -1437,22 +1468,27 @@ __device__ __forceinline__ void wide_samples(const KParams& P, uint32_t k, uint3
 // persistent over the list, so a section smaller than the list (the host sizes it from an older
 // plan's count) still renders every listed item.  They record no cost: an item's cost word keeps
 // its lane-mode measurement until a refresh frame renders it one lane per sample again.
-template <int G>
 __device__ __forceinline__ void wide_section(const KParams& P)
 {
-    const uint32_t n = P.hf_ver ? min(P.hf_plan_in->cnt_w, kWhMax) : 0u;
+    // units: 16 per item of the 16-lane list, then 4 per item of the 4-lane list
+    const uint32_t n16 = P.hf_ver ? min(P.hf_plan_in->cnt_w, kWhMax) : 0u;
+    const uint32_t n4 = P.hf_ver ? min(P.hf_plan_in->cnt_w4, kWhMax) : 0u;
     const uint32_t w = blockIdx.x * kWavesPerWG + (threadIdx.x >> 6), nw = P.wh_wgs * kWavesPerWG;
     const uint32_t ipt = P.wg_per_tile * kWavesPerWG;              // items per tile
-    for (uint32_t e = w; e < n * uint32_t(G); e += nw)
+    for (uint32_t e = w; e < n16 * 16u + n4 * 4u; e += nw)
     {
-        const uint32_t item = __builtin_amdgcn_readfirstlane(P.wh_list_in[e / uint32_t(G)]);
-        const uint32_t part = e % uint32_t(G);
+        const bool g16 = e < n16 * 16u;
+        const uint32_t u = g16 ? e : e - n16 * 16u;
+        const uint32_t item =
+            __builtin_amdgcn_readfirstlane(g16 ? P.wh_list_in[u / 16u] : P.wh_list_in[kWhMax + u / 4u]);
         const uint32_t kseq = item / ipt;
-        const uint32_t slot0 = (item - kseq * ipt) * 64u + part * (64u / uint32_t(G));
+        const uint32_t slot0 = (item - kseq * ipt) * 64u + (g16 ? (u % 16u) * 4u : (u % 4u) * 16u);
         // the parameters re-read per item (late_params): hoisted out of the loop they held ~30
         // more SGPRs across it and spilled
         const KParams& Q = late_params(P);
-        wide_samples<kVarWide, G, RT_WH_PF>(Q, Q.tile_order ? Q.tile_order[kseq] : kseq, slot0);
+        const uint32_t k = Q.tile_order ? Q.tile_order[kseq] : kseq;
+        if (g16) wide_samples<kVarWide, 16, RT_WH_PF>(Q, k, slot0);
+        else wide_samples<kVarWide, 4, RT_WH_PF>(Q, k, slot0);
     }
 }
 
@@ -1467,7 +1503,7 @@ __global__ void __launch_bounds__(kWG) k_render_lanes(KParams P)
     if (!block_of_launch<VAR>(P, b)) return;
     const uint32_t item = b * kWavesPerWG + (threadIdx.x >> 6);
     if constexpr ((VAR & kVarWideHeavy) != 0)
-        if (P.wh_wgs && P.hf_ver && P.wh_mark_in[item] == P.hf_ver) return;   // traced by the wide section
+        if (P.wh_wgs && P.hf_ver && (P.wh_mark_in[item] >> 1) == P.hf_ver) return;   // traced by the wide section
     if constexpr ((VAR & kVarWaveClock) != 0)
     {
         // debug arm (RT_KERNEL_FLAG_WAVE_CLOCK): s_memtime at the item's start and end, and how
@@ -1512,7 +1548,7 @@ __global__ void __launch_bounds__(kWG) k_render_lanes(KParams P)
 // (its own register allocation: folded into the lane kernel it cost 106 SGPRs and spills)
 __global__ void __launch_bounds__(kWG) k_render_wh(KParams P)
 {
-    wide_section<16>(P);
+    wide_section(P);
 }
 
 // RT_KERNEL_WIDE: every tile in wide mode (the A/B arm of the two-phase frame)
@@ -2290,14 +2326,15 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
             {
                 RT_HIP(hipMalloc(&c->lists, sizeof(uint32_t) * 2 * kHfFrontMax));
                 RT_HIP(hipMalloc(&c->plans, sizeof(HfPlan) * 2));
-                RT_HIP(hipMalloc(&c->wh_lists, sizeof(uint32_t) * 2 * kWhMax));
-                RT_HIP(hipHostMalloc(&c->wh_cnt, sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent));
+                RT_HIP(hipMalloc(&c->wh_lists, sizeof(uint32_t) * 4 * kWhMax));
+                RT_HIP(hipHostMalloc(&c->wh_cnt, 2 * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent));
             }
         }
         RT_HIP(hipMemsetAsync(c->marks, 0, sizeof(uint32_t) * 2 * c->cap_blocks, st));
         RT_HIP(hipMemsetAsync(c->wh_marks, 0, sizeof(uint32_t) * 2 * kWavesPerWG * c->cap_blocks, st));
         RT_HIP(hipMemsetAsync(c->plans, 0, sizeof(HfPlan) * 2, st));
-        *(volatile uint32_t *)c->wh_cnt = 0u;
+        ((volatile uint32_t *)c->wh_cnt)[0] = 0u;
+        ((volatile uint32_t *)c->wh_cnt)[1] = 0u;
         std::memcpy(c->key, key, sizeof(key));
         c->nblocks = uint32_t(blocks);
         // front: an eighth of the blocks, capped, a multiple of the XCD count so the natural
@@ -2329,17 +2366,17 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
         // the device-side list may already be longer (the section is persistent over it)
         // refresh: every kWhRefresh-th frame renders every item one lane per sample, so the
         // next plan re-ranks all items on lane-mode costs (the wide set is otherwise sticky)
-        const uint32_t G = 16u;
-        const uint32_t cnt = *(volatile uint32_t *)c->wh_cnt;
+        const uint32_t units = 16u * ((volatile uint32_t *)c->wh_cnt)[0] + 4u * ((volatile uint32_t *)c->wh_cnt)[1];
         P.wh_on = 1u;
         P.wh_refresh = (c->frames - 1u) % kWhRefresh == 0u;       // frames counts this one
-        P.wh_wgs = P.wh_refresh ? 0u : (cnt * G + kWavesPerWG - 1u) / kWavesPerWG;
+        P.wh_wgs = P.wh_refresh ? 0u : (units + kWavesPerWG - 1u) / kWavesPerWG;
         P.wh_floor = wh_tunable("RT_WH_FLOOR", kWhFloor);
         P.wh_alpha16 = wh_tunable("RT_WH_ALPHA16", P.nranks >= 8u ? kWhAlpha16Wide : kWhAlpha16);
+        P.wh_alpha16_4 = wh_tunable("RT_WH_ALPHA16_4", P.wh_alpha16);          // = alpha: no 4-lane tier
         P.wh_mark_in = c->wh_marks + size_t(v & 1u) * kWavesPerWG * c->cap_blocks;
         P.wh_mark_out = c->wh_marks + size_t((v + 1u) & 1u) * kWavesPerWG * c->cap_blocks;
-        P.wh_list_in = c->wh_lists + size_t(v & 1u) * kWhMax;
-        P.wh_list_out = c->wh_lists + size_t((v + 1u) & 1u) * kWhMax;
+        P.wh_list_in = c->wh_lists + size_t(v & 1u) * 2u * kWhMax;
+        P.wh_list_out = c->wh_lists + size_t((v + 1u) & 1u) * 2u * kWhMax;
         void *dev = nullptr;
         RT_HIP(hipHostGetDevicePointer(&dev, c->wh_cnt, 0));
         P.wh_host_cnt = static_cast<uint32_t *>(dev);
@@ -3240,7 +3277,7 @@ int rt_debug_wide_items(rt_scene *s, uint32_t *count)
     for (const HfCtx& h : s->hf)
         if (h.wh_cnt && (!c || h.used > c->used)) c = &h;
     if (c) RT_HIP(hipDeviceSynchronize());
-    *count = c ? *(volatile uint32_t *)c->wh_cnt : 0u;
+    *count = c ? ((volatile uint32_t *)c->wh_cnt)[0] + ((volatile uint32_t *)c->wh_cnt)[1] : 0u;
     return RT_OK;
 }
 

@@ -24,7 +24,8 @@ spec.loader.exec_module(rtm)
 ap = argparse.ArgumentParser()
 ap.add_argument("--alphas", default="4,8,16")
 ap.add_argument("--floors", default="200000")
-ap.add_argument("--fronts", default="0")
+ap.add_argument("--fronts", default="1")
+ap.add_argument("--alphas4", default="", help="RT_WH_ALPHA16_4 values (4-lane tier); empty = no tier")
 ap.add_argument("--no-parity", action="store_true")
 ap.add_argument("--scenes", default="1,8,5")
 ap.add_argument("--ns", default="1,2,4,8")
@@ -70,14 +71,16 @@ for sid in [int(x) for x in a.scenes.split(",")]:
         print("parity", sid, n, ok, flush=True)
     for n in [int(x) for x in a.ns.split(",")]:
         buf = torch.empty(rtm.shard_elems(W, H, n), dtype=torch.int32, device="cuda")
-        arms = [("auto", 0, None, None, None)] + [(f"wh_a{al}_f{fl}_fr{fr}", WH, al, fl, fr)
-                                                   for al in a.alphas.split(",") for fl in a.floors.split(",")
-                                                   for fr in a.fronts.split(",")]
-        for name, k, al, fl, fr in arms:
+        arms = [("auto", 0x100, None, None, None, None)] + [
+            (f"wh_a{al}_l{a4 or al}_f{fl}_fr{fr}", WH, al, fl, fr, a4 or al)
+            for al in a.alphas.split(",") for fl in a.floors.split(",") for fr in a.fronts.split(",")
+            for a4 in (a.alphas4.split(",") if a.alphas4 else [""])]
+        for name, k, al, fl, fr, a4 in arms:
             if al is not None:
                 os.environ["RT_WH_ALPHA16"] = al
                 os.environ["RT_WH_FLOOR"] = fl
                 os.environ["RT_WH_FRONT"] = fr
+                os.environ["RT_WH_ALPHA16_4"] = a4
             # a fresh scene per arm: the wide list is sticky per launch shape, and the front
             # section is sized when a shape's state is created
             g.close()
