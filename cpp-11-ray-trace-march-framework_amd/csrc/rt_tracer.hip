@@ -144,6 +144,7 @@ struct KParams
     const HfPlan *hf_plan_in;   // the current plan (also the previous measurement's max and sum)
     HfPlan *hf_plan_out;        // the next plan, cleared by the measured frame's first lane
     uint32_t *hf_cost;          // per work item: shader cycles of its wave in the measured frame
+    uint32_t *hf_ticket;        // k_hf_plan's finished-workgroup count (the last one marks)
                                 // (a wide item: the sum over its waves)
     // wide section (kVarWideHeavy; wh_on == 0: off).  k_render_wh's wh_wgs workgroups trace the
     // work items the current plan lists as heavy (wh_list_in, plan->cnt_w of them), G lanes per
@@ -1102,7 +1103,7 @@ __device__ __forceinline__ uint32_t xcd_band_block(uint32_t b, uint32_t nb, uint
 // cost milliseconds, measured).
 __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks)
 {
-    __shared__ uint32_t s_max, s_hi, s_lo, s_w, s_w4, s_bhi, s_blo, s_bw, s_bw4;
+    __shared__ uint32_t s_max, s_hi, s_lo, s_w, s_w4, s_bhi, s_blo, s_bw, s_bw4, s_last;
     __shared__ unsigned long long s_sum;
     const uint32_t b = blockIdx.x * kWG + threadIdx.x;
     if (threadIdx.x == 0u)
@@ -1204,25 +1205,34 @@ __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks)
             }
         }
     }
-    // the block marks are written by a second pass over the final list (k_hf_mark), so a slot
-    // claimed by both levels marks only the block whose entry survived
-}
-
-// Marks the blocks of the new plan's list (after k_hf_plan): the front section of the frames
-// using it renders exactly the slots [0, cnt_hi) and [front - cnt_lo, front) that do not overlap.
-// Also hands the wide section's item count to the host (it sizes the section of later launches).
-__global__ void __launch_bounds__(kWG) k_hf_mark(KParams P)
-{
-    const uint32_t j = blockIdx.x * kWG + threadIdx.x;
-    const HfPlan pl = *P.hf_plan_out;
-    const uint32_t hi = min(pl.cnt_hi, P.hf_front);
-    const uint32_t lo = min(pl.cnt_lo, P.hf_front - hi);
-    if (j < P.hf_front && (j < hi || j >= P.hf_front - lo)) P.hf_mark_out[P.hf_list_out[j]] = P.hf_ver + 1u;
-    if (j == 0u && P.wh_host_cnt)
+    // The block marks are written by a second pass over the final list, so a slot claimed by
+    // both levels marks only the block whose entry survived.  That pass runs in the workgroup
+    // that finishes last (a ticket after a release fence), not in a second launch: a kernel
+    // launch costs ~4 us, as much as the whole plan at a rank of 8.
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0u) s_last = atomicAdd(P.hf_ticket, 1u) == gridDim.x - 1u;
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();
+    const volatile HfPlan *vp = P.hf_plan_out;
+    const uint32_t ch = vp->cnt_hi, cl = vp->cnt_lo;
+    const uint32_t nhi = min(ch, P.hf_front);
+    const uint32_t nlo = min(cl, P.hf_front - nhi);
+    const volatile uint32_t *vl = P.hf_list_out;
+    for (uint32_t j = threadIdx.x; j < P.hf_front; j += kWG)
+        if (j < nhi || j >= P.hf_front - nlo) P.hf_mark_out[vl[j]] = P.hf_ver + 1u;
+    if (threadIdx.x == 0u)
     {
-        volatile uint32_t *h = P.wh_host_cnt;
-        h[0] = min(pl.cnt_w, kWhMax);
-        h[1] = min(pl.cnt_w4, kWhMax);
+        // hands the wide section's item counts to the host (they size the section of later
+        // launches) and re-arms the ticket
+        if (P.wh_host_cnt)
+        {
+            volatile uint32_t *h = P.wh_host_cnt;
+            h[0] = min(vp->cnt_w, kWhMax);
+            h[1] = min(vp->cnt_w4, kWhMax);
+        }
+        *P.hf_ticket = 0u;
     }
 }
 
@@ -1514,9 +1524,11 @@ __global__ void __launch_bounds__(kWG) k_render_lanes(KParams P)
             wave_counters()[1] = 0u;
         }
         wave_lds_sync();
+        const uint64_t r0 = __builtin_amdgcn_s_memrealtime();
         const uint64_t t0 = __builtin_amdgcn_s_memtime();
         process_item<TRI, VAR>(P, item);
         const uint64_t t1 = __builtin_amdgcn_s_memtime();
+        const uint64_t r1 = __builtin_amdgcn_s_memrealtime();
         if ((threadIdx.x & 63u) == 0u)
         {
             P.wave_clk[4 * size_t(item)] = t0;
@@ -1525,8 +1537,14 @@ __global__ void __launch_bounds__(kWG) k_render_lanes(KParams P)
         wave_lds_sync();
         if ((threadIdx.x & 63u) == 0u)
         {
-            P.wave_clk[4 * size_t(item) + 2] = wave_counters()[0];
-            P.wave_clk[4 * size_t(item) + 3] = wave_counters()[1];
+            // high bits: the XCD the wave ran on (bits 32-35 of word 2) and the low 28 bits of
+            // the device-wide 100 MHz s_memrealtime at its start (word 2, bits 36-63) and end
+            // (word 3, bits 32-59): s_memtime counts per clock domain, so launch timelines use
+            // the real-time clock
+            P.wave_clk[4 * size_t(item) + 2] = wave_counters()[0] |
+                                               (uint64_t(__builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u) << 32) |
+                                               ((r0 & 0xFFFFFFFull) << 36);
+            P.wave_clk[4 * size_t(item) + 3] = wave_counters()[1] | ((r1 & 0xFFFFFFFull) << 32);
         }
     }
     else
@@ -2073,6 +2091,7 @@ struct HfCtx
     uint32_t *cost = nullptr;           // [cap_blocks * kWavesPerWG] wave cycles of the last frame
     uint32_t *lists = nullptr;          // [2][kHfFrontMax], by plan version parity
     HfPlan *plans = nullptr;            // [2], by plan version parity
+    uint32_t *ticket = nullptr;         // k_hf_plan's workgroup ticket
     uint32_t *wh_marks = nullptr;       // [2][cap_blocks * kWavesPerWG] wide items, by version parity
     uint32_t *wh_lists = nullptr;       // [2][kWhMax]
     uint32_t *wh_cnt = nullptr;         // host-mapped: the newest plan's wide item count
@@ -2291,7 +2310,7 @@ constexpr uint32_t kWhFloor = 100000;
 constexpr uint32_t kWhRefresh = 128;        // frames between refresh frames (a multiple of kHfPeriod)
 constexpr uint32_t kWhAlpha16 = 16;
 constexpr uint32_t kWhAlpha16Wide = 32;
-uint32_t wh_tunable(const char *name, uint32_t dflt)
+uint32_t env_tunable(const char *name, uint32_t dflt)
 {
     const char *e = std::getenv(name);
     return e && *e ? uint32_t(std::strtoul(e, nullptr, 0)) : dflt;
@@ -2326,6 +2345,7 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
             {
                 RT_HIP(hipMalloc(&c->lists, sizeof(uint32_t) * 2 * kHfFrontMax));
                 RT_HIP(hipMalloc(&c->plans, sizeof(HfPlan) * 2));
+                RT_HIP(hipMalloc(&c->ticket, sizeof(uint32_t)));
                 RT_HIP(hipMalloc(&c->wh_lists, sizeof(uint32_t) * 4 * kWhMax));
                 RT_HIP(hipHostMalloc(&c->wh_cnt, 2 * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent));
             }
@@ -2333,6 +2353,7 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
         RT_HIP(hipMemsetAsync(c->marks, 0, sizeof(uint32_t) * 2 * c->cap_blocks, st));
         RT_HIP(hipMemsetAsync(c->wh_marks, 0, sizeof(uint32_t) * 2 * kWavesPerWG * c->cap_blocks, st));
         RT_HIP(hipMemsetAsync(c->plans, 0, sizeof(HfPlan) * 2, st));
+        RT_HIP(hipMemsetAsync(c->ticket, 0, sizeof(uint32_t), st));
         ((volatile uint32_t *)c->wh_cnt)[0] = 0u;
         ((volatile uint32_t *)c->wh_cnt)[1] = 0u;
         std::memcpy(c->key, key, sizeof(key));
@@ -2351,7 +2372,8 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
     // against, so it lists nothing) and then every kHfPeriod-th
     P.hf_measure = c->frames < 2u || c->frames % kHfPeriod == 0u;
     c->frames++;
-    P.hf_floor = kHfFloor;
+    P.hf_floor = env_tunable("RT_HF_FLOOR", kHfFloor);
+    P.hf_ticket = c->ticket;
     P.hf_mark_in = c->marks + size_t(v & 1u) * c->cap_blocks;
     P.hf_mark_out = c->marks + size_t((v + 1u) & 1u) * c->cap_blocks;
     P.hf_list_in = c->lists + size_t(v & 1u) * kHfFrontMax;
@@ -2370,9 +2392,9 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
         P.wh_on = 1u;
         P.wh_refresh = (c->frames - 1u) % kWhRefresh == 0u;       // frames counts this one
         P.wh_wgs = P.wh_refresh ? 0u : (units + kWavesPerWG - 1u) / kWavesPerWG;
-        P.wh_floor = wh_tunable("RT_WH_FLOOR", kWhFloor);
-        P.wh_alpha16 = wh_tunable("RT_WH_ALPHA16", P.nranks >= 8u ? kWhAlpha16Wide : kWhAlpha16);
-        P.wh_alpha16_4 = wh_tunable("RT_WH_ALPHA16_4", P.wh_alpha16);          // = alpha: no 4-lane tier
+        P.wh_floor = env_tunable("RT_WH_FLOOR", kWhFloor);
+        P.wh_alpha16 = env_tunable("RT_WH_ALPHA16", P.nranks >= 8u ? kWhAlpha16Wide : kWhAlpha16);
+        P.wh_alpha16_4 = env_tunable("RT_WH_ALPHA16_4", P.wh_alpha16);          // = alpha: no 4-lane tier
         P.wh_mark_in = c->wh_marks + size_t(v & 1u) * kWavesPerWG * c->cap_blocks;
         P.wh_mark_out = c->wh_marks + size_t((v + 1u) & 1u) * kWavesPerWG * c->cap_blocks;
         P.wh_list_in = c->wh_lists + size_t(v & 1u) * 2u * kWhMax;
@@ -2575,7 +2597,8 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
         // heavy-first order: AUTO grid frames large enough that blocks start in several rounds
         const bool front = kind == RT_KERNEL_AUTO && P.isect == RT_ISECT_GRID && !(kvar & kVarWaveClock) &&
                            !(f->kernel & RT_KERNEL_FLAG_STATIC_ORDER) &&
-                           (blocks >= kHfMinBlocks || (wide_heavy && blocks >= 64u && wh_tunable("RT_WH_FRONT", 1u)));
+                           (blocks >= env_tunable("RT_HF_MIN_BLOCKS", kHfMinBlocks) ||
+                            (wide_heavy && blocks >= 64u && env_tunable("RT_WH_FRONT", 1u)));
         if (front || wide_heavy)
         {
             if (int rc = hf_prepare(s, P, blocks, kvar, front, st)) return rc;
@@ -2607,7 +2630,6 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
         if ((P.hf_front || P.wh_on) && P.hf_measure)
         {
             hipLaunchKernelGGL(k_hf_plan, dim3(uint32_t((blocks + kWG - 1) / kWG)), wg, 0, st, P, uint32_t(blocks));
-            hipLaunchKernelGGL(k_hf_mark, dim3(std::max(1u, (P.hf_front + kWG - 1) / kWG)), wg, 0, st, P);
         }
     }
     else
@@ -2953,6 +2975,7 @@ int rt_scene_destroy(rt_scene *s)
             (void)hipFree(h.cost);
             (void)hipFree(h.lists);
             (void)hipFree(h.plans);
+            (void)hipFree(h.ticket);
             (void)hipFree(h.wh_marks);
             (void)hipFree(h.wh_lists);
             if (h.wh_cnt) (void)hipHostFree(h.wh_cnt);

@@ -252,8 +252,10 @@ int  rt_debug_primitives(int kind, const float *in, uint32_t n, float *out, int 
    receives the mismatch count per biased exponent. */
 int  rt_debug_rcp_check(uint64_t *bad_by_exponent, int device);
 /* Per 64-sample work item of the last RT_KERNEL_FLAG_WAVE_CLOCK launch on this scene, in launch
-   item order, four words: {start, end} shader clock, records tested in wave-uniform list loops,
-   iterations of the per-lane list loop.  out holds 4 x max_items words; *n_items = how many
+   item order, four words: {start, end} shader clock (s_memtime: per clock domain, for
+   durations), records tested in wave-uniform list loops (bits 0-31; bits 32-35: the wave's XCD;
+   bits 36-63: low 28 bits of the 100 MHz s_memrealtime at its start), iterations of the
+   per-lane list loop (bits 0-31; bits 32-59: s_memrealtime at its end).  out holds 4 x max_items words; *n_items = how many
    items the launch wrote. */
 int  rt_debug_wave_clocks(rt_scene *s, uint64_t *out, uint32_t max_items, uint32_t *n_items);
 

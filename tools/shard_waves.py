@@ -32,24 +32,30 @@ for i in range(frames):
 ms = g.last_kernel_ms()
 clk = g.wave_clocks().astype(np.int64)
 g.close()
-s, e = clk[:, 0], clk[:, 1]
-ok = (s > 0) & (e > s) & (e - s < (1 << 32))
-s, e = s[ok], e[ok]
-t0 = s.min()
-s, e = s - t0, e - t0
-span = int(e.max())
-d = e - s
-order = np.argsort(e)
-q = lambda a, p: int(np.percentile(a, p))
-# resident waves at 20 points of the span
+c = clk.astype(np.uint64)
+xcd = ((c[:, 2] >> np.uint64(32)) & np.uint64(15)).astype(np.int64)
+rs = ((c[:, 2] >> np.uint64(36)) & np.uint64(0xFFFFFFF)).astype(np.int64)      # 100 MHz ticks
+re_ = ((c[:, 3] >> np.uint64(32)) & np.uint64(0xFFFFFFF)).astype(np.int64)
+re_ = np.where(re_ < rs, re_ + (1 << 28), re_)
+ok = (clk[:, 0] > 0) & (clk[:, 1] > clk[:, 0]) & (clk[:, 1] - clk[:, 0] < (1 << 32))
+d_all = (clk[:, 1] - clk[:, 0])[ok]
+s_, e_ = rs[ok], re_[ok]
+t0 = s_.min()
+s_, e_ = (s_ - t0) * 10, (e_ - t0) * 10                       # ns
+span = int(e_.max())
 pts = np.linspace(0, span, 21)[:-1]
-res = [int(((s <= p) & (e > p)).sum()) for p in pts]
-last = order[-20:]
+order = np.argsort(e_)
 out = {"scene": sid, "rank": r, "nranks": n, "items": int(ok.sum()), "kernel_ms": round(ms, 4),
-       "span_cycles": span, "cycles_per_ms": round(span / ms) if ms else None,
-       "wave_cycles": {"p50": q(d, 50), "p90": q(d, 90), "p99": q(d, 99), "max": int(d.max()), "sum": int(d.sum())},
-       "sum_over_8192_slots": int(d.sum() / 8192),
-       "resident_waves_over_span": res,
-       "last20_finish": [{"start": int(s[i]), "dur": int(d[i])} for i in last],
-       "start_p99": q(s, 99), "start_max": int(s.max())}
+       "span_ns_realtime": span,
+       "wave_cycles": {"p50": int(np.percentile(d_all, 50)), "p90": int(np.percentile(d_all, 90)),
+                       "p99": int(np.percentile(d_all, 99)), "max": int(d_all.max()), "sum": int(d_all.sum())},
+       "wave_ns": {"p50": int(np.percentile(e_ - s_, 50)), "p99": int(np.percentile(e_ - s_, 99)),
+                   "max": int((e_ - s_).max())},
+       "cycles_per_ns": round(float(np.median(d_all / np.maximum(e_ - s_, 1))), 3),
+       "sum_over_8192_slots_ns": int((e_ - s_).sum() / 8192),
+       "start_ns": {"p10": int(np.percentile(s_, 10)), "p50": int(np.percentile(s_, 50)),
+                    "p90": int(np.percentile(s_, 90)), "max": int(s_.max())},
+       "resident_waves_20pts": [int(((s_ <= p) & (e_ > p)).sum()) for p in pts],
+       "last5": [{"start_ns": int(s_[i]), "dur_ns": int(e_[i] - s_[i])} for i in order[-5:]],
+       "per_xcd_end_ns": [int(e_[xcd[ok] == x].max()) if (xcd[ok] == x).any() else None for x in range(8)]}
 print(json.dumps(out))

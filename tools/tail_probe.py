@@ -69,7 +69,7 @@ for sid in (8, 5):
     alone = []
     for s16 in range(16):
         it = k_local * 16 + s16
-        alone.append((int(clk[it, 1] - clk[it, 0]), item_max[(t_star, s16)], int(clk[it, 2]), int(clk[it, 3])))
+        alone.append((int(clk[it, 1] - clk[it, 0]), item_max[(t_star, s16)], int(clk[it, 2]) & 0xFFFFFFFF, int(clk[it, 3]) & 0xFFFFFFFF))
     g.render_frame_device(fc, out.data_ptr(), st.cuda_stream)
     torch.cuda.synchronize()
     clk_f = g.wave_clocks().astype(np.int64)
