@@ -72,7 +72,6 @@ constexpr int kVarPackedRem = 4096;         // one packed remaining-cells word (
 constexpr int kVarXcdBands = 8192;          // XCD-aware block -> tile order
 constexpr int kVarWaveClock = 32768;        // RT_KERNEL_FLAG_WAVE_CLOCK: per-item s_memtime (debug)
 constexpr int kVarUniform = 65536;          // scalar loop for wave-uniform cell lists
-constexpr int kVarBail = 131072;            // RT_KERNEL_FLAG_BAIL_WIDE phase 1: test budget + pixel queue
 constexpr int kVarLdsCells = 262144;        // RT_KERNEL_FLAG_LDS_CELLS: long uniform lists staged in LDS
 constexpr int kVarWideHeavy = 524288;       // RT_KERNEL_FLAG_WIDE_HEAVY: heavy items traced wide at the start
 constexpr int kVarCenterOut = 1048576;      // RT_KERNEL_FLAG_CENTER_OUT: XCD row turns from the middle out
@@ -162,11 +161,6 @@ struct KParams
     const uint32_t *wh_list_in;
     uint32_t *wh_list_out;
     uint32_t *wh_host_cnt;      // host-mapped: the newest plan's {cnt_w, cnt_w4} (sizes the next launches)
-    uint32_t bail_tests;        // BAIL_WIDE phase 1: test budget per sample
-    uint32_t *bail_count;       // BAIL_WIDE: queued pixels
-    uint32_t *bail_queue;       // BAIL_WIDE: (local tile << 8 | Morton pixel) per queued pixel
-    float4 *bail_state;         // BAIL_WIDE: per sample slot of a queued pixel, 2 x float4: the walk
-                                // state where phase 1 stopped, or (kb > ke) its finished colour
     // output
     uint32_t *out;
     uint32_t pitch;             // frame mode: words per row of out
@@ -574,8 +568,7 @@ template <bool STATS, int TRI, int VAR>
 __device__ __forceinline__ bool grid_intersect(const KParams& P, float ox, float oy, float oz,
                                                float dx, float dy, float dz,
                                                float& t, float& u, float& v, uint32_t& tri,
-                                               uint32_t& voxel, uint32_t& steps, uint32_t& tests,
-                                               bool *bailed = nullptr, uint32_t bail_idx = 0u)   // work item
+                                               uint32_t& voxel, uint32_t& steps, uint32_t& tests)
 {
     float nct0, nct1, nct2, dt0, dt1, dt2;
     int rem0, rem1, rem2, cs0, cs1, cs2, cell;
@@ -593,7 +586,6 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, float ox, float
         // iterations whatever nct holds.
         int skip = 0;
         int remp = rem0 | (rem1 << 11) | (rem2 << 22);      // kVarPackedRem only
-        int budget = int(P.bail_tests);                      // kVarBail only
         for (;;)
         {
             if (STATS) { voxel = uint32_t(cell); steps++; }
@@ -614,68 +606,39 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, float ox, float
                 RT_DDA_ADVANCE_PACKED(nct_ax, more);
             else
                 RT_DDA_ADVANCE_ADD(nct_ax, more);
-            if constexpr ((VAR & kVarBail) != 0)
+            // one exit test per iteration (a hit, or the grid's end here or in the empty run
+            // below), and the result read from t after the loop: the walk's loop-carried state
+            // stays in VGPRs instead of per-exit lane masks (SALU per wave, PMC-measured)
+            bool hit = false;
+            if (kb < ke) hit = test_cell<STATS, TRI, VAR>(P, ox, oy, oz, dx, dy, dz, kb, ke, nct_ax, t, u, v, tri, tests);
+            bool done = hit | !more;
+            if constexpr ((VAR & kVarSkipRun) != 0 && (VAR & kVarPackedRem) != 0 && !STATS)
             {
-                // two-phase arm: a sample whose walk would pass bail_tests tests stops here and
-                // is resumed by the wide phase (k_render_bailed); nothing of it is stored.
-                // Branch-free count (ke - kb is 0 for skipped and empty cells); the stop shares
-                // the walk's exit, so the loop keeps two exits, not three.
-                budget -= int(ke - kb);
-                if (kb < ke && budget >= 0 &&
-                    test_cell<STATS, TRI, VAR>(P, ox, oy, oz, dx, dy, dz, kb, ke, nct_ax, t, u, v, tri, tests))
-                    return true;
-                if (!more || budget < 0)
+                // Wave-uniform empty run: while every active lane is inside a run of cells the
+                // distance field proves empty, the wave takes bare DDA steps -- the same advances
+                // and the same exits as one iteration per cell, with no cell word or test work.
+                // Uniform, so no lane waits on another's run; the run ends when the first lane's
+                // does.  (A lane inside a run has no hit and more == true, so done is false.)
+                if (__all(skip > 0))
                 {
-                    *bailed = budget < 0;
-                    if (budget < 0)
+                    do
                     {
-                        // where the walk stopped: the untested cell [kb, ke) with its exit time
-                        // and the state after its step -- phase 2 resumes exactly here
-                        const size_t bi = 2 * ((size_t(bail_idx) << 6) | (threadIdx.x & 63u));
-                        P.bail_state[bi] = make_float4(nct0, nct1, nct2, nct_ax);
-                        P.bail_state[bi + 1] =
-                            make_float4(__int_as_float(remp), __int_as_float(cell), __uint_as_float(kb),
-                                        __uint_as_float(ke));
-                    }
-                    break;
+                        skip--;
+                        const float m_ = __builtin_fminf(__builtin_fminf(nct0, nct1), nct2);
+                        const bool a2_ = nct2 == m_;
+                        const bool a1_ = !a2_ && nct1 == m_;
+                        const bool a0_ = !a2_ && !a1_;
+                        remp -= a2_ ? (1 << 22) : (a1_ ? (1 << 11) : 1);
+                        more = (remp & kRemGuards) == 0;
+                        nct0 += a0_ ? dt0 : 0.0f;
+                        nct1 += a1_ ? dt1 : 0.0f;
+                        nct2 += a2_ ? dt2 : 0.0f;
+                        cell += a2_ ? cs2 : (a1_ ? cs1 : cs0);
+                    } while (__all((skip > 0) & more));
+                    done = !more;
                 }
             }
-            else
-            {
-                // one exit test per iteration (a hit, or the grid's end here or in the empty run
-                // below), and the result read from t after the loop: the walk's loop-carried state
-                // stays in VGPRs instead of per-exit lane masks (SALU per wave, PMC-measured)
-                bool hit = false;
-                if (kb < ke) hit = test_cell<STATS, TRI, VAR>(P, ox, oy, oz, dx, dy, dz, kb, ke, nct_ax, t, u, v, tri, tests);
-                bool done = hit | !more;
-                if constexpr ((VAR & kVarSkipRun) != 0 && (VAR & kVarPackedRem) != 0 && !STATS)
-                {
-                    // Wave-uniform empty run: while every active lane is inside a run of cells the
-                    // distance field proves empty, the wave takes bare DDA steps -- the same advances
-                    // and the same exits as one iteration per cell, with no cell word or test work.
-                    // Uniform, so no lane waits on another's run; the run ends when the first lane's
-                    // does.  (A lane inside a run has no hit and more == true, so done is false.)
-                    if (__all(skip > 0))
-                    {
-                        do
-                        {
-                            skip--;
-                            const float m_ = __builtin_fminf(__builtin_fminf(nct0, nct1), nct2);
-                            const bool a2_ = nct2 == m_;
-                            const bool a1_ = !a2_ && nct1 == m_;
-                            const bool a0_ = !a2_ && !a1_;
-                            remp -= a2_ ? (1 << 22) : (a1_ ? (1 << 11) : 1);
-                            more = (remp & kRemGuards) == 0;
-                            nct0 += a0_ ? dt0 : 0.0f;
-                            nct1 += a1_ ? dt1 : 0.0f;
-                            nct2 += a2_ ? dt2 : 0.0f;
-                            cell += a2_ ? cs2 : (a1_ ? cs1 : cs0);
-                        } while (__all((skip > 0) & more));
-                        done = !more;
-                    }
-                }
-                if (done) break;
-            }
+            if (done) break;
         }
         return t != rtd::kFltMax;                            // t is only set by a hit
     }
@@ -840,8 +803,7 @@ __device__ __forceinline__ bool ray_march(const KParams& P, float ox, float oy, 
 // renderer.cpp:88-122: one sample -> its colour contribution
 template <bool STATS, int TRI, int VAR>
 __device__ __forceinline__ void trace_sample(const KParams& P, uint32_t px, uint32_t py, uint32_t s, float& cr,
-                                             float& cg, float& cb, rt_sample_rec *rec, bool *bailed = nullptr,
-                                             uint32_t bail_idx = 0u)
+                                             float& cg, float& cb, rt_sample_rec *rec)
 {
     const float2 so = P.smp[s];
     float dx, dy, dz;
@@ -856,7 +818,7 @@ __device__ __forceinline__ void trace_sample(const KParams& P, uint32_t px, uint
         hit = brute_intersect<STATS>(P, P.org[0], P.org[1], P.org[2], dx, dy, dz, t, u, v, tri, tests);
     else
         hit = grid_intersect<STATS, TRI, VAR>(P, P.org[0], P.org[1], P.org[2], dx, dy, dz, t, u, v, tri, voxel,
-                                              steps, tests, bailed, bail_idx);
+                                              steps, tests);
     const KParams& Q = late_params(P);
     if constexpr ((VAR & (kVarMarch | kVarBrute)) == 0)
         if ((VAR & kVarOriginPre) && TRI == RT_TRI_MOLLER_TRUMBORE && hit)
@@ -962,53 +924,20 @@ __device__ __forceinline__ void process_item(const KParams& P, uint32_t item)
     item = __builtin_amdgcn_readfirstlane(item);
     const uint32_t lane = threadIdx.x & 63u;
     float cr = 0.0f, cg = 0.0f, cb = 0.0f;
-    bool bailed = false;
     {
         const ItemCoord ic = item_coord(P, item, lane);
         if (ic.valid)
-            trace_sample<false, TRI, VAR>(P, ic.x, ic.y, ic.s, cr, cg, cb, nullptr, &bailed, item);
+            trace_sample<false, TRI, VAR>(P, ic.x, ic.y, ic.s, cr, cg, cb, nullptr);
     }
     const KParams& Q = late_params(P);
     const ItemCoord ic = item_coord(Q, item, lane);
     const uint32_t base = lane & ~(Q.spp - 1u);
     float sr = 0.0f, sg = 0.0f, sb = 0.0f;
-    bool pixel_bailed = false;
     for (uint32_t k = 0; k < Q.spp; k++)
     {
         sr += __shfl(cr, int(base + k), 64);
         sg += __shfl(cg, int(base + k), 64);
         sb += __shfl(cb, int(base + k), 64);
-        if (VAR & kVarBail) pixel_bailed |= __shfl(int(bailed), int(base + k), 64) != 0;
-    }
-    if constexpr ((VAR & kVarBail) != 0)
-    {
-        // a pixel with a bailed sample goes to the wide phase whole (its samples are summed
-        // there, in order); one atomic per wave reserves the queue slots
-        const bool enq = pixel_bailed && ic.valid && ic.s == 0;
-        const uint64_t m = __ballot(enq);
-        if (m)
-        {
-            uint32_t base_q = 0u;
-            if (lane == uint32_t(__builtin_ctzll(m))) base_q = atomicAdd(Q.bail_count, uint32_t(__popcll(m)));
-            base_q = __shfl(base_q, int(__builtin_ctzll(m)), 64);
-            if (enq)
-            {
-                const uint32_t r = uint32_t(__builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32),
-                                                                      __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u)));
-                Q.bail_queue[base_q + r] = (ic.c.k << 8) | ic.p;
-            }
-        }
-        if (pixel_bailed)
-        {
-            // the pixel's finished samples hand their colour to phase 2 (kb = 1 > ke = 0)
-            if (ic.valid && !bailed)
-            {
-                const size_t i = 2 * (size_t(item) * 64u + lane);
-                Q.bail_state[i] = make_float4(cr, cg, cb, 0.0f);
-                Q.bail_state[i + 1] = make_float4(0.0f, 0.0f, __uint_as_float(1u), __uint_as_float(0u));
-            }
-            return;
-        }
     }
     if (ic.valid && ic.s == 0)
     {
@@ -1028,17 +957,7 @@ __device__ __forceinline__ void process_item(const KParams& P, uint32_t item)
 // order); on a device with another XCD count only the locality changes.
 constexpr uint32_t kXcds = 8;
 constexpr uint32_t kWideG = 4;              // RT_KERNEL_WIDE: lanes per sample
-constexpr uint32_t kBailTests = 256;        // BAIL_WIDE: default phase-1 test budget per sample
-constexpr uint32_t kBailAutoRanks = 4;      // AUTO: two-phase arm from this many shard ranks ...
-constexpr uint32_t kBailAutoRefs = 128;     // ... on scenes with a cell this dense, 16 lanes per
-// sample, and a budget that shrinks as the shard does (tools/shard_scaling.py)
-__host__ __device__ constexpr uint32_t bail_auto_tests(uint32_t nranks)
-{
-    // re-tuned in round 2 (phase 1 got cheaper with the packed record test): killeroo rank of 8
-    // 0.26 / 0.25 / 0.27 ms at 128 / 192 / 256, rank of 4 flat over 192..384
-    // (profiles/r02h_shard_budgets.json); below 4 ranks one phase with heavy-first order wins
-    return nranks >= 16u ? 128u : 192u;
-}
+constexpr uint32_t kWhAutoRefs = 128;       // AUTO: wide section for shards of scenes with a cell this dense
 // Heavy-first order (AUTO): front-section capacity, smallest launch it is used for, and the
 // floor of the heavy threshold in shader cycles (~40 us at 2.4 GHz)
 #ifndef RT_HF_FRONT
@@ -1280,7 +1199,7 @@ __device__ __forceinline__ bool block_of_launch(const KParams& P, uint32_t& b)
 // One sample of the wide mode, traced by the G lanes of a group (sub = this lane's index in it):
 // the same walk in every lane of the group, each cell's list split over the group.  Returns the
 // sample's colour in every lane of the group.
-template <int VAR, int G, bool RESUME = false, bool PF = true>
+template <int VAR, int G, bool PF = true>
 __device__ __forceinline__ void wide_trace(const KParams& P, uint32_t k, uint32_t slot, uint32_t sub, float& cr,
                                            float& cg, float& cb)
 {
@@ -1289,21 +1208,6 @@ __device__ __forceinline__ void wide_trace(const KParams& P, uint32_t k, uint32_
     cr = cg = cb = 0.0f;
     {
         const ItemCoord ic = tile_slot_coord(P, k, slot);
-        float4 st0, st1;
-        if (RESUME && ic.valid)
-        {
-            // phase 2: the sample's state from phase 1 (slot index = item * 64 + lane there)
-            const size_t i = 2 * (size_t(k) * kTilePix * P.spp + slot);
-            st0 = P.bail_state[i];
-            st1 = P.bail_state[i + 1];
-            if (__float_as_uint(st1.z) > __float_as_uint(st1.w))
-            {
-                cr = st0.x;                       // finished in phase 1
-                cg = st0.y;
-                cb = st0.z;
-                return;
-            }
-        }
         if (ic.valid)
         {
             const float2 so = P.smp[ic.s];
@@ -1319,44 +1223,22 @@ __device__ __forceinline__ void wide_trace(const KParams& P, uint32_t k, uint32_
             {
                 int skip = 0;
                 int remp = rem0 | (rem1 << 11) | (rem2 << 22);
-                bool pending = false;
-                if (RESUME)
-                {
-                    nct0 = st0.x;
-                    nct1 = st0.y;
-                    nct2 = st0.z;
-                    remp = __float_as_int(st1.x);
-                    cell = __float_as_int(st1.y);
-                    pending = true;
-                }
                 for (;;)
                 {
                     uint32_t kb = 0u, ke = 0u;
                     float nct_ax;
                     bool more;
-                    if (RESUME && pending)
+                    if (skip == 0)
                     {
-                        // the cell phase 1 stopped before testing, then the walk from its step on
-                        kb = __float_as_uint(st1.z);
-                        ke = __float_as_uint(st1.w);
-                        nct_ax = st0.w;
-                        more = (remp & kRemGuards) == 0;
-                        pending = false;
+                        const uint32_t w = P.cellw[uint32_t(cell)];
+                        const uint32_t cnt = w & 2047u;
+                        kb = w >> 11;
+                        ke = kb + cnt;
+                        skip = cnt ? 0 : int(kb) - 1;
                     }
                     else
-                    {
-                        if (skip == 0)
-                        {
-                            const uint32_t w = P.cellw[uint32_t(cell)];
-                            const uint32_t cnt = w & 2047u;
-                            kb = w >> 11;
-                            ke = kb + cnt;
-                            skip = cnt ? 0 : int(kb) - 1;
-                        }
-                        else
-                            skip--;
-                        RT_DDA_ADVANCE_PACKED(nct_ax, more);
-                    }
+                        skip--;
+                    RT_DDA_ADVANCE_PACKED(nct_ax, more);
                     if (kb < ke)
                     {
                         // tb starts at the cell's exit time (test_cell's bound); a lane that takes
@@ -1453,7 +1335,7 @@ __device__ __forceinline__ void wide_samples(const KParams& P, uint32_t k, uint3
     const uint32_t lane = threadIdx.x & 63u, sub = lane & uint32_t(G - 1), grp = lane / uint32_t(G);
     const uint32_t slot = slot0 + grp;
     float cr, cg, cb;
-    wide_trace<VAR, G, false, PF>(P, k, slot, sub, cr, cg, cb);
+    wide_trace<VAR, G, PF>(P, k, slot, sub, cr, cg, cb);
     // the pixel's samples are the groups grp0 .. grp0 + spp - 1 of this wave: sum in sample order
     const ItemCoord ic = tile_slot_coord(P, k, slot);
     const uint32_t grp0 = grp & ~(P.spp - 1u);
@@ -1579,57 +1461,6 @@ __global__ void __launch_bounds__(kWG) k_render_wide(KParams P)
     const uint32_t g = witem * (64u / uint32_t(G));                   // first slot, launch order
     const uint32_t kseq = g / per_tile;
     wide_samples<VAR, G>(P, P.tile_order ? P.tile_order[kseq] : kseq, g - kseq * per_tile);
-}
-
-// RT_KERNEL_FLAG_BAIL_WIDE, phase 1: the AUTO kernel with the test budget
-template <int VAR>
-__global__ void __launch_bounds__(kWG) k_render_bail1(KParams P)
-{
-    const uint32_t b = (VAR & kVarXcdBands) ? xcd_band_block(blockIdx.x, gridDim.x, P.xcd_chunk) : blockIdx.x;
-    process_item<RT_TRI_MOLLER_TRUMBORE, VAR>(P, b * kWavesPerWG + (threadIdx.x >> 6));
-}
-
-// RT_KERNEL_FLAG_BAIL_WIDE, phase 2 (AUTO, spp <= 16).  Phase 1 is the AUTO kernel with a test
-// budget: a sample whose walk would pass bail_tests triangle tests stops, and its pixel goes to
-// bail_queue instead of the frame.  Those are the samples that made the frame's critical path
-// (~1000 serial tests per lane in the densest tiles).  This kernel resumes the queued pixels'
-// walks in the wide mode: G lanes per sample split every cell's list, so each lane's chain is
-// 1/G as long, and the pixel's samples are summed in order as in phase 1.  Persistent waves take
-// queue entries round-robin; every pixel is stored by exactly one phase.
-template <int VAR, int G>
-__global__ void __launch_bounds__(kWG) k_render_bailed(KParams P)
-{
-    const uint32_t n = *P.bail_count;                                // phase 1 finished on this stream
-    const uint32_t lpp = P.spp * uint32_t(G);                        // lanes per pixel (<= 64)
-    const uint32_t per_wave = 64u / lpp;
-    const uint32_t lane = threadIdx.x & 63u, g = lane / lpp, r = lane - g * lpp;
-    const uint32_t smp = r / uint32_t(G), sub = r - smp * uint32_t(G);
-    const uint32_t nwaves = gridDim.x * kWavesPerWG;
-    for (uint32_t e0 = (blockIdx.x * kWavesPerWG + (threadIdx.x >> 6)) * per_wave; e0 < n; e0 += nwaves * per_wave)
-    {
-        const uint32_t e = e0 + g;
-        const bool live = e < n;
-        const uint32_t q = live ? P.bail_queue[e] : 0u;
-        const uint32_t k = q >> 8, p = q & 255u;
-        float cr = 0.0f, cg = 0.0f, cb = 0.0f;
-        if (live) wide_trace<VAR, G, true>(P, k, p * P.spp + smp, sub, cr, cg, cb);
-        float sr = 0.0f, sg = 0.0f, sb = 0.0f;
-        for (uint32_t j = 0; j < P.spp; j++)
-        {
-            const int src = int(g * lpp + j * uint32_t(G));
-            sr += __shfl(cr, src, 64);
-            sg += __shfl(cg, src, 64);
-            sb += __shfl(cb, src, 64);
-        }
-        if (live && r == 0u)
-        {
-            const ItemCoord ic = tile_slot_coord(P, k, p * P.spp);
-            const uint32_t word = rtd::pack_bgra8(rtd::gamma_half(average(P, sr)),
-                                                  rtd::gamma_half(average(P, sg)),
-                                                  rtd::gamma_half(average(P, sb)));
-            store_pixel(P, ic.c, ic.p, ic.x, ic.y, word);
-        }
-    }
 }
 
 // RT_KERNEL_COMPACT (grid intersector, spp a power of two <= 64): wavefront active-ray
@@ -2126,11 +1957,6 @@ struct rt_scene
     // frefs hold the per-reference terms of this camera origin (bit patterns; valid once computed)
     bool fref_valid = false;
     uint32_t fref_org[3] = { 0, 0, 0 };
-    uint32_t *d_bail = nullptr;     // RT_KERNEL_FLAG_BAIL_WIDE: queued-pixel count + queue
-    size_t bail_cap = 0;
-    float4 *d_bail_state = nullptr; // RT_KERNEL_FLAG_BAIL_WIDE: phase 1 -> phase 2 per-sample state
-    size_t bail_state_cap = 0;
-    uint32_t bail_wgs = 1024;       // phase-2 persistent grid: 4 workgroups per CU
     uint64_t *d_clk = nullptr;      // RT_KERNEL_FLAG_WAVE_CLOCK records of the last such launch
     size_t clk_cap = 0;
     uint32_t clk_items = 0;
@@ -2207,7 +2033,7 @@ constexpr uint32_t kKernelFlags = RT_KERNEL_FLAG_CENTER_OUT | RT_KERNEL_FLAG_STA
                                   RT_KERNEL_FLAG_WIDE_HEAVY |
                                   RT_KERNEL_FLAG_LDS_CELLS | RT_KERNEL_FLAG_ONE_PHASE | RT_KERNEL_FLAG_EXHAUSTIVE |
                                   RT_KERNEL_FLAG_WAVE_CLOCK |
-                                  RT_KERNEL_FLAG_BAIL_WIDE | RT_KERNEL_BUDGET_MASK;
+                                  RT_KERNEL_BUDGET_MASK;
 
 int validate_frame(const rt_frame *f)
 {
@@ -2393,8 +2219,12 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
         P.wh_refresh = (c->frames - 1u) % kWhRefresh == 0u;       // frames counts this one
         P.wh_wgs = P.wh_refresh ? 0u : (units + kWavesPerWG - 1u) / kWavesPerWG;
         P.wh_floor = env_tunable("RT_WH_FLOOR", kWhFloor);
-        P.wh_alpha16 = env_tunable("RT_WH_ALPHA16", P.nranks >= 8u ? kWhAlpha16Wide : kWhAlpha16);
-        P.wh_alpha16_4 = env_tunable("RT_WH_ALPHA16_4", P.wh_alpha16);          // = alpha: no 4-lane tier
+        const uint32_t alpha = env_tunable("RT_WH_ALPHA16", P.nranks >= 8u ? kWhAlpha16Wide : kWhAlpha16);
+        // spp <= 4: 16 lanes per sample (a 4-lane tier below it only on request, measured no
+        // gain); spp 8-16: a pixel's samples fill a wave at 4 lanes each, so every item takes
+        // the 4-lane tier
+        P.wh_alpha16 = P.spp <= 4u ? alpha : 0xFFFFFFFFu;
+        P.wh_alpha16_4 = P.spp <= 4u ? env_tunable("RT_WH_ALPHA16_4", alpha) : alpha;
         P.wh_mark_in = c->wh_marks + size_t(v & 1u) * kWavesPerWG * c->cap_blocks;
         P.wh_mark_out = c->wh_marks + size_t((v + 1u) & 1u) * kWavesPerWG * c->cap_blocks;
         P.wh_list_in = c->wh_lists + size_t(v & 1u) * 2u * kWhMax;
@@ -2508,60 +2338,18 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
     const uint32_t budget = (f->kernel & RT_KERNEL_BUDGET_MASK) >> RT_KERNEL_BUDGET_SHIFT;
     // the wide arms need AUTO's full record/count layout and at most 64 / 4 samples per pixel
     const bool wide_ok = auto_path && (var & ~(kVarCenterOut)) == kVarAuto && P.spp * kWideG <= 64u;
-    // AUTO takes the two-phase arm for a shard of >= 2 ranks of a scene with dense cells: there a
-    // rank's launch is bound by its few ~1000-test waves, which the wide phase splits 16 ways
-    // (measured, tools/shard_scaling.py, killeroo rank of 2 / 4 / 8: 0.60 / 0.50 / 0.46 ms with
-    // the plain kernel -> 0.48 / 0.35 / 0.25 with budgets 384 / 192 / 128).  On a whole frame,
-    // or a scene without dense cells, phase 1's budget count and the re-trace cost more than
-    // they save.
-    // AUTO takes the wide section (kVarWideHeavy: the wide code's layout, spp <= 4) for a shard of
-    // >= 2 ranks of a scene with dense cells: there a rank's launch is bound by its few ~1000-test
-    // waves, which the section splits 16 ways beside the lane kernel (measured, tools/wh_probe.py,
-    // killeroo rank of 2 / 4 / 8: 0.36 / 0.33 / 0.25 ms with the lane kernel alone -> 0.35 / 0.20
-    // / 0.15).  On a whole frame the lanes are busy with other items anyway and
-    // the section's repeated walks cost more than they save (+1-3 %).
-    const bool wide_heavy = wide_ok && kind == RT_KERNEL_AUTO && P.spp <= 4u && !(f->kernel & RT_KERNEL_FLAG_BAIL_WIDE) &&
+    // AUTO takes the wide section (kVarWideHeavy: the wide code's layout, spp <= 16) for a shard
+    // of >= 2 ranks of a scene with dense cells: there a rank's launch is bound by its few
+    // ~1000-test waves, which the section splits 16 ways (4 for spp 8-16) beside the lane kernel
+    // (measured, tools/wh_probe.py, killeroo rank of 2 / 4 / 8: 0.36 / 0.33 / 0.25 ms with the
+    // two-phase arm it replaced -> 0.35 / 0.20 / 0.15).  On a whole frame the
+    // lanes are busy with other items anyway and the section's repeated walks cost more than they
+    // save (+1-3 %).
+    const bool wide_heavy = wide_ok && kind == RT_KERNEL_AUTO &&
                             ((f->kernel & RT_KERNEL_FLAG_WIDE_HEAVY) ||
-                             (P.nranks >= 2u && s->max_cell_refs >= kBailAutoRefs && !(f->kernel & RT_KERNEL_FLAG_ONE_PHASE)));
-    const bool bail_auto = kind == RT_KERNEL_AUTO && P.nranks >= kBailAutoRanks && s->max_cell_refs >= kBailAutoRefs &&
-                           !(f->kernel & RT_KERNEL_FLAG_ONE_PHASE) && !wide_heavy;
-    const bool bail = wide_ok && kind == RT_KERNEL_AUTO && (bail_auto || (f->kernel & RT_KERNEL_FLAG_BAIL_WIDE));
-    const bool g16 = ((f->kernel & RT_KERNEL_FLAG_WIDE16) || (bail_auto && !(f->kernel & RT_KERNEL_FLAG_BAIL_WIDE))) &&
-                     P.spp * 16u <= 64u;
-    if (bail)
-    {
-        const size_t need = size_t(n_local_tiles) * kTilePix + 1u;   // count + one entry per pixel
-        if (need > s->bail_cap)
-        {
-            // grows once per larger frame; the steady state allocates nothing
-            if (s->d_bail) RT_HIP(hipFree(s->d_bail));
-            s->d_bail = nullptr;
-            RT_HIP(hipMalloc(&s->d_bail, sizeof(uint32_t) * need));
-            s->bail_cap = need;
-        }
-        P.bail_tests = budget ? 16u * budget
-                              : ((f->kernel & RT_KERNEL_FLAG_BAIL_WIDE) ? kBailTests : bail_auto_tests(P.nranks));
-        const size_t nstate = size_t(n_local_tiles) * kTilePix * P.spp * 2u;   // 2 float4 per sample slot
-        if (nstate > s->bail_state_cap)
-        {
-            if (s->d_bail_state) RT_HIP(hipFree(s->d_bail_state));
-            s->d_bail_state = nullptr;
-            RT_HIP(hipMalloc(&s->d_bail_state, sizeof(float4) * nstate));
-            s->bail_state_cap = nstate;
-        }
-        P.bail_state = s->d_bail_state;
-        P.bail_count = s->d_bail;
-        P.bail_queue = s->d_bail + 1;
-        RT_HIP(hipMemsetAsync(s->d_bail, 0, sizeof(uint32_t), st));
-        RT_HIP(mark(kt0));
-        hipLaunchKernelGGL((k_render_bail1<kVarAuto | kVarBail>), dim3(uint32_t(blocks)), wg, 0, st, P);
-        if (g16)
-            hipLaunchKernelGGL((k_render_bailed<kVarWide, 16>), dim3(s->bail_wgs), wg, 0, st, P);
-        else
-            hipLaunchKernelGGL((k_render_bailed<kVarWide, kWideG>), dim3(s->bail_wgs), wg, 0, st, P);
-        RT_HIP(mark(kt1));
-    }
-    else if (wide_ok && kind == RT_KERNEL_WIDE)
+                             (P.nranks >= 2u && s->max_cell_refs >= kWhAutoRefs && !(f->kernel & RT_KERNEL_FLAG_ONE_PHASE)));
+    const bool g16 = (f->kernel & RT_KERNEL_FLAG_WIDE16) && P.spp * 16u <= 64u;
+    if (wide_ok && kind == RT_KERNEL_WIDE)
     {
         const uint32_t G = g16 ? 16u : kWideG;
         P.xcd_chunk *= G;
@@ -2758,7 +2546,6 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
     std::unique_ptr<rt_scene> s(new rt_scene());
     s->device = device;
     s->compact_wgs = 8u * uint32_t(std::max(1, ncus));
-    s->bail_wgs = 4u * uint32_t(std::max(1, ncus));
     for (int a = 0; a < 3; a++)
     {
         s->dims[a] = g.dims[a];
@@ -2967,8 +2754,6 @@ int rt_scene_destroy(rt_scene *s)
         (void)hipFree(s->d_tridist);
         (void)hipFree(s->d_distblk);
         (void)hipFree(s->d_clk);
-        (void)hipFree(s->d_bail);
-        (void)hipFree(s->d_bail_state);
         for (HfCtx& h : s->hf)
         {
             (void)hipFree(h.marks);

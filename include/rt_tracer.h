@@ -88,8 +88,7 @@ enum rt_kernel {
                                   sample, distance-skipping 3D-DDA, per-camera-origin triangle records,
                                   wave-uniform cell lists on scalar loads, XCD-aware tile rows, and the
                                   heavy-first block order; for >= 2-rank shards of dense scenes at
-                                  spp <= 4 the wide section (RT_KERNEL_FLAG_WIDE_HEAVY), at spp 8-16
-                                  from 4 ranks the two-phase arm (RT_KERNEL_FLAG_BAIL_WIDE) */
+                                  spp <= 16 the wide section (RT_KERNEL_FLAG_WIDE_HEAVY) */
     RT_KERNEL_LANES = 1,       /* the plain per-lane kernel: one lane per sample, the reference's walk
                                   and ray/triangle test cell by cell (A/B baseline) */
     RT_KERNEL_PIXEL_LOOP = 2,  /* one lane per pixel looping over its samples (any spp) */
@@ -103,33 +102,31 @@ enum rt_kernel {
     RT_KERNEL_FLAG_CENTER_OUT = 0x10, /* OR-able (AUTO): the XCDs' row turns start at the frame's
                                          middle row and move outward (A/B arm of the row order) */
     RT_KERNEL_FLAG_STATIC_ORDER = 0x20, /* OR-able (AUTO): no heavy-first block order (A/B arm) */
-    RT_KERNEL_FLAG_WIDE16 = 0x40,     /* OR-able (WIDE kernel, BAIL_WIDE phase 2; spp <= 4): 16 lanes
-                                         per sample instead of 4 */
+    RT_KERNEL_FLAG_WIDE16 = 0x40,     /* OR-able (WIDE kernel; spp <= 4): 16 lanes per sample
+                                         instead of 4 */
     RT_KERNEL_FLAG_LDS_CELLS = 0x80,  /* OR-able (AUTO): a wave-uniform list of >= 16 references is
                                          staged through LDS 64 records at a time */
-    RT_KERNEL_FLAG_ONE_PHASE = 0x100, /* OR-able (AUTO): never the two-phase arm, also for shards of
+    RT_KERNEL_FLAG_ONE_PHASE = 0x100, /* OR-able (AUTO): the lane kernel alone, also for shards of
                                          dense scenes (A/B arm of the rank-count policy) */
-    RT_KERNEL_FLAG_WIDE_HEAVY = 0x200, /* OR-able (AUTO, spp <= 4; AUTO's own choice for >= 2-rank
+    RT_KERNEL_FLAG_WIDE_HEAVY = 0x200, /* OR-able (AUTO, spp <= 16; AUTO's own choice for >= 2-rank
                                           shards of dense scenes): work items that earlier frames of
                                           the same launch shape measured as heavy are traced wide (16
-                                          lanes per sample) by a kernel on the scene's side stream,
-                                          beside the one-lane-per-sample kernel (fork / join) */
+                                          lanes per sample, 4 for spp 8-16) by a kernel on the scene's
+                                          side stream, beside the one-lane-per-sample kernel (fork /
+                                          join) */
     RT_KERNEL_FLAG_EXHAUSTIVE = 0x8000, /* OR-able, ray march: evaluate every triangle per step
                                            (no block culling; A/B arm, identical results) */
     RT_KERNEL_FLAG_WAVE_CLOCK = 0x400000, /* OR-able (AUTO), debug: record s_memtime {start, end} of
                                              every 64-sample work item (rt_debug_wave_clocks) */
     RT_KERNEL_BUDGET_SHIFT = 24,      /* bits 24-30: RT_KERNEL_COMPACT: lanes that must be idle before
-                                         a wave refills (1..64; 0 = default 48); BAIL_WIDE: phase-1
-                                         test budget / 16 (0 = default) */
+                                         a wave refills (1..64; 0 = default 48) */
     RT_KERNEL_BUDGET_MASK = 0x7F000000,
     RT_KERNEL_COMPACT_REFILL_SHIFT = RT_KERNEL_BUDGET_SHIFT,
     RT_KERNEL_COMPACT_REFILL_MASK = RT_KERNEL_BUDGET_MASK,
 };
-/* OR-able (AUTO, grid, Moller-Trumbore, spp <= 16): two-phase frame.  Samples whose walk would
-   pass a triangle-test budget (bits 24-30 x 16, 0 = 256) stop; their pixels' walks are resumed
-   by a second kernel with 4 (or, WIDE16, 16) lanes per sample splitting each cell's list.
-   Bit 31 (not an enum constant: it does not fit a C int). */
-#define RT_KERNEL_FLAG_BAIL_WIDE 0x80000000u
+/* Bit 31 was RT_KERNEL_FLAG_BAIL_WIDE, the two-phase arm (a test budget per sample, then the
+   stopped samples resumed 4 or 16 lanes per sample by a second kernel).  RT_KERNEL_FLAG_WIDE_HEAVY
+   replaced it in round 2; a frame that sets the bit is rejected. */
 
 /* Per-frame parameters: what Renderer::RenderTile reads from the Scene and itself. */
 typedef struct rt_frame {

@@ -80,7 +80,7 @@ def test_bench_run_steps_two_ranks_gloo():
 @pytest.mark.gpu
 @pytest.mark.timeout(240)
 def test_bench_two_ranks_one_gpu_rehearsal():
-    """The whole N > 1 bench path on the GPU -- AUTO's shard kernels (two-phase arm on
+    """The whole N > 1 bench path on the GPU -- AUTO's shard kernels (wide section on
     killeroo), the all-gather, the K3 un-permute and the max-over-ranks timing -- as two
     processes on one device under gloo (RCCL needs one GPU per rank).  Rank 0's --check
     compares both assembled 1080p frames with a one-GPU render, byte for byte."""

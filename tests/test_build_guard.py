@@ -60,9 +60,9 @@ def test_render_kernels_do_not_spill(tmp_path):
         assert sc == 0, f"{n} spills {sc} B/lane"
     # the AUTO kernel (kVarAuto = 80398: lanes + wave gate + distance skip + origin terms + Newton
     # reciprocal + packed counts + uniform cells + empty runs + XCD rows), its fallbacks for scenes
-    # outside the reciprocal / packing ranges, its arms and the two-phase phase 1 keep 8 waves/SIMD
+    # outside the reciprocal / packing ranges, and its arms keep 8 waves/SIMD
     for key in ("k_render_lanesILi0ELi80398E", "k_render_lanesILi0ELi78350E", "k_render_lanesILi0ELi76298E",
                 "k_render_lanesILi0ELi74250E", "k_render_lanesILi0ELi1128974E", "k_render_lanesILi0ELi0E",
-                "k_render_bail1", "k_render_compact"):
+                "k_render_compact"):
         arm = [v for n, v in render.items() if key in n]
         assert arm and all(a[2] == 8 for a in arm), (key, arm)

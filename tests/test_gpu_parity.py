@@ -172,18 +172,15 @@ def test_newton_reciprocal_exhaustive():
 
 def test_auto_equals_arms(golden, scenes):
     """AUTO (heavy-first order) and its static-order, centre-out and LDS-staged arms, the plain
-    LANES kernel, the wide kernel (4 and 16 lanes per sample) and the two-phase arm (budgets 256
-    and 64: many pixels resumed by the wide phase) render the reference's bytes on the two bench
-    scenes and the densest one."""
+    LANES kernel and the wide kernel (4 and 16 lanes per sample) render the reference's bytes on
+    the two bench scenes and the densest one."""
     A = rtm.RT_KERNEL_AUTO
     for sid in (1, 5, 8):
         hs, gs = scenes(sid)
         want = golden["frames_1080p4"][str(sid)]["bgra_sha256"]
         for k in (A, A | rtm.RT_KERNEL_FLAG_STATIC_ORDER, A | rtm.RT_KERNEL_FLAG_CENTER_OUT,
                   A | rtm.RT_KERNEL_FLAG_LDS_CELLS, rtm.RT_KERNEL_LANES,
-                  rtm.RT_KERNEL_WIDE, rtm.RT_KERNEL_WIDE | rtm.RT_KERNEL_FLAG_WIDE16,
-                  rtm.RT_KERNEL_FLAG_BAIL_WIDE, rtm.RT_KERNEL_FLAG_BAIL_WIDE | (4 << 24),
-                  rtm.RT_KERNEL_FLAG_BAIL_WIDE | rtm.RT_KERNEL_FLAG_WIDE16 | (4 << 24)):
+                  rtm.RT_KERNEL_WIDE, rtm.RT_KERNEL_WIDE | rtm.RT_KERNEL_FLAG_WIDE16):
             img = gs.render_frame(gs.frame(1920, 1080, 4, kernel=k))
             assert hashlib.sha256(img.tobytes()).hexdigest() == want, (sid, hex(k))
 
@@ -256,15 +253,20 @@ def test_hip_graph_capture_replay(golden, scenes):
 
 
 @pytest.mark.parametrize("spp", [1, 2, 4, 16, 32])
-def test_wide_and_two_phase_vs_oracle(scenes, oracle, spp):
-    """Wide kernel and two-phase arm on ragged frames at every spp they take (32 falls back to
-    AUTO), budget 16 tests so most pixels go through the wide phase."""
+def test_wide_vs_oracle(scenes, oracle, spp):
+    """Wide kernel (4 and 16 lanes per sample) on ragged frames at every spp it takes (32 falls
+    back to AUTO)."""
     hs, gs = scenes(5)
     exp, _, _ = oracle.render(5, 97, 61, spp)
-    for k in (rtm.RT_KERNEL_WIDE, rtm.RT_KERNEL_FLAG_BAIL_WIDE | (1 << 24),
-              rtm.RT_KERNEL_WIDE | rtm.RT_KERNEL_FLAG_WIDE16,
-              rtm.RT_KERNEL_FLAG_BAIL_WIDE | rtm.RT_KERNEL_FLAG_WIDE16 | (1 << 24)):
+    for k in (rtm.RT_KERNEL_WIDE, rtm.RT_KERNEL_WIDE | rtm.RT_KERNEL_FLAG_WIDE16):
         np.testing.assert_array_equal(gs.render_frame(gs.frame(97, 61, spp, kernel=k)), exp, err_msg=hex(k))
+
+
+def test_removed_two_phase_flag_rejected(scenes):
+    """Bit 31 (the two-phase arm, replaced by the wide section) fails loudly."""
+    hs, gs = scenes(1)
+    with pytest.raises(rtm.RtError):
+        gs.render_frame(gs.frame(32, 32, 4, kernel=0x80000000))
 
 
 @pytest.mark.parametrize("sid,spp", [(5, 1), (5, 4), (5, 64), (8, 2), (8, 16), (4, 4)])
@@ -301,7 +303,7 @@ def test_shard_partition_dense_scenes(golden, scenes, sid, nranks):
     assert hashlib.sha256(img.tobytes()).hexdigest() == golden["frames_1080p4"][str(sid)]["bgra_sha256"]
 
 
-@pytest.mark.parametrize("sid,nranks,kernel", [(8, 8, 0), (5, 4, 0), (8, 2, 0x200), (5, 1, 0x200)])
+@pytest.mark.parametrize("sid,nranks,kernel", [(8, 8, 0), (5, 4, 0), (8, 2, 0x200), (5, 1, 0x200), (8, 4, 0)])
 def test_wide_heavy_shard_frames(golden, scenes, sid, nranks, kernel):
     """RT_KERNEL_FLAG_WIDE_HEAVY over consecutive frames of every rank: frames 0-1 render one
     lane per sample and measure, later frames trace the listed heavy items on the side stream
@@ -335,21 +337,23 @@ def test_wide_heavy_shard_frames(golden, scenes, sid, nranks, kernel):
     assert hashlib.sha256(img.tobytes()).hexdigest() == golden["frames_1080p4"][str(sid)]["bgra_sha256"]
 
 
-@pytest.mark.parametrize("spp", [1, 2, 4])
-def test_wide_heavy_ragged_vs_oracle(scenes, oracle, spp, monkeypatch):
-    """The wide section on ragged frames (partial tiles, spp 1/2/4) with the floor lowered so
-    that most items go wide, over 70 frames: the sticky list, the refresh frame (frame 64 renders
-    every item one lane per sample) and the re-listing after it all render the reference's
-    bytes."""
+@pytest.mark.parametrize("spp,alpha4", [(1, None), (2, None), (4, None), (4, "1"), (8, None), (16, None)])
+def test_wide_heavy_ragged_vs_oracle(scenes, oracle, spp, alpha4, monkeypatch):
+    """The wide section on ragged frames (partial tiles) with the floor lowered so that most
+    items go wide, over 136 frames: the sticky list, the refresh frame (frame 128 renders every
+    item one lane per sample) and the re-listing after it all render the reference's bytes.
+    spp <= 4 takes 16 lanes per sample (with alpha4 also a 4-lane tier), spp 8 / 16 only 4."""
     monkeypatch.setenv("RT_WH_FLOOR", "2000")
-    monkeypatch.setenv("RT_WH_ALPHA16", "1")
+    monkeypatch.setenv("RT_WH_ALPHA16", "2")
+    if alpha4:
+        monkeypatch.setenv("RT_WH_ALPHA16_4", alpha4)
     hs, gs = scenes(8)
     exp, _, _ = oracle.render(8, 97, 61, spp)
     f = gs.frame(97, 61, spp, kernel=rtm.RT_KERNEL_AUTO | rtm.RT_KERNEL_FLAG_WIDE_HEAVY)
     listed = 0
-    for i in range(70):
+    for i in range(136):
         np.testing.assert_array_equal(gs.render_frame(f), exp, err_msg=str(i))
-        if i in (3, 40, 69):
+        if i in (3, 60, 130):
             listed = max(listed, gs.wide_items())
     assert listed > 0
 
