@@ -980,7 +980,10 @@ constexpr uint32_t kWhMax = 4096;
 constexpr uint32_t kHfMinBlocks = RT_HF_MIN_BLOCKS;   // below ~2 rounds of workgroups every block starts early
 constexpr uint32_t kHfFloor = RT_HF_FLOOR;
 constexpr uint32_t kHfShift = RT_HF_SHIFT;  // heavy: cost > last max >> kHfShift; very heavy: >> 1
-constexpr uint32_t kHfPeriod = 4;           // a plan from every 4th frame of a launch shape
+#ifndef RT_HF_PERIOD
+#define RT_HF_PERIOD 16
+#endif
+constexpr uint32_t kHfPeriod = RT_HF_PERIOD;   // a plan from every kHfPeriod-th frame of a launch shape
 // A plan lists blocks only when the slowest block is a real tail: its cost (one wave's
 // duration) above kHfTail / 16 of the estimated frame span, sum of wave costs / resident waves
 constexpr uint32_t kHfTail = 6;
@@ -1970,12 +1973,13 @@ struct rt_scene
     float *h_smp_pinned = nullptr;
     // internal stream + timing events
     hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t ev1 = nullptr;       // after each launch's last kernel (ordering only, no timestamp)
     bool ev_recorded = false;
     // render-kernel-only timing: event pair around the render kernel(s) of each launch (not the
     // heavy-first planning kernels), a ring of the last kTimeRing launches (rt_kernel_times)
     hipEvent_t kt0[kTimeRing] = {}, kt1[kTimeRing] = {};
     uint32_t kt_next = 0, kt_count = 0;
+    uint32_t kt_last = kTimeRing;   // ring slot of the last timed launch (kTimeRing: none)
     hipStream_t last_stream = nullptr;  // stream of the last launch (cross-stream ordering)
     // RT_KERNEL_FLAG_WIDE_HEAVY: side stream of the wide section, fork / join events
     hipStream_t side = nullptr;
@@ -2303,7 +2307,6 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
         var = kVarMarch | ((f->kernel & RT_KERNEL_FLAG_EXHAUSTIVE) ? kVarExhaustive : 0);
     else if (lanes && P.isect == RT_ISECT_BRUTE_FORCE)
         var = kVarBrute;
-    RT_HIP(hipEventRecord(s->ev0, st));
     // kernel-time events only outside stream capture (a captured record has no time to read)
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     RT_HIP(hipStreamIsCapturing(st, &cap));
@@ -2441,6 +2444,7 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
     s->ev_recorded = true;
     if (timed)
     {
+        s->kt_last = kslot;
         s->kt_next = (kslot + 1u) % kTimeRing;
         s->kt_count = std::min(s->kt_count + 1u, kTimeRing);
     }
@@ -2729,8 +2733,7 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
                                         tridist.size() + distblk.size()) +
                       sizeof(uint32_t) * cellw.size();
     RT_HIP(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
-    RT_HIP(hipEventCreate(&s->ev0));
-    RT_HIP(hipEventCreate(&s->ev1));
+    RT_HIP(hipEventCreateWithFlags(&s->ev1, hipEventDisableTiming));
 
     *out = s.release();
     return RT_OK;
@@ -2772,7 +2775,6 @@ int rt_scene_destroy(rt_scene *s)
         (void)hipFree(s->d_frame);
         if (s->h_smp_pinned) (void)hipHostFree(s->h_smp_pinned);
         if (s->h_frame) (void)hipHostFree(s->h_frame);
-        if (s->ev0) (void)hipEventDestroy(s->ev0);
         if (s->ev1) (void)hipEventDestroy(s->ev1);
         for (hipEvent_t e : s->band_ev) if (e) (void)hipEventDestroy(e);
         for (hipEvent_t e : s->kt0) if (e) (void)hipEventDestroy(e);
@@ -2858,9 +2860,10 @@ int rt_unshard_device(uint32_t width, uint32_t height, uint32_t nranks, const ui
 int rt_last_kernel_ms(rt_scene *s, float *ms)
 {
     if (!s || !ms) return fail(RT_E_INVALID, "NULL argument");
-    if (!s->ev_recorded) return fail(RT_E_INVALID, "no kernel recorded yet");
-    RT_HIP(hipEventSynchronize(s->ev1));
-    RT_HIP(hipEventElapsedTime(ms, s->ev0, s->ev1));
+    std::lock_guard<std::mutex> lk(s->mtx);
+    if (s->kt_last >= kTimeRing) return fail(RT_E_INVALID, "no timed kernel recorded yet");
+    RT_HIP(hipEventSynchronize(s->kt1[s->kt_last]));
+    RT_HIP(hipEventElapsedTime(ms, s->kt0[s->kt_last], s->kt1[s->kt_last]));
     return RT_OK;
 }
 

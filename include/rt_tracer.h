@@ -223,8 +223,8 @@ int  rt_render_shard_device(rt_scene *scene, const rt_frame *frame, uint32_t ran
 int  rt_unshard_device(uint32_t width, uint32_t height, uint32_t nranks,
                        const uint32_t *d_gathered, uint32_t *d_bgra, void *hip_stream);
 
-/* Kernel time of the last rendering call on this scene measured with HIP events on the
- * launch stream (ms), for roofline accounting.  Only valid after that stream completed. */
+/* Render-kernel time of the last timed rendering call on this scene (ms): the HIP events on the
+ * launch stream immediately around its render kernel(s), as rt_kernel_times.  Waits for them. */
 int  rt_last_kernel_ms(rt_scene *scene, float *ms);
 /* Render-kernel durations (ms, HIP events recorded on the launch stream immediately around the
  * render kernel(s) of each launch -- not the heavy-first planning kernels), for the launches since
