@@ -63,7 +63,7 @@ TRACER_SYMBOLS = [
     "rt_get_device_count", "rt_scene_create", "rt_scene_destroy", "rt_scene_device_bytes",
     "rt_render_tiles", "rt_render_frame_device", "rt_shard_elems", "rt_render_shard_device",
     "rt_unshard_device", "rt_last_kernel_ms", "rt_trace_samples", "rt_debug_primitives",
-    "rt_debug_rcp_check", "rt_debug_wave_clocks", "rt_debug_heavy_first", "rt_debug_wide_items",
+    "rt_debug_rcp_check", "rt_debug_wave_clocks", "rt_debug_heavy_first", "rt_debug_wide_items", "rt_scene_set_timing",
     "rt_sample_table", "rt_last_error", "rt_abi_version", "rt_grid_build", "rt_grid_free",
     "rt_scene_create_from_mesh", "rt_kernel_times", "rt_render_frame_host", "rt_frame_host_wait", "rt_host_alloc",
     "rt_host_free",
@@ -175,6 +175,8 @@ def tracer_lib():
                                                ctypes.POINTER(c_u32)]
         if hasattr(L, "rt_debug_wide_items"):
             L.rt_debug_wide_items.argtypes = [vp, ctypes.POINTER(c_u32)]
+        if hasattr(L, "rt_scene_set_timing"):
+            L.rt_scene_set_timing.argtypes = [vp, c_u32]
         L.rt_sample_table.argtypes = [c_u32, vp]
         L.rt_last_error.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
         L.rt_get_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
@@ -542,6 +544,11 @@ class GpuScene:
         _check(L.rt_debug_heavy_first(self._h, ctypes.byref(f), ctypes.byref(n), ctypes.byref(e)), L,
                "rt_debug_heavy_first")
         return f.value, n.value, e.value
+
+    def set_timing(self, every):
+        """Time every `every`-th render launch of this scene (1: all, 0: none; default 8)."""
+        L = tracer_lib()
+        _check(L.rt_scene_set_timing(self._h, every), L, "rt_scene_set_timing")
 
     def wide_items(self):
         """RT_KERNEL_FLAG_WIDE_HEAVY: work items the newest plan lists for the wide section."""

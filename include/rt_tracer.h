@@ -227,9 +227,13 @@ int  rt_unshard_device(uint32_t width, uint32_t height, uint32_t nranks,
  * launch stream immediately around its render kernel(s), as rt_kernel_times.  Waits for them. */
 int  rt_last_kernel_ms(rt_scene *scene, float *ms);
 /* Render-kernel durations (ms, HIP events recorded on the launch stream immediately around the
- * render kernel(s) of each launch -- not the heavy-first planning kernels), for the launches since
- * the previous call, oldest first, at most max_n and at most the last 64.  Waits for them. */
+ * render kernel(s) of a launch -- not the heavy-first planning kernels), for the timed launches
+ * since the previous call, oldest first, at most max_n and at most the last 64.  Waits for them.
+ * A launch is timed when it is the n-th, 2n-th, ... of the scene (rt_scene_set_timing, default
+ * n = 8): a timed event pair costs ~10 us of device time per launch. */
 int  rt_kernel_times(rt_scene *scene, float *ms, uint32_t max_n, uint32_t *n);
+/* Times every `every`-th launch from the next one on (1: every launch, 0: none). */
+int  rt_scene_set_timing(rt_scene *scene, uint32_t every);
 
 /* ---- parity / debug ---------------------------------------------------------------- */
 /* Per-sample records for pixels [x0,x0+w) x [y0,y0+h), order (y, x, sample).  Synchronous. */

@@ -473,16 +473,22 @@ def test_render_frame_device_on_torch_stream(golden, scenes):
 
 
 def test_kernel_times_ring(scenes):
-    """rt_kernel_times: one positive render-kernel time per launch since the previous call."""
+    """rt_kernel_times: one positive render-kernel time per timed launch since the previous call;
+    rt_scene_set_timing(1) times every launch, (4) every 4th from the next launch on, (0) none."""
     import torch
     hs, gs = scenes(1)
     out = torch.zeros(1920 * 1080, dtype=torch.int32, device="cuda")
-    gs.kernel_times()
-    for _ in range(3):
-        gs.render_frame_device(gs.frame(1920, 1080, 4), out.data_ptr(), 0)
-    t = gs.kernel_times()
-    assert len(t) == 3 and (t > 0.01).all() and (t < 50).all()
-    assert len(gs.kernel_times()) == 0
+    try:
+        for every, launches, want in ((1, 3, 3), (4, 9, 3), (0, 5, 0)):
+            gs.set_timing(every)
+            gs.kernel_times()
+            for _ in range(launches):
+                gs.render_frame_device(gs.frame(1920, 1080, 4), out.data_ptr(), 0)
+            t = gs.kernel_times()
+            assert len(t) == want and (t > 0.01).all() and (t < 50).all(), (every, t)
+            assert len(gs.kernel_times()) == 0
+    finally:
+        gs.set_timing(8)
 
 
 def test_framebuffer_tile_pool_drop_in(golden, scenes, tmp_path):

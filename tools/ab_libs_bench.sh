@@ -4,6 +4,6 @@
 set -o pipefail
 for r in $(seq 1 ${3:-3}); do
 for L in $1 $2; do
-  RT_TRACER_LIB=$L timeout -k 10 200 python3 -u bench.py --no-cpu-baseline --no-end-to-end > gpurun_out/abl_${L}_$r.json 2>/dev/null || exit $?
-  echo $L $r $(python3 -c "import json;d=json.load(open('gpurun_out/abl_${L}_$r.json'));print(d['ms_per_step'], {k:v['kernel_ms'] for k,v in d['per_scene'].items()})")
+  RT_TRACER_LIB=$L timeout -k 10 200 python3 -u ${AB_CMD:-bench.py --no-cpu-baseline --no-end-to-end} > gpurun_out/abl_${L}_$r.json 2>/dev/null || exit $?
+  echo $L $r $(tail -c 2000 gpurun_out/abl_${L}_$r.json | python3 -c "import sys,json;t=sys.stdin.read().strip().splitlines()[-1];print(json.loads(t)['ms_per_step'] if t.startswith('{') else t)")
 done; done
