@@ -195,6 +195,14 @@ __device__ __forceinline__ uint32_t *wave_counters()
     return c + (threadIdx.x >> 6) * 2u;
 }
 
+// Wave-uniform "every active lane": the predicate's lane mask against exec.  Pass a single
+// compare: a predicate combined from several is materialised in a VGPR and compared back
+// (2 VALU per vote, seen in the empty-run loop's ISA), where a compare's mask is the ballot.
+__device__ __forceinline__ bool wave_all(bool p)
+{
+    return __builtin_amdgcn_ballot_w64(p) == __builtin_amdgcn_ballot_w64(true);
+}
+
 __device__ __forceinline__ bool first_active_lane()
 {
     return (threadIdx.x & 63u) == uint32_t(__ffsll((long long)__ballot(1)) - 1);
@@ -265,7 +273,7 @@ __device__ __forceinline__ bool test_cell(const KParams& P, float ox, float oy, 
         // registers and the records arrive through the scalar cache (s_load), off the
         // vector-memory path; results are the same ray/record pairs in the same order.
         const uint32_t kb0 = __builtin_amdgcn_readfirstlane(kb), ke0 = __builtin_amdgcn_readfirstlane(ke);
-        if (__all((kb == kb0) & (ke == ke0)))
+        if (wave_all(((kb ^ kb0) | (ke ^ ke0)) == 0u))
         {
             if constexpr ((VAR & kVarWaveClock) != 0)
                 if (first_active_lane()) wave_counters()[0] += ke0 - kb0;
@@ -619,7 +627,7 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, float ox, float
                 // and the same exits as one iteration per cell, with no cell word or test work.
                 // Uniform, so no lane waits on another's run; the run ends when the first lane's
                 // does.  (A lane inside a run has no hit and more == true, so done is false.)
-                if (__all(skip > 0))
+                if (wave_all(skip > 0))
                 {
                     do
                     {
@@ -634,7 +642,9 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, float ox, float
                         nct1 += a1_ ? dt1 : 0.0f;
                         nct2 += a2_ ? dt2 : 0.0f;
                         cell += a2_ ? cs2 : (a1_ ? cs1 : cs0);
-                    } while (__all((skip > 0) & more));
+                        // (skip > 0) & more as ONE integer compare (skip >= 0 here)
+                    } while (wave_all(((uint32_t(remp) & uint32_t(kRemGuards)) | (uint32_t(skip - 1) & 0x80000000u)) ==
+                                      0u));
                     done = !more;
                 }
             }
