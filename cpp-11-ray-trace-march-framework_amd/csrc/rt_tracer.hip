@@ -261,7 +261,9 @@ __device__ __forceinline__ bool test_cell(const KParams& P, float ox, float oy, 
     constexpr bool PRE = (VAR & kVarOriginPre) != 0 && TRI == RT_TRI_MOLLER_TRUMBORE;
     constexpr bool F = (VAR & kVarFastRcp) != 0;
     const rtd::f2v ra = {dx, dy}, rc = {dy, dz};   // the ray as the record test's register pairs
-    const float tb0 = __builtin_fminf(t, nct_ax);
+    // min(t, nct_ax) as a compare and select: neither is ever NaN (and -0 / +0 compare equal in
+    // every later '<'), and fminf would canonicalise both operands first (2 more VALU per cell)
+    const float tb0 = t < nct_ax ? t : nct_ax;
     // every accepted hit lowers tb strictly, so "some hit was taken" is tb < tb0; u, v and tri
     // are updated in place (the caller's values stand when nothing is taken)
     float tb = tb0;
@@ -273,7 +275,11 @@ __device__ __forceinline__ bool test_cell(const KParams& P, float ox, float oy, 
         // registers and the records arrive through the scalar cache (s_load), off the
         // vector-memory path; results are the same ray/record pairs in the same order.
         const uint32_t kb0 = __builtin_amdgcn_readfirstlane(kb), ke0 = __builtin_amdgcn_readfirstlane(ke);
-        if (wave_all(((kb ^ kb0) | (ke ^ ke0)) == 0u))
+        // one integer compare for the vote (the empty asm keeps the compiler from splitting it
+        // back into two equalities, which materialises the combined predicate in a VGPR)
+        uint32_t diff = (kb ^ kb0) | (ke ^ ke0);
+        asm volatile("" : "+v"(diff));
+        if (wave_all(diff == 0u))
         {
             if constexpr ((VAR & kVarWaveClock) != 0)
                 if (first_active_lane()) wave_counters()[0] += ke0 - kb0;
