@@ -87,7 +87,10 @@ constexpr uint32_t kDistBlock = 32;         // triangles per culling block of th
 // heavy-first plan (one per list version): blocks listed at each of the two priority levels,
 // the maximum block cost, the work items listed for the wide section (kVarWideHeavy) and the
 // sum of wave costs of the measured frame
-struct HfPlan { uint32_t cnt_hi, cnt_lo, maxc, cnt_w; unsigned long long sum; uint32_t cnt_w4, pad; };
+// sum_full: the sum of wave costs of the last measured frame that rendered every item one lane
+// per sample (the wide section's span estimate; carried over by the plans of other frames)
+struct HfPlan { uint32_t cnt_hi, cnt_lo, maxc, cnt_w; unsigned long long sum; uint32_t cnt_w4, pad;
+                unsigned long long sum_full; };
 
 struct KParams
 {
@@ -1057,11 +1060,15 @@ __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks)
     {
         c = reinterpret_cast<const uint4 *>(P.hf_cost)[b];                // kWavesPerWG == 4
         sum = (c.x >> 4) + (c.y >> 4) + (c.z >> 4) + (c.w >> 4);          // in 16-cycle units
-        if (P.wh_on && last.sum)
+        if (P.wh_on && !P.wh_wgs && last.sum_full)
         {
             // wide section: items above a fraction of the frame span estimated from the last
-            // measurement (sum of wave costs over the resident waves)
-            const uint64_t span = (last.sum << 4) / kHfSlots;
+            // measurement of every item one lane per sample (sum of wave costs over the resident
+            // waves).  New items are listed only from such frames (the first ones of a shape, the
+            // refresh frames): with the section running, the lane waves' costs shrink as items
+            // leave them, which pulled the span estimate down and listed ever more items
+            // (killeroo's rank of 4: 298 -> 587 items over 100 frames, measured).
+            const uint64_t span = (last.sum_full << 4) / kHfSlots;
             const uint32_t thr = max(P.wh_floor, uint32_t(min<uint64_t>(span * P.wh_alpha16 / 16u, 0xFFFFFFFFull)));
             const uint32_t thr4 = max(P.wh_floor, uint32_t(min<uint64_t>(span * P.wh_alpha16_4 / 16u, 0xFFFFFFFFull)));
             wmask = uint32_t(c.x > thr) | (uint32_t(c.y > thr) << 1) | (uint32_t(c.z > thr) << 2) |
@@ -1102,6 +1109,15 @@ __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks)
     {
         if (s_max) atomicMax(&P.hf_plan_out->maxc, s_max);
         if (s_sum) atomicAdd(&P.hf_plan_out->sum, s_sum);
+        if (P.wh_on)
+        {
+            if (!P.wh_wgs)
+            {
+                if (s_sum) atomicAdd(&P.hf_plan_out->sum_full, s_sum);
+            }
+            else if (blockIdx.x == 0u)
+                P.hf_plan_out->sum_full = last.sum_full;      // carried
+        }
         s_bhi = s_hi ? atomicAdd(&P.hf_plan_out->cnt_hi, s_hi) : 0u;
         s_blo = s_lo ? atomicAdd(&P.hf_plan_out->cnt_lo, s_lo) : 0u;
         s_bw = s_w ? atomicAdd(&P.hf_plan_out->cnt_w, s_w) : 0u;

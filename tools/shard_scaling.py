@@ -5,7 +5,9 @@ before the gather.  Per (scene, kernel, N, rank): median of HIP-event times arou
 render_shard_device (all kernels of the launch) over 8 reps after 3 warm-ups (heavy-first
 planning frames included).  pair_max_ms[k][N] = max over ranks of (Cornell + killeroo).
 
-    python3 tools/shard_scaling.py [kernel ...]      (default: 0 = AUTO, 0x100 = AUTO one-phase)
+    python3 tools/shard_scaling.py [--steady] [kernel ...]   (default: 0 = AUTO, 0x100 = lane kernel only)
+--steady: per-launch time of 32 back-to-back launches of the rank (bench.py's steady state, no
+per-launch events) instead of the median of single launches each between its own events.
 """
 import importlib.util
 import json
@@ -22,7 +24,8 @@ spec.loader.exec_module(rtm)
 torch.cuda.set_device(0)
 st = torch.cuda.current_stream()
 W, H, SPP = 1920, 1080, 4
-kernels = [int(k, 0) for k in sys.argv[1:]] or [0, 0x100]
+STEADY = "--steady" in sys.argv
+kernels = [int(k, 0) for k in sys.argv[1:] if k != "--steady"] or [0, 0x100]
 NS = (1, 2, 4, 8)
 res = {"per_rank": {}, "pair_max_ms": {}, "scene_max_ms": {}}
 for sid in (1, 8, 5):
@@ -33,14 +36,28 @@ for sid in (1, 8, 5):
             buf = torch.empty(rtm.shard_elems(W, H, n), dtype=torch.int32, device="cuda")
             for r in range(n):
                 ts = []
-                for rep in range(11):
-                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                    e0.record(st)
-                    g.render_shard_device(f, r, n, buf.data_ptr(), st.cuda_stream)
-                    e1.record(st)
-                    torch.cuda.synchronize()
-                    if rep >= 3:
-                        ts.append(e0.elapsed_time(e1))
+                if STEADY:
+                    # like bench.py: back-to-back launches of this rank's shard, one event pair
+                    # around a run of them (per-launch events cost ~10 us each), warm-ups first
+                    for _ in range(20):
+                        g.render_shard_device(f, r, n, buf.data_ptr(), st.cuda_stream)
+                    for rep in range(3):
+                        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                        e0.record(st)
+                        for _ in range(32):
+                            g.render_shard_device(f, r, n, buf.data_ptr(), st.cuda_stream)
+                        e1.record(st)
+                        torch.cuda.synchronize()
+                        ts.append(e0.elapsed_time(e1) / 32)
+                else:
+                    for rep in range(11):
+                        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                        e0.record(st)
+                        g.render_shard_device(f, r, n, buf.data_ptr(), st.cuda_stream)
+                        e1.record(st)
+                        torch.cuda.synchronize()
+                        if rep >= 3:
+                            ts.append(e0.elapsed_time(e1))
                 res["per_rank"][f"s{sid}_k{k:#x}_n{n}_r{r}"] = round(sorted(ts)[len(ts) // 2], 4)
             res["scene_max_ms"][f"s{sid}_k{k:#x}_n{n}"] = max(res["per_rank"][f"s{sid}_k{k:#x}_n{n}_r{r}"] for r in range(n))
         print(sid, k, {n: res["scene_max_ms"][f"s{sid}_k{k:#x}_n{n}"] for n in NS}, flush=True)
@@ -51,4 +68,4 @@ for k in kernels:
 print(json.dumps(res["pair_max_ms"]))
 os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
 lib = os.path.splitext(os.path.basename(os.environ.get("RT_TRACER_LIB", "librt_tracer.so")))[0]
-json.dump(res, open(os.path.join(ROOT, "gpurun_out", f"shard_scaling_{lib}.json"), "w"), indent=1)
+json.dump(res, open(os.path.join(ROOT, "gpurun_out", f"shard_scaling_{lib}{'_steady' if STEADY else ''}.json"), "w"), indent=1)
