@@ -2168,13 +2168,12 @@ int ensure_origin_terms(rt_scene *s, const KParams& P, hipStream_t st)
 
 // kVarWideHeavy thresholds: an item goes wide above max(floor, alpha16 / 16 x estimated span)
 // shader cycles; RT_WH_FLOOR / RT_WH_ALPHA16 override them (A/B sweeps)
-// (tools/wh_probe.py sweeps, profiles/r02m_wide_heavy_sweep.json: the floor keeps Cornell's
-// items in the lanes -- at 60000 cycles its rank of 8 lists ~900 items and doubles -- and the
-// span factor is 1x below 8 ranks, 2x from 8)
+// (tools/wh_probe.py / env_probe.py sweeps: the floor keeps Cornell's items in the lanes -- at
+// 60000 cycles its rank of 8 lists ~900 items and doubles; the span factor 2x is best at 2, 4
+// and 8 ranks once items are listed from full frames only, profiles/r02t_wide_heavy_alpha_*)
 constexpr uint32_t kWhFloor = 100000;
 constexpr uint32_t kWhRefresh = 128;        // frames between refresh frames (a multiple of kHfPeriod)
-constexpr uint32_t kWhAlpha16 = 16;
-constexpr uint32_t kWhAlpha16Wide = 32;
+constexpr uint32_t kWhAlpha16 = 32;
 uint32_t env_tunable(const char *name, uint32_t dflt)
 {
     const char *e = std::getenv(name);
@@ -2258,7 +2257,7 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
         P.wh_refresh = (c->frames - 1u) % kWhRefresh == 0u;       // frames counts this one
         P.wh_wgs = P.wh_refresh ? 0u : (units + kWavesPerWG - 1u) / kWavesPerWG;
         P.wh_floor = env_tunable("RT_WH_FLOOR", kWhFloor);
-        const uint32_t alpha = env_tunable("RT_WH_ALPHA16", P.nranks >= 8u ? kWhAlpha16Wide : kWhAlpha16);
+        const uint32_t alpha = env_tunable("RT_WH_ALPHA16", kWhAlpha16);
         // spp <= 4: 16 lanes per sample (a 4-lane tier below it only on request, measured no
         // gain); spp 8-16: a pixel's samples fill a wave at 4 lanes each, so every item takes
         // the 4-lane tier

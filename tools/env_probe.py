@@ -28,6 +28,7 @@ ap.add_argument("--kernel", default="0")
 ap.add_argument("--reps", type=int, default=16)
 ap.add_argument("--warm", type=int, default=12)
 ap.add_argument("--rounds", type=int, default=2)
+ap.add_argument("--steady", action="store_true", help="back-to-back launches (bench-like timing)")
 ap.add_argument("--ranks", default="all", help="'all' or a comma list of ranks to time")
 ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "env_probe.json"))
 a = ap.parse_args()
@@ -46,13 +47,26 @@ for sid in [int(x) for x in a.scenes.split(",")]:
             for name, env in arms.items():
                 for k in keys:
                     os.environ.pop(k, None)
-                os.environ.update(env)
+                os.environ.update({k: v for k, v in env.items() if not k.startswith("_")})
                 worst = 0.0
                 for r in ranks:
                     g = rtm.GpuScene(hs, 0)
-                    f = g.frame(W, H, SPP, kernel=int(a.kernel, 0))
+                    f = g.frame(W, H, SPP, kernel=int(env.get("_kernel", a.kernel), 0))
                     ts = []
-                    for rep in range(a.warm + a.reps):
+                    if a.steady:
+                        # bench-like: back-to-back launches, one event pair around 16 of them
+                        for _ in range(a.warm):
+                            g.render_shard_device(f, r, n, buf.data_ptr(), st.cuda_stream)
+                        torch.cuda.synchronize()
+                        for rep in range(max(3, a.reps // 4)):
+                            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                            e0.record(st)
+                            for _ in range(16):
+                                g.render_shard_device(f, r, n, buf.data_ptr(), st.cuda_stream)
+                            e1.record(st)
+                            torch.cuda.synchronize()
+                            ts.append(e0.elapsed_time(e1) / 16)
+                    for rep in range(0 if a.steady else a.warm + a.reps):
                         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                         e0.record(st)
                         g.render_shard_device(f, r, n, buf.data_ptr(), st.cuda_stream)
