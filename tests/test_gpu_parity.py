@@ -304,13 +304,16 @@ def test_shard_partition_dense_scenes(golden, scenes, sid, nranks):
 
 
 @pytest.mark.parametrize("sid,nranks,kernel", [(8, 8, 0), (5, 4, 0), (8, 2, 0x200), (5, 1, 0x200), (8, 4, 0)])
-def test_wide_heavy_shard_frames(golden, scenes, sid, nranks, kernel):
+def test_wide_heavy_shard_frames(golden, scenes, sid, nranks, kernel, monkeypatch):
     """RT_KERNEL_FLAG_WIDE_HEAVY over consecutive frames of every rank: frames 0-1 render one
     lane per sample and measure, later frames trace the listed heavy items on the side stream
     (16 lanes per sample); every frame's shard equals the one-lane-per-sample shard, and the
     partition reassembles into the reference frame.  kernel 0: AUTO's own policy (>= 2 ranks of
     a dense scene), 0x200: the flag forced (also on a whole frame)."""
     import torch
+    if nranks == 1:
+        # a whole frame's span is long: at the default threshold (2x span) nothing is listed
+        monkeypatch.setenv("RT_WH_ALPHA16", "4")
     hs, gs = scenes(sid)
     W, H = 1920, 1080
     f = gs.frame(W, H, 4, kernel=kernel)
