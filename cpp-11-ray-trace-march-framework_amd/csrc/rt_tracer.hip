@@ -109,6 +109,8 @@ struct KParams
     uint32_t max_steps;         // bound of the CSR-offset walk: no DDA walk is longer than dx+dy+dz
     const uint32_t *off;
     const uint32_t *cellw;      // packed cell words (start << 11 | count) or null
+    const uint32_t *cellwo;     // the dist-skip walks' words: 8 ray-octant copies, or = cellw
+    uint32_t oct_stride;        // words per octant copy (ncells), 0 when cellwo == cellw
     const float4 *refs;
     const float4 *frefs;        // per camera origin (kVarOriginPre), 3 float4 per reference
     const float4 *shade;
@@ -579,6 +581,14 @@ __device__ __forceinline__ bool dda_setup(const KParams& P, float ox, float oy, 
     return true;
 }
 
+// Offset of the ray's octant copy in P.cellwo (0 when there is one copy).  An axis with d == 0
+// never steps, so either sign is right for it (-0.0 counts as +).
+__device__ __forceinline__ int oct_offset(const KParams& P, float dx, float dy, float dz)
+{
+    const uint32_t o = uint32_t(dx < 0.0f) | (uint32_t(dy < 0.0f) << 1) | (uint32_t(dz < 0.0f) << 2);
+    return int(o * P.oct_stride);
+}
+
 // grid.cpp:159-281 Grid::Intersect (NEW_GRID_TRAVERSAL), axis arrays unrolled into scalars
 // so nothing is runtime-indexed (no scratch).  Counters are compiled in only for records.
 template <bool STATS, int TRI, int VAR>
@@ -603,15 +613,17 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, float ox, float
         // iterations whatever nct holds.
         int skip = 0;
         int remp = rem0 | (rem1 << 11) | (rem2 << 22);      // kVarPackedRem only
+        const int coff = oct_offset(P, dx, dy, dz);
+        cell += coff;
         for (;;)
         {
-            if (STATS) { voxel = uint32_t(cell); steps++; }
+            if (STATS) { voxel = uint32_t(cell - coff); steps++; }
             uint32_t kb = 0, ke = 0;
             float nct_ax;
             bool more;
             if (skip == 0)
             {
-                const uint32_t w = P.cellw[uint32_t(cell)];
+                const uint32_t w = P.cellwo[uint32_t(cell)];
                 const uint32_t cnt = w & 2047u;
                 kb = w >> 11;
                 ke = kb + cnt;
@@ -1258,6 +1270,7 @@ __device__ __forceinline__ void wide_trace(const KParams& P, uint32_t k, uint32_
             {
                 int skip = 0;
                 int remp = rem0 | (rem1 << 11) | (rem2 << 22);
+                cell += oct_offset(P, dx, dy, dz);
                 for (;;)
                 {
                     uint32_t kb = 0u, ke = 0u;
@@ -1265,7 +1278,7 @@ __device__ __forceinline__ void wide_trace(const KParams& P, uint32_t k, uint32_
                     bool more;
                     if (skip == 0)
                     {
-                        const uint32_t w = P.cellw[uint32_t(cell)];
+                        const uint32_t w = P.cellwo[uint32_t(cell)];
                         const uint32_t cnt = w & 2047u;
                         kb = w >> 11;
                         ke = kb + cnt;
@@ -1980,7 +1993,7 @@ struct rt_scene
     uint32_t dims[3] = { 0, 0, 0 };
     float bmin[3], bmax[3], cw = 0, icw = 0;
     uint32_t ncells = 0, nrefs = 0, ntris = 0, max_cell_refs = 0;
-    uint32_t *d_off = nullptr, *d_cellw = nullptr;
+    uint32_t *d_off = nullptr, *d_cellw = nullptr, *d_cellwo = nullptr, oct_stride = 0;
     float4 *d_refs = nullptr, *d_shade = nullptr, *d_facen = nullptr, *d_frefs = nullptr;
     float4 *d_trimt = nullptr, *d_tridist = nullptr, *d_distblk = nullptr;
     uint32_t ndist_blk = 0;
@@ -2125,6 +2138,8 @@ void frame_params(const rt_scene *s, const rt_frame *f, KParams& P)
     P.max_steps = s->dims[0] + s->dims[1] + s->dims[2] + 3;
     P.off = s->d_off;
     P.cellw = s->d_cellw;
+    P.cellwo = s->d_cellwo ? s->d_cellwo : s->d_cellw;
+    P.oct_stride = s->d_cellwo ? s->oct_stride : 0u;
     P.refs = s->d_refs;
     P.frefs = s->d_frefs;
     P.shade = s->d_shade;
@@ -2642,7 +2657,7 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
         facen[i] = make_float4(t.n[0], t.n[1], t.n[2], 0.0f);
     }
     // Packed cell ranges: start < 2^21 and count < 2^11 for every cell -> one load per DDA step
-    std::vector<uint32_t> cellw;
+    std::vector<uint32_t> cellw, cellwo;
     bool packable = nr < (1u << 21);
     for (uint32_t c = 0; c < nc && packable; c++) packable = g.cell_offsets[c + 1] - g.cell_offsets[c] < 2048u;
     if (packable)
@@ -2680,6 +2695,44 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
             const uint32_t cnt = g.cell_offsets[c + 1] - g.cell_offsets[c];
             cellw[c] = cnt ? ((g.cell_offsets[c] << 11) | cnt)
                            : (std::min<uint32_t>(dist[c] == 0xFFFFFFFFu ? 0x1FFFFFu : dist[c], 0x1FFFFFu) << 11);
+        }
+        // Per ray octant (sign of dx, dy, dz) a directional bound: D(c) = the side of the largest
+        // empty cube with corner c that extends along the octant's signs (cells outside the grid
+        // count as empty).  j steps of a walk in that octant move each coordinate by 0..j in the
+        // octant's direction, so the next D-1 cells are empty -- the same contract as the L-inf
+        // word, and D >= the L-inf distance.  D(c) = 1 + min of D over the 7 forward neighbours
+        // (the 3-D largest-square recurrence).  RT_OCT_DIST=0 keeps the L-inf words (A/B arm).
+        const char *oe = std::getenv("RT_OCT_DIST");
+        if (!(oe && oe[0] == '0'))
+        {
+            constexpr uint32_t kInf = 0x1FFFFFu;
+            cellwo.resize(size_t(8) * nc);
+            std::vector<uint32_t> D(nc);
+            for (uint32_t o = 0; o < 8; o++)
+            {
+                const int sx = (o & 1) ? -1 : 1, sy = (o & 2) ? -1 : 1, sz = (o & 4) ? -1 : 1;
+                auto at = [&](int x, int y, int z) -> uint32_t {
+                    if (x < 0 || y < 0 || z < 0 || x >= int(dxs) || y >= int(dys) || z >= int(dzs)) return kInf;
+                    return D[uint32_t(x) + uint32_t(z) * dxs + uint32_t(y) * dxs * dzs];
+                };
+                for (int iy = 0; iy < int(dys); iy++)
+                    for (int iz = 0; iz < int(dzs); iz++)
+                        for (int ix = 0; ix < int(dxs); ix++)
+                        {
+                            // visit forward neighbours first: against the octant's direction
+                            const int x = sx > 0 ? int(dxs) - 1 - ix : ix;
+                            const int y = sy > 0 ? int(dys) - 1 - iy : iy;
+                            const int z = sz > 0 ? int(dzs) - 1 - iz : iz;
+                            const uint32_t c = uint32_t(x) + uint32_t(z) * dxs + uint32_t(y) * dxs * dzs;
+                            if (g.cell_offsets[c + 1] != g.cell_offsets[c]) { D[c] = 0; continue; }
+                            uint32_t m = kInf;
+                            for (int n = 1; n < 8; n++)
+                                m = std::min(m, at(x + ((n & 1) ? sx : 0), y + ((n & 2) ? sy : 0), z + ((n & 4) ? sz : 0)));
+                            D[c] = std::min(kInf, m + 1);
+                        }
+                for (uint32_t c = 0; c < nc; c++)
+                    cellwo[size_t(o) * nc + c] = (cellw[c] & 2047u) ? cellw[c] : (D[c] << 11);
+            }
         }
     }
     for (uint32_t c = 0; c < nc; c++)
@@ -2764,11 +2817,17 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
     {
         RT_HIP(hipMalloc(&s->d_cellw, sizeof(uint32_t) * nc));
         RT_HIP(hipMemcpy(s->d_cellw, cellw.data(), sizeof(uint32_t) * nc, hipMemcpyHostToDevice));
+        if (!cellwo.empty())
+        {
+            RT_HIP(hipMalloc(&s->d_cellwo, sizeof(uint32_t) * cellwo.size()));
+            RT_HIP(hipMemcpy(s->d_cellwo, cellwo.data(), sizeof(uint32_t) * cellwo.size(), hipMemcpyHostToDevice));
+            s->oct_stride = nc;
+        }
     }
     s->device_bytes = sizeof(uint32_t) * (nc + 1) +
                       sizeof(float4) * (refs.size() + nfrefs + shade.size() + facen.size() + trimt.size() +
                                         tridist.size() + distblk.size()) +
-                      sizeof(uint32_t) * cellw.size();
+                      sizeof(uint32_t) * (cellw.size() + cellwo.size());
     RT_HIP(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
     RT_HIP(hipEventCreateWithFlags(&s->ev1, hipEventDisableTiming));
 
@@ -2790,6 +2849,7 @@ int rt_scene_destroy(rt_scene *s)
         (void)hipFree(s->d_shade);
         (void)hipFree(s->d_facen);
         (void)hipFree(s->d_cellw);
+        (void)hipFree(s->d_cellwo);
         (void)hipFree(s->d_trimt);
         (void)hipFree(s->d_tridist);
         (void)hipFree(s->d_distblk);
