@@ -137,6 +137,38 @@ def test_full_frame_1080p4(golden, scenes, sid):
     assert hashlib.sha256(hit_ids(recs).tobytes()).hexdigest() == g["hits_sha256"]
 
 
+def test_octant_words_arms(golden, monkeypatch):
+    """The empty-run words are chosen at scene creation: RT_OCT_DIST=0 (one L-inf word per
+    cell) and the default octant copies both render the reference's bytes on every scene, and
+    their shards of 8 ranks (where AUTO adds the wide section on dense scenes) agree."""
+    import torch
+    arm = "0"
+    for sid in range(10):
+        hs = rtm.HostScene.load(sid)
+        monkeypatch.setenv("RT_OCT_DIST", arm)
+        ga = rtm.GpuScene(hs, 0)
+        monkeypatch.delenv("RT_OCT_DIST")
+        gb = rtm.GpuScene(hs, 0)
+        try:
+            want = golden["frames_1080p4"][str(sid)]["bgra_sha256"]
+            for g in (ga, gb):
+                img = g.render_frame(g.frame(1920, 1080, 4))
+                assert hashlib.sha256(img.tobytes()).hexdigest() == want, (sid, arm)
+            e = rtm.shard_elems(1920, 1080, 8)
+            a = torch.zeros(e, dtype=torch.int32, device="cuda")
+            b = torch.zeros(e, dtype=torch.int32, device="cuda")
+            st = torch.cuda.current_stream().cuda_stream
+            for r in (0, 7):
+                ga.render_shard_device(ga.frame(1920, 1080, 4), r, 8, a.data_ptr(), st)
+                gb.render_shard_device(gb.frame(1920, 1080, 4), r, 8, b.data_ptr(), st)
+                torch.cuda.synchronize()
+                assert torch.equal(a, b), (sid, arm, r)
+        finally:
+            ga.close()
+            gb.close()
+            hs.close()
+
+
 @pytest.mark.parametrize("sid", range(10))
 def test_full_frame_compaction_kernel(golden, scenes, sid):
     """RT_KERNEL_COMPACT (wavefront active-ray compaction) at refill thresholds 1 (refill as soon
