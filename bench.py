@@ -155,9 +155,11 @@ def valu_roofline(rtm, kernel_ms, args, world, algorithmic):
         return roof
     with open(path) as fh:
         c = json.load(fh)
-    src = rtm.kernel_source_hash()
+    # the hash baked into the LOADED library at build time, not the files on disk: a stale
+    # prebuilt librt_tracer.so cannot pass with counters of newer sources
+    src = rtm.library_build_hash()
     if c.get("source_hash") != src:
-        roof["counters"] = f"refused: counters are for sources {c.get('source_hash')}, timed build is {src}"
+        roof["counters"] = f"refused: counters are for sources {c.get('source_hash')}, timed library is {src}"
         return roof
     if c.get("workload") != want:
         roof["counters"] = f"refused: counters are for {c.get('workload')}, not {want}"

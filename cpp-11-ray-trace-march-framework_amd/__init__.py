@@ -40,13 +40,8 @@ MESH_DATA_DIR = os.path.join(REPO, "data", "meshes")     # cornell_box_quads.txt
 
 RT_TRI_MOLLER_TRUMBORE, RT_TRI_BARYCENTRIC = 0, 1
 RT_KERNEL_AUTO, RT_KERNEL_LANES, RT_KERNEL_PIXEL_LOOP, RT_KERNEL_COMPACT = 0, 1, 2, 3
-RT_KERNEL_WIDE = 5
 RT_KERNEL_KIND_MASK = 0x07
-RT_KERNEL_FLAG_CENTER_OUT = 0x10
-RT_KERNEL_FLAG_STATIC_ORDER = 0x20
-RT_KERNEL_FLAG_WIDE16 = 0x40
 RT_KERNEL_FLAG_LDS_CELLS = 0x80
-RT_KERNEL_FLAG_ONE_PHASE = 0x100
 RT_KERNEL_FLAG_WIDE_HEAVY = 0x200
 RT_KERNEL_FLAG_EXHAUSTIVE = 0x8000
 RT_KERNEL_FLAG_WAVE_CLOCK = 0x400000
@@ -66,7 +61,7 @@ TRACER_SYMBOLS = [
     "rt_debug_rcp_check", "rt_debug_wave_clocks", "rt_debug_heavy_first", "rt_debug_wide_items", "rt_scene_set_timing",
     "rt_sample_table", "rt_last_error", "rt_abi_version", "rt_grid_build", "rt_grid_free",
     "rt_scene_create_from_mesh", "rt_kernel_times", "rt_render_frame_host", "rt_frame_host_wait", "rt_host_alloc",
-    "rt_host_free",
+    "rt_host_free", "rt_render_hits_device", "rt_scene_info_get", "rt_build_hash",
 ]
 HOST_SYMBOLS = [
     "rth_scene_load", "rth_scene_from_mesh", "rth_scene_free", "rth_scene_desc",
@@ -124,6 +119,13 @@ class SceneStats(ctypes.Structure):
                 ("empty_cells", c_u32), ("grid_build_s", ctypes.c_double)]
 
 
+class SceneInfo(ctypes.Structure):
+    _fields_ = [("octant_words", c_u32), ("packed_cells", c_u32), ("rcp_safe", c_u32), ("pack_ok", c_u32),
+                ("max_cell_refs", c_u32), ("hf_floor", c_u32), ("hf_min_blocks", c_u32), ("wh_floor", c_u32),
+                ("wh_alpha16", c_u32), ("wh_auto_refs", c_u32), ("hf_contexts", c_u32),
+                ("hf_evictions", ctypes.c_uint64), ("device_bytes", ctypes.c_uint64)]
+
+
 SAMPLE_REC_DTYPE = np.dtype([("hit", "<u4"), ("tri", "<u4"), ("voxel", "<u4"), ("steps", "<u4"),
                              ("tests", "<u4"), ("t", "<f4"), ("u", "<f4"), ("v", "<f4"),
                              ("r", "<f4"), ("g", "<f4"), ("b", "<f4"), ("pad", "<u4")])
@@ -164,6 +166,10 @@ def tracer_lib():
             L.rt_host_free.argtypes = [vp]
         L.rt_shard_elems.argtypes = [c_u32, c_u32, c_u32, ctypes.POINTER(ctypes.c_uint64)]
         L.rt_render_shard_device.argtypes = [vp, ctypes.POINTER(Frame), c_u32, c_u32, vp, vp]
+        if hasattr(L, "rt_render_hits_device"):      # ABI 5
+            L.rt_render_hits_device.argtypes = [vp, ctypes.POINTER(Frame), c_u32, c_u32, vp, vp, vp]
+            L.rt_scene_info_get.argtypes = [vp, ctypes.POINTER(SceneInfo)]
+            L.rt_build_hash.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
         L.rt_unshard_device.argtypes = [c_u32, c_u32, c_u32, vp, vp, vp]
         L.rt_last_kernel_ms.argtypes = [vp, ctypes.POINTER(c_f32)]
         L.rt_trace_samples.argtypes = [vp, ctypes.POINTER(Frame), c_u32, c_u32, c_u32, c_u32, vp]
@@ -243,6 +249,15 @@ def _ptr(a):
 
 def scene_path(scene_id):
     return os.path.join(SCENE_DIR, f"scene{scene_id}.rtscene")
+
+
+def library_build_hash():
+    """The kernel-source hash baked into the LOADED librt_tracer.so at build time (csrc/Makefile);
+    equal to kernel_source_hash() when the library was built from the sources on disk."""
+    L = tracer_lib()
+    buf = ctypes.create_string_buffer(64)
+    _check(L.rt_build_hash(buf, 64), L, "rt_build_hash")
+    return buf.value.decode()
 
 
 def device_count():
@@ -525,6 +540,21 @@ class GpuScene:
         _check(L.rt_render_shard_device(self._h, ctypes.byref(frame), rank, nranks,
                                         ctypes.c_void_p(d_ptr), ctypes.c_void_p(stream)), L,
                "rt_render_shard_device")
+
+    def render_hits_device(self, frame, rank, nranks, d_out, d_hits, stream=0):
+        """The frame (nranks 1) or a rank's shard, through the same launch path as
+        render_frame_device / render_shard_device, plus per-sample hit triangles into
+        d_hits[(y*W + x)*spp + s] (0xFFFFFFFF on a miss)."""
+        L = tracer_lib()
+        _check(L.rt_render_hits_device(self._h, ctypes.byref(frame), rank, nranks, ctypes.c_void_p(d_out),
+                                       ctypes.c_void_p(d_hits), ctypes.c_void_p(stream)), L, "rt_render_hits_device")
+
+    def info(self):
+        """rt_scene_info: what rt_scene_create chose and the tunables it read (dict)."""
+        L = tracer_lib()
+        i = SceneInfo()
+        _check(L.rt_scene_info_get(self._h, ctypes.byref(i)), L, "rt_scene_info_get")
+        return {k: getattr(i, k) for k, _ in SceneInfo._fields_}
 
     def wave_clocks(self):
         """Per work item of the last RT_KERNEL_FLAG_WAVE_CLOCK launch: {start, end} s_memtime,

@@ -74,7 +74,6 @@ constexpr int kVarWaveClock = 32768;        // RT_KERNEL_FLAG_WAVE_CLOCK: per-it
 constexpr int kVarUniform = 65536;          // scalar loop for wave-uniform cell lists
 constexpr int kVarLdsCells = 262144;        // RT_KERNEL_FLAG_LDS_CELLS: long uniform lists staged in LDS
 constexpr int kVarWideHeavy = 524288;       // RT_KERNEL_FLAG_WIDE_HEAVY: heavy items traced wide at the start
-constexpr int kVarCenterOut = 1048576;      // RT_KERNEL_FLAG_CENTER_OUT: XCD row turns from the middle out
 // AUTO's traversal: every feature above that is exact for every scene ...
 constexpr int kVarAutoCore = kVarWaveGate | kVarDistSkip | kVarOriginPre | kVarXcdBands | kVarUniform;
 // ... plus the two that need a scene property (rt_scene::rcp_safe, rt_scene::pack_ok)
@@ -89,8 +88,7 @@ constexpr uint32_t kDistBlock = 32;         // triangles per culling block of th
 // sum of wave costs of the measured frame
 // sum_full: the sum of wave costs of the last measured frame that rendered every item one lane
 // per sample (the wide section's span estimate; carried over by the plans of other frames)
-struct HfPlan { uint32_t cnt_hi, cnt_lo, maxc, cnt_w; unsigned long long sum; uint32_t cnt_w4, pad;
-                unsigned long long sum_full; };
+struct HfPlan { uint32_t cnt_hi, cnt_lo, maxc, cnt_w; unsigned long long sum; unsigned long long sum_full; };
 
 struct KParams
 {
@@ -151,25 +149,26 @@ struct KParams
     uint32_t *hf_ticket;        // k_hf_plan's finished-workgroup count (the last one marks)
                                 // (a wide item: the sum over its waves)
     // wide section (kVarWideHeavy; wh_on == 0: off).  k_render_wh's wh_wgs workgroups trace the
-    // work items the current plan lists as heavy (wh_list_in, plan->cnt_w of them), G lanes per
-    // sample, and the lane waves skip items whose wh_mark_in == hf_ver; with wh_wgs == 0 (no
-    // list seen yet, or a refresh frame) the lane waves render every item.  k_hf_plan lists an
-    // item when its lane-mode cost passes max(wh_floor, wh_alpha16 / 16 x the estimated frame
-    // span), and keeps the current plan's items (their cost words still hold the lane-mode cost
-    // of the last frame that measured them) except in a refresh frame.
-    uint32_t wh_on, wh_wgs, wh_refresh;
+    // work items the current plan lists as heavy (wh_list_in, plan->cnt_w of them), wh_g lanes
+    // per sample (16 at spp <= 4, 4 at spp 8-16), and the lane waves skip items whose
+    // wh_mark_in == hf_ver; with wh_wgs == 0 (no list seen yet, or a refresh frame) the lane
+    // waves render every item.  k_hf_plan lists an item when its lane-mode cost passes
+    // max(wh_floor, wh_alpha16 / 16 x the estimated frame span), and keeps the current plan's
+    // items (their cost words still hold the lane-mode cost of the last frame that measured
+    // them) except in a refresh frame.
+    uint32_t wh_on, wh_wgs, wh_refresh, wh_g;
     uint32_t wh_floor, wh_alpha16;
-    uint32_t wh_alpha16_4;      // items between max(floor, wh_alpha16_4 / 16 x span) and the 16-lane
-                                // threshold go wide 4 lanes per sample (second list, wh_list + kWhMax)
     const uint32_t *wh_mark_in;
     uint32_t *wh_mark_out;
     const uint32_t *wh_list_in;
     uint32_t *wh_list_out;
-    uint32_t *wh_host_cnt;      // host-mapped: the newest plan's {cnt_w, cnt_w4} (sizes the next launches)
+    uint32_t *wh_host_cnt;      // host-mapped: the newest plan's cnt_w (sizes the next launches)
     // output
     uint32_t *out;
     uint32_t pitch;             // frame mode: words per row of out
     uint32_t shard_mode;        // 1: out[local_tile * 256 + ty*16 + tx]
+    uint32_t *hits;             // rt_render_hits_device: per-sample hit triangle, [(y*W + x)*spp + s]
+                                // (read after the walk through late_params; NULL in the plain calls)
     rt_sample_rec *recs;        // debug kernel only
     uint32_t rec_x0, rec_y0, rec_w, rec_h;
 };
@@ -831,10 +830,11 @@ __device__ __forceinline__ bool ray_march(const KParams& P, float ox, float oy, 
     return false;
 }
 
-// renderer.cpp:88-122: one sample -> its colour contribution
+// renderer.cpp:88-122: one sample -> its colour contribution; hit_tri = the hit triangle
+// (Grid::Intersect's tri_idx, renderer.cpp:105) or kNoTri
 template <bool STATS, int TRI, int VAR>
 __device__ __forceinline__ void trace_sample(const KParams& P, uint32_t px, uint32_t py, uint32_t s, float& cr,
-                                             float& cg, float& cb, rt_sample_rec *rec)
+                                             float& cg, float& cb, uint32_t& hit_tri, rt_sample_rec *rec)
 {
     const float2 so = P.smp[s];
     float dx, dy, dz;
@@ -871,6 +871,7 @@ __device__ __forceinline__ void trace_sample(const KParams& P, uint32_t px, uint
         const float m = float(py) / float(Q.H);                  // renderer.cpp:121
         cr = cg = cb = m;
     }
+    hit_tri = hit ? tri : rtd::kNoTri;
     if (STATS)
     {
         rec->hit = hit;
@@ -955,13 +956,17 @@ __device__ __forceinline__ void process_item(const KParams& P, uint32_t item)
     item = __builtin_amdgcn_readfirstlane(item);
     const uint32_t lane = threadIdx.x & 63u;
     float cr = 0.0f, cg = 0.0f, cb = 0.0f;
+    uint32_t hit_tri = rtd::kNoTri;
     {
         const ItemCoord ic = item_coord(P, item, lane);
         if (ic.valid)
-            trace_sample<false, TRI, VAR>(P, ic.x, ic.y, ic.s, cr, cg, cb, nullptr);
+            trace_sample<false, TRI, VAR>(P, ic.x, ic.y, ic.s, cr, cg, cb, hit_tri, nullptr);
     }
     const KParams& Q = late_params(P);
     const ItemCoord ic = item_coord(Q, item, lane);
+    // rt_render_hits_device only: the sample's hit triangle, after the walk (a scalar test of a
+    // kernel parameter; the walk above is the same code whatever the pointer holds)
+    if (Q.hits && ic.valid) Q.hits[(size_t(ic.y) * Q.W + ic.x) * Q.spp + ic.s] = hit_tri;
     const uint32_t base = lane & ~(Q.spp - 1u);
     float sr = 0.0f, sg = 0.0f, sb = 0.0f;
     for (uint32_t k = 0; k < Q.spp; k++)
@@ -987,50 +992,20 @@ __device__ __forceinline__ void process_item(const KParams& P, uint32_t item)
 // A bijection on [0, nblocks) for any grid size (the tail past whole 8-turn rounds keeps its
 // order); on a device with another XCD count only the locality changes.
 constexpr uint32_t kXcds = 8;
-constexpr uint32_t kWideG = 4;              // RT_KERNEL_WIDE: lanes per sample
-constexpr uint32_t kWhAutoRefs = 128;       // AUTO: wide section for shards of scenes with a cell this dense
-// Heavy-first order (AUTO): front-section capacity, smallest launch it is used for, and the
-// floor of the heavy threshold in shader cycles (~40 us at 2.4 GHz)
-#ifndef RT_HF_FRONT
-#define RT_HF_FRONT 1024
-#endif
-#ifndef RT_HF_SHIFT
-#define RT_HF_SHIFT 2
-#endif
-#ifndef RT_HF_FLOOR
-#define RT_HF_FLOOR 100000
-#endif
-constexpr uint32_t kHfFrontMax = RT_HF_FRONT;   // blocks (4 waves each): half the chip's wave slots
-constexpr uint32_t kWhMax = 4096;
-#ifndef RT_WH_PF
-#define RT_WH_PF false                      // kVarWideHeavy: one-ahead record prefetch in the wide waves
-#endif           // kVarWideHeavy: work items the wide section can list
-#ifndef RT_HF_MIN_BLOCKS
-#define RT_HF_MIN_BLOCKS 4096
-#endif
-constexpr uint32_t kHfMinBlocks = RT_HF_MIN_BLOCKS;   // below ~2 rounds of workgroups every block starts early
-constexpr uint32_t kHfFloor = RT_HF_FLOOR;
-constexpr uint32_t kHfShift = RT_HF_SHIFT;  // heavy: cost > last max >> kHfShift; very heavy: >> 1
-#ifndef RT_HF_PERIOD
-#define RT_HF_PERIOD 16
-#endif
-constexpr uint32_t kHfPeriod = RT_HF_PERIOD;   // a plan from every kHfPeriod-th frame of a launch shape
+// Heavy-first order (AUTO): front-section capacity and the shape of the heavy threshold.  The
+// floor and the smallest launch it is used for are per-scene tunables (rt_scene, read once at
+// creation).
+constexpr uint32_t kHfFrontMax = 1024;      // blocks (4 waves each): half the chip's wave slots
+constexpr uint32_t kWhMax = 4096;           // kVarWideHeavy: work items the wide section can list
+constexpr uint32_t kHfShift = 2;            // heavy: cost > last max >> kHfShift; very heavy: >> 1
+constexpr uint32_t kHfPeriod = 16;          // a plan from every kHfPeriod-th frame of a launch shape
 // A plan lists blocks only when the slowest block is a real tail: its cost (one wave's
 // duration) above kHfTail / 16 of the estimated frame span, sum of wave costs / resident waves
 constexpr uint32_t kHfTail = 6;
 constexpr uint32_t kHfSlots = 256u * 4u * 8u;   // resident waves: 256 CUs x 4 SIMDs x 8
-constexpr int kHfCtxs = 4;                  // launch shapes remembered per scene
+constexpr int kHfCtxs = 16;                 // launch shapes remembered per scene (a process driving
+                                            // the 8 ranks of two scenes' shards keeps all of them)
 
-// Center-out row order (kVarCenterOut): dispatch turn j takes row m, m - 1, m + 1, m - 2, ...
-// (m = R / 2), a bijection on [0, R).  A camera frames its subject, so the dense rows -- whose
-// waves are the launch's longest -- start first instead of mid-launch.
-__device__ __forceinline__ uint32_t center_out_row(uint32_t j, uint32_t R)
-{
-    const uint32_t m = R / 2u;
-    return (j & 1u) ? m - (j + 1u) / 2u : m + j / 2u;
-}
-
-template <bool CENTER = false>
 __device__ __forceinline__ uint32_t xcd_band_block(uint32_t b, uint32_t nb, uint32_t chunk)
 {
     if (chunk == 0u)
@@ -1043,7 +1018,7 @@ __device__ __forceinline__ uint32_t xcd_band_block(uint32_t b, uint32_t nb, uint
     if (b >= full) return b;
     const uint32_t x = b % kXcds, i = b / kXcds;
     const uint32_t row = (i / chunk) * kXcds + x;
-    return (CENTER ? center_out_row(row, full / chunk) : row) * chunk + i % chunk;
+    return row * chunk + i % chunk;
 }
 
 // Heavy-first planning, after a measured frame's render kernel on its stream: per block the cost
@@ -1056,17 +1031,17 @@ __device__ __forceinline__ uint32_t xcd_band_block(uint32_t b, uint32_t nb, uint
 // cost milliseconds, measured).
 __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks)
 {
-    __shared__ uint32_t s_max, s_hi, s_lo, s_w, s_w4, s_bhi, s_blo, s_bw, s_bw4, s_last;
+    __shared__ uint32_t s_max, s_hi, s_lo, s_w, s_bhi, s_blo, s_bw, s_last;
     __shared__ unsigned long long s_sum;
     const uint32_t b = blockIdx.x * kWG + threadIdx.x;
     if (threadIdx.x == 0u)
     {
-        s_max = s_hi = s_lo = s_w = s_w4 = 0u;
+        s_max = s_hi = s_lo = s_w = 0u;
         s_sum = 0ull;
     }
     __syncthreads();
     const HfPlan last = *P.hf_plan_in;
-    uint32_t cost = 0u, sum = 0u, wmask = 0u, w4mask = 0u;     // w4mask: the 4-lane tier
+    uint32_t cost = 0u, sum = 0u, wmask = 0u;
     uint4 c = make_uint4(0u, 0u, 0u, 0u);
     if (b < nblocks)
     {
@@ -1082,40 +1057,29 @@ __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks)
             // (killeroo's rank of 4: 298 -> 587 items over 100 frames, measured).
             const uint64_t span = (last.sum_full << 4) / kHfSlots;
             const uint32_t thr = max(P.wh_floor, uint32_t(min<uint64_t>(span * P.wh_alpha16 / 16u, 0xFFFFFFFFull)));
-            const uint32_t thr4 = max(P.wh_floor, uint32_t(min<uint64_t>(span * P.wh_alpha16_4 / 16u, 0xFFFFFFFFull)));
             wmask = uint32_t(c.x > thr) | (uint32_t(c.y > thr) << 1) | (uint32_t(c.z > thr) << 2) |
                     (uint32_t(c.w > thr) << 3);
-            if (thr4 < thr)
-                w4mask = (uint32_t(c.x > thr4) | (uint32_t(c.y > thr4) << 1) | (uint32_t(c.z > thr4) << 2) |
-                          (uint32_t(c.w > thr4) << 3)) & ~wmask;
         }
         if (P.wh_on && !P.wh_refresh && P.hf_ver)
         {
-            // sticky: the current plan's items keep their tier (mark = version << 1 | 4-lane tier)
+            // sticky: the current plan's items stay listed (mark = the plan version)
             const uint4 m = reinterpret_cast<const uint4 *>(P.wh_mark_in)[b];
-            const uint32_t mv[4] = { m.x, m.y, m.z, m.w };
-            for (uint32_t j = 0; j < kWavesPerWG; j++)
-                if ((mv[j] >> 1) == P.hf_ver && !((wmask | w4mask) & (1u << j)))
-                {
-                    if (mv[j] & 1u) w4mask |= 1u << j;
-                    else wmask |= 1u << j;
-                }
+            wmask |= uint32_t(m.x == P.hf_ver) | (uint32_t(m.y == P.hf_ver) << 1) | (uint32_t(m.z == P.hf_ver) << 2) |
+                     (uint32_t(m.w == P.hf_ver) << 3);
         }
-        const uint32_t any = wmask | w4mask;
         // the heavy-first order ranks a block by its slowest wave left in the lane section
-        cost = max(max((any & 1u) ? 0u : c.x, (any & 2u) ? 0u : c.y),
-                   max((any & 4u) ? 0u : c.z, (any & 8u) ? 0u : c.w));
+        cost = max(max((wmask & 1u) ? 0u : c.x, (wmask & 2u) ? 0u : c.y),
+                   max((wmask & 4u) ? 0u : c.z, (wmask & 8u) ? 0u : c.w));
     }
     const bool tail = uint64_t(last.maxc) * kHfSlots * 16u > uint64_t(kHfTail) * (last.sum << 4);
     const uint32_t thr = max(P.hf_floor, last.maxc >> kHfShift);
     const bool heavy = P.hf_front && tail && cost > thr;
     const bool hi = heavy && cost > (last.maxc >> 1);
-    uint32_t rank = 0u, wrank = 0u, w4rank = 0u;
+    uint32_t rank = 0u, wrank = 0u;
     if (cost) atomicMax(&s_max, cost);
     if (sum) atomicAdd(&s_sum, (unsigned long long)sum);
     if (heavy) rank = atomicAdd(hi ? &s_hi : &s_lo, 1u);
     if (wmask) wrank = atomicAdd(&s_w, uint32_t(__popc(wmask)));
-    if (w4mask) w4rank = atomicAdd(&s_w4, uint32_t(__popc(w4mask)));
     __syncthreads();
     if (threadIdx.x == 0u)
     {
@@ -1133,7 +1097,6 @@ __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks)
         s_bhi = s_hi ? atomicAdd(&P.hf_plan_out->cnt_hi, s_hi) : 0u;
         s_blo = s_lo ? atomicAdd(&P.hf_plan_out->cnt_lo, s_lo) : 0u;
         s_bw = s_w ? atomicAdd(&P.hf_plan_out->cnt_w, s_w) : 0u;
-        s_bw4 = s_w4 ? atomicAdd(&P.hf_plan_out->cnt_w4, s_w4) : 0u;
     }
     __syncthreads();
     if (heavy)
@@ -1150,27 +1113,16 @@ __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks)
     // wide items: listed and marked for the next plan's frames (beyond kWhMax they stay in the
     // lane section)
     for (uint32_t j = 0; j < kWavesPerWG; j++)
-    {
-        const uint32_t item = b * kWavesPerWG + j;
         if (wmask & (1u << j))
         {
+            const uint32_t item = b * kWavesPerWG + j;
             const uint32_t r = s_bw + wrank++;
             if (r < kWhMax)
             {
                 P.wh_list_out[r] = item;
-                P.wh_mark_out[item] = (P.hf_ver + 1u) << 1;
+                P.wh_mark_out[item] = P.hf_ver + 1u;
             }
         }
-        else if (w4mask & (1u << j))
-        {
-            const uint32_t r = s_bw4 + w4rank++;
-            if (r < kWhMax)
-            {
-                P.wh_list_out[kWhMax + r] = item;
-                P.wh_mark_out[item] = ((P.hf_ver + 1u) << 1) | 1u;
-            }
-        }
-    }
     // The block marks are written by a second pass over the final list, so a slot claimed by
     // both levels marks only the block whose entry survived.  That pass runs in the workgroup
     // that finishes last (a ticket after a release fence), not in a second launch: a kernel
@@ -1190,14 +1142,9 @@ __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks)
         if (j < nhi || j >= P.hf_front - nlo) P.hf_mark_out[vl[j]] = P.hf_ver + 1u;
     if (threadIdx.x == 0u)
     {
-        // hands the wide section's item counts to the host (they size the section of later
+        // hands the wide section's item count to the host (it sizes the section of later
         // launches) and re-arms the ticket
-        if (P.wh_host_cnt)
-        {
-            volatile uint32_t *h = P.wh_host_cnt;
-            h[0] = min(vp->cnt_w, kWhMax);
-            h[1] = min(vp->cnt_w4, kWhMax);
-        }
+        if (P.wh_host_cnt) *(volatile uint32_t *)P.wh_host_cnt = min(vp->cnt_w, kWhMax);
         *P.hf_ticket = 0u;
     }
 }
@@ -1228,25 +1175,24 @@ __device__ __forceinline__ bool block_of_launch(const KParams& P, uint32_t& b)
         }
         const uint32_t q = bid - front;
         const uint32_t nb = nblk - front;
-        b = (VAR & kVarXcdBands) ? xcd_band_block<(VAR & kVarCenterOut) != 0>(q, nb, P.xcd_chunk) : q;
+        b = (VAR & kVarXcdBands) ? xcd_band_block(q, nb, P.xcd_chunk) : q;
         return P.hf_ver == 0u || P.hf_mark_in[b] != P.hf_ver;
     }
-    b = (VAR & kVarXcdBands) ? xcd_band_block<(VAR & kVarCenterOut) != 0>(bid, nblk, P.xcd_chunk) : bid;
+    b = (VAR & kVarXcdBands) ? xcd_band_block(bid, nblk, P.xcd_chunk) : bid;
     return true;
 }
 
-// RT_KERNEL_WIDE (AUTO's record layout, spp a power of two <= 64 / G): G lanes per sample.
-// The heaviest waves of a frame (killeroo's body, scene 5's cat) run ~1000 triangle tests per
-// lane in a serial chain -- ~1M cycles per wave, the launch's critical path once a rank renders
-// 1/8 of the frame.  Here the G lanes of a group walk the same ray (identical state, so
-// identical control flow) and split each cell's list: sublane j tests references kb + j,
-// kb + j + G, ... with strict '<' in ascending order, and a butterfly over the group takes the
-// lexicographic minimum of (t, k) -- the first minimum in list order, exactly what
+// The wide section's per-sample trace (AUTO's record layout, spp a power of two <= 64 / G): G
+// lanes per sample.  The heaviest waves of a frame (killeroo's body, scene 5's cat) run ~1000
+// triangle tests per lane in a serial chain -- ~1M cycles per wave, the launch's critical path
+// once a rank renders 1/8 of the frame.  Here the G lanes of a group walk the same ray (identical
+// state, so identical control flow) and split each cell's list: sublane j tests references
+// kb + j, kb + j + G, ... with strict '<' in ascending order, and a butterfly over the group takes
+// the lexicographic minimum of (t, k) -- the first minimum in list order, exactly what
 // grid.cpp:258-266 keeps.  The chain per lane shrinks by G; the DDA walk is repeated G times.
-// One sample of the wide mode, traced by the G lanes of a group (sub = this lane's index in it):
-// the same walk in every lane of the group, each cell's list split over the group.  Returns the
-// sample's colour in every lane of the group.
-template <int VAR, int G, bool PF = true>
+// Returns the sample's colour in every lane of the group (and stores its hit triangle for
+// rt_render_hits_device).
+template <int VAR, int G>
 __device__ __forceinline__ void wide_trace(const KParams& P, uint32_t k, uint32_t slot, uint32_t sub, float& cr,
                                            float& cg, float& cb)
 {
@@ -1293,37 +1239,11 @@ __device__ __forceinline__ void wide_trace(const KParams& P, uint32_t k, uint32_
                         // nothing keeps (nct_ax, ~0), which every taken (t < nct_ax, k) beats
                         float bt = __builtin_fminf(rtd::kFltMax, nct_ax), bu = 0.0f, bv = 0.0f;
                         uint32_t bk = 0xFFFFFFFFu;
-                        // record k + G loads while record k is tested: the wide phase runs few,
-                        // latency-bound waves, so the extra registers cost no throughput
-                        float4 n0, n1, n2, n3;
-                        if (PF && kb + sub < ke)
-                        {
-                            const float4 *rp = P.frefs + size_t(kb + sub) * 4u;
-                            n0 = rp[0];
-                            n1 = rp[1];
-                            n2 = rp[2];
-                            n3 = rp[3];
-                        }
                         const rtd::f2v ra = {dx, dy}, rc = {dy, dz};
                         for (uint32_t k = kb + sub; k < ke; k += uint32_t(G))
                         {
-                            float4 r0 = n0, r1 = n1, r2 = n2, r3 = n3;
-                            if (!PF)
-                            {
-                                const float4 *rp = P.frefs + size_t(k) * 4u;
-                                r0 = rp[0];
-                                r1 = rp[1];
-                                r2 = rp[2];
-                                r3 = rp[3];
-                            }
-                            else if (k + uint32_t(G) < ke)
-                            {
-                                const float4 *rp = P.frefs + size_t(k + uint32_t(G)) * 4u;
-                                n0 = rp[0];
-                                n1 = rp[1];
-                                n2 = rp[2];
-                                n3 = rp[3];
-                            }
+                            const float4 *rp = P.frefs + size_t(k) * 4u;
+                            const float4 r0 = rp[0], r1 = rp[1], r2 = rp[2], r3 = rp[3];
                             float inv, cu;
                             const bool ok1 = rtd::mt_rec_first<(VAR & kVarFastRcp) != 0>(
                                 ra, rc, rtd::f2v{r0.x, r0.y}, rtd::f2v{r0.z, r0.w}, rtd::f2v{r1.x, r1.y},
@@ -1372,18 +1292,20 @@ __device__ __forceinline__ void wide_trace(const KParams& P, uint32_t k, uint32_
             }
             else
                 cr = cg = cb = float(ic.y) / float(Q.H);                   // renderer.cpp:121
+            // rt_render_hits_device only (a scalar test of a kernel parameter)
+            if (Q.hits && sub == 0u) Q.hits[(size_t(ic.y) * Q.W + ic.x) * Q.spp + ic.s] = hit ? tri : rtd::kNoTri;
         }
     }
 }
 
 // One wave of the wide mode: the 64 / G consecutive sample slots slot0 .. of local tile k.
-template <int VAR, int G, bool PF = true>
+template <int VAR, int G>
 __device__ __forceinline__ void wide_samples(const KParams& P, uint32_t k, uint32_t slot0)
 {
     const uint32_t lane = threadIdx.x & 63u, sub = lane & uint32_t(G - 1), grp = lane / uint32_t(G);
     const uint32_t slot = slot0 + grp;
     float cr, cg, cb;
-    wide_trace<VAR, G, PF>(P, k, slot, sub, cr, cg, cb);
+    wide_trace<VAR, G>(P, k, slot, sub, cr, cg, cb);
     // the pixel's samples are the groups grp0 .. grp0 + spp - 1 of this wave: sum in sample order
     const ItemCoord ic = tile_slot_coord(P, k, slot);
     const uint32_t grp0 = grp & ~(P.spp - 1u);
@@ -1404,31 +1326,27 @@ __device__ __forceinline__ void wide_samples(const KParams& P, uint32_t k, uint3
 }
 
 // kVarWideHeavy: the launch's wide section.  Its waves take the current plan's heavy work items
-// in list order, G waves per item (each 64 / G of the item's sample slots, G lanes per sample):
-// persistent over the list, so a section smaller than the list (the host sizes it from an older
-// plan's count) still renders every listed item.  They record no cost: an item's cost word keeps
-// its lane-mode measurement until a refresh frame renders it one lane per sample again.
+// in list order, wh_g waves per item (each 64 / wh_g of the item's sample slots, wh_g lanes per
+// sample): persistent over the list, so a section smaller than the list (the host sizes it from
+// an older plan's count) still renders every listed item.  They record no cost: an item's cost
+// word keeps its lane-mode measurement until a refresh frame renders it one lane per sample again.
 __device__ __forceinline__ void wide_section(const KParams& P)
 {
-    // units: 16 per item of the 16-lane list, then 4 per item of the 4-lane list
-    const uint32_t n16 = P.hf_ver ? min(P.hf_plan_in->cnt_w, kWhMax) : 0u;
-    const uint32_t n4 = P.hf_ver ? min(P.hf_plan_in->cnt_w4, kWhMax) : 0u;
+    const uint32_t n = P.hf_ver ? min(P.hf_plan_in->cnt_w, kWhMax) : 0u;
+    const uint32_t G = P.wh_g;                                      // 16 (spp <= 4) or 4 (spp 8-16)
     const uint32_t w = blockIdx.x * kWavesPerWG + (threadIdx.x >> 6), nw = P.wh_wgs * kWavesPerWG;
     const uint32_t ipt = P.wg_per_tile * kWavesPerWG;              // items per tile
-    for (uint32_t e = w; e < n16 * 16u + n4 * 4u; e += nw)
+    for (uint32_t e = w; e < n * G; e += nw)
     {
-        const bool g16 = e < n16 * 16u;
-        const uint32_t u = g16 ? e : e - n16 * 16u;
-        const uint32_t item =
-            __builtin_amdgcn_readfirstlane(g16 ? P.wh_list_in[u / 16u] : P.wh_list_in[kWhMax + u / 4u]);
+        const uint32_t item = __builtin_amdgcn_readfirstlane(P.wh_list_in[e / G]);
         const uint32_t kseq = item / ipt;
-        const uint32_t slot0 = (item - kseq * ipt) * 64u + (g16 ? (u % 16u) * 4u : (u % 4u) * 16u);
+        const uint32_t slot0 = (item - kseq * ipt) * 64u + (e % G) * (64u / G);
         // the parameters re-read per item (late_params): hoisted out of the loop they held ~30
         // more SGPRs across it and spilled
         const KParams& Q = late_params(P);
         const uint32_t k = Q.tile_order ? Q.tile_order[kseq] : kseq;
-        if (g16) wide_samples<kVarWide, 16, RT_WH_PF>(Q, k, slot0);
-        else wide_samples<kVarWide, 4, RT_WH_PF>(Q, k, slot0);
+        if (G == 16u) wide_samples<kVarWide, 16>(Q, k, slot0);
+        else wide_samples<kVarWide, 4>(Q, k, slot0);
     }
 }
 
@@ -1443,7 +1361,7 @@ __global__ void __launch_bounds__(kWG) k_render_lanes(KParams P)
     if (!block_of_launch<VAR>(P, b)) return;
     const uint32_t item = b * kWavesPerWG + (threadIdx.x >> 6);
     if constexpr ((VAR & kVarWideHeavy) != 0)
-        if (P.wh_wgs && P.hf_ver && (P.wh_mark_in[item] >> 1) == P.hf_ver) return;   // traced by the wide section
+        if (P.wh_wgs && P.hf_ver && P.wh_mark_in[item] == P.hf_ver) return;   // traced by the wide section
     if constexpr ((VAR & kVarWaveClock) != 0)
     {
         // debug arm (RT_KERNEL_FLAG_WAVE_CLOCK): s_memtime at the item's start and end, and how
@@ -1497,18 +1415,6 @@ __global__ void __launch_bounds__(kWG) k_render_lanes(KParams P)
 __global__ void __launch_bounds__(kWG) k_render_wh(KParams P)
 {
     wide_section(P);
-}
-
-// RT_KERNEL_WIDE: every tile in wide mode (the A/B arm of the two-phase frame)
-template <int VAR, int G>
-__global__ void __launch_bounds__(kWG) k_render_wide(KParams P)
-{
-    const uint32_t b = (VAR & kVarXcdBands) ? xcd_band_block(blockIdx.x, gridDim.x, P.xcd_chunk) : blockIdx.x;
-    const uint32_t witem = __builtin_amdgcn_readfirstlane(b * kWavesPerWG + (threadIdx.x >> 6));
-    const uint32_t per_tile = kTilePix * P.spp;                       // sample slots per tile
-    const uint32_t g = witem * (64u / uint32_t(G));                   // first slot, launch order
-    const uint32_t kseq = g / per_tile;
-    wide_samples<VAR, G>(P, P.tile_order ? P.tile_order[kseq] : kseq, g - kseq * per_tile);
 }
 
 // RT_KERNEL_COMPACT (grid intersector, spp a power of two <= 64): wavefront active-ray
@@ -1576,6 +1482,7 @@ k_render_compact(KParams P, uint32_t n_items, uint32_t refill)
                 }
                 else
                     cr = cg = cb = float(ic.y) / float(P.H);                    // renderer.cpp:121
+                if (P.hits) P.hits[(size_t(ic.y) * P.W + ic.x) * P.spp + ic.s] = hit ? tri : rtd::kNoTri;
             }
             L.col[wv][slot][0][j] = cr;
             L.col[wv][slot][1][j] = cg;
@@ -1737,7 +1644,9 @@ __global__ void __launch_bounds__(kWG) k_render_pixel_loop(KParams P)
     for (uint32_t s = 0; s < P.spp; s++)
     {
         float cr, cg, cb;
-        trace_sample<false, TRI, VAR>(P, x, y, s, cr, cg, cb, nullptr);
+        uint32_t hit_tri;
+        trace_sample<false, TRI, VAR>(P, x, y, s, cr, cg, cb, hit_tri, nullptr);
+        if (P.hits) P.hits[(size_t(y) * P.W + x) * P.spp + s] = hit_tri;
         sr += cr; sg += cg; sb += cb;
     }
     store_pixel(P, c, p, x, y, rtd::pack_bgra8(rtd::gamma_half(average(P, sr)), rtd::gamma_half(average(P, sg)),
@@ -1752,18 +1661,19 @@ __global__ void __launch_bounds__(kWG) k_trace_records(KParams P, uint32_t n)
     const uint32_t s = i % P.spp, pix = i / P.spp;
     const uint32_t x = P.rec_x0 + pix % P.rec_w, y = P.rec_y0 + pix / P.rec_w;
     float cr, cg, cb;
+    uint32_t ht;
     // Records walk the distance-skipping traversal with the wave-gated test, so the per-sample
     // parity tests (hit, tri, voxel, steps, tests) cover the walk the frames take.
     if (P.isect == RT_ISECT_RAY_MARCH)
-        trace_sample<true, RT_TRI_MOLLER_TRUMBORE, kVarMarch>(P, x, y, s, cr, cg, cb, &P.recs[i]);
+        trace_sample<true, RT_TRI_MOLLER_TRUMBORE, kVarMarch>(P, x, y, s, cr, cg, cb, ht, &P.recs[i]);
     else if (P.isect == RT_ISECT_RAY_MARCH + 0x100)   // exhaustive arm (RT_KERNEL_FLAG_EXHAUSTIVE)
-        trace_sample<true, RT_TRI_MOLLER_TRUMBORE, kVarMarch | kVarExhaustive>(P, x, y, s, cr, cg, cb, &P.recs[i]);
+        trace_sample<true, RT_TRI_MOLLER_TRUMBORE, kVarMarch | kVarExhaustive>(P, x, y, s, cr, cg, cb, ht, &P.recs[i]);
     else if (P.isect == RT_ISECT_BRUTE_FORCE)
-        trace_sample<true, RT_TRI_MOLLER_TRUMBORE, kVarBrute>(P, x, y, s, cr, cg, cb, &P.recs[i]);
+        trace_sample<true, RT_TRI_MOLLER_TRUMBORE, kVarBrute>(P, x, y, s, cr, cg, cb, ht, &P.recs[i]);
     else if (P.tri_test == RT_TRI_BARYCENTRIC)
-        trace_sample<true, RT_TRI_BARYCENTRIC, kVarDistSkip>(P, x, y, s, cr, cg, cb, &P.recs[i]);
+        trace_sample<true, RT_TRI_BARYCENTRIC, kVarDistSkip>(P, x, y, s, cr, cg, cb, ht, &P.recs[i]);
     else
-        trace_sample<true, RT_TRI_MOLLER_TRUMBORE, kVarWaveGate | kVarDistSkip>(P, x, y, s, cr, cg, cb, &P.recs[i]);
+        trace_sample<true, RT_TRI_MOLLER_TRUMBORE, kVarWaveGate | kVarDistSkip>(P, x, y, s, cr, cg, cb, ht, &P.recs[i]);
 }
 
 // K3: gathered shards [rank][local tile][256] -> frame
@@ -2012,6 +1922,16 @@ struct rt_scene
     // AUTO heavy-first order: per launch shape, which blocks the previous frame found heavy
     HfCtx hf[kHfCtxs];
     uint64_t hf_clock = 0;
+    uint64_t hf_evictions = 0;      // launch shapes that displaced another's state (rt_scene_info)
+    // scheduling tunables, read ONCE from the environment at rt_scene_create (A/B sweeps): the
+    // launch path never calls getenv
+    uint32_t hf_floor = 100000;     // RT_HF_FLOOR: heavy-first threshold floor, shader cycles
+    uint32_t hf_min_blocks = 4096;  // RT_HF_MIN_BLOCKS: smallest whole launch taking the heavy-first order
+    uint32_t wh_floor = 100000;     // RT_WH_FLOOR: wide-section threshold floor, shader cycles
+    uint32_t wh_alpha16 = 32;       // RT_WH_ALPHA16: wide threshold, sixteenths of the estimated span
+    uint32_t wh_auto_refs = 128;    // RT_WH_AUTO_REFS: AUTO takes the wide section for >= 2-rank
+                                    // shards of scenes with a cell list this long
+    bool octant_words = false;      // 8 ray-octant copies of the empty-run words (else one L-inf word)
     // sample table cache
     float2 *d_smp = nullptr;
     uint32_t smp_cap = 0;
@@ -2081,11 +2001,8 @@ int prepare_samples(rt_scene *s, const rt_frame *f, uint32_t spp)
     return RT_OK;
 }
 
-constexpr uint32_t kKernelFlags = RT_KERNEL_FLAG_CENTER_OUT | RT_KERNEL_FLAG_STATIC_ORDER | RT_KERNEL_FLAG_WIDE16 |
-                                  RT_KERNEL_FLAG_WIDE_HEAVY |
-                                  RT_KERNEL_FLAG_LDS_CELLS | RT_KERNEL_FLAG_ONE_PHASE | RT_KERNEL_FLAG_EXHAUSTIVE |
-                                  RT_KERNEL_FLAG_WAVE_CLOCK |
-                                  RT_KERNEL_BUDGET_MASK;
+constexpr uint32_t kKernelFlags = RT_KERNEL_FLAG_WIDE_HEAVY | RT_KERNEL_FLAG_LDS_CELLS | RT_KERNEL_FLAG_EXHAUSTIVE |
+                                  RT_KERNEL_FLAG_WAVE_CLOCK | RT_KERNEL_BUDGET_MASK;
 
 int validate_frame(const rt_frame *f)
 {
@@ -2097,8 +2014,8 @@ int validate_frame(const rt_frame *f)
     if (f->intersector == RT_ISECT_BRUTE_FORCE && f->tri_test != RT_TRI_MOLLER_TRUMBORE)
         return fail(RT_E_INVALID, "IntersectBruteForce uses IntersectRayTri only (renderer.cpp:176)");
     const uint32_t kind = f->kernel & RT_KERNEL_KIND_MASK;
-    if (kind > RT_KERNEL_WIDE || kind == 4u || (f->kernel & ~(RT_KERNEL_KIND_MASK | kKernelFlags)))
-        return fail(RT_E_INVALID, "unknown kernel");
+    if (kind > RT_KERNEL_COMPACT || (f->kernel & ~(RT_KERNEL_KIND_MASK | kKernelFlags)))
+        return fail(RT_E_INVALID, "unknown or removed kernel kind / flag");
     const uint32_t spp = std::max(1u, f->spp);
     if (spp > 4096) return fail(RT_E_INVALID, "spp must be <= 4096");
     if (kind == RT_KERNEL_COMPACT && ((f->kernel & RT_KERNEL_BUDGET_MASK) >> RT_KERNEL_BUDGET_SHIFT) > 64u)
@@ -2181,14 +2098,9 @@ int ensure_origin_terms(rt_scene *s, const KParams& P, hipStream_t st)
     return RT_OK;
 }
 
-// kVarWideHeavy thresholds: an item goes wide above max(floor, alpha16 / 16 x estimated span)
-// shader cycles; RT_WH_FLOOR / RT_WH_ALPHA16 override them (A/B sweeps)
-// (tools/wh_probe.py / env_probe.py sweeps: the floor keeps Cornell's items in the lanes -- at
-// 60000 cycles its rank of 8 lists ~900 items and doubles; the span factor 2x is best at 2, 4
-// and 8 ranks once items are listed from full frames only, profiles/r02t_wide_heavy_alpha_*)
-constexpr uint32_t kWhFloor = 100000;
 constexpr uint32_t kWhRefresh = 128;        // frames between refresh frames (a multiple of kHfPeriod)
-constexpr uint32_t kWhAlpha16 = 32;
+
+// One tunable from the environment (rt_scene_create only).
 uint32_t env_tunable(const char *name, uint32_t dflt)
 {
     const char *e = std::getenv(name);
@@ -2210,8 +2122,15 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
         c = &s->hf[0];
         for (HfCtx& h : s->hf)
             if (h.used < c->used) c = &h;
+        if (c->used) s->hf_evictions++;
+        // invalidated first: if an allocation below fails, no later launch may match the old
+        // shape and read freed (null) state arrays
+        std::memset(c->key, 0, sizeof(c->key));
+        c->frames = 0;
+        c->ver = 0;
         if (blocks > c->cap_blocks || !c->lists)
         {
+            c->cap_blocks = 0;
             if (c->marks) RT_HIP(hipFree(c->marks));
             if (c->cost) RT_HIP(hipFree(c->cost));
             if (c->wh_marks) RT_HIP(hipFree(c->wh_marks));
@@ -2219,29 +2138,26 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
             RT_HIP(hipMalloc(&c->marks, sizeof(uint32_t) * 2 * blocks));
             RT_HIP(hipMalloc(&c->cost, sizeof(uint32_t) * kWavesPerWG * blocks));
             RT_HIP(hipMalloc(&c->wh_marks, sizeof(uint32_t) * 2 * kWavesPerWG * blocks));
-            c->cap_blocks = uint32_t(blocks);
             if (!c->lists)
             {
-                RT_HIP(hipMalloc(&c->lists, sizeof(uint32_t) * 2 * kHfFrontMax));
                 RT_HIP(hipMalloc(&c->plans, sizeof(HfPlan) * 2));
                 RT_HIP(hipMalloc(&c->ticket, sizeof(uint32_t)));
-                RT_HIP(hipMalloc(&c->wh_lists, sizeof(uint32_t) * 4 * kWhMax));
-                RT_HIP(hipHostMalloc(&c->wh_cnt, 2 * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent));
+                RT_HIP(hipMalloc(&c->wh_lists, sizeof(uint32_t) * 2 * kWhMax));
+                RT_HIP(hipHostMalloc(&c->wh_cnt, sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent));
+                RT_HIP(hipMalloc(&c->lists, sizeof(uint32_t) * 2 * kHfFrontMax));   // last: marks completion
             }
+            c->cap_blocks = uint32_t(blocks);
         }
         RT_HIP(hipMemsetAsync(c->marks, 0, sizeof(uint32_t) * 2 * c->cap_blocks, st));
         RT_HIP(hipMemsetAsync(c->wh_marks, 0, sizeof(uint32_t) * 2 * kWavesPerWG * c->cap_blocks, st));
         RT_HIP(hipMemsetAsync(c->plans, 0, sizeof(HfPlan) * 2, st));
         RT_HIP(hipMemsetAsync(c->ticket, 0, sizeof(uint32_t), st));
-        ((volatile uint32_t *)c->wh_cnt)[0] = 0u;
-        ((volatile uint32_t *)c->wh_cnt)[1] = 0u;
-        std::memcpy(c->key, key, sizeof(key));
+        *(volatile uint32_t *)c->wh_cnt = 0u;
         c->nblocks = uint32_t(blocks);
         // front: an eighth of the blocks, capped, a multiple of the XCD count so the natural
         // section keeps its block -> XCD assignment
         c->front = front ? std::min<uint32_t>(kHfFrontMax, uint32_t(blocks / 8u) & ~(kXcds - 1u)) : 0u;
-        c->frames = 0;
-        c->ver = 0;
+        std::memcpy(c->key, key, sizeof(key));          // valid only now
     }
     c->used = ++s->hf_clock;
     const uint32_t v = c->ver;
@@ -2251,7 +2167,7 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
     // against, so it lists nothing) and then every kHfPeriod-th
     P.hf_measure = c->frames < 2u || c->frames % kHfPeriod == 0u;
     c->frames++;
-    P.hf_floor = env_tunable("RT_HF_FLOOR", kHfFloor);
+    P.hf_floor = s->hf_floor;
     P.hf_ticket = c->ticket;
     P.hf_mark_in = c->marks + size_t(v & 1u) * c->cap_blocks;
     P.hf_mark_out = c->marks + size_t((v + 1u) & 1u) * c->cap_blocks;
@@ -2262,26 +2178,23 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
     P.hf_cost = c->cost;
     if (var & kVarWideHeavy)
     {
-        // the section holds G waves per listed item of the newest plan the host has seen (a
+        // spp <= 4: 16 lanes per sample; spp 8-16: a pixel's samples fill a wave at 4 lanes each.
+        // The section holds wh_g waves per listed item of the newest plan the host has seen (a
         // plan or two old: the count is read without waiting); at least one workgroup, since
-        // the device-side list may already be longer (the section is persistent over it)
-        // refresh: every kWhRefresh-th frame renders every item one lane per sample, so the
-        // next plan re-ranks all items on lane-mode costs (the wide set is otherwise sticky)
-        const uint32_t units = 16u * ((volatile uint32_t *)c->wh_cnt)[0] + 4u * ((volatile uint32_t *)c->wh_cnt)[1];
+        // the device-side list may already be longer (the section is persistent over it).
+        // Refresh: every kWhRefresh-th frame renders every item one lane per sample, so the next
+        // plan re-ranks all items on lane-mode costs (the wide set is otherwise sticky).
+        P.wh_g = P.spp <= 4u ? 16u : 4u;
+        const uint32_t units = P.wh_g * *(volatile uint32_t *)c->wh_cnt;
         P.wh_on = 1u;
         P.wh_refresh = (c->frames - 1u) % kWhRefresh == 0u;       // frames counts this one
         P.wh_wgs = P.wh_refresh ? 0u : (units + kWavesPerWG - 1u) / kWavesPerWG;
-        P.wh_floor = env_tunable("RT_WH_FLOOR", kWhFloor);
-        const uint32_t alpha = env_tunable("RT_WH_ALPHA16", kWhAlpha16);
-        // spp <= 4: 16 lanes per sample (a 4-lane tier below it only on request, measured no
-        // gain); spp 8-16: a pixel's samples fill a wave at 4 lanes each, so every item takes
-        // the 4-lane tier
-        P.wh_alpha16 = P.spp <= 4u ? alpha : 0xFFFFFFFFu;
-        P.wh_alpha16_4 = P.spp <= 4u ? env_tunable("RT_WH_ALPHA16_4", alpha) : alpha;
+        P.wh_floor = s->wh_floor;
+        P.wh_alpha16 = s->wh_alpha16;
         P.wh_mark_in = c->wh_marks + size_t(v & 1u) * kWavesPerWG * c->cap_blocks;
         P.wh_mark_out = c->wh_marks + size_t((v + 1u) & 1u) * kWavesPerWG * c->cap_blocks;
-        P.wh_list_in = c->wh_lists + size_t(v & 1u) * 2u * kWhMax;
-        P.wh_list_out = c->wh_lists + size_t((v + 1u) & 1u) * 2u * kWhMax;
+        P.wh_list_in = c->wh_lists + size_t(v & 1u) * kWhMax;
+        P.wh_list_out = c->wh_lists + size_t((v + 1u) & 1u) * kWhMax;
         void *dev = nullptr;
         RT_HIP(hipHostGetDevicePointer(&dev, c->wh_cnt, 0));
         P.wh_host_cnt = static_cast<uint32_t *>(dev);
@@ -2307,7 +2220,6 @@ kfn_t lanes_kernel(int tri, int var)
         return k_render_lanes<RT_TRI_MOLLER_TRUMBORE, kVarAutoCore | kVarPackedRem | kVarSkipRun>;
     case kVarAutoCore | kVarFastRcp: return k_render_lanes<RT_TRI_MOLLER_TRUMBORE, kVarAutoCore | kVarFastRcp>;
     case kVarAutoCore: return k_render_lanes<RT_TRI_MOLLER_TRUMBORE, kVarAutoCore>;
-    case kVarAuto | kVarCenterOut: return k_render_lanes<RT_TRI_MOLLER_TRUMBORE, kVarAuto | kVarCenterOut>;
     case kVarAuto | kVarWideHeavy: return k_render_lanes<RT_TRI_MOLLER_TRUMBORE, kVarAuto | kVarWideHeavy>;
     case kVarAuto | kVarWaveClock: return k_render_lanes<RT_TRI_MOLLER_TRUMBORE, kVarAuto | kVarWaveClock>;
     case kVarAuto | kVarLdsCells: return k_render_lanes<RT_TRI_MOLLER_TRUMBORE, kVarAuto | kVarLdsCells>;
@@ -2338,18 +2250,16 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
     // whole rows interleave over the XCDs, so each L2 sees compact rows AND the frame's cost
     // spreads evenly (half rows put every left half on the even XCDs).
     P.xcd_chunk = ((P.tiles_x + P.nranks - 1u) / P.nranks) * P.wg_per_tile;
-    // AUTO (and the COMPACT / WIDE arms built on its per-ray code): the feature set of kVarAuto
-    // that this scene allows -- the Newton reciprocal needs rcp_safe, the packed counts and the
-    // empty-run loop need pack_ok.  DESIGN.md §4.1 has the measured progression.
-    const bool auto_path = lanes && grid_mt && (kind == RT_KERNEL_AUTO || kind == RT_KERNEL_COMPACT ||
-                                                kind == RT_KERNEL_WIDE);
+    // AUTO (and the COMPACT arm built on its per-ray code): the feature set of kVarAuto that this
+    // scene allows -- the Newton reciprocal needs rcp_safe, the packed counts and the empty-run
+    // loop need pack_ok.  DESIGN.md §4.1 has the measured progression.
+    const bool auto_path = lanes && grid_mt && (kind == RT_KERNEL_AUTO || kind == RT_KERNEL_COMPACT);
     int var = 0;
     if (auto_path)
     {
         var = kVarAutoCore | (s->rcp_safe ? kVarFastRcp : 0) | (s->pack_ok ? kVarPackedRem | kVarSkipRun : 0) |
               ((f->kernel & RT_KERNEL_FLAG_LDS_CELLS) ? kVarLdsCells : 0) |
-              ((f->kernel & RT_KERNEL_FLAG_WAVE_CLOCK) ? kVarWaveClock : 0) |
-              ((f->kernel & RT_KERNEL_FLAG_CENTER_OUT) ? kVarCenterOut : 0);
+              ((f->kernel & RT_KERNEL_FLAG_WAVE_CLOCK) ? kVarWaveClock : 0);
         if (int rc = ensure_origin_terms(s, P, st)) return rc;
     }
     else if (lanes && P.isect == RT_ISECT_RAY_MARCH)
@@ -2391,31 +2301,18 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
     }
     const dim3 wg(kWG);
     const uint32_t budget = (f->kernel & RT_KERNEL_BUDGET_MASK) >> RT_KERNEL_BUDGET_SHIFT;
-    // the wide arms need AUTO's full record/count layout and at most 64 / 4 samples per pixel
-    const bool wide_ok = auto_path && (var & ~(kVarCenterOut)) == kVarAuto && P.spp * kWideG <= 64u;
-    // AUTO takes the wide section (kVarWideHeavy: the wide code's layout, spp <= 16) for a shard
-    // of >= 2 ranks of a scene with dense cells: there a rank's launch is bound by its few
+    // AUTO takes the wide section (kVarWideHeavy: AUTO's full record/count layout, spp <= 16) for
+    // a shard of >= 2 ranks of a scene with dense cells: there a rank's launch is bound by its few
     // ~1000-test waves, which the section splits 16 ways (4 for spp 8-16) beside the lane kernel
     // (measured, tools/wh_probe.py, killeroo rank of 2 / 4 / 8: 0.36 / 0.33 / 0.25 ms with the
     // two-phase arm it replaced -> 0.35 / 0.20 / 0.15).  On a whole frame the
     // lanes are busy with other items anyway and the section's repeated walks cost more than they
     // save (+1-3 %).
+    const bool wide_ok = auto_path && var == kVarAuto && P.spp <= 16u;
     const bool wide_heavy = wide_ok && kind == RT_KERNEL_AUTO &&
                             ((f->kernel & RT_KERNEL_FLAG_WIDE_HEAVY) ||
-                             (P.nranks >= 2u && s->max_cell_refs >= kWhAutoRefs && !(f->kernel & RT_KERNEL_FLAG_ONE_PHASE)));
-    const bool g16 = (f->kernel & RT_KERNEL_FLAG_WIDE16) && P.spp * 16u <= 64u;
-    if (wide_ok && kind == RT_KERNEL_WIDE)
-    {
-        const uint32_t G = g16 ? 16u : kWideG;
-        P.xcd_chunk *= G;
-        RT_HIP(mark(kt0));
-        if (g16)
-            hipLaunchKernelGGL((k_render_wide<kVarWide, 16>), dim3(uint32_t(blocks) * G), wg, 0, st, P);
-        else
-            hipLaunchKernelGGL((k_render_wide<kVarWide, kWideG>), dim3(uint32_t(blocks) * G), wg, 0, st, P);
-        RT_HIP(mark(kt1));
-    }
-    else if (lanes && kind == RT_KERNEL_COMPACT && P.isect == RT_ISECT_GRID)
+                             (P.nranks >= 2u && s->max_cell_refs >= s->wh_auto_refs));
+    if (lanes && kind == RT_KERNEL_COMPACT && P.isect == RT_ISECT_GRID)
     {
         const uint32_t n_items = uint32_t(blocks * kWavesPerWG);
         const uint32_t refill = budget ? budget : kCompactRefill;
@@ -2431,17 +2328,16 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
     }
     else if (lanes)
     {
-        // AUTO, LANES, and WIDE / COMPACT where their layout does not apply
+        // AUTO, LANES, and COMPACT where its layout does not apply
         const int kvar = ((kind == RT_KERNEL_AUTO || P.isect != RT_ISECT_GRID) ? var : 0) |
                          (wide_heavy ? kVarWideHeavy : 0);
         const kfn_t fn = lanes_kernel(bary ? RT_TRI_BARYCENTRIC : RT_TRI_MOLLER_TRUMBORE, kvar);
         if (!fn) return fail(RT_E_INVALID, "kernel variant not built: " + std::to_string(kvar));
         uint32_t grid = uint32_t(blocks);
         // heavy-first order: AUTO grid frames large enough that blocks start in several rounds
+        // (and every wide-section launch of >= 64 blocks: its lane kernel's heaviest items)
         const bool front = kind == RT_KERNEL_AUTO && P.isect == RT_ISECT_GRID && !(kvar & kVarWaveClock) &&
-                           !(f->kernel & RT_KERNEL_FLAG_STATIC_ORDER) &&
-                           (blocks >= env_tunable("RT_HF_MIN_BLOCKS", kHfMinBlocks) ||
-                            (wide_heavy && blocks >= 64u && env_tunable("RT_WH_FRONT", 1u)));
+                           (blocks >= s->hf_min_blocks || (wide_heavy && blocks >= 64u));
         if (front || wide_heavy)
         {
             if (int rc = hf_prepare(s, P, blocks, kvar, front, st)) return rc;
@@ -2562,6 +2458,38 @@ int rt_get_device_count(int *count)
     return RT_OK;
 }
 
+#ifndef RT_SRC_HASH
+#define RT_SRC_HASH "unknown"
+#endif
+
+int rt_build_hash(char *buf, size_t len)
+{
+    if (!buf || len == 0) return fail(RT_E_INVALID, "bad arguments");
+    std::snprintf(buf, len, "%s", RT_SRC_HASH);
+    return RT_OK;
+}
+
+int rt_scene_info_get(rt_scene *s, rt_scene_info *out)
+{
+    if (!s || !out) return fail(RT_E_INVALID, "NULL argument");
+    std::lock_guard<std::mutex> lk(s->mtx);
+    std::memset(out, 0, sizeof(*out));
+    out->octant_words = s->octant_words;
+    out->packed_cells = s->d_cellw != nullptr;
+    out->rcp_safe = s->rcp_safe;
+    out->pack_ok = s->pack_ok;
+    out->max_cell_refs = s->max_cell_refs;
+    out->hf_floor = s->hf_floor;
+    out->hf_min_blocks = s->hf_min_blocks;
+    out->wh_floor = s->wh_floor;
+    out->wh_alpha16 = s->wh_alpha16;
+    out->wh_auto_refs = s->wh_auto_refs;
+    out->hf_contexts = kHfCtxs;
+    out->hf_evictions = s->hf_evictions;
+    out->device_bytes = s->device_bytes;
+    return RT_OK;
+}
+
 int rt_sample_table(uint32_t spp, float *out_xy)
 {
     if (!out_xy || spp == 0) return fail(RT_E_INVALID, "bad arguments");
@@ -2570,6 +2498,9 @@ int rt_sample_table(uint32_t spp, float *out_xy)
     std::memcpy(out_xy, t.data(), t.size() * sizeof(float));
     return RT_OK;
 }
+
+// Cap on the 8 octant copies of the cell words (device and host): 64 M cells at most.
+constexpr uint64_t kOctWordsMaxBytes = 256ull << 20;
 
 int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
 {
@@ -2602,6 +2533,12 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
     std::unique_ptr<rt_scene> s(new rt_scene());
     s->device = device;
     s->compact_wgs = 8u * uint32_t(std::max(1, ncus));
+    // scheduling tunables: read once here, never per launch (A/B sweeps set them per scene)
+    s->hf_floor = env_tunable("RT_HF_FLOOR", s->hf_floor);
+    s->hf_min_blocks = env_tunable("RT_HF_MIN_BLOCKS", s->hf_min_blocks);
+    s->wh_floor = env_tunable("RT_WH_FLOOR", s->wh_floor);
+    s->wh_alpha16 = env_tunable("RT_WH_ALPHA16", s->wh_alpha16);
+    s->wh_auto_refs = env_tunable("RT_WH_AUTO_REFS", s->wh_auto_refs);
     for (int a = 0; a < 3; a++)
     {
         s->dims[a] = g.dims[a];
@@ -2701,10 +2638,11 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
         // count as empty).  j steps of a walk in that octant move each coordinate by 0..j in the
         // octant's direction, so the next D-1 cells are empty -- the same contract as the L-inf
         // word, and D >= the L-inf distance.  D(c) = 1 + min of D over the 7 forward neighbours
-        // (the 3-D largest-square recurrence).  RT_OCT_DIST=0 keeps the L-inf words (A/B arm).
-        const char *oe = std::getenv("RT_OCT_DIST");
-        if (!(oe && oe[0] == '0'))
+        // (the 3-D largest-square recurrence).  RT_OCT_DIST=0 keeps the L-inf words (A/B arm),
+        // and so does a grid whose 8 copies would pass kOctWordsMaxBytes (they measured ~2 %).
+        if (env_tunable("RT_OCT_DIST", 1u) != 0u && uint64_t(nc) * 8u * 4u <= kOctWordsMaxBytes)
         {
+            s->octant_words = true;
             constexpr uint32_t kInf = 0x1FFFFFu;
             cellwo.resize(size_t(8) * nc);
             std::vector<uint32_t> D(nc);
@@ -2891,9 +2829,15 @@ int rt_scene_device_bytes(const rt_scene *s, uint64_t *bytes)
     return RT_OK;
 }
 
-int rt_render_frame_device(rt_scene *s, const rt_frame *f, uint32_t *d_bgra, void *hip_stream)
+} // extern "C"
+
+namespace {
+// The device-resident render of a whole frame (nranks == 1: d_out[y*W + x]) or of one rank's
+// interleaved 16x16 tiles (d_out = the compact shard), optionally with per-sample hit IDs.
+int render_device(rt_scene *s, const rt_frame *f, uint32_t rank, uint32_t nranks, uint32_t *d_out,
+                  uint32_t *d_hits, void *hip_stream)
 {
-    if (!s || !d_bgra) return fail(RT_E_INVALID, "NULL argument");
+    if (!s || !d_out || nranks == 0 || rank >= nranks) return fail(RT_E_INVALID, "bad arguments");
     int rc = validate_frame(f);
     if (rc) return rc;
     std::lock_guard<std::mutex> lk(s->mtx);
@@ -2904,10 +2848,22 @@ int rt_render_frame_device(rt_scene *s, const rt_frame *f, uint32_t *d_bgra, voi
     frame_params(s, f, P);
     P.rx0 = 0; P.ry0 = 0; P.rw = f->width; P.rh = f->height;
     P.tiles_x = (f->width + kTile - 1) / kTile;
-    const uint32_t tiles_y = (f->height + kTile - 1) / kTile;
-    P.rank = 0; P.nranks = 1;
-    P.out = d_bgra; P.pitch = f->width; P.shard_mode = 0;
-    return launch_render(s, f, P, P.tiles_x * tiles_y, static_cast<hipStream_t>(hip_stream));
+    const uint32_t ntiles = P.tiles_x * ((f->height + kTile - 1) / kTile);
+    P.rank = rank; P.nranks = nranks;
+    P.out = d_out;
+    P.hits = d_hits;
+    P.pitch = nranks == 1 ? f->width : 0u;
+    P.shard_mode = nranks == 1 ? 0u : 1u;
+    const uint32_t local = ntiles > rank ? (ntiles - rank + nranks - 1) / nranks : 0;
+    return launch_render(s, f, P, local, static_cast<hipStream_t>(hip_stream));
+}
+} // namespace
+
+extern "C" {
+
+int rt_render_frame_device(rt_scene *s, const rt_frame *f, uint32_t *d_bgra, void *hip_stream)
+{
+    return render_device(s, f, 0, 1, d_bgra, nullptr, hip_stream);
 }
 
 int rt_shard_elems(uint32_t width, uint32_t height, uint32_t nranks, uint64_t *elems)
@@ -2921,22 +2877,14 @@ int rt_shard_elems(uint32_t width, uint32_t height, uint32_t nranks, uint64_t *e
 int rt_render_shard_device(rt_scene *s, const rt_frame *f, uint32_t rank, uint32_t nranks, uint32_t *d_shard,
                            void *hip_stream)
 {
-    if (!s || !d_shard || nranks == 0 || rank >= nranks) return fail(RT_E_INVALID, "bad arguments");
-    int rc = validate_frame(f);
-    if (rc) return rc;
-    std::lock_guard<std::mutex> lk(s->mtx);
-    if ((rc = ensure_device(s))) return rc;
-    const uint32_t spp = std::max(1u, f->spp);
-    if ((rc = prepare_samples(s, f, spp))) return rc;
-    KParams P;
-    frame_params(s, f, P);
-    P.rx0 = 0; P.ry0 = 0; P.rw = f->width; P.rh = f->height;
-    P.tiles_x = (f->width + kTile - 1) / kTile;
-    const uint32_t ntiles = P.tiles_x * ((f->height + kTile - 1) / kTile);
-    P.rank = rank; P.nranks = nranks;
-    P.out = d_shard; P.pitch = 0; P.shard_mode = 1;
-    const uint32_t local = ntiles > rank ? (ntiles - rank + nranks - 1) / nranks : 0;
-    return launch_render(s, f, P, local, static_cast<hipStream_t>(hip_stream));
+    return render_device(s, f, rank, nranks, d_shard, nullptr, hip_stream);
+}
+
+int rt_render_hits_device(rt_scene *s, const rt_frame *f, uint32_t rank, uint32_t nranks, uint32_t *d_out,
+                          uint32_t *d_hits, void *hip_stream)
+{
+    if (!d_hits) return fail(RT_E_INVALID, "d_hits is NULL");
+    return render_device(s, f, rank, nranks, d_out, d_hits, hip_stream);
 }
 
 int rt_unshard_device(uint32_t width, uint32_t height, uint32_t nranks, const uint32_t *d_gathered,
@@ -3194,7 +3142,7 @@ int rt_debug_wide_items(rt_scene *s, uint32_t *count)
     for (const HfCtx& h : s->hf)
         if (h.wh_cnt && (!c || h.used > c->used)) c = &h;
     if (c) RT_HIP(hipDeviceSynchronize());
-    *count = c ? ((volatile uint32_t *)c->wh_cnt)[0] + ((volatile uint32_t *)c->wh_cnt)[1] : 0u;
+    *count = c ? *(volatile uint32_t *)c->wh_cnt : 0u;
     return RT_OK;
 }
 

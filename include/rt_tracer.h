@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 4
+#define RT_ABI_VERSION 5
 
 enum rt_status {
     RT_OK = 0,
@@ -95,19 +95,11 @@ enum rt_kernel {
     RT_KERNEL_COMPACT = 3,     /* AUTO's per-ray code in persistent waves with wavefront active-ray
                                   compaction: finished lanes are refilled with new samples by
                                   ballot + prefix count (grid intersector; else = LANES) */
-    /* 4 was the persistent LDS-bitmap arm (removed: measured slower) */
-    RT_KERNEL_WIDE = 5,        /* AUTO's per-ray code with 4 lanes per sample splitting every cell's
-                                  triangle list (spp <= 16; else = AUTO) */
+    /* 4 was the persistent LDS-bitmap arm and 5 the all-wide kernel (both removed after losing
+       their A/Bs; a frame naming them is rejected) */
     RT_KERNEL_KIND_MASK = 0x07,       /* the kernel kind above; the bits above it are flags */
-    RT_KERNEL_FLAG_CENTER_OUT = 0x10, /* OR-able (AUTO): the XCDs' row turns start at the frame's
-                                         middle row and move outward (A/B arm of the row order) */
-    RT_KERNEL_FLAG_STATIC_ORDER = 0x20, /* OR-able (AUTO): no heavy-first block order (A/B arm) */
-    RT_KERNEL_FLAG_WIDE16 = 0x40,     /* OR-able (WIDE kernel; spp <= 4): 16 lanes per sample
-                                         instead of 4 */
     RT_KERNEL_FLAG_LDS_CELLS = 0x80,  /* OR-able (AUTO): a wave-uniform list of >= 16 references is
                                          staged through LDS 64 records at a time */
-    RT_KERNEL_FLAG_ONE_PHASE = 0x100, /* OR-able (AUTO): the lane kernel alone, also for shards of
-                                         dense scenes (A/B arm of the rank-count policy) */
     RT_KERNEL_FLAG_WIDE_HEAVY = 0x200, /* OR-able (AUTO, spp <= 16; AUTO's own choice for >= 2-rank
                                           shards of dense scenes): work items that earlier frames of
                                           the same launch shape measured as heavy are traced wide (16
@@ -124,9 +116,10 @@ enum rt_kernel {
     RT_KERNEL_COMPACT_REFILL_SHIFT = RT_KERNEL_BUDGET_SHIFT,
     RT_KERNEL_COMPACT_REFILL_MASK = RT_KERNEL_BUDGET_MASK,
 };
-/* Bit 31 was RT_KERNEL_FLAG_BAIL_WIDE, the two-phase arm (a test budget per sample, then the
-   stopped samples resumed 4 or 16 lanes per sample by a second kernel).  RT_KERNEL_FLAG_WIDE_HEAVY
-   replaced it in round 2; a frame that sets the bit is rejected. */
+/* Removed A/B flags (they lost; a frame that sets one is rejected): 0x10 centre-out
+   row order, 0x20 static block order, 0x40 16-lane wide kernel, 0x100 one-phase shards, bit 31
+   the two-phase arm (replaced by RT_KERNEL_FLAG_WIDE_HEAVY in round 2).  The scheduling tunables
+   are read once per scene from the environment at rt_scene_create (rt_scene_info). */
 
 /* Per-frame parameters: what Renderer::RenderTile reads from the Scene and itself. */
 typedef struct rt_frame {
@@ -223,6 +216,16 @@ int  rt_render_shard_device(rt_scene *scene, const rt_frame *frame, uint32_t ran
 int  rt_unshard_device(uint32_t width, uint32_t height, uint32_t nranks,
                        const uint32_t *d_gathered, uint32_t *d_bgra, void *hip_stream);
 
+/* rt_render_frame_device (nranks == 1, d_out = the W*H frame) or rt_render_shard_device
+ * (nranks > 1, d_out = the rank's shard) that ALSO stores every traced sample's hit triangle --
+ * Grid::Intersect's tri_idx (grid.cpp:258-266, renderer.cpp:105), 0xFFFFFFFF on a miss -- into
+ * d_hits[(y*width + x)*spp + s] (frame-absolute, so the shards of all ranks fill one array).  Same
+ * launch path, same heavy-first / wide-section state and the same kernel binaries as the frame and
+ * shard entry points: the store sits after the walk behind a null test of the pointer, which is
+ * NULL in the plain calls (the parity tests pin the benchmarked kernel's hit IDs through here). */
+int  rt_render_hits_device(rt_scene *scene, const rt_frame *frame, uint32_t rank, uint32_t nranks,
+                           uint32_t *d_out, uint32_t *d_hits, void *hip_stream);
+
 /* Render-kernel time of the last timed rendering call on this scene (ms): the HIP events on the
  * launch stream immediately around its render kernel(s), as rt_kernel_times.  Waits for them. */
 int  rt_last_kernel_ms(rt_scene *scene, float *ms);
@@ -267,6 +270,26 @@ int rt_debug_heavy_first(rt_scene *s, uint32_t *front, uint32_t *listed, uint32_
 /* RT_KERNEL_FLAG_WIDE_HEAVY: work items the newest plan of the most recent wide-section launch
    shape lists for the wide section.  Synchronises the device. */
 int rt_debug_wide_items(rt_scene *s, uint32_t *count);
+
+/* What rt_scene_create chose for a scene, and the scheduling tunables it read once from the
+   environment (RT_HF_FLOOR, RT_HF_MIN_BLOCKS, RT_WH_FLOOR, RT_WH_ALPHA16, RT_WH_AUTO_REFS,
+   RT_OCT_DIST): never re-read per launch. */
+typedef struct rt_scene_info {
+    uint32_t octant_words;      /* 1: 8 ray-octant copies of the cell words (AUTO's empty runs);
+                                   0: one L-inf word per cell (RT_OCT_DIST=0, or above the size cap) */
+    uint32_t packed_cells;      /* cell ranges packed into one word per cell */
+    uint32_t rcp_safe, pack_ok; /* Newton 1/det and packed remaining-cell counts in range */
+    uint32_t max_cell_refs;
+    uint32_t hf_floor, hf_min_blocks, wh_floor, wh_alpha16, wh_auto_refs;
+    uint32_t hf_contexts;       /* heavy-first launch shapes remembered per scene */
+    uint64_t hf_evictions;      /* launch shapes evicted (each restarts its heavy-first state) */
+    uint64_t device_bytes;
+} rt_scene_info;
+int  rt_scene_info_get(rt_scene *scene, rt_scene_info *out);
+
+/* SHA-256 prefix (16 hex digits) of the kernel sources this library was compiled from, baked in
+   at build time (csrc/Makefile): counter files are matched against the LOADED library. */
+int  rt_build_hash(char *buf, size_t len);
 
 /* Hammersley table the library uses when rt_frame.sample_offsets is NULL. */
 int  rt_sample_table(uint32_t spp, float *out_xy);

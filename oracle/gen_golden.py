@@ -103,10 +103,22 @@ def crop_records(tmp):
     return crops
 
 
+def head_frame(tmp):
+    """BASELINE config 4: head at 4096x4096x16spp, BGRA8 and per-sample hit-ID SHA-256 (the hit
+    file is 1 GiB: hashed in a temporary directory, never committed)."""
+    bp, hp = os.path.join(tmp, "head.bgra"), os.path.join(tmp, "head.hits")
+    r = run(["render", os.path.join(SCENES, "scene4.rtscene"), "4096", "4096", "16", "--out", bp, "--hits", hp])
+    out = {"scene": 4, "W": 4096, "H": 4096, "spp": 16, "bgra_sha256": sha(bp), "hits_sha256": sha(hp),
+           "ref_msamples_per_s_8thr": r["msamples_per_s"]}
+    os.remove(hp)
+    print("head", r["msamples_per_s"], flush=True)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-head", action="store_true")
-    ap.add_argument("--only", choices=["crops", "bmp"],
+    ap.add_argument("--only", choices=["crops", "bmp", "head"],
                     help="regenerate one section and merge it into the existing golden.json")
     a = ap.parse_args()
     if a.only:
@@ -116,6 +128,8 @@ def main():
         tmp = tempfile.mkdtemp()
         if a.only == "crops":
             meta["crops"] = crop_records(tmp)
+        elif a.only == "head":
+            meta["frames_1080p4"]["head_4096x4096x16"] = head_frame(tmp)
         else:
             meta["bmp"] = bmp_golden(tmp)
         meta["sample_record"] = SAMPLE_RECORD
@@ -173,12 +187,7 @@ def main():
                        "hits_sha256": sha(hp), "ref_msamples_per_s_8thr": r["msamples_per_s"]}
         print("frame", sid, r["msamples_per_s"], flush=True)
     if not a.skip_head:
-        bp = os.path.join(tmp, "head.bgra")
-        r = run(["render", os.path.join(SCENES, "scene4.rtscene"), "4096", "4096", "16", "--out", bp])
-        frames["head_4096x4096x16"] = {"scene": 4, "W": 4096, "H": 4096, "spp": 16,
-                                       "bgra_sha256": sha(bp),
-                                       "ref_msamples_per_s_8thr": r["msamples_per_s"]}
-        print("head", r["msamples_per_s"], flush=True)
+        frames["head_4096x4096x16"] = head_frame(tmp)
 
     small = []
     for (sid, w, h, spp) in SMALL_FRAMES:

@@ -12,11 +12,15 @@ import bench  # noqa: E402
 
 
 class FakeRtm:
-    def __init__(self, h):
-        self.h = h
+    """lib: the hash baked into the loaded library (rt_build_hash); src: the sources on disk."""
+    def __init__(self, lib, src=None):
+        self.lib, self.src = lib, src if src is not None else lib
+
+    def library_build_hash(self):
+        return self.lib
 
     def kernel_source_hash(self):
-        return self.h
+        return self.src
 
 
 def _counters(tmp_path, h, workload="scenes[1, 8]_1920x1080x4"):
@@ -64,3 +68,13 @@ def test_roofline_missing_counters(tmp_path, monkeypatch):
     monkeypatch.setattr(bench, "ROOT", str(tmp_path))
     r = bench.valu_roofline(FakeRtm("abc123"), {1: 0.27, 8: 0.5}, _args(), 1, 1.0e13)
     assert r["frac"] is None and "missing" in r["counters"]
+
+
+def test_roofline_refuses_stale_library(tmp_path, monkeypatch):
+    """Counters collected for the sources on disk do not grade a library built from other
+    sources (a stale prebuilt librt_tracer.so): the LOADED library's baked hash decides."""
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    monkeypatch.setattr(bench, "SCENES", (1, 8))
+    _counters(tmp_path, "fresh22")
+    r = bench.valu_roofline(FakeRtm(lib="stale11", src="fresh22"), {1: 0.27, 8: 0.5}, _args(), 1, 1.0e13)
+    assert r["frac"] is None and "refused" in r["counters"] and "stale11" in r["counters"]

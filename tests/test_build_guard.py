@@ -62,7 +62,7 @@ def test_render_kernels_do_not_spill(tmp_path):
     # reciprocal + packed counts + uniform cells + empty runs + XCD rows), its fallbacks for scenes
     # outside the reciprocal / packing ranges, and its arms keep 8 waves/SIMD
     for key in ("k_render_lanesILi0ELi80398E", "k_render_lanesILi0ELi78350E", "k_render_lanesILi0ELi76298E",
-                "k_render_lanesILi0ELi74250E", "k_render_lanesILi0ELi1128974E", "k_render_lanesILi0ELi0E",
+                "k_render_lanesILi0ELi74250E", "k_render_lanesILi0ELi604686E", "k_render_lanesILi0ELi0E",
                 "k_render_compact"):
         arm = [v for n, v in render.items() if key in n]
         assert arm and all(a[2] == 8 for a in arm), (key, arm)

@@ -124,10 +124,18 @@ def test_crop_records_vs_reference_and_oracle(golden, scenes, oracle):
             np.testing.assert_array_equal(got[k], orc[k], err_msg=f"{c['name']} {k}")
 
 
+def sha_dev(t):
+    return hashlib.sha256(t.cpu().numpy().view(np.uint32).tobytes()).hexdigest()
+
+
 @pytest.mark.parametrize("sid", range(10))
 def test_full_frame_1080p4(golden, scenes, sid):
     """BASELINE configs 2/3/5: 1920x1080x4spp, BGRA8 SHA-256 and per-sample hit-ID SHA-256
-    equal the reference renderer's (all 10 built-in scenes)."""
+    equal the reference renderer's (all 10 built-in scenes).  The hit IDs come from the
+    benchmarked AUTO kernel itself (rt_render_hits_device: the same launch path and binary as
+    rt_render_frame_device, the store after the walk) on consecutive frames -- the first two in
+    the natural block order, the later ones heavy-first -- and from the debug records kernel."""
+    import torch
     g = golden["frames_1080p4"][str(sid)]
     hs, gs = scenes(sid)
     f = gs.frame(1920, 1080, 4)
@@ -135,6 +143,62 @@ def test_full_frame_1080p4(golden, scenes, sid):
     assert hashlib.sha256(img.tobytes()).hexdigest() == g["bgra_sha256"]
     recs = gs.trace_samples(f, 0, 0, 1920, 1080)
     assert hashlib.sha256(hit_ids(recs).tobytes()).hexdigest() == g["hits_sha256"]
+    out = torch.empty(1920 * 1080, dtype=torch.int32, device="cuda")
+    hits = torch.empty(1920 * 1080 * 4, dtype=torch.int32, device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    for i in range(4):
+        out.fill_(0x5A5A5A5A)
+        hits.fill_(0x5A5A5A5A)
+        gs.render_hits_device(f, 0, 1, out.data_ptr(), hits.data_ptr(), st)
+        torch.cuda.synchronize()
+        assert sha_dev(out) == g["bgra_sha256"], (sid, i)
+        assert sha_dev(hits) == g["hits_sha256"], (sid, i)
+
+
+@pytest.mark.parametrize("sid", [1, 5, 8])
+def test_shard_hits_rank_of_8(golden, scenes, sid, monkeypatch):
+    """Hit IDs of the benchmarked shard kernels at a rank of 8: every rank renders six frames of its
+    shard (frames 0-1 one lane per sample, later ones with AUTO's wide section: the listed heavy
+    items traced 16 lanes per sample with the (t, k) butterfly, the rest by the lane kernel in
+    heavy-first order); the hit IDs land frame-absolute, so the 8 shards together must hash to
+    the reference's per-sample hit-ID SHA, and the un-permuted shards to its BGRA8 SHA.  Cornell
+    has no cell of >= 128 references, so AUTO never takes the section there: its scene is made
+    with the wide threshold lowered and the section forced."""
+    import torch
+    g = golden["frames_1080p4"][str(sid)]
+    W, H, N = 1920, 1080, 8
+    kernel = rtm.RT_KERNEL_AUTO
+    own = None
+    if sid == 1:
+        monkeypatch.setenv("RT_WH_FLOOR", "2000")
+        monkeypatch.setenv("RT_WH_ALPHA16", "2")
+        hs = rtm.HostScene.load(sid)
+        own = gs = rtm.GpuScene(hs, 0)
+        kernel |= rtm.RT_KERNEL_FLAG_WIDE_HEAVY
+    else:
+        hs, gs = scenes(sid)
+    try:
+        f = gs.frame(W, H, 4, kernel=kernel)
+        e = rtm.shard_elems(W, H, N)
+        gathered = torch.zeros(N * e, dtype=torch.int32, device="cuda")
+        hits = torch.full((W * H * 4,), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+        st = torch.cuda.current_stream().cuda_stream
+        listed = 0
+        for r in range(N):
+            for _ in range(6):
+                gs.render_hits_device(f, r, N, gathered.data_ptr() + 4 * r * e, hits.data_ptr(), st)
+            torch.cuda.synchronize()
+            listed = max(listed, gs.wide_items())
+        assert listed > 0, (sid, listed)
+        assert sha_dev(hits) == g["hits_sha256"]
+        out = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+        rtm.unshard_device(W, H, N, gathered.data_ptr(), out.data_ptr(), st)
+        torch.cuda.synchronize()
+        assert sha_dev(out) == g["bgra_sha256"]
+    finally:
+        if own is not None:
+            own.close()
+            hs.close()
 
 
 def test_octant_words_arms(golden, monkeypatch):
@@ -203,18 +267,75 @@ def test_newton_reciprocal_exhaustive():
 
 
 def test_auto_equals_arms(golden, scenes):
-    """AUTO (heavy-first order) and its static-order, centre-out and LDS-staged arms, the plain
-    LANES kernel and the wide kernel (4 and 16 lanes per sample) render the reference's bytes on
-    the two bench scenes and the densest one."""
+    """AUTO (heavy-first order), its LDS-staged arm, the plain LANES kernel and the compaction
+    arm render the reference's bytes and per-sample hit IDs on the two bench scenes and the
+    densest one."""
+    import torch
     A = rtm.RT_KERNEL_AUTO
+    out = torch.empty(1920 * 1080, dtype=torch.int32, device="cuda")
+    hits = torch.empty(1920 * 1080 * 4, dtype=torch.int32, device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
     for sid in (1, 5, 8):
         hs, gs = scenes(sid)
-        want = golden["frames_1080p4"][str(sid)]["bgra_sha256"]
-        for k in (A, A | rtm.RT_KERNEL_FLAG_STATIC_ORDER, A | rtm.RT_KERNEL_FLAG_CENTER_OUT,
-                  A | rtm.RT_KERNEL_FLAG_LDS_CELLS, rtm.RT_KERNEL_LANES,
-                  rtm.RT_KERNEL_WIDE, rtm.RT_KERNEL_WIDE | rtm.RT_KERNEL_FLAG_WIDE16):
-            img = gs.render_frame(gs.frame(1920, 1080, 4, kernel=k))
-            assert hashlib.sha256(img.tobytes()).hexdigest() == want, (sid, hex(k))
+        g = golden["frames_1080p4"][str(sid)]
+        for k in (A, A | rtm.RT_KERNEL_FLAG_LDS_CELLS, rtm.RT_KERNEL_LANES, rtm.RT_KERNEL_COMPACT,
+                  rtm.RT_KERNEL_PIXEL_LOOP):
+            hits.fill_(0x5A5A5A5A)
+            gs.render_hits_device(gs.frame(1920, 1080, 4, kernel=k), 0, 1, out.data_ptr(), hits.data_ptr(), st)
+            torch.cuda.synchronize()
+            assert sha_dev(out) == g["bgra_sha256"], (sid, hex(k))
+            assert sha_dev(hits) == g["hits_sha256"], (sid, hex(k))
+
+
+def test_removed_arms_rejected(scenes):
+    """Kernel kinds and flags of arms removed after losing their A/Bs fail loudly: 4 (LDS bitmap),
+    5 (all-wide kernel), 0x10 centre-out, 0x20 static order, 0x40 16-lane wide kernel, 0x100
+    one-phase shards, bit 31 two-phase."""
+    hs, gs = scenes(1)
+    for k in (4, 5, 0x10, 0x20, 0x40, 0x100, 0x80000000):
+        with pytest.raises(rtm.RtError):
+            gs.render_frame(gs.frame(32, 32, 4, kernel=k))
+
+
+def test_scene_tunables_read_once(monkeypatch):
+    """Scheduling tunables come from the environment once, at rt_scene_create (never per launch);
+    RT_OCT_DIST=0 picks the single L-inf empty-run words."""
+    hs = rtm.HostScene.load(8)
+    a = rtm.GpuScene(hs, 0)
+    monkeypatch.setenv("RT_WH_FLOOR", "1234")
+    monkeypatch.setenv("RT_OCT_DIST", "0")
+    b = rtm.GpuScene(hs, 0)
+    try:
+        ia, ib = a.info(), b.info()
+        assert ia["wh_floor"] == 100000 and ib["wh_floor"] == 1234
+        assert ia["octant_words"] == 1 and ib["octant_words"] == 0
+        assert ia["max_cell_refs"] >= 128 and ia["rcp_safe"] == 1 and ia["pack_ok"] == 1
+        assert ia["hf_contexts"] >= 8
+        img = a.render_frame(a.frame(64, 48, 4))
+        monkeypatch.setenv("RT_WH_FLOOR", "5")
+        assert a.info()["wh_floor"] == 100000
+        np.testing.assert_array_equal(b.render_frame(b.frame(64, 48, 4)), img)
+    finally:
+        a.close()
+        b.close()
+        hs.close()
+
+
+def test_heavy_first_contexts_not_evicted_by_8_ranks(golden, scenes):
+    """One process driving all 8 ranks of a shard (tests, tools/shard_scaling.py) keeps every
+    launch shape's heavy-first state: no evictions."""
+    import torch
+    hs, gs = scenes(5)
+    f = gs.frame(1920, 1080, 4)
+    e = rtm.shard_elems(1920, 1080, 8)
+    buf = torch.zeros(e, dtype=torch.int32, device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    before = gs.info()["hf_evictions"]
+    for _ in range(3):
+        for r in range(8):
+            gs.render_shard_device(f, r, 8, buf.data_ptr(), st)
+    torch.cuda.synchronize()
+    assert gs.info()["hf_evictions"] == before
 
 
 def test_heavy_first_frames(golden, scenes):
@@ -284,23 +405,6 @@ def test_hip_graph_capture_replay(golden, scenes):
         assert hashlib.sha256(out.cpu().numpy().view(np.uint32).tobytes()).hexdigest() == want
 
 
-@pytest.mark.parametrize("spp", [1, 2, 4, 16, 32])
-def test_wide_vs_oracle(scenes, oracle, spp):
-    """Wide kernel (4 and 16 lanes per sample) on ragged frames at every spp it takes (32 falls
-    back to AUTO)."""
-    hs, gs = scenes(5)
-    exp, _, _ = oracle.render(5, 97, 61, spp)
-    for k in (rtm.RT_KERNEL_WIDE, rtm.RT_KERNEL_WIDE | rtm.RT_KERNEL_FLAG_WIDE16):
-        np.testing.assert_array_equal(gs.render_frame(gs.frame(97, 61, spp, kernel=k)), exp, err_msg=hex(k))
-
-
-def test_removed_two_phase_flag_rejected(scenes):
-    """Bit 31 (the two-phase arm, replaced by the wide section) fails loudly."""
-    hs, gs = scenes(1)
-    with pytest.raises(rtm.RtError):
-        gs.render_frame(gs.frame(32, 32, 4, kernel=0x80000000))
-
-
 @pytest.mark.parametrize("sid,spp", [(5, 1), (5, 4), (5, 64), (8, 2), (8, 16), (4, 4)])
 def test_lds_cells_vs_oracle(scenes, oracle, sid, spp):
     """LDS-staged uniform lists on ragged frames: partial waves (pixels off the frame, lanes
@@ -339,58 +443,77 @@ def test_shard_partition_dense_scenes(golden, scenes, sid, nranks):
 def test_wide_heavy_shard_frames(golden, scenes, sid, nranks, kernel, monkeypatch):
     """RT_KERNEL_FLAG_WIDE_HEAVY over consecutive frames of every rank: frames 0-1 render one
     lane per sample and measure, later frames trace the listed heavy items on the side stream
-    (16 lanes per sample); every frame's shard equals the one-lane-per-sample shard, and the
+    (16 lanes per sample); every frame's shard equals the plain LANES kernel's shard, and the
     partition reassembles into the reference frame.  kernel 0: AUTO's own policy (>= 2 ranks of
-    a dense scene), 0x200: the flag forced (also on a whole frame)."""
+    a dense scene), 0x200: the flag forced (also on a whole frame, where the default threshold
+    -- 2x the span estimate -- lists nothing: that scene is made with RT_WH_ALPHA16=4)."""
     import torch
+    own = None
     if nranks == 1:
-        # a whole frame's span is long: at the default threshold (2x span) nothing is listed
         monkeypatch.setenv("RT_WH_ALPHA16", "4")
-    hs, gs = scenes(sid)
-    W, H = 1920, 1080
-    f = gs.frame(W, H, 4, kernel=kernel)
-    f_ref = gs.frame(W, H, 4, kernel=rtm.RT_KERNEL_AUTO | rtm.RT_KERNEL_FLAG_ONE_PHASE)
-    e = rtm.shard_elems(W, H, nranks)
-    gathered = torch.zeros(nranks * e, dtype=torch.int32, device="cuda")
-    ref = torch.zeros(e, dtype=torch.int32, device="cuda")
-    stream = torch.cuda.current_stream().cuda_stream
-    listed = 0
-    for r in range(nranks):
-        gs.render_shard_device(f_ref, r, nranks, ref.data_ptr(), stream)
-        part = gathered[r * e:(r + 1) * e]
-        for i in range(6):
-            part.zero_()
-            gs.render_shard_device(f, r, nranks, part.data_ptr(), stream)
-            torch.cuda.synchronize()
-            assert torch.equal(part, ref), (sid, nranks, r, i)
-        listed = max(listed, gs.wide_items())
-    assert listed > 0, (sid, nranks)
-    out = torch.zeros(W * H, dtype=torch.int32, device="cuda")
-    rtm.unshard_device(W, H, nranks, gathered.data_ptr(), out.data_ptr(), stream)
-    torch.cuda.synchronize()
-    img = out.cpu().numpy().view(np.uint32)
-    assert hashlib.sha256(img.tobytes()).hexdigest() == golden["frames_1080p4"][str(sid)]["bgra_sha256"]
+        hs = rtm.HostScene.load(sid)
+        own = gs = rtm.GpuScene(hs, 0)
+    else:
+        hs, gs = scenes(sid)
+    try:
+        W, H = 1920, 1080
+        f = gs.frame(W, H, 4, kernel=kernel)
+        f_ref = gs.frame(W, H, 4, kernel=rtm.RT_KERNEL_LANES)
+        e = rtm.shard_elems(W, H, nranks)
+        gathered = torch.zeros(nranks * e, dtype=torch.int32, device="cuda")
+        ref = torch.zeros(e, dtype=torch.int32, device="cuda")
+        stream = torch.cuda.current_stream().cuda_stream
+        listed = 0
+        for r in range(nranks):
+            gs.render_shard_device(f_ref, r, nranks, ref.data_ptr(), stream)
+            part = gathered[r * e:(r + 1) * e]
+            for i in range(6):
+                part.zero_()
+                gs.render_shard_device(f, r, nranks, part.data_ptr(), stream)
+                torch.cuda.synchronize()
+                assert torch.equal(part, ref), (sid, nranks, r, i)
+            listed = max(listed, gs.wide_items())
+        assert listed > 0, (sid, nranks)
+        out = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+        rtm.unshard_device(W, H, nranks, gathered.data_ptr(), out.data_ptr(), stream)
+        torch.cuda.synchronize()
+        img = out.cpu().numpy().view(np.uint32)
+        assert hashlib.sha256(img.tobytes()).hexdigest() == golden["frames_1080p4"][str(sid)]["bgra_sha256"]
+    finally:
+        if own is not None:
+            own.close()
+            hs.close()
 
 
-@pytest.mark.parametrize("spp,alpha4", [(1, None), (2, None), (4, None), (4, "1"), (8, None), (16, None)])
-def test_wide_heavy_ragged_vs_oracle(scenes, oracle, spp, alpha4, monkeypatch):
+@pytest.mark.parametrize("spp", [1, 2, 4, 8, 16])
+def test_wide_heavy_ragged_vs_oracle(oracle, spp, monkeypatch):
     """The wide section on ragged frames (partial tiles) with the floor lowered so that most
     items go wide, over 136 frames: the sticky list, the refresh frame (frame 128 renders every
-    item one lane per sample) and the re-listing after it all render the reference's bytes.
-    spp <= 4 takes 16 lanes per sample (with alpha4 also a 4-lane tier), spp 8 / 16 only 4."""
+    item one lane per sample) and the re-listing after it all render the reference's bytes and
+    hit IDs.  spp <= 4 takes 16 lanes per sample, spp 8 / 16 take 4."""
+    import torch
     monkeypatch.setenv("RT_WH_FLOOR", "2000")
     monkeypatch.setenv("RT_WH_ALPHA16", "2")
-    if alpha4:
-        monkeypatch.setenv("RT_WH_ALPHA16_4", alpha4)
-    hs, gs = scenes(8)
-    exp, _, _ = oracle.render(8, 97, 61, spp)
-    f = gs.frame(97, 61, spp, kernel=rtm.RT_KERNEL_AUTO | rtm.RT_KERNEL_FLAG_WIDE_HEAVY)
-    listed = 0
-    for i in range(136):
-        np.testing.assert_array_equal(gs.render_frame(f), exp, err_msg=str(i))
-        if i in (3, 60, 130):
-            listed = max(listed, gs.wide_items())
-    assert listed > 0
+    hs = rtm.HostScene.load(8)
+    gs = rtm.GpuScene(hs, 0)
+    try:
+        exp, exph, _ = oracle.render(8, 97, 61, spp, hits=True)
+        f = gs.frame(97, 61, spp, kernel=rtm.RT_KERNEL_AUTO | rtm.RT_KERNEL_FLAG_WIDE_HEAVY)
+        out = torch.empty(97 * 61, dtype=torch.int32, device="cuda")
+        hits = torch.empty(97 * 61 * spp, dtype=torch.int32, device="cuda")
+        st = torch.cuda.current_stream().cuda_stream
+        listed = 0
+        for i in range(136):
+            gs.render_hits_device(f, 0, 1, out.data_ptr(), hits.data_ptr(), st)
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32).reshape(61, 97), exp, err_msg=str(i))
+            np.testing.assert_array_equal(hits.cpu().numpy().view(np.uint32), exph, err_msg=str(i))
+            if i in (3, 60, 130):
+                listed = max(listed, gs.wide_items())
+        assert listed > 0
+    finally:
+        gs.close()
+        hs.close()
 
 
 def test_wide_heavy_graph_replay(golden, scenes):
@@ -443,6 +566,31 @@ def test_head_4096x4096x16(golden, scenes):
     hs, gs = scenes(4)
     img = gs.render_frame(gs.frame(4096, 4096, 16))
     assert hashlib.sha256(img.tobytes()).hexdigest() == g["bgra_sha256"]
+
+
+def test_head_4096x4096x16_eight_shards(golden, scenes):
+    """BASELINE config 4's own shape: head at 4096^2 x 16 cut into the 8 ranks' interleaved 16x16
+    tiles on one device (AUTO's shard path: the wide section at 4 lanes per sample for spp 16),
+    three frames per rank; the un-permuted shards hash to the reference's frame and the
+    per-sample hit IDs of all ranks to the reference's hit-ID SHA (application.cpp:368-378)."""
+    import torch
+    g = golden["frames_1080p4"]["head_4096x4096x16"]
+    hs, gs = scenes(4)
+    W = H = 4096
+    N, spp = 8, 16
+    f = gs.frame(W, H, spp)
+    e = rtm.shard_elems(W, H, N)
+    gathered = torch.zeros(N * e, dtype=torch.int32, device="cuda")
+    hits = torch.full((W * H * spp,), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    for r in range(N):
+        for _ in range(3):
+            gs.render_hits_device(f, r, N, gathered.data_ptr() + 4 * r * e, hits.data_ptr(), st)
+    out = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+    rtm.unshard_device(W, H, N, gathered.data_ptr(), out.data_ptr(), st)
+    torch.cuda.synchronize()
+    assert sha_dev(out) == g["bgra_sha256"]
+    assert sha_dev(hits) == g["hits_sha256"]
 
 
 def test_render_tiles_subset(scenes):

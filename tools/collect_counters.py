@@ -6,7 +6,7 @@ pass under its own time limit), driving tools/render_loop.py (one scene's 1080p 
 N times).  Per scene it keeps the median over the k_render_* dispatches after the first two
 (warm-up / heavy-first bootstrap) and writes
 
-    profiles/counters_<workload>.json = {"source_hash": rtm.kernel_source_hash(), "workload": ...,
+    profiles/counters_<workload>.json = {"source_hash": rtm.library_build_hash() (the loaded library's), "workload": ...,
                               "scenes": {"1": {"SQ_INSTS_VALU": ..., "FETCH_SIZE_KiB": ...,
                                                "WRITE_SIZE_KiB": ..., "hbm_bytes": ...}, ...}}
 
@@ -104,7 +104,7 @@ def main():
         c["hbm_bytes"] = round((2 * c["FETCH_SIZE_KiB"] + c["WRITE_SIZE_KiB"]) * 1024)
         c["valu_per_wave"] = round(c["SQ_INSTS_VALU"] / c["SQ_WAVES"], 1)
         c["lane_util"] = round(c["SQ_THREAD_CYCLES_VALU"] / max(1.0, c["SQ_ACTIVE_INST_VALU"]), 2)
-    out = {"source_hash": rtm.kernel_source_hash(), "workload": f"scenes{a.scenes}_{W}x{H}x{S}",
+    out = {"source_hash": rtm.library_build_hash(), "workload": f"scenes{a.scenes}_{W}x{H}x{S}",
            "workload_name": a.workload,
            "kernel": "AUTO (rt_kernel 0)", "frames_per_scene": a.frames,
            "statistic": "per scene, median over its k_render_* dispatches after its first two",
