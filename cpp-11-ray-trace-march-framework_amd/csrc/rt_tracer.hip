@@ -2832,9 +2832,10 @@ int rt_scene_device_bytes(const rt_scene *s, uint64_t *bytes)
 } // extern "C"
 
 namespace {
-// The device-resident render of a whole frame (nranks == 1: d_out[y*W + x]) or of one rank's
-// interleaved 16x16 tiles (d_out = the compact shard), optionally with per-sample hit IDs.
-int render_device(rt_scene *s, const rt_frame *f, uint32_t rank, uint32_t nranks, uint32_t *d_out,
+// The device-resident render of a whole frame (shard false: d_out[y*W + x]) or of one rank's
+// interleaved 16x16 tiles (shard true: d_out = the compact shard, also for nranks == 1),
+// optionally with per-sample hit IDs.
+int render_device(rt_scene *s, const rt_frame *f, uint32_t rank, uint32_t nranks, bool shard, uint32_t *d_out,
                   uint32_t *d_hits, void *hip_stream)
 {
     if (!s || !d_out || nranks == 0 || rank >= nranks) return fail(RT_E_INVALID, "bad arguments");
@@ -2852,8 +2853,8 @@ int render_device(rt_scene *s, const rt_frame *f, uint32_t rank, uint32_t nranks
     P.rank = rank; P.nranks = nranks;
     P.out = d_out;
     P.hits = d_hits;
-    P.pitch = nranks == 1 ? f->width : 0u;
-    P.shard_mode = nranks == 1 ? 0u : 1u;
+    P.pitch = shard ? 0u : f->width;
+    P.shard_mode = shard ? 1u : 0u;
     const uint32_t local = ntiles > rank ? (ntiles - rank + nranks - 1) / nranks : 0;
     return launch_render(s, f, P, local, static_cast<hipStream_t>(hip_stream));
 }
@@ -2863,7 +2864,7 @@ extern "C" {
 
 int rt_render_frame_device(rt_scene *s, const rt_frame *f, uint32_t *d_bgra, void *hip_stream)
 {
-    return render_device(s, f, 0, 1, d_bgra, nullptr, hip_stream);
+    return render_device(s, f, 0, 1, false, d_bgra, nullptr, hip_stream);
 }
 
 int rt_shard_elems(uint32_t width, uint32_t height, uint32_t nranks, uint64_t *elems)
@@ -2877,14 +2878,14 @@ int rt_shard_elems(uint32_t width, uint32_t height, uint32_t nranks, uint64_t *e
 int rt_render_shard_device(rt_scene *s, const rt_frame *f, uint32_t rank, uint32_t nranks, uint32_t *d_shard,
                            void *hip_stream)
 {
-    return render_device(s, f, rank, nranks, d_shard, nullptr, hip_stream);
+    return render_device(s, f, rank, nranks, true, d_shard, nullptr, hip_stream);
 }
 
 int rt_render_hits_device(rt_scene *s, const rt_frame *f, uint32_t rank, uint32_t nranks, uint32_t *d_out,
                           uint32_t *d_hits, void *hip_stream)
 {
     if (!d_hits) return fail(RT_E_INVALID, "d_hits is NULL");
-    return render_device(s, f, rank, nranks, d_out, d_hits, hip_stream);
+    return render_device(s, f, rank, nranks, nranks > 1, d_out, d_hits, hip_stream);
 }
 
 int rt_unshard_device(uint32_t width, uint32_t height, uint32_t nranks, const uint32_t *d_gathered,
