@@ -71,8 +71,9 @@ HOST_SYMBOLS = [
     "rth_framebuffer_start_rendering", "rth_framebuffer_read", "rth_framebuffer_save_bmp",
     "rth_last_error", "rth_scene_set_id", "rth_scene_save", "rth_mesh_read", "rth_mesh_normalize_dimensions",
     "rth_mesh_transform", "rth_mesh_add_quad", "rth_mesh_add_mesh", "rth_mesh_data", "rth_mesh_free",
-    "rth_look_at", "rth_scene_table",
+    "rth_look_at", "rth_scene_table", "rth_framebuffer_create_multi", "rth_framebuffer_transport",
 ]
+RTH_TRANSPORT_NONE, RTH_TRANSPORT_RCCL, RTH_TRANSPORT_DEVICE_COPY = 0, 1, 2
 
 
 class RtError(RuntimeError):
@@ -209,6 +210,8 @@ def host_lib():
         L.rth_scene_camera.argtypes = [vp, ctypes.POINTER(c_f32), vp]
         L.rth_scene_stats_get.argtypes = [vp, ctypes.POINTER(SceneStats)]
         L.rth_framebuffer_create.argtypes = [vp, vp, c_u32, ctypes.POINTER(vp)]
+        L.rth_framebuffer_create_multi.argtypes = [vp, vp, c_u32, c_u32, ctypes.POINTER(vp)]
+        L.rth_framebuffer_transport.argtypes = [vp, ctypes.POINTER(c_u32), ctypes.POINTER(c_u32)]
         L.rth_framebuffer_free.argtypes = [vp]
         L.rth_framebuffer_free.restype = None
         L.rth_framebuffer_set_sample_count.argtypes = [vp, c_u32]
@@ -661,13 +664,31 @@ class Renderer:
     worker pool whose ``RenderTile`` is served by one batched GPU launch per frame.
     """
 
-    def __init__(self, host_scene, gpu_scene, nthreads=0):
+    def __init__(self, host_scene, gpu_scene, nthreads=0, devices=None):
         self.host, self.gpu = host_scene, gpu_scene
         L, h = host_lib(), ctypes.c_void_p()
-        _check(L.rth_framebuffer_create(gpu_scene._h, host_scene._h, nthreads, ctypes.byref(h)),
-               L, "rth_framebuffer_create")
+        if devices is None:
+            _check(L.rth_framebuffer_create(gpu_scene._h, host_scene._h, nthreads, ctypes.byref(h)),
+                   L, "rth_framebuffer_create")
+        else:
+            dv = np.ascontiguousarray(devices, np.int32)
+            _check(L.rth_framebuffer_create_multi(host_scene._h, _ptr(dv), len(dv), nthreads, ctypes.byref(h)),
+                   L, "rth_framebuffer_create_multi")
         self._h = h
         self.width = self.height = 1
+
+    @classmethod
+    def multi(cls, host_scene, devices, nthreads=0):
+        """The Framebuffer served by several GPUs (rth_framebuffer_create_multi): devices[i]
+        renders rank i's tiles; one RCCL gather to devices[0] when every device is listed once."""
+        return cls(host_scene, None, nthreads, devices=list(devices))
+
+    def transport(self):
+        """(rth_transport, ranks) of this framebuffer: 0 none (one device), 1 RCCL, 2 device copies."""
+        L = host_lib()
+        t, n = c_u32(), c_u32()
+        _check(L.rth_framebuffer_transport(self._h, ctypes.byref(t), ctypes.byref(n)), L, "rth_framebuffer_transport")
+        return t.value, n.value
 
     def set_sample_count(self, spp):
         L = host_lib()

@@ -15,6 +15,10 @@
 
 #include "../../include/rt_host.h"
 
+#include <dlfcn.h>
+#include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
+
 #include <algorithm>
 #include <array>
 #include <atomic>
@@ -473,22 +477,15 @@ private:
     uint32_t m_frame_seed = 1;
 };
 
-// Renderer (renderer.h) with the tile callback served by the GPU: the first worker of a frame
-// issues the whole frame as ONE launch whose copy-back lands, tile row by tile row, in this
-// renderer's page-locked frame (rt_render_frame_host); every worker then waits only for its own
-// tile row and copies its tile straight out of that frame while holding the tile's mutex (the
+// Renderer (renderer.h) with the tile callback served by GPU frames: the first worker of a frame
+// issues the whole frame (Issue: one launch per device) whose copy-back lands, tile row by tile
+// row, in this renderer's page-locked frame; every worker then waits only for its own tile row
+// (WaitRows) and copies its tile straight out of that frame while holding the tile's mutex (the
 // reference's locking contract, framebuffer.cpp:71-74).  One DMA pass and one tile copy per pixel.
-class GpuRenderer : public Framebuffer
+class FrameRenderer : public Framebuffer
 {
 public:
-    GpuRenderer(rt_scene* gpu, const rth_scene* host, uint32_t nthreads)
-        : Framebuffer(nthreads), m_gpu(gpu), m_host(host) { }
-    ~GpuRenderer() override
-    {
-        Shutdown();
-        DrainFrame();
-        if (m_frame) rt_host_free(m_frame);
-    }
+    explicit FrameRenderer(uint32_t nthreads) : Framebuffer(nthreads) { }
 
     void SetSampleCount(uint32_t cnt) { m_spp = std::max(1u, cnt); }   // renderer.cpp:18-22
     void SetOptions(uint32_t tri_test, uint32_t kernel) { m_tri_test = tri_test; m_kernel = kernel; }
@@ -504,6 +501,23 @@ public:
     }
 
 protected:
+    // One frame into the page-locked frame: band b holds rows [ends[b-1], ends[b]).  Asynchronous;
+    // WaitRows(y1) returns once rows [0, y1) have landed.  On failure: an RT_E* code, message in
+    // m_err.
+    virtual int Issue(const rt_frame& f, uint32_t* host_frame, const uint32_t* ends, uint32_t nb) = 0;
+    virtual int WaitRows(uint32_t y1) = 0;
+    virtual int AllocHost(size_t bytes, void** p) = 0;
+    virtual void FreeHost(void* p) = 0;
+
+    // derived destructors: Shutdown(), then this (workers call the derived WaitRows)
+    void ReleaseFrame()
+    {
+        DrainFrame();
+        if (m_frame) FreeHost(m_frame);
+        m_frame = nullptr;
+        m_frame_cap = 0;
+    }
+
     void BeginFrame() override
     {
         std::lock_guard<std::mutex> g(m_frame_mtx);
@@ -526,11 +540,11 @@ protected:
         }
         uint32_t x0, y0, x1, y1;
         tile.GetPosition(x0, y0, x1, y1);
-        const int rc = rt_frame_host_wait(m_gpu, y1);
+        const int rc = WaitRows(y1);
         if (rc != RT_OK)
         {
             std::lock_guard<std::mutex> g(m_frame_mtx);
-            SetError(rc);
+            m_status = rc;
             return false;
         }
         uint32_t* buf = tile.GetBuffer();
@@ -541,20 +555,14 @@ protected:
         return true;
     }
 
-private:
-    void SetError(int rc)
-    {
-        m_status = rc;
-        char msg[512];
-        rt_last_error(msg, sizeof(msg));
-        m_err = msg;
-    }
+    std::string m_err;
 
+private:
     // A frame's copy-back may still be landing in m_frame (workers stopped early): wait it out
     // before the frame memory is reused or freed.
     void DrainFrame()
     {
-        if (m_issued && m_issued_h) (void)rt_frame_host_wait(m_gpu, m_issued_h);
+        if (m_issued && m_issued_h) (void)WaitRows(m_issued_h);
         m_issued = false;
     }
 
@@ -564,19 +572,19 @@ private:
         if (words > m_frame_cap)
         {
             DrainFrame();
-            if (m_frame) rt_host_free(m_frame);
+            if (m_frame) FreeHost(m_frame);
             m_frame = nullptr;
             m_frame_cap = 0;
             void* p = nullptr;
-            const int rc = rt_host_alloc(words * 4, &p);
-            if (rc != RT_OK) { SetError(rc); return; }
+            const int rc = AllocHost(words * 4, &p);
+            if (rc != RT_OK) { m_status = rc; return; }
             m_frame = static_cast<uint32_t*>(p);
             m_frame_cap = words;
         }
         rt_frame f;
         std::memset(&f, 0, sizeof(f));
-        std::memcpy(f.cam, m_host->cam, sizeof(f.cam));         // Scene::GetCameraParameters
-        f.fov = m_host->fov;
+        std::memcpy(f.cam, m_host_cam, sizeof(f.cam));          // Scene::GetCameraParameters
+        f.fov = m_host_fov;
         f.width = m_width;
         f.height = m_height;
         f.spp = m_spp;
@@ -592,14 +600,17 @@ private:
             const uint32_t e = (j == kTilesY - 1) ? m_height : (j + 1) * (m_height / kTilesY);
             if (e > (nb ? ends[nb - 1] : 0u)) ends[nb++] = e;
         }
-        const int rc = rt_render_frame_host(m_gpu, &f, m_frame, ends, nb);
-        if (rc != RT_OK) { SetError(rc); return; }
+        const int rc = Issue(f, m_frame, ends, nb);
+        if (rc != RT_OK) { m_status = rc; return; }
         m_issued = true;
         m_issued_h = m_height;
     }
 
-    rt_scene* m_gpu;
-    const rth_scene* m_host;
+protected:
+    float m_host_cam[16] = {};
+    float m_host_fov = 45.0f;
+
+private:
     uint32_t m_spp = 16;                                        // renderer.h:34
     uint32_t m_tri_test = RT_TRI_MOLLER_TRUMBORE, m_kernel = RT_KERNEL_AUTO, m_isect = RT_ISECT_GRID;
     std::mutex m_frame_mtx;
@@ -610,14 +621,338 @@ private:
     uint32_t m_issued_h = 0;
     std::atomic<uint32_t> m_tiles_done{ 0 };
     int m_status = RT_OK;
-    std::string m_err;
+};
+
+// One device: librt_tracer renders the frame in one launch and copies it back in row bands
+// (rt_render_frame_host / rt_frame_host_wait).
+class GpuRenderer : public FrameRenderer
+{
+public:
+    GpuRenderer(rt_scene* gpu, const rth_scene* host, uint32_t nthreads) : FrameRenderer(nthreads), m_gpu(gpu)
+    {
+        std::memcpy(m_host_cam, host->cam, sizeof(m_host_cam));
+        m_host_fov = host->fov;
+    }
+    ~GpuRenderer() override
+    {
+        Shutdown();
+        ReleaseFrame();
+    }
+
+protected:
+    int Issue(const rt_frame& f, uint32_t* host_frame, const uint32_t* ends, uint32_t nb) override
+    {
+        return Check(rt_render_frame_host(m_gpu, &f, host_frame, ends, nb));
+    }
+    int WaitRows(uint32_t y1) override { return Check(rt_frame_host_wait(m_gpu, y1)); }
+    int AllocHost(size_t bytes, void** p) override { return Check(rt_host_alloc(bytes, p)); }
+    void FreeHost(void* p) override { (void)rt_host_free(p); }
+
+private:
+    int Check(int rc)
+    {
+        if (rc != RT_OK)
+        {
+            char msg[512];
+            rt_last_error(msg, sizeof(msg));
+            m_err = msg;
+        }
+        return rc;
+    }
+    rt_scene* m_gpu;
+};
+
+// ================================================================= multi-GPU frame source
+// RCCL (librccl.so.1), loaded on the first multi-device framebuffer: single-device users never
+// map it, and in a process that already holds one (torch) the loader returns that one.
+struct RcclApi
+{
+    ncclResult_t (*CommInitAll)(ncclComm_t*, int, const int*) = nullptr;
+    ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*Send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*Recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*GroupStart)() = nullptr;
+    ncclResult_t (*GroupEnd)() = nullptr;
+    const char* (*ErrorString)(ncclResult_t) = nullptr;
+};
+
+const RcclApi* rccl_api(std::string& err)
+{
+    static std::mutex mtx;
+    static RcclApi api;
+    static bool tried = false, ok = false;
+    static std::string why;
+    std::lock_guard<std::mutex> g(mtx);
+    if (!tried)
+    {
+        tried = true;
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h)
+            why = std::string("cannot load librccl.so.1: ") + dlerror();
+        else
+        {
+            ok = true;
+            auto sym = [&](const char* name) {
+                void* f = dlsym(h, name);
+                if (!f) { ok = false; why = std::string("librccl.so.1 lacks ") + name; }
+                return f;
+            };
+            api.CommInitAll = reinterpret_cast<decltype(api.CommInitAll)>(sym("ncclCommInitAll"));
+            api.CommDestroy = reinterpret_cast<decltype(api.CommDestroy)>(sym("ncclCommDestroy"));
+            api.Send = reinterpret_cast<decltype(api.Send)>(sym("ncclSend"));
+            api.Recv = reinterpret_cast<decltype(api.Recv)>(sym("ncclRecv"));
+            api.GroupStart = reinterpret_cast<decltype(api.GroupStart)>(sym("ncclGroupStart"));
+            api.GroupEnd = reinterpret_cast<decltype(api.GroupEnd)>(sym("ncclGroupEnd"));
+            api.ErrorString = reinterpret_cast<decltype(api.ErrorString)>(sym("ncclGetErrorString"));
+        }
+    }
+    err = why;
+    return ok ? &api : nullptr;
+}
+
+constexpr uint32_t kMaxRanks = 64;
+
+// The Framebuffer's RenderTile served by N GPUs of this node (the drop-in for the
+// CPU pool of framebuffer.cpp:16-28, 59-92): the scene is replicated on every device (one
+// rt_scene each), device i renders rank i's interleaved 16x16 tiles compactly
+// (rt_render_shard_device), ONE gather collects the shards on devices[0], K3 un-permutes them
+// (rt_unshard_device) and the frame comes back in tile-row bands.  The gather is RCCL when every
+// device is listed once (ncclCommInitAll in this process, then one group of ncclSend on every
+// rank -- rank 0 to itself -- and ncclRecv of every rank's slice on rank 0: each peer's slice on
+// its own xGMI link, not an all-gather ring).  A device listed more than once holds several
+// logical ranks (a rehearsal of N ranks on fewer GPUs); RCCL takes each device once, so those
+// shards move by device copies instead.
+class MultiGpuRenderer : public FrameRenderer
+{
+public:
+    MultiGpuRenderer(const rth_scene* host, uint32_t nthreads) : FrameRenderer(nthreads)
+    {
+        std::memcpy(m_host_cam, host->cam, sizeof(m_host_cam));
+        m_host_fov = host->fov;
+    }
+
+    ~MultiGpuRenderer() override
+    {
+        Shutdown();
+        ReleaseFrame();
+        for (uint32_t i = 0; i < m_n; i++)
+        {
+            (void)hipSetDevice(m_dev[i]);
+            if (m_stream[i]) (void)hipStreamSynchronize(m_stream[i]);
+        }
+        for (uint32_t i = 0; i < m_n; i++)
+        {
+            (void)hipSetDevice(m_dev[i]);
+            if (m_comm[i] && m_rccl) (void)m_rccl->CommDestroy(m_comm[i]);
+            if (m_shard[i]) (void)hipFree(m_shard[i]);
+            if (m_done[i]) (void)hipEventDestroy(m_done[i]);
+            if (m_stream[i]) (void)hipStreamDestroy(m_stream[i]);
+            if (m_scene[i]) (void)rt_scene_destroy(m_scene[i]);
+        }
+        if (m_n)
+        {
+            (void)hipSetDevice(m_dev[0]);
+            if (m_gathered) (void)hipFree(m_gathered);
+            if (m_dframe) (void)hipFree(m_dframe);
+            for (hipEvent_t e : m_band_ev) if (e) (void)hipEventDestroy(e);
+        }
+    }
+
+    int Init(const rth_scene* host, const int* devices, uint32_t n)
+    {
+        m_n = n;
+        rt_scene_desc d;
+        std::memset(&d, 0, sizeof(d));
+        fill_desc(*host, d);
+        bool distinct = true;
+        for (uint32_t i = 0; i < n; i++)
+        {
+            m_dev[i] = devices[i];
+            for (uint32_t j = 0; j < i; j++) distinct = distinct && devices[j] != devices[i];
+            // one scene per rank (its own heavy-first state, as one process per GPU would have)
+            int rc = rt_scene_create(&d, devices[i], &m_scene[i]);
+            if (rc) return TracerError(rc);
+            if ((rc = Hip(hipSetDevice(devices[i]), "hipSetDevice"))) return rc;
+            if ((rc = Hip(hipStreamCreateWithFlags(&m_stream[i], hipStreamNonBlocking), "hipStreamCreate"))) return rc;
+            if ((rc = Hip(hipEventCreateWithFlags(&m_done[i], hipEventDisableTiming), "hipEventCreate"))) return rc;
+        }
+        m_transport = distinct ? RTH_TRANSPORT_RCCL : RTH_TRANSPORT_DEVICE_COPY;
+        if (distinct)
+        {
+            std::string why;
+            m_rccl = rccl_api(why);
+            if (!m_rccl) { m_err = why; return RT_E_RCCL; }
+            if (int rc = Nccl(m_rccl->CommInitAll(m_comm, int(n), devices), "ncclCommInitAll")) return rc;
+        }
+        return RT_OK;
+    }
+
+    const std::string& InitError() const { return m_err; }
+    uint32_t Transport() const { return m_transport; }
+    uint32_t Ranks() const { return m_n; }
+
+protected:
+    int AllocHost(size_t bytes, void** p) override
+    {
+        if (int rc = Hip(hipSetDevice(m_dev[0]), "hipSetDevice")) return rc;
+        return Hip(hipHostMalloc(p, bytes), "hipHostMalloc");
+    }
+    void FreeHost(void* p) override { (void)hipHostFree(p); }
+
+    int Issue(const rt_frame& f, uint32_t* host_frame, const uint32_t* ends, uint32_t nb) override
+    {
+        uint64_t elems = 0;
+        int rc = rt_shard_elems(f.width, f.height, m_n, &elems);
+        if (rc) return TracerError(rc);
+        if ((rc = Buffers(elems, size_t(f.width) * f.height))) return rc;
+        // (1) every rank renders its tiles on its own device and stream
+        for (uint32_t i = 0; i < m_n; i++)
+            if ((rc = rt_render_shard_device(m_scene[i], &f, i, m_n, m_shard[i], m_stream[i]))) return TracerError(rc);
+        // (2) one gather to rank 0
+        if (m_transport == RTH_TRANSPORT_RCCL)
+        {
+            if ((rc = Nccl(m_rccl->GroupStart(), "ncclGroupStart"))) return rc;
+            for (uint32_t i = 0; i < m_n && !rc; i++)
+                rc = Nccl(m_rccl->Send(m_shard[i], elems, ncclUint32, 0, m_comm[i], m_stream[i]), "ncclSend");
+            for (uint32_t i = 0; i < m_n && !rc; i++)
+                rc = Nccl(m_rccl->Recv(m_gathered + i * elems, elems, ncclUint32, int(i), m_comm[0], m_stream[0]),
+                          "ncclRecv");
+            const int rc2 = Nccl(m_rccl->GroupEnd(), "ncclGroupEnd");
+            if (rc || rc2) return rc ? rc : rc2;
+        }
+        else
+            for (uint32_t i = 0; i < m_n; i++)
+            {
+                if ((rc = Hip(hipSetDevice(m_dev[i]), "hipSetDevice")) ||
+                    (rc = Hip(hipEventRecord(m_done[i], m_stream[i]), "hipEventRecord")) ||
+                    (rc = Hip(hipSetDevice(m_dev[0]), "hipSetDevice")) ||
+                    (rc = Hip(hipStreamWaitEvent(m_stream[0], m_done[i], 0), "hipStreamWaitEvent")) ||
+                    (rc = Hip(hipMemcpyPeerAsync(m_gathered + i * elems, m_dev[0], m_shard[i], m_dev[i], elems * 4,
+                                                 m_stream[0]), "hipMemcpyPeerAsync")))
+                    return rc;
+            }
+        // (3) K3 un-permute on rank 0, (4) copy-back in tile-row bands
+        if ((rc = Hip(hipSetDevice(m_dev[0]), "hipSetDevice"))) return rc;
+        if ((rc = rt_unshard_device(f.width, f.height, m_n, m_gathered, m_dframe, m_stream[0]))) return TracerError(rc);
+        m_nbands = 0;
+        for (uint32_t b = 0, ya = 0; b < nb; b++)
+        {
+            const uint32_t yb = ends[b];
+            if (!m_band_ev[b] && (rc = Hip(hipEventCreateWithFlags(&m_band_ev[b], hipEventDisableTiming), "hipEventCreate")))
+                return rc;
+            if ((rc = Hip(hipMemcpyAsync(host_frame + size_t(ya) * f.width, m_dframe + size_t(ya) * f.width,
+                                         size_t(yb - ya) * f.width * 4, hipMemcpyDeviceToHost, m_stream[0]),
+                          "hipMemcpyAsync")) ||
+                (rc = Hip(hipEventRecord(m_band_ev[b], m_stream[0]), "hipEventRecord")))
+                return rc;
+            m_band_y1[b] = yb;
+            m_nbands = b + 1;
+            ya = yb;
+        }
+        return RT_OK;
+    }
+
+    int WaitRows(uint32_t y1) override
+    {
+        if (!m_nbands) return RT_OK;
+        uint32_t b = 0;
+        while (b + 1 < m_nbands && m_band_y1[b] < y1) b++;
+        return Hip(hipEventSynchronize(m_band_ev[b]), "hipEventSynchronize");
+    }
+
+private:
+    static void fill_desc(const rth_scene& s, rt_scene_desc& d)        // as rth_scene_desc
+    {
+        d.num_vertices = uint32_t(s.verts.size());
+        d.num_triangles = uint32_t(s.tris.size());
+        d.vertices = s.verts.data();
+        d.triangles = s.tris.data();
+        for (int a = 0; a < 3; a++)
+        {
+            d.grid.dims[a] = s.dims[a];
+            d.grid.aabb_min[a] = s.bmin[a];
+            d.grid.aabb_max[a] = s.bmax[a];
+        }
+        d.grid.cell_wdh = s.cw;
+        d.grid.inv_cell_wdh = s.icw;
+        d.grid.cell_offsets = s.off.data();
+        d.grid.cell_tris = s.refs.data();
+    }
+
+    int Buffers(uint64_t elems, size_t frame_words)
+    {
+        int rc;
+        if (elems > m_elems_cap)
+        {
+            for (uint32_t i = 0; i < m_n; i++)
+            {
+                if ((rc = Hip(hipSetDevice(m_dev[i]), "hipSetDevice"))) return rc;
+                if (m_shard[i]) (void)hipFree(m_shard[i]);
+                m_shard[i] = nullptr;
+                if ((rc = Hip(hipMalloc(&m_shard[i], elems * 4), "hipMalloc"))) return rc;
+            }
+            if ((rc = Hip(hipSetDevice(m_dev[0]), "hipSetDevice"))) return rc;
+            if (m_gathered) (void)hipFree(m_gathered);
+            m_gathered = nullptr;
+            if ((rc = Hip(hipMalloc(&m_gathered, elems * 4 * m_n), "hipMalloc"))) return rc;
+            m_elems_cap = elems;
+        }
+        if (frame_words > m_frame_cap)
+        {
+            if ((rc = Hip(hipSetDevice(m_dev[0]), "hipSetDevice"))) return rc;
+            if (m_dframe) (void)hipFree(m_dframe);
+            m_dframe = nullptr;
+            if ((rc = Hip(hipMalloc(&m_dframe, frame_words * 4), "hipMalloc"))) return rc;
+            m_frame_cap = frame_words;
+        }
+        return RT_OK;
+    }
+
+    int Hip(hipError_t e, const char* what)
+    {
+        if (e == hipSuccess) return RT_OK;
+        m_err = std::string(what) + ": " + hipGetErrorString(e);
+        return RT_E_HIP;
+    }
+    int Nccl(ncclResult_t r, const char* what)
+    {
+        if (r == ncclSuccess) return RT_OK;
+        m_err = std::string(what) + ": " + (m_rccl ? m_rccl->ErrorString(r) : "RCCL not loaded");
+        return RT_E_RCCL;
+    }
+    int TracerError(int rc)
+    {
+        char msg[512];
+        rt_last_error(msg, sizeof(msg));
+        m_err = msg;
+        return rc;
+    }
+
+    uint32_t m_n = 0;
+    uint32_t m_transport = RTH_TRANSPORT_NONE;
+    const RcclApi* m_rccl = nullptr;
+    int m_dev[kMaxRanks] = {};
+    rt_scene* m_scene[kMaxRanks] = {};
+    hipStream_t m_stream[kMaxRanks] = {};
+    hipEvent_t m_done[kMaxRanks] = {};
+    ncclComm_t m_comm[kMaxRanks] = {};
+    uint32_t* m_shard[kMaxRanks] = {};
+    uint64_t m_elems_cap = 0;
+    uint32_t* m_gathered = nullptr;                             // devices[0]: [rank][shard]
+    uint32_t* m_dframe = nullptr;                               // devices[0]: the frame
+    size_t m_frame_cap = 0;
+    hipEvent_t m_band_ev[16] = {};
+    uint32_t m_band_y1[16] = {};
+    uint32_t m_nbands = 0;
 };
 
 } // namespace
 
 struct rth_framebuffer
 {
-    std::unique_ptr<GpuRenderer> r;
+    std::unique_ptr<FrameRenderer> r;
+    const MultiGpuRenderer* multi = nullptr;      // rth_framebuffer_create_multi only
 };
 
 extern "C" {
@@ -739,6 +1074,30 @@ int rth_framebuffer_create(rt_scene* gpu, const rth_scene* host, uint32_t nthrea
     std::unique_ptr<rth_framebuffer> fb(new rth_framebuffer());
     fb->r.reset(new GpuRenderer(gpu, host, nthreads));
     *out = fb.release();
+    return RT_OK;
+}
+
+int rth_framebuffer_create_multi(const rth_scene* host, const int* devices, uint32_t ndevices, uint32_t nthreads,
+                                 rth_framebuffer** out)
+{
+    if (!host || !devices || !out || ndevices == 0 || ndevices > kMaxRanks)
+        return fail(RT_E_INVALID, "bad arguments (1 <= ndevices <= 64)");
+    *out = nullptr;
+    std::unique_ptr<MultiGpuRenderer> m(new MultiGpuRenderer(host, nthreads));
+    const int rc = m->Init(host, devices, ndevices);
+    if (rc) return fail(rc, m->InitError());
+    std::unique_ptr<rth_framebuffer> fb(new rth_framebuffer());
+    fb->multi = m.get();
+    fb->r.reset(m.release());
+    *out = fb.release();
+    return RT_OK;
+}
+
+int rth_framebuffer_transport(const rth_framebuffer* fb, uint32_t* transport, uint32_t* nranks)
+{
+    if (!fb || !transport || !nranks) return fail(RT_E_INVALID, "NULL argument");
+    *transport = fb->multi ? fb->multi->Transport() : RTH_TRANSPORT_NONE;
+    *nranks = fb->multi ? fb->multi->Ranks() : 1u;
     return RT_OK;
 }
 

@@ -76,6 +76,22 @@ typedef struct rth_framebuffer rth_framebuffer;
  * copies its own tile.  nthreads 0 = hardware_concurrency (framebuffer.cpp:11). */
 int  rth_framebuffer_create(rt_scene *gpu_scene, const rth_scene *host_scene, uint32_t nthreads,
                             rth_framebuffer **out);
+/* The same Framebuffer with its RenderTile served by several GPUs of this node -- the native
+ * multi-GPU drop-in for the CPU pool of framebuffer.cpp:16-28, 59-92.  The scene is
+ * replicated on every device (one rt_scene per entry of devices[], created here); per frame,
+ * device i renders rank i's interleaved 16x16 tiles (rt_render_shard_device), ONE gather brings
+ * every shard to devices[0], rt_unshard_device rebuilds the frame there and it is copied back in
+ * tile-row bands to the tiles, as in rth_framebuffer_create.  When every device is listed once
+ * the gather is RCCL: ncclCommInitAll over devices[] in this process, then one group of ncclSend
+ * (every rank, rank 0 to itself) and ncclRecv (rank 0, one slice per rank) -- each peer's slice on
+ * its own xGMI link.  A device listed more than once holds several logical ranks (a rehearsal of
+ * N ranks on fewer GPUs): RCCL takes each device once, so those shards move by device copies.
+ * RCCL (librccl.so.1) is loaded on first use; RCCL failures return RT_E_RCCL. */
+int  rth_framebuffer_create_multi(const rth_scene *host_scene, const int *devices, uint32_t ndevices,
+                                  uint32_t nthreads, rth_framebuffer **out);
+enum rth_transport { RTH_TRANSPORT_NONE = 0, RTH_TRANSPORT_RCCL = 1, RTH_TRANSPORT_DEVICE_COPY = 2 };
+/* How a framebuffer gathers its shards (enum rth_transport; NONE = one device) and its rank count. */
+int  rth_framebuffer_transport(const rth_framebuffer *fb, uint32_t *transport, uint32_t *nranks);
 void rth_framebuffer_free(rth_framebuffer *fb);
 int  rth_framebuffer_set_sample_count(rth_framebuffer *fb, uint32_t spp);   /* renderer.cpp:18-22 */
 int  rth_framebuffer_set_options(rth_framebuffer *fb, uint32_t tri_test, uint32_t kernel);

@@ -82,3 +82,14 @@ def test_library_build_hash_matches_sources():
     """The hash baked into the loaded librt_tracer.so at build time is the hash of the kernel
     sources on disk (bench.py refuses PMC counters of another build by this value)."""
     assert rtm.library_build_hash() == rtm.kernel_source_hash()
+
+
+def test_multi_gpu_framebuffer_argument_checks():
+    """rth_framebuffer_create_multi refuses an empty or oversized device list before touching a
+    GPU or RCCL (librccl.so.1 is loaded on first real use only)."""
+    L = rtm.host_lib()
+    out = ctypes.c_void_p()
+    dv = (ctypes.c_int * 1)(0)
+    assert L.rth_framebuffer_create_multi(None, dv, 1, 0, ctypes.byref(out)) == 1
+    assert L.rth_framebuffer_create_multi(ctypes.c_void_p(1), dv, 0, 0, ctypes.byref(out)) == 1
+    assert L.rth_framebuffer_create_multi(ctypes.c_void_p(1), dv, 65, 0, ctypes.byref(out)) == 1

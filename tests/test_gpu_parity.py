@@ -746,3 +746,33 @@ def test_scene_validation_fails_loudly():
     assert L.rt_scene_create(ctypes.byref(d), 0, ctypes.byref(h)) == 1     # RT_E_INVALID
     d = hs.desc()
     assert L.rt_scene_create(ctypes.byref(d), 99, ctypes.byref(h)) == 3    # RT_E_NODEVICE
+
+
+@pytest.mark.parametrize("sid,devices", [(1, [0]), (8, [0]), (1, [0, 0]), (8, [0] * 4), (5, [0] * 8)])
+def test_multi_gpu_framebuffer(golden, sid, devices, tmp_path):
+    """The native multi-GPU drop-in (rth_framebuffer_create_multi, librt_host): one rt_scene per
+    rank, every rank's shard rendered on its device, one gather to devices[0], K3 un-permute and
+    the banded copy-back to the 12x9 tiles.  [0]: one rank through RCCL (ncclCommInitAll over one
+    device; rank 0's shard moves by ncclSend / ncclRecv to itself).  Repeated devices: logical
+    ranks sharing GPU 0, shards moved by device copies (RCCL takes each device once).  Frames and
+    BMP bytes equal the reference's; three frames each, so the ranks' heavy-first / wide-section
+    state is exercised."""
+    hs = rtm.HostScene.load(sid)
+    r = rtm.Renderer.multi(hs, devices, nthreads=8)
+    try:
+        want_t = rtm.RTH_TRANSPORT_RCCL if len(set(devices)) == len(devices) else rtm.RTH_TRANSPORT_DEVICE_COPY
+        assert r.transport() == (want_t, len(devices))
+        r.set_sample_count(4)
+        r.resize(1920, 1080)
+        want = golden["frames_1080p4"][str(sid)]["bgra_sha256"]
+        assert hashlib.sha256(r.read().tobytes()).hexdigest() == want
+        for _ in range(2):
+            r.start_rendering()
+            assert hashlib.sha256(r.read().tobytes()).hexdigest() == want
+        if sid == 1:
+            bmp = tmp_path / "multi.bmp"
+            r.save_to_bmp(str(bmp))
+            assert hashlib.sha256(bmp.read_bytes()).hexdigest() == golden["bmp"]["sha256"]
+    finally:
+        r.close()
+        hs.close()
