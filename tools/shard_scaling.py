@@ -5,10 +5,13 @@ before the gather.  Per (scene, kernel, N, rank): median of HIP-event times arou
 render_shard_device (all kernels of the launch) over 8 reps after 3 warm-ups (heavy-first
 planning frames included).  pair_max_ms[k][N] = max over ranks of (Cornell + killeroo).
 
-    python3 tools/shard_scaling.py [--steady] [kernel ...]   (default: 0 = AUTO, 0x100 = lane kernel only)
+    python3 tools/shard_scaling.py [--steady] [--scenes 1 8 5] [--frame W H SPP] [--out NAME] [kernel ...]
+(kernels default: 0 = AUTO, 1 = the plain lane kernel)
 --steady: per-launch time of 32 back-to-back launches of the rank (bench.py's steady state, no
 per-launch events) instead of the median of single launches each between its own events.
+--scenes 4 --frame 4096 4096 16: BASELINE config 4 (head), its own 8-way shard shape.
 """
+import argparse
 import importlib.util
 import json
 import os
@@ -23,12 +26,19 @@ sys.modules["rtm"] = rtm
 spec.loader.exec_module(rtm)
 torch.cuda.set_device(0)
 st = torch.cuda.current_stream()
-W, H, SPP = 1920, 1080, 4
-STEADY = "--steady" in sys.argv
-kernels = [int(k, 0) for k in sys.argv[1:] if k != "--steady"] or [0, 0x100]
+ap = argparse.ArgumentParser()
+ap.add_argument("--steady", action="store_true")
+ap.add_argument("--scenes", type=int, nargs="+", default=[1, 8, 5])
+ap.add_argument("--frame", type=int, nargs=3, default=[1920, 1080, 4])
+ap.add_argument("--out", default=None)
+ap.add_argument("kernels", nargs="*")
+A = ap.parse_args()
+W, H, SPP = A.frame
+STEADY = A.steady
+kernels = [int(k, 0) for k in A.kernels] or [0, 1]
 NS = (1, 2, 4, 8)
-res = {"per_rank": {}, "pair_max_ms": {}, "scene_max_ms": {}}
-for sid in (1, 8, 5):
+res = {"frame": [W, H, SPP], "steady": STEADY, "per_rank": {}, "pair_max_ms": {}, "scene_max_ms": {}}
+for sid in A.scenes:
     g = rtm.GpuScene(rtm.HostScene.load(sid), 0)
     for k in kernels:
         f = g.frame(W, H, SPP, kernel=k)
@@ -62,10 +72,18 @@ for sid in (1, 8, 5):
             res["scene_max_ms"][f"s{sid}_k{k:#x}_n{n}"] = max(res["per_rank"][f"s{sid}_k{k:#x}_n{n}_r{r}"] for r in range(n))
         print(sid, k, {n: res["scene_max_ms"][f"s{sid}_k{k:#x}_n{n}"] for n in NS}, flush=True)
     g.close()
-for k in kernels:
-    res["pair_max_ms"][f"{k:#x}"] = {n: round(max(res["per_rank"][f"s1_k{k:#x}_n{n}_r{r}"] + res["per_rank"][f"s8_k{k:#x}_n{n}_r{r}"]
-                                                 for r in range(n)), 4) for n in NS}
-print(json.dumps(res["pair_max_ms"]))
+if 1 in A.scenes and 8 in A.scenes:
+    for k in kernels:
+        res["pair_max_ms"][f"{k:#x}"] = {n: round(max(res["per_rank"][f"s1_k{k:#x}_n{n}_r{r}"] +
+                                                      res["per_rank"][f"s8_k{k:#x}_n{n}_r{r}"] for r in range(n)), 4)
+                                         for n in NS}
+for sid in A.scenes:
+    for k in kernels:
+        base = res["scene_max_ms"][f"s{sid}_k{k:#x}_n1"]
+        res.setdefault("speedup_vs_n1", {})[f"s{sid}_k{k:#x}"] = {
+            n: round(base / res["scene_max_ms"][f"s{sid}_k{k:#x}_n{n}"], 3) for n in NS}
+print(json.dumps({"pair_max_ms": res["pair_max_ms"], "speedup_vs_n1": res.get("speedup_vs_n1")}))
 os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
 lib = os.path.splitext(os.path.basename(os.environ.get("RT_TRACER_LIB", "librt_tracer.so")))[0]
-json.dump(res, open(os.path.join(ROOT, "gpurun_out", f"shard_scaling_{lib}{'_steady' if STEADY else ''}.json"), "w"), indent=1)
+name = A.out or f"shard_scaling_{lib}{'_steady' if STEADY else ''}"
+json.dump(res, open(os.path.join(ROOT, "gpurun_out", name + ".json"), "w"), indent=1)
