@@ -148,6 +148,10 @@ def moving_camera(work, steps, warmup, static_ms):
         frames.append(pair)
 
     def step(i):
+        if work.batch:
+            work.rtm.render_batch_device([g for _, _, g, _ in work.scenes], [p[i & 1] for p in frames],
+                                         [b.data_ptr() for b in work.bufs], stream=work.stream.cuda_stream)
+            return
         for j, (sid, hs, gs, f) in enumerate(work.scenes):
             gs.render_frame_device(frames[j][i & 1], work.bufs[j].data_ptr(), work.stream.cuda_stream)
 
@@ -201,6 +205,20 @@ def valu_roofline(rtm, kernel_ms, args, world, algorithmic):
         roof["counters"] = f"refused: counters are for {c.get('workload')}, not {want}"
         return roof
     sc = c["scenes"]
+    if "batch" in kernel_ms:
+        # the step is ONE batched launch (k_render_batch): counters of that launch
+        if "batch" not in sc:
+            roof["counters"] = "refused: counters are per-scene launches, the timed step is a batched launch"
+            return roof
+        rate = sc["batch"]["SQ_INSTS_VALU"] / (kernel_ms["batch"] / 1e3)
+        roof.update({"achieved": round(rate / 1e9, 1), "frac": round(rate / VALU_PEAK, 4),
+                     "traffic": sc["batch"]["hbm_bytes"],
+                     "traffic_unit": "HBM bytes per batched launch (every scene's frame)",
+                     "counters": f"{os.path.relpath(path, ROOT)} (batched launch), source hash {src}"})
+        return roof
+    if "batch" in sc:
+        roof["counters"] = "refused: counters are of the batched launch, the timed step is per-scene launches"
+        return roof
     insts = sum(sc[str(sid)]["SQ_INSTS_VALU"] for sid in SCENES)
     rate = insts / (sum(kernel_ms.values()) / 1e3)
     roof.update({"achieved": round(rate / 1e9, 1), "frac": round(rate / VALU_PEAK, 4),
@@ -245,11 +263,14 @@ def cpu_baseline(rtm_unused=None):
 
 
 class GpuWorkload:
-    """The bench workload on this rank's GPU: one frame of every scene per step."""
+    """The bench workload on this rank's GPU: one frame of every scene per step.  batch: every
+    scene's frame of a step in ONE launch (rt_render_batch_device, up to 4 frames per launch), so
+    one frame's tail overlaps the others' work; else one launch per frame."""
 
-    def __init__(self, rtm, torch, world, rank, local, kernel):
+    def __init__(self, rtm, torch, world, rank, local, kernel, batch=True):
         self.rtm, self.torch, self.world, self.rank = rtm, torch, world, rank
-        self.graphs = None              # per-scene hipGraphs of the render launch (--graph)
+        self.batch = batch
+        self.graphs = None              # hipGraphs of the step's render launch(es) (--graph)
         self.samples = {}               # timed launches per scene in the timed region
         self.gevents = {}
         self.scenes = []
@@ -261,40 +282,46 @@ class GpuWorkload:
         n = W * H if world == 1 else rtm.shard_elems(W, H, world)
         self.bufs = [torch.empty(n, dtype=torch.int32, device="cuda") for _ in SCENES]
         self.frames = [torch.empty(W * H, dtype=torch.int32, device="cuda") for _ in SCENES]
+        # scenes whose kernel-time ring holds a launch's time: every scene, or the first scene of
+        # every batch launch
+        self.timed = list(range(0, len(SCENES), rtm.MAX_BATCH)) if batch else list(range(len(SCENES)))
+
     def stream_ctx(self):
         return self.torch.cuda.stream(self.stream)
 
-    def render(self, i):
+    def render_all(self):
+        """This step's render launch(es): every scene's frame (or this rank's shard of it)."""
         if self.graphs is not None:
-            sid = self.scenes[i][0]
             a = self.torch.cuda.Event(enable_timing=True)
             b = self.torch.cuda.Event(enable_timing=True)
             a.record(self.stream)
-            self.graphs[i].replay()
+            self.graphs.replay()
             b.record(self.stream)
-            self.gevents.setdefault(sid, []).append((a, b))
+            self.gevents.setdefault("step", []).append((a, b))
             return
-        self._launch(i)
+        self._launch()
 
-    def _launch(self, i):
-        sid, hs, gs, f = self.scenes[i]
-        if self.world == 1:
-            gs.render_frame_device(f, self.bufs[i].data_ptr(), self.stream.cuda_stream)
-        else:
-            gs.render_shard_device(f, self.rank, self.world, self.bufs[i].data_ptr(), self.stream.cuda_stream)
+    def _launch(self):
+        st = self.stream.cuda_stream
+        if self.batch:
+            self.rtm.render_batch_device([g for _, _, g, _ in self.scenes], [f for _, _, _, f in self.scenes],
+                                         [b.data_ptr() for b in self.bufs], self.rank, self.world, stream=st)
+            return
+        for i, (sid, hs, gs, f) in enumerate(self.scenes):
+            if self.world == 1:
+                gs.render_frame_device(f, self.bufs[i].data_ptr(), st)
+            else:
+                gs.render_shard_device(f, self.rank, self.world, self.bufs[i].data_ptr(), st)
 
     def capture(self):
-        """One hipGraph per scene holding that scene's render launch (after the warm-up, so the
+        """One hipGraph holding the step's render launch(es) (after the warm-up, so the
         heavy-first order is the one the warm-up frames planned; replays keep it)."""
         self.sync()
-        graphs = []
-        for i in range(len(self.scenes)):
-            g = self.torch.cuda.CUDAGraph()
-            with self.torch.cuda.graph(g, stream=self.stream):
-                self._launch(i)
-            graphs.append(g)
+        g = self.torch.cuda.CUDAGraph()
+        with self.torch.cuda.graph(g, stream=self.stream):
+            self._launch()
         self.sync()
-        self.graphs = graphs
+        self.graphs = g
 
     def reset_times(self):
         self.gevents = {}
@@ -310,19 +337,24 @@ class GpuWorkload:
         self.torch.cuda.synchronize()
 
     def kernel_ms(self, steps):
-        """Mean render-kernel ms per scene over the timed steps: HIP events the library records
-        on the launch stream immediately around each render kernel (rt_kernel_times)."""
-        out = {}
+        """Mean render-kernel ms per step: HIP events the library records on the launch stream
+        immediately around each render launch (rt_kernel_times) -- per scene with one launch per
+        frame, per batch launch (keyed "batch", summed over a step's launches) when batched."""
         if self.graphs is not None:
-            # HIP events on the launch stream around each replay of the scene's one-kernel graph
-            return {sid: float(np.mean([a.elapsed_time(b) for a, b in ev])) for sid, ev in self.gevents.items()}
-        for sid, hs, gs, f in self.scenes:
+            # HIP events on the launch stream around each replay of the step's graph
+            return {"batch" if self.batch else "step": float(np.mean([a.elapsed_time(b) for a, b in self.gevents["step"]]))}
+        out = {}
+        want = min((steps + TIME_EVERY - 1) // TIME_EVERY, 64)
+        for i in self.timed:
+            sid, hs, gs, f = self.scenes[i]
             # every TIME_EVERY-th launch is timed (a timed event pair costs ~10 us of device time)
             t = gs.kernel_times()
-            if len(t) != min((steps + TIME_EVERY - 1) // TIME_EVERY, 64):
+            if len(t) != want:
                 raise SystemExit(f"scene {sid}: {len(t)} kernel times for {steps} timed steps")
             out[sid] = float(np.mean(t))
             self.samples[sid] = len(t)
+        if self.batch:
+            return {"batch": sum(out.values())}
         return out
 
     def close(self):
@@ -374,16 +406,14 @@ def run_steps(work, world, rank, steps, warmup, dist=None, graph=False):
         return work.rtm.all_gather_shards(work.bufs[i], world, out=gathered[i], async_op=True)
 
     def step():
-        pending = []
-        for i in range(len(SCENES)):
-            work.render(i)
-            if world > 1:
-                pending.append(collect(i))
-        for i, (g, h) in enumerate(pending):
-            if h is not None:
-                h.wait()
-            if rank == 0:
-                work.unshard(i, g)
+        work.render_all()
+        if world > 1:
+            pending = [collect(i) for i in range(len(SCENES))]
+            for i, (g, h) in enumerate(pending):
+                if h is not None:
+                    h.wait()
+                if rank == 0:
+                    work.unshard(i, g)
 
     ctx = work.stream_ctx() if hasattr(work, "stream_ctx") else contextlib.nullcontext()
     with ctx:
@@ -425,7 +455,9 @@ def main():
     ap.add_argument("--no-end-to-end", action="store_true")
     ap.add_argument("--no-moving-camera", action="store_true")
     ap.add_argument("--graph", action="store_true",
-                    help="replay each scene's render launch from a hipGraph captured after the warm-up")
+                    help="replay the step's render launch(es) from a hipGraph captured after the warm-up")
+    ap.add_argument("--no-batch", action="store_true",
+                    help="one launch per frame instead of the step's frames in one batched launch")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="bench")
     ap.add_argument("--check", action="store_true",
                     help="after timing, rank 0 compares every assembled frame with a one-GPU render")
@@ -455,7 +487,7 @@ def main():
             dist.init_process_group(args.dist_backend)
 
     rtm = load_package()
-    work = GpuWorkload(rtm, torch, world, rank, local, args.kernel)
+    work = GpuWorkload(rtm, torch, world, rank, local, args.kernel, batch=not args.no_batch)
     elapsed = run_steps(work, world, rank, args.steps, args.warmup, dist if world > 1 else None,
                         graph=args.graph)
     kernel_ms = work.kernel_ms(args.steps)
@@ -468,6 +500,15 @@ def main():
         launch_bytes = {sid: ab[sid]["bytes_per_sample"] * W * H * SPP / world for sid in SCENES}
         achieved = sum(launch_bytes.values()) / (sum(kernel_ms.values()) / 1e3)
         roof = valu_roofline(rtm, kernel_ms, args, world, achieved)
+        per_scene = {}
+        for sid in SCENES:
+            e = {"bytes_per_sample": round(ab[sid]["bytes_per_sample"], 1), "survey_bytes_per_sample": SURVEY_B[sid],
+                 "voxels": round(ab[sid]["voxels"], 2), "tri_tests": round(ab[sid]["tri_tests"], 2),
+                 "hit": round(ab[sid]["hit"], 4)}
+            if sid in kernel_ms:
+                e.update({"kernel_ms": round(kernel_ms[sid], 4), "kernel_ms_samples": work.samples.get(sid),
+                          "kernel_msamples_per_s": round(W * H * SPP / world / kernel_ms[sid] / 1e3, 1)})
+            per_scene[str(sid)] = e
         out = {
             "metric": METRIC[args.workload],
             "value": round(value, 3),
@@ -485,17 +526,13 @@ def main():
             "config": {"workload": f"scenes{list(SCENES)}_{W}x{H}x{SPP}", "scenes": list(SCENES),
                        "width": W, "height": H, "spp": SPP, "kernel": args.kernel,
                        "parallelism": f"tile-shard x{world}" + (" + RCCL gather to rank 0" if world > 1 else ""),
-                       "launch": "hipGraph per scene" if args.graph else "direct",
+                       "launch": ("hipGraph of " if args.graph else "") +
+                                 ("the step's frames batched, <= 4 per launch (rt_render_batch_device)"
+                                  if work.batch else "one launch per frame"),
                        "camera": "static: each scene's own camera every step, so the per-origin "
                                  "triangle records (k_origin_pre) are computed once; see moving_camera"},
-            "per_scene": {str(sid): {"kernel_ms": round(kernel_ms[sid], 4),
-                                     "kernel_ms_samples": work.samples.get(sid),
-                                     "kernel_msamples_per_s": round(W * H * SPP / world / kernel_ms[sid] / 1e3, 1),
-                                     "bytes_per_sample": round(ab[sid]["bytes_per_sample"], 1),
-                                     "survey_bytes_per_sample": SURVEY_B[sid],
-                                     "voxels": round(ab[sid]["voxels"], 2),
-                                     "tri_tests": round(ab[sid]["tri_tests"], 2),
-                                     "hit": round(ab[sid]["hit"], 4)} for sid in SCENES},
+            "kernel_ms_per_step": round(sum(kernel_ms.values()), 4),
+            "per_scene": per_scene,
             "roofline": roof,
             "cpu_baseline": None,
         }

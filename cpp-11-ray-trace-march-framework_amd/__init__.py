@@ -61,8 +61,9 @@ TRACER_SYMBOLS = [
     "rt_debug_rcp_check", "rt_debug_wave_clocks", "rt_debug_heavy_first", "rt_debug_wide_items", "rt_scene_set_timing",
     "rt_sample_table", "rt_last_error", "rt_abi_version", "rt_grid_build", "rt_grid_free",
     "rt_scene_create_from_mesh", "rt_kernel_times", "rt_render_frame_host", "rt_frame_host_wait", "rt_host_alloc",
-    "rt_host_free", "rt_render_hits_device", "rt_scene_info_get", "rt_build_hash",
+    "rt_host_free", "rt_render_hits_device", "rt_scene_info_get", "rt_build_hash", "rt_render_batch_device",
 ]
+MAX_BATCH = 4                            # frames per rt_render_batch_device launch
 HOST_SYMBOLS = [
     "rth_scene_load", "rth_scene_from_mesh", "rth_scene_free", "rth_scene_desc",
     "rth_scene_camera", "rth_scene_stats_get", "rth_framebuffer_create", "rth_framebuffer_free",
@@ -171,6 +172,7 @@ def tracer_lib():
             L.rt_render_hits_device.argtypes = [vp, ctypes.POINTER(Frame), c_u32, c_u32, vp, vp, vp]
             L.rt_scene_info_get.argtypes = [vp, ctypes.POINTER(SceneInfo)]
             L.rt_build_hash.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
+            L.rt_render_batch_device.argtypes = [vp, ctypes.POINTER(Frame), c_u32, c_u32, c_u32, vp, vp, vp]
         L.rt_unshard_device.argtypes = [c_u32, c_u32, c_u32, vp, vp, vp]
         L.rt_last_kernel_ms.argtypes = [vp, ctypes.POINTER(c_f32)]
         L.rt_trace_samples.argtypes = [vp, ctypes.POINTER(Frame), c_u32, c_u32, c_u32, c_u32, vp]
@@ -619,6 +621,21 @@ class GpuScene:
             self.close()
         except Exception:
             pass
+
+
+def render_batch_device(scenes, frames, d_outs, rank=0, nranks=1, d_hits=None, stream=0):
+    """rt_render_batch_device: frames[i] of scenes[i] into device buffer d_outs[i] (frame or the
+    rank's shard), up to MAX_BATCH frames per launch in ONE grid; d_hits[i] (optional) receives
+    per-sample hit IDs.  Same outputs as one render_frame_device / render_shard_device each."""
+    n = len(scenes)
+    assert len(frames) == n and len(d_outs) == n
+    sp = (ctypes.c_void_p * n)(*[g._h.value for g in scenes])
+    fr = (Frame * n)(*frames)
+    outs = (ctypes.c_void_p * n)(*d_outs)
+    hits = (ctypes.c_void_p * n)(*d_hits) if d_hits is not None else None
+    L = tracer_lib()
+    _check(L.rt_render_batch_device(sp, fr, n, rank, nranks, outs, hits, ctypes.c_void_p(stream)), L,
+           "rt_render_batch_device")
 
 
 def shard_elems(width, height, nranks):

@@ -24,6 +24,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstddef>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -216,17 +217,49 @@ __device__ __forceinline__ bool first_active_lane()
 // walk (output, shading, tile bookkeeping) are taken from here, so the compiler reloads them
 // with s_load after the walk instead of holding ~30 SGPRs of them live across it (the render
 // kernels' SGPR budget decides 8 vs 7 waves per SIMD).  The empty asm hides the pointer's
-// origin (a register round trip), so these loads cannot be merged with the kernel entry's.  Only for kernels whose
-// first argument is the KParams.
-__device__ __forceinline__ const KParams& late_params(const KParams& P)
+// origin (a register round trip), so these loads cannot be merged with the kernel entry's.
+// off: byte offset of the frame's KParams in the kernarg segment (0 for the single-frame
+// kernels, whose first argument is the KParams; a frame of KBatch in the batch kernel).
+__device__ __forceinline__ const KParams& late_params(const KParams& P, uint32_t off = 0u)
 {
     (void)P;
-    const uint64_t a = uint64_t(__builtin_amdgcn_kernarg_segment_ptr());
+    const uint64_t a = uint64_t(__builtin_amdgcn_kernarg_segment_ptr()) + off;
     uint32_t lo = uint32_t(a), hi = uint32_t(a >> 32);
     asm volatile("" : "+v"(lo), "+v"(hi));
     lo = __builtin_amdgcn_readfirstlane(lo);
     hi = __builtin_amdgcn_readfirstlane(hi);
     return *(const KParams *)(const __attribute__((address_space(4))) KParams *)((uint64_t(hi) << 32) | lo);
+}
+
+// Multi-frame launch (rt_render_batch_device): up to kMaxBatch frames -- of different scenes --
+// in ONE grid, so one frame's tail overlaps the others' work and the heavy-first order ranks the
+// blocks of all of them.  p[0] also carries the batch's heavy-first / wide-section state (its
+// block and item indices are the launch's, frame-major); every other field is per frame.
+constexpr uint32_t kMaxBatch = 4;
+struct KBatch
+{
+    KParams p[kMaxBatch];
+    uint32_t nframes;
+    uint32_t base[kMaxBatch + 1];   // first launch block of each frame; base[nframes] = all blocks
+};
+
+// The batch kernels' KBatch, re-read from the kernarg segment (as late_params).
+__device__ __forceinline__ const KBatch& late_batch()
+{
+    const uint64_t a = uint64_t(__builtin_amdgcn_kernarg_segment_ptr());
+    uint32_t lo = uint32_t(a), hi = uint32_t(a >> 32);
+    asm volatile("" : "+v"(lo), "+v"(hi));
+    lo = __builtin_amdgcn_readfirstlane(lo);
+    hi = __builtin_amdgcn_readfirstlane(hi);
+    return *(const KBatch *)(const __attribute__((address_space(4))) KBatch *)((uint64_t(hi) << 32) | lo);
+}
+
+// Frame of launch block b (wave-uniform).
+__device__ __forceinline__ uint32_t batch_frame(const KBatch& B, uint32_t b)
+{
+    uint32_t f = 0;
+    for (uint32_t j = 1; j < kMaxBatch; j++) f += (j < B.nframes && b >= B.base[j]) ? 1u : 0u;
+    return f;
 }
 
 // CSR range of a cell: one u32 load of the packed (start << 11 | count) word when the scene
@@ -834,7 +867,8 @@ __device__ __forceinline__ bool ray_march(const KParams& P, float ox, float oy, 
 // (Grid::Intersect's tri_idx, renderer.cpp:105) or kNoTri
 template <bool STATS, int TRI, int VAR>
 __device__ __forceinline__ void trace_sample(const KParams& P, uint32_t px, uint32_t py, uint32_t s, float& cr,
-                                             float& cg, float& cb, uint32_t& hit_tri, rt_sample_rec *rec)
+                                             float& cg, float& cb, uint32_t& hit_tri, rt_sample_rec *rec,
+                                             uint32_t off = 0u)
 {
     const float2 so = P.smp[s];
     float dx, dy, dz;
@@ -850,7 +884,7 @@ __device__ __forceinline__ void trace_sample(const KParams& P, uint32_t px, uint
     else
         hit = grid_intersect<STATS, TRI, VAR>(P, P.org[0], P.org[1], P.org[2], dx, dy, dz, t, u, v, tri, voxel,
                                               steps, tests);
-    const KParams& Q = late_params(P);
+    const KParams& Q = late_params(P, off);
     if constexpr ((VAR & (kVarMarch | kVarBrute)) == 0)
         if ((VAR & kVarOriginPre) && TRI == RT_TRI_MOLLER_TRUMBORE && hit)
             tri = __float_as_uint(Q.refs[3 * size_t(tri) + 2].y);     // CSR reference -> triangle id
@@ -951,7 +985,7 @@ __device__ __forceinline__ ItemCoord item_coord(const KParams& P, uint32_t item,
 // samples across its adjacent lanes in sample order (renderer.cpp:87-122, hazard H10) and
 // stores the packed pixel (renderer.cpp:124-133).
 template <int TRI, int VAR>
-__device__ __forceinline__ void process_item(const KParams& P, uint32_t item)
+__device__ __forceinline__ void process_item(const KParams& P, uint32_t item, uint32_t off = 0u)
 {
     item = __builtin_amdgcn_readfirstlane(item);
     const uint32_t lane = threadIdx.x & 63u;
@@ -960,9 +994,9 @@ __device__ __forceinline__ void process_item(const KParams& P, uint32_t item)
     {
         const ItemCoord ic = item_coord(P, item, lane);
         if (ic.valid)
-            trace_sample<false, TRI, VAR>(P, ic.x, ic.y, ic.s, cr, cg, cb, hit_tri, nullptr);
+            trace_sample<false, TRI, VAR>(P, ic.x, ic.y, ic.s, cr, cg, cb, hit_tri, nullptr, off);
     }
-    const KParams& Q = late_params(P);
+    const KParams& Q = late_params(P, off);
     const ItemCoord ic = item_coord(Q, item, lane);
     // rt_render_hits_device only: the sample's hit triangle, after the walk (a scalar test of a
     // kernel parameter; the walk above is the same code whatever the pointer holds)
@@ -1330,6 +1364,9 @@ __device__ __forceinline__ void wide_samples(const KParams& P, uint32_t k, uint3
 // sample): persistent over the list, so a section smaller than the list (the host sizes it from
 // an older plan's count) still renders every listed item.  They record no cost: an item's cost
 // word keeps its lane-mode measurement until a refresh frame renders it one lane per sample again.
+// In a batch (KBatch, BATCH = true) P is p[0] (the batch's list, launch-wide item indices) and each
+// item is rendered with its own frame's parameters.
+template <bool BATCH>
 __device__ __forceinline__ void wide_section(const KParams& P)
 {
     const uint32_t n = P.hf_ver ? min(P.hf_plan_in->cnt_w, kWhMax) : 0u;
@@ -1338,12 +1375,20 @@ __device__ __forceinline__ void wide_section(const KParams& P)
     const uint32_t ipt = P.wg_per_tile * kWavesPerWG;              // items per tile
     for (uint32_t e = w; e < n * G; e += nw)
     {
-        const uint32_t item = __builtin_amdgcn_readfirstlane(P.wh_list_in[e / G]);
+        uint32_t item = __builtin_amdgcn_readfirstlane(P.wh_list_in[e / G]);
+        uint32_t off = 0u;
+        if constexpr (BATCH)
+        {
+            const KBatch& B = late_batch();
+            const uint32_t f = batch_frame(B, item / kWavesPerWG);
+            item -= B.base[f] * kWavesPerWG;                      // the frame's own item index
+            off = uint32_t(offsetof(KBatch, p)) + f * uint32_t(sizeof(KParams));
+        }
         const uint32_t kseq = item / ipt;
         const uint32_t slot0 = (item - kseq * ipt) * 64u + (e % G) * (64u / G);
         // the parameters re-read per item (late_params): hoisted out of the loop they held ~30
         // more SGPRs across it and spilled
-        const KParams& Q = late_params(P);
+        const KParams& Q = late_params(P, off);
         const uint32_t k = Q.tile_order ? Q.tile_order[kseq] : kseq;
         if (G == 16u) wide_samples<kVarWide, 16>(Q, k, slot0);
         else wide_samples<kVarWide, 4>(Q, k, slot0);
@@ -1414,7 +1459,40 @@ __global__ void __launch_bounds__(kWG) k_render_lanes(KParams P)
 // (its own register allocation: folded into the lane kernel it cost 106 SGPRs and spills)
 __global__ void __launch_bounds__(kWG) k_render_wh(KParams P)
 {
-    wide_section(P);
+    wide_section<false>(P);
+}
+
+// The multi-frame launch (KBatch): the launch's blocks are the frames' blocks, frame-major; the
+// heavy-first order (p[0]'s state) ranks them all, and every wave renders its item with its own
+// frame's parameters (KParams re-read from the kernarg segment at the frame's offset).
+template <int TRI, int VAR>
+__global__ void __launch_bounds__(kWG) k_render_batch(KBatch B)
+{
+    __shared__ uint32_t t0s[kWavesPerWG];
+    volatile uint32_t *t0v = t0s;                 // a wave's start time waits in LDS across the walk
+    uint32_t b;
+    if (!block_of_launch<VAR>(B.p[0], b)) return;
+    const uint32_t gitem = b * kWavesPerWG + (threadIdx.x >> 6);       // launch-wide item
+    if constexpr ((VAR & kVarWideHeavy) != 0)
+        if (B.p[0].wh_wgs && B.p[0].hf_ver && B.p[0].wh_mark_in[gitem] == B.p[0].hf_ver) return;
+    const uint32_t f = batch_frame(B, b);
+    const uint32_t off = uint32_t(offsetof(KBatch, p)) + f * uint32_t(sizeof(KParams));
+    const uint32_t item = gitem - B.base[f] * kWavesPerWG;
+    const bool hf = B.p[0].hf_measure != 0u;
+    if (hf && (threadIdx.x & 63u) == 0u) t0v[threadIdx.x >> 6] = uint32_t(__builtin_amdgcn_s_memtime());
+    process_item<TRI, VAR>(late_params(B.p[0], off), item, off);
+    const KParams& Q = late_params(B.p[0], uint32_t(offsetof(KBatch, p)));
+    if (Q.hf_measure)
+    {
+        const uint32_t t1 = uint32_t(__builtin_amdgcn_s_memtime());
+        const uint32_t t0 = __builtin_amdgcn_readfirstlane(t0v[threadIdx.x >> 6]);
+        if ((threadIdx.x & 63u) == 0u) Q.hf_cost[__builtin_amdgcn_readfirstlane(gitem)] = t1 - t0;
+    }
+}
+
+__global__ void __launch_bounds__(kWG) k_render_wh_batch(KBatch B)
+{
+    wide_section<true>(B.p[0]);
 }
 
 // RT_KERNEL_COMPACT (grid intersector, spp a power of two <= 64): wavefront active-ray
@@ -1873,7 +1951,7 @@ void dist_record(const float *p0, const float *p1, const float *p2, float4 *r)
 // Heavy-first state of one launch shape (device arrays; see KParams::hf_*)
 struct HfCtx
 {
-    uint64_t key[4] = { 0, 0, 0, 0 };   // launch shape: blocks, spp, region, shard, variant
+    uint64_t key[5] = { 0, 0, 0, 0, 0 };   // launch shape: blocks, spp, region, shard, variant, batch
     uint32_t nblocks = 0, front = 0;
     uint32_t cap_blocks = 0;            // allocated marks per buffer
     uint32_t *marks = nullptr;          // [2][cap_blocks]
@@ -2109,11 +2187,13 @@ uint32_t env_tunable(const char *name, uint32_t dflt)
 
 // Heavy-first state for this launch shape (AUTO): fills P.hf_*.  A new shape takes the least
 // recently used context and clears it on the launch stream (no host synchronisation).
-int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hipStream_t st)
+// batch: 0 for a single-frame launch, else an identity of the batch (its scenes and frame count).
+int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hipStream_t st, uint64_t batch = 0)
 {
-    const uint64_t key[4] = { (blocks << 16) | (uint64_t(P.spp) << 1) | 1u,
+    const uint64_t key[5] = { (blocks << 16) | (uint64_t(P.spp) << 1) | 1u,
                               (uint64_t(P.rx0) << 32) | P.ry0, (uint64_t(P.rw) << 32) | P.rh,
-                              (uint64_t(P.rank) << 40) | (uint64_t(P.nranks) << 20) | uint64_t(uint32_t(var) >> 12) };
+                              (uint64_t(P.rank) << 40) | (uint64_t(P.nranks) << 20) | uint64_t(uint32_t(var) >> 12),
+                              batch };
     HfCtx *c = nullptr;
     for (HfCtx& h : s->hf)
         if (std::memcmp(h.key, key, sizeof(key)) == 0) c = &h;
@@ -2395,6 +2475,130 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
         s->kt_last = kslot;
         s->kt_next = (kslot + 1u) % kTimeRing;
         s->kt_count = std::min(s->kt_count + 1u, kTimeRing);
+    }
+    return RT_OK;
+}
+
+
+// k_render_batch instantiation of a variant (nullptr: the frames take one launch each)
+typedef void (*kbfn_t)(KBatch);
+kbfn_t batch_kernel(int var)
+{
+    if (var == kVarAuto) return k_render_batch<RT_TRI_MOLLER_TRUMBORE, kVarAuto>;
+    if (var == (kVarAuto | kVarWideHeavy)) return k_render_batch<RT_TRI_MOLLER_TRUMBORE, kVarAuto | kVarWideHeavy>;
+    return nullptr;
+}
+
+static_assert(sizeof(KBatch) <= 4096, "kernel arguments are limited to 4 KiB");
+
+// n frames (2 <= n <= kMaxBatch, scenes on one device, mutexes held by the caller) in ONE launch
+// of k_render_batch.  P[i] holds frame i's parameters (frame_params + region + shard + outputs).
+// Returns RT_E_INVALID with *batched == false, doing nothing, when the frames cannot share a
+// launch (the caller then renders them one launch each).
+int launch_batch(rt_scene *const *S, const rt_frame *F, uint32_t n, KParams *P, uint32_t n_local_tiles,
+                 hipStream_t st, bool *batched)
+{
+    *batched = false;
+    if (n < 2 || n > kMaxBatch || n_local_tiles == 0) return RT_E_INVALID;
+    const uint32_t spp = P[0].spp;
+    if (!use_lanes(&F[0], spp) || spp > 16u) return RT_E_INVALID;
+    int var = -1;
+    bool wide_heavy = false;
+    for (uint32_t i = 0; i < n; i++)
+    {
+        const uint32_t kind = F[i].kernel & RT_KERNEL_KIND_MASK;
+        if (kind != RT_KERNEL_AUTO || (F[i].kernel & ~uint32_t(RT_KERNEL_FLAG_WIDE_HEAVY)) != 0u) return RT_E_INVALID;
+        if (P[i].isect != RT_ISECT_GRID || P[i].tri_test != RT_TRI_MOLLER_TRUMBORE) return RT_E_INVALID;
+        if (P[i].W != P[0].W || P[i].H != P[0].H || P[i].spp != spp || S[i]->device != S[0]->device)
+            return RT_E_INVALID;
+        const int v = kVarAutoCore | (S[i]->rcp_safe ? kVarFastRcp : 0) |
+                      (S[i]->pack_ok ? kVarPackedRem | kVarSkipRun : 0);
+        if (var >= 0 && v != var) return RT_E_INVALID;
+        var = v;
+        wide_heavy = wide_heavy || (F[i].kernel & RT_KERNEL_FLAG_WIDE_HEAVY) ||
+                     (P[i].nranks >= 2u && S[i]->max_cell_refs >= S[0]->wh_auto_refs);
+    }
+    if (var != kVarAuto) return RT_E_INVALID;
+    const int kvar = var | (wide_heavy ? kVarWideHeavy : 0);
+    const kbfn_t fn = batch_kernel(kvar);
+    if (!fn) return RT_E_INVALID;
+    *batched = true;
+    KBatch KB;
+    std::memset(&KB, 0, sizeof(KB));
+    const uint32_t wgpt = (kTilePix * spp) / kWG;
+    const uint64_t fblocks = uint64_t(n_local_tiles) * wgpt;
+    const uint64_t blocks = fblocks * n;
+    if (blocks > 0x3FFFFFFFull) return fail(RT_E_INVALID, "batch too large for one launch");
+    KB.nframes = n;
+    for (uint32_t i = 0; i <= n; i++) KB.base[i] = uint32_t(fblocks * i);
+    for (uint32_t i = n + 1; i <= kMaxBatch; i++) KB.base[i] = uint32_t(blocks);
+    // per-origin records of every scene, and the cross-stream order of every scene's state
+    for (uint32_t i = 0; i < n; i++)
+    {
+        P[i].wg_per_tile = wgpt;
+        P[i].xcd_chunk = ((P[i].tiles_x + P[i].nranks - 1u) / P[i].nranks) * wgpt;
+        rt_scene *s = S[i];
+        bool first = true;
+        for (uint32_t j = 0; j < i; j++) first = first && S[j] != s;
+        if (!first) continue;
+        if (s->ev_recorded && st != s->last_stream) RT_HIP(hipStreamWaitEvent(st, s->ev1, 0));
+        s->last_stream = st;
+        if (int rc = ensure_origin_terms(s, P[i], st)) return rc;
+    }
+    // the batch's heavy-first / wide-section state lives in scene 0's table, keyed by the batch
+    uint64_t ident = n;
+    for (uint32_t i = 0; i < n; i++) ident = ident * 0x9E3779B97F4A7C15ull + uint64_t(uintptr_t(S[i]));
+    rt_scene *s0 = S[0];
+    const bool front = blocks >= s0->hf_min_blocks || (wide_heavy && blocks >= 64u);
+    if (front || wide_heavy)
+        if (int rc = hf_prepare(s0, P[0], blocks, kvar, front, st, ident | 1u)) return rc;
+    uint32_t grid = uint32_t(blocks) + P[0].hf_front;
+    for (uint32_t i = 0; i < n; i++) KB.p[i] = P[i];
+    // timing: scene 0's ring (one timed launch for the whole batch)
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    RT_HIP(hipStreamIsCapturing(st, &cap));
+    const bool timed = cap == hipStreamCaptureStatusNone && s0->time_every && s0->launches % s0->time_every == 0u;
+    s0->launches++;
+    const uint32_t kslot = s0->kt_next;
+    if (timed && !s0->kt0[kslot])
+    {
+        RT_HIP(hipEventCreate(&s0->kt0[kslot]));
+        RT_HIP(hipEventCreate(&s0->kt1[kslot]));
+    }
+    if (timed) RT_HIP(hipEventRecord(s0->kt0[kslot], st));
+    const dim3 wg(kWG);
+    if (P[0].wh_wgs)
+    {
+        if (!s0->side)
+        {
+            RT_HIP(hipStreamCreateWithFlags(&s0->side, hipStreamNonBlocking));
+            RT_HIP(hipEventCreateWithFlags(&s0->ev_fork, hipEventDisableTiming));
+            RT_HIP(hipEventCreateWithFlags(&s0->ev_join, hipEventDisableTiming));
+        }
+        RT_HIP(hipEventRecord(s0->ev_fork, st));
+        RT_HIP(hipStreamWaitEvent(s0->side, s0->ev_fork, 0));
+        hipLaunchKernelGGL(k_render_wh_batch, dim3(P[0].wh_wgs), wg, 0, s0->side, KB);
+    }
+    hipLaunchKernelGGL(fn, dim3(grid), wg, 0, st, KB);
+    if (P[0].wh_wgs)
+    {
+        RT_HIP(hipEventRecord(s0->ev_join, s0->side));
+        RT_HIP(hipStreamWaitEvent(st, s0->ev_join, 0));
+    }
+    if (timed) RT_HIP(hipEventRecord(s0->kt1[kslot], st));
+    if ((P[0].hf_front || P[0].wh_on) && P[0].hf_measure)
+        hipLaunchKernelGGL(k_hf_plan, dim3(uint32_t((blocks + kWG - 1) / kWG)), wg, 0, st, KB.p[0], uint32_t(blocks));
+    RT_HIP(hipGetLastError());
+    for (uint32_t i = 0; i < n; i++)
+    {
+        RT_HIP(hipEventRecord(S[i]->ev1, st));
+        S[i]->ev_recorded = true;
+    }
+    if (timed)
+    {
+        s0->kt_last = kslot;
+        s0->kt_next = (kslot + 1u) % kTimeRing;
+        s0->kt_count = std::min(s0->kt_count + 1u, kTimeRing);
     }
     return RT_OK;
 }
@@ -2832,6 +3036,22 @@ int rt_scene_device_bytes(const rt_scene *s, uint64_t *bytes)
 } // extern "C"
 
 namespace {
+// Frame parameters of a device-resident render (see render_device); returns the local tile count.
+uint32_t device_params(const rt_scene *s, const rt_frame *f, uint32_t rank, uint32_t nranks, bool shard,
+                       uint32_t *d_out, uint32_t *d_hits, KParams& P)
+{
+    frame_params(s, f, P);
+    P.rx0 = 0; P.ry0 = 0; P.rw = f->width; P.rh = f->height;
+    P.tiles_x = (f->width + kTile - 1) / kTile;
+    const uint32_t ntiles = P.tiles_x * ((f->height + kTile - 1) / kTile);
+    P.rank = rank; P.nranks = nranks;
+    P.out = d_out;
+    P.hits = d_hits;
+    P.pitch = shard ? 0u : f->width;
+    P.shard_mode = shard ? 1u : 0u;
+    return ntiles > rank ? (ntiles - rank + nranks - 1) / nranks : 0;
+}
+
 // The device-resident render of a whole frame (shard false: d_out[y*W + x]) or of one rank's
 // interleaved 16x16 tiles (shard true: d_out = the compact shard, also for nranks == 1),
 // optionally with per-sample hit IDs.
@@ -2846,17 +3066,38 @@ int render_device(rt_scene *s, const rt_frame *f, uint32_t rank, uint32_t nranks
     const uint32_t spp = std::max(1u, f->spp);
     if ((rc = prepare_samples(s, f, spp))) return rc;
     KParams P;
-    frame_params(s, f, P);
-    P.rx0 = 0; P.ry0 = 0; P.rw = f->width; P.rh = f->height;
-    P.tiles_x = (f->width + kTile - 1) / kTile;
-    const uint32_t ntiles = P.tiles_x * ((f->height + kTile - 1) / kTile);
-    P.rank = rank; P.nranks = nranks;
-    P.out = d_out;
-    P.hits = d_hits;
-    P.pitch = shard ? 0u : f->width;
-    P.shard_mode = shard ? 1u : 0u;
-    const uint32_t local = ntiles > rank ? (ntiles - rank + nranks - 1) / nranks : 0;
+    const uint32_t local = device_params(s, f, rank, nranks, shard, d_out, d_hits, P);
     return launch_render(s, f, P, local, static_cast<hipStream_t>(hip_stream));
+}
+
+// rt_render_batch_device's frames [0, n): one k_render_batch launch when they can share it.
+int render_batch_chunk(rt_scene *const *S, const rt_frame *F, uint32_t n, uint32_t rank, uint32_t nranks,
+                       uint32_t *const *outs, uint32_t *const *hits, void *hip_stream)
+{
+    bool batched = false;
+    if (n >= 2)
+    {
+        std::vector<rt_scene *> uniq(S, S + n);
+        std::sort(uniq.begin(), uniq.end());
+        uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
+        std::vector<std::unique_lock<std::mutex>> locks;
+        for (rt_scene *s : uniq) locks.emplace_back(s->mtx);
+        int rc = ensure_device(S[0]);
+        if (rc) return rc;
+        KParams P[kMaxBatch];
+        uint32_t local = 0;
+        for (uint32_t i = 0; i < n; i++)
+        {
+            if ((rc = prepare_samples(S[i], &F[i], std::max(1u, F[i].spp)))) return rc;
+            local = device_params(S[i], &F[i], rank, nranks, nranks > 1, outs[i], hits ? hits[i] : nullptr, P[i]);
+        }
+        rc = launch_batch(S, F, n, P, local, static_cast<hipStream_t>(hip_stream), &batched);
+        if (batched) return rc;
+    }
+    for (uint32_t i = 0; i < n; i++)
+        if (int rc = render_device(S[i], &F[i], rank, nranks, nranks > 1, outs[i], hits ? hits[i] : nullptr, hip_stream))
+            return rc;
+    return RT_OK;
 }
 } // namespace
 
@@ -2879,6 +3120,22 @@ int rt_render_shard_device(rt_scene *s, const rt_frame *f, uint32_t rank, uint32
                            void *hip_stream)
 {
     return render_device(s, f, rank, nranks, true, d_shard, nullptr, hip_stream);
+}
+
+int rt_render_batch_device(rt_scene *const *scenes, const rt_frame *frames, uint32_t n, uint32_t rank,
+                           uint32_t nranks, uint32_t *const *d_outs, uint32_t *const *d_hits, void *hip_stream)
+{
+    if (!scenes || !frames || !d_outs || nranks == 0 || rank >= nranks) return fail(RT_E_INVALID, "bad arguments");
+    for (uint32_t i = 0; i < n; i++)
+    {
+        if (!scenes[i] || !d_outs[i]) return fail(RT_E_INVALID, "NULL scene or output");
+        if (int rc = validate_frame(&frames[i])) return rc;
+    }
+    for (uint32_t i = 0; i < n; i += kMaxBatch)
+        if (int rc = render_batch_chunk(scenes + i, frames + i, std::min(kMaxBatch, n - i), rank, nranks, d_outs + i,
+                                        d_hits ? d_hits + i : nullptr, hip_stream))
+            return rc;
+    return RT_OK;
 }
 
 int rt_render_hits_device(rt_scene *s, const rt_frame *f, uint32_t rank, uint32_t nranks, uint32_t *d_out,

@@ -25,10 +25,11 @@ class CpuWorkload:
         self.frames = [None for _ in scenes]
         self.renders = 0
 
-    def render(self, i):
-        shard = self.rtm.shard_from_frame(self.full[i], self.rank, self.world)
-        self.bufs[i].copy_(torch.from_numpy(shard.view(np.int32)))
-        self.renders += 1
+    def render_all(self):
+        for i in range(len(self.full)):
+            shard = self.rtm.shard_from_frame(self.full[i], self.rank, self.world)
+            self.bufs[i].copy_(torch.from_numpy(shard.view(np.int32)))
+            self.renders += 1
 
     def unshard(self, i, gathered):
         self.frames[i] = self.rtm.frame_from_shards(gathered.numpy().view(np.uint32), W, H, self.world)

@@ -776,3 +776,123 @@ def test_multi_gpu_framebuffer(golden, sid, devices, tmp_path):
     finally:
         r.close()
         hs.close()
+
+
+def _batch_check(golden, gss, sids, W, H, N, reps, kernel=0):
+    """Renders the scenes' frames as batched launches (rt_render_batch_device) -- every rank of N
+    when N > 1 -- `reps` times, then checks every frame and every per-sample hit ID against the
+    reference's SHA-256s."""
+    import torch
+    st = torch.cuda.current_stream().cuda_stream
+    fs = [g.frame(W, H, 4, kernel=kernel) for g in gss]
+    hits = [torch.full((W * H * 4,), 0x5A5A5A5A, dtype=torch.int32, device="cuda") for _ in sids]
+    if N == 1:
+        outs = [torch.zeros(W * H, dtype=torch.int32, device="cuda") for _ in sids]
+        for _ in range(reps):
+            rtm.render_batch_device(gss, fs, [o.data_ptr() for o in outs], d_hits=[h.data_ptr() for h in hits],
+                                    stream=st)
+    else:
+        e = rtm.shard_elems(W, H, N)
+        gathered = [torch.zeros(N * e, dtype=torch.int32, device="cuda") for _ in sids]
+        for r in range(N):
+            for _ in range(reps):
+                rtm.render_batch_device(gss, fs, [gd.data_ptr() + 4 * r * e for gd in gathered], rank=r, nranks=N,
+                                        d_hits=[h.data_ptr() for h in hits], stream=st)
+        outs = [torch.zeros(W * H, dtype=torch.int32, device="cuda") for _ in sids]
+        for gd, o in zip(gathered, outs):
+            rtm.unshard_device(W, H, N, gd.data_ptr(), o.data_ptr(), st)
+    torch.cuda.synchronize()
+    for sid, o, h in zip(sids, outs, hits):
+        g = golden["frames_1080p4"][str(sid)]
+        assert sha_dev(o) == g["bgra_sha256"], (sid, N)
+        assert sha_dev(h) == g["hits_sha256"], (sid, N)
+
+
+@pytest.mark.parametrize("N", [1, 2, 8])
+def test_batch_bench_pair(golden, scenes, N):
+    """The bench step as one batched launch (Cornell + killeroo, k_render_batch): frames and hit IDs
+    of both scenes equal the reference's, after six launches per rank (natural order, heavy-first
+    order across both frames, and at N >= 2 the batch's wide section on killeroo's heavy items)."""
+    sids = (1, 8)
+    gss = [scenes(s)[1] for s in sids]
+    _batch_check(golden, gss, sids, 1920, 1080, N, 6)
+
+
+def test_batch_all_ten_scenes(golden, scenes):
+    """BASELINE config 5 through rt_render_batch_device: 10 frames = launches of 4 + 4 + 2 frames."""
+    sids = tuple(range(10))
+    _batch_check(golden, [scenes(s)[1] for s in sids], sids, 1920, 1080, 1, 3)
+
+
+def test_batch_same_scene_twice_and_fallback(golden, scenes):
+    """A scene may appear twice in one batch; frames that cannot share a launch (another kernel
+    kind) take one launch each -- outputs identical either way."""
+    import torch
+    st = torch.cuda.current_stream().cuda_stream
+    g8 = scenes(8)[1]
+    g1 = scenes(1)[1]
+    want8 = golden["frames_1080p4"]["8"]["bgra_sha256"]
+    want1 = golden["frames_1080p4"]["1"]["bgra_sha256"]
+    outs = [torch.zeros(1920 * 1080, dtype=torch.int32, device="cuda") for _ in range(3)]
+    for kernels in ((0, 0, 0), (0, rtm.RT_KERNEL_LANES, 0)):
+        fs = [g8.frame(1920, 1080, 4, kernel=kernels[0]), g1.frame(1920, 1080, 4, kernel=kernels[1]),
+              g8.frame(1920, 1080, 4, kernel=kernels[2])]
+        for _ in range(3):
+            rtm.render_batch_device([g8, g1, g8], fs, [o.data_ptr() for o in outs], stream=st)
+        torch.cuda.synchronize()
+        assert [sha_dev(o) for o in outs] == [want8, want1, want8], kernels
+
+
+@pytest.mark.parametrize("spp", [1, 2, 8, 16])
+def test_batch_ragged_vs_oracle(scenes, oracle, spp):
+    """Batched launches of ragged frames (partial 16x16 tiles in every frame of the grid) of a
+    dense and a light scene, whole and as 3 ranks' shards, equal the oracle's frames."""
+    import torch
+    st = torch.cuda.current_stream().cuda_stream
+    sids = (5, 1)
+    gss = [scenes(s)[1] for s in sids]
+    W, H = 97, 61
+    exp = [oracle.render(s, W, H, spp)[0] for s in sids]
+    fs = [g.frame(W, H, spp) for g in gss]
+    outs = [torch.zeros(W * H, dtype=torch.int32, device="cuda") for _ in sids]
+    for _ in range(4):
+        rtm.render_batch_device(gss, fs, [o.data_ptr() for o in outs], stream=st)
+    torch.cuda.synchronize()
+    for o, x in zip(outs, exp):
+        np.testing.assert_array_equal(o.cpu().numpy().view(np.uint32).reshape(H, W), x)
+    N = 3
+    e = rtm.shard_elems(W, H, N)
+    gathered = [torch.zeros(N * e, dtype=torch.int32, device="cuda") for _ in sids]
+    for r in range(N):
+        for _ in range(4):
+            rtm.render_batch_device(gss, fs, [g.data_ptr() + 4 * r * e for g in gathered], rank=r, nranks=N, stream=st)
+    for g, o in zip(gathered, outs):
+        rtm.unshard_device(W, H, N, g.data_ptr(), o.data_ptr(), st)
+    torch.cuda.synchronize()
+    for o, x in zip(outs, exp):
+        np.testing.assert_array_equal(o.cpu().numpy().view(np.uint32).reshape(H, W), x)
+
+
+def test_batch_graph_replay(golden, scenes):
+    """The batched step inside a captured HIP graph (bench.py --graph), after warm-up launches:
+    replays render both reference frames."""
+    import torch
+    sids = (1, 8)
+    gss = [scenes(s)[1] for s in sids]
+    fs = [g.frame(1920, 1080, 4) for g in gss]
+    outs = [torch.zeros(1920 * 1080, dtype=torch.int32, device="cuda") for _ in sids]
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            rtm.render_batch_device(gss, fs, [o.data_ptr() for o in outs], stream=s.cuda_stream)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        rtm.render_batch_device(gss, fs, [o.data_ptr() for o in outs], stream=s.cuda_stream)
+    for _ in range(2):
+        for o in outs:
+            o.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        for sid, o in zip(sids, outs):
+            assert sha_dev(o) == golden["frames_1080p4"][str(sid)]["bgra_sha256"]

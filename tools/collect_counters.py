@@ -71,6 +71,9 @@ def main():
     ap.add_argument("--frames", type=int, default=12)
     ap.add_argument("--out", default=None, help="default profiles/counters_<workload>.json")
     ap.add_argument("--work", default=os.path.join(ROOT, "gpurun_out", "counters"))
+    ap.add_argument("--batch", action="store_true",
+                    help="the workload's frames in one rt_render_batch_device launch per step (bench.py's "
+                         "step): counters per batch dispatch, stored under scenes['batch']")
     a = ap.parse_args()
     a.scenes, a.size = WORKLOADS[a.workload]
     if a.out is None:
@@ -80,13 +83,14 @@ def main():
     os.makedirs(a.work, exist_ok=True)
     env = dict(os.environ, TMPDIR="/tmp")
     W, H, S = a.size
-    res = {str(sid): {} for sid in a.scenes}
+    keys = ["batch"] if a.batch else [str(sid) for sid in a.scenes]
+    res = {k: {} for k in keys}
     for tag, counters in SETS.items():
         d = os.path.join(a.work, f"{a.workload}_{tag}")
         cmd = ["timeout", "-k", "10", "300", "rocprofv3", "--pmc"] + counters.split() + [
             "--output-format", "csv", "-d", d, "-o", "run", "--",
             "python3", os.path.join(ROOT, "tools", "render_loop.py"), "--scenes", *map(str, a.scenes),
-            "--frames", str(a.frames), "--size", str(W), str(H), str(S)]
+            "--frames", str(a.frames), "--size", str(W), str(H), str(S)] + (["--batch"] if a.batch else [])
         with open(d + ".log", "w") as log:
             rc = subprocess.run(cmd, cwd="/tmp", env=env, stdout=log, stderr=subprocess.STDOUT).returncode
         print(f"{a.workload} {tag} rc={rc}", flush=True)
@@ -95,10 +99,10 @@ def main():
         f = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
         if not f:
             sys.exit(f"no counter csv under {d}")
-        for sid, m in zip(a.scenes, medians(f[0], len(a.scenes))):
-            res[str(sid)].update(m)
-    for sid in a.scenes:
-        c = res[str(sid)]
+        for k, m in zip(keys, medians(f[0], len(keys))):
+            res[k].update(m)
+    for k in keys:
+        c = res[k]
         c["FETCH_SIZE_KiB"] = c.pop("FETCH_SIZE", None)
         c["WRITE_SIZE_KiB"] = c.pop("WRITE_SIZE", None)
         c["hbm_bytes"] = round((2 * c["FETCH_SIZE_KiB"] + c["WRITE_SIZE_KiB"]) * 1024)
@@ -106,8 +110,10 @@ def main():
         c["lane_util"] = round(c["SQ_THREAD_CYCLES_VALU"] / max(1.0, c["SQ_ACTIVE_INST_VALU"]), 2)
     out = {"source_hash": rtm.library_build_hash(), "workload": f"scenes{a.scenes}_{W}x{H}x{S}",
            "workload_name": a.workload,
-           "kernel": "AUTO (rt_kernel 0)", "frames_per_scene": a.frames,
-           "statistic": "per scene, median over its k_render_* dispatches after its first two",
+           "kernel": "AUTO (rt_kernel 0)" + (", batched launch (k_render_batch)" if a.batch else ""),
+           "frames_per_scene": a.frames,
+           "statistic": ("per batch dispatch (all scenes' frames)" if a.batch else "per scene") +
+                        ", median over its k_render_* dispatches after its first two",
            "hbm_note": "hbm_bytes = (2 x FETCH_SIZE + WRITE_SIZE) KiB x 1024 (gfx950 FETCH_SIZE "
                        "counts half of a wide read; MI355X_MICROARCH.md)",
            "scenes": res}

@@ -16,6 +16,7 @@ ap.add_argument("--scenes", type=int, nargs="+", default=None, help="several sce
 ap.add_argument("--frames", type=int, default=10)
 ap.add_argument("--kernel", type=lambda x: int(x, 0), default=0)
 ap.add_argument("--size", type=int, nargs=3, default=[1920, 1080, 4])
+ap.add_argument("--batch", action="store_true", help="all scenes' frames in one rt_render_batch_device launch per frame")
 a = ap.parse_args()
 if a.lib:
     os.environ["RT_TRACER_LIB"] = a.lib
@@ -28,6 +29,16 @@ torch.cuda.set_device(0)
 st = torch.cuda.current_stream()
 W, H, S = a.size
 out = torch.empty(W * H, dtype=torch.int32, device="cuda")
+if a.batch:
+    sids = a.scenes or [a.scene]
+    gs = [rtm.GpuScene(rtm.HostScene.load(sid), 0) for sid in sids]
+    fs = [g.frame(W, H, S, kernel=a.kernel) for g in gs]
+    outs = [torch.empty(W * H, dtype=torch.int32, device="cuda") for _ in sids]
+    for _ in range(a.frames):
+        rtm.render_batch_device(gs, fs, [o.data_ptr() for o in outs], stream=st.cuda_stream)
+    torch.cuda.synchronize()
+    print("batch frames", a.frames, "scenes", sids)
+    sys.exit(0)
 for sid in (a.scenes or [a.scene]):
     g = rtm.GpuScene(rtm.HostScene.load(sid), 0)
     f = g.frame(W, H, S, kernel=a.kernel)

@@ -31,6 +31,8 @@ ap.add_argument("--steady", action="store_true")
 ap.add_argument("--scenes", type=int, nargs="+", default=[1, 8, 5])
 ap.add_argument("--frame", type=int, nargs=3, default=[1920, 1080, 4])
 ap.add_argument("--out", default=None)
+ap.add_argument("--batch", action="store_true",
+                help="also time each rank's frames of ALL --scenes as one batched launch (rt_render_batch_device)")
 ap.add_argument("kernels", nargs="*")
 A = ap.parse_args()
 W, H, SPP = A.frame
@@ -72,6 +74,34 @@ for sid in A.scenes:
             res["scene_max_ms"][f"s{sid}_k{k:#x}_n{n}"] = max(res["per_rank"][f"s{sid}_k{k:#x}_n{n}_r{r}"] for r in range(n))
         print(sid, k, {n: res["scene_max_ms"][f"s{sid}_k{k:#x}_n{n}"] for n in NS}, flush=True)
     g.close()
+if A.batch:
+    gs = [rtm.GpuScene(rtm.HostScene.load(sid), 0) for sid in A.scenes]
+    fs = [g.frame(W, H, SPP) for g in gs]
+    res["batch_max_ms"] = {}
+    for n in NS:
+        bufs = [torch.empty(rtm.shard_elems(W, H, n), dtype=torch.int32, device="cuda") for _ in gs]
+        worst = 0.0
+        for r in range(n):
+            run = lambda: rtm.render_batch_device(gs, fs, [b.data_ptr() for b in bufs], rank=r, nranks=n,
+                                                  stream=st.cuda_stream)
+            ts = []
+            for _ in range(20):
+                run()
+            for rep in range(3):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(st)
+                for _ in range(32):
+                    run()
+                e1.record(st)
+                torch.cuda.synchronize()
+                ts.append(e0.elapsed_time(e1) / 32)
+            v = round(sorted(ts)[1], 4)
+            res["per_rank"][f"batch_n{n}_r{r}"] = v
+            worst = max(worst, v)
+        res["batch_max_ms"][n] = worst
+        print("batch", A.scenes, n, worst, flush=True)
+    for g in gs:
+        g.close()
 if 1 in A.scenes and 8 in A.scenes:
     for k in kernels:
         res["pair_max_ms"][f"{k:#x}"] = {n: round(max(res["per_rank"][f"s1_k{k:#x}_n{n}_r{r}"] +
@@ -82,7 +112,8 @@ for sid in A.scenes:
         base = res["scene_max_ms"][f"s{sid}_k{k:#x}_n1"]
         res.setdefault("speedup_vs_n1", {})[f"s{sid}_k{k:#x}"] = {
             n: round(base / res["scene_max_ms"][f"s{sid}_k{k:#x}_n{n}"], 3) for n in NS}
-print(json.dumps({"pair_max_ms": res["pair_max_ms"], "speedup_vs_n1": res.get("speedup_vs_n1")}))
+print(json.dumps({"pair_max_ms": res["pair_max_ms"], "batch_max_ms": res.get("batch_max_ms"),
+                  "speedup_vs_n1": res.get("speedup_vs_n1")}))
 os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
 lib = os.path.splitext(os.path.basename(os.environ.get("RT_TRACER_LIB", "librt_tracer.so")))[0]
 name = A.out or f"shard_scaling_{lib}{'_steady' if STEADY else ''}"
