@@ -1,0 +1,90 @@
+#!/usr/bin/env python3
+"""In-process A/B of a scene tunable (read once at rt_scene_create, e.g. RT_PRIO, RT_WH_ALPHA16):
+for each value, fresh scenes are made and every rank of N = 1, 2, 4, 8 is timed in steady state
+(20 warm-up launches, then 3 x 32 back-to-back launches between one event pair) -- the bench
+pair as one batched launch per rank (rt_render_batch_device) and, with --per-scene, one launch
+per scene.  Values are interleaved over --rounds rounds; per (value, N) the max over ranks of
+the median.  Also reports the wide section's listed items per rank.
+
+    python3 tools/tunable_sweep.py --env RT_PRIO --values 0 1 2 3 [--scenes 1 8] [--rounds 2]
+"""
+import argparse
+import importlib.util
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+spec = importlib.util.spec_from_file_location("rtm", os.path.join(ROOT, "cpp-11-ray-trace-march-framework_amd", "__init__.py"))
+rtm = importlib.util.module_from_spec(spec)
+sys.modules["rtm"] = rtm
+spec.loader.exec_module(rtm)
+ap = argparse.ArgumentParser()
+ap.add_argument("--env", required=True)
+ap.add_argument("--values", nargs="+", required=True)
+ap.add_argument("--scenes", type=int, nargs="+", default=[1, 8])
+ap.add_argument("--frame", type=int, nargs=3, default=[1920, 1080, 4])
+ap.add_argument("--ns", type=int, nargs="+", default=[1, 2, 4, 8])
+ap.add_argument("--rounds", type=int, default=2)
+ap.add_argument("--per-scene", action="store_true")
+ap.add_argument("--out", default="tunable_sweep")
+A = ap.parse_args()
+torch.cuda.set_device(0)
+st = torch.cuda.current_stream()
+W, H, SPP = A.frame
+hs = {sid: rtm.HostScene.load(sid) for sid in A.scenes}
+
+
+def steady(run):
+    for _ in range(20):
+        run()
+    ts = []
+    for _ in range(3):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(32):
+            run()
+        e1.record(st)
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1) / 32)
+    return sorted(ts)[1]
+
+
+res = {"env": A.env, "scenes": A.scenes, "frame": A.frame, "batch": {}, "per_scene": {}, "wide_items": {}}
+for rnd in range(A.rounds):
+    for v in A.values:
+        os.environ[A.env] = v
+        gs = [rtm.GpuScene(hs[sid], 0) for sid in A.scenes]
+        fs = [g.frame(W, H, SPP) for g in gs]
+        for n in A.ns:
+            bufs = [torch.empty(rtm.shard_elems(W, H, n) if n > 1 else W * H, dtype=torch.int32, device="cuda")
+                    for _ in gs]
+            worst, items = 0.0, []
+            for r in range(n):
+                t = steady(lambda: rtm.render_batch_device(gs, fs, [b.data_ptr() for b in bufs], rank=r, nranks=n,
+                                                           stream=st.cuda_stream))
+                worst = max(worst, t)
+                items.append(gs[0].wide_items())
+            res["batch"].setdefault(v, {}).setdefault(str(n), []).append(round(worst, 4))
+            res["wide_items"].setdefault(v, {})[str(n)] = items
+            if A.per_scene:
+                worst = 0.0
+                for r in range(n):
+                    tot = 0.0
+                    for g, f, b in zip(gs, fs, bufs):
+                        if n == 1:
+                            tot += steady(lambda: g.render_frame_device(f, b.data_ptr(), st.cuda_stream))
+                        else:
+                            tot += steady(lambda: g.render_shard_device(f, r, n, b.data_ptr(), st.cuda_stream))
+                    worst = max(worst, tot)
+                res["per_scene"].setdefault(v, {}).setdefault(str(n), []).append(round(worst, 4))
+            print(rnd, A.env, v, n, res["batch"][v][str(n)][-1], flush=True)
+        for g in gs:
+            g.close()
+summary = {v: {n: min(ts) for n, ts in d.items()} for v, d in res["batch"].items()}
+res["batch_best_of_rounds"] = summary
+print(json.dumps({"batch_best_of_rounds": summary, "per_scene": res["per_scene"]}))
+os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+json.dump(res, open(os.path.join(ROOT, "gpurun_out", A.out + ".json"), "w"), indent=1)
