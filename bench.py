@@ -456,8 +456,10 @@ def main():
     ap.add_argument("--no-moving-camera", action="store_true")
     ap.add_argument("--graph", action="store_true",
                     help="replay the step's render launch(es) from a hipGraph captured after the warm-up")
-    ap.add_argument("--no-batch", action="store_true",
-                    help="one launch per frame instead of the step's frames in one batched launch")
+    ap.add_argument("--batch", choices=["auto", "on", "off"], default="auto",
+                    help="the step's frames in one batched launch (rt_render_batch_device) or one launch per "
+                         "frame; auto = batched for N > 1 ranks, where it measured 13-14 %% faster at N = 2 and 8 "
+                         "and 1 %% slower at N = 1 (profiles/r03d_ab_wave_priority.json)")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="bench")
     ap.add_argument("--check", action="store_true",
                     help="after timing, rank 0 compares every assembled frame with a one-GPU render")
@@ -487,7 +489,8 @@ def main():
             dist.init_process_group(args.dist_backend)
 
     rtm = load_package()
-    work = GpuWorkload(rtm, torch, world, rank, local, args.kernel, batch=not args.no_batch)
+    batch = args.batch == "on" or (args.batch == "auto" and world > 1)
+    work = GpuWorkload(rtm, torch, world, rank, local, args.kernel, batch=batch)
     elapsed = run_steps(work, world, rank, args.steps, args.warmup, dist if world > 1 else None,
                         graph=args.graph)
     kernel_ms = work.kernel_ms(args.steps)

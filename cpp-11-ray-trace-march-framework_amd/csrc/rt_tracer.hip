@@ -139,8 +139,6 @@ struct KParams
     uint32_t hf_front;          // front section size (blocks, a multiple of 8)
     uint32_t hf_ver;            // version of the plan this frame uses (0: none yet)
     uint32_t hf_measure;        // 1: this frame records wave costs for the next plan
-    uint32_t prio;              // wave priority of the critical path (rt_scene::prio, RT_PRIO): bit 0
-                                // wide-section waves at s_setprio 2, bit 1 heavy-first front blocks at 1
     uint32_t hf_floor;          // a block is heavy above max(hf_floor, last max >> kHfShift) cycles
     const uint32_t *hf_mark_in; // per block: == hf_ver when the current plan lists it
     uint32_t *hf_mark_out;      // per block: hf_ver + 1 when the next plan lists it
@@ -1406,7 +1404,6 @@ __global__ void __launch_bounds__(kWG) k_render_lanes(KParams P)
     volatile uint32_t *t0v = t0s;                 // a wave's start time waits in LDS across the walk
     uint32_t b;
     if (!block_of_launch<VAR>(P, b)) return;
-    if ((P.prio & 2u) && blockIdx.x < P.hf_front) __builtin_amdgcn_s_setprio(1);   // the heavy blocks
     const uint32_t item = b * kWavesPerWG + (threadIdx.x >> 6);
     if constexpr ((VAR & kVarWideHeavy) != 0)
         if (P.wh_wgs && P.hf_ver && P.wh_mark_in[item] == P.hf_ver) return;   // traced by the wide section
@@ -1462,7 +1459,6 @@ __global__ void __launch_bounds__(kWG) k_render_lanes(KParams P)
 // (its own register allocation: folded into the lane kernel it cost 106 SGPRs and spills)
 __global__ void __launch_bounds__(kWG) k_render_wh(KParams P)
 {
-    if (P.prio & 1u) __builtin_amdgcn_s_setprio(2);
     wide_section<false>(P);
 }
 
@@ -1476,7 +1472,6 @@ __global__ void __launch_bounds__(kWG) k_render_batch(KBatch B)
     volatile uint32_t *t0v = t0s;                 // a wave's start time waits in LDS across the walk
     uint32_t b;
     if (!block_of_launch<VAR>(B.p[0], b)) return;
-    if ((B.p[0].prio & 2u) && blockIdx.x < B.p[0].hf_front) __builtin_amdgcn_s_setprio(1);   // the heavy blocks
     const uint32_t gitem = b * kWavesPerWG + (threadIdx.x >> 6);       // launch-wide item
     if constexpr ((VAR & kVarWideHeavy) != 0)
         if (B.p[0].wh_wgs && B.p[0].hf_ver && B.p[0].wh_mark_in[gitem] == B.p[0].hf_ver) return;
@@ -1497,7 +1492,6 @@ __global__ void __launch_bounds__(kWG) k_render_batch(KBatch B)
 
 __global__ void __launch_bounds__(kWG) k_render_wh_batch(KBatch B)
 {
-    if (B.p[0].prio & 1u) __builtin_amdgcn_s_setprio(2);
     wide_section<true>(B.p[0]);
 }
 
@@ -2015,7 +2009,6 @@ struct rt_scene
     uint32_t wh_alpha16 = 32;       // RT_WH_ALPHA16: wide threshold, sixteenths of the estimated span
     uint32_t wh_auto_refs = 128;    // RT_WH_AUTO_REFS: AUTO takes the wide section for >= 2-rank
                                     // shards of scenes with a cell list this long
-    uint32_t prio = 0;              // RT_PRIO: KParams::prio (critical-path wave priority; A/B)
     bool octant_words = false;      // 8 ray-octant copies of the empty-run words (else one L-inf word)
     // sample table cache
     float2 *d_smp = nullptr;
@@ -2255,7 +2248,6 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
     P.hf_measure = c->frames < 2u || c->frames % kHfPeriod == 0u;
     c->frames++;
     P.hf_floor = s->hf_floor;
-    P.prio = s->prio;
     P.hf_ticket = c->ticket;
     P.hf_mark_in = c->marks + size_t(v & 1u) * c->cap_blocks;
     P.hf_mark_out = c->marks + size_t((v + 1u) & 1u) * c->cap_blocks;
@@ -2751,7 +2743,6 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
     s->wh_floor = env_tunable("RT_WH_FLOOR", s->wh_floor);
     s->wh_alpha16 = env_tunable("RT_WH_ALPHA16", s->wh_alpha16);
     s->wh_auto_refs = env_tunable("RT_WH_AUTO_REFS", s->wh_auto_refs);
-    s->prio = env_tunable("RT_PRIO", s->prio);
     for (int a = 0; a < 3; a++)
     {
         s->dims[a] = g.dims[a];

@@ -16,9 +16,9 @@ if [ "${TESTS:-1}" = 1 ]; then
     ok $rc || exit $rc
     [ $rc -eq 0 ] || exit $rc
 fi
-timeout -k 10 300 python -u bench.py --no-cpu-baseline > gpurun_out/${T}_bench_batch.json 2> gpurun_out/${T}_bench_batch.err
+timeout -k 10 300 python -u bench.py --no-cpu-baseline --batch on > gpurun_out/${T}_bench_batch.json 2> gpurun_out/${T}_bench_batch.err
 rc=$?; echo "bench batch rc=$rc"; cut -c1-400 gpurun_out/${T}_bench_batch.json; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-end-to-end --no-batch > gpurun_out/${T}_bench_nobatch.json 2> gpurun_out/${T}_bench_nobatch.err
+timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-end-to-end --batch off > gpurun_out/${T}_bench_nobatch.json 2> gpurun_out/${T}_bench_nobatch.err
 rc=$?; echo "bench no-batch rc=$rc"; cut -c1-400 gpurun_out/${T}_bench_nobatch.json; [ $rc -eq 0 ] || exit $rc
 if [ "${SCALE:-1}" = 1 ]; then
     timeout -k 10 400 python -u tools/shard_scaling.py --steady --batch --scenes 1 8 --out ${T}_shard_scaling 0 \
