@@ -75,6 +75,7 @@ constexpr int kVarWaveClock = 32768;        // RT_KERNEL_FLAG_WAVE_CLOCK: per-it
 constexpr int kVarUniform = 65536;          // scalar loop for wave-uniform cell lists
 constexpr int kVarLdsCells = 262144;        // RT_KERNEL_FLAG_LDS_CELLS: long uniform lists staged in LDS
 constexpr int kVarWideHeavy = 524288;       // RT_KERNEL_FLAG_WIDE_HEAVY: heavy items traced wide at the start
+constexpr int kVarWideFused = 1048576;      // batch kernel: the wide section's blocks lead the same grid
 // AUTO's traversal: every feature above that is exact for every scene ...
 constexpr int kVarAutoCore = kVarWaveGate | kVarDistSkip | kVarOriginPre | kVarXcdBands | kVarUniform;
 // ... plus the two that need a scene property (rt_scene::rcp_safe, rt_scene::pack_ok)
@@ -1189,9 +1190,8 @@ __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks)
 // block has nothing to do.  The marks read here are never written by this launch (the next
 // frame's marks live in the other buffer), so every wave of a block decides alike.
 template <int VAR>
-__device__ __forceinline__ bool block_of_launch(const KParams& P, uint32_t& b)
+__device__ __forceinline__ bool block_of_launch(const KParams& P, uint32_t& b, uint32_t bid, uint32_t nblk)
 {
-    const uint32_t bid = blockIdx.x, nblk = gridDim.x;
     if ((VAR & kVarWideHeavy) && P.hf_measure && bid == 0u && threadIdx.x == 0u)
         *P.hf_plan_out = HfPlan{};                            // k_hf_plan runs after this kernel
     if (P.hf_front)
@@ -1367,11 +1367,11 @@ __device__ __forceinline__ void wide_samples(const KParams& P, uint32_t k, uint3
 // In a batch (KBatch, BATCH = true) P is p[0] (the batch's list, launch-wide item indices) and each
 // item is rendered with its own frame's parameters.
 template <bool BATCH>
-__device__ __forceinline__ void wide_section(const KParams& P)
+__device__ __forceinline__ void wide_section(const KParams& P, uint32_t bid)
 {
     const uint32_t n = P.hf_ver ? min(P.hf_plan_in->cnt_w, kWhMax) : 0u;
     const uint32_t G = P.wh_g;                                      // 16 (spp <= 4) or 4 (spp 8-16)
-    const uint32_t w = blockIdx.x * kWavesPerWG + (threadIdx.x >> 6), nw = P.wh_wgs * kWavesPerWG;
+    const uint32_t w = bid * kWavesPerWG + (threadIdx.x >> 6), nw = P.wh_wgs * kWavesPerWG;
     const uint32_t ipt = P.wg_per_tile * kWavesPerWG;              // items per tile
     for (uint32_t e = w; e < n * G; e += nw)
     {
@@ -1403,7 +1403,7 @@ __global__ void __launch_bounds__(kWG) k_render_lanes(KParams P)
     __shared__ uint32_t t0s[kWavesPerWG];
     volatile uint32_t *t0v = t0s;                 // a wave's start time waits in LDS across the walk
     uint32_t b;
-    if (!block_of_launch<VAR>(P, b)) return;
+    if (!block_of_launch<VAR>(P, b, blockIdx.x, gridDim.x)) return;
     const uint32_t item = b * kWavesPerWG + (threadIdx.x >> 6);
     if constexpr ((VAR & kVarWideHeavy) != 0)
         if (P.wh_wgs && P.hf_ver && P.wh_mark_in[item] == P.hf_ver) return;   // traced by the wide section
@@ -1459,7 +1459,7 @@ __global__ void __launch_bounds__(kWG) k_render_lanes(KParams P)
 // (its own register allocation: folded into the lane kernel it cost 106 SGPRs and spills)
 __global__ void __launch_bounds__(kWG) k_render_wh(KParams P)
 {
-    wide_section<false>(P);
+    wide_section<false>(P, blockIdx.x);
 }
 
 // The multi-frame launch (KBatch): the launch's blocks are the frames' blocks, frame-major; the
@@ -1470,8 +1470,22 @@ __global__ void __launch_bounds__(kWG) k_render_batch(KBatch B)
 {
     __shared__ uint32_t t0s[kWavesPerWG];
     volatile uint32_t *t0v = t0s;                 // a wave's start time waits in LDS across the walk
+    // kVarWideFused: the wide section's wh_wgs workgroups lead the grid (dispatched first, no
+    // side stream and no fork / join between the two), the lane blocks follow
+    uint32_t bid = blockIdx.x, nblk = gridDim.x;
+    if constexpr ((VAR & kVarWideFused) != 0)
+    {
+        const uint32_t nw = B.p[0].wh_wgs;
+        if (bid < nw)
+        {
+            wide_section<true>(B.p[0], bid);
+            return;
+        }
+        bid -= nw;
+        nblk -= nw;
+    }
     uint32_t b;
-    if (!block_of_launch<VAR>(B.p[0], b)) return;
+    if (!block_of_launch<VAR>(B.p[0], b, bid, nblk)) return;
     const uint32_t gitem = b * kWavesPerWG + (threadIdx.x >> 6);       // launch-wide item
     if constexpr ((VAR & kVarWideHeavy) != 0)
         if (B.p[0].wh_wgs && B.p[0].hf_ver && B.p[0].wh_mark_in[gitem] == B.p[0].hf_ver) return;
@@ -1492,7 +1506,7 @@ __global__ void __launch_bounds__(kWG) k_render_batch(KBatch B)
 
 __global__ void __launch_bounds__(kWG) k_render_wh_batch(KBatch B)
 {
-    wide_section<true>(B.p[0]);
+    wide_section<true>(B.p[0], blockIdx.x);
 }
 
 // RT_KERNEL_COMPACT (grid intersector, spp a power of two <= 64): wavefront active-ray
@@ -2009,6 +2023,8 @@ struct rt_scene
     uint32_t wh_alpha16 = 32;       // RT_WH_ALPHA16: wide threshold, sixteenths of the estimated span
     uint32_t wh_auto_refs = 128;    // RT_WH_AUTO_REFS: AUTO takes the wide section for >= 2-rank
                                     // shards of scenes with a cell list this long
+    uint32_t wh_fused = 1;          // RT_WH_FUSED: a batch's wide section leads the batch kernel's grid
+                                    // (0: its own kernel on the side stream, fork / join)
     bool octant_words = false;      // 8 ray-octant copies of the empty-run words (else one L-inf word)
     // sample table cache
     float2 *d_smp = nullptr;
@@ -2486,6 +2502,8 @@ kbfn_t batch_kernel(int var)
 {
     if (var == kVarAuto) return k_render_batch<RT_TRI_MOLLER_TRUMBORE, kVarAuto>;
     if (var == (kVarAuto | kVarWideHeavy)) return k_render_batch<RT_TRI_MOLLER_TRUMBORE, kVarAuto | kVarWideHeavy>;
+    if (var == (kVarAuto | kVarWideHeavy | kVarWideFused))
+        return k_render_batch<RT_TRI_MOLLER_TRUMBORE, kVarAuto | kVarWideHeavy | kVarWideFused>;
     return nullptr;
 }
 
@@ -2519,7 +2537,8 @@ int launch_batch(rt_scene *const *S, const rt_frame *F, uint32_t n, KParams *P, 
                      (P[i].nranks >= 2u && S[i]->max_cell_refs >= S[0]->wh_auto_refs);
     }
     if (var != kVarAuto) return RT_E_INVALID;
-    const int kvar = var | (wide_heavy ? kVarWideHeavy : 0);
+    const bool fused = wide_heavy && S[0]->wh_fused;
+    const int kvar = var | (wide_heavy ? kVarWideHeavy : 0) | (fused ? kVarWideFused : 0);
     const kbfn_t fn = batch_kernel(kvar);
     if (!fn) return RT_E_INVALID;
     *batched = true;
@@ -2552,7 +2571,10 @@ int launch_batch(rt_scene *const *S, const rt_frame *F, uint32_t n, KParams *P, 
     const bool front = blocks >= s0->hf_min_blocks || (wide_heavy && blocks >= 64u);
     if (front || wide_heavy)
         if (int rc = hf_prepare(s0, P[0], blocks, kvar, front, st, ident | 1u)) return rc;
-    uint32_t grid = uint32_t(blocks) + P[0].hf_front;
+    // fused: the wide section's workgroups lead the grid, a multiple of the XCD count so the lane
+    // blocks keep their block -> XCD assignment
+    if (fused && P[0].wh_wgs) P[0].wh_wgs = (P[0].wh_wgs + kXcds - 1u) & ~(kXcds - 1u);
+    uint32_t grid = uint32_t(blocks) + P[0].hf_front + (fused ? P[0].wh_wgs : 0u);
     for (uint32_t i = 0; i < n; i++) KB.p[i] = P[i];
     // timing: scene 0's ring (one timed launch for the whole batch)
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
@@ -2567,7 +2589,7 @@ int launch_batch(rt_scene *const *S, const rt_frame *F, uint32_t n, KParams *P, 
     }
     if (timed) RT_HIP(hipEventRecord(s0->kt0[kslot], st));
     const dim3 wg(kWG);
-    if (P[0].wh_wgs)
+    if (P[0].wh_wgs && !fused)
     {
         if (!s0->side)
         {
@@ -2580,7 +2602,7 @@ int launch_batch(rt_scene *const *S, const rt_frame *F, uint32_t n, KParams *P, 
         hipLaunchKernelGGL(k_render_wh_batch, dim3(P[0].wh_wgs), wg, 0, s0->side, KB);
     }
     hipLaunchKernelGGL(fn, dim3(grid), wg, 0, st, KB);
-    if (P[0].wh_wgs)
+    if (P[0].wh_wgs && !fused)
     {
         RT_HIP(hipEventRecord(s0->ev_join, s0->side));
         RT_HIP(hipStreamWaitEvent(st, s0->ev_join, 0));
@@ -2743,6 +2765,7 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
     s->wh_floor = env_tunable("RT_WH_FLOOR", s->wh_floor);
     s->wh_alpha16 = env_tunable("RT_WH_ALPHA16", s->wh_alpha16);
     s->wh_auto_refs = env_tunable("RT_WH_AUTO_REFS", s->wh_auto_refs);
+    s->wh_fused = env_tunable("RT_WH_FUSED", s->wh_fused);
     for (int a = 0; a < 3; a++)
     {
         s->dims[a] = g.dims[a];
