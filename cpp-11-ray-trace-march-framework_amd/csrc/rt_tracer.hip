@@ -76,6 +76,7 @@ constexpr int kVarUniform = 65536;          // scalar loop for wave-uniform cell
 constexpr int kVarLdsCells = 262144;        // RT_KERNEL_FLAG_LDS_CELLS: long uniform lists staged in LDS
 constexpr int kVarWideHeavy = 524288;       // RT_KERNEL_FLAG_WIDE_HEAVY: heavy items traced wide at the start
 constexpr int kVarWideFused = 1048576;      // batch kernel: the wide section's blocks lead the same grid
+constexpr int kVarWideG4 = 2097152;         // the wide section at 4 lanes per sample (spp 8-16; else 16)
 // AUTO's traversal: every feature above that is exact for every scene ...
 constexpr int kVarAutoCore = kVarWaveGate | kVarDistSkip | kVarOriginPre | kVarXcdBands | kVarUniform;
 // ... plus the two that need a scene property (rt_scene::rcp_safe, rt_scene::pack_ok)
@@ -1366,11 +1367,10 @@ __device__ __forceinline__ void wide_samples(const KParams& P, uint32_t k, uint3
 // word keeps its lane-mode measurement until a refresh frame renders it one lane per sample again.
 // In a batch (KBatch, BATCH = true) P is p[0] (the batch's list, launch-wide item indices) and each
 // item is rendered with its own frame's parameters.
-template <bool BATCH>
+template <bool BATCH, uint32_t G>
 __device__ __forceinline__ void wide_section(const KParams& P, uint32_t bid)
 {
     const uint32_t n = P.hf_ver ? min(P.hf_plan_in->cnt_w, kWhMax) : 0u;
-    const uint32_t G = P.wh_g;                                      // 16 (spp <= 4) or 4 (spp 8-16)
     const uint32_t w = bid * kWavesPerWG + (threadIdx.x >> 6), nw = P.wh_wgs * kWavesPerWG;
     const uint32_t ipt = P.wg_per_tile * kWavesPerWG;              // items per tile
     for (uint32_t e = w; e < n * G; e += nw)
@@ -1390,8 +1390,7 @@ __device__ __forceinline__ void wide_section(const KParams& P, uint32_t bid)
         // more SGPRs across it and spilled
         const KParams& Q = late_params(P, off);
         const uint32_t k = Q.tile_order ? Q.tile_order[kseq] : kseq;
-        if (G == 16u) wide_samples<kVarWide, 16>(Q, k, slot0);
-        else wide_samples<kVarWide, 4>(Q, k, slot0);
+        wide_samples<kVarWide, int(G)>(Q, k, slot0);
     }
 }
 
@@ -1457,16 +1456,22 @@ __global__ void __launch_bounds__(kWG) k_render_lanes(KParams P)
 
 // kVarWideHeavy: the wide section, launched on the scene's side stream beside the lane kernel
 // (its own register allocation: folded into the lane kernel it cost 106 SGPRs and spills)
+template <uint32_t G>
 __global__ void __launch_bounds__(kWG) k_render_wh(KParams P)
 {
-    wide_section<false>(P, blockIdx.x);
+    wide_section<false, G>(P, blockIdx.x);
 }
 
 // The multi-frame launch (KBatch): the launch's blocks are the frames' blocks, frame-major; the
 // heavy-first order (p[0]'s state) ranks them all, and every wave renders its item with its own
 // frame's parameters (KParams re-read from the kernarg segment at the frame's offset).
+#ifdef RT_BATCH_W8      // A/B build: the fused variant forced to 8 waves / SIMD (1 VGPR spills)
+#define RT_BATCH_ATTR __attribute__((amdgpu_waves_per_eu(8, 8)))
+#else
+#define RT_BATCH_ATTR
+#endif
 template <int TRI, int VAR>
-__global__ void __launch_bounds__(kWG) k_render_batch(KBatch B)
+__global__ void __launch_bounds__(kWG) RT_BATCH_ATTR k_render_batch(KBatch B)
 {
     __shared__ uint32_t t0s[kWavesPerWG];
     volatile uint32_t *t0v = t0s;                 // a wave's start time waits in LDS across the walk
@@ -1478,7 +1483,7 @@ __global__ void __launch_bounds__(kWG) k_render_batch(KBatch B)
         const uint32_t nw = B.p[0].wh_wgs;
         if (bid < nw)
         {
-            wide_section<true>(B.p[0], bid);
+            wide_section<true, (VAR & kVarWideG4) ? 4u : 16u>(B.p[0], bid);
             return;
         }
         bid -= nw;
@@ -1504,9 +1509,10 @@ __global__ void __launch_bounds__(kWG) k_render_batch(KBatch B)
     }
 }
 
+template <uint32_t G>
 __global__ void __launch_bounds__(kWG) k_render_wh_batch(KBatch B)
 {
-    wide_section<true>(B.p[0], blockIdx.x);
+    wide_section<true, G>(B.p[0], blockIdx.x);
 }
 
 // RT_KERNEL_COMPACT (grid intersector, spp a power of two <= 64): wavefront active-ray
@@ -2453,7 +2459,8 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
             }
             RT_HIP(hipEventRecord(s->ev_fork, st));
             RT_HIP(hipStreamWaitEvent(s->side, s->ev_fork, 0));
-            hipLaunchKernelGGL(k_render_wh, dim3(P.wh_wgs), wg, 0, s->side, P);
+            if (P.wh_g == 4u) hipLaunchKernelGGL(k_render_wh<4>, dim3(P.wh_wgs), wg, 0, s->side, P);
+            else hipLaunchKernelGGL(k_render_wh<16>, dim3(P.wh_wgs), wg, 0, s->side, P);
         }
         hipLaunchKernelGGL(fn, dim3(grid), wg, 0, st, P);
         if (P.wh_wgs)
@@ -2504,6 +2511,8 @@ kbfn_t batch_kernel(int var)
     if (var == (kVarAuto | kVarWideHeavy)) return k_render_batch<RT_TRI_MOLLER_TRUMBORE, kVarAuto | kVarWideHeavy>;
     if (var == (kVarAuto | kVarWideHeavy | kVarWideFused))
         return k_render_batch<RT_TRI_MOLLER_TRUMBORE, kVarAuto | kVarWideHeavy | kVarWideFused>;
+    if (var == (kVarAuto | kVarWideHeavy | kVarWideFused | kVarWideG4))
+        return k_render_batch<RT_TRI_MOLLER_TRUMBORE, kVarAuto | kVarWideHeavy | kVarWideFused | kVarWideG4>;
     return nullptr;
 }
 
@@ -2537,8 +2546,11 @@ int launch_batch(rt_scene *const *S, const rt_frame *F, uint32_t n, KParams *P, 
                      (P[i].nranks >= 2u && S[i]->max_cell_refs >= S[0]->wh_auto_refs);
     }
     if (var != kVarAuto) return RT_E_INVALID;
-    const bool fused = wide_heavy && S[0]->wh_fused;
-    const int kvar = var | (wide_heavy ? kVarWideHeavy : 0) | (fused ? kVarWideFused : 0);
+    // fused (measured, profiles/r03f_ab_wide_fused.json): 18 % faster at a rank of 8, 9 % at 4,
+    // 4 % slower at 2 -- taken from 4 ranks on
+    const bool fused = wide_heavy && S[0]->wh_fused && P[0].nranks >= 4u;
+    const int kvar = var | (wide_heavy ? kVarWideHeavy : 0) | (fused ? kVarWideFused : 0) |
+                     (fused && spp > 4u ? kVarWideG4 : 0);
     const kbfn_t fn = batch_kernel(kvar);
     if (!fn) return RT_E_INVALID;
     *batched = true;
@@ -2599,7 +2611,8 @@ int launch_batch(rt_scene *const *S, const rt_frame *F, uint32_t n, KParams *P, 
         }
         RT_HIP(hipEventRecord(s0->ev_fork, st));
         RT_HIP(hipStreamWaitEvent(s0->side, s0->ev_fork, 0));
-        hipLaunchKernelGGL(k_render_wh_batch, dim3(P[0].wh_wgs), wg, 0, s0->side, KB);
+        if (P[0].wh_g == 4u) hipLaunchKernelGGL(k_render_wh_batch<4>, dim3(P[0].wh_wgs), wg, 0, s0->side, KB);
+        else hipLaunchKernelGGL(k_render_wh_batch<16>, dim3(P[0].wh_wgs), wg, 0, s0->side, KB);
     }
     hipLaunchKernelGGL(fn, dim3(grid), wg, 0, st, KB);
     if (P[0].wh_wgs && !fused)
