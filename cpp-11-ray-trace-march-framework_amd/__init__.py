@@ -124,7 +124,7 @@ class SceneStats(ctypes.Structure):
 class SceneInfo(ctypes.Structure):
     _fields_ = [("octant_words", c_u32), ("packed_cells", c_u32), ("rcp_safe", c_u32), ("pack_ok", c_u32),
                 ("max_cell_refs", c_u32), ("hf_floor", c_u32), ("hf_min_blocks", c_u32), ("wh_floor", c_u32),
-                ("wh_alpha16", c_u32), ("wh_auto_refs", c_u32), ("hf_contexts", c_u32),
+                ("wh_alpha16", c_u32), ("wh_auto_refs", c_u32), ("wh_fused", c_u32), ("hf_contexts", c_u32),
                 ("hf_evictions", ctypes.c_uint64), ("device_bytes", ctypes.c_uint64)]
 
 

@@ -2723,6 +2723,7 @@ int rt_scene_info_get(rt_scene *s, rt_scene_info *out)
     out->wh_floor = s->wh_floor;
     out->wh_alpha16 = s->wh_alpha16;
     out->wh_auto_refs = s->wh_auto_refs;
+    out->wh_fused = s->wh_fused;
     out->hf_contexts = kHfCtxs;
     out->hf_evictions = s->hf_evictions;
     out->device_bytes = s->device_bytes;

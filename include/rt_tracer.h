@@ -287,7 +287,7 @@ int rt_debug_wide_items(rt_scene *s, uint32_t *count);
 
 /* What rt_scene_create chose for a scene, and the scheduling tunables it read once from the
    environment (RT_HF_FLOOR, RT_HF_MIN_BLOCKS, RT_WH_FLOOR, RT_WH_ALPHA16, RT_WH_AUTO_REFS,
-   RT_OCT_DIST): never re-read per launch. */
+   RT_WH_FUSED, RT_OCT_DIST): never re-read per launch. */
 typedef struct rt_scene_info {
     uint32_t octant_words;      /* 1: 8 ray-octant copies of the cell words (AUTO's empty runs);
                                    0: one L-inf word per cell (RT_OCT_DIST=0, or above the size cap) */
@@ -295,6 +295,8 @@ typedef struct rt_scene_info {
     uint32_t rcp_safe, pack_ok; /* Newton 1/det and packed remaining-cell counts in range */
     uint32_t max_cell_refs;
     uint32_t hf_floor, hf_min_blocks, wh_floor, wh_alpha16, wh_auto_refs;
+    uint32_t wh_fused;          /* batched shards of >= 4 ranks: the wide section leads the batch
+                                   kernel's grid (else its own kernel on a side stream) */
     uint32_t hf_contexts;       /* heavy-first launch shapes remembered per scene */
     uint64_t hf_evictions;      /* launch shapes evicted (each restarts its heavy-first state) */
     uint64_t device_bytes;

@@ -44,7 +44,7 @@ rc=$?; echo "trace rc=$rc"; [ $rc -eq 0 ] || exit $rc
 cd $R
 timeout -k 10 600 bash tools/batch10_profile.sh $T 0 3 536870915 1073741827 > gpurun_out/${T}_batch10.log 2>&1
 rc=$?; echo "batch10 profile rc=$rc"; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python3 -u tools/shard_scaling.py 0 0x100 > gpurun_out/${T}_shard.log 2>&1
+timeout -k 10 300 python3 -u tools/shard_scaling.py --steady --batch 0 1 > gpurun_out/${T}_shard.log 2>&1
 rc=$?; echo "shard rc=$rc"; tail -n1 gpurun_out/${T}_shard.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 200 python3 -u tools/tail_probe.py 0 > gpurun_out/${T}_tail_probe.log 2>&1
 rc=$?; echo "tail probe rc=$rc"; exit $rc

@@ -25,7 +25,7 @@ torch.cuda.set_device(0)
 st = torch.cuda.current_stream()
 g = rtm.GpuScene(rtm.HostScene.load(sid), 0)
 g.set_timing(1)                         # last_kernel_ms below: the last launch
-f = g.frame(1920, 1080, 4, kernel=rtm.RT_KERNEL_AUTO | rtm.RT_KERNEL_FLAG_WAVE_CLOCK | rtm.RT_KERNEL_FLAG_ONE_PHASE)
+f = g.frame(1920, 1080, 4, kernel=rtm.RT_KERNEL_AUTO | rtm.RT_KERNEL_FLAG_WAVE_CLOCK)
 buf = torch.empty(rtm.shard_elems(1920, 1080, n), dtype=torch.int32, device="cuda")
 for i in range(frames):
     g.render_shard_device(f, r, n, buf.data_ptr(), st.cuda_stream)
