@@ -1465,13 +1465,10 @@ __global__ void __launch_bounds__(kWG) k_render_wh(KParams P)
 // The multi-frame launch (KBatch): the launch's blocks are the frames' blocks, frame-major; the
 // heavy-first order (p[0]'s state) ranks them all, and every wave renders its item with its own
 // frame's parameters (KParams re-read from the kernarg segment at the frame's offset).
-#ifdef RT_BATCH_W8      // A/B build: the fused variant forced to 8 waves / SIMD (1 VGPR spills)
-#define RT_BATCH_ATTR __attribute__((amdgpu_waves_per_eu(8, 8)))
-#else
-#define RT_BATCH_ATTR
-#endif
+// (The fused variant holds 83 SGPRs: 7 waves / SIMD.  Forced to 8 it spills a VGPR and measured
+// slower: rank of 4 / 8 0.256 / 0.139 ms vs 0.241 / 0.136, profiles/r03g_ab_wide_fused_*.json.)
 template <int TRI, int VAR>
-__global__ void __launch_bounds__(kWG) RT_BATCH_ATTR k_render_batch(KBatch B)
+__global__ void __launch_bounds__(kWG) k_render_batch(KBatch B)
 {
     __shared__ uint32_t t0s[kWavesPerWG];
     volatile uint32_t *t0v = t0s;                 // a wave's start time waits in LDS across the walk
