@@ -40,7 +40,7 @@ if [ "${SCALE:-1}" = 1 ]; then
     timeout -k 10 400 python -u tools/shard_scaling.py --steady --batch --scenes 1 8 --out ${T}_shard_scaling_bench 0 \
         > gpurun_out/${T}_shard_bench.log 2>&1
     rc=$?; echo "shard bench rc=$rc"; tail -1 gpurun_out/${T}_shard_bench.log; [ $rc -eq 0 ] || exit $rc
-    timeout -k 10 500 python -u tools/shard_scaling.py --steady --batch --scenes 4 --frame 4096 4096 16 \
+    timeout -k 10 500 python -u tools/shard_scaling.py --steady --scenes 4 --frame 4096 4096 16 \
         --out ${T}_shard_scaling_head 0 > gpurun_out/${T}_shard_head.log 2>&1
     rc=$?; echo "shard head rc=$rc"; tail -1 gpurun_out/${T}_shard_head.log; [ $rc -eq 0 ] || exit $rc
 fi
