@@ -58,7 +58,7 @@ TRACER_SYMBOLS = [
     "rt_get_device_count", "rt_scene_create", "rt_scene_destroy", "rt_scene_device_bytes",
     "rt_render_tiles", "rt_render_frame_device", "rt_shard_elems", "rt_render_shard_device",
     "rt_unshard_device", "rt_last_kernel_ms", "rt_trace_samples", "rt_debug_primitives",
-    "rt_debug_rcp_check", "rt_debug_wave_clocks", "rt_debug_heavy_first", "rt_debug_wide_items", "rt_scene_set_timing",
+    "rt_debug_rcp_check", "rt_debug_gamma_check", "rt_debug_wave_clocks", "rt_debug_heavy_first", "rt_debug_wide_items", "rt_scene_set_timing",
     "rt_sample_table", "rt_last_error", "rt_abi_version", "rt_grid_build", "rt_grid_free",
     "rt_scene_create_from_mesh", "rt_kernel_times", "rt_render_frame_host", "rt_frame_host_wait", "rt_host_alloc",
     "rt_host_free", "rt_render_hits_device", "rt_scene_info_get", "rt_build_hash", "rt_render_batch_device",
@@ -178,6 +178,8 @@ def tracer_lib():
         L.rt_trace_samples.argtypes = [vp, ctypes.POINTER(Frame), c_u32, c_u32, c_u32, c_u32, vp]
         L.rt_debug_primitives.argtypes = [ctypes.c_int, vp, c_u32, vp, ctypes.c_int]
         L.rt_debug_rcp_check.argtypes = [vp, ctypes.c_int]
+        if hasattr(L, "rt_debug_gamma_check"):
+            L.rt_debug_gamma_check.argtypes = [vp, ctypes.c_int]
         L.rt_debug_wave_clocks.argtypes = [vp, vp, c_u32, ctypes.POINTER(c_u32)]
         if hasattr(L, "rt_debug_heavy_first"):       # absent in builds before ABI 3 (A/B runs)
             L.rt_debug_heavy_first.argtypes = [vp, ctypes.POINTER(c_u32), ctypes.POINTER(c_u32),
@@ -661,6 +663,15 @@ def debug_rcp_check(device=0):
     L = tracer_lib()
     _check(L.rt_debug_rcp_check(_ptr(bad), device), L, "rt_debug_rcp_check")
     return bad
+
+
+def debug_gamma_check(device=0):
+    """Non-negative floats whose packed gamma byte differs between the hardware and the correctly
+    rounded square root (all of them are checked; 0 expected)."""
+    bad = np.zeros(1, np.uint64)
+    L = tracer_lib()
+    _check(L.rt_debug_gamma_check(_ptr(bad), device), L, "rt_debug_gamma_check")
+    return int(bad[0])
 
 
 def debug_primitives(kind, records, device=0):

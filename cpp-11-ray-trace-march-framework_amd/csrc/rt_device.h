@@ -38,18 +38,18 @@ __device__ __forceinline__ uint32_t pack_bgra8(float r, float g, float b)
 // on 678,030 inputs (hazard H6).
 __device__ __forceinline__ float gamma_half(float x) { return __builtin_sqrtf(x); }
 
-// lin_alg.h:138-156 Dot (accumulates from T() = 0) and Normalize (1/sqrt, then scale)
-__device__ __forceinline__ void normalize3(float& x, float& y, float& z)
+// One channel of pack_bgra8 (lin_alg.h:128-130)
+__device__ __forceinline__ uint32_t pack_channel(float c)
 {
-    float d = 0.0f;
-    d += x * x;
-    d += y * y;
-    d += z * z;
-    const float len = 1.0f / __builtin_sqrtf(d);
-    x = x * len;
-    y = y * len;
-    z = z * len;
+    return c > 1.0f ? 255u : uint32_t(cvt_i32_x86(c * 255.0f)) & 255u;
 }
+
+// The hardware square root (v_sqrt_f32, within 1 ulp, no correction steps: 1 VALU instead of
+// ~15).  rt_debug_gamma_check proves pack_channel(gamma_fast(x)) == pack_channel(gamma_half(x))
+// for EVERY non-negative float x, so the packed bytes are the reference's (hazard H6 chain:
+// sqrtf == powf(., .5f) in bytes, oracle/gamma_exhaustive.c); the float colour stays within
+// 1 ulp of the correctly rounded one (the contract's 1e-5 relative).
+__device__ __forceinline__ float gamma_fast(float x) { return __builtin_amdgcn_sqrtf(x); }
 
 __device__ __forceinline__ float dot3(float ax, float ay, float az, float bx, float by, float bz)
 {
@@ -75,6 +75,21 @@ __device__ __forceinline__ float rcp_nr(float x)
     const float e = __builtin_fmaf(-x, r, 1.0f);
     return __builtin_fmaf(e, r, r);
 }
+
+// 1.0f / x where rcp_nr is proven equal to the correctly rounded division (2^-126 <= |x| < kRcpHi,
+// rt_debug_rcp_check over every float); lanes outside that range (zero, denormal, huge, inf, NaN
+// -- rare) take the division behind a wave-uniform branch, so the common wave pays only the vote.
+// Same bits as 1.0f / x for every x.
+__device__ __forceinline__ float rcp_exact(float x)
+{
+    float r = rcp_nr(x);
+    const float ax = __builtin_fabsf(x);
+    const bool ok = ax >= 0x1p-126f && ax < kRcpHi;
+    if (__builtin_amdgcn_ballot_w64(!ok) != 0ull)
+        r = ok ? r : 1.0f / x;
+    return r;
+}
+
 
 // triangle.h:15-107 IntersectRayTri, non-culling branch. e1 = v1 - v0 and e2 = v2 - v0 are
 // precomputed on the host with the same single IEEE subtraction (triangle.h:41-42).
@@ -350,7 +365,7 @@ __device__ __forceinline__ bool point_in_aabb(float px, float py, float pz, cons
 __device__ __forceinline__ bool ray_aabb(float ox, float oy, float oz, float dx, float dy, float dz,
                                          const float* mn, const float* mx, float& tmin, float& tmax)
 {
-    const float ix = 1.0f / dx, iy = 1.0f / dy, iz = 1.0f / dz;
+    const float ix = rcp_exact(dx), iy = rcp_exact(dy), iz = rcp_exact(dz);   // = 1.0f / d
     const bool sx = ix < 0.0f, sy = iy < 0.0f, sz = iz < 0.0f;
     tmin = ((sx ? mx[0] : mn[0]) - ox) * ix;
     tmax = ((sx ? mn[0] : mx[0]) - ox) * ix;
@@ -367,20 +382,60 @@ __device__ __forceinline__ bool ray_aabb(float ox, float oy, float oz, float dx,
     return true;
 }
 
-// camera.h:20-21, 40-45: perspective ray direction. The per-frame constants fov_xs
+// lin_alg.h:138-156 Dot (accumulates from T() = 0) and Normalize (1/sqrt, then scale; the
+// reciprocal by rcp_exact: same bits as 1.0f / sqrt)
+__device__ __forceinline__ void normalize3(float& x, float& y, float& z)
+{
+    float d = 0.0f;
+    d += x * x;
+    d += y * y;
+    d += z * z;
+    const float len = rcp_exact(__builtin_sqrtf(d));
+    x = x * len;
+    y = y * len;
+    z = z * len;
+}
+
+// camera.h:39-46 from the camera-space (x, y) of a sample (z = -1): Normalize (lin_alg.h:151-156:
+// 1/sqrt then scale; the reciprocal by rcp_exact, same bits) and Transf3x3 (lin_alg.h:495-509,
+// row-vector convention: m[r][c], r = input component).
+__device__ __forceinline__ void dir_from_xy(const float* m, float x, float y, float& dx, float& dy, float& dz)
+{
+    float z = -1.0f;
+    float d = 0.0f;
+    d += x * x;
+    d += y * y;
+    d += z * z;
+    const float len = rcp_exact(__builtin_sqrtf(d));
+    x = x * len;
+    y = y * len;
+    z = z * len;
+    dx = x * m[0] + y * m[3] + z * m[6];
+    dy = x * m[1] + y * m[4] + z * m[7];
+    dz = x * m[2] + y * m[5] + z * m[8];
+}
+
+// camera.h:20-21, 40-42: the camera-space x of pixel column px / y of row py at sample offset
+// (sx, sy).  The kernels read both from per-frame tables built on the host with these same
+// operations (rt_scene's ndc tables: x depends on (px, s) only, y on (py, s) only).
+__host__ __device__ __forceinline__ float cam_x(uint32_t px, float sx, uint32_t W, float fov_xs)
+{
+    const float ndc_x = (float(px) + sx) / float(W) * 2.0f - 1.0f;
+    return ndc_x * fov_xs;
+}
+__host__ __device__ __forceinline__ float cam_y(uint32_t py, float sy, uint32_t H, float fov_xs, float aspect)
+{
+    const float ndc_y = (float(py) + sy) / float(H) * 2.0f - 1.0f;
+    return ndc_y * fov_xs / aspect;
+}
+
+// camera.h:8-47 GenerateRay, perspective branch. The per-frame constants fov_xs
 // (= (float)tan(double), hazard H5), aspect and the origin are computed on the host.
 __device__ __forceinline__ void gen_dir(const float* m, float fov_xs, float aspect, uint32_t px, uint32_t py,
                                         uint32_t W, uint32_t H, float sx, float sy,
                                         float& dx, float& dy, float& dz)
 {
-    const float ndc_x = (float(px) + sx) / float(W) * 2.0f - 1.0f;
-    const float ndc_y = (float(py) + sy) / float(H) * 2.0f - 1.0f;
-    float x = ndc_x * fov_xs, y = ndc_y * fov_xs / aspect, z = -1.0f;
-    normalize3(x, y, z);
-    // lin_alg.h:495-509 Transf3x3 (row-vector convention: m[r][c], r = input component)
-    dx = x * m[0] + y * m[3] + z * m[6];
-    dy = x * m[1] + y * m[4] + z * m[7];
-    dz = x * m[2] + y * m[5] + z * m[8];
+    dir_from_xy(m, cam_x(px, sx, W, fov_xs), cam_y(py, sy, H, fov_xs, aspect), dx, dy, dz);
 }
 
 // triangle.h:158-161 + lin_alg.h:151-156 + renderer.cpp:110-117

@@ -102,6 +102,8 @@ struct KParams
     uint32_t W, H, spp, spp_shift;
     float inv_spp;              // 2^-spp_shift when spp is a power of two (x/spp == x*inv_spp), else 0
     const float2 *smp;          // [spp] sample offsets
+    const float *ndcx;          // [W * spp] camera-space x of (column, sample): rtd::cam_x, per frame shape
+    const float *ndcy;          // [H * spp] camera-space y of (row, sample): rtd::cam_y
     // grid (grid.h:28-39)
     float bmin[3], bmax[3];
     float cw, icw;
@@ -208,6 +210,15 @@ __device__ __forceinline__ uint32_t *wave_counters()
 __device__ __forceinline__ bool wave_all(bool p)
 {
     return __builtin_amdgcn_ballot_w64(p) == __builtin_amdgcn_ballot_w64(true);
+}
+
+// v of lane (lane & ~3) + J: a DPP quad_perm broadcast within each quad of lanes (every lane of
+// the quad must be active, as in process_item's resolve, where the whole wave is)
+template <int J>
+__device__ __forceinline__ float quad_bcast(float v)
+{
+    constexpr int ctrl = J | (J << 2) | (J << 4) | (J << 6);
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), ctrl, 0xF, 0xF, false));
 }
 
 __device__ __forceinline__ bool first_active_lane()
@@ -872,9 +883,8 @@ __device__ __forceinline__ void trace_sample(const KParams& P, uint32_t px, uint
                                              float& cg, float& cb, uint32_t& hit_tri, rt_sample_rec *rec,
                                              uint32_t off = 0u)
 {
-    const float2 so = P.smp[s];
     float dx, dy, dz;
-    rtd::gen_dir(P.m, P.fov_xs, P.aspect, px, py, P.W, P.H, so.x, so.y, dx, dy, dz);
+    rtd::dir_from_xy(P.m, P.ndcx[px * P.spp + s], P.ndcy[py * P.spp + s], dx, dy, dz);    // camera.h:8-47
     float t = 0.0f, u = 0.0f, v = 0.0f;
     uint32_t tri = rtd::kNoTri, voxel = rtd::kNoTri, steps = 0, tests = 0;
     bool hit;
@@ -1003,18 +1013,29 @@ __device__ __forceinline__ void process_item(const KParams& P, uint32_t item, ui
     // rt_render_hits_device only: the sample's hit triangle, after the walk (a scalar test of a
     // kernel parameter; the walk above is the same code whatever the pointer holds)
     if (Q.hits && ic.valid) Q.hits[(size_t(ic.y) * Q.W + ic.x) * Q.spp + ic.s] = hit_tri;
-    const uint32_t base = lane & ~(Q.spp - 1u);
     float sr = 0.0f, sg = 0.0f, sb = 0.0f;
-    for (uint32_t k = 0; k < Q.spp; k++)
+    if (Q.spp == 4u)
     {
-        sr += __shfl(cr, int(base + k), 64);
-        sg += __shfl(cg, int(base + k), 64);
-        sb += __shfl(cb, int(base + k), 64);
+        // the bench's 4 spp: a pixel's samples are one quad of lanes, so each sample's colour is
+        // a quad broadcast (DPP, one VALU) instead of an LDS permute; same values, same order
+        sr = sr + quad_bcast<0>(cr) + quad_bcast<1>(cr) + quad_bcast<2>(cr) + quad_bcast<3>(cr);
+        sg = sg + quad_bcast<0>(cg) + quad_bcast<1>(cg) + quad_bcast<2>(cg) + quad_bcast<3>(cg);
+        sb = sb + quad_bcast<0>(cb) + quad_bcast<1>(cb) + quad_bcast<2>(cb) + quad_bcast<3>(cb);
+    }
+    else
+    {
+        const uint32_t base = lane & ~(Q.spp - 1u);
+        for (uint32_t k = 0; k < Q.spp; k++)
+        {
+            sr += __shfl(cr, int(base + k), 64);
+            sg += __shfl(cg, int(base + k), 64);
+            sb += __shfl(cb, int(base + k), 64);
+        }
     }
     if (ic.valid && ic.s == 0)
     {
-        const uint32_t word = rtd::pack_bgra8(rtd::gamma_half(average(Q, sr)), rtd::gamma_half(average(Q, sg)),
-                                              rtd::gamma_half(average(Q, sb)));
+        const uint32_t word = rtd::pack_bgra8(rtd::gamma_fast(average(Q, sr)), rtd::gamma_fast(average(Q, sg)),
+                                              rtd::gamma_fast(average(Q, sb)));
         store_pixel(Q, ic.c, ic.p, ic.x, ic.y, word);
     }
 }
@@ -1238,9 +1259,8 @@ __device__ __forceinline__ void wide_trace(const KParams& P, uint32_t k, uint32_
         const ItemCoord ic = tile_slot_coord(P, k, slot);
         if (ic.valid)
         {
-            const float2 so = P.smp[ic.s];
             float dx, dy, dz;
-            rtd::gen_dir(P.m, P.fov_xs, P.aspect, ic.x, ic.y, P.W, P.H, so.x, so.y, dx, dy, dz);
+            rtd::dir_from_xy(P.m, P.ndcx[ic.x * P.spp + ic.s], P.ndcy[ic.y * P.spp + ic.s], dx, dy, dz);
             float nct0, nct1, nct2, dt0, dt1, dt2;
             int rem0, rem1, rem2, cs0, cs1, cs2, cell;
             bool hit = false;
@@ -1354,8 +1374,8 @@ __device__ __forceinline__ void wide_samples(const KParams& P, uint32_t k, uint3
     }
     if (ic.valid && ic.s == 0 && sub == 0)
     {
-        const uint32_t word = rtd::pack_bgra8(rtd::gamma_half(average(P, sr)), rtd::gamma_half(average(P, sg)),
-                                              rtd::gamma_half(average(P, sb)));
+        const uint32_t word = rtd::pack_bgra8(rtd::gamma_fast(average(P, sr)), rtd::gamma_fast(average(P, sg)),
+                                              rtd::gamma_fast(average(P, sb)));
         store_pixel(P, ic.c, ic.p, ic.x, ic.y, word);
     }
 }
@@ -1607,9 +1627,9 @@ k_render_compact(KParams P, uint32_t n_items, uint32_t refill)
             }
             if (ic.valid && ic.s == 0)
             {
-                const uint32_t word = rtd::pack_bgra8(rtd::gamma_half(average(P, sr)),
-                                                      rtd::gamma_half(average(P, sg)),
-                                                      rtd::gamma_half(average(P, sb)));
+                const uint32_t word = rtd::pack_bgra8(rtd::gamma_fast(average(P, sr)),
+                                                      rtd::gamma_fast(average(P, sg)),
+                                                      rtd::gamma_fast(average(P, sb)));
                 store_pixel(P, ic.c, ic.p, ic.x, ic.y, word);
             }
         }
@@ -1664,8 +1684,8 @@ k_render_compact(KParams P, uint32_t n_items, uint32_t refill)
                     const ItemCoord ic = item_coord(P, L.item[wv][slot], j);
                     if (ic.valid)
                     {
-                        const float2 so = P.smp[ic.s];
-                        rtd::gen_dir(P.m, P.fov_xs, P.aspect, ic.x, ic.y, P.W, P.H, so.x, so.y, dx, dy, dz);
+                        rtd::dir_from_xy(P.m, P.ndcx[ic.x * P.spp + ic.s], P.ndcy[ic.y * P.spp + ic.s], dx, dy,
+                                         dz);
                         if (dda_setup(P, ox, oy, oz, dx, dy, dz, nct0, nct1, nct2, dt0, dt1, dt2, rem0, rem1, rem2,
                                       cs0, cs1, cs2, cell))
                         {
@@ -1744,8 +1764,8 @@ __global__ void __launch_bounds__(kWG) k_render_pixel_loop(KParams P)
         if (P.hits) P.hits[(size_t(y) * P.W + x) * P.spp + s] = hit_tri;
         sr += cr; sg += cg; sb += cb;
     }
-    store_pixel(P, c, p, x, y, rtd::pack_bgra8(rtd::gamma_half(average(P, sr)), rtd::gamma_half(average(P, sg)),
-                                               rtd::gamma_half(average(P, sb))));
+    store_pixel(P, c, p, x, y, rtd::pack_bgra8(rtd::gamma_fast(average(P, sr)), rtd::gamma_fast(average(P, sg)),
+                                               rtd::gamma_fast(average(P, sb))));
 }
 
 // Debug records: one thread per sample of the rectangle, order (y, x, s)
@@ -1812,6 +1832,18 @@ __global__ void __launch_bounds__(kWG) k_rcp_check(unsigned long long *bad)
         if (ex == 255u || (b & 0x7FFFFFFFu) == 0u) continue;
         const float x = __uint_as_float(b);
         if (__float_as_uint(rtd::rcp_nr(x)) != __float_as_uint(1.0f / x)) atomicAdd(&bad[ex], 1ull);
+    }
+}
+
+// Exhaustive check of the packed gamma bytes: every non-negative float (bits 0 .. 0x7F800000,
+// +inf included), pack_channel of the hardware sqrt vs of the correctly rounded one.
+__global__ void __launch_bounds__(kWG) k_gamma_check(unsigned long long *bad)
+{
+    for (uint32_t b = blockIdx.x * blockDim.x + threadIdx.x; b <= 0x7F800000u; b += gridDim.x * blockDim.x)
+    {
+        const float x = __uint_as_float(b);
+        if (rtd::pack_channel(rtd::gamma_fast(x)) != rtd::pack_channel(rtd::gamma_half(x))) atomicAdd(bad, 1ull);
+        if (b == 0x7F800000u) break;
     }
 }
 
@@ -1897,7 +1929,7 @@ __global__ void __launch_bounds__(kWG) k_primitives(int kind, const float *in, u
     {
         const float *a = in + 3 * i;
         float *o = out + 4 * i;
-        const float r = rtd::gamma_half(a[0]), g = rtd::gamma_half(a[1]), b = rtd::gamma_half(a[2]);
+        const float r = rtd::gamma_fast(a[0]), g = rtd::gamma_fast(a[1]), b = rtd::gamma_fast(a[2]);   // the resolve's
         o[0] = r; o[1] = g; o[2] = b; o[3] = __uint_as_float(rtd::pack_bgra8(r, g, b));
     }
     else if (kind == 4)
@@ -2029,6 +2061,11 @@ struct rt_scene
     uint32_t wh_fused = 1;          // RT_WH_FUSED: a batch's wide section leads the batch kernel's grid
                                     // (0: its own kernel on the side stream, fork / join)
     bool octant_words = false;      // 8 ray-octant copies of the empty-run words (else one L-inf word)
+    // camera-space x / y tables of the current frame shape (prepare_ndc)
+    float *d_ndc = nullptr;
+    size_t ndc_cap = 0;
+    std::vector<float> ndc_key;
+    uint32_t ndc_w = 0, ndc_spp = 0;
     // sample table cache
     float2 *d_smp = nullptr;
     uint32_t smp_cap = 0;
@@ -2073,14 +2110,78 @@ int ensure_device(const rt_scene *s)
 }
 
 // Uploads the frame's sample table if it differs from the cached one.
-int prepare_samples(rt_scene *s, const rt_frame *f, uint32_t spp)
+// The scene's per-frame constants that live in device memory are rewritten only after its last
+// launch has finished with them (launches are asynchronous; the copies are not stream-ordered).
+int wait_scene_idle(rt_scene *s)
+{
+    if (s->ev_recorded) RT_HIP(hipEventSynchronize(s->ev1));
+    return RT_OK;
+}
+
+// camera.h:41-42 fov_xs = (float)tan(double(DegToRad(fov) / 2)) (H5), computed on the host
+float fov_xs_of(const rt_frame *f)
+{
+    const float hfov = f->fov * float(0.0174532925);           // lin_alg.h:232 DegToRad
+    return float(::tan(double(hfov / 2.0f)));
+}
+
+// Camera-space x per (column, sample) and y per (row, sample) of GenerateRay (camera.h:20-21,
+// 40-42): the only parts of a ray's direction that depend on the pixel and the sample offsets
+// alone, computed here with the kernels' own operations (rtd::cam_x / cam_y: IEEE float on the
+// host too, no contraction) and uploaded when the frame shape changes.  tbl = the sample table.
+std::vector<float> ndc_key(const rt_frame *f, uint32_t spp, const std::vector<float>& tbl)
+{
+    std::vector<float> key = { float(f->width), float(f->height), float(spp), fov_xs_of(f),
+                               float(f->width) / float(f->height) };
+    key.insert(key.end(), tbl.begin(), tbl.end());
+    return key;
+}
+
+// the sample table of a frame (rt_frame.sample_offsets, or the Hammersley table)
+std::vector<float> sample_table(const rt_frame *f, uint32_t spp)
 {
     std::vector<float> tbl;
     if (f->sample_offsets)
         tbl.assign(f->sample_offsets, f->sample_offsets + 2 * size_t(spp));
     else
         hammersley(spp, tbl);
+    return tbl;
+}
+
+int prepare_ndc(rt_scene *s, const rt_frame *f, uint32_t spp, const std::vector<float>& tbl)
+{
+    const float fx = fov_xs_of(f), aspect = float(f->width) / float(f->height);
+    std::vector<float> key = ndc_key(f, spp, tbl);
+    if (key == s->ndc_key) return RT_OK;
+    const size_t n = (size_t(f->width) + f->height) * spp;
+    std::vector<float> h(n);
+    for (uint32_t x = 0; x < f->width; x++)
+        for (uint32_t k = 0; k < spp; k++) h[size_t(x) * spp + k] = rtd::cam_x(x, tbl[2 * k], f->width, fx);
+    float *hy = h.data() + size_t(f->width) * spp;
+    for (uint32_t y = 0; y < f->height; y++)
+        for (uint32_t k = 0; k < spp; k++) hy[size_t(y) * spp + k] = rtd::cam_y(y, tbl[2 * k + 1], f->height, fx, aspect);
+    if (int rc = wait_scene_idle(s)) return rc;
+    if (n > s->ndc_cap)
+    {
+        if (s->d_ndc) RT_HIP(hipFree(s->d_ndc));
+        s->d_ndc = nullptr;
+        s->ndc_cap = 0;
+        RT_HIP(hipMalloc(&s->d_ndc, n * sizeof(float)));
+        s->ndc_cap = n;
+    }
+    RT_HIP(hipMemcpy(s->d_ndc, h.data(), n * sizeof(float), hipMemcpyHostToDevice));
+    s->ndc_key = key;
+    s->ndc_w = f->width;
+    s->ndc_spp = spp;
+    return RT_OK;
+}
+
+int prepare_samples(rt_scene *s, const rt_frame *f, uint32_t spp)
+{
+    const std::vector<float> tbl = sample_table(f, spp);
+    if (int rc = prepare_ndc(s, f, spp, tbl)) return rc;
     if (tbl == s->smp_host) return RT_OK;
+    if (int rc = wait_scene_idle(s)) return rc;
     if (spp > s->smp_cap)
     {
         if (s->d_smp) RT_HIP(hipFree(s->d_smp));
@@ -2129,9 +2230,10 @@ void frame_params(const rt_scene *s, const rt_frame *f, KParams& P)
     const float (*c)[4] = reinterpret_cast<const float (*)[4]>(f->cam);
     for (int r = 0; r < 3; r++)
         for (int k = 0; k < 3; k++) P.m[3 * r + k] = c[r][k];
-    const float hfov = f->fov * float(0.0174532925);           // lin_alg.h:232 DegToRad
-    P.fov_xs = float(::tan(double(hfov / 2.0f)));               // camera.h:42, double tan (H5)
+    P.fov_xs = fov_xs_of(f);                                    // camera.h:42, double tan (H5)
     P.aspect = float(f->width) / float(f->height);
+    P.ndcx = s->d_ndc;                                          // prepare_ndc (this frame's shape)
+    P.ndcy = s->d_ndc + size_t(s->ndc_w) * s->ndc_spp;
     for (int k = 0; k < 3; k++)                                 // lin_alg.h:518-535
         P.org[k] = 0.0f * c[0][k] + 0.0f * c[1][k] + 0.0f * c[2][k] + c[3][k];
     P.W = f->width;
@@ -3045,6 +3147,7 @@ int rt_scene_destroy(rt_scene *s)
         if (s->ev_fork) (void)hipEventDestroy(s->ev_fork);
         if (s->ev_join) (void)hipEventDestroy(s->ev_join);
         (void)hipFree(s->d_smp);
+        (void)hipFree(s->d_ndc);
         (void)hipFree(s->d_frame);
         if (s->h_smp_pinned) (void)hipHostFree(s->h_smp_pinned);
         if (s->h_frame) (void)hipHostFree(s->h_frame);
@@ -3125,7 +3228,15 @@ int render_batch_chunk(rt_scene *const *S, const rt_frame *F, uint32_t n, uint32
             if ((rc = prepare_samples(S[i], &F[i], std::max(1u, F[i].spp)))) return rc;
             local = device_params(S[i], &F[i], rank, nranks, nranks > 1, outs[i], hits ? hits[i] : nullptr, P[i]);
         }
-        rc = launch_batch(S, F, n, P, local, static_cast<hipStream_t>(hip_stream), &batched);
+        // a scene listed twice with another camera table / sample table than its last frame's
+        // would read the last one's: such batches take one launch per frame
+        bool tables_ok = true;
+        for (uint32_t i = 0; i < n; i++)
+        {
+            const uint32_t spp = std::max(1u, F[i].spp);
+            tables_ok = tables_ok && ndc_key(&F[i], spp, sample_table(&F[i], spp)) == S[i]->ndc_key;
+        }
+        if (tables_ok) rc = launch_batch(S, F, n, P, local, static_cast<hipStream_t>(hip_stream), &batched);
         if (batched) return rc;
     }
     for (uint32_t i = 0; i < n; i++)
@@ -3453,6 +3564,24 @@ int rt_debug_rcp_check(uint64_t *bad_by_exponent, int device)
     if (e == hipSuccess) e = hipMemcpy(bad_by_exponent, d_bad, 256 * sizeof(uint64_t), hipMemcpyDeviceToHost);
     (void)hipFree(d_bad);
     if (e != hipSuccess) return fail(RT_E_HIP, std::string("rt_debug_rcp_check: ") + hipGetErrorString(e));
+    return RT_OK;
+}
+
+int rt_debug_gamma_check(uint64_t *mismatches, int device)
+{
+    if (!mismatches) return fail(RT_E_INVALID, "NULL argument");
+    RT_HIP(hipSetDevice(device));
+    unsigned long long *d_bad = nullptr;
+    RT_HIP(hipMalloc(&d_bad, sizeof(unsigned long long)));
+    hipError_t e = hipMemset(d_bad, 0, sizeof(unsigned long long));
+    if (e == hipSuccess)
+    {
+        hipLaunchKernelGGL(k_gamma_check, dim3(8192), dim3(kWG), 0, nullptr, d_bad);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpy(mismatches, d_bad, sizeof(uint64_t), hipMemcpyDeviceToHost);
+    (void)hipFree(d_bad);
+    if (e != hipSuccess) return fail(RT_E_HIP, std::string("rt_debug_gamma_check: ") + hipGetErrorString(e));
     return RT_OK;
 }
 

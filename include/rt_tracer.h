@@ -269,6 +269,10 @@ int  rt_debug_primitives(int kind, const float *in, uint32_t n, float *out, int 
    correctly rounded 1.0f / x for all 2^32 - 2^24 finite nonzero floats; bad_by_exponent[256]
    receives the mismatch count per biased exponent. */
 int  rt_debug_rcp_check(uint64_t *bad_by_exponent, int device);
+/* Exhaustive check of the resolve's gamma: for every non-negative float x (+inf included) the
+   packed byte of the hardware square root (rtd::gamma_fast) against that of the correctly rounded
+   sqrtf; *mismatches receives the count (0 = the kernels may use the hardware form). */
+int  rt_debug_gamma_check(uint64_t *mismatches, int device);
 /* Per 64-sample work item of the last RT_KERNEL_FLAG_WAVE_CLOCK launch on this scene, in launch
    item order, four words: {start, end} shader clock (s_memtime: per clock domain, for
    durations), records tested in wave-uniform list loops (bits 0-31; bits 32-35: the wave's XCD;

@@ -266,6 +266,13 @@ def test_newton_reciprocal_exhaustive():
     assert int(bad[1:253].sum()) == 0, {e: int(c) for e, c in enumerate(bad) if c}
 
 
+def test_gamma_hardware_sqrt_exhaustive():
+    """The resolve's gamma uses the hardware square root: its packed byte equals the correctly
+    rounded sqrtf's -- and so powf(., .5f)'s (test_gamma_exhaustive.py) -- for every non-negative
+    float."""
+    assert rtm.debug_gamma_check(0) == 0
+
+
 def test_auto_equals_arms(golden, scenes):
     """AUTO (heavy-first order), its LDS-staged arm, the plain LANES kernel and the compaction
     arm render the reference's bytes and per-sample hit IDs on the two bench scenes and the
