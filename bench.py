@@ -4,8 +4,9 @@
 A step renders one full 1920x1080x4spp frame of each scene (2 x 8,294,400 samples) through
 the HIP path into device memory (scene data resident in HBM before timing starts).  With
 N > 1 ranks (torchrun, one process per GPU, RCCL) every rank renders its interleaved 16x16
-tiles of each frame (tile t -> rank t % N), the shards are all-gathered over xGMI and rank 0
-un-permutes them into the frame (K3): strong scaling of a fixed frame.
+tiles of each frame (tile t -> rank t % N), the shards are gathered to rank 0 over xGMI (one
+step's gather overlapping the next step's render) and rank 0 un-permutes them into the frame
+(K3): strong scaling of a fixed frame.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload bench|head4096|batch10]
 
@@ -150,10 +151,10 @@ def moving_camera(work, steps, warmup, static_ms):
     def step(i):
         if work.batch:
             work.rtm.render_batch_device([g for _, _, g, _ in work.scenes], [p[i & 1] for p in frames],
-                                         [b.data_ptr() for b in work.bufs], stream=work.stream.cuda_stream)
+                                         [b.data_ptr() for b in work.bufs[0]], stream=work.stream.cuda_stream)
             return
         for j, (sid, hs, gs, f) in enumerate(work.scenes):
-            gs.render_frame_device(frames[j][i & 1], work.bufs[j].data_ptr(), work.stream.cuda_stream)
+            gs.render_frame_device(frames[j][i & 1], work.bufs[0][j].data_ptr(), work.stream.cuda_stream)
 
     with work.stream_ctx():
         for i in range(warmup):
@@ -270,7 +271,7 @@ class GpuWorkload:
     def __init__(self, rtm, torch, world, rank, local, kernel, batch=True):
         self.rtm, self.torch, self.world, self.rank = rtm, torch, world, rank
         self.batch = batch
-        self.graphs = None              # hipGraphs of the step's render launch(es) (--graph)
+        self.graphs = None              # per buffer set: hipGraph of the step's render launch(es) (--graph)
         self.samples = {}               # timed launches per scene in the timed region
         self.gevents = {}
         self.scenes = []
@@ -280,7 +281,10 @@ class GpuWorkload:
             self.scenes.append((sid, hs, gs, gs.frame(W, H, SPP, kernel=kernel)))
         self.stream = torch.cuda.Stream()       # every launch, capture and collective of a step
         n = W * H if world == 1 else rtm.shard_elems(W, H, world)
-        self.bufs = [torch.empty(n, dtype=torch.int32, device="cuda") for _ in SCENES]
+        # bufs[set][scene]: two sets for N > 1, so one step's shards can be gathered while the next
+        # step renders into the other set (run_steps); one set at N = 1 (nothing is gathered)
+        self.bufs = [[torch.empty(n, dtype=torch.int32, device="cuda") for _ in SCENES]
+                     for _ in range(2 if world > 1 else 1)]
         self.frames = [torch.empty(W * H, dtype=torch.int32, device="cuda") for _ in SCENES]
         # scenes whose kernel-time ring holds a launch's time: every scene, or the first scene of
         # every batch launch
@@ -289,39 +293,44 @@ class GpuWorkload:
     def stream_ctx(self):
         return self.torch.cuda.stream(self.stream)
 
-    def render_all(self):
-        """This step's render launch(es): every scene's frame (or this rank's shard of it)."""
+    def render_all(self, p=0):
+        """This step's render launch(es) into buffer set p: every scene's frame (or this rank's
+        shard of it)."""
         if self.graphs is not None:
             a = self.torch.cuda.Event(enable_timing=True)
             b = self.torch.cuda.Event(enable_timing=True)
             a.record(self.stream)
-            self.graphs.replay()
+            self.graphs[p].replay()
             b.record(self.stream)
             self.gevents.setdefault("step", []).append((a, b))
             return
-        self._launch()
+        self._launch(p)
 
-    def _launch(self):
+    def _launch(self, p):
         st = self.stream.cuda_stream
+        bufs = self.bufs[p]
         if self.batch:
             self.rtm.render_batch_device([g for _, _, g, _ in self.scenes], [f for _, _, _, f in self.scenes],
-                                         [b.data_ptr() for b in self.bufs], self.rank, self.world, stream=st)
+                                         [b.data_ptr() for b in bufs], self.rank, self.world, stream=st)
             return
         for i, (sid, hs, gs, f) in enumerate(self.scenes):
             if self.world == 1:
-                gs.render_frame_device(f, self.bufs[i].data_ptr(), st)
+                gs.render_frame_device(f, bufs[i].data_ptr(), st)
             else:
-                gs.render_shard_device(f, self.rank, self.world, self.bufs[i].data_ptr(), st)
+                gs.render_shard_device(f, self.rank, self.world, bufs[i].data_ptr(), st)
 
     def capture(self):
-        """One hipGraph holding the step's render launch(es) (after the warm-up, so the
-        heavy-first order is the one the warm-up frames planned; replays keep it)."""
+        """One hipGraph per buffer set holding the step's render launch(es) (after the warm-up, so
+        the heavy-first order is the one the warm-up frames planned; replays keep it)."""
         self.sync()
-        g = self.torch.cuda.CUDAGraph()
-        with self.torch.cuda.graph(g, stream=self.stream):
-            self._launch()
+        graphs = []
+        for p in range(len(self.bufs)):
+            g = self.torch.cuda.CUDAGraph()
+            with self.torch.cuda.graph(g, stream=self.stream):
+                self._launch(p)
+            graphs.append(g)
         self.sync()
-        self.graphs = g
+        self.graphs = graphs
 
     def reset_times(self):
         self.gevents = {}
@@ -371,7 +380,7 @@ def check_frames(work, world):
     for i, (sid, hs, gs, f) in enumerate(work.scenes):
         f1 = gs.frame(W, H, SPP)
         gs.render_frame_device(f1, ref.data_ptr(), work.stream.cuda_stream)
-        got = work.frames[i] if world > 1 else work.bufs[i]
+        got = work.frames[i] if world > 1 else work.bufs[0][i]
         work.sync()
         if not torch.equal(ref, got):
             raise SystemExit(f"scene {sid}: frame assembled from {world} ranks differs from the one-GPU render")
@@ -380,45 +389,65 @@ def check_frames(work, world):
 
 def run_steps(work, world, rank, steps, warmup, dist=None, graph=False):
     """W untimed warm-up steps, then K timed steps between barrier+sync on both sides; returns
-    the max-over-ranks wall time.  A step renders every scene (this rank's tiles when N > 1);
-    each scene's shards are gathered to rank 0 (one RCCL gather: every peer sends its slice on
-    its own xGMI link) as soon as that scene is rendered, so the gather of scene 1 overlaps the
-    render of scene 8, and rank 0 un-permutes the frames."""
+    the max-over-ranks wall time.  A step renders every scene (this rank's tiles when N > 1) and
+    gathers each scene's shards to rank 0 (one RCCL gather: every peer sends its slice on its
+    own xGMI link), where K3 un-permutes them into the frame.
+
+    N > 1 is software-pipelined over two shard-buffer sets (work.bufs[set][scene]): step i
+    renders into set i % 2 and issues its gathers, and only then waits for step i-1's gathers
+    and un-permutes them, so one step's gather runs on the collective stream while the next
+    step renders.  The stream waits keep every buffer safe: step i+1 renders into step i-1's set
+    after the wait on step i-1's gathers, and rank 0's gather buffers of a set are refilled two
+    steps later, after K3 read them.  The pipeline is drained (the last step's frames assembled)
+    before the timed region ends."""
+    nsets = len(work.bufs)
     gathered = []
     if world > 1:
         import torch
-        gathered = [torch.empty(world * b.numel(), dtype=b.dtype, device=b.device) if rank == 0 else None
-                    for b in work.bufs]
+        gathered = [[torch.empty(world * b.numel(), dtype=b.dtype, device=b.device) if rank == 0 else None
+                     for b in bset] for bset in work.bufs]
 
     rooted = [True]    # one RCCL gather to rank 0; the all-gather if this torch build lacks it
 
-    def collect(i):
+    def collect(p, i):
+        buf = work.bufs[p][i]
         if rooted[0]:
             try:
-                return work.rtm.gather_shards(work.bufs[i], world, dst=0, out=gathered[i], async_op=True)
+                return work.rtm.gather_shards(buf, world, dst=0, out=gathered[p][i], async_op=True)
             except (RuntimeError, NotImplementedError) as e:    # raised on every rank alike
                 print(f"bench: rooted gather unavailable ({e}); using the all-gather", file=sys.stderr)
                 rooted[0] = False
-        if gathered[i] is None:
+        if gathered[p][i] is None:
             import torch
-            gathered[i] = torch.empty(world * work.bufs[i].numel(), dtype=work.bufs[i].dtype,
-                                      device=work.bufs[i].device)
-        return work.rtm.all_gather_shards(work.bufs[i], world, out=gathered[i], async_op=True)
+            gathered[p][i] = torch.empty(world * buf.numel(), dtype=buf.dtype, device=buf.device)
+        return work.rtm.all_gather_shards(buf, world, out=gathered[p][i], async_op=True)
+
+    pending = []       # the previous step's gathers: [(gathered, handle)] per scene
+    it = [0]
+
+    def finish():
+        """Wait for the pending step's gathers (a stream wait under RCCL) and un-permute them."""
+        for i, (g, h) in enumerate(pending):
+            if h is not None:
+                h.wait()
+            if rank == 0:
+                work.unshard(i, g)
+        pending.clear()
 
     def step():
-        work.render_all()
+        p = it[0] % nsets
+        it[0] += 1
+        work.render_all(p)
         if world > 1:
-            pending = [collect(i) for i in range(len(SCENES))]
-            for i, (g, h) in enumerate(pending):
-                if h is not None:
-                    h.wait()
-                if rank == 0:
-                    work.unshard(i, g)
+            issued = [collect(p, i) for i in range(len(SCENES))]
+            finish()
+            pending.extend(issued)
 
     ctx = work.stream_ctx() if hasattr(work, "stream_ctx") else contextlib.nullcontext()
     with ctx:
         for _ in range(warmup):
             step()
+        finish()
         if graph:
             work.capture()
     work.sync()
@@ -430,13 +459,14 @@ def run_steps(work, world, rank, steps, warmup, dist=None, graph=False):
     with ctx:
         for _ in range(steps):
             step()
+        finish()                       # the last step's frames are assembled inside the timed region
     work.sync()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
         import torch
-        dev = work.bufs[0].device
+        dev = work.bufs[0][0].device
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())

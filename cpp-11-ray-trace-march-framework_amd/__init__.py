@@ -45,6 +45,7 @@ RT_KERNEL_FLAG_LDS_CELLS = 0x80
 RT_KERNEL_FLAG_WIDE_HEAVY = 0x200
 RT_KERNEL_FLAG_EXHAUSTIVE = 0x8000
 RT_KERNEL_FLAG_WAVE_CLOCK = 0x400000
+RT_KERNEL_FLAG_COOP_PAIRS = 0x1000
 RT_KERNEL_BUDGET_SHIFT = 24              # COMPACT: idle lanes before a refill (1..64)
 RT_KERNEL_BUDGET_MASK = 0x7F000000
 RT_KERNEL_COMPACT_REFILL_SHIFT = RT_KERNEL_BUDGET_SHIFT
@@ -767,11 +768,21 @@ class Renderer:
 
 
 # ------------------------------------------------------------------ multi-GPU helpers
+SHARD_ROT = 3     # rt_tracer.hip kShardRot: tile rows rotated by 3 columns per row before the deal
+
+
 def shard_tile_ids(width, height, rank, nranks):
-    """Tile indices (16x16 tiles, row-major) owned by `rank`: t % nranks == rank."""
+    """Tile indices (16x16 tiles, row-major) owned by `rank`, in local-tile order:
+    the rotated number t' = ty * tiles_x + (tx + SHARD_ROT * ty) % tiles_x of a tile is dealt
+    t' % nranks == rank (no rotation at one rank), as rt_tracer.hip's shard_tile_xy."""
     tiles_x = (width + SHARD_TILE - 1) // SHARD_TILE
     tiles_y = (height + SHARD_TILE - 1) // SHARD_TILE
-    return list(range(rank, tiles_x * tiles_y, nranks))
+    out = []
+    for tp in range(rank, tiles_x * tiles_y, nranks):
+        ty, xr = divmod(tp, tiles_x)
+        rot = (SHARD_ROT * ty) % tiles_x if nranks > 1 else 0
+        out.append(ty * tiles_x + (xr - rot) % tiles_x)
+    return out
 
 
 def shard_from_frame(frame, rank, nranks):
@@ -795,7 +806,8 @@ def frame_from_shards(gathered, width, height, nranks):
     elems = gathered.size // nranks
     tiles_x = (width + SHARD_TILE - 1) // SHARD_TILE
     y, x = np.mgrid[0:height, 0:width]
-    t = (y // 16) * tiles_x + x // 16
+    rot = (SHARD_ROT * (y // 16)) % tiles_x if nranks > 1 else 0
+    t = (y // 16) * tiles_x + (x // 16 + rot) % tiles_x
     r, k = t % nranks, t // nranks
     return gathered[r * elems + k * 256 + (y % 16) * 16 + (x % 16)].astype(np.uint32)
 

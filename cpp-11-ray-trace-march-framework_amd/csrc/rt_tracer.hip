@@ -77,6 +77,7 @@ constexpr int kVarLdsCells = 262144;        // RT_KERNEL_FLAG_LDS_CELLS: long un
 constexpr int kVarWideHeavy = 524288;       // RT_KERNEL_FLAG_WIDE_HEAVY: heavy items traced wide at the start
 constexpr int kVarWideFused = 1048576;      // batch kernel: the wide section's blocks lead the same grid
 constexpr int kVarWideG4 = 2097152;         // the wide section at 4 lanes per sample (spp 8-16; else 16)
+constexpr int kVarCoop = 4194304;           // RT_KERNEL_FLAG_COOP_PAIRS: divergent cell lists as (ray, record) pairs
 // AUTO's traversal: every feature above that is exact for every scene ...
 constexpr int kVarAutoCore = kVarWaveGate | kVarDistSkip | kVarOriginPre | kVarXcdBands | kVarUniform;
 // ... plus the two that need a scene property (rt_scene::rcp_safe, rt_scene::pack_ok)
@@ -130,7 +131,7 @@ struct KParams
     // work decomposition
     uint32_t rx0, ry0, rw, rh;  // region of the frame rendered by this launch
     uint32_t tiles_x;           // 16x16 tiles across the region
-    uint32_t rank, nranks;      // tile t is ours iff t % nranks == rank, local index t / nranks
+    uint32_t rank, nranks;      // local tile k = row-rotated tile rank + k * nranks (shard_tile_xy)
     uint32_t wg_per_tile;
     uint32_t xcd_chunk;         // kVarXcdBands: consecutive blocks per XCD turn (0 = one band each)
     uint64_t *wave_clk;         // kVarWaveClock: {start, end, uniform tests, lane-loop iterations} per item
@@ -298,7 +299,45 @@ typedef float vf4 __attribute__((ext_vector_type(4)));
 // are written by k_origin_pre, an earlier launch) select s_load through the scalar cache
 typedef const __attribute__((address_space(4))) vf4 cvf4;
 
+// The per-lane list loop of the per-camera-record test: this lane's list [kb, ke) in order
+// (grid.cpp:243-267), lowering tb on every accepted hit.  The first-half terms (r0..r2) per
+// iteration, the second-half terms (r3) only when the gate passes.  Measured against a one-ahead
+// prefetch in VGPRs (+12, 6 waves/SIMD) and by LDS-DMA into a per-wave slot
+// (global_load_lds_dwordx4; no VGPRs, but four DMA issues per record): both slower on the frame
+// and no shorter on the lone heavy waves (profiles/r02e_ab_lane_prefetch.json).
+template <bool STATS, int VAR>
+__device__ __forceinline__ void lane_list(const KParams& P, rtd::f2v ra, rtd::f2v rc, uint32_t kb, uint32_t ke,
+                                          float& tb, float& u, float& v, uint32_t& tri, uint32_t& tests)
+{
+    constexpr bool F = (VAR & kVarFastRcp) != 0;
+    for (uint32_t k = kb; k < ke; k++)
+    {
+        if constexpr ((VAR & kVarWaveClock) != 0)
+            if (first_active_lane()) wave_counters()[1] += 1u;
+        if (STATS) tests++;
+        const float4 *rp = P.frefs + size_t(k) * 4u;     // one address, immediate offsets
+        const float4 r0 = rp[0], r1 = rp[1], r2 = rp[2];
+        float inv, pu;
+        const bool ok1 = rtd::mt_rec_first<F>(ra, rc, rtd::f2v{r0.x, r0.y}, rtd::f2v{r0.z, r0.w},
+                                              rtd::f2v{r1.x, r1.y}, rtd::f2v{r1.z, r1.w},
+                                              rtd::f2v{r2.x, r2.y}, inv, pu);
+        if (__any(ok1))
+        {
+            const float2 r3 = *reinterpret_cast<const float2 *>(rp + 3);
+            float pv, pt;
+            const bool h = ok1 & rtd::mt_rec_second(ra, rc, rtd::f2v{r2.z, r2.w}, r3.x, r3.y, inv, pu, pv, pt);
+            const bool take = h & (pt < tb);
+            tb = take ? pt : tb;
+            u = take ? pu : u;
+            v = take ? pv : v;
+            tri = take ? k : tri;
+        }
+    }
+}
+
 // Tests a cell's list [kb, ke) in order (grid.cpp:243-267); true when it produced a hit.
+// kVarCoop: a list the testing lanes do not share is not tested here -- *defer is set and the
+// caller's wave-cooperative pass (coop_cells) tests it.
 // grid.cpp:258-260 accepts cur_t when cur_t < t && cur_t < next_crossing_t[step_axis].  t is
 // FLT_MAX on entry (a hit ends the walk, grid.cpp:270-271) and neither bound is ever NaN, so the
 // two compares are one against tb = min(t, nct_ax), which every accepted hit lowers to its t:
@@ -306,7 +345,7 @@ typedef const __attribute__((address_space(4))) vf4 cvf4;
 template <bool STATS, int TRI, int VAR>
 __device__ __forceinline__ bool test_cell(const KParams& P, float ox, float oy, float oz, float dx, float dy,
                                           float dz, uint32_t kb, uint32_t ke, float nct_ax, float& t,
-                                          float& u, float& v, uint32_t& tri, uint32_t& tests)
+                                          float& u, float& v, uint32_t& tri, uint32_t& tests, bool *defer = nullptr)
 {
     constexpr bool PRE = (VAR & kVarOriginPre) != 0 && TRI == RT_TRI_MOLLER_TRUMBORE;
     constexpr bool F = (VAR & kVarFastRcp) != 0;
@@ -459,34 +498,13 @@ __device__ __forceinline__ bool test_cell(const KParams& P, float ox, float oy, 
     {
         if (!uniform_done)
         {
-            // Per-lane lists: the first-half terms (r0..r2) per iteration, the second-half terms
-            // (r3) only when the gate passes.  Measured against a one-ahead prefetch in VGPRs
-            // (+12, 6 waves/SIMD) and by LDS-DMA into a per-wave slot (global_load_lds_dwordx4;
-            // no VGPRs, but four DMA issues per record): both slower on the frame and no shorter
-            // on the lone heavy waves (profiles/r02e_ab_lane_prefetch.json).
-            for (uint32_t k = kb; k < ke; k++)
+            if constexpr ((VAR & kVarCoop) != 0)
             {
-                if constexpr ((VAR & kVarWaveClock) != 0)
-                    if (first_active_lane()) wave_counters()[1] += 1u;
-                if (STATS) tests++;
-                const float4 *rp = P.frefs + size_t(k) * 4u;     // one address, immediate offsets
-                const float4 r0 = rp[0], r1 = rp[1], r2 = rp[2];
-                float inv, pu;
-                const bool ok1 = rtd::mt_rec_first<F>(ra, rc, rtd::f2v{r0.x, r0.y}, rtd::f2v{r0.z, r0.w},
-                                                      rtd::f2v{r1.x, r1.y}, rtd::f2v{r1.z, r1.w},
-                                                      rtd::f2v{r2.x, r2.y}, inv, pu);
-                if (__any(ok1))
-                {
-                    const float2 r3 = *reinterpret_cast<const float2 *>(rp + 3);
-                    float pv, pt;
-                    const bool h = ok1 & rtd::mt_rec_second(ra, rc, rtd::f2v{r2.z, r2.w}, r3.x, r3.y, inv, pu, pv, pt);
-                    const bool take = h & (pt < tb);
-                    tb = take ? pt : tb;
-                    u = take ? pu : u;
-                    v = take ? pv : v;
-                    tri = take ? k : tri;
-                }
+                *defer = true;
+                return false;
             }
+            else
+                lane_list<STATS, VAR>(P, ra, rc, kb, ke, tb, u, v, tri, tests);
         }
     }
     else
@@ -518,6 +536,149 @@ __device__ __forceinline__ bool test_cell(const KParams& P, float ox, float oy, 
     }
     t = tb < tb0 ? tb : t;
     return t != rtd::kFltMax;                                  // grid.cpp:270-271
+}
+
+// kVarCoop: the wave-cooperative pass over the cell lists the lanes do NOT share (SURVEY §7 step 4,
+// the north_star's ballot/prefix compaction of the traversal): at such a DDA step the per-lane loop
+// runs max(L) iterations while the wave holds sum(L) useful (ray, record) pairs -- killeroo 1080p x 4:
+// 1.04 M per-lane iterations at 64 % lane utilisation (tools/wave_sim.cpp).  Here every lane still
+// walking (owners and lanes in empty cells alike) takes a contiguous run of ceil(T / n) of the T
+// pairs, in (owner, list position) order:
+//  * T, each owner's first pair S (exclusive prefix of L in lane order) and max(L) come from
+//    bit-plane ballots (L < 2^11: the packed cell word's count);
+//  * owners publish {S, end, kb - S, tb0, ray direction} in the wave's LDS slots by owner ordinal;
+//    a helper finds the owner of its first pair by binary search over the starts and moves to the
+//    next owner where its run crosses an end;
+//  * a helper keeps the lexicographic minimum of (t, list position) over its accepted pairs -- a
+//    hit with t < tb0 = min(t, nct_ax), exactly grid.cpp:258-260's condition -- and merges it into
+//    the owner's slot with one 64-bit LDS atomic min per owner it served.  t >= 0 (+0 for -0:
+//    the reference's '<' does not tell them apart), so its bits order like the floats, and the
+//    minimum is the reference's first minimum in list order (strict '<', H8);
+//  * each owner re-tests its winning record with its own ray for the exact t, u, v.
+// Not beneficial (ceil(T / n) + kCoopMargin >= max(L)): the owners run lane_list as before.
+constexpr uint32_t kCoopMargin = 6;     // setup cost in record-test iterations
+
+struct CoopOwner { uint32_t end, kbase; float tb0, dx, dy, dz; };
+
+template <int VAR>
+__device__ __forceinline__ bool coop_cells(const KParams& P, float dx, float dy, float dz, bool own, uint32_t kb,
+                                           uint32_t ke, float nct_ax, float& t, float& u, float& v, uint32_t& tri)
+{
+    constexpr bool F = (VAR & kVarFastRcp) != 0;
+    const uint32_t L = own ? ke - kb : 0u;
+    const uint64_t act = __ballot(1);
+    const uint32_t nact = uint32_t(__popcll(act));
+    auto below = [](uint64_t m) {                 // set bits of m in the lanes below this one
+        return __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
+    };
+    uint32_t S = 0u, T = 0u, top = 0u;
+    for (uint32_t b = 0; b < 11u; b++)
+    {
+        const uint64_t m = __ballot((L >> b) & 1u);
+        S += below(m) << b;
+        T += uint32_t(__popcll(m)) << b;
+        top = m ? b : top;
+    }
+    uint32_t M = 0u;                              // max(L): the highest bit planes in turn
+    bool cand = own;
+    for (int b = int(top); b >= 0; b--)
+    {
+        const bool has = cand && ((L >> b) & 1u);
+        if (__ballot(has))
+        {
+            M |= 1u << b;
+            cand = has;
+        }
+    }
+    const rtd::f2v ra = {dx, dy}, rc = {dy, dz};
+    const float tb0 = t < nct_ax ? t : nct_ax;
+    const uint32_t R = (T + nact - 1u) / nact;    // pairs per helper
+    if (R + kCoopMargin >= M)
+    {
+        float tb = tb0;
+        uint32_t tests = 0u;
+        if (own) lane_list<false, VAR>(P, ra, rc, kb, ke, tb, u, v, tri, tests);
+        if (tb < tb0) t = tb;
+        return own && t != rtd::kFltMax;
+    }
+    __shared__ uint32_t s_start[kWavesPerWG][64];
+    __shared__ CoopOwner s_own[kWavesPerWG][64];
+    __shared__ unsigned long long s_best[kWavesPerWG][64];
+    const uint32_t w = threadIdx.x >> 6;
+    const uint64_t om = __ballot(own);
+    const uint32_t nown = uint32_t(__popcll(om));
+    const uint32_t oo = below(om);                // owner ordinal (starts ascend with it)
+    if (own)
+    {
+        s_start[w][oo] = S;
+        s_own[w][oo] = CoopOwner{S + L, kb - S, tb0, dx, dy, dz};
+        s_best[w][oo] = ~0ull;
+    }
+    wave_lds_sync();
+    uint32_t p = below(act) * R;
+    const uint32_t pend = min(p + R, T);
+    uint32_t o = 0u;                              // the last owner whose start is <= p
+    for (uint32_t st = 32u; st; st >>= 1)
+        if (o + st < nown && s_start[w][o + st] <= p) o += st;
+    CoopOwner c = s_own[w][o];
+    unsigned long long best = ~0ull;
+    for (uint32_t j = 0; j < R; j++)
+    {
+        if (p < pend)
+        {
+            const uint32_t k = c.kbase + p;
+            const float4 *rp = P.frefs + size_t(k) * 4u;
+            const float4 r0 = rp[0], r1 = rp[1], r2 = rp[2];
+            const rtd::f2v pa = {c.dx, c.dy}, pc = {c.dy, c.dz};
+            float inv, pu;
+            const bool ok1 = rtd::mt_rec_first<F>(pa, pc, rtd::f2v{r0.x, r0.y}, rtd::f2v{r0.z, r0.w},
+                                                  rtd::f2v{r1.x, r1.y}, rtd::f2v{r1.z, r1.w}, rtd::f2v{r2.x, r2.y},
+                                                  inv, pu);
+            if (__any(ok1))
+            {
+                const float2 r3 = *reinterpret_cast<const float2 *>(rp + 3);
+                float pv, pt;
+                const bool h = ok1 & rtd::mt_rec_second(pa, pc, rtd::f2v{r2.z, r2.w}, r3.x, r3.y, inv, pu, pv, pt);
+                // (t, pair index): within one owner the pair index orders like the list position
+                const unsigned long long key = (uint64_t(__float_as_uint(pt + 0.0f)) << 32) | uint64_t(p);
+                best = (h & (pt < c.tb0) & (key < best)) ? key : best;
+            }
+            p++;
+            if (p == c.end && p < pend)
+            {
+                if (best != ~0ull) atomicMin(&s_best[w][o], best);
+                best = ~0ull;
+                o++;
+                c = s_own[w][o];
+            }
+        }
+    }
+    if (best != ~0ull) atomicMin(&s_best[w][o], best);
+    wave_lds_sync();
+    bool hit = false;
+    if (own)
+    {
+        const unsigned long long b = s_best[w][oo];
+        if (b != ~0ull)
+        {
+            // the winner re-tested with this lane's own ray: the values the per-lane loop keeps
+            const uint32_t k = uint32_t(b) - S + kb;
+            const float4 *rp = P.frefs + size_t(k) * 4u;
+            const float4 r0 = rp[0], r1 = rp[1], r2 = rp[2];
+            const float2 r3 = *reinterpret_cast<const float2 *>(rp + 3);
+            float inv, pu, pv, pt;
+            rtd::mt_rec_first<F>(ra, rc, rtd::f2v{r0.x, r0.y}, rtd::f2v{r0.z, r0.w}, rtd::f2v{r1.x, r1.y},
+                                 rtd::f2v{r1.z, r1.w}, rtd::f2v{r2.x, r2.y}, inv, pu);
+            rtd::mt_rec_second(ra, rc, rtd::f2v{r2.z, r2.w}, r3.x, r3.y, inv, pu, pv, pt);
+            t = pt;
+            u = pu;
+            v = pv;
+            tri = k;
+            hit = true;
+        }
+    }
+    wave_lds_sync();                              // the slots are reused by the next pass
+    return hit;
 }
 
 // One DDA advance over plain local variables (grid.cpp:236-239 + 274-277), exact because
@@ -684,7 +845,15 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, float ox, float
             // below), and the result read from t after the loop: the walk's loop-carried state
             // stays in VGPRs instead of per-exit lane masks (SALU per wave, PMC-measured)
             bool hit = false;
-            if (kb < ke) hit = test_cell<STATS, TRI, VAR>(P, ox, oy, oz, dx, dy, dz, kb, ke, nct_ax, t, u, v, tri, tests);
+            bool defer = false;
+            if (kb < ke)
+                hit = test_cell<STATS, TRI, VAR>(P, ox, oy, oz, dx, dy, dz, kb, ke, nct_ax, t, u, v, tri, tests, &defer);
+            if constexpr ((VAR & kVarCoop) != 0)
+                if (__any(defer))       // every lane still walking helps (converged here)
+                {
+                    const bool h = coop_cells<VAR>(P, dx, dy, dz, defer, kb, ke, nct_ax, t, u, v, tri);
+                    hit = defer ? h : hit;
+                }
             bool done = hit | !more;
             if constexpr ((VAR & kVarSkipRun) != 0 && (VAR & kVarPackedRem) != 0 && !STATS)
             {
@@ -936,15 +1105,39 @@ __device__ __forceinline__ void trace_sample(const KParams& P, uint32_t px, uint
 // Tile bookkeeping: block -> (local tile k, sub-block)
 struct TileCoord { uint32_t k, sub, tx0, ty0; };
 
+// Shard deal (nranks > 1): tile (tx, ty) has the row-rotated number
+// t' = ty * tiles_x + (tx + kShardRot * ty) mod tiles_x, and rank r owns t' = r, r + N, r + 2N, ...
+// as its local tiles 0, 1, 2, ...  The rotation turns t mod N's column stripes (1920 / 16 = 120
+// columns: every rank held the same columns in every row, so a compact heavy region fell on the
+// few ranks owning its columns) into a lattice; a rank's consecutive local tiles still lie in one
+// tile row (XCD bands, shard layout and shard sizes are unchanged).  One rank: no rotation.
+#ifndef RT_SHARD_ROT
+#define RT_SHARD_ROT 3
+#endif
+constexpr uint32_t kShardRot = RT_SHARD_ROT;
+
+__host__ __device__ __forceinline__ void shard_tile_xy(uint32_t k, uint32_t rank, uint32_t nranks, uint32_t tiles_x,
+                                                       uint32_t& tx, uint32_t& ty)
+{
+    const uint32_t t = rank + k * nranks;
+    ty = t / tiles_x;
+    tx = t - ty * tiles_x;
+    if (nranks > 1u)
+    {
+        const uint32_t r = (kShardRot * ty) % tiles_x;
+        tx = tx >= r ? tx - r : tx + tiles_x - r;
+    }
+}
+
 __device__ __forceinline__ TileCoord tile_of_block(const KParams& P)
 {
     TileCoord c;
     c.k = blockIdx.x / P.wg_per_tile;
     c.sub = blockIdx.x - c.k * P.wg_per_tile;
-    const uint32_t t = P.rank + c.k * P.nranks;
-    const uint32_t tyi = t / P.tiles_x;
-    c.tx0 = P.rx0 + (t - tyi * P.tiles_x) * kTile;
-    c.ty0 = P.ry0 + tyi * kTile;
+    uint32_t tx, ty;
+    shard_tile_xy(c.k, P.rank, P.nranks, P.tiles_x, tx, ty);
+    c.tx0 = P.rx0 + tx * kTile;
+    c.ty0 = P.ry0 + ty * kTile;
     return c;
 }
 
@@ -970,10 +1163,10 @@ __device__ __forceinline__ ItemCoord tile_slot_coord(const KParams& P, uint32_t 
 {
     ItemCoord ic;
     ic.c.k = k;
-    const uint32_t t = P.rank + ic.c.k * P.nranks;
-    const uint32_t tyi = t / P.tiles_x;
-    ic.c.tx0 = P.rx0 + (t - tyi * P.tiles_x) * kTile;
-    ic.c.ty0 = P.ry0 + tyi * kTile;
+    uint32_t tx, ty;
+    shard_tile_xy(k, P.rank, P.nranks, P.tiles_x, tx, ty);
+    ic.c.tx0 = P.rx0 + tx * kTile;
+    ic.c.ty0 = P.ry0 + ty * kTile;
     ic.p = slot >> P.spp_shift;                               // pixel index in the tile (Morton)
     ic.s = slot & (P.spp - 1u);
     ic.x = ic.c.tx0 + compact_bits(ic.p);
@@ -1798,7 +1991,10 @@ __global__ void __launch_bounds__(kWG) k_unshard(const uint32_t *g, uint32_t *ou
     const uint32_t x = blockIdx.x * 64 + (threadIdx.x & 63u);
     const uint32_t y = blockIdx.y * 4 + (threadIdx.x >> 6);
     if (x >= W || y >= H) return;
-    const uint32_t t = (y / kTile) * tiles_x + x / kTile;
+    // the inverse of shard_tile_xy's deal
+    const uint32_t ty = y / kTile, rot = nranks > 1u ? (kShardRot * ty) % tiles_x : 0u;
+    const uint32_t tr = x / kTile + rot;
+    const uint32_t t = ty * tiles_x + (tr >= tiles_x ? tr - tiles_x : tr);
     const uint32_t r = t % nranks, k = t / nranks;
     out[size_t(y) * W + x] = g[r * shard_elems + size_t(k) * kTilePix + (y % kTile) * kTile + (x % kTile)];
 }
@@ -2200,7 +2396,7 @@ int prepare_samples(rt_scene *s, const rt_frame *f, uint32_t spp)
 }
 
 constexpr uint32_t kKernelFlags = RT_KERNEL_FLAG_WIDE_HEAVY | RT_KERNEL_FLAG_LDS_CELLS | RT_KERNEL_FLAG_EXHAUSTIVE |
-                                  RT_KERNEL_FLAG_WAVE_CLOCK | RT_KERNEL_BUDGET_MASK;
+                                  RT_KERNEL_FLAG_WAVE_CLOCK | RT_KERNEL_FLAG_COOP_PAIRS | RT_KERNEL_BUDGET_MASK;
 
 int validate_frame(const rt_frame *f)
 {
@@ -2426,6 +2622,9 @@ kfn_t lanes_kernel(int tri, int var)
     case kVarAuto | kVarLdsCells: return k_render_lanes<RT_TRI_MOLLER_TRUMBORE, kVarAuto | kVarLdsCells>;
     case kVarAuto | kVarLdsCells | kVarWaveClock:
         return k_render_lanes<RT_TRI_MOLLER_TRUMBORE, kVarAuto | kVarLdsCells | kVarWaveClock>;
+    case kVarAuto | kVarCoop: return k_render_lanes<RT_TRI_MOLLER_TRUMBORE, kVarAuto | kVarCoop>;
+    case kVarAuto | kVarCoop | kVarWideHeavy:
+        return k_render_lanes<RT_TRI_MOLLER_TRUMBORE, kVarAuto | kVarCoop | kVarWideHeavy>;
     default: return nullptr;
     }
 }
@@ -2461,6 +2660,8 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
         var = kVarAutoCore | (s->rcp_safe ? kVarFastRcp : 0) | (s->pack_ok ? kVarPackedRem | kVarSkipRun : 0) |
               ((f->kernel & RT_KERNEL_FLAG_LDS_CELLS) ? kVarLdsCells : 0) |
               ((f->kernel & RT_KERNEL_FLAG_WAVE_CLOCK) ? kVarWaveClock : 0);
+        // the cooperative pair pass needs the full AUTO walk (packed counts, empty runs, records)
+        if ((f->kernel & RT_KERNEL_FLAG_COOP_PAIRS) && var == kVarAuto && kind == RT_KERNEL_AUTO) var |= kVarCoop;
         if (int rc = ensure_origin_terms(s, P, st)) return rc;
     }
     else if (lanes && P.isect == RT_ISECT_RAY_MARCH)
@@ -2509,7 +2710,7 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
     // two-phase arm it replaced -> 0.35 / 0.20 / 0.15).  On a whole frame the
     // lanes are busy with other items anyway and the section's repeated walks cost more than they
     // save (+1-3 %).
-    const bool wide_ok = auto_path && var == kVarAuto && P.spp <= 16u;
+    const bool wide_ok = auto_path && (var & ~kVarCoop) == kVarAuto && P.spp <= 16u;
     const bool wide_heavy = wide_ok && kind == RT_KERNEL_AUTO &&
                             ((f->kernel & RT_KERNEL_FLAG_WIDE_HEAVY) ||
                              (P.nranks >= 2u && s->max_cell_refs >= s->wh_auto_refs));

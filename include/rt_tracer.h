@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 5
+#define RT_ABI_VERSION 6   /* 6: row-rotated shard deal */
 
 enum rt_status {
     RT_OK = 0,
@@ -106,6 +106,12 @@ enum rt_kernel {
                                           lanes per sample, 4 for spp 8-16) by a kernel on the scene's
                                           side stream, beside the one-lane-per-sample kernel (fork /
                                           join) */
+    RT_KERNEL_FLAG_COOP_PAIRS = 0x1000, /* OR-able (AUTO, grid): at a DDA step whose testing lanes
+                                           sit in different cells, every lane still walking takes
+                                           an equal run of the wave's (ray, record) pairs (ballot
+                                           prefix sums, LDS owner slots, a (t, position) minimum per
+                                           ray) instead of each lane looping its own list (A/B arm,
+                                           identical results) */
     RT_KERNEL_FLAG_EXHAUSTIVE = 0x8000, /* OR-able, ray march: evaluate every triangle per step
                                            (no block culling; A/B arm, identical results) */
     RT_KERNEL_FLAG_WAVE_CLOCK = 0x400000, /* OR-able (AUTO), debug: record s_memtime {start, end} of
@@ -206,8 +212,11 @@ int  rt_host_free(void *p);
 int  rt_render_frame_device(rt_scene *scene, const rt_frame *frame, uint32_t *d_bgra,
                             void *hip_stream);
 
-/* Multi-GPU sharding: the frame is cut into 16x16 pixel tiles, numbered row-major; tile t
- * is owned by rank t % nranks.  A rank renders its tiles compactly into d_shard
+/* Multi-GPU sharding: the frame is cut into 16x16 pixel tiles; tile (tx, ty) gets the
+ * row-rotated number t' = ty*tiles_x + (tx + 3*ty) % tiles_x (tiles_x = ceil(width/16); no
+ * rotation when nranks == 1) and is owned by rank t' % nranks as its local tile t' / nranks.  The
+ * rotation spreads a compact heavy region over every rank (plain t % nranks deals whole tile
+ * columns to a rank when nranks divides tiles_x).  A rank renders its tiles compactly into d_shard
  * (rt_shard_elems words, tile-local row-major, 256 words per tile); after an all-gather of
  * the equal-sized shards, rt_unshard_device rebuilds the frame. */
 int  rt_shard_elems(uint32_t width, uint32_t height, uint32_t nranks, uint64_t *elems);

@@ -1,6 +1,8 @@
-"""bench.py's multi-rank step (render shard -> all-gather -> rank-0 un-permute -> timing with
-barrier + max over ranks) driven under gloo on CPU, world_size 2.  The GPU render is replaced
-by the oracle rendering this rank's tiles; everything else is bench.run_steps itself."""
+"""bench.py's multi-rank step (render shard -> gather -> rank-0 un-permute -> timing with
+barrier + max over ranks, pipelined over two shard-buffer sets) driven under gloo on CPU,
+world_size 2.  The GPU render is replaced by the oracle's frame of this rank's tiles, XORed with
+the step number so a frame assembled from the wrong step or buffer set shows; everything else
+is bench.run_steps itself."""
 import os
 import socket
 
@@ -21,14 +23,20 @@ class CpuWorkload:
         orc = Oracle()
         self.full = [orc.render(sid, W, H, SPP, nthreads=1)[0] for sid in scenes]
         n = rtm.shard_elems(W, H, world)
-        self.bufs = [torch.zeros(n, dtype=torch.int32) for _ in scenes]
+        self.bufs = [[torch.zeros(n, dtype=torch.int32) for _ in scenes] for _ in range(2)]
         self.frames = [None for _ in scenes]
         self.renders = 0
+        self.sets = []
 
-    def render_all(self):
+    def expected(self, i, step):
+        return self.full[i] ^ np.uint32(step)
+
+    def render_all(self, p=0):
+        step = self.renders // len(self.full)
+        self.sets.append(p)
         for i in range(len(self.full)):
-            shard = self.rtm.shard_from_frame(self.full[i], self.rank, self.world)
-            self.bufs[i].copy_(torch.from_numpy(shard.view(np.int32)))
+            shard = self.rtm.shard_from_frame(self.expected(i, step), self.rank, self.world)
+            self.bufs[p][i].copy_(torch.from_numpy(shard.view(np.int32)))
             self.renders += 1
 
     def unshard(self, i, gathered):
@@ -51,7 +59,9 @@ def _worker(rank, world, port, q):
         work = CpuWorkload(rtm, world, rank, bench.SCENES)
         elapsed = bench.run_steps(work, world, rank, steps=3, warmup=1, dist=dist)
         if rank == 0:
-            same = all(np.array_equal(work.frames[i], work.full[i]) for i in range(len(bench.SCENES)))
+            # the drained pipeline holds the last (4th) step's frames; steps alternate buffer sets
+            same = all(np.array_equal(work.frames[i], work.expected(i, 3)) for i in range(len(bench.SCENES)))
+            same = same and work.sets == [0, 1, 0, 1]
             q.put(("ok", same, elapsed, work.renders))
         dist.barrier()
     except Exception as e:  # pragma: no cover

@@ -1,5 +1,5 @@
 """Multi-rank sharding on CPU (gloo, world_size 2 and 3): every rank renders only the 16x16
-tiles it owns (t % N == rank), shards are all-gathered and gathered to rank 0, rank 0
+tiles it owns (row-rotated t' % N == rank), shards are all-gathered and gathered to rank 0, rank 0
 un-permutes, and the frame is
 byte-identical to the single-process frame (partition invariance).
 The per-tile pixels come from the oracle here; on GPUs the same layout is produced by

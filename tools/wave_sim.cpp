@@ -143,6 +143,7 @@ int main(int argc, char **argv)
     const uint32_t nth = std::max(1u, std::thread::hardware_concurrency());
     std::vector<Acc> acc(nth);
     std::atomic<uint32_t> next(0);
+    std::vector<double> item_cost(nitems, 0.0);     // modelled VALU of each work item (shard balance)
     std::vector<std::thread> pool;
     for (uint32_t th = 0; th < nth; th++)
         pool.emplace_back([&, th]() {
@@ -166,6 +167,7 @@ int main(int argc, char **argv)
                     maxlen = std::max<uint32_t>(maxlen, uint32_t(lanes[l].cell.size()));
                 }
                 Acc& a = acc[th];
+                const Acc a0 = a;
                 a.waves++;
                 a.steps += maxlen;
                 // AUTO's two loops (grid_intersect): an outer iteration processes cell j of every
@@ -235,6 +237,11 @@ int main(int argc, char **argv)
                     const int b = int(10.0 * sum / (64.0 * mx));
                     a.hist_util[b]++; a.hist_util_w[b] += mx;
                 }
+                // VALU model of the item (per wave instruction counts of AUTO's loops):
+                // outer DDA iteration ~35, bare empty-run step ~22, uniform record ~25, per-lane
+                // list iteration ~35, ray setup + resolve ~150
+                item_cost[item] = 150.0 + 35.0 * double(a.outer - a0.outer) + 22.0 * double(a.inner - a0.inner) +
+                                  25.0 * double(a.uni_recs - a0.uni_recs) + 35.0 * double(a.lane_iters - a0.lane_iters);
             }
         });
     for (auto& t : pool) t.join();
@@ -256,6 +263,28 @@ int main(int argc, char **argv)
     for (int i = 0; i < 11; i++) std::printf("%s%llu", i ? ", " : "", (unsigned long long)a.hist_util[i]);
     std::printf("],\n \"lane_iterations_by_util_decile\": [");
     for (int i = 0; i < 11; i++) std::printf("%s%llu", i ? ", " : "", (unsigned long long)a.hist_util_w[i]);
-    std::printf("]}\n");
+    std::printf("],\n \"shard_balance\": {");
+    // per-rank modelled cost of tile-shard mappings: owner(tx, ty) = (ty * tiles_x + (tx + s * ty) mod
+    // tiles_x) mod N, i.e. every tile row rotated by s columns per row before the t mod N deal
+    // (s = 0: the plain t mod N), as max over ranks / mean
+    std::vector<double> tile_cost(tiles_x * tiles_y, 0.0);
+    for (uint32_t i = 0; i < nitems; i++) tile_cost[i / items_per_tile] += item_cost[i];
+    const char *sep = "";
+    for (uint32_t N : {2u, 4u, 8u})
+    {
+        std::printf("%s\"%u\": {", sep, N); sep = ", ";
+        for (uint32_t sh = 0; sh < 8; sh++)
+        {
+            std::vector<double> r(N, 0.0);
+            for (uint32_t ty = 0; ty < tiles_y; ty++)
+                for (uint32_t tx = 0; tx < tiles_x; tx++)
+                    r[(ty * tiles_x + (tx + sh * ty) % tiles_x) % N] += tile_cost[ty * tiles_x + tx];
+            double mx = 0, sum = 0;
+            for (double v : r) { mx = std::max(mx, v); sum += v; }
+            std::printf("%s\"s%u\": %.4f", sh ? ", " : "", sh, mx / (sum / N));
+        }
+        std::printf("}");
+    }
+    std::printf("}}\n");
     return 0;
 }
