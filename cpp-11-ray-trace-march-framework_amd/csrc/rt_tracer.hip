@@ -1227,8 +1227,8 @@ __device__ __forceinline__ void process_item(const KParams& P, uint32_t item, ui
     }
     if (ic.valid && ic.s == 0)
     {
-        const uint32_t word = rtd::pack_bgra8(rtd::gamma_fast(average(Q, sr)), rtd::gamma_fast(average(Q, sg)),
-                                              rtd::gamma_fast(average(Q, sb)));
+        const uint32_t word = rtd::pack_bgra8(rtd::gamma_half(average(Q, sr)), rtd::gamma_half(average(Q, sg)),
+                                              rtd::gamma_half(average(Q, sb)));
         store_pixel(Q, ic.c, ic.p, ic.x, ic.y, word);
     }
 }
@@ -1567,8 +1567,8 @@ __device__ __forceinline__ void wide_samples(const KParams& P, uint32_t k, uint3
     }
     if (ic.valid && ic.s == 0 && sub == 0)
     {
-        const uint32_t word = rtd::pack_bgra8(rtd::gamma_fast(average(P, sr)), rtd::gamma_fast(average(P, sg)),
-                                              rtd::gamma_fast(average(P, sb)));
+        const uint32_t word = rtd::pack_bgra8(rtd::gamma_half(average(P, sr)), rtd::gamma_half(average(P, sg)),
+                                              rtd::gamma_half(average(P, sb)));
         store_pixel(P, ic.c, ic.p, ic.x, ic.y, word);
     }
 }
@@ -1820,9 +1820,9 @@ k_render_compact(KParams P, uint32_t n_items, uint32_t refill)
             }
             if (ic.valid && ic.s == 0)
             {
-                const uint32_t word = rtd::pack_bgra8(rtd::gamma_fast(average(P, sr)),
-                                                      rtd::gamma_fast(average(P, sg)),
-                                                      rtd::gamma_fast(average(P, sb)));
+                const uint32_t word = rtd::pack_bgra8(rtd::gamma_half(average(P, sr)),
+                                                      rtd::gamma_half(average(P, sg)),
+                                                      rtd::gamma_half(average(P, sb)));
                 store_pixel(P, ic.c, ic.p, ic.x, ic.y, word);
             }
         }
@@ -1957,8 +1957,8 @@ __global__ void __launch_bounds__(kWG) k_render_pixel_loop(KParams P)
         if (P.hits) P.hits[(size_t(y) * P.W + x) * P.spp + s] = hit_tri;
         sr += cr; sg += cg; sb += cb;
     }
-    store_pixel(P, c, p, x, y, rtd::pack_bgra8(rtd::gamma_fast(average(P, sr)), rtd::gamma_fast(average(P, sg)),
-                                               rtd::gamma_fast(average(P, sb))));
+    store_pixel(P, c, p, x, y, rtd::pack_bgra8(rtd::gamma_half(average(P, sr)), rtd::gamma_half(average(P, sg)),
+                                               rtd::gamma_half(average(P, sb))));
 }
 
 // Debug records: one thread per sample of the rectangle, order (y, x, s)
@@ -2125,7 +2125,7 @@ __global__ void __launch_bounds__(kWG) k_primitives(int kind, const float *in, u
     {
         const float *a = in + 3 * i;
         float *o = out + 4 * i;
-        const float r = rtd::gamma_fast(a[0]), g = rtd::gamma_fast(a[1]), b = rtd::gamma_fast(a[2]);   // the resolve's
+        const float r = rtd::gamma_half(a[0]), g = rtd::gamma_half(a[1]), b = rtd::gamma_half(a[2]);   // the resolve's
         o[0] = r; o[1] = g; o[2] = b; o[3] = __uint_as_float(rtd::pack_bgra8(r, g, b));
     }
     else if (kind == 4)

@@ -280,7 +280,8 @@ int  rt_debug_primitives(int kind, const float *in, uint32_t n, float *out, int 
 int  rt_debug_rcp_check(uint64_t *bad_by_exponent, int device);
 /* Exhaustive check of the resolve's gamma: for every non-negative float x (+inf included) the
    packed byte of the hardware square root (rtd::gamma_fast) against that of the correctly rounded
-   sqrtf; *mismatches receives the count (0 = the kernels may use the hardware form). */
+   sqrtf; *mismatches receives the count (0 would let the kernels use the hardware form; MI355X
+   reports 80, so the resolve keeps sqrtf). */
 int  rt_debug_gamma_check(uint64_t *mismatches, int device);
 /* Per 64-sample work item of the last RT_KERNEL_FLAG_WAVE_CLOCK launch on this scene, in launch
    item order, four words: {start, end} shader clock (s_memtime: per clock domain, for

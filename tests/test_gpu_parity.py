@@ -267,10 +267,11 @@ def test_newton_reciprocal_exhaustive():
 
 
 def test_gamma_hardware_sqrt_exhaustive():
-    """The resolve's gamma uses the hardware square root: its packed byte equals the correctly
-    rounded sqrtf's -- and so powf(., .5f)'s (test_gamma_exhaustive.py) -- for every non-negative
-    float."""
-    assert rtm.debug_gamma_check(0) == 0
+    """Why the resolve keeps the correctly rounded sqrtf (hazard H6): the hardware square root
+    (v_sqrt_f32, 1 ulp) packs a different byte than sqrtf -- and so powf(., .5f) -- for some
+    non-negative floats (80 on MI355X), which shows up in full frames of several scenes; the
+    kernels' own gamma is pinned by the device KAT and every frame SHA."""
+    assert rtm.debug_gamma_check(0) > 0
 
 
 def test_auto_equals_arms(golden, scenes):
