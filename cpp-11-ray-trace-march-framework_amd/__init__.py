@@ -23,7 +23,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 # Everything librt_tracer.so is compiled from: PMC counter files are valid only for this hash
 KERNEL_SOURCES = ("csrc/rt_tracer.hip", "csrc/rt_grid_build.hip", "csrc/rt_device.h",
-                  "csrc/rt_internal.h", "csrc/Makefile", "../include/rt_tracer.h")
+                  "csrc/rt_internal.h", "csrc/rt_box_words.h", "csrc/Makefile", "../include/rt_tracer.h")
 
 
 def kernel_source_hash():
@@ -126,7 +126,8 @@ class SceneInfo(ctypes.Structure):
     _fields_ = [("octant_words", c_u32), ("packed_cells", c_u32), ("rcp_safe", c_u32), ("pack_ok", c_u32),
                 ("max_cell_refs", c_u32), ("hf_floor", c_u32), ("hf_min_blocks", c_u32), ("wh_floor", c_u32),
                 ("wh_alpha16", c_u32), ("wh_auto_refs", c_u32), ("wh_fused", c_u32), ("hf_contexts", c_u32),
-                ("hf_evictions", ctypes.c_uint64), ("device_bytes", ctypes.c_uint64)]
+                ("hf_evictions", ctypes.c_uint64), ("device_bytes", ctypes.c_uint64),
+                ("box_words", c_u32), ("reserved", c_u32)]
 
 
 SAMPLE_REC_DTYPE = np.dtype([("hit", "<u4"), ("tri", "<u4"), ("voxel", "<u4"), ("steps", "<u4"),

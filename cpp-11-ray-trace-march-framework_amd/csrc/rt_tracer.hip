@@ -36,6 +36,7 @@
 #include "../../include/rt_tracer.h"
 #include "rt_device.h"
 #include "rt_internal.h"
+#include "rt_box_words.h"
 
 namespace {
 
@@ -115,6 +116,8 @@ struct KParams
     const uint32_t *cellw;      // packed cell words (start << 11 | count) or null
     const uint32_t *cellwo;     // the dist-skip walks' words: 8 ray-octant copies, or = cellw
     uint32_t oct_stride;        // words per octant copy (ncells), 0 when cellwo == cellw
+    const uint32_t *cellwb;     // kVarSkipRun: box-run words, 24 copies (ray octant x major axis)
+    uint32_t box_stride;        // words per copy (ncells)
     const float4 *refs;
     const float4 *frefs;        // per camera origin (kVarOriginPre), 3 float4 per reference
     const float4 *shade;
@@ -730,6 +733,65 @@ constexpr int kRemGuards = int((1u << 10) | (1u << 21) | (1u << 31));
         cell += a2_ ? cs2 : (a1_ ? cs1 : cs0);                                                 \
     } while (0)
 
+// RT_DDA_ADVANCE_PACKED without the exit test: a step inside a proven-empty run (the
+// empty-run blocks of grid_intersect read MORE from the packed word after the block).
+#define RT_DDA_BARE_STEP()                                                                     \
+    do {                                                                                       \
+        const float m_ = __builtin_fminf(__builtin_fminf(nct0, nct1), nct2);                   \
+        const bool a2_ = nct2 == m_;                                                           \
+        const bool a1_ = !a2_ && nct1 == m_;                                                   \
+        const bool a0_ = !a2_ && !a1_;                                                         \
+        remp -= a2_ ? (1 << 22) : (a1_ ? (1 << 11) : 1);                                       \
+        nct0 += a0_ ? dt0 : 0.0f;                                                              \
+        nct1 += a1_ ? dt1 : 0.0f;                                                              \
+        nct2 += a2_ ? dt2 : 0.0f;                                                              \
+        cell += a2_ ? cs2 : (a1_ ? cs1 : cs0);                                                 \
+    } while (0)
+
+// Empty-run steps in blocks with one vote per block (1) or one vote per step (0, the round-2 loop)
+#ifndef RT_SKIP_BLOCKS
+#define RT_SKIP_BLOCKS 1
+#endif
+// AUTO's empty runs over the box-run words (1, build_box_words) or the octant cube words (0)
+#ifndef RT_BOX_RUN
+#define RT_BOX_RUN 1
+#endif
+
+// The box-run walk's step: RT_DDA_ADVANCE_PACKED, with the step axis' unit also taken from the
+// box counts (boxw, build_box_words' empty-cell layout = the packed counts' layout): a count
+// that was 0 borrows into its guard bit when the step leaves the box.
+#define RT_DDA_ADVANCE_BOX(NCT_AX, MORE)                                                       \
+    do {                                                                                       \
+        const float m_ = __builtin_fminf(__builtin_fminf(nct0, nct1), nct2);                   \
+        const bool a2_ = nct2 == m_;                                                           \
+        const bool a1_ = !a2_ && nct1 == m_;                                                   \
+        const bool a0_ = !a2_ && !a1_;                                                         \
+        NCT_AX = m_;                                                                           \
+        const int u_ = a2_ ? (1 << 22) : (a1_ ? (1 << 11) : 1);                                \
+        remp -= u_;                                                                            \
+        boxw -= u_;                                                                            \
+        MORE = (remp & kRemGuards) == 0;                                                       \
+        nct0 += a0_ ? dt0 : 0.0f;                                                              \
+        nct1 += a1_ ? dt1 : 0.0f;                                                              \
+        nct2 += a2_ ? dt2 : 0.0f;                                                              \
+        cell += a2_ ? cs2 : (a1_ ? cs1 : cs0);                                                 \
+    } while (0)
+#define RT_DDA_BOX_BARE_STEP()                                                                 \
+    do {                                                                                       \
+        const float m_ = __builtin_fminf(__builtin_fminf(nct0, nct1), nct2);                   \
+        const bool a2_ = nct2 == m_;                                                           \
+        const bool a1_ = !a2_ && nct1 == m_;                                                   \
+        const bool a0_ = !a2_ && !a1_;                                                         \
+        const int u_ = a2_ ? (1 << 22) : (a1_ ? (1 << 11) : 1);                                \
+        remp -= u_;                                                                            \
+        boxw -= u_;                                                                            \
+        nct0 += a0_ ? dt0 : 0.0f;                                                              \
+        nct1 += a1_ ? dt1 : 0.0f;                                                              \
+        nct2 += a2_ ? dt2 : 0.0f;                                                              \
+        cell += a2_ ? cs2 : (a1_ ? cs1 : cs0);                                                 \
+    } while (0)
+constexpr int kBoxUnits3 = 3 | (3 << 11) | (3 << 22);   // 3 in every box-count field
+
 // Grid entry + per-axis DDA setup of Grid::Intersect (aabb.h:9-83, grid.h:44-51,
 // grid.cpp:174-216), axis arrays unrolled into scalars.  Instead of pos/step/out per axis the
 // walk keeps the cells left before 'pos == out' (rem) and the signed GridIdx stride of a step
@@ -795,6 +857,16 @@ __device__ __forceinline__ int oct_offset(const KParams& P, float dx, float dy, 
     return int(o * P.oct_stride);
 }
 
+// Offset of the ray's box-run copy in P.cellwb: octant (as oct_offset) x 3 + major axis (the
+// largest |d| component; any choice is exact, the copy only shapes the boxes for speed).
+__device__ __forceinline__ int box_offset(const KParams& P, float dx, float dy, float dz)
+{
+    const uint32_t o = uint32_t(dx < 0.0f) | (uint32_t(dy < 0.0f) << 1) | (uint32_t(dz < 0.0f) << 2);
+    const float ax = __builtin_fabsf(dx), ay = __builtin_fabsf(dy), az = __builtin_fabsf(dz);
+    const uint32_t m = (ax >= ay && ax >= az) ? 0u : (ay >= az ? 1u : 2u);
+    return int((o * 3u + m) * P.box_stride);
+}
+
 // grid.cpp:159-281 Grid::Intersect (NEW_GRID_TRAVERSAL), axis arrays unrolled into scalars
 // so nothing is runtime-indexed (no scratch).  Counters are compiled in only for records.
 template <bool STATS, int TRI, int VAR>
@@ -809,6 +881,80 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, float ox, float
                    cell))
         return false;
     t = rtd::kFltMax;
+
+#if RT_BOX_RUN
+    if constexpr ((VAR & kVarSkipRun) != 0 && (VAR & kVarPackedRem) != 0)
+    {
+        // Box runs (AUTO; build_box_words): a looked-up empty cell hands the lane an empty box
+        // (its corner at the cell, extending along the ray's octant) as per-axis step counts in
+        // the packed counts' layout.  Every step takes its axis unit from both words; while no
+        // box count has borrowed, the lane is inside the box and its cell is empty: no lookup,
+        // no test.  A non-empty cell's word leaves boxw = 0, so the next step borrows and looks
+        // the next cell up.  Same cells in the same order, same tests: only lookups of
+        // proven-empty cells are skipped.  Termination as below: every iteration that does not
+        // exit decrements a positive remaining-cell count.
+        int remp = rem0 | (rem1 << 11) | (rem2 << 22);
+        int boxw = kRemGuards;                              // no box yet: look the first cell up
+        const int coff = box_offset(P, dx, dy, dz);
+        cell += coff;
+        for (;;)
+        {
+            if (STATS) { voxel = uint32_t(cell - coff); steps++; }
+            uint32_t kb = 0, ke = 0;
+            float nct_ax;
+            bool more;
+            if ((boxw & kRemGuards) != 0)
+            {
+                const uint32_t w = P.cellwb[uint32_t(cell)];
+                const uint32_t ne = uint32_t(int(w) >> 31);           // all ones: a non-empty cell
+                kb = (w >> 11) & 0xFFFFFu;
+                ke = kb + (w & ne & 2047u);
+                boxw = int(w & ~ne);
+            }
+            RT_DDA_ADVANCE_BOX(nct_ax, more);
+            bool hit = false;
+            bool defer = false;
+            if (kb < ke)
+                hit = test_cell<STATS, TRI, VAR>(P, ox, oy, oz, dx, dy, dz, kb, ke, nct_ax, t, u, v, tri, tests, &defer);
+            if constexpr ((VAR & kVarCoop) != 0)
+                if (__any(defer))
+                {
+                    const bool h = coop_cells<VAR>(P, dx, dy, dz, defer, kb, ke, nct_ax, t, u, v, tri);
+                    hit = defer ? h : hit;
+                }
+            if constexpr (!STATS)
+            {
+                // Wave-uniform runs while every active lane is inside its box and the grid: blocks
+                // of 4 bare steps while every box count of every lane is >= 3 (the first three
+                // steps of a block stay inside; the fourth may leave, which the next vote sees),
+                // then single steps.  A lane leaving the grid inside a block keeps stepping to the
+                // block's end harmlessly (its state is dead; the guard borrow of its remaining-
+                // cell count is sticky for far more steps than a block holds).  A lane that hit
+                // holds boxw < 0 (guard set), so runs only start when no lane hit.
+                // (if + do-while: a while loop's exit edge made the compiler copy the whole walk
+                // state every iteration)
+                if (wave_all(((uint32_t(boxw) | uint32_t(remp)) & uint32_t(kRemGuards)) == 0u))
+                {
+                    if (wave_all(((uint32_t(boxw - kBoxUnits3) | uint32_t(remp)) & uint32_t(kRemGuards)) == 0u))
+                        do
+                        {
+                            RT_DDA_BOX_BARE_STEP();
+                            RT_DDA_BOX_BARE_STEP();
+                            RT_DDA_BOX_BARE_STEP();
+                            RT_DDA_BOX_BARE_STEP();
+                        } while (wave_all(((uint32_t(boxw - kBoxUnits3) | uint32_t(remp)) & uint32_t(kRemGuards)) == 0u));
+                    if (wave_all(((uint32_t(boxw) | uint32_t(remp)) & uint32_t(kRemGuards)) == 0u))
+                        do
+                            RT_DDA_BOX_BARE_STEP();
+                        while (wave_all(((uint32_t(boxw) | uint32_t(remp)) & uint32_t(kRemGuards)) == 0u));
+                    more = (remp & kRemGuards) == 0;
+                }
+            }
+            if (hit | !more) break;
+        }
+        return t != rtd::kFltMax;                            // t is only set by a hit
+    }
+#endif
 
     if (P.cellw && (VAR & kVarDistSkip))
     {
@@ -864,6 +1010,40 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, float ox, float
                 // does.  (A lane inside a run has no hit and more == true, so done is false.)
                 if (wave_all(skip > 0))
                 {
+#if RT_SKIP_BLOCKS
+                    // Blocks of 4, then 2, then 1 bare steps: one vote per block instead of one per
+                    // step, and no exit test inside a block.  A lane that leaves the grid inside a
+                    // block keeps stepping to the block's end, harmlessly: its state is dead (the
+                    // walk ends with no further lookup), and the borrow into a guard bit is sticky
+                    // for far more steps than a block holds (a field must count down 2^10 / 2^9
+                    // more times to clear it), so MORE read after the block is the exit test.  The
+                    // vote also requires every lane inside the grid: a lane with MORE false at the
+                    // entry (it left the grid on an empty cell's step) takes no block.
+                    auto run_ok = [&](int n) {    // (skip >= n) & more, as ONE integer compare
+                        return wave_all(((uint32_t(remp) & uint32_t(kRemGuards)) | (uint32_t(skip - n) & 0x80000000u)) ==
+                                        0u);
+                    };
+                    while (run_ok(4))
+                    {
+                        RT_DDA_BARE_STEP();
+                        RT_DDA_BARE_STEP();
+                        RT_DDA_BARE_STEP();
+                        RT_DDA_BARE_STEP();
+                        skip -= 4;
+                    }
+                    if (run_ok(2))
+                    {
+                        RT_DDA_BARE_STEP();
+                        RT_DDA_BARE_STEP();
+                        skip -= 2;
+                    }
+                    if (run_ok(1))
+                    {
+                        RT_DDA_BARE_STEP();
+                        skip -= 1;
+                    }
+                    more = (remp & kRemGuards) == 0;
+#else
                     do
                     {
                         skip--;
@@ -880,6 +1060,7 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, float ox, float
                         // (skip > 0) & more as ONE integer compare (skip >= 0 here)
                     } while (wave_all(((uint32_t(remp) & uint32_t(kRemGuards)) | (uint32_t(skip - 1) & 0x80000000u)) ==
                                       0u));
+#endif
                     done = !more;
                 }
             }
@@ -2227,6 +2408,7 @@ struct rt_scene
     float bmin[3], bmax[3], cw = 0, icw = 0;
     uint32_t ncells = 0, nrefs = 0, ntris = 0, max_cell_refs = 0;
     uint32_t *d_off = nullptr, *d_cellw = nullptr, *d_cellwo = nullptr, oct_stride = 0;
+    uint32_t *d_cellwb = nullptr, box_stride = 0;  // box-run words: 24 copies (octant x major axis)
     float4 *d_refs = nullptr, *d_shade = nullptr, *d_facen = nullptr, *d_frefs = nullptr;
     float4 *d_trimt = nullptr, *d_tridist = nullptr, *d_distblk = nullptr;
     uint32_t ndist_blk = 0;
@@ -2257,6 +2439,7 @@ struct rt_scene
     uint32_t wh_fused = 1;          // RT_WH_FUSED: a batch's wide section leads the batch kernel's grid
                                     // (0: its own kernel on the side stream, fork / join)
     bool octant_words = false;      // 8 ray-octant copies of the empty-run words (else one L-inf word)
+    bool box_words = false;         // 24 box-run word copies: AUTO's empty runs (kVarSkipRun)
     // camera-space x / y tables of the current frame shape (prepare_ndc)
     float *d_ndc = nullptr;
     size_t ndc_cap = 0;
@@ -2296,6 +2479,12 @@ struct rt_scene
 };
 
 namespace {
+
+// AUTO's packed counts + empty-run loop: dims <= 512 and (box-run build) the box words exist
+bool auto_runs(const rt_scene *s)
+{
+    return s->pack_ok && (RT_BOX_RUN == 0 || s->box_words);
+}
 
 int ensure_device(const rt_scene *s)
 {
@@ -2452,6 +2641,8 @@ void frame_params(const rt_scene *s, const rt_frame *f, KParams& P)
     P.cellw = s->d_cellw;
     P.cellwo = s->d_cellwo ? s->d_cellwo : s->d_cellw;
     P.oct_stride = s->d_cellwo ? s->oct_stride : 0u;
+    P.cellwb = s->d_cellwb;
+    P.box_stride = s->box_stride;
     P.refs = s->d_refs;
     P.frefs = s->d_frefs;
     P.shade = s->d_shade;
@@ -2657,7 +2848,7 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
     int var = 0;
     if (auto_path)
     {
-        var = kVarAutoCore | (s->rcp_safe ? kVarFastRcp : 0) | (s->pack_ok ? kVarPackedRem | kVarSkipRun : 0) |
+        var = kVarAutoCore | (s->rcp_safe ? kVarFastRcp : 0) | (auto_runs(s) ? kVarPackedRem | kVarSkipRun : 0) |
               ((f->kernel & RT_KERNEL_FLAG_LDS_CELLS) ? kVarLdsCells : 0) |
               ((f->kernel & RT_KERNEL_FLAG_WAVE_CLOCK) ? kVarWaveClock : 0);
         // the cooperative pair pass needs the full AUTO walk (packed counts, empty runs, records)
@@ -2839,7 +3030,7 @@ int launch_batch(rt_scene *const *S, const rt_frame *F, uint32_t n, KParams *P, 
         if (P[i].W != P[0].W || P[i].H != P[0].H || P[i].spp != spp || S[i]->device != S[0]->device)
             return RT_E_INVALID;
         const int v = kVarAutoCore | (S[i]->rcp_safe ? kVarFastRcp : 0) |
-                      (S[i]->pack_ok ? kVarPackedRem | kVarSkipRun : 0);
+                      (auto_runs(S[i]) ? kVarPackedRem | kVarSkipRun : 0);
         if (var >= 0 && v != var) return RT_E_INVALID;
         var = v;
         wide_heavy = wide_heavy || (F[i].kernel & RT_KERNEL_FLAG_WIDE_HEAVY) ||
@@ -3014,6 +3205,7 @@ int rt_scene_info_get(rt_scene *s, rt_scene_info *out)
     std::lock_guard<std::mutex> lk(s->mtx);
     std::memset(out, 0, sizeof(*out));
     out->octant_words = s->octant_words;
+    out->box_words = s->box_words;
     out->packed_cells = s->d_cellw != nullptr;
     out->rcp_safe = s->rcp_safe;
     out->pack_ok = s->pack_ok;
@@ -3041,6 +3233,8 @@ int rt_sample_table(uint32_t spp, float *out_xy)
 
 // Cap on the 8 octant copies of the cell words (device and host): 64 M cells at most.
 constexpr uint64_t kOctWordsMaxBytes = 256ull << 20;
+// ... and on the 24 box-run copies
+constexpr uint64_t kBoxWordsMaxBytes = 384ull << 20;
 
 int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
 {
@@ -3135,7 +3329,7 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
         facen[i] = make_float4(t.n[0], t.n[1], t.n[2], 0.0f);
     }
     // Packed cell ranges: start < 2^21 and count < 2^11 for every cell -> one load per DDA step
-    std::vector<uint32_t> cellw, cellwo;
+    std::vector<uint32_t> cellw, cellwo, cellwb;
     bool packable = nr < (1u << 21);
     for (uint32_t c = 0; c < nc && packable; c++) packable = g.cell_offsets[c + 1] - g.cell_offsets[c] < 2048u;
     if (packable)
@@ -3212,6 +3406,12 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
                 for (uint32_t c = 0; c < nc; c++)
                     cellwo[size_t(o) * nc + c] = (cellw[c] & 2047u) ? cellw[c] : (D[c] << 11);
             }
+        }
+        // AUTO's box-run words (build_box_words): the non-empty words keep start < 2^20
+        if (RT_BOX_RUN && nr < (1u << 20) && uint64_t(nc) * 24u * 4u <= kBoxWordsMaxBytes)
+        {
+            rtbox::build_box_words(g.cell_offsets, g.dims, cellwb);
+            s->box_words = true;
         }
     }
     for (uint32_t c = 0; c < nc; c++)
@@ -3302,11 +3502,17 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
             RT_HIP(hipMemcpy(s->d_cellwo, cellwo.data(), sizeof(uint32_t) * cellwo.size(), hipMemcpyHostToDevice));
             s->oct_stride = nc;
         }
+        if (!cellwb.empty())
+        {
+            RT_HIP(hipMalloc(&s->d_cellwb, sizeof(uint32_t) * cellwb.size()));
+            RT_HIP(hipMemcpy(s->d_cellwb, cellwb.data(), sizeof(uint32_t) * cellwb.size(), hipMemcpyHostToDevice));
+            s->box_stride = nc;
+        }
     }
     s->device_bytes = sizeof(uint32_t) * (nc + 1) +
                       sizeof(float4) * (refs.size() + nfrefs + shade.size() + facen.size() + trimt.size() +
                                         tridist.size() + distblk.size()) +
-                      sizeof(uint32_t) * (cellw.size() + cellwo.size());
+                      sizeof(uint32_t) * (cellw.size() + cellwo.size() + cellwb.size());
     RT_HIP(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
     RT_HIP(hipEventCreateWithFlags(&s->ev1, hipEventDisableTiming));
 
@@ -3329,6 +3535,7 @@ int rt_scene_destroy(rt_scene *s)
         (void)hipFree(s->d_facen);
         (void)hipFree(s->d_cellw);
         (void)hipFree(s->d_cellwo);
+        (void)hipFree(s->d_cellwb);
         (void)hipFree(s->d_trimt);
         (void)hipFree(s->d_tridist);
         (void)hipFree(s->d_distblk);

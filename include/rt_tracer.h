@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 6   /* 6: row-rotated shard deal */
+#define RT_ABI_VERSION 7   /* 7: rt_scene_info.box_words (box-run empty runs); 6: row-rotated shard deal */
 
 enum rt_status {
     RT_OK = 0,
@@ -314,6 +314,10 @@ typedef struct rt_scene_info {
     uint32_t hf_contexts;       /* heavy-first launch shapes remembered per scene */
     uint64_t hf_evictions;      /* launch shapes evicted (each restarts its heavy-first state) */
     uint64_t device_bytes;
+    uint32_t box_words;         /* 1: AUTO's empty runs use the 24 box-run word copies (octant x major
+                                   axis); 0: none (references >= 2^20 or above the size cap: AUTO then
+                                   walks without the packed counts and empty runs) */
+    uint32_t reserved;
 } rt_scene_info;
 int  rt_scene_info_get(rt_scene *scene, rt_scene_info *out);
 

@@ -40,7 +40,7 @@ def test_struct_layouts():
 
 def test_host_side_entry_points_without_gpu():
     L = rtm.tracer_lib()
-    assert L.rt_abi_version() == 6
+    assert L.rt_abi_version() == 7
     # Hammersley table matches the reference's (renderer.cpp:49-60), 4 spp in SURVEY H12
     np.testing.assert_array_equal(rtm.sample_table(4), [[-.5, -.5], [-.25, 0], [0, -.25], [.25, .25]])
     e = rtm.shard_elems(1920, 1080, 8)

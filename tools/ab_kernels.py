@@ -19,7 +19,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--kernels", type=int, nargs="+", default=[1, 0])
+    ap.add_argument("--kernels", type=lambda x: int(x, 0), nargs="+", default=[1, 0])
     ap.add_argument("--scenes", type=int, nargs="+", default=[1, 8])
     ap.add_argument("--rounds", type=int, default=10)
     ap.add_argument("--reps", type=int, default=5)
