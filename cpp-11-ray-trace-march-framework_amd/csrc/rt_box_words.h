@@ -13,7 +13,8 @@ namespace rtbox {
 //   non-empty cell: 0x80000000 | start << 11 | count        (start < 2^20, count < 2^11)
 //   empty cell:     (E0 - 1) | (E1 - 1) << 11 | (E2 - 1) << 22
 // where E0 x E1 x E2 cells (x, y, z) is an empty box with its corner at the cell, extending along
-// the octant's signs (cells outside the grid count as empty).  A walk in octant o starting in the
+// the octant's signs (cells outside the grid count as empty while the shape is chosen; the
+// stored box is clipped to the grid).  A walk in octant o starting in the
 // cell stays in that box while it has taken fewer than E_a steps along every axis a, whatever its
 // direction inside the octant -- so the counts are decremented with the packed remaining-cell
 // counts' own axis unit, and the walk needs the next cell word only when one borrows (DESIGN.md
@@ -105,7 +106,15 @@ inline void build_box_words(const uint32_t *off, const uint32_t dims[3], std::ve
                         E[m] = bl;
                         E[a] = be;
                         E[b] = be;
-                        for (int k = 0; k < 3; k++) E[k] = std::min(E[k] - 1u, field_max[k]);
+                        // clipped to the grid: a field never exceeds the walk's remaining-cell
+                        // count along its axis (the cells left before the grid's far face), so a
+                        // box run's borrow also catches the walk leaving the grid
+                        const int pos[3] = { x, y, z };
+                        for (int k = 0; k < 3; k++)
+                        {
+                            const uint32_t rem = uint32_t(sg[k] > 0 ? dimv[k] - 1 - pos[k] : pos[k]);
+                            E[k] = std::min(std::min(E[k] - 1u, field_max[k]), rem);
+                        }
                         w[c] = E[0] | (E[1] << 11) | (E[2] << 22);
                     }
         }

@@ -224,6 +224,12 @@ __device__ __forceinline__ float quad_bcast(float v)
     constexpr int ctrl = J | (J << 2) | (J << 4) | (J << 6);
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), ctrl, 0xF, 0xF, false));
 }
+template <int J>
+__device__ __forceinline__ uint32_t quad_bcast_u(uint32_t v)
+{
+    constexpr int ctrl = J | (J << 2) | (J << 4) | (J << 6);
+    return uint32_t(__builtin_amdgcn_update_dpp(0, int(v), ctrl, 0xF, 0xF, false));
+}
 
 __device__ __forceinline__ bool first_active_lane()
 {
@@ -776,19 +782,17 @@ constexpr int kRemGuards = int((1u << 10) | (1u << 21) | (1u << 31));
         nct2 += a2_ ? dt2 : 0.0f;                                                              \
         cell += a2_ ? cs2 : (a1_ ? cs1 : cs0);                                                 \
     } while (0)
+// A step inside a box run: only the crossing times and the box counts move; the run's end
+// rebuilds the cell index and the remaining-cell counts from the box counts' difference.
 #define RT_DDA_BOX_BARE_STEP()                                                                 \
     do {                                                                                       \
         const float m_ = __builtin_fminf(__builtin_fminf(nct0, nct1), nct2);                   \
         const bool a2_ = nct2 == m_;                                                           \
-        const bool a1_ = !a2_ && nct1 == m_;                                                   \
-        const bool a0_ = !a2_ && !a1_;                                                         \
-        const int u_ = a2_ ? (1 << 22) : (a1_ ? (1 << 11) : 1);                                \
-        remp -= u_;                                                                            \
-        boxw -= u_;                                                                            \
-        nct0 += a0_ ? dt0 : 0.0f;                                                              \
-        nct1 += a1_ ? dt1 : 0.0f;                                                              \
+        const bool e1_ = nct1 == m_;                                                           \
+        boxw -= a2_ ? (1 << 22) : (e1_ ? (1 << 11) : 1);                                       \
+        nct0 += (a2_ | e1_) ? 0.0f : dt0;                                                      \
+        nct1 += (e1_ & !a2_) ? dt1 : 0.0f;                                                     \
         nct2 += a2_ ? dt2 : 0.0f;                                                              \
-        cell += a2_ ? cs2 : (a1_ ? cs1 : cs0);                                                 \
     } while (0)
 constexpr int kBoxUnits3 = 3 | (3 << 11) | (3 << 22);   // 3 in every box-count field
 
@@ -924,29 +928,34 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, float ox, float
                 }
             if constexpr (!STATS)
             {
-                // Wave-uniform runs while every active lane is inside its box and the grid: blocks
-                // of 4 bare steps while every box count of every lane is >= 3 (the first three
-                // steps of a block stay inside; the fourth may leave, which the next vote sees),
-                // then single steps.  A lane leaving the grid inside a block keeps stepping to the
-                // block's end harmlessly (its state is dead; the guard borrow of its remaining-
-                // cell count is sticky for far more steps than a block holds).  A lane that hit
-                // holds boxw < 0 (guard set), so runs only start when no lane hit.
-                // (if + do-while: a while loop's exit edge made the compiler copy the whole walk
-                // state every iteration)
-                if (wave_all(((uint32_t(boxw) | uint32_t(remp)) & uint32_t(kRemGuards)) == 0u))
+                // Wave-uniform runs while every active lane is inside its box (the boxes are clipped
+                // to the grid, so inside the box is inside the grid): blocks of 4 bare steps while
+                // every box count of every lane is >= 3 (the first three steps of a block stay
+                // inside; the fourth may leave, which the next vote sees), then single steps.  A
+                // bare step moves only the crossing times and boxw; the run's end rebuilds the
+                // cell index and the remaining-cell counts from the box counts' difference, which
+                // is sum n_a * unit_a over the run's n_a steps along axis a (n_a <= 1024, 1024,
+                // 512: no field of the difference carries).  A lane that hit holds boxw < 0
+                // (guard set), so runs only start when no lane hit.  (if + do-while: a while
+                // loop's exit edge made the compiler copy the whole walk state every iteration.)
+                if (wave_all((uint32_t(boxw) & uint32_t(kRemGuards)) == 0u))
                 {
-                    if (wave_all(((uint32_t(boxw - kBoxUnits3) | uint32_t(remp)) & uint32_t(kRemGuards)) == 0u))
+                    const uint32_t b0 = uint32_t(boxw);
+                    if (wave_all((uint32_t(boxw - kBoxUnits3) & uint32_t(kRemGuards)) == 0u))
                         do
                         {
                             RT_DDA_BOX_BARE_STEP();
                             RT_DDA_BOX_BARE_STEP();
                             RT_DDA_BOX_BARE_STEP();
                             RT_DDA_BOX_BARE_STEP();
-                        } while (wave_all(((uint32_t(boxw - kBoxUnits3) | uint32_t(remp)) & uint32_t(kRemGuards)) == 0u));
-                    if (wave_all(((uint32_t(boxw) | uint32_t(remp)) & uint32_t(kRemGuards)) == 0u))
+                        } while (wave_all((uint32_t(boxw - kBoxUnits3) & uint32_t(kRemGuards)) == 0u));
+                    if (wave_all((uint32_t(boxw) & uint32_t(kRemGuards)) == 0u))
                         do
                             RT_DDA_BOX_BARE_STEP();
-                        while (wave_all(((uint32_t(boxw) | uint32_t(remp)) & uint32_t(kRemGuards)) == 0u));
+                        while (wave_all((uint32_t(boxw) & uint32_t(kRemGuards)) == 0u));
+                    const uint32_t d = b0 - uint32_t(boxw);
+                    remp -= int(d);
+                    cell += int(d & 2047u) * cs0 + int((d >> 11) & 2047u) * cs1 + int(d >> 22) * cs2;
                     more = (remp & kRemGuards) == 0;
                 }
             }
@@ -1391,10 +1400,24 @@ __device__ __forceinline__ void process_item(const KParams& P, uint32_t item, ui
     if (Q.spp == 4u)
     {
         // the bench's 4 spp: a pixel's samples are one quad of lanes, so each sample's colour is
-        // a quad broadcast (DPP, one VALU) instead of an LDS permute; same values, same order
-        sr = sr + quad_bcast<0>(cr) + quad_bcast<1>(cr) + quad_bcast<2>(cr) + quad_bcast<3>(cr);
-        sg = sg + quad_bcast<0>(cg) + quad_bcast<1>(cg) + quad_bcast<2>(cg) + quad_bcast<3>(cg);
-        sb = sb + quad_bcast<0>(cb) + quad_bcast<1>(cb) + quad_bcast<2>(cb) + quad_bcast<3>(cb);
+        // a quad broadcast (DPP, one VALU) instead of an LDS permute; same values, same order.
+        // renderer.cpp:87-122 starts the sum at 0.0f; 0.0f + x == x for every colour (>= +0:
+        // (n + 1) * 0.5 of a normalised component, py / H, t / 3 -- never -0), so the sum
+        // starts at the first sample
+        sr = quad_bcast<0>(cr) + quad_bcast<1>(cr) + quad_bcast<2>(cr) + quad_bcast<3>(cr);
+        sg = quad_bcast<0>(cg) + quad_bcast<1>(cg) + quad_bcast<2>(cg) + quad_bcast<3>(cg);
+        sb = quad_bcast<0>(cb) + quad_bcast<1>(cb) + quad_bcast<2>(cb) + quad_bcast<3>(cb);
+        // ... and the quad's lanes 0, 1, 2 resolve one channel each (b, g, r: the byte at their
+        // position in pack_bgra8's word; lane 3 contributes the zero alpha byte), so the correctly
+        // rounded square root and the packing run once per wave instead of three times; the
+        // bytes meet in the pixel's lane by quad broadcasts (same per-channel arithmetic)
+        const uint32_t j = lane & 3u;
+        const float c = j == 0u ? sb : (j == 1u ? sg : sr);
+        uint32_t v = rtd::pack_channel(rtd::gamma_half(c * 0.25f)) << (8u * j);   // renderer.cpp:124, exact
+        v = j == 3u ? 0u : v;
+        const uint32_t word = quad_bcast_u<0>(v) | quad_bcast_u<1>(v) | quad_bcast_u<2>(v);
+        if (ic.valid && ic.s == 0) store_pixel(Q, ic.c, ic.p, ic.x, ic.y, word);
+        return;
     }
     else
     {

@@ -4,10 +4,11 @@
 // x major axis) and every cell:
 //   * a non-empty cell's word is 0x80000000 | start << 11 | count of its CSR range;
 //   * an empty cell's word has bit 31 and the guard bits 10 / 21 clear, and its box -- E0 x E1 x E2
-//     cells with the corner at the cell, extending along the octant's signs, clipped to the grid --
-//     holds no non-empty cell (3-D prefix sums of the occupancy).
-// Prints "cells <checked> boxcells <sum of box volumes> loads_bound <mean box volume>" and exits 1
-// on the first violation.
+//     cells with the corner at the cell, extending along the octant's signs -- lies inside the grid
+//     (the kernel's box runs rely on it to see the grid exit) and holds no non-empty cell (3-D
+//     prefix sums of the occupancy).
+// Prints "cells <checked> empty <empty cells> mean_box_volume <cells>" and exits 1 on the first
+// violation.
 //   g++ -O2 -std=c++11 -pthread -I oracle tests/box_words_check.cpp -o box_words_check
 //   ./box_words_check data/scenes/scene8.rtscene
 #include "../oracle/cpu_tracer.cpp"
@@ -79,6 +80,12 @@ int main(int argc, char **argv)
                         for (int a = 0; a < 3; a++)
                         {
                             const int far = p[a] + sg[a] * (E[a] - 1);
+                            if (far < 0 || far >= D[a])
+                            {
+                                std::fprintf(stderr, "copy %u cell (%d,%d,%d): box leaves the grid along axis %d\n",
+                                             o * 3 + m, x, y, z, a);
+                                return 1;
+                            }
                             lo[a] = std::max(0, std::min(p[a], far));
                             hi[a] = std::min(D[a], std::max(p[a], far) + 1);
                         }

@@ -150,6 +150,7 @@ int main(int argc, char **argv)
     const uint32_t nth = std::max(1u, std::thread::hardware_concurrency());
     std::atomic<uint32_t> next(0);
     std::atomic<uint64_t> outer(0), inner(0), loads(0), waves(0), steps(0);
+    std::atomic<uint64_t> uni_recs(0), lane_iters(0), lane_useful(0), test_iters(0), chain_axis(0), chain_tot(0);
     std::vector<std::thread> pool;
     for (uint32_t th = 0; th < nth; th++)
         pool.emplace_back([&]() {
@@ -175,6 +176,57 @@ int main(int argc, char **argv)
                     s_ += lanes[l].cell.size();
                 }
                 w_++;
+                // test-step uniformity: per outer iteration, the lanes looking up a non-empty cell
+                auto tally = [&](const std::vector<std::pair<uint32_t, uint32_t>>& tl, uint64_t& ur, uint64_t& li,
+                                 uint64_t& lu, uint64_t& ti) {
+                    if (tl.empty()) return;
+                    ti++;
+                    bool uni = true; uint32_t mx = 0, sum = 0;
+                    for (auto& p : tl) { if (p.first != tl[0].first) uni = false; mx = std::max(mx, p.second); sum += p.second; }
+                    if (uni) ur += mx; else { li += mx; lu += sum; }
+                };
+                uint64_t ur_ = 0, li_ = 0, lu_ = 0, ti_ = 0;
+                if (policy == 4)
+                {
+                    // per-lane runs: each outer iteration every active lane looks its cell up
+                    // (testing it when non-empty) and, when empty, jumps to its box's exit cell
+                    std::vector<uint32_t> pos(64, 0);
+                    for (;;)
+                    {
+                        std::vector<std::pair<uint32_t, uint32_t>> tl;
+                        uint32_t act = 0, mx_ax[3] = {0, 0, 0}, mx_tot = 0;
+                        for (uint32_t l = 0; l < 64; l++)
+                        {
+                            const Walk& wk = lanes[l];
+                            if (pos[l] >= wk.cell.size()) continue;
+                            act++;
+                            l_++;
+                            const uint32_t j = pos[l], c = wk.cell[j];
+                            if (wk.len[j]) { tl.push_back({c, wk.len[j]}); pos[l] = j + 1; continue; }
+                            const uint32_t w = boxw[size_t(wk.oct * 3u + wk.maj) * ncells + c];
+                            int bcnt[3] = { int(w & 1023u), int((w >> 11) & 1023u), int((w >> 22) & 511u) };
+                            uint32_t k = j, nax[3] = {0, 0, 0};
+                            while (k + 1 < wk.cell.size())
+                            {
+                                const int ax = axis_of(s, wk.cell[k], wk.cell[k + 1]);
+                                k++;
+                                nax[ax]++;
+                                if (--bcnt[ax] < 0) break;
+                            }
+                            for (int q = 0; q < 3; q++) mx_ax[q] = std::max(mx_ax[q], nax[q]);
+                            mx_tot = std::max(mx_tot, nax[0] + nax[1] + nax[2]);
+                            if (k + 1 >= wk.cell.size() && bcnt[0] >= 0 && bcnt[1] >= 0 && bcnt[2] >= 0) k = uint32_t(wk.cell.size());
+                            pos[l] = k;
+                        }
+                        if (!act) break;
+                        o_++;
+                        tally(tl, ur_, li_, lu_, ti_);
+                        chain_axis += mx_ax[0] + mx_ax[1] + mx_ax[2];
+                        chain_tot += mx_tot;
+                    }
+                    uni_recs += ur_; lane_iters += li_; lane_useful += lu_; test_iters += ti_;
+                    continue;
+                }
                 // known[l] > 0: the lane's current cell is proven empty (no lookup); bc: box counts
                 int known[64] = {}, bc[64][3] = {};
                 auto advance = [&](uint32_t l, uint32_t j) {      // the step from cell j to j + 1
@@ -186,10 +238,12 @@ int main(int argc, char **argv)
                 while (j < maxlen)
                 {
                     uint32_t act = 0;
+                    std::vector<std::pair<uint32_t, uint32_t>> tl;
                     for (uint32_t l = 0; l < 64; l++)
                     {
                         if (j >= lanes[l].cell.size()) continue;
                         act++;
+                        if (known[l] == 0 && lanes[l].len[j]) tl.push_back({lanes[l].cell[j], lanes[l].len[j]});
                         if (known[l] == 0)
                         {
                             l_++;
@@ -215,6 +269,7 @@ int main(int argc, char **argv)
                     }
                     if (!act) break;
                     o_++;
+                    tally(tl, ur_, li_, lu_, ti_);
                     j++;
                     for (;;)        // wave-uniform bare steps while every active lane's cell is known empty
                     {
@@ -228,11 +283,16 @@ int main(int argc, char **argv)
                         j++;
                     }
                 }
+                uni_recs += ur_; lane_iters += li_; lane_useful += lu_; test_iters += ti_;
             }
             outer += o_; inner += i_; loads += l_; waves += w_; steps += s_;
         });
+    // (policy 2's tallies are added per item below)
     for (auto& t : pool) t.join();
     std::printf("{\"policy\": %d, \"outer_per_wave\": %.2f, \"inner_per_wave\": %.2f, \"loads_per_lane\": %.2f, "
-                "\"steps_per_lane\": %.2f}\n", policy, double(outer) / waves, double(inner) / waves,
-                double(loads) / (64.0 * waves), double(steps) / (64.0 * waves));
+                "\"steps_per_lane\": %.2f, \"uniform_records_per_wave\": %.2f, \"lane_iterations_per_wave\": %.2f, "
+                "\"lane_util\": %.3f, \"test_iterations_per_wave\": %.2f, \"chain_axis_max_per_wave\": %.2f, \"chain_total_max_per_wave\": %.2f}\n", policy, double(outer) / waves,
+                double(inner) / waves, double(loads) / (64.0 * waves), double(steps) / (64.0 * waves),
+                double(uni_recs) / waves, double(lane_iters) / waves, double(lane_useful) / (64.0 * std::max<uint64_t>(1, lane_iters)),
+                double(test_iters) / waves, double(chain_axis) / waves, double(chain_tot) / waves);
 }
