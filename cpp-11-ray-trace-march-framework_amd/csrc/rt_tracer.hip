@@ -758,6 +758,10 @@ constexpr int kRemGuards = int((1u << 10) | (1u << 21) | (1u << 31));
 #ifndef RT_SKIP_BLOCKS
 #define RT_SKIP_BLOCKS 1
 #endif
+// spp 4: the pixel's quad resolves one channel per lane (1) or its first lane all three (0)
+#ifndef RT_QUAD_RESOLVE
+#define RT_QUAD_RESOLVE 1
+#endif
 // AUTO's empty runs over the box-run words (1, build_box_words) or the octant cube words (0)
 #ifndef RT_BOX_RUN
 #define RT_BOX_RUN 1
@@ -1411,6 +1415,7 @@ __device__ __forceinline__ void process_item(const KParams& P, uint32_t item, ui
         // position in pack_bgra8's word; lane 3 contributes the zero alpha byte), so the correctly
         // rounded square root and the packing run once per wave instead of three times; the
         // bytes meet in the pixel's lane by quad broadcasts (same per-channel arithmetic)
+#if RT_QUAD_RESOLVE
         const uint32_t j = lane & 3u;
         const float c = j == 0u ? sb : (j == 1u ? sg : sr);
         uint32_t v = rtd::pack_channel(rtd::gamma_half(c * 0.25f)) << (8u * j);   // renderer.cpp:124, exact
@@ -1418,6 +1423,7 @@ __device__ __forceinline__ void process_item(const KParams& P, uint32_t item, ui
         const uint32_t word = quad_bcast_u<0>(v) | quad_bcast_u<1>(v) | quad_bcast_u<2>(v);
         if (ic.valid && ic.s == 0) store_pixel(Q, ic.c, ic.p, ic.x, ic.y, word);
         return;
+#endif
     }
     else
     {
