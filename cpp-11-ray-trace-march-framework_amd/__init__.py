@@ -127,7 +127,7 @@ class SceneInfo(ctypes.Structure):
                 ("max_cell_refs", c_u32), ("hf_floor", c_u32), ("hf_min_blocks", c_u32), ("wh_floor", c_u32),
                 ("wh_alpha16", c_u32), ("wh_auto_refs", c_u32), ("wh_fused", c_u32), ("hf_contexts", c_u32),
                 ("hf_evictions", ctypes.c_uint64), ("device_bytes", ctypes.c_uint64),
-                ("box_words", c_u32), ("reserved", c_u32)]
+                ("box_words", c_u32), ("wh_alpha16_n2", c_u32)]
 
 
 SAMPLE_REC_DTYPE = np.dtype([("hit", "<u4"), ("tri", "<u4"), ("voxel", "<u4"), ("steps", "<u4"),

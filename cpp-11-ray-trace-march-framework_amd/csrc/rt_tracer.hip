@@ -2463,6 +2463,8 @@ struct rt_scene
     uint32_t hf_min_blocks = 4096;  // RT_HF_MIN_BLOCKS: smallest whole launch taking the heavy-first order
     uint32_t wh_floor = 100000;     // RT_WH_FLOOR: wide-section threshold floor, shader cycles
     uint32_t wh_alpha16 = 32;       // RT_WH_ALPHA16: wide threshold, sixteenths of the estimated span
+    uint32_t wh_alpha16_n2 = 16;    // RT_WH_ALPHA16_N2: the same for a rank of 2 of a batched step
+                                    // (measured, profiles/r03o_alpha_n2_sweep.json)
     uint32_t wh_auto_refs = 128;    // RT_WH_AUTO_REFS: AUTO takes the wide section for >= 2-rank
                                     // shards of scenes with a cell list this long
     uint32_t wh_fused = 1;          // RT_WH_FUSED: a batch's wide section leads the batch kernel's grid
@@ -2807,7 +2809,10 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
         P.wh_refresh = (c->frames - 1u) % kWhRefresh == 0u;       // frames counts this one
         P.wh_wgs = P.wh_refresh ? 0u : (units + kWavesPerWG - 1u) / kWavesPerWG;
         P.wh_floor = s->wh_floor;
-        P.wh_alpha16 = s->wh_alpha16;
+        // a rank of 2 of a batched step lists more (its span estimate includes the other frames'
+        // work); one scene's own rank-of-2 launch measured 25 % slower with it
+        // (profiles/r03o_shard_scaling_bench.json), so it keeps the default
+        P.wh_alpha16 = (P.nranks == 2u && batch != 0u) ? s->wh_alpha16_n2 : s->wh_alpha16;
         P.wh_mark_in = c->wh_marks + size_t(v & 1u) * kWavesPerWG * c->cap_blocks;
         P.wh_mark_out = c->wh_marks + size_t((v + 1u) & 1u) * kWavesPerWG * c->cap_blocks;
         P.wh_list_in = c->wh_lists + size_t(v & 1u) * kWhMax;
@@ -3243,6 +3248,7 @@ int rt_scene_info_get(rt_scene *s, rt_scene_info *out)
     out->hf_min_blocks = s->hf_min_blocks;
     out->wh_floor = s->wh_floor;
     out->wh_alpha16 = s->wh_alpha16;
+    out->wh_alpha16_n2 = s->wh_alpha16_n2;
     out->wh_auto_refs = s->wh_auto_refs;
     out->wh_fused = s->wh_fused;
     out->hf_contexts = kHfCtxs;
@@ -3301,6 +3307,7 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
     s->hf_min_blocks = env_tunable("RT_HF_MIN_BLOCKS", s->hf_min_blocks);
     s->wh_floor = env_tunable("RT_WH_FLOOR", s->wh_floor);
     s->wh_alpha16 = env_tunable("RT_WH_ALPHA16", s->wh_alpha16);
+    s->wh_alpha16_n2 = env_tunable("RT_WH_ALPHA16_N2", s->wh_alpha16_n2);
     s->wh_auto_refs = env_tunable("RT_WH_AUTO_REFS", s->wh_auto_refs);
     s->wh_fused = env_tunable("RT_WH_FUSED", s->wh_fused);
     for (int a = 0; a < 3; a++)

@@ -300,8 +300,8 @@ int rt_debug_heavy_first(rt_scene *s, uint32_t *front, uint32_t *listed, uint32_
 int rt_debug_wide_items(rt_scene *s, uint32_t *count);
 
 /* What rt_scene_create chose for a scene, and the scheduling tunables it read once from the
-   environment (RT_HF_FLOOR, RT_HF_MIN_BLOCKS, RT_WH_FLOOR, RT_WH_ALPHA16, RT_WH_AUTO_REFS,
-   RT_WH_FUSED, RT_OCT_DIST): never re-read per launch. */
+   environment (RT_HF_FLOOR, RT_HF_MIN_BLOCKS, RT_WH_FLOOR, RT_WH_ALPHA16, RT_WH_ALPHA16_N2,
+   RT_WH_AUTO_REFS, RT_WH_FUSED, RT_OCT_DIST): never re-read per launch. */
 typedef struct rt_scene_info {
     uint32_t octant_words;      /* 1: 8 ray-octant copies of the cell words (AUTO's empty runs);
                                    0: one L-inf word per cell (RT_OCT_DIST=0, or above the size cap) */
@@ -317,7 +317,7 @@ typedef struct rt_scene_info {
     uint32_t box_words;         /* 1: AUTO's empty runs use the 24 box-run word copies (octant x major
                                    axis); 0: none (references >= 2^20 or above the size cap: AUTO then
                                    walks without the packed counts and empty runs) */
-    uint32_t reserved;
+    uint32_t wh_alpha16_n2;     /* RT_WH_ALPHA16_N2: the wide threshold at a rank of 2 of a batched step */
 } rt_scene_info;
 int  rt_scene_info_get(rt_scene *scene, rt_scene_info *out);
 

@@ -319,6 +319,7 @@ def test_scene_tunables_read_once(monkeypatch):
         assert ia["octant_words"] == 1 and ib["octant_words"] == 0
         assert ia["max_cell_refs"] >= 128 and ia["rcp_safe"] == 1 and ia["pack_ok"] == 1
         assert ia["hf_contexts"] >= 8
+        assert ia["box_words"] == 1 and ib["box_words"] == 1 and ia["wh_alpha16_n2"] == 16
         img = a.render_frame(a.frame(64, 48, 4))
         monkeypatch.setenv("RT_WH_FLOOR", "5")
         assert a.info()["wh_floor"] == 100000
