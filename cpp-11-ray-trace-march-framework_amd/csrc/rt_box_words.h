@@ -36,9 +36,13 @@ constexpr uint32_t kBoxRatio = RT_BOX_RATIO;
 constexpr uint32_t kBoxSquareCap = 64;      // cross-section sides searched
 constexpr uint32_t kBoxLenCap = 128;        // box length along m searched
 constexpr bool kBoxExtend = RT_BOX_EXTEND != 0;   // the chosen cross-section's box runs on along m while it stays empty
+#ifndef RT_BOX_GROW
+#define RT_BOX_GROW 1
+#endif
+constexpr bool kBoxGrow = RT_BOX_GROW != 0;       // then grows each cross side (and m again) while the box stays empty
 
 inline void build_box_words(const uint32_t *off, const uint32_t dims[3], std::vector<uint32_t>& out,
-                            uint32_t ratio = kBoxRatio, bool extend = kBoxExtend)
+                            uint32_t ratio = kBoxRatio, bool extend = kBoxExtend, bool grow = kBoxGrow)
 {
     const int dimv[3] = { int(dims[0]), int(dims[1]), int(dims[2]) };
     const uint32_t nc = dims[0] * dims[1] * dims[2];
@@ -47,6 +51,30 @@ inline void build_box_words(const uint32_t *off, const uint32_t dims[3], std::ve
         return uint32_t(x) + uint32_t(z) * dims[0] + uint32_t(y) * dims[0] * dims[2];
     };
     out.assign(size_t(24) * nc, 0u);
+    // occupancy prefix sums over [0, x) x [0, y) x [0, z) (grow: O(1) box-emptiness queries)
+    const size_t px = size_t(dimv[0]) + 1, py = size_t(dimv[1]) + 1, pz = size_t(dimv[2]) + 1;
+    std::vector<uint32_t> PS;
+    auto pidx = [&](int x, int y, int z) { return (size_t(x) * py + size_t(y)) * pz + size_t(z); };
+    if (grow)
+    {
+        PS.assign(px * py * pz, 0u);
+        for (int x = 1; x <= dimv[0]; x++)
+            for (int y = 1; y <= dimv[1]; y++)
+                for (int z = 1; z <= dimv[2]; z++)
+                {
+                    const uint32_t c = idx(x - 1, y - 1, z - 1);
+                    PS[pidx(x, y, z)] = (off[c + 1] != off[c] ? 1u : 0u) + PS[pidx(x - 1, y, z)] + PS[pidx(x, y - 1, z)] +
+                                        PS[pidx(x, y, z - 1)] - PS[pidx(x - 1, y - 1, z)] - PS[pidx(x - 1, y, z - 1)] -
+                                        PS[pidx(x, y - 1, z - 1)] + PS[pidx(x - 1, y - 1, z - 1)];
+                }
+    }
+    // no non-empty cell in the cells [lo, hi) (clipped to the grid by the caller)
+    auto empty_box = [&](const int lo[3], const int hi[3]) {
+        const int64_t v = int64_t(PS[pidx(hi[0], hi[1], hi[2])]) - PS[pidx(lo[0], hi[1], hi[2])] - PS[pidx(hi[0], lo[1], hi[2])] -
+                          PS[pidx(hi[0], hi[1], lo[2])] + PS[pidx(lo[0], lo[1], hi[2])] + PS[pidx(lo[0], hi[1], lo[2])] +
+                          PS[pidx(hi[0], lo[1], lo[2])] - PS[pidx(lo[0], lo[1], lo[2])];
+        return v == 0;
+    };
     // one copy (octant o, major axis m) per task; the copies are independent
     auto copy = [&](uint32_t o, int m, std::vector<uint16_t>& S) {
         const int sg[3] = { (o & 1) ? -1 : 1, (o & 2) ? -1 : 1, (o & 4) ? -1 : 1 };
@@ -114,6 +142,31 @@ inline void build_box_words(const uint32_t *off, const uint32_t dims[3], std::ve
                         {
                             const uint32_t rem = uint32_t(sg[k] > 0 ? dimv[k] - 1 - pos[k] : pos[k]);
                             E[k] = std::min(std::min(E[k] - 1u, field_max[k]), rem);
+                        }
+                        if (grow)
+                        {
+                            // E[k] now counts cells beyond the corner; grow one side at a time by one
+                            // cell while the box stays empty and inside the grid and the field
+                            auto fits = [&](const uint32_t *e) {
+                                int lo[3], hi[3];
+                                for (int k = 0; k < 3; k++)
+                                {
+                                    const int far = pos[k] + sg[k] * int(e[k]);
+                                    lo[k] = std::min(pos[k], far);
+                                    hi[k] = std::max(pos[k], far) + 1;
+                                    if (lo[k] < 0 || hi[k] > dimv[k]) return false;
+                                }
+                                return empty_box(lo, hi);
+                            };
+                            const int order[3] = { a, b, m };
+                            for (int k : order)
+                                while (E[k] < field_max[k] && E[k] < (k == m ? kBoxLenCap : kBoxSquareCap))
+                                {
+                                    uint32_t e2[3] = { E[0], E[1], E[2] };
+                                    e2[k]++;
+                                    if (!fits(e2)) break;
+                                    E[k]++;
+                                }
                         }
                         w[c] = E[0] | (E[1] << 11) | (E[2] << 22);
                     }

@@ -137,7 +137,7 @@ int main(int argc, char **argv)
     const std::vector<uint32_t> octD = octant_dist(s);
     std::vector<uint32_t> boxw;
     rtbox::build_box_words(s.off.data(), s.dim, boxw, argc > 6 ? uint32_t(std::atoi(argv[6])) : rtbox::kBoxRatio,
-                           argc > 8 ? std::atoi(argv[8]) != 0 : rtbox::kBoxExtend);
+                           argc > 8 ? std::atoi(argv[8]) != 0 : rtbox::kBoxExtend, argc > 9 ? std::atoi(argv[9]) != 0 : rtbox::kBoxGrow);
     const uint32_t ncells = s.dim[0] * s.dim[1] * s.dim[2];
     const uint32_t W = std::atoi(argv[2]), H = std::atoi(argv[3]), spp = std::atoi(argv[4]);
     const int policy = std::atoi(argv[5]);
