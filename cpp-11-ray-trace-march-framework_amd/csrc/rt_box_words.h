@@ -2,7 +2,10 @@
 // by rt_tracer.hip (rt_scene_create) and by the CPU checks (tests/test_box_words.py, tools/box_sim.cpp).
 #pragma once
 #include <algorithm>
+#include <atomic>
 #include <cstdint>
+#include <new>
+#include <stdexcept>
 #include <thread>
 #include <vector>
 
@@ -41,7 +44,8 @@ constexpr bool kBoxExtend = RT_BOX_EXTEND != 0;   // the chosen cross-section's 
 #endif
 constexpr bool kBoxGrow = RT_BOX_GROW != 0;       // then grows each cross side (and m again) while the box stays empty
 
-inline void build_box_words(const uint32_t *off, const uint32_t dims[3], std::vector<uint32_t>& out,
+// Returns false (out emptied) when a host allocation fails.
+inline bool build_box_words(const uint32_t *off, const uint32_t dims[3], std::vector<uint32_t>& out,
                             uint32_t ratio = kBoxRatio, bool extend = kBoxExtend, bool grow = kBoxGrow)
 {
     const int dimv[3] = { int(dims[0]), int(dims[1]), int(dims[2]) };
@@ -50,14 +54,30 @@ inline void build_box_words(const uint32_t *off, const uint32_t dims[3], std::ve
     auto idx = [&](int x, int y, int z) {                      // grid.h:41-42 GridIdx
         return uint32_t(x) + uint32_t(z) * dims[0] + uint32_t(y) * dims[0] * dims[2];
     };
-    out.assign(size_t(24) * nc, 0u);
+    try
+    {
+        out.assign(size_t(24) * nc, 0u);
+    }
+    catch (const std::bad_alloc&)
+    {
+        out.clear();
+        return false;
+    }
     // occupancy prefix sums over [0, x) x [0, y) x [0, z) (grow: O(1) box-emptiness queries)
     const size_t px = size_t(dimv[0]) + 1, py = size_t(dimv[1]) + 1, pz = size_t(dimv[2]) + 1;
     std::vector<uint32_t> PS;
     auto pidx = [&](int x, int y, int z) { return (size_t(x) * py + size_t(y)) * pz + size_t(z); };
     if (grow)
     {
-        PS.assign(px * py * pz, 0u);
+        try
+        {
+            PS.assign(px * py * pz, 0u);
+        }
+        catch (const std::bad_alloc&)
+        {
+            out.clear();
+            return false;
+        }
         for (int x = 1; x <= dimv[0]; x++)
             for (int y = 1; y <= dimv[1]; y++)
                 for (int z = 1; z <= dimv[2]; z++)
@@ -174,12 +194,34 @@ inline void build_box_words(const uint32_t *off, const uint32_t dims[3], std::ve
     };
     const uint32_t nth = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
     std::vector<std::thread> pool;
-    for (uint32_t t = 0; t < nth; t++)
-        pool.emplace_back([&, t]() {
+    std::atomic<bool> failed(false);
+    auto task = [&](uint32_t t) {
+        try
+        {
             std::vector<uint16_t> S(nc);
             for (uint32_t k = t; k < 24u; k += nth) copy(k / 3u, int(k % 3u), S);
-        });
+        }
+        catch (const std::bad_alloc&)
+        {
+            failed = true;
+        }
+    };
+    try
+    {
+        for (uint32_t t = 1; t < nth; t++) pool.emplace_back(task, t);
+    }
+    catch (const std::exception&)       // no threads: the remaining tasks run here
+    {
+    }
+    for (uint32_t t = uint32_t(pool.size()) + 1u; t < nth; t++) task(t);
+    task(0);
     for (std::thread& th : pool) th.join();
+    if (failed)
+    {
+        out.clear();
+        return false;
+    }
+    return true;
 }
 
 }  // namespace rtbox

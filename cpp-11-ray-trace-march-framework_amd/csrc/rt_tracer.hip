@@ -958,7 +958,7 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, float ox, float
                             RT_DDA_BOX_BARE_STEP();
                         while (wave_all((uint32_t(boxw) & uint32_t(kRemGuards)) == 0u));
                     const uint32_t d = b0 - uint32_t(boxw);
-                    remp -= int(d);
+                    remp = int(uint32_t(remp) - d);           // wrapping (d may reach 2^31)
                     cell += int(d & 2047u) * cs0 + int((d >> 11) & 2047u) * cs1 + int(d >> 22) * cs2;
                     more = (remp & kRemGuards) == 0;
                 }
@@ -3446,8 +3446,8 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
         // AUTO's box-run words (build_box_words): the non-empty words keep start < 2^20
         if (RT_BOX_RUN && nr < (1u << 20) && uint64_t(nc) * 24u * 4u <= kBoxWordsMaxBytes)
         {
-            rtbox::build_box_words(g.cell_offsets, g.dims, cellwb);
-            s->box_words = true;
+            s->box_words = rtbox::build_box_words(g.cell_offsets, g.dims, cellwb);
+            if (!s->box_words) cellwb.clear();          // out of host memory: AUTO walks without them
         }
     }
     for (uint32_t c = 0; c < nc; c++)

@@ -25,7 +25,7 @@ int main(int argc, char **argv)
     const int D[3] = { int(s.dim[0]), int(s.dim[1]), int(s.dim[2]) };
     const uint32_t nc = s.dim[0] * s.dim[1] * s.dim[2];
     std::vector<uint32_t> w;
-    rtbox::build_box_words(s.off.data(), s.dim, w);
+    if (!rtbox::build_box_words(s.off.data(), s.dim, w)) { std::fprintf(stderr, "build failed\n"); return 1; }
     if (w.size() != size_t(24) * nc) { std::fprintf(stderr, "size %zu\n", w.size()); return 1; }
     // occupancy prefix sums P[x][y][z] over [0, x) x [0, y) x [0, z)
     auto pidx = [&](int x, int y, int z) { return (size_t(x) * (D[1] + 1) + y) * (D[2] + 1) + z; };
