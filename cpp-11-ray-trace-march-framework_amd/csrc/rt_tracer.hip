@@ -137,7 +137,8 @@ struct KParams
     uint32_t rank, nranks;      // local tile k = row-rotated tile rank + k * nranks (shard_tile_xy)
     uint32_t wg_per_tile;
     uint32_t xcd_chunk;         // kVarXcdBands: consecutive blocks per XCD turn (0 = one band each)
-    uint64_t *wave_clk;         // kVarWaveClock: {start, end, uniform tests, lane-loop iterations} per item
+    uint32_t vblocks;           // k_render_lanes_w64: the 256-lane launch blocks its one-wave grid runs
+    uint64_t *wave_clk;        // kVarWaveClock: {start, end, uniform tests, lane-loop iterations} per item
     const uint32_t *tile_order; // tile order (position -> local tile) or null = natural order
     // heavy-first block order (AUTO; hf_front == 0: off).  Blocks [0, hf_front) render the blocks
     // the current plan (version hf_ver) lists as heavy, most expensive level first; blocks from
@@ -1614,14 +1615,16 @@ __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks)
 // rest walk the natural (XCD-banded) order, skipping the listed blocks.  Returns false when this
 // block has nothing to do.  The marks read here are never written by this launch (the next
 // frame's marks live in the other buffer), so every wave of a block decides alike.
+// lead: the first lane of launch block 0's first wave (the one that clears the next plan).
 template <int VAR>
-__device__ __forceinline__ bool block_of_launch(const KParams& P, uint32_t& b, uint32_t bid, uint32_t nblk)
+__device__ __forceinline__ bool block_of_launch(const KParams& P, uint32_t& b, uint32_t bid, uint32_t nblk,
+                                                bool lead)
 {
-    if ((VAR & kVarWideHeavy) && P.hf_measure && bid == 0u && threadIdx.x == 0u)
+    if ((VAR & kVarWideHeavy) && P.hf_measure && lead)
         *P.hf_plan_out = HfPlan{};                            // k_hf_plan runs after this kernel
     if (P.hf_front)
     {
-        if (P.hf_measure && bid == 0u && threadIdx.x == 0u)
+        if (P.hf_measure && lead)
             *P.hf_plan_out = HfPlan{};                        // k_hf_plan runs after this kernel
         const uint32_t front = P.hf_front;
         if (bid < front)
@@ -1817,16 +1820,14 @@ __device__ __forceinline__ void wide_section(const KParams& P, uint32_t bid)
     }
 }
 
-// RT_KERNEL_LANES / AUTO: one lane per sample (spp = 2^spp_shift <= 64), one work item per
-// wave.  Heavy-first order: see block_of_launch and k_hf_plan; wide section: wide_section.
+// Wave `wib` (0-3) of launch block bid of nblk: its work item after the heavy-first / XCD-band map.
 template <int TRI, int VAR>
-__global__ void __launch_bounds__(kWG) k_render_lanes(KParams P)
+__device__ __forceinline__ void lanes_block_wave(const KParams& P, uint32_t bid, uint32_t nblk, uint32_t wib,
+                                                 volatile uint32_t *t0v)
 {
-    __shared__ uint32_t t0s[kWavesPerWG];
-    volatile uint32_t *t0v = t0s;                 // a wave's start time waits in LDS across the walk
     uint32_t b;
-    if (!block_of_launch<VAR>(P, b, blockIdx.x, gridDim.x)) return;
-    const uint32_t item = b * kWavesPerWG + (threadIdx.x >> 6);
+    if (!block_of_launch<VAR>(P, b, bid, nblk, bid == 0u && wib == 0u && (threadIdx.x & 63u) == 0u)) return;
+    const uint32_t item = b * kWavesPerWG + wib;
     if constexpr ((VAR & kVarWideHeavy) != 0)
         if (P.wh_wgs && P.hf_ver && P.wh_mark_in[item] == P.hf_ver) return;   // traced by the wide section
     if constexpr ((VAR & kVarWaveClock) != 0)
@@ -1877,6 +1878,40 @@ __global__ void __launch_bounds__(kWG) k_render_lanes(KParams P)
     }
 }
 
+// RT_KERNEL_LANES / AUTO: one lane per sample (spp = 2^spp_shift <= 64), one work item per
+// wave.  Heavy-first order: see block_of_launch and k_hf_plan; wide section: wide_section.
+template <int TRI, int VAR>
+__global__ void __launch_bounds__(kWG) k_render_lanes(KParams P)
+{
+    __shared__ uint32_t t0s[kWavesPerWG];
+    volatile uint32_t *t0v = t0s;                 // a wave's start time waits in LDS across the walk
+    lanes_block_wave<TRI, VAR>(P, blockIdx.x, gridDim.x, threadIdx.x >> 6, t0v);
+}
+
+// The same launch blocks as one-wave workgroups (AUTO's whole-frame launches of >= wg64_min_blocks
+// blocks; rt_scene::wg64).  A wave slot that frees up takes the next workgroup by itself instead of
+// waiting until three more slots of its CU are free for a 256-lane workgroup: with waves of very
+// different lengths (killeroo 1080p x 4: median 13 us, p99 100 us, max 450 us) the dispatched
+// 256-lane grid held only ~75 % of the 8,192 wave slots mid-frame (profiles/r03q_waves_*.json).
+// Workgroup w runs wave r % 4 of launch block (r / 4) * 8 + w % 8, r = w / 8, so every block keeps
+// the XCD its 256-lane workgroup had (workgroups w and w + 8 share one under the dispatcher's
+// round-robin deal: the XCD bands of xcd_band_block hold) and the launch keeps its block order
+// (the heavy-first front first).  Grid: 4 x vblocks rounded up to 8; pixels and per-sample
+// arithmetic are unchanged (process_item per work item, as in k_render_lanes).  Measured in-process
+// (tools/launch_ab.py, profiles/r03w_w64_all.json, 1080p x 4 steady): killeroo 0.390 -> 0.369 ms,
+// head 0.258 -> 0.251, the 10 scenes 2.99 -> 2.95 ms; resident waves on per-XCD work queues
+// (one returning atomic per item) lost 10-60 % to the dequeues (profiles/r03u_launch_ab_pq_w64.json, r03v_persist_*.json).
+template <int TRI, int VAR>
+__global__ void __launch_bounds__(64) k_render_lanes_w64(KParams P)
+{
+    __shared__ uint32_t t0s[1];
+    const uint32_t w = blockIdx.x, r = w / kXcds;
+    const uint32_t vbid = (r >> 2) * kXcds + w % kXcds;
+    const KParams& Q = late_params(P);
+    if (vbid >= Q.vblocks) return;
+    lanes_block_wave<TRI, VAR>(P, vbid, Q.vblocks, r & 3u, t0s);
+}
+
 // kVarWideHeavy: the wide section, launched on the scene's side stream beside the lane kernel
 // (its own register allocation: folded into the lane kernel it cost 106 SGPRs and spills)
 template <uint32_t G>
@@ -1910,7 +1945,7 @@ __global__ void __launch_bounds__(kWG) k_render_batch(KBatch B)
         nblk -= nw;
     }
     uint32_t b;
-    if (!block_of_launch<VAR>(B.p[0], b, bid, nblk)) return;
+    if (!block_of_launch<VAR>(B.p[0], b, bid, nblk, bid == 0u && threadIdx.x == 0u)) return;
     const uint32_t gitem = b * kWavesPerWG + (threadIdx.x >> 6);       // launch-wide item
     if constexpr ((VAR & kVarWideHeavy) != 0)
         if (B.p[0].wh_wgs && B.p[0].hf_ver && B.p[0].wh_mark_in[gitem] == B.p[0].hf_ver) return;
@@ -2469,6 +2504,8 @@ struct rt_scene
                                     // shards of scenes with a cell list this long
     uint32_t wh_fused = 1;          // RT_WH_FUSED: a batch's wide section leads the batch kernel's grid
                                     // (0: its own kernel on the side stream, fork / join)
+    uint32_t wg64 = 1;              // RT_WG64: AUTO launches of >= wg64_min_blocks 256-lane blocks run
+    uint32_t wg64_min_blocks = 8192; // as one-wave workgroups (k_render_lanes_w64; RT_WG64_MIN_BLOCKS)
     bool octant_words = false;      // 8 ray-octant copies of the empty-run words (else one L-inf word)
     bool box_words = false;         // 24 box-run word copies: AUTO's empty runs (kVarSkipRun)
     // camera-space x / y tables of the current frame shape (prepare_ndc)
@@ -2970,6 +3007,16 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
             if (int rc = hf_prepare(s, P, blocks, kvar, front, st)) return rc;
             grid += P.hf_front;
         }
+        // one-wave workgroups (k_render_lanes_w64): the same blocks, each wave dispatched by itself
+        kfn_t lfn = fn;
+        uint32_t lgrid = grid, lwg = kWG;
+        if (s->wg64 && kvar == kVarAuto && grid >= s->wg64_min_blocks)
+        {
+            lfn = k_render_lanes_w64<RT_TRI_MOLLER_TRUMBORE, kVarAuto>;
+            P.vblocks = grid;
+            lgrid = kWavesPerWG * ((grid + kXcds - 1u) / kXcds * kXcds);
+            lwg = 64u;
+        }
         RT_HIP(mark(kt0));
         if (P.wh_wgs)
         {
@@ -2987,7 +3034,7 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
             if (P.wh_g == 4u) hipLaunchKernelGGL(k_render_wh<4>, dim3(P.wh_wgs), wg, 0, s->side, P);
             else hipLaunchKernelGGL(k_render_wh<16>, dim3(P.wh_wgs), wg, 0, s->side, P);
         }
-        hipLaunchKernelGGL(fn, dim3(grid), wg, 0, st, P);
+        hipLaunchKernelGGL(lfn, dim3(lgrid), dim3(lwg), 0, st, P);
         if (P.wh_wgs)
         {
             RT_HIP(hipEventRecord(s->ev_join, s->side));
@@ -3305,6 +3352,8 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
     // scheduling tunables: read once here, never per launch (A/B sweeps set them per scene)
     s->hf_floor = env_tunable("RT_HF_FLOOR", s->hf_floor);
     s->hf_min_blocks = env_tunable("RT_HF_MIN_BLOCKS", s->hf_min_blocks);
+    s->wg64 = env_tunable("RT_WG64", s->wg64);
+    s->wg64_min_blocks = env_tunable("RT_WG64_MIN_BLOCKS", s->wg64_min_blocks);
     s->wh_floor = env_tunable("RT_WH_FLOOR", s->wh_floor);
     s->wh_alpha16 = env_tunable("RT_WH_ALPHA16", s->wh_alpha16);
     s->wh_alpha16_n2 = env_tunable("RT_WH_ALPHA16_N2", s->wh_alpha16_n2);
