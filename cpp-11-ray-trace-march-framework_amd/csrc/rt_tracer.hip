@@ -1793,11 +1793,12 @@ __device__ __forceinline__ void wide_samples(const KParams& P, uint32_t k, uint3
 // word keeps its lane-mode measurement until a refresh frame renders it one lane per sample again.
 // In a batch (KBatch, BATCH = true) P is p[0] (the batch's list, launch-wide item indices) and each
 // item is rendered with its own frame's parameters.
+// w: this wave's index in the section (4 per 256-lane workgroup, or one per one-wave workgroup).
 template <bool BATCH, uint32_t G>
-__device__ __forceinline__ void wide_section(const KParams& P, uint32_t bid)
+__device__ __forceinline__ void wide_section(const KParams& P, uint32_t w)
 {
     const uint32_t n = P.hf_ver ? min(P.hf_plan_in->cnt_w, kWhMax) : 0u;
-    const uint32_t w = bid * kWavesPerWG + (threadIdx.x >> 6), nw = P.wh_wgs * kWavesPerWG;
+    const uint32_t nw = P.wh_wgs * kWavesPerWG;
     const uint32_t ipt = P.wg_per_tile * kWavesPerWG;              // items per tile
     for (uint32_t e = w; e < n * G; e += nw)
     {
@@ -1917,7 +1918,37 @@ __global__ void __launch_bounds__(64) k_render_lanes_w64(KParams P)
 template <uint32_t G>
 __global__ void __launch_bounds__(kWG) k_render_wh(KParams P)
 {
-    wide_section<false, G>(P, blockIdx.x);
+    wide_section<false, G>(P, blockIdx.x * kWavesPerWG + (threadIdx.x >> 6));
+}
+
+// The multi-frame launch (KBatch): the launch's blocks are the frames' blocks, frame-major; the
+// heavy-first order (p[0]'s state) ranks them all, and every wave renders its item with its own
+// frame's parameters (KParams re-read from the kernarg segment at the frame's offset).
+// (The fused variant holds 83 SGPRs: 7 waves / SIMD.  Forced to 8 it spills a VGPR and measured
+// slower: rank of 4 / 8 0.256 / 0.139 ms vs 0.241 / 0.136, profiles/r03g_ab_wide_fused_*.json.)
+// Wave `wib` of launch block bid of nblk's lane blocks (after the fused wide section's workgroups).
+template <int TRI, int VAR>
+__device__ __forceinline__ void batch_block_wave(const KBatch& B, uint32_t bid, uint32_t nblk, uint32_t wib,
+                                                 volatile uint32_t *t0v)
+{
+    uint32_t b;
+    if (!block_of_launch<VAR>(B.p[0], b, bid, nblk, bid == 0u && wib == 0u && (threadIdx.x & 63u) == 0u)) return;
+    const uint32_t gitem = b * kWavesPerWG + wib;                    // launch-wide item
+    if constexpr ((VAR & kVarWideHeavy) != 0)
+        if (B.p[0].wh_wgs && B.p[0].hf_ver && B.p[0].wh_mark_in[gitem] == B.p[0].hf_ver) return;
+    const uint32_t f = batch_frame(B, b);
+    const uint32_t off = uint32_t(offsetof(KBatch, p)) + f * uint32_t(sizeof(KParams));
+    const uint32_t item = gitem - B.base[f] * kWavesPerWG;
+    const bool hf = B.p[0].hf_measure != 0u;
+    if (hf && (threadIdx.x & 63u) == 0u) t0v[threadIdx.x >> 6] = uint32_t(__builtin_amdgcn_s_memtime());
+    process_item<TRI, VAR>(late_params(B.p[0], off), item, off);
+    const KParams& Q = late_params(B.p[0], uint32_t(offsetof(KBatch, p)));
+    if (Q.hf_measure)
+    {
+        const uint32_t t1 = uint32_t(__builtin_amdgcn_s_memtime());
+        const uint32_t t0 = __builtin_amdgcn_readfirstlane(t0v[threadIdx.x >> 6]);
+        if ((threadIdx.x & 63u) == 0u) Q.hf_cost[__builtin_amdgcn_readfirstlane(gitem)] = t1 - t0;
+    }
 }
 
 // The multi-frame launch (KBatch): the launch's blocks are the frames' blocks, frame-major; the
@@ -1938,36 +1969,44 @@ __global__ void __launch_bounds__(kWG) k_render_batch(KBatch B)
         const uint32_t nw = B.p[0].wh_wgs;
         if (bid < nw)
         {
-            wide_section<true, (VAR & kVarWideG4) ? 4u : 16u>(B.p[0], bid);
+            wide_section<true, (VAR & kVarWideG4) ? 4u : 16u>(B.p[0], bid * kWavesPerWG + (threadIdx.x >> 6));
             return;
         }
         bid -= nw;
         nblk -= nw;
     }
-    uint32_t b;
-    if (!block_of_launch<VAR>(B.p[0], b, bid, nblk, bid == 0u && threadIdx.x == 0u)) return;
-    const uint32_t gitem = b * kWavesPerWG + (threadIdx.x >> 6);       // launch-wide item
-    if constexpr ((VAR & kVarWideHeavy) != 0)
-        if (B.p[0].wh_wgs && B.p[0].hf_ver && B.p[0].wh_mark_in[gitem] == B.p[0].hf_ver) return;
-    const uint32_t f = batch_frame(B, b);
-    const uint32_t off = uint32_t(offsetof(KBatch, p)) + f * uint32_t(sizeof(KParams));
-    const uint32_t item = gitem - B.base[f] * kWavesPerWG;
-    const bool hf = B.p[0].hf_measure != 0u;
-    if (hf && (threadIdx.x & 63u) == 0u) t0v[threadIdx.x >> 6] = uint32_t(__builtin_amdgcn_s_memtime());
-    process_item<TRI, VAR>(late_params(B.p[0], off), item, off);
-    const KParams& Q = late_params(B.p[0], uint32_t(offsetof(KBatch, p)));
-    if (Q.hf_measure)
+    batch_block_wave<TRI, VAR>(B, bid, nblk, threadIdx.x >> 6, t0v);
+}
+
+// k_render_batch as one-wave workgroups (k_render_lanes_w64's map): the fused wide section's
+// 4 x wh_wgs waves first, then wave r % 4 of lane block (r / 4) * 8 + w % 8, r = w / 8, of the
+// p[0].vblocks lane blocks.
+template <int TRI, int VAR>
+__global__ void __launch_bounds__(64) k_render_batch_w64(KBatch B)
+{
+    __shared__ uint32_t t0s[1];
+    uint32_t w = blockIdx.x;
+    if constexpr ((VAR & kVarWideFused) != 0)
     {
-        const uint32_t t1 = uint32_t(__builtin_amdgcn_s_memtime());
-        const uint32_t t0 = __builtin_amdgcn_readfirstlane(t0v[threadIdx.x >> 6]);
-        if ((threadIdx.x & 63u) == 0u) Q.hf_cost[__builtin_amdgcn_readfirstlane(gitem)] = t1 - t0;
+        const uint32_t nw = B.p[0].wh_wgs * kWavesPerWG;
+        if (w < nw)
+        {
+            wide_section<true, (VAR & kVarWideG4) ? 4u : 16u>(B.p[0], w);
+            return;
+        }
+        w -= nw;
     }
+    const uint32_t r = w / kXcds;
+    const uint32_t vbid = (r >> 2) * kXcds + w % kXcds;
+    const uint32_t nv = late_params(B.p[0], uint32_t(offsetof(KBatch, p))).vblocks;
+    if (vbid >= nv) return;
+    batch_block_wave<TRI, VAR>(B, vbid, nv, r & 3u, t0s);
 }
 
 template <uint32_t G>
 __global__ void __launch_bounds__(kWG) k_render_wh_batch(KBatch B)
 {
-    wide_section<true, G>(B.p[0], blockIdx.x);
+    wide_section<true, G>(B.p[0], blockIdx.x * kWavesPerWG + (threadIdx.x >> 6));
 }
 
 // RT_KERNEL_COMPACT (grid intersector, spp a power of two <= 64): wavefront active-ray
@@ -2506,6 +2545,7 @@ struct rt_scene
                                     // (0: its own kernel on the side stream, fork / join)
     uint32_t wg64 = 1;              // RT_WG64: AUTO launches of >= wg64_min_blocks 256-lane blocks run
     uint32_t wg64_min_blocks = 8192; // as one-wave workgroups (k_render_lanes_w64; RT_WG64_MIN_BLOCKS)
+    uint32_t wg64_batch_min_blocks = 0;  // the same for batched launches (RT_WG64_BATCH_MIN_BLOCKS)
     bool octant_words = false;      // 8 ray-octant copies of the empty-run words (else one L-inf word)
     bool box_words = false;         // 24 box-run word copies: AUTO's empty runs (kVarSkipRun)
     // camera-space x / y tables of the current frame shape (prepare_ndc)
@@ -3077,14 +3117,19 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
 
 // k_render_batch instantiation of a variant (nullptr: the frames take one launch each)
 typedef void (*kbfn_t)(KBatch);
-kbfn_t batch_kernel(int var)
+template <int VAR>
+kbfn_t batch_kernel_of(bool w64)
 {
-    if (var == kVarAuto) return k_render_batch<RT_TRI_MOLLER_TRUMBORE, kVarAuto>;
-    if (var == (kVarAuto | kVarWideHeavy)) return k_render_batch<RT_TRI_MOLLER_TRUMBORE, kVarAuto | kVarWideHeavy>;
+    return w64 ? k_render_batch_w64<RT_TRI_MOLLER_TRUMBORE, VAR> : k_render_batch<RT_TRI_MOLLER_TRUMBORE, VAR>;
+}
+kbfn_t batch_kernel(int var, bool w64)
+{
+    if (var == kVarAuto) return batch_kernel_of<kVarAuto>(w64);
+    if (var == (kVarAuto | kVarWideHeavy)) return batch_kernel_of<kVarAuto | kVarWideHeavy>(w64);
     if (var == (kVarAuto | kVarWideHeavy | kVarWideFused))
-        return k_render_batch<RT_TRI_MOLLER_TRUMBORE, kVarAuto | kVarWideHeavy | kVarWideFused>;
+        return batch_kernel_of<kVarAuto | kVarWideHeavy | kVarWideFused>(w64);
     if (var == (kVarAuto | kVarWideHeavy | kVarWideFused | kVarWideG4))
-        return k_render_batch<RT_TRI_MOLLER_TRUMBORE, kVarAuto | kVarWideHeavy | kVarWideFused | kVarWideG4>;
+        return batch_kernel_of<kVarAuto | kVarWideHeavy | kVarWideFused | kVarWideG4>(w64);
     return nullptr;
 }
 
@@ -3123,8 +3168,7 @@ int launch_batch(rt_scene *const *S, const rt_frame *F, uint32_t n, KParams *P, 
     const bool fused = wide_heavy && S[0]->wh_fused && P[0].nranks >= 4u;
     const int kvar = var | (wide_heavy ? kVarWideHeavy : 0) | (fused ? kVarWideFused : 0) |
                      (fused && spp > 4u ? kVarWideG4 : 0);
-    const kbfn_t fn = batch_kernel(kvar);
-    if (!fn) return RT_E_INVALID;
+    if (!batch_kernel(kvar, false)) return RT_E_INVALID;
     *batched = true;
     KBatch KB;
     std::memset(&KB, 0, sizeof(KB));
@@ -3159,6 +3203,19 @@ int launch_batch(rt_scene *const *S, const rt_frame *F, uint32_t n, KParams *P, 
     // blocks keep their block -> XCD assignment
     if (fused && P[0].wh_wgs) P[0].wh_wgs = (P[0].wh_wgs + kXcds - 1u) & ~(kXcds - 1u);
     uint32_t grid = uint32_t(blocks) + P[0].hf_front + (fused ? P[0].wh_wgs : 0u);
+    // one-wave workgroups (k_render_batch_w64, as k_render_lanes_w64): the same blocks and order.
+    // Not beside a wide section: measured there (tools/tunable_sweep.py RT_WG64, the bench pair,
+    // profiles/r03y_wg64_batch_sweep.json) a rank of 2 / 4 / 8 took 0.354 / 0.207 / 0.118 ms vs
+    // 0.336 / 0.190 / 0.119 with 256-lane workgroups; without one (N = 1) 0.569 vs 0.598
+    const bool w64 = s0->wg64 != 0u && !wide_heavy && uint32_t(blocks) + P[0].hf_front >= s0->wg64_batch_min_blocks;
+    uint32_t bwg = kWG;
+    if (w64)
+    {
+        P[0].vblocks = uint32_t(blocks) + P[0].hf_front;
+        grid = kWavesPerWG * ((fused ? P[0].wh_wgs : 0u) + (P[0].vblocks + kXcds - 1u) / kXcds * kXcds);
+        bwg = 64u;
+    }
+    const kbfn_t fn = batch_kernel(kvar, w64);
     for (uint32_t i = 0; i < n; i++) KB.p[i] = P[i];
     // timing: scene 0's ring (one timed launch for the whole batch)
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
@@ -3186,7 +3243,7 @@ int launch_batch(rt_scene *const *S, const rt_frame *F, uint32_t n, KParams *P, 
         if (P[0].wh_g == 4u) hipLaunchKernelGGL(k_render_wh_batch<4>, dim3(P[0].wh_wgs), wg, 0, s0->side, KB);
         else hipLaunchKernelGGL(k_render_wh_batch<16>, dim3(P[0].wh_wgs), wg, 0, s0->side, KB);
     }
-    hipLaunchKernelGGL(fn, dim3(grid), wg, 0, st, KB);
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(bwg), 0, st, KB);
     if (P[0].wh_wgs && !fused)
     {
         RT_HIP(hipEventRecord(s0->ev_join, s0->side));
@@ -3354,6 +3411,7 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
     s->hf_min_blocks = env_tunable("RT_HF_MIN_BLOCKS", s->hf_min_blocks);
     s->wg64 = env_tunable("RT_WG64", s->wg64);
     s->wg64_min_blocks = env_tunable("RT_WG64_MIN_BLOCKS", s->wg64_min_blocks);
+    s->wg64_batch_min_blocks = env_tunable("RT_WG64_BATCH_MIN_BLOCKS", s->wg64_batch_min_blocks);
     s->wh_floor = env_tunable("RT_WH_FLOOR", s->wh_floor);
     s->wh_alpha16 = env_tunable("RT_WH_ALPHA16", s->wh_alpha16);
     s->wh_alpha16_n2 = env_tunable("RT_WH_ALPHA16_N2", s->wh_alpha16_n2);
