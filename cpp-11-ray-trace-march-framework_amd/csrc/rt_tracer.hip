@@ -2009,6 +2009,13 @@ __global__ void __launch_bounds__(kWG) k_render_wh_batch(KBatch B)
     wide_section<true, G>(B.p[0], blockIdx.x * kWavesPerWG + (threadIdx.x >> 6));
 }
 
+// k_render_wh_batch as one-wave workgroups (beside a one-wave lane grid, rt_scene::wg64_wide)
+template <uint32_t G>
+__global__ void __launch_bounds__(64) k_render_wh_batch_w64(KBatch B)
+{
+    wide_section<true, G>(B.p[0], blockIdx.x);
+}
+
 // RT_KERNEL_COMPACT (grid intersector, spp a power of two <= 64): wavefront active-ray
 // compaction.  In the LANES kernel a wave lives until its slowest ray ends, so lanes whose ray
 // already hit (or left the grid) idle through the rest of the walk (~23 % of lane-cycles on
@@ -2546,6 +2553,9 @@ struct rt_scene
     uint32_t wg64 = 1;              // RT_WG64: AUTO launches of >= wg64_min_blocks 256-lane blocks run
     uint32_t wg64_min_blocks = 8192; // as one-wave workgroups (k_render_lanes_w64; RT_WG64_MIN_BLOCKS)
     uint32_t wg64_batch_min_blocks = 0;  // the same for batched launches (RT_WG64_BATCH_MIN_BLOCKS)
+    uint32_t wg64_wide = 0xA;       // RT_WG64_WIDE: bit log2(N) (3: N >= 8): one-wave workgroups also
+                                    // for a rank of N's batch with a wide section
+    uint32_t wh_fused_min_ranks = 2; // RT_WH_FUSED_MIN_RANKS: smallest rank count of a fused section
     bool octant_words = false;      // 8 ray-octant copies of the empty-run words (else one L-inf word)
     bool box_words = false;         // 24 box-run word copies: AUTO's empty runs (kVarSkipRun)
     // camera-space x / y tables of the current frame shape (prepare_ndc)
@@ -3164,8 +3174,9 @@ int launch_batch(rt_scene *const *S, const rt_frame *F, uint32_t n, KParams *P, 
     }
     if (var != kVarAuto) return RT_E_INVALID;
     // fused (measured, profiles/r03f_ab_wide_fused.json): 18 % faster at a rank of 8, 9 % at 4,
-    // 4 % slower at 2 -- taken from 4 ranks on
-    const bool fused = wide_heavy && S[0]->wh_fused && P[0].nranks >= 4u;
+    // 4 % slower at 2 on the build of that A/B; re-measured on the current one, a rank of 2 takes
+    // 0.321 ms fused vs 0.338 (profiles/r03aa_wg64_wide_fused2_sweep.json): fused from 2 ranks
+    const bool fused = wide_heavy && S[0]->wh_fused && P[0].nranks >= S[0]->wh_fused_min_ranks;
     const int kvar = var | (wide_heavy ? kVarWideHeavy : 0) | (fused ? kVarWideFused : 0) |
                      (fused && spp > 4u ? kVarWideG4 : 0);
     if (!batch_kernel(kvar, false)) return RT_E_INVALID;
@@ -3204,10 +3215,14 @@ int launch_batch(rt_scene *const *S, const rt_frame *F, uint32_t n, KParams *P, 
     if (fused && P[0].wh_wgs) P[0].wh_wgs = (P[0].wh_wgs + kXcds - 1u) & ~(kXcds - 1u);
     uint32_t grid = uint32_t(blocks) + P[0].hf_front + (fused ? P[0].wh_wgs : 0u);
     // one-wave workgroups (k_render_batch_w64, as k_render_lanes_w64): the same blocks and order.
-    // Not beside a wide section: measured there (tools/tunable_sweep.py RT_WG64, the bench pair,
-    // profiles/r03y_wg64_batch_sweep.json) a rank of 2 / 4 / 8 took 0.354 / 0.207 / 0.118 ms vs
-    // 0.336 / 0.190 / 0.119 with 256-lane workgroups; without one (N = 1) 0.569 vs 0.598
-    const bool w64 = s0->wg64 != 0u && !wide_heavy && uint32_t(blocks) + P[0].hf_front >= s0->wg64_batch_min_blocks;
+    // Without a wide section (N = 1) the bench pair took 0.569 vs 0.598 ms with 256-lane
+    // workgroups (profiles/r03y_wg64_batch_sweep.json).  Beside one, per rank count (wg64_wide, bit
+    // log2 N, 3 for N >= 8): with the section fused from 2 ranks and one-wave workgroups on both
+    // (profiles/r03aa_wg64_wide_*.json) a rank of 2 took 0.306 ms (0.321 with 256-lane ones, 0.338
+    // unfused), of 8 0.117 (0.121); a rank of 4 0.206 vs 0.193, so 4 keeps 256-lane workgroups
+    const uint32_t lg_ranks = P[0].nranks >= 8u ? 3u : (P[0].nranks >= 4u ? 2u : (P[0].nranks >= 2u ? 1u : 0u));
+    const bool w64 = s0->wg64 != 0u && (!wide_heavy || ((s0->wg64_wide >> lg_ranks) & 1u) != 0u) &&
+                     uint32_t(blocks) + P[0].hf_front >= s0->wg64_batch_min_blocks;
     uint32_t bwg = kWG;
     if (w64)
     {
@@ -3240,7 +3255,11 @@ int launch_batch(rt_scene *const *S, const rt_frame *F, uint32_t n, KParams *P, 
         }
         RT_HIP(hipEventRecord(s0->ev_fork, st));
         RT_HIP(hipStreamWaitEvent(s0->side, s0->ev_fork, 0));
-        if (P[0].wh_g == 4u) hipLaunchKernelGGL(k_render_wh_batch<4>, dim3(P[0].wh_wgs), wg, 0, s0->side, KB);
+        if (w64 && P[0].wh_g == 4u)
+            hipLaunchKernelGGL(k_render_wh_batch_w64<4>, dim3(kWavesPerWG * P[0].wh_wgs), dim3(64), 0, s0->side, KB);
+        else if (w64)
+            hipLaunchKernelGGL(k_render_wh_batch_w64<16>, dim3(kWavesPerWG * P[0].wh_wgs), dim3(64), 0, s0->side, KB);
+        else if (P[0].wh_g == 4u) hipLaunchKernelGGL(k_render_wh_batch<4>, dim3(P[0].wh_wgs), wg, 0, s0->side, KB);
         else hipLaunchKernelGGL(k_render_wh_batch<16>, dim3(P[0].wh_wgs), wg, 0, s0->side, KB);
     }
     hipLaunchKernelGGL(fn, dim3(grid), dim3(bwg), 0, st, KB);
@@ -3417,6 +3436,8 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
     s->wh_alpha16_n2 = env_tunable("RT_WH_ALPHA16_N2", s->wh_alpha16_n2);
     s->wh_auto_refs = env_tunable("RT_WH_AUTO_REFS", s->wh_auto_refs);
     s->wh_fused = env_tunable("RT_WH_FUSED", s->wh_fused);
+    s->wg64_wide = env_tunable("RT_WG64_WIDE", s->wg64_wide);
+    s->wh_fused_min_ranks = env_tunable("RT_WH_FUSED_MIN_RANKS", s->wh_fused_min_ranks);
     for (int a = 0; a < 3; a++)
     {
         s->dims[a] = g.dims[a];

@@ -817,11 +817,12 @@ def _batch_check(golden, gss, sids, W, H, N, reps, kernel=0):
         assert sha_dev(h) == g["hits_sha256"], (sid, N)
 
 
-@pytest.mark.parametrize("N", [1, 2, 8])
+@pytest.mark.parametrize("N", [1, 2, 4, 8])
 def test_batch_bench_pair(golden, scenes, N):
     """The bench step as one batched launch (Cornell + killeroo, k_render_batch): frames and hit IDs
     of both scenes equal the reference's, after six launches per rank (natural order, heavy-first
-    order across both frames, and at N >= 2 the batch's wide section on killeroo's heavy items)."""
+    order across both frames, and at N >= 2 the batch's wide section on killeroo's heavy items,
+    fused into the batch grid; one-wave workgroups at N = 1, 2 and 8, 256-lane ones at 4)."""
     sids = (1, 8)
     gss = [scenes(s)[1] for s in sids]
     _batch_check(golden, gss, sids, 1920, 1080, N, 6)

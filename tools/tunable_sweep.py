@@ -30,7 +30,11 @@ ap.add_argument("--ns", type=int, nargs="+", default=[1, 2, 4, 8])
 ap.add_argument("--rounds", type=int, default=2)
 ap.add_argument("--per-scene", action="store_true")
 ap.add_argument("--out", default="tunable_sweep")
+ap.add_argument("--extra-env", nargs="*", default=[], help="K=V pairs set for every value (before the scenes)")
 A = ap.parse_args()
+for kv in A.extra_env:
+    k, v = kv.split("=", 1)
+    os.environ[k] = v
 torch.cuda.set_device(0)
 st = torch.cuda.current_stream()
 W, H, SPP = A.frame
