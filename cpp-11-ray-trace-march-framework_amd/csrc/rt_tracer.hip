@@ -2545,6 +2545,7 @@ struct rt_scene
     uint32_t wh_floor = 100000;     // RT_WH_FLOOR: wide-section threshold floor, shader cycles
     uint32_t wh_alpha16 = 32;       // RT_WH_ALPHA16: wide threshold, sixteenths of the estimated span
     uint32_t wh_alpha16_n2 = 16;    // RT_WH_ALPHA16_N2: the same for a rank of 2 of a batched step
+    uint32_t wh_alpha16_n4 = 28;    // RT_WH_ALPHA16_N4: the same for a rank of 3-7 of a batched step
                                     // (measured, profiles/r03o_alpha_n2_sweep.json)
     uint32_t wh_auto_refs = 128;    // RT_WH_AUTO_REFS: AUTO takes the wide section for >= 2-rank
                                     // shards of scenes with a cell list this long
@@ -2899,7 +2900,12 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
         // a rank of 2 of a batched step lists more (its span estimate includes the other frames'
         // work); one scene's own rank-of-2 launch measured 25 % slower with it
         // (profiles/r03o_shard_scaling_bench.json), so it keeps the default
-        P.wh_alpha16 = (P.nranks == 2u && batch != 0u) ? s->wh_alpha16_n2 : s->wh_alpha16;
+        // and a rank of 4-7 of a batched step one notch lower than the default (rank of 4, measured
+        // in profiles/r03ad_alpha_n4_n8.json: 0.182 ms at 28/16 vs 0.191 at 32/16, 0.219 at 36/16;
+        // a rank of 8 keeps 32/16: 0.117 vs 0.119 at 28/16)
+        P.wh_alpha16 = (P.nranks == 2u && batch != 0u)                  ? s->wh_alpha16_n2
+                       : (P.nranks >= 3u && P.nranks < 8u && batch != 0u) ? s->wh_alpha16_n4
+                                                                          : s->wh_alpha16;
         P.wh_mark_in = c->wh_marks + size_t(v & 1u) * kWavesPerWG * c->cap_blocks;
         P.wh_mark_out = c->wh_marks + size_t((v + 1u) & 1u) * kWavesPerWG * c->cap_blocks;
         P.wh_list_in = c->wh_lists + size_t(v & 1u) * kWhMax;
@@ -3434,6 +3440,7 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
     s->wh_floor = env_tunable("RT_WH_FLOOR", s->wh_floor);
     s->wh_alpha16 = env_tunable("RT_WH_ALPHA16", s->wh_alpha16);
     s->wh_alpha16_n2 = env_tunable("RT_WH_ALPHA16_N2", s->wh_alpha16_n2);
+    s->wh_alpha16_n4 = env_tunable("RT_WH_ALPHA16_N4", s->wh_alpha16_n4);
     s->wh_auto_refs = env_tunable("RT_WH_AUTO_REFS", s->wh_auto_refs);
     s->wh_fused = env_tunable("RT_WH_FUSED", s->wh_fused);
     s->wg64_wide = env_tunable("RT_WG64_WIDE", s->wg64_wide);
