@@ -7,6 +7,7 @@ per scene.  Values are interleaved over --rounds rounds; per (value, N) the max 
 the median.  Also reports the wide section's listed items per rank.
 
     python3 tools/tunable_sweep.py --env RT_PRIO --values 0 1 2 3 [--scenes 1 8] [--rounds 2]
+    python3 tools/tunable_sweep.py --env KERNEL --values 0 0x1000    (frame kernel values instead)
 """
 import argparse
 import importlib.util
@@ -59,9 +60,11 @@ def steady(run):
 res = {"env": A.env, "scenes": A.scenes, "frame": A.frame, "batch": {}, "per_scene": {}, "wide_items": {}}
 for rnd in range(A.rounds):
     for v in A.values:
-        os.environ[A.env] = v
+        if A.env != "KERNEL":
+            os.environ[A.env] = v
+        kern = int(v, 0) if A.env == "KERNEL" else 0   # --env KERNEL: the values are rt_frame.kernel
         gs = [rtm.GpuScene(hs[sid], 0) for sid in A.scenes]
-        fs = [g.frame(W, H, SPP) for g in gs]
+        fs = [g.frame(W, H, SPP, kernel=kern) for g in gs]
         for n in A.ns:
             bufs = [torch.empty(rtm.shard_elems(W, H, n) if n > 1 else W * H, dtype=torch.int32, device="cuda")
                     for _ in gs]
