@@ -231,8 +231,57 @@ def valu_roofline(rtm, kernel_ms, args, world, algorithmic):
     return roof
 
 
+REFDRIVER = os.path.join(ROOT, "oracle", "_ref", "refdriver")
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            return next(l.split(":", 1)[1].strip() for l in f if l.startswith("model name"))
+    except Exception:
+        return platform.processor()
+
+
+def cpu_baseline_reference():
+    """The reference itself on this host: oracle/_ref/refdriver is the reference's own grid.cpp /
+    mesh.cpp / sampling.cpp / ... translation units (compiled from /root/reference by oracle/Makefile,
+    shipped prebuilt like librt_tracer.so) around a restatement of renderer.cpp's tile loop and the
+    12x9 std::thread tile pool of framebuffer.cpp; it renders the committed post-setup scene files.
+    None when the binary is absent or fails (the port below is then the baseline)."""
+    import subprocess
+    if not os.access(REFDRIVER, os.X_OK):
+        return None
+    cores = host_cores()
+    cw, ch, cs = CPU_FRAME
+    # median of 5 after a warm-up render (SURVEY 8d); 3 for a step of > 100 M samples
+    reps = 5 if len(SCENES) * cw * ch * cs <= 100_000_000 else 3
+    tot = 0.0
+    for sid in SCENES:
+        scene = os.path.join(ROOT, "data", "scenes", f"scene{sid}.rtscene")
+        try:
+            subprocess.run([REFDRIVER, "render", scene, str(cw), str(ch), str(cs), "--threads", str(cores),
+                            "--reps", "1"], check=True, capture_output=True, timeout=300)     # warm-up
+            out = subprocess.run([REFDRIVER, "render", scene, str(cw), str(ch), str(cs), "--threads", str(cores),
+                                  "--reps", str(reps)], check=True, capture_output=True, text=True, timeout=600)
+            line = next(l for l in out.stdout.splitlines() if l.startswith("RESULT "))
+            tot += float(json.loads(line[len("RESULT "):])["median_s"])
+        except Exception as e:          # noqa: BLE001 -- any failure: fall back to the port
+            print(f"bench: reference CPU baseline unavailable ({type(e).__name__}: {e}); using the port",
+                  file=sys.stderr)
+            return None
+    return {"value": round(len(SCENES) * cw * ch * cs / tot / 1e6, 3), "unit": "Msamples/s",
+            "cores": cores, "kind": "reference",
+            "sample": f"full frames of scenes {list(SCENES)} at {cw}x{ch}x{cs} by oracle/_ref/refdriver (the "
+                      f"reference's own translation units), 12x9 tile pool, per scene the median of {reps} after "
+                      f"1 warm-up; cpu: {cpu_model()}"}
+
+
 def cpu_baseline(rtm_unused=None):
-    """Oracle (CPU restatement of the reference's std::thread tile pool) on this host."""
+    """The CPU baseline: the reference itself (cpu_baseline_reference) where its driver is present,
+    else the oracle's CPU restatement of the reference's std::thread tile pool (kind "port")."""
+    ref = cpu_baseline_reference()
+    if ref is not None:
+        return ref
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from conftest import Oracle
     orc = Oracle()
@@ -251,16 +300,10 @@ def cpu_baseline(rtm_unused=None):
             tot += s
         times.append(tot)
     med = sorted(times)[reps // 2]
-    model = ""
-    try:
-        with open("/proc/cpuinfo") as f:
-            model = next(l.split(":", 1)[1].strip() for l in f if l.startswith("model name"))
-    except Exception:
-        pass
     return {"value": round(len(SCENES) * cw * ch * cs / med / 1e6, 3), "unit": "Msamples/s",
             "cores": cores, "kind": "port",
             "sample": f"full frames of scenes {list(SCENES)} at {cw}x{ch}x{cs}, 12x9 tile pool, "
-                      f"median of {reps} after 1 warm-up; cpu: {model or platform.processor()}"}
+                      f"median of {reps} after 1 warm-up; cpu: {cpu_model()}"}
 
 
 class GpuWorkload:
