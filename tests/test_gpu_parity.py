@@ -817,6 +817,38 @@ def _batch_check(golden, gss, sids, W, H, N, reps, kernel=0):
         assert sha_dev(h) == g["hits_sha256"], (sid, N)
 
 
+@pytest.mark.parametrize("sid", [1, 8])
+def test_one_wave_workgroups_ragged(scenes, sid, monkeypatch):
+    """AUTO's one-wave-workgroup grid (k_render_lanes_w64) on a ragged frame whose launch block
+    count is not a multiple of 8 (1936x1072x4: 121 x 67 tiles, 32,428 blocks + the heavy-first
+    front): six consecutive frames and their per-sample hit IDs equal those of a scene made with
+    RT_WG64=0 (the 256-lane grid, pinned to the reference elsewhere)."""
+    import torch
+    W, H = 1936, 1072
+    st = torch.cuda.current_stream().cuda_stream
+    hs, gs = scenes(sid)
+    monkeypatch.setenv("RT_WG64", "0")
+    g256 = rtm.GpuScene(hs, 0)
+    try:
+        outs, hitss = [], []
+        for g in (gs, g256):
+            f = g.frame(W, H, 4)
+            out = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+            hits = torch.zeros(W * H * 4, dtype=torch.int32, device="cuda")
+            for i in range(6):
+                out.fill_(0x5A5A5A5A)
+                hits.fill_(0x5A5A5A5A)
+                g.render_hits_device(f, 0, 1, out.data_ptr(), hits.data_ptr(), st)
+                torch.cuda.synchronize()
+                if outs:
+                    assert torch.equal(out, outs[0]) and torch.equal(hits, hitss[0]), (sid, i)
+            outs.append(out.clone())
+            hitss.append(hits.clone())
+        assert int((outs[0] == 0x5A5A5A5A).sum()) == 0
+    finally:
+        g256.close()
+
+
 @pytest.mark.parametrize("N", [1, 2, 4, 8])
 def test_batch_bench_pair(golden, scenes, N):
     """The bench step as one batched launch (Cornell + killeroo, k_render_batch): frames and hit IDs
