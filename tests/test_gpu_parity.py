@@ -817,14 +817,15 @@ def _batch_check(golden, gss, sids, W, H, N, reps, kernel=0):
         assert sha_dev(h) == g["hits_sha256"], (sid, N)
 
 
-@pytest.mark.parametrize("sid", [1, 8])
-def test_one_wave_workgroups_ragged(scenes, sid, monkeypatch):
-    """AUTO's one-wave-workgroup grid (k_render_lanes_w64) on a ragged frame whose launch block
+@pytest.mark.parametrize("sid,W,H,spp", [(1, 1936, 1072, 4), (8, 1936, 1072, 4), (8, 1920, 1080, 2),
+                                         (8, 1280, 720, 8), (5, 960, 540, 16)])
+def test_one_wave_workgroups_ragged(scenes, sid, W, H, spp, monkeypatch):
+    """AUTO's one-wave-workgroup grid (k_render_lanes_w64) -- on a ragged frame whose launch block
     count is not a multiple of 8 (1936x1072x4: 121 x 67 tiles, 32,428 blocks + the heavy-first
-    front): six consecutive frames and their per-sample hit IDs equal those of a scene made with
-    RT_WG64=0 (the 256-lane grid, pinned to the reference elsewhere)."""
+    front) and at spp 2 / 8 / 16 (1 / 8 / 16 blocks per tile): six consecutive frames and their
+    per-sample hit IDs equal those of a scene made with RT_WG64=0 (the 256-lane grid, pinned to
+    the reference elsewhere)."""
     import torch
-    W, H = 1936, 1072
     st = torch.cuda.current_stream().cuda_stream
     hs, gs = scenes(sid)
     monkeypatch.setenv("RT_WG64", "0")
@@ -832,9 +833,9 @@ def test_one_wave_workgroups_ragged(scenes, sid, monkeypatch):
     try:
         outs, hitss = [], []
         for g in (gs, g256):
-            f = g.frame(W, H, 4)
+            f = g.frame(W, H, spp)
             out = torch.zeros(W * H, dtype=torch.int32, device="cuda")
-            hits = torch.zeros(W * H * 4, dtype=torch.int32, device="cuda")
+            hits = torch.zeros(W * H * spp, dtype=torch.int32, device="cuda")
             for i in range(6):
                 out.fill_(0x5A5A5A5A)
                 hits.fill_(0x5A5A5A5A)
