@@ -133,28 +133,44 @@ def end_to_end(rtm, work, reps=7):
             "note": "host-buffer delivery incl. PCIe; value is never the bench value"}
 
 
+ORBIT_DEG = 0.5          # moving_camera: degrees the camera orbits the scene per frame
+
+
+def orbit_cam(cam, deg):
+    """The camera matrix (row-vector convention, translation in row 3: lin_alg.h Matrix44f) orbited by
+    `deg` degrees about the world y axis through the origin (the scenes are normalised around it,
+    mesh.cpp:120-136): M' = M x R_y, so position and orientation turn together."""
+    a = np.deg2rad(deg)
+    r = np.array([[np.cos(a), 0, -np.sin(a), 0], [0, 1, 0, 0], [np.sin(a), 0, np.cos(a), 0], [0, 0, 0, 1]],
+                 np.float64)
+    return (np.asarray(cam, np.float64).reshape(4, 4) @ r).astype(np.float32).reshape(16)
+
+
 def moving_camera(work, steps, warmup, static_ms):
-    """The same step with the camera origin changing every frame (two origins alternating, 1e-3
-    apart): k_origin_pre recomputes the per-origin triangle records before every render and the
-    heavy-first order runs on the previous frames' view -- what an interactive renderer with a
-    moving camera pays.  The bench value is the static-camera step (the scene's own camera)."""
+    """The same step with the camera orbiting the scene, ORBIT_DEG per frame: every frame has a new
+    origin (k_origin_pre recomputes the per-origin triangle records before its render) and a new view,
+    so the heavy-first order and the wide list come from frames of other views -- what an interactive
+    renderer with a moving camera pays.  The bench value is the static-camera step."""
     torch = work.torch
+    nfr = warmup + steps
     frames = []
     for sid, hs, gs, f in work.scenes:
-        pair = []
-        for j in range(2):
+        seq = []
+        for j in range(nfr):
             g = gs.frame(W, H, SPP, kernel=f.kernel)
-            g.cam[12] = float(np.float32(hs.cam[12]) + np.float32(1e-3 * j))
-            pair.append(g)
-        frames.append(pair)
+            c = orbit_cam(hs.cam, ORBIT_DEG * (j + 1))
+            for k in range(16):
+                g.cam[k] = float(c[k])
+            seq.append(g)
+        frames.append(seq)
 
     def step(i):
         if work.batch:
-            work.rtm.render_batch_device([g for _, _, g, _ in work.scenes], [p[i & 1] for p in frames],
+            work.rtm.render_batch_device([g for _, _, g, _ in work.scenes], [p[i] for p in frames],
                                          [b.data_ptr() for b in work.bufs[0]], stream=work.stream.cuda_stream)
             return
         for j, (sid, hs, gs, f) in enumerate(work.scenes):
-            gs.render_frame_device(frames[j][i & 1], work.bufs[0][j].data_ptr(), work.stream.cuda_stream)
+            gs.render_frame_device(frames[j][i], work.bufs[0][j].data_ptr(), work.stream.cuda_stream)
 
     with work.stream_ctx():
         for i in range(warmup):
@@ -163,17 +179,57 @@ def moving_camera(work, steps, warmup, static_ms):
     t0 = time.perf_counter()
     with work.stream_ctx():
         for i in range(steps):
-            step(i)
+            step(warmup + i)
     work.sync()
     ms = (time.perf_counter() - t0) / steps * 1e3
+    # the scenes' own cameras again for the rest of the run (their per-origin records come back)
+    with work.stream_ctx():
+        for j, (sid, hs, gs, f) in enumerate(work.scenes):
+            gs.render_frame_device(f, work.bufs[0][j].data_ptr(), work.stream.cuda_stream)
+    work.sync()
     return {"value": round(len(work.scenes) * W * H * SPP / (ms / 1e3) / 1e6, 3), "unit": "Msamples/s",
             "ms_per_step": round(ms, 4), "steps": steps, "warmup": warmup,
-            "origin_pre_ms_per_frame": round((ms - static_ms) / len(work.scenes), 4),
-            "note": "camera origin alternates between two positions every frame: k_origin_pre runs "
-                    "before every render; never the bench value"}
+            "orbit_deg_per_frame": ORBIT_DEG, "orbit_deg_total": round(ORBIT_DEG * nfr, 2),
+            "vs_static": round(static_ms / ms, 4),
+            "note": f"the camera orbits the scene {ORBIT_DEG} deg per frame about the world y axis: a new "
+                    "origin (k_origin_pre before every render) and a new view every frame; never the bench value"}
 
 
-def valu_roofline(rtm, kernel_ms, args, world, algorithmic):
+def first_frame(rtm, torch):
+    """The first frame of a new launch shape: fresh scene objects (no heavy-first plan, no per-origin
+    records, no camera tables yet -- what the reference pays after a resize, 'r', a spp change or a
+    scene switch, application.cpp:63-88), timed from the render call to the frame in HBM (wall clock,
+    includes the host-side setup and k_origin_pre) and by HIP events around the launch."""
+    out = {}
+    st = torch.cuda.Stream()
+    buf = torch.empty(W * H, dtype=torch.int32, device="cuda")
+    for sid in SCENES:
+        hs = rtm.HostScene.load(sid)
+        gs = rtm.GpuScene(hs, torch.cuda.current_device())
+        try:
+            f = gs.frame(W, H, SPP)
+            torch.cuda.synchronize()
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            t0 = time.perf_counter()
+            a.record(st)
+            gs.render_frame_device(f, buf.data_ptr(), st.cuda_stream)
+            b.record(st)
+            b.synchronize()
+            wall = time.perf_counter() - t0
+            # the second frame of the shape (still no plan: the first measured frames list nothing)
+            c = torch.cuda.Event(enable_timing=True)
+            gs.render_frame_device(f, buf.data_ptr(), st.cuda_stream)
+            c.record(st)
+            c.synchronize()
+            out[str(sid)] = {"wall_ms": round(wall * 1e3, 4), "device_ms": round(a.elapsed_time(b), 4),
+                             "second_frame_device_ms": round(b.elapsed_time(c), 4)}
+        finally:
+            gs.close()
+            hs.close()
+    return out
+
+
+def valu_roofline(rtm, kernel_ms, args, world, algorithmic, step_ms=None, work=None):
     """The bound that binds: VALU issue.  SQ_INSTS_VALU per launch comes from
     profiles/counters_<workload>.json (tools/collect_counters.py, rocprofv3 --pmc on this workload), used
     only when its source_hash equals the hash of the kernel sources being timed; achieved =
@@ -211,7 +267,11 @@ def valu_roofline(rtm, kernel_ms, args, world, algorithmic):
         if "batch" not in sc:
             roof["counters"] = "refused: counters are per-scene launches, the timed step is a batched launch"
             return roof
-        rate = sc["batch"]["SQ_INSTS_VALU"] / (kernel_ms["batch"] / 1e3)
+        fb = work.scenes[0][2].info()["batch_fallbacks"] if work is not None else 0
+        if fb:
+            roof["counters"] = f"refused: {fb} batch chunk(s) fell back to one launch per frame"
+            return roof
+        rate = sc["batch"]["SQ_INSTS_VALU"] / ((step_ms or kernel_ms["batch"]) / 1e3)
         roof.update({"achieved": round(rate / 1e9, 1), "frac": round(rate / VALU_PEAK, 4),
                      "traffic": sc["batch"]["hbm_bytes"],
                      "traffic_unit": "HBM bytes per batched launch (every scene's frame)",
@@ -221,7 +281,7 @@ def valu_roofline(rtm, kernel_ms, args, world, algorithmic):
         roof["counters"] = "refused: counters are of the batched launch, the timed step is per-scene launches"
         return roof
     insts = sum(sc[str(sid)]["SQ_INSTS_VALU"] for sid in SCENES)
-    rate = insts / (sum(kernel_ms.values()) / 1e3)
+    rate = insts / ((step_ms or sum(kernel_ms.values())) / 1e3)
     roof.update({"achieved": round(rate / 1e9, 1), "frac": round(rate / VALU_PEAK, 4),
                  "traffic": round(sum(sc[str(sid)]["hbm_bytes"] for sid in SCENES) / len(SCENES)),
                  "traffic_unit": "HBM bytes per launch (mean over scenes)",
@@ -240,6 +300,28 @@ def cpu_model():
             return next(l.split(":", 1)[1].strip() for l in f if l.startswith("model name"))
     except Exception:
         return platform.processor()
+
+
+def host_cpu_limits():
+    """What bounds the CPU baseline's threads here: the affinity set, the cgroup CPU quota
+    (cpu.max, v2; cfs quota / period, v1) and OMP_NUM_THREADS (16 on the GPU box)."""
+    lim = {"affinity_cores": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None,
+           "os_cpu_count": os.cpu_count(), "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
+           "cgroup_cpu_quota": None}
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            lim["cgroup_cpu_quota"] = "max" if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+                q = int(f.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                per = int(f.read())
+            lim["cgroup_cpu_quota"] = "max" if q < 0 else round(q / per, 2)
+        except (OSError, ValueError):
+            pass
+    return lim
 
 
 def cpu_baseline_reference():
@@ -270,7 +352,7 @@ def cpu_baseline_reference():
                   file=sys.stderr)
             return None
     return {"value": round(len(SCENES) * cw * ch * cs / tot / 1e6, 3), "unit": "Msamples/s",
-            "cores": cores, "kind": "reference",
+            "cores": cores, "kind": "reference", "limits": host_cpu_limits(),
             "sample": f"full frames of scenes {list(SCENES)} at {cw}x{ch}x{cs} by oracle/_ref/refdriver (the "
                       f"reference's own translation units), 12x9 tile pool, per scene the median of {reps} after "
                       f"1 warm-up; cpu: {cpu_model()}"}
@@ -301,7 +383,7 @@ def cpu_baseline(rtm_unused=None):
         times.append(tot)
     med = sorted(times)[reps // 2]
     return {"value": round(len(SCENES) * cw * ch * cs / med / 1e6, 3), "unit": "Msamples/s",
-            "cores": cores, "kind": "port",
+            "cores": cores, "kind": "port", "limits": host_cpu_limits(),
             "sample": f"full frames of scenes {list(SCENES)} at {cw}x{ch}x{cs}, 12x9 tile pool, "
                       f"median of {reps} after 1 warm-up; cpu: {cpu_model()}"}
 
@@ -335,6 +417,19 @@ class GpuWorkload:
 
     def stream_ctx(self):
         return self.torch.cuda.stream(self.stream)
+
+    def mark(self):
+        """A timing event recorded on the launch stream (every render launch of a step runs there)."""
+        e = self.torch.cuda.Event(enable_timing=True)
+        e.record(self.stream)
+        return e
+
+    def span_ms(self, steps):
+        """Device ms per step between the events around the timed region's launches: every render
+        launch of the K steps is inside (plus the heavy-first plan kernel of every 16th frame and the
+        few-us gaps between launches, so it bounds the kernels' mean duration from above)."""
+        a, b = self.span
+        return a.elapsed_time(b) / steps
 
     def render_all(self, p=0):
         """This step's render launch(es) into buffer set p: every scene's frame (or this rank's
@@ -408,6 +503,9 @@ class GpuWorkload:
         if self.batch:
             return {"batch": sum(out.values())}
         return out
+
+    def launches_per_step(self):
+        return (len(SCENES) + self.rtm.MAX_BATCH - 1) // self.rtm.MAX_BATCH if self.batch else len(SCENES)
 
     def close(self):
         for sid, hs, gs, f in self.scenes:
@@ -500,10 +598,13 @@ def run_steps(work, world, rank, steps, warmup, dist=None, graph=False):
     work.sync()
     t0 = time.perf_counter()
     with ctx:
+        span0 = work.mark()            # HIP events on the launch stream around ALL the timed launches
         for _ in range(steps):
             step()
+        span1 = work.mark()
         finish()                       # the last step's frames are assembled inside the timed region
     work.sync()
+    work.span = (span0, span1)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -527,6 +628,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-end-to-end", action="store_true")
     ap.add_argument("--no-moving-camera", action="store_true")
+    ap.add_argument("--no-first-frame", action="store_true")
     ap.add_argument("--graph", action="store_true",
                     help="replay the step's render launch(es) from a hipGraph captured after the warm-up")
     ap.add_argument("--batch", choices=["auto", "on", "off"], default="auto",
@@ -567,6 +669,7 @@ def main():
     elapsed = run_steps(work, world, rank, args.steps, args.warmup, dist if world > 1 else None,
                         graph=args.graph)
     kernel_ms = work.kernel_ms(args.steps)
+    step_ms = work.span_ms(args.steps)
     samples_per_step = len(SCENES) * W * H * SPP          # all ranks together
     value = samples_per_step * args.steps / elapsed / 1e6
 
@@ -574,8 +677,11 @@ def main():
         # algorithmic bytes per launch (this rank's launch covers 1/world of the frame)
         ab = {sid: algorithmic_bytes(gs, f) for sid, hs, gs, f in work.scenes}
         launch_bytes = {sid: ab[sid]["bytes_per_sample"] * W * H * SPP / world for sid in SCENES}
-        achieved = sum(launch_bytes.values()) / (sum(kernel_ms.values()) / 1e3)
-        roof = valu_roofline(rtm, kernel_ms, args, world, achieved)
+        achieved = sum(launch_bytes.values()) / (step_ms / 1e3)
+        roof = valu_roofline(rtm, kernel_ms, args, world, achieved, step_ms, work)
+        roof["duration"] = {"ms_per_step": round(step_ms, 4), "launches": args.steps * work.launches_per_step(),
+                            "source": "HIP events on the launch stream around all the timed steps' render launches "
+                                      "(gaps and the every-16th-frame plan kernel included: a conservative duration)"}
         per_scene = {}
         for sid in SCENES:
             e = {"bytes_per_sample": round(ab[sid]["bytes_per_sample"], 1), "survey_bytes_per_sample": SURVEY_B[sid],
@@ -607,7 +713,8 @@ def main():
                                   if work.batch else "one launch per frame"),
                        "camera": "static: each scene's own camera every step, so the per-origin "
                                  "triangle records (k_origin_pre) are computed once; see moving_camera"},
-            "kernel_ms_per_step": round(sum(kernel_ms.values()), 4),
+            "kernel_ms_per_step": round(step_ms, 4),
+            "kernel_ms_sampled": {str(k): round(v, 4) for k, v in kernel_ms.items()},
             "per_scene": per_scene,
             "roofline": roof,
             "cpu_baseline": None,
@@ -620,6 +727,8 @@ def main():
             out["end_to_end"] = end_to_end(rtm, work)
         if world == 1 and not args.graph and not args.no_moving_camera:
             out["moving_camera"] = moving_camera(work, args.steps, min(args.warmup, 20), elapsed / args.steps * 1e3)
+        if world == 1 and args.workload == "bench" and not args.no_first_frame:
+            out["first_frame_ms"] = first_frame(rtm, torch)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline()
         print(json.dumps(out), flush=True)

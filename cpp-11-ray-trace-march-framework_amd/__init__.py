@@ -45,7 +45,6 @@ RT_KERNEL_FLAG_LDS_CELLS = 0x80
 RT_KERNEL_FLAG_WIDE_HEAVY = 0x200
 RT_KERNEL_FLAG_EXHAUSTIVE = 0x8000
 RT_KERNEL_FLAG_WAVE_CLOCK = 0x400000
-RT_KERNEL_FLAG_COOP_PAIRS = 0x1000
 RT_KERNEL_BUDGET_SHIFT = 24              # COMPACT: idle lanes before a refill (1..64)
 RT_KERNEL_BUDGET_MASK = 0x7F000000
 RT_KERNEL_COMPACT_REFILL_SHIFT = RT_KERNEL_BUDGET_SHIFT
@@ -63,6 +62,7 @@ TRACER_SYMBOLS = [
     "rt_sample_table", "rt_last_error", "rt_abi_version", "rt_grid_build", "rt_grid_free",
     "rt_scene_create_from_mesh", "rt_kernel_times", "rt_render_frame_host", "rt_frame_host_wait", "rt_host_alloc",
     "rt_host_free", "rt_render_hits_device", "rt_scene_info_get", "rt_build_hash", "rt_render_batch_device",
+    "rt_render_records_device",
 ]
 MAX_BATCH = 4                            # frames per rt_render_batch_device launch
 HOST_SYMBOLS = [
@@ -127,7 +127,8 @@ class SceneInfo(ctypes.Structure):
                 ("max_cell_refs", c_u32), ("hf_floor", c_u32), ("hf_min_blocks", c_u32), ("wh_floor", c_u32),
                 ("wh_alpha16", c_u32), ("wh_auto_refs", c_u32), ("wh_fused", c_u32), ("hf_contexts", c_u32),
                 ("hf_evictions", ctypes.c_uint64), ("device_bytes", ctypes.c_uint64),
-                ("box_words", c_u32), ("wh_alpha16_n2", c_u32)]
+                ("box_words", c_u32), ("wh_alpha16_n2", c_u32), ("pad0", c_u32),
+                ("batch_launches", ctypes.c_uint64), ("batch_fallbacks", ctypes.c_uint64)]
 
 
 SAMPLE_REC_DTYPE = np.dtype([("hit", "<u4"), ("tri", "<u4"), ("voxel", "<u4"), ("steps", "<u4"),
@@ -175,6 +176,9 @@ def tracer_lib():
             L.rt_scene_info_get.argtypes = [vp, ctypes.POINTER(SceneInfo)]
             L.rt_build_hash.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
             L.rt_render_batch_device.argtypes = [vp, ctypes.POINTER(Frame), c_u32, c_u32, c_u32, vp, vp, vp]
+        if hasattr(L, "rt_render_records_device"):   # ABI 8
+            L.rt_render_records_device.argtypes = [vp, ctypes.POINTER(Frame), c_u32, c_u32, c_u32, vp,
+                                                   ctypes.POINTER(Tile), vp, vp]
         L.rt_unshard_device.argtypes = [c_u32, c_u32, c_u32, vp, vp, vp]
         L.rt_last_kernel_ms.argtypes = [vp, ctypes.POINTER(c_f32)]
         L.rt_trace_samples.argtypes = [vp, ctypes.POINTER(Frame), c_u32, c_u32, c_u32, c_u32, vp]
@@ -640,6 +644,22 @@ def render_batch_device(scenes, frames, d_outs, rank=0, nranks=1, d_hits=None, s
     L = tracer_lib()
     _check(L.rt_render_batch_device(sp, fr, n, rank, nranks, outs, hits, ctypes.c_void_p(stream)), L,
            "rt_render_batch_device")
+
+
+def render_records_device(scenes, frames, d_outs, rects, d_recs, rank=0, nranks=1, stream=0):
+    """rt_render_records_device: the benchmarked launch path (one frame: the frame / shard entry
+    points; several: the batched launch) plus per-sample records of the samples inside rects[i] =
+    (x0, y0, x1, y1) into device buffer d_recs[i] (SAMPLE_REC_DTYPE, order (y, x, sample))."""
+    n = len(scenes)
+    assert len(frames) == n and len(d_outs) == n and len(rects) == n and len(d_recs) == n
+    sp = (ctypes.c_void_p * n)(*[g._h.value for g in scenes])
+    fr = (Frame * n)(*frames)
+    outs = (ctypes.c_void_p * n)(*d_outs)
+    rc = (Tile * n)(*[Tile(*r) for r in rects])
+    recs = (ctypes.c_void_p * n)(*d_recs)
+    L = tracer_lib()
+    _check(L.rt_render_records_device(sp, fr, n, rank, nranks, outs, rc, recs, ctypes.c_void_p(stream)), L,
+           "rt_render_records_device")
 
 
 def shard_elems(width, height, nranks):

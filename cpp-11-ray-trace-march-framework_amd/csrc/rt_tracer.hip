@@ -78,7 +78,6 @@ constexpr int kVarLdsCells = 262144;        // RT_KERNEL_FLAG_LDS_CELLS: long un
 constexpr int kVarWideHeavy = 524288;       // RT_KERNEL_FLAG_WIDE_HEAVY: heavy items traced wide at the start
 constexpr int kVarWideFused = 1048576;      // batch kernel: the wide section's blocks lead the same grid
 constexpr int kVarWideG4 = 2097152;         // the wide section at 4 lanes per sample (spp 8-16; else 16)
-constexpr int kVarCoop = 4194304;           // RT_KERNEL_FLAG_COOP_PAIRS: divergent cell lists as (ray, record) pairs
 // AUTO's traversal: every feature above that is exact for every scene ...
 constexpr int kVarAutoCore = kVarWaveGate | kVarDistSkip | kVarOriginPre | kVarXcdBands | kVarUniform;
 // ... plus the two that need a scene property (rt_scene::rcp_safe, rt_scene::pack_ok)
@@ -346,8 +345,6 @@ __device__ __forceinline__ void lane_list(const KParams& P, rtd::f2v ra, rtd::f2
 }
 
 // Tests a cell's list [kb, ke) in order (grid.cpp:243-267); true when it produced a hit.
-// kVarCoop: a list the testing lanes do not share is not tested here -- *defer is set and the
-// caller's wave-cooperative pass (coop_cells) tests it.
 // grid.cpp:258-260 accepts cur_t when cur_t < t && cur_t < next_crossing_t[step_axis].  t is
 // FLT_MAX on entry (a hit ends the walk, grid.cpp:270-271) and neither bound is ever NaN, so the
 // two compares are one against tb = min(t, nct_ax), which every accepted hit lowers to its t:
@@ -355,7 +352,7 @@ __device__ __forceinline__ void lane_list(const KParams& P, rtd::f2v ra, rtd::f2
 template <bool STATS, int TRI, int VAR>
 __device__ __forceinline__ bool test_cell(const KParams& P, float ox, float oy, float oz, float dx, float dy,
                                           float dz, uint32_t kb, uint32_t ke, float nct_ax, float& t,
-                                          float& u, float& v, uint32_t& tri, uint32_t& tests, bool *defer = nullptr)
+                                          float& u, float& v, uint32_t& tri, uint32_t& tests)
 {
     constexpr bool PRE = (VAR & kVarOriginPre) != 0 && TRI == RT_TRI_MOLLER_TRUMBORE;
     constexpr bool F = (VAR & kVarFastRcp) != 0;
@@ -506,16 +503,7 @@ __device__ __forceinline__ bool test_cell(const KParams& P, float ox, float oy, 
     }
     if constexpr (PRE)
     {
-        if (!uniform_done)
-        {
-            if constexpr ((VAR & kVarCoop) != 0)
-            {
-                *defer = true;
-                return false;
-            }
-            else
-                lane_list<STATS, VAR>(P, ra, rc, kb, ke, tb, u, v, tri, tests);
-        }
+        if (!uniform_done) lane_list<STATS, VAR>(P, ra, rc, kb, ke, tb, u, v, tri, tests);
     }
     else
     for (uint32_t k = kb; k < ke; k++)
@@ -546,149 +534,6 @@ __device__ __forceinline__ bool test_cell(const KParams& P, float ox, float oy, 
     }
     t = tb < tb0 ? tb : t;
     return t != rtd::kFltMax;                                  // grid.cpp:270-271
-}
-
-// kVarCoop: the wave-cooperative pass over the cell lists the lanes do NOT share (SURVEY §7 step 4,
-// the north_star's ballot/prefix compaction of the traversal): at such a DDA step the per-lane loop
-// runs max(L) iterations while the wave holds sum(L) useful (ray, record) pairs -- killeroo 1080p x 4:
-// 1.04 M per-lane iterations at 64 % lane utilisation (tools/wave_sim.cpp).  Here every lane still
-// walking (owners and lanes in empty cells alike) takes a contiguous run of ceil(T / n) of the T
-// pairs, in (owner, list position) order:
-//  * T, each owner's first pair S (exclusive prefix of L in lane order) and max(L) come from
-//    bit-plane ballots (L < 2^11: the packed cell word's count);
-//  * owners publish {S, end, kb - S, tb0, ray direction} in the wave's LDS slots by owner ordinal;
-//    a helper finds the owner of its first pair by binary search over the starts and moves to the
-//    next owner where its run crosses an end;
-//  * a helper keeps the lexicographic minimum of (t, list position) over its accepted pairs -- a
-//    hit with t < tb0 = min(t, nct_ax), exactly grid.cpp:258-260's condition -- and merges it into
-//    the owner's slot with one 64-bit LDS atomic min per owner it served.  t >= 0 (+0 for -0:
-//    the reference's '<' does not tell them apart), so its bits order like the floats, and the
-//    minimum is the reference's first minimum in list order (strict '<', H8);
-//  * each owner re-tests its winning record with its own ray for the exact t, u, v.
-// Not beneficial (ceil(T / n) + kCoopMargin >= max(L)): the owners run lane_list as before.
-constexpr uint32_t kCoopMargin = 6;     // setup cost in record-test iterations
-
-struct CoopOwner { uint32_t end, kbase; float tb0, dx, dy, dz; };
-
-template <int VAR>
-__device__ __forceinline__ bool coop_cells(const KParams& P, float dx, float dy, float dz, bool own, uint32_t kb,
-                                           uint32_t ke, float nct_ax, float& t, float& u, float& v, uint32_t& tri)
-{
-    constexpr bool F = (VAR & kVarFastRcp) != 0;
-    const uint32_t L = own ? ke - kb : 0u;
-    const uint64_t act = __ballot(1);
-    const uint32_t nact = uint32_t(__popcll(act));
-    auto below = [](uint64_t m) {                 // set bits of m in the lanes below this one
-        return __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
-    };
-    uint32_t S = 0u, T = 0u, top = 0u;
-    for (uint32_t b = 0; b < 11u; b++)
-    {
-        const uint64_t m = __ballot((L >> b) & 1u);
-        S += below(m) << b;
-        T += uint32_t(__popcll(m)) << b;
-        top = m ? b : top;
-    }
-    uint32_t M = 0u;                              // max(L): the highest bit planes in turn
-    bool cand = own;
-    for (int b = int(top); b >= 0; b--)
-    {
-        const bool has = cand && ((L >> b) & 1u);
-        if (__ballot(has))
-        {
-            M |= 1u << b;
-            cand = has;
-        }
-    }
-    const rtd::f2v ra = {dx, dy}, rc = {dy, dz};
-    const float tb0 = t < nct_ax ? t : nct_ax;
-    const uint32_t R = (T + nact - 1u) / nact;    // pairs per helper
-    if (R + kCoopMargin >= M)
-    {
-        float tb = tb0;
-        uint32_t tests = 0u;
-        if (own) lane_list<false, VAR>(P, ra, rc, kb, ke, tb, u, v, tri, tests);
-        if (tb < tb0) t = tb;
-        return own && t != rtd::kFltMax;
-    }
-    __shared__ uint32_t s_start[kWavesPerWG][64];
-    __shared__ CoopOwner s_own[kWavesPerWG][64];
-    __shared__ unsigned long long s_best[kWavesPerWG][64];
-    const uint32_t w = threadIdx.x >> 6;
-    const uint64_t om = __ballot(own);
-    const uint32_t nown = uint32_t(__popcll(om));
-    const uint32_t oo = below(om);                // owner ordinal (starts ascend with it)
-    if (own)
-    {
-        s_start[w][oo] = S;
-        s_own[w][oo] = CoopOwner{S + L, kb - S, tb0, dx, dy, dz};
-        s_best[w][oo] = ~0ull;
-    }
-    wave_lds_sync();
-    uint32_t p = below(act) * R;
-    const uint32_t pend = min(p + R, T);
-    uint32_t o = 0u;                              // the last owner whose start is <= p
-    for (uint32_t st = 32u; st; st >>= 1)
-        if (o + st < nown && s_start[w][o + st] <= p) o += st;
-    CoopOwner c = s_own[w][o];
-    unsigned long long best = ~0ull;
-    for (uint32_t j = 0; j < R; j++)
-    {
-        if (p < pend)
-        {
-            const uint32_t k = c.kbase + p;
-            const float4 *rp = P.frefs + size_t(k) * 4u;
-            const float4 r0 = rp[0], r1 = rp[1], r2 = rp[2];
-            const rtd::f2v pa = {c.dx, c.dy}, pc = {c.dy, c.dz};
-            float inv, pu;
-            const bool ok1 = rtd::mt_rec_first<F>(pa, pc, rtd::f2v{r0.x, r0.y}, rtd::f2v{r0.z, r0.w},
-                                                  rtd::f2v{r1.x, r1.y}, rtd::f2v{r1.z, r1.w}, rtd::f2v{r2.x, r2.y},
-                                                  inv, pu);
-            if (__any(ok1))
-            {
-                const float2 r3 = *reinterpret_cast<const float2 *>(rp + 3);
-                float pv, pt;
-                const bool h = ok1 & rtd::mt_rec_second(pa, pc, rtd::f2v{r2.z, r2.w}, r3.x, r3.y, inv, pu, pv, pt);
-                // (t, pair index): within one owner the pair index orders like the list position
-                const unsigned long long key = (uint64_t(__float_as_uint(pt + 0.0f)) << 32) | uint64_t(p);
-                best = (h & (pt < c.tb0) & (key < best)) ? key : best;
-            }
-            p++;
-            if (p == c.end && p < pend)
-            {
-                if (best != ~0ull) atomicMin(&s_best[w][o], best);
-                best = ~0ull;
-                o++;
-                c = s_own[w][o];
-            }
-        }
-    }
-    if (best != ~0ull) atomicMin(&s_best[w][o], best);
-    wave_lds_sync();
-    bool hit = false;
-    if (own)
-    {
-        const unsigned long long b = s_best[w][oo];
-        if (b != ~0ull)
-        {
-            // the winner re-tested with this lane's own ray: the values the per-lane loop keeps
-            const uint32_t k = uint32_t(b) - S + kb;
-            const float4 *rp = P.frefs + size_t(k) * 4u;
-            const float4 r0 = rp[0], r1 = rp[1], r2 = rp[2];
-            const float2 r3 = *reinterpret_cast<const float2 *>(rp + 3);
-            float inv, pu, pv, pt;
-            rtd::mt_rec_first<F>(ra, rc, rtd::f2v{r0.x, r0.y}, rtd::f2v{r0.z, r0.w}, rtd::f2v{r1.x, r1.y},
-                                 rtd::f2v{r1.z, r1.w}, rtd::f2v{r2.x, r2.y}, inv, pu);
-            rtd::mt_rec_second(ra, rc, rtd::f2v{r2.z, r2.w}, r3.x, r3.y, inv, pu, pv, pt);
-            t = pt;
-            u = pu;
-            v = pv;
-            tri = k;
-            hit = true;
-        }
-    }
-    wave_lds_sync();                              // the slots are reused by the next pass
-    return hit;
 }
 
 // One DDA advance over plain local variables (grid.cpp:236-239 + 274-277), exact because
@@ -876,6 +721,68 @@ __device__ __forceinline__ int box_offset(const KParams& P, float dx, float dy, 
     return int((o * 3u + m) * P.box_stride);
 }
 
+// Records of the product walks (rt_render_records_device): the GridIdx of the last cell walked on a
+// miss, from the state the walk ends in.  The exit step along axis a borrowed into the guard bit of
+// a's packed remaining-cell count -- the LOWEST set guard, since a borrow only carries upward -- and
+// `cell` already includes that step.  The walk itself is unchanged: this runs after it, and only a
+// record store reads the result.
+constexpr uint32_t kVoxelUnknown = 0xFFFFFFFEu;     // not recoverable from this walk's end state
+__device__ __forceinline__ uint32_t exit_voxel(int remp, int cell, int cs0, int cs1, int cs2)
+{
+    const uint32_t g = uint32_t(remp) & uint32_t(kRemGuards);
+    return uint32_t(cell - ((g & (1u << 10)) ? cs0 : ((g & (1u << 21)) ? cs1 : cs2)));
+}
+
+// The cell whose CSR list holds reference k: off[c] <= k < off[c + 1] (records of a hit: the walk
+// accepts a hit only inside the cell being tested, grid.cpp:258-271, so this is that cell).
+__device__ __forceinline__ uint32_t cell_of_ref(const KParams& P, uint32_t k)
+{
+    uint32_t lo = 0u, hi = uint32_t(P.dim[0]) * uint32_t(P.dim[1]) * uint32_t(P.dim[2]);   // off[hi] = R > k
+    while (hi - lo > 1u)
+    {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (P.off[mid] <= k) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// The colour words of a record (store_record; the wide section stores them after its resolve).
+__device__ __forceinline__ void store_record_colour(const KParams& Q, uint32_t px, uint32_t py, uint32_t s, float r,
+                                                    float g, float b)
+{
+    const uint32_t rx = px - Q.rec_x0, ry = py - Q.rec_y0;
+    if (rx >= Q.rec_w || ry >= Q.rec_h) return;
+    volatile uint32_t *o = reinterpret_cast<volatile uint32_t *>(Q.recs + (size_t(ry) * Q.rec_w + rx) * Q.spp + s);
+    o[8] = __float_as_uint(r);
+    o[9] = __float_as_uint(g);
+    o[10] = __float_as_uint(b);
+    o[11] = 0u;
+}
+
+// One per-sample record (rt_sample_rec) of a product kernel, for samples inside the requested
+// rectangle: rec[((y - y0) * w + (x - x0)) * spp + s].  DDA steps and tests are not counted by the
+// product walks (0xFFFFFFFF; k_trace_records pins them).
+__device__ __forceinline__ void store_record(const KParams& Q, uint32_t px, uint32_t py, uint32_t s, bool hit,
+                                             uint32_t tri, uint32_t voxel, float t, float u, float v, float r,
+                                             float g, float b)
+{
+    const uint32_t rx = px - Q.rec_x0, ry = py - Q.rec_y0;
+    if (rx >= Q.rec_w || ry >= Q.rec_h) return;
+    // word by word (volatile: no dwordx4 merging, which would need 12 consecutive VGPRs here and
+    // raise the kernels' register count)
+    volatile uint32_t *o = reinterpret_cast<volatile uint32_t *>(Q.recs + (size_t(ry) * Q.rec_w + rx) * Q.spp + s);
+    o[0] = hit ? 1u : 0u;
+    o[1] = hit ? tri : rtd::kNoTri;
+    o[2] = voxel;
+    o[3] = 0xFFFFFFFFu;
+    o[4] = 0xFFFFFFFFu;
+    o[5] = hit ? __float_as_uint(t) : 0u;
+    o[6] = hit ? __float_as_uint(u) : 0u;
+    o[7] = hit ? __float_as_uint(v) : 0u;
+    if (r == r) store_record_colour(Q, px, py, s, r, g, b);
+}
+
 // grid.cpp:159-281 Grid::Intersect (NEW_GRID_TRAVERSAL), axis arrays unrolled into scalars
 // so nothing is runtime-indexed (no scratch).  Counters are compiled in only for records.
 template <bool STATS, int TRI, int VAR>
@@ -922,15 +829,7 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, float ox, float
             }
             RT_DDA_ADVANCE_BOX(nct_ax, more);
             bool hit = false;
-            bool defer = false;
-            if (kb < ke)
-                hit = test_cell<STATS, TRI, VAR>(P, ox, oy, oz, dx, dy, dz, kb, ke, nct_ax, t, u, v, tri, tests, &defer);
-            if constexpr ((VAR & kVarCoop) != 0)
-                if (__any(defer))
-                {
-                    const bool h = coop_cells<VAR>(P, dx, dy, dz, defer, kb, ke, nct_ax, t, u, v, tri);
-                    hit = defer ? h : hit;
-                }
+            if (kb < ke) hit = test_cell<STATS, TRI, VAR>(P, ox, oy, oz, dx, dy, dz, kb, ke, nct_ax, t, u, v, tri, tests);
             if constexpr (!STATS)
             {
                 // Wave-uniform runs while every active lane is inside its box (the boxes are clipped
@@ -966,6 +865,9 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, float ox, float
             }
             if (hit | !more) break;
         }
+        // records only: the exit cell in the ray's box-word copy (trace_sample removes the copy's
+        // offset, so nothing extra is live across the walk)
+        if constexpr (!STATS) voxel = exit_voxel(remp, cell, cs0, cs1, cs2);
         return t != rtd::kFltMax;                            // t is only set by a hit
     }
 #endif
@@ -1005,15 +907,7 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, float ox, float
             // below), and the result read from t after the loop: the walk's loop-carried state
             // stays in VGPRs instead of per-exit lane masks (SALU per wave, PMC-measured)
             bool hit = false;
-            bool defer = false;
-            if (kb < ke)
-                hit = test_cell<STATS, TRI, VAR>(P, ox, oy, oz, dx, dy, dz, kb, ke, nct_ax, t, u, v, tri, tests, &defer);
-            if constexpr ((VAR & kVarCoop) != 0)
-                if (__any(defer))       // every lane still walking helps (converged here)
-                {
-                    const bool h = coop_cells<VAR>(P, dx, dy, dz, defer, kb, ke, nct_ax, t, u, v, tri);
-                    hit = defer ? h : hit;
-                }
+            if (kb < ke) hit = test_cell<STATS, TRI, VAR>(P, ox, oy, oz, dx, dy, dz, kb, ke, nct_ax, t, u, v, tri, tests);
             bool done = hit | !more;
             if constexpr ((VAR & kVarSkipRun) != 0 && (VAR & kVarPackedRem) != 0 && !STATS)
             {
@@ -1080,6 +974,13 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, float ox, float
             }
             if (done) break;
         }
+        // a lane leaving the grid inside a block of bare steps stepped on: its last cell is lost
+        if constexpr (!STATS)
+        {
+            if constexpr ((VAR & kVarSkipRun) != 0) voxel = kVoxelUnknown;
+            else if constexpr ((VAR & kVarPackedRem) != 0) voxel = exit_voxel(remp, cell - coff, cs0, cs1, cs2);
+            else voxel = uint32_t(cell - coff - (rem0 < 0 ? cs0 : (rem1 < 0 ? cs1 : cs2)));   // rem_a went to -1
+        }
         return t != rtd::kFltMax;                            // t is only set by a hit
     }
 
@@ -1098,6 +999,7 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, float ox, float
             return true;
         if (!more) break;
     }
+    if constexpr (!STATS) voxel = uint32_t(cell - (rem0 < 0 ? cs0 : (rem1 < 0 ? cs1 : cs2)));   // records only
     return false;
 }
 
@@ -1240,12 +1142,16 @@ __device__ __forceinline__ bool ray_march(const KParams& P, float ox, float oy, 
     return false;
 }
 
+// What a product walk leaves for rt_render_records_device: hit, t, u, v, the CSR reference of the hit
+// and the walk's end cell (raw: a box-run miss's cell still in its box-word copy).
+struct SampleOut { bool hit; float t, u, v; uint32_t voxel, csr; };
+
 // renderer.cpp:88-122: one sample -> its colour contribution; hit_tri = the hit triangle
 // (Grid::Intersect's tri_idx, renderer.cpp:105) or kNoTri
 template <bool STATS, int TRI, int VAR>
 __device__ __forceinline__ void trace_sample(const KParams& P, uint32_t px, uint32_t py, uint32_t s, float& cr,
                                              float& cg, float& cb, uint32_t& hit_tri, rt_sample_rec *rec,
-                                             uint32_t off = 0u)
+                                             uint32_t off = 0u, SampleOut *so = nullptr)
 {
     float dx, dy, dz;
     rtd::dir_from_xy(P.m, P.ndcx[px * P.spp + s], P.ndcy[py * P.spp + s], dx, dy, dz);    // camera.h:8-47
@@ -1261,9 +1167,18 @@ __device__ __forceinline__ void trace_sample(const KParams& P, uint32_t px, uint
         hit = grid_intersect<STATS, TRI, VAR>(P, P.org[0], P.org[1], P.org[2], dx, dy, dz, t, u, v, tri, voxel,
                                               steps, tests);
     const KParams& Q = late_params(P, off);
-    if constexpr ((VAR & (kVarMarch | kVarBrute)) == 0)
-        if ((VAR & kVarOriginPre) && TRI == RT_TRI_MOLLER_TRUMBORE && hit)
-            tri = __float_as_uint(Q.refs[3 * size_t(tri) + 2].y);     // CSR reference -> triangle id
+    constexpr bool CSR_TRI = (VAR & (kVarMarch | kVarBrute)) == 0 && (VAR & kVarOriginPre) && TRI == RT_TRI_MOLLER_TRUMBORE;
+    if (so)                     // the walk's outcome for a record (process_item stores it)
+    {
+        so->hit = hit;
+        so->t = t;
+        so->u = u;
+        so->v = v;
+        so->voxel = voxel;
+        so->csr = CSR_TRI ? tri : rtd::kNoTri;
+    }
+    if constexpr (CSR_TRI)
+        if (hit) tri = __float_as_uint(Q.refs[3 * size_t(tri) + 2].y);     // CSR reference -> triangle id
     if constexpr ((VAR & kVarMarch) != 0)
     {
         // The reference's RayMarch leaves u, v, tri_idx unset (renderer.cpp:103), so the
@@ -1380,6 +1295,25 @@ __device__ __forceinline__ ItemCoord item_coord(const KParams& P, uint32_t item,
     return tile_slot_coord(P, P.tile_order ? P.tile_order[kseq] : kseq, slot);   // local tile k
 }
 
+// The record of one sample of AUTO's walk (rt_render_records_device): the accepted cell of a hit from
+// its CSR reference; a box-run miss's end cell moved out of its box-word copy (the ray's direction
+// recomputed here, so neither the pixel nor the copy's offset stays live across the walk).
+template <int VAR>
+__device__ __forceinline__ void process_record(const KParams& Q, const ItemCoord& ic, const SampleOut& so,
+                                               uint32_t tri, float cr, float cg, float cb)
+{
+    uint32_t vox = so.voxel;
+    if (so.hit)
+        vox = so.csr != rtd::kNoTri ? cell_of_ref(Q, so.csr) : kVoxelUnknown;
+    else if (vox < kVoxelUnknown && RT_BOX_RUN && (VAR & kVarSkipRun) && (VAR & kVarPackedRem))
+    {
+        float dx, dy, dz;
+        rtd::dir_from_xy(Q.m, Q.ndcx[ic.x * Q.spp + ic.s], Q.ndcy[ic.y * Q.spp + ic.s], dx, dy, dz);
+        vox -= uint32_t(box_offset(Q, dx, dy, dz));
+    }
+    store_record(Q, ic.x, ic.y, ic.s, so.hit, tri, vox, so.t, so.u, so.v, cr, cg, cb);
+}
+
 // One wave-sized work item = 64 consecutive sample slots of a 16x16 tile in Morton order
 // (a 2^k x 2^k pixel block x spp samples).  Traces the lane's sample, sums the pixel's
 // samples across its adjacent lanes in sample order (renderer.cpp:87-122, hazard H10) and
@@ -1391,16 +1325,19 @@ __device__ __forceinline__ void process_item(const KParams& P, uint32_t item, ui
     const uint32_t lane = threadIdx.x & 63u;
     float cr = 0.0f, cg = 0.0f, cb = 0.0f;
     uint32_t hit_tri = rtd::kNoTri;
+    SampleOut so{false, 0.0f, 0.0f, 0.0f, rtd::kNoTri, rtd::kNoTri};
     {
         const ItemCoord ic = item_coord(P, item, lane);
         if (ic.valid)
-            trace_sample<false, TRI, VAR>(P, ic.x, ic.y, ic.s, cr, cg, cb, hit_tri, nullptr, off);
+            trace_sample<false, TRI, VAR>(P, ic.x, ic.y, ic.s, cr, cg, cb, hit_tri, nullptr, off, &so);
     }
     const KParams& Q = late_params(P, off);
     const ItemCoord ic = item_coord(Q, item, lane);
     // rt_render_hits_device only: the sample's hit triangle, after the walk (a scalar test of a
     // kernel parameter; the walk above is the same code whatever the pointer holds)
     if (Q.hits && ic.valid) Q.hits[(size_t(ic.y) * Q.W + ic.x) * Q.spp + ic.s] = hit_tri;
+    // rt_render_records_device only, likewise: the sample's record (process_record)
+    if (Q.recs && ic.valid) process_record<VAR>(Q, ic, so, hit_tri, cr, cg, cb);
     float sr = 0.0f, sg = 0.0f, sb = 0.0f;
     if (Q.spp == 4u)
     {
@@ -1656,7 +1593,7 @@ __device__ __forceinline__ bool block_of_launch(const KParams& P, uint32_t& b, u
 // rt_render_hits_device).
 template <int VAR, int G>
 __device__ __forceinline__ void wide_trace(const KParams& P, uint32_t k, uint32_t slot, uint32_t sub, float& cr,
-                                           float& cg, float& cb)
+                                           float& cg, float& cb, uint32_t& hit_tri)
 {
     static_assert((VAR & kVarOriginPre) && (VAR & kVarDistSkip) && (VAR & kVarPackedRem), "AUTO layout");
     const float ox = P.org[0], oy = P.org[1], oz = P.org[2];
@@ -1738,11 +1675,38 @@ __device__ __forceinline__ void wide_trace(const KParams& P, uint32_t k, uint32_
                             v = bv;
                             tri = bk;
                             hit = true;
+                            // rt_render_records_device only: the walk's words of the record, where
+                            // the walk ends (nothing of it stays live past the loop; the pixel
+                            // again from k and slot); the colour words after the resolve
+                            if (P.recs && sub == 0u)
+                            {
+                                const ItemCoord rc = tile_slot_coord(P, k, slot);
+                                store_record(P, rc.x, rc.y, rc.s, true, __float_as_uint(P.refs[3 * size_t(bk) + 2].y),
+                                             cell_of_ref(P, bk), bt, bu, bv, __builtin_nanf(""), 0.0f, 0.0f);
+                            }
                             break;
                         }
                     }
-                    if (!more) break;
+                    if (!more)
+                    {
+                        // records of a miss: one cell per iteration here, so the exit step is the
+                        // last one taken
+                        if (P.recs && sub == 0u)
+                        {
+                            const ItemCoord rc = tile_slot_coord(P, k, slot);
+                            store_record(P, rc.x, rc.y, rc.s, false, 0u,
+                                         exit_voxel(remp, cell, cs0, cs1, cs2) - uint32_t(oct_offset(P, dx, dy, dz)),
+                                         0.0f, 0.0f, 0.0f, __builtin_nanf(""), 0.0f, 0.0f);
+                        }
+                        break;
+                    }
                 }
+            }
+            else if (P.recs && sub == 0u)      // records of a ray that misses the grid
+            {
+                const ItemCoord rc = tile_slot_coord(P, k, slot);
+                store_record(P, rc.x, rc.y, rc.s, false, 0u, rtd::kNoTri, 0.0f, 0.0f, 0.0f, __builtin_nanf(""), 0.0f,
+                             0.0f);
             }
             const KParams& Q = P;
             if (hit)
@@ -1753,8 +1717,7 @@ __device__ __forceinline__ void wide_trace(const KParams& P, uint32_t k, uint32_
             }
             else
                 cr = cg = cb = float(ic.y) / float(Q.H);                   // renderer.cpp:121
-            // rt_render_hits_device only (a scalar test of a kernel parameter)
-            if (Q.hits && sub == 0u) Q.hits[(size_t(ic.y) * Q.W + ic.x) * Q.spp + ic.s] = hit ? tri : rtd::kNoTri;
+            hit_tri = hit ? tri : rtd::kNoTri;
         }
     }
 }
@@ -1766,9 +1729,13 @@ __device__ __forceinline__ void wide_samples(const KParams& P, uint32_t k, uint3
     const uint32_t lane = threadIdx.x & 63u, sub = lane & uint32_t(G - 1), grp = lane / uint32_t(G);
     const uint32_t slot = slot0 + grp;
     float cr, cg, cb;
-    wide_trace<VAR, G>(P, k, slot, sub, cr, cg, cb);
+    uint32_t hit_tri = rtd::kNoTri;
+    wide_trace<VAR, G>(P, k, slot, sub, cr, cg, cb, hit_tri);
     // the pixel's samples are the groups grp0 .. grp0 + spp - 1 of this wave: sum in sample order
     const ItemCoord ic = tile_slot_coord(P, k, slot);
+    // rt_render_hits_device / rt_render_records_device only (scalar tests of kernel parameters)
+    if (P.hits && sub == 0u && ic.valid) P.hits[(size_t(ic.y) * P.W + ic.x) * P.spp + ic.s] = hit_tri;
+    if (P.recs && sub == 0u && ic.valid) store_record_colour(P, ic.x, ic.y, ic.s, cr, cg, cb);
     const uint32_t grp0 = grp & ~(P.spp - 1u);
     float sr = 0.0f, sg = 0.0f, sb = 0.0f;
     for (uint32_t j = 0; j < P.spp; j++)
@@ -1786,6 +1753,20 @@ __device__ __forceinline__ void wide_samples(const KParams& P, uint32_t k, uint3
     }
 }
 
+// kVarWaveClock: the four words of one wave's record (rt_debug_wave_clocks): s_memtime at its start and
+// end (per clock domain: durations), and the XCD it ran on (bits 32-35 of word 2) with the low 28 bits
+// of the device-wide 100 MHz s_memrealtime at its start (word 2, bits 36-63) and end (word 3, bits
+// 32-59): launch timelines use the real-time clock.  c0 / c1: the words' low 32 bits.
+__device__ __forceinline__ void store_wave_clock(uint64_t *clk, uint32_t idx, uint64_t t0, uint64_t t1, uint64_t r0,
+                                                 uint64_t r1, uint32_t c0, uint32_t c1)
+{
+    clk[4 * size_t(idx)] = t0;
+    clk[4 * size_t(idx) + 1] = t1;
+    clk[4 * size_t(idx) + 2] = c0 | (uint64_t(__builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u) << 32) |
+                               ((r0 & 0xFFFFFFFull) << 36);
+    clk[4 * size_t(idx) + 3] = c1 | ((r1 & 0xFFFFFFFull) << 32);
+}
+
 // kVarWideHeavy: the launch's wide section.  Its waves take the current plan's heavy work items
 // in list order, wh_g waves per item (each 64 / wh_g of the item's sample slots, wh_g lanes per
 // sample): persistent over the list, so a section smaller than the list (the host sizes it from
@@ -1794,7 +1775,7 @@ __device__ __forceinline__ void wide_samples(const KParams& P, uint32_t k, uint3
 // In a batch (KBatch, BATCH = true) P is p[0] (the batch's list, launch-wide item indices) and each
 // item is rendered with its own frame's parameters.
 // w: this wave's index in the section (4 per 256-lane workgroup, or one per one-wave workgroup).
-template <bool BATCH, uint32_t G>
+template <bool BATCH, uint32_t G, bool CLK = false>
 __device__ __forceinline__ void wide_section(const KParams& P, uint32_t w)
 {
     const uint32_t n = P.hf_ver ? min(P.hf_plan_in->cnt_w, kWhMax) : 0u;
@@ -1817,7 +1798,21 @@ __device__ __forceinline__ void wide_section(const KParams& P, uint32_t w)
         // more SGPRs across it and spilled
         const KParams& Q = late_params(P, off);
         const uint32_t k = Q.tile_order ? Q.tile_order[kseq] : kseq;
-        wide_samples<kVarWide, int(G)>(Q, k, slot0);
+        if constexpr (CLK && BATCH)
+        {
+            // kVarWaveClock: one record per (listed item, wave) of the section, after the batch's lane
+            // items: word 2's low bits = 0x80000000 | list position, word 3's = the launch-wide item
+            const uint64_t r0 = __builtin_amdgcn_s_memrealtime(), t0 = __builtin_amdgcn_s_memtime();
+            wide_samples<kVarWide, int(G)>(Q, k, slot0);
+            const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+            const KBatch& B = late_batch();
+            const KParams& Q0 = late_params(P, uint32_t(offsetof(KBatch, p)));
+            if ((threadIdx.x & 63u) == 0u)
+                store_wave_clock(Q0.wave_clk, B.base[B.nframes] * kWavesPerWG + e, t0, t1, r0, r1, 0x80000000u | e / G,
+                                 __builtin_amdgcn_readfirstlane(Q0.wh_list_in[e / G]));
+        }
+        else
+            wide_samples<kVarWide, int(G)>(Q, k, slot0);
     }
 }
 
@@ -1846,23 +1841,9 @@ __device__ __forceinline__ void lanes_block_wave(const KParams& P, uint32_t bid,
         process_item<TRI, VAR>(P, item);
         const uint64_t t1 = __builtin_amdgcn_s_memtime();
         const uint64_t r1 = __builtin_amdgcn_s_memrealtime();
-        if ((threadIdx.x & 63u) == 0u)
-        {
-            P.wave_clk[4 * size_t(item)] = t0;
-            P.wave_clk[4 * size_t(item) + 1] = t1;
-        }
         wave_lds_sync();
         if ((threadIdx.x & 63u) == 0u)
-        {
-            // high bits: the XCD the wave ran on (bits 32-35 of word 2) and the low 28 bits of
-            // the device-wide 100 MHz s_memrealtime at its start (word 2, bits 36-63) and end
-            // (word 3, bits 32-59): s_memtime counts per clock domain, so launch timelines use
-            // the real-time clock
-            P.wave_clk[4 * size_t(item) + 2] = wave_counters()[0] |
-                                               (uint64_t(__builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u) << 32) |
-                                               ((r0 & 0xFFFFFFFull) << 36);
-            P.wave_clk[4 * size_t(item) + 3] = wave_counters()[1] | ((r1 & 0xFFFFFFFull) << 32);
-        }
+            store_wave_clock(P.wave_clk, item, t0, t1, r0, r1, wave_counters()[0], wave_counters()[1]);
     }
     else
     {
@@ -1939,6 +1920,21 @@ __device__ __forceinline__ void batch_block_wave(const KBatch& B, uint32_t bid, 
     const uint32_t f = batch_frame(B, b);
     const uint32_t off = uint32_t(offsetof(KBatch, p)) + f * uint32_t(sizeof(KParams));
     const uint32_t item = gitem - B.base[f] * kWavesPerWG;
+    if constexpr ((VAR & kVarWaveClock) != 0)
+    {
+        // debug arm: the wave's clocks at its launch-wide item index (rt_debug_wave_clocks; the
+        // batch's heavy-first / wide-section machinery runs as in the product launch)
+        const uint64_t r0 = __builtin_amdgcn_s_memrealtime(), t0 = __builtin_amdgcn_s_memtime();
+        process_item<TRI, VAR>(late_params(B.p[0], off), item, off);
+        const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+        const KParams& Q = late_params(B.p[0], uint32_t(offsetof(KBatch, p)));
+        if ((threadIdx.x & 63u) == 0u)
+        {
+            store_wave_clock(Q.wave_clk, gitem, t0, t1, r0, r1, f, 0u);
+            if (Q.hf_measure) Q.hf_cost[gitem] = uint32_t(t1 - t0);
+        }
+        return;
+    }
     const bool hf = B.p[0].hf_measure != 0u;
     if (hf && (threadIdx.x & 63u) == 0u) t0v[threadIdx.x >> 6] = uint32_t(__builtin_amdgcn_s_memtime());
     process_item<TRI, VAR>(late_params(B.p[0], off), item, off);
@@ -1969,7 +1965,8 @@ __global__ void __launch_bounds__(kWG) k_render_batch(KBatch B)
         const uint32_t nw = B.p[0].wh_wgs;
         if (bid < nw)
         {
-            wide_section<true, (VAR & kVarWideG4) ? 4u : 16u>(B.p[0], bid * kWavesPerWG + (threadIdx.x >> 6));
+            wide_section<true, (VAR & kVarWideG4) ? 4u : 16u, (VAR & kVarWaveClock) != 0>(
+                B.p[0], bid * kWavesPerWG + (threadIdx.x >> 6));
             return;
         }
         bid -= nw;
@@ -1991,7 +1988,7 @@ __global__ void __launch_bounds__(64) k_render_batch_w64(KBatch B)
         const uint32_t nw = B.p[0].wh_wgs * kWavesPerWG;
         if (w < nw)
         {
-            wide_section<true, (VAR & kVarWideG4) ? 4u : 16u>(B.p[0], w);
+            wide_section<true, (VAR & kVarWideG4) ? 4u : 16u, (VAR & kVarWaveClock) != 0>(B.p[0], w);
             return;
         }
         w -= nw;
@@ -2538,6 +2535,8 @@ struct rt_scene
     HfCtx hf[kHfCtxs];
     uint64_t hf_clock = 0;
     uint64_t hf_evictions = 0;      // launch shapes that displaced another's state (rt_scene_info)
+    uint64_t batch_launches = 0;    // rt_render_batch_device chunks led by this scene: one launch ...
+    uint64_t batch_fallbacks = 0;   // ... or one launch per frame (frames that cannot share a launch)
     // scheduling tunables, read ONCE from the environment at rt_scene_create (A/B sweeps): the
     // launch path never calls getenv
     uint32_t hf_floor = 100000;     // RT_HF_FLOOR: heavy-first threshold floor, shader cycles
@@ -2564,6 +2563,11 @@ struct rt_scene
     size_t ndc_cap = 0;
     std::vector<float> ndc_key;
     uint32_t ndc_w = 0, ndc_spp = 0;
+    // the frame description the tables above were built for (prepare_samples' fast check: width,
+    // height, spp, fov bits and the caller's sample table; no table rebuild per launch)
+    uint32_t fp_w = 0, fp_h = 0, fp_spp = 0, fp_fov = 0;
+    bool fp_valid = false, fp_custom = false;
+    std::vector<float> fp_tbl;
     // sample table cache
     float2 *d_smp = nullptr;
     uint32_t smp_cap = 0;
@@ -2680,11 +2684,36 @@ int prepare_ndc(rt_scene *s, const rt_frame *f, uint32_t spp, const std::vector<
     return RT_OK;
 }
 
+int remember_tables(rt_scene *s, const rt_frame *f, uint32_t spp, const std::vector<float>& tbl)
+{
+    s->fp_w = f->width;
+    s->fp_h = f->height;
+    s->fp_spp = spp;
+    std::memcpy(&s->fp_fov, &f->fov, 4);
+    s->fp_custom = f->sample_offsets != nullptr;
+    s->fp_tbl = tbl;
+    s->fp_valid = true;
+    return RT_OK;
+}
+
+// true when the scene's camera-space and sample tables are those of this frame (no host work)
+bool tables_match(const rt_scene *s, const rt_frame *f, uint32_t spp)
+{
+    uint32_t fov;
+    std::memcpy(&fov, &f->fov, 4);
+    if (!s->fp_valid || s->fp_w != f->width || s->fp_h != f->height || s->fp_spp != spp || s->fp_fov != fov ||
+        s->fp_custom != (f->sample_offsets != nullptr))
+        return false;
+    return !f->sample_offsets || std::memcmp(s->fp_tbl.data(), f->sample_offsets, sizeof(float) * 2 * spp) == 0;
+}
+
 int prepare_samples(rt_scene *s, const rt_frame *f, uint32_t spp)
 {
+    if (tables_match(s, f, spp)) return RT_OK;
+    s->fp_valid = false;
     const std::vector<float> tbl = sample_table(f, spp);
     if (int rc = prepare_ndc(s, f, spp, tbl)) return rc;
-    if (tbl == s->smp_host) return RT_OK;
+    if (tbl == s->smp_host) return remember_tables(s, f, spp, tbl);
     if (int rc = wait_scene_idle(s)) return rc;
     if (spp > s->smp_cap)
     {
@@ -2700,11 +2729,11 @@ int prepare_samples(rt_scene *s, const rt_frame *f, uint32_t spp)
     std::memcpy(s->h_smp_pinned, tbl.data(), tbl.size() * sizeof(float));
     RT_HIP(hipMemcpy(s->d_smp, s->h_smp_pinned, tbl.size() * sizeof(float), hipMemcpyHostToDevice));
     s->smp_host = tbl;
-    return RT_OK;
+    return remember_tables(s, f, spp, tbl);
 }
 
 constexpr uint32_t kKernelFlags = RT_KERNEL_FLAG_WIDE_HEAVY | RT_KERNEL_FLAG_LDS_CELLS | RT_KERNEL_FLAG_EXHAUSTIVE |
-                                  RT_KERNEL_FLAG_WAVE_CLOCK | RT_KERNEL_FLAG_COOP_PAIRS | RT_KERNEL_BUDGET_MASK;
+                                  RT_KERNEL_FLAG_WAVE_CLOCK | RT_KERNEL_BUDGET_MASK;
 
 int validate_frame(const rt_frame *f)
 {
@@ -2940,9 +2969,6 @@ kfn_t lanes_kernel(int tri, int var)
     case kVarAuto | kVarLdsCells: return k_render_lanes<RT_TRI_MOLLER_TRUMBORE, kVarAuto | kVarLdsCells>;
     case kVarAuto | kVarLdsCells | kVarWaveClock:
         return k_render_lanes<RT_TRI_MOLLER_TRUMBORE, kVarAuto | kVarLdsCells | kVarWaveClock>;
-    case kVarAuto | kVarCoop: return k_render_lanes<RT_TRI_MOLLER_TRUMBORE, kVarAuto | kVarCoop>;
-    case kVarAuto | kVarCoop | kVarWideHeavy:
-        return k_render_lanes<RT_TRI_MOLLER_TRUMBORE, kVarAuto | kVarCoop | kVarWideHeavy>;
     default: return nullptr;
     }
 }
@@ -2978,8 +3004,6 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
         var = kVarAutoCore | (s->rcp_safe ? kVarFastRcp : 0) | (auto_runs(s) ? kVarPackedRem | kVarSkipRun : 0) |
               ((f->kernel & RT_KERNEL_FLAG_LDS_CELLS) ? kVarLdsCells : 0) |
               ((f->kernel & RT_KERNEL_FLAG_WAVE_CLOCK) ? kVarWaveClock : 0);
-        // the cooperative pair pass needs the full AUTO walk (packed counts, empty runs, records)
-        if ((f->kernel & RT_KERNEL_FLAG_COOP_PAIRS) && var == kVarAuto && kind == RT_KERNEL_AUTO) var |= kVarCoop;
         if (int rc = ensure_origin_terms(s, P, st)) return rc;
     }
     else if (lanes && P.isect == RT_ISECT_RAY_MARCH)
@@ -3028,7 +3052,7 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
     // two-phase arm it replaced -> 0.35 / 0.20 / 0.15).  On a whole frame the
     // lanes are busy with other items anyway and the section's repeated walks cost more than they
     // save (+1-3 %).
-    const bool wide_ok = auto_path && (var & ~kVarCoop) == kVarAuto && P.spp <= 16u;
+    const bool wide_ok = auto_path && var == kVarAuto && P.spp <= 16u;
     const bool wide_heavy = wide_ok && kind == RT_KERNEL_AUTO &&
                             ((f->kernel & RT_KERNEL_FLAG_WIDE_HEAVY) ||
                              (P.nranks >= 2u && s->max_cell_refs >= s->wh_auto_refs));
@@ -3146,6 +3170,11 @@ kbfn_t batch_kernel(int var, bool w64)
         return batch_kernel_of<kVarAuto | kVarWideHeavy | kVarWideFused>(w64);
     if (var == (kVarAuto | kVarWideHeavy | kVarWideFused | kVarWideG4))
         return batch_kernel_of<kVarAuto | kVarWideHeavy | kVarWideFused | kVarWideG4>(w64);
+    // RT_KERNEL_FLAG_WAVE_CLOCK (debug timelines, tools/batch_waves.py): the bench pair's batched step
+    // at one rank and with the fused wide section
+    if (var == (kVarAuto | kVarWaveClock)) return batch_kernel_of<kVarAuto | kVarWaveClock>(w64);
+    if (var == (kVarAuto | kVarWideHeavy | kVarWideFused | kVarWaveClock))
+        return batch_kernel_of<kVarAuto | kVarWideHeavy | kVarWideFused | kVarWaveClock>(w64);
     return nullptr;
 }
 
@@ -3167,7 +3196,10 @@ int launch_batch(rt_scene *const *S, const rt_frame *F, uint32_t n, KParams *P, 
     for (uint32_t i = 0; i < n; i++)
     {
         const uint32_t kind = F[i].kernel & RT_KERNEL_KIND_MASK;
-        if (kind != RT_KERNEL_AUTO || (F[i].kernel & ~uint32_t(RT_KERNEL_FLAG_WIDE_HEAVY)) != 0u) return RT_E_INVALID;
+        if (kind != RT_KERNEL_AUTO ||
+            (F[i].kernel & ~uint32_t(RT_KERNEL_FLAG_WIDE_HEAVY | RT_KERNEL_FLAG_WAVE_CLOCK)) != 0u ||
+            (F[i].kernel & RT_KERNEL_FLAG_WAVE_CLOCK) != (F[0].kernel & RT_KERNEL_FLAG_WAVE_CLOCK))
+            return RT_E_INVALID;
         if (P[i].isect != RT_ISECT_GRID || P[i].tri_test != RT_TRI_MOLLER_TRUMBORE) return RT_E_INVALID;
         if (P[i].W != P[0].W || P[i].H != P[0].H || P[i].spp != spp || S[i]->device != S[0]->device)
             return RT_E_INVALID;
@@ -3183,8 +3215,9 @@ int launch_batch(rt_scene *const *S, const rt_frame *F, uint32_t n, KParams *P, 
     // 4 % slower at 2 on the build of that A/B; re-measured on the current one, a rank of 2 takes
     // 0.321 ms fused vs 0.338 (profiles/r03aa_wg64_wide_fused2_sweep.json): fused from 2 ranks
     const bool fused = wide_heavy && S[0]->wh_fused && P[0].nranks >= S[0]->wh_fused_min_ranks;
+    const bool clk = (F[0].kernel & RT_KERNEL_FLAG_WAVE_CLOCK) != 0u;
     const int kvar = var | (wide_heavy ? kVarWideHeavy : 0) | (fused ? kVarWideFused : 0) |
-                     (fused && spp > 4u ? kVarWideG4 : 0);
+                     (fused && spp > 4u ? kVarWideG4 : 0) | (clk ? kVarWaveClock : 0);
     if (!batch_kernel(kvar, false)) return RT_E_INVALID;
     *batched = true;
     KBatch KB;
@@ -3237,6 +3270,21 @@ int launch_batch(rt_scene *const *S, const rt_frame *F, uint32_t n, KParams *P, 
         bwg = 64u;
     }
     const kbfn_t fn = batch_kernel(kvar, w64);
+    if (clk)
+    {
+        // one record per lane item and per (listed item, wave) of the wide section
+        const size_t need = (size_t(blocks) * kWavesPerWG + size_t(kWhMax) * 16u) * 4u;
+        if (need > s0->clk_cap)
+        {
+            if (s0->d_clk) RT_HIP(hipFree(s0->d_clk));
+            s0->d_clk = nullptr;
+            RT_HIP(hipMalloc(&s0->d_clk, need * sizeof(uint64_t)));
+            s0->clk_cap = need;
+        }
+        RT_HIP(hipMemsetAsync(s0->d_clk, 0, need * sizeof(uint64_t), st));
+        s0->clk_items = uint32_t(need / 4u);
+        P[0].wave_clk = s0->d_clk;
+    }
     for (uint32_t i = 0; i < n; i++) KB.p[i] = P[i];
     // timing: scene 0's ring (one timed launch for the whole batch)
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
@@ -3382,6 +3430,8 @@ int rt_scene_info_get(rt_scene *s, rt_scene_info *out)
     out->wh_fused = s->wh_fused;
     out->hf_contexts = kHfCtxs;
     out->hf_evictions = s->hf_evictions;
+    out->batch_launches = s->batch_launches;
+    out->batch_fallbacks = s->batch_fallbacks;
     out->device_bytes = s->device_bytes;
     return RT_OK;
 }
@@ -3752,6 +3802,19 @@ int rt_scene_device_bytes(const rt_scene *s, uint64_t *bytes)
 } // extern "C"
 
 namespace {
+// Per-sample records requested from the product kernels (rt_render_records_device): the
+// rectangle's samples land in d[((y - y0) * w + (x - x0)) * spp + s].
+struct RecOut { rt_sample_rec *d; uint32_t x0, y0, w, h; };
+
+void set_records(KParams& P, const RecOut& r)
+{
+    P.recs = r.d;
+    P.rec_x0 = r.x0;
+    P.rec_y0 = r.y0;
+    P.rec_w = r.w;
+    P.rec_h = r.h;
+}
+
 // Frame parameters of a device-resident render (see render_device); returns the local tile count.
 uint32_t device_params(const rt_scene *s, const rt_frame *f, uint32_t rank, uint32_t nranks, bool shard,
                        uint32_t *d_out, uint32_t *d_hits, KParams& P)
@@ -3772,7 +3835,7 @@ uint32_t device_params(const rt_scene *s, const rt_frame *f, uint32_t rank, uint
 // interleaved 16x16 tiles (shard true: d_out = the compact shard, also for nranks == 1),
 // optionally with per-sample hit IDs.
 int render_device(rt_scene *s, const rt_frame *f, uint32_t rank, uint32_t nranks, bool shard, uint32_t *d_out,
-                  uint32_t *d_hits, void *hip_stream)
+                  uint32_t *d_hits, void *hip_stream, const RecOut *recs = nullptr)
 {
     if (!s || !d_out || nranks == 0 || rank >= nranks) return fail(RT_E_INVALID, "bad arguments");
     int rc = validate_frame(f);
@@ -3783,15 +3846,21 @@ int render_device(rt_scene *s, const rt_frame *f, uint32_t rank, uint32_t nranks
     if ((rc = prepare_samples(s, f, spp))) return rc;
     KParams P;
     const uint32_t local = device_params(s, f, rank, nranks, shard, d_out, d_hits, P);
+    if (recs) set_records(P, *recs);
     return launch_render(s, f, P, local, static_cast<hipStream_t>(hip_stream));
 }
 
-// rt_render_batch_device's frames [0, n): one k_render_batch launch when they can share it.
+// rt_render_batch_device's frames [0, n): one k_render_batch launch when they can share it.  The
+// cheap checks (one device) come before anything touches a scene's device state; a scene listed
+// twice with another frame shape or sample table than its last frame's would read the last one's
+// tables, so such batches take one launch per frame (counted in rt_scene_info.batch_fallbacks).
 int render_batch_chunk(rt_scene *const *S, const rt_frame *F, uint32_t n, uint32_t rank, uint32_t nranks,
-                       uint32_t *const *outs, uint32_t *const *hits, void *hip_stream)
+                       uint32_t *const *outs, uint32_t *const *hits, const RecOut *recs, void *hip_stream)
 {
     bool batched = false;
-    if (n >= 2)
+    bool one_device = true;
+    for (uint32_t i = 1; i < n; i++) one_device = one_device && S[i]->device == S[0]->device;
+    if (n >= 2 && one_device)
     {
         std::vector<rt_scene *> uniq(S, S + n);
         std::sort(uniq.begin(), uniq.end());
@@ -3806,20 +3875,25 @@ int render_batch_chunk(rt_scene *const *S, const rt_frame *F, uint32_t n, uint32
         {
             if ((rc = prepare_samples(S[i], &F[i], std::max(1u, F[i].spp)))) return rc;
             local = device_params(S[i], &F[i], rank, nranks, nranks > 1, outs[i], hits ? hits[i] : nullptr, P[i]);
+            if (recs) set_records(P[i], recs[i]);
         }
-        // a scene listed twice with another camera table / sample table than its last frame's
-        // would read the last one's: such batches take one launch per frame
         bool tables_ok = true;
-        for (uint32_t i = 0; i < n; i++)
-        {
-            const uint32_t spp = std::max(1u, F[i].spp);
-            tables_ok = tables_ok && ndc_key(&F[i], spp, sample_table(&F[i], spp)) == S[i]->ndc_key;
-        }
+        for (uint32_t i = 0; i < n; i++) tables_ok = tables_ok && tables_match(S[i], &F[i], std::max(1u, F[i].spp));
         if (tables_ok) rc = launch_batch(S, F, n, P, local, static_cast<hipStream_t>(hip_stream), &batched);
-        if (batched) return rc;
+        if (batched)
+        {
+            S[0]->batch_launches++;
+            return rc;
+        }
+    }
+    if (n >= 2)
+    {
+        std::lock_guard<std::mutex> lk(S[0]->mtx);
+        S[0]->batch_fallbacks++;
     }
     for (uint32_t i = 0; i < n; i++)
-        if (int rc = render_device(S[i], &F[i], rank, nranks, nranks > 1, outs[i], hits ? hits[i] : nullptr, hip_stream))
+        if (int rc = render_device(S[i], &F[i], rank, nranks, nranks > 1, outs[i], hits ? hits[i] : nullptr, hip_stream,
+                                   recs ? &recs[i] : nullptr))
             return rc;
     return RT_OK;
 }
@@ -3857,7 +3931,34 @@ int rt_render_batch_device(rt_scene *const *scenes, const rt_frame *frames, uint
     }
     for (uint32_t i = 0; i < n; i += kMaxBatch)
         if (int rc = render_batch_chunk(scenes + i, frames + i, std::min(kMaxBatch, n - i), rank, nranks, d_outs + i,
-                                        d_hits ? d_hits + i : nullptr, hip_stream))
+                                        d_hits ? d_hits + i : nullptr, nullptr, hip_stream))
+            return rc;
+    return RT_OK;
+}
+
+int rt_render_records_device(rt_scene *const *scenes, const rt_frame *frames, uint32_t n, uint32_t rank,
+                             uint32_t nranks, uint32_t *const *d_outs, const rt_tile *rects,
+                             rt_sample_rec *const *d_recs, void *hip_stream)
+{
+    if (!scenes || !frames || !d_outs || !rects || !d_recs || n == 0 || nranks == 0 || rank >= nranks)
+        return fail(RT_E_INVALID, "bad arguments");
+    std::vector<RecOut> ro(n);
+    for (uint32_t i = 0; i < n; i++)
+    {
+        if (!scenes[i] || !d_outs[i] || !d_recs[i]) return fail(RT_E_INVALID, "NULL scene, output or record array");
+        if (int rc = validate_frame(&frames[i])) return rc;
+        if ((frames[i].kernel & RT_KERNEL_KIND_MASK) != RT_KERNEL_AUTO || frames[i].intersector != RT_ISECT_GRID ||
+            frames[i].tri_test != RT_TRI_MOLLER_TRUMBORE)
+            return fail(RT_E_INVALID, "records come from AUTO's grid / IntersectRayTri path only");
+        const rt_tile& r = rects[i];
+        if (r.x1 <= r.x0 || r.y1 <= r.y0 || r.x1 > frames[i].width || r.y1 > frames[i].height)
+            return fail(RT_E_INVALID, "record rectangle outside the frame or empty");
+        ro[i] = RecOut{ d_recs[i], r.x0, r.y0, r.x1 - r.x0, r.y1 - r.y0 };
+    }
+    if (n == 1) return render_device(scenes[0], &frames[0], rank, nranks, nranks > 1, d_outs[0], nullptr, hip_stream, &ro[0]);
+    for (uint32_t i = 0; i < n; i += kMaxBatch)
+        if (int rc = render_batch_chunk(scenes + i, frames + i, std::min(kMaxBatch, n - i), rank, nranks, d_outs + i,
+                                        nullptr, ro.data() + i, hip_stream))
             return rc;
     return RT_OK;
 }

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 7   /* 7: rt_scene_info.box_words (box-run empty runs); 6: row-rotated shard deal */
+#define RT_ABI_VERSION 8   /* 8: rt_render_records_device, rt_scene_info batch counters; 7: rt_scene_info.box_words (box-run empty runs); 6: row-rotated shard deal */
 
 enum rt_status {
     RT_OK = 0,
@@ -106,12 +106,6 @@ enum rt_kernel {
                                           lanes per sample, 4 for spp 8-16) by a kernel on the scene's
                                           side stream, beside the one-lane-per-sample kernel (fork /
                                           join) */
-    RT_KERNEL_FLAG_COOP_PAIRS = 0x1000, /* OR-able (AUTO, grid): at a DDA step whose testing lanes
-                                           sit in different cells, every lane still walking takes
-                                           an equal run of the wave's (ray, record) pairs (ballot
-                                           prefix sums, LDS owner slots, a (t, position) minimum per
-                                           ray) instead of each lane looping its own list (A/B arm,
-                                           identical results) */
     RT_KERNEL_FLAG_EXHAUSTIVE = 0x8000, /* OR-able, ray march: evaluate every triangle per step
                                            (no block culling; A/B arm, identical results) */
     RT_KERNEL_FLAG_WAVE_CLOCK = 0x400000, /* OR-able (AUTO), debug: record s_memtime {start, end} of
@@ -124,7 +118,8 @@ enum rt_kernel {
 };
 /* Removed A/B flags (they lost; a frame that sets one is rejected): 0x10 centre-out
    row order, 0x20 static block order, 0x40 16-lane wide kernel, 0x100 one-phase shards, bit 31
-   the two-phase arm (replaced by RT_KERNEL_FLAG_WIDE_HEAVY in round 2).  The scheduling tunables
+   the two-phase arm (replaced by RT_KERNEL_FLAG_WIDE_HEAVY in round 2), 0x1000 the wave-cooperative
+   (ray, record) pair pass (round 3; it lost inside the batched step at every rank count).  The scheduling tunables
    are read once per scene from the environment at rt_scene_create (rt_scene_info). */
 
 /* Per-frame parameters: what Renderer::RenderTile reads from the Scene and itself. */
@@ -249,6 +244,21 @@ int  rt_render_batch_device(rt_scene *const *scenes, const rt_frame *frames, uin
                             uint32_t nranks, uint32_t *const *d_outs, uint32_t *const *d_hits,
                             void *hip_stream);
 
+/* The benchmarked launch path with per-sample records (the parity pin of the product kernels'
+ * walk): as rt_render_frame_device / rt_render_shard_device (n == 1) or rt_render_batch_device
+ * (n >= 2; one batched launch where the frames can share it), and in addition every traced sample
+ * of frame i inside rects[i] (frame pixels [x0, x1) x [y0, y1)) stores its record
+ * d_recs[i][((y - y0) * (x1 - x0) + (x - x0)) * spp + s]: hit, Grid::Intersect's tri_idx, the GridIdx
+ * of the accepted cell (of the last cell walked on a miss; 0xFFFFFFFF when the ray misses the grid;
+ * grid.cpp:243-271), t, u, v (grid.cpp:258-266) and the sample's colour (renderer.cpp:107-121).
+ * steps / tests are 0xFFFFFFFF: the product walks skip proven-empty cells and do not count
+ * (rt_trace_samples reports them).  Same kernels and the same walk code as the plain entry points:
+ * the stores sit after the walk behind a null test of the record pointer.  AUTO frames only (grid
+ * intersector, IntersectRayTri). */
+int  rt_render_records_device(rt_scene *const *scenes, const rt_frame *frames, uint32_t n, uint32_t rank,
+                              uint32_t nranks, uint32_t *const *d_outs, const rt_tile *rects,
+                              rt_sample_rec *const *d_recs, void *hip_stream);
+
 /* Render-kernel time of the last timed rendering call on this scene (ms): the HIP events on the
  * launch stream immediately around its render kernel(s), as rt_kernel_times.  Waits for them. */
 int  rt_last_kernel_ms(rt_scene *scene, float *ms);
@@ -318,6 +328,11 @@ typedef struct rt_scene_info {
                                    axis); 0: none (references >= 2^20 or above the size cap: AUTO then
                                    walks without the packed counts and empty runs) */
     uint32_t wh_alpha16_n2;     /* RT_WH_ALPHA16_N2: the wide threshold at a rank of 2 of a batched step */
+    uint32_t pad0;
+    uint64_t batch_launches;    /* rt_render_batch_device chunks led by this scene (frames[0]) that ran as
+                                   ONE launch ... */
+    uint64_t batch_fallbacks;   /* ... and that fell back to one launch per frame (frames that cannot
+                                   share a launch): the batch's kernel time then covers only frame 0 */
 } rt_scene_info;
 int  rt_scene_info_get(rt_scene *scene, rt_scene_info *out);
 

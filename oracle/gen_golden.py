@@ -103,6 +103,33 @@ def crop_records(tmp):
     return crops
 
 
+def record_shas(tmp, sids=range(10)):
+    """Full 1920x1080x4 frames, per-sample record columns of the reference's own walk
+    (refdriver_instr samples over the whole frame; its columns 0-7 checked equal to the plain
+    refdriver's): SHA-256 of the (t, u, v) words, of the accepted / last cell (GridIdx) and of
+    the (r, g, b) colour words, each as a row-major u32 array in (y, x, sample) order.  Pins the
+    product kernels' float depth / barycentrics and voxel ids on whole frames (the 265 MB record
+    files are hashed in a temporary directory, never committed)."""
+    out = {}
+    for sid in sids:
+        args = ["samples", os.path.join(SCENES, f"scene{sid}.rtscene"), "1920", "1080", "4", "0", "0", "1920",
+                "1080"]
+        pp, ip = os.path.join(tmp, "plain.rec"), os.path.join(tmp, "instr.rec")
+        run(args + [pp])
+        run(args + [ip], exe=REF_INSTR)
+        with open(pp, "rb") as f:
+            plain = np.frombuffer(f.read(), "<u4").reshape(-1, 8)
+        with open(ip, "rb") as f:
+            inst = np.frombuffer(f.read(), "<u4").reshape(-1, 11)
+        assert np.array_equal(plain, inst[:, :8]), sid
+        os.remove(pp)
+        os.remove(ip)
+        h = lambda a: hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+        out[str(sid)] = {"tuv_sha256": h(inst[:, 2:5]), "voxel_sha256": h(inst[:, 8]), "rgb_sha256": h(inst[:, 5:8])}
+        print("records", sid, flush=True)
+    return out
+
+
 def head_frame(tmp):
     """BASELINE config 4: head at 4096x4096x16spp, BGRA8 and per-sample hit-ID SHA-256 (the hit
     file is 1 GiB: hashed in a temporary directory, never committed)."""
@@ -118,7 +145,7 @@ def head_frame(tmp):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-head", action="store_true")
-    ap.add_argument("--only", choices=["crops", "bmp", "head"],
+    ap.add_argument("--only", choices=["crops", "bmp", "head", "records"],
                     help="regenerate one section and merge it into the existing golden.json")
     a = ap.parse_args()
     if a.only:
@@ -130,6 +157,9 @@ def main():
             meta["crops"] = crop_records(tmp)
         elif a.only == "head":
             meta["frames_1080p4"]["head_4096x4096x16"] = head_frame(tmp)
+        elif a.only == "records":
+            for sid, d in record_shas(tmp).items():
+                meta["frames_1080p4"][sid].update(d)
         else:
             meta["bmp"] = bmp_golden(tmp)
         meta["sample_record"] = SAMPLE_RECORD
@@ -201,6 +231,8 @@ def main():
         small.append({"scene": sid, "W": w, "H": h, "spp": spp, "name": name})
 
     crops = crop_records(tmp)
+    for sid, d in record_shas(tmp).items():
+        frames[sid].update(d)
     meta = {
         "generator": "oracle/gen_golden.py via oracle/_ref/refdriver (reference sources, g++ "
                      "-O3 -std=c++11, no -march)",

@@ -36,11 +36,13 @@ def test_struct_layouts():
     assert ctypes.sizeof(rtm.Vertex) == 24 and ctypes.sizeof(rtm.Triangle) == 24
     assert rtm.SAMPLE_REC_DTYPE.itemsize == 48
     assert ctypes.sizeof(rtm.Tile) == 16
+    # rt_scene_info: the batch counters sit after an explicit pad word (8-byte aligned)
+    assert rtm.SceneInfo.batch_launches.offset % 8 == 0 and ctypes.sizeof(rtm.SceneInfo) == rtm.SceneInfo.batch_fallbacks.offset + 8
 
 
 def test_host_side_entry_points_without_gpu():
     L = rtm.tracer_lib()
-    assert L.rt_abi_version() == 7
+    assert L.rt_abi_version() == 8
     # Hammersley table matches the reference's (renderer.cpp:49-60), 4 spp in SURVEY H12
     np.testing.assert_array_equal(rtm.sample_table(4), [[-.5, -.5], [-.25, 0], [0, -.25], [.25, .25]])
     e = rtm.shard_elems(1920, 1080, 8)

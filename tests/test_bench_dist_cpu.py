@@ -4,6 +4,7 @@ world_size 2.  The GPU render is replaced by the oracle's frame of this rank's t
 the step number so a frame assembled from the wrong step or buffer set shows; everything else
 is bench.run_steps itself."""
 import os
+import time
 import socket
 
 import numpy as np
@@ -44,6 +45,9 @@ class CpuWorkload:
 
     def sync(self):
         pass
+
+    def mark(self):
+        return time.perf_counter()
 
     def reset_times(self):
         pass

@@ -61,8 +61,19 @@ def test_render_kernels_do_not_spill(tmp_path):
     # the AUTO kernel (kVarAuto = 80398: lanes + wave gate + distance skip + origin terms + Newton
     # reciprocal + packed counts + uniform cells + empty runs + XCD rows), its fallbacks for scenes
     # outside the reciprocal / packing ranges, and its arms keep 8 waves/SIMD
+    # Also every kernel bench.py dispatches: the one-wave-workgroup AUTO kernels (k_render_lanes_w64,
+    # the N = 1 bench step; k_render_batch_w64, the batched step at 1, 2 and >= 8 ranks, with the wide
+    # section fused in front: kVarWideHeavy 524288, kVarWideFused 1048576, kVarWideG4 2097152), the
+    # 256-lane batch kernels (a rank of 3-7) and the wide-section kernels
     for key in ("k_render_lanesILi0ELi80398E", "k_render_lanesILi0ELi78350E", "k_render_lanesILi0ELi76298E",
                 "k_render_lanesILi0ELi74250E", "k_render_lanesILi0ELi604686E", "k_render_lanesILi0ELi0E",
-                "k_render_compact"):
+                "k_render_compact", "k_render_lanes_w64ILi0ELi80398E", "k_render_batch_w64ILi0ELi80398E",
+                "k_render_batch_w64ILi0ELi604686E", "k_render_batch_w64ILi0ELi1653262E",
+                "k_render_batch_w64ILi0ELi3750414E", "k_render_batchILi0ELi80398E", "k_render_batchILi0ELi604686E",
+                "k_render_batchILi0ELi1653262E", "k_render_batchILi0ELi3750414E", "k_render_whILj16E",
+                "k_render_whILj4E", "k_render_wh_batchILj16E", "k_render_wh_batch_w64ILj16E"):
         arm = [v for n, v in render.items() if key in n]
         assert arm and all(a[2] == 8 for a in arm), (key, arm)
+    # the bench's own kernels are pinned by name (a renamed kernel must update this guard)
+    dispatched = ("k_render_lanes_w64", "k_render_batch_w64", "k_render_batch")
+    assert all(any(d + "I" in n for n in render) for d in dispatched), sorted(render)

@@ -298,9 +298,9 @@ def test_auto_equals_arms(golden, scenes):
 def test_removed_arms_rejected(scenes):
     """Kernel kinds and flags of arms removed after losing their A/Bs fail loudly: 4 (LDS bitmap),
     5 (all-wide kernel), 0x10 centre-out, 0x20 static order, 0x40 16-lane wide kernel, 0x100
-    one-phase shards, bit 31 two-phase."""
+    one-phase shards, 0x1000 the cooperative pair pass, bit 31 two-phase."""
     hs, gs = scenes(1)
-    for k in (4, 5, 0x10, 0x20, 0x40, 0x100, 0x80000000):
+    for k in (4, 5, 0x10, 0x20, 0x40, 0x100, 0x1000, 0x80000000):
         with pytest.raises(rtm.RtError):
             gs.render_frame(gs.frame(32, 32, 4, kernel=k))
 
@@ -939,68 +939,3 @@ def test_batch_graph_replay(golden, scenes):
         torch.cuda.synchronize()
         for sid, o in zip(sids, outs):
             assert sha_dev(o) == golden["frames_1080p4"][str(sid)]["bgra_sha256"]
-
-
-@pytest.mark.parametrize("sid", range(10))
-def test_coop_pairs_full_frame_hits(golden, scenes, sid):
-    """RT_KERNEL_FLAG_COOP_PAIRS (the wave-cooperative (ray, record) pair pass over the lists the
-    lanes do not share): BGRA8 and per-sample hit-ID SHA-256 equal the reference's on all 10
-    scenes at 1920x1080x4, on consecutive frames (natural, then heavy-first block order).  Quads
-    with one normal on both triangles (Cornell, killeroo's ground) make hit IDs the only check of
-    the pass's (t, list position) tie-break."""
-    import torch
-    g = golden["frames_1080p4"][str(sid)]
-    hs, gs = scenes(sid)
-    f = gs.frame(1920, 1080, 4, kernel=rtm.RT_KERNEL_AUTO | rtm.RT_KERNEL_FLAG_COOP_PAIRS)
-    out = torch.empty(1920 * 1080, dtype=torch.int32, device="cuda")
-    hits = torch.empty(1920 * 1080 * 4, dtype=torch.int32, device="cuda")
-    st = torch.cuda.current_stream().cuda_stream
-    for i in range(3):
-        out.fill_(0x5A5A5A5A)
-        hits.fill_(0x5A5A5A5A)
-        gs.render_hits_device(f, 0, 1, out.data_ptr(), hits.data_ptr(), st)
-        torch.cuda.synchronize()
-        assert sha_dev(out) == g["bgra_sha256"], (sid, i)
-        assert sha_dev(hits) == g["hits_sha256"], (sid, i)
-
-
-@pytest.mark.parametrize("sid", [5, 8])
-def test_coop_pairs_shards_rank_of_8(golden, scenes, sid):
-    """The pair pass in AUTO's rank-of-8 shard kernels (with the wide section on these dense
-    scenes): the 8 shards' frame-absolute hit IDs hash to the reference's, the un-permuted shards
-    to its BGRA8."""
-    import torch
-    g = golden["frames_1080p4"][str(sid)]
-    W, H, N = 1920, 1080, 8
-    hs, gs = scenes(sid)
-    f = gs.frame(W, H, 4, kernel=rtm.RT_KERNEL_AUTO | rtm.RT_KERNEL_FLAG_COOP_PAIRS)
-    e = rtm.shard_elems(W, H, N)
-    gathered = torch.zeros(N * e, dtype=torch.int32, device="cuda")
-    hits = torch.full((W * H * 4,), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
-    st = torch.cuda.current_stream().cuda_stream
-    for r in range(N):
-        for _ in range(4):
-            gs.render_hits_device(f, r, N, gathered.data_ptr() + 4 * r * e, hits.data_ptr(), st)
-    torch.cuda.synchronize()
-    assert sha_dev(hits) == g["hits_sha256"]
-    out = torch.zeros(W * H, dtype=torch.int32, device="cuda")
-    rtm.unshard_device(W, H, N, gathered.data_ptr(), out.data_ptr(), st)
-    torch.cuda.synchronize()
-    assert sha_dev(out) == g["bgra_sha256"]
-
-
-@pytest.mark.parametrize("sid,spp", [(8, 1), (8, 2), (5, 8), (4, 16), (1, 3)])
-def test_coop_pairs_ragged_vs_oracle(scenes, oracle, sid, spp):
-    """The pair pass on ragged frames (partial tiles, so waves with idle lanes) at other sample
-    counts: frame and per-sample hit IDs equal the CPU restatement's."""
-    import torch
-    W, H = 200, 150
-    hs, gs = scenes(sid)
-    exp, exp_hits, _ = oracle.render(sid, W, H, spp, hits=True)
-    f = gs.frame(W, H, spp, kernel=rtm.RT_KERNEL_AUTO | rtm.RT_KERNEL_FLAG_COOP_PAIRS)
-    out = torch.zeros(W * H, dtype=torch.int32, device="cuda")
-    hits = torch.full((W * H * spp,), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
-    gs.render_hits_device(f, 0, 1, out.data_ptr(), hits.data_ptr(), torch.cuda.current_stream().cuda_stream)
-    torch.cuda.synchronize()
-    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32).reshape(H, W), exp)
-    np.testing.assert_array_equal(hits.cpu().numpy().view(np.uint32), exp_hits)

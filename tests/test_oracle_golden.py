@@ -126,3 +126,16 @@ def test_kat_dist(oracle):
     got = oracle.kat("dist", rin, 1)
     np.testing.assert_array_equal(bits(got), bits(exp))      # same x86 NaNs on both sides
     assert np.isnan(exp).sum() > 100
+
+
+@pytest.mark.parametrize("sid", [1, 8])
+def test_full_frame_record_shas(oracle, golden, sid):
+    """The oracle's per-sample (t, u, v), voxel and colour words over a whole 1920x1080x4 frame
+    hash to the reference walk's (refdriver_instr, oracle/gen_golden.py record_shas) -- the same
+    SHAs the GPU record tests check the product kernels against."""
+    g = golden["frames_1080p4"][str(sid)]
+    rec = oracle.records(sid, 1920, 1080, 4, 0, 0, 1920, 1080).view(np.uint32).reshape(-1, 12)
+    h = lambda a: hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+    assert h(rec[:, 5:8]) == g["tuv_sha256"]
+    assert h(rec[:, 2]) == g["voxel_sha256"]
+    assert h(rec[:, 8:11]) == g["rgb_sha256"]
