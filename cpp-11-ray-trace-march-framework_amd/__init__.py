@@ -62,7 +62,7 @@ TRACER_SYMBOLS = [
     "rt_sample_table", "rt_last_error", "rt_abi_version", "rt_grid_build", "rt_grid_free",
     "rt_scene_create_from_mesh", "rt_kernel_times", "rt_render_frame_host", "rt_frame_host_wait", "rt_host_alloc",
     "rt_host_free", "rt_render_hits_device", "rt_scene_info_get", "rt_build_hash", "rt_render_batch_device",
-    "rt_render_records_device",
+    "rt_render_records_device", "rt_render_frame_host_tiled",
 ]
 MAX_BATCH = 4                            # frames per rt_render_batch_device launch
 HOST_SYMBOLS = [
@@ -176,6 +176,8 @@ def tracer_lib():
             L.rt_scene_info_get.argtypes = [vp, ctypes.POINTER(SceneInfo)]
             L.rt_build_hash.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
             L.rt_render_batch_device.argtypes = [vp, ctypes.POINTER(Frame), c_u32, c_u32, c_u32, vp, vp, vp]
+        if hasattr(L, "rt_render_frame_host_tiled"):   # ABI 8
+            L.rt_render_frame_host_tiled.argtypes = [vp, ctypes.POINTER(Frame), vp, c_u32, c_u32, c_u32]
         if hasattr(L, "rt_render_records_device"):   # ABI 8
             L.rt_render_records_device.argtypes = [vp, ctypes.POINTER(Frame), c_u32, c_u32, c_u32, vp,
                                                    ctypes.POINTER(Tile), vp, vp]
@@ -531,6 +533,13 @@ class GpuScene:
         _check(L.rt_render_frame_host(self._h, ctypes.byref(frame), ctypes.c_void_p(host_frame.ptr),
                                       arr, n), L, "rt_render_frame_host")
 
+    def render_frame_host_tiled(self, frame, host_frame, tiles_x=12, tiles_y=9, nlaunch=3):
+        """Asynchronous whole frame into a PinnedFrame in the Framebuffer's tile-buffer layout
+        (rt_render_frame_host_tiled); follow with wait_rows().  tile_views() cuts it into tiles."""
+        L = tracer_lib()
+        _check(L.rt_render_frame_host_tiled(self._h, ctypes.byref(frame), ctypes.c_void_p(host_frame.ptr), tiles_x,
+                                            tiles_y, nlaunch), L, "rt_render_frame_host_tiled")
+
     def kernel_times(self):
         """Render-kernel ms of the launches since the previous call (at most the last 64)."""
         L = tracer_lib()
@@ -660,6 +669,23 @@ def render_records_device(scenes, frames, d_outs, rects, d_recs, rank=0, nranks=
     L = tracer_lib()
     _check(L.rt_render_records_device(sp, fr, n, rank, nranks, outs, rc, recs, ctypes.c_void_p(stream)), L,
            "rt_render_records_device")
+
+
+def framebuffer_tiles(width, height, tiles_x=12, tiles_y=9):
+    """Framebuffer::Resize's tiles (framebuffer.cpp:106-117): [(x0, y0, x1, y1)] in tile order."""
+    tw, th = width // tiles_x, height // tiles_y
+    return [(c * tw, r * th, width if c == tiles_x - 1 else (c + 1) * tw, height if r == tiles_y - 1 else (r + 1) * th)
+            for r in range(tiles_y) for c in range(tiles_x)]
+
+
+def tile_views(flat, width, height, tiles_x=12, tiles_y=9):
+    """The tile buffers of rt_render_frame_host_tiled's layout as (h, w) views of `flat` (uint32 words):
+    tile (c, r) at word y0 * width + (y1 - y0) * x0, row-major at its own width."""
+    out = []
+    for (x0, y0, x1, y1) in framebuffer_tiles(width, height, tiles_x, tiles_y):
+        o = y0 * width + (y1 - y0) * x0
+        out.append(flat[o:o + (x1 - x0) * (y1 - y0)].reshape(y1 - y0, x1 - x0))
+    return out
 
 
 def shard_elems(width, height, nranks):

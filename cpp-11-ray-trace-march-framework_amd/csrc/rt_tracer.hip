@@ -92,7 +92,8 @@ constexpr uint32_t kDistBlock = 32;         // triangles per culling block of th
 // sum of wave costs of the measured frame
 // sum_full: the sum of wave costs of the last measured frame that rendered every item one lane
 // per sample (the wide section's span estimate; carried over by the plans of other frames)
-struct HfPlan { uint32_t cnt_hi, cnt_lo, maxc, cnt_w; unsigned long long sum; unsigned long long sum_full; };
+// cnt_w4: work items listed for the wide section's second tier (4 lanes per sample)
+struct HfPlan { uint32_t cnt_hi, cnt_lo, maxc, cnt_w; unsigned long long sum; unsigned long long sum_full; uint32_t cnt_w4, pad; };
 
 struct KParams
 {
@@ -165,17 +166,25 @@ struct KParams
     // max(wh_floor, wh_alpha16 / 16 x the estimated frame span), and keeps the current plan's
     // items (their cost words still hold the lane-mode cost of the last frame that measured
     // them) except in a refresh frame.
+    // Two tiers at spp <= 4 (wh_beta16 != 0): items above the alpha threshold take 16 lanes per sample,
+    // items between the beta and the alpha thresholds 4 (the list's second half, wh_list + kWhMax;
+    // their marks carry bit 31)
     uint32_t wh_on, wh_wgs, wh_refresh, wh_g;
-    uint32_t wh_floor, wh_alpha16;
+    uint32_t wh_floor, wh_alpha16, wh_beta16;
     const uint32_t *wh_mark_in;
     uint32_t *wh_mark_out;
     const uint32_t *wh_list_in;
     uint32_t *wh_list_out;
-    uint32_t *wh_host_cnt;      // host-mapped: the newest plan's cnt_w (sizes the next launches)
+    uint32_t *wh_host_cnt;      // host-mapped: the newest plan's wave count (sizes the next launches)
     // output
     uint32_t *out;
     uint32_t pitch;             // frame mode: words per row of out
-    uint32_t shard_mode;        // 1: out[local_tile * 256 + ty*16 + tx]
+    uint32_t shard_mode;        // 1: out[local_tile * 256 + ty*16 + tx]; 2: the framebuffer's tile buffers
+    // shard_mode 2 (rt_render_frame_host_tiled): the fb_tx x fb_ty tile grid of Framebuffer::Resize
+    // (framebuffer.cpp:106-117: tiles fb_tw x fb_th, the last column / row absorbs the remainder), each
+    // tile's buffer row-major at its own width (framebuffer.h:41-45), the buffers in tile order
+    uint32_t fb_tw, fb_th, fb_tx, fb_ty;
+    uint32_t fb_mtw, fb_mth;    // ceil(2^32 / fb_tw), ceil(2^32 / fb_th): x / fb_tw as one mul_hi
     uint32_t *hits;             // rt_render_hits_device: per-sample hit triangle, [(y*W + x)*spp + s]
                                 // (read after the walk through late_params; NULL in the plain calls)
     rt_sample_rec *recs;        // debug kernel only
@@ -747,7 +756,7 @@ __device__ __forceinline__ uint32_t cell_of_ref(const KParams& P, uint32_t k)
     return lo;
 }
 
-// The colour words of a record (store_record; the wide section stores them after its resolve).
+// The colour words of a record (the wide section stores them after its resolve).
 __device__ __forceinline__ void store_record_colour(const KParams& Q, uint32_t px, uint32_t py, uint32_t s, float r,
                                                     float g, float b)
 {
@@ -757,30 +766,35 @@ __device__ __forceinline__ void store_record_colour(const KParams& Q, uint32_t p
     o[8] = __float_as_uint(r);
     o[9] = __float_as_uint(g);
     o[10] = __float_as_uint(b);
-    o[11] = 0u;
 }
 
 // One per-sample record (rt_sample_rec) of a product kernel, for samples inside the requested
-// rectangle: rec[((y - y0) * w + (x - x0)) * spp + s].  DDA steps and tests are not counted by the
-// product walks (0xFFFFFFFF; k_trace_records pins them).
+// rectangle: rec[((y - y0) * w + (x - x0)) * spp + s], in RAW form -- what the walk leaves, with no
+// extra lookups in the product kernels (their register budget decides their occupancy): a hit's CSR
+// reference (tri word), a miss's end cell as the walk holds it (voxel word, still inside its copy of
+// the cell words).  k_record_fixup then maps the reference to Grid::Intersect's tri_idx and the cell
+// it lies in, and moves a raw end cell out of its copy (kRecRaw* in the pad word).  DDA steps and
+// tests are not counted by the product walks (0xFFFFFFFF; k_trace_records pins them).
+constexpr uint32_t kRecMagic = 0xF1A90000u;     // pad word of a raw record (a -1-filled word is not)
+constexpr uint32_t kRecRawCsr = 1u;             // tri word = CSR reference of the hit
+constexpr uint32_t kRecRawBox = 2u;             // voxel word = end cell in the ray's box-word copy
+constexpr uint32_t kRecRawOct = 4u;             // voxel word = end cell in the ray's octant copy
 __device__ __forceinline__ void store_record(const KParams& Q, uint32_t px, uint32_t py, uint32_t s, bool hit,
-                                             uint32_t tri, uint32_t voxel, float t, float u, float v, float r,
-                                             float g, float b)
+                                             uint32_t tri, uint32_t voxel, float t, float u, float v, uint32_t raw)
 {
     const uint32_t rx = px - Q.rec_x0, ry = py - Q.rec_y0;
     if (rx >= Q.rec_w || ry >= Q.rec_h) return;
-    // word by word (volatile: no dwordx4 merging, which would need 12 consecutive VGPRs here and
-    // raise the kernels' register count)
+    // word by word (volatile: no dwordx4 merging, which needs consecutive VGPRs)
     volatile uint32_t *o = reinterpret_cast<volatile uint32_t *>(Q.recs + (size_t(ry) * Q.rec_w + rx) * Q.spp + s);
     o[0] = hit ? 1u : 0u;
     o[1] = hit ? tri : rtd::kNoTri;
-    o[2] = voxel;
+    o[2] = hit ? rtd::kNoTri : voxel;
     o[3] = 0xFFFFFFFFu;
     o[4] = 0xFFFFFFFFu;
     o[5] = hit ? __float_as_uint(t) : 0u;
     o[6] = hit ? __float_as_uint(u) : 0u;
     o[7] = hit ? __float_as_uint(v) : 0u;
-    if (r == r) store_record_colour(Q, px, py, s, r, g, b);
+    o[11] = kRecMagic | (hit ? (raw & kRecRawCsr) : (raw & ~kRecRawCsr));
 }
 
 // grid.cpp:159-281 Grid::Intersect (NEW_GRID_TRAVERSAL), axis arrays unrolled into scalars
@@ -1254,7 +1268,20 @@ __device__ __forceinline__ TileCoord tile_of_block(const KParams& P)
 __device__ __forceinline__ void store_pixel(const KParams& P, const TileCoord& c, uint32_t p, uint32_t x,
                                             uint32_t y, uint32_t word)
 {
-    if (P.shard_mode)
+    if (P.shard_mode == 2u)
+    {
+        // the Framebuffer's tile buffers back to back in tile order c + r * fb_tx: tile (c, r) starts
+        // at y0 * W + th_r * x0 (the tiles above it, then the row's tiles left of it, all th_r tall),
+        // pixel (x, y) at buf[(x - x0) + (y - y0) * tw_c] (renderer.cpp:133).  x, y < 2^16 and the
+        // tile sizes < 2^16, so the mul_hi quotients are exact.
+        const uint32_t c = P.fb_tw ? min(__umulhi(x, P.fb_mtw), P.fb_tx - 1u) : P.fb_tx - 1u;
+        const uint32_t r = P.fb_th ? min(__umulhi(y, P.fb_mth), P.fb_ty - 1u) : P.fb_ty - 1u;
+        const uint32_t x0 = c * P.fb_tw, y0 = r * P.fb_th;
+        const uint32_t tw = c == P.fb_tx - 1u ? P.W - x0 : P.fb_tw;
+        const uint32_t th = r == P.fb_ty - 1u ? P.H - y0 : P.fb_th;
+        P.out[size_t(y0) * P.W + size_t(th) * x0 + (y - y0) * tw + (x - x0)] = word;
+    }
+    else if (P.shard_mode)
         P.out[size_t(c.k) * kTilePix + compact_bits(p >> 1) * kTile + compact_bits(p)] = word;
     else
         P.out[size_t(y - P.ry0) * P.pitch + (x - P.rx0)] = word;     // renderer.cpp:133
@@ -1295,23 +1322,16 @@ __device__ __forceinline__ ItemCoord item_coord(const KParams& P, uint32_t item,
     return tile_slot_coord(P, P.tile_order ? P.tile_order[kseq] : kseq, slot);   // local tile k
 }
 
-// The record of one sample of AUTO's walk (rt_render_records_device): the accepted cell of a hit from
-// its CSR reference; a box-run miss's end cell moved out of its box-word copy (the ray's direction
-// recomputed here, so neither the pixel nor the copy's offset stays live across the walk).
+// The record of one sample of AUTO's walk (rt_render_records_device), raw (store_record): a box-run
+// miss's end cell is still in its box-word copy.
 template <int VAR>
-__device__ __forceinline__ void process_record(const KParams& Q, const ItemCoord& ic, const SampleOut& so,
-                                               uint32_t tri, float cr, float cg, float cb)
+__device__ __forceinline__ void process_record(const KParams& Q, const ItemCoord& ic, const SampleOut& so, float cr,
+                                               float cg, float cb)
 {
-    uint32_t vox = so.voxel;
-    if (so.hit)
-        vox = so.csr != rtd::kNoTri ? cell_of_ref(Q, so.csr) : kVoxelUnknown;
-    else if (vox < kVoxelUnknown && RT_BOX_RUN && (VAR & kVarSkipRun) && (VAR & kVarPackedRem))
-    {
-        float dx, dy, dz;
-        rtd::dir_from_xy(Q.m, Q.ndcx[ic.x * Q.spp + ic.s], Q.ndcy[ic.y * Q.spp + ic.s], dx, dy, dz);
-        vox -= uint32_t(box_offset(Q, dx, dy, dz));
-    }
-    store_record(Q, ic.x, ic.y, ic.s, so.hit, tri, vox, so.t, so.u, so.v, cr, cg, cb);
+    constexpr uint32_t box = (RT_BOX_RUN && (VAR & kVarSkipRun) && (VAR & kVarPackedRem)) ? kRecRawBox : 0u;
+    store_record(Q, ic.x, ic.y, ic.s, so.hit, so.csr, so.voxel, so.t, so.u, so.v,
+                 (so.csr != rtd::kNoTri ? kRecRawCsr : 0u) | (so.voxel < kVoxelUnknown ? box : 0u));
+    store_record_colour(Q, ic.x, ic.y, ic.s, cr, cg, cb);
 }
 
 // One wave-sized work item = 64 consecutive sample slots of a 16x16 tile in Morton order
@@ -1337,7 +1357,7 @@ __device__ __forceinline__ void process_item(const KParams& P, uint32_t item, ui
     // kernel parameter; the walk above is the same code whatever the pointer holds)
     if (Q.hits && ic.valid) Q.hits[(size_t(ic.y) * Q.W + ic.x) * Q.spp + ic.s] = hit_tri;
     // rt_render_records_device only, likewise: the sample's record (process_record)
-    if (Q.recs && ic.valid) process_record<VAR>(Q, ic, so, hit_tri, cr, cg, cb);
+    if (Q.recs && ic.valid) process_record<VAR>(Q, ic, so, cr, cg, cb);
     float sr = 0.0f, sg = 0.0f, sb = 0.0f;
     if (Q.spp == 4u)
     {
@@ -1429,17 +1449,17 @@ __device__ __forceinline__ uint32_t xcd_band_block(uint32_t b, uint32_t nb, uint
 // cost milliseconds, measured).
 __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks)
 {
-    __shared__ uint32_t s_max, s_hi, s_lo, s_w, s_bhi, s_blo, s_bw, s_last;
+    __shared__ uint32_t s_max, s_hi, s_lo, s_w, s_w4, s_bhi, s_blo, s_bw, s_bw4, s_last;
     __shared__ unsigned long long s_sum;
     const uint32_t b = blockIdx.x * kWG + threadIdx.x;
     if (threadIdx.x == 0u)
     {
-        s_max = s_hi = s_lo = s_w = 0u;
+        s_max = s_hi = s_lo = s_w = s_w4 = 0u;
         s_sum = 0ull;
     }
     __syncthreads();
     const HfPlan last = *P.hf_plan_in;
-    uint32_t cost = 0u, sum = 0u, wmask = 0u;
+    uint32_t cost = 0u, sum = 0u, wmask = 0u, wmask4 = 0u;
     uint4 c = make_uint4(0u, 0u, 0u, 0u);
     if (b < nblocks)
     {
@@ -1457,27 +1477,39 @@ __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks)
             const uint32_t thr = max(P.wh_floor, uint32_t(min<uint64_t>(span * P.wh_alpha16 / 16u, 0xFFFFFFFFull)));
             wmask = uint32_t(c.x > thr) | (uint32_t(c.y > thr) << 1) | (uint32_t(c.z > thr) << 2) |
                     (uint32_t(c.w > thr) << 3);
+            // second tier (4 lanes per sample): items between the beta and the alpha thresholds
+            const uint32_t thr4 = P.wh_beta16 ? max(P.wh_floor, uint32_t(min<uint64_t>(span * P.wh_beta16 / 16u,
+                                                                                         0xFFFFFFFFull)))
+                                              : 0xFFFFFFFFu;
+            wmask4 = (uint32_t(c.x > thr4) | (uint32_t(c.y > thr4) << 1) | (uint32_t(c.z > thr4) << 2) |
+                      (uint32_t(c.w > thr4) << 3)) & ~wmask;
         }
         if (P.wh_on && !P.wh_refresh && P.hf_ver)
         {
-            // sticky: the current plan's items stay listed (mark = the plan version)
+            // sticky: the current plan's items stay listed in their tier (mark = the plan version,
+            // bit 31 = the second tier)
             const uint4 m = reinterpret_cast<const uint4 *>(P.wh_mark_in)[b];
-            wmask |= uint32_t(m.x == P.hf_ver) | (uint32_t(m.y == P.hf_ver) << 1) | (uint32_t(m.z == P.hf_ver) << 2) |
-                     (uint32_t(m.w == P.hf_ver) << 3);
+            const uint32_t in = uint32_t((m.x & 0x7FFFFFFFu) == P.hf_ver) | (uint32_t((m.y & 0x7FFFFFFFu) == P.hf_ver) << 1) |
+                                (uint32_t((m.z & 0x7FFFFFFFu) == P.hf_ver) << 2) |
+                                (uint32_t((m.w & 0x7FFFFFFFu) == P.hf_ver) << 3);
+            const uint32_t t4 = (m.x >> 31) | ((m.y >> 31) << 1) | ((m.z >> 31) << 2) | ((m.w >> 31) << 3);
+            wmask |= in & ~t4;
+            wmask4 = (wmask4 | (in & t4)) & ~wmask;
         }
         // the heavy-first order ranks a block by its slowest wave left in the lane section
-        cost = max(max((wmask & 1u) ? 0u : c.x, (wmask & 2u) ? 0u : c.y),
-                   max((wmask & 4u) ? 0u : c.z, (wmask & 8u) ? 0u : c.w));
+        const uint32_t wm = wmask | wmask4;
+        cost = max(max((wm & 1u) ? 0u : c.x, (wm & 2u) ? 0u : c.y), max((wm & 4u) ? 0u : c.z, (wm & 8u) ? 0u : c.w));
     }
     const bool tail = uint64_t(last.maxc) * kHfSlots * 16u > uint64_t(kHfTail) * (last.sum << 4);
     const uint32_t thr = max(P.hf_floor, last.maxc >> kHfShift);
     const bool heavy = P.hf_front && tail && cost > thr;
     const bool hi = heavy && cost > (last.maxc >> 1);
-    uint32_t rank = 0u, wrank = 0u;
+    uint32_t rank = 0u, wrank = 0u, wrank4 = 0u;
     if (cost) atomicMax(&s_max, cost);
     if (sum) atomicAdd(&s_sum, (unsigned long long)sum);
     if (heavy) rank = atomicAdd(hi ? &s_hi : &s_lo, 1u);
     if (wmask) wrank = atomicAdd(&s_w, uint32_t(__popc(wmask)));
+    if (wmask4) wrank4 = atomicAdd(&s_w4, uint32_t(__popc(wmask4)));
     __syncthreads();
     if (threadIdx.x == 0u)
     {
@@ -1495,6 +1527,7 @@ __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks)
         s_bhi = s_hi ? atomicAdd(&P.hf_plan_out->cnt_hi, s_hi) : 0u;
         s_blo = s_lo ? atomicAdd(&P.hf_plan_out->cnt_lo, s_lo) : 0u;
         s_bw = s_w ? atomicAdd(&P.hf_plan_out->cnt_w, s_w) : 0u;
+        s_bw4 = s_w4 ? atomicAdd(&P.hf_plan_out->cnt_w4, s_w4) : 0u;
     }
     __syncthreads();
     if (heavy)
@@ -1521,6 +1554,16 @@ __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks)
                 P.wh_mark_out[item] = P.hf_ver + 1u;
             }
         }
+        else if (wmask4 & (1u << j))
+        {
+            const uint32_t item = b * kWavesPerWG + j;
+            const uint32_t r = s_bw4 + wrank4++;
+            if (r < kWhMax)
+            {
+                P.wh_list_out[kWhMax + r] = item;
+                P.wh_mark_out[item] = (P.hf_ver + 1u) | 0x80000000u;
+            }
+        }
     // The block marks are written by a second pass over the final list, so a slot claimed by
     // both levels marks only the block whose entry survived.  That pass runs in the workgroup
     // that finishes last (a ticket after a release fence), not in a second launch: a kernel
@@ -1542,7 +1585,8 @@ __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks)
     {
         // hands the wide section's item count to the host (it sizes the section of later
         // launches) and re-arms the ticket
-        if (P.wh_host_cnt) *(volatile uint32_t *)P.wh_host_cnt = min(vp->cnt_w, kWhMax);
+        if (P.wh_host_cnt)
+            *(volatile uint32_t *)P.wh_host_cnt = P.wh_g * min(vp->cnt_w, kWhMax) + (P.wh_g == 16u ? 4u * min(vp->cnt_w4, kWhMax) : 0u);
         *P.hf_ticket = 0u;
     }
 }
@@ -1591,9 +1635,11 @@ __device__ __forceinline__ bool block_of_launch(const KParams& P, uint32_t& b, u
 // grid.cpp:258-266 keeps.  The chain per lane shrinks by G; the DDA walk is repeated G times.
 // Returns the sample's colour in every lane of the group (and stores its hit triangle for
 // rt_render_hits_device).
-template <int VAR, int G>
-__device__ __forceinline__ void wide_trace(const KParams& P, uint32_t k, uint32_t slot, uint32_t sub, float& cr,
-                                           float& cg, float& cb, uint32_t& hit_tri)
+// (G: a wave-uniform value -- 16, or 4 -- so both tiers of the wide section share one code path and
+// one register allocation; the butterfly's trip count follows it.)
+template <int VAR>
+__device__ __forceinline__ void wide_trace(const KParams& P, uint32_t k, uint32_t slot, uint32_t sub, uint32_t G,
+                                           float& cr, float& cg, float& cb, uint32_t& hit_tri)
 {
     static_assert((VAR & kVarOriginPre) && (VAR & kVarDistSkip) && (VAR & kVarPackedRem), "AUTO layout");
     const float ox = P.org[0], oy = P.org[1], oz = P.org[2];
@@ -1607,7 +1653,7 @@ __device__ __forceinline__ void wide_trace(const KParams& P, uint32_t k, uint32_
             float nct0, nct1, nct2, dt0, dt1, dt2;
             int rem0, rem1, rem2, cs0, cs1, cs2, cell;
             bool hit = false;
-            float u = 0.0f, v = 0.0f;
+            float t = 0.0f, u = 0.0f, v = 0.0f;
             uint32_t tri = 0u;
             if (dda_setup(P, ox, oy, oz, dx, dy, dz, nct0, nct1, nct2, dt0, dt1, dt2, rem0, rem1, rem2, cs0, cs1,
                           cs2, cell))
@@ -1638,7 +1684,7 @@ __device__ __forceinline__ void wide_trace(const KParams& P, uint32_t k, uint32_
                         float bt = __builtin_fminf(rtd::kFltMax, nct_ax), bu = 0.0f, bv = 0.0f;
                         uint32_t bk = 0xFFFFFFFFu;
                         const rtd::f2v ra = {dx, dy}, rc = {dy, dz};
-                        for (uint32_t k = kb + sub; k < ke; k += uint32_t(G))
+                        for (uint32_t k = kb + sub; k < ke; k += G)
                         {
                             const float4 *rp = P.frefs + size_t(k) * 4u;
                             const float4 r0 = rp[0], r1 = rp[1], r2 = rp[2], r3 = rp[3];
@@ -1658,7 +1704,7 @@ __device__ __forceinline__ void wide_trace(const KParams& P, uint32_t k, uint32_
                                 bk = take ? k : bk;
                             }
                         }
-                        for (int m = 1; m < G; m <<= 1)
+                        for (int m = 1; m < int(G); m <<= 1)
                         {
                             const float ot = __shfl_xor(bt, m, 64), ou = __shfl_xor(bu, m, 64),
                                         ov = __shfl_xor(bv, m, 64);
@@ -1675,15 +1721,7 @@ __device__ __forceinline__ void wide_trace(const KParams& P, uint32_t k, uint32_
                             v = bv;
                             tri = bk;
                             hit = true;
-                            // rt_render_records_device only: the walk's words of the record, where
-                            // the walk ends (nothing of it stays live past the loop; the pixel
-                            // again from k and slot); the colour words after the resolve
-                            if (P.recs && sub == 0u)
-                            {
-                                const ItemCoord rc = tile_slot_coord(P, k, slot);
-                                store_record(P, rc.x, rc.y, rc.s, true, __float_as_uint(P.refs[3 * size_t(bk) + 2].y),
-                                             cell_of_ref(P, bk), bt, bu, bv, __builtin_nanf(""), 0.0f, 0.0f);
-                            }
+                            t = bt;
                             break;
                         }
                     }
@@ -1691,12 +1729,14 @@ __device__ __forceinline__ void wide_trace(const KParams& P, uint32_t k, uint32_
                     {
                         // records of a miss: one cell per iteration here, so the exit step is the
                         // last one taken
+                        // rt_render_records_device only: a miss's raw record where the walk ends
+                        // (the walk state it needs stays live no further; the pixel again from k and
+                        // slot); the colour words after the resolve
                         if (P.recs && sub == 0u)
                         {
                             const ItemCoord rc = tile_slot_coord(P, k, slot);
-                            store_record(P, rc.x, rc.y, rc.s, false, 0u,
-                                         exit_voxel(remp, cell, cs0, cs1, cs2) - uint32_t(oct_offset(P, dx, dy, dz)),
-                                         0.0f, 0.0f, 0.0f, __builtin_nanf(""), 0.0f, 0.0f);
+                            store_record(P, rc.x, rc.y, rc.s, false, 0u, exit_voxel(remp, cell, cs0, cs1, cs2), 0.0f,
+                                         0.0f, 0.0f, kRecRawOct);
                         }
                         break;
                     }
@@ -1705,10 +1745,14 @@ __device__ __forceinline__ void wide_trace(const KParams& P, uint32_t k, uint32_
             else if (P.recs && sub == 0u)      // records of a ray that misses the grid
             {
                 const ItemCoord rc = tile_slot_coord(P, k, slot);
-                store_record(P, rc.x, rc.y, rc.s, false, 0u, rtd::kNoTri, 0.0f, 0.0f, 0.0f, __builtin_nanf(""), 0.0f,
-                             0.0f);
+                store_record(P, rc.x, rc.y, rc.s, false, 0u, rtd::kNoTri, 0.0f, 0.0f, 0.0f, 0u);
             }
             const KParams& Q = P;
+            if (hit && Q.recs && sub == 0u)               // a hit's raw record (records only)
+            {
+                const ItemCoord rc = tile_slot_coord(Q, k, slot);
+                store_record(Q, rc.x, rc.y, rc.s, true, tri, 0u, t, u, v, kRecRawCsr);
+            }
             if (hit)
             {
                 tri = __float_as_uint(Q.refs[3 * size_t(tri) + 2].y);     // CSR reference -> triangle id
@@ -1723,14 +1767,14 @@ __device__ __forceinline__ void wide_trace(const KParams& P, uint32_t k, uint32_
 }
 
 // One wave of the wide mode: the 64 / G consecutive sample slots slot0 .. of local tile k.
-template <int VAR, int G>
-__device__ __forceinline__ void wide_samples(const KParams& P, uint32_t k, uint32_t slot0)
+template <int VAR>
+__device__ __forceinline__ void wide_samples(const KParams& P, uint32_t k, uint32_t slot0, uint32_t G)
 {
-    const uint32_t lane = threadIdx.x & 63u, sub = lane & uint32_t(G - 1), grp = lane / uint32_t(G);
+    const uint32_t lane = threadIdx.x & 63u, sub = lane & (G - 1u), grp = lane >> (31u - __builtin_clz(G));
     const uint32_t slot = slot0 + grp;
     float cr, cg, cb;
     uint32_t hit_tri = rtd::kNoTri;
-    wide_trace<VAR, G>(P, k, slot, sub, cr, cg, cb, hit_tri);
+    wide_trace<VAR>(P, k, slot, sub, G, cr, cg, cb, hit_tri);
     // the pixel's samples are the groups grp0 .. grp0 + spp - 1 of this wave: sum in sample order
     const ItemCoord ic = tile_slot_coord(P, k, slot);
     // rt_render_hits_device / rt_render_records_device only (scalar tests of kernel parameters)
@@ -1740,7 +1784,7 @@ __device__ __forceinline__ void wide_samples(const KParams& P, uint32_t k, uint3
     float sr = 0.0f, sg = 0.0f, sb = 0.0f;
     for (uint32_t j = 0; j < P.spp; j++)
     {
-        const int src = int((grp0 + j) * uint32_t(G));
+        const int src = int((grp0 + j) * G);
         sr += __shfl(cr, src, 64);
         sg += __shfl(cg, src, 64);
         sb += __shfl(cb, src, 64);
@@ -1779,11 +1823,16 @@ template <bool BATCH, uint32_t G, bool CLK = false>
 __device__ __forceinline__ void wide_section(const KParams& P, uint32_t w)
 {
     const uint32_t n = P.hf_ver ? min(P.hf_plan_in->cnt_w, kWhMax) : 0u;
+    // the second tier (G = 16 only): 4 lanes per sample, 4 waves per item, after the first tier's
+    const uint32_t n4 = (G == 16u && P.hf_ver) ? min(P.hf_plan_in->cnt_w4, kWhMax) : 0u;
     const uint32_t nw = P.wh_wgs * kWavesPerWG;
     const uint32_t ipt = P.wg_per_tile * kWavesPerWG;              // items per tile
-    for (uint32_t e = w; e < n * G; e += nw)
+    for (uint32_t e = w; e < n * G + n4 * 4u; e += nw)
     {
-        uint32_t item = __builtin_amdgcn_readfirstlane(P.wh_list_in[e / G]);
+        const bool t4 = e >= n * G;                                 // wave-uniform
+        const uint32_t e4 = e - n * G;
+        const uint32_t li = t4 ? kWhMax + e4 / 4u : e / G;          // list entry
+        uint32_t item = __builtin_amdgcn_readfirstlane(P.wh_list_in[li]);
         uint32_t off = 0u;
         if constexpr (BATCH)
         {
@@ -1793,26 +1842,31 @@ __device__ __forceinline__ void wide_section(const KParams& P, uint32_t w)
             off = uint32_t(offsetof(KBatch, p)) + f * uint32_t(sizeof(KParams));
         }
         const uint32_t kseq = item / ipt;
-        const uint32_t slot0 = (item - kseq * ipt) * 64u + (e % G) * (64u / G);
+        const uint32_t slot0 = (item - kseq * ipt) * 64u + (t4 ? (e4 % 4u) * 16u : (e % G) * (64u / G));
         // the parameters re-read per item (late_params): hoisted out of the loop they held ~30
         // more SGPRs across it and spilled
         const KParams& Q = late_params(P, off);
         const uint32_t k = Q.tile_order ? Q.tile_order[kseq] : kseq;
+        uint64_t r0 = 0, t0 = 0;
+        if constexpr (CLK && BATCH)
+        {
+            r0 = __builtin_amdgcn_s_memrealtime();
+            t0 = __builtin_amdgcn_s_memtime();
+        }
+        wide_samples<kVarWide>(Q, k, slot0, __builtin_amdgcn_readfirstlane(t4 ? 4u : G));
         if constexpr (CLK && BATCH)
         {
             // kVarWaveClock: one record per (listed item, wave) of the section, after the batch's lane
-            // items: word 2's low bits = 0x80000000 | list position, word 3's = the launch-wide item
-            const uint64_t r0 = __builtin_amdgcn_s_memrealtime(), t0 = __builtin_amdgcn_s_memtime();
-            wide_samples<kVarWide, int(G)>(Q, k, slot0);
+            // items: word 2's low bits = 0x80000000 | 0x40000000 for the second tier | list entry,
+            // word 3's = the launch-wide item
             const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
             const KBatch& B = late_batch();
             const KParams& Q0 = late_params(P, uint32_t(offsetof(KBatch, p)));
             if ((threadIdx.x & 63u) == 0u)
-                store_wave_clock(Q0.wave_clk, B.base[B.nframes] * kWavesPerWG + e, t0, t1, r0, r1, 0x80000000u | e / G,
-                                 __builtin_amdgcn_readfirstlane(Q0.wh_list_in[e / G]));
+                store_wave_clock(Q0.wave_clk, B.base[B.nframes] * kWavesPerWG + e, t0, t1, r0, r1,
+                                 0x80000000u | (t4 ? 0x40000000u : 0u) | li,
+                                 __builtin_amdgcn_readfirstlane(Q0.wh_list_in[li]));
         }
-        else
-            wide_samples<kVarWide, int(G)>(Q, k, slot0);
     }
 }
 
@@ -1825,7 +1879,7 @@ __device__ __forceinline__ void lanes_block_wave(const KParams& P, uint32_t bid,
     if (!block_of_launch<VAR>(P, b, bid, nblk, bid == 0u && wib == 0u && (threadIdx.x & 63u) == 0u)) return;
     const uint32_t item = b * kWavesPerWG + wib;
     if constexpr ((VAR & kVarWideHeavy) != 0)
-        if (P.wh_wgs && P.hf_ver && P.wh_mark_in[item] == P.hf_ver) return;   // traced by the wide section
+        if (P.wh_wgs && P.hf_ver && (P.wh_mark_in[item] & 0x7FFFFFFFu) == P.hf_ver) return;   // the wide section's
     if constexpr ((VAR & kVarWaveClock) != 0)
     {
         // debug arm (RT_KERNEL_FLAG_WAVE_CLOCK): s_memtime at the item's start and end, and how
@@ -1916,7 +1970,7 @@ __device__ __forceinline__ void batch_block_wave(const KBatch& B, uint32_t bid, 
     if (!block_of_launch<VAR>(B.p[0], b, bid, nblk, bid == 0u && wib == 0u && (threadIdx.x & 63u) == 0u)) return;
     const uint32_t gitem = b * kWavesPerWG + wib;                    // launch-wide item
     if constexpr ((VAR & kVarWideHeavy) != 0)
-        if (B.p[0].wh_wgs && B.p[0].hf_ver && B.p[0].wh_mark_in[gitem] == B.p[0].hf_ver) return;
+        if (B.p[0].wh_wgs && B.p[0].hf_ver && (B.p[0].wh_mark_in[gitem] & 0x7FFFFFFFu) == B.p[0].hf_ver) return;
     const uint32_t f = batch_frame(B, b);
     const uint32_t off = uint32_t(offsetof(KBatch, p)) + f * uint32_t(sizeof(KParams));
     const uint32_t item = gitem - B.base[f] * kWavesPerWG;
@@ -2272,6 +2326,34 @@ __global__ void __launch_bounds__(kWG) k_trace_records(KParams P, uint32_t n)
         trace_sample<true, RT_TRI_MOLLER_TRUMBORE, kVarWaveGate | kVarDistSkip>(P, x, y, s, cr, cg, cb, ht, &P.recs[i]);
 }
 
+// rt_render_records_device: the raw records (store_record) of the rectangle made final -- a hit's CSR
+// reference becomes Grid::Intersect's tri_idx (the reference's triangle) and the cell whose list holds it
+// (the cell the hit was accepted in, grid.cpp:258-271); a miss's end cell leaves its copy of the cell
+// words (the ray's direction again, camera.h:8-47, picks the copy).  Records no launch wrote are left.
+__global__ void __launch_bounds__(kWG) k_record_fixup(KParams P, uint32_t n)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t *o = reinterpret_cast<uint32_t *>(P.recs + i);
+    const uint32_t fl = o[11];
+    if ((fl & 0xFFFF0000u) != kRecMagic) return;
+    if (fl & kRecRawCsr)
+    {
+        const uint32_t k = o[1];
+        o[1] = __float_as_uint(P.refs[3 * size_t(k) + 2].y);
+        o[2] = cell_of_ref(P, k);
+    }
+    else if (fl & (kRecRawBox | kRecRawOct))
+    {
+        const uint32_t s = i % P.spp, pix = i / P.spp;
+        const uint32_t x = P.rec_x0 + pix % P.rec_w, y = P.rec_y0 + pix / P.rec_w;
+        float dx, dy, dz;
+        rtd::dir_from_xy(P.m, P.ndcx[x * P.spp + s], P.ndcy[y * P.spp + s], dx, dy, dz);
+        o[2] -= uint32_t((fl & kRecRawBox) ? box_offset(P, dx, dy, dz) : oct_offset(P, dx, dy, dz));
+    }
+    o[11] = 0u;
+}
+
 // K3: gathered shards [rank][local tile][256] -> frame
 __global__ void __launch_bounds__(kWG) k_unshard(const uint32_t *g, uint32_t *out, uint32_t W, uint32_t H,
                                                  uint32_t tiles_x, uint32_t nranks, uint64_t shard_elems)
@@ -2545,6 +2627,9 @@ struct rt_scene
     uint32_t wh_alpha16 = 32;       // RT_WH_ALPHA16: wide threshold, sixteenths of the estimated span
     uint32_t wh_alpha16_n2 = 16;    // RT_WH_ALPHA16_N2: the same for a rank of 2 of a batched step
     uint32_t wh_alpha16_n4 = 28;    // RT_WH_ALPHA16_N4: the same for a rank of 3-7 of a batched step
+    uint32_t wh_beta16 = 0;         // RT_WH_BETA16: the second tier's threshold (4 lanes per sample),
+    uint32_t wh_beta16_n2 = 0;      // sixteenths of the span estimate, for a rank of >= 8 / of 2
+    uint32_t wh_beta16_n4 = 0;      // (RT_WH_BETA16_N2) / of 3-7 (RT_WH_BETA16_N4); 0: one tier
                                     // (measured, profiles/r03o_alpha_n2_sweep.json)
     uint32_t wh_auto_refs = 128;    // RT_WH_AUTO_REFS: AUTO takes the wide section for >= 2-rank
                                     // shards of scenes with a cell list this long
@@ -2599,6 +2684,10 @@ struct rt_scene
     uint32_t band_y1[kMaxBands] = {};
     uint32_t nbands = 0;
     hipEvent_t tile_ev[kTileBands] = {};
+    // rt_render_frame_host_tiled: the second launch stream of its row-band launches and the fork
+    // event (the frame's per-origin records ready) / join event (the other stream's work done)
+    hipStream_t stream2 = nullptr;
+    hipEvent_t ev_t_fork = nullptr, ev_t_join = nullptr;
 };
 
 namespace {
@@ -2878,7 +2967,7 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
             {
                 RT_HIP(hipMalloc(&c->plans, sizeof(HfPlan) * 2));
                 RT_HIP(hipMalloc(&c->ticket, sizeof(uint32_t)));
-                RT_HIP(hipMalloc(&c->wh_lists, sizeof(uint32_t) * 2 * kWhMax));
+                RT_HIP(hipMalloc(&c->wh_lists, sizeof(uint32_t) * 2 * 2 * kWhMax));   // [version][tier][kWhMax]
                 RT_HIP(hipHostMalloc(&c->wh_cnt, sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent));
                 RT_HIP(hipMalloc(&c->lists, sizeof(uint32_t) * 2 * kHfFrontMax));   // last: marks completion
             }
@@ -2921,7 +3010,7 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
         // Refresh: every kWhRefresh-th frame renders every item one lane per sample, so the next
         // plan re-ranks all items on lane-mode costs (the wide set is otherwise sticky).
         P.wh_g = P.spp <= 4u ? 16u : 4u;
-        const uint32_t units = P.wh_g * *(volatile uint32_t *)c->wh_cnt;
+        const uint32_t units = *(volatile uint32_t *)c->wh_cnt;         // waves: k_hf_plan counts them
         P.wh_on = 1u;
         P.wh_refresh = (c->frames - 1u) % kWhRefresh == 0u;       // frames counts this one
         P.wh_wgs = P.wh_refresh ? 0u : (units + kWavesPerWG - 1u) / kWavesPerWG;
@@ -2935,10 +3024,16 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
         P.wh_alpha16 = (P.nranks == 2u && batch != 0u)                  ? s->wh_alpha16_n2
                        : (P.nranks >= 3u && P.nranks < 8u && batch != 0u) ? s->wh_alpha16_n4
                                                                           : s->wh_alpha16;
+        // the second tier (4 lanes per sample, spp <= 4)
+        P.wh_beta16 = P.wh_g != 16u ? 0u
+                      : (P.nranks == 2u && batch != 0u)                  ? s->wh_beta16_n2
+                      : (P.nranks >= 3u && P.nranks < 8u && batch != 0u) ? s->wh_beta16_n4
+                                                                         : s->wh_beta16;
+        if (P.wh_beta16 >= P.wh_alpha16) P.wh_beta16 = 0u;
         P.wh_mark_in = c->wh_marks + size_t(v & 1u) * kWavesPerWG * c->cap_blocks;
         P.wh_mark_out = c->wh_marks + size_t((v + 1u) & 1u) * kWavesPerWG * c->cap_blocks;
-        P.wh_list_in = c->wh_lists + size_t(v & 1u) * kWhMax;
-        P.wh_list_out = c->wh_lists + size_t((v + 1u) & 1u) * kWhMax;
+        P.wh_list_in = c->wh_lists + size_t(v & 1u) * 2u * kWhMax;
+        P.wh_list_out = c->wh_lists + size_t((v + 1u) & 1u) * 2u * kWhMax;
         void *dev = nullptr;
         RT_HIP(hipHostGetDevicePointer(&dev, c->wh_cnt, 0));
         P.wh_host_cnt = static_cast<uint32_t *>(dev);
@@ -2974,7 +3069,8 @@ kfn_t lanes_kernel(int tri, int var)
 }
 
 // Launches the render kernel over region/shard described by P (tiles_x, rank, ...).
-int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_tiles, hipStream_t st)
+int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_tiles, hipStream_t st,
+                  bool order_streams = true)
 {
     if (n_local_tiles == 0) return RT_OK;
     const bool lanes = use_lanes(f, P.spp);
@@ -2987,7 +3083,8 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
     const bool grid_mt = P.isect == RT_ISECT_GRID && !bary;
     // The per-camera records (frefs) are scene state: a launch on another stream than the last
     // one waits for it, so frames of one scene never overlap on the device.
-    if (s->ev_recorded && st != s->last_stream) RT_HIP(hipStreamWaitEvent(st, s->ev1, 0));
+    // (order_streams false: the caller orders its streams itself, rt_render_frame_host_tiled)
+    if (order_streams && s->ev_recorded && st != s->last_stream) RT_HIP(hipStreamWaitEvent(st, s->ev1, 0));
     s->last_stream = st;
     // kVarXcdBands turn size: one row of this launch's tiles (ceil(tiles_x / nranks) local tiles
     // span a full frame row in shard mode).  Measured best of 1/4 .. 4 rows and 1..16 tiles:
@@ -3273,7 +3370,7 @@ int launch_batch(rt_scene *const *S, const rt_frame *F, uint32_t n, KParams *P, 
     if (clk)
     {
         // one record per lane item and per (listed item, wave) of the wide section
-        const size_t need = (size_t(blocks) * kWavesPerWG + size_t(kWhMax) * 16u) * 4u;
+        const size_t need = (size_t(blocks) * kWavesPerWG + size_t(kWhMax) * 20u) * 4u;
         if (need > s0->clk_cap)
         {
             if (s0->d_clk) RT_HIP(hipFree(s0->d_clk));
@@ -3491,6 +3588,9 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
     s->wh_alpha16 = env_tunable("RT_WH_ALPHA16", s->wh_alpha16);
     s->wh_alpha16_n2 = env_tunable("RT_WH_ALPHA16_N2", s->wh_alpha16_n2);
     s->wh_alpha16_n4 = env_tunable("RT_WH_ALPHA16_N4", s->wh_alpha16_n4);
+    s->wh_beta16 = env_tunable("RT_WH_BETA16", s->wh_beta16);
+    s->wh_beta16_n2 = env_tunable("RT_WH_BETA16_N2", s->wh_beta16 ? s->wh_beta16 : s->wh_beta16_n2);
+    s->wh_beta16_n4 = env_tunable("RT_WH_BETA16_N4", s->wh_beta16 ? s->wh_beta16 : s->wh_beta16_n4);
     s->wh_auto_refs = env_tunable("RT_WH_AUTO_REFS", s->wh_auto_refs);
     s->wh_fused = env_tunable("RT_WH_FUSED", s->wh_fused);
     s->wg64_wide = env_tunable("RT_WG64_WIDE", s->wg64_wide);
@@ -3786,6 +3886,9 @@ int rt_scene_destroy(rt_scene *s)
         for (hipEvent_t e : s->kt1) if (e) (void)hipEventDestroy(e);
         for (hipEvent_t e : s->tile_ev) if (e) (void)hipEventDestroy(e);
         if (s->stream) (void)hipStreamDestroy(s->stream);
+        if (s->stream2) (void)hipStreamDestroy(s->stream2);
+        if (s->ev_t_fork) (void)hipEventDestroy(s->ev_t_fork);
+        if (s->ev_t_join) (void)hipEventDestroy(s->ev_t_join);
 
     }
     delete s;
@@ -3955,11 +4058,33 @@ int rt_render_records_device(rt_scene *const *scenes, const rt_frame *frames, ui
             return fail(RT_E_INVALID, "record rectangle outside the frame or empty");
         ro[i] = RecOut{ d_recs[i], r.x0, r.y0, r.x1 - r.x0, r.y1 - r.y0 };
     }
-    if (n == 1) return render_device(scenes[0], &frames[0], rank, nranks, nranks > 1, d_outs[0], nullptr, hip_stream, &ro[0]);
-    for (uint32_t i = 0; i < n; i += kMaxBatch)
-        if (int rc = render_batch_chunk(scenes + i, frames + i, std::min(kMaxBatch, n - i), rank, nranks, d_outs + i,
-                                        nullptr, ro.data() + i, hip_stream))
+    if (n == 1)
+    {
+        if (int rc = render_device(scenes[0], &frames[0], rank, nranks, nranks > 1, d_outs[0], nullptr, hip_stream,
+                                   &ro[0]))
             return rc;
+    }
+    else
+        for (uint32_t i = 0; i < n; i += kMaxBatch)
+            if (int rc = render_batch_chunk(scenes + i, frames + i, std::min(kMaxBatch, n - i), rank, nranks,
+                                            d_outs + i, nullptr, ro.data() + i, hip_stream))
+                return rc;
+    // the raw records made final (k_record_fixup), per frame on the launch stream
+    for (uint32_t i = 0; i < n; i++)
+    {
+        rt_scene *s = scenes[i];
+        std::lock_guard<std::mutex> lk(s->mtx);
+        if (int rc = ensure_device(s)) return rc;
+        if (int rc = prepare_samples(s, &frames[i], std::max(1u, frames[i].spp))) return rc;
+        KParams P;
+        frame_params(s, &frames[i], P);
+        set_records(P, ro[i]);
+        const uint64_t nrec = uint64_t(ro[i].w) * ro[i].h * P.spp;
+        if (nrec > 0xFFFFFFFFull) return fail(RT_E_INVALID, "record rectangle too large");
+        hipLaunchKernelGGL(k_record_fixup, dim3(uint32_t((nrec + kWG - 1) / kWG)), dim3(kWG), 0,
+                           static_cast<hipStream_t>(hip_stream), P, uint32_t(nrec));
+        RT_HIP(hipGetLastError());
+    }
     return RT_OK;
 }
 
@@ -4138,18 +4263,97 @@ int rt_render_frame_host(rt_scene *s, const rt_frame *f, uint32_t *h_bgra, const
     return RT_OK;
 }
 
+int rt_render_frame_host_tiled(rt_scene *s, const rt_frame *f, uint32_t *h_tiles, uint32_t tiles_x, uint32_t tiles_y,
+                               uint32_t nlaunch)
+{
+    if (!s || !h_tiles || tiles_x == 0 || tiles_y == 0 || nlaunch == 0) return fail(RT_E_INVALID, "bad arguments");
+    int rc = validate_frame(f);
+    if (rc) return rc;
+    const uint32_t W = f->width, H = f->height;
+    if (tiles_y > kMaxBands) return fail(RT_E_INVALID, "more than 64 tile rows");
+    std::lock_guard<std::mutex> lk(s->mtx);
+    if ((rc = ensure_device(s))) return rc;
+    const uint32_t spp = std::max(1u, f->spp);
+    if ((rc = prepare_samples(s, f, spp))) return rc;
+    if ((rc = ensure_frame(s, size_t(W) * H, false))) return rc;
+    if (!s->stream2)
+    {
+        RT_HIP(hipStreamCreateWithFlags(&s->stream2, hipStreamNonBlocking));
+        RT_HIP(hipEventCreateWithFlags(&s->ev_t_fork, hipEventDisableTiming));
+        RT_HIP(hipEventCreateWithFlags(&s->ev_t_join, hipEventDisableTiming));
+    }
+    // Framebuffer::Resize's tile rows (framebuffer.cpp:106-117): row r spans [r * th, (r + 1) * th),
+    // the last one to H; launch j renders tile rows [j * R / n, (j + 1) * R / n)
+    const uint32_t tw = W / tiles_x, th = H / tiles_y;
+    const uint32_t nl = std::min(nlaunch, tiles_y);
+    auto row_y = [&](uint32_t r) { return r >= tiles_y ? H : r * th; };
+    hipStream_t st[2] = { s->stream, s->stream2 };
+    // both streams after everything earlier on this scene (the scene's tables and records are shared)
+    if (s->ev_recorded) RT_HIP(hipStreamWaitEvent(st[0], s->ev1, 0));
+    KParams P0;
+    frame_params(s, f, P0);
+    if (use_lanes(f, spp) && P0.isect == RT_ISECT_GRID && P0.tri_test == RT_TRI_MOLLER_TRUMBORE &&
+        ((f->kernel & RT_KERNEL_KIND_MASK) == RT_KERNEL_AUTO || (f->kernel & RT_KERNEL_KIND_MASK) == RT_KERNEL_COMPACT))
+        if ((rc = ensure_origin_terms(s, P0, st[0]))) return rc;
+    RT_HIP(hipEventRecord(s->ev_t_fork, st[0]));
+    RT_HIP(hipStreamWaitEvent(st[1], s->ev_t_fork, 0));
+    s->nbands = 0;
+    for (uint32_t j = 0; j < nl; j++)
+    {
+        const uint32_t r0 = j * tiles_y / nl, r1 = (j + 1) * tiles_y / nl;
+        const uint32_t ya = row_y(r0), yb = row_y(r1);
+        if (ya >= yb) continue;
+        KParams P = P0;
+        P.rx0 = 0; P.ry0 = ya; P.rw = W; P.rh = yb - ya;
+        P.tiles_x = (W + kTile - 1) / kTile;
+        P.rank = 0; P.nranks = 1;
+        P.out = s->d_frame; P.pitch = W; P.shard_mode = 2;
+        P.fb_tw = tw; P.fb_th = th; P.fb_tx = tiles_x; P.fb_ty = tiles_y;
+        P.fb_mtw = tw ? uint32_t(((1ull << 32) + tw - 1) / tw) : 0u;
+        P.fb_mth = th ? uint32_t(((1ull << 32) + th - 1) / th) : 0u;
+        // launches alternate between the two streams, so one launch's tail overlaps the next one's
+        // start and its tile rows' copy-back overlaps the next launch's render
+        hipStream_t sj = st[j & 1u];
+        if ((rc = launch_render(s, f, P, P.tiles_x * ((P.rh + kTile - 1) / kTile), sj, false))) return rc;
+        for (uint32_t r = r0; r < r1; r++)
+        {
+            // tile row r's buffers are bytes [y0 * W, y1 * W) of the tile layout: one contiguous copy
+            const uint32_t y0 = row_y(r), y1 = row_y(r + 1);
+            if (y0 >= y1) continue;
+            const uint32_t b = s->nbands;
+            if (!s->band_ev[b]) RT_HIP(hipEventCreateWithFlags(&s->band_ev[b], hipEventDisableTiming));
+            RT_HIP(hipMemcpyAsync(h_tiles + size_t(y0) * W, s->d_frame + size_t(y0) * W, size_t(y1 - y0) * W * 4,
+                                  hipMemcpyDeviceToHost, sj));
+            RT_HIP(hipEventRecord(s->band_ev[b], sj));
+            s->band_y1[b] = y1;
+            s->nbands = b + 1;
+        }
+    }
+    // the frame is done when both streams are: join on the first one, whose event ev1 marks it
+    RT_HIP(hipEventRecord(s->ev_t_join, st[1]));
+    RT_HIP(hipStreamWaitEvent(st[0], s->ev_t_join, 0));
+    RT_HIP(hipEventRecord(s->ev1, st[0]));
+    s->ev_recorded = true;
+    s->last_stream = st[0];
+    // bands land per tile row but not in row order across the two streams: rt_frame_host_wait(y1)
+    // needs every row below y1, so a band's wait covers the bands before it (events in row order)
+    return RT_OK;
+}
+
 int rt_frame_host_wait(rt_scene *s, uint32_t y1)
 {
     if (!s) return fail(RT_E_INVALID, "NULL argument");
-    hipEvent_t ev = nullptr;
+    hipEvent_t ev[kMaxBands];
+    uint32_t n = 0;
     {
         std::lock_guard<std::mutex> lk(s->mtx);
         if (s->nbands == 0) return fail(RT_E_INVALID, "no rt_render_frame_host in flight");
-        uint32_t b = 0;
-        while (b + 1 < s->nbands && s->band_y1[b] < y1) b++;
-        ev = s->band_ev[b];
+        // every band below y1 (rt_render_frame_host_tiled's bands land from two streams, so a later
+        // band may be done before an earlier one); a finished event costs nothing to wait on
+        while (n < s->nbands && (n == 0 || s->band_y1[n - 1] < y1)) { ev[n] = s->band_ev[n]; n++; }
     }
-    RT_HIP(hipEventSynchronize(ev));     // events are only re-recorded by a later frame
+    for (uint32_t b = 0; b < n; b++)
+        RT_HIP(hipEventSynchronize(ev[b]));     // events are only re-recorded by a later frame
     return RT_OK;
 }
 

@@ -346,7 +346,7 @@ public:
     {
         for (const auto& t : m_tiles)
             for (uint32_t y = 0; y < t.GetHeight(); y++)
-                std::memcpy(bitmap + size_t(t.y0 + y) * m_width + t.x0, &t.bgra[size_t(y) * t.GetWidth()],
+                std::memcpy(bitmap + size_t(t.y0 + y) * m_width + t.x0, t.GetBuffer() + size_t(y) * t.GetWidth(),
                             size_t(t.GetWidth()) * 4);
     }
 
@@ -356,16 +356,21 @@ protected:
         void GetPosition(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d) const { a = x0; b = y0; c = x1; d = y1; }
         uint32_t GetWidth() const { return x1 - x0; }
         uint32_t GetHeight() const { return y1 - y0; }
-        uint32_t* GetBuffer() { return &bgra[0]; }
+        // the tile's buffer: its own, or (a renderer's zero-copy frame) its view into that frame,
+        // laid out the same way (row-major at the tile's width)
+        uint32_t* GetBuffer() { return view ? view : &bgra[0]; }
+        const uint32_t* GetBuffer() const { return view ? view : &bgra[0]; }
         void SetPosition(uint32_t a, uint32_t b, uint32_t c, uint32_t d)
         {
             x0 = a; y0 = b; x1 = c; y1 = d;
+            view = nullptr;
             bgra.assign(std::max<size_t>(1, size_t(GetWidth()) * GetHeight()), 0);
             clear_pending = false;
         }
-        void Clear() { std::fill(bgra.begin(), bgra.end(), 0u); }
+        void Clear() { std::fill(GetBuffer(), GetBuffer() + size_t(GetWidth()) * GetHeight(), 0u); }
         std::mutex mtx;
         std::vector<uint32_t> bgra = std::vector<uint32_t>(1, 0);
+        uint32_t* view = nullptr;
         uint32_t x0 = 0, y0 = 0, x1 = 1, y1 = 1;
         bool clear_pending = false;                             // StartRendering's clear, deferred
     };
@@ -494,10 +499,12 @@ public:
     const std::string& LastError() const { return m_err; }
 
     // The last frame, whole, when every tile of it was delivered (else nullptr): what
-    // SaveToBMP's assembly (framebuffer.cpp:197-216) would rebuild from the tiles.
+    // SaveToBMP's assembly (framebuffer.cpp:197-216) would rebuild from the tiles.  (A tiled frame
+    // holds the tile buffers themselves: the assembly runs.)
     const uint32_t* CompleteFrame() const
     {
-        return (m_status == RT_OK && m_issued && m_tiles_done.load() == kTilesX * kTilesY) ? m_frame : nullptr;
+        return (!Tiled() && m_status == RT_OK && m_issued && m_tiles_done.load() == kTilesX * kTilesY) ? m_frame
+                                                                                                      : nullptr;
     }
 
 protected:
@@ -506,6 +513,9 @@ protected:
     // m_err.
     virtual int Issue(const rt_frame& f, uint32_t* host_frame, const uint32_t* ends, uint32_t nb) = 0;
     virtual int WaitRows(uint32_t y1) = 0;
+    // true: Issue delivers the frame as the tiles' own buffers (rt_render_frame_host_tiled's layout):
+    // the tiles are views into the page-locked frame and RenderTile copies nothing
+    virtual bool Tiled() const { return false; }
     virtual int AllocHost(size_t bytes, void** p) = 0;
     virtual void FreeHost(void* p) = 0;
 
@@ -547,10 +557,13 @@ protected:
             m_status = rc;
             return false;
         }
-        uint32_t* buf = tile.GetBuffer();
-        for (uint32_t y = 0; y < tile.GetHeight(); y++)        // renderer.cpp:133 layout
-            std::memcpy(buf + size_t(y) * tile.GetWidth(), m_frame + size_t(y0 + y) * m_width + x0,
-                        size_t(tile.GetWidth()) * 4);
+        if (!Tiled())
+        {
+            uint32_t* buf = tile.GetBuffer();
+            for (uint32_t y = 0; y < tile.GetHeight(); y++)    // renderer.cpp:133 layout
+                std::memcpy(buf + size_t(y) * tile.GetWidth(), m_frame + size_t(y0 + y) * m_width + x0,
+                            size_t(tile.GetWidth()) * 4);
+        }
         m_tiles_done.fetch_add(1);
         return true;
     }
@@ -580,6 +593,12 @@ private:
             if (rc != RT_OK) { m_status = rc; return; }
             m_frame = static_cast<uint32_t*>(p);
             m_frame_cap = words;
+        }
+        if (Tiled())
+        {
+            // the tiles' buffers are views of the frame's tile layout: tile (c, r) at word
+            // y0 * W + th_r * x0 (rt_render_frame_host_tiled), row-major at its own width
+            for (auto& t : m_tiles) t.view = m_frame + size_t(t.y0) * m_width + size_t(t.GetHeight()) * t.x0;
         }
         rt_frame f;
         std::memset(&f, 0, sizeof(f));
@@ -632,6 +651,10 @@ public:
     {
         std::memcpy(m_host_cam, host->cam, sizeof(m_host_cam));
         m_host_fov = host->fov;
+        const char* e = std::getenv("RTH_TILED");
+        m_tiled = !(e && *e == '0');
+        const char* l = std::getenv("RTH_LAUNCHES");
+        m_launches = l && *l ? std::max(1, std::atoi(l)) : 3;
     }
     ~GpuRenderer() override
     {
@@ -640,11 +663,18 @@ public:
     }
 
 protected:
+    // The zero-copy drop-in: the tile buffers are views of the page-locked frame, which the kernels
+    // write in the tiles' layout and which comes back one tile row per D2H copy, rendered in
+    // m_launches row-band launches on two streams (copies overlap the next band's render).
+    // RTH_TILED=0 keeps the row-major frame + per-tile copy (A/B arm).
     int Issue(const rt_frame& f, uint32_t* host_frame, const uint32_t* ends, uint32_t nb) override
     {
+        if (m_tiled)
+            return Check(rt_render_frame_host_tiled(m_gpu, &f, host_frame, kTilesX, kTilesY, m_launches));
         return Check(rt_render_frame_host(m_gpu, &f, host_frame, ends, nb));
     }
     int WaitRows(uint32_t y1) override { return Check(rt_frame_host_wait(m_gpu, y1)); }
+    bool Tiled() const override { return m_tiled; }
     int AllocHost(size_t bytes, void** p) override { return Check(rt_host_alloc(bytes, p)); }
     void FreeHost(void* p) override { (void)rt_host_free(p); }
 
@@ -660,6 +690,8 @@ private:
         return rc;
     }
     rt_scene* m_gpu;
+    bool m_tiled = true;
+    uint32_t m_launches = 3;    // row-band launches per frame (RTH_LAUNCHES)
 };
 
 // ================================================================= multi-GPU frame source

@@ -195,6 +195,19 @@ int  rt_render_tiles(rt_scene *scene, const rt_frame *frame, const rt_tile *tile
 int  rt_render_frame_host(rt_scene *scene, const rt_frame *frame, uint32_t *h_bgra,
                           const uint32_t *band_y1, uint32_t nbands);
 int  rt_frame_host_wait(rt_scene *scene, uint32_t y1);
+/* The drop-in's zero-copy form: the frame lands in h_tiles laid out as the tile buffers of the
+ * reference's Framebuffer (framebuffer.cpp:94-122, framebuffer.h:41-45): a tiles_x x tiles_y grid,
+ * tile (c, r) = pixels [c*tw, c < tiles_x-1 ? (c+1)*tw : width) x [r*th, r < tiles_y-1 ? (r+1)*th :
+ * height) with tw = width / tiles_x, th = height / tiles_y; the tiles' buffers back to back in tile
+ * order c + r*tiles_x, each row-major at its own width (so buffer (c, r) starts at word
+ * r*th*width + th_r*c*tw, th_r = that row's height).  A Framebuffer whose tile buffers are those
+ * views needs no copy at all: the kernels write this layout (renderer.cpp:133's buf[x + y*tileW]),
+ * and each tile row is ONE contiguous D2H copy.  The frame is rendered in `nlaunch` launches of
+ * consecutive tile rows alternating over two streams, so one launch's tile-row copies overlap the
+ * next launch's render.  Asynchronous; rt_frame_host_wait(scene, y1) as above (tile rows are
+ * y-bands).  h_tiles: width*height words of page-locked memory (rt_host_alloc). */
+int  rt_render_frame_host_tiled(rt_scene *scene, const rt_frame *frame, uint32_t *h_tiles, uint32_t tiles_x,
+                                uint32_t tiles_y, uint32_t nlaunch);
 /* Page-locked host memory (hipHostMalloc) for rt_render_frame_host. */
 int  rt_host_alloc(size_t bytes, void **out);
 int  rt_host_free(void *p);

@@ -745,6 +745,72 @@ def test_render_frame_host_bands(golden, scenes):
         pf.close()
 
 
+@pytest.mark.parametrize("sid", [1, 8])
+def test_render_frame_host_tiled(golden, scenes, sid):
+    """rt_render_frame_host_tiled (the zero-copy drop-in): the frame lands as the 12x9 Framebuffer's
+    tile buffers (framebuffer.cpp:106-117, renderer.cpp:133 layout), rendered in 1, 2, 3 or 9 row-band
+    launches on two streams; tile row r is final once rt_frame_host_wait(its y1) returns, and the
+    tiles reassemble to the reference's frame."""
+    hs, gs = scenes(sid)
+    W, H = 1920, 1080
+    want = golden["frames_1080p4"][str(sid)]["bgra_sha256"]
+    pf = rtm.PinnedFrame(W, H)
+    try:
+        flat = pf.array.reshape(-1)
+        for nl in (3, 1, 2, 9, 3):
+            flat[:] = 0xDEADBEEF
+            gs.render_frame_host_tiled(gs.frame(W, H, 4), pf, 12, 9, nl)
+            gs.wait_rows(120)
+            tiles = rtm.tile_views(flat, W, H)
+            head = [t.copy() for t in tiles[:12]]
+            gs.wait_rows(H)
+            for a, b in zip(head, tiles[:12]):
+                np.testing.assert_array_equal(a, b)
+            img = np.zeros((H, W), np.uint32)
+            for (x0, y0, x1, y1), t in zip(rtm.framebuffer_tiles(W, H), tiles):
+                img[y0:y1, x0:x1] = t
+            assert hashlib.sha256(img.tobytes()).hexdigest() == want, nl
+    finally:
+        pf.close()
+
+
+def test_render_frame_host_tiled_ragged(golden, scenes):
+    """The tile layout on frames whose 12x9 tiles are ragged or empty (width < 12 or height < 9
+    makes whole tile columns / rows empty): every small scene-1 fixture, tile by tile."""
+    hs, gs = scenes(1)
+    for fr in golden["small_frames"]:
+        if fr["scene"] != 1:
+            continue
+        W, H, spp = fr["W"], fr["H"], fr["spp"]
+        exp = read_gz(os.path.join("frames", fr["name"] + ".bgra.gz"), "<u4").reshape(H, W)
+        pf = rtm.PinnedFrame(W, H)
+        try:
+            gs.render_frame_host_tiled(gs.frame(W, H, spp), pf, 12, 9, 3)
+            gs.wait_rows(H)
+            for (x0, y0, x1, y1), t in zip(rtm.framebuffer_tiles(W, H), rtm.tile_views(pf.array.reshape(-1), W, H)):
+                np.testing.assert_array_equal(t, exp[y0:y1, x0:x1], err_msg=fr["name"])
+        finally:
+            pf.close()
+
+
+def test_framebuffer_copy_arm_equals_zero_copy(golden, scenes, monkeypatch):
+    """RTH_TILED=0 keeps the row-major frame with one copy per tile (the A/B arm of the zero-copy
+    drop-in): the same frames, BMP-assembled, on both."""
+    hs, gs = scenes(8)
+    monkeypatch.setenv("RTH_TILED", "0")
+    ra = rtm.Renderer(hs, gs)
+    monkeypatch.delenv("RTH_TILED")
+    rb = rtm.Renderer(hs, gs)
+    try:
+        for r in (ra, rb):
+            r.set_sample_count(4)
+            r.resize(1920, 1080)
+            assert hashlib.sha256(r.read().tobytes()).hexdigest() == golden["frames_1080p4"]["8"]["bgra_sha256"]
+    finally:
+        ra.close()
+        rb.close()
+
+
 def test_scene_validation_fails_loudly():
     import ctypes
     hs = rtm.HostScene.load(1)
@@ -757,7 +823,8 @@ def test_scene_validation_fails_loudly():
     assert L.rt_scene_create(ctypes.byref(d), 99, ctypes.byref(h)) == 3    # RT_E_NODEVICE
 
 
-@pytest.mark.parametrize("sid,devices", [(1, [0]), (8, [0]), (1, [0, 0]), (8, [0] * 4), (5, [0] * 8)])
+@pytest.mark.parametrize("sid,devices", [(1, [0]), (8, [0]), (1, [0, 0]), (8, [0] * 4), (5, [0] * 8),
+                                         (8, [0, 1]), (5, [0, 1, 2, 3]), (8, list(range(8)))])
 def test_multi_gpu_framebuffer(golden, sid, devices, tmp_path):
     """The native multi-GPU drop-in (rth_framebuffer_create_multi, librt_host): one rt_scene per
     rank, every rank's shard rendered on its device, one gather to devices[0], K3 un-permute and
@@ -765,7 +832,10 @@ def test_multi_gpu_framebuffer(golden, sid, devices, tmp_path):
     device; rank 0's shard moves by ncclSend / ncclRecv to itself).  Repeated devices: logical
     ranks sharing GPU 0, shards moved by device copies (RCCL takes each device once).  Frames and
     BMP bytes equal the reference's; three frames each, so the ranks' heavy-first / wide-section
-    state is exercised."""
+    state is exercised.  Distinct devices (skipped where the box has fewer): the real RCCL path, a
+    grouped ncclSend on every rank's stream and ncclRecv into device 0."""
+    if max(devices) >= rtm.device_count():
+        pytest.skip(f"needs {max(devices) + 1} GPUs")
     hs = rtm.HostScene.load(sid)
     r = rtm.Renderer.multi(hs, devices, nthreads=8)
     try:
@@ -884,6 +954,63 @@ def test_batch_same_scene_twice_and_fallback(golden, scenes):
             rtm.render_batch_device([g8, g1, g8], fs, [o.data_ptr() for o in outs], stream=st)
         torch.cuda.synchronize()
         assert [sha_dev(o) for o in outs] == [want8, want1, want8], kernels
+
+
+def test_batch_fallback_counters_and_changed_shape(golden, scenes):
+    """rt_scene_info's batch counters: a batch of one frame shape runs as ONE launch; a scene listed
+    twice with two frame shapes (its tables can hold one) falls back to a launch per frame -- outputs
+    equal either way."""
+    import torch
+    st = torch.cuda.current_stream().cuda_stream
+    hs = rtm.HostScene.load(8)
+    g = rtm.GpuScene(hs, 0)
+    try:
+        a = torch.zeros(1920 * 1080, dtype=torch.int32, device="cuda")
+        b = torch.zeros(1920 * 1080, dtype=torch.int32, device="cuda")
+        rtm.render_batch_device([g, g], [g.frame(1920, 1080, 4), g.frame(1920, 1080, 4)], [a.data_ptr(), b.data_ptr()],
+                                stream=st)
+        torch.cuda.synchronize()
+        i = g.info()
+        assert (i["batch_launches"], i["batch_fallbacks"]) == (1, 0)
+        assert sha_dev(a) == sha_dev(b) == golden["frames_1080p4"]["8"]["bgra_sha256"]
+        small = torch.zeros(200 * 150, dtype=torch.int32, device="cuda")
+        rtm.render_batch_device([g, g], [g.frame(1920, 1080, 4), g.frame(200, 150, 16)], [a.data_ptr(), small.data_ptr()],
+                                stream=st)
+        torch.cuda.synchronize()
+        i = g.info()
+        assert (i["batch_launches"], i["batch_fallbacks"]) == (1, 1)
+        assert sha_dev(a) == golden["frames_1080p4"]["8"]["bgra_sha256"]
+        exp = read_gz(os.path.join("frames", "scene8_200x150x16.bgra.gz"), "<u4")
+        np.testing.assert_array_equal(small.cpu().numpy().view(np.uint32), exp)
+    finally:
+        g.close()
+        hs.close()
+
+
+def test_batch_scenes_on_two_devices(golden):
+    """Scenes on different devices cannot share a launch: the batch takes one launch per frame, each
+    on its scene's own device, with that device's tables (nothing is prepared on another GPU)."""
+    import torch
+    if rtm.device_count() < 2:
+        pytest.skip("needs 2 GPUs")
+    h1, h8 = rtm.HostScene.load(1), rtm.HostScene.load(8)
+    g1, g8 = rtm.GpuScene(h1, 0), rtm.GpuScene(h8, 1)
+    try:
+        o1 = torch.zeros(1920 * 1080, dtype=torch.int32, device="cuda:0")
+        o8 = torch.zeros(1920 * 1080, dtype=torch.int32, device="cuda:1")
+        for _ in range(2):
+            rtm.render_batch_device([g1, g8], [g1.frame(1920, 1080, 4), g8.frame(1920, 1080, 4)],
+                                    [o1.data_ptr(), o8.data_ptr()])
+            torch.cuda.synchronize(0)
+            torch.cuda.synchronize(1)
+            assert sha_dev(o1) == golden["frames_1080p4"]["1"]["bgra_sha256"]
+            assert sha_dev(o8) == golden["frames_1080p4"]["8"]["bgra_sha256"]
+        assert g1.info()["batch_fallbacks"] == 2
+    finally:
+        g1.close()
+        g8.close()
+        h1.close()
+        h8.close()
 
 
 @pytest.mark.parametrize("spp", [1, 2, 8, 16])
