@@ -2580,6 +2580,7 @@ struct HfCtx
     uint32_t frames = 0;                // frames rendered with this shape
     uint32_t ver = 0;                   // version of the newest plan launched
     uint64_t used = 0;                  // LRU stamp
+    uint64_t cam = 0;                   // camera signature of the last frame (cam_signature)
 };
 
 } // namespace
@@ -2641,6 +2642,8 @@ struct rt_scene
     uint32_t wg64_wide = 0xA;       // RT_WG64_WIDE: bit log2(N) (3: N >= 8): one-wave workgroups also
                                     // for a rank of N's batch with a wide section
     uint32_t wh_fused_min_ranks = 2; // RT_WH_FUSED_MIN_RANKS: smallest rank count of a fused section
+    uint32_t hf_follow = 1;         // RT_HF_FOLLOW: re-plan the heavy-first order on every frame whose
+                                    // camera moved (0: every kHfPeriod-th frame only)
     bool octant_words = false;      // 8 ray-octant copies of the empty-run words (else one L-inf word)
     bool box_words = false;         // 24 box-run word copies: AUTO's empty runs (kVarSkipRun)
     // camera-space x / y tables of the current frame shape (prepare_ndc)
@@ -2930,11 +2933,26 @@ uint32_t env_tunable(const char *name, uint32_t dflt)
     return e && *e ? uint32_t(std::strtoul(e, nullptr, 0)) : dflt;
 }
 
+// The camera of a frame as one 64-bit signature (FNV-1a over the bits of the rotation, the origin
+// and the field of view): heavy-first plans are re-measured when it changes between frames.
+uint64_t cam_signature(const KParams& P, uint64_t h = 0xcbf29ce484222325ull)
+{
+    float v[13];
+    std::memcpy(v, P.m, sizeof(P.m));
+    std::memcpy(v + 9, P.org, sizeof(P.org));
+    v[12] = P.fov_xs;
+    const unsigned char *b = reinterpret_cast<const unsigned char *>(v);
+    for (size_t i = 0; i < sizeof(v); i++) h = (h ^ b[i]) * 0x100000001b3ull;
+    return h;
+}
+
 // Heavy-first state for this launch shape (AUTO): fills P.hf_*.  A new shape takes the least
 // recently used context and clears it on the launch stream (no host synchronisation).
 // batch: 0 for a single-frame launch, else an identity of the batch (its scenes and frame count).
-int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hipStream_t st, uint64_t batch = 0)
+int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hipStream_t st, uint64_t batch = 0,
+               uint64_t cam_sig = 0)
 {
+    if (!batch) cam_sig = cam_signature(P);
     const uint64_t key[5] = { (blocks << 16) | (uint64_t(P.spp) << 1) | 1u,
                               (uint64_t(P.rx0) << 32) | P.ry0, (uint64_t(P.rw) << 32) | P.rh,
                               (uint64_t(P.rank) << 40) | (uint64_t(P.nranks) << 20) | uint64_t(uint32_t(var) >> 12),
@@ -2990,7 +3008,11 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
     P.hf_ver = v;
     // measured: the first two frames (the first plan has no earlier maximum to test a tail
     // against, so it lists nothing) and then every kHfPeriod-th
-    P.hf_measure = c->frames < 2u || c->frames % kHfPeriod == 0u;
+    // ... and every frame whose camera differs from the previous frame's: a moving camera's heavy
+    // blocks move with the view, so the plan comes from the newest view (one frame old) instead of
+    // one up to kHfPeriod frames old
+    P.hf_measure = c->frames < 2u || c->frames % kHfPeriod == 0u || (s->hf_follow && cam_sig != c->cam);
+    c->cam = cam_sig;
     c->frames++;
     P.hf_floor = s->hf_floor;
     P.hf_ticket = c->ticket;
@@ -3344,8 +3366,10 @@ int launch_batch(rt_scene *const *S, const rt_frame *F, uint32_t n, KParams *P, 
     for (uint32_t i = 0; i < n; i++) ident = ident * 0x9E3779B97F4A7C15ull + uint64_t(uintptr_t(S[i]));
     rt_scene *s0 = S[0];
     const bool front = blocks >= s0->hf_min_blocks || (wide_heavy && blocks >= 64u);
+    uint64_t cams = 0xcbf29ce484222325ull;
+    for (uint32_t i = 0; i < n; i++) cams = cam_signature(P[i], cams);
     if (front || wide_heavy)
-        if (int rc = hf_prepare(s0, P[0], blocks, kvar, front, st, ident | 1u)) return rc;
+        if (int rc = hf_prepare(s0, P[0], blocks, kvar, front, st, ident | 1u, cams)) return rc;
     // fused: the wide section's workgroups lead the grid, a multiple of the XCD count so the lane
     // blocks keep their block -> XCD assignment
     if (fused && P[0].wh_wgs) P[0].wh_wgs = (P[0].wh_wgs + kXcds - 1u) & ~(kXcds - 1u);
@@ -3595,6 +3619,7 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
     s->wh_fused = env_tunable("RT_WH_FUSED", s->wh_fused);
     s->wg64_wide = env_tunable("RT_WG64_WIDE", s->wg64_wide);
     s->wh_fused_min_ranks = env_tunable("RT_WH_FUSED_MIN_RANKS", s->wh_fused_min_ranks);
+    s->hf_follow = env_tunable("RT_HF_FOLLOW", s->hf_follow);
     for (int a = 0; a < 3; a++)
     {
         s->dims[a] = g.dims[a];

@@ -21,3 +21,5 @@ run e2e 300 python -u tools/e2e_ab.py --arm "copy=;RTH_TILED=0" --arm "t1=;RTH_L
 run beta 600 python -u tools/tunable_sweep.py --env RT_WH_BETA16 --values 0 8 12 16 20 --ns 2 4 8 --rounds 2 \
     --out ${T}_beta_sweep
 RT_WH_BETA16=12 run waves_n8_b12 200 python -u tools/batch_waves.py --rank 0 --nranks 8 --frames 40 --out ${T}_waves_n8_b12
+RT_HF_FOLLOW=0 run mc_follow0 300 python -u bench.py --no-cpu-baseline --no-end-to-end --no-first-frame --steps 100 --warmup 20
+RT_HF_FOLLOW=1 run mc_follow1 300 python -u bench.py --no-cpu-baseline --no-end-to-end --no-first-frame --steps 100 --warmup 20
