@@ -84,6 +84,8 @@ constexpr int kVarAutoCore = kVarWaveGate | kVarDistSkip | kVarOriginPre | kVarX
 constexpr int kVarAuto = kVarAutoCore | kVarFastRcp | kVarPackedRem | kVarSkipRun;
 // the wide phase / wide kernel: AUTO's per-ray code, per-lane lists, no empty-run loop
 constexpr int kVarWide = kVarWaveGate | kVarDistSkip | kVarOriginPre | kVarFastRcp | kVarPackedRem | kVarXcdBands;
+// RT_KERNEL_COMPACT on AUTO's walk (box words present, rcp_safe)
+constexpr int kVarCompactBox = kVarWide | kVarSkipRun;
 constexpr uint32_t kMarchSteps = 128;       // renderer.cpp:26
 constexpr uint32_t kDistBlock = 32;         // triangles per culling block of the distance kernels
 
@@ -2113,6 +2115,10 @@ k_render_compact(KParams P, uint32_t n_items, uint32_t refill)
     bool hit = false;
     float nct0 = 0.0f, nct1 = 0.0f, nct2 = 0.0f, dt0 = 0.0f, dt1 = 0.0f, dt2 = 0.0f;
     int rem0 = 0, rem1 = 0, rem2 = 0, cs0 = 0, cs1 = 0, cs2 = 0, cell = 0, skip = 0;
+    // AUTO's box-run walk (kVarSkipRun + kVarPackedRem: box words present): packed remaining-cell
+    // counts and the lane's box counts; a lane inside its empty box steps without a lookup
+    constexpr bool BOX = RT_BOX_RUN && (VAR & kVarSkipRun) && (VAR & kVarPackedRem);
+    int remp = 0, boxw = 0;
     for (;;)
     {
         // (1) store the colours of finished samples (renderer.cpp:107-121)
@@ -2227,6 +2233,12 @@ k_render_compact(KParams P, uint32_t n_items, uint32_t refill)
                             state = 1u;
                             t = rtd::kFltMax;
                             skip = 0;
+                            if constexpr (BOX)
+                            {
+                                remp = rem0 | (rem1 << 11) | (rem2 << 22);
+                                boxw = kRemGuards;              // look the first cell up
+                                cell += box_offset(P, dx, dy, dz);
+                            }
                         }
                     }
                 }
@@ -2247,7 +2259,33 @@ k_render_compact(KParams P, uint32_t n_items, uint32_t refill)
         const uint32_t wmin = drained ? 0u : walk_min;
         do
         {
-            if (state == 1u)
+            if (BOX && state == 1u)
+            {
+                // one DDA iteration of the box-run walk (grid_intersect's, per lane: the lanes of a
+                // refilled wave are at different points of their walks, so no wave-uniform runs)
+                uint32_t kb = 0u, ke = 0u;
+                if ((boxw & kRemGuards) != 0)
+                {
+                    const uint32_t w = P.cellwb[uint32_t(cell)];
+                    const uint32_t ne = uint32_t(int(w) >> 31);
+                    kb = (w >> 11) & 0xFFFFFu;
+                    ke = kb + (w & ne & 2047u);
+                    boxw = int(w & ~ne);
+                }
+                float nct_ax;
+                bool more;
+                RT_DDA_ADVANCE_BOX(nct_ax, more);
+                uint32_t tests = 0u;
+                if (kb < ke &&
+                    test_cell<false, TRI, VAR>(P, ox, oy, oz, dx, dy, dz, kb, ke, nct_ax, t, u, v, tri, tests))
+                {
+                    state = 2u;
+                    hit = true;
+                }
+                else if (!more)                   // terminates: see grid_intersect
+                    state = 2u;
+            }
+            else if (state == 1u)
             {
                 uint32_t kb = 0u, ke = 0u;
                 if ((VAR & kVarDistSkip) && P.cellw)
@@ -3184,6 +3222,11 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
         if (bary)
             hipLaunchKernelGGL((k_render_compact<RT_TRI_BARYCENTRIC, kVarDistSkip>), grid, wg, 0, st, P, n_items,
                                refill);
+        else if (auto_runs(s) && s->rcp_safe)
+            // AUTO's walk and record test: box runs, packed counts, the Newton 1/det (the wave-uniform
+            // scalar list loop left out: its SGPRs made the persistent kernel spill to scratch)
+            hipLaunchKernelGGL((k_render_compact<RT_TRI_MOLLER_TRUMBORE, kVarCompactBox>), grid, wg, 0, st, P,
+                               n_items, refill);
         else
             hipLaunchKernelGGL((k_render_compact<RT_TRI_MOLLER_TRUMBORE, kVarWaveGate | kVarDistSkip | kVarOriginPre>),
                                grid, wg, 0, st, P, n_items, refill);
