@@ -326,6 +326,11 @@ public:
     // Blocks until every worker has finished the current frame (the reference's join).
     void Wait()
     {
+        // spin briefly first: a GPU frame ends within a millisecond, and a condition-variable wake-up
+        // costs tens of microseconds of it (the frame's last worker sets m_done_gen)
+        const uint64_t gen = m_generation_seen.load(std::memory_order_acquire);
+        for (int i = 0; i < 200000 && m_done_gen.load(std::memory_order_acquire) < gen; i++)
+            std::this_thread::yield();
         std::unique_lock<std::mutex> lk(m_pool_mtx);
         m_pool_cv.wait(lk, [&] { return m_threads_done == m_running; });
         lk.unlock();
@@ -422,6 +427,7 @@ private:
             m_running = m_num_cpus;
             m_start = std::chrono::steady_clock::now();
             m_generation++;
+            m_generation_seen.store(m_generation, std::memory_order_release);
         }
         m_pool_cv.notify_all();
     }
@@ -464,6 +470,7 @@ private:
         {
             if (!m_threads_stop)
                 m_last_frame_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - m_start).count();
+            m_done_gen.store(m_generation, std::memory_order_release);
             m_pool_cv.notify_all();
         }
     }
@@ -475,6 +482,7 @@ private:
     std::mutex m_pool_mtx;                                      // generation / done counters
     std::condition_variable m_pool_cv;
     uint64_t m_generation = 0;
+    std::atomic<uint64_t> m_generation_seen{ 0 }, m_done_gen{ 0 };   // Wait's spin phase
     uint32_t m_threads_done = 0, m_running = 0;
     bool m_shutdown = false;
     std::chrono::steady_clock::time_point m_start;
@@ -528,12 +536,20 @@ protected:
         m_frame_cap = 0;
     }
 
+    // The frame is issued here, by the thread that starts it (Resize / StartRendering), before the
+    // workers are woken: the GPU starts at once instead of after a worker's wake-up, and the workers'
+    // wake-up overlaps the render.  (A stopped frame issues nothing: RenderTile's check.)
     void BeginFrame() override
     {
         std::lock_guard<std::mutex> g(m_frame_mtx);
         m_frame_ready = false;
         m_status = RT_OK;
         m_tiles_done = 0;
+        if (!m_threads_stop && m_issue_early)
+        {
+            m_frame_ready = true;
+            IssueFrame();
+        }
     }
 
     bool RenderTile(Tile& tile) override
@@ -569,6 +585,7 @@ protected:
     }
 
     std::string m_err;
+    bool m_issue_early = true;          // RTH_ISSUE_EARLY=0: the first worker issues the frame (A/B)
 
 private:
     // A frame's copy-back may still be landing in m_frame (workers stopped early): wait it out
@@ -655,6 +672,8 @@ public:
         m_tiled = !(e && *e == '0');
         const char* l = std::getenv("RTH_LAUNCHES");
         m_launches = l && *l ? std::max(1, std::atoi(l)) : 3;
+        const char* ie = std::getenv("RTH_ISSUE_EARLY");
+        m_issue_early = !(ie && *ie == '0');
     }
     ~GpuRenderer() override
     {

@@ -74,6 +74,9 @@ def main():
     ap.add_argument("--batch", action="store_true",
                     help="the workload's frames in one rt_render_batch_device launch per step (bench.py's "
                          "step): counters per batch dispatch, stored under scenes['batch']")
+    ap.add_argument("--rank", type=int, default=0, help="--batch: rank of --nranks (one rank's batched shards)")
+    ap.add_argument("--nranks", type=int, default=1)
+    ap.add_argument("--sets", nargs="+", default=list(SETS), help="counter sets to collect (default all)")
     a = ap.parse_args()
     a.scenes, a.size = WORKLOADS[a.workload]
     if a.out is None:
@@ -85,12 +88,13 @@ def main():
     W, H, S = a.size
     keys = ["batch"] if a.batch else [str(sid) for sid in a.scenes]
     res = {k: {} for k in keys}
-    for tag, counters in SETS.items():
+    for tag, counters in [(t, SETS[t]) for t in a.sets]:
         d = os.path.join(a.work, f"{a.workload}_{tag}")
         cmd = ["timeout", "-k", "10", "300", "rocprofv3", "--pmc"] + counters.split() + [
             "--output-format", "csv", "-d", d, "-o", "run", "--",
             "python3", os.path.join(ROOT, "tools", "render_loop.py"), "--scenes", *map(str, a.scenes),
-            "--frames", str(a.frames), "--size", str(W), str(H), str(S)] + (["--batch"] if a.batch else [])
+            "--frames", str(a.frames), "--size", str(W), str(H), str(S)] + (
+            ["--batch", "--rank", str(a.rank), "--nranks", str(a.nranks)] if a.batch else [])
         with open(d + ".log", "w") as log:
             rc = subprocess.run(cmd, cwd="/tmp", env=env, stdout=log, stderr=subprocess.STDOUT).returncode
         print(f"{a.workload} {tag} rc={rc}", flush=True)
@@ -103,12 +107,18 @@ def main():
             res[k].update(m)
     for k in keys:
         c = res[k]
-        c["FETCH_SIZE_KiB"] = c.pop("FETCH_SIZE", None)
-        c["WRITE_SIZE_KiB"] = c.pop("WRITE_SIZE", None)
-        c["hbm_bytes"] = round((2 * c["FETCH_SIZE_KiB"] + c["WRITE_SIZE_KiB"]) * 1024)
-        c["valu_per_wave"] = round(c["SQ_INSTS_VALU"] / c["SQ_WAVES"], 1)
-        c["lane_util"] = round(c["SQ_THREAD_CYCLES_VALU"] / max(1.0, c["SQ_ACTIVE_INST_VALU"]), 2)
+        if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+            c["FETCH_SIZE_KiB"] = c.pop("FETCH_SIZE")
+            c["WRITE_SIZE_KiB"] = c.pop("WRITE_SIZE")
+            c["hbm_bytes"] = round((2 * c["FETCH_SIZE_KiB"] + c["WRITE_SIZE_KiB"]) * 1024)
+        if "SQ_INSTS_VALU" in c:
+            c["valu_per_wave"] = round(c["SQ_INSTS_VALU"] / c["SQ_WAVES"], 1)
+            # resident wave slots per shader engine (of 256): SQ_WAVE_CYCLES counts in quad-cycles
+            c["resident_slots_per_se"] = round(4 * c["SQ_WAVE_CYCLES"] / max(1.0, c["SQ_BUSY_CYCLES"]), 1)
+        if "SQ_THREAD_CYCLES_VALU" in c:
+            c["lane_util"] = round(c["SQ_THREAD_CYCLES_VALU"] / max(1.0, c["SQ_ACTIVE_INST_VALU"]), 2)
     out = {"source_hash": rtm.library_build_hash(), "workload": f"scenes{a.scenes}_{W}x{H}x{S}",
+           "rank": a.rank, "nranks": a.nranks,
            "workload_name": a.workload,
            "kernel": "AUTO (rt_kernel 0)" + (", batched launch (k_render_batch)" if a.batch else ""),
            "frames_per_scene": a.frames,

@@ -17,6 +17,8 @@ ap.add_argument("--frames", type=int, default=10)
 ap.add_argument("--kernel", type=lambda x: int(x, 0), default=0)
 ap.add_argument("--size", type=int, nargs=3, default=[1920, 1080, 4])
 ap.add_argument("--batch", action="store_true", help="all scenes' frames in one rt_render_batch_device launch per frame")
+ap.add_argument("--rank", type=int, default=0, help="--batch: this rank's shards of the frames")
+ap.add_argument("--nranks", type=int, default=1)
 a = ap.parse_args()
 if a.lib:
     os.environ["RT_TRACER_LIB"] = a.lib
@@ -33,11 +35,12 @@ if a.batch:
     sids = a.scenes or [a.scene]
     gs = [rtm.GpuScene(rtm.HostScene.load(sid), 0) for sid in sids]
     fs = [g.frame(W, H, S, kernel=a.kernel) for g in gs]
-    outs = [torch.empty(W * H, dtype=torch.int32, device="cuda") for _ in sids]
+    n = W * H if a.nranks == 1 else rtm.shard_elems(W, H, a.nranks)
+    outs = [torch.empty(n, dtype=torch.int32, device="cuda") for _ in sids]
     for _ in range(a.frames):
-        rtm.render_batch_device(gs, fs, [o.data_ptr() for o in outs], stream=st.cuda_stream)
+        rtm.render_batch_device(gs, fs, [o.data_ptr() for o in outs], a.rank, a.nranks, stream=st.cuda_stream)
     torch.cuda.synchronize()
-    print("batch frames", a.frames, "scenes", sids)
+    print("batch frames", a.frames, "scenes", sids, "rank", a.rank, "of", a.nranks)
     sys.exit(0)
 for sid in (a.scenes or [a.scene]):
     g = rtm.GpuScene(rtm.HostScene.load(sid), 0)
