@@ -666,6 +666,10 @@ def main():
     rtm = load_package()
     batch = args.batch == "on" or (args.batch == "auto" and world > 1)
     work = GpuWorkload(rtm, torch, world, rank, local, args.kernel, batch=batch)
+    # the per-sample counts behind the algorithmic bytes come from the debug records
+    # kernel over whole frames: gathered before the warm-up, so the timed region follows sustained
+    # GPU work (setup, not a step: the K timed steps are the same launches either way)
+    ab = {sid: algorithmic_bytes(gs, f) for sid, hs, gs, f in work.scenes} if rank == 0 else None
     elapsed = run_steps(work, world, rank, args.steps, args.warmup, dist if world > 1 else None,
                         graph=args.graph)
     kernel_ms = work.kernel_ms(args.steps)
@@ -675,7 +679,6 @@ def main():
 
     if rank == 0:
         # algorithmic bytes per launch (this rank's launch covers 1/world of the frame)
-        ab = {sid: algorithmic_bytes(gs, f) for sid, hs, gs, f in work.scenes}
         launch_bytes = {sid: ab[sid]["bytes_per_sample"] * W * H * SPP / world for sid in SCENES}
         achieved = sum(launch_bytes.values()) / (step_ms / 1e3)
         roof = valu_roofline(rtm, kernel_ms, args, world, achieved, step_ms, work)
