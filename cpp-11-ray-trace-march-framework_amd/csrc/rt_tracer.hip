@@ -227,6 +227,21 @@ __device__ __forceinline__ bool wave_all(bool p)
     return __builtin_amdgcn_ballot_w64(p) == __builtin_amdgcn_ballot_w64(true);
 }
 
+// The minimum of x over the wave's active lanes (wave-uniform): start from the first active lane's
+// value and move to the first lane below it until none is (a few rounds: each takes a strictly
+// smaller value).  A NaN x never compares below, so T may stay NaN -- callers only compare x < T.
+__device__ __forceinline__ float wave_min_active(float x)
+{
+    float T = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x)));
+    for (;;)
+    {
+        const uint64_t b = __builtin_amdgcn_ballot_w64(x < T);
+        if (b == 0u) break;
+        T = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), int(__builtin_ctzll(b))));
+    }
+    return T;
+}
+
 // v of lane (lane & ~3) + J: a DPP quad_perm broadcast within each quad of lanes (every lane of
 // the quad must be active, as in process_item's resolve, where the whole wave is)
 template <int J>
@@ -623,6 +638,14 @@ constexpr int kRemGuards = int((1u << 10) | (1u << 21) | (1u << 31));
 #ifndef RT_BOX_RUN
 #define RT_BOX_RUN 1
 #endif
+// AUTO's box runs (grid_intersect): 0 wave-uniform bare steps while every lane is inside its box
+// (lock-step), 1 per lane (each lane jumps to just before its own box exit: per-axis add chains),
+// 2 time-synchronised (every lane to the wave's lowest exit bound), 3 per lane up to the wave's
+// first contact, lock-step after it, 4 as 3 with time-synchronised runs after it, 5 as 3 with a new
+// approach whenever the whole wave is inside boxes again
+#ifndef RT_LANE_RUNS
+#define RT_LANE_RUNS 3
+#endif
 
 // The box-run walk's step: RT_DDA_ADVANCE_PACKED, with the step axis' unit also taken from the
 // box counts (boxw, build_box_words' empty-cell layout = the packed counts' layout): a count
@@ -829,6 +852,8 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, float ox, float
         int boxw = kRemGuards;                              // no box yet: look the first cell up
         const int coff = box_offset(P, dx, dy, dz);
         cell += coff;
+        constexpr int kLaneRuns = STATS ? 0 : RT_LANE_RUNS;
+        bool sync = kLaneRuns < 3;                          // wave-uniform (RT_LANE_RUNS 3-5)
         for (;;)
         {
             if (STATS) { voxel = uint32_t(cell - coff); steps++; }
@@ -843,23 +868,95 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, float ox, float
                 ke = kb + (w & ne & 2047u);
                 boxw = int(w & ~ne);
             }
+            if (kLaneRuns >= 3 && !sync)
+            {
+                // Approach (RT_LANE_RUNS 3-5): per-lane box runs up to each lane's first non-empty
+                // cell, where the lane waits (no step, no test; the cell is looked up again)
+                // until every active lane of the wave is at its own: from then on the wave walks
+                // in lock-step, so rays of a wave that cross the same cells test them together
+                // (wave-uniform lists).  Waiting changes no lane's walk, only when it is taken.
+                if (wave_all(kb < ke))
+                    sync = true;
+                else if (kb < ke)
+                {
+                    boxw = kRemGuards;
+                    continue;
+                }
+            }
             RT_DDA_ADVANCE_BOX(nct_ax, more);
             bool hit = false;
             if (kb < ke) hit = test_cell<STATS, TRI, VAR>(P, ox, oy, oz, dx, dy, dz, kb, ke, nct_ax, t, u, v, tri, tests);
             if constexpr (!STATS)
             {
-                // Wave-uniform runs while every active lane is inside its box (the boxes are clipped
-                // to the grid, so inside the box is inside the grid): blocks of 4 bare steps while
-                // every box count of every lane is >= 3 (the first three steps of a block stay
-                // inside; the fourth may leave, which the next vote sees), then single steps.  A
-                // bare step moves only the crossing times and boxw; the run's end rebuilds the
-                // cell index and the remaining-cell counts from the box counts' difference, which
-                // is sum n_a * unit_a over the run's n_a steps along axis a (n_a <= 1024, 1024,
-                // 512: no field of the difference carries).  A lane that hit holds boxw < 0
-                // (guard set), so runs only start when no lane hit.  (if + do-while: a while
-                // loop's exit edge made the compiler copy the whole walk state every iteration.)
-                if (wave_all((uint32_t(boxw) & uint32_t(kRemGuards)) == 0u))
+                const bool inside = (uint32_t(boxw) & uint32_t(kRemGuards)) == 0u;
+                const bool approach = kLaneRuns == 1 || (kLaneRuns >= 3 && !sync);
+                bool lane_run = approach && inside;
+                bool wave_run = !approach && wave_all(inside);     // wave-uniform
+                if (kLaneRuns == 5 && wave_run)
                 {
+                    // (5) the whole wave inside boxes again: a new approach
+                    lane_run = true;
+                    wave_run = false;
+                    sync = false;
+                }
+                constexpr bool kTsync = kLaneRuns == 2 || kLaneRuns == 4;
+                if (lane_run || (kTsync && wave_run))
+                {
+                    // Per-lane box runs (1; 3 before the wave's first contact).  Inside a box the
+                    // three crossing-time sequences are independent add chains
+                    // x_a(k+1) = fl(x_a(k) + dt_a), and the box is left at the first of the
+                    // (f_a + 1)-th crossings E_a = x_a(f_a) (f_a = the box field).  tl is a lower
+                    // bound of every E_a: fma(f, dt, x) is within 2^-24 |.| of x + f dt and the
+                    // chain within f 2^-24 max|x_k| <= f 2^-24 (|x| + |E|) of it, so
+                    // E_a >= e_a - (f_a + 2) 2^-23 (|e_a| + |x_a|) with room for the bound's own
+                    // roundings.  Each axis then takes its crossings below tl (at most f_a of
+                    // them): every taken crossing is < tl <= every untaken one, so these are
+                    // exactly the walk's next sum c_a steps, in some order, all inside the box
+                    // (empty cells, no test, no exit).  Bare steps then run to the box's exit
+                    // (normally one) -- the same cells, crossing times and exits as one step per
+                    // cell.  A lane that hit or left the grid holds a borrowed guard.
+                    // Time-synchronised runs (2): while every lane is inside its box, all lanes
+                    // take their crossings below the wave's lowest bound, then bare steps run
+                    // wave-uniformly to the first lane's box exit.
+                    const uint32_t b0 = uint32_t(boxw);
+                    const int f0 = boxw & 1023, f1 = (boxw >> 11) & 1023, f2 = int(uint32_t(boxw) >> 22);
+                    auto lo = [](float x, float dtv, int f) {    // (a still axis: x = FLT_MAX, dt = 0)
+                        const float e = __builtin_fmaf(float(f), dtv, x), k = float(f + 2) * 0x1p-23f;
+                        return e - __builtin_fmaf(__builtin_fabsf(x), k, __builtin_fabsf(e) * k);
+                    };
+                    float tl = __builtin_fminf(__builtin_fminf(lo(nct0, dt0, f0), lo(nct1, dt1, f1)), lo(nct2, dt2, f2));
+                    if (kTsync && wave_run) tl = wave_min_active(tl);
+                    int c0 = 0, c1 = 0, c2 = 0;
+                    while (nct0 < tl && c0 < f0) { nct0 += dt0; c0++; }
+                    while (nct1 < tl && c1 < f1) { nct1 += dt1; c1++; }
+                    while (nct2 < tl && c2 < f2) { nct2 += dt2; c2++; }
+                    boxw -= c0 + (c1 << 11) + (c2 << 22);
+                    if (kTsync && wave_run)
+                        do
+                            RT_DDA_BOX_BARE_STEP();
+                        while (wave_all((uint32_t(boxw) & uint32_t(kRemGuards)) == 0u));
+                    else
+                        do
+                            RT_DDA_BOX_BARE_STEP();
+                        while ((uint32_t(boxw) & uint32_t(kRemGuards)) == 0u);
+                    const uint32_t d = b0 - uint32_t(boxw);
+                    remp = int(uint32_t(remp) - d);           // wrapping (d may reach 2^31)
+                    cell += int(d & 2047u) * cs0 + int((d >> 11) & 2047u) * cs1 + int(d >> 22) * cs2;
+                    more = (remp & kRemGuards) == 0;
+                }
+                else if (wave_run)
+                {
+                    // Wave-uniform runs while every active lane is inside its box (the boxes are
+                    // clipped to the grid, so inside the box is inside the grid): blocks of 4 bare
+                    // steps while every box count of every lane is >= 3 (the first three steps of a
+                    // block stay inside; the fourth may leave, which the next vote sees), then
+                    // single steps.  A bare step moves only the crossing times and boxw; the run's
+                    // end rebuilds the cell index and the remaining-cell counts from the box
+                    // counts' difference, which is sum n_a * unit_a over the run's n_a steps along
+                    // axis a (n_a <= 1024, 1024, 512: no field of the difference carries).  A lane
+                    // that hit holds boxw < 0 (guard set), so runs only start when no lane hit.
+                    // (if + do-while: a while loop's exit edge made the compiler copy the whole
+                    // walk state every iteration.)
                     const uint32_t b0 = uint32_t(boxw);
                     if (wave_all((uint32_t(boxw - kBoxUnits3) & uint32_t(kRemGuards)) == 0u))
                         do

@@ -227,6 +227,68 @@ int main(int argc, char **argv)
                     uni_recs += ur_; lane_iters += li_; lane_useful += lu_; test_iters += ti_;
                     continue;
                 }
+                if (policy == 5)
+                {
+                    // hybrid: one step per lane per outer iteration (lookups as policy 2), and when
+                    // after it every active lane is inside its box, each lane jumps to its own
+                    // box's exit (per-lane add chains), instead of wave-uniform bare steps
+                    std::vector<uint32_t> pos(64, 0);
+                    int inbox[64] = {}, bcn[64][3] = {};
+                    for (;;)
+                    {
+                        std::vector<std::pair<uint32_t, uint32_t>> tl;
+                        uint32_t act = 0;
+                        for (uint32_t l = 0; l < 64; l++)
+                        {
+                            const Walk& wk = lanes[l];
+                            if (pos[l] >= wk.cell.size()) continue;
+                            act++;
+                            const uint32_t j = pos[l], c = wk.cell[j];
+                            if (!inbox[l])
+                            {
+                                l_++;
+                                if (wk.len[j]) tl.push_back({c, wk.len[j]});
+                                else
+                                {
+                                    const uint32_t w = boxw[size_t(wk.oct * 3u + wk.maj) * ncells + c];
+                                    bcn[l][0] = int(w & 1023u); bcn[l][1] = int((w >> 11) & 1023u); bcn[l][2] = int((w >> 22) & 511u);
+                                    inbox[l] = 1;
+                                }
+                            }
+                            if (j + 1 < wk.cell.size() && inbox[l])
+                                if (--bcn[l][axis_of(s, wk.cell[j], wk.cell[j + 1])] < 0) inbox[l] = 0;
+                            pos[l] = j + 1;
+                        }
+                        if (!act) break;
+                        o_++;
+                        tally(tl, ur_, li_, lu_, ti_);
+                        bool all = true; uint32_t n = 0;
+                        for (uint32_t l = 0; l < 64; l++)
+                            if (pos[l] < lanes[l].cell.size()) { n++; if (!inbox[l]) all = false; }
+                        if (!n || !all) continue;
+                        uint32_t mx_ax[3] = {0, 0, 0};
+                        for (uint32_t l = 0; l < 64; l++)
+                        {
+                            const Walk& wk = lanes[l];
+                            if (pos[l] >= wk.cell.size()) continue;
+                            uint32_t k = pos[l], nax[3] = {0, 0, 0};
+                            while (k + 1 < wk.cell.size())
+                            {
+                                const int ax = axis_of(s, wk.cell[k], wk.cell[k + 1]);
+                                k++;
+                                if (--bcn[l][ax] < 0) { inbox[l] = 0; break; }
+                                nax[ax]++;
+                            }
+                            if (k + 1 >= wk.cell.size() && inbox[l]) k = uint32_t(wk.cell.size());
+                            for (int q = 0; q < 3; q++) mx_ax[q] = std::max(mx_ax[q], nax[q]);
+                            pos[l] = k;
+                        }
+                        i_++;
+                        chain_axis += mx_ax[0] + mx_ax[1] + mx_ax[2];
+                    }
+                    uni_recs += ur_; lane_iters += li_; lane_useful += lu_; test_iters += ti_;
+                    continue;
+                }
                 // known[l] > 0: the lane's current cell is proven empty (no lookup); bc: box counts
                 int known[64] = {}, bc[64][3] = {};
                 auto advance = [&](uint32_t l, uint32_t j) {      // the step from cell j to j + 1
