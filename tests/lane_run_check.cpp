@@ -10,6 +10,8 @@
 //   g++ -O2 -std=c++11 -pthread -ffp-contract=off -I oracle tests/lane_run_check.cpp -o /tmp/lane_run_check
 //   /tmp/lane_run_check data/scenes/scene8.rtscene 1920 1080 4
 //   /tmp/lane_run_check data/scenes/scene8.rtscene random 2000000 7
+// A fifth argument 'shrink' replaces each jump's bound by a random value between the lane's next
+// crossing and the bound (a wave's lower bound: RT_LANE_RUNS 2 and 4).
 #include "../oracle/cpu_tracer.cpp"
 #include "../cpp-11-ray-trace-march-framework_amd/csrc/rt_box_words.h"
 
@@ -73,7 +75,7 @@ void ref_walk(const Scene& s, const V3 o, const V3 d, std::vector<Ev>& ev, uint3
 
 // AUTO's box-run walk with the per-lane jump, as grid_intersect writes it
 void lane_walk(const Scene& s, const std::vector<uint32_t>& boxw_all, const V3 o, const V3 d, std::vector<Ev>& ev,
-               uint32_t& last, uint64_t& taken, uint64_t& bare, uint64_t& runs)
+               uint32_t& last, uint64_t& taken, uint64_t& bare, uint64_t& runs, bool shrink, uint64_t& rng)
 {
     ev.clear(); last = ~0u;
     float nct[3], dt[3]; int pos[3], step[3], out[3];
@@ -132,7 +134,16 @@ void lane_walk(const Scene& s, const std::vector<uint32_t>& boxw_all, const V3 o
                 const float e = std::fma(float(f[a]), dt[a], nct[a]), k = float(f[a] + 2) * 1.1920928955078125e-7f;
                 lo[a] = e - std::fma(std::fabs(nct[a]), k, std::fabs(e) * k);
             }
-            const float tl = std::fmin(std::fmin(lo[0], lo[1]), lo[2]);
+            float tl = std::fmin(std::fmin(lo[0], lo[1]), lo[2]);
+            if (shrink)
+            {
+                // a wave's lower bound (time-synchronised runs) is any T <= tl: pull tl down
+                // towards the lane's next crossing by a pseudo-random fraction
+                rng = rng * 6364136223846793005ull + 1442695040888963407ull;
+                const float fr = float(rng >> 40) * (1.0f / 16777216.0f);
+                const float m = std::fmin(std::fmin(nct[0], nct[1]), nct[2]);
+                if (tl > m) tl = tl - fr * (tl - m);
+            }
             int c[3] = {0, 0, 0};
             for (int a = 0; a < 3; a++)
                 while (nct[a] < tl && c[a] < f[a]) { nct[a] += dt[a]; c[a]++; }
@@ -155,13 +166,14 @@ void lane_walk(const Scene& s, const std::vector<uint32_t>& boxw_all, const V3 o
 
 int main(int argc, char **argv)
 {
-    if (argc < 5) { std::fprintf(stderr, "usage: lane_run_check scene.rtscene (W H spp | random N seed)\n"); return 2; }
+    if (argc < 5) { std::fprintf(stderr, "usage: lane_run_check scene.rtscene (W H spp | random N seed) [shrink]\n"); return 2; }
     Scene s;
     if (!ReadScene(argv[1], s)) return 1;
     BuildGrid(s, 64);
     std::vector<uint32_t> boxw;
     rtbox::build_box_words(s.off.data(), s.dim, boxw, rtbox::kBoxRatio, rtbox::kBoxExtend, rtbox::kBoxGrow);
     const bool rnd = std::strcmp(argv[2], "random") == 0;
+    const bool shrink = argc > 5 && std::strcmp(argv[5], "shrink") == 0;   // T = any bound <= tl
     const uint32_t W = rnd ? 1024u : uint32_t(std::atoi(argv[2])), spp = rnd ? 1u : uint32_t(std::atoi(argv[4]));
     const uint32_t H = rnd ? uint32_t((std::strtoull(argv[3], nullptr, 10) + 1023) / 1024) : uint32_t(std::atoi(argv[3]));
     const uint64_t seed = rnd ? std::strtoull(argv[4], nullptr, 10) : 0;
@@ -206,7 +218,7 @@ int main(int argc, char **argv)
     for (uint32_t th = 0; th < nth; th++)
         pool.emplace_back([&]() {
             std::vector<Ev> a, b;
-            uint64_t tk = 0, br = 0, rn = 0, nr = 0, ne = 0, nb = 0;
+            uint64_t tk = 0, br = 0, rn = 0, nr = 0, ne = 0, nb = 0, rng = 0x243F6A8885A308D3ull;
             for (;;)
             {
                 const uint32_t y = next.fetch_add(1);
@@ -219,7 +231,7 @@ int main(int argc, char **argv)
                         else GenRay(s.cam, x, y, W, H, smp[2 * si], smp[2 * si + 1], s.fov, o, d);
                         uint32_t la, lb;
                         ref_walk(s, o, d, a, la);
-                        lane_walk(s, boxw, o, d, b, lb, tk, br, rn);
+                        lane_walk(s, boxw, o, d, b, lb, tk, br, rn, shrink, rng);
                         nr++;
                         ne += a.size();
                         bool ok = a.size() == b.size();

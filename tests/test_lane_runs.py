@@ -43,3 +43,12 @@ def test_lane_runs_bench_frame(tmp_path_factory, sid):
 def test_lane_runs_random_rays(tmp_path_factory, sid):
     _run(_checker(tmp_path_factory), os.path.join(ROOT, "data", "scenes", f"scene{sid}.rtscene"), "random", 1000000,
          sid + 11)
+
+
+@pytest.mark.parametrize("sid", [1, 5, 8])
+def test_lane_runs_any_lower_bound(tmp_path_factory, sid):
+    """Time-synchronised runs take each lane's crossings below the WAVE's lowest bound: any T <= the
+    lane's own bound must give the same walk (T drawn between the next crossing and the bound)."""
+    exe = _checker(tmp_path_factory)
+    _run(exe, os.path.join(ROOT, "data", "scenes", f"scene{sid}.rtscene"), 960, 540, 4, "shrink")
+    _run(exe, os.path.join(ROOT, "data", "scenes", f"scene{sid}.rtscene"), "random", 500000, sid + 3, "shrink")
