@@ -680,6 +680,17 @@ constexpr int kRemGuards = int((1u << 10) | (1u << 21) | (1u << 31));
     } while (0)
 constexpr int kBoxUnits3 = 3 | (3 << 11) | (3 << 22);   // 3 in every box-count field
 
+// A lower bound of x(f) = the add chain x, fl(x + dt), ... after f steps (a box run's exit crossing
+// along one axis; grid_intersect's per-lane runs).  Only compared against crossing times, never part
+// of a pixel's arithmetic: its two explicit FMAs (the fused f dt + x, and the margin) are the
+// only ones outside rtd::rcp_nr (tests/test_build_guard.py).  A still axis (x = FLT_MAX, dt = 0)
+// gives ~FLT_MAX.
+__device__ __forceinline__ float box_exit_bound(float x, float dtv, int f)
+{
+    const float e = __builtin_fmaf(float(f), dtv, x), k = float(f + 2) * 0x1p-23f;
+    return e - __builtin_fmaf(__builtin_fabsf(x), k, __builtin_fabsf(e) * k);
+}
+
 // Grid entry + per-axis DDA setup of Grid::Intersect (aabb.h:9-83, grid.h:44-51,
 // grid.cpp:174-216), axis arrays unrolled into scalars.  Instead of pos/step/out per axis the
 // walk keeps the cells left before 'pos == out' (rem) and the signed GridIdx stride of a step
@@ -906,7 +917,7 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, float ox, float
                     // three crossing-time sequences are independent add chains
                     // x_a(k+1) = fl(x_a(k) + dt_a), and the box is left at the first of the
                     // (f_a + 1)-th crossings E_a = x_a(f_a) (f_a = the box field).  tl is a lower
-                    // bound of every E_a: fma(f, dt, x) is within 2^-24 |.| of x + f dt and the
+                    // bound of every E_a: f dt + x fused (one rounding) is within 2^-24 |.| of it, the
                     // chain within f 2^-24 max|x_k| <= f 2^-24 (|x| + |E|) of it, so
                     // E_a >= e_a - (f_a + 2) 2^-23 (|e_a| + |x_a|) with room for the bound's own
                     // roundings.  Each axis then takes its crossings below tl (at most f_a of
@@ -920,11 +931,8 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, float ox, float
                     // wave-uniformly to the first lane's box exit.
                     const uint32_t b0 = uint32_t(boxw);
                     const int f0 = boxw & 1023, f1 = (boxw >> 11) & 1023, f2 = int(uint32_t(boxw) >> 22);
-                    auto lo = [](float x, float dtv, int f) {    // (a still axis: x = FLT_MAX, dt = 0)
-                        const float e = __builtin_fmaf(float(f), dtv, x), k = float(f + 2) * 0x1p-23f;
-                        return e - __builtin_fmaf(__builtin_fabsf(x), k, __builtin_fabsf(e) * k);
-                    };
-                    float tl = __builtin_fminf(__builtin_fminf(lo(nct0, dt0, f0), lo(nct1, dt1, f1)), lo(nct2, dt2, f2));
+                    float tl = __builtin_fminf(__builtin_fminf(box_exit_bound(nct0, dt0, f0), box_exit_bound(nct1, dt1, f1)),
+                                               box_exit_bound(nct2, dt2, f2));
                     if (kTsync && wave_run) tl = wave_min_active(tl);
                     int c0 = 0, c1 = 0, c2 = 0;
                     while (nct0 < tl && c0 < f0) { nct0 += dt0; c0++; }
@@ -4480,19 +4488,16 @@ int rt_render_frame_host_tiled(rt_scene *s, const rt_frame *f, uint32_t *h_tiles
         // start and its tile rows' copy-back overlaps the next launch's render
         hipStream_t sj = st[j & 1u];
         if ((rc = launch_render(s, f, P, P.tiles_x * ((P.rh + kTile - 1) / kTile), sj, false))) return rc;
-        for (uint32_t r = r0; r < r1; r++)
-        {
-            // tile row r's buffers are bytes [y0 * W, y1 * W) of the tile layout: one contiguous copy
-            const uint32_t y0 = row_y(r), y1 = row_y(r + 1);
-            if (y0 >= y1) continue;
-            const uint32_t b = s->nbands;
-            if (!s->band_ev[b]) RT_HIP(hipEventCreateWithFlags(&s->band_ev[b], hipEventDisableTiming));
-            RT_HIP(hipMemcpyAsync(h_tiles + size_t(y0) * W, s->d_frame + size_t(y0) * W, size_t(y1 - y0) * W * 4,
-                                  hipMemcpyDeviceToHost, sj));
-            RT_HIP(hipEventRecord(s->band_ev[b], sj));
-            s->band_y1[b] = y1;
-            s->nbands = b + 1;
-        }
+        // the launch's tile rows are words [ya * W, yb * W) of the tile layout: ONE contiguous copy
+        // (a copy per tile row cost ~14 us of launch overhead each, measured: 9 copies of a whole
+        // frame 0.50 ms vs one 0.37, profiles/r04l_e2e_breakdown.json)
+        const uint32_t b = s->nbands;
+        if (!s->band_ev[b]) RT_HIP(hipEventCreateWithFlags(&s->band_ev[b], hipEventDisableTiming));
+        RT_HIP(hipMemcpyAsync(h_tiles + size_t(ya) * W, s->d_frame + size_t(ya) * W, size_t(yb - ya) * W * 4,
+                              hipMemcpyDeviceToHost, sj));
+        RT_HIP(hipEventRecord(s->band_ev[b], sj));
+        s->band_y1[b] = yb;
+        s->nbands = b + 1;
     }
     // the frame is done when both streams are: join on the first one, whose event ev1 marks it
     RT_HIP(hipEventRecord(s->ev_t_join, st[1]));

@@ -326,6 +326,14 @@ public:
     // Blocks until every worker has finished the current frame (the reference's join).
     void Wait()
     {
+        if (m_inline_pending)
+        {
+            // a frame completed by the waiting thread itself (CompletesInline): its tiles, in tile-row
+            // order, each under its mutex as a worker would mark it
+            m_inline_pending = false;
+            FinishInline();
+            m_last_frame_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - m_start).count();
+        }
         // spin briefly first: a GPU frame ends within a millisecond, and a condition-variable wake-up
         // costs tens of microseconds of it (the frame's last worker sets m_done_gen)
         const uint64_t gen = m_generation_seen.load(std::memory_order_acquire);
@@ -384,6 +392,11 @@ protected:
     // it returned early (stop flag, renderer.cpp:76-77) and the tile keeps its cleared state.
     virtual bool RenderTile(Tile& tile) = 0;
     virtual void BeginFrame() { }
+    // true: BeginFrame produces the whole frame by itself (a GPU frame issued from the starting
+    // thread), so no worker is woken: Wait() runs FinishInline, which delivers every tile in the
+    // calling thread.  The pool's wake-ups and hand-offs cost 0.1-0.4 ms of a 0.2-0.4 ms frame.
+    virtual bool CompletesInline() const { return false; }
+    virtual void FinishInline() { }
 
     void KillAllWorkerThreads()                                 // framebuffer.cpp:30-41
     {
@@ -415,6 +428,18 @@ protected:
 private:
     void CreateWorkerThreads()                                  // framebuffer.cpp:16-28
     {
+        if (CompletesInline() && !m_threads_stop)
+        {
+            std::lock_guard<std::mutex> lk(m_pool_mtx);
+            m_start = std::chrono::steady_clock::now();
+            BeginFrame();
+            m_threads_done = m_running = 0;
+            m_generation++;
+            m_generation_seen.store(m_generation, std::memory_order_release);
+            m_done_gen.store(m_generation, std::memory_order_release);
+            m_inline_pending = true;
+            return;
+        }
         BeginFrame();
         m_work_queue.clear();
         for (uint32_t i = 0; i < kTilesX * kTilesY; i++) m_work_queue.push_back(i);
@@ -485,6 +510,7 @@ private:
     std::atomic<uint64_t> m_generation_seen{ 0 }, m_done_gen{ 0 };   // Wait's spin phase
     uint32_t m_threads_done = 0, m_running = 0;
     bool m_shutdown = false;
+    bool m_inline_pending = false;                              // CompletesInline: Wait delivers the frame
     std::chrono::steady_clock::time_point m_start;
     double m_last_frame_s = 0.0;
     uint32_t m_frame_seed = 1;
@@ -545,10 +571,39 @@ protected:
         m_frame_ready = false;
         m_status = RT_OK;
         m_tiles_done = 0;
+        m_rows_ready = 0;
         if (!m_threads_stop && m_issue_early)
         {
             m_frame_ready = true;
             IssueFrame();
+        }
+    }
+
+    // The inline delivery (RTH_POOL=0, the default): the starting thread issued the frame in
+    // BeginFrame; the waiting thread takes its tiles row by row -- one wait per tile row, then each
+    // tile of the row under its mutex, as RenderTile would (a copy only for the row-major frame).
+    bool CompletesInline() const override { return m_inline && m_issue_early; }
+    void FinishInline() override
+    {
+        for (auto& t : m_tiles)
+        {
+            if (t.y1 > m_rows_ready.load())
+            {
+                {
+                    std::lock_guard<std::mutex> g(m_frame_mtx);
+                    if (!m_frame_ready || m_status != RT_OK) return;
+                }
+                const int rc = WaitRows(t.y1);
+                if (rc != RT_OK)
+                {
+                    std::lock_guard<std::mutex> g(m_frame_mtx);
+                    m_status = rc;
+                    return;
+                }
+                m_rows_ready.store(t.y1);
+            }
+            std::lock_guard<std::mutex> g(t.mtx);
+            if (RenderTile(t)) t.clear_pending = false;
         }
     }
 
@@ -566,7 +621,7 @@ protected:
         }
         uint32_t x0, y0, x1, y1;
         tile.GetPosition(x0, y0, x1, y1);
-        const int rc = WaitRows(y1);
+        const int rc = y1 <= m_rows_ready.load() ? RT_OK : WaitRows(y1);
         if (rc != RT_OK)
         {
             std::lock_guard<std::mutex> g(m_frame_mtx);
@@ -586,6 +641,7 @@ protected:
 
     std::string m_err;
     bool m_issue_early = true;          // RTH_ISSUE_EARLY=0: the first worker issues the frame (A/B)
+    bool m_inline = true;               // RTH_POOL=1: the worker pool delivers the tiles (A/B)
 
 private:
     // A frame's copy-back may still be landing in m_frame (workers stopped early): wait it out
@@ -656,6 +712,7 @@ private:
     bool m_issued = false;
     uint32_t m_issued_h = 0;
     std::atomic<uint32_t> m_tiles_done{ 0 };
+    std::atomic<uint32_t> m_rows_ready{ 0 };                    // rows [0, m_rows_ready) known landed
     int m_status = RT_OK;
 };
 
@@ -671,9 +728,11 @@ public:
         const char* e = std::getenv("RTH_TILED");
         m_tiled = !(e && *e == '0');
         const char* l = std::getenv("RTH_LAUNCHES");
-        m_launches = l && *l ? std::max(1, std::atoi(l)) : 3;
+        m_launches = l && *l ? std::max(1, std::atoi(l)) : 1;
         const char* ie = std::getenv("RTH_ISSUE_EARLY");
         m_issue_early = !(ie && *ie == '0');
+        const char* po = std::getenv("RTH_POOL");
+        m_inline = !(po && *po == '1');
     }
     ~GpuRenderer() override
     {
@@ -710,7 +769,7 @@ private:
     }
     rt_scene* m_gpu;
     bool m_tiled = true;
-    uint32_t m_launches = 3;    // row-band launches per frame (RTH_LAUNCHES)
+    uint32_t m_launches = 1;    // row-band launches per frame (RTH_LAUNCHES)
 };
 
 // ================================================================= multi-GPU frame source

@@ -202,10 +202,11 @@ int  rt_frame_host_wait(rt_scene *scene, uint32_t y1);
  * order c + r*tiles_x, each row-major at its own width (so buffer (c, r) starts at word
  * r*th*width + th_r*c*tw, th_r = that row's height).  A Framebuffer whose tile buffers are those
  * views needs no copy at all: the kernels write this layout (renderer.cpp:133's buf[x + y*tileW]),
- * and each tile row is ONE contiguous D2H copy.  The frame is rendered in `nlaunch` launches of
- * consecutive tile rows alternating over two streams, so one launch's tile-row copies overlap the
- * next launch's render.  Asynchronous; rt_frame_host_wait(scene, y1) as above (tile rows are
- * y-bands).  h_tiles: width*height words of page-locked memory (rt_host_alloc). */
+ * and consecutive tile rows are contiguous.  The frame is rendered in `nlaunch` launches of
+ * consecutive tile rows alternating over two streams, each followed by ONE D2H copy of its rows,
+ * so one launch's copy overlaps the next launch's render (the drop-in uses 1: a whole-frame launch
+ * keeps the heavy-first order).  Asynchronous; rt_frame_host_wait(scene, y1) as above (a launch's
+ * rows are one band).  h_tiles: width*height words of page-locked memory (rt_host_alloc). */
 int  rt_render_frame_host_tiled(rt_scene *scene, const rt_frame *frame, uint32_t *h_tiles, uint32_t tiles_x,
                                 uint32_t tiles_y, uint32_t nlaunch);
 /* Page-locked host memory (hipHostMalloc) for rt_render_frame_host. */
