@@ -41,7 +41,6 @@ MESH_DATA_DIR = os.path.join(REPO, "data", "meshes")     # cornell_box_quads.txt
 RT_TRI_MOLLER_TRUMBORE, RT_TRI_BARYCENTRIC = 0, 1
 RT_KERNEL_AUTO, RT_KERNEL_LANES, RT_KERNEL_PIXEL_LOOP, RT_KERNEL_COMPACT = 0, 1, 2, 3
 RT_KERNEL_KIND_MASK = 0x07
-RT_KERNEL_FLAG_LDS_CELLS = 0x80
 RT_KERNEL_FLAG_WIDE_HEAVY = 0x200
 RT_KERNEL_FLAG_EXHAUSTIVE = 0x8000
 RT_KERNEL_FLAG_WAVE_CLOCK = 0x400000

@@ -59,8 +59,6 @@ constexpr uint32_t kTile = 16;              // shard / scheduling tile edge (pix
 constexpr uint32_t kTilePix = kTile * kTile;
 constexpr uint32_t kWG = 256;               // lanes per workgroup
 constexpr uint32_t kWavesPerWG = kWG / 64u;
-constexpr uint32_t kLdsStage = 64;          // kVarLdsCells: records per LDS chunk (4 KiB per wave)
-constexpr uint32_t kLdsMinRefs = 16;        // kVarLdsCells: shortest list staged through LDS
 // Traversal features, combined into the VAR template argument of the render kernels.
 constexpr int kVarWaveGate = 2;             // skip a test's second half when no lane needs it
 constexpr int kVarSkipRun = 4;              // wave-uniform proven-empty runs in a tight loop
@@ -74,7 +72,6 @@ constexpr int kVarPackedRem = 4096;         // one packed remaining-cells word (
 constexpr int kVarXcdBands = 8192;          // XCD-aware block -> tile order
 constexpr int kVarWaveClock = 32768;        // RT_KERNEL_FLAG_WAVE_CLOCK: per-item s_memtime (debug)
 constexpr int kVarUniform = 65536;          // scalar loop for wave-uniform cell lists
-constexpr int kVarLdsCells = 262144;        // RT_KERNEL_FLAG_LDS_CELLS: long uniform lists staged in LDS
 constexpr int kVarWideHeavy = 524288;       // RT_KERNEL_FLAG_WIDE_HEAVY: heavy items traced wide at the start
 constexpr int kVarWideFused = 1048576;      // batch kernel: the wide section's blocks lead the same grid
 constexpr int kVarWideG4 = 2097152;         // the wide section at 4 lanes per sample (spp 8-16; else 16)
@@ -334,6 +331,10 @@ typedef float vf4 __attribute__((ext_vector_type(4)));
 // are written by k_origin_pre, an earlier launch) select s_load through the scalar cache
 typedef const __attribute__((address_space(4))) vf4 cvf4;
 
+// The wide section walks AUTO's box runs with per-lane jumps (1) or the octant cube words (0)
+#ifndef RT_WIDE_BOX
+#define RT_WIDE_BOX 1
+#endif
 // The per-lane list loop of the per-camera-record test: this lane's list [kb, ke) in order
 // (grid.cpp:243-267), lowering tb on every accepted hit.  The first-half terms (r0..r2) per
 // iteration, the second-half terms (r3) only when the gate passes.  Measured against a one-ahead
@@ -406,71 +407,6 @@ __device__ __forceinline__ bool test_cell(const KParams& P, float ox, float oy, 
             if constexpr ((VAR & kVarWaveClock) != 0)
                 if (first_active_lane()) wave_counters()[0] += ke0 - kb0;
             cvf4 *crefs = (cvf4 *)P.frefs;
-            if constexpr ((VAR & kVarLdsCells) != 0)
-            {
-                // A long list (the dense cells behind the latency tail) is staged
-                // through LDS kLdsStage records at a time: the active lanes copy a chunk with all
-                // its loads in flight at once, then every lane reads each record at one uniform
-                // LDS address.  One memory round trip per chunk instead of one exposed scalar-load
-                // latency per record; same records, same order.
-                if (ke0 - kb0 >= kLdsMinRefs)
-                {
-                    __shared__ float4 s_cells[kWavesPerWG * kLdsStage * 4u];
-                    float4 *st = s_cells + (threadIdx.x >> 6) * (kLdsStage * 4u);
-                    const uint64_t act = __ballot(1);
-                    const uint32_t rank = __builtin_amdgcn_mbcnt_hi(uint32_t(act >> 32),
-                                                                    __builtin_amdgcn_mbcnt_lo(uint32_t(act), 0u));
-                    const uint32_t nact = uint32_t(__popcll(act));
-                    for (uint32_t base = kb0; base < ke0; base += kLdsStage)
-                    {
-                        const uint32_t n3 = 4u * min(kLdsStage, ke0 - base);
-                        const float4 *src = P.frefs + size_t(base) * 4u;
-                        if (act == ~0ull)
-                        {
-                            // full wave: LDS-DMA, no VGPR staging (writes base + lane x 16 B; lanes
-                            // past the chunk re-read its last float4 into unused slots)
-                            const uint32_t lane = threadIdx.x & 63u;
-                            for (uint32_t j = 0; 64u * j < n3; j++)
-                                __builtin_amdgcn_global_load_lds(
-                                    (__attribute__((address_space(1))) void *)(src + min(lane + 64u * j, n3 - 1u)),
-                                    (__attribute__((address_space(3))) void *)(st + 64u * j), 16, 0, 0);
-                        }
-                        else
-                            for (uint32_t q = rank; q < n3; q += nact)
-                                st[q] = src[q];
-                        wave_lds_sync();
-                        for (uint32_t i = 0; 4u * i < n3; i++)
-                        {
-                            // the whole record in one LDS round trip (the empty asm keeps the reads
-                            // of its second half from being sunk into the gate)
-                            const float4 r0 = st[4u * i], r1 = st[4u * i + 1u], r2 = st[4u * i + 2u],
-                                         r3 = st[4u * i + 3u];
-                            asm volatile("" ::"v"(r0.x), "v"(r0.y), "v"(r0.z), "v"(r0.w), "v"(r1.x), "v"(r1.y),
-                                         "v"(r1.z), "v"(r1.w), "v"(r2.x), "v"(r2.y), "v"(r2.z), "v"(r2.w),
-                                         "v"(r3.x), "v"(r3.y));
-                            if (STATS) tests++;
-                            float inv, cu;
-                            const bool ok1 = rtd::mt_rec_first<F>(ra, rc, rtd::f2v{r0.x, r0.y}, rtd::f2v{r0.z, r0.w},
-                                                                  rtd::f2v{r1.x, r1.y}, rtd::f2v{r1.z, r1.w},
-                                                                  rtd::f2v{r2.x, r2.y}, inv, cu);
-                            if (__any(ok1))
-                            {
-                                float cv, ct;
-                                const bool hit = ok1 & rtd::mt_rec_second(ra, rc, rtd::f2v{r2.z, r2.w}, r3.x, r3.y, inv,
-                                                                          cu, cv, ct);
-                                const bool take = hit & (ct < tb);
-                                tb = take ? ct : tb;
-                                u = take ? cu : u;
-                                v = take ? cv : v;
-                                tri = take ? base + i : tri;
-                            }
-                        }
-                        wave_lds_sync();                  // reads of this chunk before the next copy
-                    }
-                    uniform_done = true;
-                }
-            }
-            if (!uniform_done)
             {
                 // software pipeline over two register sets in turn: record k + 1 is in flight
                 // while record k is tested, with no per-record register copies (scalar loads may
@@ -1765,6 +1701,49 @@ __device__ __forceinline__ void wide_trace(const KParams& P, uint32_t k, uint32_
             if (dda_setup(P, ox, oy, oz, dx, dy, dz, nct0, nct1, nct2, dt0, dt1, dt2, rem0, rem1, rem2, cs0, cs1,
                           cs2, cell))
             {
+#if RT_WIDE_BOX
+                // AUTO's box-run walk (grid_intersect) with per-lane runs: the G lanes of a sample
+                // walk identically, and the samples of a wave share no list loop (each lane tests
+                // its own share of its sample's cell), so every group jumps through its empty
+                // boxes on its own (box_exit_bound's add chains, then the exit step)
+                int remp = rem0 | (rem1 << 11) | (rem2 << 22);
+                int boxw = kRemGuards;
+                cell += box_offset(P, dx, dy, dz);
+                for (;;)
+                {
+                    uint32_t kb = 0u, ke = 0u;
+                    float nct_ax;
+                    bool more;
+                    if ((boxw & kRemGuards) != 0)
+                    {
+                        const uint32_t w = P.cellwb[uint32_t(cell)];
+                        const uint32_t ne = uint32_t(int(w) >> 31);
+                        kb = (w >> 11) & 0xFFFFFu;
+                        ke = kb + (w & ne & 2047u);
+                        boxw = int(w & ~ne);
+                    }
+                    RT_DDA_ADVANCE_BOX(nct_ax, more);
+                    if ((uint32_t(boxw) & uint32_t(kRemGuards)) == 0u)
+                    {
+                        const uint32_t b0 = uint32_t(boxw);
+                        const int f0 = boxw & 1023, f1 = (boxw >> 11) & 1023, f2 = int(uint32_t(boxw) >> 22);
+                        const float tl = __builtin_fminf(__builtin_fminf(box_exit_bound(nct0, dt0, f0),
+                                                                         box_exit_bound(nct1, dt1, f1)),
+                                                         box_exit_bound(nct2, dt2, f2));
+                        int c0 = 0, c1 = 0, c2 = 0;
+                        while (nct0 < tl && c0 < f0) { nct0 += dt0; c0++; }
+                        while (nct1 < tl && c1 < f1) { nct1 += dt1; c1++; }
+                        while (nct2 < tl && c2 < f2) { nct2 += dt2; c2++; }
+                        boxw -= c0 + (c1 << 11) + (c2 << 22);
+                        do
+                            RT_DDA_BOX_BARE_STEP();
+                        while ((uint32_t(boxw) & uint32_t(kRemGuards)) == 0u);
+                        const uint32_t d = b0 - uint32_t(boxw);
+                        remp = int(uint32_t(remp) - d);
+                        cell += int(d & 2047u) * cs0 + int((d >> 11) & 2047u) * cs1 + int(d >> 22) * cs2;
+                        more = (remp & kRemGuards) == 0;
+                    }
+#else
                 int skip = 0;
                 int remp = rem0 | (rem1 << 11) | (rem2 << 22);
                 cell += oct_offset(P, dx, dy, dz);
@@ -1784,6 +1763,7 @@ __device__ __forceinline__ void wide_trace(const KParams& P, uint32_t k, uint32_
                     else
                         skip--;
                     RT_DDA_ADVANCE_PACKED(nct_ax, more);
+#endif
                     if (kb < ke)
                     {
                         // tb starts at the cell's exit time (test_cell's bound); a lane that takes
@@ -1834,8 +1814,8 @@ __device__ __forceinline__ void wide_trace(const KParams& P, uint32_t k, uint32_
                     }
                     if (!more)
                     {
-                        // records of a miss: one cell per iteration here, so the exit step is the
-                        // last one taken
+                        // records of a miss: the exit step is the last one taken (the lowest
+                        // borrowed guard)
                         // rt_render_records_device only: a miss's raw record where the walk ends
                         // (the walk state it needs stays live no further; the pixel again from k and
                         // slot); the colour words after the resolve
@@ -1843,7 +1823,7 @@ __device__ __forceinline__ void wide_trace(const KParams& P, uint32_t k, uint32_
                         {
                             const ItemCoord rc = tile_slot_coord(P, k, slot);
                             store_record(P, rc.x, rc.y, rc.s, false, 0u, exit_voxel(remp, cell, cs0, cs1, cs2), 0.0f,
-                                         0.0f, 0.0f, kRecRawOct);
+                                         0.0f, 0.0f, RT_WIDE_BOX ? kRecRawBox : kRecRawOct);
                         }
                         break;
                     }
@@ -2084,14 +2064,24 @@ __device__ __forceinline__ void batch_block_wave(const KBatch& B, uint32_t bid, 
     if constexpr ((VAR & kVarWaveClock) != 0)
     {
         // debug arm: the wave's clocks at its launch-wide item index (rt_debug_wave_clocks; the
-        // batch's heavy-first / wide-section machinery runs as in the product launch)
+        // batch's heavy-first / wide-section machinery runs as in the product launch), with the
+        // frame (bits 0-3) and the records it tested in wave-uniform loops (bits 4-31), and its
+        // per-lane list iterations
+        if ((threadIdx.x & 63u) == 0u)
+        {
+            wave_counters()[0] = 0u;
+            wave_counters()[1] = 0u;
+        }
+        wave_lds_sync();
         const uint64_t r0 = __builtin_amdgcn_s_memrealtime(), t0 = __builtin_amdgcn_s_memtime();
         process_item<TRI, VAR>(late_params(B.p[0], off), item, off);
         const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+        wave_lds_sync();
         const KParams& Q = late_params(B.p[0], uint32_t(offsetof(KBatch, p)));
         if ((threadIdx.x & 63u) == 0u)
         {
-            store_wave_clock(Q.wave_clk, gitem, t0, t1, r0, r1, f, 0u);
+            store_wave_clock(Q.wave_clk, gitem, t0, t1, r0, r1, f | (min(wave_counters()[0], 0x0FFFFFFFu) << 4),
+                             wave_counters()[1]);
             if (Q.hf_measure) Q.hf_cost[gitem] = uint32_t(t1 - t0);
         }
         return;
@@ -2967,7 +2957,7 @@ int prepare_samples(rt_scene *s, const rt_frame *f, uint32_t spp)
     return remember_tables(s, f, spp, tbl);
 }
 
-constexpr uint32_t kKernelFlags = RT_KERNEL_FLAG_WIDE_HEAVY | RT_KERNEL_FLAG_LDS_CELLS | RT_KERNEL_FLAG_EXHAUSTIVE |
+constexpr uint32_t kKernelFlags = RT_KERNEL_FLAG_WIDE_HEAVY | RT_KERNEL_FLAG_EXHAUSTIVE |
                                   RT_KERNEL_FLAG_WAVE_CLOCK | RT_KERNEL_BUDGET_MASK;
 
 int validate_frame(const rt_frame *f)
@@ -3226,9 +3216,6 @@ kfn_t lanes_kernel(int tri, int var)
     case kVarAutoCore: return k_render_lanes<RT_TRI_MOLLER_TRUMBORE, kVarAutoCore>;
     case kVarAuto | kVarWideHeavy: return k_render_lanes<RT_TRI_MOLLER_TRUMBORE, kVarAuto | kVarWideHeavy>;
     case kVarAuto | kVarWaveClock: return k_render_lanes<RT_TRI_MOLLER_TRUMBORE, kVarAuto | kVarWaveClock>;
-    case kVarAuto | kVarLdsCells: return k_render_lanes<RT_TRI_MOLLER_TRUMBORE, kVarAuto | kVarLdsCells>;
-    case kVarAuto | kVarLdsCells | kVarWaveClock:
-        return k_render_lanes<RT_TRI_MOLLER_TRUMBORE, kVarAuto | kVarLdsCells | kVarWaveClock>;
     default: return nullptr;
     }
 }
@@ -3264,7 +3251,6 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
     if (auto_path)
     {
         var = kVarAutoCore | (s->rcp_safe ? kVarFastRcp : 0) | (auto_runs(s) ? kVarPackedRem | kVarSkipRun : 0) |
-              ((f->kernel & RT_KERNEL_FLAG_LDS_CELLS) ? kVarLdsCells : 0) |
               ((f->kernel & RT_KERNEL_FLAG_WAVE_CLOCK) ? kVarWaveClock : 0);
         if (int rc = ensure_origin_terms(s, P, st)) return rc;
     }

@@ -98,8 +98,8 @@ enum rt_kernel {
     /* 4 was the persistent LDS-bitmap arm and 5 the all-wide kernel (both removed after losing
        their A/Bs; a frame naming them is rejected) */
     RT_KERNEL_KIND_MASK = 0x07,       /* the kernel kind above; the bits above it are flags */
-    RT_KERNEL_FLAG_LDS_CELLS = 0x80,  /* OR-able (AUTO): a wave-uniform list of >= 16 references is
-                                         staged through LDS 64 records at a time */
+    /* 0x80 was RT_KERNEL_FLAG_LDS_CELLS (long uniform lists staged through LDS; removed in round 4
+       after losing on every scene; a frame naming it is rejected) */
     RT_KERNEL_FLAG_WIDE_HEAVY = 0x200, /* OR-able (AUTO, spp <= 16; AUTO's own choice for >= 2-rank
                                           shards of dense scenes): work items that earlier frames of
                                           the same launch shape measured as heavy are traced wide (16

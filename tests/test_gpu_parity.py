@@ -286,8 +286,7 @@ def test_auto_equals_arms(golden, scenes):
     for sid in (1, 5, 8):
         hs, gs = scenes(sid)
         g = golden["frames_1080p4"][str(sid)]
-        for k in (A, A | rtm.RT_KERNEL_FLAG_LDS_CELLS, rtm.RT_KERNEL_LANES, rtm.RT_KERNEL_COMPACT,
-                  rtm.RT_KERNEL_PIXEL_LOOP):
+        for k in (A, rtm.RT_KERNEL_LANES, rtm.RT_KERNEL_COMPACT, rtm.RT_KERNEL_PIXEL_LOOP):
             hits.fill_(0x5A5A5A5A)
             gs.render_hits_device(gs.frame(1920, 1080, 4, kernel=k), 0, 1, out.data_ptr(), hits.data_ptr(), st)
             torch.cuda.synchronize()
@@ -297,10 +296,10 @@ def test_auto_equals_arms(golden, scenes):
 
 def test_removed_arms_rejected(scenes):
     """Kernel kinds and flags of arms removed after losing their A/Bs fail loudly: 4 (LDS bitmap),
-    5 (all-wide kernel), 0x10 centre-out, 0x20 static order, 0x40 16-lane wide kernel, 0x100
-    one-phase shards, 0x1000 the cooperative pair pass, bit 31 two-phase."""
+    5 (all-wide kernel), 0x10 centre-out, 0x20 static order, 0x40 16-lane wide kernel, 0x80
+    LDS-staged lists, 0x100 one-phase shards, 0x1000 the cooperative pair pass, bit 31 two-phase."""
     hs, gs = scenes(1)
-    for k in (4, 5, 0x10, 0x20, 0x40, 0x100, 0x1000, 0x80000000):
+    for k in (4, 5, 0x10, 0x20, 0x40, 0x80, 0x100, 0x1000, 0x80000000):
         with pytest.raises(rtm.RtError):
             gs.render_frame(gs.frame(32, 32, 4, kernel=k))
 
@@ -412,17 +411,6 @@ def test_hip_graph_capture_replay(golden, scenes):
         g.replay()
         torch.cuda.synchronize()
         assert hashlib.sha256(out.cpu().numpy().view(np.uint32).tobytes()).hexdigest() == want
-
-
-@pytest.mark.parametrize("sid,spp", [(5, 1), (5, 4), (5, 64), (8, 2), (8, 16), (4, 4)])
-def test_lds_cells_vs_oracle(scenes, oracle, sid, spp):
-    """LDS-staged uniform lists on ragged frames: partial waves (pixels off the frame, lanes
-    already done) take the register copy, full waves the LDS-DMA copy; frames equal the
-    reference's."""
-    hs, gs = scenes(sid)
-    exp, _, _ = oracle.render(sid, 97, 61, spp)
-    k = rtm.RT_KERNEL_AUTO | rtm.RT_KERNEL_FLAG_LDS_CELLS
-    np.testing.assert_array_equal(gs.render_frame(gs.frame(97, 61, spp, kernel=k)), exp)
 
 
 @pytest.mark.parametrize("sid,nranks", [(8, 8), (5, 8), (8, 3), (4, 16), (8, 2), (5, 4)])

@@ -71,7 +71,9 @@ def main():
     re_ = np.where(re_ < rs, re_ + (1 << 28), re_)
     cyc = (c[:, 1] - c[:, 0]).astype(np.int64)
     wide = (lo2 & 0x80000000) != 0
-    frame = np.where(wide, -1, lo2)
+    frame = np.where(wide, -1, lo2 & 15)
+    uni = np.where(wide, 0, lo2 >> 4)                  # lane waves: records tested wave-uniformly
+    lit = np.where(wide, 0, lo3)                       # ... and per-lane list iterations
     t0 = rs.min()
     s_, e_ = (rs - t0) * 10, (re_ - t0) * 10                      # ns
     d_ = e_ - s_
@@ -102,7 +104,11 @@ def main():
            "start_ns_max": int(s_.max()), "kinds": kinds, "resident_40pts": res,
            "cycles_per_ns": round(float(np.median(cyc / np.maximum(d_, 1))), 3),
            "last10": [{"kind": "wide" if wide[i] else f"lane_frame{frame[i]}", "item": int(lo3[i]) if wide[i] else None,
-                       "start_ns": int(s_[i]), "dur_ns": int(d_[i]), "xcd": int(xcd[i])} for i in order[-10:]],
+                       "start_ns": int(s_[i]), "dur_ns": int(d_[i]), "xcd": int(xcd[i]),
+                       "uniform_records": int(uni[i]), "lane_iterations": int(lit[i])} for i in order[-10:]],
+           "longest_lane_waves": [{"frame": int(frame[i]), "dur_ns": int(d_[i]), "start_ns": int(s_[i]),
+                                   "uniform_records": int(uni[i]), "lane_iterations": int(lit[i])}
+                                  for i in np.argsort(np.where(wide, -1, d_))[-12:][::-1]],
            "per_xcd_end_ns": [int(e_[xcd == x].max()) if (xcd == x).any() else None for x in range(8)],
            "batch_fallbacks": info["batch_fallbacks"]}
     line = json.dumps(out)
