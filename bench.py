@@ -405,6 +405,9 @@ class GpuWorkload:
             gs = rtm.GpuScene(hs, local)
             self.scenes.append((sid, hs, gs, gs.frame(W, H, SPP, kernel=kernel)))
         self.stream = torch.cuda.Stream()       # every launch, capture and collective of a step
+        # rank 0's assembly (K3 un-permute of the gathered shards) runs on its own stream, beside the
+        # next step's render: K3 streams the frames through HBM while the render kernel is VALU-bound
+        self.asm_stream = torch.cuda.Stream() if world > 1 and rank == 0 else None
         n = W * H if world == 1 else rtm.shard_elems(W, H, world)
         # bufs[set][scene]: two sets for N > 1, so one step's shards can be gathered while the next
         # step renders into the other set (run_steps); one set at N = 1 (nothing is gathered)
@@ -476,9 +479,9 @@ class GpuWorkload:
             gs.set_timing(TIME_EVERY)       # the timed region's launches 0, 8, 16, ... get event pairs
             gs.kernel_times()
 
-    def unshard(self, i, gathered):
+    def unshard(self, i, gathered, stream=None):
         self.rtm.unshard_device(W, H, self.world, gathered.data_ptr(), self.frames[i].data_ptr(),
-                                self.stream.cuda_stream)
+                                (stream or self.stream).cuda_stream)
 
     def sync(self):
         self.torch.cuda.synchronize()
@@ -564,15 +567,30 @@ def run_steps(work, world, rank, steps, warmup, dist=None, graph=False):
         return work.rtm.all_gather_shards(buf, world, out=gathered[p][i], async_op=True)
 
     pending = []       # the previous step's gathers: [(gathered, handle)] per scene
+    pending_set = [None]
+    asm_done = [None] * nsets      # rank 0: event after the K3s that read a set's gather buffers
     it = [0]
+    asm = getattr(work, "asm_stream", None)
 
     def finish():
-        """Wait for the pending step's gathers (a stream wait under RCCL) and un-permute them."""
-        for i, (g, h) in enumerate(pending):
-            if h is not None:
-                h.wait()
-            if rank == 0:
-                work.unshard(i, g)
+        """Wait for the pending step's gathers (a stream wait under RCCL) and un-permute them.  On
+        rank 0 both happen on the assembly stream, so K3 overlaps the next step's render."""
+        if asm is not None and pending:
+            import torch
+            with torch.cuda.stream(asm):
+                for i, (g, h) in enumerate(pending):
+                    if h is not None:
+                        h.wait()
+                    work.unshard(i, g, asm)
+                ev = torch.cuda.Event()
+                ev.record(asm)
+                asm_done[pending_set[0]] = ev
+        else:
+            for i, (g, h) in enumerate(pending):
+                if h is not None:
+                    h.wait()
+                if rank == 0:
+                    work.unshard(i, g)
         pending.clear()
 
     def step():
@@ -580,9 +598,13 @@ def run_steps(work, world, rank, steps, warmup, dist=None, graph=False):
         it[0] += 1
         work.render_all(p)
         if world > 1:
+            if asm_done[p] is not None:
+                # this set's gather buffers are refilled only after the K3s that read them
+                work.stream.wait_event(asm_done[p])
             issued = [collect(p, i) for i in range(len(SCENES))]
             finish()
             pending.extend(issued)
+            pending_set[0] = p
 
     ctx = work.stream_ctx() if hasattr(work, "stream_ctx") else contextlib.nullcontext()
     with ctx:

@@ -1,0 +1,55 @@
+#!/usr/bin/env python3
+"""Per-step device time of the bench pair from a cold start (fresh scenes, the bench's launch
+sequence: Cornell then killeroo per step), each step between its own event pair: how many steps
+the heavy-first plan and the clocks take to settle (bench.py --steps 20 --warmup 5 vs 200/100).
+
+    python3 tools/frame_series.py [--steps 60] [--out name]
+"""
+import argparse
+import importlib.util
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+spec = importlib.util.spec_from_file_location("rtm", os.path.join(ROOT, "cpp-11-ray-trace-march-framework_amd",
+                                                                  "__init__.py"))
+rtm = importlib.util.module_from_spec(spec)
+sys.modules["rtm"] = rtm
+spec.loader.exec_module(rtm)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=60)
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    torch.cuda.set_device(0)
+    st = torch.cuda.current_stream()
+    gs = [rtm.GpuScene(rtm.HostScene.load(s), 0) for s in (1, 8)]
+    fs = [g.frame(1920, 1080, 4) for g in gs]
+    outs = [torch.empty(1920 * 1080, dtype=torch.int32, device="cuda") for _ in gs]
+    ev = []
+    for i in range(a.steps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for g, f, o in zip(gs, fs, outs):
+            g.render_frame_device(f, o.data_ptr(), st.cuda_stream)
+        e1.record(st)
+        ev.append((e0, e1))
+    torch.cuda.synchronize()
+    ms = [round(x.elapsed_time(y), 4) for x, y in ev]
+    for g in gs:
+        g.close()
+    res = {"steps": a.steps, "step_ms": ms,
+           "mean_steps_5_25": round(sum(ms[5:25]) / 20, 4), "mean_steps_last20": round(sum(ms[-20:]) / 20, 4)}
+    print(json.dumps(res))
+    if a.out:
+        with open(os.path.join(ROOT, "gpurun_out", a.out + ".json"), "w") as fh:
+            fh.write(json.dumps(res) + "\n")
+
+
+if __name__ == "__main__":
+    main()
