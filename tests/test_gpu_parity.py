@@ -436,6 +436,51 @@ def test_shard_partition_dense_scenes(golden, scenes, sid, nranks):
     assert hashlib.sha256(img.tobytes()).hexdigest() == golden["frames_1080p4"][str(sid)]["bgra_sha256"]
 
 
+def _batched_rank_frames(golden, nranks, frames=6):
+    """Six batched rank-of-N steps of the bench pair from fresh scenes (the environment's tunables);
+    returns the newest plan's wide-section wave count after checking both assembled frames."""
+    import torch
+    hss = [rtm.HostScene.load(s) for s in (1, 8)]
+    gss = [rtm.GpuScene(h, 0) for h in hss]
+    try:
+        W, H = 1920, 1080
+        fs = [g.frame(W, H, 4) for g in gss]
+        e = rtm.shard_elems(W, H, nranks)
+        gathered = [torch.zeros(nranks * e, dtype=torch.int32, device="cuda") for _ in gss]
+        stream = torch.cuda.current_stream().cuda_stream
+        waves = 0
+        for _ in range(frames):
+            for r in range(nranks):
+                rtm.render_batch_device(gss, fs, [g.data_ptr() + 4 * r * e for g in gathered], r, nranks,
+                                        stream=stream)
+            torch.cuda.synchronize()
+            waves = max(waves, gss[0].wide_items())
+        for sid, g in zip((1, 8), gathered):
+            out = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+            rtm.unshard_device(W, H, nranks, g.data_ptr(), out.data_ptr(), stream)
+            torch.cuda.synchronize()
+            assert hashlib.sha256(out.cpu().numpy().tobytes()).hexdigest() == \
+                golden["frames_1080p4"][str(sid)]["bgra_sha256"], (sid, nranks)
+        return waves
+    finally:
+        for g in gss:
+            g.close()
+        for h in hss:
+            h.close()
+
+
+@pytest.mark.parametrize("nranks,beta", [(8, 20), (4, 16), (2, 12)])
+def test_second_wide_tier_batched_frames(golden, nranks, beta, monkeypatch):
+    """The wide section's second tier (RT_WH_BETA16: items between beta/16 and alpha/16 of the span
+    estimate traced 4 lanes per sample, after the first tier's 16): the bench pair's
+    batched rank-of-N launches over 6 frames, both partitions reassembled into the reference
+    frames, with the tier listing items (more section waves than without it)."""
+    base = _batched_rank_frames(golden, nranks)
+    monkeypatch.setenv("RT_WH_BETA16", str(beta))
+    tiered = _batched_rank_frames(golden, nranks)
+    assert tiered > base, (base, tiered)
+
+
 @pytest.mark.parametrize("sid,nranks,kernel", [(8, 8, 0), (5, 4, 0), (8, 2, 0x200), (5, 1, 0x200), (8, 4, 0)])
 def test_wide_heavy_shard_frames(golden, scenes, sid, nranks, kernel, monkeypatch):
     """RT_KERNEL_FLAG_WIDE_HEAVY over consecutive frames of every rank: frames 0-1 render one
