@@ -688,22 +688,22 @@ def main():
     rtm = load_package()
     batch = args.batch == "on" or (args.batch == "auto" and world > 1)
     work = GpuWorkload(rtm, torch, world, rank, local, args.kernel, batch=batch)
-    # The supplementary legs of the line (first frame, the drop-in end to end, the orbiting camera)
-    # and the per-sample counts behind the algorithmic bytes (the debug records kernel
-    # over whole frames) run BEFORE the warm-up, so the timed steps follow sustained GPU work as a
-    # serving GPU's would: after the idle host setup (scene tables, box words) a 5-step warm-up
-    # leaves the clocks ramping through the first ~30 timed steps (0.60 -> 0.55 ms per step from a
-    # cold start, 0.55 from the first step right after other GPU work: profiles/r04t_frame_series_cold.json,
-    # r04final_series_burn.json).  The K timed steps are the same launches either way.
+    # The per-sample counts behind the algorithmic bytes (the debug records kernel over
+    # whole frames, reduced on the host) first; then the supplementary legs that keep the GPU busy
+    # (the drop-in end to end, the orbiting camera) run BEFORE the warm-up, so the timed steps follow
+    # sustained GPU work as a serving GPU's would: after an idle host phase (scene tables, box
+    # words, the counts' reduction) a 5-step warm-up leaves the clocks ramping through the first ~30
+    # timed steps (0.60 -> 0.55 ms per step from a cold start, 0.55 from the first step right after
+    # other GPU work: profiles/r04t_frame_series_cold.json, r04final_series_burn.json).  The K timed
+    # steps are the same launches either way.  (first_frame makes fresh scenes -- host setup, an idle
+    # GPU -- so it runs after the timed region.)
+    ab = {sid: algorithmic_bytes(gs, f) for sid, hs, gs, f in work.scenes} if rank == 0 else None
     extra = {}
     if rank == 0 and world == 1:
-        if args.workload == "bench" and not args.no_first_frame:
-            extra["first_frame_ms"] = first_frame(rtm, torch)
         if args.workload == "bench" and not args.no_end_to_end:
             extra["end_to_end"] = end_to_end(rtm, work)
         if not args.graph and not args.no_moving_camera:
             extra["moving_camera"] = moving_camera(work, args.steps, min(args.warmup, 20), None)
-    ab = {sid: algorithmic_bytes(gs, f) for sid, hs, gs, f in work.scenes} if rank == 0 else None
     elapsed = run_steps(work, world, rank, args.steps, args.warmup, dist if world > 1 else None,
                         graph=args.graph)
     kernel_ms = work.kernel_ms(args.steps)
@@ -766,8 +766,8 @@ def main():
             mc = extra["moving_camera"]
             mc["vs_static"] = round(elapsed / args.steps * 1e3 / mc["ms_per_step"], 4)
             out["moving_camera"] = mc
-        if "first_frame_ms" in extra:
-            out["first_frame_ms"] = extra["first_frame_ms"]
+        if world == 1 and args.workload == "bench" and not args.no_first_frame:
+            out["first_frame_ms"] = first_frame(rtm, torch)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline()
         print(json.dumps(out), flush=True)
