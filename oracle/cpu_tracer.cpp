@@ -840,4 +840,18 @@ void orc_kat_shade(const float *in, uint32_t n, float *out)
     }
 }
 
+// orc_render with another camera (Scene::GetCameraParameters' matrix and fov replaced): the same
+// restated tile pool over a copy of the scene (test infrastructure: custom-view parity of the
+// product walk -- cameras inside the grid, axis-aligned views)
+int orc_render_cam(const orc_scene *h, uint32_t W, uint32_t H, uint32_t spp, const float *cam16, float fov,
+                   uint32_t *out, uint32_t *hit_ids)
+{
+    if (!h || !cam16) return 1;
+    orc_scene c = *h;
+    std::memcpy(&c.s.cam[0][0], cam16, 64);
+    c.s.fov = fov;
+    double sec = 0.0;
+    return orc_render(&c, W, H, spp, 0, 0, out, hit_ids, &sec);
+}
+
 } // extern "C"

@@ -58,6 +58,10 @@ int        orc_scene_mesh(const orc_scene *s, float *vertices, uint32_t *triangl
  * hit_ids (optional, W*H*spp): tri index per sample or 0xFFFFFFFF.  seconds = pool span. */
 int orc_render(const orc_scene *s, uint32_t W, uint32_t H, uint32_t spp, uint32_t tri_test,
                uint32_t nthreads, uint32_t *out_bgra, uint32_t *hit_ids, double *seconds);
+/* orc_render (Grid::Intersect, Moller-Trumbore) from another camera: cam16 = the view matrix as
+ * Scene::GetCameraParameters returns it, fov in degrees. */
+int orc_render_cam(const orc_scene *s, uint32_t W, uint32_t H, uint32_t spp, const float *cam16, float fov,
+                   uint32_t *out_bgra, uint32_t *hit_ids);
 /* Per-sample records for the pixel rectangle [x0,x0+w) x [y0,y0+h), order (y, x, s). */
 int orc_trace_samples(const orc_scene *s, uint32_t W, uint32_t H, uint32_t spp, uint32_t tri_test,
                       uint32_t x0, uint32_t y0, uint32_t w, uint32_t h, orc_rec *out);

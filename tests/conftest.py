@@ -75,6 +75,7 @@ class Oracle:
         L.orc_scene_csr.argtypes = [vp, vp, vp]
         L.orc_render.argtypes = [vp] + [ctypes.c_uint32] * 5 + [vp, vp, ctypes.POINTER(ctypes.c_double)]
         L.orc_trace_samples.argtypes = [vp] + [ctypes.c_uint32] * 8 + [vp]
+        L.orc_render_cam.argtypes = [vp] + [ctypes.c_uint32] * 3 + [vp, ctypes.c_float, vp, vp]
         for fn in ("orc_kat_ray_tri", "orc_kat_ray_aabb", "orc_kat_genray", "orc_kat_bgra8",
                    "orc_kat_shade", "orc_kat_dist"):
             getattr(L, fn).argtypes = [vp, ctypes.c_uint32, vp]
@@ -110,6 +111,15 @@ class Oracle:
                                ctypes.c_void_p(hid.ctypes.data) if hits else None, ctypes.byref(sec))
         assert rc == 0
         return out.reshape(H, W), (hid if hits else None), sec.value
+
+    def render_cam(self, sid, W, H, spp, cam16, fov):
+        """orc_render from another camera (view matrix cam16, fov degrees): (frame, hit ids)."""
+        out = np.zeros(W * H, np.uint32)
+        hid = np.zeros(W * H * spp, np.uint32)
+        cam = np.ascontiguousarray(cam16, np.float32)
+        assert self.L.orc_render_cam(self.scene(sid), W, H, spp, ctypes.c_void_p(cam.ctypes.data), float(fov),
+                                     ctypes.c_void_p(out.ctypes.data), ctypes.c_void_p(hid.ctypes.data)) == 0
+        return out.reshape(H, W), hid
 
     def records(self, sid, W, H, spp, x0, y0, w, h, tri_test=0):
         rtm = load_package()

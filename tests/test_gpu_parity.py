@@ -436,6 +436,73 @@ def test_shard_partition_dense_scenes(golden, scenes, sid, nranks):
     assert hashlib.sha256(img.tobytes()).hexdigest() == golden["frames_1080p4"][str(sid)]["bgra_sha256"]
 
 
+def _custom_views(info):
+    """Views that stress the walk: the camera inside the grid looking straight down -z (the middle
+    column's and row's first samples have exactly-zero direction components: still axes), the same
+    turned 90 degrees about y (down -x), the scene's camera orbited 37 degrees (bench.py's orbit), and
+    a corner of the grid's box looking across it (BuildLookAtMatrix)."""
+    lo, hi = np.array(info.aabb_min[:], np.float32), np.array(info.aabb_max[:], np.float32)
+    ctr = (lo + hi) * np.float32(0.5)
+    down_z = np.eye(4, dtype=np.float32)
+    down_z[3, :3] = ctr + np.float32(0.1) * (hi - lo)
+    rot = np.array([[0, 0, 1, 0], [0, 1, 0, 0], [-1, 0, 0, 0], [0, 0, 0, 1]], np.float32)
+    down_x = rot.copy()
+    down_x[3, :3] = ctr - np.float32(0.2) * (hi - lo)
+    a = np.deg2rad(37.0)
+    ry = np.array([[np.cos(a), 0, -np.sin(a), 0], [0, 1, 0, 0], [np.sin(a), 0, np.cos(a), 0], [0, 0, 0, 1]])
+    orbit = (np.array(info.cam[:], np.float64).reshape(4, 4) @ ry).astype(np.float32)
+    corner = rtm.look_at(lo - np.float32(0.3) * (hi - lo), ctr).reshape(4, 4)
+    return {"inside_down_z": down_z.reshape(16), "inside_down_x": down_x.reshape(16),
+            "orbit37": orbit.reshape(16), "corner": corner.reshape(16)}
+
+
+@pytest.mark.parametrize("sid", [1, 5, 8])
+def test_custom_views_vs_oracle(scenes, oracle, sid):
+    """AUTO (box runs, per-lane jumps up to the first contact, lock-step after) from views the
+    scenes' own cameras never take -- inside the grid, axis-aligned, orbited, from a corner -- frame
+    and per-sample hit triangles equal to the oracle's Grid::Intersect walk from the same view."""
+    import torch
+    hs, gs = scenes(sid)
+    info = oracle.info(sid)
+    W, H, SPP = 256, 144, 4
+    out = torch.empty(W * H, dtype=torch.int32, device="cuda")
+    hits = torch.empty(W * H * SPP, dtype=torch.int32, device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    for name, cam in _custom_views(info).items():
+        f = gs.frame(W, H, SPP)
+        for k in range(16):
+            f.cam[k] = float(cam[k])
+        exp, exp_hits = oracle.render_cam(sid, W, H, SPP, cam, info.fov)
+        for rep in range(2):                         # a new origin, then the same one again
+            hits.fill_(0x5A5A5A5A)
+            gs.render_hits_device(f, 0, 1, out.data_ptr(), hits.data_ptr(), st)
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32).reshape(H, W), exp, err_msg=name)
+            np.testing.assert_array_equal(hits.cpu().numpy().view(np.uint32), exp_hits, err_msg=name)
+
+
+def test_custom_view_full_frame_one_wave_kernel(scenes, oracle):
+    """The orbited view of killeroo at the bench's 1920x1080x4 (the one-wave-workgroup kernel and the
+    heavy-first order from its second frame on): frames and hit triangles equal the oracle's."""
+    import torch
+    hs, gs = scenes(8)
+    info = oracle.info(8)
+    W, H, SPP = 1920, 1080, 4
+    cam = _custom_views(info)["orbit37"]
+    f = gs.frame(W, H, SPP)
+    for k in range(16):
+        f.cam[k] = float(cam[k])
+    exp, exp_hits = oracle.render_cam(8, W, H, SPP, cam, info.fov)
+    out = torch.empty(W * H, dtype=torch.int32, device="cuda")
+    hits = torch.empty(W * H * SPP, dtype=torch.int32, device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    for rep in range(4):
+        gs.render_hits_device(f, 0, 1, out.data_ptr(), hits.data_ptr(), st)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy().view(np.uint32).reshape(H, W), exp), rep
+        assert np.array_equal(hits.cpu().numpy().view(np.uint32), exp_hits), rep
+
+
 def _batched_rank_frames(golden, nranks, frames=6):
     """Six batched rank-of-N steps of the bench pair from fresh scenes (the environment's tunables);
     returns the newest plan's wide-section wave count after checking both assembled frames."""

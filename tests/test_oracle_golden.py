@@ -139,3 +139,14 @@ def test_full_frame_record_shas(oracle, golden, sid):
     assert h(rec[:, 5:8]) == g["tuv_sha256"]
     assert h(rec[:, 2]) == g["voxel_sha256"]
     assert h(rec[:, 8:11]) == g["rgb_sha256"]
+
+
+def test_oracle_render_cam_with_own_camera_equals_render(oracle):
+    """orc_render_cam (test infrastructure for custom views) with the scene's own camera and fov
+    reproduces orc_render: same frame, same hit ids."""
+    for sid in (1, 8):
+        i = oracle.info(sid)
+        exp, hid, _ = oracle.render(sid, 64, 36, 4, hits=True)
+        got, ghid = oracle.render_cam(sid, 64, 36, 4, np.array(i.cam[:], np.float32), i.fov)
+        np.testing.assert_array_equal(got, exp)
+        np.testing.assert_array_equal(ghid, hid)
