@@ -616,25 +616,13 @@ constexpr int kRemGuards = int((1u << 10) | (1u << 21) | (1u << 31));
     } while (0)
 constexpr int kBoxUnits3 = 3 | (3 << 11) | (3 << 22);   // 3 in every box-count field
 
-// A lower bound of every axis' box-exit crossing x_a(f_a) = the add chain x_a, fl(x_a + dt_a), ...
-// after f_a steps (grid_intersect's per-lane runs).  With every crossing time >= 0 the chain is
-// >= (x + f dt)(1 - 2^-24)^f and the fused e = fl(f dt + x) <= (x + f dt)(1 + 2^-24), so
-// x(f) >= e (1 - (f + 1) 2^-24) >= e (1 - 2^-14) (f <= 1023): min_a e_a (1 - 2^-13), rounded once,
-// lies below them all.  A negative crossing time (a ray entering the grid a rounding past a wall)
-// gets -inf: no chain, the bare steps take the box.  A still axis (x = FLT_MAX, dt = 0) gives
-// FLT_MAX; an infinite dt a NaN or inf that the minimum skips.  Only compared against crossing
-// times, never part of a pixel's arithmetic: its explicit FMA is the only one outside rtd::rcp_nr
-// (tests/test_build_guard.py; the exactness argument is replayed in tests/lane_run_check.cpp).
-__device__ __forceinline__ float box_exit_bound(float x0, float x1, float x2, float dt0, float dt1, float dt2,
-                                                int f0, int f1, int f2)
+// A lower bound of x(f) = the add chain x, fl(x + dt), ... after f steps (a box run's exit crossing
+// along one axis; grid_intersect's per-lane runs).  Only compared against crossing times, never part
+// of a pixel's arithmetic: its two explicit FMAs (the fused f dt + x, and the margin) are the
+// only ones outside rtd::rcp_nr (tests/test_build_guard.py).  A still axis (x = FLT_MAX, dt = 0)
+// gives ~FLT_MAX.
+__device__ __forceinline__ float box_exit_bound(float x, float dtv, int f)
 {
-    auto fused = [](float x, float dtv, int f) { return __builtin_fmaf(float(f), dtv, x); };
-    const float m = __builtin_fminf(__builtin_fminf(fused(x0, dt0, f0), fused(x1, dt1, f1)), fused(x2, dt2, f2));
-    return (x0 >= 0.0f && x1 >= 0.0f && x2 >= 0.0f) ? m * (1.0f - 0x1p-13f) : -__builtin_inff();
-}
-__device__ __forceinline__ float box_exit_bound_axis(float x, float dtv, int f)
-{   // one axis' bound, any sign: the chain is within f 2^-24 (|x| + |e|) of the fused e, which is
-    // within 2^-24 |e| of x + f dt (the wide section's walk)
     const float e = __builtin_fmaf(float(f), dtv, x), k = float(f + 2) * 0x1p-23f;
     return e - __builtin_fmaf(__builtin_fabsf(x), k, __builtin_fabsf(e) * k);
 }
@@ -671,18 +659,23 @@ __device__ __forceinline__ bool dda_setup(const KParams& P, float ox, float oy, 
     const int pos0 = to_voxel(gx, 0), pos1 = to_voxel(gy, 1), pos2 = to_voxel(gz, 2);
     dt0 = dt1 = dt2 = 0.0f;
     rem0 = rem1 = rem2 = cs0 = cs1 = cs2 = 0;
-    // Both signs through ONE division each, no branch (a wave whose rays point both ways along an
-    // axis ran both branches' divisions): the crossing's wall is ToPos(pos + 1) for d > 0 and
-    // ToPos(pos) for d < 0, the same expression either way, and -cw / d == cw / |d| bit for bit
-    // (IEEE division is sign-symmetric).  A still axis (d == 0) selects FLT_MAX / 0 afterwards.
     auto setup = [&](float d, float g, int pos, int a, int stride, float& nct, float& dtv, int& rem, int& cs) {
-        const bool up = d > 0.0f, still = d == 0.0f;
-        const float q = ((P.bmin[a] + float(pos + (up ? 1 : 0)) * P.cw) - g) / d;
-        const float dd = P.cw / __builtin_fabsf(d);
-        nct = still ? rtd::kFltMax : enter_t + q;
-        dtv = still ? 0.0f : dd;
-        rem = still ? 0 : (up ? P.dim[a] - 1 - pos : pos);    // steps until pos + 1 == dim / pos - 1 == -1
-        cs = still ? 0 : (up ? stride : -stride);
+        if (d == 0.0f)
+            nct = rtd::kFltMax;
+        else if (d > 0.0f)
+        {
+            nct = enter_t + ((P.bmin[a] + float(pos + 1) * P.cw) - g) / d;
+            dtv = P.cw / d;
+            rem = P.dim[a] - 1 - pos;           // steps until pos + 1 == dim
+            cs = stride;
+        }
+        else
+        {
+            nct = enter_t + ((P.bmin[a] + float(pos) * P.cw) - g) / d;
+            dtv = -P.cw / d;
+            rem = pos;                          // steps until pos - 1 == -1
+            cs = -stride;
+        }
     };
     setup(dx, gx, pos0, 0, 1, nct0, dt0, rem0, cs0);
     setup(dy, gy, pos1, 1, P.dxdz, nct1, dt1, rem1, cs1);
@@ -874,7 +867,8 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, float ox, float
                     // wave-uniformly to the first lane's box exit.
                     const uint32_t b0 = uint32_t(boxw);
                     const int f0 = boxw & 1023, f1 = (boxw >> 11) & 1023, f2 = int(uint32_t(boxw) >> 22);
-                    float tl = box_exit_bound(nct0, nct1, nct2, dt0, dt1, dt2, f0, f1, f2);
+                    float tl = __builtin_fminf(__builtin_fminf(box_exit_bound(nct0, dt0, f0), box_exit_bound(nct1, dt1, f1)),
+                                               box_exit_bound(nct2, dt2, f2));
                     if (kTsync && wave_run) tl = wave_min_active(tl);
                     int c0 = 0, c1 = 0, c2 = 0;
                     while (nct0 < tl && c0 < f0) { nct0 += dt0; c0++; }
@@ -1733,11 +1727,9 @@ __device__ __forceinline__ void wide_trace(const KParams& P, uint32_t k, uint32_
                     {
                         const uint32_t b0 = uint32_t(boxw);
                         const int f0 = boxw & 1023, f1 = (boxw >> 11) & 1023, f2 = int(uint32_t(boxw) >> 22);
-                        // (the per-axis bound: the fused kernel's register allocation holds 64 VGPRs
-                        // with it, 72 with box_exit_bound's shared form)
-                        const float tl = __builtin_fminf(__builtin_fminf(box_exit_bound_axis(nct0, dt0, f0),
-                                                                         box_exit_bound_axis(nct1, dt1, f1)),
-                                                         box_exit_bound_axis(nct2, dt2, f2));
+                        const float tl = __builtin_fminf(__builtin_fminf(box_exit_bound(nct0, dt0, f0),
+                                                                         box_exit_bound(nct1, dt1, f1)),
+                                                         box_exit_bound(nct2, dt2, f2));
                         int c0 = 0, c1 = 0, c2 = 0;
                         while (nct0 < tl && c0 < f0) { nct0 += dt0; c0++; }
                         while (nct1 < tl && c1 < f1) { nct1 += dt1; c1++; }

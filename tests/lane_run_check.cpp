@@ -11,8 +11,7 @@
 //   /tmp/lane_run_check data/scenes/scene8.rtscene 1920 1080 4
 //   /tmp/lane_run_check data/scenes/scene8.rtscene random 2000000 7
 // A fifth argument 'shrink' replaces each jump's bound by a random value between the lane's next
-// crossing and the bound (a wave's lower bound: RT_LANE_RUNS 2 and 4); 'axis' uses the per-axis
-// bound of the wide section's walk (box_exit_bound_axis) instead of box_exit_bound.
+// crossing and the bound (a wave's lower bound: RT_LANE_RUNS 2 and 4).
 #include "../oracle/cpu_tracer.cpp"
 #include "../cpp-11-ray-trace-march-framework_amd/csrc/rt_box_words.h"
 
@@ -76,8 +75,7 @@ void ref_walk(const Scene& s, const V3 o, const V3 d, std::vector<Ev>& ev, uint3
 
 // AUTO's box-run walk with the per-lane jump, as grid_intersect writes it
 void lane_walk(const Scene& s, const std::vector<uint32_t>& boxw_all, const V3 o, const V3 d, std::vector<Ev>& ev,
-               uint32_t& last, uint64_t& taken, uint64_t& bare, uint64_t& runs, bool shrink, bool axis_bound,
-               uint64_t& rng)
+               uint32_t& last, uint64_t& taken, uint64_t& bare, uint64_t& runs, bool shrink, uint64_t& rng)
 {
     ev.clear(); last = ~0u;
     float nct[3], dt[3]; int pos[3], step[3], out[3];
@@ -130,26 +128,13 @@ void lane_walk(const Scene& s, const std::vector<uint32_t>& boxw_all, const V3 o
             runs++;
             const uint32_t b0 = boxw;
             const int f[3] = {int(boxw & 1023u), int((boxw >> 11) & 1023u), int(boxw >> 22)};
-            // box_exit_bound (csrc/rt_tracer.hip): with every crossing time >= 0 the chain after f
-            // adds is >= e (1 - (f + 1) 2^-24) >= e (1 - 2^-14) for the fused e = f dt + x (f <= 1023),
-            // so min_a e_a (1 - 2^-13), rounded, lies below every exit crossing; a negative crossing
-            // time (a ray that entered the grid a rounding before a wall) takes no chain
-            float e[3];
-            for (int a = 0; a < 3; a++) e[a] = std::fma(float(f[a]), dt[a], nct[a]);
-            const bool nonneg = nct[0] >= 0.0f && nct[1] >= 0.0f && nct[2] >= 0.0f;
-            float tl = nonneg ? std::fmin(std::fmin(e[0], e[1]), e[2]) * (1.0f - 1.220703125e-4f)
-                              : -std::numeric_limits<float>::infinity();
-            if (axis_bound)
+            float lo[3];
+            for (int a = 0; a < 3; a++)
             {
-                // box_exit_bound_axis (the wide section's walk): per axis, any sign
-                float lo[3];
-                for (int a = 0; a < 3; a++)
-                {
-                    const float k = float(f[a] + 2) * 1.1920928955078125e-7f;
-                    lo[a] = e[a] - std::fma(std::fabs(nct[a]), k, std::fabs(e[a]) * k);
-                }
-                tl = std::fmin(std::fmin(lo[0], lo[1]), lo[2]);
+                const float e = std::fma(float(f[a]), dt[a], nct[a]), k = float(f[a] + 2) * 1.1920928955078125e-7f;
+                lo[a] = e - std::fma(std::fabs(nct[a]), k, std::fabs(e) * k);
             }
+            float tl = std::fmin(std::fmin(lo[0], lo[1]), lo[2]);
             if (shrink)
             {
                 // a wave's lower bound (time-synchronised runs) is any T <= tl: pull tl down
@@ -189,7 +174,6 @@ int main(int argc, char **argv)
     rtbox::build_box_words(s.off.data(), s.dim, boxw, rtbox::kBoxRatio, rtbox::kBoxExtend, rtbox::kBoxGrow);
     const bool rnd = std::strcmp(argv[2], "random") == 0;
     const bool shrink = argc > 5 && std::strcmp(argv[5], "shrink") == 0;   // T = any bound <= tl
-    const bool axis_bound = argc > 5 && std::strcmp(argv[5], "axis") == 0;  // box_exit_bound_axis
     const uint32_t W = rnd ? 1024u : uint32_t(std::atoi(argv[2])), spp = rnd ? 1u : uint32_t(std::atoi(argv[4]));
     const uint32_t H = rnd ? uint32_t((std::strtoull(argv[3], nullptr, 10) + 1023) / 1024) : uint32_t(std::atoi(argv[3]));
     const uint64_t seed = rnd ? std::strtoull(argv[4], nullptr, 10) : 0;
@@ -247,7 +231,7 @@ int main(int argc, char **argv)
                         else GenRay(s.cam, x, y, W, H, smp[2 * si], smp[2 * si + 1], s.fov, o, d);
                         uint32_t la, lb;
                         ref_walk(s, o, d, a, la);
-                        lane_walk(s, boxw, o, d, b, lb, tk, br, rn, shrink, axis_bound, rng);
+                        lane_walk(s, boxw, o, d, b, lb, tk, br, rn, shrink, rng);
                         nr++;
                         ne += a.size();
                         bool ok = a.size() == b.size();

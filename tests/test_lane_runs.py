@@ -36,7 +36,7 @@ def _run(exe, *args):
 def test_lane_runs_bench_frame(tmp_path_factory, sid):
     out = _run(_checker(tmp_path_factory), os.path.join(ROOT, "data", "scenes", f"scene{sid}.rtscene"), 1920, 1080, 4)
     # the bound is tight: after the add chains the box's exit is (almost always) the next step
-    assert out["bare_steps_per_run"] < 1.02, out
+    assert out["bare_steps_per_run"] < 1.01, out
 
 
 @pytest.mark.parametrize("sid", [1, 5, 8])
@@ -52,11 +52,3 @@ def test_lane_runs_any_lower_bound(tmp_path_factory, sid):
     exe = _checker(tmp_path_factory)
     _run(exe, os.path.join(ROOT, "data", "scenes", f"scene{sid}.rtscene"), 960, 540, 4, "shrink")
     _run(exe, os.path.join(ROOT, "data", "scenes", f"scene{sid}.rtscene"), "random", 500000, sid + 3, "shrink")
-
-
-@pytest.mark.parametrize("sid", [1, 5, 8])
-def test_lane_runs_per_axis_bound(tmp_path_factory, sid):
-    """The wide section's walk bounds each axis separately (box_exit_bound_axis, any sign)."""
-    exe = _checker(tmp_path_factory)
-    _run(exe, os.path.join(ROOT, "data", "scenes", f"scene{sid}.rtscene"), 960, 540, 4, "axis")
-    _run(exe, os.path.join(ROOT, "data", "scenes", f"scene{sid}.rtscene"), "random", 500000, sid + 5, "axis")
