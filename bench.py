@@ -166,8 +166,9 @@ def moving_camera(work, steps, warmup, static_ms):
 
     def step(i):
         if work.batch:
-            work.rtm.render_batch_device([g for _, _, g, _ in work.scenes], [p[i] for p in frames],
-                                         [b.data_ptr() for b in work.bufs[0]], stream=work.stream.cuda_stream)
+            o = work.order
+            work.rtm.render_batch_device([work.scenes[j][2] for j in o], [frames[j][i] for j in o],
+                                         [work.bufs[0][j].data_ptr() for j in o], stream=work.stream.cuda_stream)
             return
         for j, (sid, hs, gs, f) in enumerate(work.scenes):
             gs.render_frame_device(frames[j][i], work.bufs[0][j].data_ptr(), work.stream.cuda_stream)
@@ -263,7 +264,7 @@ def valu_roofline(rtm, kernel_ms, args, world, algorithmic, step_ms=None, work=N
         return roof
     sc = c["scenes"]
     if "batch" in kernel_ms:
-        # the step is ONE batched launch (k_render_batch): counters of that launch
+        # the step is batched launch(es) (k_render_batch): counters summed over a step's launches
         if "batch" not in sc:
             roof["counters"] = "refused: counters are per-scene launches, the timed step is a batched launch"
             return roof
@@ -274,7 +275,7 @@ def valu_roofline(rtm, kernel_ms, args, world, algorithmic, step_ms=None, work=N
         rate = sc["batch"]["SQ_INSTS_VALU"] / ((step_ms or kernel_ms["batch"]) / 1e3)
         roof.update({"achieved": round(rate / 1e9, 1), "frac": round(rate / VALU_PEAK, 4),
                      "traffic": sc["batch"]["hbm_bytes"],
-                     "traffic_unit": "HBM bytes per batched launch (every scene's frame)",
+                     "traffic_unit": "HBM bytes per step's batched launch(es) (every scene's frame)",
                      "counters": f"{os.path.relpath(path, ROOT)} (batched launch), source hash {src}"})
         return roof
     if "batch" in sc:
@@ -390,8 +391,9 @@ def cpu_baseline(rtm_unused=None):
 
 class GpuWorkload:
     """The bench workload on this rank's GPU: one frame of every scene per step.  batch: every
-    scene's frame of a step in ONE launch (rt_render_batch_device, up to 4 frames per launch), so
-    one frame's tail overlaps the others' work; else one launch per frame."""
+    scene's frame of a step in batched launches (rt_render_batch_device, up to MAX_BATCH = 6 frames
+    per launch, config 5 as 5 + 5), so one frame's tail overlaps the others' work; else one launch
+    per frame."""
 
     def __init__(self, rtm, torch, world, rank, local, kernel, batch=True):
         self.rtm, self.torch, self.world, self.rank = rtm, torch, world, rank
@@ -416,7 +418,15 @@ class GpuWorkload:
         self.frames = [torch.empty(W * H, dtype=torch.int32, device="cuda") for _ in SCENES]
         # scenes whose kernel-time ring holds a launch's time: every scene, or the first scene of
         # every batch launch
-        self.timed = list(range(0, len(SCENES), rtm.MAX_BATCH)) if batch else list(range(len(SCENES)))
+        # batched with 2+ launches per step (config 5): the frames ordered so that each launch's
+        # frames carry near-equal cost (rtm.batch_order over each frame's own launch time, measured
+        # here, before the warm-up)
+        self.order, self.costs = list(range(len(SCENES))), None
+        if batch and len(rtm.batch_chunks(len(SCENES))) > 1:
+            self.costs = rtm.frame_costs([g for _, _, g, _ in self.scenes], [f for _, _, _, f in self.scenes],
+                                         [b.data_ptr() for b in self.frames], stream=self.stream.cuda_stream)
+            self.order = rtm.batch_order(self.costs)
+        self.timed = [self.order[i] for i, _ in rtm.batch_chunks(len(SCENES))] if batch else list(range(len(SCENES)))
 
     def stream_ctx(self):
         return self.torch.cuda.stream(self.stream)
@@ -451,8 +461,9 @@ class GpuWorkload:
         st = self.stream.cuda_stream
         bufs = self.bufs[p]
         if self.batch:
-            self.rtm.render_batch_device([g for _, _, g, _ in self.scenes], [f for _, _, _, f in self.scenes],
-                                         [b.data_ptr() for b in bufs], self.rank, self.world, stream=st)
+            o = self.order
+            self.rtm.render_batch_device([self.scenes[i][2] for i in o], [self.scenes[i][3] for i in o],
+                                         [bufs[i].data_ptr() for i in o], self.rank, self.world, stream=st)
             return
         for i, (sid, hs, gs, f) in enumerate(self.scenes):
             if self.world == 1:
@@ -508,7 +519,7 @@ class GpuWorkload:
         return out
 
     def launches_per_step(self):
-        return (len(SCENES) + self.rtm.MAX_BATCH - 1) // self.rtm.MAX_BATCH if self.batch else len(SCENES)
+        return len(self.rtm.batch_chunks(len(SCENES))) if self.batch else len(SCENES)
 
     def close(self):
         for sid, hs, gs, f in self.scenes:
@@ -654,9 +665,11 @@ def main():
     ap.add_argument("--graph", action="store_true",
                     help="replay the step's render launch(es) from a hipGraph captured after the warm-up")
     ap.add_argument("--batch", choices=["auto", "on", "off"], default="auto",
-                    help="the step's frames in one batched launch (rt_render_batch_device) or one launch per "
-                         "frame; auto = batched for N > 1 ranks, where it measured 13-14 %% faster at N = 2 and 8 "
-                         "and 1 %% slower at N = 1 (profiles/r03d_ab_wave_priority.json)")
+                    help="the step's frames in batched launches (rt_render_batch_device, up to MAX_BATCH "
+                         "frames each) or one launch per frame; auto = batched whenever the step has 2+ frames: "
+                         "13-14 %% faster at N = 2 and 8 (profiles/r03d_ab_wave_priority.json) and, on the "
+                         "round-4 build, at N = 1 the bench pair 0.541 vs 0.552 ms and config 5 2.79 vs 3.00 ms "
+                         "per step (profiles/r04ab_batch_n1.json)")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="bench")
     ap.add_argument("--check", action="store_true",
                     help="after timing, rank 0 compares every assembled frame with a one-GPU render")
@@ -686,7 +699,7 @@ def main():
             dist.init_process_group(args.dist_backend)
 
     rtm = load_package()
-    batch = args.batch == "on" or (args.batch == "auto" and world > 1)
+    batch = args.batch == "on" or (args.batch == "auto" and len(SCENES) >= 2)
     work = GpuWorkload(rtm, torch, world, rank, local, args.kernel, batch=batch)
     # The per-sample counts behind the algorithmic bytes (the debug records kernel over
     # whole frames, reduced on the host) first; then the supplementary legs that keep the GPU busy
@@ -746,8 +759,11 @@ def main():
                        "width": W, "height": H, "spp": SPP, "kernel": args.kernel,
                        "parallelism": f"tile-shard x{world}" + (" + RCCL gather to rank 0" if world > 1 else ""),
                        "launch": ("hipGraph of " if args.graph else "") +
-                                 ("the step's frames batched, <= 4 per launch (rt_render_batch_device)"
-                                  if work.batch else "one launch per frame"),
+                                 (f"the step's frames batched as {[c for _, c in rtm.batch_chunks(len(SCENES))]} "
+                                  "frames per launch (rt_render_batch_device)" if work.batch else "one launch per frame"),
+                       "frame_order": [SCENES[i] for i in work.order] if work.batch else list(SCENES),
+                       "frame_costs_ms": ({str(SCENES[i]): round(c, 4) for i, c in enumerate(work.costs)}
+                                          if work.costs else None),
                        "camera": "static: each scene's own camera every step, so the per-origin "
                                  "triangle records (k_origin_pre) are computed once; see moving_camera"},
             "kernel_ms_per_step": round(step_ms, 4),

@@ -63,7 +63,8 @@ TRACER_SYMBOLS = [
     "rt_host_free", "rt_render_hits_device", "rt_scene_info_get", "rt_build_hash", "rt_render_batch_device",
     "rt_render_records_device", "rt_render_frame_host_tiled",
 ]
-MAX_BATCH = 4                            # frames per rt_render_batch_device launch
+MAX_BATCH = 6                            # frames per rt_render_batch_device launch (kMaxBatch)
+
 HOST_SYMBOLS = [
     "rth_scene_load", "rth_scene_from_mesh", "rth_scene_free", "rth_scene_desc",
     "rth_scene_camera", "rth_scene_stats_get", "rth_framebuffer_create", "rth_framebuffer_free",
@@ -637,6 +638,49 @@ class GpuScene:
             self.close()
         except Exception:
             pass
+
+
+def batch_chunks(n):
+    """(first frame, frames) of each launch rt_render_batch_device makes for n frames:
+    ceil(n / MAX_BATCH) launches of near-equal size (rt_tracer.hip batch_chunk_len)."""
+    out, i = [], 0
+    while i < n:
+        left = n - i
+        k = (left + MAX_BATCH - 1) // MAX_BATCH
+        c = (left + k - 1) // k
+        out.append((i, c))
+        i += c
+    return out
+
+
+def batch_order(costs):
+    """A frame order for rt_render_batch_device whose in-order launches (batch_chunks) carry
+    near-equal cost: frames heaviest first, each into the launch with the least cost so far that
+    still has room, launch-major.  Measured on config 5 (profiles/r04ad_batch_partition.json): the
+    three heaviest scenes in one launch cost 2-3 % against a mix."""
+    chunks = batch_chunks(len(costs))
+    bins, load = [[] for _ in chunks], [0.0] * len(chunks)
+    for i in sorted(range(len(costs)), key=lambda i: (-costs[i], i)):
+        j = min((j for j in range(len(chunks)) if len(bins[j]) < chunks[j][1]), key=lambda j: (load[j], j))
+        bins[j].append(i)
+        load[j] += costs[i]
+    return [i for b in bins for i in b]
+
+
+def frame_costs(scenes, frames, d_outs, stream=0, reps=4, restore_every=8):
+    """Device ms of each frame rendered alone (render_frame_device into d_outs[i], the minimum over
+    reps launches from the scene's own kernel-time ring; the ring is drained and the scene's timing
+    set back to every restore_every-th launch): the costs batch_order balances."""
+    out = []
+    for g, f, d in zip(scenes, frames, d_outs):
+        g.set_timing(1)
+        g.kernel_times()
+        for _ in range(reps):
+            g.render_frame_device(f, d, stream)
+        t = g.kernel_times()
+        g.set_timing(restore_every)
+        out.append(float(min(t)))
+    return out
 
 
 def render_batch_device(scenes, frames, d_outs, rank=0, nranks=1, d_hits=None, stream=0):

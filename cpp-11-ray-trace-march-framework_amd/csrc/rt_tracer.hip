@@ -281,7 +281,8 @@ __device__ __forceinline__ const KParams& late_params(const KParams& P, uint32_t
 // in ONE grid, so one frame's tail overlaps the others' work and the heavy-first order ranks the
 // blocks of all of them.  p[0] also carries the batch's heavy-first / wide-section state (its
 // block and item indices are the launch's, frame-major); every other field is per frame.
-constexpr uint32_t kMaxBatch = 4;
+// 6 frames keep KBatch (~3.6 KiB) inside the 4 KiB kernarg limit (static_assert below).
+constexpr uint32_t kMaxBatch = 6;
 struct KBatch
 {
     KParams p[kMaxBatch];
@@ -306,6 +307,15 @@ __device__ __forceinline__ uint32_t batch_frame(const KBatch& B, uint32_t b)
     uint32_t f = 0;
     for (uint32_t j = 1; j < kMaxBatch; j++) f += (j < B.nframes && b >= B.base[j]) ? 1u : 0u;
     return f;
+}
+
+// Frames in the launch that starts at frame `start` of an n-frame batch: ceil(n / kMaxBatch)
+// launches of near-equal size (10 frames: 5 + 5), each with one tail.  Mirrored by the binding's
+// batch_chunks().
+inline uint32_t batch_chunk_len(uint32_t n, uint32_t start)
+{
+    const uint32_t left = n - start, k = (left + kMaxBatch - 1u) / kMaxBatch;
+    return (left + k - 1u) / k;
 }
 
 // CSR range of a cell: one u32 load of the packed (start << 11 | count) word when the scene
@@ -4191,10 +4201,14 @@ int rt_render_batch_device(rt_scene *const *scenes, const rt_frame *frames, uint
         if (!scenes[i] || !d_outs[i]) return fail(RT_E_INVALID, "NULL scene or output");
         if (int rc = validate_frame(&frames[i])) return rc;
     }
-    for (uint32_t i = 0; i < n; i += kMaxBatch)
-        if (int rc = render_batch_chunk(scenes + i, frames + i, std::min(kMaxBatch, n - i), rank, nranks, d_outs + i,
+    for (uint32_t i = 0; i < n;)
+    {
+        const uint32_t c = batch_chunk_len(n, i);
+        if (int rc = render_batch_chunk(scenes + i, frames + i, c, rank, nranks, d_outs + i,
                                         d_hits ? d_hits + i : nullptr, nullptr, hip_stream))
             return rc;
+        i += c;
+    }
     return RT_OK;
 }
 
@@ -4224,10 +4238,14 @@ int rt_render_records_device(rt_scene *const *scenes, const rt_frame *frames, ui
             return rc;
     }
     else
-        for (uint32_t i = 0; i < n; i += kMaxBatch)
-            if (int rc = render_batch_chunk(scenes + i, frames + i, std::min(kMaxBatch, n - i), rank, nranks,
-                                            d_outs + i, nullptr, ro.data() + i, hip_stream))
+        for (uint32_t i = 0; i < n;)
+        {
+            const uint32_t c = batch_chunk_len(n, i);
+            if (int rc = render_batch_chunk(scenes + i, frames + i, c, rank, nranks, d_outs + i, nullptr,
+                                            ro.data() + i, hip_stream))
                 return rc;
+            i += c;
+        }
     // the raw records made final (k_record_fixup), per frame on the launch stream
     for (uint32_t i = 0; i < n; i++)
     {

@@ -244,16 +244,16 @@ int  rt_unshard_device(uint32_t width, uint32_t height, uint32_t nranks,
 int  rt_render_hits_device(rt_scene *scene, const rt_frame *frame, uint32_t rank, uint32_t nranks,
                            uint32_t *d_out, uint32_t *d_hits, void *hip_stream);
 
-/* Several frames -- of one or more scenes on one device -- in ONE launch (at most 4 per launch;
- * longer lists take one launch per 4): frame i renders into d_outs[i] exactly as
+/* Several frames -- of one or more scenes on one device -- in ONE launch (at most 6 per launch;
+ * longer lists take ceil(n / 6) launches of near-equal size, 10 frames as 5 + 5): frame i renders into d_outs[i] exactly as
  * rt_render_frame_device (nranks == 1) or rt_render_shard_device (nranks > 1: rank's shard) would,
  * and, when d_hits and d_hits[i] are non-NULL, stores per-sample hit IDs as rt_render_hits_device.
  * The frames' blocks share one grid, so one frame's tail overlaps the others' work and AUTO's
  * heavy-first order (and, for dense shards, the wide section) ranks the blocks of all of them; the
  * batch keeps its own heavy-first state.  Frames that cannot share a launch (another kernel kind
  * or flag, different size / spp, scenes on different devices or outside AUTO's full traversal
- * variant) take one launch each.  Asynchronous on hip_stream; kernel time lands in scenes[0]'s
- * rt_kernel_times ring. */
+ * variant) take one launch each.  Asynchronous on hip_stream; each launch's kernel time lands in
+ * the rt_kernel_times ring of its first frame's scene. */
 int  rt_render_batch_device(rt_scene *const *scenes, const rt_frame *frames, uint32_t n, uint32_t rank,
                             uint32_t nranks, uint32_t *const *d_outs, uint32_t *const *d_hits,
                             void *hip_stream);

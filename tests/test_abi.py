@@ -88,6 +88,35 @@ def test_library_build_hash_matches_sources():
     assert rtm.library_build_hash() == rtm.kernel_source_hash()
 
 
+def test_batch_chunks_mirror_the_library():
+    """rtm.batch_chunks restates rt_render_batch_device's split (batch_chunk_len, kMaxBatch):
+    ceil(n / MAX_BATCH) launches of near-equal size that cover the frames in order; bench.py and
+    tools/collect_counters.py time and count a step's launches by it."""
+    src = open(os.path.join(PKG_DIR, "csrc", "rt_tracer.hip")).read()
+    assert int(re.search(r"constexpr uint32_t kMaxBatch = (\d+);", src).group(1)) == rtm.MAX_BATCH
+    for n in range(1, 40):
+        ch = rtm.batch_chunks(n)
+        assert [i for i, _ in ch] == [sum(c for _, c in ch[:k]) for k in range(len(ch))]
+        assert sum(c for _, c in ch) == n and len(ch) == -(-n // rtm.MAX_BATCH)
+        assert max(c for _, c in ch) - min(c for _, c in ch) <= 1 and max(c for _, c in ch) <= rtm.MAX_BATCH
+    assert rtm.batch_chunks(10) == [(0, 5), (5, 5)] and rtm.batch_chunks(2) == [(0, 2)]
+
+
+def test_batch_order_balances_launches():
+    """rtm.batch_order: a permutation whose in-order launches (batch_chunks) take the heaviest
+    frames apart -- config 5's measured per-frame costs give launches within 4 % of each other."""
+    costs = [0.205, 0.187, 0.268, 0.222, 0.264, 0.553, 0.228, 0.384, 0.377, 0.285]
+    o = rtm.batch_order(costs)
+    assert sorted(o) == list(range(10))
+    loads = [sum(costs[i] for i in o[s:s + n]) for s, n in rtm.batch_chunks(10)]
+    assert max(loads) / min(loads) < 1.04
+    assert not {5, 7, 8} <= set(o[:5]) and not {5, 7, 8} <= set(o[5:])
+    assert rtm.batch_order([1.0, 2.0]) == [1, 0] and rtm.batch_order([]) == []
+    for n in range(1, 20):
+        c = [float((7 * i) % 5 + 1) for i in range(n)]
+        assert sorted(rtm.batch_order(c)) == list(range(n))
+
+
 def test_multi_gpu_framebuffer_argument_checks():
     """rth_framebuffer_create_multi refuses an empty or oversized device list before touching a
     GPU or RCCL (librccl.so.1 is loaded on first real use only)."""

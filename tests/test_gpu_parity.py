@@ -1032,9 +1032,16 @@ def test_batch_bench_pair(golden, scenes, N):
 
 
 def test_batch_all_ten_scenes(golden, scenes):
-    """BASELINE config 5 through rt_render_batch_device: 10 frames = launches of 4 + 4 + 2 frames."""
+    """BASELINE config 5 through rt_render_batch_device: 10 frames = two launches of 5 frames
+    (rtm.batch_chunks), each led by its first frame's scene, none falling back."""
     sids = tuple(range(10))
-    _batch_check(golden, [scenes(s)[1] for s in sids], sids, 1920, 1080, 1, 3)
+    gss = [scenes(s)[1] for s in sids]
+    assert rtm.batch_chunks(10) == [(0, 5), (5, 5)]
+    before = [(g.info()["batch_launches"], g.info()["batch_fallbacks"]) for g in gss]
+    _batch_check(golden, gss, sids, 1920, 1080, 1, 3)
+    after = [(g.info()["batch_launches"], g.info()["batch_fallbacks"]) for g in gss]
+    assert [(a[0] - b[0], a[1] - b[1]) for a, b in zip(after, before)] == \
+        [(3, 0) if i in (0, 5) else (0, 0) for i in range(10)]
 
 
 def test_batch_same_scene_twice_and_fallback(golden, scenes):

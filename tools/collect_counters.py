@@ -45,16 +45,26 @@ def load_rtm():
     return m
 
 
-def medians(path, nscenes):
+def medians(path, nscenes, per_step=0):
     """Per scene (dispatch order: frames of scene 0, then scene 1, ...) and counter: the median
-    over that scene's k_render_* dispatches after its first two."""
+    over that scene's k_render_* dispatches after its first two.  per_step > 0 (--batch): every
+    per_step consecutive dispatches are one step's batched launches; the median of their sums
+    over the steps after the first two (one key)."""
     per = {}
     for r in csv.DictReader(open(path)):
-        if "k_render" not in r["Kernel_Name"]:
+        # --batch: only the batched launches (render_loop's per-frame cost launches are not a step's)
+        if ("k_render_batch" if per_step else "k_render") not in r["Kernel_Name"]:
             continue
         d = per.setdefault(r["Counter_Name"], {})
         k = int(r["Dispatch_Id"])
         d[k] = d.get(k, 0.0) + float(r["Counter_Value"])
+    if per_step:
+        out = {}
+        for name, disp in per.items():
+            vals = [disp[k] for k in sorted(disp)]
+            steps = sorted(sum(vals[i:i + per_step]) for i in range(2 * per_step, len(vals) - per_step + 1, per_step))
+            out[name] = steps[len(steps) // 2]
+        return [out]
     out = [dict() for _ in range(nscenes)]
     for name, disp in per.items():
         vals = [disp[k] for k in sorted(disp)]
@@ -103,7 +113,7 @@ def main():
         f = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
         if not f:
             sys.exit(f"no counter csv under {d}")
-        for k, m in zip(keys, medians(f[0], len(keys))):
+        for k, m in zip(keys, medians(f[0], len(keys), len(rtm.batch_chunks(len(a.scenes))) if a.batch else 0)):
             res[k].update(m)
     for k in keys:
         c = res[k]
@@ -122,8 +132,9 @@ def main():
            "workload_name": a.workload,
            "kernel": "AUTO (rt_kernel 0)" + (", batched launch (k_render_batch)" if a.batch else ""),
            "frames_per_scene": a.frames,
-           "statistic": ("per batch dispatch (all scenes' frames)" if a.batch else "per scene") +
-                        ", median over its k_render_* dispatches after its first two",
+           "statistic": (f"per step: the sum over its batched launches {rtm.batch_chunks(len(a.scenes))} "
+                         "(all scenes' frames), median over the steps after the first two" if a.batch else
+                         "per scene, median over its k_render_* dispatches after its first two"),
            "hbm_note": "hbm_bytes = (2 x FETCH_SIZE + WRITE_SIZE) KiB x 1024 (gfx950 FETCH_SIZE "
                        "counts half of a wide read; MI355X_MICROARCH.md)",
            "scenes": res}

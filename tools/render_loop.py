@@ -37,10 +37,16 @@ if a.batch:
     fs = [g.frame(W, H, S, kernel=a.kernel) for g in gs]
     n = W * H if a.nranks == 1 else rtm.shard_elems(W, H, a.nranks)
     outs = [torch.empty(n, dtype=torch.int32, device="cuda") for _ in sids]
+    order = list(range(len(sids)))
+    if len(rtm.batch_chunks(len(sids))) > 1:
+        # bench.py's order (its per-frame cost launches are filtered out by collect_counters)
+        full = [torch.empty(W * H, dtype=torch.int32, device="cuda") for _ in sids]
+        order = rtm.batch_order(rtm.frame_costs(gs, fs, [o.data_ptr() for o in full], stream=st.cuda_stream))
+    gs, fs, outs = [gs[i] for i in order], [fs[i] for i in order], [outs[i] for i in order]
     for _ in range(a.frames):
         rtm.render_batch_device(gs, fs, [o.data_ptr() for o in outs], a.rank, a.nranks, stream=st.cuda_stream)
     torch.cuda.synchronize()
-    print("batch frames", a.frames, "scenes", sids, "rank", a.rank, "of", a.nranks)
+    print("batch frames", a.frames, "scenes", [sids[i] for i in order], "rank", a.rank, "of", a.nranks)
     sys.exit(0)
 for sid in (a.scenes or [a.scene]):
     g = rtm.GpuScene(rtm.HostScene.load(sid), 0)
