@@ -277,6 +277,18 @@ def valu_roofline(rtm, kernel_ms, args, world, algorithmic, step_ms=None, work=N
                      "traffic": sc["batch"]["hbm_bytes"],
                      "traffic_unit": "HBM bytes per step's batched launch(es) (every scene's frame)",
                      "counters": f"{os.path.relpath(path, ROOT)} (batched launch), source hash {src}"})
+        # each frame alone (GpuWorkload's cost launches) against per-scene-launch counters, when
+        # collected for this build (tools/gpu_r04final.sh): which scenes sit furthest below the bound
+        ps = os.path.join(ROOT, "profiles", f"counters_{args.workload}_per_scene.json")
+        if work is not None and work.costs and os.path.exists(ps):
+            with open(ps) as fh:
+                c2 = json.load(fh)
+            if c2.get("source_hash") == src and c2.get("workload") == want:
+                roof["per_scene_valu_frac"] = {
+                    str(sid): round(c2["scenes"][str(sid)]["SQ_INSTS_VALU"] / (work.costs[i] / 1e3) / VALU_PEAK, 4)
+                    for i, sid in enumerate(SCENES)}
+                roof["per_scene_note"] = ("each scene's frame in its own launch (frame_costs: the minimum of 4) "
+                                          f"against {os.path.relpath(ps, ROOT)}; the timed step is batched")
         return roof
     if "batch" in sc:
         roof["counters"] = "refused: counters are of the batched launch, the timed step is per-scene launches"
