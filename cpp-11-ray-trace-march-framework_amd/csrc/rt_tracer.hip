@@ -1496,15 +1496,17 @@ __device__ __forceinline__ uint32_t xcd_band_block(uint32_t b, uint32_t nb, uint
 // of its slowest wave; blocks above max(hf_floor, last max >> kHfShift) are listed for the next
 // frames -- above last max >> 1 at the front of the front section, the rest from its back -- and
 // marked so the natural order skips them.  Nothing is listed when the last measurement showed no
-// tail (its slowest block well under the frame's estimated span).  One thread per block; each
-// workgroup reduces its maximum and sum and reserves its list slots with ONE atomic per level
-// (the render waves themselves touch no atomics: thousands of same-address atomics from waves
-// cost milliseconds, measured).
+// tail (its slowest block well under the frame's estimated span).  Each thread takes kHfPlanPer
+// blocks (kWG apart, so the cost loads stay coalesced); each workgroup reduces its maximum and sum
+// and reserves its list slots with ONE atomic per level (the render waves themselves touch no
+// atomics: thousands of same-address atomics from waves cost milliseconds, measured).  The plan's
+// time is those same-address atomics: one block per thread (1,013 workgroups for the batched
+// bench pair) took 26.6 us per plan, which a moving camera pays every frame.
+constexpr uint32_t kHfPlanPer = 8;
 __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks)
 {
     __shared__ uint32_t s_max, s_hi, s_lo, s_w, s_w4, s_bhi, s_blo, s_bw, s_bw4, s_last;
     __shared__ unsigned long long s_sum;
-    const uint32_t b = blockIdx.x * kWG + threadIdx.x;
     if (threadIdx.x == 0u)
     {
         s_max = s_hi = s_lo = s_w = s_w4 = 0u;
@@ -1512,57 +1514,70 @@ __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks)
     }
     __syncthreads();
     const HfPlan last = *P.hf_plan_in;
-    uint32_t cost = 0u, sum = 0u, wmask = 0u, wmask4 = 0u;
-    uint4 c = make_uint4(0u, 0u, 0u, 0u);
-    if (b < nblocks)
-    {
-        c = reinterpret_cast<const uint4 *>(P.hf_cost)[b];                // kWavesPerWG == 4
-        sum = (c.x >> 4) + (c.y >> 4) + (c.z >> 4) + (c.w >> 4);          // in 16-cycle units
-        if (P.wh_on && !P.wh_wgs && last.sum_full)
-        {
-            // wide section: items above a fraction of the frame span estimated from the last
-            // measurement of every item one lane per sample (sum of wave costs over the resident
-            // waves).  New items are listed only from such frames (the first ones of a shape, the
-            // refresh frames): with the section running, the lane waves' costs shrink as items
-            // leave them, which pulled the span estimate down and listed ever more items
-            // (killeroo's rank of 4: 298 -> 587 items over 100 frames, measured).
-            const uint64_t span = (last.sum_full << 4) / kHfSlots;
-            const uint32_t thr = max(P.wh_floor, uint32_t(min<uint64_t>(span * P.wh_alpha16 / 16u, 0xFFFFFFFFull)));
-            wmask = uint32_t(c.x > thr) | (uint32_t(c.y > thr) << 1) | (uint32_t(c.z > thr) << 2) |
-                    (uint32_t(c.w > thr) << 3);
-            // second tier (4 lanes per sample): items between the beta and the alpha thresholds
-            const uint32_t thr4 = P.wh_beta16 ? max(P.wh_floor, uint32_t(min<uint64_t>(span * P.wh_beta16 / 16u,
-                                                                                         0xFFFFFFFFull)))
-                                              : 0xFFFFFFFFu;
-            wmask4 = (uint32_t(c.x > thr4) | (uint32_t(c.y > thr4) << 1) | (uint32_t(c.z > thr4) << 2) |
-                      (uint32_t(c.w > thr4) << 3)) & ~wmask;
-        }
-        if (P.wh_on && !P.wh_refresh && P.hf_ver)
-        {
-            // sticky: the current plan's items stay listed in their tier (mark = the plan version,
-            // bit 31 = the second tier)
-            const uint4 m = reinterpret_cast<const uint4 *>(P.wh_mark_in)[b];
-            const uint32_t in = uint32_t((m.x & 0x7FFFFFFFu) == P.hf_ver) | (uint32_t((m.y & 0x7FFFFFFFu) == P.hf_ver) << 1) |
-                                (uint32_t((m.z & 0x7FFFFFFFu) == P.hf_ver) << 2) |
-                                (uint32_t((m.w & 0x7FFFFFFFu) == P.hf_ver) << 3);
-            const uint32_t t4 = (m.x >> 31) | ((m.y >> 31) << 1) | ((m.z >> 31) << 2) | ((m.w >> 31) << 3);
-            wmask |= in & ~t4;
-            wmask4 = (wmask4 | (in & t4)) & ~wmask;
-        }
-        // the heavy-first order ranks a block by its slowest wave left in the lane section
-        const uint32_t wm = wmask | wmask4;
-        cost = max(max((wm & 1u) ? 0u : c.x, (wm & 2u) ? 0u : c.y), max((wm & 4u) ? 0u : c.z, (wm & 8u) ? 0u : c.w));
-    }
     const bool tail = uint64_t(last.maxc) * kHfSlots * 16u > uint64_t(kHfTail) * (last.sum << 4);
     const uint32_t thr = max(P.hf_floor, last.maxc >> kHfShift);
-    const bool heavy = P.hf_front && tail && cost > thr;
-    const bool hi = heavy && cost > (last.maxc >> 1);
-    uint32_t rank = 0u, wrank = 0u, wrank4 = 0u;
-    if (cost) atomicMax(&s_max, cost);
-    if (sum) atomicAdd(&s_sum, (unsigned long long)sum);
-    if (heavy) rank = atomicAdd(hi ? &s_hi : &s_lo, 1u);
-    if (wmask) wrank = atomicAdd(&s_w, uint32_t(__popc(wmask)));
-    if (wmask4) wrank4 = atomicAdd(&s_w4, uint32_t(__popc(wmask4)));
+    const uint32_t b0 = blockIdx.x * (kWG * kHfPlanPer) + threadIdx.x;
+    uint32_t tmax = 0u, wmasks = 0u, wmasks4 = 0u, heavy = 0u, hi = 0u;
+    unsigned long long tsum = 0ull;
+    uint32_t rank[kHfPlanPer], wrank[kHfPlanPer], wrank4[kHfPlanPer];
+#pragma unroll
+    for (uint32_t j = 0; j < kHfPlanPer; j++)
+    {
+        const uint32_t b = b0 + j * kWG;
+        uint32_t cost = 0u, sum = 0u, wmask = 0u, wmask4 = 0u;
+        if (b < nblocks)
+        {
+            const uint4 c = reinterpret_cast<const uint4 *>(P.hf_cost)[b];      // kWavesPerWG == 4
+            sum = (c.x >> 4) + (c.y >> 4) + (c.z >> 4) + (c.w >> 4);          // in 16-cycle units
+            if (P.wh_on && !P.wh_wgs && last.sum_full)
+            {
+                // wide section: items above a fraction of the frame span estimated from the last
+                // measurement of every item one lane per sample (sum of wave costs over the resident
+                // waves).  New items are listed only from such frames (the first ones of a shape, the
+                // refresh frames): with the section running, the lane waves' costs shrink as items
+                // leave them, which pulled the span estimate down and listed ever more items
+                // (killeroo's rank of 4: 298 -> 587 items over 100 frames, measured).
+                const uint64_t span = (last.sum_full << 4) / kHfSlots;
+                const uint32_t wt = max(P.wh_floor, uint32_t(min<uint64_t>(span * P.wh_alpha16 / 16u, 0xFFFFFFFFull)));
+                wmask = uint32_t(c.x > wt) | (uint32_t(c.y > wt) << 1) | (uint32_t(c.z > wt) << 2) |
+                        (uint32_t(c.w > wt) << 3);
+                // second tier (4 lanes per sample): items between the beta and the alpha thresholds
+                const uint32_t wt4 = P.wh_beta16 ? max(P.wh_floor, uint32_t(min<uint64_t>(span * P.wh_beta16 / 16u,
+                                                                                            0xFFFFFFFFull)))
+                                                 : 0xFFFFFFFFu;
+                wmask4 = (uint32_t(c.x > wt4) | (uint32_t(c.y > wt4) << 1) | (uint32_t(c.z > wt4) << 2) |
+                          (uint32_t(c.w > wt4) << 3)) & ~wmask;
+            }
+            if (P.wh_on && !P.wh_refresh && P.hf_ver)
+            {
+                // sticky: the current plan's items stay listed in their tier (mark = the plan version,
+                // bit 31 = the second tier)
+                const uint4 m = reinterpret_cast<const uint4 *>(P.wh_mark_in)[b];
+                const uint32_t in = uint32_t((m.x & 0x7FFFFFFFu) == P.hf_ver) | (uint32_t((m.y & 0x7FFFFFFFu) == P.hf_ver) << 1) |
+                                    (uint32_t((m.z & 0x7FFFFFFFu) == P.hf_ver) << 2) |
+                                    (uint32_t((m.w & 0x7FFFFFFFu) == P.hf_ver) << 3);
+                const uint32_t t4 = (m.x >> 31) | ((m.y >> 31) << 1) | ((m.z >> 31) << 2) | ((m.w >> 31) << 3);
+                wmask |= in & ~t4;
+                wmask4 = (wmask4 | (in & t4)) & ~wmask;
+            }
+            // the heavy-first order ranks a block by its slowest wave left in the lane section
+            const uint32_t wm = wmask | wmask4;
+            cost = max(max((wm & 1u) ? 0u : c.x, (wm & 2u) ? 0u : c.y), max((wm & 4u) ? 0u : c.z, (wm & 8u) ? 0u : c.w));
+        }
+        const bool hv = P.hf_front && tail && cost > thr;
+        const bool h1 = hv && cost > (last.maxc >> 1);
+        tmax = max(tmax, cost);
+        tsum += sum;
+        rank[j] = hv ? atomicAdd(h1 ? &s_hi : &s_lo, 1u) : 0u;
+        wrank[j] = wmask ? atomicAdd(&s_w, uint32_t(__popc(wmask))) : 0u;
+        wrank4[j] = wmask4 ? atomicAdd(&s_w4, uint32_t(__popc(wmask4))) : 0u;
+        heavy |= uint32_t(hv) << j;
+        hi |= uint32_t(h1) << j;
+        wmasks |= wmask << (4u * j);
+        wmasks4 |= wmask4 << (4u * j);
+    }
+    if (tmax) atomicMax(&s_max, tmax);
+    if (tsum) atomicAdd(&s_sum, tsum);
     __syncthreads();
     if (threadIdx.x == 0u)
     {
@@ -1583,40 +1598,48 @@ __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks)
         s_bw4 = s_w4 ? atomicAdd(&P.hf_plan_out->cnt_w4, s_w4) : 0u;
     }
     __syncthreads();
-    if (heavy)
+#pragma unroll
+    for (uint32_t j = 0; j < kHfPlanPer; j++)
     {
-        // very heavy blocks fill the front section from its start, the others from its end; a
-        // level that runs into the other is cut (those blocks stay in the natural order)
-        const uint32_t r = (hi ? s_bhi : s_blo) + rank;
-        if (r < P.hf_front)
+        const uint32_t b = b0 + j * kWG;
+        if ((heavy >> j) & 1u)
         {
-            const uint32_t slot = hi ? r : P.hf_front - 1u - r;
-            P.hf_list_out[slot] = b;           // may be overwritten by the other level: see below
+            // very heavy blocks fill the front section from its start, the others from its end; a
+            // level that runs into the other is cut (those blocks stay in the natural order)
+            const bool h1 = (hi >> j) & 1u;
+            const uint32_t r = (h1 ? s_bhi : s_blo) + rank[j];
+            if (r < P.hf_front)
+            {
+                const uint32_t slot = h1 ? r : P.hf_front - 1u - r;
+                P.hf_list_out[slot] = b;           // may be overwritten by the other level: see below
+            }
         }
+        // wide items: listed and marked for the next plan's frames (beyond kWhMax they stay in the
+        // lane section)
+        const uint32_t wmask = (wmasks >> (4u * j)) & 15u, wmask4 = (wmasks4 >> (4u * j)) & 15u;
+        uint32_t wr = wrank[j], wr4 = wrank4[j];
+        for (uint32_t k = 0; k < kWavesPerWG; k++)
+            if (wmask & (1u << k))
+            {
+                const uint32_t item = b * kWavesPerWG + k;
+                const uint32_t r = s_bw + wr++;
+                if (r < kWhMax)
+                {
+                    P.wh_list_out[r] = item;
+                    P.wh_mark_out[item] = P.hf_ver + 1u;
+                }
+            }
+            else if (wmask4 & (1u << k))
+            {
+                const uint32_t item = b * kWavesPerWG + k;
+                const uint32_t r = s_bw4 + wr4++;
+                if (r < kWhMax)
+                {
+                    P.wh_list_out[kWhMax + r] = item;
+                    P.wh_mark_out[item] = (P.hf_ver + 1u) | 0x80000000u;
+                }
+            }
     }
-    // wide items: listed and marked for the next plan's frames (beyond kWhMax they stay in the
-    // lane section)
-    for (uint32_t j = 0; j < kWavesPerWG; j++)
-        if (wmask & (1u << j))
-        {
-            const uint32_t item = b * kWavesPerWG + j;
-            const uint32_t r = s_bw + wrank++;
-            if (r < kWhMax)
-            {
-                P.wh_list_out[r] = item;
-                P.wh_mark_out[item] = P.hf_ver + 1u;
-            }
-        }
-        else if (wmask4 & (1u << j))
-        {
-            const uint32_t item = b * kWavesPerWG + j;
-            const uint32_t r = s_bw4 + wrank4++;
-            if (r < kWhMax)
-            {
-                P.wh_list_out[kWhMax + r] = item;
-                P.wh_mark_out[item] = (P.hf_ver + 1u) | 0x80000000u;
-            }
-        }
     // The block marks are written by a second pass over the final list, so a slot claimed by
     // both levels marks only the block whose entry survived.  That pass runs in the workgroup
     // that finishes last (a ticket after a release fence), not in a second launch: a kernel
@@ -3386,7 +3409,8 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
         RT_HIP(mark(kt1));
         if ((P.hf_front || P.wh_on) && P.hf_measure)
         {
-            hipLaunchKernelGGL(k_hf_plan, dim3(uint32_t((blocks + kWG - 1) / kWG)), wg, 0, st, P, uint32_t(blocks));
+            hipLaunchKernelGGL(k_hf_plan, dim3(uint32_t((blocks + kWG * kHfPlanPer - 1) / (kWG * kHfPlanPer))), wg, 0, st, P,
+                               uint32_t(blocks));
         }
     }
     else
@@ -3589,7 +3613,8 @@ int launch_batch(rt_scene *const *S, const rt_frame *F, uint32_t n, KParams *P, 
     }
     if (timed) RT_HIP(hipEventRecord(s0->kt1[kslot], st));
     if ((P[0].hf_front || P[0].wh_on) && P[0].hf_measure)
-        hipLaunchKernelGGL(k_hf_plan, dim3(uint32_t((blocks + kWG - 1) / kWG)), wg, 0, st, KB.p[0], uint32_t(blocks));
+        hipLaunchKernelGGL(k_hf_plan, dim3(uint32_t((blocks + kWG * kHfPlanPer - 1) / (kWG * kHfPlanPer))), wg, 0, st,
+                           KB.p[0], uint32_t(blocks));
     RT_HIP(hipGetLastError());
     for (uint32_t i = 0; i < n; i++)
     {
