@@ -1044,6 +1044,27 @@ def test_batch_all_ten_scenes(golden, scenes):
         [(3, 0) if i in (0, 5) else (0, 0) for i in range(10)]
 
 
+def test_batch_cost_ordered_ten_scenes(golden, scenes):
+    """bench.py's config-5 step: each frame timed in its own launch (rtm.frame_costs, the library's
+    event ring), the frames reordered by rtm.batch_order into two cost-balanced launches of 5;
+    every frame and its per-sample hit IDs still equal the reference's."""
+    import torch
+    sids = tuple(range(10))
+    gss = [scenes(s)[1] for s in sids]
+    fs = [g.frame(1920, 1080, 4) for g in gss]
+    tmp = [torch.zeros(1920 * 1080, dtype=torch.int32, device="cuda") for _ in sids]
+    costs = rtm.frame_costs(gss, fs, [t.data_ptr() for t in tmp], stream=torch.cuda.current_stream().cuda_stream)
+    assert len(costs) == 10 and all(0.0 < c < 50.0 for c in costs), costs
+    for sid, t in zip(sids, tmp):
+        assert sha_dev(t) == golden["frames_1080p4"][str(sid)]["bgra_sha256"], sid
+    order = rtm.batch_order(costs)
+    assert sorted(order) == list(range(10))
+    # the heaviest frame (scene 5, room + cat) and the next two never share one launch
+    heavy = sorted(range(10), key=lambda i: -costs[i])[:3]
+    assert not set(heavy) <= set(order[:5]) and not set(heavy) <= set(order[5:]), (costs, order)
+    _batch_check(golden, [gss[i] for i in order], tuple(sids[i] for i in order), 1920, 1080, 1, 3)
+
+
 def test_batch_same_scene_twice_and_fallback(golden, scenes):
     """A scene may appear twice in one batch; frames that cannot share a launch (another kernel
     kind) take one launch each -- outputs identical either way."""
