@@ -34,6 +34,8 @@ ARMS = {
     "4+3+3 lpt": [[5, 3, 1, 0], [7, 9, 6], [8, 2, 4]],
     "5+5 lpt 2 streams": [[5, 9, 4, 3, 1], [7, 8, 2, 6, 0]],
     "4+3+3 lpt 3 streams": [[5, 3, 1, 0], [7, 9, 6], [8, 2, 4]],
+    "6 with 5,7,8 + 4": [[5, 7, 8, 0, 1, 3], [2, 4, 6, 9]],
+    "6 lpt-ish + 4": [[5, 9, 2, 0, 1, 3], [7, 8, 4, 6]],
 }
 
 
