@@ -34,6 +34,7 @@ SETS = {
     "valu": "SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_ANY",
     "fetch": "FETCH_SIZE",
     "write": "WRITE_SIZE",
+    "tcc": "TCC_HIT_sum TCC_MISS_sum",
 }
 
 
