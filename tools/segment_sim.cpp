@@ -17,7 +17,7 @@
 // the costs: serial = cells + tests of the walk; segmented = max over the segments up to the
 // hit's of (cells + tests + chain adds / 8) -- the lanes after the hit's segment are cut.
 //   g++ -O2 -std=c++11 -pthread -ffp-contract=off -I oracle tools/segment_sim.cpp -o /tmp/segment_sim
-//   /tmp/segment_sim data/scenes/scene8.rtscene 1920 1080 4 [J=16]
+//   /tmp/segment_sim data/scenes/scene8.rtscene 1920 1080 4 [J=16] [G=1 list lanes] [cell weight=1]
 #include "../oracle/cpu_tracer.cpp"
 
 #include <algorithm>
@@ -38,11 +38,17 @@ int main(int argc, char **argv)
     BuildGrid(s, 64);
     const uint32_t W = std::atoi(argv[2]), H = std::atoi(argv[3]), spp = std::atoi(argv[4]);
     const int J = argc > 5 ? std::atoi(argv[5]) : 16;
+    // lanes splitting each cell's list (the wide section's G): a cell costs 1 + ceil(tests / G)
+    const uint32_t G = argc > 6 ? uint32_t(std::atoi(argv[6])) : 1u;
+    // a cell's own cost in test units (its word, list range and first record are dependent memory
+    // round trips: on the GPU a cell iteration costs a few tests' latency)
+    const float Wc = argc > 7 ? float(std::atof(argv[7])) : 1.0f;
     const std::vector<float> smp = Hammersley(spp);
     std::atomic<uint32_t> next(0);
     std::atomic<uint64_t> mismatches(0), checks(0), rays(0);
     const size_t nth = std::max(1u, std::thread::hardware_concurrency());
     std::vector<std::vector<std::pair<float, float>>> costs(nth);   // (serial, segmented) per ray
+    std::vector<std::vector<float>> split(nth);                     // list split only, per ray
     std::vector<std::thread> pool;
     for (size_t th = 0; th < nth; th++)
         pool.emplace_back([&, th]() {
@@ -113,7 +119,9 @@ int main(int argc, char **argv)
                         }
                         // segments
                         float serial = 0.0f;
-                        for (const CellState& c : walk) serial += 1.0f + float(c.tests);
+                        for (const CellState& c : walk) serial += Wc + float(c.tests);
+                        float listsplit = 0.0f;                            // one segment, G lanes
+                        for (const CellState& c : walk) listsplit += Wc + float((c.tests + G - 1u) / G);
                         std::vector<size_t> first(J + 1, walk.size());   // first walk cell of segment j
                         std::vector<float> adds(J + 1, 0.0f);
                         first[0] = 0;
@@ -175,10 +183,12 @@ int main(int argc, char **argv)
                             const size_t a = first[j], b = std::max(first[j], first[j + 1]);
                             if (a >= walk.size()) break;
                             float c = adds[j] / 8.0f;
-                            for (size_t i = a; i < std::min(b, walk.size()); i++) c += 1.0f + float(walk[i].tests);
+                            for (size_t i = a; i < std::min(b, walk.size()); i++)
+                                c += Wc + float((walk[i].tests + G - 1u) / G);
                             lat = std::max(lat, c);
                         }
                         costs[th].push_back(std::make_pair(serial, lat));
+                        split[th].push_back(listsplit);
                     }
             }
             mismatches += mm;
@@ -187,24 +197,34 @@ int main(int argc, char **argv)
         });
     for (auto& t : pool) t.join();
     std::vector<std::pair<float, float>> all;
+    std::vector<float> lsp;
     for (auto& v : costs) all.insert(all.end(), v.begin(), v.end());
-    std::sort(all.begin(), all.end(), [](const std::pair<float, float>& a, const std::pair<float, float>& b) {
-        return a.first > b.first;
-    });
-    auto summary = [&](double frac, double& ser, double& seg) {
+    for (auto& v : split) lsp.insert(lsp.end(), v.begin(), v.end());
+    std::vector<size_t> idx(all.size());
+    for (size_t i = 0; i < idx.size(); i++) idx[i] = i;
+    std::sort(idx.begin(), idx.end(), [&](size_t a, size_t b) { return all[a].first > all[b].first; });
+    double l1 = 0.0, l01 = 0.0;
+    auto summary = [&](double frac, double& ser, double& seg, double& ls) {
         const size_t n = std::max<size_t>(1, size_t(double(all.size()) * frac));
-        ser = seg = 0.0;
-        for (size_t i = 0; i < n; i++) { ser += all[i].first; seg += all[i].second; }
+        ser = seg = ls = 0.0;
+        for (size_t i = 0; i < n && i < idx.size(); i++)
+        {
+            ser += all[idx[i]].first;
+            seg += all[idx[i]].second;
+            ls += lsp[idx[i]];
+        }
         ser /= double(n);
         seg /= double(n);
+        ls /= double(n);
     };
-    double s1, g1, s01, g01, sa, ga;
-    summary(0.01, s1, g1);
-    summary(0.001, s01, g01);
-    summary(1.0, sa, ga);
-    std::printf("{\"scene\": \"%s\", \"segments\": %d, \"rays\": %llu, \"state_checks\": %llu, \"mismatches\": %llu, "
+    double s1, g1, s01, g01, sa, ga, la;
+    summary(0.01, s1, g1, l1);
+    summary(0.001, s01, g01, l01);
+    summary(1.0, sa, ga, la);
+    std::printf("{\"scene\": \"%s\", \"segments\": %d, \"list_lanes\": %u, \"top1pct_list_split_only\": %.1f, "
+                "\"top0.1pct_list_split_only\": %.1f, \"rays\": %llu, \"state_checks\": %llu, \"mismatches\": %llu, "
                 "\"mean_serial\": %.1f, \"mean_segmented\": %.1f, \"top1pct_serial\": %.1f, \"top1pct_segmented\": %.1f, "
                 "\"top0.1pct_serial\": %.1f, \"top0.1pct_segmented\": %.1f, \"max_serial\": %.1f}\n",
-                argv[1], J, (unsigned long long)rays.load(), (unsigned long long)checks.load(),
+                argv[1], J, G, l1, l01, (unsigned long long)rays.load(), (unsigned long long)checks.load(),
                 (unsigned long long)mismatches.load(), sa, ga, s1, g1, s01, g01, all.empty() ? 0.0 : all[0].first);
 }
