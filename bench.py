@@ -430,11 +430,13 @@ class GpuWorkload:
         self.frames = [torch.empty(W * H, dtype=torch.int32, device="cuda") for _ in SCENES]
         # scenes whose kernel-time ring holds a launch's time: every scene, or the first scene of
         # every batch launch
-        # batched with 2+ launches per step (config 5): the frames ordered so that each launch's
-        # frames carry near-equal cost (rtm.batch_order over each frame's own launch time, measured
-        # here, before the warm-up)
+        # batched at one rank: the frames ordered so that each launch's frames carry near-equal
+        # cost and each launch lists its heaviest frame first (rtm.batch_order over each frame's
+        # own launch time, measured here, before the warm-up): config 5 2.774 vs 2.786 ms with the
+        # light frames first, the bench pair 0.547 (killeroo first) vs 0.552
+        # (profiles/r04ao_batch_partition_order.json).  N > 1 keeps the scene order.
         self.order, self.costs = list(range(len(SCENES))), None
-        if batch and len(rtm.batch_chunks(len(SCENES))) > 1:
+        if batch and world == 1 and len(SCENES) >= 2:
             self.costs = rtm.frame_costs([g for _, _, g, _ in self.scenes], [f for _, _, _, f in self.scenes],
                                          [b.data_ptr() for b in self.frames], stream=self.stream.cuda_stream)
             self.order = rtm.batch_order(self.costs)

@@ -36,6 +36,9 @@ ARMS = {
     "4+3+3 lpt 3 streams": [[5, 3, 1, 0], [7, 9, 6], [8, 2, 4]],
     "6 with 5,7,8 + 4": [[5, 7, 8, 0, 1, 3], [2, 4, 6, 9]],
     "6 lpt-ish + 4": [[5, 9, 2, 0, 1, 3], [7, 8, 4, 6]],
+    "5+5 lpt light first": [[1, 3, 4, 9, 5], [0, 6, 2, 8, 7]],
+    "pair 1,8": [[1, 8]],
+    "pair 8,1": [[8, 1]],
 }
 
 

@@ -38,7 +38,7 @@ if a.batch:
     n = W * H if a.nranks == 1 else rtm.shard_elems(W, H, a.nranks)
     outs = [torch.empty(n, dtype=torch.int32, device="cuda") for _ in sids]
     order = list(range(len(sids)))
-    if len(rtm.batch_chunks(len(sids))) > 1:
+    if len(sids) >= 2 and a.nranks == 1:
         # bench.py's order (its per-frame cost launches are filtered out by collect_counters)
         full = [torch.empty(W * H, dtype=torch.int32, device="cuda") for _ in sids]
         order = rtm.batch_order(rtm.frame_costs(gs, fs, [o.data_ptr() for o in full], stream=st.cuda_stream))
