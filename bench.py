@@ -97,11 +97,18 @@ def host_cores():
 
 def end_to_end(rtm, work, reps=7):
     """The drop-in path the reference calls (framebuffer.cpp:59-92, renderer.cpp:133): the host
-    Framebuffer's 12x9 tile workers with the GPU RenderTile -- one launch, copy-back in tile-row
-    bands into page-locked memory, each worker copying its tile out -- timed per frame from
-    rth_framebuffer_start_rendering's call to its return (pool start -> last tile in its host
-    buffer), median of `reps` after one warm-up.  Also the frame alone into host memory
-    (rt_render_frame_host + wait = kernel + PCIe D2H)."""
+    Framebuffer's 12x9 tiles with the GPU RenderTile -- one whole-frame launch written in the tile
+    buffers' own layout into page-locked memory, copied back once -- in two forms, median of `reps`
+    after one warm-up each:
+      framebuffer_ms  the synchronous call (rth_framebuffer_start_rendering: start -> every tile
+                      delivered, by the waiting thread);
+      async_*         the reference's own threading (framebuffer.cpp:124-134, 149-193):
+                      start_rendering_async returns at once (async_return_ms), the delivery thread
+                      hands every tile over under its mutex, and a Draw-like poll (try_lock + dirty
+                      flag, no texture upload) observes the last one (async_last_tile_ms: start ->
+                      the poll seeing all 108 tiles; async_delivery_ms: start -> last tile delivered,
+                      the delivery thread's own clock).
+    Also the frame alone into host memory (rt_render_frame_host + wait = kernel + PCIe D2H)."""
     nthreads = host_cores()
     per = {}
     for sid, hs, gs, f in work.scenes:
@@ -113,6 +120,20 @@ def end_to_end(rtm, work, reps=7):
             t0 = time.perf_counter()
             r.start_rendering()
             ts.append(time.perf_counter() - t0)
+        ta, tr, td = [], [], []
+        for i in range(reps + 1):
+            t0 = time.perf_counter()
+            r.start_rendering_async()
+            t1 = time.perf_counter()
+            done = 0
+            while done < 108:
+                done = r.draw(None)[1]
+            t2 = time.perf_counter()
+            d = r.wait()
+            if i:
+                tr.append(t1 - t0)
+                ta.append(t2 - t0)
+                td.append(d)
         r.close()
         pf = rtm.PinnedFrame(W, H)
         hf = []
@@ -125,12 +146,17 @@ def end_to_end(rtm, work, reps=7):
                     hf.append(time.perf_counter() - t0)
         finally:
             pf.close()
-        per[str(sid)] = {"framebuffer_ms": round(1e3 * sorted(ts)[len(ts) // 2], 4),
-                         "frame_to_host_ms": round(1e3 * sorted(hf)[len(hf) // 2], 4)}
+        med = lambda v: round(1e3 * sorted(v)[len(v) // 2], 4)      # noqa: E731
+        per[str(sid)] = {"framebuffer_ms": med(ts), "async_return_ms": med(tr), "async_last_tile_ms": med(ta),
+                         "async_delivery_ms": med(td), "frame_to_host_ms": med(hf)}
     tot = sum(p["framebuffer_ms"] for p in per.values())
+    tot_async = sum(p["async_last_tile_ms"] for p in per.values())
     return {"value": round(len(work.scenes) * W * H * SPP / (tot / 1e3) / 1e6, 3), "unit": "Msamples/s",
-            "ms_per_step": round(tot, 4), "threads": nthreads, "per_scene": per,
-            "note": "host-buffer delivery incl. PCIe; value is never the bench value"}
+            "ms_per_step": round(tot, 4),
+            "async_value": round(len(work.scenes) * W * H * SPP / (tot_async / 1e3) / 1e6, 3),
+            "async_ms_per_step": round(tot_async, 4), "threads": nthreads, "per_scene": per,
+            "note": "host-buffer delivery incl. PCIe; value: the synchronous call, async_value: start -> last "
+                    "tile seen by the Draw poll; never the bench value"}
 
 
 ORBIT_DEG = 0.5          # moving_camera: degrees the camera orbits the scene per frame
@@ -556,6 +582,110 @@ def check_frames(work, world):
     return f"{len(work.scenes)} frames equal to the one-GPU render"
 
 
+class Collective:
+    """The step's gathers, one per scene: ONE rooted gather to rank 0 (dist.gather: under RCCL grouped
+    ncclSend / ncclRecv, every peer's slice on its own xGMI link; rtm.gather_shards), or the all-gather
+    where the rooted one is unavailable -- which one ran, and why, goes into the bench line."""
+
+    def __init__(self, work, world, rank):
+        import torch
+        self.work, self.world, self.rank = work, world, rank
+        self.kind = "gather"
+        self.fallback = None
+        self.gathered = [[torch.empty(world * b.numel(), dtype=b.dtype, device=b.device) if rank == 0 else None
+                          for b in bset] for bset in work.bufs]
+        try:
+            import torch.distributed as dist
+            if dist.get_backend() == "gloo" and work.bufs[0][0].is_cuda:
+                # rtm.gather_shards: gloo has no gather of CUDA tensors, it all-gathers them
+                self.kind, self.fallback = "all_gather", "gloo on CUDA tensors (rehearsal): no rooted gather"
+        except (RuntimeError, ValueError):
+            pass
+
+    def issue(self, p, i):
+        """Scene i's shards of buffer set p -> rank 0 (async); returns (gathered, work handle)."""
+        buf = self.work.bufs[p][i]
+        if self.kind == "gather":
+            try:
+                return self.work.rtm.gather_shards(buf, self.world, dst=0, out=self.gathered[p][i], async_op=True)
+            except (RuntimeError, NotImplementedError) as e:    # raised on every rank alike
+                print(f"bench: rooted gather unavailable ({e}); using the all-gather", file=sys.stderr)
+                self.kind, self.fallback = "all_gather", f"rooted gather unavailable: {type(e).__name__}: {e}"[:200]
+        if self.gathered[p][i] is None:
+            import torch
+            self.gathered[p][i] = torch.empty(self.world * buf.numel(), dtype=buf.dtype, device=buf.device)
+        return self.work.rtm.all_gather_shards(buf, self.world, out=self.gathered[p][i], async_op=True)
+
+
+def span_ms(work, steps):
+    """Device (HIP events) or, for the CPU rehearsal's workload, host ms per step of this rank's timed
+    render launches."""
+    a, b = work.span
+    if isinstance(a, float):
+        return (b - a) * 1e3 / steps
+    return a.elapsed_time(b) / steps
+
+
+def dist_report(work, world, rank, dist, steps, elapsed, reps=8):
+    """N > 1 (every rank calls it after the timed region): what a step is made of, on rank 0 (None
+    elsewhere).  render_ms: every rank's render span per step (its HIP events around its timed launches),
+    max / min / mean and per rank, gathered to rank 0 -- the step's max-over-ranks wall time against the
+    slowest rank's render shows what the gathers and the un-permute add.  gather_ms: the step's gathers
+    alone (every scene's shards to rank 0), `reps` times after a barrier: on the launch stream between HIP
+    events (RCCL: the collective stream is ordered after the first and before the second by the work
+    handle's wait) and by the host clock around a synchronised call; rank 0's (the root's) median, and the
+    max over ranks.  collective: which one ran (rooted gather or all-gather, with the reason), the backend
+    and the world size the communicator saw."""
+    import torch
+    coll = work.coll
+    dev = work.bufs[0][0].device
+    mine = torch.zeros(2 * world, dtype=torch.float64, device=dev)
+    mine[rank] = span_ms(work, steps)
+    ev_ms, wall_ms = [], []
+    cuda = dev.type == "cuda" and dist.get_backend() != "gloo"
+    for _ in range(reps):
+        dist.barrier()
+        work.sync()
+        t0 = time.perf_counter()
+        a = b = None
+        if cuda:
+            a = torch.cuda.Event(enable_timing=True)
+            a.record(work.stream)
+        with (work.stream_ctx() if hasattr(work, "stream_ctx") else contextlib.nullcontext()):
+            hs = [coll.issue(0, i) for i in range(len(work.bufs[0]))]
+            for _, h in hs:
+                if h is not None:
+                    h.wait()
+            if cuda:
+                b = torch.cuda.Event(enable_timing=True)
+                b.record(work.stream)
+        work.sync()
+        wall_ms.append((time.perf_counter() - t0) * 1e3)
+        if cuda:
+            ev_ms.append(a.elapsed_time(b))
+    med = lambda v: sorted(v)[len(v) // 2] if v else None       # noqa: E731
+    mine[world + rank] = med(ev_ms) if ev_ms else med(wall_ms)
+    dist.all_reduce(mine)                     # every slot is written by one rank only: a gather to all
+    vals = mine.cpu().numpy()
+    if rank != 0:
+        return None
+    render = [round(float(x), 4) for x in vals[:world]]
+    gath = [round(float(x), 4) for x in vals[world:]]
+    step = elapsed / steps * 1e3
+    return {"backend": dist.get_backend(), "world_size": dist.get_world_size(),
+            "collective": coll.kind, "collective_fallback": coll.fallback,
+            "collective_detail": ("dist.gather to rank 0 (RCCL: grouped ncclSend / ncclRecv, one peer per xGMI link)"
+                                  if coll.kind == "gather" else "dist.all_gather_into_tensor / gloo all_gather"),
+            "render_ms": {"max": max(render), "min": min(render), "mean": round(sum(render) / world, 4),
+                          "per_rank": render, "source": "each rank's HIP events around its timed render launches"},
+            "gather_ms": {"rank0": gath[0], "max": max(gath), "per_rank": gath,
+                          "source": ("HIP events on the launch stream around the step's gathers"
+                                     if ev_ms else "host clock around the synchronised gathers"),
+                          "rank0_wall_ms": round(med(wall_ms), 4), "reps": reps},
+            "step_ms": round(step, 4),
+            "step_minus_slowest_render_ms": round(step - max(render), 4)}
+
+
 def run_steps(work, world, rank, steps, warmup, dist=None, graph=False):
     """W untimed warm-up steps, then K timed steps between barrier+sync on both sides; returns
     the max-over-ranks wall time.  A step renders every scene (this rank's tiles when N > 1) and
@@ -570,26 +700,9 @@ def run_steps(work, world, rank, steps, warmup, dist=None, graph=False):
     steps later, after K3 read them.  The pipeline is drained (the last step's frames assembled)
     before the timed region ends."""
     nsets = len(work.bufs)
-    gathered = []
-    if world > 1:
-        import torch
-        gathered = [[torch.empty(world * b.numel(), dtype=b.dtype, device=b.device) if rank == 0 else None
-                     for b in bset] for bset in work.bufs]
-
-    rooted = [True]    # one RCCL gather to rank 0; the all-gather if this torch build lacks it
-
-    def collect(p, i):
-        buf = work.bufs[p][i]
-        if rooted[0]:
-            try:
-                return work.rtm.gather_shards(buf, world, dst=0, out=gathered[p][i], async_op=True)
-            except (RuntimeError, NotImplementedError) as e:    # raised on every rank alike
-                print(f"bench: rooted gather unavailable ({e}); using the all-gather", file=sys.stderr)
-                rooted[0] = False
-        if gathered[p][i] is None:
-            import torch
-            gathered[p][i] = torch.empty(world * buf.numel(), dtype=buf.dtype, device=buf.device)
-        return work.rtm.all_gather_shards(buf, world, out=gathered[p][i], async_op=True)
+    coll = Collective(work, world, rank) if world > 1 else None
+    work.coll = coll
+    collect = coll.issue if coll is not None else None
 
     pending = []       # the previous step's gathers: [(gathered, handle)] per scene
     pending_set = [None]
@@ -735,6 +848,7 @@ def main():
                         graph=args.graph)
     kernel_ms = work.kernel_ms(args.steps)
     step_ms = work.span_ms(args.steps)
+    drep = dist_report(work, world, rank, dist, args.steps, elapsed) if world > 1 else None
     samples_per_step = len(SCENES) * W * H * SPP          # all ranks together
     value = samples_per_step * args.steps / elapsed / 1e6
 
@@ -786,6 +900,8 @@ def main():
             "roofline": roof,
             "cpu_baseline": None,
         }
+        if drep is not None:
+            out["distributed"] = drep
         if args.check:
             out["check"] = check_frames(work, world)
         if args.one_device or args.dist_backend != "nccl":

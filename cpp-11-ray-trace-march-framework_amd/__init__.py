@@ -22,7 +22,8 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 # Everything librt_tracer.so is compiled from: PMC counter files are valid only for this hash
-KERNEL_SOURCES = ("csrc/rt_tracer.hip", "csrc/rt_grid_build.hip", "csrc/rt_device.h",
+KERNEL_SOURCES = ("csrc/rt_kernels.hip", "csrc/rt_walk.h", "csrc/rt_kparams.h", "csrc/rt_plan.hip",
+                  "csrc/rt_scene.h", "csrc/rt_tracer.hip", "csrc/rt_grid_build.hip", "csrc/rt_device.h",
                   "csrc/rt_internal.h", "csrc/rt_box_words.h", "csrc/Makefile", "../include/rt_tracer.h")
 
 
@@ -70,7 +71,8 @@ HOST_SYMBOLS = [
     "rth_scene_camera", "rth_scene_stats_get", "rth_framebuffer_create", "rth_framebuffer_free",
     "rth_framebuffer_set_sample_count", "rth_framebuffer_set_options", "rth_framebuffer_set_intersector",
     "rth_framebuffer_resize",
-    "rth_framebuffer_start_rendering", "rth_framebuffer_read", "rth_framebuffer_save_bmp",
+    "rth_framebuffer_start_rendering", "rth_framebuffer_start_rendering_async", "rth_framebuffer_draw",
+    "rth_framebuffer_wait", "rth_framebuffer_read", "rth_framebuffer_save_bmp",
     "rth_last_error", "rth_scene_set_id", "rth_scene_save", "rth_mesh_read", "rth_mesh_normalize_dimensions",
     "rth_mesh_transform", "rth_mesh_add_quad", "rth_mesh_add_mesh", "rth_mesh_data", "rth_mesh_free",
     "rth_look_at", "rth_scene_table", "rth_framebuffer_create_multi", "rth_framebuffer_transport",
@@ -231,6 +233,9 @@ def host_lib():
         L.rth_framebuffer_set_intersector.argtypes = [vp, c_u32]
         L.rth_framebuffer_resize.argtypes = [vp, c_u32, c_u32, ctypes.POINTER(ctypes.c_double)]
         L.rth_framebuffer_start_rendering.argtypes = [vp, ctypes.POINTER(ctypes.c_double)]
+        L.rth_framebuffer_start_rendering_async.argtypes = [vp]
+        L.rth_framebuffer_draw.argtypes = [vp, vp, ctypes.POINTER(c_u32), ctypes.POINTER(c_u32)]
+        L.rth_framebuffer_wait.argtypes = [vp, ctypes.POINTER(ctypes.c_double)]
         L.rth_framebuffer_read.argtypes = [vp, vp]
         L.rth_framebuffer_save_bmp.argtypes = [vp, ctypes.c_char_p]
         L.rth_last_error.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
@@ -533,9 +538,10 @@ class GpuScene:
         _check(L.rt_render_frame_host(self._h, ctypes.byref(frame), ctypes.c_void_p(host_frame.ptr),
                                       arr, n), L, "rt_render_frame_host")
 
-    def render_frame_host_tiled(self, frame, host_frame, tiles_x=12, tiles_y=9, nlaunch=3):
+    def render_frame_host_tiled(self, frame, host_frame, tiles_x=12, tiles_y=9, nlaunch=1):
         """Asynchronous whole frame into a PinnedFrame in the Framebuffer's tile-buffer layout
-        (rt_render_frame_host_tiled); follow with wait_rows().  tile_views() cuts it into tiles."""
+        (rt_render_frame_host_tiled; nlaunch row-band launches, 1 as the drop-in issues it); follow
+        with wait_rows().  tile_views() cuts it into tiles."""
         L = tracer_lib()
         _check(L.rt_render_frame_host_tiled(self._h, ctypes.byref(frame), ctypes.c_void_p(host_frame.ptr), tiles_x,
                                             tiles_y, nlaunch), L, "rt_render_frame_host_tiled")
@@ -642,7 +648,7 @@ class GpuScene:
 
 def batch_chunks(n):
     """(first frame, frames) of each launch rt_render_batch_device makes for n frames:
-    ceil(n / MAX_BATCH) launches of near-equal size (rt_tracer.hip batch_chunk_len)."""
+    ceil(n / MAX_BATCH) launches of near-equal size (rt_kparams.h batch_chunk_len)."""
     out, i = [], 0
     while i < n:
         left = n - i
@@ -835,6 +841,31 @@ class Renderer:
                "rth_framebuffer_start_rendering")
         return s.value
 
+    def start_rendering_async(self):
+        """Framebuffer::StartRendering as the reference threads it (framebuffer.cpp:124-134): returns
+        at once; the tiles arrive in the background (draw() observes them, wait() joins)."""
+        L = host_lib()
+        _check(L.rth_framebuffer_start_rendering_async(self._h), L, "rth_framebuffer_start_rendering_async")
+
+    def draw(self, display=None):
+        """Framebuffer::Draw (framebuffer.cpp:149-193) into `display` (H x W uint32, the GL textures'
+        stand-in; None: count only): (tiles uploaded, tiles of the frame delivered so far)."""
+        L = host_lib()
+        up, done = c_u32(), c_u32()
+        if display is not None:
+            assert display.dtype == np.uint32 and display.shape == (self.height, self.width) and \
+                display.flags["C_CONTIGUOUS"]
+        _check(L.rth_framebuffer_draw(self._h, None if display is None else _ptr(display), ctypes.byref(up),
+                                      ctypes.byref(done)), L, "rth_framebuffer_draw")
+        return up.value, done.value
+
+    def wait(self):
+        """Joins the frame started by start_rendering_async; returns start -> last tile seconds."""
+        s = ctypes.c_double()
+        L = host_lib()
+        _check(L.rth_framebuffer_wait(self._h, ctypes.byref(s)), L, "rth_framebuffer_wait")
+        return s.value
+
     def read(self):
         out = np.zeros((self.height, self.width), np.uint32)
         L = host_lib()
@@ -858,13 +889,13 @@ class Renderer:
 
 
 # ------------------------------------------------------------------ multi-GPU helpers
-SHARD_ROT = 3     # rt_tracer.hip kShardRot: tile rows rotated by 3 columns per row before the deal
+SHARD_ROT = 3     # rt_kparams.h kShardRot: tile rows rotated by 3 columns per row before the deal
 
 
 def shard_tile_ids(width, height, rank, nranks):
     """Tile indices (16x16 tiles, row-major) owned by `rank`, in local-tile order:
     the rotated number t' = ty * tiles_x + (tx + SHARD_ROT * ty) % tiles_x of a tile is dealt
-    t' % nranks == rank (no rotation at one rank), as rt_tracer.hip's shard_tile_xy."""
+    t' % nranks == rank (no rotation at one rank), as rt_kparams.h's shard_tile_xy."""
     tiles_x = (width + SHARD_TILE - 1) // SHARD_TILE
     tiles_y = (height + SHARD_TILE - 1) // SHARD_TILE
     out = []

@@ -1,0 +1,296 @@
+// rt_plan.hip -- the heavy-first order and the wide section's item list:
+// k_hf_plan, which turns a measured frame's per-wave costs into the next frames' plan, and the host
+// side that keeps one plan context per launch shape (hf_prepare).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+
+#include "rt_scene.h"
+
+namespace rtk {
+namespace {
+
+// Heavy-first planning, after a measured frame's render kernel on its stream: per block the cost
+// of its slowest wave; blocks above max(hf_floor, last max >> kHfShift) are listed for the next
+// frames -- above last max >> 1 at the front of the front section, the rest from its back -- and
+// marked so the natural order skips them.  Nothing is listed when the last measurement showed no
+// tail (its slowest block well under the frame's estimated span).  Each thread takes kHfPlanPer
+// blocks (kWG apart, so the cost loads stay coalesced); each workgroup reduces its maximum and sum
+// and reserves its list slots with ONE atomic per level (the render waves themselves touch no
+// atomics: thousands of same-address atomics from waves cost milliseconds, measured).  The plan's
+// time is those same-address atomics: one block per thread (1,013 workgroups for the batched
+// bench pair) took 26.6 us per plan, which a moving camera pays every frame.
+__global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks)
+{
+    __shared__ uint32_t s_max, s_hi, s_lo, s_w, s_bhi, s_blo, s_bw, s_last;
+    __shared__ unsigned long long s_sum;
+    if (threadIdx.x == 0u)
+    {
+        s_max = s_hi = s_lo = s_w = 0u;
+        s_sum = 0ull;
+    }
+    __syncthreads();
+    const HfPlan last = *P.hf_plan_in;
+    const bool tail = uint64_t(last.maxc) * kHfSlots * 16u > uint64_t(kHfTail) * (last.sum << 4);
+    const uint32_t thr = max(P.hf_floor, last.maxc >> kHfShift);
+    const uint32_t b0 = blockIdx.x * (kWG * kHfPlanPer) + threadIdx.x;
+    uint32_t tmax = 0u, wmasks = 0u, heavy = 0u, hi = 0u;
+    unsigned long long tsum = 0ull;
+    uint32_t rank[kHfPlanPer], wrank[kHfPlanPer];
+#pragma unroll
+    for (uint32_t j = 0; j < kHfPlanPer; j++)
+    {
+        const uint32_t b = b0 + j * kWG;
+        uint32_t cost = 0u, sum = 0u, wmask = 0u;
+        if (b < nblocks)
+        {
+            const uint4 c = reinterpret_cast<const uint4 *>(P.hf_cost)[b];      // kWavesPerWG == 4
+            sum = (c.x >> 4) + (c.y >> 4) + (c.z >> 4) + (c.w >> 4);          // in 16-cycle units
+            if (P.wh_on && !P.wh_wgs && last.sum_full)
+            {
+                // wide section: items above a fraction of the frame span estimated from the last
+                // measurement of every item one lane per sample (sum of wave costs over the resident
+                // waves).  New items are listed only from such frames (the first ones of a shape, the
+                // refresh frames): with the section running, the lane waves' costs shrink as items
+                // leave them, which pulled the span estimate down and listed ever more items
+                // (killeroo's rank of 4: 298 -> 587 items over 100 frames, measured).
+                const uint64_t span = (last.sum_full << 4) / kHfSlots;
+                const uint32_t wt = max(P.wh_floor, uint32_t(min<uint64_t>(span * P.wh_alpha16 / 16u, 0xFFFFFFFFull)));
+                wmask = uint32_t(c.x > wt) | (uint32_t(c.y > wt) << 1) | (uint32_t(c.z > wt) << 2) |
+                        (uint32_t(c.w > wt) << 3);
+            }
+            if (P.wh_on && !P.wh_refresh && P.hf_ver)
+            {
+                // sticky: the current plan's items stay listed (mark = the plan version)
+                const uint4 m = reinterpret_cast<const uint4 *>(P.wh_mark_in)[b];
+                wmask |= uint32_t(m.x == P.hf_ver) | (uint32_t(m.y == P.hf_ver) << 1) | (uint32_t(m.z == P.hf_ver) << 2) |
+                         (uint32_t(m.w == P.hf_ver) << 3);
+            }
+            // the heavy-first order ranks a block by its slowest wave left in the lane section
+            const uint32_t wm = wmask;
+            cost = max(max((wm & 1u) ? 0u : c.x, (wm & 2u) ? 0u : c.y), max((wm & 4u) ? 0u : c.z, (wm & 8u) ? 0u : c.w));
+        }
+        const bool hv = P.hf_front && tail && cost > thr;
+        const bool h1 = hv && cost > (last.maxc >> 1);
+        tmax = max(tmax, cost);
+        tsum += sum;
+        rank[j] = hv ? atomicAdd(h1 ? &s_hi : &s_lo, 1u) : 0u;
+        wrank[j] = wmask ? atomicAdd(&s_w, uint32_t(__popc(wmask))) : 0u;
+        heavy |= uint32_t(hv) << j;
+        hi |= uint32_t(h1) << j;
+        wmasks |= wmask << (4u * j);
+    }
+    if (tmax) atomicMax(&s_max, tmax);
+    if (tsum) atomicAdd(&s_sum, tsum);
+    __syncthreads();
+    if (threadIdx.x == 0u)
+    {
+        if (s_max) atomicMax(&P.hf_plan_out->maxc, s_max);
+        if (s_sum) atomicAdd(&P.hf_plan_out->sum, s_sum);
+        if (P.wh_on)
+        {
+            if (!P.wh_wgs)
+            {
+                if (s_sum) atomicAdd(&P.hf_plan_out->sum_full, s_sum);
+            }
+            else if (blockIdx.x == 0u)
+                P.hf_plan_out->sum_full = last.sum_full;      // carried
+        }
+        s_bhi = s_hi ? atomicAdd(&P.hf_plan_out->cnt_hi, s_hi) : 0u;
+        s_blo = s_lo ? atomicAdd(&P.hf_plan_out->cnt_lo, s_lo) : 0u;
+        s_bw = s_w ? atomicAdd(&P.hf_plan_out->cnt_w, s_w) : 0u;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t j = 0; j < kHfPlanPer; j++)
+    {
+        const uint32_t b = b0 + j * kWG;
+        if ((heavy >> j) & 1u)
+        {
+            // very heavy blocks fill the front section from its start, the others from its end; a
+            // level that runs into the other is cut (those blocks stay in the natural order)
+            const bool h1 = (hi >> j) & 1u;
+            const uint32_t r = (h1 ? s_bhi : s_blo) + rank[j];
+            if (r < P.hf_front)
+            {
+                const uint32_t slot = h1 ? r : P.hf_front - 1u - r;
+                P.hf_list_out[slot] = b;           // may be overwritten by the other level: see below
+            }
+        }
+        // wide items: listed and marked for the next plan's frames (beyond kWhMax they stay in the
+        // lane section)
+        const uint32_t wmask = (wmasks >> (4u * j)) & 15u;
+        uint32_t wr = wrank[j];
+        for (uint32_t k = 0; k < kWavesPerWG; k++)
+            if (wmask & (1u << k))
+            {
+                const uint32_t item = b * kWavesPerWG + k;
+                const uint32_t r = s_bw + wr++;
+                if (r < kWhMax)
+                {
+                    P.wh_list_out[r] = item;
+                    P.wh_mark_out[item] = P.hf_ver + 1u;
+                }
+            }
+    }
+    // The block marks are written by a second pass over the final list, so a slot claimed by
+    // both levels marks only the block whose entry survived.  That pass runs in the workgroup
+    // that finishes last (a ticket after a release fence), not in a second launch: a kernel
+    // launch costs ~4 us, as much as the whole plan at a rank of 8.
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0u) s_last = atomicAdd(P.hf_ticket, 1u) == gridDim.x - 1u;
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();
+    const volatile HfPlan *vp = P.hf_plan_out;
+    const uint32_t ch = vp->cnt_hi, cl = vp->cnt_lo;
+    const uint32_t nhi = min(ch, P.hf_front);
+    const uint32_t nlo = min(cl, P.hf_front - nhi);
+    const volatile uint32_t *vl = P.hf_list_out;
+    for (uint32_t j = threadIdx.x; j < P.hf_front; j += kWG)
+        if (j < nhi || j >= P.hf_front - nlo) P.hf_mark_out[vl[j]] = P.hf_ver + 1u;
+    if (threadIdx.x == 0u)
+    {
+        // hands the wide section's item count to the host (it sizes the section of later
+        // launches) and re-arms the ticket
+        if (P.wh_host_cnt)
+            *(volatile uint32_t *)P.wh_host_cnt = P.wh_g * min(vp->cnt_w, kWhMax);
+        *P.hf_ticket = 0u;
+    }
+}
+
+} // namespace
+
+knfn_t hf_plan_kernel() { return k_hf_plan; }
+
+constexpr uint32_t kWhRefresh = 128;        // frames between refresh frames (a multiple of kHfPeriod)
+
+
+// The camera of a frame as one 64-bit signature (FNV-1a over the bits of the rotation, the origin
+// and the field of view): heavy-first plans are re-measured when it changes between frames.
+uint64_t cam_signature(const KParams& P, uint64_t h)
+{
+    float v[13];
+    std::memcpy(v, P.m, sizeof(P.m));
+    std::memcpy(v + 9, P.org, sizeof(P.org));
+    v[12] = P.fov_xs;
+    const unsigned char *b = reinterpret_cast<const unsigned char *>(v);
+    for (size_t i = 0; i < sizeof(v); i++) h = (h ^ b[i]) * 0x100000001b3ull;
+    return h;
+}
+
+// Heavy-first state for this launch shape (AUTO): fills P.hf_*.  A new shape takes the least
+// recently used context and clears it on the launch stream (no host synchronisation).
+// batch: 0 for a single-frame launch, else an identity of the batch (its scenes and frame count).
+int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hipStream_t st, uint64_t batch,
+               uint64_t cam_sig)
+{
+    if (!batch) cam_sig = cam_signature(P);
+    const uint64_t key[5] = { (blocks << 16) | (uint64_t(P.spp) << 1) | 1u,
+                              (uint64_t(P.rx0) << 32) | P.ry0, (uint64_t(P.rw) << 32) | P.rh,
+                              (uint64_t(P.rank) << 40) | (uint64_t(P.nranks) << 20) | uint64_t(uint32_t(var) >> 12),
+                              batch };
+    HfCtx *c = nullptr;
+    for (HfCtx& h : s->hf)
+        if (std::memcmp(h.key, key, sizeof(key)) == 0) c = &h;
+    if (!c)
+    {
+        c = &s->hf[0];
+        for (HfCtx& h : s->hf)
+            if (h.used < c->used) c = &h;
+        if (c->used) s->hf_evictions++;
+        // invalidated first: if an allocation below fails, no later launch may match the old
+        // shape and read freed (null) state arrays
+        std::memset(c->key, 0, sizeof(c->key));
+        c->frames = 0;
+        c->ver = 0;
+        if (blocks > c->cap_blocks || !c->lists)
+        {
+            c->cap_blocks = 0;
+            if (c->marks) RT_HIP(hipFree(c->marks));
+            if (c->cost) RT_HIP(hipFree(c->cost));
+            if (c->wh_marks) RT_HIP(hipFree(c->wh_marks));
+            c->marks = c->cost = c->wh_marks = nullptr;
+            RT_HIP(hipMalloc(&c->marks, sizeof(uint32_t) * 2 * blocks));
+            RT_HIP(hipMalloc(&c->cost, sizeof(uint32_t) * kWavesPerWG * blocks));
+            RT_HIP(hipMalloc(&c->wh_marks, sizeof(uint32_t) * 2 * kWavesPerWG * blocks));
+            if (!c->lists)
+            {
+                RT_HIP(hipMalloc(&c->plans, sizeof(HfPlan) * 2));
+                RT_HIP(hipMalloc(&c->ticket, sizeof(uint32_t)));
+                RT_HIP(hipMalloc(&c->wh_lists, sizeof(uint32_t) * 2 * kWhMax));   // [version][kWhMax]
+                RT_HIP(hipHostMalloc(&c->wh_cnt, sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent));
+                RT_HIP(hipMalloc(&c->lists, sizeof(uint32_t) * 2 * kHfFrontMax));   // last: marks completion
+            }
+            c->cap_blocks = uint32_t(blocks);
+        }
+        RT_HIP(hipMemsetAsync(c->marks, 0, sizeof(uint32_t) * 2 * c->cap_blocks, st));
+        RT_HIP(hipMemsetAsync(c->wh_marks, 0, sizeof(uint32_t) * 2 * kWavesPerWG * c->cap_blocks, st));
+        RT_HIP(hipMemsetAsync(c->plans, 0, sizeof(HfPlan) * 2, st));
+        RT_HIP(hipMemsetAsync(c->ticket, 0, sizeof(uint32_t), st));
+        *(volatile uint32_t *)c->wh_cnt = 0u;
+        c->nblocks = uint32_t(blocks);
+        // front: an eighth of the blocks, capped, a multiple of the XCD count so the natural
+        // section keeps its block -> XCD assignment
+        c->front = front ? std::min<uint32_t>(kHfFrontMax, uint32_t(blocks / 8u) & ~(kXcds - 1u)) : 0u;
+        std::memcpy(c->key, key, sizeof(key));          // valid only now
+    }
+    c->used = ++s->hf_clock;
+    const uint32_t v = c->ver;
+    P.hf_front = c->front;
+    P.hf_ver = v;
+    // measured: the first two frames (the first plan has no earlier maximum to test a tail
+    // against, so it lists nothing) and then every kHfPeriod-th
+    // ... and every frame whose camera differs from the previous frame's: a moving camera's heavy
+    // blocks move with the view, so the plan comes from the newest view (one frame old) instead of
+    // one up to kHfPeriod frames old
+    P.hf_measure = c->frames < 2u || c->frames % kHfPeriod == 0u || (s->hf_follow && cam_sig != c->cam);
+    c->cam = cam_sig;
+    c->frames++;
+    P.hf_floor = s->hf_floor;
+    P.hf_ticket = c->ticket;
+    P.hf_mark_in = c->marks + size_t(v & 1u) * c->cap_blocks;
+    P.hf_mark_out = c->marks + size_t((v + 1u) & 1u) * c->cap_blocks;
+    P.hf_list_in = c->lists + size_t(v & 1u) * kHfFrontMax;
+    P.hf_list_out = c->lists + size_t((v + 1u) & 1u) * kHfFrontMax;
+    P.hf_plan_in = c->plans + (v & 1u);
+    P.hf_plan_out = c->plans + ((v + 1u) & 1u);
+    P.hf_cost = c->cost;
+    if (var & kVarWideHeavy)
+    {
+        // spp <= 4: 16 lanes per sample; spp 8-16: a pixel's samples fill a wave at 4 lanes each.
+        // The section holds wh_g waves per listed item of the newest plan the host has seen (a
+        // plan or two old: the count is read without waiting); at least one workgroup, since
+        // the device-side list may already be longer (the section is persistent over it).
+        // Refresh: every kWhRefresh-th frame renders every item one lane per sample, so the next
+        // plan re-ranks all items on lane-mode costs (the wide set is otherwise sticky).
+        P.wh_g = P.spp <= 4u ? 16u : 4u;
+        const uint32_t units = *(volatile uint32_t *)c->wh_cnt;         // waves: k_hf_plan counts them
+        P.wh_on = 1u;
+        P.wh_refresh = (c->frames - 1u) % kWhRefresh == 0u;       // frames counts this one
+        P.wh_wgs = P.wh_refresh ? 0u : (units + kWavesPerWG - 1u) / kWavesPerWG;
+        P.wh_floor = s->wh_floor;
+        // a rank of 2 of a batched step lists more (its span estimate includes the other frames'
+        // work); one scene's own rank-of-2 launch measured 25 % slower with it
+        // (profiles/r03o_shard_scaling_bench.json), so it keeps the default
+        // and a rank of 4-7 of a batched step one notch lower than the default (rank of 4, measured
+        // in profiles/r03ad_alpha_n4_n8.json: 0.182 ms at 28/16 vs 0.191 at 32/16, 0.219 at 36/16;
+        // a rank of 8 keeps 32/16: 0.117 vs 0.119 at 28/16)
+        P.wh_alpha16 = (P.nranks == 2u && batch != 0u)                  ? s->wh_alpha16_n2
+                       : (P.nranks >= 3u && P.nranks < 8u && batch != 0u) ? s->wh_alpha16_n4
+                                                                          : s->wh_alpha16;
+        P.wh_mark_in = c->wh_marks + size_t(v & 1u) * kWavesPerWG * c->cap_blocks;
+        P.wh_mark_out = c->wh_marks + size_t((v + 1u) & 1u) * kWavesPerWG * c->cap_blocks;
+        P.wh_list_in = c->wh_lists + size_t(v & 1u) * kWhMax;
+        P.wh_list_out = c->wh_lists + size_t((v + 1u) & 1u) * kWhMax;
+        void *dev = nullptr;
+        RT_HIP(hipHostGetDevicePointer(&dev, c->wh_cnt, 0));
+        P.wh_host_cnt = static_cast<uint32_t *>(dev);
+    }
+    if (P.hf_measure) c->ver = v + 1u;                  // the plan launched after this frame
+    return RT_OK;
+}
+
+} // namespace rtk

@@ -1,0 +1,157 @@
+// rt_scene.h -- the library's scene object (struct rt_scene, opaque in the C ABI) and the host
+// functions rt_tracer.hip and rt_plan.hip share.  Not part of the ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/rt_tracer.h"
+#include "rt_internal.h"
+#include "rt_kparams.h"
+
+// HIP call -> RT_E_HIP with the call's text and the runtime's message (rt_last_error)
+#define RT_HIP(expr)                                                                      \
+    do {                                                                                  \
+        hipError_t e_ = (expr);                                                           \
+        if (e_ != hipSuccess)                                                             \
+            return rt_internal_fail(RT_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+namespace rtk {
+
+// Heavy-first state of one launch shape (device arrays; see KParams::hf_*)
+struct HfCtx
+{
+    uint64_t key[5] = { 0, 0, 0, 0, 0 };   // launch shape: blocks, spp, region, shard, variant, batch
+    uint32_t nblocks = 0, front = 0;
+    uint32_t cap_blocks = 0;            // allocated marks per buffer
+    uint32_t *marks = nullptr;          // [2][cap_blocks]
+    uint32_t *cost = nullptr;           // [cap_blocks * kWavesPerWG] wave cycles of the last frame
+    uint32_t *lists = nullptr;          // [2][kHfFrontMax], by plan version parity
+    HfPlan *plans = nullptr;            // [2], by plan version parity
+    uint32_t *ticket = nullptr;         // k_hf_plan's workgroup ticket
+    uint32_t *wh_marks = nullptr;       // [2][cap_blocks * kWavesPerWG] wide items, by version parity
+    uint32_t *wh_lists = nullptr;       // [2][kWhMax]
+    uint32_t *wh_cnt = nullptr;         // host-mapped: the newest plan's wide item count
+    uint32_t frames = 0;                // frames rendered with this shape
+    uint32_t ver = 0;                   // version of the newest plan launched
+    uint64_t used = 0;                  // LRU stamp
+    uint64_t cam = 0;                   // camera signature of the last frame (cam_signature)
+};
+
+} // namespace rtk
+
+constexpr uint32_t kTimeRing = 64;  // rt_kernel_times: launches kept
+constexpr uint32_t kTimeEvery = 8;  // default: every 8th launch gets the timed event pair
+constexpr uint32_t kMaxBands = 64;   // rt_render_frame_host: row bands per frame
+constexpr uint32_t kTileBands = 8;   // rt_render_tiles: D2H bands overlapped with the scatter
+
+struct rt_scene
+{
+    int device = 0;
+    std::mutex mtx;
+    uint32_t dims[3] = { 0, 0, 0 };
+    float bmin[3], bmax[3], cw = 0, icw = 0;
+    uint32_t ncells = 0, nrefs = 0, ntris = 0, max_cell_refs = 0;
+    uint32_t *d_off = nullptr, *d_cellw = nullptr, *d_cellwo = nullptr, oct_stride = 0;
+    uint32_t *d_cellwb = nullptr, box_stride = 0;  // box-run words: 24 copies (octant x major axis)
+    float4 *d_refs = nullptr, *d_shade = nullptr, *d_facen = nullptr, *d_frefs = nullptr;
+    float4 *d_trimt = nullptr, *d_tridist = nullptr, *d_distblk = nullptr;
+    uint32_t ndist_blk = 0;
+    float scene_scale = 0.0f;
+    float vmin[3] = { 0, 0, 0 }, vmax[3] = { 0, 0, 0 };
+    uint64_t device_bytes = 0;
+    uint32_t compact_wgs = 2048;    // RT_KERNEL_COMPACT grid: 8 x 256-lane workgroups per CU
+    bool rcp_safe = false;          // every |det| of the ray/tri test is far below 2^126 (FAST_RCP)
+    bool pack_ok = false;           // dims <= 512: the remaining-cell counts pack into one word
+    // frefs hold the per-reference terms of this camera origin (bit patterns; valid once computed)
+    bool fref_valid = false;
+    uint32_t fref_org[3] = { 0, 0, 0 };
+    uint64_t *d_clk = nullptr;      // RT_KERNEL_FLAG_WAVE_CLOCK records of the last such launch
+    size_t clk_cap = 0;
+    uint32_t clk_items = 0;
+    // AUTO heavy-first order: per launch shape, which blocks the previous frame found heavy
+    rtk::HfCtx hf[rtk::kHfCtxs];
+    uint64_t hf_clock = 0;
+    uint64_t hf_evictions = 0;      // launch shapes that displaced another's state (rt_scene_info)
+    uint64_t batch_launches = 0;    // rt_render_batch_device chunks led by this scene: one launch ...
+    uint64_t batch_fallbacks = 0;   // ... or one launch per frame (frames that cannot share a launch)
+    // scheduling tunables, read ONCE from the environment at rt_scene_create (A/B sweeps): the
+    // launch path never calls getenv
+    uint32_t hf_floor = 100000;     // RT_HF_FLOOR: heavy-first threshold floor, shader cycles
+    uint32_t hf_min_blocks = 4096;  // RT_HF_MIN_BLOCKS: smallest whole launch taking the heavy-first order
+    uint32_t wh_floor = 100000;     // RT_WH_FLOOR: wide-section threshold floor, shader cycles
+    uint32_t wh_alpha16 = 32;       // RT_WH_ALPHA16: wide threshold, sixteenths of the estimated span
+    uint32_t wh_alpha16_n2 = 16;    // RT_WH_ALPHA16_N2: the same for a rank of 2 of a batched step
+    uint32_t wh_alpha16_n4 = 28;    // RT_WH_ALPHA16_N4: the same for a rank of 3-7 of a batched step
+    uint32_t wh_auto_refs = 128;    // RT_WH_AUTO_REFS: AUTO takes the wide section for >= 2-rank
+                                    // shards of scenes with a cell list this long
+    uint32_t wg64 = 1;              // RT_WG64: AUTO launches of >= wg64_min_blocks 256-lane blocks run
+    uint32_t wg64_min_blocks = 8192; // as one-wave workgroups (k_render_lanes_w64; RT_WG64_MIN_BLOCKS)
+    uint32_t wg64_batch_min_blocks = 0;  // the same for batched launches (RT_WG64_BATCH_MIN_BLOCKS)
+    uint32_t wg64_wide = 0xA;       // RT_WG64_WIDE: bit log2(N) (3: N >= 8): one-wave workgroups also
+                                    // for a rank of N's batch with a wide section
+    uint32_t hf_follow = 1;         // RT_HF_FOLLOW: re-plan the heavy-first order on every frame whose
+                                    // camera moved (0: every kHfPeriod-th frame only)
+    bool octant_words = false;      // 8 ray-octant copies of the empty-run words (else one L-inf word)
+    bool box_words = false;         // 24 box-run word copies: AUTO's empty runs (kVarSkipRun)
+    // camera-space x / y tables of the current frame shape (prepare_ndc)
+    float *d_ndc = nullptr;
+    size_t ndc_cap = 0;
+    std::vector<float> ndc_key;
+    uint32_t ndc_w = 0, ndc_spp = 0;
+    // the frame description the tables above were built for (prepare_samples' fast check: width,
+    // height, spp, fov bits and the caller's sample table; no table rebuild per launch)
+    uint32_t fp_w = 0, fp_h = 0, fp_spp = 0, fp_fov = 0;
+    bool fp_valid = false, fp_custom = false;
+    std::vector<float> fp_tbl;
+    // sample table cache
+    float2 *d_smp = nullptr;
+    uint32_t smp_cap = 0;
+    std::vector<float> smp_host;
+    float *h_smp_pinned = nullptr;
+    // internal stream + timing events
+    hipStream_t stream = nullptr;
+    hipEvent_t ev1 = nullptr;       // after each launch's last kernel (ordering only, no timestamp)
+    bool ev_recorded = false;
+    // render-kernel-only timing: event pair around the render kernel(s) of each launch (not the
+    // heavy-first planning kernels), a ring of the last kTimeRing launches (rt_kernel_times)
+    hipEvent_t kt0[kTimeRing] = {}, kt1[kTimeRing] = {};
+    uint32_t kt_next = 0, kt_count = 0;
+    uint32_t kt_last = kTimeRing;   // ring slot of the last timed launch (kTimeRing: none)
+    uint32_t time_every = kTimeEvery; // rt_scene_set_timing: time every n-th launch (0: none)
+    uint64_t launches = 0;
+    hipStream_t last_stream = nullptr;  // stream of the last launch (cross-stream ordering)
+    // RT_KERNEL_FLAG_WIDE_HEAVY: side stream of the wide section, fork / join events
+    hipStream_t side = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    // staging for rt_render_tiles / records
+    uint32_t *d_frame = nullptr;
+    size_t frame_cap = 0;
+    uint32_t *h_frame = nullptr;
+    size_t hframe_cap = 0;
+    // D2H row bands: rt_render_frame_host's (band_ev/band_y1, read by rt_frame_host_wait) and
+    // rt_render_tiles' own (tile_ev), each event recorded after its band's copy
+    hipEvent_t band_ev[kMaxBands] = {};
+    uint32_t band_y1[kMaxBands] = {};
+    uint32_t nbands = 0;
+    hipEvent_t tile_ev[kTileBands] = {};
+    // rt_render_frame_host_tiled: the second launch stream of its row-band launches and the fork
+    // event (the frame's per-origin records ready) / join event (the other stream's work done)
+    hipStream_t stream2 = nullptr;
+    hipEvent_t ev_t_fork = nullptr, ev_t_join = nullptr;
+};
+
+namespace rtk {
+
+// rt_plan.hip: the heavy-first / wide-section state of this launch shape (fills P.hf_*, P.wh_*)
+// batch: 0 for a single-frame launch, else an identity of the batch (its scenes and frame count)
+int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hipStream_t st, uint64_t batch = 0,
+               uint64_t cam_sig = 0);
+// The camera of a frame as one 64-bit signature (FNV-1a over the rotation, origin and fov bits)
+uint64_t cam_signature(const KParams& P, uint64_t h = 0xcbf29ce484222325ull);
+
+} // namespace rtk

@@ -316,12 +316,12 @@ public:
         CreateWorkerThreads();
     }
 
-    void StartRendering()                                       // framebuffer.cpp:124-134
-    {
-        KillAllWorkerThreads();
-        for (auto& t : m_tiles) t.clear_pending = true;         // Tile::Clear, deferred
-        CreateWorkerThreads();
-    }
+    // framebuffer.cpp:124-134.  The synchronous form (rth_framebuffer_start_rendering) is followed by
+    // Wait(); StartRenderingAsync is the reference's own threading: it returns at once, and the frame's
+    // tiles are delivered in the background -- by the worker pool, or (an inline frame) by the
+    // delivery thread -- each under its mutex with its dirty flag set, for Draw to pick up.
+    void StartRendering() { Start(false); }
+    void StartRenderingAsync() { Start(true); }
 
     // Blocks until every worker has finished the current frame (the reference's join).
     void Wait()
@@ -331,20 +331,32 @@ public:
             // a frame completed by the waiting thread itself (CompletesInline): its tiles, in tile-row
             // order, each under its mutex as a worker would mark it
             m_inline_pending = false;
-            FinishInline();
+            FinishInline(false);
             m_last_frame_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - m_start).count();
         }
         // spin briefly first: a GPU frame ends within a millisecond, and a condition-variable wake-up
-        // costs tens of microseconds of it (the frame's last worker sets m_done_gen)
+        // costs tens of microseconds of it (the frame's last worker sets m_done_gen).  The spin is
+        // bounded by time (2 ms), so a long frame -- CPU-bound or multi-GPU -- blocks instead.
         const uint64_t gen = m_generation_seen.load(std::memory_order_acquire);
-        for (int i = 0; i < 200000 && m_done_gen.load(std::memory_order_acquire) < gen; i++)
-            std::this_thread::yield();
+        if (m_done_gen.load(std::memory_order_acquire) < gen)
+        {
+            const auto spin_end = std::chrono::steady_clock::now() + std::chrono::milliseconds(2);
+            for (uint32_t i = 1; m_done_gen.load(std::memory_order_acquire) < gen; i++)
+            {
+                std::this_thread::yield();
+                if ((i & 63u) == 0u && std::chrono::steady_clock::now() > spin_end) break;
+            }
+        }
         std::unique_lock<std::mutex> lk(m_pool_mtx);
         m_pool_cv.wait(lk, [&] { return m_threads_done == m_running; });
         lk.unlock();
+        bool unreached = false;
+        for (const auto& t : m_tiles) unreached = unreached || t.clear_pending;
+        if (unreached) DrainIssued();                           // no copy-back lands in them after the clear
         for (auto& t : m_tiles)                                 // tiles the frame did not reach
             if (t.clear_pending)
             {
+                std::lock_guard<std::mutex> g(t.mtx);
                 t.Clear();
                 t.clear_pending = false;
             }
@@ -353,6 +365,36 @@ public:
     double LastFrameSeconds() const { return m_last_frame_s; }
     uint32_t Width() const { return m_width; }
     uint32_t Height() const { return m_height; }
+
+    // framebuffer.cpp:149-193 Draw, with the tiles' GL textures replaced by `display` (width x height
+    // words, row-major; NULL: count only).  A tile whose mutex is free (try_lock, as Draw) and whose
+    // buffer changed since its last upload (dirty) is copied into its rectangle and its dirty flag
+    // reset (Tile::UpdateTexture); a tile StartRendering cleared shows cleared until then.  Returns the
+    // tiles uploaded; *done = the current frame's tiles delivered so far (of kTilesX * kTilesY).
+    uint32_t Draw(uint32_t* display, uint32_t* done)
+    {
+        uint32_t updated = 0, ndone = 0;
+        for (auto& t : m_tiles)
+        {
+            if (!t.mtx.try_lock()) continue;
+            ndone += t.delivered ? 1u : 0u;
+            if (display && (t.dirty || t.texture_clear))
+            {
+                for (uint32_t y = 0; y < t.GetHeight(); y++)
+                {
+                    uint32_t* row = display + size_t(t.y0 + y) * m_width + t.x0;
+                    if (t.dirty) std::memcpy(row, t.GetBuffer() + size_t(y) * t.GetWidth(), size_t(t.GetWidth()) * 4);
+                    else std::fill(row, row + t.GetWidth(), 0u);
+                }
+                updated += t.dirty ? 1u : 0u;
+                t.dirty = false;
+                t.texture_clear = false;
+            }
+            t.mtx.unlock();
+        }
+        if (done) *done = ndone;
+        return updated;
+    }
 
     // framebuffer.cpp:195-221 SaveToBMP's assembly step; bitmap row 0 = pixel row 0
     void Assemble(uint32_t* bitmap) const
@@ -379,13 +421,20 @@ protected:
             view = nullptr;
             bgra.assign(std::max<size_t>(1, size_t(GetWidth()) * GetHeight()), 0);
             clear_pending = false;
+            dirty = delivered = false;
+            texture_clear = true;
         }
+        // a worker (or the delivery) finished the tile: under its mutex
+        void MarkDelivered() { clear_pending = false; dirty = delivered = true; }
         void Clear() { std::fill(GetBuffer(), GetBuffer() + size_t(GetWidth()) * GetHeight(), 0u); }
         std::mutex mtx;
         std::vector<uint32_t> bgra = std::vector<uint32_t>(1, 0);
         uint32_t* view = nullptr;
         uint32_t x0 = 0, y0 = 0, x1 = 1, y1 = 1;
         bool clear_pending = false;                             // StartRendering's clear, deferred
+        bool dirty = false;                                     // framebuffer.h:54-65 m_dirty
+        bool delivered = false;                                 // done in the current frame
+        bool texture_clear = true;                              // Draw shows the tile cleared
     };
 
     // true = the whole tile buffer was written (renderer.cpp:74-135 writes every pixel), false =
@@ -396,7 +445,10 @@ protected:
     // thread), so no worker is woken: Wait() runs FinishInline, which delivers every tile in the
     // calling thread.  The pool's wake-ups and hand-offs cost 0.1-0.4 ms of a 0.2-0.4 ms frame.
     virtual bool CompletesInline() const { return false; }
-    virtual void FinishInline() { }
+    // async: run by the delivery thread (StartRenderingAsync), which stops between tiles when asked
+    virtual void FinishInline(bool async) { (void)async; }
+    // waits out a frame's copy-back still in flight (a stopped frame's tiles are cleared after it)
+    virtual void DrainIssued() { }
 
     void KillAllWorkerThreads()                                 // framebuffer.cpp:30-41
     {
@@ -418,6 +470,7 @@ protected:
         for (auto& th : m_threads)
             if (th.joinable()) th.join();
         m_threads.clear();
+        if (m_delivery.joinable()) m_delivery.join();
     }
 
     uint32_t m_width = 1, m_height = 1;
@@ -426,18 +479,44 @@ protected:
     std::array<Tile, kTilesX * kTilesY> m_tiles;
 
 private:
+    void Start(bool async)
+    {
+        KillAllWorkerThreads();
+        for (auto& t : m_tiles)                                 // Tile::Clear + UpdateTexture, deferred
+        {
+            std::lock_guard<std::mutex> g(t.mtx);
+            t.clear_pending = true;
+            t.dirty = t.delivered = false;
+            t.texture_clear = true;
+        }
+        m_async = async;
+        CreateWorkerThreads();
+    }
+
     void CreateWorkerThreads()                                  // framebuffer.cpp:16-28
     {
         if (CompletesInline() && !m_threads_stop)
         {
-            std::lock_guard<std::mutex> lk(m_pool_mtx);
-            m_start = std::chrono::steady_clock::now();
-            BeginFrame();
-            m_threads_done = m_running = 0;
-            m_generation++;
-            m_generation_seen.store(m_generation, std::memory_order_release);
-            m_done_gen.store(m_generation, std::memory_order_release);
-            m_inline_pending = true;
+            {
+                std::lock_guard<std::mutex> lk(m_pool_mtx);
+                m_start = std::chrono::steady_clock::now();
+                BeginFrame();
+                m_generation++;
+                m_generation_seen.store(m_generation, std::memory_order_release);
+                if (!m_async)
+                {
+                    m_threads_done = m_running = 0;
+                    m_done_gen.store(m_generation, std::memory_order_release);
+                    m_inline_pending = true;
+                    return;
+                }
+                // asynchronous: the delivery thread takes the frame's tiles as they land
+                if (!m_delivery.joinable()) m_delivery = std::thread(&Framebuffer::DeliveryThread, this);
+                m_threads_done = 0;
+                m_running = 1;
+                m_deliver_gen++;
+            }
+            m_pool_cv.notify_all();
             return;
         }
         BeginFrame();
@@ -466,6 +545,32 @@ private:
         return t;
     }
 
+    // The asynchronous inline frame's delivery: one parked thread (a frame's wake-up costs one
+    // thread, not the pool's), which runs FinishInline and then reports the frame done as the pool's
+    // last worker would.
+    void DeliveryThread()
+    {
+        uint64_t seen = 0;
+        for (;;)
+        {
+            {
+                std::unique_lock<std::mutex> lk(m_pool_mtx);
+                m_pool_cv.wait(lk, [&] { return m_shutdown || m_deliver_gen != seen; });
+                if (m_shutdown) return;
+                seen = m_deliver_gen;
+            }
+            FinishInline(true);
+            std::lock_guard<std::mutex> lk(m_pool_mtx);
+            if (++m_threads_done == m_running)
+            {
+                if (!m_threads_stop)
+                    m_last_frame_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - m_start).count();
+                m_done_gen.store(m_generation, std::memory_order_release);
+                m_pool_cv.notify_all();
+            }
+        }
+    }
+
     void PoolThread(uint32_t)
     {
         uint64_t seen = 0;
@@ -488,7 +593,7 @@ private:
             Tile* tile = GetNextTileFromQueue();
             if (!tile) break;
             std::lock_guard<std::mutex> g(tile->mtx);
-            if (RenderTile(*tile)) tile->clear_pending = false;
+            if (RenderTile(*tile)) tile->MarkDelivered();       // framebuffer.cpp:72-77 SetDirty(true)
         }
         std::lock_guard<std::mutex> lk(m_pool_mtx);
         if (++m_threads_done == m_running)
@@ -504,6 +609,9 @@ private:
     std::vector<uint32_t> m_work_queue;
     std::mutex m_queue_mtx;
     std::vector<std::thread> m_threads;
+    std::thread m_delivery;                                     // StartRenderingAsync's inline frames
+    uint64_t m_deliver_gen = 0;
+    bool m_async = false;                                       // the current frame was started async
     std::mutex m_pool_mtx;                                      // generation / done counters
     std::condition_variable m_pool_cv;
     uint64_t m_generation = 0;
@@ -583,10 +691,17 @@ protected:
     // BeginFrame; the waiting thread takes its tiles row by row -- one wait per tile row, then each
     // tile of the row under its mutex, as RenderTile would (a copy only for the row-major frame).
     bool CompletesInline() const override { return m_inline && m_issue_early; }
-    void FinishInline() override
+    void FinishInline(bool async) override
     {
         for (auto& t : m_tiles)
         {
+            if (async && m_threads_stop)
+            {
+                // stopped (the next StartRendering / Resize): the frame's copy-back still lands in the
+                // tiles' buffers, so it is waited out before Wait clears the tiles not reached
+                DrainFrame();
+                return;
+            }
             if (t.y1 > m_rows_ready.load())
             {
                 {
@@ -603,9 +718,11 @@ protected:
                 m_rows_ready.store(t.y1);
             }
             std::lock_guard<std::mutex> g(t.mtx);
-            if (RenderTile(t)) t.clear_pending = false;
+            if (RenderTile(t)) t.MarkDelivered();
         }
     }
+
+    void DrainIssued() override { DrainFrame(); }
 
     bool RenderTile(Tile& tile) override
     {
@@ -1254,6 +1371,27 @@ int rth_framebuffer_start_rendering(rth_framebuffer* fb, double* seconds)
 {
     if (!fb) return fail(RT_E_INVALID, "NULL argument");
     fb->r->StartRendering();
+    return finish_frame(fb, seconds);
+}
+
+int rth_framebuffer_start_rendering_async(rth_framebuffer* fb)
+{
+    if (!fb) return fail(RT_E_INVALID, "NULL argument");
+    fb->r->StartRenderingAsync();
+    return fb->r->LastStatus() != RT_OK ? fail(fb->r->LastStatus(), fb->r->LastError()) : RT_OK;
+}
+
+int rth_framebuffer_draw(rth_framebuffer* fb, uint32_t* display, uint32_t* tiles_updated, uint32_t* tiles_done)
+{
+    if (!fb) return fail(RT_E_INVALID, "NULL argument");
+    const uint32_t u = fb->r->Draw(display, tiles_done);
+    if (tiles_updated) *tiles_updated = u;
+    return RT_OK;
+}
+
+int rth_framebuffer_wait(rth_framebuffer* fb, double* seconds)
+{
+    if (!fb) return fail(RT_E_INVALID, "NULL argument");
     return finish_frame(fb, seconds);
 }
 

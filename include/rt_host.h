@@ -101,6 +101,17 @@ int  rth_framebuffer_set_intersector(rth_framebuffer *fb, uint32_t intersector);
  * the frame is complete.  seconds = pool start -> last tile (framebuffer.cpp:21, 86). */
 int  rth_framebuffer_resize(rth_framebuffer *fb, uint32_t width, uint32_t height, double *seconds);
 int  rth_framebuffer_start_rendering(rth_framebuffer *fb, double *seconds);  /* 'r' key */
+/* The reference's own threading (framebuffer.cpp:124-134, 149-193): start_rendering_async returns
+ * at once; the frame's tiles are delivered in the background (one delivery thread, or the worker
+ * pool with RTH_POOL=1), each under its tile mutex with its dirty flag set (framebuffer.cpp:72-77).
+ * draw is Framebuffer::Draw with the GL textures replaced by `display` (width*height words,
+ * row-major; NULL: only count): every tile whose mutex is free (try_lock) and whose dirty flag is
+ * set is copied into its rectangle and the flag reset; tiles_done = the frame's tiles delivered so
+ * far (of 108).  wait joins the frame (what the next start / resize does first); seconds = start ->
+ * last tile delivered. */
+int  rth_framebuffer_start_rendering_async(rth_framebuffer *fb);
+int  rth_framebuffer_draw(rth_framebuffer *fb, uint32_t *display, uint32_t *tiles_updated, uint32_t *tiles_done);
+int  rth_framebuffer_wait(rth_framebuffer *fb, double *seconds);
 /* Assembled frame (row 0 = bottom row, like SaveToBMP), width*height words. */
 int  rth_framebuffer_read(const rth_framebuffer *fb, uint32_t *out_bgra);
 /* Framebuffer::SaveToBMP -> WriteBitmap (bmp_writer.cpp:27-57): 32-bpp bottom-up BMP. */

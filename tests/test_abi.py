@@ -92,7 +92,7 @@ def test_batch_chunks_mirror_the_library():
     """rtm.batch_chunks restates rt_render_batch_device's split (batch_chunk_len, kMaxBatch):
     ceil(n / MAX_BATCH) launches of near-equal size that cover the frames in order; bench.py and
     tools/collect_counters.py time and count a step's launches by it."""
-    src = open(os.path.join(PKG_DIR, "csrc", "rt_tracer.hip")).read()
+    src = open(os.path.join(PKG_DIR, "csrc", "rt_kparams.h")).read()
     assert int(re.search(r"constexpr uint32_t kMaxBatch = (\d+);", src).group(1)) == rtm.MAX_BATCH
     for n in range(1, 40):
         ch = rtm.batch_chunks(n)

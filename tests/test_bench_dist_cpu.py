@@ -62,34 +62,51 @@ def _worker(rank, world, port, q):
         rtm = load_package()
         work = CpuWorkload(rtm, world, rank, bench.SCENES)
         elapsed = bench.run_steps(work, world, rank, steps=3, warmup=1, dist=dist)
+        report = bench.dist_report(work, world, rank, dist, 3, elapsed, reps=3)
         if rank == 0:
             # the drained pipeline holds the last (4th) step's frames; steps alternate buffer sets
             same = all(np.array_equal(work.frames[i], work.expected(i, 3)) for i in range(len(bench.SCENES)))
             same = same and work.sets == [0, 1, 0, 1]
-            q.put(("ok", same, elapsed, work.renders))
+            q.put(("ok", same, elapsed, work.renders, report))
+        else:
+            assert report is None
         dist.barrier()
     except Exception as e:  # pragma: no cover
-        q.put(("err", repr(e), 0, 0))
+        q.put(("err", repr(e), 0, 0, None))
     finally:
         dist.destroy_process_group()
 
 
-def test_bench_run_steps_two_ranks_gloo():
+@pytest.mark.parametrize("world", [2, 4])
+def test_bench_run_steps_gloo(world):
+    """run_steps over `world` gloo ranks, then the N > 1 line's self-explaining fields
+    (bench.dist_report): the collective that ran (the rooted gather: gloo gathers CPU tensors), the
+    backend and the communicator's size, every rank's render span (max / min / mean) and the gathers'
+    own duration, all on rank 0."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    status, same, elapsed, renders = q.get(timeout=300)
+    status, same, elapsed, renders, rep = q.get(timeout=300)
     for p in procs:
         p.join(timeout=120)
     assert status == "ok", same
     assert same
     assert elapsed > 0
     assert renders == (3 + 1) * 2        # (steps + warmup) x scenes
+    assert rep["backend"] == "gloo" and rep["world_size"] == world
+    assert rep["collective"] == "gather" and rep["collective_fallback"] is None
+    r = rep["render_ms"]
+    assert len(r["per_rank"]) == world and all(x > 0 for x in r["per_rank"])
+    assert r["min"] <= r["mean"] <= r["max"] == max(r["per_rank"])
+    g = rep["gather_ms"]
+    assert len(g["per_rank"]) == world and g["rank0"] > 0 and g["max"] >= g["rank0"]
+    assert g["source"].startswith("host clock") and g["reps"] == 3
+    assert rep["step_ms"] > 0
 
 
 @pytest.mark.gpu
@@ -115,3 +132,6 @@ def test_bench_two_ranks_one_gpu_rehearsal():
     line = next(l for l in r.stdout.splitlines() if l.startswith("{"))
     out = json.loads(line)
     assert out["n_gpus"] == 2 and out["check"] == "2 frames equal to the one-GPU render"
+    d = out["distributed"]
+    assert d["backend"] == "gloo" and d["world_size"] == 2 and d["collective"] == "all_gather"
+    assert d["collective_fallback"] and len(d["render_ms"]["per_rank"]) == 2 and d["gather_ms"]["rank0"] > 0

@@ -15,7 +15,8 @@ import pytest
 
 from conftest import PKG_DIR
 
-SRC = os.path.join(PKG_DIR, "csrc", "rt_tracer.hip")
+SRC = os.path.join(PKG_DIR, "csrc", "rt_kernels.hip")
+WALK = os.path.join(PKG_DIR, "csrc", "rt_walk.h")
 GRID_SRC = os.path.join(PKG_DIR, "csrc", "rt_grid_build.hip")
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize",
@@ -37,12 +38,12 @@ def test_device_ir_has_no_contraction_or_fast_math(tmp_path, src):
     # pixel's arithmetic; tests/test_lane_runs.py); any other llvm.fma would be a contraction in
     # disguise
     assert not re.search(r"\bllvm\.fma\.f64\b", ir)
-    for f in (SRC, GRID_SRC, os.path.join(PKG_DIR, "csrc", "rt_device.h")):
+    for f in (SRC, WALK, GRID_SRC, os.path.join(PKG_DIR, "csrc", "rt_device.h")):
         text = open(f).read().splitlines()
         lines = [l for l in text if re.search(r"\bfmaf?\b|__builtin_fma", l)]
         assert all("__builtin_fmaf(" in l for l in lines), lines
-        assert len(lines) == (0 if f == GRID_SRC else 2), (f, lines)
-        if f == SRC:
+        assert len(lines) == (0 if f in (SRC, GRID_SRC) else 2), (f, lines)
+        if f == WALK:
             i = next(j for j, l in enumerate(text) if "float box_exit_bound(" in l)
             assert all(l in text[i:i + 5] for l in lines), lines
     for flag in (" contract ", " afn ", " arcp ", " nnan ", " ninf ", " nsz ", " reassoc ", " fast "):
@@ -74,9 +75,9 @@ def test_render_kernels_do_not_spill(tmp_path):
     for key in ("k_render_lanesILi0ELi80398E", "k_render_lanesILi0ELi78350E", "k_render_lanesILi0ELi76298E",
                 "k_render_lanesILi0ELi74250E", "k_render_lanesILi0ELi604686E", "k_render_lanesILi0ELi0E",
                 "k_render_compact", "k_render_lanes_w64ILi0ELi80398E", "k_render_batch_w64ILi0ELi80398E",
-                "k_render_batch_w64ILi0ELi604686E", "k_render_batch_w64ILi0ELi1653262E",
-                "k_render_batch_w64ILi0ELi3750414E", "k_render_batchILi0ELi80398E", "k_render_batchILi0ELi604686E",
-                "k_render_whILj16E", "k_render_whILj4E", "k_render_wh_batchILj16E", "k_render_wh_batch_w64ILj16E"):
+                "k_render_batch_w64ILi0ELi1653262E",
+                "k_render_batch_w64ILi0ELi3750414E", "k_render_batchILi0ELi80398E", 
+                "k_render_whILj16E", "k_render_whILj4E"):
         arm = [v for n, v in render.items() if key in n]
         assert arm and all(a[2] == 8 for a in arm), (key, arm)
     # the 256-lane batch kernels with the wide section fused in (a rank of 3-7): their 84-91 SGPRs

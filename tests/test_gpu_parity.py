@@ -536,18 +536,6 @@ def _batched_rank_frames(golden, nranks, frames=6):
             h.close()
 
 
-@pytest.mark.parametrize("nranks,beta", [(8, 20), (4, 16), (2, 12)])
-def test_second_wide_tier_batched_frames(golden, nranks, beta, monkeypatch):
-    """The wide section's second tier (RT_WH_BETA16: items between beta/16 and alpha/16 of the span
-    estimate traced 4 lanes per sample, after the first tier's 16): the bench pair's
-    batched rank-of-N launches over 6 frames, both partitions reassembled into the reference
-    frames, with the tier listing items (more section waves than without it)."""
-    base = _batched_rank_frames(golden, nranks)
-    monkeypatch.setenv("RT_WH_BETA16", str(beta))
-    tiered = _batched_rank_frames(golden, nranks)
-    assert tiered > base, (base, tiered)
-
-
 @pytest.mark.parametrize("sid,nranks,kernel", [(8, 8, 0), (5, 4, 0), (8, 2, 0x200), (5, 1, 0x200), (8, 4, 0)])
 def test_wide_heavy_shard_frames(golden, scenes, sid, nranks, kernel, monkeypatch):
     """RT_KERNEL_FLAG_WIDE_HEAVY over consecutive frames of every rank: frames 0-1 render one
@@ -802,6 +790,46 @@ def test_framebuffer_tile_pool_drop_in(golden, scenes, tmp_path):
     assert data[54:] == img.tobytes()
     r.start_rendering()
     assert hashlib.sha256(r.read().tobytes()).hexdigest() == golden["frames_1080p4"]["1"]["bgra_sha256"]
+    r.close()
+
+
+@pytest.mark.parametrize("pool", ["0", "1"])
+def test_framebuffer_async_draw(golden, scenes, monkeypatch, pool):
+    """The reference's own threading (framebuffer.cpp:124-134, 149-193): start_rendering_async returns
+    at once, and a Draw-like poll observes the tiles as they are delivered -- each under its mutex with
+    its dirty flag set (try_lock, one upload per tile per frame) -- by the delivery thread (inline
+    frames, pool "0") or the worker pool (RTH_POOL=1).  The drawn display and the read frame equal
+    the reference's; a frame stopped by the next start leaves no torn tile."""
+    import time
+    monkeypatch.setenv("RTH_POOL", pool)
+    hs, gs = scenes(8)
+    r = rtm.Renderer(hs, gs)
+    r.set_sample_count(4)
+    r.resize(1920, 1080)
+    gold = golden["frames_1080p4"]["8"]["bgra_sha256"]
+    disp = np.full((1080, 1920), 0xDEADBEEF, np.uint32)
+    for rep in range(3):
+        r.start_rendering_async()
+        uploads, done = 0, 0
+        t0 = time.perf_counter()
+        while done < 108:
+            up, done = r.draw(disp)
+            uploads += up
+            assert time.perf_counter() - t0 < 30, (rep, done)
+        up, done = r.draw(disp)
+        uploads += up
+        assert (done, uploads) == (108, 108), rep
+        assert r.draw(disp) == (0, 108)                     # nothing dirty any more
+        assert hashlib.sha256(disp.tobytes()).hexdigest() == gold, rep
+        assert r.wait() > 0.0
+        assert hashlib.sha256(r.read().tobytes()).hexdigest() == gold, rep
+    # started again before the first frame is drawn: the first one is stopped (its tiles either
+    # delivered whole or cleared), the second is complete
+    r.start_rendering_async()
+    r.start_rendering_async()
+    r.wait()
+    assert r.draw(None)[1] == 108
+    assert hashlib.sha256(r.read().tobytes()).hexdigest() == gold
     r.close()
 
 

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Register / occupancy table of every kernel in rt_tracer.hip (compiler resource remarks):
+"""Register / occupancy table of every kernel in rt_kernels.hip (compiler resource remarks):
     python3 tools/kernel_regs.py [-DRT_TB=0 ...]"""
 import os
 import re
@@ -7,7 +7,7 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SRC = os.path.join(ROOT, "cpp-11-ray-trace-march-framework_amd", "csrc", "rt_tracer.hip")
+SRC = os.path.join(ROOT, "cpp-11-ray-trace-march-framework_amd", "csrc", "rt_kernels.hip")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-slp-vectorize"]
 out = subprocess.run(["/opt/rocm/bin/hipcc"] + FLAGS + sys.argv[1:] + ["-c", "-o", "/tmp/kr.o", SRC,
                       "-Rpass-analysis=kernel-resource-usage"], capture_output=True, text=True).stderr
