@@ -58,7 +58,7 @@ TRACER_SYMBOLS = [
     "rt_get_device_count", "rt_scene_create", "rt_scene_destroy", "rt_scene_device_bytes",
     "rt_render_tiles", "rt_render_frame_device", "rt_shard_elems", "rt_render_shard_device",
     "rt_unshard_device", "rt_last_kernel_ms", "rt_trace_samples", "rt_debug_primitives",
-    "rt_debug_rcp_check", "rt_debug_gamma_check", "rt_debug_wave_clocks", "rt_debug_heavy_first", "rt_debug_wide_items", "rt_scene_set_timing",
+    "rt_debug_rcp_check", "rt_debug_gamma_check", "rt_debug_wave_clocks", "rt_debug_heavy_first", "rt_debug_wide_items", "rt_debug_wide_tiers", "rt_scene_set_timing",
     "rt_sample_table", "rt_last_error", "rt_abi_version", "rt_grid_build", "rt_grid_free",
     "rt_scene_create_from_mesh", "rt_kernel_times", "rt_render_frame_host", "rt_frame_host_wait", "rt_host_alloc",
     "rt_host_free", "rt_render_hits_device", "rt_scene_info_get", "rt_build_hash", "rt_render_batch_device",
@@ -196,6 +196,7 @@ def tracer_lib():
                                                ctypes.POINTER(c_u32)]
         if hasattr(L, "rt_debug_wide_items"):
             L.rt_debug_wide_items.argtypes = [vp, ctypes.POINTER(c_u32)]
+        L.rt_debug_wide_tiers.argtypes = [vp, ctypes.POINTER(c_u32), ctypes.POINTER(c_u32)]
         if hasattr(L, "rt_scene_set_timing"):
             L.rt_scene_set_timing.argtypes = [vp, c_u32]
         L.rt_sample_table.argtypes = [c_u32, vp]
@@ -614,6 +615,13 @@ class GpuScene:
         n = c_u32()
         _check(L.rt_debug_wide_items(self._h, ctypes.byref(n)), L, "rt_debug_wide_items")
         return n.value
+
+    def wide_tiers(self):
+        """(lane-split tier items, segmented tier items) of the newest plan (rt_debug_wide_tiers)."""
+        L = tracer_lib()
+        a, b = c_u32(), c_u32()
+        _check(L.rt_debug_wide_tiers(self._h, ctypes.byref(a), ctypes.byref(b)), L, "rt_debug_wide_tiers")
+        return a.value, b.value
 
     def last_kernel_ms(self):
         ms = c_f32()

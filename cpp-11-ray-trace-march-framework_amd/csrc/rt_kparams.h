@@ -31,6 +31,7 @@ constexpr int kVarUniform = 65536;          // scalar loop for wave-uniform cell
 constexpr int kVarWideHeavy = 524288;       // RT_KERNEL_FLAG_WIDE_HEAVY: heavy items traced wide at the start
 constexpr int kVarWideFused = 1048576;      // batch kernel: the wide section's blocks lead the same grid
 constexpr int kVarWideG4 = 2097152;         // the wide section at 4 lanes per sample (spp 8-16; else 16)
+constexpr int kVarWideSeg = 4194304;        // the wide section's segmented tier: 4 t-segments x 16 lanes per sample
 // AUTO's traversal: every feature above that is exact for every scene ...
 constexpr int kVarAutoCore = kVarWaveGate | kVarDistSkip | kVarOriginPre | kVarXcdBands | kVarUniform;
 // ... plus the two that need a scene property (rt_scene::rcp_safe, rt_scene::pack_ok)
@@ -48,7 +49,8 @@ constexpr uint32_t kCompactRefill = 48;     // RT_KERNEL_COMPACT default: refill
 // sum of wave costs of the measured frame
 // sum_full: the sum of wave costs of the last measured frame that rendered every item one lane
 // per sample (the wide section's span estimate; carried over by the plans of other frames)
-struct HfPlan { uint32_t cnt_hi, cnt_lo, maxc, cnt_w; unsigned long long sum; unsigned long long sum_full; };
+// cnt_s: work items listed for the wide section's segmented tier (kVarWideSeg; the list's second half)
+struct HfPlan { uint32_t cnt_hi, cnt_lo, maxc, cnt_w; unsigned long long sum; unsigned long long sum_full; uint32_t cnt_s, pad; };
 
 struct KParams
 {
@@ -123,6 +125,12 @@ struct KParams
     // them) except in a refresh frame.
     uint32_t wh_on, wh_wgs, wh_refresh, wh_g;
     uint32_t wh_floor, wh_alpha16;
+    // kVarWideSeg: items above wh_seg_alpha16 / 16 of the span estimate are listed for the segmented tier
+    // (one wave per sample slot: 64 per item; the list's second half, wh_list + kWhMax; marks with bit
+    // 31), the others above wh_alpha16 / 16 for the wh_g-lane tier
+    uint32_t wh_seg, wh_seg_alpha16;
+    float4 *wh_col;             // kVarWideSeg: per list entry, the 64 sample slots' colours (cross-wave resolve)
+    uint32_t *wh_px;            // kVarWideSeg: per list entry, arrivals per pixel (<= 64 pixels)
     const uint32_t *wh_mark_in;
     uint32_t *wh_mark_out;
     const uint32_t *wh_list_in;
@@ -226,7 +234,7 @@ kfn_t lanes_w64_kernel(int var);               // k_render_lanes_w64<MT, var>
 kfn_t wide_kernel(uint32_t g);                 // k_render_wh<g>, g = 4 or 16
 kfn_t pixel_loop_kernel(int tri, int var);     // k_render_pixel_loop<tri, var>
 kcfn_t compact_kernel(int tri, int var);       // k_render_compact<tri, var>(P, n_items, refill)
-kbfn_t batch_kernel(int var, bool w64);        // k_render_batch / k_render_batch_w64<MT, var>
+kbfn_t batch_kernel(int var, bool w64, bool o8 = false);   // k_render_batch / _w64 / _w64_o8<MT, var>
 knfn_t trace_records_kernel();                 // k_trace_records(P, n)
 knfn_t record_fixup_kernel();                  // k_record_fixup(P, n)
 knfn_t hf_plan_kernel();                       // k_hf_plan(P, nblocks) (rt_plan.hip)

@@ -23,11 +23,11 @@ namespace {
 // bench pair) took 26.6 us per plan, which a moving camera pays every frame.
 __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks)
 {
-    __shared__ uint32_t s_max, s_hi, s_lo, s_w, s_bhi, s_blo, s_bw, s_last;
+    __shared__ uint32_t s_max, s_hi, s_lo, s_w, s_s, s_bhi, s_blo, s_bw, s_bs, s_last;
     __shared__ unsigned long long s_sum;
     if (threadIdx.x == 0u)
     {
-        s_max = s_hi = s_lo = s_w = 0u;
+        s_max = s_hi = s_lo = s_w = s_s = 0u;
         s_sum = 0ull;
     }
     __syncthreads();
@@ -35,14 +35,14 @@ __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks)
     const bool tail = uint64_t(last.maxc) * kHfSlots * 16u > uint64_t(kHfTail) * (last.sum << 4);
     const uint32_t thr = max(P.hf_floor, last.maxc >> kHfShift);
     const uint32_t b0 = blockIdx.x * (kWG * kHfPlanPer) + threadIdx.x;
-    uint32_t tmax = 0u, wmasks = 0u, heavy = 0u, hi = 0u;
+    uint32_t tmax = 0u, wmasks = 0u, smasks = 0u, heavy = 0u, hi = 0u;
     unsigned long long tsum = 0ull;
-    uint32_t rank[kHfPlanPer], wrank[kHfPlanPer];
+    uint32_t rank[kHfPlanPer], wrank[kHfPlanPer], srank[kHfPlanPer];
 #pragma unroll
     for (uint32_t j = 0; j < kHfPlanPer; j++)
     {
         const uint32_t b = b0 + j * kWG;
-        uint32_t cost = 0u, sum = 0u, wmask = 0u;
+        uint32_t cost = 0u, sum = 0u, wmask = 0u, smask = 0u;
         if (b < nblocks)
         {
             const uint4 c = reinterpret_cast<const uint4 *>(P.hf_cost)[b];      // kWavesPerWG == 4
@@ -59,16 +59,28 @@ __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks)
                 const uint32_t wt = max(P.wh_floor, uint32_t(min<uint64_t>(span * P.wh_alpha16 / 16u, 0xFFFFFFFFull)));
                 wmask = uint32_t(c.x > wt) | (uint32_t(c.y > wt) << 1) | (uint32_t(c.z > wt) << 2) |
                         (uint32_t(c.w > wt) << 3);
+                // the segmented tier (kVarWideSeg): the heaviest items, one wave per sample
+                if (P.wh_seg)
+                {
+                    const uint32_t ws = max(P.wh_floor, uint32_t(min<uint64_t>(span * P.wh_seg_alpha16 / 16u, 0xFFFFFFFFull)));
+                    smask = uint32_t(c.x > ws) | (uint32_t(c.y > ws) << 1) | (uint32_t(c.z > ws) << 2) |
+                            (uint32_t(c.w > ws) << 3);
+                    wmask &= ~smask;
+                }
             }
             if (P.wh_on && !P.wh_refresh && P.hf_ver)
             {
-                // sticky: the current plan's items stay listed (mark = the plan version)
+                // sticky: the current plan's items stay listed in their tier (mark = the plan version,
+                // bit 31: the segmented tier)
                 const uint4 m = reinterpret_cast<const uint4 *>(P.wh_mark_in)[b];
-                wmask |= uint32_t(m.x == P.hf_ver) | (uint32_t(m.y == P.hf_ver) << 1) | (uint32_t(m.z == P.hf_ver) << 2) |
-                         (uint32_t(m.w == P.hf_ver) << 3);
+                const uint32_t v = P.hf_ver, vs = P.hf_ver | 0x80000000u;
+                wmask |= uint32_t(m.x == v) | (uint32_t(m.y == v) << 1) | (uint32_t(m.z == v) << 2) | (uint32_t(m.w == v) << 3);
+                smask |= uint32_t(m.x == vs) | (uint32_t(m.y == vs) << 1) | (uint32_t(m.z == vs) << 2) |
+                         (uint32_t(m.w == vs) << 3);
+                wmask &= ~smask;
             }
             // the heavy-first order ranks a block by its slowest wave left in the lane section
-            const uint32_t wm = wmask;
+            const uint32_t wm = wmask | smask;
             cost = max(max((wm & 1u) ? 0u : c.x, (wm & 2u) ? 0u : c.y), max((wm & 4u) ? 0u : c.z, (wm & 8u) ? 0u : c.w));
         }
         const bool hv = P.hf_front && tail && cost > thr;
@@ -77,9 +89,11 @@ __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks)
         tsum += sum;
         rank[j] = hv ? atomicAdd(h1 ? &s_hi : &s_lo, 1u) : 0u;
         wrank[j] = wmask ? atomicAdd(&s_w, uint32_t(__popc(wmask))) : 0u;
+        srank[j] = smask ? atomicAdd(&s_s, uint32_t(__popc(smask))) : 0u;
         heavy |= uint32_t(hv) << j;
         hi |= uint32_t(h1) << j;
         wmasks |= wmask << (4u * j);
+        smasks |= smask << (4u * j);
     }
     if (tmax) atomicMax(&s_max, tmax);
     if (tsum) atomicAdd(&s_sum, tsum);
@@ -100,6 +114,7 @@ __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks)
         s_bhi = s_hi ? atomicAdd(&P.hf_plan_out->cnt_hi, s_hi) : 0u;
         s_blo = s_lo ? atomicAdd(&P.hf_plan_out->cnt_lo, s_lo) : 0u;
         s_bw = s_w ? atomicAdd(&P.hf_plan_out->cnt_w, s_w) : 0u;
+        s_bs = s_s ? atomicAdd(&P.hf_plan_out->cnt_s, s_s) : 0u;
     }
     __syncthreads();
 #pragma unroll
@@ -120,8 +135,8 @@ __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks)
         }
         // wide items: listed and marked for the next plan's frames (beyond kWhMax they stay in the
         // lane section)
-        const uint32_t wmask = (wmasks >> (4u * j)) & 15u;
-        uint32_t wr = wrank[j];
+        const uint32_t wmask = (wmasks >> (4u * j)) & 15u, smask = (smasks >> (4u * j)) & 15u;
+        uint32_t wr = wrank[j], sr = srank[j];
         for (uint32_t k = 0; k < kWavesPerWG; k++)
             if (wmask & (1u << k))
             {
@@ -131,6 +146,16 @@ __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks)
                 {
                     P.wh_list_out[r] = item;
                     P.wh_mark_out[item] = P.hf_ver + 1u;
+                }
+            }
+            else if (smask & (1u << k))
+            {
+                const uint32_t item = b * kWavesPerWG + k;
+                const uint32_t r = s_bs + sr++;
+                if (r < kWhMax)
+                {
+                    P.wh_list_out[kWhMax + r] = item;
+                    P.wh_mark_out[item] = (P.hf_ver + 1u) | 0x80000000u;
                 }
             }
     }
@@ -156,7 +181,7 @@ __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks)
         // hands the wide section's item count to the host (it sizes the section of later
         // launches) and re-arms the ticket
         if (P.wh_host_cnt)
-            *(volatile uint32_t *)P.wh_host_cnt = P.wh_g * min(vp->cnt_w, kWhMax);
+            *(volatile uint32_t *)P.wh_host_cnt = P.wh_g * min(vp->cnt_w, kWhMax) + 64u * min(vp->cnt_s, kWhMax);
         *P.hf_ticket = 0u;
     }
 }
@@ -220,7 +245,7 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
             {
                 RT_HIP(hipMalloc(&c->plans, sizeof(HfPlan) * 2));
                 RT_HIP(hipMalloc(&c->ticket, sizeof(uint32_t)));
-                RT_HIP(hipMalloc(&c->wh_lists, sizeof(uint32_t) * 2 * kWhMax));   // [version][kWhMax]
+                RT_HIP(hipMalloc(&c->wh_lists, sizeof(uint32_t) * 2 * 2 * kWhMax));   // [version][tier][kWhMax]
                 RT_HIP(hipHostMalloc(&c->wh_cnt, sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent));
                 RT_HIP(hipMalloc(&c->lists, sizeof(uint32_t) * 2 * kHfFrontMax));   // last: marks completion
             }
@@ -283,8 +308,21 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
                                                                           : s->wh_alpha16;
         P.wh_mark_in = c->wh_marks + size_t(v & 1u) * kWavesPerWG * c->cap_blocks;
         P.wh_mark_out = c->wh_marks + size_t((v + 1u) & 1u) * kWavesPerWG * c->cap_blocks;
-        P.wh_list_in = c->wh_lists + size_t(v & 1u) * kWhMax;
-        P.wh_list_out = c->wh_lists + size_t((v + 1u) & 1u) * kWhMax;
+        // the segmented tier (kVarWideSeg): one wave per sample slot, the pixel's samples resolved
+        // across waves through the context's scratch (the counters start at 0; the last arrival of a
+        // pixel re-arms its counter)
+        P.wh_seg = (var & kVarWideSeg) ? 1u : 0u;
+        P.wh_seg_alpha16 = s->wh_seg_alpha16;
+        if (P.wh_seg && !c->seg_col)
+        {
+            RT_HIP(hipMalloc(&c->seg_col, sizeof(float4) * 64u * kWhMax));
+            RT_HIP(hipMalloc(&c->seg_px, sizeof(uint32_t) * 64u * kWhMax));
+            RT_HIP(hipMemsetAsync(c->seg_px, 0, sizeof(uint32_t) * 64u * kWhMax, st));
+        }
+        P.wh_col = c->seg_col;
+        P.wh_px = c->seg_px;
+        P.wh_list_in = c->wh_lists + size_t(v & 1u) * 2u * kWhMax;
+        P.wh_list_out = c->wh_lists + size_t((v + 1u) & 1u) * 2u * kWhMax;
         void *dev = nullptr;
         RT_HIP(hipHostGetDevicePointer(&dev, c->wh_cnt, 0));
         P.wh_host_cnt = static_cast<uint32_t *>(dev);

@@ -36,6 +36,8 @@ struct HfCtx
     uint32_t *wh_marks = nullptr;       // [2][cap_blocks * kWavesPerWG] wide items, by version parity
     uint32_t *wh_lists = nullptr;       // [2][kWhMax]
     uint32_t *wh_cnt = nullptr;         // host-mapped: the newest plan's wide item count
+    float4 *seg_col = nullptr;          // kVarWideSeg scratch: [kWhMax][64] sample colours
+    uint32_t *seg_px = nullptr;         // kVarWideSeg scratch: [kWhMax][64] arrivals per pixel
     uint32_t frames = 0;                // frames rendered with this shape
     uint32_t ver = 0;                   // version of the newest plan launched
     uint64_t used = 0;                  // LRU stamp
@@ -92,6 +94,11 @@ struct rt_scene
     uint32_t wg64 = 1;              // RT_WG64: AUTO launches of >= wg64_min_blocks 256-lane blocks run
     uint32_t wg64_min_blocks = 8192; // as one-wave workgroups (k_render_lanes_w64; RT_WG64_MIN_BLOCKS)
     uint32_t wg64_batch_min_blocks = 0;  // the same for batched launches (RT_WG64_BATCH_MIN_BLOCKS)
+    uint32_t wh_seg_alpha16 = 32;   // RT_WH_SEG_ALPHA16: the segmented tier's threshold, sixteenths of the span
+    uint32_t wh_seg_min_ranks = 0;  // RT_WH_SEG_MIN_RANKS: a batch of >= this many ranks (spp <= 4) traces its
+                                    // heaviest wide items in the segmented tier (kVarWideSeg; 0: never, the
+                                    // default: measured slower)
+    uint32_t wg64_o8 = 1;           // RT_WG64_O8: the fused one-wave batch kernels held to 8 waves / SIMD
     uint32_t wg64_wide = 0xA;       // RT_WG64_WIDE: bit log2(N) (3: N >= 8): one-wave workgroups also
                                     // for a rank of N's batch with a wide section
     uint32_t hf_follow = 1;         // RT_HF_FOLLOW: re-plan the heavy-first order on every frame whose

@@ -551,8 +551,10 @@ int launch_batch(rt_scene *const *S, const rt_frame *F, uint32_t n, KParams *P, 
     // removed in round 5)
     const bool fused = wide_heavy;
     const bool clk = (F[0].kernel & RT_KERNEL_FLAG_WAVE_CLOCK) != 0u;
+    // the segmented tier (kVarWideSeg): a rank of >= wh_seg_min_ranks at spp <= 4
+    const bool seg = fused && spp <= 4u && S[0]->wh_seg_min_ranks != 0u && P[0].nranks >= S[0]->wh_seg_min_ranks;
     const int kvar = var | (wide_heavy ? kVarWideHeavy : 0) | (fused ? kVarWideFused : 0) |
-                     (fused && spp > 4u ? kVarWideG4 : 0) | (clk ? kVarWaveClock : 0);
+                     (fused && spp > 4u ? kVarWideG4 : 0) | (seg ? kVarWideSeg : 0) | (clk ? kVarWaveClock : 0);
     if (!batch_kernel(kvar, false)) return RT_E_INVALID;
     const uint32_t wgpt = (kTilePix * spp) / kWG;
     const uint64_t fblocks = uint64_t(n_local_tiles) * wgpt;
@@ -606,11 +608,11 @@ int launch_batch(rt_scene *const *S, const rt_frame *F, uint32_t n, KParams *P, 
         grid = kWavesPerWG * ((fused ? P[0].wh_wgs : 0u) + (P[0].vblocks + kXcds - 1u) / kXcds * kXcds);
         bwg = 64u;
     }
-    const kbfn_t fn = batch_kernel(kvar, w64);
+    const kbfn_t fn = batch_kernel(kvar, w64, s0->wg64_o8 != 0u && (kvar & kVarWideFused) != 0);
     if (clk)
     {
         // one record per lane item and per (listed item, wave) of the wide section
-        const size_t need = (size_t(blocks) * kWavesPerWG + size_t(kWhMax) * 20u) * 4u;
+        const size_t need = (size_t(blocks) * kWavesPerWG + size_t(kWhMax) * (16u + 64u)) * 4u;
         if (need > s0->clk_cap)
         {
             if (s0->d_clk) RT_HIP(hipFree(s0->d_clk));
@@ -809,6 +811,9 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
     s->wh_alpha16_n4 = env_tunable("RT_WH_ALPHA16_N4", s->wh_alpha16_n4);
     s->wh_auto_refs = env_tunable("RT_WH_AUTO_REFS", s->wh_auto_refs);
     s->wg64_wide = env_tunable("RT_WG64_WIDE", s->wg64_wide);
+    s->wh_seg_min_ranks = env_tunable("RT_WH_SEG_MIN_RANKS", s->wh_seg_min_ranks);
+    s->wg64_o8 = env_tunable("RT_WG64_O8", s->wg64_o8);
+    s->wh_seg_alpha16 = env_tunable("RT_WH_SEG_ALPHA16", s->wh_seg_alpha16);
     s->hf_follow = env_tunable("RT_HF_FOLLOW", s->hf_follow);
     for (int a = 0; a < 3; a++)
     {
@@ -1085,6 +1090,8 @@ int rt_scene_destroy(rt_scene *s)
             (void)hipFree(h.ticket);
             (void)hipFree(h.wh_marks);
             (void)hipFree(h.wh_lists);
+            (void)hipFree(h.seg_col);
+            (void)hipFree(h.seg_px);
             if (h.wh_cnt) (void)hipHostFree(h.wh_cnt);
         }
         if (s->side) (void)hipStreamDestroy(s->side);
@@ -1659,6 +1666,25 @@ int rt_debug_wide_items(rt_scene *s, uint32_t *count)
         if (h.wh_cnt && (!c || h.used > c->used)) c = &h;
     if (c) RT_HIP(hipDeviceSynchronize());
     *count = c ? *(volatile uint32_t *)c->wh_cnt : 0u;
+    return RT_OK;
+}
+
+int rt_debug_wide_tiers(rt_scene *s, uint32_t *split, uint32_t *seg)
+{
+    if (!s || !split || !seg) return fail(RT_E_INVALID, "NULL argument");
+    std::lock_guard<std::mutex> lk(s->mtx);
+    int rc;
+    if ((rc = ensure_device(s))) return rc;
+    *split = *seg = 0u;
+    const HfCtx *c = nullptr;
+    for (const HfCtx& h : s->hf)
+        if (h.wh_cnt && (!c || h.used > c->used)) c = &h;
+    if (!c || !c->ver) return RT_OK;
+    RT_HIP(hipDeviceSynchronize());
+    HfPlan pl;
+    RT_HIP(hipMemcpy(&pl, c->plans + (c->ver & 1u), sizeof(pl), hipMemcpyDeviceToHost));
+    *split = std::min(pl.cnt_w, kWhMax);
+    *seg = std::min(pl.cnt_s, kWhMax);
     return RT_OK;
 }
 

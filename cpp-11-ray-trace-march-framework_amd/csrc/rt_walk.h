@@ -405,7 +405,8 @@ __device__ __forceinline__ float box_exit_bound(float x, float dtv, int f)
 // (cs): grid.cpp:274-277 exits after the same steps.  False when the ray misses the grid.
 __device__ __forceinline__ bool dda_setup(const KParams& P, float ox, float oy, float oz, float dx, float dy, float dz,
                                           float& nct0, float& nct1, float& nct2, float& dt0, float& dt1, float& dt2,
-                                          int& rem0, int& rem1, int& rem2, int& cs0, int& cs1, int& cs2, int& cell)
+                                          int& rem0, int& rem1, int& rem2, int& cs0, int& cs1, int& cs2, int& cell,
+                                          float *enter_out = nullptr)
 {
     float enter_t, leave_t, gx, gy, gz;
     if (rtd::point_in_aabb(ox, oy, oz, P.bmin, P.bmax))
@@ -453,6 +454,7 @@ __device__ __forceinline__ bool dda_setup(const KParams& P, float ox, float oy, 
     setup(dy, gy, pos1, 1, P.dxdz, nct1, dt1, rem1, cs1);
     setup(dz, gz, pos2, 2, P.dim[0], nct2, dt2, rem2, cs2);
     cell = pos0 + pos2 * P.dim[0] + pos1 * P.dxdz;
+    if (enter_out) *enter_out = enter_t;
     return true;
 }
 

@@ -319,9 +319,13 @@ int  rt_debug_wave_clocks(rt_scene *s, uint64_t *out, uint32_t max_items, uint32
    front section holds, *listed = blocks the last frame listed for the next one (heavy waves found),
    *epoch = frames rendered with this shape.  Synchronises the device. */
 int rt_debug_heavy_first(rt_scene *s, uint32_t *front, uint32_t *listed, uint32_t *epoch);
-/* RT_KERNEL_FLAG_WIDE_HEAVY: work items the newest plan of the most recent wide-section launch
-   shape lists for the wide section.  Synchronises the device. */
+/* RT_KERNEL_FLAG_WIDE_HEAVY: the wide section's waves for the items the newest plan of the most
+   recent wide-section launch shape lists (16 or 4 per item of the lane-split tier, 64 per item of the
+   segmented tier).  Synchronises the device. */
 int rt_debug_wide_items(rt_scene *s, uint32_t *count);
+/* The same plan's items per tier: *split = the lane-split tier's (16 or 4 lanes per sample), *seg =
+   the segmented tier's (4 t-segments x 16 lanes per sample, kVarWideSeg).  Synchronises the device. */
+int rt_debug_wide_tiers(rt_scene *s, uint32_t *split, uint32_t *seg);
 
 /* What rt_scene_create chose for a scene, and the scheduling tunables it read once from the
    environment (RT_HF_FLOOR, RT_HF_MIN_BLOCKS, RT_WH_FLOOR, RT_WH_ALPHA16, RT_WH_ALPHA16_N2,

@@ -22,6 +22,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REF = os.path.join(ROOT, "oracle", "_ref", "refdriver")
 REF_INSTR = os.path.join(ROOT, "oracle", "_ref", "refdriver_instr")   # grid.cpp + ref_instr.h
+REF_BARY = os.path.join(ROOT, "oracle", "_ref", "refdriver_bary")     # grid.cpp + ref_bary.h
 GOLD = os.path.join(ROOT, "tests", "golden")
 SCENES = os.path.join(ROOT, "data", "scenes")
 MESHES = "/root/reference/meshes"
@@ -130,6 +131,146 @@ def record_shas(tmp, sids=range(10)):
     return out
 
 
+def rec_shas(inst, cols=("hit_tri", "tuv", "voxel", "rgb", "steps", "tests")):
+    """SHA-256 of record columns (11-word refdriver_instr records, (y, x, sample) order): hit_tri =
+    the hit triangle or 0xFFFFFFFF per sample, tuv = (t, u, v), rgb = the shaded colour, voxel = the
+    accepted / last GridIdx, steps / tests = the walk's DDA iterations / ray-triangle tests."""
+    h = lambda a: hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()    # noqa: E731
+    sel = {"hit_tri": lambda: np.where(inst[:, 0] == 1, inst[:, 1], np.uint32(0xFFFFFFFF)).astype("<u4"),
+           "tuv": lambda: inst[:, 2:5], "voxel": lambda: inst[:, 8], "rgb": lambda: inst[:, 5:8],
+           "steps": lambda: inst[:, 9], "tests": lambda: inst[:, 10]}
+    return {f"{c}_sha256": h(sel[c]()) for c in cols}
+
+
+def instr_records(tmp, sid, W, H, spp, rect=None, view=None, exe=REF_INSTR, check_plain=True):
+    """refdriver_instr (or refdriver_bary) samples over rect (default: the whole frame), checked equal
+    in columns 0-7 to the plain refdriver's (the instrumentation only counts)."""
+    x0, y0, w, h = rect or (0, 0, W, H)
+    args = ["samples", os.path.join(SCENES, f"scene{sid}.rtscene"), str(W), str(H), str(spp), str(x0), str(y0),
+            str(w), str(h)]
+    ip = os.path.join(tmp, "instr.rec")
+    extra = ["--view", view] if view else []
+    run(args + [ip] + extra, exe=exe)
+    inst = np.fromfile(ip, "<u4").reshape(-1, 11)
+    os.remove(ip)
+    if check_plain:
+        pp = os.path.join(tmp, "plain.rec")
+        run(args + [pp] + extra)
+        plain = np.fromfile(pp, "<u4").reshape(-1, 8)
+        os.remove(pp)
+        assert np.array_equal(plain, inst[:, :8]), (sid, W, H, spp, rect)
+    return inst
+
+
+VIEW_SCENES = (1, 5, 8)
+VIEW_FRAME = (256, 144, 4)
+
+
+def view_cams(tmp, sid):
+    """The views of tests/test_gpu_parity.py::_custom_views, from the scene file's camera and the
+    reference grid's AABB (golden scenes[sid]): inside the grid looking down -z and down -x, the
+    scene's camera orbited 37 degrees about y, and a corner of the grid's box looking at its centre
+    through the reference's own BuildLookAtMatrix (refdriver look-at).  -> {name: (cam16 f32, fov)}"""
+    with open(os.path.join(SCENES, f"scene{sid}.rtscene"), "rb") as f:
+        raw = f.read(80)
+    fov = np.frombuffer(raw[12:16], "<f4")[0]
+    cam = np.frombuffer(raw[16:80], "<f4").copy()
+    with open(os.path.join(GOLD, "golden.json")) as f:
+        g = json.load(f)["scenes"][str(sid)]
+    lo = np.array([int(x, 16) for x in g["aabb_min_bits"]], np.uint32).view(np.float32)
+    hi = np.array([int(x, 16) for x in g["aabb_max_bits"]], np.uint32).view(np.float32)
+    ctr = (lo + hi) * np.float32(0.5)
+    down_z = np.eye(4, dtype=np.float32)
+    down_z[3, :3] = ctr + np.float32(0.1) * (hi - lo)
+    rot = np.array([[0, 0, 1, 0], [0, 1, 0, 0], [-1, 0, 0, 0], [0, 0, 0, 1]], np.float32)
+    down_x = rot.copy()
+    down_x[3, :3] = ctr - np.float32(0.2) * (hi - lo)
+    a = np.deg2rad(37.0)
+    ry = np.array([[np.cos(a), 0, -np.sin(a), 0], [0, 1, 0, 0], [np.sin(a), 0, np.cos(a), 0], [0, 0, 0, 1]])
+    orbit = (cam.astype(np.float64).reshape(4, 4) @ ry).astype(np.float32)
+    eye = lo - np.float32(0.3) * (hi - lo)
+    lp = os.path.join(tmp, "lookat.f32")
+    subprocess.run([REF, "look-at"] + [float(x).hex() for x in eye] + [float(x).hex() for x in ctr] + [lp], check=True)
+    corner = np.fromfile(lp, "<f4")
+    return {"inside_down_z": (down_z.reshape(16), fov), "inside_down_x": (down_x.reshape(16), fov),
+            "orbit37": (orbit.reshape(16), fov), "corner": (corner, fov)}
+
+
+def views(tmp):
+    """The reference from views its scenes' own cameras never take (the north_star's "same camera",
+    for any camera; GenerateRay camera.h:8-47 and Grid::Intersect from there): per scene 1, 5, 8 and
+    view (view_cams) at 256x144x4, the view (camera + fov bits), the frame and per-sample hit-ID
+    SHA-256 (refdriver render --view) and the record SHAs of every sample (refdriver_instr)."""
+    out = {}
+    W, H, spp = VIEW_FRAME
+    for sid in VIEW_SCENES:
+        for name, (cam, fov) in view_cams(tmp, sid).items():
+            vp = os.path.join(tmp, "v.view")
+            with open(vp, "wb") as f:
+                f.write(np.asarray(cam, "<f4").tobytes() + np.asarray([fov], "<f4").tobytes())
+            bp, hp = os.path.join(tmp, "v.bgra"), os.path.join(tmp, "v.hits")
+            run(["render", os.path.join(SCENES, f"scene{sid}.rtscene"), str(W), str(H), str(spp), "--out", bp,
+                 "--hits", hp, "--view", vp])
+            e = {"scene": sid, "view": name, "W": W, "H": H, "spp": spp,
+                 "cam_bits": [f"{x:08x}" for x in np.asarray(cam, "<f4").view("<u4")],
+                 "fov_bits": f"{int(np.asarray([fov], '<f4').view('<u4')[0]):08x}",
+                 "bgra_sha256": sha(bp), "hits_sha256": sha(hp)}
+            e.update(rec_shas(instr_records(tmp, sid, W, H, spp, view=vp)))
+            out[f"scene{sid}_{name}"] = e
+            print("view", sid, name, flush=True)
+    return out
+
+
+SPP_CROPS = [(1, 952, 532), (5, 952, 532), (8, 952, 532), (8, 640, 720)]
+
+
+def spp_crops(tmp):
+    """16x16-pixel crops of the 1920x1080 frames at spp 1, 16 and 64 (the bench is spp 4): record SHAs
+    of the reference's walk (refdriver_instr), all columns."""
+    out = []
+    for spp in (1, 16, 64):
+        for sid, x0, y0 in SPP_CROPS:
+            e = {"scene": sid, "W": 1920, "H": 1080, "spp": spp, "x0": x0, "y0": y0, "w": 16, "h": 16}
+            e.update(rec_shas(instr_records(tmp, sid, 1920, 1080, spp, rect=(x0, y0, 16, 16))))
+            out.append(e)
+        print("spp crops", spp, flush=True)
+    return out
+
+
+def head_records(tmp):
+    """Scene 4 (head) at 1024x1024x16 (SURVEY 8d's count frame for config 4): record SHAs of every
+    sample (16.7 M, hashed in a temporary directory)."""
+    e = {"scene": 4, "W": 1024, "H": 1024, "spp": 16}
+    e.update(rec_shas(instr_records(tmp, 4, 1024, 1024, 16), ("hit_tri", "tuv", "voxel", "rgb")))
+    print("head records", flush=True)
+    return e
+
+
+def bary(tmp):
+    """Grid::Intersect with the reference's second ray/triangle test, IntersectRayTriBarycentric
+    (triangle.h:210-226, with the face normal), through refdriver_bary (grid.cpp compiled with
+    ref_bary.h: the substitution grid.cpp:442-449 comments out): all 10 scenes at 1920x1080x4 (frame
+    and per-sample hit-ID SHA-256), each scene's (952, 532) crop's record SHAs (all columns), and
+    scenes 1 and 8's whole-frame record SHAs."""
+    frames, crops = {}, []
+    for sid in range(10):
+        bp, hp = os.path.join(tmp, "b.bgra"), os.path.join(tmp, "b.hits")
+        run(["render", os.path.join(SCENES, f"scene{sid}.rtscene"), "1920", "1080", "4", "--out", bp, "--hits", hp],
+            exe=REF_BARY)
+        frames[str(sid)] = {"W": 1920, "H": 1080, "spp": 4, "bgra_sha256": sha(bp), "hits_sha256": sha(hp)}
+        e = {"scene": sid, "W": 1920, "H": 1080, "spp": 4, "x0": 952, "y0": 532, "w": 16, "h": 16}
+        e.update(rec_shas(instr_records(tmp, sid, 1920, 1080, 4, rect=(952, 532, 16, 16), exe=REF_BARY,
+                                        check_plain=False)))
+        crops.append(e)
+        if sid in (1, 8):
+            frames[str(sid)].update(rec_shas(instr_records(tmp, sid, 1920, 1080, 4, exe=REF_BARY, check_plain=False),
+                                             ("hit_tri", "tuv", "voxel", "rgb")))
+        print("bary", sid, flush=True)
+    return {"frames_1080p4": frames, "crops": crops,
+            "generator": "oracle/_ref/refdriver_bary: the reference's grid.cpp with IntersectRayTriBarycentric "
+                         "(oracle/ref_bary.h), its own triangle.h"}
+
+
 def head_frame(tmp):
     """BASELINE config 4: head at 4096x4096x16spp, BGRA8 and per-sample hit-ID SHA-256 (the hit
     file is 1 GiB: hashed in a temporary directory, never committed)."""
@@ -145,7 +286,8 @@ def head_frame(tmp):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-head", action="store_true")
-    ap.add_argument("--only", choices=["crops", "bmp", "head", "records"],
+    ap.add_argument("--only", choices=["crops", "bmp", "head", "records", "views", "spp_crops", "head_records",
+                                       "bary"],
                     help="regenerate one section and merge it into the existing golden.json")
     a = ap.parse_args()
     if a.only:
@@ -160,6 +302,14 @@ def main():
         elif a.only == "records":
             for sid, d in record_shas(tmp).items():
                 meta["frames_1080p4"][sid].update(d)
+        elif a.only == "views":
+            meta["views"] = views(tmp)
+        elif a.only == "spp_crops":
+            meta["spp_crops"] = spp_crops(tmp)
+        elif a.only == "head_records":
+            meta["head_1024x1024x16_records"] = head_records(tmp)
+        elif a.only == "bary":
+            meta["bary"] = bary(tmp)
         else:
             meta["bmp"] = bmp_golden(tmp)
         meta["sample_record"] = SAMPLE_RECORD
@@ -239,6 +389,10 @@ def main():
         "scenes": scenes, "frames_1080p4": frames, "small_frames": small, "crops": crops,
         "sample_record": SAMPLE_RECORD, "bmp": bmp_golden(tmp),
     }
+    with open(os.path.join(GOLD, "golden.json"), "w") as f:     # view_cams reads the scenes' AABBs
+        json.dump(meta, f, indent=1, sort_keys=True)
+    meta.update({"views": views(tmp), "spp_crops": spp_crops(tmp),
+                 "head_1024x1024x16_records": head_records(tmp), "bary": bary(tmp)})
     with open(os.path.join(GOLD, "golden.json"), "w") as f:
         json.dump(meta, f, indent=1, sort_keys=True)
     print("wrote", os.path.join(GOLD, "golden.json"))

@@ -817,12 +817,22 @@ int main(int argc, char **argv)
         return 0;
     }
 
+    if (cmd == "look-at" && argc == 9)
+    {
+        // Matrix44f::BuildLookAtMatrix (lin_alg.h:431-467), the reference's own, with the default up
+        // vector: eye (3 floats) and target (3 floats) read as %a / decimal, 16 floats written raw
+        Matrix44f m;
+        m.BuildLookAtMatrix(Vec3f(std::strtof(argv[2], nullptr), std::strtof(argv[3], nullptr), std::strtof(argv[4], nullptr)),
+                            Vec3f(std::strtof(argv[5], nullptr), std::strtof(argv[6], nullptr), std::strtof(argv[7], nullptr)));
+        return WriteFile(argv[8], &m.m_mat[0][0], 16 * sizeof(float)) ? 0 : 1;
+    }
+
     if (cmd == "kat" && argc == 3)
         return CmdKat(argv[2]);
     if (cmd == "kat-dist" && argc == 3)
         return CmdKatDist(argv[2]);
 
-    if ((cmd == "grid" && argc == 4) || (cmd == "render" && argc >= 6) || (cmd == "samples" && argc == 11) ||
+    if ((cmd == "grid" && argc == 4) || (cmd == "render" && argc >= 6) || (cmd == "samples" && argc >= 11) ||
         (cmd == "alt-samples" && argc == 12))
     {
         SceneFile sf;
@@ -850,6 +860,16 @@ int main(int argc, char **argv)
         fr.width = uint(std::atoi(argv[3]));
         fr.height = uint(std::atoi(argv[4]));
         fr.spp = std::max(1u, uint(std::atoi(argv[5])));   // Renderer::SetSampleCount
+        // --view <file>: another camera (f32 Matrix44f m_mat[16] + f32 fov, raw) in place of the scene's
+        // (Scene::GetCameraParameters, scene.h:17-19): any view through the same GenerateRay and walk
+        for (int i = (cmd == "samples" ? 11 : 6); i + 1 < argc; i++)
+            if (std::string(argv[i]) == "--view")
+            {
+                std::FILE *vf = std::fopen(argv[i + 1], "rb");
+                const bool vok = vf && std::fread(&fr.cam.m_mat[0][0], 4, 16, vf) == 16 && std::fread(&fr.fov, 4, 1, vf) == 1;
+                if (vf) std::fclose(vf);
+                if (!vok) { std::fprintf(stderr, "bad view file\n"); return 1; }
+            }
 
         if (cmd == "samples")
         {

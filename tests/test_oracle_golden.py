@@ -150,3 +150,74 @@ def test_oracle_render_cam_with_own_camera_equals_render(oracle):
         got, ghid = oracle.render_cam(sid, 64, 36, 4, np.array(i.cam[:], np.float32), i.fov)
         np.testing.assert_array_equal(got, exp)
         np.testing.assert_array_equal(ghid, hid)
+
+
+def _rec_shas(rec, cols):
+    """SHA-256 of record columns of u32 [n, 12] rt_sample_rec rows (oracle/gen_golden.py rec_shas)."""
+    h = lambda a: hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()    # noqa: E731
+    sel = {"hit_tri": lambda: np.where(rec[:, 0] == 1, rec[:, 1], np.uint32(0xFFFFFFFF)).astype("<u4"),
+           "tuv": lambda: rec[:, 5:8], "voxel": lambda: rec[:, 2], "rgb": lambda: rec[:, 8:11],
+           "steps": lambda: rec[:, 3], "tests": lambda: rec[:, 4]}
+    return {f"{c}_sha256": h(sel[c]()) for c in cols}
+
+
+ALL_COLS = ("hit_tri", "tuv", "voxel", "rgb", "steps", "tests")
+
+
+def _view_cam(v):
+    cam = np.array([int(x, 16) for x in v["cam_bits"]], np.uint32).view(np.float32)
+    fov = float(np.array([int(v["fov_bits"], 16)], np.uint32).view(np.float32)[0])
+    return cam, fov
+
+
+def test_views_oracle_frames_match_reference(oracle, golden):
+    """The reference from views its scenes' own cameras never take (refdriver render --view, 12 views
+    of scenes 1, 5, 8 at 256x144x4): the restatement's frames and per-sample hit IDs from the same
+    views equal them -- the restatement the GPU custom-view tests used to be checked against alone."""
+    views = golden["views"]
+    assert len(views) == 12
+    for name, v in views.items():
+        cam, fov = _view_cam(v)
+        img, hid = oracle.render_cam(v["scene"], v["W"], v["H"], v["spp"], cam, fov)
+        assert hashlib.sha256(img.tobytes()).hexdigest() == v["bgra_sha256"], name
+        assert hashlib.sha256(hid.tobytes()).hexdigest() == v["hits_sha256"], name
+        assert v["hit_tri_sha256"] == v["hits_sha256"], name      # render and samples agree
+
+
+def test_look_at_restatement_matches_reference(golden, oracle, rtm):
+    """rth_look_at (the host's restatement of Matrix44f::BuildLookAtMatrix, lin_alg.h:431-467) gives the
+    corner views' cameras the reference's own BuildLookAtMatrix computed (refdriver look-at)."""
+    for sid in (1, 5, 8):
+        v = golden["views"][f"scene{sid}_corner"]
+        i = oracle.info(sid)
+        lo, hi = np.array(i.aabb_min[:], np.float32), np.array(i.aabb_max[:], np.float32)
+        ctr = (lo + hi) * np.float32(0.5)
+        got = rtm.look_at(lo - np.float32(0.3) * (hi - lo), ctr)
+        assert [f"{x:08x}" for x in got.view(np.uint32)] == v["cam_bits"], sid
+
+
+def test_spp_crops_oracle_matches_reference(oracle, golden):
+    """16x16 crops at spp 1, 16 and 64: the restatement's records (hit, t/u/v, voxel, colour, DDA steps,
+    tests) hash to the reference walk's."""
+    for c in golden["spp_crops"]:
+        rec = oracle.records(c["scene"], c["W"], c["H"], c["spp"], c["x0"], c["y0"], c["w"], c["h"])
+        got = _rec_shas(rec.view(np.uint32).reshape(-1, 12), ALL_COLS)
+        assert all(got[k] == c[k] for k in got), (c["scene"], c["spp"], c["x0"])
+
+
+def test_bary_crops_oracle_matches_reference(oracle, golden):
+    """Grid::Intersect with IntersectRayTriBarycentric (refdriver_bary: the reference's own grid.cpp and
+    triangle.h, oracle/ref_bary.h): the restatement's barycentric records on every scene's crop hash to it."""
+    for c in golden["bary"]["crops"]:
+        rec = oracle.records(c["scene"], c["W"], c["H"], c["spp"], c["x0"], c["y0"], c["w"], c["h"], tri_test=1)
+        got = _rec_shas(rec.view(np.uint32).reshape(-1, 12), ALL_COLS)
+        assert all(got[k] == c[k] for k in got), c["scene"]
+
+
+@pytest.mark.parametrize("sid", [1, 5, 8])
+def test_bary_frames_oracle_matches_reference(oracle, golden, sid):
+    """The barycentric walk's 1920x1080x4 frame and per-sample hit IDs (the restatement vs refdriver_bary)."""
+    b = golden["bary"]["frames_1080p4"][str(sid)]
+    img, hid, _ = oracle.render(sid, 1920, 1080, 4, tri_test=1, hits=True)
+    assert hashlib.sha256(img.tobytes()).hexdigest() == b["bgra_sha256"]
+    assert hashlib.sha256(hid.tobytes()).hexdigest() == b["hits_sha256"]

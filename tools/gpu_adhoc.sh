@@ -2,11 +2,14 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"; mkdir -p gpurun_out; export TMPDIR=/tmp
 T=${1:-adhoc}
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread -k "cull or crop or full_frame_1080p4 or small_frames or head or auto_equals" > gpurun_out/${T}_pytest.log 2>&1
-rc=$?; tail -3 gpurun_out/${T}_pytest.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python3 -u tools/ab_libs.py --arm cull=librt_tracer.so:0 --arm nocull=librt_tracer.so:512 --arm c24=librt_tracer_c24.so:0 --arm c64=librt_tracer_c64.so:0 --arm base=librt_tracer_nocull.so:0 --scenes 1 8 5 4 --rounds 6 > gpurun_out/${T}_ab.json 2> gpurun_out/${T}_ab.err
-rc=$?; cat gpurun_out/${T}_ab.json; [ $rc -eq 0 ] || exit $rc
-RT_TRACER_LIB=librt_tracer_c24.so timeout -k 10 200 python3 tools/tail_probe.py 0 > gpurun_out/${T}_tp.log 2>&1
-rc=$?; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python3 -u tools/shard_scaling.py 0 > gpurun_out/${T}_shard.log 2>&1
-rc=$?; tail -n1 gpurun_out/${T}_shard.log; exit $rc
+run() {
+    local name=$1 secs=$2; shift 2
+    timeout -k 10 "$secs" "$@" > gpurun_out/${T}_${name}.log 2>&1
+    local rc=$?
+    echo "$name rc=$rc"
+    [ $rc -eq 0 ] || { tail -5 gpurun_out/${T}_${name}.log; exit $rc; }
+}
+run w8_o8 120 python3 -u tools/batch_waves.py --rank 0 --nranks 8 --out ${T}_w8_o8
+run ab_o8 600 python -u tools/tunable_sweep.py --env RT_WG64_O8 --values 0 1 --ns 2 4 8 --rounds 3 --out ${T}_ab_o8
+run ab_wide_policy 600 python -u tools/tunable_sweep.py --env RT_WG64_WIDE --values 10 14 --ns 4 --rounds 3 --out ${T}_ab_wide_policy
+run ab_alpha 600 python -u tools/tunable_sweep.py --env RT_WH_ALPHA16 --values 32 28 24 20 --ns 8 --rounds 2 --out ${T}_ab_alpha
