@@ -190,6 +190,41 @@ __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks)
 
 knfn_t hf_plan_kernel() { return k_hf_plan; }
 
+// k_hf_plan after a measured frame.  A plan lists a block only against the PREVIOUS measurement (its
+// maximum and span decide the thresholds), so the first measured frame of a launch shape listed
+// nothing and its second frame ran in the natural order too (killeroo 1080p x 4: 0.62 ms against 0.36
+// in steady state, BENCH_r04 first_frame_ms).  After that frame a second pass ranks the same wave
+// costs against the first pass's maximum and span: the second frame already runs heavy-first.  The
+// passes alternate the plan / list / mark buffers by version parity, as consecutive frames do
+// (hf_prepare bumps the version by 2).
+int launch_plans(const KParams& P, uint64_t blocks, hipStream_t st)
+{
+    const dim3 grid(uint32_t((blocks + kWG * kHfPlanPer - 1) / (kWG * kHfPlanPer))), wg(kWG);
+    hipLaunchKernelGGL(k_hf_plan, grid, wg, 0, st, P, uint32_t(blocks));
+    if (P.hf_ver == 0u)
+    {
+        KParams Q = P;
+        Q.hf_ver = 1u;
+        Q.hf_plan_in = P.hf_plan_out;
+        Q.hf_plan_out = const_cast<HfPlan *>(P.hf_plan_in);
+        Q.hf_list_in = P.hf_list_out;
+        Q.hf_list_out = const_cast<uint32_t *>(P.hf_list_in);
+        Q.hf_mark_in = P.hf_mark_out;
+        Q.hf_mark_out = const_cast<uint32_t *>(P.hf_mark_in);
+        if (P.wh_on)
+        {
+            Q.wh_list_in = P.wh_list_out;
+            Q.wh_list_out = const_cast<uint32_t *>(P.wh_list_in);
+            Q.wh_mark_in = P.wh_mark_out;
+            Q.wh_mark_out = const_cast<uint32_t *>(P.wh_mark_in);
+        }
+        RT_HIP(hipMemsetAsync(Q.hf_plan_out, 0, sizeof(HfPlan), st));
+        hipLaunchKernelGGL(k_hf_plan, grid, wg, 0, st, Q, uint32_t(blocks));
+    }
+    RT_HIP(hipGetLastError());
+    return RT_OK;
+}
+
 constexpr uint32_t kWhRefresh = 128;        // frames between refresh frames (a multiple of kHfPeriod)
 
 
@@ -327,7 +362,8 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
         RT_HIP(hipHostGetDevicePointer(&dev, c->wh_cnt, 0));
         P.wh_host_cnt = static_cast<uint32_t *>(dev);
     }
-    if (P.hf_measure) c->ver = v + 1u;                  // the plan launched after this frame
+    // the plan launched after this frame (two passes after the shape's first frame: launch_plans)
+    if (P.hf_measure) c->ver = v + (v == 0u ? 2u : 1u);
     return RT_OK;
 }
 

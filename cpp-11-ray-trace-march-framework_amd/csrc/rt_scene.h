@@ -158,6 +158,9 @@ namespace rtk {
 // batch: 0 for a single-frame launch, else an identity of the batch (its scenes and frame count)
 int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hipStream_t st, uint64_t batch = 0,
                uint64_t cam_sig = 0);
+// The plan kernel(s) after a measured frame on its stream (k_hf_plan; two passes after a shape's first
+// measured frame, see launch_plans)
+int launch_plans(const KParams& P, uint64_t blocks, hipStream_t st);
 // The camera of a frame as one 64-bit signature (FNV-1a over the rotation, origin and fov bits)
 uint64_t cam_signature(const KParams& P, uint64_t h = 0xcbf29ce484222325ull);
 

@@ -486,10 +486,7 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
         }
         RT_HIP(mark(kt1));
         if ((P.hf_front || P.wh_on) && P.hf_measure)
-        {
-            hipLaunchKernelGGL(hf_plan_kernel(), dim3(uint32_t((blocks + kWG * kHfPlanPer - 1) / (kWG * kHfPlanPer))), wg, 0, st, P,
-                               uint32_t(blocks));
-        }
+            if (int rc = launch_plans(P, blocks, st)) return rc;
     }
     else
     {
@@ -637,12 +634,10 @@ int launch_batch(rt_scene *const *S, const rt_frame *F, uint32_t n, KParams *P, 
         RT_HIP(hipEventCreate(&s0->kt1[kslot]));
     }
     if (timed) RT_HIP(hipEventRecord(s0->kt0[kslot], st));
-    const dim3 wg(kWG);
     hipLaunchKernelGGL(fn, dim3(grid), dim3(bwg), 0, st, KB);
     if (timed) RT_HIP(hipEventRecord(s0->kt1[kslot], st));
     if ((P[0].hf_front || P[0].wh_on) && P[0].hf_measure)
-        hipLaunchKernelGGL(hf_plan_kernel(), dim3(uint32_t((blocks + kWG * kHfPlanPer - 1) / (kWG * kHfPlanPer))), wg, 0, st,
-                           KB.p[0], uint32_t(blocks));
+        if (int rc = launch_plans(KB.p[0], blocks, st)) return rc;
     RT_HIP(hipGetLastError());
     for (uint32_t i = 0; i < n; i++)
     {

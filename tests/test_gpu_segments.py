@@ -4,7 +4,7 @@ A listed heavy work item is traced one wave per sample: the sample's walk is spl
 t-segments (each starts from S(T_j), "every axis crossing below T_j taken", a state of the
 reference's DDA) of 16 list lanes each, the first segment with a hit wins, and the pixel's samples
 (traced by different waves) are summed in sample order by the wave whose arrival completes the pixel.
-The bench step takes the tier at a rank of >= 4 (RT_WH_SEG_MIN_RANKS); these tests force it wider --
+The tier is an A/B arm, off by default (RT_WH_SEG_MIN_RANKS=0); these tests force it on and wide --
 lower wide thresholds, more ranks, ragged frames, spp 1 / 2 / 4 -- and compare frames, per-sample hit
 IDs and the per-sample records (t, u, v, voxel, colour) with the reference's fixtures and the oracle.
 """
