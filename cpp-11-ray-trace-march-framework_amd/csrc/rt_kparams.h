@@ -105,7 +105,7 @@ struct KParams
     uint32_t hf_front;          // front section size (blocks, a multiple of 8)
     uint32_t hf_ver;            // version of the plan this frame uses (0: none yet)
     uint32_t hf_measure;        // 1: this frame records wave costs for the next plan
-    uint32_t hf_floor;          // a block is heavy above max(hf_floor, last max >> kHfShift) cycles
+    uint32_t hf_floor;          // a block is heavy above max(hf_floor, last max >> hf_shift (RT_HF_SHIFT)) cycles
     const uint32_t *hf_mark_in; // per block: == hf_ver when the current plan lists it
     uint32_t *hf_mark_out;      // per block: hf_ver + 1 when the next plan lists it
     const uint32_t *hf_list_in; // the current plan's front: [0, cnt_hi) and [front - cnt_lo, front)
@@ -187,9 +187,8 @@ constexpr uint32_t kXcds = 8;
 // Heavy-first order (AUTO): front-section capacity and the shape of the heavy threshold.  The
 // floor and the smallest launch it is used for are per-scene tunables (rt_scene, read once at
 // creation).
-constexpr uint32_t kHfFrontMax = 1024;      // blocks (4 waves each): half the chip's wave slots
+constexpr uint32_t kHfFrontMax = 4096;      // blocks (4 waves each): the front list's capacity (hf_front_max)
 constexpr uint32_t kWhMax = 4096;           // kVarWideHeavy: work items the wide section can list
-constexpr uint32_t kHfShift = 2;            // heavy: cost > last max >> kHfShift; very heavy: >> 1
 constexpr uint32_t kHfPeriod = 16;          // a plan from every kHfPeriod-th frame of a launch shape
 // A plan lists blocks only when the slowest block is a real tail: its cost (one wave's
 // duration) above kHfTail / 16 of the estimated frame span, sum of wave costs / resident waves
@@ -237,7 +236,6 @@ kcfn_t compact_kernel(int tri, int var);       // k_render_compact<tri, var>(P, 
 kbfn_t batch_kernel(int var, bool w64, bool o8 = false);   // k_render_batch / _w64 / _w64_o8<MT, var>
 knfn_t trace_records_kernel();                 // k_trace_records(P, n)
 knfn_t record_fixup_kernel();                  // k_record_fixup(P, n)
-knfn_t hf_plan_kernel();                       // k_hf_plan(P, nblocks) (rt_plan.hip)
 using origin_pre_fn = void (*)(const float4 *, float4 *, uint32_t, float, float, float);
 using unshard_fn = void (*)(const uint32_t *, uint32_t *, uint32_t, uint32_t, uint32_t, uint32_t, uint64_t);
 using check_fn = void (*)(unsigned long long *);

@@ -12,7 +12,7 @@ namespace rtk {
 namespace {
 
 // Heavy-first planning, after a measured frame's render kernel on its stream: per block the cost
-// of its slowest wave; blocks above max(hf_floor, last max >> kHfShift) are listed for the next
+// of its slowest wave; blocks above max(hf_floor, last max >> hf_shift (RT_HF_SHIFT)) are listed for the next
 // frames -- above last max >> 1 at the front of the front section, the rest from its back -- and
 // marked so the natural order skips them.  Nothing is listed when the last measurement showed no
 // tail (its slowest block well under the frame's estimated span).  Each thread takes kHfPlanPer
@@ -21,7 +21,7 @@ namespace {
 // atomics: thousands of same-address atomics from waves cost milliseconds, measured).  The plan's
 // time is those same-address atomics: one block per thread (1,013 workgroups for the batched
 // bench pair) took 26.6 us per plan, which a moving camera pays every frame.
-__global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks)
+__global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks, uint32_t shift)
 {
     __shared__ uint32_t s_max, s_hi, s_lo, s_w, s_s, s_bhi, s_blo, s_bw, s_bs, s_last;
     __shared__ unsigned long long s_sum;
@@ -33,7 +33,7 @@ __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks)
     __syncthreads();
     const HfPlan last = *P.hf_plan_in;
     const bool tail = uint64_t(last.maxc) * kHfSlots * 16u > uint64_t(kHfTail) * (last.sum << 4);
-    const uint32_t thr = max(P.hf_floor, last.maxc >> kHfShift);
+    const uint32_t thr = max(P.hf_floor, last.maxc >> shift);
     const uint32_t b0 = blockIdx.x * (kWG * kHfPlanPer) + threadIdx.x;
     uint32_t tmax = 0u, wmasks = 0u, smasks = 0u, heavy = 0u, hi = 0u;
     unsigned long long tsum = 0ull;
@@ -188,7 +188,6 @@ __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks)
 
 } // namespace
 
-knfn_t hf_plan_kernel() { return k_hf_plan; }
 
 // k_hf_plan after a measured frame.  A plan lists a block only against the PREVIOUS measurement (its
 // maximum and span decide the thresholds), so the first measured frame of a launch shape listed
@@ -197,10 +196,10 @@ knfn_t hf_plan_kernel() { return k_hf_plan; }
 // costs against the first pass's maximum and span: the second frame already runs heavy-first.  The
 // passes alternate the plan / list / mark buffers by version parity, as consecutive frames do
 // (hf_prepare bumps the version by 2).
-int launch_plans(const KParams& P, uint64_t blocks, hipStream_t st)
+int launch_plans(const rt_scene *s, const KParams& P, uint64_t blocks, hipStream_t st)
 {
     const dim3 grid(uint32_t((blocks + kWG * kHfPlanPer - 1) / (kWG * kHfPlanPer))), wg(kWG);
-    hipLaunchKernelGGL(k_hf_plan, grid, wg, 0, st, P, uint32_t(blocks));
+    hipLaunchKernelGGL(k_hf_plan, grid, wg, 0, st, P, uint32_t(blocks), s->hf_shift);
     if (P.hf_ver == 0u)
     {
         KParams Q = P;
@@ -219,7 +218,7 @@ int launch_plans(const KParams& P, uint64_t blocks, hipStream_t st)
             Q.wh_mark_out = const_cast<uint32_t *>(P.wh_mark_in);
         }
         RT_HIP(hipMemsetAsync(Q.hf_plan_out, 0, sizeof(HfPlan), st));
-        hipLaunchKernelGGL(k_hf_plan, grid, wg, 0, st, Q, uint32_t(blocks));
+        hipLaunchKernelGGL(k_hf_plan, grid, wg, 0, st, Q, uint32_t(blocks), s->hf_shift);
     }
     RT_HIP(hipGetLastError());
     return RT_OK;
@@ -292,9 +291,11 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
         RT_HIP(hipMemsetAsync(c->ticket, 0, sizeof(uint32_t), st));
         *(volatile uint32_t *)c->wh_cnt = 0u;
         c->nblocks = uint32_t(blocks);
-        // front: an eighth of the blocks, capped, a multiple of the XCD count so the natural
-        // section keeps its block -> XCD assignment
-        c->front = front ? std::min<uint32_t>(kHfFrontMax, uint32_t(blocks / 8u) & ~(kXcds - 1u)) : 0u;
+        // front: 1 / hf_front_div of the blocks (an eighth), capped at hf_front_max (1024), a multiple
+        // of the XCD count so the natural section keeps its block -> XCD assignment
+        c->front = front ? std::min<uint32_t>(std::min(s->hf_front_max, kHfFrontMax),
+                                              uint32_t(blocks / std::max(s->hf_front_div, 1u)) & ~(kXcds - 1u))
+                         : 0u;
         std::memcpy(c->key, key, sizeof(key));          // valid only now
     }
     c->used = ++s->hf_clock;

@@ -85,6 +85,9 @@ struct rt_scene
     // launch path never calls getenv
     uint32_t hf_floor = 100000;     // RT_HF_FLOOR: heavy-first threshold floor, shader cycles
     uint32_t hf_min_blocks = 4096;  // RT_HF_MIN_BLOCKS: smallest whole launch taking the heavy-first order
+    uint32_t hf_front_div = 8;      // RT_HF_FRONT_DIV: the front section holds 1 / this of a launch's blocks ...
+    uint32_t hf_front_max = 1024;   // RT_HF_FRONT_MAX: ... at most this many (<= kHfFrontMax)
+    uint32_t hf_shift = 2;          // RT_HF_SHIFT: heavy = cost > last max >> hf_shift (very heavy: >> 1)
     uint32_t wh_floor = 100000;     // RT_WH_FLOOR: wide-section threshold floor, shader cycles
     uint32_t wh_alpha16 = 32;       // RT_WH_ALPHA16: wide threshold, sixteenths of the estimated span
     uint32_t wh_alpha16_n2 = 16;    // RT_WH_ALPHA16_N2: the same for a rank of 2 of a batched step
@@ -98,7 +101,8 @@ struct rt_scene
     uint32_t wh_seg_min_ranks = 0;  // RT_WH_SEG_MIN_RANKS: a batch of >= this many ranks (spp <= 4) traces its
                                     // heaviest wide items in the segmented tier (kVarWideSeg; 0: never, the
                                     // default: measured slower)
-    uint32_t wg64_o8 = 1;           // RT_WG64_O8: the fused one-wave batch kernels held to 8 waves / SIMD
+    uint32_t wg64_o8 = 0x2;         // RT_WG64_O8: bit log2(N) (3: N >= 8): a rank of N's fused one-wave
+                                    // batch kernel held to 8 waves / SIMD
     uint32_t wg64_wide = 0xA;       // RT_WG64_WIDE: bit log2(N) (3: N >= 8): one-wave workgroups also
                                     // for a rank of N's batch with a wide section
     uint32_t hf_follow = 1;         // RT_HF_FOLLOW: re-plan the heavy-first order on every frame whose
@@ -160,7 +164,7 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
                uint64_t cam_sig = 0);
 // The plan kernel(s) after a measured frame on its stream (k_hf_plan; two passes after a shape's first
 // measured frame, see launch_plans)
-int launch_plans(const KParams& P, uint64_t blocks, hipStream_t st);
+int launch_plans(const rt_scene *s, const KParams& P, uint64_t blocks, hipStream_t st);
 // The camera of a frame as one 64-bit signature (FNV-1a over the rotation, origin and fov bits)
 uint64_t cam_signature(const KParams& P, uint64_t h = 0xcbf29ce484222325ull);
 

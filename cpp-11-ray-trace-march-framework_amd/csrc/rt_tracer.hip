@@ -486,7 +486,7 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
         }
         RT_HIP(mark(kt1));
         if ((P.hf_front || P.wh_on) && P.hf_measure)
-            if (int rc = launch_plans(P, blocks, st)) return rc;
+            if (int rc = launch_plans(s, P, blocks, st)) return rc;
     }
     else
     {
@@ -605,7 +605,11 @@ int launch_batch(rt_scene *const *S, const rt_frame *F, uint32_t n, KParams *P, 
         grid = kWavesPerWG * ((fused ? P[0].wh_wgs : 0u) + (P[0].vblocks + kXcds - 1u) / kXcds * kXcds);
         bwg = 64u;
     }
-    const kbfn_t fn = batch_kernel(kvar, w64, s0->wg64_o8 != 0u && (kvar & kVarWideFused) != 0);
+    // the fused one-wave kernel held to 8 waves / SIMD (76 SGPRs; the plain build's 83 admit 7), per
+    // rank count (wg64_o8, bit log2 N): a rank of 2 0.2925 vs 0.3025 ms, of 8 0.1171-0.1182 vs
+    // 0.1139-0.1151 (profiles/r05f_ab_o8.json), so 2 only
+    const bool o8 = ((s0->wg64_o8 >> lg_ranks) & 1u) != 0u && (kvar & kVarWideFused) != 0;
+    const kbfn_t fn = batch_kernel(kvar, w64, o8);
     if (clk)
     {
         // one record per lane item and per (listed item, wave) of the wide section
@@ -637,7 +641,7 @@ int launch_batch(rt_scene *const *S, const rt_frame *F, uint32_t n, KParams *P, 
     hipLaunchKernelGGL(fn, dim3(grid), dim3(bwg), 0, st, KB);
     if (timed) RT_HIP(hipEventRecord(s0->kt1[kslot], st));
     if ((P[0].hf_front || P[0].wh_on) && P[0].hf_measure)
-        if (int rc = launch_plans(KB.p[0], blocks, st)) return rc;
+        if (int rc = launch_plans(s0, KB.p[0], blocks, st)) return rc;
     RT_HIP(hipGetLastError());
     for (uint32_t i = 0; i < n; i++)
     {
@@ -797,6 +801,9 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
     // scheduling tunables: read once here, never per launch (A/B sweeps set them per scene)
     s->hf_floor = env_tunable("RT_HF_FLOOR", s->hf_floor);
     s->hf_min_blocks = env_tunable("RT_HF_MIN_BLOCKS", s->hf_min_blocks);
+    s->hf_front_div = env_tunable("RT_HF_FRONT_DIV", s->hf_front_div);
+    s->hf_front_max = env_tunable("RT_HF_FRONT_MAX", s->hf_front_max);
+    s->hf_shift = std::min(env_tunable("RT_HF_SHIFT", s->hf_shift), 8u);
     s->wg64 = env_tunable("RT_WG64", s->wg64);
     s->wg64_min_blocks = env_tunable("RT_WG64_MIN_BLOCKS", s->wg64_min_blocks);
     s->wg64_batch_min_blocks = env_tunable("RT_WG64_BATCH_MIN_BLOCKS", s->wg64_batch_min_blocks);
