@@ -196,10 +196,37 @@ __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks, ui
 // costs against the first pass's maximum and span: the second frame already runs heavy-first.  The
 // passes alternate the plan / list / mark buffers by version parity, as consecutive frames do
 // (hf_prepare bumps the version by 2).
-int launch_plans(const rt_scene *s, const KParams& P, uint64_t blocks, hipStream_t st)
+// Later plans (a current version exists) run on the scene's plan stream, forked after the measured
+// frame: the next frame keeps the current plan and does not wait for this one (on the launch stream
+// the plan took ~20 us per scene after every 16th frame: the 16-step spikes of a frame series,
+// profiles/r05k_frame_series*.json).  hf_prepare adopts it (a stream wait on its event) at the second
+// frame after, or at the next measured frame (which reuses the plan's buffers).  Inside a stream
+// capture every plan stays on the launch stream.
+int launch_plans(rt_scene *s, const KParams& P, uint64_t blocks, hipStream_t st)
 {
     const dim3 grid(uint32_t((blocks + kWG * kHfPlanPer - 1) / (kWG * kHfPlanPer))), wg(kWG);
+    HfCtx *c = s->hf_last;
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    RT_HIP(hipStreamIsCapturing(st, &cap));
+    if (P.hf_ver != 0u && c && cap == hipStreamCaptureStatusNone)
+    {
+        if (!s->plan_st)
+        {
+            RT_HIP(hipStreamCreateWithFlags(&s->plan_st, hipStreamNonBlocking));
+            RT_HIP(hipEventCreateWithFlags(&s->ev_plan_fork, s->ev_order_flags));
+        }
+        if (!c->pend_ev) RT_HIP(hipEventCreateWithFlags(&c->pend_ev, s->ev_order_flags));
+        RT_HIP(hipEventRecord(s->ev_plan_fork, st));
+        RT_HIP(hipStreamWaitEvent(s->plan_st, s->ev_plan_fork, 0));
+        hipLaunchKernelGGL(k_hf_plan, grid, wg, 0, s->plan_st, P, uint32_t(blocks), s->hf_shift);
+        RT_HIP(hipEventRecord(c->pend_ev, s->plan_st));
+        c->pend = P.hf_ver + 1u;
+        c->pend_age = 0;
+        RT_HIP(hipGetLastError());
+        return RT_OK;
+    }
     hipLaunchKernelGGL(k_hf_plan, grid, wg, 0, st, P, uint32_t(blocks), s->hf_shift);
+    if (c) c->ver = P.hf_ver + (P.hf_ver == 0u ? 2u : 1u);
     if (P.hf_ver == 0u)
     {
         KParams Q = P;
@@ -260,6 +287,11 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
         for (HfCtx& h : s->hf)
             if (h.used < c->used) c = &h;
         if (c->used) s->hf_evictions++;
+        if (c->pend)
+        {
+            RT_HIP(hipEventSynchronize(c->pend_ev));      // its plan still writes these buffers
+            c->pend = 0u;
+        }
         // invalidated first: if an allocation below fails, no later launch may match the old
         // shape and read freed (null) state arrays
         std::memset(c->key, 0, sizeof(c->key));
@@ -299,15 +331,34 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
         std::memcpy(c->key, key, sizeof(key));          // valid only now
     }
     c->used = ++s->hf_clock;
-    const uint32_t v = c->ver;
-    P.hf_front = c->front;
-    P.hf_ver = v;
+    s->hf_last = c;
     // measured: the first two frames (the first plan has no earlier maximum to test a tail
     // against, so it lists nothing) and then every kHfPeriod-th
     // ... and every frame whose camera differs from the previous frame's: a moving camera's heavy
     // blocks move with the view, so the plan comes from the newest view (one frame old) instead of
     // one up to kHfPeriod frames old
     P.hf_measure = c->frames < 2u || c->frames % kHfPeriod == 0u || (s->hf_follow && cam_sig != c->cam);
+    if (c->pend)
+    {
+        // a plan on the plan stream (launch_plans): adopted by the second frame after it and by a
+        // measured frame; inside a stream capture (no wait on an outside event) the current plan
+        // stays and nothing is measured
+        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+        RT_HIP(hipStreamIsCapturing(st, &cap));
+        if (cap != hipStreamCaptureStatusNone)
+            P.hf_measure = 0u;
+        else if (P.hf_measure || c->pend_age >= 1u)
+        {
+            RT_HIP(hipStreamWaitEvent(st, c->pend_ev, 0));
+            c->ver = c->pend;
+            c->pend = 0u;
+        }
+        else
+            c->pend_age++;
+    }
+    const uint32_t v = c->ver;
+    P.hf_front = c->front;
+    P.hf_ver = v;
     c->cam = cam_sig;
     c->frames++;
     P.hf_floor = s->hf_floor;
@@ -363,8 +414,6 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
         RT_HIP(hipHostGetDevicePointer(&dev, c->wh_cnt, 0));
         P.wh_host_cnt = static_cast<uint32_t *>(dev);
     }
-    // the plan launched after this frame (two passes after the shape's first frame: launch_plans)
-    if (P.hf_measure) c->ver = v + (v == 0u ? 2u : 1u);
     return RT_OK;
 }
 

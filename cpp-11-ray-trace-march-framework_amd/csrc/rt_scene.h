@@ -39,7 +39,12 @@ struct HfCtx
     float4 *seg_col = nullptr;          // kVarWideSeg scratch: [kWhMax][64] sample colours
     uint32_t *seg_px = nullptr;         // kVarWideSeg scratch: [kWhMax][64] arrivals per pixel
     uint32_t frames = 0;                // frames rendered with this shape
-    uint32_t ver = 0;                   // version of the newest plan launched
+    uint32_t ver = 0;                   // version of the plan the frames use
+    // a plan launched on the scene's plan stream after a measured frame (launch_plans): version pend
+    // (0: none), adopted -- the launch stream waits for pend_ev -- by the second frame after it, or
+    // by the next frame that measures
+    uint32_t pend = 0, pend_age = 0;
+    hipEvent_t pend_ev = nullptr;
     uint64_t used = 0;                  // LRU stamp
     uint64_t cam = 0;                   // camera signature of the last frame (cam_signature)
 };
@@ -130,7 +135,12 @@ struct rt_scene
     bool ev_recorded = false;
     // render-kernel-only timing: event pair around the render kernel(s) of each launch (not the
     // heavy-first planning kernels), a ring of the last kTimeRing launches (rt_kernel_times)
+    rtk::HfCtx *hf_last = nullptr;       // the context of the last hf_prepare (launch_plans)
+    hipStream_t plan_st = nullptr;       // k_hf_plan after a measured frame, beside the next frame
+    hipEvent_t ev_plan_fork = nullptr;
     hipEvent_t kt0[kTimeRing] = {}, kt1[kTimeRing] = {};
+    unsigned ev_time_flags = hipEventDefault;            // kt0 / kt1 (RT_EVENT_SYSFENCE, rt_scene_create)
+    unsigned ev_order_flags = hipEventDisableTiming;     // ev1, ev_fork, ev_join
     uint32_t kt_next = 0, kt_count = 0;
     uint32_t kt_last = kTimeRing;   // ring slot of the last timed launch (kTimeRing: none)
     uint32_t time_every = kTimeEvery; // rt_scene_set_timing: time every n-th launch (0: none)
@@ -164,7 +174,7 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
                uint64_t cam_sig = 0);
 // The plan kernel(s) after a measured frame on its stream (k_hf_plan; two passes after a shape's first
 // measured frame, see launch_plans)
-int launch_plans(const rt_scene *s, const KParams& P, uint64_t blocks, hipStream_t st);
+int launch_plans(rt_scene *s, const KParams& P, uint64_t blocks, hipStream_t st);
 // The camera of a frame as one 64-bit signature (FNV-1a over the rotation, origin and fov bits)
 uint64_t cam_signature(const KParams& P, uint64_t h = 0xcbf29ce484222325ull);
 

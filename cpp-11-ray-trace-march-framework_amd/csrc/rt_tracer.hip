@@ -18,6 +18,7 @@
 //   face_n    float4[T]           face normal (IntersectRayTriBarycentric only)
 
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <cmath>
@@ -386,8 +387,8 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
     hipEvent_t kt0 = nullptr, kt1 = nullptr;        // null stand for "not timed"
     if (timed && !s->kt0[kslot])
     {
-        RT_HIP(hipEventCreate(&s->kt0[kslot]));
-        RT_HIP(hipEventCreate(&s->kt1[kslot]));
+        RT_HIP(hipEventCreateWithFlags(&s->kt0[kslot], s->ev_time_flags));
+        RT_HIP(hipEventCreateWithFlags(&s->kt1[kslot], s->ev_time_flags));
     }
     if (timed)
     {
@@ -462,29 +463,31 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
             lgrid = kWavesPerWG * ((grid + kXcds - 1u) / kXcds * kXcds);
             lwg = 64u;
         }
-        RT_HIP(mark(kt0));
         if (P.wh_wgs)
         {
+            RT_HIP(mark(kt0));
             // the wide section runs on the side stream beside the lane kernel (fork / join by
             // events, so the pair also captures into a hipGraph); submitted first so its waves
             // -- the frame's longest -- start first
             if (!s->side)
             {
                 RT_HIP(hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking));
-                RT_HIP(hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming));
-                RT_HIP(hipEventCreateWithFlags(&s->ev_join, hipEventDisableTiming));
+                RT_HIP(hipEventCreateWithFlags(&s->ev_fork, s->ev_order_flags));
+                RT_HIP(hipEventCreateWithFlags(&s->ev_join, s->ev_order_flags));
             }
             RT_HIP(hipEventRecord(s->ev_fork, st));
             RT_HIP(hipStreamWaitEvent(s->side, s->ev_fork, 0));
             hipLaunchKernelGGL(wide_kernel(P.wh_g), dim3(P.wh_wgs), wg, 0, s->side, P);
         }
-        hipLaunchKernelGGL(lfn, dim3(lgrid), dim3(lwg), 0, st, P);
         if (P.wh_wgs)
         {
+            hipLaunchKernelGGL(lfn, dim3(lgrid), dim3(lwg), 0, st, P);
             RT_HIP(hipEventRecord(s->ev_join, s->side));
             RT_HIP(hipStreamWaitEvent(st, s->ev_join, 0));
+            RT_HIP(mark(kt1));
         }
-        RT_HIP(mark(kt1));
+        else    // a timed launch carries its events in the dispatch itself (no marker packets)
+            hipExtLaunchKernelGGL(lfn, dim3(lgrid), dim3(lwg), 0, st, kt0, kt1, 0u, P);
         if ((P.hf_front || P.wh_on) && P.hf_measure)
             if (int rc = launch_plans(s, P, blocks, st)) return rc;
     }
@@ -634,12 +637,13 @@ int launch_batch(rt_scene *const *S, const rt_frame *F, uint32_t n, KParams *P, 
     const uint32_t kslot = s0->kt_next;
     if (timed && !s0->kt0[kslot])
     {
-        RT_HIP(hipEventCreate(&s0->kt0[kslot]));
-        RT_HIP(hipEventCreate(&s0->kt1[kslot]));
+        RT_HIP(hipEventCreateWithFlags(&s0->kt0[kslot], s0->ev_time_flags));
+        RT_HIP(hipEventCreateWithFlags(&s0->kt1[kslot], s0->ev_time_flags));
     }
-    if (timed) RT_HIP(hipEventRecord(s0->kt0[kslot], st));
-    hipLaunchKernelGGL(fn, dim3(grid), dim3(bwg), 0, st, KB);
-    if (timed) RT_HIP(hipEventRecord(s0->kt1[kslot], st));
+    // a timed launch carries its start / stop events in the dispatch itself: separate event records
+    // around it cost a measured 3-4 % of that frame (profiles/r05j_frame_series_*.json, steps 8, 24, ...)
+    hipExtLaunchKernelGGL(fn, dim3(grid), dim3(bwg), 0, st, timed ? s0->kt0[kslot] : nullptr,
+                          timed ? s0->kt1[kslot] : nullptr, 0u, KB);
     if ((P[0].hf_front || P[0].wh_on) && P[0].hf_measure)
         if (int rc = launch_plans(s0, KB.p[0], blocks, st)) return rc;
     RT_HIP(hipGetLastError());
@@ -817,6 +821,16 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
     s->wg64_o8 = env_tunable("RT_WG64_O8", s->wg64_o8);
     s->wh_seg_alpha16 = env_tunable("RT_WH_SEG_ALPHA16", s->wh_seg_alpha16);
     s->hf_follow = env_tunable("RT_HF_FOLLOW", s->hf_follow);
+    // The library's own events order device work (ev1: a scene's frames on different streams; the
+    // side-stream fork / join) or time kernels (kt0 / kt1); none of them hands memory to the host.
+    // A default event record ends in a system-scope release (L2 write-back and invalidate), which
+    // the next frame pays in refetches; device scope is enough for these (RT_EVENT_SYSFENCE=1: the
+    // default flags, A/B).  The host-visible band / tile events keep the default.
+    if (env_tunable("RT_EVENT_SYSFENCE", 0u) == 0u)
+    {
+        s->ev_time_flags = hipEventDisableSystemFence;
+        s->ev_order_flags = hipEventDisableTiming | hipEventReleaseToDevice;
+    }
     for (int a = 0; a < 3; a++)
     {
         s->dims[a] = g.dims[a];
@@ -1057,7 +1071,7 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
                                         tridist.size() + distblk.size()) +
                       sizeof(uint32_t) * (cellw.size() + cellwo.size() + cellwb.size());
     RT_HIP(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
-    RT_HIP(hipEventCreateWithFlags(&s->ev1, hipEventDisableTiming));
+    RT_HIP(hipEventCreateWithFlags(&s->ev1, s->ev_order_flags));
 
     *out = s.release();
     return RT_OK;
@@ -1071,6 +1085,8 @@ int rt_scene_destroy(rt_scene *s)
         (void)hipSetDevice(s->device);
         if (s->stream) (void)hipStreamSynchronize(s->stream);
         if (s->last_stream && s->ev_recorded) (void)hipEventSynchronize(s->ev1);
+        if (s->plan_st) (void)hipStreamSynchronize(s->plan_st);
+        if (s->side) (void)hipStreamSynchronize(s->side);
         (void)hipFree(s->d_off);
         (void)hipFree(s->d_refs);
         (void)hipFree(s->d_frefs);
@@ -1095,8 +1111,11 @@ int rt_scene_destroy(rt_scene *s)
             (void)hipFree(h.seg_col);
             (void)hipFree(h.seg_px);
             if (h.wh_cnt) (void)hipHostFree(h.wh_cnt);
+            if (h.pend_ev) (void)hipEventDestroy(h.pend_ev);
         }
         if (s->side) (void)hipStreamDestroy(s->side);
+        if (s->plan_st) (void)hipStreamDestroy(s->plan_st);
+        if (s->ev_plan_fork) (void)hipEventDestroy(s->ev_plan_fork);
         if (s->ev_fork) (void)hipEventDestroy(s->ev_fork);
         if (s->ev_join) (void)hipEventDestroy(s->ev_join);
         (void)hipFree(s->d_smp);
@@ -1652,9 +1671,10 @@ int rt_debug_heavy_first(rt_scene *s, uint32_t *front, uint32_t *listed, uint32_
     if (!c) return RT_OK;
     RT_HIP(hipDeviceSynchronize());
     HfPlan pl;
-    RT_HIP(hipMemcpy(&pl, c->plans + (c->ver & 1u), sizeof(pl), hipMemcpyDeviceToHost));
+    const uint32_t nv = c->pend ? c->pend : c->ver;        // the newest plan launched
+    RT_HIP(hipMemcpy(&pl, c->plans + (nv & 1u), sizeof(pl), hipMemcpyDeviceToHost));
     *front = c->front;
-    *listed = c->ver ? std::min(pl.cnt_hi + pl.cnt_lo, c->front) : 0u;
+    *listed = nv ? std::min(pl.cnt_hi + pl.cnt_lo, c->front) : 0u;
     *epoch = c->frames;
     return RT_OK;
 }
@@ -1681,10 +1701,11 @@ int rt_debug_wide_tiers(rt_scene *s, uint32_t *split, uint32_t *seg)
     const HfCtx *c = nullptr;
     for (const HfCtx& h : s->hf)
         if (h.wh_cnt && (!c || h.used > c->used)) c = &h;
-    if (!c || !c->ver) return RT_OK;
+    const uint32_t nv = c ? (c->pend ? c->pend : c->ver) : 0u;     // the newest plan launched
+    if (!nv) return RT_OK;
     RT_HIP(hipDeviceSynchronize());
     HfPlan pl;
-    RT_HIP(hipMemcpy(&pl, c->plans + (c->ver & 1u), sizeof(pl), hipMemcpyDeviceToHost));
+    RT_HIP(hipMemcpy(&pl, c->plans + (nv & 1u), sizeof(pl), hipMemcpyDeviceToHost));
     *split = std::min(pl.cnt_w, kWhMax);
     *seg = std::min(pl.cnt_s, kWhMax);
     return RT_OK;

@@ -9,6 +9,10 @@ run() {
     echo "$name rc=$rc"
     [ $rc -eq 0 ] || { tail -5 gpurun_out/${T}_${name}.log; exit $rc; }
 }
-run ab_front 400 python -u tools/tunable_sweep.py --env RT_HF_FRONT_DIV --values 8 4 2 --ns 1 2 4 8 --rounds 2 --extra-env RT_HF_FRONT_MAX=4096 --out ${T}_ab_front
-run ab_front1024 300 python -u tools/tunable_sweep.py --env RT_HF_FRONT_DIV --values 8 4 2 --ns 2 4 8 --rounds 2 --out ${T}_ab_front1024
-run ab_shift 300 python -u tools/tunable_sweep.py --env RT_HF_SHIFT --values 2 3 --ns 1 2 4 8 --rounds 2 --out ${T}_ab_shift
+B="python -u bench.py --no-cpu-baseline --no-end-to-end --no-first-frame"
+run pytest 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread
+run ser 100 python3 -u tools/frame_series.py --steps 60 --burn 1500 --out ${T}_ser
+run ser2 100 python3 -u tools/frame_series.py --steps 60 --burn 1500 --out ${T}_ser2
+run bench 150 $B
+run b10 200 $B --workload batch10 --no-moving-camera
+run sweep 300 python -u tools/tunable_sweep.py --env RT_HF_FLOOR --values 100000 --ns 1 2 4 8 --rounds 2 --out ${T}_sweep

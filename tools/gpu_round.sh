@@ -1,11 +1,11 @@
 #!/bin/bash
-# Round-4 end measurement on one MI355X, three gpurun calls:
+# Round end measurement on one MI355X, three gpurun calls:
 #   A: GPU tests, smoke, PMC counters of the timed sources for the three workloads
 #      (profiles/counters_<workload>.json via gpurun_out/)
 #   B: the three bench lines (bench, head4096 = config 4, batch10 = config 5) and the driver's 20 + 5
 #   C: rocprofv3 kernel trace of the bench command, per-rank shard scaling with the gather
 #      rehearsal (bench pair, head), counters of a rank-of-8 batched step
-#   gpurun -- bash tools/gpu_r04final.sh <tag> A|B|C
+#   gpurun -- bash tools/gpu_round.sh <tag> A|B|C
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 R=$PWD
