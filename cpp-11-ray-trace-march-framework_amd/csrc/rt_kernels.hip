@@ -1174,6 +1174,27 @@ __global__ void __launch_bounds__(kWG) k_unshard(const uint32_t *g, uint32_t *ou
     out[size_t(y) * W + x] = g[r * shard_elems + size_t(k) * kTilePix + (y % kTile) * kTile + (x % kTile)];
 }
 
+// A frame shape's tables (TabParams): ndc[x * spp + k] = cam_x(x, smp_k.x), then
+// ndc[W * spp + y * spp + k] = cam_y(y, smp_k.y) (camera.h:20-21 with the host's fov_xs and aspect),
+// and smp[k] = the sample table -- the same values the host path computes and copies.
+__global__ void __launch_bounds__(kWG) k_frame_tables(float *ndc, float2 *smp, TabParams T)
+{
+    const uint32_t i = blockIdx.x * kWG + threadIdx.x;
+    const uint32_t nx = T.W * T.spp, n = (T.W + T.H) * T.spp;
+    if (i < T.spp) smp[i] = make_float2(T.smp[2 * i], T.smp[2 * i + 1]);
+    if (i >= n) return;
+    if (i < nx)
+    {
+        const uint32_t x = i / T.spp, k = i - x * T.spp;
+        ndc[i] = rtd::cam_x(x, T.smp[2 * k], T.W, T.fx);
+    }
+    else
+    {
+        const uint32_t j = i - nx, y = j / T.spp, k = j - y * T.spp;
+        ndc[i] = rtd::cam_y(y, T.smp[2 * k + 1], T.H, T.fx, T.aspect);
+    }
+}
+
 // Per-camera-origin records (kVarOriginPre): for CSR reference k, tvec = o - v0,
 // qvec = tvec x e1 and DOT(e2, qvec) exactly as triangle.h:82, 90, 98 compute them, in the
 // packed-pair layout of rtd::make_frec (64 B per reference).
@@ -1410,6 +1431,7 @@ kbfn_t batch_kernel(int var, bool w64, bool o8)
 knfn_t trace_records_kernel() { return k_trace_records; }
 knfn_t record_fixup_kernel() { return k_record_fixup; }
 origin_pre_fn origin_pre_kernel() { return k_origin_pre; }
+tables_fn frame_tables_kernel() { return k_frame_tables; }
 unshard_fn unshard_kernel() { return k_unshard; }
 check_fn rcp_check_kernel() { return k_rcp_check; }
 check_fn gamma_check_kernel() { return k_gamma_check; }

@@ -151,6 +151,16 @@ struct KParams
     uint32_t rec_x0, rec_y0, rec_w, rec_h;
 };
 
+// A frame shape's camera-space tables (KParams::ndcx / ndcy, smp), written on the device by
+// k_frame_tables from rtd::cam_x / cam_y (the host's restatement uses the same IEEE operations).
+constexpr uint32_t kTabMaxSpp = 64;
+struct TabParams
+{
+    float fx, aspect;               // fov_xs (double tan on the host, H5), width / height
+    uint32_t W, H, spp;
+    float smp[2 * kTabMaxSpp];      // the sample table (Hammersley or rt_frame.sample_offsets)
+};
+
 // Multi-frame launch (rt_render_batch_device): up to kMaxBatch frames -- of different scenes --
 // in ONE grid, so one frame's tail overlaps the others' work and the heavy-first order ranks the
 // blocks of all of them.  p[0] also carries the batch's heavy-first / wide-section state (its
@@ -241,6 +251,8 @@ using unshard_fn = void (*)(const uint32_t *, uint32_t *, uint32_t, uint32_t, ui
 using check_fn = void (*)(unsigned long long *);
 using primitives_fn = void (*)(int, const float *, uint32_t, float *);
 origin_pre_fn origin_pre_kernel();
+using tables_fn = void (*)(float *, float2 *, TabParams);
+tables_fn frame_tables_kernel();                // k_frame_tables(ndc, smp, T)
 unshard_fn unshard_kernel();
 check_fn rcp_check_kernel();
 check_fn gamma_check_kernel();

@@ -7,6 +7,7 @@
 #include <cstring>
 
 #include "rt_scene.h"
+#include "rt_walk.h"
 
 namespace rtk {
 namespace {
@@ -186,8 +187,99 @@ __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks, ui
     }
 }
 
-} // namespace
+// A new launch shape's first frame has no measured costs, and in the natural order its heaviest waves
+// start late (killeroo 1080p x 4: 0.60-0.63 ms against 0.38-0.40 planned, profiles/r05i_first_frame_
+// probe.json).  This proxy writes a cost per work item from four of its rays (sample 0 of the 4x4
+// pixel block's corners at 4 spp): a walk of the L-inf distance words (Grid::Intersect's cells, empty
+// runs skipped) without triangle tests, that counts the cells looked up and the references of the
+// first kmax non-empty cells (a ray that meets geometry mostly hits within a few of them; one that
+// grazes or misses walks on), at most lmax lookups (the kernel's time is its longest walk: uncapped,
+// killeroo's took 62 us).  It also reduces the costs' maximum and sum into `stats` (a plan's
+// measurement fields), so ONE k_hf_plan pass ranks them as if a frame had measured them.
+// Nothing here touches a pixel: it only orders the first frame's blocks.
+__global__ void __launch_bounds__(kWG) k_hf_proxy(KParams P, uint32_t nitems, uint32_t kmax, uint32_t lmax,
+                                                  uint32_t wl, uint32_t wt, HfPlan *stats)
+{
+    __shared__ uint32_t s_max;
+    __shared__ unsigned long long s_sum;
+    if (threadIdx.x == 0u)
+    {
+        s_max = 0u;
+        s_sum = 0ull;
+    }
+    __syncthreads();
+    const uint32_t g = blockIdx.x * kWG + threadIdx.x;
+    const uint32_t item = g >> 2, q = g & 3u;
+    uint32_t cost = 0u;
+    if (item < nitems)
+    {
+        const uint32_t slot = (q * 21u) & ~(P.spp - 1u);          // sample 0 of pixel 0, 5, 10, 15 at 4 spp
+        const ItemCoord ic = item_coord(P, item, slot);
+        float dx, dy, dz;
+        float nct0, nct1, nct2, dt0, dt1, dt2;
+        int rem0, rem1, rem2, cs0, cs1, cs2, cell;
+        if (ic.valid)
+        {
+            rtd::dir_from_xy(P.m, P.ndcx[ic.x * P.spp], P.ndcy[ic.y * P.spp], dx, dy, dz);
+            if (dda_setup(P, P.org[0], P.org[1], P.org[2], dx, dy, dz, nct0, nct1, nct2, dt0, dt1, dt2, rem0, rem1,
+                          rem2, cs0, cs1, cs2, cell))
+            {
+                uint32_t looks = 0u, refs = 0u, ne = 0u, skip = 0u;
+                for (;;)
+                {
+                    if (skip == 0u)
+                    {
+                        const uint32_t w = P.cellw[uint32_t(cell)];
+                        const uint32_t cnt = w & 2047u;
+                        refs += cnt;
+                        if ((cnt && ++ne >= kmax) || ++looks >= lmax) break;
+                        skip = cnt ? 0u : (w >> 11) - (w >> 11 ? 1u : 0u);
+                    }
+                    else
+                        skip--;
+                    // one DDA step along the axis of the nearest crossing; out of the grid ends it
+                    if (nct0 <= nct1 && nct0 <= nct2)
+                    {
+                        if (rem0-- == 0) break;
+                        cell += cs0;
+                        nct0 += dt0;
+                    }
+                    else if (nct1 <= nct2)
+                    {
+                        if (rem1-- == 0) break;
+                        cell += cs1;
+                        nct1 += dt1;
+                    }
+                    else
+                    {
+                        if (rem2-- == 0) break;
+                        cell += cs2;
+                        nct2 += dt2;
+                    }
+                }
+                cost = 64u * (looks * wl + refs * wt);
+            }
+            else
+                cost = 64u;
+        }
+    }
+    cost += __shfl_xor(cost, 1, 64);
+    cost += __shfl_xor(cost, 2, 64);
+    if (item < nitems && q == 0u)
+    {
+        P.hf_cost[item] = cost;
+        atomicMax(&s_max, cost);
+        atomicAdd(&s_sum, (unsigned long long)(cost >> 4));
+    }
+    __syncthreads();
+    if (threadIdx.x == 0u)
+    {
+        if (s_max) atomicMax(&stats->maxc, s_max);
+        if (s_sum) atomicAdd(&stats->sum, s_sum);
+    }
+}
 
+} // namespace
 
 // k_hf_plan after a measured frame.  A plan lists a block only against the PREVIOUS measurement (its
 // maximum and span decide the thresholds), so the first measured frame of a launch shape listed
@@ -208,7 +300,10 @@ int launch_plans(rt_scene *s, const KParams& P, uint64_t blocks, hipStream_t st)
     HfCtx *c = s->hf_last;
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     RT_HIP(hipStreamIsCapturing(st, &cap));
-    if (P.hf_ver != 0u && c && cap == hipStreamCaptureStatusNone)
+    // two passes: a shape's first measurement (version 0), and the first one after a proxy plan (its
+    // maximum and span are in proxy units): the second pass ranks against the first's
+    const bool twice = P.hf_ver == 0u || (c && c->proxied);
+    if (!twice && c && cap == hipStreamCaptureStatusNone)
     {
         if (!s->plan_st)
         {
@@ -226,11 +321,15 @@ int launch_plans(rt_scene *s, const KParams& P, uint64_t blocks, hipStream_t st)
         return RT_OK;
     }
     hipLaunchKernelGGL(k_hf_plan, grid, wg, 0, st, P, uint32_t(blocks), s->hf_shift);
-    if (c) c->ver = P.hf_ver + (P.hf_ver == 0u ? 2u : 1u);
-    if (P.hf_ver == 0u)
+    if (c)
+    {
+        c->ver = P.hf_ver + (twice ? 2u : 1u);
+        c->proxied = false;
+    }
+    if (twice)
     {
         KParams Q = P;
-        Q.hf_ver = 1u;
+        Q.hf_ver = P.hf_ver + 1u;
         Q.hf_plan_in = P.hf_plan_out;
         Q.hf_plan_out = const_cast<HfPlan *>(P.hf_plan_in);
         Q.hf_list_in = P.hf_list_out;
@@ -296,31 +395,36 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
         // shape and read freed (null) state arrays
         std::memset(c->key, 0, sizeof(c->key));
         c->frames = 0;
+        c->proxied = false;
         c->ver = 0;
-        if (blocks > c->cap_blocks || !c->lists)
+        if (blocks > c->cap_blocks || !c->mem)
         {
+            // ONE device allocation per context (a new launch shape's first frame waits for the
+            // host's allocation calls: seven of them took ~0.1 ms, profiles/r05i_first_frame_probe.json),
+            // the cleared arrays first so one memset clears them: plans [2], ticket (+ pad to 16 B),
+            // marks [2][cap], wh_marks [2][4 cap]; then cost [4 cap], lists [2][kHfFrontMax],
+            // wh_lists [2][2][kWhMax] ([version][tier])
             c->cap_blocks = 0;
-            if (c->marks) RT_HIP(hipFree(c->marks));
-            if (c->cost) RT_HIP(hipFree(c->cost));
-            if (c->wh_marks) RT_HIP(hipFree(c->wh_marks));
-            c->marks = c->cost = c->wh_marks = nullptr;
-            RT_HIP(hipMalloc(&c->marks, sizeof(uint32_t) * 2 * blocks));
-            RT_HIP(hipMalloc(&c->cost, sizeof(uint32_t) * kWavesPerWG * blocks));
-            RT_HIP(hipMalloc(&c->wh_marks, sizeof(uint32_t) * 2 * kWavesPerWG * blocks));
-            if (!c->lists)
-            {
-                RT_HIP(hipMalloc(&c->plans, sizeof(HfPlan) * 2));
-                RT_HIP(hipMalloc(&c->ticket, sizeof(uint32_t)));
-                RT_HIP(hipMalloc(&c->wh_lists, sizeof(uint32_t) * 2 * 2 * kWhMax));   // [version][tier][kWhMax]
-                RT_HIP(hipHostMalloc(&c->wh_cnt, sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent));
-                RT_HIP(hipMalloc(&c->lists, sizeof(uint32_t) * 2 * kHfFrontMax));   // last: marks completion
-            }
+            if (c->mem) RT_HIP(hipFree(c->mem));
+            c->mem = nullptr;
+            const size_t head = sizeof(HfPlan) * 2 + 16u;
+            const size_t cleared = head + sizeof(uint32_t) * (2u + 2u * kWavesPerWG) * blocks;
+            const size_t bytes = cleared + sizeof(uint32_t) * (kWavesPerWG * blocks + 2u * kHfFrontMax + 4u * kWhMax);
+            RT_HIP(hipMalloc(&c->mem, bytes));
+            char *m = static_cast<char *>(c->mem);
+            c->plans = reinterpret_cast<HfPlan *>(m);
+            c->ticket = reinterpret_cast<uint32_t *>(m + sizeof(HfPlan) * 2);
+            c->marks = reinterpret_cast<uint32_t *>(m + head);
+            c->wh_marks = c->marks + 2u * blocks;
+            c->cost = c->wh_marks + 2u * kWavesPerWG * blocks;
+            c->lists = c->cost + kWavesPerWG * blocks;
+            c->wh_lists = c->lists + 2u * kHfFrontMax;
+            c->cleared_bytes = cleared;
             c->cap_blocks = uint32_t(blocks);
         }
-        RT_HIP(hipMemsetAsync(c->marks, 0, sizeof(uint32_t) * 2 * c->cap_blocks, st));
-        RT_HIP(hipMemsetAsync(c->wh_marks, 0, sizeof(uint32_t) * 2 * kWavesPerWG * c->cap_blocks, st));
-        RT_HIP(hipMemsetAsync(c->plans, 0, sizeof(HfPlan) * 2, st));
-        RT_HIP(hipMemsetAsync(c->ticket, 0, sizeof(uint32_t), st));
+        RT_HIP(hipMemsetAsync(c->mem, 0, c->cleared_bytes, st));
+        c->wh_cnt = s->h_wh_cnt + (c - s->hf);         // the scene's mapped counters (rt_scene_create)
+        c->wh_cnt_dev = s->d_wh_cnt + (c - s->hf);
         *(volatile uint32_t *)c->wh_cnt = 0u;
         c->nblocks = uint32_t(blocks);
         // front: 1 / hf_front_div of the blocks (an eighth), capped at hf_front_max (1024), a multiple
@@ -410,9 +514,37 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
         P.wh_px = c->seg_px;
         P.wh_list_in = c->wh_lists + size_t(v & 1u) * 2u * kWhMax;
         P.wh_list_out = c->wh_lists + size_t((v + 1u) & 1u) * 2u * kWhMax;
-        void *dev = nullptr;
-        RT_HIP(hipHostGetDevicePointer(&dev, c->wh_cnt, 0));
-        P.wh_host_cnt = static_cast<uint32_t *>(dev);
+        P.wh_host_cnt = c->wh_cnt_dev;
+    }
+    // a new shape's first frame (one frame, no wide section): a plan from the cost proxy
+    if (c->frames == 1u && !batch && P.hf_front && !P.wh_on && s->hf_proxy && P.cellw && P.spp <= 64u)
+    {
+        // the proxy's costs and their maximum / sum as version 1's measurement, then one plan pass
+        // (version 1 -> 2) on the launch stream; every array it touches was cleared with the context
+        const uint32_t nitems = uint32_t(blocks) * kWavesPerWG;
+        hipLaunchKernelGGL(k_hf_proxy, dim3((4u * nitems + kWG - 1u) / kWG), dim3(kWG), 0, st, P, nitems,
+                           s->hf_proxy_cells, s->hf_proxy_looks, s->hf_proxy_wl, s->hf_proxy_wt, c->plans + 1);
+        KParams Q = P;
+        Q.hf_floor = 0u;                // proxy units: only the plan's relative thresholds apply
+        Q.hf_ver = 1u;
+        Q.hf_plan_in = c->plans + 1;
+        Q.hf_plan_out = c->plans;
+        Q.hf_list_in = c->lists + kHfFrontMax;
+        Q.hf_list_out = c->lists;
+        Q.hf_mark_in = c->marks + c->cap_blocks;
+        Q.hf_mark_out = c->marks;
+        const dim3 pg(uint32_t((blocks + kWG * kHfPlanPer - 1) / (kWG * kHfPlanPer)));
+        hipLaunchKernelGGL(k_hf_plan, pg, dim3(kWG), 0, st, Q, uint32_t(blocks), s->hf_shift);
+        RT_HIP(hipGetLastError());
+        c->ver = 2u;
+        c->proxied = true;              // the plan after this frame ranks twice (launch_plans)
+        P.hf_ver = c->ver;
+        P.hf_mark_in = c->marks + size_t(c->ver & 1u) * c->cap_blocks;
+        P.hf_mark_out = c->marks + size_t((c->ver + 1u) & 1u) * c->cap_blocks;
+        P.hf_list_in = c->lists + size_t(c->ver & 1u) * kHfFrontMax;
+        P.hf_list_out = c->lists + size_t((c->ver + 1u) & 1u) * kHfFrontMax;
+        P.hf_plan_in = c->plans + (c->ver & 1u);
+        P.hf_plan_out = c->plans + ((c->ver + 1u) & 1u);
     }
     return RT_OK;
 }

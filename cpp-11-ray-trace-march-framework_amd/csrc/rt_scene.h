@@ -28,6 +28,8 @@ struct HfCtx
     uint64_t key[5] = { 0, 0, 0, 0, 0 };   // launch shape: blocks, spp, region, shard, variant, batch
     uint32_t nblocks = 0, front = 0;
     uint32_t cap_blocks = 0;            // allocated marks per buffer
+    void *mem = nullptr;                // one allocation holding the arrays below (hf_prepare)
+    size_t cleared_bytes = 0;           // its head that a new shape clears
     uint32_t *marks = nullptr;          // [2][cap_blocks]
     uint32_t *cost = nullptr;           // [cap_blocks * kWavesPerWG] wave cycles of the last frame
     uint32_t *lists = nullptr;          // [2][kHfFrontMax], by plan version parity
@@ -35,7 +37,8 @@ struct HfCtx
     uint32_t *ticket = nullptr;         // k_hf_plan's workgroup ticket
     uint32_t *wh_marks = nullptr;       // [2][cap_blocks * kWavesPerWG] wide items, by version parity
     uint32_t *wh_lists = nullptr;       // [2][kWhMax]
-    uint32_t *wh_cnt = nullptr;         // host-mapped: the newest plan's wide item count
+    uint32_t *wh_cnt = nullptr;         // host-mapped: the newest plan's wide item count (rt_scene::h_wh_cnt)
+    uint32_t *wh_cnt_dev = nullptr;     // its device address
     float4 *seg_col = nullptr;          // kVarWideSeg scratch: [kWhMax][64] sample colours
     uint32_t *seg_px = nullptr;         // kVarWideSeg scratch: [kWhMax][64] arrivals per pixel
     uint32_t frames = 0;                // frames rendered with this shape
@@ -45,6 +48,7 @@ struct HfCtx
     // by the next frame that measures
     uint32_t pend = 0, pend_age = 0;
     hipEvent_t pend_ev = nullptr;
+    bool proxied = false;               // the current plan came from k_hf_proxy's costs
     uint64_t used = 0;                  // LRU stamp
     uint64_t cam = 0;                   // camera signature of the last frame (cam_signature)
 };
@@ -82,6 +86,8 @@ struct rt_scene
     uint32_t clk_items = 0;
     // AUTO heavy-first order: per launch shape, which blocks the previous frame found heavy
     rtk::HfCtx hf[rtk::kHfCtxs];
+    uint32_t *h_wh_cnt = nullptr;       // [kHfCtxs] host-mapped counters of the contexts (one allocation)
+    uint32_t *d_wh_cnt = nullptr;
     uint64_t hf_clock = 0;
     uint64_t hf_evictions = 0;      // launch shapes that displaced another's state (rt_scene_info)
     uint64_t batch_launches = 0;    // rt_render_batch_device chunks led by this scene: one launch ...
@@ -93,6 +99,13 @@ struct rt_scene
     uint32_t hf_front_div = 8;      // RT_HF_FRONT_DIV: the front section holds 1 / this of a launch's blocks ...
     uint32_t hf_front_max = 1024;   // RT_HF_FRONT_MAX: ... at most this many (<= kHfFrontMax)
     uint32_t hf_shift = 2;          // RT_HF_SHIFT: heavy = cost > last max >> hf_shift (very heavy: >> 1)
+    uint32_t hf_proxy = 0;          // RT_HF_PROXY: a new shape's first frame is planned from k_hf_proxy's costs
+                                    // (an A/B arm: killeroo's first frame 0.70 -> 0.63 ms, every other
+                                    // scene's slower by the proxy's time)
+    uint32_t hf_proxy_cells = 6;    // RT_HF_PROXY_CELLS: non-empty cells a proxy ray counts ...
+    uint32_t hf_proxy_looks = 32;   // RT_HF_PROXY_LOOKS: ... in at most this many lookups
+    uint32_t hf_proxy_wl = 4;       // RT_HF_PROXY_WL / _WT: weight of a cell lookup / of a reference
+    uint32_t hf_proxy_wt = 1;
     uint32_t wh_floor = 100000;     // RT_WH_FLOOR: wide-section threshold floor, shader cycles
     uint32_t wh_alpha16 = 32;       // RT_WH_ALPHA16: wide threshold, sixteenths of the estimated span
     uint32_t wh_alpha16_n2 = 16;    // RT_WH_ALPHA16_N2: the same for a rank of 2 of a batched step
@@ -118,6 +131,8 @@ struct rt_scene
     float *d_ndc = nullptr;
     size_t ndc_cap = 0;
     std::vector<float> ndc_key;
+    rtk::TabParams tab = {};            // the tables' parameters while tab_dirty (flush_tables)
+    bool tab_dirty = false;
     uint32_t ndc_w = 0, ndc_spp = 0;
     // the frame description the tables above were built for (prepare_samples' fast check: width,
     // height, spp, fov bits and the caller's sample table; no table rebuild per launch)

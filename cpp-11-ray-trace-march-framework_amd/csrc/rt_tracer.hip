@@ -23,6 +23,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstddef>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -40,6 +41,25 @@
 using namespace rtk;
 
 namespace {
+// RT_HOST_TRACE=1: the host time of a render call's phases, printed to stderr per call (a new frame
+// shape's first call waits for the host; this names what it waits for)
+struct HostTrace
+{
+    bool on = std::getenv("RT_HOST_TRACE") != nullptr;
+    std::chrono::steady_clock::time_point t0;
+    char buf[512];
+    int len = 0;
+    void start() { if (on) { t0 = std::chrono::steady_clock::now(); len = 0; } }
+    void mark(const char *what)
+    {
+        if (!on || len > 400) return;
+        const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+        len += std::snprintf(buf + len, sizeof(buf) - size_t(len), " %s %.1f", what, us);
+    }
+    void end() { if (on) std::fprintf(stderr, "rt_host_trace:%s\n", buf); }
+};
+HostTrace g_ht;
+
 
 thread_local std::string g_err;
 
@@ -155,6 +175,19 @@ std::vector<float> sample_table(const rt_frame *f, uint32_t spp)
     return tbl;
 }
 
+// The frame tables of prepare_samples' device path, written on stream st after every launch that
+// may still read the old ones (st's own, and the scene's last launch on another stream: ev1).
+int flush_tables(rt_scene *s, hipStream_t st)
+{
+    if (!s->tab_dirty) return RT_OK;
+    if (s->ev_recorded && st != s->last_stream) RT_HIP(hipStreamWaitEvent(st, s->ev1, 0));
+    const uint32_t n = (s->tab.W + s->tab.H) * s->tab.spp;
+    hipLaunchKernelGGL(frame_tables_kernel(), dim3((n + kWG - 1) / kWG), dim3(kWG), 0, st, s->d_ndc, s->d_smp, s->tab);
+    RT_HIP(hipGetLastError());
+    s->tab_dirty = false;
+    return RT_OK;
+}
+
 int prepare_ndc(rt_scene *s, const rt_frame *f, uint32_t spp, const std::vector<float>& tbl)
 {
     const float fx = fov_xs_of(f), aspect = float(f->width) / float(f->height);
@@ -211,6 +244,29 @@ int prepare_samples(rt_scene *s, const rt_frame *f, uint32_t spp)
     if (tables_match(s, f, spp)) return RT_OK;
     s->fp_valid = false;
     const std::vector<float> tbl = sample_table(f, spp);
+    const size_t n = (size_t(f->width) + f->height) * spp;
+    if (spp <= kTabMaxSpp && n <= s->ndc_cap)
+    {
+        // the tables are written on the device, in stream order before the frame's launch
+        // (flush_tables): a new frame shape costs no host wait and no synchronous copy
+        std::vector<float> key = ndc_key(f, spp, tbl);
+        if (key != s->ndc_key || tbl != s->smp_host)
+        {
+            s->tab.fx = fov_xs_of(f);
+            s->tab.aspect = float(f->width) / float(f->height);
+            s->tab.W = f->width;
+            s->tab.H = f->height;
+            s->tab.spp = spp;
+            std::memcpy(s->tab.smp, tbl.data(), tbl.size() * sizeof(float));
+            s->tab_dirty = true;
+            s->ndc_key = key;
+            s->ndc_w = f->width;
+            s->ndc_spp = spp;
+            s->smp_host = tbl;
+        }
+        return remember_tables(s, f, spp, tbl);
+    }
+    s->tab_dirty = false;           // a pending device write is superseded (its key differs: spp)
     if (int rc = prepare_ndc(s, f, spp, tbl)) return rc;
     if (tbl == s->smp_host) return remember_tables(s, f, spp, tbl);
     if (int rc = wait_scene_idle(s)) return rc;
@@ -355,6 +411,8 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
     // one waits for it, so frames of one scene never overlap on the device.
     // (order_streams false: the caller orders its streams itself, rt_render_frame_host_tiled)
     if (order_streams && s->ev_recorded && st != s->last_stream) RT_HIP(hipStreamWaitEvent(st, s->ev1, 0));
+    if (int rc = flush_tables(s, st)) return rc;
+    g_ht.mark("tables");
     s->last_stream = st;
     // kVarXcdBands turn size: one row of this launch's tiles (ceil(tiles_x / nranks) local tiles
     // span a full frame row in shard mode).  Measured best of 1/4 .. 4 rows and 1..16 tiles:
@@ -371,6 +429,7 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
         var = kVarAutoCore | (s->rcp_safe ? kVarFastRcp : 0) | (auto_runs(s) ? kVarPackedRem | kVarSkipRun : 0) |
               ((f->kernel & RT_KERNEL_FLAG_WAVE_CLOCK) ? kVarWaveClock : 0);
         if (int rc = ensure_origin_terms(s, P, st)) return rc;
+        g_ht.mark("origin");
     }
     else if (lanes && P.isect == RT_ISECT_RAY_MARCH)
         var = kVarMarch | ((f->kernel & RT_KERNEL_FLAG_EXHAUSTIVE) ? kVarExhaustive : 0);
@@ -451,6 +510,7 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
         if (front || wide_heavy)
         {
             if (int rc = hf_prepare(s, P, blocks, kvar, front, st)) return rc;
+            g_ht.mark("hf_prepare");
             grid += P.hf_front;
         }
         // one-wave workgroups (k_render_lanes_w64): the same blocks, each wave dispatched by itself
@@ -502,6 +562,7 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
         RT_HIP(mark(kt1));
     }
     RT_HIP(hipGetLastError());
+    g_ht.mark("launched");
     RT_HIP(hipEventRecord(s->ev1, st));
     s->ev_recorded = true;
     if (timed)
@@ -576,6 +637,7 @@ int launch_batch(rt_scene *const *S, const rt_frame *F, uint32_t n, KParams *P, 
         for (uint32_t j = 0; j < i; j++) first = first && S[j] != s;
         if (!first) continue;
         if (s->ev_recorded && st != s->last_stream) RT_HIP(hipStreamWaitEvent(st, s->ev1, 0));
+        if (int rc = flush_tables(s, st)) return rc;
         s->last_stream = st;
         if (int rc = ensure_origin_terms(s, P[i], st)) return rc;
     }
@@ -808,6 +870,11 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
     s->hf_front_div = env_tunable("RT_HF_FRONT_DIV", s->hf_front_div);
     s->hf_front_max = env_tunable("RT_HF_FRONT_MAX", s->hf_front_max);
     s->hf_shift = std::min(env_tunable("RT_HF_SHIFT", s->hf_shift), 8u);
+    s->hf_proxy = env_tunable("RT_HF_PROXY", s->hf_proxy);
+    s->hf_proxy_cells = std::max(env_tunable("RT_HF_PROXY_CELLS", s->hf_proxy_cells), 1u);
+    s->hf_proxy_looks = std::max(env_tunable("RT_HF_PROXY_LOOKS", s->hf_proxy_looks), 1u);
+    s->hf_proxy_wl = env_tunable("RT_HF_PROXY_WL", s->hf_proxy_wl);
+    s->hf_proxy_wt = env_tunable("RT_HF_PROXY_WT", s->hf_proxy_wt);
     s->wg64 = env_tunable("RT_WG64", s->wg64);
     s->wg64_min_blocks = env_tunable("RT_WG64_MIN_BLOCKS", s->wg64_min_blocks);
     s->wg64_batch_min_blocks = env_tunable("RT_WG64_BATCH_MIN_BLOCKS", s->wg64_batch_min_blocks);
@@ -1072,6 +1139,26 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
                       sizeof(uint32_t) * (cellw.size() + cellwo.size() + cellwb.size());
     RT_HIP(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
     RT_HIP(hipEventCreateWithFlags(&s->ev1, s->ev_order_flags));
+    // the plan stream (launch_plans) and the first timed launch's events: created here, not by a
+    // frame (a stream's creation took ~0.33 ms of the second frame's call, profiles/r05p_host_trace.log)
+    RT_HIP(hipStreamCreateWithFlags(&s->plan_st, hipStreamNonBlocking));
+    RT_HIP(hipEventCreateWithFlags(&s->ev_plan_fork, s->ev_order_flags));
+    RT_HIP(hipEventCreateWithFlags(&s->kt0[0], s->ev_time_flags));
+    RT_HIP(hipEventCreateWithFlags(&s->kt1[0], s->ev_time_flags));
+    // the heavy-first contexts' host-mapped counters, and the frame tables at a 4K x 16 spp capacity:
+    // allocated here so a new launch shape's first frame waits for no allocation call
+    RT_HIP(hipHostMalloc(&s->h_wh_cnt, sizeof(uint32_t) * kHfCtxs, hipHostMallocMapped | hipHostMallocCoherent));
+    std::memset(s->h_wh_cnt, 0, sizeof(uint32_t) * kHfCtxs);
+    {
+        void *dev = nullptr;
+        RT_HIP(hipHostGetDevicePointer(&dev, s->h_wh_cnt, 0));
+        s->d_wh_cnt = static_cast<uint32_t *>(dev);
+    }
+    s->ndc_cap = size_t(4096 + 4096) * 16u;
+    RT_HIP(hipMalloc(&s->d_ndc, s->ndc_cap * sizeof(float)));
+    s->smp_cap = 64u;
+    RT_HIP(hipMalloc(&s->d_smp, sizeof(float2) * s->smp_cap));
+    RT_HIP(hipHostMalloc(&s->h_smp_pinned, sizeof(float2) * s->smp_cap));
 
     *out = s.release();
     return RT_OK;
@@ -1101,18 +1188,12 @@ int rt_scene_destroy(rt_scene *s)
         (void)hipFree(s->d_clk);
         for (HfCtx& h : s->hf)
         {
-            (void)hipFree(h.marks);
-            (void)hipFree(h.cost);
-            (void)hipFree(h.lists);
-            (void)hipFree(h.plans);
-            (void)hipFree(h.ticket);
-            (void)hipFree(h.wh_marks);
-            (void)hipFree(h.wh_lists);
+            (void)hipFree(h.mem);
             (void)hipFree(h.seg_col);
             (void)hipFree(h.seg_px);
-            if (h.wh_cnt) (void)hipHostFree(h.wh_cnt);
             if (h.pend_ev) (void)hipEventDestroy(h.pend_ev);
         }
+        if (s->h_wh_cnt) (void)hipHostFree(s->h_wh_cnt);
         if (s->side) (void)hipStreamDestroy(s->side);
         if (s->plan_st) (void)hipStreamDestroy(s->plan_st);
         if (s->ev_plan_fork) (void)hipEventDestroy(s->ev_plan_fork);
@@ -1187,13 +1268,18 @@ int render_device(rt_scene *s, const rt_frame *f, uint32_t rank, uint32_t nranks
     int rc = validate_frame(f);
     if (rc) return rc;
     std::lock_guard<std::mutex> lk(s->mtx);
+    g_ht.start();
     if ((rc = ensure_device(s))) return rc;
     const uint32_t spp = std::max(1u, f->spp);
     if ((rc = prepare_samples(s, f, spp))) return rc;
+    g_ht.mark("samples");
     KParams P;
     const uint32_t local = device_params(s, f, rank, nranks, shard, d_out, d_hits, P);
     if (recs) set_records(P, *recs);
-    return launch_render(s, f, P, local, static_cast<hipStream_t>(hip_stream));
+    rc = launch_render(s, f, P, local, static_cast<hipStream_t>(hip_stream));
+    g_ht.mark("done");
+    g_ht.end();
+    return rc;
 }
 
 // rt_render_batch_device's frames [0, n): one k_render_batch launch when they can share it.  The
@@ -1555,6 +1641,7 @@ int rt_render_frame_host_tiled(rt_scene *s, const rt_frame *f, uint32_t *h_tiles
     if (use_lanes(f, spp) && P0.isect == RT_ISECT_GRID && P0.tri_test == RT_TRI_MOLLER_TRUMBORE &&
         ((f->kernel & RT_KERNEL_KIND_MASK) == RT_KERNEL_AUTO || (f->kernel & RT_KERNEL_KIND_MASK) == RT_KERNEL_COMPACT))
         if ((rc = ensure_origin_terms(s, P0, st[0]))) return rc;
+    if ((rc = flush_tables(s, st[0]))) return rc;      // before the fork: both streams read them
     RT_HIP(hipEventRecord(s->ev_t_fork, st[0]));
     RT_HIP(hipStreamWaitEvent(st[1], s->ev_t_fork, 0));
     s->nbands = 0;
@@ -1636,6 +1723,11 @@ int rt_trace_samples(rt_scene *s, const rt_frame *f, uint32_t x0, uint32_t y0, u
     P.recs = d_rec;
     P.rec_x0 = x0; P.rec_y0 = y0; P.rec_w = w; P.rec_h = h;
     if (P.isect == RT_ISECT_RAY_MARCH && (f->kernel & RT_KERNEL_FLAG_EXHAUSTIVE)) P.isect += 0x100;
+    if ((rc = flush_tables(s, s->stream)))
+    {
+        (void)hipFree(d_rec);
+        return rc;
+    }
     hipLaunchKernelGGL(trace_records_kernel(), dim3((n + kWG - 1) / kWG), dim3(kWG), 0, s->stream, P, n);
     hipError_t e = hipGetLastError();
     if (e == hipSuccess) e = hipMemcpyAsync(out, d_rec, sizeof(rt_sample_rec) * n, hipMemcpyDeviceToHost, s->stream);

@@ -1,6 +1,7 @@
 # ad-hoc GPU session; edited per experiment
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"; mkdir -p gpurun_out; export TMPDIR=/tmp
+R=$PWD
 T=${1:-adhoc}
 run() {
     local name=$1 secs=$2; shift 2
@@ -9,10 +10,6 @@ run() {
     echo "$name rc=$rc"
     [ $rc -eq 0 ] || { tail -5 gpurun_out/${T}_${name}.log; exit $rc; }
 }
-B="python -u bench.py --no-cpu-baseline --no-end-to-end --no-first-frame"
-run pytest 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread
-run ser 100 python3 -u tools/frame_series.py --steps 60 --burn 1500 --out ${T}_ser
-run ser2 100 python3 -u tools/frame_series.py --steps 60 --burn 1500 --out ${T}_ser2
-run bench 150 $B
-run b10 200 $B --workload batch10 --no-moving-camera
-run sweep 300 python -u tools/tunable_sweep.py --env RT_HF_FLOOR --values 100000 --ns 1 2 4 8 --rounds 2 --out ${T}_sweep
+FF="python3 -u tools/first_frame_probe.py --scenes 1 8 --reps 2"
+run ff_trace0 120 env RT_HOST_TRACE=1 RT_HF_PROXY=0 $FF --out ${T}_ff_trace0
+run ff_trace1 120 env RT_HOST_TRACE=1 RT_HF_PROXY_CELLS=3 $FF --out ${T}_ff_trace1
