@@ -64,7 +64,7 @@ TRACER_SYMBOLS = [
     "rt_host_free", "rt_render_hits_device", "rt_scene_info_get", "rt_build_hash", "rt_render_batch_device",
     "rt_render_records_device", "rt_render_frame_host_tiled",
 ]
-MAX_BATCH = 6                            # frames per rt_render_batch_device launch (kMaxBatch)
+MAX_BATCH = 10                           # frames per rt_render_batch_device launch (kMaxBatch)
 
 HOST_SYMBOLS = [
     "rth_scene_load", "rth_scene_from_mesh", "rth_scene_free", "rth_scene_desc",

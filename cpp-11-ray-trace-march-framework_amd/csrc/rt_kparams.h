@@ -165,8 +165,9 @@ struct TabParams
 // in ONE grid, so one frame's tail overlaps the others' work and the heavy-first order ranks the
 // blocks of all of them.  p[0] also carries the batch's heavy-first / wide-section state (its
 // block and item indices are the launch's, frame-major); every other field is per frame.
-// 6 frames keep KBatch (~3.6 KiB) inside the 4 KiB kernarg limit (static_assert below).
-constexpr uint32_t kMaxBatch = 6;
+// 10 frames (config 5's whole step) make KBatch ~5.9 KiB of kernel arguments: the runtime passes
+// them intact past 4 KiB (tools/probe/kernarg_probe.hip, 8 KiB checked on the MI355X).
+constexpr uint32_t kMaxBatch = 10;
 struct KBatch
 {
     KParams p[kMaxBatch];
@@ -174,7 +175,7 @@ struct KBatch
     uint32_t base[kMaxBatch + 1];   // first launch block of each frame; base[nframes] = all blocks
 };
 
-static_assert(sizeof(KBatch) <= 4096, "kernel arguments are limited to 4 KiB");
+static_assert(sizeof(KBatch) <= 8192, "kernel arguments checked up to 8 KiB");
 
 // Frames in the launch that starts at frame `start` of an n-frame batch: ceil(n / kMaxBatch)
 // launches of near-equal size (10 frames: 5 + 5), each with one tail.  Mirrored by the binding's

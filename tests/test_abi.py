@@ -99,18 +99,23 @@ def test_batch_chunks_mirror_the_library():
         assert [i for i, _ in ch] == [sum(c for _, c in ch[:k]) for k in range(len(ch))]
         assert sum(c for _, c in ch) == n and len(ch) == -(-n // rtm.MAX_BATCH)
         assert max(c for _, c in ch) - min(c for _, c in ch) <= 1 and max(c for _, c in ch) <= rtm.MAX_BATCH
-    assert rtm.batch_chunks(10) == [(0, 5), (5, 5)] and rtm.batch_chunks(2) == [(0, 2)]
+    assert rtm.batch_chunks(10) == [(0, 10)] and rtm.batch_chunks(12) == [(0, 6), (6, 6)] and rtm.batch_chunks(2) == [(0, 2)]
 
 
 def test_batch_order_balances_launches():
     """rtm.batch_order: a permutation whose in-order launches (batch_chunks) take the heaviest
-    frames apart -- config 5's measured per-frame costs give launches within 4 % of each other."""
+    frames apart -- twice config 5's measured per-frame costs give launches within 4 % of each
+    other -- each launch's heaviest frame first."""
     costs = [0.205, 0.187, 0.268, 0.222, 0.264, 0.553, 0.228, 0.384, 0.377, 0.285]
     o = rtm.batch_order(costs)
     assert sorted(o) == list(range(10))
-    loads = [sum(costs[i] for i in o[s:s + n]) for s, n in rtm.batch_chunks(10)]
+    assert rtm.batch_chunks(10) == [(0, 10)] and o[0] == 5           # one launch, heaviest frame first
+    c20 = costs + [x * 1.01 for x in costs]                           # two launches of 10
+    o = rtm.batch_order(c20)
+    assert sorted(o) == list(range(20))
+    loads = [sum(c20[i] for i in o[s:s + n]) for s, n in rtm.batch_chunks(20)]
     assert max(loads) / min(loads) < 1.04
-    assert not {5, 7, 8} <= set(o[:5]) and not {5, 7, 8} <= set(o[5:])
+    assert not {5, 15, 7, 17} <= set(o[:10]) and not {5, 15, 7, 17} <= set(o[10:])
     assert rtm.batch_order([1.0, 2.0]) == [1, 0] and rtm.batch_order([]) == []
     for n in range(1, 20):
         c = [float((7 * i) % 5 + 1) for i in range(n)]

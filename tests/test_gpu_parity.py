@@ -1060,21 +1060,29 @@ def test_batch_bench_pair(golden, scenes, N):
 
 
 def test_batch_all_ten_scenes(golden, scenes):
-    """BASELINE config 5 through rt_render_batch_device: 10 frames = two launches of 5 frames
-    (rtm.batch_chunks), each led by its first frame's scene, none falling back."""
+    """BASELINE config 5 through rt_render_batch_device: 10 frames = ONE launch (kMaxBatch 10, ~5.9 KiB
+    of kernel arguments), led by its first frame's scene, none falling back; 12 frames (two scenes
+    twice) = two launches of 6."""
     sids = tuple(range(10))
     gss = [scenes(s)[1] for s in sids]
-    assert rtm.batch_chunks(10) == [(0, 5), (5, 5)]
+    assert rtm.batch_chunks(10) == [(0, 10)]
     before = [(g.info()["batch_launches"], g.info()["batch_fallbacks"]) for g in gss]
     _batch_check(golden, gss, sids, 1920, 1080, 1, 3)
     after = [(g.info()["batch_launches"], g.info()["batch_fallbacks"]) for g in gss]
     assert [(a[0] - b[0], a[1] - b[1]) for a, b in zip(after, before)] == \
-        [(3, 0) if i in (0, 5) else (0, 0) for i in range(10)]
+        [(3, 0) if i == 0 else (0, 0) for i in range(10)]
+    sids12 = sids + (1, 8)
+    assert rtm.batch_chunks(12) == [(0, 6), (6, 6)]
+    before = [(g.info()["batch_launches"], g.info()["batch_fallbacks"]) for g in gss]
+    _batch_check(golden, [gss[s] for s in sids12], sids12, 1920, 1080, 1, 2)
+    after = [(g.info()["batch_launches"], g.info()["batch_fallbacks"]) for g in gss]
+    assert [(a[0] - b[0], a[1] - b[1]) for a, b in zip(after, before)] == \
+        [(2, 0) if i in (0, 6) else (0, 0) for i in range(10)]
 
 
 def test_batch_cost_ordered_ten_scenes(golden, scenes):
     """bench.py's config-5 step: each frame timed in its own launch (rtm.frame_costs, the library's
-    event ring), the frames reordered by rtm.batch_order into two cost-balanced launches of 5;
+    event ring), the frames reordered by rtm.batch_order (one launch of 10, the heaviest frame first);
     every frame and its per-sample hit IDs still equal the reference's."""
     import torch
     sids = tuple(range(10))
@@ -1087,9 +1095,8 @@ def test_batch_cost_ordered_ten_scenes(golden, scenes):
         assert sha_dev(t) == golden["frames_1080p4"][str(sid)]["bgra_sha256"], sid
     order = rtm.batch_order(costs)
     assert sorted(order) == list(range(10))
-    # the heaviest frame (scene 5, room + cat) and the next two never share one launch
-    heavy = sorted(range(10), key=lambda i: -costs[i])[:3]
-    assert not set(heavy) <= set(order[:5]) and not set(heavy) <= set(order[5:]), (costs, order)
+    # the heaviest frame (scene 5, room + cat) leads the one launch
+    assert order[0] == max(range(10), key=lambda i: costs[i]), (costs, order)
     _batch_check(golden, [gss[i] for i in order], tuple(sids[i] for i in order), 1920, 1080, 1, 3)
 
 

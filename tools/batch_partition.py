@@ -37,6 +37,8 @@ ARMS = {
     "6 with 5,7,8 + 4": [[5, 7, 8, 0, 1, 3], [2, 4, 6, 9]],
     "6 lpt-ish + 4": [[5, 9, 2, 0, 1, 3], [7, 8, 4, 6]],
     "5+5 lpt light first": [[1, 3, 4, 9, 5], [0, 6, 2, 8, 7]],
+    "10 lpt": [[5, 7, 8, 9, 2, 4, 6, 3, 0, 1]],
+    "10 natural": [list(range(10))],
     "pair 1,8": [[1, 8]],
     "pair 8,1": [[8, 1]],
 }

@@ -10,6 +10,10 @@ run() {
     echo "$name rc=$rc"
     [ $rc -eq 0 ] || { tail -5 gpurun_out/${T}_${name}.log; exit $rc; }
 }
-FF="python3 -u tools/first_frame_probe.py --scenes 1 8 --reps 2"
-run ff_trace0 120 env RT_HOST_TRACE=1 RT_HF_PROXY=0 $FF --out ${T}_ff_trace0
-run ff_trace1 120 env RT_HOST_TRACE=1 RT_HF_PROXY_CELLS=3 $FF --out ${T}_ff_trace1
+B="python -u bench.py --no-cpu-baseline --no-end-to-end --no-first-frame"
+run pytest 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread
+run part 300 python3 -u tools/batch_partition.py --arms "5+5 lpt" "10 lpt" "10 natural" --rounds 6 --out ${T}_part
+run part_f2k 300 env RT_HF_FRONT_MAX=2048 python3 -u tools/batch_partition.py --arms "5+5 lpt" "10 lpt" --rounds 6 --out ${T}_part_f2k
+run part_f4k 300 env RT_HF_FRONT_MAX=4096 python3 -u tools/batch_partition.py --arms "5+5 lpt" "10 lpt" --rounds 6 --out ${T}_part_f4k
+run b10 200 $B --workload batch10 --no-moving-camera
+run bench 150 $B
