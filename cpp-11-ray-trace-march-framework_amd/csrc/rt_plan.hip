@@ -427,11 +427,12 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
         c->wh_cnt_dev = s->d_wh_cnt + (c - s->hf);
         *(volatile uint32_t *)c->wh_cnt = 0u;
         c->nblocks = uint32_t(blocks);
-        // front: 1 / hf_front_div of the blocks (an eighth), capped at hf_front_max (2048), a multiple
-        // of the XCD count so the natural section keeps its block -> XCD assignment
-        c->front = front ? std::min<uint32_t>(std::min(s->hf_front_max, kHfFrontMax),
-                                              uint32_t(blocks / std::max(s->hf_front_div, 1u)) & ~(kXcds - 1u))
-                         : 0u;
+        // front: 1 / hf_front_div of the blocks (an eighth), capped at hf_front_max (1024) -- or 1 / 128 of
+        // a larger launch's blocks -- at most kHfFrontMax, a multiple of the XCD count so the natural
+        // section keeps its block -> XCD assignment
+        const uint32_t fr = std::max(std::min(s->hf_front_max, uint32_t(blocks / std::max(s->hf_front_div, 1u))),
+                                     uint32_t(blocks / 128u));
+        c->front = front ? std::min(fr, kHfFrontMax) & ~(kXcds - 1u) : 0u;
         std::memcpy(c->key, key, sizeof(key));          // valid only now
     }
     c->used = ++s->hf_clock;

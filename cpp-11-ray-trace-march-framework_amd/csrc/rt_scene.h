@@ -97,8 +97,9 @@ struct rt_scene
     uint32_t hf_floor = 100000;     // RT_HF_FLOOR: heavy-first threshold floor, shader cycles
     uint32_t hf_min_blocks = 4096;  // RT_HF_MIN_BLOCKS: smallest whole launch taking the heavy-first order
     uint32_t hf_front_div = 8;      // RT_HF_FRONT_DIV: the front section holds 1 / this of a launch's blocks ...
-    uint32_t hf_front_max = 2048;   // RT_HF_FRONT_MAX: ... at most this many (<= kHfFrontMax; config 5 in one
-                                    // launch 2.731 vs 2.741 ms at 1024, profiles/r05q_batch10_partition_front.json)
+    uint32_t hf_front_max = 1024;   // RT_HF_FRONT_MAX: ... at most this many, or 1 / 128 of the blocks if more
+                                    // (<= kHfFrontMax: config 5's one launch of 324,000 blocks ran 2.731 / 2.734
+                                    // ms at 2048 / 4096 against 2.741 at 1024, profiles/r05q_batch10_partition_front.json)
     uint32_t hf_shift = 2;          // RT_HF_SHIFT: heavy = cost > last max >> hf_shift (very heavy: >> 1)
     uint32_t hf_proxy = 0;          // RT_HF_PROXY: a new shape's first frame is planned from k_hf_proxy's costs
                                     // (an A/B arm: killeroo's first frame 0.70 -> 0.63 ms, every other
