@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--steps", type=int, default=60)
     ap.add_argument("--out", default=None)
     ap.add_argument("--burn", type=int, default=0, help="frames of another scene object rendered first")
+    ap.add_argument("--kernel-times", action="store_true", help="also each launch's render-kernel ms (timing every launch)")
     a = ap.parse_args()
     torch.cuda.set_device(0)
     st = torch.cuda.current_stream()
@@ -41,6 +42,10 @@ def main():
         torch.cuda.synchronize()
     fs = [g.frame(1920, 1080, 4) for g in gs]
     outs = [torch.empty(1920 * 1080, dtype=torch.int32, device="cuda") for _ in gs]
+    if a.kernel_times:
+        for g in gs:
+            g.set_timing(1)
+            g.kernel_times()
     ev = []
     for i in range(a.steps):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -51,12 +56,15 @@ def main():
         ev.append((e0, e1))
     torch.cuda.synchronize()
     ms = [round(x.elapsed_time(y), 4) for x, y in ev]
+    kt = [[round(float(t), 4) for t in g.kernel_times()] for g in gs] if a.kernel_times else None
     for g in gs:
         g.close()
     if a.burn:
         b.close()
     res = {"steps": a.steps, "step_ms": ms,
            "mean_steps_5_25": round(sum(ms[5:25]) / 20, 4), "mean_steps_last20": round(sum(ms[-20:]) / 20, 4)}
+    if kt is not None:
+        res["kernel_ms"] = {"1": kt[0], "8": kt[1]}
     print(json.dumps(res))
     if a.out:
         with open(os.path.join(ROOT, "gpurun_out", a.out + ".json"), "w") as fh:
