@@ -308,11 +308,12 @@ int launch_plans(rt_scene *s, const KParams& P, uint64_t blocks, hipStream_t st)
         if (!s->plan_st)
         {
             RT_HIP(hipStreamCreateWithFlags(&s->plan_st, hipStreamNonBlocking));
-            RT_HIP(hipEventCreateWithFlags(&s->ev_plan_fork, s->ev_order_flags));
         }
         if (!c->pend_ev) RT_HIP(hipEventCreateWithFlags(&c->pend_ev, s->ev_order_flags));
-        RT_HIP(hipEventRecord(s->ev_plan_fork, st));
-        RT_HIP(hipStreamWaitEvent(s->plan_st, s->ev_plan_fork, 0));
+        // forked after the measured launch's own completion event (ev_last, the dispatch's stop
+        // event): a marker packet on the launch stream here put ~13 us between that launch and the
+        // next one (rocprofv3 kernel trace of a frame series, profiles/r05t_series_kernel_trace.csv)
+        RT_HIP(hipStreamWaitEvent(s->plan_st, s->ev_last->ev, 0));
         hipLaunchKernelGGL(k_hf_plan, grid, wg, 0, s->plan_st, P, uint32_t(blocks), s->hf_shift);
         RT_HIP(hipEventRecord(c->pend_ev, s->plan_st));
         c->pend = P.hf_ver + 1u;

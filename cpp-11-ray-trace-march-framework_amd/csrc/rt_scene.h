@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -21,6 +22,21 @@
     } while (0)
 
 namespace rtk {
+
+// A HIP event shared by the scenes whose last launch it marks: a batched launch's stop event is every
+// batched scene's "last launch" (rt_scene::ev_last), so it lives while any of them refers to it.
+struct EvHolder
+{
+    hipEvent_t ev = nullptr;
+    EvHolder() = default;
+    EvHolder(const EvHolder&) = delete;
+    EvHolder& operator=(const EvHolder&) = delete;
+    ~EvHolder()
+    {
+        if (ev) (void)hipEventDestroy(ev);
+    }
+};
+using EvRef = std::shared_ptr<EvHolder>;
 
 // Heavy-first state of one launch shape (device arrays; see KParams::hf_*)
 struct HfCtx
@@ -148,14 +164,19 @@ struct rt_scene
     float *h_smp_pinned = nullptr;
     // internal stream + timing events
     hipStream_t stream = nullptr;
-    hipEvent_t ev1 = nullptr;       // after each launch's last kernel (ordering only, no timestamp)
+    // Ordering of the scene's launches across streams and against host rewrites of its state: ev_last
+    // completes when the scene's last launch has.  The product launches carry it as the dispatch's own
+    // stop event (hipExtLaunchKernelGGL: ev_done, or the timed launch's kt1), so no marker packet sits
+    // between two frames on a stream -- a marker after each launch cost 2 % of the bench step and of
+    // config 5's (profiles/r05u_marker_ab.json); the other launch paths record ev_own after theirs.
+    rtk::EvRef ev_own, ev_done, ev_last;
     bool ev_recorded = false;
     // render-kernel-only timing: event pair around the render kernel(s) of each launch (not the
     // heavy-first planning kernels), a ring of the last kTimeRing launches (rt_kernel_times)
     rtk::HfCtx *hf_last = nullptr;       // the context of the last hf_prepare (launch_plans)
     hipStream_t plan_st = nullptr;       // k_hf_plan after a measured frame, beside the next frame
-    hipEvent_t ev_plan_fork = nullptr;
-    hipEvent_t kt0[kTimeRing] = {}, kt1[kTimeRing] = {};
+    hipEvent_t kt0[kTimeRing] = {};
+    rtk::EvRef kt1[kTimeRing];          // a timed launch's stop event (also its ev_last)
     unsigned ev_time_flags = hipEventDefault;            // kt0 / kt1 (RT_EVENT_SYSFENCE, rt_scene_create)
     unsigned ev_order_flags = hipEventDisableTiming;     // ev1, ev_fork, ev_join
     uint32_t kt_next = 0, kt_count = 0;

@@ -60,6 +60,15 @@ struct HostTrace
 };
 HostTrace g_ht;
 
+// a new shared event (rt_scene::ev_last and its sources)
+int new_event(rtk::EvRef& r, unsigned flags)
+{
+    rtk::EvRef n = std::make_shared<rtk::EvHolder>();
+    RT_HIP(hipEventCreateWithFlags(&n->ev, flags));
+    r = std::move(n);
+    return RT_OK;
+}
+
 
 thread_local std::string g_err;
 
@@ -141,7 +150,7 @@ int ensure_device(const rt_scene *s)
 // launch has finished with them (launches are asynchronous; the copies are not stream-ordered).
 int wait_scene_idle(rt_scene *s)
 {
-    if (s->ev_recorded) RT_HIP(hipEventSynchronize(s->ev1));
+    if (s->ev_recorded) RT_HIP(hipEventSynchronize(s->ev_last->ev));
     return RT_OK;
 }
 
@@ -180,7 +189,7 @@ std::vector<float> sample_table(const rt_frame *f, uint32_t spp)
 int flush_tables(rt_scene *s, hipStream_t st)
 {
     if (!s->tab_dirty) return RT_OK;
-    if (s->ev_recorded && st != s->last_stream) RT_HIP(hipStreamWaitEvent(st, s->ev1, 0));
+    if (s->ev_recorded && st != s->last_stream) RT_HIP(hipStreamWaitEvent(st, s->ev_last->ev, 0));
     const uint32_t n = (s->tab.W + s->tab.H) * s->tab.spp;
     hipLaunchKernelGGL(frame_tables_kernel(), dim3((n + kWG - 1) / kWG), dim3(kWG), 0, st, s->d_ndc, s->d_smp, s->tab);
     RT_HIP(hipGetLastError());
@@ -410,7 +419,7 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
     // The per-camera records (frefs) are scene state: a launch on another stream than the last
     // one waits for it, so frames of one scene never overlap on the device.
     // (order_streams false: the caller orders its streams itself, rt_render_frame_host_tiled)
-    if (order_streams && s->ev_recorded && st != s->last_stream) RT_HIP(hipStreamWaitEvent(st, s->ev1, 0));
+    if (order_streams && s->ev_recorded && st != s->last_stream) RT_HIP(hipStreamWaitEvent(st, s->ev_last->ev, 0));
     if (int rc = flush_tables(s, st)) return rc;
     g_ht.mark("tables");
     s->last_stream = st;
@@ -444,16 +453,16 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
     s->launches++;
     const uint32_t kslot = s->kt_next;
     hipEvent_t kt0 = nullptr, kt1 = nullptr;        // null stand for "not timed"
-    if (timed && !s->kt0[kslot])
-    {
-        RT_HIP(hipEventCreateWithFlags(&s->kt0[kslot], s->ev_time_flags));
-        RT_HIP(hipEventCreateWithFlags(&s->kt1[kslot], s->ev_time_flags));
-    }
+    if (timed && !s->kt0[kslot]) RT_HIP(hipEventCreateWithFlags(&s->kt0[kslot], s->ev_time_flags));
+    // a ring slot's stop event still marking another scene's last launch is left to it
+    if (timed && (!s->kt1[kslot] || s->kt1[kslot].use_count() > 1))
+        if (int rc = new_event(s->kt1[kslot], s->ev_time_flags)) return rc;
     if (timed)
     {
         kt0 = s->kt0[kslot];
-        kt1 = s->kt1[kslot];
+        kt1 = s->kt1[kslot]->ev;
     }
+    bool stop_done = false;             // the launch carried its own stop event (ev_last set)
     auto mark = [&](hipEvent_t e) { return e ? hipEventRecord(e, st) : hipSuccess; };
     if (var & kVarWaveClock)
     {
@@ -545,9 +554,20 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
             RT_HIP(hipEventRecord(s->ev_join, s->side));
             RT_HIP(hipStreamWaitEvent(st, s->ev_join, 0));
             RT_HIP(mark(kt1));
+            RT_HIP(hipEventRecord(s->ev_own->ev, st));     // (launch_plans forks after ev_last)
+            s->ev_last = s->ev_own;
+            stop_done = true;
+            s->ev_recorded = true;
         }
-        else    // a timed launch carries its events in the dispatch itself (no marker packets)
-            hipExtLaunchKernelGGL(lfn, dim3(lgrid), dim3(lwg), 0, st, kt0, kt1, 0u, P);
+        else
+        {
+            // the dispatch carries its own events (no marker packets): the timed launch's pair, or
+            // the scene's completion event alone
+            s->ev_last = timed ? s->kt1[kslot] : s->ev_done;
+            hipExtLaunchKernelGGL(lfn, dim3(lgrid), dim3(lwg), 0, st, kt0, s->ev_last->ev, 0u, P);
+            stop_done = true;
+            s->ev_recorded = true;
+        }
         if ((P.hf_front || P.wh_on) && P.hf_measure)
             if (int rc = launch_plans(s, P, blocks, st)) return rc;
     }
@@ -563,8 +583,12 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
     }
     RT_HIP(hipGetLastError());
     g_ht.mark("launched");
-    RT_HIP(hipEventRecord(s->ev1, st));
-    s->ev_recorded = true;
+    if (!stop_done)
+    {
+        RT_HIP(hipEventRecord(s->ev_own->ev, st));
+        s->ev_last = s->ev_own;
+        s->ev_recorded = true;
+    }
     if (timed)
     {
         s->kt_last = kslot;
@@ -636,7 +660,7 @@ int launch_batch(rt_scene *const *S, const rt_frame *F, uint32_t n, KParams *P, 
         bool first = true;
         for (uint32_t j = 0; j < i; j++) first = first && S[j] != s;
         if (!first) continue;
-        if (s->ev_recorded && st != s->last_stream) RT_HIP(hipStreamWaitEvent(st, s->ev1, 0));
+        if (s->ev_recorded && st != s->last_stream) RT_HIP(hipStreamWaitEvent(st, s->ev_last->ev, 0));
         if (int rc = flush_tables(s, st)) return rc;
         s->last_stream = st;
         if (int rc = ensure_origin_terms(s, P[i], st)) return rc;
@@ -697,23 +721,23 @@ int launch_batch(rt_scene *const *S, const rt_frame *F, uint32_t n, KParams *P, 
     const bool timed = cap == hipStreamCaptureStatusNone && s0->time_every && s0->launches % s0->time_every == 0u;
     s0->launches++;
     const uint32_t kslot = s0->kt_next;
-    if (timed && !s0->kt0[kslot])
-    {
-        RT_HIP(hipEventCreateWithFlags(&s0->kt0[kslot], s0->ev_time_flags));
-        RT_HIP(hipEventCreateWithFlags(&s0->kt1[kslot], s0->ev_time_flags));
-    }
+    if (timed && !s0->kt0[kslot]) RT_HIP(hipEventCreateWithFlags(&s0->kt0[kslot], s0->ev_time_flags));
+    if (timed && (!s0->kt1[kslot] || s0->kt1[kslot].use_count() > 1))
+        if (int rc = new_event(s0->kt1[kslot], s0->ev_time_flags)) return rc;
+    // the dispatch's stop event marks every batched scene's last launch (no marker per scene: ten of
+    // them cost config 5's step 50 us, profiles/r05u_marker_ab.json)
+    const rtk::EvRef stop = timed ? s0->kt1[kslot] : s0->ev_done;
     // a timed launch carries its start / stop events in the dispatch itself: separate event records
     // around it cost a measured 3-4 % of that frame (profiles/r05j_frame_series_*.json, steps 8, 24, ...)
-    hipExtLaunchKernelGGL(fn, dim3(grid), dim3(bwg), 0, st, timed ? s0->kt0[kslot] : nullptr,
-                          timed ? s0->kt1[kslot] : nullptr, 0u, KB);
+    hipExtLaunchKernelGGL(fn, dim3(grid), dim3(bwg), 0, st, timed ? s0->kt0[kslot] : nullptr, stop->ev, 0u, KB);
+    for (uint32_t i = 0; i < n; i++)
+    {
+        S[i]->ev_last = stop;
+        S[i]->ev_recorded = true;
+    }
     if ((P[0].hf_front || P[0].wh_on) && P[0].hf_measure)
         if (int rc = launch_plans(s0, KB.p[0], blocks, st)) return rc;
     RT_HIP(hipGetLastError());
-    for (uint32_t i = 0; i < n; i++)
-    {
-        RT_HIP(hipEventRecord(S[i]->ev1, st));
-        S[i]->ev_recorded = true;
-    }
     if (timed)
     {
         s0->kt_last = kslot;
@@ -1138,13 +1162,14 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
                                         tridist.size() + distblk.size()) +
                       sizeof(uint32_t) * (cellw.size() + cellwo.size() + cellwb.size());
     RT_HIP(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
-    RT_HIP(hipEventCreateWithFlags(&s->ev1, s->ev_order_flags));
+    if (int rc = new_event(s->ev_own, s->ev_order_flags)) return rc;
+    if (int rc = new_event(s->ev_done, s->ev_time_flags)) return rc;     // a dispatch's stop event
+    s->ev_last = s->ev_own;
     // the plan stream (launch_plans) and the first timed launch's events: created here, not by a
     // frame (a stream's creation took ~0.33 ms of the second frame's call, profiles/r05p_host_trace.log)
     RT_HIP(hipStreamCreateWithFlags(&s->plan_st, hipStreamNonBlocking));
-    RT_HIP(hipEventCreateWithFlags(&s->ev_plan_fork, s->ev_order_flags));
     RT_HIP(hipEventCreateWithFlags(&s->kt0[0], s->ev_time_flags));
-    RT_HIP(hipEventCreateWithFlags(&s->kt1[0], s->ev_time_flags));
+    if (int rc = new_event(s->kt1[0], s->ev_time_flags)) return rc;
     // the heavy-first contexts' host-mapped counters, and the frame tables at a 4K x 16 spp capacity:
     // allocated here so a new launch shape's first frame waits for no allocation call
     RT_HIP(hipHostMalloc(&s->h_wh_cnt, sizeof(uint32_t) * kHfCtxs, hipHostMallocMapped | hipHostMallocCoherent));
@@ -1171,7 +1196,7 @@ int rt_scene_destroy(rt_scene *s)
         std::lock_guard<std::mutex> lk(s->mtx);
         (void)hipSetDevice(s->device);
         if (s->stream) (void)hipStreamSynchronize(s->stream);
-        if (s->last_stream && s->ev_recorded) (void)hipEventSynchronize(s->ev1);
+        if (s->last_stream && s->ev_recorded) (void)hipEventSynchronize(s->ev_last->ev);
         if (s->plan_st) (void)hipStreamSynchronize(s->plan_st);
         if (s->side) (void)hipStreamSynchronize(s->side);
         (void)hipFree(s->d_off);
@@ -1196,7 +1221,6 @@ int rt_scene_destroy(rt_scene *s)
         if (s->h_wh_cnt) (void)hipHostFree(s->h_wh_cnt);
         if (s->side) (void)hipStreamDestroy(s->side);
         if (s->plan_st) (void)hipStreamDestroy(s->plan_st);
-        if (s->ev_plan_fork) (void)hipEventDestroy(s->ev_plan_fork);
         if (s->ev_fork) (void)hipEventDestroy(s->ev_fork);
         if (s->ev_join) (void)hipEventDestroy(s->ev_join);
         (void)hipFree(s->d_smp);
@@ -1204,10 +1228,12 @@ int rt_scene_destroy(rt_scene *s)
         (void)hipFree(s->d_frame);
         if (s->h_smp_pinned) (void)hipHostFree(s->h_smp_pinned);
         if (s->h_frame) (void)hipHostFree(s->h_frame);
-        if (s->ev1) (void)hipEventDestroy(s->ev1);
+        s->ev_own.reset();             // shared events: destroyed with their last reference
+        s->ev_done.reset();
+        s->ev_last.reset();
         for (hipEvent_t e : s->band_ev) if (e) (void)hipEventDestroy(e);
         for (hipEvent_t e : s->kt0) if (e) (void)hipEventDestroy(e);
-        for (hipEvent_t e : s->kt1) if (e) (void)hipEventDestroy(e);
+        for (rtk::EvRef& e : s->kt1) e.reset();
         for (hipEvent_t e : s->tile_ev) if (e) (void)hipEventDestroy(e);
         if (s->stream) (void)hipStreamDestroy(s->stream);
         if (s->stream2) (void)hipStreamDestroy(s->stream2);
@@ -1423,7 +1449,8 @@ int rt_render_records_device(rt_scene *const *scenes, const rt_frame *frames, ui
         RT_HIP(hipGetLastError());
         // the fixup reads the scene's tables (camera-space x / y, CSR offsets): a later call that
         // rewrites them (prepare_samples -> wait_scene_idle) must wait for it, as for a render launch
-        RT_HIP(hipEventRecord(s->ev1, static_cast<hipStream_t>(hip_stream)));
+        RT_HIP(hipEventRecord(s->ev_own->ev, static_cast<hipStream_t>(hip_stream)));
+        s->ev_last = s->ev_own;
         s->ev_recorded = true;
         s->last_stream = static_cast<hipStream_t>(hip_stream);
     }
@@ -1457,8 +1484,8 @@ int rt_last_kernel_ms(rt_scene *s, float *ms)
     if (!s || !ms) return fail(RT_E_INVALID, "NULL argument");
     std::lock_guard<std::mutex> lk(s->mtx);
     if (s->kt_last >= kTimeRing) return fail(RT_E_INVALID, "no timed kernel recorded yet");
-    RT_HIP(hipEventSynchronize(s->kt1[s->kt_last]));
-    RT_HIP(hipEventElapsedTime(ms, s->kt0[s->kt_last], s->kt1[s->kt_last]));
+    RT_HIP(hipEventSynchronize(s->kt1[s->kt_last]->ev));
+    RT_HIP(hipEventElapsedTime(ms, s->kt0[s->kt_last], s->kt1[s->kt_last]->ev));
     return RT_OK;
 }
 
@@ -1484,8 +1511,8 @@ int rt_kernel_times(rt_scene *s, float *ms, uint32_t max_n, uint32_t *n)
         // a pair that cannot be read (a launch that failed between its two records) is skipped
         const uint32_t slot = (next + kTimeRing - cnt + i) % kTimeRing;
         float v = 0.0f;
-        if (hipEventSynchronize(s->kt1[slot]) == hipSuccess &&
-            hipEventElapsedTime(&v, s->kt0[slot], s->kt1[slot]) == hipSuccess && v >= 0.0f)
+        if (hipEventSynchronize(s->kt1[slot]->ev) == hipSuccess &&
+            hipEventElapsedTime(&v, s->kt0[slot], s->kt1[slot]->ev) == hipSuccess && v >= 0.0f)
             ms[got++] = v;
         else
             (void)hipGetLastError();
@@ -1635,7 +1662,7 @@ int rt_render_frame_host_tiled(rt_scene *s, const rt_frame *f, uint32_t *h_tiles
     auto row_y = [&](uint32_t r) { return r >= tiles_y ? H : r * th; };
     hipStream_t st[2] = { s->stream, s->stream2 };
     // both streams after everything earlier on this scene (the scene's tables and records are shared)
-    if (s->ev_recorded) RT_HIP(hipStreamWaitEvent(st[0], s->ev1, 0));
+    if (s->ev_recorded) RT_HIP(hipStreamWaitEvent(st[0], s->ev_last->ev, 0));
     KParams P0;
     frame_params(s, f, P0);
     if (use_lanes(f, spp) && P0.isect == RT_ISECT_GRID && P0.tri_test == RT_TRI_MOLLER_TRUMBORE &&
@@ -1676,7 +1703,8 @@ int rt_render_frame_host_tiled(rt_scene *s, const rt_frame *f, uint32_t *h_tiles
     // the frame is done when both streams are: join on the first one, whose event ev1 marks it
     RT_HIP(hipEventRecord(s->ev_t_join, st[1]));
     RT_HIP(hipStreamWaitEvent(st[0], s->ev_t_join, 0));
-    RT_HIP(hipEventRecord(s->ev1, st[0]));
+    RT_HIP(hipEventRecord(s->ev_own->ev, st[0]));
+    s->ev_last = s->ev_own;
     s->ev_recorded = true;
     s->last_stream = st[0];
     // bands land per tile row but not in row order across the two streams: rt_frame_host_wait(y1)
