@@ -686,7 +686,7 @@ def dist_report(work, world, rank, dist, steps, elapsed, reps=8):
             "step_minus_slowest_render_ms": round(step - max(render), 4)}
 
 
-def run_steps(work, world, rank, steps, warmup, dist=None, graph=False):
+def run_steps(work, world, rank, steps, warmup, dist=None, graph=False, clock_warmup=0.2):
     """W untimed warm-up steps, then K timed steps between barrier+sync on both sides; returns
     the max-over-ranks wall time.  A step renders every scene (this rank's tiles when N > 1) and
     gathers each scene's shards to rank 0 (one RCCL gather: every peer sends its slice on its
@@ -746,6 +746,18 @@ def run_steps(work, world, rank, steps, warmup, dist=None, graph=False):
 
     ctx = work.stream_ctx() if hasattr(work, "stream_ctx") else contextlib.nullcontext()
     with ctx:
+        # clock warm-up: from an idle GPU the clocks ramp over the first ~30 steps (a batched pair step
+        # 0.61 -> 0.54 ms, profiles/r05w_batched_series_cold.json), so the step's renders run untimed
+        # for `clock_warmup` seconds first -- renders only, so no rank waits on another's collectives
+        t_end = time.perf_counter() + clock_warmup
+        n = 0
+        while time.perf_counter() < t_end:
+            work.render_all(n % nsets)
+            n += 1
+            if n % 8 == 0:
+                work.sync()
+        work.sync()
+        work.clock_warmup = {"s": clock_warmup, "renders": n}
         for _ in range(warmup):
             step()
         finish()
@@ -789,6 +801,8 @@ def main():
     ap.add_argument("--no-end-to-end", action="store_true")
     ap.add_argument("--no-moving-camera", action="store_true")
     ap.add_argument("--no-first-frame", action="store_true")
+    ap.add_argument("--clock-warmup", type=float, default=0.2,
+                    help="seconds of untimed renders before the W warm-up steps (the GPU clocks ramp from idle)")
     ap.add_argument("--graph", action="store_true",
                     help="replay the step's render launch(es) from a hipGraph captured after the warm-up")
     ap.add_argument("--batch", choices=["auto", "on", "off"], default="auto",
@@ -845,7 +859,7 @@ def main():
         if not args.graph and not args.no_moving_camera:
             extra["moving_camera"] = moving_camera(work, args.steps, min(args.warmup, 20), None)
     elapsed = run_steps(work, world, rank, args.steps, args.warmup, dist if world > 1 else None,
-                        graph=args.graph)
+                        graph=args.graph, clock_warmup=args.clock_warmup)
     kernel_ms = work.kernel_ms(args.steps)
     step_ms = work.span_ms(args.steps)
     drep = dist_report(work, world, rank, dist, args.steps, elapsed) if world > 1 else None
@@ -876,6 +890,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "clock_warmup": getattr(work, "clock_warmup", None),
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "strong",

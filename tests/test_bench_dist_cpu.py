@@ -61,7 +61,7 @@ def _worker(rank, world, port, q):
         bench.W, bench.H, bench.SPP = W, H, SPP
         rtm = load_package()
         work = CpuWorkload(rtm, world, rank, bench.SCENES)
-        elapsed = bench.run_steps(work, world, rank, steps=3, warmup=1, dist=dist)
+        elapsed = bench.run_steps(work, world, rank, steps=3, warmup=1, dist=dist, clock_warmup=0.0)
         report = bench.dist_report(work, world, rank, dist, 3, elapsed, reps=3)
         if rank == 0:
             # the drained pipeline holds the last (4th) step's frames; steps alternate buffer sets

@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--burn", type=int, default=0, help="frames of another scene object rendered first")
     ap.add_argument("--kernel-times", action="store_true", help="also each launch's render-kernel ms (timing every launch)")
+    ap.add_argument("--batch", action="store_true", help="both frames of a step in one batched launch (the bench's N = 1 step)")
+    ap.add_argument("--time-every", type=int, default=0, help="rt_scene_set_timing before the series (0: the library default)")
     a = ap.parse_args()
     torch.cuda.set_device(0)
     st = torch.cuda.current_stream()
@@ -46,12 +48,19 @@ def main():
         for g in gs:
             g.set_timing(1)
             g.kernel_times()
+    elif a.time_every:
+        for g in gs:
+            g.set_timing(a.time_every)
     ev = []
     for i in range(a.steps):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(st)
-        for g, f, o in zip(gs, fs, outs):
-            g.render_frame_device(f, o.data_ptr(), st.cuda_stream)
+        if a.batch:
+            rtm.render_batch_device([gs[1], gs[0]], [fs[1], fs[0]], [outs[1].data_ptr(), outs[0].data_ptr()],
+                                    stream=st.cuda_stream)
+        else:
+            for g, f, o in zip(gs, fs, outs):
+                g.render_frame_device(f, o.data_ptr(), st.cuda_stream)
         e1.record(st)
         ev.append((e0, e1))
     torch.cuda.synchronize()

@@ -11,10 +11,11 @@ run() {
     [ $rc -eq 0 ] || { tail -5 gpurun_out/${T}_${name}.log; exit $rc; }
 }
 B="python -u bench.py --no-cpu-baseline --no-end-to-end --no-first-frame --no-moving-camera"
-run pytest 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread
-run b 100 $B
+run serb 100 python3 -u tools/frame_series.py --steps 40 --batch --time-every 8 --out ${T}_serb
+run serb2 100 python3 -u tools/frame_series.py --steps 40 --batch --time-every 8 --out ${T}_serb2
 run b2 100 $B --steps 20 --warmup 5
-run c 150 $B --workload batch10
-run ser 100 python3 -u tools/frame_series.py --steps 60 --burn 200 --out ${T}_ser
-run ser2 100 python3 -u tools/frame_series.py --steps 60 --burn 200 --out ${T}_ser2
-run sweep 300 python -u tools/tunable_sweep.py --env RT_HF_FLOOR --values 100000 --ns 1 2 4 8 --rounds 2 --out ${T}_sweep
+run b3 100 $B --steps 20 --warmup 5
+cd /tmp
+timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d $R/gpurun_out/${T}_btrace -o run -- \
+    python3 $R/bench.py --no-cpu-baseline --no-end-to-end --no-first-frame --no-moving-camera --steps 20 --warmup 5 > $R/gpurun_out/${T}_btrace.log 2>&1
+echo "btrace rc=$?"
