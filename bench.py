@@ -433,9 +433,14 @@ class GpuWorkload:
     per launch, config 5 as 5 + 5), so one frame's tail overlaps the others' work; else one launch
     per frame."""
 
-    def __init__(self, rtm, torch, world, rank, local, kernel, batch=True):
+    def __init__(self, rtm, torch, world, rank, local, kernel, batch=True, overlap=False):
         self.rtm, self.torch, self.world, self.rank = rtm, torch, world, rank
         self.batch = batch
+        # overlap (batched launches, RT_KERNEL_FLAG_OVERLAP): consecutive steps alternate two launch
+        # streams and two buffer sets, so one step's render tail runs under the next step's start
+        self.overlap = overlap and batch
+        if self.overlap:
+            kernel |= rtm.RT_KERNEL_FLAG_OVERLAP
         self.graphs = None              # per buffer set: hipGraph of the step's render launch(es) (--graph)
         self.samples = {}               # timed launches per scene in the timed region
         self.gevents = {}
@@ -445,14 +450,16 @@ class GpuWorkload:
             gs = rtm.GpuScene(hs, local)
             self.scenes.append((sid, hs, gs, gs.frame(W, H, SPP, kernel=kernel)))
         self.stream = torch.cuda.Stream()       # every launch, capture and collective of a step
+        self.streams = [self.stream] + ([torch.cuda.Stream()] if self.overlap else [])
         # rank 0's assembly (K3 un-permute of the gathered shards) runs on its own stream, beside the
         # next step's render: K3 streams the frames through HBM while the render kernel is VALU-bound
         self.asm_stream = torch.cuda.Stream() if world > 1 and rank == 0 else None
         n = W * H if world == 1 else rtm.shard_elems(W, H, world)
         # bufs[set][scene]: two sets for N > 1, so one step's shards can be gathered while the next
-        # step renders into the other set (run_steps); one set at N = 1 (nothing is gathered)
+        # step renders into the other set (run_steps), and with overlap (step i renders set i % 2 on
+        # stream i % 2); else one set at N = 1 (nothing is gathered)
         self.bufs = [[torch.empty(n, dtype=torch.int32, device="cuda") for _ in SCENES]
-                     for _ in range(2 if world > 1 else 1)]
+                     for _ in range(2 if world > 1 or self.overlap else 1)]
         self.frames = [torch.empty(W * H, dtype=torch.int32, device="cuda") for _ in SCENES]
         # scenes whose kernel-time ring holds a launch's time: every scene, or the first scene of
         # every batch launch
@@ -468,13 +475,22 @@ class GpuWorkload:
             self.order = rtm.batch_order(self.costs)
         self.timed = [self.order[i] for i, _ in rtm.batch_chunks(len(SCENES))] if batch else list(range(len(SCENES)))
 
-    def stream_ctx(self):
-        return self.torch.cuda.stream(self.stream)
+    def stream_ctx(self, p=0):
+        return self.torch.cuda.stream(self.streams[p % len(self.streams)])
 
-    def mark(self):
-        """A timing event recorded on the launch stream (every render launch of a step runs there)."""
+    def mark(self, end=False):
+        """A timing event on the launch stream; with overlap the second stream joins it: its later
+        launches wait for the start mark, the end mark waits for its earlier ones."""
         e = self.torch.cuda.Event(enable_timing=True)
+        if end:
+            for s in self.streams[1:]:
+                j = self.torch.cuda.Event()
+                j.record(s)
+                self.stream.wait_event(j)
         e.record(self.stream)
+        if not end:
+            for s in self.streams[1:]:
+                s.wait_event(e)
         return e
 
     def span_ms(self, steps):
@@ -498,7 +514,7 @@ class GpuWorkload:
         self._launch(p)
 
     def _launch(self, p):
-        st = self.stream.cuda_stream
+        st = self.streams[p % len(self.streams)].cuda_stream
         bufs = self.bufs[p]
         if self.batch:
             o = self.order
@@ -731,18 +747,24 @@ def run_steps(work, world, rank, steps, warmup, dist=None, graph=False, clock_wa
                     work.unshard(i, g)
         pending.clear()
 
+    streams = getattr(work, "streams", None)
+
     def step():
         p = it[0] % nsets
         it[0] += 1
-        work.render_all(p)
-        if world > 1:
-            if asm_done[p] is not None:
-                # this set's gather buffers are refilled only after the K3s that read them
-                work.stream.wait_event(asm_done[p])
-            issued = [collect(p, i) for i in range(len(SCENES))]
-            finish()
-            pending.extend(issued)
-            pending_set[0] = p
+        # with overlap, set p renders (and gathers) on stream p: the step's work, its collectives and
+        # the waits below are ordered on that stream, beside the other stream's step
+        sctx = work.stream_ctx(p) if streams and len(streams) > 1 else contextlib.nullcontext()
+        with sctx:
+            work.render_all(p)
+            if world > 1:
+                if asm_done[p] is not None:
+                    # this set's gather buffers are refilled only after the K3s that read them
+                    (streams[p % len(streams)] if streams else work.stream).wait_event(asm_done[p])
+                issued = [collect(p, i) for i in range(len(SCENES))]
+                finish()
+                pending.extend(issued)
+                pending_set[0] = p
 
     ctx = work.stream_ctx() if hasattr(work, "stream_ctx") else contextlib.nullcontext()
     with ctx:
@@ -773,7 +795,7 @@ def run_steps(work, world, rank, steps, warmup, dist=None, graph=False, clock_wa
         span0 = work.mark()            # HIP events on the launch stream around ALL the timed launches
         for _ in range(steps):
             step()
-        span1 = work.mark()
+        span1 = work.mark(end=True) if streams else work.mark()
         finish()                       # the last step's frames are assembled inside the timed region
     work.sync()
     work.span = (span0, span1)
@@ -801,6 +823,9 @@ def main():
     ap.add_argument("--no-end-to-end", action="store_true")
     ap.add_argument("--no-moving-camera", action="store_true")
     ap.add_argument("--no-first-frame", action="store_true")
+    ap.add_argument("--overlap", choices=["on", "off"], default="on",
+                    help="consecutive steps' batched launches on two streams with RT_KERNEL_FLAG_OVERLAP (one "
+                         "step's tail under the next step's start); off: one stream")
     ap.add_argument("--clock-warmup", type=float, default=0.2,
                     help="seconds of untimed renders before the W warm-up steps (the GPU clocks ramp from idle)")
     ap.add_argument("--graph", action="store_true",
@@ -841,7 +866,8 @@ def main():
 
     rtm = load_package()
     batch = args.batch == "on" or (args.batch == "auto" and len(SCENES) >= 2)
-    work = GpuWorkload(rtm, torch, world, rank, local, args.kernel, batch=batch)
+    work = GpuWorkload(rtm, torch, world, rank, local, args.kernel, batch=batch,
+                       overlap=args.overlap == "on" and not args.graph)
     # The per-sample counts behind the algorithmic bytes (the debug records kernel over
     # whole frames, reduced on the host) first; then the supplementary legs that keep the GPU busy
     # (the drop-in end to end, the orbiting camera) run BEFORE the warm-up, so the timed steps follow
@@ -903,7 +929,9 @@ def main():
                        "parallelism": f"tile-shard x{world}" + (" + RCCL gather to rank 0" if world > 1 else ""),
                        "launch": ("hipGraph of " if args.graph else "") +
                                  (f"the step's frames batched as {[c for _, c in rtm.batch_chunks(len(SCENES))]} "
-                                  "frames per launch (rt_render_batch_device)" if work.batch else "one launch per frame"),
+                                  "frames per launch (rt_render_batch_device)" if work.batch else "one launch per frame") +
+                                 ("; consecutive steps on two streams, RT_KERNEL_FLAG_OVERLAP (a step's tail under the "
+                                  "next step's start; measured frames ordered)" if work.overlap else ""),
                        "frame_order": [SCENES[i] for i in work.order] if work.batch else list(SCENES),
                        "frame_costs_ms": ({str(SCENES[i]): round(c, 4) for i, c in enumerate(work.costs)}
                                           if work.costs else None),

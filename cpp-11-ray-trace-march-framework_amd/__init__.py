@@ -45,6 +45,7 @@ RT_KERNEL_KIND_MASK = 0x07
 RT_KERNEL_FLAG_WIDE_HEAVY = 0x200
 RT_KERNEL_FLAG_EXHAUSTIVE = 0x8000
 RT_KERNEL_FLAG_WAVE_CLOCK = 0x400000
+RT_KERNEL_FLAG_OVERLAP = 0x800000
 RT_KERNEL_BUDGET_SHIFT = 24              # COMPACT: idle lanes before a refill (1..64)
 RT_KERNEL_BUDGET_MASK = 0x7F000000
 RT_KERNEL_COMPACT_REFILL_SHIFT = RT_KERNEL_BUDGET_SHIFT

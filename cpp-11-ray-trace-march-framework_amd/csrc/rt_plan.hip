@@ -370,17 +370,39 @@ uint64_t cam_signature(const KParams& P, uint64_t h)
 // Heavy-first state for this launch shape (AUTO): fills P.hf_*.  A new shape takes the least
 // recently used context and clears it on the launch stream (no host synchronisation).
 // batch: 0 for a single-frame launch, else an identity of the batch (its scenes and frame count).
+// The key of a launch shape's heavy-first context
+void hf_key(const KParams& P, uint64_t blocks, int var, uint64_t batch, uint64_t key[5])
+{
+    key[0] = (blocks << 16) | (uint64_t(P.spp) << 1) | 1u;
+    key[1] = (uint64_t(P.rx0) << 32) | P.ry0;
+    key[2] = (uint64_t(P.rw) << 32) | P.rh;
+    key[3] = (uint64_t(P.rank) << 40) | (uint64_t(P.nranks) << 20) | uint64_t(uint32_t(var) >> 12);
+    key[4] = batch;
+}
+
+bool measures(const rt_scene *s, const HfCtx& c, uint64_t cam_sig)
+{
+    return c.frames < 2u || c.frames % kHfPeriod == 0u || (s->hf_follow && cam_sig != c.cam);
+}
+
+HfPeek hf_peek(const rt_scene *s, const KParams& P, uint64_t blocks, int var, uint64_t batch, uint64_t cam_sig)
+{
+    uint64_t key[5];
+    hf_key(P, blocks, var, batch, key);
+    for (const HfCtx& h : s->hf)
+        if (std::memcmp(h.key, key, sizeof(key)) == 0) return HfPeek{ true, measures(s, h, cam_sig) };
+    return HfPeek{ false, true };
+}
+
 int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hipStream_t st, uint64_t batch,
                uint64_t cam_sig)
 {
     if (!batch) cam_sig = cam_signature(P);
-    const uint64_t key[5] = { (blocks << 16) | (uint64_t(P.spp) << 1) | 1u,
-                              (uint64_t(P.rx0) << 32) | P.ry0, (uint64_t(P.rw) << 32) | P.rh,
-                              (uint64_t(P.rank) << 40) | (uint64_t(P.nranks) << 20) | uint64_t(uint32_t(var) >> 12),
-                              batch };
+    uint64_t key[5];
+    hf_key(P, blocks, var, batch, key);
     HfCtx *c = nullptr;
     for (HfCtx& h : s->hf)
-        if (std::memcmp(h.key, key, sizeof(key)) == 0) c = &h;
+        if (std::memcmp(h.key, key, sizeof(h.key)) == 0) c = &h;
     if (!c)
     {
         c = &s->hf[0];
@@ -434,7 +456,7 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
         const uint32_t fr = std::max(std::min(s->hf_front_max, uint32_t(blocks / std::max(s->hf_front_div, 1u))),
                                      uint32_t(blocks / 128u));
         c->front = front ? std::min(fr, kHfFrontMax) & ~(kXcds - 1u) : 0u;
-        std::memcpy(c->key, key, sizeof(key));          // valid only now
+        std::memcpy(c->key, key, sizeof(c->key));       // valid only now
     }
     c->used = ++s->hf_clock;
     s->hf_last = c;
@@ -443,7 +465,7 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
     // ... and every frame whose camera differs from the previous frame's: a moving camera's heavy
     // blocks move with the view, so the plan comes from the newest view (one frame old) instead of
     // one up to kHfPeriod frames old
-    P.hf_measure = c->frames < 2u || c->frames % kHfPeriod == 0u || (s->hf_follow && cam_sig != c->cam);
+    P.hf_measure = measures(s, *c, cam_sig) ? 1u : 0u;
     if (c->pend)
     {
         // a plan on the plan stream (launch_plans): adopted by the second frame after it and by a

@@ -166,10 +166,12 @@ struct rt_scene
     hipStream_t stream = nullptr;
     // Ordering of the scene's launches across streams and against host rewrites of its state: ev_last
     // completes when the scene's last launch has.  The product launches carry it as the dispatch's own
-    // stop event (hipExtLaunchKernelGGL: ev_done, or the timed launch's kt1), so no marker packet sits
+    // stop event (hipExtLaunchKernelGGL: a free one of ev_done[], or the timed launch's kt1), so no marker packet sits
     // between two frames on a stream -- a marker after each launch cost 2 % of the bench step and of
     // config 5's (profiles/r05u_marker_ab.json); the other launch paths record ev_own after theirs.
-    rtk::EvRef ev_own, ev_done, ev_last;
+    rtk::EvRef ev_own, ev_last;
+    rtk::EvRef ev_done[4];              // stop events, each re-recorded only when no scene refers to it
+    rtk::EvRef ev_prev;                 // RT_KERNEL_FLAG_OVERLAP: the launch ev_last's launch overlaps (else null)
     bool ev_recorded = false;
     // render-kernel-only timing: event pair around the render kernel(s) of each launch (not the
     // heavy-first planning kernels), a ring of the last kTimeRing launches (rt_kernel_times)
@@ -210,6 +212,10 @@ namespace rtk {
 // batch: 0 for a single-frame launch, else an identity of the batch (its scenes and frame count)
 int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hipStream_t st, uint64_t batch = 0,
                uint64_t cam_sig = 0);
+// What hf_prepare would find for this launch, without side effects: whether the shape's context exists
+// (no allocation, no eviction) and whether this frame would be measured (RT_KERNEL_FLAG_OVERLAP)
+struct HfPeek { bool found, measure; };
+HfPeek hf_peek(const rt_scene *s, const KParams& P, uint64_t blocks, int var, uint64_t batch, uint64_t cam_sig);
 // The plan kernel(s) after a measured frame on its stream (k_hf_plan; two passes after a shape's first
 // measured frame, see launch_plans)
 int launch_plans(rt_scene *s, const KParams& P, uint64_t blocks, hipStream_t st);

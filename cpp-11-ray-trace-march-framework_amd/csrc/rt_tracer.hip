@@ -69,6 +69,23 @@ int new_event(rtk::EvRef& r, unsigned flags)
     return RT_OK;
 }
 
+// A stop event for the scene's next untimed launch: one of ev_done[] that no scene still holds as its
+// ev_last / ev_prev (re-recording a held one would make that scene wait for this launch instead of
+// its own), else a new one in a slot
+int free_done_event(rt_scene *s, rtk::EvRef& out)
+{
+    for (rtk::EvRef& e : s->ev_done)
+        if (e && e.use_count() == 1)
+        {
+            out = e;
+            return RT_OK;
+        }
+    rtk::EvRef& slot = s->ev_done[0];
+    if (int rc = new_event(slot, s->ev_time_flags)) return rc;
+    out = slot;
+    return RT_OK;
+}
+
 
 thread_local std::string g_err;
 
@@ -151,6 +168,20 @@ int ensure_device(const rt_scene *s)
 int wait_scene_idle(rt_scene *s)
 {
     if (s->ev_recorded) RT_HIP(hipEventSynchronize(s->ev_last->ev));
+    if (s->ev_prev) RT_HIP(hipEventSynchronize(s->ev_prev->ev));
+    s->ev_prev.reset();
+    return RT_OK;
+}
+
+// Orders stream st after every launch of scene s that may still run: the last one (ev_last, implicit
+// on its own stream) and, when that one overlapped its predecessor (RT_KERNEL_FLAG_OVERLAP), the
+// predecessor (ev_prev).  The caller's next launch on st then follows them all.
+int order_all(rt_scene *s, hipStream_t st)
+{
+    if (!s->ev_recorded) return RT_OK;
+    if (st != s->last_stream) RT_HIP(hipStreamWaitEvent(st, s->ev_last->ev, 0));
+    if (s->ev_prev) RT_HIP(hipStreamWaitEvent(st, s->ev_prev->ev, 0));
+    s->ev_prev.reset();
     return RT_OK;
 }
 
@@ -189,7 +220,7 @@ std::vector<float> sample_table(const rt_frame *f, uint32_t spp)
 int flush_tables(rt_scene *s, hipStream_t st)
 {
     if (!s->tab_dirty) return RT_OK;
-    if (s->ev_recorded && st != s->last_stream) RT_HIP(hipStreamWaitEvent(st, s->ev_last->ev, 0));
+    if (int rc = order_all(s, st)) return rc;
     const uint32_t n = (s->tab.W + s->tab.H) * s->tab.spp;
     hipLaunchKernelGGL(frame_tables_kernel(), dim3((n + kWG - 1) / kWG), dim3(kWG), 0, st, s->d_ndc, s->d_smp, s->tab);
     RT_HIP(hipGetLastError());
@@ -297,7 +328,7 @@ int prepare_samples(rt_scene *s, const rt_frame *f, uint32_t spp)
 }
 
 constexpr uint32_t kKernelFlags = RT_KERNEL_FLAG_WIDE_HEAVY | RT_KERNEL_FLAG_EXHAUSTIVE |
-                                  RT_KERNEL_FLAG_WAVE_CLOCK | RT_KERNEL_BUDGET_MASK;
+                                  RT_KERNEL_FLAG_WAVE_CLOCK | RT_KERNEL_FLAG_OVERLAP | RT_KERNEL_BUDGET_MASK;
 
 int validate_frame(const rt_frame *f)
 {
@@ -417,9 +448,11 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
     const bool bary = P.tri_test == RT_TRI_BARYCENTRIC;
     const bool grid_mt = P.isect == RT_ISECT_GRID && !bary;
     // The per-camera records (frefs) are scene state: a launch on another stream than the last
-    // one waits for it, so frames of one scene never overlap on the device.
+    // one waits for it, so one scene's single-frame launches never overlap on the device (batched
+    // launches may, RT_KERNEL_FLAG_OVERLAP: launch_batch).
     // (order_streams false: the caller orders its streams itself, rt_render_frame_host_tiled)
-    if (order_streams && s->ev_recorded && st != s->last_stream) RT_HIP(hipStreamWaitEvent(st, s->ev_last->ev, 0));
+    if (order_streams)
+        if (int rc = order_all(s, st)) return rc;
     if (int rc = flush_tables(s, st)) return rc;
     g_ht.mark("tables");
     s->last_stream = st;
@@ -563,7 +596,10 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
         {
             // the dispatch carries its own events (no marker packets): the timed launch's pair, or
             // the scene's completion event alone
-            s->ev_last = timed ? s->kt1[kslot] : s->ev_done;
+            if (timed)
+                s->ev_last = s->kt1[kslot];
+            else if (int rc = free_done_event(s, s->ev_last))
+                return rc;
             hipExtLaunchKernelGGL(lfn, dim3(lgrid), dim3(lwg), 0, st, kt0, s->ev_last->ev, 0u, P);
             stop_done = true;
             s->ev_recorded = true;
@@ -616,7 +652,7 @@ int launch_batch(rt_scene *const *S, const rt_frame *F, uint32_t n, KParams *P, 
     {
         const uint32_t kind = F[i].kernel & RT_KERNEL_KIND_MASK;
         if (kind != RT_KERNEL_AUTO ||
-            (F[i].kernel & ~uint32_t(RT_KERNEL_FLAG_WIDE_HEAVY | RT_KERNEL_FLAG_WAVE_CLOCK)) != 0u ||
+            (F[i].kernel & ~uint32_t(RT_KERNEL_FLAG_WIDE_HEAVY | RT_KERNEL_FLAG_WAVE_CLOCK | RT_KERNEL_FLAG_OVERLAP)) != 0u ||
             (F[i].kernel & RT_KERNEL_FLAG_WAVE_CLOCK) != (F[0].kernel & RT_KERNEL_FLAG_WAVE_CLOCK))
             return RT_E_INVALID;
         if (P[i].isect != RT_ISECT_GRID || P[i].tri_test != RT_TRI_MOLLER_TRUMBORE) return RT_E_INVALID;
@@ -651,20 +687,6 @@ int launch_batch(rt_scene *const *S, const rt_frame *F, uint32_t n, KParams *P, 
     KB.nframes = n;
     for (uint32_t i = 0; i <= n; i++) KB.base[i] = uint32_t(fblocks * i);
     for (uint32_t i = n + 1; i <= kMaxBatch; i++) KB.base[i] = uint32_t(blocks);
-    // per-origin records of every scene, and the cross-stream order of every scene's state
-    for (uint32_t i = 0; i < n; i++)
-    {
-        P[i].wg_per_tile = wgpt;
-        P[i].xcd_chunk = ((P[i].tiles_x + P[i].nranks - 1u) / P[i].nranks) * wgpt;
-        rt_scene *s = S[i];
-        bool first = true;
-        for (uint32_t j = 0; j < i; j++) first = first && S[j] != s;
-        if (!first) continue;
-        if (s->ev_recorded && st != s->last_stream) RT_HIP(hipStreamWaitEvent(st, s->ev_last->ev, 0));
-        if (int rc = flush_tables(s, st)) return rc;
-        s->last_stream = st;
-        if (int rc = ensure_origin_terms(s, P[i], st)) return rc;
-    }
     // the batch's heavy-first / wide-section state lives in scene 0's table, keyed by the batch
     uint64_t ident = n;
     for (uint32_t i = 0; i < n; i++) ident = ident * 0x9E3779B97F4A7C15ull + uint64_t(uintptr_t(S[i]));
@@ -672,6 +694,49 @@ int launch_batch(rt_scene *const *S, const rt_frame *F, uint32_t n, KParams *P, 
     const bool front = blocks >= s0->hf_min_blocks || (wide_heavy && blocks >= 64u);
     uint64_t cams = 0xcbf29ce484222325ull;
     for (uint32_t i = 0; i < n; i++) cams = cam_signature(P[i], cams);
+    for (uint32_t i = 0; i < n; i++)
+    {
+        P[i].wg_per_tile = wgpt;
+        P[i].xcd_chunk = ((P[i].tiles_x + P[i].nranks - 1u) / P[i].nranks) * wgpt;
+    }
+    // RT_KERNEL_FLAG_OVERLAP (every frame of the batch): this launch may run beside the scenes' last
+    // launch on another stream -- its tail under this launch's start -- when no scene state changes
+    // between them: the frame tables and the per-origin records stay, the batch's heavy-first
+    // context exists and this frame is not measured (a measured frame clears and rewrites plan
+    // buffers that an older version's frames read), no wave clocks or segmented-tier scratch
+    // (per-scene buffers).  At most two launches of a scene are in flight: an overlapped launch
+    // waits for the one before the launch it overlaps (ev_prev).
+    bool overlap = !clk && !seg;
+    for (uint32_t i = 0; i < n; i++)
+    {
+        uint32_t ob[3];
+        std::memcpy(ob, P[i].org, sizeof(ob));
+        overlap = overlap && (F[i].kernel & RT_KERNEL_FLAG_OVERLAP) && !S[i]->tab_dirty && S[i]->fref_valid &&
+                  std::memcmp(ob, S[i]->fref_org, sizeof(ob)) == 0;
+    }
+    if (overlap && (front || wide_heavy))
+    {
+        const HfPeek pk = hf_peek(s0, P[0], blocks, kvar, ident | 1u, cams);
+        overlap = pk.found && !pk.measure;
+    }
+    // per-origin records of every scene, and the cross-stream order of every scene's state
+    for (uint32_t i = 0; i < n; i++)
+    {
+        rt_scene *s = S[i];
+        bool first = true;
+        for (uint32_t j = 0; j < i; j++) first = first && S[j] != s;
+        if (!first) continue;
+        if (overlap && s->ev_recorded && st != s->last_stream)
+        {
+            if (s->ev_prev) RT_HIP(hipStreamWaitEvent(st, s->ev_prev->ev, 0));
+            s->ev_prev = s->ev_last;
+        }
+        else if (int rc = order_all(s, st))
+            return rc;
+        if (int rc = flush_tables(s, st)) return rc;
+        s->last_stream = st;
+        if (int rc = ensure_origin_terms(s, P[i], st)) return rc;
+    }
     if (front || wide_heavy)
         if (int rc = hf_prepare(s0, P[0], blocks, kvar, front, st, ident | 1u, cams)) return rc;
     // fused: the wide section's workgroups lead the grid, a multiple of the XCD count so the lane
@@ -726,7 +791,9 @@ int launch_batch(rt_scene *const *S, const rt_frame *F, uint32_t n, KParams *P, 
         if (int rc = new_event(s0->kt1[kslot], s0->ev_time_flags)) return rc;
     // the dispatch's stop event marks every batched scene's last launch (no marker per scene: ten of
     // them cost config 5's step 50 us, profiles/r05u_marker_ab.json)
-    const rtk::EvRef stop = timed ? s0->kt1[kslot] : s0->ev_done;
+    rtk::EvRef stop = timed ? s0->kt1[kslot] : nullptr;
+    if (!timed)
+        if (int rc = free_done_event(s0, stop)) return rc;
     // a timed launch carries its start / stop events in the dispatch itself: separate event records
     // around it cost a measured 3-4 % of that frame (profiles/r05j_frame_series_*.json, steps 8, 24, ...)
     hipExtLaunchKernelGGL(fn, dim3(grid), dim3(bwg), 0, st, timed ? s0->kt0[kslot] : nullptr, stop->ev, 0u, KB);
@@ -1163,7 +1230,8 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
                       sizeof(uint32_t) * (cellw.size() + cellwo.size() + cellwb.size());
     RT_HIP(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
     if (int rc = new_event(s->ev_own, s->ev_order_flags)) return rc;
-    if (int rc = new_event(s->ev_done, s->ev_time_flags)) return rc;     // a dispatch's stop event
+    for (rtk::EvRef& e : s->ev_done)                                    // dispatches' stop events
+        if (int rc = new_event(e, s->ev_time_flags)) return rc;
     s->ev_last = s->ev_own;
     // the plan stream (launch_plans) and the first timed launch's events: created here, not by a
     // frame (a stream's creation took ~0.33 ms of the second frame's call, profiles/r05p_host_trace.log)
@@ -1197,6 +1265,7 @@ int rt_scene_destroy(rt_scene *s)
         (void)hipSetDevice(s->device);
         if (s->stream) (void)hipStreamSynchronize(s->stream);
         if (s->last_stream && s->ev_recorded) (void)hipEventSynchronize(s->ev_last->ev);
+        if (s->ev_prev) (void)hipEventSynchronize(s->ev_prev->ev);
         if (s->plan_st) (void)hipStreamSynchronize(s->plan_st);
         if (s->side) (void)hipStreamSynchronize(s->side);
         (void)hipFree(s->d_off);
@@ -1229,8 +1298,9 @@ int rt_scene_destroy(rt_scene *s)
         if (s->h_smp_pinned) (void)hipHostFree(s->h_smp_pinned);
         if (s->h_frame) (void)hipHostFree(s->h_frame);
         s->ev_own.reset();             // shared events: destroyed with their last reference
-        s->ev_done.reset();
+        for (rtk::EvRef& e : s->ev_done) e.reset();
         s->ev_last.reset();
+        s->ev_prev.reset();
         for (hipEvent_t e : s->band_ev) if (e) (void)hipEventDestroy(e);
         for (hipEvent_t e : s->kt0) if (e) (void)hipEventDestroy(e);
         for (rtk::EvRef& e : s->kt1) e.reset();
@@ -1662,7 +1732,12 @@ int rt_render_frame_host_tiled(rt_scene *s, const rt_frame *f, uint32_t *h_tiles
     auto row_y = [&](uint32_t r) { return r >= tiles_y ? H : r * th; };
     hipStream_t st[2] = { s->stream, s->stream2 };
     // both streams after everything earlier on this scene (the scene's tables and records are shared)
-    if (s->ev_recorded) RT_HIP(hipStreamWaitEvent(st[0], s->ev_last->ev, 0));
+    if (s->ev_recorded)
+    {
+        RT_HIP(hipStreamWaitEvent(st[0], s->ev_last->ev, 0));
+        if (s->ev_prev) RT_HIP(hipStreamWaitEvent(st[0], s->ev_prev->ev, 0));
+        s->ev_prev.reset();
+    }
     KParams P0;
     frame_params(s, f, P0);
     if (use_lanes(f, spp) && P0.isect == RT_ISECT_GRID && P0.tri_test == RT_TRI_MOLLER_TRUMBORE &&

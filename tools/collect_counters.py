@@ -35,6 +35,11 @@ SETS = {
     "fetch": "FETCH_SIZE",
     "write": "WRITE_SIZE",
     "tcc": "TCC_HIT_sum TCC_MISS_sum",
+    # latency: SQ_INST_LEVEL_* / SQ_INSTS_* = mean cycles a VMEM / SMEM instruction is outstanding
+    "lat": "SQ_INSTS_VMEM_RD SQ_INST_LEVEL_VMEM SQ_INSTS_SMEM SQ_INST_LEVEL_SMEM SQ_ACTIVE_INST_VMEM "
+           "SQ_ACTIVE_INST_SCA SQ_WAIT_ANY SQ_INSTS_LDS",
+    "tcp": "TCP_PERF_SEL_TOTAL_HIT_LRU_READ TCP_PERF_SEL_TOTAL_MISS_LRU_READ TCP_PERF_SEL_TOTAL_MISS_EVICT_READ "
+           "TCP_PENDING_STALL_CYCLES",
 }
 
 

@@ -50,7 +50,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpu
     > $R/gpurun_out/${T}_bench_under_rocprof.json 2> $R/gpurun_out/${T}_trace.err
 rc=$?; echo "trace rc=$rc"; [ $rc -eq 0 ] || exit $rc
 cd $R
-run shard_bench 400 python -u tools/shard_scaling.py --steady --batch --scenes 1 8 --out ${T}_shard_scaling_bench 0
+run shard_bench 500 python -u tools/shard_scaling.py --steady --batch --overlap --scenes 1 8 --out ${T}_shard_scaling_bench 0
 run shard_head 500 python -u tools/shard_scaling.py --steady --scenes 4 --frame 4096 4096 16 --out ${T}_shard_scaling_head 0
 run counters_n8 300 python3 -u tools/collect_counters.py --workload bench --batch --rank 0 --nranks 8 --frames 24 \
     --sets sq --out gpurun_out/${T}_counters_batch_n8.json --work gpurun_out/${T}_pmc_n8

@@ -33,6 +33,9 @@ ap.add_argument("--frame", type=int, nargs=3, default=[1920, 1080, 4])
 ap.add_argument("--out", default=None)
 ap.add_argument("--batch", action="store_true",
                 help="also time each rank's frames of ALL --scenes as one batched launch (rt_render_batch_device)")
+ap.add_argument("--overlap", action="store_true",
+                help="--batch: also consecutive launches alternating two streams with RT_KERNEL_FLAG_OVERLAP "
+                     "(bench.py's step); batch_max_ms is then that, batch_max_ms_one_stream the other")
 ap.add_argument("kernels", nargs="*")
 A = ap.parse_args()
 W, H, SPP = A.frame
@@ -77,29 +80,53 @@ for sid in A.scenes:
 if A.batch:
     gs = [rtm.GpuScene(rtm.HostScene.load(sid), 0) for sid in A.scenes]
     fs = [g.frame(W, H, SPP) for g in gs]
+    fo = [g.frame(W, H, SPP, kernel=rtm.RT_KERNEL_FLAG_OVERLAP) for g in gs]
+    st2 = torch.cuda.Stream()
     res["batch_max_ms"] = {}
+    if A.overlap:
+        res["batch_max_ms_one_stream"] = {}
     for n in NS:
-        bufs = [torch.empty(rtm.shard_elems(W, H, n), dtype=torch.int32, device="cuda") for _ in gs]
-        worst = 0.0
-        for r in range(n):
-            run = lambda: rtm.render_batch_device(gs, fs, [b.data_ptr() for b in bufs], rank=r, nranks=n,
-                                                  stream=st.cuda_stream)
-            ts = []
-            for _ in range(20):
-                run()
-            for rep in range(3):
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record(st)
-                for _ in range(32):
+        sets = [[torch.empty(rtm.shard_elems(W, H, n), dtype=torch.int32, device="cuda") for _ in gs]
+                for _ in range(2)]
+        bufs = sets[0]
+        arms = ("overlap", "one_stream") if A.overlap else ("one_stream",)
+        worsts = {}
+        for arm in arms:
+            worst = 0.0
+            for r in range(n):
+                k = [0]
+
+                def run(r=r, arm=arm):
+                    # overlap: step i on stream i % 2 into buffer set i % 2 (bench.py's step)
+                    p = k[0] % 2 if arm == "overlap" else 0
+                    k[0] += 1
+                    s = (st, st2)[p]
+                    rtm.render_batch_device(gs, fo if arm == "overlap" else fs, [b.data_ptr() for b in sets[p]],
+                                            rank=r, nranks=n, stream=s.cuda_stream)
+                ts = []
+                for _ in range(20):
                     run()
-                e1.record(st)
-                torch.cuda.synchronize()
-                ts.append(e0.elapsed_time(e1) / 32)
-            v = round(sorted(ts)[1], 4)
-            res["per_rank"][f"batch_n{n}_r{r}"] = v
-            worst = max(worst, v)
+                for rep in range(3):
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(st)
+                    st2.wait_event(e0)
+                    for _ in range(32):
+                        run()
+                    j = torch.cuda.Event()
+                    j.record(st2)
+                    st.wait_event(j)
+                    e1.record(st)
+                    torch.cuda.synchronize()
+                    ts.append(e0.elapsed_time(e1) / 32)
+                v = round(sorted(ts)[1], 4)
+                res["per_rank"][f"batch_n{n}_r{r}" + ("" if arm == arms[0] else "_one_stream")] = v
+                worst = max(worst, v)
+            worsts[arm] = worst
+        worst = worsts[arms[0]]
         res["batch_max_ms"][n] = worst
-        print("batch", A.scenes, n, worst, flush=True)
+        if A.overlap:
+            res["batch_max_ms_one_stream"][n] = worsts["one_stream"]
+        print("batch", A.scenes, n, worsts, flush=True)
         if n > 1:
             # gather rehearsal, timed beside the render: rank 0's own share of a step's assembly on
             # ONE GPU -- the (n - 1) remote shards of each frame copied into its gather buffer
