@@ -445,9 +445,9 @@ class GpuWorkload:
     def __init__(self, rtm, torch, world, rank, local, kernel, batch=True, overlap=False):
         self.rtm, self.torch, self.world, self.rank = rtm, torch, world, rank
         self.batch = batch
-        # overlap (batched launches, RT_KERNEL_FLAG_OVERLAP): consecutive steps alternate two launch
+        # overlap (RT_KERNEL_FLAG_OVERLAP): consecutive steps alternate two launch
         # streams and two buffer sets, so one step's render tail runs under the next step's start
-        self.overlap = overlap and batch
+        self.overlap = overlap
         if self.overlap:
             kernel |= rtm.RT_KERNEL_FLAG_OVERLAP
         self.graphs = None              # per buffer set: hipGraph of the step's render launch(es) (--graph)

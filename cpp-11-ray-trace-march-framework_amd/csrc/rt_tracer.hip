@@ -448,10 +448,32 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
     const bool bary = P.tri_test == RT_TRI_BARYCENTRIC;
     const bool grid_mt = P.isect == RT_ISECT_GRID && !bary;
     // The per-camera records (frefs) are scene state: a launch on another stream than the last
-    // one waits for it, so one scene's single-frame launches never overlap on the device (batched
-    // launches may, RT_KERNEL_FLAG_OVERLAP: launch_batch).
+    // one waits for it -- unless the caller allows overlap (RT_KERNEL_FLAG_OVERLAP) and nothing the
+    // two launches share changes between them (as launch_batch): AUTO's lane kernel (not the wide
+    // section's side-stream pair, not the wave clocks), the same tables and camera origin, and an
+    // existing launch shape whose frame is not measured.
     // (order_streams false: the caller orders its streams itself, rt_render_frame_host_tiled)
-    if (order_streams)
+    bool overlap = false;
+    if (order_streams && (f->kernel & RT_KERNEL_FLAG_OVERLAP) && s->ev_recorded && st != s->last_stream &&
+        kind == RT_KERNEL_AUTO && lanes && grid_mt && !(f->kernel & (RT_KERNEL_FLAG_WAVE_CLOCK | RT_KERNEL_FLAG_WIDE_HEAVY)) &&
+        !(P.nranks >= 2u && s->max_cell_refs >= s->wh_auto_refs) && P.spp <= 64u && !s->tab_dirty && s->fref_valid)
+    {
+        uint32_t ob[3];
+        std::memcpy(ob, P.org, sizeof(ob));
+        overlap = std::memcmp(ob, s->fref_org, sizeof(ob)) == 0;
+        const int v = kVarAutoCore | (s->rcp_safe ? kVarFastRcp : 0) | (auto_runs(s) ? kVarPackedRem | kVarSkipRun : 0);
+        if (overlap && blocks >= s->hf_min_blocks)
+        {
+            const HfPeek pk = hf_peek(s, P, blocks, v, 0u, cam_signature(P));
+            overlap = pk.found && !pk.measure;
+        }
+    }
+    if (overlap)
+    {
+        if (s->ev_prev) RT_HIP(hipStreamWaitEvent(st, s->ev_prev->ev, 0));
+        s->ev_prev = s->ev_last;
+    }
+    else if (order_streams)
         if (int rc = order_all(s, st)) return rc;
     if (int rc = flush_tables(s, st)) return rc;
     g_ht.mark("tables");

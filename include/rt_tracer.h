@@ -110,14 +110,14 @@ enum rt_kernel {
                                            (no block culling; A/B arm, identical results) */
     RT_KERNEL_FLAG_WAVE_CLOCK = 0x400000, /* OR-able (AUTO), debug: record s_memtime {start, end} of
                                              every 64-sample work item (rt_debug_wave_clocks) */
-    RT_KERNEL_FLAG_OVERLAP = 0x800000, /* OR-able (AUTO, batched launches: every frame of the batch):
-                                          the caller lets this launch run beside the scenes' previous
-                                          launch when that one is on another stream (it writes other
-                                          output buffers), so the previous frame's tail overlaps this
-                                          one's start.  The library still orders the two when scene state
+    RT_KERNEL_FLAG_OVERLAP = 0x800000, /* OR-able (AUTO; in a batch: every frame of it): the caller
+                                          lets this launch run beside the scene's previous launch when
+                                          that one is on another stream (it writes other output
+                                          buffers), so the previous frame's tail overlaps this one's
+                                          start.  The library still orders the two when scene state
                                           changes between them (frame tables, camera origin, a new launch
-                                          shape, a measured frame); at most two launches of a scene run
-                                          at once.  Single-frame launches ignore it (ordered). */
+                                          shape, a measured frame, a single frame's wide-section pair, wave
+                                          clocks); at most two launches of a scene run at once. */
     RT_KERNEL_BUDGET_SHIFT = 24,      /* bits 24-30: RT_KERNEL_COMPACT: lanes that must be idle before
                                          a wave refills (1..64; 0 = default 48) */
     RT_KERNEL_BUDGET_MASK = 0x7F000000,

@@ -122,16 +122,21 @@ def test_overlap_refresh_frame(golden, monkeypatch):
             h.close()
 
 
-def test_overlap_flag_single_frame_is_ordered(golden, scenes):
-    """A single-frame launch with the flag (no batch) is ordered as before: frames on alternating
-    streams still equal the reference's."""
+@pytest.mark.parametrize("sid", [8, 4])
+def test_overlap_single_frames(golden, scenes, sid):
+    """Single-frame AUTO launches with the flag on alternating streams (killeroo; head's scene at
+    1080p), 40 steps into 8 sentinel-refilled buffers: every frame equals the reference's."""
     import torch
-    hs, gs = scenes(8)
+    hs, gs = scenes(sid)
     f = gs.frame(W, H, SPP, kernel=rtm.RT_KERNEL_FLAG_OVERLAP)
     streams = [torch.cuda.Stream(), torch.cuda.Stream()]
-    outs = [torch.zeros(W * H, dtype=torch.int32, device="cuda") for _ in range(2)]
-    for i in range(6):
-        gs.render_frame_device(f, outs[i % 2].data_ptr(), streams[i % 2].cuda_stream)
-    torch.cuda.synchronize()
-    for o in outs:
-        assert sha(o) == golden["frames_1080p4"]["8"]["bgra_sha256"]
+    outs = [torch.zeros(W * H, dtype=torch.int32, device="cuda") for _ in range(8)]
+    for i in range(40):
+        s = streams[i % 2]
+        with torch.cuda.stream(s):
+            outs[i % 8].fill_(0x5A5A5A5A)
+        gs.render_frame_device(f, outs[i % 8].data_ptr(), s.cuda_stream)
+        if i % 8 == 7:
+            torch.cuda.synchronize()
+            for o in outs:
+                assert sha(o) == golden["frames_1080p4"][str(sid)]["bgra_sha256"], (sid, i)

@@ -10,10 +10,6 @@ run() {
     echo "$name rc=$rc"
     [ $rc -eq 0 ] || { tail -5 gpurun_out/${T}_${name}.log; exit $rc; }
 }
-run bench 150 python -u bench.py --no-cpu-baseline
-run bench_off 150 python -u bench.py --no-cpu-baseline --overlap off --no-end-to-end --no-moving-camera --no-first-frame
-run b2 100 python -u bench.py --no-cpu-baseline --steps 20 --warmup 5
-run c 150 python -u bench.py --no-cpu-baseline --workload batch10
-run c_off 150 python -u bench.py --no-cpu-baseline --workload batch10 --overlap off
-run h 150 python -u bench.py --no-cpu-baseline --workload head4096 --no-end-to-end --no-moving-camera
-run shard 500 python -u tools/shard_scaling.py --steady --batch --overlap --scenes 1 8 --out ${T}_shard 0
+run ovtests 500 python -u -m pytest tests/test_gpu_overlap.py -x -v --timeout 300 --timeout-method thread
+run h 150 python -u bench.py --no-cpu-baseline --workload head4096 --no-end-to-end --no-moving-camera --batch off
+run h_off 150 python -u bench.py --no-cpu-baseline --workload head4096 --no-end-to-end --no-moving-camera --batch off --overlap off
