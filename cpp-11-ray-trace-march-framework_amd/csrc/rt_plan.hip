@@ -348,6 +348,11 @@ int launch_plans(rt_scene *s, const KParams& P, uint64_t blocks, hipStream_t st)
         hipLaunchKernelGGL(k_hf_plan, grid, wg, 0, st, Q, uint32_t(blocks), s->hf_shift);
     }
     RT_HIP(hipGetLastError());
+    // plans on the launch stream are part of the scene's last launch: a launch on another stream orders
+    // after them, not only after the render (ev_last was the render's own stop event).  Measured frames
+    // are never overlapped, so no ev_prev refers to ev_own here.
+    RT_HIP(hipEventRecord(s->ev_own->ev, st));
+    s->ev_last = s->ev_own;
     return RT_OK;
 }
 

@@ -10,6 +10,5 @@ run() {
     echo "$name rc=$rc"
     [ $rc -eq 0 ] || { tail -5 gpurun_out/${T}_${name}.log; exit $rc; }
 }
-run ovtests 500 python -u -m pytest tests/test_gpu_overlap.py -x -v --timeout 300 --timeout-method thread
-run h 150 python -u bench.py --no-cpu-baseline --workload head4096 --no-end-to-end --no-moving-camera --batch off
-run h_off 150 python -u bench.py --no-cpu-baseline --workload head4096 --no-end-to-end --no-moving-camera --batch off --overlap off
+run single 300 python3 -u tools/overlap_stress.py --reps 4 --steps 24
+run batch 300 python3 -u tools/overlap_stress.py --batch --reps 6 --steps 40

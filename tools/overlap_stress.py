@@ -1,0 +1,68 @@
+#!/usr/bin/env python3
+"""Stress for RT_KERNEL_FLAG_OVERLAP's single-frame path: per scene and repetition, a FRESH scene object
+renders `steps` 1080p x 4 frames on two alternating streams into 8 sentinel-refilled buffers; every
+frame is compared with a one-stream reference frame.  Reports, per bad frame, the step, how many
+pixels still hold the sentinel (never written) and how many differ otherwise."""
+import argparse
+import importlib.util
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+spec = importlib.util.spec_from_file_location("rtm", os.path.join(ROOT, "cpp-11-ray-trace-march-framework_amd", "__init__.py"))
+rtm = importlib.util.module_from_spec(spec)
+sys.modules["rtm"] = rtm
+spec.loader.exec_module(rtm)
+ap = argparse.ArgumentParser()
+ap.add_argument("--scenes", type=int, nargs="+", default=[4, 8, 1, 5])
+ap.add_argument("--reps", type=int, default=4)
+ap.add_argument("--steps", type=int, default=24)
+ap.add_argument("--batch", action="store_true", help="the pair (8, 1) batched instead of single frames")
+A = ap.parse_args()
+torch.cuda.set_device(0)
+W, H, SPP = 1920, 1080, 4
+S = 0x5A5A5A5A
+streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+bad = []
+for sid in ([0] if A.batch else A.scenes):
+    sids = (8, 1) if A.batch else (sid,)
+    hss = [rtm.HostScene.load(x) for x in sids]
+    rg = [rtm.GpuScene(h, 0) for h in hss]
+    refs = [torch.zeros(W * H, dtype=torch.int32, device="cuda") for _ in sids]
+    for g, r in zip(rg, refs):
+        for _ in range(2):
+            g.render_frame_device(g.frame(W, H, SPP), r.data_ptr())
+    torch.cuda.synchronize()
+    for g in rg:
+        g.close()
+    for rep in range(A.reps):
+        gs = [rtm.GpuScene(h, 0) for h in hss]
+        fs = [g.frame(W, H, SPP, kernel=rtm.RT_KERNEL_FLAG_OVERLAP) for g in gs]
+        outs = [[torch.zeros(W * H, dtype=torch.int32, device="cuda") for _ in sids] for _ in range(8)]
+        for i in range(A.steps):
+            s = streams[i % 2]
+            with torch.cuda.stream(s):
+                for o in outs[i % 8]:
+                    o.fill_(S)
+            if A.batch:
+                rtm.render_batch_device(gs, fs, [o.data_ptr() for o in outs[i % 8]], stream=s.cuda_stream)
+            else:
+                gs[0].render_frame_device(fs[0], outs[i % 8][0].data_ptr(), s.cuda_stream)
+            if i % 8 == 7:
+                torch.cuda.synchronize()
+                for q in range(8):
+                    for k, o in enumerate(outs[q]):
+                        if not torch.equal(o, refs[k]):
+                            row = {"scene": sids[k], "rep": rep, "step": i - 7 + q, "sentinel": int((o == S).sum()),
+                                   "other": int(((o != refs[k]) & (o != S)).sum())}
+                            bad.append(row)
+                            print(json.dumps(row), flush=True)
+        torch.cuda.synchronize()
+        for g in gs:
+            g.close()
+    for h in hss:
+        h.close()
+print(json.dumps({"bad_frames": len(bad)}))
