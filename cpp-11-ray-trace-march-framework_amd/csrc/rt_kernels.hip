@@ -62,17 +62,16 @@ __device__ __forceinline__ uint32_t xcd_band_block(uint32_t b, uint32_t nb, uint
 // rest walk the natural (XCD-banded) order, skipping the listed blocks.  Returns false when this
 // block has nothing to do.  The marks read here are never written by this launch (the next
 // frame's marks live in the other buffer), so every wave of a block decides alike.
-// lead: the first lane of launch block 0's first wave (the one that clears the next plan).
+// lead: the first lane of launch block 0's first wave (unused since round 5: launch_plans clears the next plan).
 template <int VAR>
 __device__ __forceinline__ bool block_of_launch(const KParams& P, uint32_t& b, uint32_t bid, uint32_t nblk,
                                                 bool lead)
 {
-    if ((VAR & kVarWideHeavy) && P.hf_measure && lead)
-        *P.hf_plan_out = HfPlan{};                            // k_hf_plan runs after this kernel
+    // (the next plan's counters are cleared by launch_plans right before k_hf_plan, not here: a
+    // measured frame may run beside a frame that still reads the buffer it would clear)
+    (void)lead;
     if (P.hf_front)
     {
-        if (P.hf_measure && lead)
-            *P.hf_plan_out = HfPlan{};                        // k_hf_plan runs after this kernel
         const uint32_t front = P.hf_front;
         if (bid < front)
         {

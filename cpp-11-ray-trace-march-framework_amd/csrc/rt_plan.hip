@@ -314,6 +314,10 @@ int launch_plans(rt_scene *s, const KParams& P, uint64_t blocks, hipStream_t st)
         // event): a marker packet on the launch stream here put ~13 us between that launch and the
         // next one (rocprofv3 kernel trace of a frame series, profiles/r05t_series_kernel_trace.csv)
         RT_HIP(hipStreamWaitEvent(s->plan_st, s->ev_last->ev, 0));
+        // a measured frame that overlapped its predecessor (RT_KERNEL_FLAG_OVERLAP): the plan rewrites
+        // the buffers of the version before this frame's, which that predecessor may read
+        if (s->ev_prev) RT_HIP(hipStreamWaitEvent(s->plan_st, s->ev_prev->ev, 0));
+        RT_HIP(hipMemsetAsync(P.hf_plan_out, 0, sizeof(HfPlan), s->plan_st));
         hipLaunchKernelGGL(k_hf_plan, grid, wg, 0, s->plan_st, P, uint32_t(blocks), s->hf_shift);
         RT_HIP(hipEventRecord(c->pend_ev, s->plan_st));
         c->pend = P.hf_ver + 1u;
@@ -321,6 +325,7 @@ int launch_plans(rt_scene *s, const KParams& P, uint64_t blocks, hipStream_t st)
         RT_HIP(hipGetLastError());
         return RT_OK;
     }
+    RT_HIP(hipMemsetAsync(P.hf_plan_out, 0, sizeof(HfPlan), st));
     hipLaunchKernelGGL(k_hf_plan, grid, wg, 0, st, P, uint32_t(blocks), s->hf_shift);
     if (c)
     {
@@ -395,8 +400,9 @@ HfPeek hf_peek(const rt_scene *s, const KParams& P, uint64_t blocks, int var, ui
     uint64_t key[5];
     hf_key(P, blocks, var, batch, key);
     for (const HfCtx& h : s->hf)
-        if (std::memcmp(h.key, key, sizeof(key)) == 0) return HfPeek{ true, measures(s, h, cam_sig) };
-    return HfPeek{ false, true };
+        if (std::memcmp(h.key, key, sizeof(key)) == 0)
+            return HfPeek{ true, measures(s, h, cam_sig), h.frames >= 2u && h.pend == 0u && !h.proxied };
+    return HfPeek{ false, true, false };
 }
 
 int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hipStream_t st, uint64_t batch,

@@ -465,7 +465,7 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
         if (overlap && blocks >= s->hf_min_blocks)
         {
             const HfPeek pk = hf_peek(s, P, blocks, v, 0u, cam_signature(P));
-            overlap = pk.found && !pk.measure;
+            overlap = pk.found && (!pk.measure || pk.measure_ok);
         }
     }
     if (overlap)
@@ -739,7 +739,7 @@ int launch_batch(rt_scene *const *S, const rt_frame *F, uint32_t n, KParams *P, 
     if (overlap && (front || wide_heavy))
     {
         const HfPeek pk = hf_peek(s0, P[0], blocks, kvar, ident | 1u, cams);
-        overlap = pk.found && !pk.measure;
+        overlap = pk.found && (!pk.measure || pk.measure_ok);
     }
     // per-origin records of every scene, and the cross-stream order of every scene's state
     for (uint32_t i = 0; i < n; i++)

@@ -1,7 +1,8 @@
 """RT_KERNEL_FLAG_OVERLAP: consecutive batched launches of the same scenes on two streams, each step's
-tail running under the next step's start (DESIGN.md §4.19).  The library orders the two launches
-whenever scene state changes between them (new shape, measured frames every 16th frame, plan
-adoption, the wide list's refresh frame); every other pair of steps overlaps.  Every frame of every
+tail running under the next step's start (DESIGN.md §4.20).  The library orders the two launches
+whenever scene state changes between them (a new shape and its first two frames, a new camera
+origin, a pending plan); every other pair of steps overlaps, measured frames included (their plan
+then waits for both frames in flight).  Every frame of every
 step -- through the measured frames, the plan stream's adoptions and (at N > 1) the wide section's
 listing and refresh -- must equal the reference's frame, and the per-sample hit IDs its hit IDs."""
 import hashlib
@@ -48,6 +49,7 @@ def _overlap_steps(golden, gss, sids, N, steps, check_every, hits_every=0):
     sets = [[torch.zeros(N * e, dtype=torch.int32, device="cuda") for _ in gss] for _ in range(nsets)]
     hits = [torch.full((W * H * SPP,), 0x5A5A5A5A, dtype=torch.int32, device="cuda") for _ in gss]
     out = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()            # (torch's allocations fill on its own stream, not on these)
     checked = 0
     for i in range(steps):
         s = streams[i % 2]
@@ -131,6 +133,7 @@ def test_overlap_single_frames(golden, scenes, sid):
     f = gs.frame(W, H, SPP, kernel=rtm.RT_KERNEL_FLAG_OVERLAP)
     streams = [torch.cuda.Stream(), torch.cuda.Stream()]
     outs = [torch.zeros(W * H, dtype=torch.int32, device="cuda") for _ in range(8)]
+    torch.cuda.synchronize()            # (torch's zero fill runs on its own stream, not on these)
     for i in range(40):
         s = streams[i % 2]
         with torch.cuda.stream(s):

@@ -10,5 +10,7 @@ run() {
     echo "$name rc=$rc"
     [ $rc -eq 0 ] || { tail -5 gpurun_out/${T}_${name}.log; exit $rc; }
 }
-run single 300 python3 -u tools/overlap_stress.py --reps 4 --steps 24
+run ovt 300 python -u -m pytest tests/test_gpu_overlap.py -x -q --timeout 200 --timeout-method thread
+run single 300 python3 -u tools/overlap_stress.py --reps 4 --steps 40
+run single_nf 300 python3 -u tools/overlap_stress.py --reps 2 --steps 40 --no-flag
 run batch 300 python3 -u tools/overlap_stress.py --batch --reps 6 --steps 40

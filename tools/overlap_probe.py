@@ -66,6 +66,7 @@ for rnd in range(A.rounds):
         for n in A.ns:
             e = rtm.shard_elems(W, H, n) if n > 1 else W * H
             sets = [[torch.zeros(e, dtype=torch.int32, device="cuda") for _ in gs] for _ in range(2)]
+            torch.cuda.synchronize()
             worst = 0.0
             for r in range(n):
                 def run(i, r=r):

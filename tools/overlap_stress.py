@@ -21,6 +21,8 @@ ap.add_argument("--scenes", type=int, nargs="+", default=[4, 8, 1, 5])
 ap.add_argument("--reps", type=int, default=4)
 ap.add_argument("--steps", type=int, default=24)
 ap.add_argument("--batch", action="store_true", help="the pair (8, 1) batched instead of single frames")
+ap.add_argument("--no-flag", action="store_true", help="without RT_KERNEL_FLAG_OVERLAP (ordered launches)")
+ap.add_argument("--one-stream", action="store_true")
 A = ap.parse_args()
 torch.cuda.set_device(0)
 W, H, SPP = 1920, 1080, 4
@@ -40,10 +42,11 @@ for sid in ([0] if A.batch else A.scenes):
         g.close()
     for rep in range(A.reps):
         gs = [rtm.GpuScene(h, 0) for h in hss]
-        fs = [g.frame(W, H, SPP, kernel=rtm.RT_KERNEL_FLAG_OVERLAP) for g in gs]
+        fs = [g.frame(W, H, SPP, kernel=0 if A.no_flag else rtm.RT_KERNEL_FLAG_OVERLAP) for g in gs]
         outs = [[torch.zeros(W * H, dtype=torch.int32, device="cuda") for _ in sids] for _ in range(8)]
+        torch.cuda.synchronize()        # torch's zero fill runs on its own stream, not on the render streams
         for i in range(A.steps):
-            s = streams[i % 2]
+            s = streams[0 if A.one_stream else i % 2]
             with torch.cuda.stream(s):
                 for o in outs[i % 8]:
                     o.fill_(S)
@@ -56,8 +59,13 @@ for sid in ([0] if A.batch else A.scenes):
                 for q in range(8):
                     for k, o in enumerate(outs[q]):
                         if not torch.equal(o, refs[k]):
+                            d = (o != refs[k]).view(H, W)
+                            rows = torch.nonzero(d.any(dim=1)).flatten()
                             row = {"scene": sids[k], "rep": rep, "step": i - 7 + q, "sentinel": int((o == S).sum()),
-                                   "other": int(((o != refs[k]) & (o != S)).sum())}
+                                   "other": int(((o != refs[k]) & (o != S)).sum()),
+                                   "rows": [int(rows.min()), int(rows.max())] if len(rows) else None,
+                                   "sample": [hex(int(o.view(H, W)[rows[0], c]) & 0xFFFFFFFF) for c in range(0, W, 480)] if len(rows) else None,
+                                   "ref": [hex(int(refs[k].view(H, W)[rows[0], c]) & 0xFFFFFFFF) for c in range(0, W, 480)] if len(rows) else None}
                             bad.append(row)
                             print(json.dumps(row), flush=True)
         torch.cuda.synchronize()
