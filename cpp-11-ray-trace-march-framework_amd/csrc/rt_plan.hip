@@ -488,7 +488,9 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
             P.hf_measure = 0u;
         else if (P.hf_measure || c->pend_age >= 1u)
         {
-            RT_HIP(hipStreamWaitEvent(st, c->pend_ev, 0));
+            // (a plan that has finished needs no wait packet: a stream wait costs the launch stream a
+            // few us of idle chip even on a completed event)
+            if (hipEventQuery(c->pend_ev) != hipSuccess) RT_HIP(hipStreamWaitEvent(st, c->pend_ev, 0));
             c->ver = c->pend;
             c->pend = 0u;
         }

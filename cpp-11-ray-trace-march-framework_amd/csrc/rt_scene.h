@@ -172,6 +172,7 @@ struct rt_scene
     rtk::EvRef ev_own, ev_last;
     rtk::EvRef ev_done[4];              // stop events, each re-recorded only when no scene refers to it
     rtk::EvRef ev_prev;                 // RT_KERNEL_FLAG_OVERLAP: the launch ev_last's launch overlaps (else null)
+    hipStream_t prev_stream = nullptr;  // ... and its stream
     bool ev_recorded = false;
     // render-kernel-only timing: event pair around the render kernel(s) of each launch (not the
     // heavy-first planning kernels), a ring of the last kTimeRing launches (rt_kernel_times)

@@ -173,15 +173,32 @@ int wait_scene_idle(rt_scene *s)
     return RT_OK;
 }
 
+// st waits for e -- unless e has already completed (a stream wait enqueues a packet that idles the
+// chip for a few us even then)
+hipError_t wait_unless_done(hipStream_t st, hipEvent_t e)
+{
+    return hipEventQuery(e) == hipSuccess ? hipSuccess : hipStreamWaitEvent(st, e, 0);
+}
+
 // Orders stream st after every launch of scene s that may still run: the last one (ev_last, implicit
 // on its own stream) and, when that one overlapped its predecessor (RT_KERNEL_FLAG_OVERLAP), the
 // predecessor (ev_prev).  The caller's next launch on st then follows them all.
 int order_all(rt_scene *s, hipStream_t st)
 {
     if (!s->ev_recorded) return RT_OK;
-    if (st != s->last_stream) RT_HIP(hipStreamWaitEvent(st, s->ev_last->ev, 0));
-    if (s->ev_prev) RT_HIP(hipStreamWaitEvent(st, s->ev_prev->ev, 0));
+    if (st != s->last_stream) RT_HIP(wait_unless_done(st, s->ev_last->ev));
+    if (s->ev_prev && s->prev_stream != st) RT_HIP(wait_unless_done(st, s->ev_prev->ev));
     s->ev_prev.reset();
+    return RT_OK;
+}
+
+// An overlapped launch on st (RT_KERNEL_FLAG_OVERLAP): it may run beside the scene's last launch, but
+// after the one before that (at most two in flight)
+int order_overlap(rt_scene *s, hipStream_t st)
+{
+    if (s->ev_prev && s->prev_stream != st) RT_HIP(wait_unless_done(st, s->ev_prev->ev));
+    s->ev_prev = s->ev_last;
+    s->prev_stream = s->last_stream;
     return RT_OK;
 }
 
@@ -470,8 +487,7 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
     }
     if (overlap)
     {
-        if (s->ev_prev) RT_HIP(hipStreamWaitEvent(st, s->ev_prev->ev, 0));
-        s->ev_prev = s->ev_last;
+        if (int rc = order_overlap(s, st)) return rc;
     }
     else if (order_streams)
         if (int rc = order_all(s, st)) return rc;
@@ -750,8 +766,7 @@ int launch_batch(rt_scene *const *S, const rt_frame *F, uint32_t n, KParams *P, 
         if (!first) continue;
         if (overlap && s->ev_recorded && st != s->last_stream)
         {
-            if (s->ev_prev) RT_HIP(hipStreamWaitEvent(st, s->ev_prev->ev, 0));
-            s->ev_prev = s->ev_last;
+            if (int rc = order_overlap(s, st)) return rc;
         }
         else if (int rc = order_all(s, st))
             return rc;

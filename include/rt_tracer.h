@@ -116,8 +116,9 @@ enum rt_kernel {
                                           buffers), so the previous frame's tail overlaps this one's
                                           start.  The library still orders the two when scene state
                                           changes between them (frame tables, camera origin, a new launch
-                                          shape, a measured frame, a single frame's wide-section pair, wave
-                                          clocks); at most two launches of a scene run at once. */
+                                          shape and its first two frames, a pending plan, a single frame's
+                                          wide-section pair, wave clocks); at most two launches of a
+                                          scene run at once. */
     RT_KERNEL_BUDGET_SHIFT = 24,      /* bits 24-30: RT_KERNEL_COMPACT: lanes that must be idle before
                                          a wave refills (1..64; 0 = default 48) */
     RT_KERNEL_BUDGET_MASK = 0x7F000000,

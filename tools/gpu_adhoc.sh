@@ -10,7 +10,10 @@ run() {
     echo "$name rc=$rc"
     [ $rc -eq 0 ] || { tail -5 gpurun_out/${T}_${name}.log; exit $rc; }
 }
-run ovt 300 python -u -m pytest tests/test_gpu_overlap.py -x -q --timeout 200 --timeout-method thread
+run pytest 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread
 run single 300 python3 -u tools/overlap_stress.py --reps 4 --steps 40
-run single_nf 300 python3 -u tools/overlap_stress.py --reps 2 --steps 40 --no-flag
 run batch 300 python3 -u tools/overlap_stress.py --batch --reps 6 --steps 40
+run ser 100 python3 -u tools/frame_series.py --steps 60 --burn 1500 --out ${T}_ser
+run bench 150 python -u bench.py --no-cpu-baseline --no-end-to-end --no-first-frame --no-moving-camera
+run c 150 python -u bench.py --no-cpu-baseline --workload batch10 --no-moving-camera
+run ov 300 python3 -u tools/overlap_probe.py --rounds 2 --out ${T}_ov
