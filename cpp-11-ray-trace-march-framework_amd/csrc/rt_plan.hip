@@ -22,7 +22,11 @@ namespace {
 // atomics: thousands of same-address atomics from waves cost milliseconds, measured).  The plan's
 // time is those same-address atomics: one block per thread (1,013 workgroups for the batched
 // bench pair) took 26.6 us per plan, which a moving camera pays every frame.
-__global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks, uint32_t shift)
+// pos16 (RT_HF_POS16, 0: off): a block is heavy when its cost exceeds pos16 / 16 of the span left
+// after its natural start (b / nblocks of the estimated span, sum of wave costs / kHfSlots) -- a
+// late block needs less to make the tail than an early one -- and last max >> pos_shift.
+__global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks, uint32_t shift, uint32_t pos16,
+                                                 uint32_t pos_shift)
 {
     __shared__ uint32_t s_max, s_hi, s_lo, s_w, s_s, s_bhi, s_blo, s_bw, s_bs, s_last;
     __shared__ unsigned long long s_sum;
@@ -34,7 +38,8 @@ __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks, ui
     __syncthreads();
     const HfPlan last = *P.hf_plan_in;
     const bool tail = uint64_t(last.maxc) * kHfSlots * 16u > uint64_t(kHfTail) * (last.sum << 4);
-    const uint32_t thr = max(P.hf_floor, last.maxc >> shift);
+    const uint32_t thr = max(P.hf_floor, last.maxc >> (pos16 ? pos_shift : shift));
+    const uint64_t span = (last.sum << 4) / kHfSlots;
     const uint32_t b0 = blockIdx.x * (kWG * kHfPlanPer) + threadIdx.x;
     uint32_t tmax = 0u, wmasks = 0u, smasks = 0u, heavy = 0u, hi = 0u;
     unsigned long long tsum = 0ull;
@@ -84,7 +89,10 @@ __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks, ui
             const uint32_t wm = wmask | smask;
             cost = max(max((wm & 1u) ? 0u : c.x, (wm & 2u) ? 0u : c.y), max((wm & 4u) ? 0u : c.z, (wm & 8u) ? 0u : c.w));
         }
-        const bool hv = P.hf_front && tail && cost > thr;
+        uint32_t tb = thr;
+        if (pos16 && b < nblocks)
+            tb = max(tb, uint32_t(min<uint64_t>(span * pos16 / 16u * (nblocks - b) / nblocks, 0xFFFFFFFFull)));
+        const bool hv = P.hf_front && tail && cost > tb;
         const bool h1 = hv && cost > (last.maxc >> 1);
         tmax = max(tmax, cost);
         tsum += sum;
@@ -303,6 +311,10 @@ int launch_plans(rt_scene *s, const KParams& P, uint64_t blocks, hipStream_t st)
     // two passes: a shape's first measurement (version 0), and the first one after a proxy plan (its
     // maximum and span are in proxy units): the second pass ranks against the first's
     const bool twice = P.hf_ver == 0u || (c && c->proxied);
+    // the position-aware threshold for single-frame launches; a batched launch keeps max >> shift
+    // (the bench pair's batched step: 0.5396 vs 0.5318 ms with it, scenes 4 / 5 in their own launches
+    // 0.2486 / 0.4518 vs 0.252 / 0.46: profiles/r05ar_hf_pos_sweep.json)
+    const uint32_t pos16 = (c && c->key[4] != 0u) ? s->hf_pos16_batch : s->hf_pos16;
     if (!twice && c && cap == hipStreamCaptureStatusNone)
     {
         if (!s->plan_st)
@@ -318,7 +330,7 @@ int launch_plans(rt_scene *s, const KParams& P, uint64_t blocks, hipStream_t st)
         // the buffers of the version before this frame's, which that predecessor may read
         if (s->ev_prev) RT_HIP(hipStreamWaitEvent(s->plan_st, s->ev_prev->ev, 0));
         RT_HIP(hipMemsetAsync(P.hf_plan_out, 0, sizeof(HfPlan), s->plan_st));
-        hipLaunchKernelGGL(k_hf_plan, grid, wg, 0, s->plan_st, P, uint32_t(blocks), s->hf_shift);
+        hipLaunchKernelGGL(k_hf_plan, grid, wg, 0, s->plan_st, P, uint32_t(blocks), s->hf_shift, pos16, s->hf_pos_shift);
         RT_HIP(hipEventRecord(c->pend_ev, s->plan_st));
         c->pend = P.hf_ver + 1u;
         c->pend_age = 0;
@@ -326,7 +338,7 @@ int launch_plans(rt_scene *s, const KParams& P, uint64_t blocks, hipStream_t st)
         return RT_OK;
     }
     RT_HIP(hipMemsetAsync(P.hf_plan_out, 0, sizeof(HfPlan), st));
-    hipLaunchKernelGGL(k_hf_plan, grid, wg, 0, st, P, uint32_t(blocks), s->hf_shift);
+    hipLaunchKernelGGL(k_hf_plan, grid, wg, 0, st, P, uint32_t(blocks), s->hf_shift, pos16, s->hf_pos_shift);
     if (c)
     {
         c->ver = P.hf_ver + (twice ? 2u : 1u);
@@ -350,7 +362,7 @@ int launch_plans(rt_scene *s, const KParams& P, uint64_t blocks, hipStream_t st)
             Q.wh_mark_out = const_cast<uint32_t *>(P.wh_mark_in);
         }
         RT_HIP(hipMemsetAsync(Q.hf_plan_out, 0, sizeof(HfPlan), st));
-        hipLaunchKernelGGL(k_hf_plan, grid, wg, 0, st, Q, uint32_t(blocks), s->hf_shift);
+        hipLaunchKernelGGL(k_hf_plan, grid, wg, 0, st, Q, uint32_t(blocks), s->hf_shift, pos16, s->hf_pos_shift);
     }
     RT_HIP(hipGetLastError());
     // plans on the launch stream are part of the scene's last launch: a launch on another stream orders
@@ -571,7 +583,7 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
         Q.hf_mark_in = c->marks + c->cap_blocks;
         Q.hf_mark_out = c->marks;
         const dim3 pg(uint32_t((blocks + kWG * kHfPlanPer - 1) / (kWG * kHfPlanPer)));
-        hipLaunchKernelGGL(k_hf_plan, pg, dim3(kWG), 0, st, Q, uint32_t(blocks), s->hf_shift);
+        hipLaunchKernelGGL(k_hf_plan, pg, dim3(kWG), 0, st, Q, uint32_t(blocks), s->hf_shift, s->hf_pos16, s->hf_pos_shift);
         RT_HIP(hipGetLastError());
         c->ver = 2u;
         c->proxied = true;              // the plan after this frame ranks twice (launch_plans)

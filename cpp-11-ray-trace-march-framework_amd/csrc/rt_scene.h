@@ -117,6 +117,10 @@ struct rt_scene
                                     // (<= kHfFrontMax: config 5's one launch of 324,000 blocks ran 2.731 / 2.734
                                     // ms at 2048 / 4096 against 2.741 at 1024, profiles/r05q_batch10_partition_front.json)
     uint32_t hf_shift = 2;          // RT_HF_SHIFT: heavy = cost > last max >> hf_shift (very heavy: >> 1)
+    uint32_t hf_pos16 = 16;         // RT_HF_POS16: position-aware threshold (k_hf_plan) of single-frame
+                                    // launches, sixteenths of the span left; 0: max >> hf_shift
+    uint32_t hf_pos16_batch = 0;    // RT_HF_POS16_BATCH: the same for batched launches
+    uint32_t hf_pos_shift = 4;      // RT_HF_POS_SHIFT: with it, heavy also needs cost > last max >> this
     uint32_t hf_proxy = 0;          // RT_HF_PROXY: a new shape's first frame is planned from k_hf_proxy's costs
                                     // (an A/B arm: killeroo's first frame 0.70 -> 0.63 ms, every other
                                     // scene's slower by the proxy's time)

@@ -998,6 +998,9 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
     s->hf_front_div = env_tunable("RT_HF_FRONT_DIV", s->hf_front_div);
     s->hf_front_max = env_tunable("RT_HF_FRONT_MAX", s->hf_front_max);
     s->hf_shift = std::min(env_tunable("RT_HF_SHIFT", s->hf_shift), 8u);
+    s->hf_pos16 = std::min(env_tunable("RT_HF_POS16", s->hf_pos16), 64u);
+    s->hf_pos16_batch = std::min(env_tunable("RT_HF_POS16_BATCH", s->hf_pos16_batch), 64u);
+    s->hf_pos_shift = std::min(env_tunable("RT_HF_POS_SHIFT", s->hf_pos_shift), 16u);
     s->hf_proxy = env_tunable("RT_HF_PROXY", s->hf_proxy);
     s->hf_proxy_cells = std::max(env_tunable("RT_HF_PROXY_CELLS", s->hf_proxy_cells), 1u);
     s->hf_proxy_looks = std::max(env_tunable("RT_HF_PROXY_LOOKS", s->hf_proxy_looks), 1u);

@@ -80,11 +80,14 @@ for rnd in range(A.rounds):
                 worst = 0.0
                 for r in range(n):
                     tot = 0.0
-                    for g, f, b in zip(gs, fs, bufs):
+                    for sid, g, f, b in zip(A.scenes, gs, fs, bufs):
                         if n == 1:
-                            tot += steady(lambda: g.render_frame_device(f, b.data_ptr(), st.cuda_stream))
+                            t = steady(lambda: g.render_frame_device(f, b.data_ptr(), st.cuda_stream))
                         else:
-                            tot += steady(lambda: g.render_shard_device(f, r, n, b.data_ptr(), st.cuda_stream))
+                            t = steady(lambda: g.render_shard_device(f, r, n, b.data_ptr(), st.cuda_stream))
+                        tot += t
+                        if n == 1:
+                            res.setdefault("each_scene", {}).setdefault(v, {}).setdefault(str(sid), []).append(round(t, 4))
                     worst = max(worst, tot)
                 res["per_scene"].setdefault(v, {}).setdefault(str(n), []).append(round(worst, 4))
             print(rnd, A.env, v, n, res["batch"][v][str(n)][-1], flush=True)
@@ -92,6 +95,6 @@ for rnd in range(A.rounds):
             g.close()
 summary = {v: {n: min(ts) for n, ts in d.items()} for v, d in res["batch"].items()}
 res["batch_best_of_rounds"] = summary
-print(json.dumps({"batch_best_of_rounds": summary, "per_scene": res["per_scene"]}))
+print(json.dumps({"batch_best_of_rounds": summary, "per_scene": res["per_scene"], "each_scene": res.get("each_scene")}))
 os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
 json.dump(res, open(os.path.join(ROOT, "gpurun_out", A.out + ".json"), "w"), indent=1)
