@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <utility>
 #include <cstring>
 
 #include "rt_scene.h"
@@ -417,6 +418,34 @@ HfPeek hf_peek(const rt_scene *s, const KParams& P, uint64_t blocks, int var, ui
     return HfPeek{ false, true, false };
 }
 
+// ONE device allocation per context (a new launch shape's first frame waits for the host's
+// allocation calls: seven of them took ~0.1 ms, profiles/r05i_first_frame_probe.json), the cleared
+// arrays first so one memset clears them: plans [2], ticket (+ pad to 16 B), marks [2][cap],
+// wh_marks [2][4 cap]; then cost [4 cap], lists [2][kHfFrontMax], wh_lists [2][2][kWhMax]
+// ([version][tier]).  rt_scene_create sizes the first context for kHfPreBlocks, so a first frame up
+// to that shape allocates nothing.
+int hf_alloc(HfCtx *c, uint64_t blocks)
+{
+    c->cap_blocks = 0;
+    if (c->mem) RT_HIP(hipFree(c->mem));
+    c->mem = nullptr;
+    const size_t head = sizeof(HfPlan) * 2 + 16u;
+    const size_t cleared = head + sizeof(uint32_t) * (2u + 2u * kWavesPerWG) * blocks;
+    const size_t bytes = cleared + sizeof(uint32_t) * (kWavesPerWG * blocks + 2u * kHfFrontMax + 4u * kWhMax);
+    RT_HIP(hipMalloc(&c->mem, bytes));
+    char *m = static_cast<char *>(c->mem);
+    c->plans = reinterpret_cast<HfPlan *>(m);
+    c->ticket = reinterpret_cast<uint32_t *>(m + sizeof(HfPlan) * 2);
+    c->marks = reinterpret_cast<uint32_t *>(m + head);
+    c->wh_marks = c->marks + 2u * blocks;
+    c->cost = c->wh_marks + 2u * kWavesPerWG * blocks;
+    c->lists = c->cost + kWavesPerWG * blocks;
+    c->wh_lists = c->lists + 2u * kHfFrontMax;
+    c->cleared_bytes = cleared;
+    c->cap_blocks = uint32_t(blocks);
+    return RT_OK;
+}
+
 int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hipStream_t st, uint64_t batch,
                uint64_t cam_sig)
 {
@@ -437,6 +466,11 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
             RT_HIP(hipEventSynchronize(c->pend_ev));      // its plan still writes these buffers
             c->pend = 0u;
         }
+        if (c->fence)
+        {
+            RT_HIP(hipEventSynchronize(c->fence_ev));
+            c->fence = false;
+        }
         // invalidated first: if an allocation below fails, no later launch may match the old
         // shape and read freed (null) state arrays
         std::memset(c->key, 0, sizeof(c->key));
@@ -444,30 +478,7 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
         c->proxied = false;
         c->ver = 0;
         if (blocks > c->cap_blocks || !c->mem)
-        {
-            // ONE device allocation per context (a new launch shape's first frame waits for the
-            // host's allocation calls: seven of them took ~0.1 ms, profiles/r05i_first_frame_probe.json),
-            // the cleared arrays first so one memset clears them: plans [2], ticket (+ pad to 16 B),
-            // marks [2][cap], wh_marks [2][4 cap]; then cost [4 cap], lists [2][kHfFrontMax],
-            // wh_lists [2][2][kWhMax] ([version][tier])
-            c->cap_blocks = 0;
-            if (c->mem) RT_HIP(hipFree(c->mem));
-            c->mem = nullptr;
-            const size_t head = sizeof(HfPlan) * 2 + 16u;
-            const size_t cleared = head + sizeof(uint32_t) * (2u + 2u * kWavesPerWG) * blocks;
-            const size_t bytes = cleared + sizeof(uint32_t) * (kWavesPerWG * blocks + 2u * kHfFrontMax + 4u * kWhMax);
-            RT_HIP(hipMalloc(&c->mem, bytes));
-            char *m = static_cast<char *>(c->mem);
-            c->plans = reinterpret_cast<HfPlan *>(m);
-            c->ticket = reinterpret_cast<uint32_t *>(m + sizeof(HfPlan) * 2);
-            c->marks = reinterpret_cast<uint32_t *>(m + head);
-            c->wh_marks = c->marks + 2u * blocks;
-            c->cost = c->wh_marks + 2u * kWavesPerWG * blocks;
-            c->lists = c->cost + kWavesPerWG * blocks;
-            c->wh_lists = c->lists + 2u * kHfFrontMax;
-            c->cleared_bytes = cleared;
-            c->cap_blocks = uint32_t(blocks);
-        }
+            if (int rc = hf_alloc(c, blocks)) return rc;
         RT_HIP(hipMemsetAsync(c->mem, 0, c->cleared_bytes, st));
         c->wh_cnt = s->h_wh_cnt + (c - s->hf);         // the scene's mapped counters (rt_scene_create)
         c->wh_cnt_dev = s->d_wh_cnt + (c - s->hf);
@@ -489,20 +500,43 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
     // blocks move with the view, so the plan comes from the newest view (one frame old) instead of
     // one up to kHfPeriod frames old
     P.hf_measure = measures(s, *c, cam_sig) ? 1u : 0u;
-    if (c->pend)
+    if (c->fence || c->pend)
     {
+        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+        RT_HIP(hipStreamIsCapturing(st, &cap));
+        // the adopted plan's fence (see HfCtx::fence); a capture cannot wait on an outside event, so
+        // the host waits for it there
+        if (c->fence)
+        {
+            if (hipEventQuery(c->fence_ev) == hipSuccess)
+                c->fence = false;
+            else if (cap != hipStreamCaptureStatusNone)
+            {
+                RT_HIP(hipEventSynchronize(c->fence_ev));
+                c->fence = false;
+            }
+            else if (st != c->fence_st)
+                RT_HIP(hipStreamWaitEvent(st, c->fence_ev, 0));
+        }
         // a plan on the plan stream (launch_plans): adopted by the second frame after it and by a
         // measured frame; inside a stream capture (no wait on an outside event) the current plan
         // stays and nothing is measured
-        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-        RT_HIP(hipStreamIsCapturing(st, &cap));
-        if (cap != hipStreamCaptureStatusNone)
+        if (!c->pend)
+            ;
+        else if (cap != hipStreamCaptureStatusNone)
             P.hf_measure = 0u;
         else if (P.hf_measure || c->pend_age >= 1u)
         {
             // (a plan that has finished needs no wait packet: a stream wait costs the launch stream a
-            // few us of idle chip even on a completed event)
-            if (hipEventQuery(c->pend_ev) != hipSuccess) RT_HIP(hipStreamWaitEvent(st, c->pend_ev, 0));
+            // few us of idle chip even on a completed event).  One still running becomes the fence
+            // of the frames after this one, which may run on another stream beside it.
+            if (hipEventQuery(c->pend_ev) != hipSuccess)
+            {
+                RT_HIP(hipStreamWaitEvent(st, c->pend_ev, 0));
+                std::swap(c->pend_ev, c->fence_ev);     // launch_plans records the next plan elsewhere
+                c->fence = true;
+                c->fence_st = st;
+            }
             c->ver = c->pend;
             c->pend = 0u;
         }

@@ -64,6 +64,13 @@ struct HfCtx
     // by the next frame that measures
     uint32_t pend = 0, pend_age = 0;
     hipEvent_t pend_ev = nullptr;
+    // an adopted plan still running: EVERY later frame of the shape waits for it (fence_ev), not only
+    // the adopting one -- an overlapped frame on the other stream orders only after the launch two
+    // back, and read the plan's buffers while k_hf_plan wrote them (blocks left unrendered,
+    // tools/overlap_stress.py --prebatch)
+    bool fence = false;
+    hipEvent_t fence_ev = nullptr;
+    hipStream_t fence_st = nullptr;     // the adopting frame's stream (already ordered after it)
     bool proxied = false;               // the current plan came from k_hf_proxy's costs
     uint64_t used = 0;                  // LRU stamp
     uint64_t cam = 0;                   // camera signature of the last frame (cam_signature)
@@ -213,6 +220,10 @@ struct rt_scene
 
 namespace rtk {
 
+// rt_plan.hip: one context's device state sized for `blocks` (frees the old)
+int hf_alloc(HfCtx *c, uint64_t blocks);
+// the first context's capacity at rt_scene_create: a 1080p x 4 frame's 32,640 blocks
+constexpr uint64_t kHfPreBlocks = 32768;
 // rt_plan.hip: the heavy-first / wide-section state of this launch shape (fills P.hf_*, P.wh_*)
 // batch: 0 for a single-frame launch, else an identity of the batch (its scenes and frame count)
 int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hipStream_t st, uint64_t batch = 0,

@@ -1292,6 +1292,9 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
     s->smp_cap = 64u;
     RT_HIP(hipMalloc(&s->d_smp, sizeof(float2) * s->smp_cap));
     RT_HIP(hipHostMalloc(&s->h_smp_pinned, sizeof(float2) * s->smp_cap));
+    // and the first heavy-first context's state (a new shape's first frame took ~25 us of host time
+    // in hf_prepare's hipMalloc: RT_HOST_TRACE, profiles/r05at_host_trace.log)
+    if (int rc = hf_alloc(&s->hf[0], kHfPreBlocks)) return rc;
 
     *out = s.release();
     return RT_OK;
@@ -1326,6 +1329,7 @@ int rt_scene_destroy(rt_scene *s)
             (void)hipFree(h.seg_col);
             (void)hipFree(h.seg_px);
             if (h.pend_ev) (void)hipEventDestroy(h.pend_ev);
+            if (h.fence_ev) (void)hipEventDestroy(h.fence_ev);
         }
         if (s->h_wh_cnt) (void)hipHostFree(s->h_wh_cnt);
         if (s->side) (void)hipStreamDestroy(s->side);

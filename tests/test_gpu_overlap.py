@@ -143,3 +143,40 @@ def test_overlap_single_frames(golden, scenes, sid):
             torch.cuda.synchronize()
             for o in outs:
                 assert sha(o) == golden["frames_1080p4"][str(sid)]["bgra_sha256"], (sid, i)
+
+
+def test_overlap_single_frames_after_batch(golden):
+    """The race behind a rare bad frame: a plan adopted by frame 4 of a new single-frame shape while
+    k_hf_plan still ran, and frame 5 -- overlapped on the other stream, ordered only after frame 3 --
+    read the plan's buffers mid-write (blocks never rendered).  Every later frame now waits for an
+    adopted plan that is still running (HfCtx::fence).  Reproduced 7 times in 12 by scenes that first
+    rendered config 5's overlapped batch (tools/overlap_stress.py --prebatch); here 4 fresh scene sets,
+    each frame of 16 single-frame steps of scene 4 checked against the reference's."""
+    import torch
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    want = golden["frames_1080p4"]["4"]["bgra_sha256"]
+    for rep in range(4):
+        hss = [rtm.HostScene.load(s) for s in range(10)]
+        gss = [rtm.GpuScene(h, 0) for h in hss]
+        try:
+            fs = [g.frame(W, H, SPP, kernel=rtm.RT_KERNEL_FLAG_OVERLAP) for g in gss]
+            bo = [[torch.empty(W * H, dtype=torch.int32, device="cuda") for _ in gss] for _ in range(2)]
+            outs = [torch.zeros(W * H, dtype=torch.int32, device="cuda") for _ in range(16)]
+            torch.cuda.synchronize()
+            for i in range(24):
+                rtm.render_batch_device(gss, fs, [o.data_ptr() for o in bo[i % 2]], stream=streams[i % 2].cuda_stream)
+            torch.cuda.synchronize()
+            for i in range(16):
+                s = streams[i % 2]
+                with torch.cuda.stream(s):
+                    outs[i].fill_(0x5A5A5A5A)
+                gss[4].render_frame_device(fs[4], outs[i].data_ptr(), s.cuda_stream)
+            torch.cuda.synchronize()
+            for i, o in enumerate(outs):
+                assert sha(o) == want, (rep, i)
+        finally:
+            torch.cuda.synchronize()
+            for g in gss:
+                g.close()
+            for h in hss:
+                h.close()

@@ -23,6 +23,8 @@ ap.add_argument("--steps", type=int, default=24)
 ap.add_argument("--batch", action="store_true", help="the pair (8, 1) batched instead of single frames")
 ap.add_argument("--no-flag", action="store_true", help="without RT_KERNEL_FLAG_OVERLAP (ordered launches)")
 ap.add_argument("--one-stream", action="store_true")
+ap.add_argument("--prebatch", action="store_true",
+                help="each fresh scene first renders 24 overlapped steps of config 5's ten-frame batch (as test_gpu_overlap)")
 A = ap.parse_args()
 torch.cuda.set_device(0)
 W, H, SPP = 1920, 1080, 4
@@ -42,6 +44,17 @@ for sid in ([0] if A.batch else A.scenes):
         g.close()
     for rep in range(A.reps):
         gs = [rtm.GpuScene(h, 0) for h in hss]
+        if A.prebatch:
+            others = {x: rtm.GpuScene(rtm.HostScene.load(x), 0) for x in range(10) if x not in sids}
+            allg = [gs[sids.index(x)] if x in sids else others[x] for x in range(10)]
+            bf = [g.frame(W, H, SPP, kernel=rtm.RT_KERNEL_FLAG_OVERLAP) for g in allg]
+            bo = [[torch.empty(W * H, dtype=torch.int32, device="cuda") for _ in range(10)] for _ in range(2)]
+            torch.cuda.synchronize()
+            for i in range(24):
+                rtm.render_batch_device(allg, bf, [o.data_ptr() for o in bo[i % 2]], stream=streams[i % 2].cuda_stream)
+            torch.cuda.synchronize()
+            for g in others.values():
+                g.close()
         fs = [g.frame(W, H, SPP, kernel=0 if A.no_flag else rtm.RT_KERNEL_FLAG_OVERLAP) for g in gs]
         outs = [[torch.zeros(W * H, dtype=torch.int32, device="cuda") for _ in sids] for _ in range(8)]
         torch.cuda.synchronize()        # torch's zero fill runs on its own stream, not on the render streams
