@@ -183,12 +183,15 @@ hipError_t wait_unless_done(hipStream_t st, hipEvent_t e)
 // Orders stream st after every launch of scene s that may still run: the last one (ev_last, implicit
 // on its own stream) and, when that one overlapped its predecessor (RT_KERNEL_FLAG_OVERLAP), the
 // predecessor (ev_prev).  The caller's next launch on st then follows them all.
+// The last launch becomes the "launch two back" of the next one: an overlapped launch after this one
+// on a third stream is ordered by nothing else.
 int order_all(rt_scene *s, hipStream_t st)
 {
     if (!s->ev_recorded) return RT_OK;
     if (st != s->last_stream) RT_HIP(wait_unless_done(st, s->ev_last->ev));
     if (s->ev_prev && s->prev_stream != st) RT_HIP(wait_unless_done(st, s->ev_prev->ev));
-    s->ev_prev.reset();
+    s->ev_prev = s->ev_last;
+    s->prev_stream = s->last_stream;
     return RT_OK;
 }
 

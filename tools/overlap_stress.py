@@ -23,13 +23,14 @@ ap.add_argument("--steps", type=int, default=24)
 ap.add_argument("--batch", action="store_true", help="the pair (8, 1) batched instead of single frames")
 ap.add_argument("--no-flag", action="store_true", help="without RT_KERNEL_FLAG_OVERLAP (ordered launches)")
 ap.add_argument("--one-stream", action="store_true")
+ap.add_argument("--nstreams", type=int, default=2, help="streams the steps rotate over")
 ap.add_argument("--prebatch", action="store_true",
                 help="each fresh scene first renders 24 overlapped steps of config 5's ten-frame batch (as test_gpu_overlap)")
 A = ap.parse_args()
 torch.cuda.set_device(0)
 W, H, SPP = 1920, 1080, 4
 S = 0x5A5A5A5A
-streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+streams = [torch.cuda.Stream() for _ in range(max(2, A.nstreams))]
 bad = []
 for sid in ([0] if A.batch else A.scenes):
     sids = (8, 1) if A.batch else (sid,)
@@ -59,7 +60,7 @@ for sid in ([0] if A.batch else A.scenes):
         outs = [[torch.zeros(W * H, dtype=torch.int32, device="cuda") for _ in sids] for _ in range(8)]
         torch.cuda.synchronize()        # torch's zero fill runs on its own stream, not on the render streams
         for i in range(A.steps):
-            s = streams[0 if A.one_stream else i % 2]
+            s = streams[0 if A.one_stream else i % A.nstreams]
             with torch.cuda.stream(s):
                 for o in outs[i % 8]:
                     o.fill_(S)
