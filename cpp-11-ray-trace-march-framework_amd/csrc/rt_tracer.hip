@@ -454,6 +454,13 @@ int ensure_origin_terms(rt_scene *s, const KParams& P, hipStream_t st)
     return RT_OK;
 }
 
+// AUTO's own choice of the wide section for a single-frame launch (a shard of >= 2 ranks of a scene
+// with dense cells, or a whole frame of a scene with very dense ones)
+bool auto_wide(const rt_scene *s, const KParams& P)
+{
+    return P.nranks >= 2u ? s->max_cell_refs >= s->wh_auto_refs : s->max_cell_refs >= s->wh_auto_refs_n1;
+}
+
 // Launches the render kernel over region/shard described by P (tiles_x, rank, ...).
 int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_tiles, hipStream_t st,
                   bool order_streams = true)
@@ -476,7 +483,7 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
     bool overlap = false;
     if (order_streams && (f->kernel & RT_KERNEL_FLAG_OVERLAP) && s->ev_recorded && st != s->last_stream &&
         kind == RT_KERNEL_AUTO && lanes && grid_mt && !(f->kernel & (RT_KERNEL_FLAG_WAVE_CLOCK | RT_KERNEL_FLAG_WIDE_HEAVY)) &&
-        !(P.nranks >= 2u && s->max_cell_refs >= s->wh_auto_refs) && P.spp <= 64u && !s->tab_dirty && s->fref_valid)
+        !auto_wide(s, P) && P.spp <= 64u && !s->tab_dirty && s->fref_valid)
     {
         uint32_t ob[3];
         std::memcpy(ob, P.org, sizeof(ob));
@@ -559,11 +566,12 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
     // (measured, tools/wh_probe.py, killeroo rank of 2 / 4 / 8: 0.36 / 0.33 / 0.25 ms with the
     // two-phase arm it replaced -> 0.35 / 0.20 / 0.15).  On a whole frame the
     // lanes are busy with other items anyway and the section's repeated walks cost more than they
-    // save (+1-3 %).
+    // save (+1-3 %) -- except where a cell holds >= wh_auto_refs_n1 references: scene 5 (1,226) 0.4487
+    // vs 0.4695 ms, while killeroo (426) and scene 4 (132) lose 1-6 % (profiles/r05aq_dense_scene_
+    // tunables.json, r05av_wide_n1.json).
     const bool wide_ok = auto_path && var == kVarAuto && P.spp <= 16u;
     const bool wide_heavy = wide_ok && kind == RT_KERNEL_AUTO &&
-                            ((f->kernel & RT_KERNEL_FLAG_WIDE_HEAVY) ||
-                             (P.nranks >= 2u && s->max_cell_refs >= s->wh_auto_refs));
+                            ((f->kernel & RT_KERNEL_FLAG_WIDE_HEAVY) || auto_wide(s, P));
     if (lanes && kind == RT_KERNEL_COMPACT && P.isect == RT_ISECT_GRID)
     {
         const uint32_t n_items = uint32_t(blocks * kWavesPerWG);
@@ -1017,6 +1025,7 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
     s->wh_alpha16_n2 = env_tunable("RT_WH_ALPHA16_N2", s->wh_alpha16_n2);
     s->wh_alpha16_n4 = env_tunable("RT_WH_ALPHA16_N4", s->wh_alpha16_n4);
     s->wh_auto_refs = env_tunable("RT_WH_AUTO_REFS", s->wh_auto_refs);
+    s->wh_auto_refs_n1 = env_tunable("RT_WH_AUTO_REFS_N1", s->wh_auto_refs_n1);
     s->wg64_wide = env_tunable("RT_WG64_WIDE", s->wg64_wide);
     s->wh_seg_min_ranks = env_tunable("RT_WH_SEG_MIN_RANKS", s->wh_seg_min_ranks);
     s->wg64_o8 = env_tunable("RT_WG64_O8", s->wg64_o8);
