@@ -141,11 +141,11 @@ struct rt_scene
     uint32_t wh_alpha16_n4 = 28;    // RT_WH_ALPHA16_N4: the same for a rank of 3-7 of a batched step
     uint32_t wh_auto_refs = 128;    // RT_WH_AUTO_REFS: AUTO takes the wide section for >= 2-rank
                                     // shards of scenes with a cell list this long
-    uint32_t wh_auto_refs_n1 = 1024; // RT_WH_AUTO_REFS_N1: ... and for a whole frame (one rank, single-frame
-                                    // launch) of a scene with a cell of this many references (scene 5: 1,226)
     uint32_t wg64 = 1;              // RT_WG64: AUTO launches of >= wg64_min_blocks 256-lane blocks run
     uint32_t wg64_min_blocks = 8192; // as one-wave workgroups (k_render_lanes_w64; RT_WG64_MIN_BLOCKS)
     uint32_t wg64_batch_min_blocks = 0;  // the same for batched launches (RT_WG64_BATCH_MIN_BLOCKS)
+    uint32_t wg64_max_refs = 1024;  // RT_WG64_MAX_REFS: single-frame launches of scenes with a cell of this many
+                                    // references keep 256-lane workgroups
     uint32_t wh_seg_alpha16 = 32;   // RT_WH_SEG_ALPHA16: the segmented tier's threshold, sixteenths of the span
     uint32_t wh_seg_min_ranks = 0;  // RT_WH_SEG_MIN_RANKS: a batch of >= this many ranks (spp <= 4) traces its
                                     // heaviest wide items in the segmented tier (kVarWideSeg; 0: never, the

@@ -454,11 +454,11 @@ int ensure_origin_terms(rt_scene *s, const KParams& P, hipStream_t st)
     return RT_OK;
 }
 
-// AUTO's own choice of the wide section for a single-frame launch (a shard of >= 2 ranks of a scene
-// with dense cells, or a whole frame of a scene with very dense ones)
+// AUTO's own choice of the wide section for a single-frame launch: a shard of >= 2 ranks of a scene
+// with dense cells
 bool auto_wide(const rt_scene *s, const KParams& P)
 {
-    return P.nranks >= 2u ? s->max_cell_refs >= s->wh_auto_refs : s->max_cell_refs >= s->wh_auto_refs_n1;
+    return P.nranks >= 2u && s->max_cell_refs >= s->wh_auto_refs;
 }
 
 // Launches the render kernel over region/shard described by P (tiles_x, rank, ...).
@@ -566,9 +566,7 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
     // (measured, tools/wh_probe.py, killeroo rank of 2 / 4 / 8: 0.36 / 0.33 / 0.25 ms with the
     // two-phase arm it replaced -> 0.35 / 0.20 / 0.15).  On a whole frame the
     // lanes are busy with other items anyway and the section's repeated walks cost more than they
-    // save (+1-3 %) -- except where a cell holds >= wh_auto_refs_n1 references: scene 5 (1,226) 0.4487
-    // vs 0.4695 ms, while killeroo (426) and scene 4 (132) lose 1-6 % (profiles/r05aq_dense_scene_
-    // tunables.json, r05av_wide_n1.json).
+    // save (+1-3 %).
     const bool wide_ok = auto_path && var == kVarAuto && P.spp <= 16u;
     const bool wide_heavy = wide_ok && kind == RT_KERNEL_AUTO &&
                             ((f->kernel & RT_KERNEL_FLAG_WIDE_HEAVY) || auto_wide(s, P));
@@ -607,7 +605,10 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
         // one-wave workgroups (k_render_lanes_w64): the same blocks, each wave dispatched by itself
         kfn_t lfn = fn;
         uint32_t lgrid = grid, lwg = kWG;
-        if (s->wg64 && kvar == kVarAuto && grid >= s->wg64_min_blocks)
+        // (not for a scene with very dense cells: scene 5, a cell of 1,226 references, runs its whole
+        // frame 3 % faster in 256-lane workgroups, while killeroo (426) and scene 4 (132) run 4-6 %
+        // slower that way: profiles/r05av_wg64_dense.json)
+        if (s->wg64 && kvar == kVarAuto && grid >= s->wg64_min_blocks && s->max_cell_refs < s->wg64_max_refs)
         {
             lfn = lanes_w64_kernel(kVarAuto);
             P.vblocks = grid;
@@ -1025,7 +1026,7 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
     s->wh_alpha16_n2 = env_tunable("RT_WH_ALPHA16_N2", s->wh_alpha16_n2);
     s->wh_alpha16_n4 = env_tunable("RT_WH_ALPHA16_N4", s->wh_alpha16_n4);
     s->wh_auto_refs = env_tunable("RT_WH_AUTO_REFS", s->wh_auto_refs);
-    s->wh_auto_refs_n1 = env_tunable("RT_WH_AUTO_REFS_N1", s->wh_auto_refs_n1);
+    s->wg64_max_refs = env_tunable("RT_WG64_MAX_REFS", s->wg64_max_refs);
     s->wg64_wide = env_tunable("RT_WG64_WIDE", s->wg64_wide);
     s->wh_seg_min_ranks = env_tunable("RT_WH_SEG_MIN_RANKS", s->wh_seg_min_ranks);
     s->wg64_o8 = env_tunable("RT_WG64_O8", s->wg64_o8);

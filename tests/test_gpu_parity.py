@@ -155,6 +155,38 @@ def test_full_frame_1080p4(golden, scenes, sid):
         assert sha_dev(hits) == g["hits_sha256"], (sid, i)
 
 
+def test_whole_frame_series_scene5(golden):
+    """A scene with a cell of >= 1,024 references (scene 5: 1,226) renders single frames in 256-lane
+    workgroups, not one-wave ones (RT_WG64_MAX_REFS): 36 consecutive 1080p x 4 frames
+    of a fresh scene -- the natural-order and measured frames, the measured frames 16 and 32 and the
+    plan adoptions -- each frame and its per-sample hit IDs equal the reference's."""
+    import torch
+    g = golden["frames_1080p4"]["5"]
+    hs = rtm.HostScene.load(5)
+    gs = rtm.GpuScene(hs, 0)
+    try:
+        assert gs.info()["max_cell_refs"] >= 1024
+        f = gs.frame(1920, 1080, 4)
+        out = torch.empty(1920 * 1080, dtype=torch.int32, device="cuda")
+        hits = torch.empty(1920 * 1080 * 4, dtype=torch.int32, device="cuda")
+        st = torch.cuda.current_stream().cuda_stream
+        for i in range(36):
+            out.fill_(0x5A5A5A5A)
+            if i % 4 == 1:
+                hits.fill_(0x5A5A5A5A)
+                gs.render_hits_device(f, 0, 1, out.data_ptr(), hits.data_ptr(), st)
+            else:
+                gs.render_frame_device(f, out.data_ptr(), st)
+            torch.cuda.synchronize()
+            assert sha_dev(out) == g["bgra_sha256"], i
+            if i % 4 == 1:
+                assert sha_dev(hits) == g["hits_sha256"], i
+    finally:
+        torch.cuda.synchronize()
+        gs.close()
+        hs.close()
+
+
 @pytest.mark.parametrize("sid", [1, 5, 8])
 def test_shard_hits_rank_of_8(golden, scenes, sid, monkeypatch):
     """Hit IDs of the benchmarked shard kernels at a rank of 8: every rank renders six frames of its
