@@ -483,6 +483,8 @@ class GpuWorkload:
                                          [b.data_ptr() for b in self.frames], stream=self.stream.cuda_stream)
             self.order = rtm.batch_order(self.costs)
         self.timed = [self.order[i] for i, _ in rtm.batch_chunks(len(SCENES))] if batch else list(range(len(SCENES)))
+        self.active = list(range(len(SCENES)))     # the scenes a step renders (per_scene_steps: one at a time)
+        self.latency = {}                          # kernel_ms: median of the sampled launches' own durations
 
     def stream_ctx(self, p=0):
         return self.torch.cuda.stream(self.streams[p % len(self.streams)])
@@ -525,12 +527,14 @@ class GpuWorkload:
     def _launch(self, p):
         st = self.streams[p % len(self.streams)].cuda_stream
         bufs = self.bufs[p]
-        if self.batch:
-            o = self.order
+        if self.batch and len(self.active) >= 2:
+            o = [i for i in self.order if i in self.active]
             self.rtm.render_batch_device([self.scenes[i][2] for i in o], [self.scenes[i][3] for i in o],
                                          [bufs[i].data_ptr() for i in o], self.rank, self.world, stream=st)
             return
         for i, (sid, hs, gs, f) in enumerate(self.scenes):
+            if i not in self.active:
+                continue
             if self.world == 1:
                 gs.render_frame_device(f, bufs[i].data_ptr(), st)
             else:
@@ -578,6 +582,7 @@ class GpuWorkload:
             if len(t) != want:
                 raise SystemExit(f"scene {sid}: {len(t)} kernel times for {steps} timed steps")
             out[sid] = float(np.mean(t))
+            self.latency[sid] = float(np.median(t))
             self.samples[sid] = len(t)
         if self.batch:
             return {"batch": sum(out.values())}
@@ -729,7 +734,7 @@ def run_steps(work, world, rank, steps, warmup, dist=None, graph=False, clock_wa
     work.coll = coll
     collect = coll.issue if coll is not None else None
 
-    pending = []       # the previous step's gathers: [(gathered, handle)] per scene
+    pending = []       # the previous step's gathers: [(scene index, (gathered, handle))]
     pending_set = [None]
     asm_done = [None] * nsets      # rank 0: event after the K3s that read a set's gather buffers
     it = [0]
@@ -741,7 +746,7 @@ def run_steps(work, world, rank, steps, warmup, dist=None, graph=False, clock_wa
         if asm is not None and pending:
             import torch
             with torch.cuda.stream(asm):
-                for i, (g, h) in enumerate(pending):
+                for i, (g, h) in pending:
                     if h is not None:
                         h.wait()
                     work.unshard(i, g, asm)
@@ -749,7 +754,7 @@ def run_steps(work, world, rank, steps, warmup, dist=None, graph=False, clock_wa
                 ev.record(asm)
                 asm_done[pending_set[0]] = ev
         else:
-            for i, (g, h) in enumerate(pending):
+            for i, (g, h) in pending:
                 if h is not None:
                     h.wait()
                 if rank == 0:
@@ -770,7 +775,7 @@ def run_steps(work, world, rank, steps, warmup, dist=None, graph=False, clock_wa
                 if asm_done[p] is not None:
                     # this set's gather buffers are refilled only after the K3s that read them
                     (streams[p % len(streams)] if streams else work.stream).wait_event(asm_done[p])
-                issued = [collect(p, i) for i in range(len(SCENES))]
+                issued = [(i, collect(p, i)) for i in getattr(work, "active", range(len(SCENES)))]
                 finish()
                 pending.extend(issued)
                 pending_set[0] = p
@@ -820,6 +825,46 @@ def run_steps(work, world, rank, steps, warmup, dist=None, graph=False, clock_wa
     return elapsed
 
 
+def per_scene_steps(work, world, rank, dist, steps, warmup):
+    """BASELINE.md §4 reports Cornell and killeroo separately: after the timed region, each scene ALONE
+    through the same step (its frame, or at N > 1 this rank's shard of it, the gather to rank 0 and K3,
+    with the same overlap setting), `steps` timed steps after `warmup`; max-over-ranks wall time per
+    step and its Msamples/s.  Rank 0 gets {scene: {...}}, the others None."""
+    full, graphs = list(work.active), getattr(work, "graphs", None)
+    work.graphs = None
+    res = {}
+    try:
+        for i in full:
+            work.active = [i]
+            el = run_steps(work, world, rank, steps, warmup, dist, clock_warmup=0.0)
+            ms = el / steps * 1e3
+            res[str(SCENES[i])] = {"ms_per_step": round(ms, 4), "value": round(W * H * SPP / ms / 1e3, 3),
+                                   "unit": "Msamples/s", "steps": steps, "warmup": warmup}
+    finally:
+        work.active, work.graphs = full, graphs
+    return res if rank == 0 else None
+
+
+def one_stream_steps(work, world, rank, dist, steps, warmup, kernel):
+    """The bench step again with RT_KERNEL_FLAG_OVERLAP off (every launch on one stream, each waiting for
+    the one before): the like-for-like figure of rounds before the overlap, and the per-frame latency of
+    a launch that has the chip to itself.  Rank 0 gets {value, ms_per_step, frame_latency_ms}."""
+    saved = (work.scenes, work.streams, work.overlap)
+    work.scenes = [(sid, hs, gs, gs.frame(W, H, SPP, kernel=kernel)) for sid, hs, gs, f in work.scenes]
+    work.streams, work.overlap = [work.stream], False
+    try:
+        el = run_steps(work, world, rank, steps, warmup, dist, clock_warmup=0.0)
+        work.kernel_ms(steps)
+        lat = sum(work.latency.values())
+    finally:
+        work.scenes, work.streams, work.overlap = saved
+    ms = el / steps * 1e3
+    if rank != 0:
+        return None
+    return {"value": round(len(SCENES) * W * H * SPP / ms / 1e3, 3), "unit": "Msamples/s", "ms_per_step": round(ms, 4),
+            "frame_latency_ms": round(lat, 4), "steps": steps, "warmup": warmup}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -832,6 +877,8 @@ def main():
     ap.add_argument("--no-end-to-end", action="store_true")
     ap.add_argument("--no-moving-camera", action="store_true")
     ap.add_argument("--no-first-frame", action="store_true")
+    ap.add_argument("--no-legs", action="store_true",
+                    help="skip the one-stream and per-scene legs after the timed region")
     ap.add_argument("--overlap", choices=["on", "off"], default="on",
                     help="consecutive steps' batched launches on two streams with RT_KERNEL_FLAG_OVERLAP (one "
                          "step's tail under the next step's start); off: one stream")
@@ -897,8 +944,19 @@ def main():
     elapsed = run_steps(work, world, rank, args.steps, args.warmup, dist if world > 1 else None,
                         graph=args.graph, clock_warmup=args.clock_warmup)
     kernel_ms = work.kernel_ms(args.steps)
+    latency = dict(work.latency)
     step_ms = work.span_ms(args.steps)
     drep = dist_report(work, world, rank, dist, args.steps, elapsed) if world > 1 else None
+    # the supplementary legs after the timed region (the bench value above is final): the step with one
+    # stream (no overlap), and each bench scene alone; bounded so the default run stays short
+    leg_steps, leg_warm = min(args.steps, 50), min(args.warmup, 10)
+    legs = {}
+    if args.workload == "bench" and not args.no_legs:
+        if work.overlap:
+            legs["one_stream"] = one_stream_steps(work, world, rank, dist if world > 1 else None, leg_steps,
+                                                  leg_warm, args.kernel)
+        legs["per_scene_steps"] = per_scene_steps(work, world, rank, dist if world > 1 else None, leg_steps,
+                                                  leg_warm)
     samples_per_step = len(SCENES) * W * H * SPP          # all ranks together
     value = samples_per_step * args.steps / elapsed / 1e6
 
@@ -947,6 +1005,11 @@ def main():
                                           if work.costs else None),
                        "camera": "static: each scene's own camera every step, so the per-origin "
                                  "triangle records (k_origin_pre) are computed once; see moving_camera"},
+            "overlap": work.overlap,
+            # a launch's own start-to-end time (the timed dispatches' events), median, summed over the
+            # step's launches: with overlap a launch shares the chip with its neighbour, so this is the
+            # latency of one frame, while ms_per_step is the interval between frames
+            "frame_latency_ms": round(sum(latency.values()), 4) if latency else None,
             "kernel_ms_per_step": round(step_ms, 4),
             "kernel_ms_sampled": {str(k): round(v, 4) for k, v in kernel_ms.items()},
             "per_scene": per_scene,
@@ -955,6 +1018,14 @@ def main():
         }
         if drep is not None:
             out["distributed"] = drep
+        if legs.get("one_stream"):
+            os_ = legs["one_stream"]
+            out["value_one_stream"] = os_["value"]
+            out["one_stream"] = os_
+        if legs.get("per_scene_steps"):
+            out["per_scene_steps"] = legs["per_scene_steps"]
+            out["per_scene_steps_note"] = ("each scene alone through the same step (render, and at N > 1 the "
+                                           "gather to rank 0 + K3), overlap as the main run; BASELINE.md §4")
         if args.check:
             out["check"] = check_frames(work, world)
         if args.one_device or args.dist_backend != "nccl":

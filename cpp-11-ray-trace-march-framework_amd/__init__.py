@@ -59,7 +59,7 @@ TRACER_SYMBOLS = [
     "rt_get_device_count", "rt_scene_create", "rt_scene_destroy", "rt_scene_device_bytes",
     "rt_render_tiles", "rt_render_frame_device", "rt_shard_elems", "rt_render_shard_device",
     "rt_unshard_device", "rt_last_kernel_ms", "rt_trace_samples", "rt_debug_primitives",
-    "rt_debug_rcp_check", "rt_debug_gamma_check", "rt_debug_wave_clocks", "rt_debug_heavy_first", "rt_debug_wide_items", "rt_debug_wide_tiers", "rt_scene_set_timing",
+    "rt_debug_rcp_check", "rt_debug_gamma_check", "rt_debug_wave_clocks", "rt_debug_heavy_first", "rt_debug_wide_items", "rt_debug_wide_tiers", "rt_debug_set_plan_delay", "rt_scene_set_timing",
     "rt_sample_table", "rt_last_error", "rt_abi_version", "rt_grid_build", "rt_grid_free",
     "rt_scene_create_from_mesh", "rt_kernel_times", "rt_render_frame_host", "rt_frame_host_wait", "rt_host_alloc",
     "rt_host_free", "rt_render_hits_device", "rt_scene_info_get", "rt_build_hash", "rt_render_batch_device",
@@ -130,7 +130,7 @@ class SceneInfo(ctypes.Structure):
                 ("max_cell_refs", c_u32), ("hf_floor", c_u32), ("hf_min_blocks", c_u32), ("wh_floor", c_u32),
                 ("wh_alpha16", c_u32), ("wh_auto_refs", c_u32), ("wh_fused", c_u32), ("hf_contexts", c_u32),
                 ("hf_evictions", ctypes.c_uint64), ("device_bytes", ctypes.c_uint64),
-                ("box_words", c_u32), ("wh_alpha16_n2", c_u32), ("pad0", c_u32),
+                ("box_words", c_u32), ("wh_alpha16_n2", c_u32), ("wh_lds", c_u32),
                 ("batch_launches", ctypes.c_uint64), ("batch_fallbacks", ctypes.c_uint64)]
 
 
@@ -198,6 +198,7 @@ def tracer_lib():
         if hasattr(L, "rt_debug_wide_items"):
             L.rt_debug_wide_items.argtypes = [vp, ctypes.POINTER(c_u32)]
         L.rt_debug_wide_tiers.argtypes = [vp, ctypes.POINTER(c_u32), ctypes.POINTER(c_u32)]
+        L.rt_debug_set_plan_delay.argtypes = [vp, c_u32]
         if hasattr(L, "rt_scene_set_timing"):
             L.rt_scene_set_timing.argtypes = [vp, c_u32]
         L.rt_sample_table.argtypes = [c_u32, vp]
@@ -617,8 +618,14 @@ class GpuScene:
         _check(L.rt_debug_wide_items(self._h, ctypes.byref(n)), L, "rt_debug_wide_items")
         return n.value
 
+    def set_plan_delay(self, us):
+        """Tests only: every later k_hf_plan of this scene idles `us` microseconds first
+        (rt_debug_set_plan_delay)."""
+        L = tracer_lib()
+        _check(L.rt_debug_set_plan_delay(self._h, int(us)), L, "rt_debug_set_plan_delay")
+
     def wide_tiers(self):
-        """(lane-split tier items, segmented tier items) of the newest plan (rt_debug_wide_tiers)."""
+        """(listed items, items the LDS tier renders) of the newest plan (rt_debug_wide_tiers)."""
         L = tracer_lib()
         a, b = c_u32(), c_u32()
         _check(L.rt_debug_wide_tiers(self._h, ctypes.byref(a), ctypes.byref(b)), L, "rt_debug_wide_tiers")

@@ -284,254 +284,6 @@ __device__ __forceinline__ void wide_samples(const KParams& P, uint32_t k, uint3
     }
 }
 
-// The segmented wide tier (kVarWideSeg): ONE sample per wave, its walk split into kSegs exact
-// t-segments of 16 list lanes each.  For a boundary c, S(c) = "every axis
-// crossing x_a(k) < c taken" is a state of the reference's DDA: it always steps the axis of a
-// smallest next crossing (ties in its axis order), so every crossing below c is taken before any at
-// or above it.  Segment j starts from S(T_j) -- per axis the reference's own add chain
-// x_a(k + 1) = fl(x_a(k) + dt_a) (grid.cpp:277) counted up to T_j, position start + k_a steps --
-// and walks AUTO's box runs, testing a cell (its list split 16 ways, wide_trace's butterfly for the
-// first minimum) only while the cell's exit crossing min(nct) is below T_j+1: from there the cell
-// is segment j + 1's.  Every cell of the walk is tested by exactly one segment with the reference's
-// own exit bound tb = min(t, nct_ax), and the ray's hit is the first segment's that has one (a
-// segment stops as soon as a lower one has hit: it could only find a later cell).  A segment whose
-// start lies past the grid's exit (some axis's exit crossing x_a(rem_a) < T_j) is empty.  The
-// boundaries split [enter_t, the grid exit] evenly (any values are exact; these balance the cells).
-// Checked on the CPU against the reference walk's own states: tools/segment_sim.cpp (0 mismatches
-// in 1.6 M boundaries, killeroo and room + cat).  Returns the sample's colour in every lane.
-constexpr uint32_t kSegs = 4;
-template <int VAR>
-__device__ __forceinline__ void wide_trace_seg(const KParams& P, uint32_t k, uint32_t slot, float& cr, float& cg,
-                                               float& cb, uint32_t& hit_tri)
-{
-    static_assert((VAR & kVarOriginPre) && (VAR & kVarDistSkip) && (VAR & kVarPackedRem), "AUTO layout");
-    constexpr uint32_t G = 64u / kSegs;
-    __shared__ uint32_t s_seg_hit[kWavesPerWG];     // per wave: bit j = segment j has its hit
-    volatile uint32_t *seg_hit = s_seg_hit + (threadIdx.x >> 6);
-    const uint32_t lane = threadIdx.x & 63u, seg = lane / G, sub = lane & (G - 1u);
-    const float ox = P.org[0], oy = P.org[1], oz = P.org[2];
-    cr = cg = cb = 0.0f;
-    hit_tri = rtd::kNoTri;
-    const ItemCoord ic = tile_slot_coord(P, k, slot);
-    if (!ic.valid) return;                                        // wave-uniform
-    float dx, dy, dz;
-    rtd::dir_from_xy(P.m, P.ndcx[ic.x * P.spp + ic.s], P.ndcy[ic.y * P.spp + ic.s], dx, dy, dz);
-    float nct0, nct1, nct2, dt0, dt1, dt2, enter_t = 0.0f;
-    int rem0, rem1, rem2, cs0, cs1, cs2, cell;
-    bool hit = false, exited = false;
-    float t = 0.0f, u = 0.0f, v = 0.0f;
-    uint32_t tri = 0u, exit_vox = rtd::kNoTri;
-    const bool in_grid = dda_setup(P, ox, oy, oz, dx, dy, dz, nct0, nct1, nct2, dt0, dt1, dt2, rem0, rem1, rem2, cs0,
-                                   cs1, cs2, cell, &enter_t);
-    if (in_grid)
-    {
-        if (lane == 0u) *seg_hit = 0u;
-        wave_lds_sync();
-        // the grid's exit along the ray, roughly (the first axis to run out of cells); the segment
-        // boundaries only need to be some floats, so their rounding does not matter
-        float t_end = rtd::kFltMax;
-        if (dt0 > 0.0f) t_end = __builtin_fminf(t_end, nct0 + float(rem0) * dt0);
-        if (dt1 > 0.0f) t_end = __builtin_fminf(t_end, nct1 + float(rem1) * dt1);
-        if (dt2 > 0.0f) t_end = __builtin_fminf(t_end, nct2 + float(rem2) * dt2);
-        const bool split = t_end < rtd::kFltMax && t_end > enter_t;   // else segment 0 walks it all
-        const float span = t_end - enter_t;
-        const float hi = (split && seg + 1u < kSegs) ? enter_t + span * float(seg + 1u) * (1.0f / float(kSegs))
-                                                     : __builtin_inff();
-        bool live = split || seg == 0u;
-        if (split && seg > 0u)
-        {
-            // S(lo): per axis the crossings below lo, at most rem_a + 1 (the (rem_a + 1)-th leaves the
-            // grid: the walk has ended before lo, the segment is empty)
-            const float lo = enter_t + span * float(seg) * (1.0f / float(kSegs));
-            int k0 = 0, k1 = 0, k2 = 0;
-            while (nct0 < lo && k0 <= rem0) { nct0 += dt0; k0++; }
-            while (nct1 < lo && k1 <= rem1) { nct1 += dt1; k1++; }
-            while (nct2 < lo && k2 <= rem2) { nct2 += dt2; k2++; }
-            live = k0 <= rem0 && k1 <= rem1 && k2 <= rem2;
-            rem0 -= k0; rem1 -= k1; rem2 -= k2;
-            cell += k0 * cs0 + k1 * cs1 + k2 * cs2;
-        }
-        int remp = rem0 | (rem1 << 11) | (rem2 << 22);
-        int boxw = kRemGuards;
-        cell += box_offset(P, dx, dy, dz);
-        while (live)
-        {
-            uint32_t kb = 0u, ke = 0u;
-            float nct_ax;
-            bool more;
-            if ((boxw & kRemGuards) != 0)
-            {
-                const uint32_t w = P.cellwb[uint32_t(cell)];
-                const uint32_t ne = uint32_t(int(w) >> 31);
-                kb = (w >> 11) & 0xFFFFFu;
-                ke = kb + (w & ne & 2047u);
-                boxw = int(w & ~ne);
-            }
-            // this cell is the next segment's once its exit crossing reaches hi; and nothing after
-            // a lower segment's hit can matter
-            if (!(__builtin_fminf(__builtin_fminf(nct0, nct1), nct2) < hi) || (*seg_hit & ((1u << seg) - 1u)) != 0u)
-                break;
-            RT_DDA_ADVANCE_BOX(nct_ax, more);
-            if ((uint32_t(boxw) & uint32_t(kRemGuards)) == 0u)
-            {
-                // per-lane box run (grid_intersect's): add chains to just before the box's exit
-                const uint32_t b0 = uint32_t(boxw);
-                const int f0 = boxw & 1023, f1 = (boxw >> 11) & 1023, f2 = int(uint32_t(boxw) >> 22);
-                const float tl = __builtin_fminf(__builtin_fminf(box_exit_bound(nct0, dt0, f0),
-                                                                 box_exit_bound(nct1, dt1, f1)),
-                                                 box_exit_bound(nct2, dt2, f2));
-                int c0 = 0, c1 = 0, c2 = 0;
-                while (nct0 < tl && c0 < f0) { nct0 += dt0; c0++; }
-                while (nct1 < tl && c1 < f1) { nct1 += dt1; c1++; }
-                while (nct2 < tl && c2 < f2) { nct2 += dt2; c2++; }
-                boxw -= c0 + (c1 << 11) + (c2 << 22);
-                do
-                    RT_DDA_BOX_BARE_STEP();
-                while ((uint32_t(boxw) & uint32_t(kRemGuards)) == 0u);
-                const uint32_t d = b0 - uint32_t(boxw);
-                remp = int(uint32_t(remp) - d);
-                cell += int(d & 2047u) * cs0 + int((d >> 11) & 2047u) * cs1 + int(d >> 22) * cs2;
-                more = (remp & kRemGuards) == 0;
-            }
-            if (kb < ke)
-            {
-                float bt = __builtin_fminf(rtd::kFltMax, nct_ax), bu = 0.0f, bv = 0.0f;
-                uint32_t bk = 0xFFFFFFFFu;
-                const rtd::f2v ra = {dx, dy}, rc = {dy, dz};
-                for (uint32_t q = kb + sub; q < ke; q += G)
-                {
-                    const float4 *rp = P.frefs + size_t(q) * 4u;
-                    const float4 r0 = rp[0], r1 = rp[1], r2 = rp[2], r3 = rp[3];
-                    float inv, cu;
-                    const bool ok1 = rtd::mt_rec_first<(VAR & kVarFastRcp) != 0>(
-                        ra, rc, rtd::f2v{r0.x, r0.y}, rtd::f2v{r0.z, r0.w}, rtd::f2v{r1.x, r1.y}, rtd::f2v{r1.z, r1.w},
-                        rtd::f2v{r2.x, r2.y}, inv, cu);
-                    if (__any(ok1))
-                    {
-                        float cv, ct;
-                        const bool h = ok1 & rtd::mt_rec_second(ra, rc, rtd::f2v{r2.z, r2.w}, r3.x, r3.y, inv, cu, cv, ct);
-                        const bool take = h & (ct < bt);
-                        bt = take ? ct : bt;
-                        bu = take ? cu : bu;
-                        bv = take ? cv : bv;
-                        bk = take ? q : bk;
-                    }
-                }
-                for (int m = 1; m < int(G); m <<= 1)
-                {
-                    const float ot = __shfl_xor(bt, m, 64), ou = __shfl_xor(bu, m, 64), ov = __shfl_xor(bv, m, 64);
-                    const uint32_t ok = uint32_t(__shfl_xor(int(bk), m, 64));
-                    const bool better = (ot < bt) | ((ot == bt) & (ok < bk));
-                    bt = better ? ot : bt;
-                    bu = better ? ou : bu;
-                    bv = better ? ov : bv;
-                    bk = better ? ok : bk;
-                }
-                if (bk != 0xFFFFFFFFu)
-                {
-                    t = bt;
-                    u = bu;
-                    v = bv;
-                    tri = bk;
-                    hit = true;
-                    // published in this iteration (a lane that has left the loop executes nothing
-                    // until every lane has): the higher segments stop at their next cell
-                    if (sub == 0u) atomicOr((uint32_t *)seg_hit, 1u << seg);
-                    wave_lds_sync();
-                    break;
-                }
-            }
-            if (!more)
-            {
-                exited = true;
-                exit_vox = exit_voxel(remp, cell, cs0, cs1, cs2);     // raw: in the box-word copy
-                break;
-            }
-            wave_lds_sync();
-        }
-    }
-    // the ray's outcome: the first segment with a hit (else a miss; the segment that left the grid
-    // holds the exit cell for a record)
-    const uint64_t hm = __ballot(hit && sub == 0u);
-    const bool any_hit = hm != 0u;
-    const KParams& Q = P;
-    if (any_hit)
-    {
-        const int L = int(__builtin_ctzll(hm));
-        t = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t), L));
-        u = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(u), L));
-        v = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), L));
-        tri = uint32_t(__builtin_amdgcn_readlane(int(tri), L));
-        if (Q.recs && lane == 0u)                                 // a hit's raw record (records only)
-            store_record(Q, ic.x, ic.y, ic.s, true, tri, 0u, t, u, v, kRecRawCsr);
-        tri = __float_as_uint(Q.refs[3 * size_t(tri) + 2].y);     // CSR reference -> triangle id
-        const float4 a = Q.shade[3 * tri + 0], bb = Q.shade[3 * tri + 1], c = Q.shade[3 * tri + 2];
-        rtd::shade_hit(u, v, a, bb, c, cr, cg, cb);
-        hit_tri = tri;
-    }
-    else
-    {
-        if (Q.recs)
-        {
-            const uint64_t em = __ballot(exited && sub == 0u);
-            const uint32_t vox = em ? uint32_t(__builtin_amdgcn_readlane(int(exit_vox), int(__builtin_ctzll(em))))
-                                    : rtd::kNoTri;
-            if (lane == 0u)
-                store_record(Q, ic.x, ic.y, ic.s, false, 0u, vox, 0.0f, 0.0f, 0.0f, em ? kRecRawBox : 0u);
-        }
-        cr = cg = cb = float(ic.y) / float(Q.H);                   // renderer.cpp:121
-    }
-}
-
-// One wave of the segmented tier: sample slot `slot` of local tile k (wide_trace_seg), resolved
-// with the pixel's other samples, which other waves trace: each wave stores its colour write-through
-// (sc1) into the item's slot of the scratch array and adds to the pixel's counter (agent scope, after
-// its stores have drained); the wave whose add completes the pixel sums the samples IN SAMPLE ORDER
-// from those slots (sc1 loads: another XCD's L2 may hold none of them), as renderer.cpp:87-133, and
-// stores it; it re-arms the counter for the next frame (stream-ordered after this launch).  li: the
-// item's list entry (its scratch slots: the batch's, in p[0], hf_prepare; re-read from the kernarg
-// segment after the trace, so the pointers are not held in SGPRs across it).
-template <int VAR>
-__device__ __forceinline__ void wide_seg_samples(const KParams& P, uint32_t k, uint32_t slot, uint32_t li)
-{
-    float cr, cg, cb;
-    uint32_t hit_tri = rtd::kNoTri;
-    wide_trace_seg<VAR>(P, k, slot, cr, cg, cb, hit_tri);
-    const ItemCoord ic = tile_slot_coord(P, k, slot);
-    if (!ic.valid || (threadIdx.x & 63u) != 0u) return;
-    const KParams& P0 = late_params(P, uint32_t(offsetof(KBatch, p)));
-    float4 *const col = P0.wh_col;
-    uint32_t *const cnt = P0.wh_px;
-    if (P.hits) P.hits[(size_t(ic.y) * P.W + ic.x) * P.spp + ic.s] = hit_tri;
-    if (P.recs) store_record_colour(P, ic.x, ic.y, ic.s, cr, cg, cb);
-    float sr = cr, sg = cg, sb = cb;
-    const uint32_t is = slot & 63u;                               // the sample's slot in its item
-    if (P.spp > 1u)
-    {
-        float *c = reinterpret_cast<float *>(col + size_t(li) * 64u + is);
-        __hip_atomic_store(c + 0, cr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(c + 1, cg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(c + 2, cb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        uint32_t *pc = cnt + size_t(li) * 64u + (is >> P.spp_shift);
-        const uint32_t old = __hip_atomic_fetch_add(pc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (old != P.spp - 1u) return;
-        __hip_atomic_store(pc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t s0 = is & ~(P.spp - 1u);
-        sr = sg = sb = 0.0f;
-        for (uint32_t j = 0; j < P.spp; j++)
-        {
-            const float *cj = reinterpret_cast<const float *>(col + size_t(li) * 64u + s0 + j);
-            sr += __hip_atomic_load(cj + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            sg += __hip_atomic_load(cj + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            sb += __hip_atomic_load(cj + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-    const uint32_t word = rtd::pack_bgra8(rtd::gamma_half(average(P, sr)), rtd::gamma_half(average(P, sg)),
-                                          rtd::gamma_half(average(P, sb)));
-    store_pixel(P, ic.c, ic.p, ic.x, ic.y, word);
-}
-
 // kVarWaveClock: the four words of one wave's record (rt_debug_wave_clocks): s_memtime at its start and
 // end (per clock domain: durations), and the XCD it ran on (bits 32-35 of word 2) with the low 28 bits
 // of the device-wide 100 MHz s_memrealtime at its start (word 2, bits 36-63) and end (word 3, bits
@@ -553,12 +305,9 @@ __device__ __forceinline__ void store_wave_clock(uint64_t *clk, uint32_t idx, ui
 // word keeps its lane-mode measurement until a refresh frame renders it one lane per sample again.
 // In a batch (KBatch, BATCH = true) P is p[0] (the batch's list, launch-wide item indices) and each
 // item is rendered with its own frame's parameters.
-// w: this wave's index in the section (4 per 256-lane workgroup, or one per one-wave workgroup).
-// SEG (kVarWideSeg, spp <= 4): after the G-lane tier's n * G waves, the segmented tier's items
-// (the list's second half), 64 waves per item, one sample slot each.
 // One wave's share of one listed item (wide_section): list entry li, the e-th wave of the section
-// (its clock record), TIER 1: the segmented tier's sample slot q, else the G-lane tier's wave q.
-template <bool BATCH, uint32_t G, bool CLK, int TIER>
+// (its clock record), the item's wave q.
+template <bool BATCH, uint32_t G, bool CLK>
 __device__ __forceinline__ void wide_item(const KParams& P, uint32_t li, uint32_t q, uint32_t e)
 {
     const uint32_t ipt = P.wg_per_tile * kWavesPerWG;              // items per tile
@@ -572,7 +321,7 @@ __device__ __forceinline__ void wide_item(const KParams& P, uint32_t li, uint32_
         off = uint32_t(offsetof(KBatch, p)) + f * uint32_t(sizeof(KParams));
     }
     const uint32_t kseq = item / ipt;
-    const uint32_t slot0 = (item - kseq * ipt) * 64u + (TIER == 1 ? q : q * (64u / G));
+    const uint32_t slot0 = (item - kseq * ipt) * 64u + q * (64u / G);
     // the parameters re-read per item (late_params): hoisted out of the loop they held ~30
     // more SGPRs across it and spilled
     const KParams& Q = late_params(P, off);
@@ -583,15 +332,11 @@ __device__ __forceinline__ void wide_item(const KParams& P, uint32_t li, uint32_
         r0 = __builtin_amdgcn_s_memrealtime();
         t0 = __builtin_amdgcn_s_memtime();
     }
-    if constexpr (TIER == 1)
-        wide_seg_samples<kVarWide>(Q, k, slot0, li - kWhMax);
-    else
-        wide_samples<kVarWide>(Q, k, slot0, G);
+    wide_samples<kVarWide>(Q, k, slot0, G);
     if constexpr (CLK && BATCH)
     {
         // kVarWaveClock: one record per (listed item, wave) of the section, after the batch's lane
-        // items: word 2's low bits = 0x80000000 | list entry (segmented tier: kWhMax + its entry),
-        // word 3's = the launch-wide item
+        // items: word 2's low bits = 0x80000000 | list entry, word 3's = the launch-wide item
         const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
         const KBatch& B = late_batch();
         const KParams& Q0 = late_params(P, uint32_t(offsetof(KBatch, p)));
@@ -601,25 +346,64 @@ __device__ __forceinline__ void wide_item(const KParams& P, uint32_t li, uint32_
     }
 }
 
-// SEG (kVarWideSeg, spp <= 4): after the G-lane tier's n * G waves, the segmented tier's items
-// (the list's second half), 64 waves per item, one sample slot each.  Two loops, so the two tiers'
-// code shares no live ranges (one loop over both held 80 VGPRs).
-template <bool BATCH, uint32_t G, bool CLK = false, bool SEG = false>
+// w: this wave's index in the section (4 per 256-lane workgroup, or one per one-wave workgroup).
+template <bool BATCH, uint32_t G, bool CLK = false>
 __device__ __forceinline__ void wide_section(const KParams& P, uint32_t w)
 {
-    static_assert(!SEG || BATCH, "the segmented tier's scratch is the batch's (p[0])");
     const uint32_t n = P.hf_ver ? min(P.hf_plan_in->cnt_w, kWhMax) : 0u;
     const uint32_t nw = P.wh_wgs * kWavesPerWG;
-    uint32_t e = w;
-    for (; e < n * G; e += nw) wide_item<BATCH, G, CLK, 0>(P, e / G, e % G, e);
-    if constexpr (SEG)
+    for (uint32_t e = w; e < n * G; e += nw) wide_item<BATCH, G, CLK>(P, e / G, e % G, e);
+}
+
+// The wide section's LDS tier (kVarLdsSplit): ONE listed item per 256-lane workgroup.
+// Its four waves each hold the item's 64 sample slots one lane per sample -- the lane kernel's own
+// process_item, same walk (approach, lock-step, box runs, wave-uniform scalar lists) -- so their walk
+// states are identical, and every cell list the walk tests is split between them: wave w tests
+// records kb + w, kb + w + 4, ... (test_cell), and the four local first minima are reduced through
+// LDS to the lexicographic minimum (t, list position), the reference's first minimum
+// (grid.cpp:243-267, H8), which every wave then holds: the walks stay identical.  A lone heavy wave's
+// ~1,000-record chain becomes four chains of ~250 on four SIMDs; the walk is
+// repeated four times (against 16 in the G-lane tier).  Wave 0 stores the pixels.
+template <bool BATCH, bool CLK = false>
+__device__ __forceinline__ void wide_item_lds(const KParams& P, uint32_t li)
+{
+    uint32_t item = __builtin_amdgcn_readfirstlane(P.wh_list_in[li]);
+    uint32_t off = 0u;
+    if constexpr (BATCH)
     {
-        const KParams& Q0 = late_params(P, uint32_t(offsetof(KBatch, p)));
-        const uint32_t ns = Q0.hf_ver ? min(Q0.hf_plan_in->cnt_s, kWhMax) : 0u;
-        const uint32_t n2 = Q0.hf_ver ? min(Q0.hf_plan_in->cnt_w, kWhMax) : 0u;
-        for (; e < n2 * G + ns * 64u; e += nw)
-            wide_item<BATCH, G, CLK, 1>(Q0, kWhMax + (e - n2 * G) / 64u, (e - n2 * G) % 64u, e);
+        const KBatch& B = late_batch();
+        const uint32_t f = batch_frame(B, item / kWavesPerWG);
+        item -= B.base[f] * kWavesPerWG;                          // the frame's own item index
+        off = uint32_t(offsetof(KBatch, p)) + f * uint32_t(sizeof(KParams));
     }
+    uint64_t r0 = 0, t0 = 0;
+    if constexpr (CLK && BATCH)
+    {
+        r0 = __builtin_amdgcn_s_memrealtime();
+        t0 = __builtin_amdgcn_s_memtime();
+    }
+    process_item<RT_TRI_MOLLER_TRUMBORE, kVarAuto | kVarLdsSplit>(late_params(P, off), item, off);
+    // every wave has read the last reduction before any wave starts the next item's first
+    lds_barrier();
+    if constexpr (CLK && BATCH)
+    {
+        // one record per listed item (wave 0's clocks), after the batch's lane items, as wide_item's
+        const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+        const KBatch& B = late_batch();
+        const KParams& Q0 = late_params(P, uint32_t(offsetof(KBatch, p)));
+        if (threadIdx.x == 0u)
+            store_wave_clock(Q0.wave_clk, B.base[B.nframes] * kWavesPerWG + li, t0, t1, r0, r1, 0x80000000u | li,
+                             __builtin_amdgcn_readfirstlane(Q0.wh_list_in[li]));
+    }
+}
+
+// wg: this workgroup's index in the section; the list is walked workgroup by workgroup (persistent)
+template <bool BATCH, bool CLK = false>
+__device__ __forceinline__ void wide_section_lds(const KParams& P, uint32_t wg)
+{
+    const uint32_t n = P.hf_ver ? min(P.hf_plan_in->cnt_w, kWhMax) : 0u;
+    const uint32_t nwg = P.wh_wgs;
+    for (uint32_t li = wg; li < n; li += nwg) wide_item_lds<BATCH, CLK>(P, li);
 }
 
 // Wave `wib` (0-3) of launch block bid of nblk: its work item after the heavy-first / XCD-band map.
@@ -708,6 +492,12 @@ __global__ void __launch_bounds__(kWG) k_render_wh(KParams P)
     wide_section<false, G>(P, blockIdx.x * kWavesPerWG + (threadIdx.x >> 6));
 }
 
+// the same section's LDS tier (kVarLdsSplit): one listed item per workgroup
+__global__ void __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(7, 8))) k_render_wh_lds(KParams P)
+{
+    wide_section_lds<false>(P, blockIdx.x);
+}
+
 // The multi-frame launch (KBatch): the launch's blocks are the frames' blocks, frame-major; the
 // heavy-first order (p[0]'s state) ranks them all, and every wave renders its item with its own
 // frame's parameters (KParams re-read from the kernarg segment at the frame's offset).
@@ -769,7 +559,7 @@ __device__ __forceinline__ void batch_block_wave(const KBatch& B, uint32_t bid, 
 // (The fused variant holds 83 SGPRs: 7 waves / SIMD.  Forced to 8 it spills a VGPR and measured
 // slower: rank of 4 / 8 0.256 / 0.139 ms vs 0.241 / 0.136, profiles/r03g_ab_wide_fused_*.json.)
 template <int TRI, int VAR>
-__global__ void __launch_bounds__(kWG) k_render_batch(KBatch B)
+__device__ __forceinline__ void batch_body(const KBatch& B)
 {
     __shared__ uint32_t t0s[kWavesPerWG];
     volatile uint32_t *t0v = t0s;                 // a wave's start time waits in LDS across the walk
@@ -781,14 +571,33 @@ __global__ void __launch_bounds__(kWG) k_render_batch(KBatch B)
         const uint32_t nw = B.p[0].wh_wgs;
         if (bid < nw)
         {
-            wide_section<true, (VAR & kVarWideG4) ? 4u : 16u, (VAR & kVarWaveClock) != 0, (VAR & kVarWideSeg) != 0>(
-                B.p[0], bid * kWavesPerWG + (threadIdx.x >> 6));
+            if constexpr ((VAR & kVarLdsSplit) != 0)
+                wide_section_lds<true, (VAR & kVarWaveClock) != 0>(B.p[0], bid);
+            else
+                wide_section<true, (VAR & kVarWideG4) ? 4u : 16u, (VAR & kVarWaveClock) != 0>(
+                    B.p[0], bid * kWavesPerWG + (threadIdx.x >> 6));
             return;
         }
         bid -= nw;
         nblk -= nw;
     }
-    batch_block_wave<TRI, VAR>(B, bid, nblk, threadIdx.x >> 6, t0v);
+    // (the lane blocks: one work item per wave, no split)
+    batch_block_wave<TRI, VAR & ~kVarLdsSplit>(B, bid, nblk, threadIdx.x >> 6, t0v);
+}
+
+template <int TRI, int VAR>
+__global__ void __launch_bounds__(kWG) k_render_batch(KBatch B)
+{
+    batch_body<TRI, VAR>(B);
+}
+
+// The batch kernel with the wide section's LDS tier (kVarLdsSplit), held to 7 waves / SIMD: the split
+// walk needs 80 VGPRs unbounded (6 waves for the whole grid, lane blocks included), 72 at 7 waves with
+// no spill (8 spills 36 B / lane)
+template <int TRI, int VAR>
+__global__ void __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(7, 8))) k_render_batch_lds(KBatch B)
+{
+    batch_body<TRI, VAR>(B);
 }
 
 // k_render_batch as one-wave workgroups (k_render_lanes_w64's map): the fused wide section's
@@ -804,8 +613,8 @@ __device__ __forceinline__ void batch_w64_body(const KBatch& B)
         const uint32_t nw = B.p[0].wh_wgs * kWavesPerWG;
         if (w < nw)
         {
-            wide_section<true, (VAR & kVarWideG4) ? 4u : 16u, (VAR & kVarWaveClock) != 0, (VAR & kVarWideSeg) != 0>(
-                B.p[0], w);
+            static_assert((VAR & kVarLdsSplit) == 0, "the LDS tier needs 256-lane workgroups");
+            wide_section<true, (VAR & kVarWideG4) ? 4u : 16u, (VAR & kVarWaveClock) != 0>(B.p[0], w);
             return;
         }
         w -= nw;
@@ -884,6 +693,7 @@ k_render_compact(KParams P, uint32_t n_items, uint32_t refill)
     // AUTO's box-run walk (kVarSkipRun + kVarPackedRem: box words present): packed remaining-cell
     // counts and the lane's box counts; a lane inside its empty box steps without a lookup
     constexpr bool BOX = (VAR & kVarSkipRun) && (VAR & kVarPackedRem);
+    uint32_t no_par = 0u;                        // (test_cell's LDS-tier parity: unused here)
     int remp = 0, boxw = 0;
     for (;;)
     {
@@ -1043,7 +853,7 @@ k_render_compact(KParams P, uint32_t n_items, uint32_t refill)
                 RT_DDA_ADVANCE_BOX(nct_ax, more);
                 uint32_t tests = 0u;
                 if (kb < ke &&
-                    test_cell<false, TRI, VAR>(P, ox, oy, oz, dx, dy, dz, kb, ke, nct_ax, t, u, v, tri, tests))
+                    test_cell<false, TRI, VAR>(P, ox, oy, oz, dx, dy, dz, kb, ke, nct_ax, t, u, v, tri, tests, no_par))
                 {
                     state = 2u;
                     hit = true;
@@ -1074,7 +884,7 @@ k_render_compact(KParams P, uint32_t n_items, uint32_t refill)
                 RT_DDA_ADVANCE_ADD(nct_ax, more);
                 uint32_t tests = 0u;
                 if (kb < ke &&
-                    test_cell<false, TRI, VAR>(P, ox, oy, oz, dx, dy, dz, kb, ke, nct_ax, t, u, v, tri, tests))
+                    test_cell<false, TRI, VAR>(P, ox, oy, oz, dx, dy, dz, kb, ke, nct_ax, t, u, v, tri, tests, no_par))
                 {
                     state = 2u;
                     hit = true;
@@ -1363,8 +1173,9 @@ kfn_t lanes_w64_kernel(int var)
     return var == kVarAuto ? k_render_lanes_w64<RT_TRI_MOLLER_TRUMBORE, kVarAuto> : nullptr;
 }
 
-kfn_t wide_kernel(uint32_t g)
+kfn_t wide_kernel(uint32_t g, bool lds)
 {
+    if (lds) return k_render_wh_lds;
     return g == 4u ? k_render_wh<4> : (g == 16u ? k_render_wh<16> : nullptr);
 }
 
@@ -1396,34 +1207,35 @@ kcfn_t compact_kernel(int tri, int var)
 }
 
 namespace {
-// o8: the 8-wave instantiation, built for the fused product kernels only (the segmented tier's and the
-// wave-clock arms spill to scratch when held to 8; they keep their 6-7 waves)
+// o8: the 8-wave instantiation, built for the fused product kernels only (the wave-clock arm spills to
+// scratch when held to 8; it keeps its 6-7 waves).  The LDS tier runs in 256-lane workgroups only.
 template <int VAR>
 kbfn_t batch_kernel_of(bool w64, bool o8)
 {
-    constexpr bool kO8 = (VAR & kVarWideFused) != 0 && (VAR & (kVarWideSeg | kVarWaveClock)) == 0;
-    if constexpr (kO8)
-        if (w64 && o8) return k_render_batch_w64_o8<RT_TRI_MOLLER_TRUMBORE, VAR>;
-    return w64 ? k_render_batch_w64<RT_TRI_MOLLER_TRUMBORE, VAR> : k_render_batch<RT_TRI_MOLLER_TRUMBORE, VAR>;
+    if constexpr ((VAR & kVarLdsSplit) != 0)
+        return w64 ? nullptr : k_render_batch_lds<RT_TRI_MOLLER_TRUMBORE, VAR>;
+    else
+    {
+        constexpr bool kO8 = (VAR & kVarWideFused) != 0 && (VAR & kVarWaveClock) == 0;
+        if constexpr (kO8)
+            if (w64 && o8) return k_render_batch_w64_o8<RT_TRI_MOLLER_TRUMBORE, VAR>;
+        return w64 ? k_render_batch_w64<RT_TRI_MOLLER_TRUMBORE, VAR> : k_render_batch<RT_TRI_MOLLER_TRUMBORE, VAR>;
+    }
 }
 } // namespace
 
 kbfn_t batch_kernel(int var, bool w64, bool o8)
 {
+    constexpr int kFused = kVarAuto | kVarWideHeavy | kVarWideFused;
     if (var == kVarAuto) return batch_kernel_of<kVarAuto>(w64, o8);
-    if (var == (kVarAuto | kVarWideHeavy | kVarWideFused))
-        return batch_kernel_of<kVarAuto | kVarWideHeavy | kVarWideFused>(w64, o8);
-    if (var == (kVarAuto | kVarWideHeavy | kVarWideFused | kVarWideG4))
-        return batch_kernel_of<kVarAuto | kVarWideHeavy | kVarWideFused | kVarWideG4>(w64, o8);
-    if (var == (kVarAuto | kVarWideHeavy | kVarWideFused | kVarWideSeg))
-        return batch_kernel_of<kVarAuto | kVarWideHeavy | kVarWideFused | kVarWideSeg>(w64, o8);
-    if (var == (kVarAuto | kVarWideHeavy | kVarWideFused | kVarWideSeg | kVarWaveClock))
-        return batch_kernel_of<kVarAuto | kVarWideHeavy | kVarWideFused | kVarWideSeg | kVarWaveClock>(w64, o8);
+    if (var == kFused) return batch_kernel_of<kFused>(w64, o8);
+    if (var == (kFused | kVarWideG4)) return batch_kernel_of<kFused | kVarWideG4>(w64, o8);
+    if (var == (kFused | kVarLdsSplit)) return batch_kernel_of<kFused | kVarLdsSplit>(w64, o8);
     // RT_KERNEL_FLAG_WAVE_CLOCK (debug timelines, tools/batch_waves.py): the bench pair's batched step
-    // at one rank and with the fused wide section
+    // at one rank and with the fused wide section (either tier)
     if (var == (kVarAuto | kVarWaveClock)) return batch_kernel_of<kVarAuto | kVarWaveClock>(w64, o8);
-    if (var == (kVarAuto | kVarWideHeavy | kVarWideFused | kVarWaveClock))
-        return batch_kernel_of<kVarAuto | kVarWideHeavy | kVarWideFused | kVarWaveClock>(w64, o8);
+    if (var == (kFused | kVarWaveClock)) return batch_kernel_of<kFused | kVarWaveClock>(w64, o8);
+    if (var == (kFused | kVarLdsSplit | kVarWaveClock)) return batch_kernel_of<kFused | kVarLdsSplit | kVarWaveClock>(w64, o8);
     return nullptr;
 }
 

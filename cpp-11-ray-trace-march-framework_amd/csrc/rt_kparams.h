@@ -31,7 +31,8 @@ constexpr int kVarUniform = 65536;          // scalar loop for wave-uniform cell
 constexpr int kVarWideHeavy = 524288;       // RT_KERNEL_FLAG_WIDE_HEAVY: heavy items traced wide at the start
 constexpr int kVarWideFused = 1048576;      // batch kernel: the wide section's blocks lead the same grid
 constexpr int kVarWideG4 = 2097152;         // the wide section at 4 lanes per sample (spp 8-16; else 16)
-constexpr int kVarWideSeg = 4194304;        // the wide section's segmented tier: 4 t-segments x 16 lanes per sample
+constexpr int kVarLdsSplit = 4194304;       // the wide section's LDS tier: the waves of a workgroup split one
+                                            // item's cell lists, reduced through LDS (wide_section_lds)
 // AUTO's traversal: every feature above that is exact for every scene ...
 constexpr int kVarAutoCore = kVarWaveGate | kVarDistSkip | kVarOriginPre | kVarXcdBands | kVarUniform;
 // ... plus the two that need a scene property (rt_scene::rcp_safe, rt_scene::pack_ok)
@@ -49,8 +50,7 @@ constexpr uint32_t kCompactRefill = 48;     // RT_KERNEL_COMPACT default: refill
 // sum of wave costs of the measured frame
 // sum_full: the sum of wave costs of the last measured frame that rendered every item one lane
 // per sample (the wide section's span estimate; carried over by the plans of other frames)
-// cnt_s: work items listed for the wide section's segmented tier (kVarWideSeg; the list's second half)
-struct HfPlan { uint32_t cnt_hi, cnt_lo, maxc, cnt_w; unsigned long long sum; unsigned long long sum_full; uint32_t cnt_s, pad; };
+struct HfPlan { uint32_t cnt_hi, cnt_lo, maxc, cnt_w; unsigned long long sum; unsigned long long sum_full; };
 
 struct KParams
 {
@@ -111,13 +111,14 @@ struct KParams
     const uint32_t *hf_list_in; // the current plan's front: [0, cnt_hi) and [front - cnt_lo, front)
     uint32_t *hf_list_out;      // the next plan's
     const HfPlan *hf_plan_in;   // the current plan (also the previous measurement's max and sum)
-    HfPlan *hf_plan_out;        // the next plan, cleared by the measured frame's first lane
+    HfPlan *hf_plan_out;        // the next plan (cleared by launch_plans' hipMemsetAsync before k_hf_plan)
     uint32_t *hf_cost;          // per work item: shader cycles of its wave in the measured frame
     uint32_t *hf_ticket;        // k_hf_plan's finished-workgroup count (the last one marks)
                                 // (a wide item: the sum over its waves)
     // wide section (kVarWideHeavy; wh_on == 0: off).  k_render_wh's wh_wgs workgroups trace the
     // work items the current plan lists as heavy (wh_list_in, plan->cnt_w of them), wh_g lanes
-    // per sample (16 at spp <= 4, 4 at spp 8-16), and the lane waves skip items whose
+    // per sample (16 at spp <= 4, 4 at spp 8-16) -- or, in the LDS tier (kVarLdsSplit), one
+    // 256-lane workgroup per item (wh_g = 4 waves), one lane per sample -- and the lane waves skip items whose
     // wh_mark_in == hf_ver; with wh_wgs == 0 (no list seen yet, or a refresh frame) the lane
     // waves render every item.  k_hf_plan lists an item when its lane-mode cost passes
     // max(wh_floor, wh_alpha16 / 16 x the estimated frame span), and keeps the current plan's
@@ -125,12 +126,6 @@ struct KParams
     // them) except in a refresh frame.
     uint32_t wh_on, wh_wgs, wh_refresh, wh_g;
     uint32_t wh_floor, wh_alpha16;
-    // kVarWideSeg: items above wh_seg_alpha16 / 16 of the span estimate are listed for the segmented tier
-    // (one wave per sample slot: 64 per item; the list's second half, wh_list + kWhMax; marks with bit
-    // 31), the others above wh_alpha16 / 16 for the wh_g-lane tier
-    uint32_t wh_seg, wh_seg_alpha16;
-    float4 *wh_col;             // kVarWideSeg: per list entry, the 64 sample slots' colours (cross-wave resolve)
-    uint32_t *wh_px;            // kVarWideSeg: per list entry, arrivals per pixel (<= 64 pixels)
     const uint32_t *wh_mark_in;
     uint32_t *wh_mark_out;
     const uint32_t *wh_list_in;
@@ -241,7 +236,7 @@ using kcfn_t = void (*)(KParams, uint32_t, uint32_t);
 using knfn_t = void (*)(KParams, uint32_t);
 kfn_t lanes_kernel(int tri, int var);          // k_render_lanes<tri, var>
 kfn_t lanes_w64_kernel(int var);               // k_render_lanes_w64<MT, var>
-kfn_t wide_kernel(uint32_t g);                 // k_render_wh<g>, g = 4 or 16
+kfn_t wide_kernel(uint32_t g, bool lds);       // k_render_wh<g>, g = 4 or 16; k_render_wh_lds (LDS tier)
 kfn_t pixel_loop_kernel(int tri, int var);     // k_render_pixel_loop<tri, var>
 kcfn_t compact_kernel(int tri, int var);       // k_render_compact<tri, var>(P, n_items, refill)
 kbfn_t batch_kernel(int var, bool w64, bool o8 = false);   // k_render_batch / _w64 / _w64_o8<MT, var>

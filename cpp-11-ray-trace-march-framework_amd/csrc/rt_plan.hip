@@ -25,31 +25,40 @@ namespace {
 // bench pair) took 26.6 us per plan, which a moving camera pays every frame.
 // pos16 (RT_HF_POS16, 0: off): a block is heavy when its cost exceeds pos16 / 16 of the span left
 // after its natural start (b / nblocks of the estimated span, sum of wave costs / kHfSlots) -- a
-// late block needs less to make the tail than an early one -- and last max >> pos_shift.
+// late block needs less to make the tail than an early one -- and last max >> kHfPosShift.
+constexpr uint32_t kHfPosShift = 4;
+// delay (rt_debug_set_plan_delay, tests only; 0 in the product): the kernel first idles that many
+// 100 MHz ticks, so a frame that may read the plan's buffers while it runs always finds it mid-write
+// (tests/test_gpu_overlap.py, the HfCtx::fence ordering).
 __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks, uint32_t shift, uint32_t pos16,
-                                                 uint32_t pos_shift)
+                                                 uint32_t delay)
 {
-    __shared__ uint32_t s_max, s_hi, s_lo, s_w, s_s, s_bhi, s_blo, s_bw, s_bs, s_last;
+    if (delay)
+    {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (__builtin_amdgcn_s_memrealtime() - t0 < delay) __builtin_amdgcn_s_sleep(64);
+    }
+    __shared__ uint32_t s_max, s_hi, s_lo, s_w, s_bhi, s_blo, s_bw, s_last;
     __shared__ unsigned long long s_sum;
     if (threadIdx.x == 0u)
     {
-        s_max = s_hi = s_lo = s_w = s_s = 0u;
+        s_max = s_hi = s_lo = s_w = 0u;
         s_sum = 0ull;
     }
     __syncthreads();
     const HfPlan last = *P.hf_plan_in;
     const bool tail = uint64_t(last.maxc) * kHfSlots * 16u > uint64_t(kHfTail) * (last.sum << 4);
-    const uint32_t thr = max(P.hf_floor, last.maxc >> (pos16 ? pos_shift : shift));
+    const uint32_t thr = max(P.hf_floor, last.maxc >> (pos16 ? kHfPosShift : shift));
     const uint64_t span = (last.sum << 4) / kHfSlots;
     const uint32_t b0 = blockIdx.x * (kWG * kHfPlanPer) + threadIdx.x;
-    uint32_t tmax = 0u, wmasks = 0u, smasks = 0u, heavy = 0u, hi = 0u;
+    uint32_t tmax = 0u, wmasks = 0u, heavy = 0u, hi = 0u;
     unsigned long long tsum = 0ull;
-    uint32_t rank[kHfPlanPer], wrank[kHfPlanPer], srank[kHfPlanPer];
+    uint32_t rank[kHfPlanPer], wrank[kHfPlanPer];
 #pragma unroll
     for (uint32_t j = 0; j < kHfPlanPer; j++)
     {
         const uint32_t b = b0 + j * kWG;
-        uint32_t cost = 0u, sum = 0u, wmask = 0u, smask = 0u;
+        uint32_t cost = 0u, sum = 0u, wmask = 0u;
         if (b < nblocks)
         {
             const uint4 c = reinterpret_cast<const uint4 *>(P.hf_cost)[b];      // kWavesPerWG == 4
@@ -66,28 +75,16 @@ __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks, ui
                 const uint32_t wt = max(P.wh_floor, uint32_t(min<uint64_t>(span * P.wh_alpha16 / 16u, 0xFFFFFFFFull)));
                 wmask = uint32_t(c.x > wt) | (uint32_t(c.y > wt) << 1) | (uint32_t(c.z > wt) << 2) |
                         (uint32_t(c.w > wt) << 3);
-                // the segmented tier (kVarWideSeg): the heaviest items, one wave per sample
-                if (P.wh_seg)
-                {
-                    const uint32_t ws = max(P.wh_floor, uint32_t(min<uint64_t>(span * P.wh_seg_alpha16 / 16u, 0xFFFFFFFFull)));
-                    smask = uint32_t(c.x > ws) | (uint32_t(c.y > ws) << 1) | (uint32_t(c.z > ws) << 2) |
-                            (uint32_t(c.w > ws) << 3);
-                    wmask &= ~smask;
-                }
             }
             if (P.wh_on && !P.wh_refresh && P.hf_ver)
             {
-                // sticky: the current plan's items stay listed in their tier (mark = the plan version,
-                // bit 31: the segmented tier)
+                // sticky: the current plan's items stay listed (mark = the plan version)
                 const uint4 m = reinterpret_cast<const uint4 *>(P.wh_mark_in)[b];
-                const uint32_t v = P.hf_ver, vs = P.hf_ver | 0x80000000u;
+                const uint32_t v = P.hf_ver;
                 wmask |= uint32_t(m.x == v) | (uint32_t(m.y == v) << 1) | (uint32_t(m.z == v) << 2) | (uint32_t(m.w == v) << 3);
-                smask |= uint32_t(m.x == vs) | (uint32_t(m.y == vs) << 1) | (uint32_t(m.z == vs) << 2) |
-                         (uint32_t(m.w == vs) << 3);
-                wmask &= ~smask;
             }
             // the heavy-first order ranks a block by its slowest wave left in the lane section
-            const uint32_t wm = wmask | smask;
+            const uint32_t wm = wmask;
             cost = max(max((wm & 1u) ? 0u : c.x, (wm & 2u) ? 0u : c.y), max((wm & 4u) ? 0u : c.z, (wm & 8u) ? 0u : c.w));
         }
         uint32_t tb = thr;
@@ -99,11 +96,9 @@ __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks, ui
         tsum += sum;
         rank[j] = hv ? atomicAdd(h1 ? &s_hi : &s_lo, 1u) : 0u;
         wrank[j] = wmask ? atomicAdd(&s_w, uint32_t(__popc(wmask))) : 0u;
-        srank[j] = smask ? atomicAdd(&s_s, uint32_t(__popc(smask))) : 0u;
         heavy |= uint32_t(hv) << j;
         hi |= uint32_t(h1) << j;
         wmasks |= wmask << (4u * j);
-        smasks |= smask << (4u * j);
     }
     if (tmax) atomicMax(&s_max, tmax);
     if (tsum) atomicAdd(&s_sum, tsum);
@@ -124,7 +119,6 @@ __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks, ui
         s_bhi = s_hi ? atomicAdd(&P.hf_plan_out->cnt_hi, s_hi) : 0u;
         s_blo = s_lo ? atomicAdd(&P.hf_plan_out->cnt_lo, s_lo) : 0u;
         s_bw = s_w ? atomicAdd(&P.hf_plan_out->cnt_w, s_w) : 0u;
-        s_bs = s_s ? atomicAdd(&P.hf_plan_out->cnt_s, s_s) : 0u;
     }
     __syncthreads();
 #pragma unroll
@@ -145,8 +139,8 @@ __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks, ui
         }
         // wide items: listed and marked for the next plan's frames (beyond kWhMax they stay in the
         // lane section)
-        const uint32_t wmask = (wmasks >> (4u * j)) & 15u, smask = (smasks >> (4u * j)) & 15u;
-        uint32_t wr = wrank[j], sr = srank[j];
+        const uint32_t wmask = (wmasks >> (4u * j)) & 15u;
+        uint32_t wr = wrank[j];
         for (uint32_t k = 0; k < kWavesPerWG; k++)
             if (wmask & (1u << k))
             {
@@ -156,16 +150,6 @@ __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks, ui
                 {
                     P.wh_list_out[r] = item;
                     P.wh_mark_out[item] = P.hf_ver + 1u;
-                }
-            }
-            else if (smask & (1u << k))
-            {
-                const uint32_t item = b * kWavesPerWG + k;
-                const uint32_t r = s_bs + sr++;
-                if (r < kWhMax)
-                {
-                    P.wh_list_out[kWhMax + r] = item;
-                    P.wh_mark_out[item] = (P.hf_ver + 1u) | 0x80000000u;
                 }
             }
     }
@@ -191,100 +175,8 @@ __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks, ui
         // hands the wide section's item count to the host (it sizes the section of later
         // launches) and re-arms the ticket
         if (P.wh_host_cnt)
-            *(volatile uint32_t *)P.wh_host_cnt = P.wh_g * min(vp->cnt_w, kWhMax) + 64u * min(vp->cnt_s, kWhMax);
+            *(volatile uint32_t *)P.wh_host_cnt = P.wh_g * min(vp->cnt_w, kWhMax);
         *P.hf_ticket = 0u;
-    }
-}
-
-// A new launch shape's first frame has no measured costs, and in the natural order its heaviest waves
-// start late (killeroo 1080p x 4: 0.60-0.63 ms against 0.38-0.40 planned, profiles/r05i_first_frame_
-// probe.json).  This proxy writes a cost per work item from four of its rays (sample 0 of the 4x4
-// pixel block's corners at 4 spp): a walk of the L-inf distance words (Grid::Intersect's cells, empty
-// runs skipped) without triangle tests, that counts the cells looked up and the references of the
-// first kmax non-empty cells (a ray that meets geometry mostly hits within a few of them; one that
-// grazes or misses walks on), at most lmax lookups (the kernel's time is its longest walk: uncapped,
-// killeroo's took 62 us).  It also reduces the costs' maximum and sum into `stats` (a plan's
-// measurement fields), so ONE k_hf_plan pass ranks them as if a frame had measured them.
-// Nothing here touches a pixel: it only orders the first frame's blocks.
-__global__ void __launch_bounds__(kWG) k_hf_proxy(KParams P, uint32_t nitems, uint32_t kmax, uint32_t lmax,
-                                                  uint32_t wl, uint32_t wt, HfPlan *stats)
-{
-    __shared__ uint32_t s_max;
-    __shared__ unsigned long long s_sum;
-    if (threadIdx.x == 0u)
-    {
-        s_max = 0u;
-        s_sum = 0ull;
-    }
-    __syncthreads();
-    const uint32_t g = blockIdx.x * kWG + threadIdx.x;
-    const uint32_t item = g >> 2, q = g & 3u;
-    uint32_t cost = 0u;
-    if (item < nitems)
-    {
-        const uint32_t slot = (q * 21u) & ~(P.spp - 1u);          // sample 0 of pixel 0, 5, 10, 15 at 4 spp
-        const ItemCoord ic = item_coord(P, item, slot);
-        float dx, dy, dz;
-        float nct0, nct1, nct2, dt0, dt1, dt2;
-        int rem0, rem1, rem2, cs0, cs1, cs2, cell;
-        if (ic.valid)
-        {
-            rtd::dir_from_xy(P.m, P.ndcx[ic.x * P.spp], P.ndcy[ic.y * P.spp], dx, dy, dz);
-            if (dda_setup(P, P.org[0], P.org[1], P.org[2], dx, dy, dz, nct0, nct1, nct2, dt0, dt1, dt2, rem0, rem1,
-                          rem2, cs0, cs1, cs2, cell))
-            {
-                uint32_t looks = 0u, refs = 0u, ne = 0u, skip = 0u;
-                for (;;)
-                {
-                    if (skip == 0u)
-                    {
-                        const uint32_t w = P.cellw[uint32_t(cell)];
-                        const uint32_t cnt = w & 2047u;
-                        refs += cnt;
-                        if ((cnt && ++ne >= kmax) || ++looks >= lmax) break;
-                        skip = cnt ? 0u : (w >> 11) - (w >> 11 ? 1u : 0u);
-                    }
-                    else
-                        skip--;
-                    // one DDA step along the axis of the nearest crossing; out of the grid ends it
-                    if (nct0 <= nct1 && nct0 <= nct2)
-                    {
-                        if (rem0-- == 0) break;
-                        cell += cs0;
-                        nct0 += dt0;
-                    }
-                    else if (nct1 <= nct2)
-                    {
-                        if (rem1-- == 0) break;
-                        cell += cs1;
-                        nct1 += dt1;
-                    }
-                    else
-                    {
-                        if (rem2-- == 0) break;
-                        cell += cs2;
-                        nct2 += dt2;
-                    }
-                }
-                cost = 64u * (looks * wl + refs * wt);
-            }
-            else
-                cost = 64u;
-        }
-    }
-    cost += __shfl_xor(cost, 1, 64);
-    cost += __shfl_xor(cost, 2, 64);
-    if (item < nitems && q == 0u)
-    {
-        P.hf_cost[item] = cost;
-        atomicMax(&s_max, cost);
-        atomicAdd(&s_sum, (unsigned long long)(cost >> 4));
-    }
-    __syncthreads();
-    if (threadIdx.x == 0u)
-    {
-        if (s_max) atomicMax(&stats->maxc, s_max);
-        if (s_sum) atomicAdd(&stats->sum, s_sum);
     }
 }
 
@@ -309,13 +201,12 @@ int launch_plans(rt_scene *s, const KParams& P, uint64_t blocks, hipStream_t st)
     HfCtx *c = s->hf_last;
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     RT_HIP(hipStreamIsCapturing(st, &cap));
-    // two passes: a shape's first measurement (version 0), and the first one after a proxy plan (its
-    // maximum and span are in proxy units): the second pass ranks against the first's
-    const bool twice = P.hf_ver == 0u || (c && c->proxied);
+    // two passes after a shape's first measurement (version 0): the second pass ranks against the first's
+    const bool twice = P.hf_ver == 0u;
     // the position-aware threshold for single-frame launches; a batched launch keeps max >> shift
     // (the bench pair's batched step: 0.5396 vs 0.5318 ms with it, scenes 4 / 5 in their own launches
     // 0.2486 / 0.4518 vs 0.252 / 0.46: profiles/r05ar_hf_pos_sweep.json)
-    const uint32_t pos16 = (c && c->key[4] != 0u) ? s->hf_pos16_batch : s->hf_pos16;
+    const uint32_t pos16 = (c && c->key[4] != 0u) ? 0u : s->hf_pos16;
     if (!twice && c && cap == hipStreamCaptureStatusNone)
     {
         if (!s->plan_st)
@@ -331,7 +222,7 @@ int launch_plans(rt_scene *s, const KParams& P, uint64_t blocks, hipStream_t st)
         // the buffers of the version before this frame's, which that predecessor may read
         if (s->ev_prev) RT_HIP(hipStreamWaitEvent(s->plan_st, s->ev_prev->ev, 0));
         RT_HIP(hipMemsetAsync(P.hf_plan_out, 0, sizeof(HfPlan), s->plan_st));
-        hipLaunchKernelGGL(k_hf_plan, grid, wg, 0, s->plan_st, P, uint32_t(blocks), s->hf_shift, pos16, s->hf_pos_shift);
+        hipLaunchKernelGGL(k_hf_plan, grid, wg, 0, s->plan_st, P, uint32_t(blocks), s->hf_shift, pos16, s->plan_delay);
         RT_HIP(hipEventRecord(c->pend_ev, s->plan_st));
         c->pend = P.hf_ver + 1u;
         c->pend_age = 0;
@@ -339,11 +230,10 @@ int launch_plans(rt_scene *s, const KParams& P, uint64_t blocks, hipStream_t st)
         return RT_OK;
     }
     RT_HIP(hipMemsetAsync(P.hf_plan_out, 0, sizeof(HfPlan), st));
-    hipLaunchKernelGGL(k_hf_plan, grid, wg, 0, st, P, uint32_t(blocks), s->hf_shift, pos16, s->hf_pos_shift);
+    hipLaunchKernelGGL(k_hf_plan, grid, wg, 0, st, P, uint32_t(blocks), s->hf_shift, pos16, s->plan_delay);
     if (c)
     {
         c->ver = P.hf_ver + (twice ? 2u : 1u);
-        c->proxied = false;
     }
     if (twice)
     {
@@ -363,12 +253,13 @@ int launch_plans(rt_scene *s, const KParams& P, uint64_t blocks, hipStream_t st)
             Q.wh_mark_out = const_cast<uint32_t *>(P.wh_mark_in);
         }
         RT_HIP(hipMemsetAsync(Q.hf_plan_out, 0, sizeof(HfPlan), st));
-        hipLaunchKernelGGL(k_hf_plan, grid, wg, 0, st, Q, uint32_t(blocks), s->hf_shift, pos16, s->hf_pos_shift);
+        hipLaunchKernelGGL(k_hf_plan, grid, wg, 0, st, Q, uint32_t(blocks), s->hf_shift, pos16, s->plan_delay);
     }
     RT_HIP(hipGetLastError());
     // plans on the launch stream are part of the scene's last launch: a launch on another stream orders
-    // after them, not only after the render (ev_last was the render's own stop event).  Measured frames
-    // are never overlapped, so no ev_prev refers to ev_own here.
+    // after them, not only after the render (ev_last was the render's own stop event).  Plans run here
+    // only for a shape's first two frames (never overlapped: hf_peek) and inside a stream capture (no
+    // overlap there either: launch_render / launch_batch), so no ev_prev refers to ev_own here.
     RT_HIP(hipEventRecord(s->ev_own->ev, st));
     s->ev_last = s->ev_own;
     return RT_OK;
@@ -414,15 +305,14 @@ HfPeek hf_peek(const rt_scene *s, const KParams& P, uint64_t blocks, int var, ui
     hf_key(P, blocks, var, batch, key);
     for (const HfCtx& h : s->hf)
         if (std::memcmp(h.key, key, sizeof(key)) == 0)
-            return HfPeek{ true, measures(s, h, cam_sig), h.frames >= 2u && h.pend == 0u && !h.proxied };
+            return HfPeek{ true, measures(s, h, cam_sig), h.frames >= 2u && h.pend == 0u };
     return HfPeek{ false, true, false };
 }
 
 // ONE device allocation per context (a new launch shape's first frame waits for the host's
 // allocation calls: seven of them took ~0.1 ms, profiles/r05i_first_frame_probe.json), the cleared
 // arrays first so one memset clears them: plans [2], ticket (+ pad to 16 B), marks [2][cap],
-// wh_marks [2][4 cap]; then cost [4 cap], lists [2][kHfFrontMax], wh_lists [2][2][kWhMax]
-// ([version][tier]).  rt_scene_create sizes the first context for kHfPreBlocks, so a first frame up
+// wh_marks [2][4 cap]; then cost [4 cap], lists [2][kHfFrontMax], wh_lists [2][kWhMax] (by version).  rt_scene_create sizes the first context for kHfPreBlocks, so a first frame up
 // to that shape allocates nothing.
 int hf_alloc(HfCtx *c, uint64_t blocks)
 {
@@ -431,7 +321,7 @@ int hf_alloc(HfCtx *c, uint64_t blocks)
     c->mem = nullptr;
     const size_t head = sizeof(HfPlan) * 2 + 16u;
     const size_t cleared = head + sizeof(uint32_t) * (2u + 2u * kWavesPerWG) * blocks;
-    const size_t bytes = cleared + sizeof(uint32_t) * (kWavesPerWG * blocks + 2u * kHfFrontMax + 4u * kWhMax);
+    const size_t bytes = cleared + sizeof(uint32_t) * (kWavesPerWG * blocks + 2u * kHfFrontMax + 2u * kWhMax);
     RT_HIP(hipMalloc(&c->mem, bytes));
     char *m = static_cast<char *>(c->mem);
     c->plans = reinterpret_cast<HfPlan *>(m);
@@ -475,7 +365,6 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
         // shape and read freed (null) state arrays
         std::memset(c->key, 0, sizeof(c->key));
         c->frames = 0;
-        c->proxied = false;
         c->ver = 0;
         if (blocks > c->cap_blocks || !c->mem)
             if (int rc = hf_alloc(c, blocks)) return rc;
@@ -534,8 +423,10 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
             {
                 RT_HIP(hipStreamWaitEvent(st, c->pend_ev, 0));
                 std::swap(c->pend_ev, c->fence_ev);     // launch_plans records the next plan elsewhere
+#ifndef RT_DEBUG_NO_PLAN_FENCE   // (tools/build_variant.sh: the race of DESIGN.md §4.21 made visible)
                 c->fence = true;
                 c->fence_st = st;
+#endif
             }
             c->ver = c->pend;
             c->pend = 0u;
@@ -559,13 +450,16 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
     P.hf_cost = c->cost;
     if (var & kVarWideHeavy)
     {
+        c->lds = (var & kVarLdsSplit) != 0;
         // spp <= 4: 16 lanes per sample; spp 8-16: a pixel's samples fill a wave at 4 lanes each.
         // The section holds wh_g waves per listed item of the newest plan the host has seen (a
-        // plan or two old: the count is read without waiting); at least one workgroup, since
-        // the device-side list may already be longer (the section is persistent over it).
+        // plan or two old: the count is read without waiting; the section is persistent over the
+        // device-side list, which may already be longer).  wh_wgs == 0 (no list seen yet, or a
+        // refresh frame): no section, and the lane kernel renders every item itself.
         // Refresh: every kWhRefresh-th frame renders every item one lane per sample, so the next
         // plan re-ranks all items on lane-mode costs (the wide set is otherwise sticky).
-        P.wh_g = P.spp <= 4u ? 16u : 4u;
+        // The LDS tier (kVarLdsSplit): one 256-lane workgroup per item (wh_g = its 4 waves).
+        P.wh_g = (var & kVarLdsSplit) ? kWavesPerWG : (P.spp <= 4u ? 16u : 4u);
         const uint32_t units = *(volatile uint32_t *)c->wh_cnt;         // waves: k_hf_plan counts them
         P.wh_on = 1u;
         P.wh_refresh = (c->frames - 1u) % kWhRefresh == 0u;       // frames counts this one
@@ -582,52 +476,9 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
                                                                           : s->wh_alpha16;
         P.wh_mark_in = c->wh_marks + size_t(v & 1u) * kWavesPerWG * c->cap_blocks;
         P.wh_mark_out = c->wh_marks + size_t((v + 1u) & 1u) * kWavesPerWG * c->cap_blocks;
-        // the segmented tier (kVarWideSeg): one wave per sample slot, the pixel's samples resolved
-        // across waves through the context's scratch (the counters start at 0; the last arrival of a
-        // pixel re-arms its counter)
-        P.wh_seg = (var & kVarWideSeg) ? 1u : 0u;
-        P.wh_seg_alpha16 = s->wh_seg_alpha16;
-        if (P.wh_seg && !c->seg_col)
-        {
-            RT_HIP(hipMalloc(&c->seg_col, sizeof(float4) * 64u * kWhMax));
-            RT_HIP(hipMalloc(&c->seg_px, sizeof(uint32_t) * 64u * kWhMax));
-            RT_HIP(hipMemsetAsync(c->seg_px, 0, sizeof(uint32_t) * 64u * kWhMax, st));
-        }
-        P.wh_col = c->seg_col;
-        P.wh_px = c->seg_px;
-        P.wh_list_in = c->wh_lists + size_t(v & 1u) * 2u * kWhMax;
-        P.wh_list_out = c->wh_lists + size_t((v + 1u) & 1u) * 2u * kWhMax;
+        P.wh_list_in = c->wh_lists + size_t(v & 1u) * kWhMax;
+        P.wh_list_out = c->wh_lists + size_t((v + 1u) & 1u) * kWhMax;
         P.wh_host_cnt = c->wh_cnt_dev;
-    }
-    // a new shape's first frame (one frame, no wide section): a plan from the cost proxy
-    if (c->frames == 1u && !batch && P.hf_front && !P.wh_on && s->hf_proxy && P.cellw && P.spp <= 64u)
-    {
-        // the proxy's costs and their maximum / sum as version 1's measurement, then one plan pass
-        // (version 1 -> 2) on the launch stream; every array it touches was cleared with the context
-        const uint32_t nitems = uint32_t(blocks) * kWavesPerWG;
-        hipLaunchKernelGGL(k_hf_proxy, dim3((4u * nitems + kWG - 1u) / kWG), dim3(kWG), 0, st, P, nitems,
-                           s->hf_proxy_cells, s->hf_proxy_looks, s->hf_proxy_wl, s->hf_proxy_wt, c->plans + 1);
-        KParams Q = P;
-        Q.hf_floor = 0u;                // proxy units: only the plan's relative thresholds apply
-        Q.hf_ver = 1u;
-        Q.hf_plan_in = c->plans + 1;
-        Q.hf_plan_out = c->plans;
-        Q.hf_list_in = c->lists + kHfFrontMax;
-        Q.hf_list_out = c->lists;
-        Q.hf_mark_in = c->marks + c->cap_blocks;
-        Q.hf_mark_out = c->marks;
-        const dim3 pg(uint32_t((blocks + kWG * kHfPlanPer - 1) / (kWG * kHfPlanPer)));
-        hipLaunchKernelGGL(k_hf_plan, pg, dim3(kWG), 0, st, Q, uint32_t(blocks), s->hf_shift, s->hf_pos16, s->hf_pos_shift);
-        RT_HIP(hipGetLastError());
-        c->ver = 2u;
-        c->proxied = true;              // the plan after this frame ranks twice (launch_plans)
-        P.hf_ver = c->ver;
-        P.hf_mark_in = c->marks + size_t(c->ver & 1u) * c->cap_blocks;
-        P.hf_mark_out = c->marks + size_t((c->ver + 1u) & 1u) * c->cap_blocks;
-        P.hf_list_in = c->lists + size_t(c->ver & 1u) * kHfFrontMax;
-        P.hf_list_out = c->lists + size_t((c->ver + 1u) & 1u) * kHfFrontMax;
-        P.hf_plan_in = c->plans + (c->ver & 1u);
-        P.hf_plan_out = c->plans + ((c->ver + 1u) & 1u);
     }
     return RT_OK;
 }

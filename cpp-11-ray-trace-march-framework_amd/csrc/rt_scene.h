@@ -55,8 +55,7 @@ struct HfCtx
     uint32_t *wh_lists = nullptr;       // [2][kWhMax]
     uint32_t *wh_cnt = nullptr;         // host-mapped: the newest plan's wide item count (rt_scene::h_wh_cnt)
     uint32_t *wh_cnt_dev = nullptr;     // its device address
-    float4 *seg_col = nullptr;          // kVarWideSeg scratch: [kWhMax][64] sample colours
-    uint32_t *seg_px = nullptr;         // kVarWideSeg scratch: [kWhMax][64] arrivals per pixel
+    bool lds = false;                   // its wide section runs the LDS tier (kVarLdsSplit; rt_debug_wide_tiers)
     uint32_t frames = 0;                // frames rendered with this shape
     uint32_t ver = 0;                   // version of the plan the frames use
     // a plan launched on the scene's plan stream after a measured frame (launch_plans): version pend
@@ -71,7 +70,6 @@ struct HfCtx
     bool fence = false;
     hipEvent_t fence_ev = nullptr;
     hipStream_t fence_st = nullptr;     // the adopting frame's stream (already ordered after it)
-    bool proxied = false;               // the current plan came from k_hf_proxy's costs
     uint64_t used = 0;                  // LRU stamp
     uint64_t cam = 0;                   // camera signature of the last frame (cam_signature)
 };
@@ -119,22 +117,13 @@ struct rt_scene
     // launch path never calls getenv
     uint32_t hf_floor = 100000;     // RT_HF_FLOOR: heavy-first threshold floor, shader cycles
     uint32_t hf_min_blocks = 4096;  // RT_HF_MIN_BLOCKS: smallest whole launch taking the heavy-first order
-    uint32_t hf_front_div = 8;      // RT_HF_FRONT_DIV: the front section holds 1 / this of a launch's blocks ...
-    uint32_t hf_front_max = 1024;   // RT_HF_FRONT_MAX: ... at most this many, or 1 / 128 of the blocks if more
+    uint32_t hf_front_div = 8;      // the front section holds 1 / this of a launch's blocks ...
+    uint32_t hf_front_max = 1024;   // ... at most this many, or 1 / 128 of the blocks if more
                                     // (<= kHfFrontMax: config 5's one launch of 324,000 blocks ran 2.731 / 2.734
                                     // ms at 2048 / 4096 against 2.741 at 1024, profiles/r05q_batch10_partition_front.json)
     uint32_t hf_shift = 2;          // RT_HF_SHIFT: heavy = cost > last max >> hf_shift (very heavy: >> 1)
     uint32_t hf_pos16 = 16;         // RT_HF_POS16: position-aware threshold (k_hf_plan) of single-frame
                                     // launches, sixteenths of the span left; 0: max >> hf_shift
-    uint32_t hf_pos16_batch = 0;    // RT_HF_POS16_BATCH: the same for batched launches
-    uint32_t hf_pos_shift = 4;      // RT_HF_POS_SHIFT: with it, heavy also needs cost > last max >> this
-    uint32_t hf_proxy = 0;          // RT_HF_PROXY: a new shape's first frame is planned from k_hf_proxy's costs
-                                    // (an A/B arm: killeroo's first frame 0.70 -> 0.63 ms, every other
-                                    // scene's slower by the proxy's time)
-    uint32_t hf_proxy_cells = 6;    // RT_HF_PROXY_CELLS: non-empty cells a proxy ray counts ...
-    uint32_t hf_proxy_looks = 32;   // RT_HF_PROXY_LOOKS: ... in at most this many lookups
-    uint32_t hf_proxy_wl = 4;       // RT_HF_PROXY_WL / _WT: weight of a cell lookup / of a reference
-    uint32_t hf_proxy_wt = 1;
     uint32_t wh_floor = 100000;     // RT_WH_FLOOR: wide-section threshold floor, shader cycles
     uint32_t wh_alpha16 = 32;       // RT_WH_ALPHA16: wide threshold, sixteenths of the estimated span
     uint32_t wh_alpha16_n2 = 16;    // RT_WH_ALPHA16_N2: the same for a rank of 2 of a batched step
@@ -143,17 +132,17 @@ struct rt_scene
                                     // shards of scenes with a cell list this long
     uint32_t wg64 = 1;              // RT_WG64: AUTO launches of >= wg64_min_blocks 256-lane blocks run
     uint32_t wg64_min_blocks = 8192; // as one-wave workgroups (k_render_lanes_w64; RT_WG64_MIN_BLOCKS)
-    uint32_t wg64_batch_min_blocks = 0;  // the same for batched launches (RT_WG64_BATCH_MIN_BLOCKS)
+    uint32_t wg64_batch_min_blocks = 0;  // the same for batched launches
     uint32_t wg64_max_refs = 1024;  // RT_WG64_MAX_REFS: single-frame launches of scenes with a cell of this many
                                     // references keep 256-lane workgroups
-    uint32_t wh_seg_alpha16 = 32;   // RT_WH_SEG_ALPHA16: the segmented tier's threshold, sixteenths of the span
-    uint32_t wh_seg_min_ranks = 0;  // RT_WH_SEG_MIN_RANKS: a batch of >= this many ranks (spp <= 4) traces its
-                                    // heaviest wide items in the segmented tier (kVarWideSeg; 0: never, the
-                                    // default: measured slower)
+    uint32_t wh_lds = 0xE;          // RT_WH_LDS: bit log2(N) (3: N >= 8): a rank of N's wide section runs the LDS
+                                    // tier (kVarLdsSplit: one 256-lane workgroup per item, its cell lists split
+                                    // between the four waves) instead of 16 lanes per sample
     uint32_t wg64_o8 = 0x2;         // RT_WG64_O8: bit log2(N) (3: N >= 8): a rank of N's fused one-wave
                                     // batch kernel held to 8 waves / SIMD
     uint32_t wg64_wide = 0xA;       // RT_WG64_WIDE: bit log2(N) (3: N >= 8): one-wave workgroups also
                                     // for a rank of N's batch with a wide section
+    uint32_t plan_delay = 0;        // rt_debug_set_plan_delay: k_hf_plan idles this many 100 MHz ticks first (tests)
     uint32_t hf_follow = 1;         // RT_HF_FOLLOW: re-plan the heavy-first order on every frame whose
                                     // camera moved (0: every kHfPeriod-th frame only)
     bool octant_words = false;      // 8 ray-octant copies of the empty-run words (else one L-inf word)
@@ -193,8 +182,12 @@ struct rt_scene
     hipStream_t plan_st = nullptr;       // k_hf_plan after a measured frame, beside the next frame
     hipEvent_t kt0[kTimeRing] = {};
     rtk::EvRef kt1[kTimeRing];          // a timed launch's stop event (also its ev_last)
-    unsigned ev_time_flags = hipEventDefault;            // kt0 / kt1 (RT_EVENT_SYSFENCE, rt_scene_create)
-    unsigned ev_order_flags = hipEventDisableTiming;     // ev1, ev_fork, ev_join
+    // The library's own events order device work (a scene's frames on different streams; the side-stream
+    // fork / join) or time kernels (kt0 / kt1); none of them hands memory to the host.  A default event
+    // record ends in a system-scope release (L2 write-back and invalidate), which the next frame pays in
+    // refetches; device scope is enough for these.  The host-visible band / tile events keep the default.
+    unsigned ev_time_flags = hipEventDisableSystemFence;                         // kt0 / kt1
+    unsigned ev_order_flags = hipEventDisableTiming | hipEventReleaseToDevice;   // ev_own, ev_fork, ev_join
     uint32_t kt_next = 0, kt_count = 0;
     uint32_t kt_last = kTimeRing;   // ring slot of the last timed launch (kTimeRing: none)
     uint32_t time_every = kTimeEvery; // rt_scene_set_timing: time every n-th launch (0: none)

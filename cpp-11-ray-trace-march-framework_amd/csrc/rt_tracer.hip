@@ -480,8 +480,12 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
     // section's side-stream pair, not the wave clocks), the same tables and camera origin, and an
     // existing launch shape whose frame is not measured.
     // (order_streams false: the caller orders its streams itself, rt_render_frame_host_tiled)
+    // No overlap inside a stream capture: plans there run on the launch stream (launch_plans).
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    RT_HIP(hipStreamIsCapturing(st, &cap));
     bool overlap = false;
-    if (order_streams && (f->kernel & RT_KERNEL_FLAG_OVERLAP) && s->ev_recorded && st != s->last_stream &&
+    if (order_streams && cap == hipStreamCaptureStatusNone && (f->kernel & RT_KERNEL_FLAG_OVERLAP) && s->ev_recorded &&
+        st != s->last_stream &&
         kind == RT_KERNEL_AUTO && lanes && grid_mt && !(f->kernel & (RT_KERNEL_FLAG_WAVE_CLOCK | RT_KERNEL_FLAG_WIDE_HEAVY)) &&
         !auto_wide(s, P) && P.spp <= 64u && !s->tab_dirty && s->fref_valid)
     {
@@ -526,8 +530,6 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
     else if (lanes && P.isect == RT_ISECT_BRUTE_FORCE)
         var = kVarBrute;
     // kernel-time events only outside stream capture (a captured record has no time to read)
-    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    RT_HIP(hipStreamIsCapturing(st, &cap));
     // A timed event pair costs ~10 us of device time per launch (measured: bench step 0.755 ->
     // 0.736 ms without), so only every time_every-th launch is timed (rt_scene_set_timing)
     const bool timed = cap == hipStreamCaptureStatusNone && s->time_every && s->launches % s->time_every == 0u;
@@ -596,9 +598,12 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
         // (and every wide-section launch of >= 64 blocks: its lane kernel's heaviest items)
         const bool front = kind == RT_KERNEL_AUTO && P.isect == RT_ISECT_GRID && !(kvar & kVarWaveClock) &&
                            (blocks >= s->hf_min_blocks || (wide_heavy && blocks >= 64u));
+        // the wide section's LDS tier (kVarLdsSplit) per rank count (wh_lds, bit log2 N)
+        const uint32_t lg_ranks = P.nranks >= 8u ? 3u : (P.nranks >= 4u ? 2u : (P.nranks >= 2u ? 1u : 0u));
+        const bool lds = wide_heavy && ((s->wh_lds >> lg_ranks) & 1u) != 0u;
         if (front || wide_heavy)
         {
-            if (int rc = hf_prepare(s, P, blocks, kvar, front, st)) return rc;
+            if (int rc = hf_prepare(s, P, blocks, kvar | (lds ? kVarLdsSplit : 0), front, st)) return rc;
             g_ht.mark("hf_prepare");
             grid += P.hf_front;
         }
@@ -629,7 +634,7 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
             }
             RT_HIP(hipEventRecord(s->ev_fork, st));
             RT_HIP(hipStreamWaitEvent(s->side, s->ev_fork, 0));
-            hipLaunchKernelGGL(wide_kernel(P.wh_g), dim3(P.wh_wgs), wg, 0, s->side, P);
+            hipLaunchKernelGGL(wide_kernel(P.wh_g, lds), dim3(P.wh_wgs), wg, 0, s->side, P);
         }
         if (P.wh_wgs)
         {
@@ -722,10 +727,13 @@ int launch_batch(rt_scene *const *S, const rt_frame *F, uint32_t n, KParams *P, 
     // removed in round 5)
     const bool fused = wide_heavy;
     const bool clk = (F[0].kernel & RT_KERNEL_FLAG_WAVE_CLOCK) != 0u;
-    // the segmented tier (kVarWideSeg): a rank of >= wh_seg_min_ranks at spp <= 4
-    const bool seg = fused && spp <= 4u && S[0]->wh_seg_min_ranks != 0u && P[0].nranks >= S[0]->wh_seg_min_ranks;
+    const uint32_t lg_ranks = P[0].nranks >= 8u ? 3u : (P[0].nranks >= 4u ? 2u : (P[0].nranks >= 2u ? 1u : 0u));
+    // the section's LDS tier (kVarLdsSplit) per rank count (wh_lds, bit log2 N): one
+    // 256-lane workgroup per listed item, so the whole grid runs 256-lane workgroups
+    const bool lds = fused && ((S[0]->wh_lds >> lg_ranks) & 1u) != 0u;
     const int kvar = var | (wide_heavy ? kVarWideHeavy : 0) | (fused ? kVarWideFused : 0) |
-                     (fused && spp > 4u ? kVarWideG4 : 0) | (seg ? kVarWideSeg : 0) | (clk ? kVarWaveClock : 0);
+                     (fused && spp > 4u && !lds ? kVarWideG4 : 0) | (lds ? kVarLdsSplit : 0) |
+                     (clk ? kVarWaveClock : 0);
     if (!batch_kernel(kvar, false)) return RT_E_INVALID;
     const uint32_t wgpt = (kTilePix * spp) / kWG;
     const uint64_t fblocks = uint64_t(n_local_tiles) * wgpt;
@@ -754,9 +762,12 @@ int launch_batch(rt_scene *const *S, const rt_frame *F, uint32_t n, KParams *P, 
     // between them: the frame tables and the per-origin records stay, the batch's heavy-first
     // context exists and this frame is not measured (a measured frame clears and rewrites plan
     // buffers that an older version's frames read), no wave clocks or segmented-tier scratch
-    // (per-scene buffers).  At most two launches of a scene are in flight: an overlapped launch
-    // waits for the one before the launch it overlaps (ev_prev).
-    bool overlap = !clk && !seg;
+    // (per-scene buffers), no stream capture (its plans run on the launch stream).  At most two
+    // launches of a scene are in flight: an overlapped launch waits for the one before the launch it
+    // overlaps (ev_prev).
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    RT_HIP(hipStreamIsCapturing(st, &cap));
+    bool overlap = !clk && cap == hipStreamCaptureStatusNone;
     for (uint32_t i = 0; i < n; i++)
     {
         uint32_t ob[3];
@@ -798,8 +809,7 @@ int launch_batch(rt_scene *const *S, const rt_frame *F, uint32_t n, KParams *P, 
     // log2 N, 3 for N >= 8): with the section fused from 2 ranks and one-wave workgroups on both
     // (profiles/r03aa_wg64_wide_*.json) a rank of 2 took 0.306 ms (0.321 with 256-lane ones, 0.338
     // unfused), of 8 0.117 (0.121); a rank of 4 0.206 vs 0.193, so 4 keeps 256-lane workgroups
-    const uint32_t lg_ranks = P[0].nranks >= 8u ? 3u : (P[0].nranks >= 4u ? 2u : (P[0].nranks >= 2u ? 1u : 0u));
-    const bool w64 = s0->wg64 != 0u && (!wide_heavy || ((s0->wg64_wide >> lg_ranks) & 1u) != 0u) &&
+    const bool w64 = s0->wg64 != 0u && !lds && (!wide_heavy || ((s0->wg64_wide >> lg_ranks) & 1u) != 0u) &&
                      uint32_t(blocks) + P[0].hf_front >= s0->wg64_batch_min_blocks;
     uint32_t bwg = kWG;
     if (w64)
@@ -816,7 +826,7 @@ int launch_batch(rt_scene *const *S, const rt_frame *F, uint32_t n, KParams *P, 
     if (clk)
     {
         // one record per lane item and per (listed item, wave) of the wide section
-        const size_t need = (size_t(blocks) * kWavesPerWG + size_t(kWhMax) * (16u + 64u)) * 4u;
+        const size_t need = (size_t(blocks) * kWavesPerWG + size_t(kWhMax) * 16u) * 4u;
         if (need > s0->clk_cap)
         {
             if (s0->d_clk) RT_HIP(hipFree(s0->d_clk));
@@ -830,8 +840,6 @@ int launch_batch(rt_scene *const *S, const rt_frame *F, uint32_t n, KParams *P, 
     }
     for (uint32_t i = 0; i < n; i++) KB.p[i] = P[i];
     // timing: scene 0's ring (one timed launch for the whole batch)
-    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    RT_HIP(hipStreamIsCapturing(st, &cap));
     const bool timed = cap == hipStreamCaptureStatusNone && s0->time_every && s0->launches % s0->time_every == 0u;
     s0->launches++;
     const uint32_t kslot = s0->kt_next;
@@ -949,6 +957,7 @@ int rt_scene_info_get(rt_scene *s, rt_scene_info *out)
     out->wh_floor = s->wh_floor;
     out->wh_alpha16 = s->wh_alpha16;
     out->wh_alpha16_n2 = s->wh_alpha16_n2;
+    out->wh_lds = s->wh_lds;
     out->wh_auto_refs = s->wh_auto_refs;
     out->wh_fused = 1;
     out->hf_contexts = kHfCtxs;
@@ -1007,20 +1016,10 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
     // scheduling tunables: read once here, never per launch (A/B sweeps set them per scene)
     s->hf_floor = env_tunable("RT_HF_FLOOR", s->hf_floor);
     s->hf_min_blocks = env_tunable("RT_HF_MIN_BLOCKS", s->hf_min_blocks);
-    s->hf_front_div = env_tunable("RT_HF_FRONT_DIV", s->hf_front_div);
-    s->hf_front_max = env_tunable("RT_HF_FRONT_MAX", s->hf_front_max);
     s->hf_shift = std::min(env_tunable("RT_HF_SHIFT", s->hf_shift), 8u);
     s->hf_pos16 = std::min(env_tunable("RT_HF_POS16", s->hf_pos16), 64u);
-    s->hf_pos16_batch = std::min(env_tunable("RT_HF_POS16_BATCH", s->hf_pos16_batch), 64u);
-    s->hf_pos_shift = std::min(env_tunable("RT_HF_POS_SHIFT", s->hf_pos_shift), 16u);
-    s->hf_proxy = env_tunable("RT_HF_PROXY", s->hf_proxy);
-    s->hf_proxy_cells = std::max(env_tunable("RT_HF_PROXY_CELLS", s->hf_proxy_cells), 1u);
-    s->hf_proxy_looks = std::max(env_tunable("RT_HF_PROXY_LOOKS", s->hf_proxy_looks), 1u);
-    s->hf_proxy_wl = env_tunable("RT_HF_PROXY_WL", s->hf_proxy_wl);
-    s->hf_proxy_wt = env_tunable("RT_HF_PROXY_WT", s->hf_proxy_wt);
     s->wg64 = env_tunable("RT_WG64", s->wg64);
     s->wg64_min_blocks = env_tunable("RT_WG64_MIN_BLOCKS", s->wg64_min_blocks);
-    s->wg64_batch_min_blocks = env_tunable("RT_WG64_BATCH_MIN_BLOCKS", s->wg64_batch_min_blocks);
     s->wh_floor = env_tunable("RT_WH_FLOOR", s->wh_floor);
     s->wh_alpha16 = env_tunable("RT_WH_ALPHA16", s->wh_alpha16);
     s->wh_alpha16_n2 = env_tunable("RT_WH_ALPHA16_N2", s->wh_alpha16_n2);
@@ -1028,20 +1027,9 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
     s->wh_auto_refs = env_tunable("RT_WH_AUTO_REFS", s->wh_auto_refs);
     s->wg64_max_refs = env_tunable("RT_WG64_MAX_REFS", s->wg64_max_refs);
     s->wg64_wide = env_tunable("RT_WG64_WIDE", s->wg64_wide);
-    s->wh_seg_min_ranks = env_tunable("RT_WH_SEG_MIN_RANKS", s->wh_seg_min_ranks);
     s->wg64_o8 = env_tunable("RT_WG64_O8", s->wg64_o8);
-    s->wh_seg_alpha16 = env_tunable("RT_WH_SEG_ALPHA16", s->wh_seg_alpha16);
+    s->wh_lds = env_tunable("RT_WH_LDS", s->wh_lds);
     s->hf_follow = env_tunable("RT_HF_FOLLOW", s->hf_follow);
-    // The library's own events order device work (ev1: a scene's frames on different streams; the
-    // side-stream fork / join) or time kernels (kt0 / kt1); none of them hands memory to the host.
-    // A default event record ends in a system-scope release (L2 write-back and invalidate), which
-    // the next frame pays in refetches; device scope is enough for these (RT_EVENT_SYSFENCE=1: the
-    // default flags, A/B).  The host-visible band / tile events keep the default.
-    if (env_tunable("RT_EVENT_SYSFENCE", 0u) == 0u)
-    {
-        s->ev_time_flags = hipEventDisableSystemFence;
-        s->ev_order_flags = hipEventDisableTiming | hipEventReleaseToDevice;
-    }
     for (int a = 0; a < 3; a++)
     {
         s->dims[a] = g.dims[a];
@@ -1141,9 +1129,9 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
         // count as empty).  j steps of a walk in that octant move each coordinate by 0..j in the
         // octant's direction, so the next D-1 cells are empty -- the same contract as the L-inf
         // word, and D >= the L-inf distance.  D(c) = 1 + min of D over the 7 forward neighbours
-        // (the 3-D largest-square recurrence).  RT_OCT_DIST=0 keeps the L-inf words (A/B arm),
-        // and so does a grid whose 8 copies would pass kOctWordsMaxBytes (they measured ~2 %).
-        if (env_tunable("RT_OCT_DIST", 1u) != 0u && uint64_t(nc) * 8u * 4u <= kOctWordsMaxBytes)
+        // (the 3-D largest-square recurrence).  A grid whose 8 copies would pass kOctWordsMaxBytes keeps
+        // the L-inf words (they measured ~2 % slower, profiles/r02x_ab_octant_dist.json).
+        if (uint64_t(nc) * 8u * 4u <= kOctWordsMaxBytes)
         {
             s->octant_words = true;
             constexpr uint32_t kInf = 0x1FFFFFu;
@@ -1339,8 +1327,6 @@ int rt_scene_destroy(rt_scene *s)
         for (HfCtx& h : s->hf)
         {
             (void)hipFree(h.mem);
-            (void)hipFree(h.seg_col);
-            (void)hipFree(h.seg_px);
             if (h.pend_ev) (void)hipEventDestroy(h.pend_ev);
             if (h.fence_ev) (void)hipEventDestroy(h.fence_ev);
         }
@@ -1532,6 +1518,11 @@ int rt_render_records_device(rt_scene *const *scenes, const rt_frame *frames, ui
     if (!scenes || !frames || !d_outs || !rects || !d_recs || n == 0 || nranks == 0 || rank >= nranks)
         return fail(RT_E_INVALID, "bad arguments");
     std::vector<RecOut> ro(n);
+    // A records call never overlaps the scene's previous launch (RT_KERNEL_FLAG_OVERLAP is dropped): its
+    // fixup below reads the scene's tables after the render and marks the call's end with its own event.
+    std::vector<rt_frame> fr(frames, frames + n);
+    for (rt_frame& f : fr) f.kernel &= ~uint32_t(RT_KERNEL_FLAG_OVERLAP);
+    frames = fr.data();
     for (uint32_t i = 0; i < n; i++)
     {
         if (!scenes[i] || !d_outs[i] || !d_recs[i]) return fail(RT_E_INVALID, "NULL scene, output or record array");
@@ -1575,9 +1566,13 @@ int rt_render_records_device(rt_scene *const *scenes, const rt_frame *frames, ui
                            static_cast<hipStream_t>(hip_stream), P, uint32_t(nrec));
         RT_HIP(hipGetLastError());
         // the fixup reads the scene's tables (camera-space x / y, CSR offsets): a later call that
-        // rewrites them (prepare_samples -> wait_scene_idle) must wait for it, as for a render launch
-        RT_HIP(hipEventRecord(s->ev_own->ev, static_cast<hipStream_t>(hip_stream)));
-        s->ev_last = s->ev_own;
+        // rewrites them (prepare_samples -> wait_scene_idle) must wait for it, as for a render launch.
+        // Its own completion event (a free one: re-recording an event that the scene still holds as
+        // ev_prev would move that mark past the launch it stands for)
+        rtk::EvRef done;
+        if (int rc = free_done_event(s, done)) return rc;
+        RT_HIP(hipEventRecord(done->ev, static_cast<hipStream_t>(hip_stream)));
+        s->ev_last = done;
         s->ev_recorded = true;
         s->last_stream = static_cast<hipStream_t>(hip_stream);
     }
@@ -1931,6 +1926,15 @@ int rt_debug_heavy_first(rt_scene *s, uint32_t *front, uint32_t *listed, uint32_
     return RT_OK;
 }
 
+int rt_debug_set_plan_delay(rt_scene *s, uint32_t us)
+{
+    if (!s) return fail(RT_E_INVALID, "NULL scene");
+    if (us > 100000u) return fail(RT_E_INVALID, "plan delay must be <= 100000 us");
+    std::lock_guard<std::mutex> lk(s->mtx);
+    s->plan_delay = us * 100u;          // s_memrealtime ticks (100 MHz)
+    return RT_OK;
+}
+
 int rt_debug_wide_items(rt_scene *s, uint32_t *count)
 {
     if (!s || !count) return fail(RT_E_INVALID, "NULL argument");
@@ -1943,13 +1947,13 @@ int rt_debug_wide_items(rt_scene *s, uint32_t *count)
     return RT_OK;
 }
 
-int rt_debug_wide_tiers(rt_scene *s, uint32_t *split, uint32_t *seg)
+int rt_debug_wide_tiers(rt_scene *s, uint32_t *listed, uint32_t *lds)
 {
-    if (!s || !split || !seg) return fail(RT_E_INVALID, "NULL argument");
+    if (!s || !listed || !lds) return fail(RT_E_INVALID, "NULL argument");
     std::lock_guard<std::mutex> lk(s->mtx);
     int rc;
     if ((rc = ensure_device(s))) return rc;
-    *split = *seg = 0u;
+    *listed = *lds = 0u;
     const HfCtx *c = nullptr;
     for (const HfCtx& h : s->hf)
         if (h.wh_cnt && (!c || h.used > c->used)) c = &h;
@@ -1958,8 +1962,8 @@ int rt_debug_wide_tiers(rt_scene *s, uint32_t *split, uint32_t *seg)
     RT_HIP(hipDeviceSynchronize());
     HfPlan pl;
     RT_HIP(hipMemcpy(&pl, c->plans + (nv & 1u), sizeof(pl), hipMemcpyDeviceToHost));
-    *split = std::min(pl.cnt_w, kWhMax);
-    *seg = std::min(pl.cnt_s, kWhMax);
+    *listed = std::min(pl.cnt_w, kWhMax);
+    *lds = c->lds ? *listed : 0u;
     return RT_OK;
 }
 

@@ -31,6 +31,31 @@ __device__ __forceinline__ void wave_lds_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
+// Workgroup barrier for the LDS tier's reductions (kVarLdsSplit): this wave's LDS (and scalar)
+// operations complete, then s_barrier.  The memory clobber keeps the compiler from moving LDS accesses
+// across it (the s_barrier builtin alone is not a memory operation).
+__device__ __forceinline__ void lds_barrier()
+{
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// kVarLdsSplit: the per-lane (t, list position) and (u, v) of every wave of the workgroup,
+// double-buffered by reduction parity: [parity][wave][lane] each
+__device__ __forceinline__ float2 *lds_red_tk()
+{
+    __shared__ float2 r[2 * kWavesPerWG * 64];
+    return r;
+}
+__device__ __forceinline__ float2 *lds_red_uv()
+{
+    __shared__ float2 r[2 * kWavesPerWG * 64];
+    return r;
+}
+
+// kVarLdsSplit: cell lists shorter than this (in every lane) are tested whole by every wave, with no
+// reduction; longer ones are split between the workgroup's waves
+constexpr uint32_t kLdsSplitMin = 8;
+
 // kVarWaveClock debug counters of this wave: [0] records tested in wave-uniform loops,
 // [1] iterations of the per-lane list loop
 __device__ __forceinline__ uint32_t *wave_counters()
@@ -133,12 +158,15 @@ typedef const __attribute__((address_space(4))) vf4 cvf4;
 // prefetch in VGPRs (+12, 6 waves/SIMD) and by LDS-DMA into a per-wave slot
 // (global_load_lds_dwordx4; no VGPRs, but four DMA issues per record): both slower on the frame
 // and no shorter on the lone heavy waves (profiles/r02e_ab_lane_prefetch.json).
+// (kVarLdsSplit: this wave's share kb + first, kb + first + step, ... of the list)
 template <bool STATS, int VAR>
 __device__ __forceinline__ void lane_list(const KParams& P, rtd::f2v ra, rtd::f2v rc, uint32_t kb, uint32_t ke,
-                                          float& tb, float& u, float& v, uint32_t& tri, uint32_t& tests)
+                                          float& tb, float& u, float& v, uint32_t& tri, uint32_t& tests,
+                                          uint32_t first = 0u, uint32_t step = 1u)
 {
     constexpr bool F = (VAR & kVarFastRcp) != 0;
-    for (uint32_t k = kb; k < ke; k++)
+    constexpr bool SPLIT = (VAR & kVarLdsSplit) != 0;
+    for (uint32_t k = kb + (SPLIT ? first : 0u); k < ke; k += (SPLIT ? step : 1u))
     {
         if constexpr ((VAR & kVarWaveClock) != 0)
             if (first_active_lane()) wave_counters()[1] += 1u;
@@ -168,13 +196,29 @@ __device__ __forceinline__ void lane_list(const KParams& P, rtd::f2v ra, rtd::f2
 // FLT_MAX on entry (a hit ends the walk, grid.cpp:270-271) and neither bound is ever NaN, so the
 // two compares are one against tb = min(t, nct_ax), which every accepted hit lowers to its t:
 // the same hits are taken in the same order (strict '<' keeps the first of equal t, H8).
+//
+// kVarLdsSplit (the wide section's LDS tier, wide_item_lds): the workgroup's waves hold the same rays in
+// the same walk state, so they reach every call with the same lanes and lists.  When some lane's list
+// has kLdsSplitMin references or more (a vote, so alike in every wave), wave w tests only positions
+// kb + w, kb + w + 4, ...; each lane's local first minimum (t, position) is written to LDS, and after a
+// workgroup barrier every wave takes the lexicographic minimum over the four (smaller t, then the lower
+// list position: the reference's first minimum, H8) with its u, v.  The buffers alternate by parity
+// (lpar), so one barrier per reduction suffices: a wave can only overwrite a buffer after every wave
+// has passed the next barrier, i.e. finished reading it.
 template <bool STATS, int TRI, int VAR>
 __device__ __forceinline__ bool test_cell(const KParams& P, float ox, float oy, float oz, float dx, float dy,
                                           float dz, uint32_t kb, uint32_t ke, float nct_ax, float& t,
-                                          float& u, float& v, uint32_t& tri, uint32_t& tests)
+                                          float& u, float& v, uint32_t& tri, uint32_t& tests, uint32_t& lpar)
 {
     constexpr bool PRE = (VAR & kVarOriginPre) != 0 && TRI == RT_TRI_MOLLER_TRUMBORE;
     constexpr bool F = (VAR & kVarFastRcp) != 0;
+    constexpr bool SPLIT = (VAR & kVarLdsSplit) != 0;
+    static_assert(!SPLIT || (PRE && !STATS), "the LDS tier runs AUTO's record test");
+    (void)lpar;
+    // wave-uniform, and the same in every wave of the workgroup (their lanes and lists are the same)
+    bool split = false;
+    if constexpr (SPLIT) split = __any(ke - kb >= kLdsSplitMin);
+    const uint32_t first = split ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0u, step = split ? kWavesPerWG : 1u;
     const rtd::f2v ra = {dx, dy}, rc = {dy, dz};   // the ray as the record test's register pairs
     // min(t, nct_ax) as a compare and select: neither is ever NaN (and -0 / +0 compare equal in
     // every later '<'), and fminf would canonicalise both operands first (2 more VALU per cell)
@@ -199,6 +243,8 @@ __device__ __forceinline__ bool test_cell(const KParams& P, float ox, float oy, 
             if constexpr ((VAR & kVarWaveClock) != 0)
                 if (first_active_lane()) wave_counters()[0] += ke0 - kb0;
             cvf4 *crefs = (cvf4 *)P.frefs;
+            const uint32_t kfirst = kb0 + (SPLIT ? first : 0u), kstep = SPLIT ? step : 1u;
+            if (!SPLIT || kfirst < ke0)
             {
                 // software pipeline over two register sets in turn: record k + 1 is in flight
                 // while record k is tested, with no per-record register copies (scalar loads may
@@ -223,15 +269,15 @@ __device__ __forceinline__ bool test_cell(const KParams& P, float ox, float oy, 
                         tri = take ? k : tri;
                     }
                 };
-                cvf4 *np = crefs + size_t(kb0) * 4u;
+                cvf4 *np = crefs + size_t(kfirst) * 4u;
                 vf4 a0 = np[0], a1 = np[1], a2 = np[2], a3 = np[3];
-                for (uint32_t k = kb0;; k += 2u)
+                for (uint32_t k = kfirst;; k += 2u * kstep)
                 {
                     vf4 b0, b1, b2, b3;
-                    const bool more1 = k + 1u < ke0;
+                    const bool more1 = k + kstep < ke0;
                     if (more1)
                     {
-                        np = crefs + size_t(k + 1u) * 4u;
+                        np = crefs + size_t(k + kstep) * 4u;
                         b0 = np[0];
                         b1 = np[1];
                         b2 = np[2];
@@ -239,16 +285,16 @@ __device__ __forceinline__ bool test_cell(const KParams& P, float ox, float oy, 
                     }
                     test_rec(a0, a1, a2, a3, k);
                     if (!more1) break;
-                    const bool more2 = k + 2u < ke0;
+                    const bool more2 = k + 2u * kstep < ke0;
                     if (more2)
                     {
-                        np = crefs + size_t(k + 2u) * 4u;
+                        np = crefs + size_t(k + 2u * kstep) * 4u;
                         a0 = np[0];
                         a1 = np[1];
                         a2 = np[2];
                         a3 = np[3];
                     }
-                    test_rec(b0, b1, b2, b3, k + 1u);
+                    test_rec(b0, b1, b2, b3, k + kstep);
                     if (!more2) break;
                 }
             }
@@ -257,7 +303,7 @@ __device__ __forceinline__ bool test_cell(const KParams& P, float ox, float oy, 
     }
     if constexpr (PRE)
     {
-        if (!uniform_done) lane_list<STATS, VAR>(P, ra, rc, kb, ke, tb, u, v, tri, tests);
+        if (!uniform_done) lane_list<STATS, VAR>(P, ra, rc, kb, ke, tb, u, v, tri, tests, first, step);
     }
     else
     for (uint32_t k = kb; k < ke; k++)
@@ -285,6 +331,39 @@ __device__ __forceinline__ bool test_cell(const KParams& P, float ox, float oy, 
         u = take ? cu : u;
         v = take ? cv : v;
         tri = take ? id : tri;
+    }
+    if constexpr (SPLIT)
+    {
+        if (split)
+        {
+            // the four waves' first minima of this cell -> the list's (kLdsSplit: see above)
+            const uint32_t base = lpar * (kWavesPerWG * 64u), lane = threadIdx.x & 63u;
+            float2 *tk = lds_red_tk() + base, *uv = lds_red_uv() + base;
+            tk[threadIdx.x] = make_float2(tb, __uint_as_float(tb < tb0 ? tri : 0xFFFFFFFFu));
+            uv[threadIdx.x] = make_float2(u, v);
+            lds_barrier();
+            float bt = tb0;
+            uint32_t bk = 0xFFFFFFFFu, bj = 0u;
+#pragma unroll
+            for (uint32_t j = 0; j < kWavesPerWG; j++)
+            {
+                const float2 o = tk[j * 64u + lane];
+                const uint32_t ok = __float_as_uint(o.y);
+                const bool better = (o.x < bt) | ((o.x == bt) & (ok < bk));
+                bt = better ? o.x : bt;
+                bk = better ? ok : bk;
+                bj = better ? j : bj;
+            }
+            lpar ^= 1u;
+            if (bk != 0xFFFFFFFFu)
+            {
+                const float2 w = uv[bj * 64u + lane];
+                tb = bt;
+                u = w.x;
+                v = w.y;
+                tri = bk;
+            }
+        }
     }
     t = tb < tb0 ? tb : t;
     return t != rtd::kFltMax;                                  // grid.cpp:270-271
@@ -557,6 +636,7 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, float ox, float
                    cell))
         return false;
     t = rtd::kFltMax;
+    uint32_t lpar = 0u;                 // kVarLdsSplit: the reduction buffers' parity (test_cell)
 
     if constexpr ((VAR & kVarSkipRun) != 0 && (VAR & kVarPackedRem) != 0)
     {
@@ -608,7 +688,7 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, float ox, float
             }
             RT_DDA_ADVANCE_BOX(nct_ax, more);
             bool hit = false;
-            if (kb < ke) hit = test_cell<STATS, TRI, VAR>(P, ox, oy, oz, dx, dy, dz, kb, ke, nct_ax, t, u, v, tri, tests);
+            if (kb < ke) hit = test_cell<STATS, TRI, VAR>(P, ox, oy, oz, dx, dy, dz, kb, ke, nct_ax, t, u, v, tri, tests, lpar);
             const bool inside = (uint32_t(boxw) & uint32_t(kRemGuards)) == 0u;
             if (!sync && inside)
             {
@@ -714,7 +794,7 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, float ox, float
             // below), and the result read from t after the loop: the walk's loop-carried state
             // stays in VGPRs instead of per-exit lane masks (SALU per wave, PMC-measured)
             bool hit = false;
-            if (kb < ke) hit = test_cell<STATS, TRI, VAR>(P, ox, oy, oz, dx, dy, dz, kb, ke, nct_ax, t, u, v, tri, tests);
+            if (kb < ke) hit = test_cell<STATS, TRI, VAR>(P, ox, oy, oz, dx, dy, dz, kb, ke, nct_ax, t, u, v, tri, tests, lpar);
             bool done = hit | !more;
             if constexpr ((VAR & kVarSkipRun) != 0 && (VAR & kVarPackedRem) != 0 && !STATS)
             {
@@ -783,7 +863,7 @@ __device__ __forceinline__ bool grid_intersect(const KParams& P, float ox, float
         float nct_ax;
         bool more;
         RT_DDA_ADVANCE_ADD(nct_ax, more);
-        if (kb < ke && test_cell<STATS, TRI, VAR>(P, ox, oy, oz, dx, dy, dz, kb, ke, nct_ax, t, u, v, tri, tests))
+        if (kb < ke && test_cell<STATS, TRI, VAR>(P, ox, oy, oz, dx, dy, dz, kb, ke, nct_ax, t, u, v, tri, tests, lpar))
             return true;
         if (!more) break;
     }
@@ -1103,11 +1183,13 @@ __device__ __forceinline__ void process_item(const KParams& P, uint32_t item, ui
     }
     const KParams& Q = late_params(P, off);
     const ItemCoord ic = item_coord(Q, item, lane);
+    // kVarLdsSplit: the workgroup's four waves traced the same samples; wave 0 stores them
+    const bool owner = (VAR & kVarLdsSplit) == 0 || threadIdx.x < 64u;
     // rt_render_hits_device only: the sample's hit triangle, after the walk (a scalar test of a
     // kernel parameter; the walk above is the same code whatever the pointer holds)
-    if (Q.hits && ic.valid) Q.hits[(size_t(ic.y) * Q.W + ic.x) * Q.spp + ic.s] = hit_tri;
+    if (Q.hits && ic.valid && owner) Q.hits[(size_t(ic.y) * Q.W + ic.x) * Q.spp + ic.s] = hit_tri;
     // rt_render_records_device only, likewise: the sample's record (process_record)
-    if (Q.recs && ic.valid) process_record<VAR>(Q, ic, so, cr, cg, cb);
+    if (Q.recs && ic.valid && owner) process_record<VAR>(Q, ic, so, cr, cg, cb);
     float sr = 0.0f, sg = 0.0f, sb = 0.0f;
     if (Q.spp == 4u)
     {
@@ -1128,7 +1210,7 @@ __device__ __forceinline__ void process_item(const KParams& P, uint32_t item, ui
         uint32_t v = rtd::pack_channel(rtd::gamma_half(c * 0.25f)) << (8u * j);   // renderer.cpp:124, exact
         v = j == 3u ? 0u : v;
         const uint32_t word = quad_bcast_u<0>(v) | quad_bcast_u<1>(v) | quad_bcast_u<2>(v);
-        if (ic.valid && ic.s == 0) store_pixel(Q, ic.c, ic.p, ic.x, ic.y, word);
+        if (ic.valid && ic.s == 0 && owner) store_pixel(Q, ic.c, ic.p, ic.x, ic.y, word);
         return;
     }
     else
@@ -1141,7 +1223,7 @@ __device__ __forceinline__ void process_item(const KParams& P, uint32_t item, ui
             sb += __shfl(cb, int(base + k), 64);
         }
     }
-    if (ic.valid && ic.s == 0)
+    if (ic.valid && ic.s == 0 && owner)
     {
         const uint32_t word = rtd::pack_bgra8(rtd::gamma_half(average(Q, sr)), rtd::gamma_half(average(Q, sg)),
                                               rtd::gamma_half(average(Q, sb)));

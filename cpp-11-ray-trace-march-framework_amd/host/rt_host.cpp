@@ -757,7 +757,7 @@ protected:
     }
 
     std::string m_err;
-    bool m_issue_early = true;          // RTH_ISSUE_EARLY=0: the first worker issues the frame (A/B)
+    bool m_issue_early = true;          // the starting thread issues the frame (round 4: before the workers wake)
     bool m_inline = true;               // RTH_POOL=1: the worker pool delivers the tiles (A/B)
 
 private:
@@ -846,8 +846,6 @@ public:
         m_tiled = !(e && *e == '0');
         const char* l = std::getenv("RTH_LAUNCHES");
         m_launches = l && *l ? std::max(1, std::atoi(l)) : 1;
-        const char* ie = std::getenv("RTH_ISSUE_EARLY");
-        m_issue_early = !(ie && *ie == '0');
         const char* po = std::getenv("RTH_POOL");
         m_inline = !(po && *po == '1');
     }

@@ -329,19 +329,24 @@ int  rt_debug_wave_clocks(rt_scene *s, uint64_t *out, uint32_t max_items, uint32
    *epoch = frames rendered with this shape.  Synchronises the device. */
 int rt_debug_heavy_first(rt_scene *s, uint32_t *front, uint32_t *listed, uint32_t *epoch);
 /* RT_KERNEL_FLAG_WIDE_HEAVY: the wide section's waves for the items the newest plan of the most
-   recent wide-section launch shape lists (16 or 4 per item of the lane-split tier, 64 per item of the
-   segmented tier).  Synchronises the device. */
+   recent wide-section launch shape lists (16 or 4 per item of the lane-split tier, 4 per item -- one
+   256-lane workgroup -- of the LDS tier).  Synchronises the device. */
 int rt_debug_wide_items(rt_scene *s, uint32_t *count);
-/* The same plan's items per tier: *split = the lane-split tier's (16 or 4 lanes per sample), *seg =
-   the segmented tier's (4 t-segments x 16 lanes per sample, kVarWideSeg).  Synchronises the device. */
-int rt_debug_wide_tiers(rt_scene *s, uint32_t *split, uint32_t *seg);
+/* Tests only: every later heavy-first plan kernel (k_hf_plan) of this scene first idles `us`
+   microseconds (<= 100000; 0: off, the default), so a frame that could read a plan's buffers while
+   the plan writes them -- the ordering HfCtx::fence exists for -- always
+   overlaps it.  Frames stay exact: the library orders every reader after the plan. */
+int rt_debug_set_plan_delay(rt_scene *s, uint32_t us);
+/* The same plan's items: *listed = all of them, *lds = those the LDS tier renders (the launch shape's
+   section runs it: all of them, else 0; kVarLdsSplit, RT_WH_LDS).  Synchronises the device. */
+int rt_debug_wide_tiers(rt_scene *s, uint32_t *listed, uint32_t *lds);
 
 /* What rt_scene_create chose for a scene, and the scheduling tunables it read once from the
    environment (RT_HF_FLOOR, RT_HF_MIN_BLOCKS, RT_WH_FLOOR, RT_WH_ALPHA16, RT_WH_ALPHA16_N2,
-   RT_WH_AUTO_REFS, RT_WH_FUSED, RT_OCT_DIST): never re-read per launch. */
+   RT_WH_AUTO_REFS, RT_WH_LDS, ...): never re-read per launch. */
 typedef struct rt_scene_info {
     uint32_t octant_words;      /* 1: 8 ray-octant copies of the cell words (AUTO's empty runs);
-                                   0: one L-inf word per cell (RT_OCT_DIST=0, or above the size cap) */
+                                   0: one L-inf word per cell (above the size cap) */
     uint32_t packed_cells;      /* cell ranges packed into one word per cell */
     uint32_t rcp_safe, pack_ok; /* Newton 1/det and packed remaining-cell counts in range */
     uint32_t max_cell_refs;
@@ -355,7 +360,7 @@ typedef struct rt_scene_info {
                                    axis); 0: none (references >= 2^20 or above the size cap: AUTO then
                                    walks without the packed counts and empty runs) */
     uint32_t wh_alpha16_n2;     /* RT_WH_ALPHA16_N2: the wide threshold at a rank of 2 of a batched step */
-    uint32_t pad0;
+    uint32_t wh_lds;            /* RT_WH_LDS: bit log2 N (3: N >= 8) -- a rank of N's wide section runs the LDS tier */
     uint64_t batch_launches;    /* rt_render_batch_device chunks led by this scene (frames[0]) that ran as
                                    ONE launch ... */
     uint64_t batch_fallbacks;   /* ... and that fell back to one launch per frame (frames that cannot

@@ -221,6 +221,42 @@ def views(tmp):
     return out
 
 
+MOVING_SCENES = (1, 8)
+MOVING_FRAMES = (0, 1, 2, 24, 25, 26)       # orbit steps j: the camera turned ORBIT_DEG * (j + 1)
+
+
+def moving_views(tmp):
+    """The views of bench.py's moving_camera leg (the scene's own camera orbited bench.ORBIT_DEG = 0.5
+    degrees per frame about the world y axis, bench.orbit_cam) at the bench's 1920x1080x4: per scene 1
+    and 8, three consecutive frames at the orbit's start and three later ones, the exact camera bits and
+    the reference's frame / per-sample hit-ID SHA-256 from those bits (refdriver render --view: the
+    reference's GenerateRay camera.h:8-47 and Grid::Intersect for that camera)."""
+    sys.path.insert(0, ROOT)
+    import bench                    # the leg's own orbit arithmetic (numpy only at import)
+    out = {}
+    for sid in MOVING_SCENES:
+        with open(os.path.join(SCENES, f"scene{sid}.rtscene"), "rb") as f:
+            head = f.read(80)
+        assert head[:8] == b"RTSCENE1"
+        fov = np.frombuffer(head[12:16], "<f4")[0]
+        cam = np.frombuffer(head[16:80], "<f4")
+        for j in MOVING_FRAMES:
+            c = bench.orbit_cam(cam, bench.ORBIT_DEG * (j + 1))
+            vp = os.path.join(tmp, "m.view")
+            with open(vp, "wb") as f:
+                f.write(np.asarray(c, "<f4").tobytes() + np.asarray([fov], "<f4").tobytes())
+            bp, hp = os.path.join(tmp, "m.bgra"), os.path.join(tmp, "m.hits")
+            run(["render", os.path.join(SCENES, f"scene{sid}.rtscene"), "1920", "1080", "4", "--out", bp,
+                 "--hits", hp, "--view", vp])
+            out[f"scene{sid}_orbit{j}"] = {
+                "scene": sid, "orbit_step": j, "orbit_deg": bench.ORBIT_DEG * (j + 1), "W": 1920, "H": 1080, "spp": 4,
+                "cam_bits": [f"{x:08x}" for x in np.asarray(c, "<f4").view("<u4")],
+                "fov_bits": f"{int(np.asarray([fov], '<f4').view('<u4')[0]):08x}",
+                "bgra_sha256": sha(bp), "hits_sha256": sha(hp)}
+            print("moving view", sid, j, flush=True)
+    return out
+
+
 SPP_CROPS = [(1, 952, 532), (5, 952, 532), (8, 952, 532), (8, 640, 720)]
 
 
@@ -287,7 +323,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-head", action="store_true")
     ap.add_argument("--only", choices=["crops", "bmp", "head", "records", "views", "spp_crops", "head_records",
-                                       "bary"],
+                                       "bary", "moving"],
                     help="regenerate one section and merge it into the existing golden.json")
     a = ap.parse_args()
     if a.only:
@@ -310,6 +346,8 @@ def main():
             meta["head_1024x1024x16_records"] = head_records(tmp)
         elif a.only == "bary":
             meta["bary"] = bary(tmp)
+        elif a.only == "moving":
+            meta["moving_views"] = moving_views(tmp)
         else:
             meta["bmp"] = bmp_golden(tmp)
         meta["sample_record"] = SAMPLE_RECORD
@@ -391,7 +429,7 @@ def main():
     }
     with open(os.path.join(GOLD, "golden.json"), "w") as f:     # view_cams reads the scenes' AABBs
         json.dump(meta, f, indent=1, sort_keys=True)
-    meta.update({"views": views(tmp), "spp_crops": spp_crops(tmp),
+    meta.update({"views": views(tmp), "moving_views": moving_views(tmp), "spp_crops": spp_crops(tmp),
                  "head_1024x1024x16_records": head_records(tmp), "bary": bary(tmp)})
     with open(os.path.join(GOLD, "golden.json"), "w") as f:
         json.dump(meta, f, indent=1, sort_keys=True)

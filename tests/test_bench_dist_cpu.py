@@ -28,6 +28,7 @@ class CpuWorkload:
         self.frames = [None for _ in scenes]
         self.renders = 0
         self.sets = []
+        self.active = list(range(len(scenes)))      # bench.per_scene_steps renders one scene at a time
 
     def expected(self, i, step):
         return self.full[i] ^ np.uint32(step)
@@ -35,7 +36,7 @@ class CpuWorkload:
     def render_all(self, p=0):
         step = self.renders // len(self.full)
         self.sets.append(p)
-        for i in range(len(self.full)):
+        for i in self.active:
             shard = self.rtm.shard_from_frame(self.expected(i, step), self.rank, self.world)
             self.bufs[p][i].copy_(torch.from_numpy(shard.view(np.int32)))
             self.renders += 1
@@ -63,16 +64,23 @@ def _worker(rank, world, port, q):
         work = CpuWorkload(rtm, world, rank, bench.SCENES)
         elapsed = bench.run_steps(work, world, rank, steps=3, warmup=1, dist=dist, clock_warmup=0.0)
         report = bench.dist_report(work, world, rank, dist, 3, elapsed, reps=3)
+        renders = work.renders
+        # the drained pipeline holds the last (4th) step's frames; steps alternate buffer sets
+        same = all(np.array_equal(work.frames[i], work.expected(i, 3)) for i in range(len(bench.SCENES))) \
+            if rank == 0 else True
+        same = same and work.sets == [0, 1, 0, 1]
+        # BASELINE.md §4's per-scene figures: each scene alone through the same step (2 + 1 steps each)
+        work.renders = 0
+        per = bench.per_scene_steps(work, world, rank, dist, 2, 1)
         if rank == 0:
-            # the drained pipeline holds the last (4th) step's frames; steps alternate buffer sets
-            same = all(np.array_equal(work.frames[i], work.expected(i, 3)) for i in range(len(bench.SCENES)))
-            same = same and work.sets == [0, 1, 0, 1]
-            q.put(("ok", same, elapsed, work.renders, report))
+            # scene i's frame of the last step (the renders count every scene's render) assembled alone
+            same = same and work.renders == 3 * len(bench.SCENES) and work.active == [0, 1]
+            q.put(("ok", same, elapsed, renders, report, per))
         else:
-            assert report is None
+            assert report is None and per is None
         dist.barrier()
     except Exception as e:  # pragma: no cover
-        q.put(("err", repr(e), 0, 0, None))
+        q.put(("err", repr(e), 0, 0, None, None))
     finally:
         dist.destroy_process_group()
 
@@ -91,7 +99,7 @@ def test_bench_run_steps_gloo(world):
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    status, same, elapsed, renders, rep = q.get(timeout=300)
+    status, same, elapsed, renders, rep, per = q.get(timeout=300)
     for p in procs:
         p.join(timeout=120)
     assert status == "ok", same
@@ -107,6 +115,10 @@ def test_bench_run_steps_gloo(world):
     assert len(g["per_rank"]) == world and g["rank0"] > 0 and g["max"] >= g["rank0"]
     assert g["source"].startswith("host clock") and g["reps"] == 3
     assert rep["step_ms"] > 0
+    # the per-scene legs (Cornell and killeroo reported separately at every N)
+    assert sorted(per) == ["1", "8"]
+    for v in per.values():
+        assert v["ms_per_step"] > 0 and v["value"] > 0 and v["unit"] == "Msamples/s" and v["steps"] == 2
 
 
 @pytest.mark.gpu
@@ -135,3 +147,6 @@ def test_bench_two_ranks_one_gpu_rehearsal():
     d = out["distributed"]
     assert d["backend"] == "gloo" and d["world_size"] == 2 and d["collective"] == "all_gather"
     assert d["collective_fallback"] and len(d["render_ms"]["per_rank"]) == 2 and d["gather_ms"]["rank0"] > 0
+    # the overlap setting, the one-stream figure beside the value, per-frame latency and each scene alone
+    assert out["overlap"] is True and out["value_one_stream"] > 0 and out["one_stream"]["frame_latency_ms"] > 0
+    assert out["frame_latency_ms"] > 0 and sorted(out["per_scene_steps"]) == ["1", "8"]

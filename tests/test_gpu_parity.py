@@ -233,36 +233,42 @@ def test_shard_hits_rank_of_8(golden, scenes, sid, monkeypatch):
             hs.close()
 
 
-def test_octant_words_arms(golden, monkeypatch):
-    """The empty-run words are chosen at scene creation: RT_OCT_DIST=0 (one L-inf word per
-    cell) and the default octant copies both render the reference's bytes on every scene, and
-    their shards of 8 ranks (where AUTO adds the wide section on dense scenes) agree."""
+@pytest.mark.parametrize("sid", [4, 5, 8])
+def test_wide_section_tiers_agree(golden, sid, monkeypatch):
+    """The wide section's two tiers -- the LDS tier (default from 2 ranks: one 256-lane workgroup per
+    listed item, its cell lists split between the four waves and reduced through LDS) and the lane tier
+    (RT_WH_LDS=0: 16 lanes per sample, butterfly) -- render the same shards at a rank of 8, every rank,
+    through a refresh of the list, single-frame launches and batched ones; the assembled frame is the
+    reference's."""
     import torch
-    arm = "0"
-    for sid in range(10):
-        hs = rtm.HostScene.load(sid)
-        monkeypatch.setenv("RT_OCT_DIST", arm)
-        ga = rtm.GpuScene(hs, 0)
-        monkeypatch.delenv("RT_OCT_DIST")
-        gb = rtm.GpuScene(hs, 0)
-        try:
-            want = golden["frames_1080p4"][str(sid)]["bgra_sha256"]
-            for g in (ga, gb):
-                img = g.render_frame(g.frame(1920, 1080, 4))
-                assert hashlib.sha256(img.tobytes()).hexdigest() == want, (sid, arm)
-            e = rtm.shard_elems(1920, 1080, 8)
-            a = torch.zeros(e, dtype=torch.int32, device="cuda")
-            b = torch.zeros(e, dtype=torch.int32, device="cuda")
-            st = torch.cuda.current_stream().cuda_stream
-            for r in (0, 7):
-                ga.render_shard_device(ga.frame(1920, 1080, 4), r, 8, a.data_ptr(), st)
-                gb.render_shard_device(gb.frame(1920, 1080, 4), r, 8, b.data_ptr(), st)
-                torch.cuda.synchronize()
-                assert torch.equal(a, b), (sid, arm, r)
-        finally:
-            ga.close()
-            gb.close()
-            hs.close()
+    W, H, N = 1920, 1080, 8
+    hs = rtm.HostScene.load(sid)
+    monkeypatch.setenv("RT_WH_LDS", "0")
+    ga = rtm.GpuScene(hs, 0)
+    monkeypatch.delenv("RT_WH_LDS")
+    gb = rtm.GpuScene(hs, 0)
+    try:
+        assert ga.info()["wh_lds"] == 0 and gb.info()["wh_lds"] != 0
+        want = golden["frames_1080p4"][str(sid)]["bgra_sha256"]
+        e = rtm.shard_elems(W, H, N)
+        st = torch.cuda.current_stream().cuda_stream
+        for g in (ga, gb):
+            f = g.frame(W, H, 4)
+            a = torch.zeros(N * e, dtype=torch.int32, device="cuda")
+            for r in range(N):
+                for _ in range(5):
+                    a[r * e:(r + 1) * e].fill_(0x5A5A5A5A)
+                    g.render_shard_device(f, r, N, a.data_ptr() + 4 * r * e, st)
+            out = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+            rtm.unshard_device(W, H, N, a.data_ptr(), out.data_ptr(), st)
+            torch.cuda.synchronize()
+            assert sha_dev(out) == want, (sid, g is gb)
+            listed, lds = g.wide_tiers()
+            assert listed > 0 and lds == (listed if g is gb else 0), (sid, listed, lds)
+    finally:
+        ga.close()
+        gb.close()
+        hs.close()
 
 
 @pytest.mark.parametrize("sid", range(10))
@@ -337,17 +343,17 @@ def test_removed_arms_rejected(scenes):
 
 
 def test_scene_tunables_read_once(monkeypatch):
-    """Scheduling tunables come from the environment once, at rt_scene_create (never per launch);
-    RT_OCT_DIST=0 picks the single L-inf empty-run words."""
+    """Scheduling tunables come from the environment once, at rt_scene_create (never per launch)."""
     hs = rtm.HostScene.load(8)
     a = rtm.GpuScene(hs, 0)
     monkeypatch.setenv("RT_WH_FLOOR", "1234")
-    monkeypatch.setenv("RT_OCT_DIST", "0")
+    monkeypatch.setenv("RT_WH_LDS", "0")
     b = rtm.GpuScene(hs, 0)
     try:
         ia, ib = a.info(), b.info()
         assert ia["wh_floor"] == 100000 and ib["wh_floor"] == 1234
-        assert ia["octant_words"] == 1 and ib["octant_words"] == 0
+        assert ia["wh_lds"] != 0 and ib["wh_lds"] == 0
+        assert ia["octant_words"] == 1 and ib["octant_words"] == 1
         assert ia["max_cell_refs"] >= 128 and ia["rcp_safe"] == 1 and ia["pack_ok"] == 1
         assert ia["hf_contexts"] >= 8
         assert ia["box_words"] == 1 and ib["box_words"] == 1 and ia["wh_alpha16_n2"] == 16

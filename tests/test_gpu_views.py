@@ -254,3 +254,78 @@ def test_bary_full_frame_records(golden, scenes, sid):
     f = gs.frame(1920, 1080, 4, tri_test=rtm.RT_TRI_BARYCENTRIC)
     rec = np.concatenate([debug_records(gs, f, 0, y0, 1920, min(270, 1080 - y0)) for y0 in range(0, 1080, 270)])
     expect(b, shas(rec))
+
+
+@pytest.mark.parametrize("nranks", [1, 8])
+def test_moving_camera_views_batched(golden, nranks):
+    """bench.py's moving_camera leg pinned to the reference: the bench pair (killeroo first, bench.py's
+    order at one rank) orbiting 0.5 degrees per frame about the world y axis (bench.orbit_cam), 27
+    consecutive frames batched as the leg renders them -- fresh scenes, every frame a new origin
+    (k_origin_pre before its render) and a new view whose heavy-first order (and at a rank of 8 the wide
+    section's list, LDS tier) is re-planned from the frame before (RT_HF_FOLLOW), consecutive steps
+    overlapped on two streams into sentinel-filled buffers.  The frames and per-sample hit IDs of orbit
+    steps 0-2 and 24-26 equal the reference's own render of the same camera bits (refdriver render
+    --view, oracle/gen_golden.py moving_views; the bits are checked against bench.orbit_cam on the CPU,
+    tests/test_oracle_golden.py)."""
+    import sys
+    import torch
+    from conftest import ROOT
+    sys.path.insert(0, ROOT)
+    import bench
+    W, H, SPP = 1920, 1080, 4
+    sids = (8, 1)
+    mv = golden["moving_views"]
+    hss = [rtm.HostScene.load(s) for s in sids]
+    gss = [rtm.GpuScene(h, 0) for h in hss]
+    try:
+        steps = max(v["orbit_step"] for v in mv.values()) + 1
+        frames = []
+        for j in range(steps):
+            row = []
+            for sid, hs, gs in zip(sids, hss, gss):
+                f = gs.frame(W, H, SPP, kernel=rtm.RT_KERNEL_FLAG_OVERLAP)
+                c = bench.orbit_cam(hs.cam, bench.ORBIT_DEG * (j + 1))
+                for k in range(16):
+                    f.cam[k] = float(c[k])
+                key = f"scene{sid}_orbit{j}"
+                if key in mv:
+                    assert [f"{int(x):08x}" for x in np.asarray(c, np.float32).view(np.uint32)] == mv[key]["cam_bits"]
+                row.append(f)
+            frames.append(row)
+        e = W * H if nranks == 1 else rtm.shard_elems(W, H, nranks)
+        streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+        outs = {j: [torch.zeros(nranks * e, dtype=torch.int32, device="cuda") for _ in sids] for j in range(steps)
+                if f"scene{sids[0]}_orbit{j}" in mv}
+        hits = {j: [torch.full((W * H * SPP,), 0x5A5A5A5A, dtype=torch.int32, device="cuda") for _ in sids]
+                for j in outs}
+        scratch = [[torch.empty(nranks * e, dtype=torch.int32, device="cuda") for _ in sids] for _ in range(2)]
+        torch.cuda.synchronize()
+        for j in range(steps):
+            s = streams[j % 2]
+            bufs = outs.get(j, scratch[j % 2])
+            with torch.cuda.stream(s):
+                for b in bufs:
+                    b.fill_(0x5A5A5A5A)
+            for r in range(nranks):
+                rtm.render_batch_device(gss, frames[j], [b.data_ptr() + 4 * r * e for b in bufs], rank=r,
+                                        nranks=nranks, d_hits=[h.data_ptr() for h in hits[j]] if j in hits else None,
+                                        stream=s.cuda_stream)
+        torch.cuda.synchronize()
+        full = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+        st = torch.cuda.current_stream().cuda_stream
+        for j, bufs in outs.items():
+            for sid, b, h in zip(sids, bufs, hits[j]):
+                v = mv[f"scene{sid}_orbit{j}"]
+                if nranks > 1:
+                    rtm.unshard_device(W, H, nranks, b.data_ptr(), full.data_ptr(), st)
+                    torch.cuda.synchronize()
+                    b = full
+                got = hashlib.sha256(b.cpu().numpy().tobytes()).hexdigest()
+                assert got == v["bgra_sha256"], (sid, j, nranks)
+                assert hashlib.sha256(h.cpu().numpy().tobytes()).hexdigest() == v["hits_sha256"], (sid, j, nranks)
+    finally:
+        torch.cuda.synchronize()
+        for g in gss:
+            g.close()
+        for h in hss:
+            h.close()

@@ -11,7 +11,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import GOLD, load_kat, read_gz
+from conftest import GOLD, ROOT, load_kat, load_package, read_gz
 
 SCENES = list(range(10))
 
@@ -182,6 +182,33 @@ def test_views_oracle_frames_match_reference(oracle, golden):
         assert hashlib.sha256(img.tobytes()).hexdigest() == v["bgra_sha256"], name
         assert hashlib.sha256(hid.tobytes()).hexdigest() == v["hits_sha256"], name
         assert v["hit_tri_sha256"] == v["hits_sha256"], name      # render and samples agree
+
+
+def test_moving_views_cams_and_oracle_match_reference(oracle, golden):
+    """bench.py's moving_camera leg (bench.orbit_cam: the scene's camera orbited 0.5 degrees per frame)
+    gives exactly the camera bits the fixtures were rendered from by the reference (refdriver render
+    --view, oracle/gen_golden.py moving_views), and the restatement's frames and hit IDs from those views
+    equal the reference's (the first view of each scene here; every view on the GPU,
+    tests/test_gpu_views.py::test_moving_camera_views_batched)."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    mv = golden["moving_views"]
+    assert len(mv) == 12
+    cams = {}
+    for sid in (1, 8):
+        hs = load_package().HostScene.load(sid)
+        cams[sid] = (np.array(hs.cam, np.float32), hs.fov)
+        hs.close()
+    for name, v in mv.items():
+        cam, fov = cams[v["scene"]]
+        c = bench.orbit_cam(cam, bench.ORBIT_DEG * (v["orbit_step"] + 1))
+        assert [f"{x:08x}" for x in np.asarray(c, np.float32).view(np.uint32)] == v["cam_bits"], name
+        assert f"{int(np.asarray([fov], np.float32).view(np.uint32)[0]):08x}" == v["fov_bits"], name
+        if v["orbit_step"] == 0:
+            img, hid = oracle.render_cam(v["scene"], v["W"], v["H"], v["spp"], c, fov)
+            assert hashlib.sha256(img.tobytes()).hexdigest() == v["bgra_sha256"], name
+            assert hashlib.sha256(hid.tobytes()).hexdigest() == v["hits_sha256"], name
 
 
 def test_look_at_restatement_matches_reference(golden, oracle, rtm):

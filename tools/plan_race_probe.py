@@ -1,0 +1,74 @@
+#!/usr/bin/env python3
+"""The plan-adoption race of DESIGN.md §4.21 under a plan delay (rt_debug_set_plan_delay): single-frame
+steps of a fresh scene alternating two streams with RT_KERNEL_FLAG_OVERLAP, step 17 forced after step 16
+(tests/test_gpu_overlap.py::_plan_race_steps), for several delays (x one frame's device time); per step
+the pixels left at the sentinel.  Run it against the product library and the nofence variant
+(RT_TRACER_LIB=librt_tracer_nofence.so, tools/build_variant.sh).
+
+    python3 tools/plan_race_probe.py [--scene 4] [--factors 0.8 1.2 1.4 2] [--out NAME]"""
+import argparse
+import importlib.util
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+spec = importlib.util.spec_from_file_location("rtm", os.path.join(ROOT, "cpp-11-ray-trace-march-framework_amd", "__init__.py"))
+rtm = importlib.util.module_from_spec(spec)
+sys.modules["rtm"] = rtm
+spec.loader.exec_module(rtm)
+ap = argparse.ArgumentParser()
+ap.add_argument("--scene", type=int, default=4)
+ap.add_argument("--factors", type=float, nargs="+", default=[0.8, 1.2, 1.4, 2.0, 3.0])
+ap.add_argument("--frame", type=int, nargs=3, default=[1920, 1080, 4])
+ap.add_argument("--out", default=None)
+A = ap.parse_args()
+W, H, SPP = A.frame
+SENT = 0x5A5A5A5A
+hs = rtm.HostScene.load(A.scene)
+streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+gm = rtm.GpuScene(hs, 0)
+fm = gm.frame(W, H, SPP)
+scratch = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+ts = []
+for i in range(12):
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(streams[0])
+    gm.render_frame_device(fm, scratch.data_ptr(), streams[0].cuda_stream)
+    b.record(streams[0])
+    torch.cuda.synchronize()
+    if i >= 2:
+        ts.append(a.elapsed_time(b))
+ref = scratch.clone()
+gm.close()
+F = sorted(ts)[len(ts) // 2]
+res = {"scene": A.scene, "frame": [W, H, SPP], "frame_ms": F, "lib": os.environ.get("RT_TRACER_LIB", "librt_tracer.so"),
+       "runs": {}}
+for fac in A.factors:
+    gs = rtm.GpuScene(hs, 0)
+    f = gs.frame(W, H, SPP, kernel=rtm.RT_KERNEL_FLAG_OVERLAP)
+    outs = [torch.zeros(W * H, dtype=torch.int32, device="cuda") for _ in range(24)]
+    torch.cuda.synchronize()
+    gs.set_plan_delay(int(1000 * fac * F))
+    for i in range(24):
+        s = streams[i % 2]
+        if i == 17:
+            e = torch.cuda.Event()
+            e.record(streams[0])
+            s.wait_event(e)
+        with torch.cuda.stream(s):
+            outs[i].fill_(SENT)
+        gs.render_frame_device(f, outs[i].data_ptr(), s.cuda_stream)
+    torch.cuda.synchronize()
+    gs.set_plan_delay(0)
+    bad = {i: int((o == SENT).sum()) for i, o in enumerate(outs) if not torch.equal(o, ref)}
+    front, listed, epoch = gs.heavy_first()
+    res["runs"][str(fac)] = {"delay_us": int(1000 * fac * F), "bad_sentinel_px": bad, "front": front, "listed": listed,
+                             "epoch": epoch}
+    print(fac, res["runs"][str(fac)], flush=True)
+    gs.close()
+hs.close()
+os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+json.dump(res, open(os.path.join(ROOT, "gpurun_out", (A.out or "plan_race_probe") + ".json"), "w"), indent=1)
