@@ -364,10 +364,11 @@ __device__ __forceinline__ void wide_section(const KParams& P, uint32_t w)
 // (grid.cpp:243-267, H8), which every wave then holds: the walks stay identical.  A lone heavy wave's
 // ~1,000-record chain becomes four chains of ~250 on four SIMDs; the walk is
 // repeated four times (against 16 in the G-lane tier).  Wave 0 stores the pixels.
+// li: the item's entry in the LDS tier's list (the list's second half, wh_list_in + kWhMax)
 template <bool BATCH, bool CLK = false>
 __device__ __forceinline__ void wide_item_lds(const KParams& P, uint32_t li)
 {
-    uint32_t item = __builtin_amdgcn_readfirstlane(P.wh_list_in[li]);
+    uint32_t item = __builtin_amdgcn_readfirstlane(P.wh_list_in[kWhMax + li]);
     uint32_t off = 0u;
     if constexpr (BATCH)
     {
@@ -392,18 +393,29 @@ __device__ __forceinline__ void wide_item_lds(const KParams& P, uint32_t li)
         const KBatch& B = late_batch();
         const KParams& Q0 = late_params(P, uint32_t(offsetof(KBatch, p)));
         if (threadIdx.x == 0u)
-            store_wave_clock(Q0.wave_clk, B.base[B.nframes] * kWavesPerWG + li, t0, t1, r0, r1, 0x80000000u | li,
-                             __builtin_amdgcn_readfirstlane(Q0.wh_list_in[li]));
+            store_wave_clock(Q0.wave_clk, B.base[B.nframes] * kWavesPerWG + kWhMax * 16u + li, t0, t1, r0, r1,
+                             0x80000000u | (kWhMax + li), __builtin_amdgcn_readfirstlane(Q0.wh_list_in[kWhMax + li]));
     }
 }
 
-// wg: this workgroup's index in the section; the list is walked workgroup by workgroup (persistent)
-template <bool BATCH, bool CLK = false>
+// A section with both tiers (kVarLdsSplit; 256-lane workgroups): its first wh_wgs_g workgroups take the
+// G-lane tier's items (the heaviest) wave by wave, the others the LDS tier's, workgroup by workgroup, so
+// both start with the launch (each loop persistent over its list).  wg: this workgroup's index in the
+// section.
+template <bool BATCH, uint32_t G, bool CLK = false>
 __device__ __forceinline__ void wide_section_lds(const KParams& P, uint32_t wg)
 {
-    const uint32_t n = P.hf_ver ? min(P.hf_plan_in->cnt_w, kWhMax) : 0u;
-    const uint32_t nwg = P.wh_wgs;
-    for (uint32_t li = wg; li < n; li += nwg) wide_item_lds<BATCH, CLK>(P, li);
+    const uint32_t ng = P.wh_wgs_g;
+    if (wg < ng)
+    {
+        const uint32_t n = P.hf_ver ? min(P.hf_plan_in->cnt_w, kWhMax) : 0u;
+        const uint32_t nw = ng * kWavesPerWG;
+        for (uint32_t e = wg * kWavesPerWG + (threadIdx.x >> 6); e < n * G; e += nw) wide_item<BATCH, G, CLK>(P, e / G, e % G, e);
+        return;
+    }
+    const uint32_t n = P.hf_ver ? min(P.hf_plan_in->cnt_l, kWhMax) : 0u;
+    const uint32_t nwg = P.wh_wgs - ng;
+    for (uint32_t li = wg - ng; li < n; li += nwg) wide_item_lds<BATCH, CLK>(P, li);
 }
 
 // Wave `wib` (0-3) of launch block bid of nblk: its work item after the heavy-first / XCD-band map.
@@ -492,10 +504,12 @@ __global__ void __launch_bounds__(kWG) k_render_wh(KParams P)
     wide_section<false, G>(P, blockIdx.x * kWavesPerWG + (threadIdx.x >> 6));
 }
 
-// the same section's LDS tier (kVarLdsSplit): one listed item per workgroup
+// the same section with the LDS tier after it (kVarLdsSplit: one listed item per workgroup), held to 7
+// waves / SIMD (the split walk: 80 VGPRs unbounded)
+template <uint32_t G>
 __global__ void __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(7, 8))) k_render_wh_lds(KParams P)
 {
-    wide_section_lds<false>(P, blockIdx.x);
+    wide_section_lds<false, G>(P, blockIdx.x);
 }
 
 // The multi-frame launch (KBatch): the launch's blocks are the frames' blocks, frame-major; the
@@ -572,7 +586,7 @@ __device__ __forceinline__ void batch_body(const KBatch& B)
         if (bid < nw)
         {
             if constexpr ((VAR & kVarLdsSplit) != 0)
-                wide_section_lds<true, (VAR & kVarWaveClock) != 0>(B.p[0], bid);
+                wide_section_lds<true, (VAR & kVarWideG4) ? 4u : 16u, (VAR & kVarWaveClock) != 0>(B.p[0], bid);
             else
                 wide_section<true, (VAR & kVarWideG4) ? 4u : 16u, (VAR & kVarWaveClock) != 0>(
                     B.p[0], bid * kWavesPerWG + (threadIdx.x >> 6));
@@ -1175,7 +1189,7 @@ kfn_t lanes_w64_kernel(int var)
 
 kfn_t wide_kernel(uint32_t g, bool lds)
 {
-    if (lds) return k_render_wh_lds;
+    if (lds) return g == 4u ? k_render_wh_lds<4> : (g == 16u ? k_render_wh_lds<16> : nullptr);
     return g == 4u ? k_render_wh<4> : (g == 16u ? k_render_wh<16> : nullptr);
 }
 
@@ -1213,7 +1227,13 @@ template <int VAR>
 kbfn_t batch_kernel_of(bool w64, bool o8)
 {
     if constexpr ((VAR & kVarLdsSplit) != 0)
-        return w64 ? nullptr : k_render_batch_lds<RT_TRI_MOLLER_TRUMBORE, VAR>;
+    {
+        // (the wave-clock arm spills at 7 waves: unbounded, 6)
+        if constexpr ((VAR & kVarWaveClock) != 0)
+            return w64 ? nullptr : k_render_batch<RT_TRI_MOLLER_TRUMBORE, VAR>;
+        else
+            return w64 ? nullptr : k_render_batch_lds<RT_TRI_MOLLER_TRUMBORE, VAR>;
+    }
     else
     {
         constexpr bool kO8 = (VAR & kVarWideFused) != 0 && (VAR & kVarWaveClock) == 0;
@@ -1231,6 +1251,7 @@ kbfn_t batch_kernel(int var, bool w64, bool o8)
     if (var == kFused) return batch_kernel_of<kFused>(w64, o8);
     if (var == (kFused | kVarWideG4)) return batch_kernel_of<kFused | kVarWideG4>(w64, o8);
     if (var == (kFused | kVarLdsSplit)) return batch_kernel_of<kFused | kVarLdsSplit>(w64, o8);
+    if (var == (kFused | kVarWideG4 | kVarLdsSplit)) return batch_kernel_of<kFused | kVarWideG4 | kVarLdsSplit>(w64, o8);
     // RT_KERNEL_FLAG_WAVE_CLOCK (debug timelines, tools/batch_waves.py): the bench pair's batched step
     // at one rank and with the fused wide section (either tier)
     if (var == (kVarAuto | kVarWaveClock)) return batch_kernel_of<kVarAuto | kVarWaveClock>(w64, o8);

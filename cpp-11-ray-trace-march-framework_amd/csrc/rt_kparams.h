@@ -50,7 +50,8 @@ constexpr uint32_t kCompactRefill = 48;     // RT_KERNEL_COMPACT default: refill
 // sum of wave costs of the measured frame
 // sum_full: the sum of wave costs of the last measured frame that rendered every item one lane
 // per sample (the wide section's span estimate; carried over by the plans of other frames)
-struct HfPlan { uint32_t cnt_hi, cnt_lo, maxc, cnt_w; unsigned long long sum; unsigned long long sum_full; };
+// cnt_l: work items listed for the wide section's LDS tier (kVarLdsSplit; the list's second half)
+struct HfPlan { uint32_t cnt_hi, cnt_lo, maxc, cnt_w; unsigned long long sum; unsigned long long sum_full; uint32_t cnt_l, pad; };
 
 struct KParams
 {
@@ -117,8 +118,8 @@ struct KParams
                                 // (a wide item: the sum over its waves)
     // wide section (kVarWideHeavy; wh_on == 0: off).  k_render_wh's wh_wgs workgroups trace the
     // work items the current plan lists as heavy (wh_list_in, plan->cnt_w of them), wh_g lanes
-    // per sample (16 at spp <= 4, 4 at spp 8-16) -- or, in the LDS tier (kVarLdsSplit), one
-    // 256-lane workgroup per item (wh_g = 4 waves), one lane per sample -- and the lane waves skip items whose
+    // per sample (16 at spp <= 4, 4 at spp 8-16) -- and, in the LDS tier (kVarLdsSplit), the next
+    // heaviest one 256-lane workgroup per item, one lane per sample -- and the lane waves skip items whose
     // wh_mark_in == hf_ver; with wh_wgs == 0 (no list seen yet, or a refresh frame) the lane
     // waves render every item.  k_hf_plan lists an item when its lane-mode cost passes
     // max(wh_floor, wh_alpha16 / 16 x the estimated frame span), and keeps the current plan's
@@ -126,11 +127,17 @@ struct KParams
     // them) except in a refresh frame.
     uint32_t wh_on, wh_wgs, wh_refresh, wh_g;
     uint32_t wh_floor, wh_alpha16;
+    // kVarLdsSplit (wh_lds = 1): items between wh_beta16 / 16 and wh_alpha16 / 16 of the span estimate are
+    // listed for the LDS tier (one 256-lane workgroup per item; the list's second half, wh_list + kWhMax;
+    // marks with bit 31), the heavier ones for the wh_g-lane tier
+    uint32_t wh_lds, wh_beta16;
+    uint32_t wh_wgs_g;          // the first wh_wgs_g of the section's workgroups run the G-lane tier (= wh_wgs
+                                // without the LDS tier), the rest the LDS tier
     const uint32_t *wh_mark_in;
     uint32_t *wh_mark_out;
     const uint32_t *wh_list_in;
     uint32_t *wh_list_out;
-    uint32_t *wh_host_cnt;      // host-mapped: the newest plan's wave count (sizes the next launches)
+    uint32_t *wh_host_cnt;      // host-mapped [2]: the newest plan's G-lane waves and LDS items (size the next launches)
     // output
     uint32_t *out;
     uint32_t pitch;             // frame mode: words per row of out
@@ -236,7 +243,7 @@ using kcfn_t = void (*)(KParams, uint32_t, uint32_t);
 using knfn_t = void (*)(KParams, uint32_t);
 kfn_t lanes_kernel(int tri, int var);          // k_render_lanes<tri, var>
 kfn_t lanes_w64_kernel(int var);               // k_render_lanes_w64<MT, var>
-kfn_t wide_kernel(uint32_t g, bool lds);       // k_render_wh<g>, g = 4 or 16; k_render_wh_lds (LDS tier)
+kfn_t wide_kernel(uint32_t g, bool lds);       // k_render_wh<g>, g = 4 or 16; k_render_wh_lds<g> (+ the LDS tier)
 kfn_t pixel_loop_kernel(int tri, int var);     // k_render_pixel_loop<tri, var>
 kcfn_t compact_kernel(int tri, int var);       // k_render_compact<tri, var>(P, n_items, refill)
 kbfn_t batch_kernel(int var, bool w64, bool o8 = false);   // k_render_batch / _w64 / _w64_o8<MT, var>

@@ -38,11 +38,11 @@ __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks, ui
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         while (__builtin_amdgcn_s_memrealtime() - t0 < delay) __builtin_amdgcn_s_sleep(64);
     }
-    __shared__ uint32_t s_max, s_hi, s_lo, s_w, s_bhi, s_blo, s_bw, s_last;
+    __shared__ uint32_t s_max, s_hi, s_lo, s_w, s_l, s_bhi, s_blo, s_bw, s_bl, s_last;
     __shared__ unsigned long long s_sum;
     if (threadIdx.x == 0u)
     {
-        s_max = s_hi = s_lo = s_w = 0u;
+        s_max = s_hi = s_lo = s_w = s_l = 0u;
         s_sum = 0ull;
     }
     __syncthreads();
@@ -51,14 +51,14 @@ __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks, ui
     const uint32_t thr = max(P.hf_floor, last.maxc >> (pos16 ? kHfPosShift : shift));
     const uint64_t span = (last.sum << 4) / kHfSlots;
     const uint32_t b0 = blockIdx.x * (kWG * kHfPlanPer) + threadIdx.x;
-    uint32_t tmax = 0u, wmasks = 0u, heavy = 0u, hi = 0u;
+    uint32_t tmax = 0u, wmasks = 0u, lmasks = 0u, heavy = 0u, hi = 0u;
     unsigned long long tsum = 0ull;
-    uint32_t rank[kHfPlanPer], wrank[kHfPlanPer];
+    uint32_t rank[kHfPlanPer], wrank[kHfPlanPer], lrank[kHfPlanPer];
 #pragma unroll
     for (uint32_t j = 0; j < kHfPlanPer; j++)
     {
         const uint32_t b = b0 + j * kWG;
-        uint32_t cost = 0u, sum = 0u, wmask = 0u;
+        uint32_t cost = 0u, sum = 0u, wmask = 0u, lmask = 0u;
         if (b < nblocks)
         {
             const uint4 c = reinterpret_cast<const uint4 *>(P.hf_cost)[b];      // kWavesPerWG == 4
@@ -75,16 +75,27 @@ __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks, ui
                 const uint32_t wt = max(P.wh_floor, uint32_t(min<uint64_t>(span * P.wh_alpha16 / 16u, 0xFFFFFFFFull)));
                 wmask = uint32_t(c.x > wt) | (uint32_t(c.y > wt) << 1) | (uint32_t(c.z > wt) << 2) |
                         (uint32_t(c.w > wt) << 3);
+                // the LDS tier (kVarLdsSplit): the next heaviest items, one workgroup each
+                if (P.wh_lds)
+                {
+                    const uint32_t lt = max(P.wh_floor, uint32_t(min<uint64_t>(span * P.wh_beta16 / 16u, 0xFFFFFFFFull)));
+                    lmask = (uint32_t(c.x > lt) | (uint32_t(c.y > lt) << 1) | (uint32_t(c.z > lt) << 2) |
+                             (uint32_t(c.w > lt) << 3)) & ~wmask;
+                }
             }
             if (P.wh_on && !P.wh_refresh && P.hf_ver)
             {
-                // sticky: the current plan's items stay listed (mark = the plan version)
+                // sticky: the current plan's items stay listed in their tier (mark = the plan version,
+                // bit 31: the LDS tier)
                 const uint4 m = reinterpret_cast<const uint4 *>(P.wh_mark_in)[b];
-                const uint32_t v = P.hf_ver;
+                const uint32_t v = P.hf_ver, vl = P.hf_ver | 0x80000000u;
                 wmask |= uint32_t(m.x == v) | (uint32_t(m.y == v) << 1) | (uint32_t(m.z == v) << 2) | (uint32_t(m.w == v) << 3);
+                lmask |= uint32_t(m.x == vl) | (uint32_t(m.y == vl) << 1) | (uint32_t(m.z == vl) << 2) |
+                         (uint32_t(m.w == vl) << 3);
+                wmask &= ~lmask;
             }
             // the heavy-first order ranks a block by its slowest wave left in the lane section
-            const uint32_t wm = wmask;
+            const uint32_t wm = wmask | lmask;
             cost = max(max((wm & 1u) ? 0u : c.x, (wm & 2u) ? 0u : c.y), max((wm & 4u) ? 0u : c.z, (wm & 8u) ? 0u : c.w));
         }
         uint32_t tb = thr;
@@ -96,9 +107,11 @@ __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks, ui
         tsum += sum;
         rank[j] = hv ? atomicAdd(h1 ? &s_hi : &s_lo, 1u) : 0u;
         wrank[j] = wmask ? atomicAdd(&s_w, uint32_t(__popc(wmask))) : 0u;
+        lrank[j] = lmask ? atomicAdd(&s_l, uint32_t(__popc(lmask))) : 0u;
         heavy |= uint32_t(hv) << j;
         hi |= uint32_t(h1) << j;
         wmasks |= wmask << (4u * j);
+        lmasks |= lmask << (4u * j);
     }
     if (tmax) atomicMax(&s_max, tmax);
     if (tsum) atomicAdd(&s_sum, tsum);
@@ -119,6 +132,7 @@ __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks, ui
         s_bhi = s_hi ? atomicAdd(&P.hf_plan_out->cnt_hi, s_hi) : 0u;
         s_blo = s_lo ? atomicAdd(&P.hf_plan_out->cnt_lo, s_lo) : 0u;
         s_bw = s_w ? atomicAdd(&P.hf_plan_out->cnt_w, s_w) : 0u;
+        s_bl = s_l ? atomicAdd(&P.hf_plan_out->cnt_l, s_l) : 0u;
     }
     __syncthreads();
 #pragma unroll
@@ -139,8 +153,8 @@ __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks, ui
         }
         // wide items: listed and marked for the next plan's frames (beyond kWhMax they stay in the
         // lane section)
-        const uint32_t wmask = (wmasks >> (4u * j)) & 15u;
-        uint32_t wr = wrank[j];
+        const uint32_t wmask = (wmasks >> (4u * j)) & 15u, lmask = (lmasks >> (4u * j)) & 15u;
+        uint32_t wr = wrank[j], lr = lrank[j];
         for (uint32_t k = 0; k < kWavesPerWG; k++)
             if (wmask & (1u << k))
             {
@@ -150,6 +164,16 @@ __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks, ui
                 {
                     P.wh_list_out[r] = item;
                     P.wh_mark_out[item] = P.hf_ver + 1u;
+                }
+            }
+            else if (lmask & (1u << k))
+            {
+                const uint32_t item = b * kWavesPerWG + k;
+                const uint32_t r = s_bl + lr++;
+                if (r < kWhMax)
+                {
+                    P.wh_list_out[kWhMax + r] = item;
+                    P.wh_mark_out[item] = (P.hf_ver + 1u) | 0x80000000u;
                 }
             }
     }
@@ -175,7 +199,10 @@ __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks, ui
         // hands the wide section's item count to the host (it sizes the section of later
         // launches) and re-arms the ticket
         if (P.wh_host_cnt)
-            *(volatile uint32_t *)P.wh_host_cnt = P.wh_g * min(vp->cnt_w, kWhMax);
+        {
+            P.wh_host_cnt[0] = P.wh_g * min(vp->cnt_w, kWhMax);     // the G-lane tier's waves
+            P.wh_host_cnt[1] = min(vp->cnt_l, kWhMax);              // the LDS tier's items (workgroups)
+        }
         *P.hf_ticket = 0u;
     }
 }
@@ -312,7 +339,7 @@ HfPeek hf_peek(const rt_scene *s, const KParams& P, uint64_t blocks, int var, ui
 // ONE device allocation per context (a new launch shape's first frame waits for the host's
 // allocation calls: seven of them took ~0.1 ms, profiles/r05i_first_frame_probe.json), the cleared
 // arrays first so one memset clears them: plans [2], ticket (+ pad to 16 B), marks [2][cap],
-// wh_marks [2][4 cap]; then cost [4 cap], lists [2][kHfFrontMax], wh_lists [2][kWhMax] (by version).  rt_scene_create sizes the first context for kHfPreBlocks, so a first frame up
+// wh_marks [2][4 cap]; then cost [4 cap], lists [2][kHfFrontMax], wh_lists [2][2][kWhMax] ([version][tier]).  rt_scene_create sizes the first context for kHfPreBlocks, so a first frame up
 // to that shape allocates nothing.
 int hf_alloc(HfCtx *c, uint64_t blocks)
 {
@@ -321,7 +348,7 @@ int hf_alloc(HfCtx *c, uint64_t blocks)
     c->mem = nullptr;
     const size_t head = sizeof(HfPlan) * 2 + 16u;
     const size_t cleared = head + sizeof(uint32_t) * (2u + 2u * kWavesPerWG) * blocks;
-    const size_t bytes = cleared + sizeof(uint32_t) * (kWavesPerWG * blocks + 2u * kHfFrontMax + 2u * kWhMax);
+    const size_t bytes = cleared + sizeof(uint32_t) * (kWavesPerWG * blocks + 2u * kHfFrontMax + 4u * kWhMax);
     RT_HIP(hipMalloc(&c->mem, bytes));
     char *m = static_cast<char *>(c->mem);
     c->plans = reinterpret_cast<HfPlan *>(m);
@@ -369,9 +396,9 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
         if (blocks > c->cap_blocks || !c->mem)
             if (int rc = hf_alloc(c, blocks)) return rc;
         RT_HIP(hipMemsetAsync(c->mem, 0, c->cleared_bytes, st));
-        c->wh_cnt = s->h_wh_cnt + (c - s->hf);         // the scene's mapped counters (rt_scene_create)
-        c->wh_cnt_dev = s->d_wh_cnt + (c - s->hf);
-        *(volatile uint32_t *)c->wh_cnt = 0u;
+        c->wh_cnt = s->h_wh_cnt + 2 * (c - s->hf);     // the scene's mapped counters (rt_scene_create)
+        c->wh_cnt_dev = s->d_wh_cnt + 2 * (c - s->hf);
+        c->wh_cnt[0] = c->wh_cnt[1] = 0u;
         c->nblocks = uint32_t(blocks);
         // front: 1 / hf_front_div of the blocks (an eighth), capped at hf_front_max (1024) -- or 1 / 128 of
         // a larger launch's blocks -- at most kHfFrontMax, a multiple of the XCD count so the natural
@@ -439,7 +466,10 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
     P.hf_ver = v;
     c->cam = cam_sig;
     c->frames++;
-    P.hf_floor = s->hf_floor;
+    // with the LDS tier the lone heavy waves have left the lane section, and its tail is the lane waves
+    // of 40-100 us that the natural order starts late: the front takes them from half the floor (a
+    // rank of 8's one-stream step 0.110 -> 0.096 ms at 50 k cycles, profiles/r06_lds_tier_ab.json)
+    P.hf_floor = (var & kVarLdsSplit) ? s->hf_floor / 2u : s->hf_floor;
     P.hf_ticket = c->ticket;
     P.hf_mark_in = c->marks + size_t(v & 1u) * c->cap_blocks;
     P.hf_mark_out = c->marks + size_t((v + 1u) & 1u) * c->cap_blocks;
@@ -450,7 +480,6 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
     P.hf_cost = c->cost;
     if (var & kVarWideHeavy)
     {
-        c->lds = (var & kVarLdsSplit) != 0;
         // spp <= 4: 16 lanes per sample; spp 8-16: a pixel's samples fill a wave at 4 lanes each.
         // The section holds wh_g waves per listed item of the newest plan the host has seen (a
         // plan or two old: the count is read without waiting; the section is persistent over the
@@ -458,12 +487,23 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
         // refresh frame): no section, and the lane kernel renders every item itself.
         // Refresh: every kWhRefresh-th frame renders every item one lane per sample, so the next
         // plan re-ranks all items on lane-mode costs (the wide set is otherwise sticky).
-        // The LDS tier (kVarLdsSplit): one 256-lane workgroup per item (wh_g = its 4 waves).
-        P.wh_g = (var & kVarLdsSplit) ? kWavesPerWG : (P.spp <= 4u ? 16u : 4u);
-        const uint32_t units = *(volatile uint32_t *)c->wh_cnt;         // waves: k_hf_plan counts them
+        // The LDS tier (kVarLdsSplit): its items one 256-lane workgroup each (k_hf_plan counts its waves).
+        P.wh_g = P.spp <= 4u ? 16u : 4u;
+        P.wh_lds = (var & kVarLdsSplit) ? 1u : 0u;
+        P.wh_beta16 = s->wh_beta16;
+        // (k_hf_plan writes the counts: the G-lane tier's waves, the LDS tier's items)
+        const uint32_t units = c->wh_cnt[0], litems = P.wh_lds ? c->wh_cnt[1] : 0u;
         P.wh_on = 1u;
         P.wh_refresh = (c->frames - 1u) % kWhRefresh == 0u;       // frames counts this one
-        P.wh_wgs = P.wh_refresh ? 0u : (units + kWavesPerWG - 1u) / kWavesPerWG;
+        // each tier gets workgroups of its own, at least one once anything is listed (a tier's list may
+        // have grown since the counts the host saw: its loop is persistent): the G-lane tier the first
+        // wh_wgs_g, the LDS tier the rest, one item per workgroup at a time, both from the launch's start
+        P.wh_wgs = P.wh_wgs_g = 0u;
+        if (!P.wh_refresh && (units || litems))
+        {
+            P.wh_wgs_g = std::max(1u, (units + kWavesPerWG - 1u) / kWavesPerWG);
+            P.wh_wgs = P.wh_wgs_g + (P.wh_lds ? std::max(1u, litems) : 0u);
+        }
         P.wh_floor = s->wh_floor;
         // a rank of 2 of a batched step lists more (its span estimate includes the other frames'
         // work); one scene's own rank-of-2 launch measured 25 % slower with it
@@ -476,8 +516,8 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
                                                                           : s->wh_alpha16;
         P.wh_mark_in = c->wh_marks + size_t(v & 1u) * kWavesPerWG * c->cap_blocks;
         P.wh_mark_out = c->wh_marks + size_t((v + 1u) & 1u) * kWavesPerWG * c->cap_blocks;
-        P.wh_list_in = c->wh_lists + size_t(v & 1u) * kWhMax;
-        P.wh_list_out = c->wh_lists + size_t((v + 1u) & 1u) * kWhMax;
+        P.wh_list_in = c->wh_lists + size_t(v & 1u) * 2u * kWhMax;
+        P.wh_list_out = c->wh_lists + size_t((v + 1u) & 1u) * 2u * kWhMax;
         P.wh_host_cnt = c->wh_cnt_dev;
     }
     return RT_OK;

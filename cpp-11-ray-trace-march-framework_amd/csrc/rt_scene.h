@@ -53,9 +53,8 @@ struct HfCtx
     uint32_t *ticket = nullptr;         // k_hf_plan's workgroup ticket
     uint32_t *wh_marks = nullptr;       // [2][cap_blocks * kWavesPerWG] wide items, by version parity
     uint32_t *wh_lists = nullptr;       // [2][kWhMax]
-    uint32_t *wh_cnt = nullptr;         // host-mapped: the newest plan's wide item count (rt_scene::h_wh_cnt)
+    volatile uint32_t *wh_cnt = nullptr;  // host-mapped [2]: the newest plan's G-lane waves, LDS items (rt_scene::h_wh_cnt)
     uint32_t *wh_cnt_dev = nullptr;     // its device address
-    bool lds = false;                   // its wide section runs the LDS tier (kVarLdsSplit; rt_debug_wide_tiers)
     uint32_t frames = 0;                // frames rendered with this shape
     uint32_t ver = 0;                   // version of the plan the frames use
     // a plan launched on the scene's plan stream after a measured frame (launch_plans): version pend
@@ -107,7 +106,7 @@ struct rt_scene
     uint32_t clk_items = 0;
     // AUTO heavy-first order: per launch shape, which blocks the previous frame found heavy
     rtk::HfCtx hf[rtk::kHfCtxs];
-    uint32_t *h_wh_cnt = nullptr;       // [kHfCtxs] host-mapped counters of the contexts (one allocation)
+    uint32_t *h_wh_cnt = nullptr;       // [kHfCtxs][2] host-mapped counters of the contexts (one allocation)
     uint32_t *d_wh_cnt = nullptr;
     uint64_t hf_clock = 0;
     uint64_t hf_evictions = 0;      // launch shapes that displaced another's state (rt_scene_info)
@@ -131,13 +130,16 @@ struct rt_scene
     uint32_t wh_auto_refs = 128;    // RT_WH_AUTO_REFS: AUTO takes the wide section for >= 2-rank
                                     // shards of scenes with a cell list this long
     uint32_t wg64 = 1;              // RT_WG64: AUTO launches of >= wg64_min_blocks 256-lane blocks run
-    uint32_t wg64_min_blocks = 8192; // as one-wave workgroups (k_render_lanes_w64; RT_WG64_MIN_BLOCKS)
+    uint32_t wg64_min_blocks = 8192; // as one-wave workgroups (k_render_lanes_w64)
     uint32_t wg64_batch_min_blocks = 0;  // the same for batched launches
     uint32_t wg64_max_refs = 1024;  // RT_WG64_MAX_REFS: single-frame launches of scenes with a cell of this many
                                     // references keep 256-lane workgroups
-    uint32_t wh_lds = 0xE;          // RT_WH_LDS: bit log2(N) (3: N >= 8): a rank of N's wide section runs the LDS
+    uint32_t wh_lds = 0x8;          // RT_WH_LDS: bit log2(N) (3: N >= 8): a rank of N's wide section has the LDS
                                     // tier (kVarLdsSplit: one 256-lane workgroup per item, its cell lists split
-                                    // between the four waves) instead of 16 lanes per sample
+                                    // between the four waves) for its next heaviest items,
+                                    // in launches without RT_KERNEL_FLAG_OVERLAP
+    uint32_t wh_beta16 = 24;        // RT_WH_BETA16: the LDS tier's threshold, sixteenths of the span estimate
+                                    // (items above it and at most wh_alpha16 / 16)
     uint32_t wg64_o8 = 0x2;         // RT_WG64_O8: bit log2(N) (3: N >= 8): a rank of N's fused one-wave
                                     // batch kernel held to 8 waves / SIMD
     uint32_t wg64_wide = 0xA;       // RT_WG64_WIDE: bit log2(N) (3: N >= 8): one-wave workgroups also

@@ -598,9 +598,10 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
         // (and every wide-section launch of >= 64 blocks: its lane kernel's heaviest items)
         const bool front = kind == RT_KERNEL_AUTO && P.isect == RT_ISECT_GRID && !(kvar & kVarWaveClock) &&
                            (blocks >= s->hf_min_blocks || (wide_heavy && blocks >= 64u));
-        // the wide section's LDS tier (kVarLdsSplit) per rank count (wh_lds, bit log2 N)
+        // the wide section's LDS tier (kVarLdsSplit) per rank count (wh_lds, bit log2 N), without
+        // RT_KERNEL_FLAG_OVERLAP (as launch_batch)
         const uint32_t lg_ranks = P.nranks >= 8u ? 3u : (P.nranks >= 4u ? 2u : (P.nranks >= 2u ? 1u : 0u));
-        const bool lds = wide_heavy && ((s->wh_lds >> lg_ranks) & 1u) != 0u;
+        const bool lds = wide_heavy && ((s->wh_lds >> lg_ranks) & 1u) != 0u && !(f->kernel & RT_KERNEL_FLAG_OVERLAP);
         if (front || wide_heavy)
         {
             if (int rc = hf_prepare(s, P, blocks, kvar | (lds ? kVarLdsSplit : 0), front, st)) return rc;
@@ -728,11 +729,14 @@ int launch_batch(rt_scene *const *S, const rt_frame *F, uint32_t n, KParams *P, 
     const bool fused = wide_heavy;
     const bool clk = (F[0].kernel & RT_KERNEL_FLAG_WAVE_CLOCK) != 0u;
     const uint32_t lg_ranks = P[0].nranks >= 8u ? 3u : (P[0].nranks >= 4u ? 2u : (P[0].nranks >= 2u ? 1u : 0u));
-    // the section's LDS tier (kVarLdsSplit) per rank count (wh_lds, bit log2 N): one
-    // 256-lane workgroup per listed item, so the whole grid runs 256-lane workgroups
-    const bool lds = fused && ((S[0]->wh_lds >> lg_ranks) & 1u) != 0u;
+    // the section's LDS tier (kVarLdsSplit) per rank count (wh_lds, bit log2 N), for
+    // launches that do not ask to overlap the previous one (RT_KERNEL_FLAG_OVERLAP): there the launch's
+    // tail is exposed and the tier shortens it (a rank of 8's step 0.106 -> 0.096 ms), while an
+    // overlapped launch's tail is filled by the next one and the tier's 256-lane grid costs more
+    // (0.0875 -> 0.090 ms, profiles/r06_lds_tier_ab.json)
+    const bool lds = fused && ((S[0]->wh_lds >> lg_ranks) & 1u) != 0u && !(F[0].kernel & RT_KERNEL_FLAG_OVERLAP);
     const int kvar = var | (wide_heavy ? kVarWideHeavy : 0) | (fused ? kVarWideFused : 0) |
-                     (fused && spp > 4u && !lds ? kVarWideG4 : 0) | (lds ? kVarLdsSplit : 0) |
+                     (fused && spp > 4u ? kVarWideG4 : 0) | (lds ? kVarLdsSplit : 0) |
                      (clk ? kVarWaveClock : 0);
     if (!batch_kernel(kvar, false)) return RT_E_INVALID;
     const uint32_t wgpt = (kTilePix * spp) / kWG;
@@ -801,7 +805,12 @@ int launch_batch(rt_scene *const *S, const rt_frame *F, uint32_t n, KParams *P, 
         if (int rc = hf_prepare(s0, P[0], blocks, kvar, front, st, ident | 1u, cams)) return rc;
     // fused: the wide section's workgroups lead the grid, a multiple of the XCD count so the lane
     // blocks keep their block -> XCD assignment
-    if (fused && P[0].wh_wgs) P[0].wh_wgs = (P[0].wh_wgs + kXcds - 1u) & ~(kXcds - 1u);
+    // (the rounding's extra workgroups join the LDS tier, or without one the G-lane tier)
+    if (fused && P[0].wh_wgs)
+    {
+        P[0].wh_wgs = (P[0].wh_wgs + kXcds - 1u) & ~(kXcds - 1u);
+        if (!P[0].wh_lds) P[0].wh_wgs_g = P[0].wh_wgs;
+    }
     uint32_t grid = uint32_t(blocks) + P[0].hf_front + (fused ? P[0].wh_wgs : 0u);
     // one-wave workgroups (k_render_batch_w64, as k_render_lanes_w64): the same blocks and order.
     // Without a wide section (N = 1) the bench pair took 0.569 vs 0.598 ms with 256-lane
@@ -826,7 +835,7 @@ int launch_batch(rt_scene *const *S, const rt_frame *F, uint32_t n, KParams *P, 
     if (clk)
     {
         // one record per lane item and per (listed item, wave) of the wide section
-        const size_t need = (size_t(blocks) * kWavesPerWG + size_t(kWhMax) * 16u) * 4u;
+        const size_t need = (size_t(blocks) * kWavesPerWG + size_t(kWhMax) * 17u) * 4u;
         if (need > s0->clk_cap)
         {
             if (s0->d_clk) RT_HIP(hipFree(s0->d_clk));
@@ -1019,7 +1028,6 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
     s->hf_shift = std::min(env_tunable("RT_HF_SHIFT", s->hf_shift), 8u);
     s->hf_pos16 = std::min(env_tunable("RT_HF_POS16", s->hf_pos16), 64u);
     s->wg64 = env_tunable("RT_WG64", s->wg64);
-    s->wg64_min_blocks = env_tunable("RT_WG64_MIN_BLOCKS", s->wg64_min_blocks);
     s->wh_floor = env_tunable("RT_WH_FLOOR", s->wh_floor);
     s->wh_alpha16 = env_tunable("RT_WH_ALPHA16", s->wh_alpha16);
     s->wh_alpha16_n2 = env_tunable("RT_WH_ALPHA16_N2", s->wh_alpha16_n2);
@@ -1029,6 +1037,7 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
     s->wg64_wide = env_tunable("RT_WG64_WIDE", s->wg64_wide);
     s->wg64_o8 = env_tunable("RT_WG64_O8", s->wg64_o8);
     s->wh_lds = env_tunable("RT_WH_LDS", s->wh_lds);
+    s->wh_beta16 = env_tunable("RT_WH_BETA16", s->wh_beta16);
     s->hf_follow = env_tunable("RT_HF_FOLLOW", s->hf_follow);
     for (int a = 0; a < 3; a++)
     {
@@ -1281,8 +1290,8 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
     if (int rc = new_event(s->kt1[0], s->ev_time_flags)) return rc;
     // the heavy-first contexts' host-mapped counters, and the frame tables at a 4K x 16 spp capacity:
     // allocated here so a new launch shape's first frame waits for no allocation call
-    RT_HIP(hipHostMalloc(&s->h_wh_cnt, sizeof(uint32_t) * kHfCtxs, hipHostMallocMapped | hipHostMallocCoherent));
-    std::memset(s->h_wh_cnt, 0, sizeof(uint32_t) * kHfCtxs);
+    RT_HIP(hipHostMalloc(&s->h_wh_cnt, sizeof(uint32_t) * 2 * kHfCtxs, hipHostMallocMapped | hipHostMallocCoherent));
+    std::memset(s->h_wh_cnt, 0, sizeof(uint32_t) * 2 * kHfCtxs);
     {
         void *dev = nullptr;
         RT_HIP(hipHostGetDevicePointer(&dev, s->h_wh_cnt, 0));
@@ -1943,7 +1952,7 @@ int rt_debug_wide_items(rt_scene *s, uint32_t *count)
     for (const HfCtx& h : s->hf)
         if (h.wh_cnt && (!c || h.used > c->used)) c = &h;
     if (c) RT_HIP(hipDeviceSynchronize());
-    *count = c ? *(volatile uint32_t *)c->wh_cnt : 0u;
+    *count = c ? c->wh_cnt[0] + kWavesPerWG * c->wh_cnt[1] : 0u;
     return RT_OK;
 }
 
@@ -1963,7 +1972,7 @@ int rt_debug_wide_tiers(rt_scene *s, uint32_t *listed, uint32_t *lds)
     HfPlan pl;
     RT_HIP(hipMemcpy(&pl, c->plans + (nv & 1u), sizeof(pl), hipMemcpyDeviceToHost));
     *listed = std::min(pl.cnt_w, kWhMax);
-    *lds = c->lds ? *listed : 0u;
+    *lds = std::min(pl.cnt_l, kWhMax);
     return RT_OK;
 }
 

@@ -183,110 +183,26 @@ def test_overlap_single_frames_after_batch(golden):
 
 
 
-def _frame_ms(render, stream, reps=8):
-    """Median device time of one launch (render(stream)) alone on `stream`."""
-    import torch
-    ts = []
-    for i in range(reps + 2):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        render(stream)
-        e1.record(stream)
-        torch.cuda.synchronize()
-        if i >= 2:
-            ts.append(e0.elapsed_time(e1))
-    return sorted(ts)[len(ts) // 2]
 
-
-def _plan_race_steps(step_ms, render, fill, check, set_delay, streams, steps=24):
-    """The ordering HfCtx::fence guarantees (DESIGN.md §4.20, its table), made deterministic.  Steps of a
-    fresh launch shape alternate two streams with RT_KERNEL_FLAG_OVERLAP.  Step 16 is measured: its plan
-    (k_hf_plan) runs on the plan stream after it, here first idling 1.4 x one step's device time
-    (rt_debug_set_plan_delay).  Step 18 adopts the plan while it still runs (it waits for it; the plan
-    becomes the shape's fence).  Step 17 is made to start after step 16 has ended (an event the test
-    adds), so step 19 -- on the other stream, which by itself orders it only after step 17 -- is issued
-    while the plan still idles: unordered, its front section would read the cleared plan (nothing listed)
-    and its natural section, once the plan has written its marks, skip the listed blocks, leaving their
-    pixels at the sentinel.  With the fence step 19 waits for the plan, and every frame equals the
-    reference's; without it (tools/build_variant.sh nofence -DRT_DEBUG_NO_PLAN_FENCE) this fails.
-    step_ms: one step's device time alone; render(i, stream), fill(i) (on the current stream), check(i)."""
-    import torch
-    set_delay(int(1400 * step_ms))
-    torch.cuda.synchronize()
-    for i in range(steps):
-        s = streams[i % 2]
-        if i == 17:
-            e = torch.cuda.Event()
-            e.record(streams[0])
-            s.wait_event(e)
-        with torch.cuda.stream(s):
-            fill(i)
-        render(i, s)
-    torch.cuda.synchronize()
-    set_delay(0)
-    for i in range(steps):
-        check(i)
-
-
-def test_overlap_plan_race_single_frames(golden):
-    """_plan_race_steps on single-frame launches of a fresh scene 4 (head) at 1080p x 4."""
-    import torch
-    hs = rtm.HostScene.load(4)
-    gs, gm = rtm.GpuScene(hs, 0), rtm.GpuScene(hs, 0)
-    try:
-        streams = [torch.cuda.Stream(), torch.cuda.Stream()]
-        outs = [torch.zeros(W * H, dtype=torch.int32, device="cuda") for _ in range(24)]
-        scratch = torch.zeros(W * H, dtype=torch.int32, device="cuda")
-        torch.cuda.synchronize()
-        fm = gm.frame(W, H, SPP)             # (timed on its own scene: the shape under test starts fresh)
-        ms = _frame_ms(lambda s: gm.render_frame_device(fm, scratch.data_ptr(), s.cuda_stream), streams[0])
-        f = gs.frame(W, H, SPP, kernel=rtm.RT_KERNEL_FLAG_OVERLAP)
-        want = golden["frames_1080p4"]["4"]["bgra_sha256"]
-
-        def check(i):
-            assert sha(outs[i]) == want, i
-        _plan_race_steps(ms, lambda i, s: gs.render_frame_device(f, outs[i].data_ptr(), s.cuda_stream),
-                         lambda i: outs[i].fill_(0x5A5A5A5A), check, gs.set_plan_delay, streams)
-    finally:
-        torch.cuda.synchronize()
-        gs.close()
-        gm.close()
-        hs.close()
-
-
-def test_overlap_plan_race_batched(golden):
-    """_plan_race_steps on the bench pair's batched step (killeroo, Cornell) at one rank, fresh scenes."""
-    import torch
-    sids = (8, 1)
-    hss = [rtm.HostScene.load(s) for s in sids]
-    gss = [rtm.GpuScene(h, 0) for h in hss]
-    gms = [rtm.GpuScene(h, 0) for h in hss]
-    try:
-        streams = [torch.cuda.Stream(), torch.cuda.Stream()]
-        outs = [[torch.zeros(W * H, dtype=torch.int32, device="cuda") for _ in sids] for _ in range(24)]
-        scratch = [torch.zeros(W * H, dtype=torch.int32, device="cuda") for _ in sids]
-        torch.cuda.synchronize()
-        fms = [g.frame(W, H, SPP) for g in gms]
-        ms = _frame_ms(lambda s: rtm.render_batch_device(gms, fms, [b.data_ptr() for b in scratch],
-                                                          stream=s.cuda_stream), streams[0])
-        fs = [g.frame(W, H, SPP, kernel=rtm.RT_KERNEL_FLAG_OVERLAP) for g in gss]
-
-        def fill(i):
-            for b in outs[i]:
-                b.fill_(0x5A5A5A5A)
-
-        def check(i):
-            for sid, b in zip(sids, outs[i]):
-                assert sha(b) == golden["frames_1080p4"][str(sid)]["bgra_sha256"], (sid, i)
-
-        def set_delay(us):
-            gss[0].set_plan_delay(us)       # the batch's plans are scene 0's (killeroo)
-        _plan_race_steps(ms, lambda i, s: rtm.render_batch_device(gss, fs, [b.data_ptr() for b in outs[i]],
-                                                                  stream=s.cuda_stream),
-                         fill, check, set_delay, streams)
-    finally:
-        torch.cuda.synchronize()
-        for g in gss + gms:
-            g.close()
-        for h in hss:
-            h.close()
+@pytest.mark.parametrize("mode", ["single", "batched"])
+@pytest.mark.timeout(180)
+def test_overlap_plan_race(mode):
+    """The plan-adoption race of DESIGN.md §4.21 made deterministic (tests/plan_race_child.py: a plan idling
+    1.4 x a step inside k_hf_plan, rt_debug_set_plan_delay, while a frame on the other stream -- ordered only
+    by its own stream -- is issued before the plan has written its lists and marks): single-frame launches
+    of scene 4, and the bench pair's batched step.  Every frame must equal the reference's (HfCtx::fence
+    orders the frame after the plan); the library built without the fence (tools/build_variant.sh nofence
+    -DRT_DEBUG_NO_PLAN_FENCE, RT_TRACER_LIB=librt_tracer_nofence.so) fails it with thousands of sentinel
+    pixels (profiles/r06_plan_race_nofence.json).  In a child process with GPU_MAX_HW_QUEUES=16: the
+    streams need hardware queues of their own, or the runtime's 4 queues run some of them in order."""
+    import json
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, GPU_MAX_HW_QUEUES="16")
+    r = subprocess.run([sys.executable, os.path.join(here, "plan_race_child.py"), mode], env=env, capture_output=True,
+                       text=True, timeout=170)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads(next(l for l in r.stdout.splitlines() if l.startswith("{")))
+    assert out["delay_us"] > 0 and out["bad"] == {}, out

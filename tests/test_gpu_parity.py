@@ -235,11 +235,11 @@ def test_shard_hits_rank_of_8(golden, scenes, sid, monkeypatch):
 
 @pytest.mark.parametrize("sid", [4, 5, 8])
 def test_wide_section_tiers_agree(golden, sid, monkeypatch):
-    """The wide section's two tiers -- the LDS tier (default from 2 ranks: one 256-lane workgroup per
-    listed item, its cell lists split between the four waves and reduced through LDS) and the lane tier
-    (RT_WH_LDS=0: 16 lanes per sample, butterfly) -- render the same shards at a rank of 8, every rank,
-    through a refresh of the list, single-frame launches and batched ones; the assembled frame is the
-    reference's."""
+    """The wide section with its LDS tier (default from 2 ranks: the items between beta and alpha of the
+    span estimate one 256-lane workgroup each, their cell lists split between the four waves and reduced
+    through LDS; the heavier ones 16 lanes per sample) and without it (RT_WH_LDS=0: every listed item 16
+    lanes per sample, butterfly) render the same shards at a rank of 8, every rank, five frames each
+    (the lists planned, then used); the assembled frame is the reference's."""
     import torch
     W, H, N = 1920, 1080, 8
     hs = rtm.HostScene.load(sid)
@@ -264,7 +264,9 @@ def test_wide_section_tiers_agree(golden, sid, monkeypatch):
             torch.cuda.synchronize()
             assert sha_dev(out) == want, (sid, g is gb)
             listed, lds = g.wide_tiers()
-            assert listed > 0 and lds == (listed if g is gb else 0), (sid, listed, lds)
+            assert listed + lds > 0 and (g is gb or lds == 0), (sid, listed, lds)
+            if sid == 8 and g is gb:
+                assert lds > 0, (sid, listed, lds)        # killeroo's rank of 8 fills the LDS tier
     finally:
         ga.close()
         gb.close()

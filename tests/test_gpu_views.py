@@ -256,14 +256,15 @@ def test_bary_full_frame_records(golden, scenes, sid):
     expect(b, shas(rec))
 
 
-@pytest.mark.parametrize("nranks", [1, 8])
-def test_moving_camera_views_batched(golden, nranks):
+@pytest.mark.parametrize("nranks,overlap", [(1, True), (8, True), (8, False)], ids=["1", "8", "8-one-stream"])
+def test_moving_camera_views_batched(golden, nranks, overlap):
     """bench.py's moving_camera leg pinned to the reference: the bench pair (killeroo first, bench.py's
     order at one rank) orbiting 0.5 degrees per frame about the world y axis (bench.orbit_cam), 27
     consecutive frames batched as the leg renders them -- fresh scenes, every frame a new origin
     (k_origin_pre before its render) and a new view whose heavy-first order (and at a rank of 8 the wide
-    section's list, LDS tier) is re-planned from the frame before (RT_HF_FOLLOW), consecutive steps
-    overlapped on two streams into sentinel-filled buffers.  The frames and per-sample hit IDs of orbit
+    section's list) is re-planned from the frame before (RT_HF_FOLLOW), consecutive steps overlapped on two
+    streams into sentinel-filled buffers (one-stream: without RT_KERNEL_FLAG_OVERLAP, so a rank of 8's
+    section has its LDS tier).  The frames and per-sample hit IDs of orbit
     steps 0-2 and 24-26 equal the reference's own render of the same camera bits (refdriver render
     --view, oracle/gen_golden.py moving_views; the bits are checked against bench.orbit_cam on the CPU,
     tests/test_oracle_golden.py)."""
@@ -283,7 +284,7 @@ def test_moving_camera_views_batched(golden, nranks):
         for j in range(steps):
             row = []
             for sid, hs, gs in zip(sids, hss, gss):
-                f = gs.frame(W, H, SPP, kernel=rtm.RT_KERNEL_FLAG_OVERLAP)
+                f = gs.frame(W, H, SPP, kernel=rtm.RT_KERNEL_FLAG_OVERLAP if overlap else rtm.RT_KERNEL_AUTO)
                 c = bench.orbit_cam(hs.cam, bench.ORBIT_DEG * (j + 1))
                 for k in range(16):
                     f.cam[k] = float(c[k])
@@ -301,7 +302,7 @@ def test_moving_camera_views_batched(golden, nranks):
         scratch = [[torch.empty(nranks * e, dtype=torch.int32, device="cuda") for _ in sids] for _ in range(2)]
         torch.cuda.synchronize()
         for j in range(steps):
-            s = streams[j % 2]
+            s = streams[j % 2 if overlap else 0]
             bufs = outs.get(j, scratch[j % 2])
             with torch.cuda.stream(s):
                 for b in bufs:

@@ -71,6 +71,7 @@ def main():
     re_ = np.where(re_ < rs, re_ + (1 << 28), re_)
     cyc = (c[:, 1] - c[:, 0]).astype(np.int64)
     wide = (lo2 & 0x80000000) != 0
+    lds = wide & ((lo2 & 0x7FFFFFFF) >= 4096)         # the LDS tier's items (list entries from kWhMax)
     frame = np.where(wide, -1, lo2 & 15)
     uni = np.where(wide, 0, lo2 >> 4)                  # lane waves: records tested wave-uniformly
     lit = np.where(wide, 0, lo3)                       # ... and per-lane list iterations
@@ -90,7 +91,8 @@ def main():
         return int(ts[above[-1]]) if len(above) else None
     order = np.argsort(e_)
     kinds = {}
-    for name, m in (("wide", wide), *[(f"lane_frame{f}", (~wide) & (frame == f)) for f in range(len(a.scenes))]):
+    for name, m in (("wide", wide & ~lds), ("lds", lds),
+                    *[(f"lane_frame{f}", (~wide) & (frame == f)) for f in range(len(a.scenes))]):
         if not m.any():
             continue
         kinds[name] = {"waves": int(m.sum()), "start_ns": [int(s_[m].min()), q(s_[m], 50), int(s_[m].max())],
@@ -103,7 +105,7 @@ def main():
            "resident_fall_ns": {"75%": fall(0.75), "50%": fall(0.5), "25%": fall(0.25), "10%": fall(0.1)},
            "start_ns_max": int(s_.max()), "kinds": kinds, "resident_40pts": res,
            "cycles_per_ns": round(float(np.median(cyc / np.maximum(d_, 1))), 3),
-           "last10": [{"kind": "wide" if wide[i] else f"lane_frame{frame[i]}", "item": int(lo3[i]) if wide[i] else None,
+           "last10": [{"kind": ("lds" if lds[i] else "wide") if wide[i] else f"lane_frame{frame[i]}", "item": int(lo3[i]) if wide[i] else None,
                        "start_ns": int(s_[i]), "dur_ns": int(d_[i]), "xcd": int(xcd[i]),
                        "uniform_records": int(uni[i]), "lane_iterations": int(lit[i])} for i in order[-10:]],
            "longest_lane_waves": [{"frame": int(frame[i]), "dur_ns": int(d_[i]), "start_ns": int(s_[i]),

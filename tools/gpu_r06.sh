@@ -30,14 +30,40 @@ for step in "$@"; do
     records) run records 600 $PYT tests/test_gpu_records.py tests/test_gpu_overlap.py tests/test_gpu_views.py -m gpu ;;
     gpu) run gpu 1100 $PYT tests -m gpu ;;
     scale) run scale_lds 400 python3 -u tools/shard_scaling.py --steady --batch --overlap --scenes 1 8 --out ${T}_scale_lds 0
-           run scale_lanes 400 env RT_WH_LDS=0 python3 -u tools/shard_scaling.py --steady --batch --overlap --scenes 1 8 --out ${T}_scale_lanes 0 ;;
+           run scale_lanes 400 env RT_WH_LDS=0 RT_WH_BETA16=16 python3 -u tools/shard_scaling.py --steady --batch --overlap --scenes 1 8 --out ${T}_scale_lanes 0 ;;
     bench) run bench 300 python -u bench.py ;;
     race) run race_prod 200 python3 -u tools/plan_race_probe.py --out ${T}_race_prod
           run race_nofence 200 env RT_TRACER_LIB=librt_tracer_nofence.so python3 -u tools/plan_race_probe.py --out ${T}_race_nofence ;;
-    alpha) for tier in 0 14; do for a in 8 16 24 32 48; do
-               run alpha_${tier}_${a} 200 env RT_WH_LDS=$tier RT_WH_ALPHA16=$a python3 -u tools/shard_scaling.py --steady \
-                   --scenes 8 --out ${T}_alpha_${tier}_${a} 0
-           done; done ;;
+    waves) run waves_lanes 200 env RT_WH_LDS=0 python3 -u tools/batch_waves.py --out ${T}_waves_lanes
+           for b in 16 24; do
+               run waves_lds_$b 200 env RT_WH_BETA16=$b python3 -u tools/batch_waves.py --out ${T}_waves_lds_$b
+           done ;;
+    floor) for cfg in "0 16 100000" "0 16 50000" "0 16 25000" "14 16 100000" "14 16 50000" "14 16 25000" "14 24 50000" "14 24 25000"; do
+               set -- $cfg
+               run floor_$1_$2_$3 200 env RT_WH_LDS=$1 RT_WH_BETA16=$2 RT_HF_FLOOR=$3 python3 -u tools/shard_scaling.py \
+                   --steady --batch --overlap --scenes 1 8 --out ${T}_floor_$1_$2_$3 0
+           done ;;
+    floor2) for cfg in "0 16 100000" "14 16 50000" "14 24 50000" "14 24 100000" "14 32 50000"; do
+               set -- $cfg
+               run floor2_$1_$2_$3 200 env RT_WH_LDS=$1 RT_WH_BETA16=$2 RT_HF_FLOOR=$3 python3 -u tools/shard_scaling.py \
+                   --steady --batch --overlap --scenes 1 8 --out ${T}_floor2_$1_$2_$3 0
+           done
+           run waves2_lds 200 env RT_WH_BETA16=24 RT_HF_FLOOR=50000 python3 -u tools/batch_waves.py --out ${T}_waves2_lds ;;
+    order) for cfg in "0 16 100000" "0 16 50000" "14 24 50000" "8 24 50000" "8 24 30000"; do
+               set -- $cfg
+               run order_$1_$2_$3 200 env RT_WH_LDS=$1 RT_WH_BETA16=$2 RT_HF_FLOOR=$3 python3 -u tools/shard_scaling.py \
+                   --steady --batch --overlap --scenes 8 1 --out ${T}_order_$1_$2_$3 0
+           done ;;
+    queues) run q4_scale 200 python3 -u tools/shard_scaling.py --steady --batch --overlap --scenes 1 8 --out ${T}_q4_scale 0
+            run q16_scale 200 env GPU_MAX_HW_QUEUES=16 python3 -u tools/shard_scaling.py --steady --batch --overlap --scenes 1 8 --out ${T}_q16_scale 0
+            run q4_bench 300 python -u bench.py --steps 200 --warmup 100 --no-cpu-baseline --no-end-to-end --no-first-frame --no-moving-camera --no-legs
+            run q16_bench 300 env GPU_MAX_HW_QUEUES=16 python -u bench.py --steps 200 --warmup 100 --no-cpu-baseline --no-end-to-end --no-first-frame --no-moving-camera --no-legs ;;
+    raceq) run raceq_nofence 200 env GPU_MAX_HW_QUEUES=16 RT_TRACER_LIB=librt_tracer_nofence.so python3 -u tools/plan_race_probe.py --out ${T}_raceq_nofence ;;
+    tiers) for cfg in "0 32 16" "14 32 8" "14 32 12" "14 32 16" "14 32 24" "14 48 16" "14 64 16"; do
+               set -- $cfg
+               run tiers_$1_$2_$3 200 env RT_WH_LDS=$1 RT_WH_ALPHA16=$2 RT_WH_BETA16=$3 python3 -u tools/shard_scaling.py \
+                   --steady --batch --overlap --scenes 1 8 --out ${T}_tiers_$1_$2_$3 0
+           done ;;
     *) echo "unknown step $step"; exit 2 ;;
     esac
 done

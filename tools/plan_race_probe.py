@@ -21,7 +21,7 @@ sys.modules["rtm"] = rtm
 spec.loader.exec_module(rtm)
 ap = argparse.ArgumentParser()
 ap.add_argument("--scene", type=int, default=4)
-ap.add_argument("--factors", type=float, nargs="+", default=[0.8, 1.2, 1.4, 2.0, 3.0])
+ap.add_argument("--factors", type=float, nargs="+", default=[1.1, 1.4, 2.0])
 ap.add_argument("--frame", type=int, nargs=3, default=[1920, 1080, 4])
 ap.add_argument("--out", default=None)
 A = ap.parse_args()
@@ -52,6 +52,7 @@ for fac in A.factors:
     outs = [torch.zeros(W * H, dtype=torch.int32, device="cuda") for _ in range(24)]
     torch.cuda.synchronize()
     gs.set_plan_delay(int(1000 * fac * F))
+    ev = []
     for i in range(24):
         s = streams[i % 2]
         if i == 17:
@@ -60,13 +61,19 @@ for fac in A.factors:
             s.wait_event(e)
         with torch.cuda.stream(s):
             outs[i].fill_(SENT)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(s)
         gs.render_frame_device(f, outs[i].data_ptr(), s.cuda_stream)
+        b.record(s)
+        ev.append((a, b))
     torch.cuda.synchronize()
+    t0 = ev[0][0]
+    timeline = {i: (round(t0.elapsed_time(a), 4), round(t0.elapsed_time(b), 4)) for i, (a, b) in enumerate(ev) if i >= 14}
     gs.set_plan_delay(0)
     bad = {i: int((o == SENT).sum()) for i, o in enumerate(outs) if not torch.equal(o, ref)}
     front, listed, epoch = gs.heavy_first()
     res["runs"][str(fac)] = {"delay_us": int(1000 * fac * F), "bad_sentinel_px": bad, "front": front, "listed": listed,
-                             "epoch": epoch}
+                             "epoch": epoch, "timeline_ms": timeline}
     print(fac, res["runs"][str(fac)], flush=True)
     gs.close()
 hs.close()
