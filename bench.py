@@ -191,31 +191,31 @@ def moving_camera(work, steps, warmup, static_ms, clock_warmup=0.2):
         frames.append(seq)
 
     def step(i):
+        # as the static step: with overlap, consecutive steps alternate the two streams and buffer sets
+        p = i % len(work.streams)
+        st, bufs = work.streams[p].cuda_stream, work.bufs[p % len(work.bufs)]
         if work.batch:
             o = work.order
             work.rtm.render_batch_device([work.scenes[j][2] for j in o], [frames[j][i] for j in o],
-                                         [work.bufs[0][j].data_ptr() for j in o], stream=work.stream.cuda_stream)
+                                         [bufs[j].data_ptr() for j in o], stream=st)
             return
         for j, (sid, hs, gs, f) in enumerate(work.scenes):
-            gs.render_frame_device(frames[j][i], work.bufs[0][j].data_ptr(), work.stream.cuda_stream)
+            gs.render_frame_device(frames[j][i], bufs[j].data_ptr(), st)
 
-    with work.stream_ctx():
-        # the clocks first (as run_steps: from an idle GPU they ramp over ~30 steps), on the orbit's
-        # first views
-        t_end = time.perf_counter() + clock_warmup
-        n = 0
-        while time.perf_counter() < t_end:
-            step(n % max(warmup, 1))
-            n += 1
-            if n % 8 == 0:
-                work.sync()
-        for i in range(warmup):
-            step(i)
+    # the clocks first (as run_steps: from an idle GPU they ramp over ~30 steps), on the orbit's first views
+    t_end = time.perf_counter() + clock_warmup
+    n = 0
+    while time.perf_counter() < t_end:
+        step(n % max(warmup, 1))
+        n += 1
+        if n % 8 == 0:
+            work.sync()
+    for i in range(warmup):
+        step(i)
     work.sync()
     t0 = time.perf_counter()
-    with work.stream_ctx():
-        for i in range(steps):
-            step(warmup + i)
+    for i in range(steps):
+        step(warmup + i)
     work.sync()
     ms = (time.perf_counter() - t0) / steps * 1e3
     # the scenes' own cameras again for the rest of the run (their per-origin records come back)
@@ -228,7 +228,8 @@ def moving_camera(work, steps, warmup, static_ms, clock_warmup=0.2):
             "orbit_deg_per_frame": ORBIT_DEG, "orbit_deg_total": round(ORBIT_DEG * nfr, 2),
             "vs_static": round(static_ms / ms, 4) if static_ms else None,
             "note": f"the camera orbits the scene {ORBIT_DEG} deg per frame about the world y axis: a new "
-                    "origin (k_origin_pre before every render) and a new view every frame; never the bench value"}
+                    "origin (k_origin_pre before every render, into the scene's other record buffer) and a new view "
+                    "every frame, steps on the static step's streams; never the bench value"}
 
 
 def first_frame(rtm, torch):

@@ -321,9 +321,22 @@ void hf_key(const KParams& P, uint64_t blocks, int var, uint64_t batch, uint64_t
     key[4] = batch;
 }
 
-bool measures(const rt_scene *s, const HfCtx& c, uint64_t cam_sig)
+// Whether a frame of this context is measured.  pend: the plan pending after this frame's adoption (see
+// hf_prepare).  A moved camera re-plans (RT_HF_FOLLOW) only when no plan is pending: a measured frame
+// must wait for the pending plan, which reads the cost words it would write, so measuring every moved
+// frame put each frame after the previous frame's plan -- no two frames of a moving camera overlapped,
+// and every step paid the plan's latency.  A moving camera is measured every other frame instead, and
+// frame i + 2 adopts frame i's plan.
+bool measures(const rt_scene *s, const HfCtx& c, uint64_t cam_sig, uint32_t pend)
 {
-    return c.frames < 2u || c.frames % kHfPeriod == 0u || (s->hf_follow && cam_sig != c.cam);
+    return c.frames < 2u || c.frames % kHfPeriod == 0u || (s->hf_follow && cam_sig != c.cam && pend == 0u);
+}
+
+// The plan still pending after a frame's adoption step (hf_prepare: the second frame after a plan adopts
+// it; a measured frame does too, but only a frame with no plan pending is measured for a moved camera)
+uint32_t pend_after_adoption(const HfCtx& c)
+{
+    return (c.pend && c.pend_age >= 1u) ? 0u : c.pend;
 }
 
 HfPeek hf_peek(const rt_scene *s, const KParams& P, uint64_t blocks, int var, uint64_t batch, uint64_t cam_sig)
@@ -332,7 +345,10 @@ HfPeek hf_peek(const rt_scene *s, const KParams& P, uint64_t blocks, int var, ui
     hf_key(P, blocks, var, batch, key);
     for (const HfCtx& h : s->hf)
         if (std::memcmp(h.key, key, sizeof(key)) == 0)
-            return HfPeek{ true, measures(s, h, cam_sig), h.frames >= 2u && h.pend == 0u };
+            // a measured frame adopts any pending plan first (waiting for it on its stream; later frames
+            // wait for it as the fence), so it may overlap once the shape's first two frames (whose plans
+            // run on the launch stream) have passed
+            return HfPeek{ true, measures(s, h, cam_sig, pend_after_adoption(h)), h.frames >= 2u };
     return HfPeek{ false, true, false };
 }
 
@@ -412,10 +428,10 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
     s->hf_last = c;
     // measured: the first two frames (the first plan has no earlier maximum to test a tail
     // against, so it lists nothing) and then every kHfPeriod-th
-    // ... and every frame whose camera differs from the previous frame's: a moving camera's heavy
-    // blocks move with the view, so the plan comes from the newest view (one frame old) instead of
-    // one up to kHfPeriod frames old
-    P.hf_measure = measures(s, *c, cam_sig) ? 1u : 0u;
+    // ... and a frame whose camera differs from the previous frame's, when no plan is pending after its
+    // adoption step: a moving camera's heavy blocks move with the view, so the plan comes from a view
+    // two frames old instead of one up to kHfPeriod frames old (measures)
+    P.hf_measure = measures(s, *c, cam_sig, pend_after_adoption(*c)) ? 1u : 0u;
     if (c->fence || c->pend)
     {
         hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;

@@ -89,7 +89,7 @@ struct rt_scene
     uint32_t ncells = 0, nrefs = 0, ntris = 0, max_cell_refs = 0;
     uint32_t *d_off = nullptr, *d_cellw = nullptr, *d_cellwo = nullptr, oct_stride = 0;
     uint32_t *d_cellwb = nullptr, box_stride = 0;  // box-run words: 24 copies (octant x major axis)
-    float4 *d_refs = nullptr, *d_shade = nullptr, *d_facen = nullptr, *d_frefs = nullptr;
+    float4 *d_refs = nullptr, *d_shade = nullptr, *d_facen = nullptr;
     float4 *d_trimt = nullptr, *d_tridist = nullptr, *d_distblk = nullptr;
     uint32_t ndist_blk = 0;
     float scene_scale = 0.0f;
@@ -98,9 +98,15 @@ struct rt_scene
     uint32_t compact_wgs = 2048;    // RT_KERNEL_COMPACT grid: 8 x 256-lane workgroups per CU
     bool rcp_safe = false;          // every |det| of the ray/tri test is far below 2^126 (FAST_RCP)
     bool pack_ok = false;           // dims <= 512: the remaining-cell counts pack into one word
-    // frefs hold the per-reference terms of this camera origin (bit patterns; valid once computed)
-    bool fref_valid = false;
-    uint32_t fref_org[3] = { 0, 0, 0 };
+    // Per-camera-origin records (k_origin_pre), TWO buffers: a frame whose origin is in neither computes
+    // its records into the one the scene's last launch does not read, so consecutive frames of a moving
+    // camera may still overlap (RT_KERNEL_FLAG_OVERLAP): the launch before the last -- the only other one
+    // in flight -- is waited for first (order_overlap).  fref_org: each buffer's origin (bit patterns),
+    // fref_ok: computed; fref_last: bit b = the last launch reads buffer b.
+    float4 *d_frefs[2] = { nullptr, nullptr };
+    bool fref_ok[2] = { false, false };
+    uint32_t fref_org[2][3] = { { 0, 0, 0 }, { 0, 0, 0 } };
+    uint32_t fref_last = 0;
     uint64_t *d_clk = nullptr;      // RT_KERNEL_FLAG_WAVE_CLOCK records of the last such launch
     size_t clk_cap = 0;
     uint32_t clk_items = 0;

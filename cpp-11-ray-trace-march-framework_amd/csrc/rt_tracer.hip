@@ -407,7 +407,7 @@ void frame_params(const rt_scene *s, const rt_frame *f, KParams& P)
     P.cellwb = s->d_cellwb;
     P.box_stride = s->box_stride;
     P.refs = s->d_refs;
-    P.frefs = s->d_frefs;
+    P.frefs = s->d_frefs[0];                                    // ensure_origin_terms picks the buffer
     P.shade = s->d_shade;
     P.face_n = s->d_facen;
     P.tri_mt = s->d_trimt;
@@ -440,17 +440,57 @@ uint32_t env_tunable(const char *name, uint32_t dflt)
     return e && *e ? uint32_t(std::strtoul(e, nullptr, 0)) : dflt;
 }
 
-int ensure_origin_terms(rt_scene *s, const KParams& P, hipStream_t st)
+// The per-origin record buffer a frame of origin `org` reads (rt_scene::d_frefs): the one holding that
+// origin, else the one to compute it into -- never one the scene's last launch reads (mask `busy`, bit b:
+// buffer b), preferring an empty one.  -1: both are busy (a batch that read two origins of the scene).
+int fref_slot(const rt_scene *s, const float org[3], uint32_t busy, bool *compute)
 {
     uint32_t ob[3];
-    std::memcpy(ob, P.org, sizeof(ob));
-    if (s->fref_valid && std::memcmp(ob, s->fref_org, sizeof(ob)) == 0) return RT_OK;
-    if (s->nrefs)
-        hipLaunchKernelGGL(origin_pre_kernel(), dim3((s->nrefs + kWG - 1) / kWG), dim3(kWG), 0, st, s->d_refs, s->d_frefs,
-                           s->nrefs, P.org[0], P.org[1], P.org[2]);
-    RT_HIP(hipGetLastError());
-    std::memcpy(s->fref_org, ob, sizeof(ob));
-    s->fref_valid = true;
+    std::memcpy(ob, org, sizeof(ob));
+    for (int b = 0; b < 2; b++)
+        if (s->fref_ok[b] && std::memcmp(ob, s->fref_org[b], sizeof(ob)) == 0)
+        {
+            *compute = false;
+            return b;
+        }
+    *compute = true;
+    for (int b = 0; b < 2; b++)
+        if (!(busy & (1u << b)) && !s->fref_ok[b]) return b;
+    for (int b = 0; b < 2; b++)
+        if (!(busy & (1u << b))) return b;
+    return -1;
+}
+
+// A frame of this origin may overlap the scene's last launch (RT_KERNEL_FLAG_OVERLAP) as far as the
+// per-origin records go: its origin is computed, or the buffer it would be computed into is one the last
+// launch does not read.
+bool fref_overlap_ok(const rt_scene *s, const float org[3])
+{
+    bool compute;
+    return fref_slot(s, org, s->fref_last, &compute) >= 0;
+}
+
+// The per-reference origin terms for this frame's camera origin in a buffer of their own (fref_slot),
+// computed when neither buffer holds them (a moving camera pays one small launch per frame), ordered after
+// every launch that may still read that buffer (the caller has ordered st after the launch before the
+// last one, which is the only other one in flight; busy: buffers that launches of this call read already).
+// Sets P.frefs and marks the buffer in *used.
+int ensure_origin_terms(rt_scene *s, KParams& P, hipStream_t st, uint32_t busy, uint32_t *used)
+{
+    bool compute = false;
+    const int b = fref_slot(s, P.org, s->fref_last | busy, &compute);
+    if (b < 0) return fail(RT_E_INVALID, "internal: no free per-origin record buffer");
+    if (compute)
+    {
+        if (s->nrefs)
+            hipLaunchKernelGGL(origin_pre_kernel(), dim3((s->nrefs + kWG - 1) / kWG), dim3(kWG), 0, st, s->d_refs,
+                               s->d_frefs[b], s->nrefs, P.org[0], P.org[1], P.org[2]);
+        RT_HIP(hipGetLastError());
+        std::memcpy(s->fref_org[b], P.org, sizeof(s->fref_org[b]));
+        s->fref_ok[b] = true;
+    }
+    P.frefs = s->d_frefs[b];
+    *used |= 1u << b;
     return RT_OK;
 }
 
@@ -487,11 +527,9 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
     if (order_streams && cap == hipStreamCaptureStatusNone && (f->kernel & RT_KERNEL_FLAG_OVERLAP) && s->ev_recorded &&
         st != s->last_stream &&
         kind == RT_KERNEL_AUTO && lanes && grid_mt && !(f->kernel & (RT_KERNEL_FLAG_WAVE_CLOCK | RT_KERNEL_FLAG_WIDE_HEAVY)) &&
-        !auto_wide(s, P) && P.spp <= 64u && !s->tab_dirty && s->fref_valid)
+        !auto_wide(s, P) && P.spp <= 64u && !s->tab_dirty)
     {
-        uint32_t ob[3];
-        std::memcpy(ob, P.org, sizeof(ob));
-        overlap = std::memcmp(ob, s->fref_org, sizeof(ob)) == 0;
+        overlap = fref_overlap_ok(s, P.org);
         const int v = kVarAutoCore | (s->rcp_safe ? kVarFastRcp : 0) | (auto_runs(s) ? kVarPackedRem | kVarSkipRun : 0);
         if (overlap && blocks >= s->hf_min_blocks)
         {
@@ -522,9 +560,15 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
     {
         var = kVarAutoCore | (s->rcp_safe ? kVarFastRcp : 0) | (auto_runs(s) ? kVarPackedRem | kVarSkipRun : 0) |
               ((f->kernel & RT_KERNEL_FLAG_WAVE_CLOCK) ? kVarWaveClock : 0);
-        if (int rc = ensure_origin_terms(s, P, st)) return rc;
+        uint32_t used = 0;
+        if (int rc = ensure_origin_terms(s, P, st, 0u, &used)) return rc;
+        s->fref_last = used;
         g_ht.mark("origin");
     }
+    else
+        s->fref_last = 0u;                      // (this launch reads no per-origin records)
+    if (auto_path)
+        ;
     else if (lanes && P.isect == RT_ISECT_RAY_MARCH)
         var = kVarMarch | ((f->kernel & RT_KERNEL_FLAG_EXHAUSTIVE) ? kVarExhaustive : 0);
     else if (lanes && P.isect == RT_ISECT_BRUTE_FORCE)
@@ -774,32 +818,57 @@ int launch_batch(rt_scene *const *S, const rt_frame *F, uint32_t n, KParams *P, 
     bool overlap = !clk && cap == hipStreamCaptureStatusNone;
     for (uint32_t i = 0; i < n; i++)
     {
-        uint32_t ob[3];
-        std::memcpy(ob, P[i].org, sizeof(ob));
-        overlap = overlap && (F[i].kernel & RT_KERNEL_FLAG_OVERLAP) && !S[i]->tab_dirty && S[i]->fref_valid &&
-                  std::memcmp(ob, S[i]->fref_org, sizeof(ob)) == 0;
+        overlap = overlap && (F[i].kernel & RT_KERNEL_FLAG_OVERLAP) && !S[i]->tab_dirty && fref_overlap_ok(S[i], P[i].org);
+        // a scene twice in the batch at another origin: both record buffers are this launch's, so it
+        // orders after every launch of the scene; more than two origins of one scene: no batch
+        uint32_t org_i[3], org_j[3];
+        std::memcpy(org_i, P[i].org, sizeof(org_i));
+        int others = 0;
+        for (uint32_t j = 0; j < i; j++)
+        {
+            std::memcpy(org_j, P[j].org, sizeof(org_j));
+            if (S[j] == S[i] && std::memcmp(org_i, org_j, sizeof(org_i)) != 0) others++;
+        }
+        if (others) overlap = false;
+        if (others > 1) return RT_E_INVALID;
     }
     if (overlap && (front || wide_heavy))
     {
         const HfPeek pk = hf_peek(s0, P[0], blocks, kvar, ident | 1u, cams);
         overlap = pk.found && (!pk.measure || pk.measure_ok);
     }
-    // per-origin records of every scene, and the cross-stream order of every scene's state
+    // per-origin records of every frame, and the cross-stream order of every scene's state
+    uint32_t used[kMaxBatch] = {};             // per frame: its scene's record buffers this launch reads
     for (uint32_t i = 0; i < n; i++)
     {
         rt_scene *s = S[i];
-        bool first = true;
-        for (uint32_t j = 0; j < i; j++) first = first && S[j] != s;
-        if (!first) continue;
-        if (overlap && s->ev_recorded && st != s->last_stream)
+        int first = -1;
+        for (uint32_t j = 0; j < i && first < 0; j++)
+            if (S[j] == s) first = int(j);
+        if (first < 0)
         {
-            if (int rc = order_overlap(s, st)) return rc;
+            if (overlap && s->ev_recorded && st != s->last_stream)
+            {
+                if (int rc = order_overlap(s, st)) return rc;
+            }
+            else if (int rc = order_all(s, st))
+                return rc;
+            if (int rc = flush_tables(s, st)) return rc;
+            s->last_stream = st;
+            if (int rc = ensure_origin_terms(s, P[i], st, 0u, &used[i])) return rc;
         }
-        else if (int rc = order_all(s, st))
-            return rc;
-        if (int rc = flush_tables(s, st)) return rc;
-        s->last_stream = st;
-        if (int rc = ensure_origin_terms(s, P[i], st)) return rc;
+        else
+        {
+            uint32_t u = used[first];
+            if (int rc = ensure_origin_terms(s, P[i], st, u, &u)) return rc;
+            used[first] = u;
+        }
+    }
+    for (uint32_t i = 0; i < n; i++)
+    {
+        bool first = true;
+        for (uint32_t j = 0; j < i; j++) first = first && S[j] != S[i];
+        if (first) S[i]->fref_last = used[i];
     }
     if (front || wide_heavy)
         if (int rc = hf_prepare(s0, P[0], blocks, kvar, front, st, ident | 1u, cams)) return rc;
@@ -1185,7 +1254,8 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
     const size_t nfrefs = size_t(std::max(nr, 1u)) * 4;
     RT_HIP(hipMalloc(&s->d_off, sizeof(uint32_t) * (nc + 1)));
     RT_HIP(hipMalloc(&s->d_refs, sizeof(float4) * refs.size()));
-    RT_HIP(hipMalloc(&s->d_frefs, sizeof(float4) * nfrefs));
+    RT_HIP(hipMalloc(&s->d_frefs[0], sizeof(float4) * nfrefs));
+    RT_HIP(hipMalloc(&s->d_frefs[1], sizeof(float4) * nfrefs));
     RT_HIP(hipMalloc(&s->d_shade, sizeof(float4) * shade.size()));
     RT_HIP(hipMalloc(&s->d_facen, sizeof(float4) * facen.size()));
     RT_HIP(hipMemcpy(s->d_off, g.cell_offsets, sizeof(uint32_t) * (nc + 1), hipMemcpyHostToDevice));
@@ -1275,7 +1345,7 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
         }
     }
     s->device_bytes = sizeof(uint32_t) * (nc + 1) +
-                      sizeof(float4) * (refs.size() + nfrefs + shade.size() + facen.size() + trimt.size() +
+                      sizeof(float4) * (refs.size() + 2 * nfrefs + shade.size() + facen.size() + trimt.size() +
                                         tridist.size() + distblk.size()) +
                       sizeof(uint32_t) * (cellw.size() + cellwo.size() + cellwb.size());
     RT_HIP(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
@@ -1323,7 +1393,8 @@ int rt_scene_destroy(rt_scene *s)
         if (s->side) (void)hipStreamSynchronize(s->side);
         (void)hipFree(s->d_off);
         (void)hipFree(s->d_refs);
-        (void)hipFree(s->d_frefs);
+        (void)hipFree(s->d_frefs[0]);
+        (void)hipFree(s->d_frefs[1]);
         (void)hipFree(s->d_shade);
         (void)hipFree(s->d_facen);
         (void)hipFree(s->d_cellw);
@@ -1803,7 +1874,11 @@ int rt_render_frame_host_tiled(rt_scene *s, const rt_frame *f, uint32_t *h_tiles
     frame_params(s, f, P0);
     if (use_lanes(f, spp) && P0.isect == RT_ISECT_GRID && P0.tri_test == RT_TRI_MOLLER_TRUMBORE &&
         ((f->kernel & RT_KERNEL_KIND_MASK) == RT_KERNEL_AUTO || (f->kernel & RT_KERNEL_KIND_MASK) == RT_KERNEL_COMPACT))
-        if ((rc = ensure_origin_terms(s, P0, st[0]))) return rc;
+    {
+        uint32_t used = 0;                      // (every launch before this one is waited for above)
+        if ((rc = ensure_origin_terms(s, P0, st[0], 0u, &used))) return rc;
+        s->fref_last = used;
+    }
     if ((rc = flush_tables(s, st[0]))) return rc;      // before the fork: both streams read them
     RT_HIP(hipEventRecord(s->ev_t_fork, st[0]));
     RT_HIP(hipStreamWaitEvent(st[1], s->ev_t_fork, 0));

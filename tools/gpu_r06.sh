@@ -31,7 +31,10 @@ for step in "$@"; do
     gpu) run gpu 1100 $PYT tests -m gpu ;;
     scale) run scale_lds 400 python3 -u tools/shard_scaling.py --steady --batch --overlap --scenes 1 8 --out ${T}_scale_lds 0
            run scale_lanes 400 env RT_WH_LDS=0 RT_WH_BETA16=16 python3 -u tools/shard_scaling.py --steady --batch --overlap --scenes 1 8 --out ${T}_scale_lanes 0 ;;
-    bench) run bench 300 python -u bench.py ;;
+    move) run move 300 python -u bench.py --steps 200 --warmup 100 --no-cpu-baseline --no-end-to-end --no-first-frame --no-legs
+          run move_driver 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-end-to-end --no-first-frame --no-legs ;;
+    bench) run bench 300 python -u bench.py
+           run bench_driver 300 python -u bench.py --steps 20 --warmup 5 ;;
     race) run race_prod 200 python3 -u tools/plan_race_probe.py --out ${T}_race_prod
           run race_nofence 200 env RT_TRACER_LIB=librt_tracer_nofence.so python3 -u tools/plan_race_probe.py --out ${T}_race_nofence ;;
     waves) run waves_lanes 200 env RT_WH_LDS=0 python3 -u tools/batch_waves.py --out ${T}_waves_lanes
