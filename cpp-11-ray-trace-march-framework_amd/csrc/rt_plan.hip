@@ -234,7 +234,27 @@ int launch_plans(rt_scene *s, const KParams& P, uint64_t blocks, hipStream_t st)
     // (the bench pair's batched step: 0.5396 vs 0.5318 ms with it, scenes 4 / 5 in their own launches
     // 0.2486 / 0.4518 vs 0.252 / 0.46: profiles/r05ar_hf_pos_sweep.json)
     const uint32_t pos16 = (c && c->key[4] != 0u) ? 0u : s->hf_pos16;
-    if (!twice && c && cap == hipStreamCaptureStatusNone)
+    // the second pass: the first pass's outputs are its inputs, written into the buffers of the version
+    // before (the two passes alternate them by parity, as consecutive frames do)
+    KParams Q = P;
+    if (twice)
+    {
+        Q.hf_ver = P.hf_ver + 1u;
+        Q.hf_plan_in = P.hf_plan_out;
+        Q.hf_plan_out = const_cast<HfPlan *>(P.hf_plan_in);
+        Q.hf_list_in = P.hf_list_out;
+        Q.hf_list_out = const_cast<uint32_t *>(P.hf_list_in);
+        Q.hf_mark_in = P.hf_mark_out;
+        Q.hf_mark_out = const_cast<uint32_t *>(P.hf_mark_in);
+        if (P.wh_on)
+        {
+            Q.wh_list_in = P.wh_list_out;
+            Q.wh_list_out = const_cast<uint32_t *>(P.wh_list_in);
+            Q.wh_mark_in = P.wh_mark_out;
+            Q.wh_mark_out = const_cast<uint32_t *>(P.wh_mark_in);
+        }
+    }
+    if (c && cap == hipStreamCaptureStatusNone)
     {
         if (!s->plan_st)
         {
@@ -250,43 +270,33 @@ int launch_plans(rt_scene *s, const KParams& P, uint64_t blocks, hipStream_t st)
         if (s->ev_prev) RT_HIP(hipStreamWaitEvent(s->plan_st, s->ev_prev->ev, 0));
         RT_HIP(hipMemsetAsync(P.hf_plan_out, 0, sizeof(HfPlan), s->plan_st));
         hipLaunchKernelGGL(k_hf_plan, grid, wg, 0, s->plan_st, P, uint32_t(blocks), s->hf_shift, pos16, s->plan_delay);
+        // (a shape's first plans too: the first frame's time to the frame no longer includes them; its
+        // second frame, measured, adopts them)
+        if (twice)
+        {
+            RT_HIP(hipMemsetAsync(Q.hf_plan_out, 0, sizeof(HfPlan), s->plan_st));
+            hipLaunchKernelGGL(k_hf_plan, grid, wg, 0, s->plan_st, Q, uint32_t(blocks), s->hf_shift, pos16, s->plan_delay);
+        }
         RT_HIP(hipEventRecord(c->pend_ev, s->plan_st));
-        c->pend = P.hf_ver + 1u;
+        c->pend = P.hf_ver + (twice ? 2u : 1u);
         c->pend_age = 0;
         RT_HIP(hipGetLastError());
         return RT_OK;
     }
+    // inside a stream capture (no wait on an outside event): on the launch stream
     RT_HIP(hipMemsetAsync(P.hf_plan_out, 0, sizeof(HfPlan), st));
     hipLaunchKernelGGL(k_hf_plan, grid, wg, 0, st, P, uint32_t(blocks), s->hf_shift, pos16, s->plan_delay);
-    if (c)
-    {
-        c->ver = P.hf_ver + (twice ? 2u : 1u);
-    }
     if (twice)
     {
-        KParams Q = P;
-        Q.hf_ver = P.hf_ver + 1u;
-        Q.hf_plan_in = P.hf_plan_out;
-        Q.hf_plan_out = const_cast<HfPlan *>(P.hf_plan_in);
-        Q.hf_list_in = P.hf_list_out;
-        Q.hf_list_out = const_cast<uint32_t *>(P.hf_list_in);
-        Q.hf_mark_in = P.hf_mark_out;
-        Q.hf_mark_out = const_cast<uint32_t *>(P.hf_mark_in);
-        if (P.wh_on)
-        {
-            Q.wh_list_in = P.wh_list_out;
-            Q.wh_list_out = const_cast<uint32_t *>(P.wh_list_in);
-            Q.wh_mark_in = P.wh_mark_out;
-            Q.wh_mark_out = const_cast<uint32_t *>(P.wh_mark_in);
-        }
         RT_HIP(hipMemsetAsync(Q.hf_plan_out, 0, sizeof(HfPlan), st));
         hipLaunchKernelGGL(k_hf_plan, grid, wg, 0, st, Q, uint32_t(blocks), s->hf_shift, pos16, s->plan_delay);
     }
+    if (c) c->ver = P.hf_ver + (twice ? 2u : 1u);
     RT_HIP(hipGetLastError());
     // plans on the launch stream are part of the scene's last launch: a launch on another stream orders
     // after them, not only after the render (ev_last was the render's own stop event).  Plans run here
-    // only for a shape's first two frames (never overlapped: hf_peek) and inside a stream capture (no
-    // overlap there either: launch_render / launch_batch), so no ev_prev refers to ev_own here.
+    // only inside a stream capture, where nothing overlaps (launch_render / launch_batch), so no ev_prev
+    // refers to ev_own here.
     RT_HIP(hipEventRecord(s->ev_own->ev, st));
     s->ev_last = s->ev_own;
     return RT_OK;

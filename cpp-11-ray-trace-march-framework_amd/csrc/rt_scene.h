@@ -234,8 +234,7 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
 // What hf_prepare would find for this launch, without side effects: whether the shape's context exists
 // (no allocation, no eviction) and whether this frame would be measured (RT_KERNEL_FLAG_OVERLAP)
 // measure_ok: a measured frame of this shape may still overlap (its plan runs after every frame in
-// flight, launch_plans): not the shape's first two frames (their plans run on the launch stream), no
-// plan pending, not the proxy's plan
+// flight, launch_plans; a measured frame adopts a pending plan first): not the shape's first two frames
 struct HfPeek { bool found, measure, measure_ok; };
 HfPeek hf_peek(const rt_scene *s, const KParams& P, uint64_t blocks, int var, uint64_t batch, uint64_t cam_sig);
 // The plan kernel(s) after a measured frame on its stream (k_hf_plan; two passes after a shape's first

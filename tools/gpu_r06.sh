@@ -31,6 +31,8 @@ for step in "$@"; do
     gpu) run gpu 1100 $PYT tests -m gpu ;;
     scale) run scale_lds 400 python3 -u tools/shard_scaling.py --steady --batch --overlap --scenes 1 8 --out ${T}_scale_lds 0
            run scale_lanes 400 env RT_WH_LDS=0 RT_WH_BETA16=16 python3 -u tools/shard_scaling.py --steady --batch --overlap --scenes 1 8 --out ${T}_scale_lanes 0 ;;
+    first) run first_proxy 300 python3 -u tools/first_frame_probe.py --scenes 0 1 2 3 4 5 6 7 8 9 --reps 3 --out ${T}_first_proxy
+           run first_noproxy 300 env RT_TRACER_LIB=librt_tracer_noproxy.so python3 -u tools/first_frame_probe.py --scenes 0 1 2 3 4 5 6 7 8 9 --reps 3 --out ${T}_first_noproxy ;;
     move) run move 300 python -u bench.py --steps 200 --warmup 100 --no-cpu-baseline --no-end-to-end --no-first-frame --no-legs
           run move_driver 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-end-to-end --no-first-frame --no-legs ;;
     bench) run bench 300 python -u bench.py
