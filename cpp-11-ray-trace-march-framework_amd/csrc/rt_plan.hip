@@ -533,13 +533,16 @@ int hf_prepare(rt_scene *s, KParams& P, uint64_t blocks, int var, bool front, hi
         P.wh_floor = s->wh_floor;
         // a rank of 2 of a batched step lists more (its span estimate includes the other frames'
         // work); one scene's own rank-of-2 launch measured 25 % slower with it
-        // (profiles/r03o_shard_scaling_bench.json), so it keeps the default
-        // and a rank of 4-7 of a batched step one notch lower than the default (rank of 4, measured
-        // in profiles/r03ad_alpha_n4_n8.json: 0.182 ms at 28/16 vs 0.191 at 32/16, 0.219 at 36/16;
-        // a rank of 8 keeps 32/16: 0.117 vs 0.119 at 28/16)
-        P.wh_alpha16 = (P.nranks == 2u && batch != 0u)                  ? s->wh_alpha16_n2
-                       : (P.nranks >= 3u && P.nranks < 8u && batch != 0u) ? s->wh_alpha16_n4
-                                                                          : s->wh_alpha16;
+        // (profiles/r03o_shard_scaling_bench.json), so one scene's own launches keep wh_alpha16 (32/16),
+        // and a rank of 4-7 of a batched step one notch lower (rank of 4, measured in
+        // profiles/r03ad_alpha_n4_n8.json: 0.182 ms at 28/16 vs 0.191 at 32/16, 0.219 at 36/16).  A
+        // batched rank of >= 8 lists less since round 6 (wh_alpha16_n8 40/16: the bench pair's
+        // overlapped step 0.0818-0.0839 vs 0.0855-0.0868 ms at 32/16, one stream 0.096 vs 0.099; 48-64
+        // unstable; killeroo's own rank of 8 mixed, so it keeps 32: profiles/r06_lds_tier_ab.json r06l, r06m)
+        P.wh_alpha16 = batch == 0u      ? s->wh_alpha16
+                       : P.nranks == 2u ? s->wh_alpha16_n2
+                       : P.nranks < 8u  ? s->wh_alpha16_n4
+                                        : s->wh_alpha16_n8;
         P.wh_mark_in = c->wh_marks + size_t(v & 1u) * kWavesPerWG * c->cap_blocks;
         P.wh_mark_out = c->wh_marks + size_t((v + 1u) & 1u) * kWavesPerWG * c->cap_blocks;
         P.wh_list_in = c->wh_lists + size_t(v & 1u) * 2u * kWhMax;

@@ -130,9 +130,10 @@ struct rt_scene
     uint32_t hf_pos16 = 16;         // RT_HF_POS16: position-aware threshold (k_hf_plan) of single-frame
                                     // launches, sixteenths of the span left; 0: max >> hf_shift
     uint32_t wh_floor = 100000;     // RT_WH_FLOOR: wide-section threshold floor, shader cycles
-    uint32_t wh_alpha16 = 32;       // RT_WH_ALPHA16: wide threshold, sixteenths of the estimated span
+    uint32_t wh_alpha16 = 32;       // RT_WH_ALPHA16: wide threshold of single-frame launches, sixteenths of the estimated span
     uint32_t wh_alpha16_n2 = 16;    // RT_WH_ALPHA16_N2: the same for a rank of 2 of a batched step
     uint32_t wh_alpha16_n4 = 28;    // RT_WH_ALPHA16_N4: the same for a rank of 3-7 of a batched step
+    uint32_t wh_alpha16_n8 = 40;    // RT_WH_ALPHA16_N8: the same for a rank of >= 8 of a batched step
     uint32_t wh_auto_refs = 128;    // RT_WH_AUTO_REFS: AUTO takes the wide section for >= 2-rank
                                     // shards of scenes with a cell list this long
     uint32_t wg64 = 1;              // RT_WG64: AUTO launches of >= wg64_min_blocks 256-lane blocks run

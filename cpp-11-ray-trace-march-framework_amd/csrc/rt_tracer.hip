@@ -1101,6 +1101,7 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out)
     s->wh_alpha16 = env_tunable("RT_WH_ALPHA16", s->wh_alpha16);
     s->wh_alpha16_n2 = env_tunable("RT_WH_ALPHA16_N2", s->wh_alpha16_n2);
     s->wh_alpha16_n4 = env_tunable("RT_WH_ALPHA16_N4", s->wh_alpha16_n4);
+    s->wh_alpha16_n8 = env_tunable("RT_WH_ALPHA16_N8", s->wh_alpha16_n8);
     s->wh_auto_refs = env_tunable("RT_WH_AUTO_REFS", s->wh_auto_refs);
     s->wg64_max_refs = env_tunable("RT_WG64_MAX_REFS", s->wg64_max_refs);
     s->wg64_wide = env_tunable("RT_WG64_WIDE", s->wg64_wide);

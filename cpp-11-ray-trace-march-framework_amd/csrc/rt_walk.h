@@ -54,7 +54,10 @@ __device__ __forceinline__ float2 *lds_red_uv()
 
 // kVarLdsSplit: cell lists shorter than this (in every lane) are tested whole by every wave, with no
 // reduction; longer ones are split between the workgroup's waves
-constexpr uint32_t kLdsSplitMin = 8;
+#ifndef RT_LDS_SPLIT_MIN       // (tools/build_variant.sh -DRT_LDS_SPLIT_MIN=n: the A/B arms)
+#define RT_LDS_SPLIT_MIN 8
+#endif
+constexpr uint32_t kLdsSplitMin = RT_LDS_SPLIT_MIN;
 
 // kVarWaveClock debug counters of this wave: [0] records tested in wave-uniform loops,
 // [1] iterations of the per-lane list loop

@@ -126,6 +126,7 @@ def test_view_records_batched_ranks(golden, view, nranks, monkeypatch):
     import torch
     monkeypatch.setenv("RT_WH_ALPHA16", "4")
     monkeypatch.setenv("RT_WH_ALPHA16_N2", "4")
+    monkeypatch.setenv("RT_WH_ALPHA16_N8", "4")
     monkeypatch.setenv("RT_WH_FLOOR", "5000")
     vs = [golden["views"][f"scene{s}_{view}"] for s in (5, 8)]
     hss = [rtm.HostScene.load(v["scene"]) for v in vs]
@@ -173,6 +174,7 @@ def test_spp16_crop_records_rank_of_8_batched(golden, monkeypatch):
     rank's records over 5 frames, equal the reference's."""
     import torch
     monkeypatch.setenv("RT_WH_ALPHA16", "4")
+    monkeypatch.setenv("RT_WH_ALPHA16_N8", "4")
     monkeypatch.setenv("RT_WH_FLOOR", "5000")
     cs = [c for c in golden["spp_crops"] if c["spp"] == 16 and c["scene"] in (5, 8) and c["x0"] == 952]
     hss = [rtm.HostScene.load(c["scene"]) for c in cs]

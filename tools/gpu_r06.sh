@@ -31,6 +31,21 @@ for step in "$@"; do
     gpu) run gpu 1100 $PYT tests -m gpu ;;
     scale) run scale_lds 400 python3 -u tools/shard_scaling.py --steady --batch --overlap --scenes 1 8 --out ${T}_scale_lds 0
            run scale_lanes 400 env RT_WH_LDS=0 RT_WH_BETA16=16 python3 -u tools/shard_scaling.py --steady --batch --overlap --scenes 1 8 --out ${T}_scale_lanes 0 ;;
+    split) for v in split2 split16 split32; do
+               run split_$v 200 env RT_TRACER_LIB=librt_tracer_$v.so python3 -u tools/shard_scaling.py --steady --batch --overlap \
+                   --scenes 1 8 --out ${T}_split_$v 0
+           done
+           run split_base 200 python3 -u tools/shard_scaling.py --steady --batch --overlap --scenes 1 8 --out ${T}_split_base 0
+           for cfg in "40 24" "40 32" "32 20" "32 28"; do
+               set -- $cfg
+               run ab_$1_$2 200 env RT_WH_ALPHA16=$1 RT_WH_BETA16=$2 python3 -u tools/shard_scaling.py --steady --batch --overlap \
+                   --scenes 1 8 --out ${T}_ab_$1_$2 0
+           done ;;
+    alpha8) for cfg in "40 24" "48 24" "48 32" "56 32" "64 32"; do
+               set -- $cfg
+               run a8_$1_$2 200 env RT_WH_ALPHA16=$1 RT_WH_BETA16=$2 python3 -u tools/shard_scaling.py --steady --batch --overlap \
+                   --scenes 1 8 --out ${T}_a8_$1_$2 0
+           done ;;
     first) run first_proxy 300 python3 -u tools/first_frame_probe.py --scenes 0 1 2 3 4 5 6 7 8 9 --reps 3 --out ${T}_first_proxy
            run first_noproxy 300 env RT_TRACER_LIB=librt_tracer_noproxy.so python3 -u tools/first_frame_probe.py --scenes 0 1 2 3 4 5 6 7 8 9 --reps 3 --out ${T}_first_noproxy ;;
     move) run move 300 python -u bench.py --steps 200 --warmup 100 --no-cpu-baseline --no-end-to-end --no-first-frame --no-legs
