@@ -5,20 +5,21 @@
 // (aabb.h:15-32 -> aabb_tri_internal.h:112-186) and a push_back of the triangle index, so every
 // cell's list ends up in ascending triangle order.  Here, on one stream:
 //   K1 k_tri_ranges   one lane per triangle: cell range (same float arithmetic) -> candidates
-//   rocPRIM exclusive scan (64-bit) -> each triangle's first candidate
+//   exclusive scan (64-bit out) -> each triangle's first candidate
 //   K2 k_candidates   one lane per (triangle, candidate cell): cell bounds in float, SAT in
-//                     double; an overlap emits key = cell << tb | triangle, else the all-ones
-//                     sentinel (sorts last)
-//   rocPRIM radix sort of the keys over tb + cb bits: (cell, triangle) order IS the
-//                     reference's per-cell push_back order -- no stability argument needed
+//                     double; an overlap appends key = cell << tb | triangle (atomic counter,
+//                     any order: the keys are distinct)
+//   LSD radix sort of the keys over tb + cb bits, 8 bits a pass: (cell, triangle) order IS the
+//                     reference's per-cell push_back order
 //   K3 k_offsets      one lane per cell: CSR offset = lower_bound(keys, cell << tb); one lane
 //                     per reference: triangle = key & (2^tb - 1)
+// The scan and the sort are this file's own (k_scan_*, k_rs_*): a few hundred lines instead of
+// rocPRIM's template instantiations (round 6: 2.8 MB of the library's object code).
 // The grid AABB / cell size / dims (grid.cpp:18-41, mesh.cpp:112-134) are O(triangles) and are
 // computed on the host exactly as the reference does (float::min() seed, hazard H11).
-// Bit-exactness vs the reference's CSR: tests/test_gpu_parity.py::test_gpu_grid_build_*.
-#include <cstring>   // rocPRIM headers use memcpy without including it
+// Bit-exactness vs the reference's CSR: tests/test_gpu_grid.py.
+#include <cstring>
 #include <hip/hip_runtime.h>
-#include <rocprim/rocprim.hpp>
 
 #include <algorithm>
 #include <cmath>
@@ -147,7 +148,8 @@ __global__ void __launch_bounds__(256) k_candidates(GridParams G, const rt_verte
                                                     const uint4 *__restrict__ range_lo,
                                                     const uint4 *__restrict__ range_hi,
                                                     const unsigned long long *__restrict__ first, uint64_t n_cand,
-                                                    unsigned long long *keys, uint32_t *tri_hit, uint32_t *err)
+                                                    unsigned long long *keys, uint32_t *n_keys, uint32_t *tri_hit,
+                                                    uint32_t *err)
 {
     const uint64_t pidx = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     if (pidx >= n_cand) return;
@@ -173,20 +175,18 @@ __global__ void __launch_bounds__(256) k_candidates(GridParams G, const rt_verte
     const double half[3] = { (cmax[0] - cmin[0]) * 0.5f, (cmax[1] - cmin[1]) * 0.5f, (cmax[2] - cmin[2]) * 0.5f };
     const rt_triangle tr = tris[t];
     const bool hit = tri_box_overlap(ctr, half, verts[tr.v0].p, verts[tr.v1].p, verts[tr.v2].p);
-    unsigned long long key = ~0ull;
     if (hit)
     {
         // GridIdx (grid.h:41-42); the reference only asserts cell_idx < #cells (grid.cpp:119)
         const uint32_t cell = x + z * G.dims[0] + y * G.dims[0] * G.dims[2];
         if (cell < G.dims[0] * G.dims[1] * G.dims[2])
         {
-            key = (unsigned long long)cell << G.tb | t;
-            tri_hit[t] = 1u;
+            keys[atomicAdd(n_keys, 1u)] = (unsigned long long)cell << G.tb | t;   // any order: the sort
+            tri_hit[t] = 1u;                                                     // orders the keys fully
         }
         else
             atomicOr(err, 1u);
     }
-    keys[pidx] = key;
 }
 
 // K3: CSR offsets by lower_bound in the sorted keys; triangle ids from the low bits.
@@ -207,6 +207,135 @@ __global__ void __launch_bounds__(256) k_offsets(const unsigned long long *__res
         if (keys[mid] < target) lo = mid + 1; else hi = mid;
     }
     offsets[i] = lo;
+}
+
+// ---- exclusive scan: 1024 elements per 256-lane block, block sums scanned recursively ----
+constexpr uint32_t kScanBlock = 256, kScanPer = 4, kScanTile = kScanBlock * kScanPer;
+
+// Exclusive prefix of v over the block (wave64 shuffles, then the four wave totals through LDS);
+// *total = the block's sum.
+template <class T> __device__ __forceinline__ T block_exclusive(T v, T *total)
+{
+    __shared__ T wsum[kScanBlock / 64];
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    T inc = v;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1)
+    {
+        const T o = __shfl_up(inc, d, 64);
+        if (lane >= d) inc += o;
+    }
+    if (lane == 63u) wsum[w] = inc;
+    __syncthreads();
+    T base = 0, all = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < kScanBlock / 64; i++)
+    {
+        if (i < w) base += wsum[i];
+        all += wsum[i];
+    }
+    __syncthreads();                                 // wsum reusable by the next call
+    *total = all;
+    return base + inc - v;
+}
+
+template <class Tin, class Tout>
+__global__ void __launch_bounds__(kScanBlock) k_scan_tiles(const Tin *__restrict__ in, Tout *out, Tout *sums, uint32_t n)
+{
+    const uint32_t i0 = blockIdx.x * kScanTile + threadIdx.x * kScanPer;
+    Tout v[kScanPer], run = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kScanPer; k++)
+    {
+        v[k] = (i0 + k < n) ? Tout(in[i0 + k]) : Tout(0);
+        run += v[k];
+    }
+    Tout total;
+    Tout pre = block_exclusive(run, &total);
+#pragma unroll
+    for (uint32_t k = 0; k < kScanPer; k++)
+    {
+        if (i0 + k < n) out[i0 + k] = pre;
+        pre += v[k];
+    }
+    if (threadIdx.x == 0) sums[blockIdx.x] = total;
+}
+
+template <class T> __global__ void __launch_bounds__(kScanBlock) k_scan_add(T *out, const T *__restrict__ sums, uint32_t n)
+{
+    const uint32_t i0 = blockIdx.x * kScanTile + threadIdx.x * kScanPer;
+    const T add = sums[blockIdx.x];
+#pragma unroll
+    for (uint32_t k = 0; k < kScanPer; k++)
+        if (i0 + k < n) out[i0 + k] += add;
+}
+
+// ---- LSD radix sort of 64-bit keys, 8 bits a pass; 1024 keys per 256-lane block ----
+constexpr uint32_t kRsBlock = 256, kRsRounds = 4, kRsTile = kRsBlock * kRsRounds;
+
+// Per block the histogram of its tile's digits, digit-major: counts[digit * nblocks + block], so the
+// exclusive scan of counts is each (digit, block)'s first output position.
+__global__ void __launch_bounds__(kRsBlock) k_rs_count(const unsigned long long *__restrict__ keys, uint32_t n,
+                                                       uint32_t shift, uint32_t *counts)
+{
+    __shared__ uint32_t h[256];
+    h[threadIdx.x] = 0u;
+    __syncthreads();
+    const uint32_t base = blockIdx.x * kRsTile;
+#pragma unroll
+    for (uint32_t r = 0; r < kRsRounds; r++)
+    {
+        const uint32_t i = base + r * kRsBlock + threadIdx.x;
+        if (i < n) atomicAdd(&h[uint32_t(keys[i] >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    counts[threadIdx.x * gridDim.x + blockIdx.x] = h[threadIdx.x];
+}
+
+// Stable scatter: the tile's keys in index order, 256 a round; within a wave a key's rank among the
+// wave's keys of the same digit comes from eight ballots (the lanes sharing all eight bits), across
+// waves and rounds from LDS counts -- so equal digits keep their input order.
+__global__ void __launch_bounds__(kRsBlock) k_rs_scatter(const unsigned long long *__restrict__ keys, uint32_t n,
+                                                         uint32_t shift, const uint32_t *__restrict__ offs,
+                                                         unsigned long long *out)
+{
+    __shared__ uint32_t run[256];                    // keys of each digit in earlier rounds
+    __shared__ uint32_t wcnt[kRsBlock / 64][256];    // keys of each digit per wave, this round
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    run[threadIdx.x] = offs[threadIdx.x * gridDim.x + blockIdx.x];
+    const uint32_t base = blockIdx.x * kRsTile;
+    const unsigned long long below = (1ull << lane) - 1ull;
+    for (uint32_t r = 0; r < kRsRounds; r++)
+    {
+#pragma unroll
+        for (uint32_t q = 0; q < kRsBlock / 64; q++) wcnt[q][threadIdx.x] = 0u;
+        __syncthreads();
+        const uint32_t i = base + r * kRsBlock + threadIdx.x;
+        const bool valid = i < n;
+        const unsigned long long key = valid ? keys[i] : 0ull;
+        const uint32_t d = uint32_t(key >> shift) & 255u;
+        unsigned long long peers = __ballot(valid);
+#pragma unroll
+        for (uint32_t b = 0; b < 8; b++)
+        {
+            const unsigned long long set = __ballot(valid && ((d >> b) & 1u));
+            peers &= ((d >> b) & 1u) ? set : ~set;
+        }
+        const uint32_t rank = uint32_t(__popcll(peers & below));
+        if (valid && rank == 0u) wcnt[w][d] = uint32_t(__popcll(peers));
+        __syncthreads();
+        if (valid)
+        {
+            uint32_t pos = run[d] + rank;
+            for (uint32_t q = 0; q < w; q++) pos += wcnt[q][d];
+            out[pos] = key;
+        }
+        __syncthreads();
+        uint32_t add = 0u;
+#pragma unroll
+        for (uint32_t q = 0; q < kRsBlock / 64; q++) add += wcnt[q][threadIdx.x];
+        run[threadIdx.x] += add;
+    }
 }
 
 uint32_t bits_for(uint64_t v)            // smallest b with v < 2^b
@@ -273,6 +402,59 @@ struct BuildBuffers
             return rt_internal_fail(RT_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));     \
     } while (0)
 
+// Block-sum buffers of the scan levels, allocated once per build and reused by every scan.
+struct ScanLevels
+{
+    std::vector<unsigned long long *> buf;
+    std::vector<uint32_t> cap;
+};
+
+// Exclusive scan of n elements on B.st; the block sums are scanned the same way, in place.
+template <class Tin, class Tout>
+int exclusive_scan(BuildBuffers& B, ScanLevels& L, const Tin *in, Tout *out, uint32_t n, uint32_t level = 0)
+{
+    const uint32_t nb = (n + kScanTile - 1) / kScanTile;
+    if (L.buf.size() <= level)
+    {
+        L.buf.push_back(nullptr);
+        L.cap.push_back(0u);
+    }
+    if (L.cap[level] < nb)
+    {
+        RG_HIP(B.alloc(&L.buf[level], nb));          // 8 bytes an entry: either element type fits
+        L.cap[level] = nb;
+    }
+    Tout *sums = reinterpret_cast<Tout *>(L.buf[level]);
+    hipLaunchKernelGGL((k_scan_tiles<Tin, Tout>), dim3(nb), dim3(kScanBlock), 0, B.st, in, out, sums, n);
+    RG_HIP(hipGetLastError());
+    if (nb == 1u) return RT_OK;
+    if (int rc = exclusive_scan<Tout, Tout>(B, L, sums, sums, nb, level + 1)) return rc;
+    hipLaunchKernelGGL((k_scan_add<Tout>), dim3(nb), dim3(kScanBlock), 0, B.st, out, sums, n);
+    RG_HIP(hipGetLastError());
+    return RT_OK;
+}
+
+// Sorts n keys by their low `bits` bits; *sorted = the buffer (a or b) that holds the result.
+int radix_sort(BuildBuffers& B, ScanLevels& L, unsigned long long *a, unsigned long long *b, uint32_t n,
+               uint32_t bits, unsigned long long **sorted)
+{
+    const uint32_t nb = (n + kRsTile - 1) / kRsTile;
+    uint32_t *counts, *offs;
+    RG_HIP(B.alloc(&counts, size_t(256) * nb));
+    RG_HIP(B.alloc(&offs, size_t(256) * nb));
+    for (uint32_t shift = 0; shift < bits; shift += 8)
+    {
+        hipLaunchKernelGGL(k_rs_count, dim3(nb), dim3(kRsBlock), 0, B.st, a, n, shift, counts);
+        RG_HIP(hipGetLastError());
+        if (int rc = exclusive_scan<uint32_t, uint32_t>(B, L, counts, offs, 256u * nb)) return rc;
+        hipLaunchKernelGGL(k_rs_scatter, dim3(nb), dim3(kRsBlock), 0, B.st, a, n, shift, offs, b);
+        RG_HIP(hipGetLastError());
+        std::swap(a, b);
+    }
+    *sorted = a;
+    return RT_OK;
+}
+
 int build(const rt_vertex *v, uint32_t nv, const rt_triangle *t, uint32_t nt, uint32_t res, int device,
           rt_grid_desc *out, float *device_ms)
 {
@@ -292,7 +474,7 @@ int build(const rt_vertex *v, uint32_t nv, const rt_triangle *t, uint32_t nt, ui
     G.cw = g.cell_wdh;
     G.nt = nt;
     G.tb = std::max(1u, bits_for(nt - 1));
-    const uint32_t cb = bits_for(nc);                // 2^cb - 1 >= nc: the sentinel's cell field
+    const uint32_t cb = bits_for(nc);                // 2^cb > nc: every cell field, and nc << tb for K3
     if (G.tb + cb > 64) return rt_internal_fail(RT_E_INVALID, "grid too large for 64-bit keys");
 
     BuildBuffers B;
@@ -320,11 +502,8 @@ int build(const rt_vertex *v, uint32_t nv, const rt_triangle *t, uint32_t nt, ui
     RG_HIP(hipEventRecord(B.e0, B.st));
     hipLaunchKernelGGL(k_tri_ranges, dim3((nt + 255) / 256), dim3(256), 0, B.st, G, d_v, d_t, d_lo, d_hi, d_cnt);
     RG_HIP(hipGetLastError());
-    size_t tmp_bytes = 0;
-    char *d_tmp = nullptr;
-    RG_HIP(rocprim::exclusive_scan(nullptr, tmp_bytes, d_cnt, d_first, 0ull, nt, rocprim::plus<unsigned long long>(), B.st));
-    RG_HIP(B.alloc(&d_tmp, tmp_bytes));
-    RG_HIP(rocprim::exclusive_scan(d_tmp, tmp_bytes, d_cnt, d_first, 0ull, nt, rocprim::plus<unsigned long long>(), B.st));
+    ScanLevels L;
+    if (int rc = exclusive_scan<uint32_t, unsigned long long>(B, L, d_cnt, d_first, nt)) return rc;
     unsigned long long last_first = 0;
     uint32_t last_cnt = 0;
     RG_HIP(hipMemcpyAsync(&last_first, d_first + nt - 1, sizeof(last_first), hipMemcpyDeviceToHost, B.st));
@@ -332,23 +511,23 @@ int build(const rt_vertex *v, uint32_t nv, const rt_triangle *t, uint32_t nt, ui
     RG_HIP(hipStreamSynchronize(B.st));
     const uint64_t n_cand = last_first + last_cnt;
     if (n_cand >= 0x7FFFFFFFull) return rt_internal_fail(RT_E_INVALID, "too many candidate cells");
+    uint32_t *d_nkeys;
     RG_HIP(B.alloc(&d_keys, n_cand));
-    RG_HIP(B.alloc(&d_sorted, n_cand));
+    RG_HIP(B.alloc(&d_nkeys, 1));
+    RG_HIP(hipMemsetAsync(d_nkeys, 0, sizeof(uint32_t), B.st));
     hipLaunchKernelGGL(k_candidates, dim3(uint32_t((n_cand + 255) / 256)), dim3(256), 0, B.st, G, d_v, d_t, d_lo,
-                       d_hi, d_first, n_cand, d_keys, d_hit, d_err);
+                       d_hi, d_first, n_cand, d_keys, d_nkeys, d_hit, d_err);
     RG_HIP(hipGetLastError());
-    size_t sort_bytes = 0;
-    RG_HIP(rocprim::radix_sort_keys(nullptr, sort_bytes, d_keys, d_sorted, uint32_t(n_cand), 0, G.tb + cb, B.st));
-    if (sort_bytes > tmp_bytes)
-    {
-        RG_HIP(B.alloc(&d_tmp, sort_bytes));
-        tmp_bytes = sort_bytes;
-    }
-    RG_HIP(rocprim::radix_sort_keys(d_tmp, tmp_bytes, d_keys, d_sorted, uint32_t(n_cand), 0, G.tb + cb, B.st));
+    uint32_t n_keys = 0;                             // the overlapping (cell, triangle) pairs: the sort's size
+    RG_HIP(hipMemcpyAsync(&n_keys, d_nkeys, sizeof(n_keys), hipMemcpyDeviceToHost, B.st));
+    RG_HIP(hipStreamSynchronize(B.st));
+    RG_HIP(B.alloc(&d_sorted, n_keys));
+    if (n_keys)
+        if (int rc = radix_sort(B, L, d_keys, d_sorted, n_keys, G.tb + cb, &d_sorted)) return rc;
     RG_HIP(B.alloc(&d_off, size_t(nc) + 1));
-    RG_HIP(B.alloc(&d_refs, n_cand));
-    const uint64_t k3 = std::max<uint64_t>(std::max<uint64_t>(n_cand, uint64_t(nc) + 1), nt);
-    hipLaunchKernelGGL(k_offsets, dim3(uint32_t((k3 + 255) / 256)), dim3(256), 0, B.st, d_sorted, uint32_t(n_cand),
+    RG_HIP(B.alloc(&d_refs, n_keys));
+    const uint64_t k3 = std::max<uint64_t>(std::max<uint64_t>(n_keys, uint64_t(nc) + 1), nt);
+    hipLaunchKernelGGL(k_offsets, dim3(uint32_t((k3 + 255) / 256)), dim3(256), 0, B.st, d_sorted, n_keys,
                        nc, G.tb, d_hit, nt, d_off, d_refs, d_err);
     RG_HIP(hipGetLastError());
     RG_HIP(hipEventRecord(B.e1, B.st));
@@ -369,7 +548,7 @@ int build(const rt_vertex *v, uint32_t nv, const rt_triangle *t, uint32_t nt, ui
         return rt_internal_fail(RT_E_INVALID, (err & 1) ? "a triangle overlaps a cell outside the grid"
                                                         : "a triangle touches no cell (grid.cpp:121-125)");
     }
-    const uint32_t nr = h_off[nc];                   // lower_bound(nc << tb) = first sentinel
+    const uint32_t nr = h_off[nc];                   // lower_bound(nc << tb) = n_keys
     uint32_t *h_refs = static_cast<uint32_t *>(std::malloc(sizeof(uint32_t) * std::max(nr, 1u)));
     if (!h_refs)
     {

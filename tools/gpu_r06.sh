@@ -84,6 +84,20 @@ for step in "$@"; do
                run tiers_$1_$2_$3 200 env RT_WH_LDS=$1 RT_WH_ALPHA16=$2 RT_WH_BETA16=$3 python3 -u tools/shard_scaling.py \
                    --steady --batch --overlap --scenes 1 8 --out ${T}_tiers_$1_$2_$3 0
            done ;;
+    grid) run grid 300 $PYT tests/test_gpu_grid.py -m gpu
+          run grid_bench 200 python3 -u tools/grid_bench.py --out gpurun_out/${T}_grid_bench.json ;;
+    center) for c in 0 1; do
+               run first_c$c 300 env RT_HF_CENTER=$c python3 -u tools/first_frame_probe.py --scenes 0 1 2 3 4 5 6 7 8 9 --reps 3 --out ${T}_first_c$c
+           done
+           for c in 0 1 0 1; do
+               run scale_c$c 300 env RT_HF_CENTER=$c python3 -u tools/shard_scaling.py --steady --batch --overlap --scenes 1 8 --out ${T}_scale_c$c 0
+               run bench_c$c 300 env RT_HF_CENTER=$c python -u bench.py --steps 200 --warmup 100 --no-cpu-baseline --no-end-to-end --no-legs
+               run b10_c$c 300 env RT_HF_CENTER=$c python -u bench.py --workload batch10 --steps 50 --warmup 20 --no-cpu-baseline --no-end-to-end --no-first-frame --no-moving-camera --no-legs
+           done ;;
+    n1lds) for m in 0 15; do
+               run n1lds_$m 300 python3 -u tools/tunable_sweep.py --env KERNEL --values 0 0x200 --scenes 4 5 8 2 --ns 1 \
+                   --per-scene --extra-env RT_WH_LDS=$m --out ${T}_n1lds_$m
+           done ;;
     *) echo "unknown step $step"; exit 2 ;;
     esac
 done
