@@ -46,7 +46,8 @@ if a.batch:
     for _ in range(a.frames):
         rtm.render_batch_device(gs, fs, [o.data_ptr() for o in outs], a.rank, a.nranks, stream=st.cuda_stream)
     torch.cuda.synchronize()
-    print("batch frames", a.frames, "scenes", [sids[i] for i in order], "rank", a.rank, "of", a.nranks)
+    print("batch frames", a.frames, "scenes", [sids[i] for i in order], "rank", a.rank, "of", a.nranks,
+          "wide tiers (listed, lds) of the batch's plan", gs[0].wide_tiers())
     sys.exit(0)
 for sid in (a.scenes or [a.scene]):
     g = rtm.GpuScene(rtm.HostScene.load(sid), 0)
