@@ -52,5 +52,5 @@ rc=$?; echo "trace rc=$rc"; [ $rc -eq 0 ] || exit $rc
 cd $R
 run shard_bench 500 python -u tools/shard_scaling.py --steady --batch --overlap --scenes 1 8 --out ${T}_shard_scaling_bench 0
 run shard_head 500 python -u tools/shard_scaling.py --steady --scenes 4 --frame 4096 4096 16 --out ${T}_shard_scaling_head 0
-run counters_n8 300 python3 -u tools/collect_counters.py --workload bench --batch --rank 0 --nranks 8 --frames 24 \
+run counters_n8 300 python3 -u tools/collect_counters.py --workload bench --batch --rank 0 --nranks 8 --frames 64 \
     --sets sq lat --out gpurun_out/${T}_counters_batch_n8.json --work gpurun_out/${T}_pmc_n8
