@@ -266,7 +266,7 @@ def first_frame(rtm, torch):
     return out
 
 
-def valu_roofline(rtm, kernel_ms, args, world, algorithmic, step_ms=None, work=None):
+def valu_roofline(rtm, kernel_ms, args, world, algorithmic, step_ms=None, work=None, scene_ms=None):
     """The bound that binds: VALU issue.  SQ_INSTS_VALU per launch comes from
     profiles/counters_<workload>.json (tools/collect_counters.py, rocprofv3 --pmc on this workload), used
     only when its source_hash equals the hash of the kernel sources being timed; achieved =
@@ -331,12 +331,21 @@ def valu_roofline(rtm, kernel_ms, args, world, algorithmic, step_ms=None, work=N
         return roof
     insts = sum(sc[str(sid)]["SQ_INSTS_VALU"] for sid in SCENES)
     rate = insts / ((step_ms or sum(kernel_ms.values())) / 1e3)
+    # per scene: its instructions over its own step time when the per-scene legs ran (each scene alone
+    # through the same step), else over its launches' own durations (which, overlapped, span ~2 steps)
     roof.update({"achieved": round(rate / 1e9, 1), "frac": round(rate / VALU_PEAK, 4),
-                 "traffic": round(sum(sc[str(sid)]["hbm_bytes"] for sid in SCENES) / len(SCENES)),
-                 "traffic_unit": "HBM bytes per launch (mean over scenes)",
-                 "per_scene_valu_frac": {str(sid): round(sc[str(sid)]["SQ_INSTS_VALU"] / (kernel_ms[sid] / 1e3)
-                                                         / VALU_PEAK, 4) for sid in SCENES},
+                 "traffic": round(sum(sc[str(sid)]["hbm_bytes"] for sid in SCENES)),
+                 "traffic_unit": "HBM bytes per step (the sum over its per-scene launches)",
                  "counters": f"{os.path.relpath(path, ROOT)}, source hash {src}"})
+    # per scene: its instructions over its own step alone when the per-scene legs ran, else over its
+    # launches' mean duration -- not with overlapped launches, whose duration spans ~2 frames
+    overlapped = work is not None and getattr(work, "overlap", False)
+    if scene_ms or not overlapped:
+        own = {sid: (scene_ms[str(sid)]["ms_per_step"] if scene_ms else kernel_ms[sid]) for sid in SCENES}
+        roof["per_scene_valu_frac"] = {str(sid): round(sc[str(sid)]["SQ_INSTS_VALU"] / (own[sid] / 1e3) / VALU_PEAK, 4)
+                                       for sid in SCENES}
+        roof["per_scene_note"] = ("each scene's instructions over " +
+                                  ("its own step alone (per_scene_steps)" if scene_ms else "its launches' mean duration"))
     return roof
 
 
@@ -889,10 +898,11 @@ def main():
                     help="replay the step's render launch(es) from a hipGraph captured after the warm-up")
     ap.add_argument("--batch", choices=["auto", "on", "off"], default="auto",
                     help="the step's frames in batched launches (rt_render_batch_device, up to MAX_BATCH "
-                         "frames each) or one launch per frame; auto = batched whenever the step has 2+ frames: "
-                         "13-14 %% faster at N = 2 and 8 (profiles/r03d_ab_wave_priority.json) and, on the "
-                         "round-4 build, at N = 1 the bench pair 0.541 vs 0.552 ms and config 5 2.79 vs 3.00 ms "
-                         "per step (profiles/r04ab_batch_n1.json)")
+                         "frames each) or one launch per frame; auto = batched when the step has 2+ frames and "
+                         "N > 1 or --overlap off (at N = 2-8 the batched step is 18-44 %% faster, "
+                         "profiles/r06_launch_shape_ab.json; without overlap it was also at N = 1, "
+                         "profiles/r04ab_batch_n1.json), one launch per frame at N = 1 with overlap (each frame "
+                         "beside the one before it: bench pair 0.511 vs 0.529 ms, config 5 2.61 vs 2.66 ms)")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="bench")
     ap.add_argument("--check", action="store_true",
                     help="after timing, rank 0 compares every assembled frame with a one-GPU render")
@@ -922,9 +932,9 @@ def main():
             dist.init_process_group(args.dist_backend)
 
     rtm = load_package()
-    batch = args.batch == "on" or (args.batch == "auto" and len(SCENES) >= 2)
-    work = GpuWorkload(rtm, torch, world, rank, local, args.kernel, batch=batch,
-                       overlap=args.overlap == "on" and not args.graph)
+    overlap = args.overlap == "on" and not args.graph
+    batch = args.batch == "on" or (args.batch == "auto" and len(SCENES) >= 2 and (world > 1 or not overlap))
+    work = GpuWorkload(rtm, torch, world, rank, local, args.kernel, batch=batch, overlap=overlap)
     # The per-sample counts behind the algorithmic bytes (the debug records kernel over
     # whole frames, reduced on the host) first; then the supplementary legs that keep the GPU busy
     # (the drop-in end to end, the orbiting camera) run BEFORE the warm-up, so the timed steps follow
@@ -965,7 +975,8 @@ def main():
         # algorithmic bytes per launch (this rank's launch covers 1/world of the frame)
         launch_bytes = {sid: ab[sid]["bytes_per_sample"] * W * H * SPP / world for sid in SCENES}
         achieved = sum(launch_bytes.values()) / (step_ms / 1e3)
-        roof = valu_roofline(rtm, kernel_ms, args, world, achieved, step_ms, work)
+        roof = valu_roofline(rtm, kernel_ms, args, world, achieved, step_ms, work,
+                             scene_ms=legs.get("per_scene_steps"))
         roof["duration"] = {"ms_per_step": round(step_ms, 4), "launches": args.steps * work.launches_per_step(),
                             "source": "HIP events on the launch stream around all the timed steps' render launches "
                                       "(gaps and the every-16th-frame plan kernel included: a conservative duration)"}

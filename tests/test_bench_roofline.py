@@ -44,8 +44,14 @@ def test_roofline_uses_matching_counters(tmp_path, monkeypatch):
     r = bench.valu_roofline(FakeRtm("abc123"), kms, _args(), 1, 1.9e13)
     rate = (2.0e8 + 3.6e8) / (0.77e-3)
     assert r["bound"] == "valu" and abs(r["frac"] - rate / bench.VALU_PEAK) < 1e-3
-    assert r["frac"] <= 1.0 and r["traffic"] == round((1.6e7 + 3.2e7) / 2)
+    assert r["frac"] <= 1.0 and r["traffic"] == round(1.6e7 + 3.2e7)      # per step: both launches
     assert abs(r["algorithmic_frac"] - 1.9e13 / bench.HBM_PEAK) < 1e-3
+    # per scene over its own launches' duration, or over its own step alone when the legs measured it
+    assert abs(r["per_scene_valu_frac"]["8"] - 3.6e8 / 0.50e-3 / bench.VALU_PEAK) < 1e-3
+    r = bench.valu_roofline(FakeRtm("abc123"), kms, _args(), 1, 1.9e13, step_ms=0.51,
+                            scene_ms={"1": {"ms_per_step": 0.18}, "8": {"ms_per_step": 0.33}})
+    assert abs(r["frac"] - (2.0e8 + 3.6e8) / 0.51e-3 / bench.VALU_PEAK) < 1e-3
+    assert abs(r["per_scene_valu_frac"]["8"] - 3.6e8 / 0.33e-3 / bench.VALU_PEAK) < 1e-3
 
 
 def test_roofline_refuses_other_sources(tmp_path, monkeypatch):

@@ -23,14 +23,12 @@ run() {
 if [ "$PART" = A ]; then
     run pytest 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread
     run smoke 120 python -c "import __graft_entry__ as g; g.smoke()"
-    # bench.py batches a step's frames at N = 1 when it has 2+ (the bench pair, config 5): those
-    # workloads' counters are of the batched launches, summed per step; head4096 is one frame
-    for W in bench batch10; do
-        run counters_$W 330 python3 -u tools/collect_counters.py --workload $W --frames 8 --batch \
+    # bench.py renders a step's frames one launch each at N = 1 (overlapped; batched at N > 1): the
+    # counters are per scene, summed per step by bench.py
+    for W in bench batch10 head4096; do
+        run counters_$W 330 python3 -u tools/collect_counters.py --workload $W --frames 8 \
             --out gpurun_out/${T}_counters_${W}.json --work gpurun_out/${T}_pmc
     done
-    run counters_head4096 330 python3 -u tools/collect_counters.py --workload head4096 --frames 8 \
-        --out gpurun_out/${T}_counters_head4096.json --work gpurun_out/${T}_pmc
     # per-scene launches of config 5 (each scene's own VALU issue fraction, not a bench input)
     run counters_batch10_per_scene 330 python3 -u tools/collect_counters.py --workload batch10 --frames 8 \
         --sets sq --out gpurun_out/${T}_counters_batch10_per_scene.json --work gpurun_out/${T}_pmc_ps
