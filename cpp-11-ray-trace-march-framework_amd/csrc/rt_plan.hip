@@ -222,7 +222,7 @@ __global__ void __launch_bounds__(kWG) k_hf_plan(KParams P, uint32_t nblocks, ui
 // profiles/r05k_frame_series*.json).  hf_prepare adopts it (a stream wait on its event) at the second
 // frame after, or at the next measured frame (which reuses the plan's buffers).  Inside a stream
 // capture every plan stays on the launch stream.
-int launch_plans(rt_scene *s, const KParams& P, uint64_t blocks, hipStream_t st)
+int launch_plans(rt_scene *s, const KParams& P, uint64_t blocks, hipStream_t st, bool pipelined)
 {
     const dim3 grid(uint32_t((blocks + kWG * kHfPlanPer - 1) / (kWG * kHfPlanPer))), wg(kWG);
     HfCtx *c = s->hf_last;
@@ -232,8 +232,10 @@ int launch_plans(rt_scene *s, const KParams& P, uint64_t blocks, hipStream_t st)
     const bool twice = P.hf_ver == 0u;
     // the position-aware threshold for single-frame launches; a batched launch keeps max >> shift
     // (the bench pair's batched step: 0.5396 vs 0.5318 ms with it, scenes 4 / 5 in their own launches
-    // 0.2486 / 0.4518 vs 0.252 / 0.46: profiles/r05ar_hf_pos_sweep.json)
-    const uint32_t pos16 = (c && c->key[4] != 0u) ? 0u : s->hf_pos16;
+    // 0.2486 / 0.4518 vs 0.252 / 0.46: profiles/r05ar_hf_pos_sweep.json), and so does a pipelined one
+    // (RT_KERNEL_FLAG_OVERLAP: a late block's tail runs under the next launch; the bench pair as
+    // overlapped frames 0.5074 vs 0.5121 ms per step, profiles/r06_pipelined_plan_ab.json)
+    const uint32_t pos16 = ((c && c->key[4] != 0u) || pipelined) ? 0u : s->hf_pos16;
     // the second pass: the first pass's outputs are its inputs, written into the buffers of the version
     // before (the two passes alternate them by parity, as consecutive frames do)
     KParams Q = P;

@@ -240,7 +240,7 @@ struct HfPeek { bool found, measure, measure_ok; };
 HfPeek hf_peek(const rt_scene *s, const KParams& P, uint64_t blocks, int var, uint64_t batch, uint64_t cam_sig);
 // The plan kernel(s) after a measured frame on its stream (k_hf_plan; two passes after a shape's first
 // measured frame, see launch_plans)
-int launch_plans(rt_scene *s, const KParams& P, uint64_t blocks, hipStream_t st);
+int launch_plans(rt_scene *s, const KParams& P, uint64_t blocks, hipStream_t st, bool pipelined);
 // The camera of a frame as one 64-bit signature (FNV-1a over the rotation, origin and fov bits)
 uint64_t cam_signature(const KParams& P, uint64_t h = 0xcbf29ce484222325ull);
 

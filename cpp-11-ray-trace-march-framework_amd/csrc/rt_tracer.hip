@@ -657,8 +657,12 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
         uint32_t lgrid = grid, lwg = kWG;
         // (not for a scene with very dense cells: scene 5, a cell of 1,226 references, runs its whole
         // frame 3 % faster in 256-lane workgroups, while killeroo (426) and scene 4 (132) run 4-6 %
-        // slower that way: profiles/r05av_wg64_dense.json)
-        if (s->wg64 && kvar == kVarAuto && grid >= s->wg64_min_blocks && s->max_cell_refs < s->wg64_max_refs)
+        // slower that way: profiles/r05av_wg64_dense.json -- unless the launch may overlap the one before
+        // it, whose work fills the tail: config 5 as overlapped frames 2.575 vs 2.607 ms per step,
+        // profiles/r06_pipelined_plan_ab.json)
+        const bool pipelined = (f->kernel & RT_KERNEL_FLAG_OVERLAP) != 0u;
+        if (s->wg64 && kvar == kVarAuto && grid >= s->wg64_min_blocks &&
+            (s->max_cell_refs < s->wg64_max_refs || pipelined))
         {
             lfn = lanes_w64_kernel(kVarAuto);
             P.vblocks = grid;
@@ -705,7 +709,7 @@ int launch_render(rt_scene *s, const rt_frame *f, KParams& P, uint32_t n_local_t
             s->ev_recorded = true;
         }
         if ((P.hf_front || P.wh_on) && P.hf_measure)
-            if (int rc = launch_plans(s, P, blocks, st)) return rc;
+            if (int rc = launch_plans(s, P, blocks, st, pipelined)) return rc;
     }
     else
     {
@@ -938,7 +942,7 @@ int launch_batch(rt_scene *const *S, const rt_frame *F, uint32_t n, KParams *P, 
         S[i]->ev_recorded = true;
     }
     if ((P[0].hf_front || P[0].wh_on) && P[0].hf_measure)
-        if (int rc = launch_plans(s0, KB.p[0], blocks, st)) return rc;
+        if (int rc = launch_plans(s0, KB.p[0], blocks, st, false)) return rc;
     RT_HIP(hipGetLastError());
     if (timed)
     {
