@@ -332,3 +332,39 @@ def test_moving_camera_views_batched(golden, nranks, overlap):
             g.close()
         for h in hss:
             h.close()
+
+
+def test_overlap_records_rotating_streams(golden):
+    """ADVICE r05 (rt_render_records_device and RT_KERNEL_FLAG_OVERLAP): records calls whose frames carry
+    the overlap flag, interleaved with overlapped single-frame renders of the same frames, rotating over
+    THREE streams, and two camera-origin changes on the way (orbit37 -> corner -> orbit37: k_origin_pre
+    into the other per-origin record buffer while earlier launches may still read theirs).  The records
+    calls never overlap (the library strips the flag and ends each on its own completion event), so every
+    call's records and frame, and every overlapped render's frame, equal the reference's for its view."""
+    import torch
+    seq = ["orbit37"] * 4 + ["corner"] * 3 + ["orbit37"] * 2
+    hs = rtm.HostScene.load(8)
+    gs = rtm.GpuScene(hs, 0)
+    try:
+        views = {n: golden["views"][f"scene8_{n}"] for n in set(seq)}
+        fs = {n: view_frame(gs, v, kernel=rtm.RT_KERNEL_AUTO | rtm.RT_KERNEL_FLAG_OVERLAP) for n, v in views.items()}
+        W, H, spp = views["orbit37"]["W"], views["orbit37"]["H"], views["orbit37"]["spp"]
+        streams = [torch.cuda.Stream() for _ in range(3)]
+        frames = [torch.full((W * H,), 0x5A5A5A5A, dtype=torch.int32, device="cuda") for _ in seq]
+        outs = [torch.full((W * H,), 0x5A5A5A5A, dtype=torch.int32, device="cuda") for _ in seq]
+        recs = [torch.full((W * H * spp * REC_WORDS,), -1, dtype=torch.int32, device="cuda") for _ in seq]
+        torch.cuda.synchronize()            # (the fills run on torch's stream, not on these)
+        for i, n in enumerate(seq):
+            gs.render_frame_device(fs[n], frames[i].data_ptr(), streams[i % 3].cuda_stream)
+            rtm.render_records_device([gs], [fs[n]], [outs[i].data_ptr()], [(0, 0, W, H)], [recs[i].data_ptr()],
+                                      stream=streams[(i + 1) % 3].cuda_stream)
+        torch.cuda.synchronize()
+        for i, n in enumerate(seq):
+            v = views[n]
+            assert hashlib.sha256(frames[i].cpu().numpy().tobytes()).hexdigest() == v["bgra_sha256"], (i, n)
+            assert hashlib.sha256(outs[i].cpu().numpy().tobytes()).hexdigest() == v["bgra_sha256"], (i, n)
+            expect(v, shas(host(recs[i])))
+    finally:
+        torch.cuda.synchronize()
+        gs.close()
+        hs.close()
